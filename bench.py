@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""bench.py -- RANSAC hypotheses/sec on BASELINE.json config 2, 1..8 MI355X.
+
+Workload (BASELINE.json configs[1]): one synthetic PnP
+problem, 10 000 2D-3D correspondences shaped like the reference's UTM scene,
+50 % outliers, P3P minimal solver, reprojection threshold 30 px
+(main_v1.py:497-502), 100 000 hypotheses per GPU per step, inputs resident
+in HBM.  A step = sample -> P3P -> score all 10k points for every hypothesis
+of this rank's shard, global best by all-reduce(MAX) of the packed key
+(count << 32 | ~index) over RCCL, then the winner's RANSAC-phase mask.
+Weak scaling: rank r owns hypotheses [r*H, (r+1)*H) of the same Philox stream.
+
+Also reported: ms-to-best-model (adaptive termination on, LM refit on, wall
+time of the full rsac.pnp_ransac call), the scoring kernel's roofline, and
+the CPU restatement timed on this host (oracle/, 1 thread).
+
+Launch: python bench.py [--gpus 1 --steps 10 --warmup 3]; for N > 1 the driver
+runs it under torch.distributed.run with one rank per GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "code-reproduction-ransac_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import rsac  # noqa: E402
+from rsac import synth  # noqa: E402
+
+METRIC = "RANSAC hypotheses/sec + ms-to-best-model, 10k pts 50% outliers, 1/2/4/8 GPU"
+BYTES_PER_POINT = 20  # f32 X, Y, Z, u, v
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--points", type=int, default=10_000)
+    ap.add_argument("--hyps", type=int, default=100_000, help="hypotheses per GPU per step")
+    ap.add_argument("--thr", type=float, default=30.0)
+    ap.add_argument("--cpu-hyps", type=int, default=150_000, help="CPU baseline sample (hypotheses, 1 thread)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ms-to-best", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    pr = synth.pnp_problem(args.points, 0.5, seed=0)
+    K = pr["K"]
+    p3 = torch.from_numpy(pr["points3d"]).to(dev)
+    p2 = torch.from_numpy(pr["points2d"]).to(dev)
+    H = args.hyps
+    base = rank * H
+    score_ms = []
+    solve_ms = []
+
+    def step():
+        key, model, info = rsac.evaluate_range(p2, p3, K, base, H, args.thr, return_info=True, device=local)
+        score_ms.append(info.score_ms)
+        solve_ms.append(info.solve_ms)
+        if dist is not None:
+            kt = torch.tensor([key], dtype=torch.int64, device=dev)
+            dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+            gkey = int(kt.item())
+            gidx = 0xFFFFFFFF - (gkey & 0xFFFFFFFF)
+            mt = torch.from_numpy(model).to(dev)
+            dist.broadcast(mt, src=min(gidx // H, world - 1))
+            model = mt.cpu().numpy()
+        mask, cnt = rsac.pose_mask(p2, p3, K, model, args.thr, device=local)
+        return cnt
+
+    for _ in range(args.warmup):
+        step()
+    score_ms.clear()
+    solve_ms.clear()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cnt = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        et = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(et, op=dist.ReduceOp.MAX)
+        elapsed = float(et.item())
+
+    out = None
+    if rank == 0:
+        hyps_total = world * H * args.steps
+        value = hyps_total / elapsed
+        score_avg = statistics.mean(score_ms)
+        solve_avg = statistics.mean(solve_ms)
+        achieved = args.points * BYTES_PER_POINT * H / (score_avg * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_score_kernel.json")
+        if os.path.exists(pmc):
+            try:
+                d = json.load(open(pmc))
+                if d.get("points") == args.points and d.get("hyps") == H:
+                    traffic = d.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        ms_to_best = None
+        if not args.no_ms_to_best:
+            walls = []
+            for i in range(23):
+                t = time.perf_counter()
+                R, t_, m, info = rsac.pnp_ransac(p2, p3, K, 5000, args.thr, confidence=0.99, adaptive=True,
+                                                 refine=True, return_info=True, device=local)
+                torch.cuda.synchronize()
+                if i >= 3:
+                    walls.append((time.perf_counter() - t) * 1e3)
+            ms_to_best = statistics.median(walls)
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(pr, args)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "hypotheses/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (rsac.synth.pnp_problem seed 0: UTM-scale points, main_v1.py K, N(0,1px) noise)",
+            "config": {"workload": "C2: 10k 2D-3D correspondences, 50% outliers, P3P, thr 30 px, "
+                                   f"{H} hypotheses per GPU per step, global best via RCCL all-reduce(MAX)",
+                       "points": args.points, "hypotheses_per_gpu": H, "outlier_ratio": 0.5,
+                       "parallelism": f"dp{world} (hypothesis shards)"},
+            "ms_to_best_model": ms_to_best,
+            "best_inliers": int(cnt),
+            "kernels_ms": {"pnp_solve": solve_avg, "pnp_score": score_avg},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_pnp_score", "algorithmic_bytes_per_launch": args.points * BYTES_PER_POINT * H},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+def cpu_baseline(pr, args):
+    """The CPU restatement (oracle/, C, 1 thread) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import pyoracle as O
+    except Exception as e:  # oracle not built
+        return {"value": None, "error": str(e)}
+    soa = O.soa_pnp(pr["points3d"], pr["points2d"])
+    cam = O.cam_from_K(pr["K"])
+    n = args.cpu_hyps
+    O.pnp_hypotheses(soa, cam, args.thr, 0x5EED, 50)  # warm
+    t = time.perf_counter()
+    O.pnp_hypotheses(soa, cam, args.thr, 0x5EED, n)
+    dt = time.perf_counter() - t
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": n / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
+            "sample": f"{n} hypotheses of the same C2 problem (10k points), oracle/rsac_oracle.c -O2, 1 thread, "
+                      f"{dt:.1f} s",
+            "cpu_model": model, "os_cpu_count": os.cpu_count()}
+
+
+if __name__ == "__main__":
+    main()

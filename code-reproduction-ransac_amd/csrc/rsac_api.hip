@@ -1,0 +1,889 @@
+// rsac_api.hip -- the C ABI of include/rsac.h: context, input staging,
+// round loop (solve + score on the GPU, sequential scan on the host),
+// masks and refits.
+//
+// One call == one cv2.solvePnPRansac / cv2.findHomography of the reference
+// (main_v1.py:497 / main_v1.py:312), or the whole Python loop around it for
+// the batched entry points (main_v1.py:274-284, testpro-K.py:58-75).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/rsac.h"
+#include "rsac_host.h"
+#include "rsac_internal.h"
+#include "rsac_math.h"
+
+using namespace rsac;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(RSAC_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const { return (T *)p; }
+};
+
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const { return (T *)p; }
+};
+
+constexpr size_t kMaxModelBytes = size_t(32) << 30;  // hypothesis records kept resident per call
+
+}  // namespace
+
+struct rsac_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    int64_t round_size = 4096;
+    // device scratch
+    DevBuf pts, offsets, cams, thr2, models, status, counts, subsets, substatus, best, bestmodels, mask;
+    // pinned host staging
+    PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask;
+};
+
+// ---------------------------------------------------------------------------
+// problem staging
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Staged {
+    int P = 0;
+    int64_t total = 0;
+    std::vector<int64_t> off;
+    const float *d[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // device SoA
+    std::vector<float> hbuf;                                            // host SoA copy (refits, MWC check)
+    const float *h[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool host_ready = false;
+};
+
+// ncomp3 = 3 for PnP (pts3d N x 3, pts2d N x 2 -> X Y Z U V), 2 for 2D-2D (src, dst -> SX SY DX DY)
+int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const int64_t *offsets, int32_t P, int32_t n,
+                 uint32_t flags, hipStream_t s, Staged &st) {
+    st.P = P;
+    st.off.resize(P + 1);
+    if (offsets) {
+        for (int p = 0; p <= P; ++p) st.off[p] = offsets[p];
+        if (st.off[0] != 0) return fail(RSAC_EINVAL, "offsets[0] must be 0");
+        for (int p = 0; p < P; ++p)
+            if (st.off[p + 1] < st.off[p]) return fail(RSAC_EINVAL, "offsets must be non-decreasing");
+    } else {
+        st.off[0] = 0;
+        st.off[1] = n;
+    }
+    const int64_t N = st.off[P];
+    st.total = N;
+    const int nc = ncomp_a + 2;
+    if (flags & RSAC_F_DEVICE_SOA) {
+        const float *A = (const float *)a, *B = (const float *)b;
+        for (int k = 0; k < ncomp_a; ++k) st.d[k] = A + k * N;
+        st.d[ncomp_a] = B;
+        st.d[ncomp_a + 1] = B + N;
+        return RSAC_OK;
+    }
+    HIPCHK(c->pts.ensure(sizeof(float) * nc * std::max<int64_t>(N, 1)));
+    float *D = c->pts.as<float>();
+    for (int k = 0; k < nc; ++k) st.d[k] = D + k * N;
+    if (flags & RSAC_F_DEVICE_IN) {
+        if (ncomp_a == 3)
+            HIPCHK(launch_pnp_prepare((const double *)a, (const double *)b, N, D, D + N, D + 2 * N, D + 3 * N,
+                                      D + 4 * N, s));
+        else
+            HIPCHK(launch_hom_prepare((const double *)a, (const double *)b, N, D, D + N, D + 2 * N, D + 3 * N, s));
+        return RSAC_OK;
+    }
+    // host float64 AoS -> float32 SoA (the CV_32F conversion of OpenCV), pinned, one H2D copy
+    HIPCHK(c->h_pts.ensure(sizeof(float) * nc * std::max<int64_t>(N, 1)));
+    float *H = c->h_pts.as<float>();
+    const double *A = (const double *)a, *B = (const double *)b;
+    for (int64_t i = 0; i < N; ++i) {
+        for (int k = 0; k < ncomp_a; ++k) H[k * N + i] = (float)A[ncomp_a * i + k];
+        H[ncomp_a * N + i] = (float)B[2 * i];
+        H[(ncomp_a + 1) * N + i] = (float)B[2 * i + 1];
+    }
+    HIPCHK(hipMemcpyAsync(D, H, sizeof(float) * nc * N, hipMemcpyHostToDevice, s));
+    for (int k = 0; k < nc; ++k) st.h[k] = H + k * N;
+    st.host_ready = true;
+    return RSAC_OK;
+}
+
+// host copy of the staged SoA (needed by refits / the MWC homography check)
+int ensure_host_points(Staged &st, int nc, hipStream_t s) {
+    if (st.host_ready) return RSAC_OK;
+    const int64_t N = st.total;
+    st.hbuf.resize(std::max<int64_t>(nc * N, 1));
+    for (int k = 0; k < nc; ++k) {
+        HIPCHK(hipMemcpyAsync(st.hbuf.data() + k * N, st.d[k], sizeof(float) * N, hipMemcpyDeviceToHost, s));
+        st.h[k] = st.hbuf.data() + k * N;
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    st.host_ready = true;
+    return RSAC_OK;
+}
+
+// small per-problem tables: offsets (int64), cams (4 f64), thr2 (f32)
+int stage_tables(rsac_ctx *c, const Staged &st, const double *K, double thresh, hipStream_t s) {
+    const int P = st.P;
+    const size_t off_b = sizeof(int64_t) * (P + 1), cam_b = sizeof(double) * 4 * P, thr_b = sizeof(float) * P;
+    HIPCHK(c->offsets.ensure(off_b));
+    HIPCHK(c->cams.ensure(std::max<size_t>(cam_b, 32)));
+    HIPCHK(c->thr2.ensure(thr_b));
+    HIPCHK(c->h_small.ensure(off_b + cam_b + thr_b + 64));
+    char *hs = c->h_small.as<char>();
+    memcpy(hs, st.off.data(), off_b);
+    double *hc = (double *)(hs + off_b);
+    for (int p = 0; p < P; ++p) {
+        if (K) {
+            const double *k = K + 9 * p;
+            hc[4 * p] = k[0]; hc[4 * p + 1] = k[4]; hc[4 * p + 2] = k[2]; hc[4 * p + 3] = k[5];
+        } else {
+            hc[4 * p] = hc[4 * p + 1] = 1.0; hc[4 * p + 2] = hc[4 * p + 3] = 0.0;
+        }
+    }
+    float *ht = (float *)(hs + off_b + cam_b);
+    const float t2 = (float)(thresh * thresh);  // findInliers: float t = (float)(thresh*thresh)
+    for (int p = 0; p < P; ++p) ht[p] = t2;
+    HIPCHK(hipMemcpyAsync(c->offsets.p, hs, off_b, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->cams.p, hs + off_b, cam_b, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->thr2.p, hs + off_b + cam_b, thr_b, hipMemcpyHostToDevice, s));
+    return RSAC_OK;
+}
+
+int ensure_hyp_buffers(rsac_ctx *c, int P, int64_t stride, bool subsets) {
+    const size_t recs = (size_t)P * (size_t)stride;
+    if (recs * kModelStride * sizeof(double) > kMaxModelBytes)
+        return fail(RSAC_ENOMEM, "%lld hypothesis records exceed the resident budget", (long long)recs);
+    HIPCHK(c->models.ensure(recs * kModelStride * sizeof(double)));
+    HIPCHK(c->status.ensure(recs));
+    HIPCHK(c->counts.ensure(recs * sizeof(int32_t)));
+    HIPCHK(c->best.ensure(sizeof(int64_t) * P));
+    HIPCHK(c->bestmodels.ensure(sizeof(double) * kModelStride * P));
+    HIPCHK(c->h_best.ensure(sizeof(int64_t) * P));
+    HIPCHK(c->h_bestmodels.ensure(sizeof(double) * kModelStride * P));
+    if (subsets) {
+        HIPCHK(c->subsets.ensure(recs * 4 * sizeof(int32_t)));
+        HIPCHK(c->substatus.ensure(recs));
+        HIPCHK(c->h_subsets.ensure(recs * 4 * sizeof(int32_t)));
+        HIPCHK(c->h_substatus.ensure(recs));
+    }
+    return RSAC_OK;
+}
+
+hipStream_t pick_stream(rsac_ctx *c, void *stream) { return stream ? (hipStream_t)stream : c->stream; }
+
+enum class Model { PnP, Hom };
+
+// The RANSAC loop of RANSACPointSetRegistrator::run for P problems at once:
+// rounds of `round` hypotheses are solved + scored on the GPU, then every
+// unfinished problem's scan consumes them in index order.
+struct LoopOut {
+    std::vector<ScanState> scan;
+    int rounds = 0;
+    int64_t scored = 0;
+    double gpu_ms = 0, solve_ms = 0, score_ms = 0;
+};
+
+void add_times(rsac_ctx *c, double &gpu, double &solve, double &score) {
+    float a = 0, b = 0;
+    if (hipEventElapsedTime(&a, c->ev0, c->ev1) == hipSuccess) solve += a;
+    if (hipEventElapsedTime(&b, c->ev1, c->ev2) == hipSuccess) score += b;
+    gpu += (double)a + (double)b;
+}
+
+int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max_iters, double confidence,
+             uint32_t flags, hipStream_t s, LoopOut &out) {
+    const int P = st.P;
+    const int64_t H = std::max(max_iters, 1);
+    const bool adaptive = (flags & RSAC_F_ADAPTIVE) != 0;
+    const int64_t round = adaptive ? std::min<int64_t>(std::max<int64_t>(c->round_size, 64), H) : H;
+    const int64_t stride = H;
+    int r = ensure_hyp_buffers(c, P, stride, (flags & RSAC_F_SAMPLER_OPENCV) != 0);
+    if (r) return r;
+    HIPCHK(c->h_counts.ensure(sizeof(int32_t) * P * round));
+    HIPCHK(c->h_status.ensure((size_t)P * round));
+
+    PnpArgs *pa = model == Model::PnP ? (PnpArgs *)args : nullptr;
+    HomArgs *ha = model == Model::Hom ? (HomArgs *)args : nullptr;
+#define SETARG(field, val) \
+    do {                   \
+        if (pa) pa->field = (val); else ha->field = (val); \
+    } while (0)
+    SETARG(models, c->models.as<double>());
+    SETARG(status, c->status.as<int8_t>());
+    SETARG(hyp_stride, stride);
+    SETARG(subsets, (const int32_t *)nullptr);
+    SETARG(sub_status, (const int8_t *)nullptr);
+
+    if (flags & RSAC_F_SAMPLER_OPENCV) {
+        // OpenCV's subset sequence is sequential in one MWC state per call:
+        // generate the whole budget on the host (cheap), upload once.
+        int32_t *hs = c->h_subsets.as<int32_t>();
+        int8_t *hss = c->h_substatus.as<int8_t>();
+        for (int p = 0; p < P; ++p) {
+            const int np = (int)(st.off[p + 1] - st.off[p]);
+            Mwc rng;
+            int32_t *o = hs + (size_t)p * stride * 4;
+            int8_t *os = hss + (size_t)p * stride;
+            if (np < 4) {
+                memset(os, -1, stride);
+                continue;
+            }
+            const float *hom[4];
+            if (model == Model::Hom) {
+                for (int k = 0; k < 4; ++k) hom[k] = st.h[k] + st.off[p];
+            }
+            mwc_subsets(rng, np, stride, model == Model::Hom ? hom : nullptr, o, os);
+        }
+        HIPCHK(hipMemcpyAsync(c->subsets.p, hs, sizeof(int32_t) * 4 * P * stride, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->substatus.p, hss, (size_t)P * stride, hipMemcpyHostToDevice, s));
+        SETARG(subsets, c->subsets.as<int32_t>());
+        SETARG(sub_status, c->substatus.as<int8_t>());
+    }
+#undef SETARG
+
+    out.scan.assign(P, ScanState());
+    for (auto &sc : out.scan) sc.reset((int)H);
+    for (int64_t hb = 0; hb < H; hb += round) {
+        const int32_t Hr = (int32_t)std::min<int64_t>(round, H - hb);
+        HIPCHK(hipEventRecord(c->ev0, s));
+        if (pa) {
+            HIPCHK(launch_pnp_solve(*pa, P, hb, Hr, s));
+            HIPCHK(hipEventRecord(c->ev1, s));
+            HIPCHK(launch_pnp_score(*pa, P, hb, Hr, c->counts.as<int32_t>(), s));
+        } else {
+            HIPCHK(launch_hom_solve(*ha, P, hb, Hr, s));
+            HIPCHK(hipEventRecord(c->ev1, s));
+            HIPCHK(launch_hom_score(*ha, P, hb, Hr, c->counts.as<int32_t>(), s));
+        }
+        HIPCHK(hipEventRecord(c->ev2, s));
+        HIPCHK(hipMemcpy2DAsync(c->h_counts.p, sizeof(int32_t) * Hr, c->counts.as<int32_t>() + hb,
+                                sizeof(int32_t) * stride, sizeof(int32_t) * Hr, P, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpy2DAsync(c->h_status.p, Hr, c->status.as<int8_t>() + hb, stride, Hr, P,
+                                hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
+        out.rounds++;
+        out.scored += (int64_t)Hr;
+        bool all_done = true;
+        for (int p = 0; p < P; ++p) {
+            ScanState &sc = out.scan[p];
+            if (!sc.done) {
+                const int np = (int)(st.off[p + 1] - st.off[p]);
+                scan_step(sc, c->h_counts.as<int32_t>() + (size_t)p * Hr, c->h_status.as<int8_t>() + (size_t)p * Hr,
+                          Hr, np, 4, confidence);
+            }
+            all_done = all_done && sc.done;
+        }
+        if (all_done) break;
+    }
+    return RSAC_OK;
+}
+
+// masks + winning models of every problem; records of winners -> c->best
+int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const LoopOut &lo, int64_t stride,
+                 uint8_t *mask_out, uint32_t flags, hipStream_t s) {
+    const int P = st.P;
+    int64_t *hb = c->h_best.as<int64_t>();
+    for (int p = 0; p < P; ++p) hb[p] = lo.scan[p].best >= 0 ? (int64_t)p * stride + lo.scan[p].best : -1;
+    HIPCHK(hipMemcpyAsync(c->best.p, hb, sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_gather_models(c->models.as<double>(), c->best.as<int64_t>(), P, c->bestmodels.as<double>(), s));
+    HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
+                          hipMemcpyDeviceToHost, s));
+    int32_t max_n = 0;
+    for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
+    const int64_t N = st.total;
+    uint8_t *dmask;
+    if (flags & RSAC_F_DEVICE_OUT) {
+        dmask = mask_out;
+    } else {
+        HIPCHK(c->mask.ensure(std::max<int64_t>(N, 1)));
+        dmask = c->mask.as<uint8_t>();
+    }
+    if (N > 0) {
+        if (model == Model::PnP)
+            HIPCHK(launch_pnp_mask(*(PnpArgs *)args, P, max_n, c->best.as<int64_t>(), dmask, s));
+        else
+            HIPCHK(launch_hom_mask(*(HomArgs *)args, P, max_n, c->best.as<int64_t>(), dmask, s));
+    }
+    if (!(flags & RSAC_F_DEVICE_OUT) && mask_out && N > 0) {
+        HIPCHK(c->h_mask.ensure(N));
+        HIPCHK(hipMemcpyAsync(c->h_mask.p, dmask, N, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        memcpy(mask_out, c->h_mask.p, N);
+    } else {
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return RSAC_OK;
+}
+
+int check_device(rsac_ctx *c) {
+    if (!c) return fail(RSAC_EINVAL, "null context");
+    HIPCHK(hipSetDevice(c->device));
+    return RSAC_OK;
+}
+
+// mask for refits when the caller wanted the mask on the device (or not at all)
+int host_mask(rsac_ctx *c, const Staged &st, uint8_t *mask_out, uint32_t flags, hipStream_t s,
+              std::vector<uint8_t> &tmp, const uint8_t **hm) {
+    if (mask_out && !(flags & RSAC_F_DEVICE_OUT)) {
+        *hm = mask_out;
+        return RSAC_OK;
+    }
+    tmp.resize(std::max<int64_t>(st.total, 1));
+    const uint8_t *src = (flags & RSAC_F_DEVICE_OUT) && mask_out ? mask_out : c->mask.as<uint8_t>();
+    HIPCHK(hipMemcpyAsync(tmp.data(), src, st.total, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *hm = tmp.data();
+    return RSAC_OK;
+}
+
+int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *offsets, int32_t P, int32_t n,
+             const double *K, int32_t n_iters, double thr, double conf, uint64_t seed, uint32_t flags, double *R_out,
+             double *t_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out, rsac_stats *stats,
+             hipStream_t s) {
+    int r = check_device(c);
+    if (r) return r;
+    if (P <= 0 || !K) return fail(RSAC_EINVAL, "bad problem count or K");
+    Staged st;
+    r = stage_points(c, pts3d, pts2d, 3, offsets, P, n, flags, s, st);
+    if (r) return r;
+    r = stage_tables(c, st, K, thr, s);
+    if (r) return r;
+    PnpArgs a{};
+    a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
+    a.offsets = c->offsets.as<int64_t>();
+    a.cams = c->cams.as<double>();
+    a.thr2 = c->thr2.as<float>();
+    a.seed = seed;
+    a.rng_base = 0;
+    LoopOut lo;
+    r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo);
+    if (r) return r;
+    const int64_t stride = std::max(n_iters, 1);
+    r = finish_masks(c, Model::PnP, st, &a, lo, stride, mask_out, flags, s);
+    if (r) return r;
+    const double *bm = c->h_bestmodels.as<double>();
+    std::vector<uint8_t> tmpmask;
+    const uint8_t *hm = nullptr;
+    if (flags & RSAC_F_REFINE) {
+        r = ensure_host_points(st, 5, s);
+        if (r) return r;
+        r = host_mask(c, st, mask_out, flags, s, tmpmask, &hm);
+        if (r) return r;
+    }
+    int any = 0;
+    for (int p = 0; p < P; ++p) {
+        const ScanState &sc = lo.scan[p];
+        double R[9], t[3];
+        memcpy(R, bm + kModelStride * p, sizeof R);
+        memcpy(t, bm + kModelStride * p + 9, sizeof t);
+        const bool ok = sc.best >= 0;
+        if (ok && (flags & RSAC_F_REFINE)) {
+            const int64_t o = st.off[p];
+            const int np = (int)(st.off[p + 1] - o);
+            const double cam[4] = {K[9 * p], K[9 * p + 4], K[9 * p + 2], K[9 * p + 5]};
+            pnp_refine_lm(st.h[0] + o, st.h[1] + o, st.h[2] + o, st.h[3] + o, st.h[4] + o, hm + o, np, cam, R, t, 20);
+        }
+        if (R_out) memcpy(R_out + 9 * p, R, sizeof R);
+        if (t_out) memcpy(t_out + 3 * p, t, sizeof t);
+        if (status_out) status_out[p] = ok ? RSAC_OK : RSAC_NO_MODEL;
+        if (ninl_out) ninl_out[p] = sc.max_good;
+        any |= ok;
+    }
+    if (stats) {
+        stats->best_hyp = lo.scan[0].best;
+        stats->iters = lo.scan[0].iter;
+        stats->hyps_scored = lo.scored;
+        stats->n_inliers = lo.scan[0].max_good;
+        stats->rounds = lo.rounds;
+        stats->gpu_ms = lo.gpu_ms;
+        stats->solve_ms = lo.solve_ms;
+        stats->score_ms = lo.score_ms;
+    }
+    return any ? RSAC_OK : RSAC_NO_MODEL;
+}
+
+int hom_core(rsac_ctx *c, const void *src, const void *dst, const int64_t *offsets, int32_t P, int32_t n,
+             int32_t max_iters, double thr, double conf, uint64_t seed, uint32_t flags, double *H_out,
+             int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out, rsac_stats *stats, hipStream_t s) {
+    int r = check_device(c);
+    if (r) return r;
+    if (P <= 0) return fail(RSAC_EINVAL, "bad problem count");
+    if (thr <= 0) thr = 3.0;  // defaultRANSACReprojThreshold of findHomography
+    Staged st;
+    r = stage_points(c, src, dst, 2, offsets, P, n, flags, s, st);
+    if (r) return r;
+    r = stage_tables(c, st, nullptr, thr, s);
+    if (r) return r;
+    if ((flags & RSAC_F_SAMPLER_OPENCV) || (flags & RSAC_F_REFINE)) {
+        r = ensure_host_points(st, 4, s);
+        if (r) return r;
+    }
+    HomArgs a{};
+    a.SX = st.d[0]; a.SY = st.d[1]; a.DX = st.d[2]; a.DY = st.d[3];
+    a.offsets = c->offsets.as<int64_t>();
+    a.thr2 = c->thr2.as<float>();
+    a.seed = seed;
+    a.rng_base = 0;
+    LoopOut lo;
+    r = run_loop(c, Model::Hom, st, &a, max_iters, conf, flags, s, lo);
+    if (r) return r;
+    const int64_t stride = std::max(max_iters, 1);
+    r = finish_masks(c, Model::Hom, st, &a, lo, stride, mask_out, flags, s);
+    if (r) return r;
+    const double *bm = c->h_bestmodels.as<double>();
+    std::vector<uint8_t> tmpmask;
+    const uint8_t *hm = nullptr;
+    if (flags & RSAC_F_REFINE) {
+        r = host_mask(c, st, mask_out, flags, s, tmpmask, &hm);
+        if (r) return r;
+    }
+    int any = 0;
+    for (int p = 0; p < P; ++p) {
+        const ScanState &sc = lo.scan[p];
+        double Hm[9];
+        memcpy(Hm, bm + kModelStride * p, sizeof Hm);
+        const bool ok = sc.best >= 0;
+        const int64_t o = st.off[p];
+        const int np = (int)(st.off[p + 1] - o);
+        if (ok && (flags & RSAC_F_REFINE) && np > 4) {
+            double Hr[9];
+            if (hom_refine(st.h[0] + o, st.h[1] + o, st.h[2] + o, st.h[3] + o, hm + o, np, Hr)) memcpy(Hm, Hr, sizeof Hm);
+        }
+        if (H_out) memcpy(H_out + 9 * p, Hm, sizeof Hm);
+        if (status_out) status_out[p] = ok ? RSAC_OK : RSAC_NO_MODEL;
+        if (ninl_out) ninl_out[p] = sc.max_good;
+        any |= ok;
+    }
+    if (stats) {
+        stats->best_hyp = lo.scan[0].best;
+        stats->iters = lo.scan[0].iter;
+        stats->hyps_scored = lo.scored;
+        stats->n_inliers = lo.scan[0].max_good;
+        stats->rounds = lo.rounds;
+        stats->gpu_ms = lo.gpu_ms;
+        stats->solve_ms = lo.solve_ms;
+        stats->score_ms = lo.score_ms;
+    }
+    return any ? RSAC_OK : RSAC_NO_MODEL;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char *rsac_last_error(void) { return g_err.c_str(); }
+int rsac_abi_version(void) { return RSAC_ABI_VERSION; }
+
+int rsac_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rsac_create(int device, rsac_ctx **out) {
+    if (!out) return fail(RSAC_EINVAL, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RSAC_ENODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(RSAC_EINVAL, "device %d out of range (%d devices)", device, n);
+    HIPCHK(hipSetDevice(device));
+    rsac_ctx *c = new rsac_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ev2) != hipSuccess) {
+        rsac_destroy(c);
+        return fail(RSAC_EHIP, "stream/event creation failed");
+    }
+    *out = c;
+    return RSAC_OK;
+}
+
+void rsac_destroy(rsac_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf *dev[] = {&c->pts, &c->offsets, &c->cams, &c->thr2, &c->models, &c->status, &c->counts,
+                     &c->subsets, &c->substatus, &c->best, &c->bestmodels, &c->mask};
+    for (DevBuf *b : dev) b->release();
+    PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
+                     &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};
+    for (PinBuf *b : pin) b->release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev2) (void)hipEventDestroy(c->ev2);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int rsac_set_round_size(rsac_ctx *c, int64_t hyps) {
+    if (!c || hyps <= 0) return fail(RSAC_EINVAL, "bad round size");
+    c->round_size = hyps;
+    return RSAC_OK;
+}
+
+int rsac_pnp_ransac(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9], int32_t n_iters,
+                    double thr, double conf, uint64_t seed, uint32_t flags, double R_out[9], double t_out[3],
+                    uint8_t *mask_out, rsac_stats *stats, void *stream) {
+    if (n < 4) return fail(RSAC_ETOOFEW, "solvePnPRansac needs >= 4 correspondences (got %d)", n);
+    int32_t status = 0, ninl = 0;
+    return pnp_core(c, pts3d, pts2d, nullptr, 1, n, K, n_iters, thr, conf, seed, flags, R_out, t_out, &status, &ninl,
+                    mask_out, stats, pick_stream(c, stream));
+}
+
+int rsac_pnp_ransac_batched(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *offsets, int32_t P,
+                            const double *K, int32_t n_iters, double thr, double conf, uint64_t seed, uint32_t flags,
+                            double *R_out, double *t_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out,
+                            void *stream) {
+    if (!offsets) return fail(RSAC_EINVAL, "offsets required");
+    return pnp_core(c, pts3d, pts2d, offsets, P, 0, K, n_iters, thr, conf, seed, flags, R_out, t_out, status_out,
+                    ninl_out, mask_out, nullptr, pick_stream(c, stream));
+}
+
+int rsac_homography_ransac(rsac_ctx *c, const void *src, const void *dst, int32_t n, int32_t max_iters, double thr,
+                           double conf, uint64_t seed, uint32_t flags, double H_out[9], uint8_t *mask_out,
+                           rsac_stats *stats, void *stream) {
+    if (n < 4) return fail(RSAC_ETOOFEW, "findHomography needs >= 4 correspondences (got %d)", n);
+    int32_t status = 0, ninl = 0;
+    return hom_core(c, src, dst, nullptr, 1, n, max_iters, thr, conf, seed, flags, H_out, &status, &ninl, mask_out,
+                    stats, pick_stream(c, stream));
+}
+
+int rsac_homography_ransac_batched(rsac_ctx *c, const void *src, const void *dst, const int64_t *offsets, int32_t P,
+                                   int32_t max_iters, double thr, double conf, uint64_t seed, uint32_t flags,
+                                   double *H_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out,
+                                   void *stream) {
+    if (!offsets) return fail(RSAC_EINVAL, "offsets required");
+    return hom_core(c, src, dst, offsets, P, 0, max_iters, thr, conf, seed, flags, H_out, status_out, ninl_out,
+                    mask_out, nullptr, pick_stream(c, stream));
+}
+
+int rsac_score_poses(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                     const double *poses, int32_t n_poses, double thr, uint32_t flags, int32_t *counts_out,
+                     void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (n_poses <= 0 || !poses || !counts_out || !K) return fail(RSAC_EINVAL, "bad arguments");
+    hipStream_t s = pick_stream(c, stream);
+    Staged st;
+    r = stage_points(c, pts3d, pts2d, 3, nullptr, 1, n, flags, s, st);
+    if (r) return r;
+    r = stage_tables(c, st, K, thr, s);
+    if (r) return r;
+    r = ensure_hyp_buffers(c, 1, n_poses, false);
+    if (r) return r;
+    std::vector<double> rec((size_t)n_poses * kModelStride, 0.0);
+    for (int32_t h = 0; h < n_poses; ++h) {
+        memcpy(&rec[(size_t)h * kModelStride], poses + 12 * h, 12 * sizeof(double));
+        rec[(size_t)h * kModelStride + kValidSlot] = 1.0;
+    }
+    HIPCHK(hipMemcpyAsync(c->models.p, rec.data(), rec.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    PnpArgs a{};
+    a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
+    a.offsets = c->offsets.as<int64_t>();
+    a.cams = c->cams.as<double>();
+    a.thr2 = c->thr2.as<float>();
+    a.models = c->models.as<double>();
+    a.status = c->status.as<int8_t>();
+    a.hyp_stride = n_poses;
+    HIPCHK(launch_pnp_score(a, 1, 0, n_poses, c->counts.as<int32_t>(), s));
+    HIPCHK(hipMemcpyAsync(counts_out, c->counts.p, sizeof(int32_t) * n_poses, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return RSAC_OK;
+}
+
+int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                            int64_t hyp_begin, int64_t n_hyps, double thr, uint64_t seed, uint32_t flags,
+                            int64_t *key_out, double model_out[12], rsac_stats *stats, void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (n < 4) return fail(RSAC_ETOOFEW, "need >= 4 correspondences");
+    if (n_hyps <= 0 || n_hyps > INT32_MAX || !K || !key_out) return fail(RSAC_EINVAL, "bad arguments");
+    hipStream_t s = pick_stream(c, stream);
+    Staged st;
+    r = stage_points(c, pts3d, pts2d, 3, nullptr, 1, n, flags & ~RSAC_F_SAMPLER_OPENCV, s, st);
+    if (r) return r;
+    r = stage_tables(c, st, K, thr, s);
+    if (r) return r;
+    r = ensure_hyp_buffers(c, 1, n_hyps, false);
+    if (r) return r;
+    PnpArgs a{};
+    a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
+    a.offsets = c->offsets.as<int64_t>();
+    a.cams = c->cams.as<double>();
+    a.thr2 = c->thr2.as<float>();
+    a.models = c->models.as<double>();
+    a.status = c->status.as<int8_t>();
+    a.hyp_stride = n_hyps;
+    a.rng_base = hyp_begin;
+    a.seed = seed;
+    const int32_t H = (int32_t)n_hyps;
+    HIPCHK(hipEventRecord(c->ev0, s));
+    HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
+    HIPCHK(hipEventRecord(c->ev1, s));
+    HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
+    HIPCHK(hipEventRecord(c->ev2, s));
+    HIPCHK(c->h_counts.ensure(sizeof(int32_t) * H));
+    HIPCHK(c->h_status.ensure(H));
+    HIPCHK(hipMemcpyAsync(c->h_counts.p, c->counts.p, sizeof(int32_t) * H, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(c->h_status.p, c->status.p, H, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        add_times(c, stats->gpu_ms, stats->solve_ms, stats->score_ms);
+        stats->hyps_scored = H;
+        stats->rounds = 1;
+    }
+    const int32_t *cnt = c->h_counts.as<int32_t>();
+    const int8_t *sts = c->h_status.as<int8_t>();
+    int64_t best = -1;
+    int32_t bc = -1;
+    for (int32_t h = 0; h < H; ++h)
+        if (sts[h] > 0 && cnt[h] > bc) { bc = cnt[h]; best = h; }
+    if (best < 0) {
+        *key_out = -1;
+        return RSAC_NO_MODEL;
+    }
+    if (stats) {
+        stats->best_hyp = hyp_begin + best;
+        stats->n_inliers = bc;
+    }
+    const uint64_t gidx = (uint64_t)(hyp_begin + best);
+    *key_out = (int64_t)(((uint64_t)(uint32_t)bc << 32) | (0xFFFFFFFFull - (gidx & 0xFFFFFFFFull)));
+    if (model_out) {
+        double m[kModelStride];
+        HIPCHK(hipMemcpy(m, c->models.as<double>() + best * kModelStride, sizeof m, hipMemcpyDeviceToHost));
+        memcpy(model_out, m, 12 * sizeof(double));
+    }
+    return RSAC_OK;
+}
+
+static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const void *b_pts, int32_t n, const double *K,
+                           int64_t hyp_begin, int32_t H, double thr, uint64_t seed, uint32_t flags,
+                           const int32_t *subsets, int32_t *counts_out, int8_t *status_out, double *models_out,
+                           void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (H <= 0 || !counts_out || !status_out) return fail(RSAC_EINVAL, "bad arguments");
+    if (model == Model::PnP && !K) return fail(RSAC_EINVAL, "K required");
+    hipStream_t s = pick_stream(c, stream);
+    Staged st;
+    r = stage_points(c, a_pts, b_pts, model == Model::PnP ? 3 : 2, nullptr, 1, n, flags, s, st);
+    if (r) return r;
+    r = stage_tables(c, st, K, thr, s);
+    if (r) return r;
+    r = ensure_hyp_buffers(c, 1, H, subsets != nullptr);
+    if (r) return r;
+    if (subsets) {
+        int8_t *hss = c->h_substatus.as<int8_t>();
+        memcpy(c->h_subsets.p, subsets, sizeof(int32_t) * 4 * (size_t)H);
+        for (int32_t h = 0; h < H; ++h) {
+            bool ok = true;
+            for (int j = 0; j < 4; ++j) ok = ok && subsets[4 * h + j] >= 0 && subsets[4 * h + j] < n;
+            hss[h] = ok ? 1 : -1;
+        }
+        HIPCHK(hipMemcpyAsync(c->subsets.p, c->h_subsets.p, sizeof(int32_t) * 4 * (size_t)H, hipMemcpyHostToDevice,
+                              s));
+        HIPCHK(hipMemcpyAsync(c->substatus.p, hss, H, hipMemcpyHostToDevice, s));
+    }
+    if (model == Model::PnP) {
+        PnpArgs a{};
+        a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
+        a.offsets = c->offsets.as<int64_t>();
+        a.cams = c->cams.as<double>();
+        a.thr2 = c->thr2.as<float>();
+        a.models = c->models.as<double>();
+        a.status = c->status.as<int8_t>();
+        a.subsets = subsets ? c->subsets.as<int32_t>() : nullptr;
+        a.sub_status = subsets ? c->substatus.as<int8_t>() : nullptr;
+        a.hyp_stride = H;
+        a.rng_base = hyp_begin;
+        a.seed = seed;
+        HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
+        HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
+    } else {
+        HomArgs a{};
+        a.SX = st.d[0]; a.SY = st.d[1]; a.DX = st.d[2]; a.DY = st.d[3];
+        a.offsets = c->offsets.as<int64_t>();
+        a.thr2 = c->thr2.as<float>();
+        a.models = c->models.as<double>();
+        a.status = c->status.as<int8_t>();
+        a.subsets = subsets ? c->subsets.as<int32_t>() : nullptr;
+        a.sub_status = subsets ? c->substatus.as<int8_t>() : nullptr;
+        a.hyp_stride = H;
+        a.rng_base = hyp_begin;
+        a.seed = seed;
+        HIPCHK(launch_hom_solve(a, 1, 0, H, s));
+        HIPCHK(launch_hom_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
+    }
+    HIPCHK(hipMemcpyAsync(counts_out, c->counts.p, sizeof(int32_t) * H, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(status_out, c->status.p, H, hipMemcpyDeviceToHost, s));
+    if (models_out)
+        HIPCHK(hipMemcpyAsync(models_out, c->models.p, sizeof(double) * kModelStride * H, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return RSAC_OK;
+}
+
+int rsac_pnp_hypotheses(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                        int64_t hyp_begin, int32_t n_hyps, double thr, uint64_t seed, uint32_t flags,
+                        const int32_t *subsets, int32_t *counts_out, int8_t *status_out, double *models_out,
+                        void *stream) {
+    return hypotheses_core(c, Model::PnP, pts3d, pts2d, n, K, hyp_begin, n_hyps, thr, seed, flags, subsets,
+                           counts_out, status_out, models_out, stream);
+}
+
+int rsac_homography_hypotheses(rsac_ctx *c, const void *src, const void *dst, int32_t n, int64_t hyp_begin,
+                               int32_t n_hyps, double thr, uint64_t seed, uint32_t flags, const int32_t *subsets,
+                               int32_t *counts_out, int8_t *status_out, double *models_out, void *stream) {
+    return hypotheses_core(c, Model::Hom, src, dst, n, nullptr, hyp_begin, n_hyps, thr, seed, flags, subsets,
+                           counts_out, status_out, models_out, stream);
+}
+
+int rsac_pnp_mask(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                  const double model[12], double thr, uint32_t flags, uint8_t *mask_out, int32_t *count_out,
+                  void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (!model || !K) return fail(RSAC_EINVAL, "bad arguments");
+    hipStream_t s = pick_stream(c, stream);
+    Staged st;
+    r = stage_points(c, pts3d, pts2d, 3, nullptr, 1, n, flags, s, st);
+    if (r) return r;
+    r = stage_tables(c, st, K, thr, s);
+    if (r) return r;
+    r = ensure_hyp_buffers(c, 1, 1, false);
+    if (r) return r;
+    double rec[kModelStride] = {0};
+    memcpy(rec, model, 12 * sizeof(double));
+    rec[kValidSlot] = 1.0;
+    HIPCHK(hipMemcpyAsync(c->models.p, rec, sizeof rec, hipMemcpyHostToDevice, s));
+    int64_t zero = 0;
+    HIPCHK(hipMemcpyAsync(c->best.p, &zero, sizeof zero, hipMemcpyHostToDevice, s));
+    PnpArgs a{};
+    a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
+    a.offsets = c->offsets.as<int64_t>();
+    a.cams = c->cams.as<double>();
+    a.thr2 = c->thr2.as<float>();
+    a.models = c->models.as<double>();
+    uint8_t *dmask;
+    if (flags & RSAC_F_DEVICE_OUT) {
+        dmask = mask_out;
+    } else {
+        HIPCHK(c->mask.ensure(std::max(n, 1)));
+        dmask = c->mask.as<uint8_t>();
+    }
+    HIPCHK(launch_pnp_mask(a, 1, n, c->best.as<int64_t>(), dmask, s));
+    std::vector<uint8_t> hm(std::max(n, 1));
+    HIPCHK(hipMemcpyAsync(hm.data(), dmask, n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (mask_out && !(flags & RSAC_F_DEVICE_OUT)) memcpy(mask_out, hm.data(), n);
+    if (count_out) {
+        int32_t k = 0;
+        for (int i = 0; i < n; ++i) k += hm[i];
+        *count_out = k;
+    }
+    return RSAC_OK;
+}
+
+int rsac_pnp_refine(const double *pts3d, const double *pts2d, int32_t n, const double K[9], const uint8_t *mask,
+                    double R[9], double t[3], int32_t max_iter) {
+    if (n < 3 || !pts3d || !pts2d || !K || !R || !t) return fail(RSAC_EINVAL, "bad arguments");
+    std::vector<float> soa((size_t)5 * n);
+    for (int32_t i = 0; i < n; ++i) {
+        for (int k = 0; k < 3; ++k) soa[(size_t)k * n + i] = (float)pts3d[3 * i + k];
+        soa[(size_t)3 * n + i] = (float)pts2d[2 * i];
+        soa[(size_t)4 * n + i] = (float)pts2d[2 * i + 1];
+    }
+    std::vector<uint8_t> m(n, 1);
+    if (mask) memcpy(m.data(), mask, n);
+    const double cam[4] = {K[0], K[4], K[2], K[5]};
+    const float *b = soa.data();
+    return pnp_refine_lm(b, b + n, b + 2 * n, b + 3 * n, b + 4 * n, m.data(), n, cam, R, t, max_iter);
+}
+
+int rsac_homography_fit(const double *src, const double *dst, int32_t n, const uint8_t *mask, double H_out[9]) {
+    if (n < 4 || !src || !dst || !H_out) return fail(RSAC_ETOOFEW, "need >= 4 correspondences");
+    std::vector<float> soa((size_t)4 * n);
+    for (int32_t i = 0; i < n; ++i) {
+        soa[i] = (float)src[2 * i];
+        soa[(size_t)n + i] = (float)src[2 * i + 1];
+        soa[(size_t)2 * n + i] = (float)dst[2 * i];
+        soa[(size_t)3 * n + i] = (float)dst[2 * i + 1];
+    }
+    std::vector<uint8_t> m(n, 1);
+    if (mask) memcpy(m.data(), mask, n);
+    const float *b = soa.data();
+    return hom_refine(b, b + n, b + 2 * n, b + 3 * n, m.data(), n, H_out) ? RSAC_OK : RSAC_NO_MODEL;
+}
+
+void rsac_rodrigues_v2m(const double r[3], double R[9]) { rodrigues_v2m(r, R); }
+void rsac_rodrigues_m2v(const double R[9], double r[3]) { rodrigues_m2v(R, r); }
+int rsac_update_num_iters(double p, double ep, int model_points, int max_iters) {
+    return update_num_iters(p, ep, model_points, max_iters);
+}
+
+}  // extern "C"

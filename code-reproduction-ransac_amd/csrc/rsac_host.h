@@ -1,0 +1,62 @@
+// rsac_host.h -- host-side pieces of the RANSAC driver: the OpenCV MWC
+// sampler (for sampler="opencv"), RANSACUpdateNumIters, the resumable
+// sequential best-model scan, Rodrigues and the non-minimal refits.
+//
+// These run on the CPU because they are sequential by definition (the MWC
+// stream, the "first strictly greater" scan) or tiny (refits on the inliers
+// of one model).  Reference semantics: RANSACPointSetRegistrator::run /
+// getSubset (OpenCV ptsetreg.cpp) behind cv2.solvePnPRansac
+// (main_v1.py:497) and cv2.findHomography (main_v1.py:312); the refits play
+// the role of cv2.solvePnPRefineLM (main_v1.py:508) and findHomography's
+// LS + LM polish.
+#pragma once
+
+#include <stdint.h>
+
+#include <vector>
+
+namespace rsac {
+
+struct Mwc {
+    uint64_t state = ~(uint64_t)0;
+    uint32_t next() {
+        state = (uint64_t)(uint32_t)state * 4164903690u + (state >> 32);
+        return (uint32_t)state;
+    }
+    int uniform(int a, int b) { return a == b ? a : (int)(next() % (uint32_t)(b - a) + (uint32_t)a); }
+};
+
+// OpenCV getSubset sequence for H consecutive iterations; hom != nullptr
+// applies HomographyEstimatorCallback::checkSubset (sx, sy, dx, dy SoA).
+void mwc_subsets(Mwc &rng, int n, int64_t H, const float *const *hom, int32_t *out, int8_t *status);
+
+int update_num_iters(double p, double ep, int model_points, int max_iters);
+
+struct ScanState {
+    int64_t niters = 1;
+    int64_t best = -1;
+    int32_t max_good = 0;
+    int64_t iter = 0;
+    bool done = false;
+    void reset(int max_iters) {
+        niters = max_iters > 1 ? max_iters : 1;
+        best = -1; max_good = 0; iter = 0; done = false;
+    }
+};
+
+// consume hypotheses [s.iter, s.iter + count) (counts/status indexed from 0)
+void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_t count, int n, int model_points,
+               double confidence);
+
+void rodrigues_v2m(const double r[3], double R[9]);
+void rodrigues_m2v(const double R[9], double r[3]);
+
+// LM over (R, t) on masked correspondences (f32 SoA); returns iterations
+int pnp_refine_lm(const float *X, const float *Y, const float *Z, const float *U, const float *V, const uint8_t *mask,
+                  int n, const double cam[4], double R[9], double t[3], int max_iter);
+
+// least-squares normalised DLT on the inliers + 10 LM iterations
+bool hom_refine(const float *sx, const float *sy, const float *dx, const float *dy, const uint8_t *mask, int n,
+                double H[9]);
+
+}  // namespace rsac

@@ -1,0 +1,354 @@
+// rsac_host.hip -- host-side sequential parts of the driver (see rsac_host.h).
+#include "rsac_host.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <cfloat>
+
+#include "rsac_math.h"
+
+namespace rsac {
+
+void mwc_subsets(Mwc &rng, int n, int64_t H, const float *const *hom, int32_t *out, int8_t *status) {
+    for (int64_t h = 0; h < H; ++h) {
+        int32_t *idx = out + 4 * h;
+        bool found = false;
+        for (int att = 0; att < kMaxSubsetAttempts; ++att) {
+            for (int i = 0; i < 4; ++i) {
+                int r;
+                for (;;) {
+                    r = rng.uniform(0, n);
+                    bool dup = false;
+                    for (int j = 0; j < i; ++j) dup |= (idx[j] == r);
+                    if (!dup) break;
+                }
+                idx[i] = r;
+            }
+            if (hom) {
+                float sx[4], sy[4], dx[4], dy[4];
+                for (int j = 0; j < 4; ++j) {
+                    sx[j] = hom[0][idx[j]]; sy[j] = hom[1][idx[j]];
+                    dx[j] = hom[2][idx[j]]; dy[j] = hom[3][idx[j]];
+                }
+                if (!hom_check_subset(sx, sy, dx, dy)) continue;
+            }
+            found = true;
+            break;
+        }
+        status[h] = found ? 1 : -1;
+        if (!found) {
+            for (int64_t g = h + 1; g < H; ++g) status[g] = -1;
+            return;
+        }
+    }
+}
+
+int update_num_iters(double p, double ep, int model_points, int max_iters) {
+    if (model_points <= 0) return -1;
+    p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
+    double num = 1. - p;
+    if (num < DBL_MIN) num = DBL_MIN;
+    double denom = 1. - pow(1. - ep, model_points);
+    if (denom < DBL_MIN) return 0;
+    num = log(num);
+    denom = log(denom);
+    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)lrint(num / denom);
+}
+
+void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_t count, int n, int model_points,
+               double confidence) {
+    if (s.done) return;
+    const int64_t begin = s.iter;
+    int64_t i = begin;
+    for (; i < begin + count; ++i) {
+        if (i >= s.niters) break;
+        const int8_t st = status[i - begin];
+        if (st < 0) { s.done = true; break; }
+        if (st == 0) continue;
+        const int32_t c = counts[i - begin];
+        const int32_t floor_c = s.max_good > model_points - 1 ? s.max_good : model_points - 1;
+        if (c > floor_c) {
+            s.best = i;
+            s.max_good = c;
+            s.niters = update_num_iters(confidence, (double)(n - c) / n, model_points, (int)s.niters);
+        }
+    }
+    s.iter = i;
+    if (i >= s.niters) s.done = true;
+}
+
+void rodrigues_v2m(const double r[3], double R[9]) {
+    double th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    if (th < DBL_EPSILON) {
+        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    double c = cos(th), s = sin(th), c1 = 1. - c, it = 1. / th;
+    double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+    R[0] = c + c1 * x * x;     R[1] = c1 * x * y - s * z; R[2] = c1 * x * z + s * y;
+    R[3] = c1 * x * y + s * z; R[4] = c + c1 * y * y;     R[5] = c1 * y * z - s * x;
+    R[6] = c1 * x * z - s * y; R[7] = c1 * y * z + s * x; R[8] = c + c1 * z * z;
+}
+
+void rodrigues_m2v(const double R[9], double r[3]) {
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double th = acos(c);
+    if (s < 1e-5) {
+        if (c > 0) { r[0] = r[1] = r[2] = 0; return; }
+        double t;
+        t = (R[0] + 1) * 0.5; rx = sqrt(t > 0 ? t : 0);
+        t = (R[4] + 1) * 0.5; ry = sqrt(t > 0 ? t : 0) * (R[1] < 0 ? -1. : 1.);
+        t = (R[8] + 1) * 0.5; rz = sqrt(t > 0 ? t : 0) * (R[2] < 0 ? -1. : 1.);
+        if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+        double nn = sqrt(rx * rx + ry * ry + rz * rz);
+        th = th / nn;
+        r[0] = rx * th; r[1] = ry * th; r[2] = rz * th;
+        return;
+    }
+    double vth = 1 / (2 * s) * th;
+    r[0] = rx * vth; r[1] = ry * vth; r[2] = rz * vth;
+}
+
+// (A + lam diag(A)) x = b, A n x n SPD (row-major), Cholesky
+static bool chol_solve(int n, const double *A, double lam, const double *b, double *x) {
+    double L[81], y[9];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double s = A[i * n + j];
+            if (i == j) s = s + lam * A[i * n + i];
+            for (int k = 0; k < j; ++k) s = s - L[i * n + k] * L[j * n + k];
+            if (i == j) {
+                if (!(s > 0)) return false;
+                L[i * n + i] = sqrt(s);
+            } else {
+                L[i * n + j] = s / L[j * n + j];
+            }
+        }
+    for (int i = 0; i < n; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s = s - L[i * n + k] * y[k];
+        y[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double s = y[i];
+        for (int k = i + 1; k < n; ++k) s = s - L[k * n + i] * x[k];
+        x[i] = s / L[i * n + i];
+    }
+    return true;
+}
+
+static double pnp_cost(const double R[9], const double t[3], const double cam[4], const float *X, const float *Y,
+                       const float *Z, const float *U, const float *V, const uint8_t *mask, int n) {
+    double cost = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!mask[i]) continue;
+        double Xd = X[i], Yd = Y[i], Zd = Z[i];
+        double x = R[0] * Xd + R[1] * Yd + R[2] * Zd + t[0];
+        double y = R[3] * Xd + R[4] * Yd + R[5] * Zd + t[1];
+        double z = R[6] * Xd + R[7] * Yd + R[8] * Zd + t[2];
+        double iz = 1.0 / z;
+        double ru = cam[0] * x * iz + cam[2] - U[i];
+        double rv = cam[1] * y * iz + cam[3] - V[i];
+        cost += ru * ru + rv * rv;
+    }
+    return cost;
+}
+
+int pnp_refine_lm(const float *X, const float *Y, const float *Z, const float *U, const float *V, const uint8_t *mask,
+                  int n, const double cam[4], double R[9], double t[3], int max_iter) {
+    double lam = 1e-3;
+    double cost = pnp_cost(R, t, cam, X, Y, Z, U, V, mask, n);
+    int it;
+    for (it = 0; it < max_iter; ++it) {
+        double A[36] = {0}, g[6] = {0};
+        for (int i = 0; i < n; ++i) {
+            if (!mask[i]) continue;
+            double Xd = X[i], Yd = Y[i], Zd = Z[i];
+            double px = R[0] * Xd + R[1] * Yd + R[2] * Zd;
+            double py = R[3] * Xd + R[4] * Yd + R[5] * Zd;
+            double pz = R[6] * Xd + R[7] * Yd + R[8] * Zd;
+            double cx = px + t[0], cy = py + t[1], cz = pz + t[2];
+            double iz = 1.0 / cz;
+            double ru = cam[0] * cx * iz + cam[2] - U[i];
+            double rv = cam[1] * cy * iz + cam[3] - V[i];
+            double dux = cam[0] * iz, duz = -cam[0] * cx * iz * iz;
+            double dvy = cam[1] * iz, dvz = -cam[1] * cy * iz * iz;
+            double Ju[6], Jv[6];
+            Ju[0] = duz * py;             Ju[1] = dux * pz - duz * px; Ju[2] = -dux * py;
+            Jv[0] = -dvy * pz + dvz * py; Jv[1] = -dvz * px;           Jv[2] = dvy * px;
+            Ju[3] = dux; Ju[4] = 0; Ju[5] = duz;
+            Jv[3] = 0; Jv[4] = dvy; Jv[5] = dvz;
+            for (int a = 0; a < 6; ++a) {
+                g[a] += Ju[a] * ru + Jv[a] * rv;
+                for (int b = 0; b <= a; ++b) A[a * 6 + b] += Ju[a] * Ju[b] + Jv[a] * Jv[b];
+            }
+        }
+        for (int a = 0; a < 6; ++a)
+            for (int b = a + 1; b < 6; ++b) A[a * 6 + b] = A[b * 6 + a];
+        bool accepted = false;
+        while (!accepted) {
+            double d[6], mg[6];
+            for (int a = 0; a < 6; ++a) mg[a] = -g[a];
+            if (!chol_solve(6, A, lam, mg, d)) {
+                lam *= 10;
+                if (lam > 1e10) return it;
+                continue;
+            }
+            double Rw[9], Rn[9], tn[3];
+            rodrigues_v2m(d, Rw);
+            mat3mul(Rw, R, Rn);
+            for (int k = 0; k < 3; ++k) tn[k] = t[k] + d[3 + k];
+            double cn = pnp_cost(Rn, tn, cam, X, Y, Z, U, V, mask, n);
+            if (cn < cost) {
+                double rel = (cost - cn) / (cost > 1e-300 ? cost : 1e-300);
+                memcpy(R, Rn, sizeof(Rn));
+                memcpy(t, tn, sizeof(tn));
+                cost = cn;
+                lam = lam * 0.1 > 1e-12 ? lam * 0.1 : 1e-12;
+                accepted = true;
+                if (rel < 1e-12) return it + 1;
+            } else {
+                lam *= 10;
+                if (lam > 1e10) return it;
+            }
+        }
+    }
+    return it;
+}
+
+static void jacobi_min_evec(int n, double *A, double *v_out) {
+    double V[81];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0;
+        for (int i = 0; i < n; ++i)
+            for (int j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
+        if (off < 1e-300) break;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                double apq = A[p * n + q];
+                if (fabs(apq) < 1e-300) continue;
+                double app = A[p * n + p], aqq = A[q * n + q];
+                double theta = (aqq - app) / (2.0 * apq);
+                double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
+                for (int k = 0; k < n; ++k) {
+                    double akp = A[k * n + p], akq = A[k * n + q];
+                    A[k * n + p] = c * akp - s * akq;
+                    A[k * n + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double apk = A[p * n + k], aqk = A[q * n + k];
+                    A[p * n + k] = c * apk - s * aqk;
+                    A[q * n + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double vkp = V[k * n + p], vkq = V[k * n + q];
+                    V[k * n + p] = c * vkp - s * vkq;
+                    V[k * n + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    int mi = 0;
+    for (int i = 1; i < n; ++i)
+        if (A[i * n + i] < A[mi * n + mi]) mi = i;
+    for (int k = 0; k < n; ++k) v_out[k] = V[k * n + mi];
+}
+
+static double hom_cost(const double h[9], const float *sx, const float *sy, const float *dx, const float *dy,
+                       const uint8_t *mask, int n) {
+    double c = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!mask[i]) continue;
+        double x = sx[i], y = sy[i];
+        double ww = 1. / (h[6] * x + h[7] * y + 1.);
+        double ex = (h[0] * x + h[1] * y + h[2]) * ww - dx[i];
+        double ey = (h[3] * x + h[4] * y + h[5]) * ww - dy[i];
+        c += ex * ex + ey * ey;
+    }
+    return c;
+}
+
+bool hom_refine(const float *sx, const float *sy, const float *dx, const float *dy, const uint8_t *mask, int n,
+                double H[9]) {
+    std::vector<int32_t> idx;
+    for (int i = 0; i < n; ++i)
+        if (mask[i]) idx.push_back(i);
+    const int m = (int)idx.size();
+    if (m < 4) return false;
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+    for (int i = 0; i < m; ++i) {
+        int p = idx[i];
+        cmx += dx[p]; cmy += dy[p]; cMx += sx[p]; cMy += sy[p];
+    }
+    cmx /= m; cmy /= m; cMx /= m; cMy /= m;
+    for (int i = 0; i < m; ++i) {
+        int p = idx[i];
+        smx += fabs(dx[p] - cmx); smy += fabs(dy[p] - cmy);
+        sMx += fabs(sx[p] - cMx); sMy += fabs(sy[p] - cMy);
+    }
+    if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON || fabs(sMy) < DBL_EPSILON)
+        return false;
+    smx = m / smx; smy = m / smy; sMx = m / sMx; sMy = m / sMy;
+    double LtL[81] = {0};
+    for (int i = 0; i < m; ++i) {
+        int p = idx[i];
+        double x = (dx[p] - cmx) * smx, y = (dy[p] - cmy) * smy;
+        double X = (sx[p] - cMx) * sMx, Y = (sy[p] - cMy) * sMy;
+        double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
+        double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
+        for (int j = 0; j < 9; ++j)
+            for (int k = j; k < 9; ++k) LtL[j * 9 + k] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+    }
+    for (int j = 0; j < 9; ++j)
+        for (int k = 0; k < j; ++k) LtL[j * 9 + k] = LtL[k * 9 + j];
+    double hv[9];
+    jacobi_min_evec(9, LtL, hv);
+    double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+    double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+    double T[9], H0[9];
+    mat3mul(invHnorm, hv, T);
+    mat3mul(T, Hnorm2, H0);
+    double sc = 1. / H0[8];
+    for (int k = 0; k < 9; ++k) H[k] = H0[k] * sc;
+    double lam = 1e-3;
+    double cost = hom_cost(H, sx, sy, dx, dy, mask, n);
+    for (int it = 0; it < 10; ++it) {
+        double A[64] = {0}, g[8] = {0};
+        for (int i = 0; i < n; ++i) {
+            if (!mask[i]) continue;
+            double x = sx[i], y = sy[i];
+            double den = H[6] * x + H[7] * y + 1.;
+            double ww = 1. / den;
+            double Xi = (H[0] * x + H[1] * y + H[2]) * ww;
+            double Yi = (H[3] * x + H[4] * y + H[5]) * ww;
+            double ex = Xi - dx[i], ey = Yi - dy[i];
+            double Jx[8] = {x * ww, y * ww, ww, 0, 0, 0, -Xi * x * ww, -Xi * y * ww};
+            double Jy[8] = {0, 0, 0, x * ww, y * ww, ww, -Yi * x * ww, -Yi * y * ww};
+            for (int a = 0; a < 8; ++a) {
+                g[a] += Jx[a] * ex + Jy[a] * ey;
+                for (int b = 0; b <= a; ++b) A[a * 8 + b] += Jx[a] * Jx[b] + Jy[a] * Jy[b];
+            }
+        }
+        for (int a = 0; a < 8; ++a)
+            for (int b = a + 1; b < 8; ++b) A[a * 8 + b] = A[b * 8 + a];
+        double d[8], mg[8];
+        for (int a = 0; a < 8; ++a) mg[a] = -g[a];
+        if (!chol_solve(8, A, lam, mg, d)) { lam *= 10; continue; }
+        double Hn[9];
+        for (int a = 0; a < 8; ++a) Hn[a] = H[a] + d[a];
+        Hn[8] = 1.0;
+        double cn = hom_cost(Hn, sx, sy, dx, dy, mask, n);
+        if (cn < cost) { memcpy(H, Hn, sizeof(Hn)); cost = cn; lam *= 0.1; }
+        else lam *= 10;
+    }
+    return true;
+}
+
+}  // namespace rsac

@@ -1,0 +1,475 @@
+// rsac_math.h -- host+device arithmetic of the RANSAC hot path.
+//
+// Everything here decides inlier counts, so it is written to one numerics
+// contract (DESIGN.md "Numerics"): compiled with -ffp-contract=off, only
+// + - * / sqrt (IEEE, correctly rounded on gfx950 and x86-64), no FMA unless
+// written explicitly.  The CPU restatement in oracle/ follows the same
+// contract and the GPU results are checked against it bit-for-bit.
+//
+// Reference call sites served: cv2.solvePnPRansac (main_v1.py:497,
+// testpro-K.py:72), cv2.findHomography (main_v1.py:312, process.py:200),
+// cv2.projectPoints (testpro-K.py:33).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RSAC_HD __host__ __device__ __forceinline__
+
+namespace rsac {
+
+constexpr int kMaxDrawsPerSubset = 256;
+constexpr int kMaxSubsetAttempts = 10000;  // getSubset(..., rng, 10000) of RANSACPointSetRegistrator::run
+constexpr int kModelStride = 16;           // doubles per hypothesis record (R 9, t 3, valid, pad 3) / (H 9, valid@12)
+constexpr int kValidSlot = 12;
+
+RSAC_HD bool dfinite(double v) { return __builtin_isfinite(v); }
+RSAC_HD double dabs(double v) { return __builtin_fabs(v); }
+RSAC_HD double dsqrt(double v) { return __builtin_sqrt(v); }
+
+// ---------------------------------------------------------------------------
+// Philox-4x32-10: counter (hyp_lo, hyp_hi, problem, block), key = seed.
+// ---------------------------------------------------------------------------
+struct Philox {
+    uint32_t k0, k1, c0, c1, c2, c3;
+    uint32_t b[4];
+    int pos;
+
+    RSAC_HD void init(uint64_t seed, uint32_t problem, uint64_t hyp) {
+        k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32);
+        c0 = (uint32_t)hyp; c1 = (uint32_t)(hyp >> 32); c2 = problem; c3 = 0;
+        pos = 4;
+    }
+    RSAC_HD void block() {
+        uint32_t x0 = c0, x1 = c1, x2 = c2, x3 = c3, q0 = k0, q1 = k1;
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            uint64_t p0 = (uint64_t)0xD2511F53u * x0;
+            uint64_t p1 = (uint64_t)0xCD9E8D57u * x2;
+            uint32_t n0 = (uint32_t)(p1 >> 32) ^ x1 ^ q0;
+            uint32_t n1 = (uint32_t)p1;
+            uint32_t n2 = (uint32_t)(p0 >> 32) ^ x3 ^ q1;
+            uint32_t n3 = (uint32_t)p0;
+            x0 = n0; x1 = n1; x2 = n2; x3 = n3;
+            q0 += 0x9E3779B9u; q1 += 0xBB67AE85u;
+        }
+        b[0] = x0; b[1] = x1; b[2] = x2; b[3] = x3;
+        c3 += 1u;
+        pos = 0;
+    }
+    RSAC_HD uint32_t next() {
+        if (pos == 4) block();
+        uint32_t v = pos == 0 ? b[0] : pos == 1 ? b[1] : pos == 2 ? b[2] : b[3];
+        ++pos;
+        return v;
+    }
+    RSAC_HD int index(int n) { return (int)(((uint64_t)next() * (uint64_t)(uint32_t)n) >> 32); }
+
+    // s distinct indices, -1 once the per-subset draw budget is spent
+    template <int S>
+    RSAC_HD int subset(int n, int32_t (&idx)[S]) {
+        int draws = 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            for (;;) {
+                if (draws++ >= kMaxDrawsPerSubset) return -1;
+                int r = index(n);
+                bool dup = false;
+#pragma unroll
+                for (int j = 0; j < S; ++j) dup |= (j < i) && (idx[j] == r);
+                if (!dup) { idx[i] = r; break; }
+            }
+        }
+        return 0;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// PnP reprojection error: projectPoints (f64 from f32-rounded inputs, zero
+// distortion), rounded to f32, squared distance in f32.
+// ---------------------------------------------------------------------------
+struct Cam {
+    double fx, fy, cx, cy;
+};
+
+RSAC_HD float pnp_err(const double *R, const double *t, const Cam &k, double X, double Y, double Z, float uf,
+                      float vf) {
+    double x = R[0] * X + R[1] * Y; x = x + R[2] * Z; x = x + t[0];
+    double y = R[3] * X + R[4] * Y; y = y + R[5] * Z; y = y + t[1];
+    double z = R[6] * X + R[7] * Y; z = z + R[8] * Z; z = z + t[2];
+    double iz = (z != 0.0) ? 1.0 / z : 1.0;
+    x = x * iz; y = y * iz;
+    double pu = x * k.fx + k.cx;
+    double pv = y * k.fy + k.cy;
+    float dx = uf - (float)pu;
+    float dy = vf - (float)pv;
+    float e1 = dx * dx, e2 = dy * dy;
+    return e1 + e2;
+}
+
+// ---------------------------------------------------------------------------
+// P3P, Lambda Twist (Persson & Nordberg, ECCV 2018).
+// ---------------------------------------------------------------------------
+RSAC_HD void root2real(double b, double c, double &r1, double &r2) {
+    double v = b * b - 4.0 * c;
+    if (v < 0.0) { r1 = 0.5 * b; r2 = 0.5 * b; return; }
+    double y = dsqrt(v);
+    if (b < 0.0) { r1 = 0.5 * (-b + y); r2 = 2.0 * c / (-b + y); }
+    else { r1 = 2.0 * c / (-b - y); r2 = 0.5 * (-b - y); }
+}
+
+RSAC_HD double cubic_root(double b, double c, double d) {
+    double r0;
+    if (b * b >= 3.0 * c) {
+        double v = dsqrt(b * b - 3.0 * c);
+        double t1 = (-b - v) / 3.0;
+        double k = ((t1 + b) * t1 + c) * t1 + d;
+        if (k > 0.0) {
+            r0 = t1 - dsqrt(-k / (3.0 * t1 + b));
+        } else {
+            double t2 = (-b + v) / 3.0;
+            k = ((t2 + b) * t2 + c) * t2 + d;
+            r0 = t2 + dsqrt(-k / (3.0 * t2 + b));
+        }
+    } else {
+        r0 = -b / 3.0;
+        if (dabs((3.0 * r0 + 2.0 * b) * r0 + c) < 1e-4) r0 = r0 + 1.0;
+    }
+    for (int it = 0; it < 50; ++it) {
+        double fx = ((r0 + b) * r0 + c) * r0 + d;
+        if (it >= 7 && !(dabs(fx) > 1e-13)) break;
+        double fpx = (3.0 * r0 + 2.0 * b) * r0 + c;
+        r0 = r0 - fx / fpx;
+    }
+    return r0;
+}
+
+RSAC_HD double lt_resid(double l1, double l2, double l3, double a12, double a13, double a23, double b12, double b13,
+                        double b23, double &r0, double &r1, double &r2) {
+    r0 = l1 * l1 + l2 * l2 + b12 * l1 * l2 - a12;
+    r1 = l1 * l1 + l3 * l3 + b13 * l1 * l3 - a13;
+    r2 = l2 * l2 + l3 * l3 + b23 * l2 * l3 - a23;
+    return dabs(r0) + dabs(r1) + dabs(r2);
+}
+
+RSAC_HD void lt_refine(double &L0, double &L1, double &L2, double a12, double a13, double a23, double b12,
+                       double b13, double b23) {
+    for (int it = 0; it < 5; ++it) {
+        double r0, r1, r2;
+        double s0 = lt_resid(L0, L1, L2, a12, a13, a23, b12, b13, b23, r0, r1, r2);
+        if (s0 < 1e-10) break;
+        double l1 = L0, l2 = L1, l3 = L2;
+        double j0 = 2.0 * l1 + b12 * l2;
+        double j1 = 2.0 * l2 + b12 * l1;
+        double j3 = 2.0 * l1 + b13 * l3;
+        double j5 = 2.0 * l3 + b13 * l1;
+        double j7 = 2.0 * l2 + b23 * l3;
+        double j8 = 2.0 * l3 + b23 * l2;
+        double det = 1.0 / (-j0 * j5 * j7 - j1 * j3 * j8);
+        double d0 = -j5 * j7 * r0 + -j1 * j8 * r1 + j1 * j5 * r2;
+        double d1 = -j3 * j8 * r0 + j0 * j8 * r1 + -j0 * j5 * r2;
+        double d2 = j3 * j7 * r0 + -j0 * j7 * r1 + -j1 * j3 * r2;
+        double n0 = l1 - det * d0, n1 = l2 - det * d1, n2 = l3 - det * d2;
+        double q0, q1, q2;
+        double s1 = lt_resid(n0, n1, n2, a12, a13, a23, b12, b13, b23, q0, q1, q2);
+        if (s1 > s0) break;
+        L0 = n0; L1 = n1; L2 = n2;
+    }
+}
+
+// y: 3 unit bearings (row-major 3x3), x: 3 world points.  Writes up to 4
+// (R, t); returns the count.
+RSAC_HD int p3p_lambdatwist(const double *y, const double *x, double *Rs, double *ts) {
+    const double *y1 = y, *y2 = y + 3, *y3 = y + 6;
+    const double *x1 = x, *x2 = x + 3, *x3 = x + 6;
+    double b12 = -2.0 * (y1[0] * y2[0] + y1[1] * y2[1] + y1[2] * y2[2]);
+    double b13 = -2.0 * (y1[0] * y3[0] + y1[1] * y3[1] + y1[2] * y3[2]);
+    double b23 = -2.0 * (y2[0] * y3[0] + y2[1] * y3[1] + y2[2] * y3[2]);
+    double d12[3], d13[3], d23[3], d12xd13[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { d12[k] = x1[k] - x2[k]; d13[k] = x1[k] - x3[k]; d23[k] = x2[k] - x3[k]; }
+    d12xd13[0] = d12[1] * d13[2] - d12[2] * d13[1];
+    d12xd13[1] = d12[2] * d13[0] - d12[0] * d13[2];
+    d12xd13[2] = d12[0] * d13[1] - d12[1] * d13[0];
+    double a12 = d12[0] * d12[0] + d12[1] * d12[1] + d12[2] * d12[2];
+    double a13 = d13[0] * d13[0] + d13[1] * d13[1] + d13[2] * d13[2];
+    double a23 = d23[0] * d23[0] + d23[1] * d23[1] + d23[2] * d23[2];
+
+    double c31 = -0.5 * b13, c23 = -0.5 * b23, c12 = -0.5 * b12;
+    double blob = c12 * c23 * c31 - 1.0;
+    double s31 = 1.0 - c31 * c31, s23 = 1.0 - c23 * c23, s12 = 1.0 - c12 * c12;
+    double p3 = a13 * (a23 * s31 - a13 * s23);
+    double p2 = 2.0 * blob * a23 * a13 + a13 * (2.0 * a12 + a13) * s23 + a23 * (a23 - a12) * s31;
+    double p1 = a23 * (a13 - a23) * s12 - a12 * a12 * s23 - 2.0 * a12 * (blob * a23 + a13 * s23);
+    double p0 = a12 * (a12 * s23 - a23 * s12);
+    if (p3 == 0.0 || !dfinite(p3)) return 0;
+    double ip3 = 1.0 / p3;
+    p2 = p2 * ip3; p1 = p1 * ip3; p0 = p0 * ip3;
+    double g = cubic_root(p2, p1, p0);
+
+    double A00 = a23 * (1.0 - g);
+    double A01 = (a23 * b12) * 0.5;
+    double A02 = (a23 * b13 * g) * (-0.5);
+    double A11 = a23 - a12 + a13 * g;
+    double A12 = b23 * (a13 * g - a12) * 0.5;
+    double A22 = g * (a13 - a23) - a12;
+
+    // eigenvectors of the two non-zero eigenvalues (the third is 0)
+    double v1[3], v2[3], e1, e2;
+    {
+        double a01sq = A01 * A01;
+        double b = -A00 - A11 - A22;
+        double c = -a01sq - A02 * A02 - A12 * A12 + A00 * (A11 + A22) + A11 * A22;
+        root2real(b, c, e1, e2);
+        if (dabs(e1) < dabs(e2)) { double tmp = e1; e1 = e2; e2 = tmp; }
+        double m0011 = -A00 * A11;
+        double pr0 = A01 * A12 - A02 * A11;
+        double pr1 = A01 * A02 - A00 * A12;
+        {
+            double e = e1;
+            double tmp = 1.0 / (e * (A00 + A11) + m0011 - e * e + a01sq);
+            double q1 = -(e * A02 + pr0) * tmp;
+            double q2 = -(e * A12 + pr1) * tmp;
+            double rn = 1.0 / dsqrt(q1 * q1 + q2 * q2 + 1.0);
+            v1[0] = q1 * rn; v1[1] = q2 * rn; v1[2] = rn;
+        }
+        {
+            double e = e2;
+            double tmp = 1.0 / (e * (A00 + A11) + m0011 - e * e + a01sq);
+            double q1 = -(e * A02 + pr0) * tmp;
+            double q2 = -(e * A12 + pr1) * tmp;
+            double rn = 1.0 / dsqrt(q1 * q1 + q2 * q2 + 1.0);
+            v2[0] = q1 * rn; v2[1] = q2 * rn; v2[2] = rn;
+        }
+    }
+    double vq = -e2 / e1;
+    double v = dsqrt(vq > 0.0 ? vq : 0.0);
+
+    double Ls[4][3];
+    int valid = 0;
+    for (int sgn = 0; sgn < 2; ++sgn) {
+        double s = sgn == 0 ? v : -v;
+        double w2 = 1.0 / (s * v2[0] - v1[0]);
+        double w0 = (v1[1] - s * v2[1]) * w2;
+        double w1 = (v1[2] - s * v2[2]) * w2;
+        double a = 1.0 / ((a13 - a12) * w1 * w1 - a12 * b13 * w1 - a12);
+        double b = (a13 * b12 * w1 - a12 * b13 * w0 - 2.0 * w0 * w1 * (a12 - a13)) * a;
+        double c = ((a13 - a12) * w0 * w0 + a13 * b12 * w0 + a13) * a;
+        if (b * b - 4.0 * c >= 0.0) {
+            double tau[2];
+            root2real(b, c, tau[0], tau[1]);
+            for (int q = 0; q < 2; ++q) {
+                if (tau[q] > 0.0) {
+                    double tq = tau[q];
+                    double d = a23 / (tq * (b23 + tq) + 1.0);
+                    if (d > 0.0) {
+                        double l2 = dsqrt(d);
+                        double l3 = tq * l2;
+                        double l1 = w0 * l2 + w1 * l3;
+                        if (l1 >= 0.0) { Ls[valid][0] = l1; Ls[valid][1] = l2; Ls[valid][2] = l3; ++valid; }
+                    }
+                }
+            }
+        }
+    }
+    for (int i = 0; i < valid; ++i) lt_refine(Ls[i][0], Ls[i][1], Ls[i][2], a12, a13, a23, b12, b13, b23);
+
+    // X = [d12 d13 d12xd13] (columns), its inverse by the adjugate
+    double M[9] = {d12[0], d13[0], d12xd13[0], d12[1], d13[1], d12xd13[1], d12[2], d13[2], d12xd13[2]};
+    double Xi[9];
+    {
+        double c00 = M[4] * M[8] - M[5] * M[7];
+        double c01 = M[5] * M[6] - M[3] * M[8];
+        double c02 = M[3] * M[7] - M[4] * M[6];
+        double det = M[0] * c00 + M[1] * c01 + M[2] * c02;
+        if (det == 0.0 || !dfinite(det)) return 0;
+        double id = 1.0 / det;
+        Xi[0] = c00 * id; Xi[1] = (M[2] * M[7] - M[1] * M[8]) * id; Xi[2] = (M[1] * M[5] - M[2] * M[4]) * id;
+        Xi[3] = c01 * id; Xi[4] = (M[0] * M[8] - M[2] * M[6]) * id; Xi[5] = (M[2] * M[3] - M[0] * M[5]) * id;
+        Xi[6] = c02 * id; Xi[7] = (M[1] * M[6] - M[0] * M[7]) * id; Xi[8] = (M[0] * M[4] - M[1] * M[3]) * id;
+    }
+    int nout = 0;
+    for (int i = 0; i < valid; ++i) {
+        double ry1[3], ry2[3], ry3[3], yd1[3], yd2[3], yc[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { ry1[k] = y1[k] * Ls[i][0]; ry2[k] = y2[k] * Ls[i][1]; ry3[k] = y3[k] * Ls[i][2]; }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { yd1[k] = ry1[k] - ry2[k]; yd2[k] = ry1[k] - ry3[k]; }
+        yc[0] = yd1[1] * yd2[2] - yd1[2] * yd2[1];
+        yc[1] = yd1[2] * yd2[0] - yd1[0] * yd2[2];
+        yc[2] = yd1[0] * yd2[1] - yd1[1] * yd2[0];
+        double Y[9] = {yd1[0], yd2[0], yc[0], yd1[1], yd2[1], yc[1], yd1[2], yd2[2], yc[2]};
+        double *R = Rs + 9 * nout, *t = ts + 3 * nout;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc)
+                R[3 * r + cc] = Y[3 * r] * Xi[cc] + Y[3 * r + 1] * Xi[3 + cc] + Y[3 * r + 2] * Xi[6 + cc];
+        bool fin = true;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            double rx = R[3 * r] * x1[0] + R[3 * r + 1] * x1[1] + R[3 * r + 2] * x1[2];
+            t[r] = ry1[r] - rx;
+            fin = fin && dfinite(t[r]);
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) fin = fin && dfinite(R[k]);
+        if (fin) ++nout;
+    }
+    return nout;
+}
+
+RSAC_HD void bearing(const Cam &k, float uf, float vf, double *out) {
+    double xn = ((double)uf - k.cx) / k.fx;
+    double yn = ((double)vf - k.cy) / k.fy;
+    double nrm = dsqrt(xn * xn + yn * yn + 1.0);
+    out[0] = xn / nrm; out[1] = yn / nrm; out[2] = 1.0 / nrm;
+}
+
+// 4-point minimal PnP: P3P on the first three, disambiguated by the fourth.
+// pts: per sample point (X, Y, Z, u, v) already gathered.
+RSAC_HD bool pnp_minimal(const float (&X)[4], const float (&Y)[4], const float (&Z)[4], const float (&U)[4],
+                         const float (&V)[4], const Cam &k, double *R, double *t) {
+    double yb[9], xw[9];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        bearing(k, U[j], V[j], yb + 3 * j);
+        xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
+    }
+    double Rs[36], ts[12];
+    int ns = p3p_lambdatwist(yb, xw, Rs, ts);
+    if (ns == 0) return false;
+    double X4 = X[3], Y4 = Y[3], Z4 = Z[3];
+    int best = -1;
+    double best_e = 0.0;
+    for (int s = 0; s < ns; ++s) {
+        const double *Rk = Rs + 9 * s, *tk = ts + 3 * s;
+        double x = Rk[0] * X4 + Rk[1] * Y4; x = x + Rk[2] * Z4; x = x + tk[0];
+        double y = Rk[3] * X4 + Rk[4] * Y4; y = y + Rk[5] * Z4; y = y + tk[1];
+        double z = Rk[6] * X4 + Rk[7] * Y4; z = z + Rk[8] * Z4; z = z + tk[2];
+        double iz = (z != 0.0) ? 1.0 / z : 1.0;
+        double du = (x * iz) * k.fx + k.cx - (double)U[3];
+        double dv = (y * iz) * k.fy + k.cy - (double)V[3];
+        double e = du * du + dv * dv;
+        if (!(e == e)) continue;
+        if (best < 0 || e < best_e) { best = s; best_e = e; }
+    }
+    if (best < 0) return false;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) R[q] = Rs[9 * best + q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) t[q] = ts[3 * best + q];
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Homography (HomographyEstimatorCallback): checkSubset, minimal solver,
+// f32 error.
+// ---------------------------------------------------------------------------
+RSAC_HD bool have_collinear4(const float (&px)[4], const float (&py)[4]) {
+    // only the last point against every pair of earlier ones (count = 4)
+    const int i = 3;
+    for (int j = 0; j < i; ++j) {
+        double dx1 = (double)(px[j] - px[i]);
+        double dy1 = (double)(py[j] - py[i]);
+        for (int q = 0; q < j; ++q) {
+            double dx2 = (double)(px[q] - px[i]);
+            double dy2 = (double)(py[q] - py[i]);
+            if (dabs(dx2 * dy1 - dy2 * dx1) <= 1.1920928955078125e-07 * (dabs(dx1) + dabs(dy1) + dabs(dx2) + dabs(dy2)))
+                return true;
+        }
+    }
+    return false;
+}
+
+RSAC_HD double det3_rows(double a0, double a1, double b0, double b1, double c0, double c1) {
+    return a0 * (b1 * 1. - c1 * 1.) - a1 * (b0 * 1. - c0 * 1.) + 1. * (b0 * c1 - c0 * b1);
+}
+
+RSAC_HD bool hom_check_subset(const float (&sx)[4], const float (&sy)[4], const float (&dx)[4], const float (&dy)[4]) {
+    if (have_collinear4(sx, sy) || have_collinear4(dx, dy)) return false;
+    const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
+    int negative = 0;
+    for (int i = 0; i < 4; ++i) {
+        int p0 = tt[i][0], p1 = tt[i][1], p2 = tt[i][2];
+        double dA = det3_rows(sx[p0], sy[p0], sx[p1], sy[p1], sx[p2], sy[p2]);
+        double dB = det3_rows(dx[p0], dy[p0], dx[p1], dy[p1], dx[p2], dy[p2]);
+        negative += dA * dB < 0;
+    }
+    return negative == 0 || negative == 4;
+}
+
+RSAC_HD void mat3mul(const double *A, const double *B, double *C) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+// normalised 4-point DLT, 8x8 Gaussian elimination with partial pivoting
+RSAC_HD bool hom_minimal(const float (&sx)[4], const float (&sy)[4], const float (&dx)[4], const float (&dy)[4],
+                         double *H) {
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { cmx += dx[i]; cmy += dy[i]; cMx += sx[i]; cMy += sy[i]; }
+    cmx /= 4; cmy /= 4; cMx /= 4; cMy /= 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        smx += dabs(dx[i] - cmx); smy += dabs(dy[i] - cmy);
+        sMx += dabs(sx[i] - cMx); sMy += dabs(sy[i] - cMy);
+    }
+    const double eps = 2.220446049250313e-16;
+    if (dabs(smx) < eps || dabs(smy) < eps || dabs(sMx) < eps || dabs(sMy) < eps) return false;
+    smx = 4 / smx; smy = 4 / smy; sMx = 4 / sMx; sMy = 4 / sMy;
+    double A[8][9];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double x = (dx[i] - cmx) * smx, y = (dy[i] - cmy) * smy;
+        double X = (sx[i] - cMx) * sMx, Y = (sy[i] - cMy) * sMy;
+        double *r0 = A[2 * i], *r1 = A[2 * i + 1];
+        r0[0] = X; r0[1] = Y; r0[2] = 1; r0[3] = 0; r0[4] = 0; r0[5] = 0; r0[6] = -x * X; r0[7] = -x * Y; r0[8] = x;
+        r1[0] = 0; r1[1] = 0; r1[2] = 0; r1[3] = X; r1[4] = Y; r1[5] = 1; r1[6] = -y * X; r1[7] = -y * Y; r1[8] = y;
+    }
+    for (int k = 0; k < 8; ++k) {
+        int piv = k;
+        double pm = dabs(A[k][k]);
+        for (int r = k + 1; r < 8; ++r) {
+            double v = dabs(A[r][k]);
+            if (v > pm) { pm = v; piv = r; }
+        }
+        if (!(pm > 1e-10)) return false;
+        if (piv != k)
+            for (int j = 0; j < 9; ++j) { double tmp = A[k][j]; A[k][j] = A[piv][j]; A[piv][j] = tmp; }
+        for (int r = k + 1; r < 8; ++r) {
+            double f = A[r][k] / A[k][k];
+            for (int j = k + 1; j < 9; ++j) A[r][j] = A[r][j] - f * A[k][j];
+        }
+    }
+    double h[8];
+    for (int k = 7; k >= 0; --k) {
+        double s = A[k][8];
+        for (int j = k + 1; j < 8; ++j) s = s - A[k][j] * h[j];
+        h[k] = s / A[k][k];
+    }
+    double Hn[9] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], 1.0};
+    double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+    double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+    double T[9], H0[9];
+    mat3mul(invHnorm, Hn, T);
+    mat3mul(T, Hnorm2, H0);
+    double sc = 1. / H0[8];
+    bool fin = true;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) { H[q] = H0[q] * sc; fin = fin && dfinite(H[q]); }
+    return fin;
+}
+
+RSAC_HD float hom_err(const float *h, float x, float y, float u, float v) {
+    float ww = 1.f / (h[6] * x + h[7] * y + 1.f);
+    float ex = (h[0] * x + h[1] * y + h[2]) * ww - u;
+    float ey = (h[3] * x + h[4] * y + h[5]) * ww - v;
+    float e1 = ex * ex, e2 = ey * ey;
+    return e1 + e2;
+}
+
+}  // namespace rsac

@@ -1,0 +1,16 @@
+"""rsac -- MI355X-native RANSAC engine (PnP camera pose + homography).
+
+Drop-in for the RANSAC hot path of Mendel0408/Code-Reproduction-RANSAC, whose
+scripts call cv2.solvePnPRansac (main_v1.py:497) and cv2.findHomography
+(main_v1.py:312).  The compute runs in hand-written HIP kernels for gfx950
+(librsac.so, built from ../csrc) reached through a ctypes C ABI
+(include/rsac.h).  See DESIGN.md.
+"""
+from ._lib import Context, RsacError, context, lib  # noqa: F401
+from .api import (RansacInfo, evaluate_range, homography_fit, homography_ransac,  # noqa: F401
+                  homography_ransac_batched, hypotheses, pnp_ransac, pnp_ransac_batched, pose_mask, refine_pose, rodrigues,
+                  score_poses, update_num_iters)
+
+__all__ = ["pnp_ransac", "pnp_ransac_batched", "homography_ransac", "homography_ransac_batched", "score_poses",
+           "evaluate_range", "hypotheses", "pose_mask", "refine_pose", "homography_fit", "rodrigues", "update_num_iters",
+           "Context", "context", "RsacError", "RansacInfo", "lib"]

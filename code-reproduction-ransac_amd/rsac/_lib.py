@@ -1,0 +1,153 @@
+"""ctypes binding of librsac.so (include/rsac.h).
+
+The library is built in-tree by ``csrc/Makefile`` (``__graft_entry__.build()``)
+and loaded from this directory.  There is no fallback: if the HIP library is
+missing or no device is visible, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librsac.so")
+
+# status codes / flags (include/rsac.h)
+OK = 0
+NO_MODEL = 1
+EINVAL = -1
+ETOOFEW = -2
+EHIP = -3
+ENOMEM = -4
+ENODEV = -5
+
+F_SAMPLER_OPENCV = 1 << 0
+F_ADAPTIVE = 1 << 1
+F_REFINE = 1 << 2
+F_DEVICE_IN = 1 << 3
+F_DEVICE_SOA = 1 << 4
+F_DEVICE_OUT = 1 << 5
+F_EXACT_ONLY = 1 << 6
+
+ABI_VERSION = 1
+
+
+class Stats(C.Structure):
+    _fields_ = [("best_hyp", C.c_int64), ("iters", C.c_int64), ("hyps_scored", C.c_int64),
+                ("n_inliers", C.c_int32), ("rounds", C.c_int32), ("gpu_ms", C.c_double), ("solve_ms", C.c_double),
+                ("score_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# (name, restype, argtypes) -- one row per declaration of include/rsac.h
+_vp, _i32, _i64, _u32, _u64, _d = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
+SIGNATURES = [
+    ("rsac_create", C.c_int, [C.c_int, C.POINTER(_vp)]),
+    ("rsac_destroy", None, [_vp]),
+    ("rsac_last_error", C.c_char_p, []),
+    ("rsac_abi_version", C.c_int, []),
+    ("rsac_device_count", C.c_int, []),
+    ("rsac_set_round_size", C.c_int, [_vp, _i64]),
+    ("rsac_pnp_ransac", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
+                                  C.POINTER(Stats), _vp]),
+    ("rsac_pnp_ransac_batched", C.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
+                                          _vp, _vp, _vp]),
+    ("rsac_homography_ransac", C.c_int, [_vp, _vp, _vp, _i32, _i32, _d, _d, _u64, _u32, _vp, _vp,
+                                         C.POINTER(Stats), _vp]),
+    ("rsac_homography_ransac_batched", C.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
+                                                 _vp, _vp]),
+    ("rsac_score_poses", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _i32, _d, _u32, _vp, _vp]),
+    ("rsac_pnp_evaluate_range", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i64, _i64, _d, _u64, _u32,
+                                          C.POINTER(_i64), _vp, C.POINTER(Stats), _vp]),
+    ("rsac_pnp_hypotheses", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i64, _i32, _d, _u64, _u32, _vp, _vp, _vp, _vp,
+                                      _vp]),
+    ("rsac_homography_hypotheses", C.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _d, _u64, _u32, _vp, _vp, _vp, _vp,
+                                             _vp]),
+    ("rsac_pnp_mask", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _d, _u32, _vp, C.POINTER(_i32), _vp]),
+    ("rsac_pnp_refine", C.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32]),
+    ("rsac_homography_fit", C.c_int, [_vp, _vp, _i32, _vp, _vp]),
+    ("rsac_rodrigues_v2m", None, [_vp, _vp]),
+    ("rsac_rodrigues_m2v", None, [_vp, _vp]),
+    ("rsac_update_num_iters", C.c_int, [_d, _d, C.c_int, C.c_int]),
+]
+
+_lib = None
+_lock = threading.RLock()
+
+
+class RsacError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"rsac error {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load librsac.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                              f"g.build()'` (make -C code-reproduction-ransac_amd/csrc)")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        if L.rsac_abi_version() != ABI_VERSION:
+            raise ImportError("librsac.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(code):
+    if code < 0:
+        msg = lib().rsac_last_error()
+        raise RsacError(code, msg.decode() if msg else "")
+    return code
+
+
+class Context:
+    """One rsac_ctx (device scratch + stream) per (process, device)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self._h = C.c_void_p()
+        check(lib().rsac_create(device, C.byref(self._h)))
+        self.lock = threading.Lock()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_round_size(self, n: int):
+        check(lib().rsac_set_round_size(self._h, int(n)))
+
+    def close(self):
+        if self._h:
+            lib().rsac_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_contexts: dict[int, Context] = {}
+
+
+def context(device: int = 0) -> Context:
+    with _lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = Context(device)
+            _contexts[device] = ctx
+        return ctx

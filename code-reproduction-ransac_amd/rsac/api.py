@@ -1,0 +1,401 @@
+"""Python entry points over the C ABI (librsac.so).
+
+``pnp_ransac(points2D, points3D, K, n_iters, reproj_thresh) -> (R, t, inlier_mask)``
+is the north-star entry point: it replaces the RANSAC loop that
+``cv2.solvePnPRansac`` runs for the reference (main_v1.py:497-502,
+testpro-K.py:72-75, testpro.py:536-541, test_pro.py:515-520).
+``homography_ransac`` replaces ``cv2.findHomography(..., cv2.RANSAC, thr)``
+(main_v1.py:312, process.py:200).  The batched forms replace the Python loops
+around those calls (main_v1.py:274-284, testpro-K.py:58-75).
+
+Inputs may be numpy arrays (host, float64 as the reference holds them) or
+torch tensors on the GPU (float64 AoS, used in place).  Results for GPU
+inputs keep the mask on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+class _In:
+    """Marshalled input: pointer + whether it is on the device + keepalive."""
+
+    def __init__(self, a, cols: int):
+        self.device = False
+        self.torch = False
+        if _is_torch(a):
+            import torch
+            self.torch = True
+            t = a.reshape(-1, cols).to(torch.float64).contiguous()
+            self.device = t.is_cuda
+            if not self.device:
+                t = t.numpy()
+            self.keep = t
+            self.n = t.shape[0]
+            self.ptr = t.data_ptr() if self.device else t.ctypes.data
+            self.dev_index = a.device.index if self.device else None
+        else:
+            arr = np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1, cols))
+            self.keep = arr
+            self.n = arr.shape[0]
+            self.ptr = arr.ctypes.data
+            self.dev_index = None
+
+
+def _stream_of(inp: _In):
+    if inp.device:
+        import torch
+        return C.c_void_p(torch.cuda.current_stream(inp.keep.device).cuda_stream)
+    return C.c_void_p(0)
+
+
+def _device_of(inp: _In, device):
+    if device is not None:
+        return int(device)
+    if inp.dev_index is not None:
+        return int(inp.dev_index)
+    return 0
+
+
+def _flags(adaptive, refine, sampler, exact_only=False):
+    f = 0
+    if adaptive:
+        f |= L.F_ADAPTIVE
+    if refine:
+        f |= L.F_REFINE
+    if sampler == "opencv":
+        f |= L.F_SAMPLER_OPENCV
+    elif sampler != "philox":
+        raise ValueError(f"sampler must be 'philox' or 'opencv', got {sampler!r}")
+    if exact_only:
+        f |= L.F_EXACT_ONLY
+    return f
+
+
+def _mask_buffer(inp: _In, n: int):
+    if inp.device:
+        import torch
+        m = torch.empty(max(n, 1), dtype=torch.uint8, device=inp.keep.device)
+        return m, m.data_ptr(), L.F_DEVICE_OUT
+    m = np.zeros(max(n, 1), np.uint8)
+    return m, m.ctypes.data, 0
+
+
+def _finish_mask(m, n):
+    return m[:n].bool() if _is_torch(m) else m[:n].astype(bool)
+
+
+@dataclass
+class RansacInfo:
+    ok: bool
+    n_inliers: int
+    best_hyp: int
+    iters: int
+    hyps_scored: int
+    rounds: int
+    gpu_ms: float
+    solve_ms: float
+    score_ms: float
+
+
+def _info(code, st: L.Stats) -> RansacInfo:
+    return RansacInfo(ok=code == L.OK, n_inliers=st.n_inliers, best_hyp=st.best_hyp, iters=st.iters,
+                      hyps_scored=st.hyps_scored, rounds=st.rounds, gpu_ms=st.gpu_ms, solve_ms=st.solve_ms,
+                      score_ms=st.score_ms)
+
+
+def _K9(K) -> np.ndarray:
+    K = np.ascontiguousarray(np.asarray(K, dtype=np.float64).reshape(3, 3))
+    return K.reshape(9).copy()
+
+
+def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
+               confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox", adaptive: bool = True,
+               refine: bool = True, device=None, return_info: bool = False):
+    """RANSAC PnP on the GPU: (points2D, points3D, K, n_iters, reproj_thresh) -> (R, t, inlier_mask).
+
+    Defaults follow the reference call (iterationsCount=5000, reprojectionError=30,
+    confidence=0.99; main_v1.py:497-502).  ``R`` is 3x3, ``t`` (3,) with
+    x_cam = R X + t; ``inlier_mask`` is the RANSAC-phase mask (OpenCV's
+    convention).  On failure R and t are None and the mask is all False.
+    """
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    if p3.n != p2.n:
+        raise ValueError(f"points3D ({p3.n}) and points2D ({p2.n}) differ in length")
+    if p3.device != p2.device:
+        raise ValueError("points3D and points2D must both be host arrays or both GPU tensors")
+    n = p3.n
+    ctx = L.context(_device_of(p3, device))
+    flags = _flags(adaptive, refine, sampler)
+    if p3.device:
+        flags |= L.F_DEVICE_IN
+    K9 = _K9(K)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    mask, mptr, mflag = _mask_buffer(p3, n)
+    flags |= mflag
+    st = L.Stats()
+    with ctx.lock:
+        code = L.check(L.lib().rsac_pnp_ransac(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), n,
+                                               K9.ctypes.data, int(n_iters), float(reproj_thresh),
+                                               float(confidence), int(seed) & (2**64 - 1), flags, R.ctypes.data,
+                                               t.ctypes.data, C.c_void_p(mptr), C.byref(st), _stream_of(p3)))
+    m = _finish_mask(mask, n)
+    out = (R.reshape(3, 3), t, m) if code == L.OK else (None, None, m)
+    return out + (_info(code, st),) if return_info else out
+
+
+def homography_ransac(src, dst, reproj_thresh: float = 3.0, *, max_iters: int = 2000, confidence: float = 0.995,
+                      seed: int = 0x5EED, sampler: str = "opencv", adaptive: bool = True, refine: bool = True,
+                      device=None, return_info: bool = False):
+    """RANSAC homography src -> dst on the GPU: -> (H, mask).
+
+    Mirrors cv2.findHomography(src, dst, cv2.RANSAC, thr) (main_v1.py:312):
+    OpenCV's MWC subset sequence by default (sampler="opencv"), f32 error,
+    RANSAC-phase mask, then a least-squares + LM polish of H on the inliers.
+    """
+    s = _In(src, 2)
+    d = _In(dst, 2)
+    if s.n != d.n:
+        raise ValueError("src and dst differ in length")
+    n = s.n
+    ctx = L.context(_device_of(s, device))
+    flags = _flags(adaptive, refine, sampler)
+    if s.device:
+        flags |= L.F_DEVICE_IN
+    H = np.zeros(9)
+    mask, mptr, mflag = _mask_buffer(s, n)
+    flags |= mflag
+    st = L.Stats()
+    with ctx.lock:
+        code = L.check(L.lib().rsac_homography_ransac(ctx.handle, C.c_void_p(s.ptr), C.c_void_p(d.ptr), n,
+                                                      int(max_iters), float(reproj_thresh), float(confidence),
+                                                      int(seed) & (2**64 - 1), flags, H.ctypes.data,
+                                                      C.c_void_p(mptr), C.byref(st), _stream_of(s)))
+    m = _finish_mask(mask, n)
+    out = (H.reshape(3, 3), m) if code == L.OK else (None, m)
+    return out + (_info(code, st),) if return_info else out
+
+
+def _concat(parts, cols):
+    arrs = [np.asarray(p, dtype=np.float64).reshape(-1, cols) for p in parts]
+    off = np.zeros(len(arrs) + 1, np.int64)
+    off[1:] = np.cumsum([a.shape[0] for a in arrs])
+    return np.ascontiguousarray(np.concatenate(arrs, axis=0) if arrs else np.zeros((0, cols))), off
+
+
+def pnp_ransac_batched(points2D_list, points3D_list, K_list, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
+                       confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox", adaptive: bool = True,
+                       refine: bool = True, device: int = 0):
+    """P independent PnP problems in one call (K sweep of testpro-K.py:58-75, C3 of BASELINE.json).
+
+    Returns a list of (R, t, mask, n_inliers) per problem (R, t None on failure).
+    """
+    p3, off = _concat(points3D_list, 3)
+    p2, off2 = _concat(points2D_list, 2)
+    if not np.array_equal(off, off2):
+        raise ValueError("per-problem 3D/2D point counts differ")
+    P = len(off) - 1
+    Ks = np.ascontiguousarray(np.stack([np.asarray(k, np.float64).reshape(9) for k in K_list]))
+    if Ks.shape[0] != P:
+        raise ValueError("one K per problem required")
+    if P and np.diff(off).min() < 4:
+        raise ValueError("every problem needs >= 4 correspondences")
+    ctx = L.context(device)
+    flags = _flags(adaptive, refine, sampler)
+    R = np.zeros((P, 9))
+    t = np.zeros((P, 3))
+    status = np.zeros(P, np.int32)
+    ninl = np.zeros(P, np.int32)
+    mask = np.zeros(max(int(off[-1]), 1), np.uint8)
+    with ctx.lock:
+        L.check(L.lib().rsac_pnp_ransac_batched(ctx.handle, p3.ctypes.data, p2.ctypes.data, off.ctypes.data, P,
+                                                Ks.ctypes.data, int(n_iters), float(reproj_thresh), float(confidence),
+                                                int(seed) & (2**64 - 1), flags, R.ctypes.data, t.ctypes.data,
+                                                status.ctypes.data, ninl.ctypes.data, mask.ctypes.data, None))
+    out = []
+    for p in range(P):
+        m = mask[off[p]:off[p + 1]].astype(bool)
+        ok = status[p] == L.OK
+        out.append((R[p].reshape(3, 3) if ok else None, t[p] if ok else None, m, int(ninl[p])))
+    return out
+
+
+def homography_ransac_batched(src_list, dst_list, reproj_thresh: float = 3.0, *, max_iters: int = 2000,
+                              confidence: float = 0.995, seed: int = 0x5EED, sampler: str = "opencv",
+                              adaptive: bool = True, refine: bool = True, device: int = 0):
+    """P independent findHomography calls in one launch sequence (main_v1.py:274-284)."""
+    s, off = _concat(src_list, 2)
+    d, off2 = _concat(dst_list, 2)
+    if not np.array_equal(off, off2):
+        raise ValueError("per-problem src/dst counts differ")
+    P = len(off) - 1
+    if P and np.diff(off).min() < 4:
+        raise ValueError("every problem needs >= 4 correspondences")
+    ctx = L.context(device)
+    flags = _flags(adaptive, refine, sampler)
+    H = np.zeros((P, 9))
+    status = np.zeros(P, np.int32)
+    ninl = np.zeros(P, np.int32)
+    mask = np.zeros(max(int(off[-1]), 1), np.uint8)
+    with ctx.lock:
+        L.check(L.lib().rsac_homography_ransac_batched(ctx.handle, s.ctypes.data, d.ctypes.data, off.ctypes.data, P,
+                                                       int(max_iters), float(reproj_thresh), float(confidence),
+                                                       int(seed) & (2**64 - 1), flags, H.ctypes.data,
+                                                       status.ctypes.data, ninl.ctypes.data, mask.ctypes.data, None))
+    out = []
+    for p in range(P):
+        ok = status[p] == L.OK
+        out.append((H[p].reshape(3, 3) if ok else None, mask[off[p]:off[p + 1]].astype(bool), int(ninl[p])))
+    return out
+
+
+def score_poses(points2D, points3D, K, poses, reproj_thresh: float = 30.0, device=None):
+    """Inlier counts of given poses ((H, 3, 4) [R | t] or (H, 12)) -- the minimal scoring slice."""
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    poses = np.asarray(poses, np.float64)
+    if poses.ndim == 3:
+        poses = np.concatenate([poses[:, :, :3].reshape(-1, 9), poses[:, :, 3]], axis=1)
+    poses = np.ascontiguousarray(poses.reshape(-1, 12))
+    ctx = L.context(_device_of(p3, device))
+    flags = L.F_DEVICE_IN if p3.device else 0
+    counts = np.zeros(poses.shape[0], np.int32)
+    K9 = _K9(K)
+    with ctx.lock:
+        L.check(L.lib().rsac_score_poses(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n, K9.ctypes.data,
+                                         poses.ctypes.data, poses.shape[0], float(reproj_thresh), flags,
+                                         counts.ctypes.data, _stream_of(p3)))
+    return counts
+
+
+def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_thresh: float = 30.0, *,
+                   seed: int = 0x5EED, device=None, return_info: bool = False):
+    """Evaluate Philox hypotheses [hyp_begin, hyp_begin + n_hyps) of one problem.
+
+    Returns (key, model12) where key = (count << 32) | (0xFFFFFFFF - best_index) (or -1).
+    The sharded driver (rsac.parallel) all-reduces the key with MAX.
+    """
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    ctx = L.context(_device_of(p3, device))
+    flags = L.F_DEVICE_IN if p3.device else 0
+    key = C.c_int64(-1)
+    model = np.zeros(12)
+    K9 = _K9(K)
+    st = L.Stats()
+    with ctx.lock:
+        code = L.check(L.lib().rsac_pnp_evaluate_range(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n,
+                                                       K9.ctypes.data, int(hyp_begin), int(n_hyps),
+                                                       float(reproj_thresh), int(seed) & (2**64 - 1), flags,
+                                                       C.byref(key), model.ctypes.data, C.byref(st),
+                                                       _stream_of(p3)))
+    if return_info:
+        return int(key.value), model, _info(code, st)
+    return int(key.value), model
+
+
+def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024, reproj_thresh: float = 30.0, *,
+               seed: int = 0x5EED, subsets=None, device=None):
+    """Raw per-hypothesis (status, counts, models) of the GPU hot path for one problem.
+
+    model "pnp": a = points3D (N,3), b = points2D (N,2), K required.
+    model "homography": a = src (N,2), b = dst (N,2).
+    subsets: optional (n_hyps, 4) int32 index table replacing the Philox draw.
+    """
+    pnp = model == "pnp"
+    A = _In(a, 3 if pnp else 2)
+    B = _In(b, 2)
+    ctx = L.context(_device_of(A, device))
+    flags = L.F_DEVICE_IN if A.device else 0
+    counts = np.zeros(n_hyps, np.int32)
+    status = np.zeros(n_hyps, np.int8)
+    models = np.zeros((n_hyps, 16))
+    sub = None if subsets is None else np.ascontiguousarray(np.asarray(subsets, np.int32).reshape(n_hyps, 4))
+    with ctx.lock:
+        if pnp:
+            K9 = _K9(K)
+            L.check(L.lib().rsac_pnp_hypotheses(ctx.handle, C.c_void_p(A.ptr), C.c_void_p(B.ptr), A.n, K9.ctypes.data,
+                                                int(hyp_begin), int(n_hyps), float(reproj_thresh),
+                                                int(seed) & (2**64 - 1), flags,
+                                                None if sub is None else sub.ctypes.data, counts.ctypes.data,
+                                                status.ctypes.data, models.ctypes.data, _stream_of(A)))
+        else:
+            L.check(L.lib().rsac_homography_hypotheses(ctx.handle, C.c_void_p(A.ptr), C.c_void_p(B.ptr), A.n,
+                                                       int(hyp_begin), int(n_hyps), float(reproj_thresh),
+                                                       int(seed) & (2**64 - 1), flags,
+                                                       None if sub is None else sub.ctypes.data, counts.ctypes.data,
+                                                       status.ctypes.data, models.ctypes.data, _stream_of(A)))
+    return status, counts, models
+
+
+def pose_mask(points2D, points3D, K, model12, reproj_thresh: float = 30.0, device=None):
+    """RANSAC-test mask (and count) of one pose model (R 9 row-major, t 3)."""
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    ctx = L.context(_device_of(p3, device))
+    flags = L.F_DEVICE_IN if p3.device else 0
+    mask, mptr, mflag = _mask_buffer(p3, p3.n)
+    flags |= mflag
+    cnt = C.c_int32(0)
+    K9 = _K9(K)
+    m12 = np.ascontiguousarray(np.asarray(model12, np.float64).reshape(12))
+    with ctx.lock:
+        L.check(L.lib().rsac_pnp_mask(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n, K9.ctypes.data,
+                                      m12.ctypes.data, float(reproj_thresh), flags, C.c_void_p(mptr), C.byref(cnt),
+                                      _stream_of(p3)))
+    return _finish_mask(mask, p3.n), int(cnt.value)
+
+
+def refine_pose(points2D, points3D, K, R, t, mask=None, max_iter: int = 20):
+    """LM refinement of (R, t) on host arrays (cv2.solvePnPRefineLM, main_v1.py:508) -> (R, t)."""
+    P3 = np.ascontiguousarray(np.asarray(points3D, np.float64).reshape(-1, 3))
+    P2 = np.ascontiguousarray(np.asarray(points2D, np.float64).reshape(-1, 2))
+    Rr = np.ascontiguousarray(np.asarray(R, np.float64).reshape(9)).copy()
+    tr = np.ascontiguousarray(np.asarray(t, np.float64).reshape(3)).copy()
+    m = None if mask is None else np.ascontiguousarray(np.asarray(mask, np.uint8).reshape(-1))
+    K9 = _K9(K)
+    L.check(L.lib().rsac_pnp_refine(P3.ctypes.data, P2.ctypes.data, P3.shape[0], K9.ctypes.data,
+                                    None if m is None else m.ctypes.data, Rr.ctypes.data, tr.ctypes.data,
+                                    int(max_iter)))
+    return Rr.reshape(3, 3), tr
+
+
+def homography_fit(src, dst, mask=None):
+    """Least-squares normalised DLT + LM on all (or masked) points -> H (findHomography method 0)."""
+    s = np.ascontiguousarray(np.asarray(src, np.float64).reshape(-1, 2))
+    d = np.ascontiguousarray(np.asarray(dst, np.float64).reshape(-1, 2))
+    m = None if mask is None else np.ascontiguousarray(np.asarray(mask, np.uint8).reshape(-1))
+    H = np.zeros(9)
+    code = L.check(L.lib().rsac_homography_fit(s.ctypes.data, d.ctypes.data, s.shape[0],
+                                               None if m is None else m.ctypes.data, H.ctypes.data))
+    return H.reshape(3, 3) if code == L.OK else None
+
+
+def rodrigues(src):
+    """cv2.Rodrigues (main_v1.py:895): (3,) vector <-> (3, 3) matrix."""
+    a = np.ascontiguousarray(np.asarray(src, np.float64))
+    if a.size == 3:
+        R = np.zeros(9)
+        L.lib().rsac_rodrigues_v2m(a.reshape(3).ctypes.data, R.ctypes.data)
+        return R.reshape(3, 3)
+    if a.size == 9:
+        r = np.zeros(3)
+        L.lib().rsac_rodrigues_m2v(a.reshape(9).ctypes.data, r.ctypes.data)
+        return r.reshape(3, 1)
+    raise ValueError("Rodrigues expects a 3-vector or a 3x3 matrix")
+
+
+def update_num_iters(p: float, ep: float, model_points: int, max_iters: int) -> int:
+    """RANSACUpdateNumIters of OpenCV, as the driver applies it after every new best model."""
+    return int(L.lib().rsac_update_num_iters(float(p), float(ep), int(model_points), int(max_iters)))

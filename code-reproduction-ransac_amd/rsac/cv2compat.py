@@ -1,0 +1,115 @@
+"""cv2-compatible shims: the reference's call sites become a one-line import swap.
+
+    import rsac.cv2compat as cv2      # instead of `import cv2` for these calls
+
+Covered calls (signatures and return tuples of the OpenCV Python binding):
+
+* ``solvePnPRansac``   main_v1.py:497-502, testpro-K.py:72-75, testpro.py:536, test_pro.py:515
+* ``findHomography``   main_v1.py:312, process.py:200, test02.py:263, testpro.py:350, test_pro.py:351
+* ``Rodrigues``        main_v1.py:895, testpro-K.py:84, 136, 169
+* ``projectPoints``    testpro-K.py:33 (compute_reprojection_error)
+* ``solvePnPRefineLM`` main_v1.py:508-509, testpro-K.py:122-125
+
+Only zero distortion is supported: every reference call passes
+``np.zeros((4, 1))`` (main_v1.py:472, testpro-K.py:42); other values raise.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import api
+
+RANSAC = 8
+LMEDS = 4
+SOLVEPNP_ITERATIVE = 0
+SOLVEPNP_EPNP = 1
+SOLVEPNP_P3P = 2
+SOLVEPNP_AP3P = 5
+
+
+class error(Exception):
+    """Stands in for cv2.error (bad shapes, too few points)."""
+
+
+def _check_dist(distCoeffs):
+    if distCoeffs is None:
+        return
+    d = np.asarray(distCoeffs, np.float64)
+    if d.size and np.any(d != 0):
+        raise NotImplementedError("rsac supports zero distortion only (as every reference call site uses)")
+
+
+def Rodrigues(src, dst=None, jacobian=None):
+    """(3,1) vector <-> (3,3) matrix; returns (dst, None) (no Jacobian)."""
+    return api.rodrigues(src), None
+
+
+def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=None, tvec=None,
+                   useExtrinsicGuess=False, iterationsCount=100, reprojectionError=8.0, confidence=0.99,
+                   inliers=None, flags=SOLVEPNP_ITERATIVE):
+    """-> (retval, rvec (3,1), tvec (3,1), inliers (M,1) int32 or None).
+
+    Minimal kernel: P3P on 4 points (the north star's kernel; OpenCV's default
+    would be EPnP on 5).  Final pose: LM on the RANSAC inliers started from
+    the best minimal model (what SOLVEPNP_ITERATIVE's final solvePnP does).
+    """
+    _check_dist(distCoeffs)
+    P3 = np.asarray(objectPoints, np.float64).reshape(-1, 3)
+    P2 = np.asarray(imagePoints, np.float64).reshape(-1, 2)
+    if P3.shape[0] != P2.shape[0]:
+        raise error("objectPoints and imagePoints differ in length")
+    if P3.shape[0] < 4:
+        raise error("solvePnPRansac needs at least 4 points")
+    R, t, mask = api.pnp_ransac(P2, P3, cameraMatrix, int(iterationsCount), float(reprojectionError),
+                                confidence=float(confidence), adaptive=True, refine=True)
+    if R is None:
+        return False, (np.zeros((3, 1)) if rvec is None else rvec), (np.zeros((3, 1)) if tvec is None else tvec), None
+    idx = np.flatnonzero(mask).astype(np.int32).reshape(-1, 1)
+    return True, api.rodrigues(R).reshape(3, 1), t.reshape(3, 1), idx
+
+
+def findHomography(srcPoints, dstPoints, method=0, ransacReprojThreshold=3.0, mask=None, maxIters=2000,
+                   confidence=0.995):
+    """-> (H (3,3) or None, mask (N,1) uint8)."""
+    s = np.asarray(srcPoints, np.float64).reshape(-1, 2)
+    d = np.asarray(dstPoints, np.float64).reshape(-1, 2)
+    if s.shape[0] != d.shape[0]:
+        raise error("srcPoints and dstPoints differ in length")
+    if s.shape[0] < 4:
+        raise error("findHomography needs at least 4 point correspondences")
+    if method not in (0, RANSAC):
+        raise NotImplementedError("only method=0 and cv2.RANSAC are provided")
+    if method == 0 or s.shape[0] == 4:
+        # all points, no RANSAC: one least-squares fit (as OpenCV does for method 0 / 4 points)
+        return api.homography_fit(s, d), np.ones((s.shape[0], 1), np.uint8)
+    H, m = api.homography_ransac(s, d, float(ransacReprojThreshold), max_iters=int(maxIters),
+                                 confidence=float(confidence))
+    return H, np.asarray(m, np.uint8).reshape(-1, 1)
+
+
+def projectPoints(objectPoints, rvec, tvec, cameraMatrix, distCoeffs, imagePoints=None, jacobian=None,
+                  aspectRatio=0):
+    """(N,3) -> ((N,1,2) pixels, None), zero distortion, float64 as cv2 returns for f64 input."""
+    _check_dist(distCoeffs)
+    X = np.asarray(objectPoints, np.float64).reshape(-1, 3)
+    r = np.asarray(rvec, np.float64).reshape(-1)
+    R = api.rodrigues(r) if r.size == 3 else r.reshape(3, 3)
+    t = np.asarray(tvec, np.float64).reshape(3)
+    K = np.asarray(cameraMatrix, np.float64).reshape(3, 3)
+    pc = X @ R.T + t
+    z = pc[:, 2]
+    iz = np.where(z != 0, 1.0 / np.where(z != 0, z, 1.0), 1.0)
+    u = pc[:, 0] * iz * K[0, 0] + K[0, 2]
+    v = pc[:, 1] * iz * K[1, 1] + K[1, 2]
+    return np.stack([u, v], axis=1).reshape(-1, 1, 2), None
+
+
+def solvePnPRefineLM(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec, tvec, criteria=None):
+    """LM refinement of (rvec, tvec) on the given correspondences -> (rvec, tvec)."""
+    _check_dist(distCoeffs)
+    P3 = np.asarray(objectPoints, np.float64).reshape(-1, 3)
+    P2 = np.asarray(imagePoints, np.float64).reshape(-1, 2)
+    R0 = api.rodrigues(np.asarray(rvec, np.float64).reshape(3))
+    t0 = np.asarray(tvec, np.float64).reshape(3)
+    R, t = api.refine_pose(P2, P3, cameraMatrix, R0, t0)
+    return api.rodrigues(R).reshape(3, 1), t.reshape(3, 1)

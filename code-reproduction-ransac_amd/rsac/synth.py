@@ -1,0 +1,108 @@
+"""Synthetic correspondence sets shaped like the reference's scene.
+
+The reference georeferences a 2142x1620 photograph against UTM-50N points
+(main_v1.py:889-890 builds ``pos3d``/``pixels``; testpro-K.py:198-225 hard-codes
+12 of them).  No dataset ships beyond those 12 points, so benchmarks and the
+large parity cases use seeded synthetic sets of the same geometry:
+
+* intrinsics of main_v1.py:870-883 (f = 240 mm on a 127 x 178 mm plate,
+  cx = 982.666819, cy = 697.950868, image 2142 x 1620);
+* world points offset to UTM-like magnitudes (~7.39e5 E, ~2.888e6 N, ~700 m),
+  so the float32 rounding that cv2.solvePnPRansac applies matters as it does
+  in the reference;
+* inliers = exact projection + N(0, sigma) px; outliers uniform in the image.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+IMAGE_W, IMAGE_H = 2142, 1620
+UTM_ORIGIN = np.array([739000.0, 2888500.0, 700.0])
+
+
+def main_v1_K(width: int = IMAGE_W, height: int = IMAGE_H) -> np.ndarray:
+    """K of main_v1.py:870-883."""
+    fx = 240.0 / 127.0 * width
+    fy = 240.0 / 178.0 * height
+    return np.array([[fx, 0.0, 9.82666819e02], [0.0, fy, 6.97950868e02], [0.0, 0.0, 1.0]])
+
+
+def random_rotation(rng: np.random.Generator) -> np.ndarray:
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    ang = rng.uniform(0.0, np.pi)
+    kx = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(ang) * kx + (1 - np.cos(ang)) * (kx @ kx)
+
+
+def pnp_problem(n: int, outlier_ratio: float = 0.5, seed: int = 0, noise_px: float = 1.0, K=None,
+                depth=(300.0, 1500.0)):
+    """One synthetic PnP problem.
+
+    Returns dict(points3d (n,3) f64, points2d (n,2) f64, K, R, t, inlier (n,) bool).
+    The ground-truth camera sits 500-1500 m from the cloud like the UTM scene.
+    """
+    rng = np.random.default_rng(seed)
+    K = main_v1_K() if K is None else np.asarray(K, np.float64)
+    R = random_rotation(rng)
+    centre = UTM_ORIGIN + rng.uniform(-500.0, 500.0, size=3) * np.array([1.0, 1.0, 0.1])
+    t = -R @ centre
+    u = rng.uniform(0.0, IMAGE_W, size=n)
+    v = rng.uniform(0.0, IMAGE_H, size=n)
+    d = rng.uniform(depth[0], depth[1], size=n)
+    Kinv = np.linalg.inv(K)
+    rays = (Kinv @ np.stack([u, v, np.ones(n)])).T
+    pc = rays * (d / rays[:, 2])[:, None]
+    pw = (pc - t) @ R  # R^T (pc - t)
+    proj = (K @ pc.T).T
+    px = proj[:, :2] / proj[:, 2:3] + rng.normal(0.0, noise_px, size=(n, 2))
+    n_out = int(round(outlier_ratio * n))
+    out_idx = rng.permutation(n)[:n_out]
+    inlier = np.ones(n, bool)
+    inlier[out_idx] = False
+    px[out_idx, 0] = rng.uniform(0.0, IMAGE_W, size=n_out)
+    px[out_idx, 1] = rng.uniform(0.0, IMAGE_H, size=n_out)
+    return dict(points3d=pw, points2d=px, K=K, R=R, t=t, inlier=inlier)
+
+
+def homography_problem(n: int, outlier_ratio: float = 0.3, seed: int = 0, noise_px: float = 1.0):
+    """Synthetic plane-to-image correspondences (src like the pos2 of main_v1.py:306-311)."""
+    rng = np.random.default_rng(seed)
+    src = rng.uniform(-1.0, 1.0, size=(n, 2)) * np.array([0.6, 0.2])
+    H = np.array([[1500.0, 40.0, 1000.0], [30.0, -1400.0, 700.0], [0.05, 0.3, 1.0]])
+    H = H + rng.normal(0.0, 1.0, size=(3, 3)) * np.array([[50, 20, 50], [20, 50, 50], [0.01, 0.02, 0]])
+    hs = np.c_[src, np.ones(n)] @ H.T
+    dst = hs[:, :2] / hs[:, 2:3] + rng.normal(0.0, noise_px, size=(n, 2))
+    n_out = int(round(outlier_ratio * n))
+    out_idx = rng.permutation(n)[:n_out]
+    inlier = np.ones(n, bool)
+    inlier[out_idx] = False
+    dst[out_idx, 0] = rng.uniform(0.0, IMAGE_W, size=n_out)
+    dst[out_idx, 1] = rng.uniform(0.0, IMAGE_H, size=n_out)
+    return dict(src=src, dst=dst, H=H / H[2, 2], inlier=inlier)
+
+
+# the 12 hard-coded correspondences and the known camera origin of testpro-K.py:198-234
+TESTPRO_K_POS3D = np.array([
+    [739031.2, 2888840.39, 726.0], [738995.929, 2888848.16, 724.0], [738963.052, 2888845.45, 721.0],
+    [739173.616, 2888834.91, 697.0], [739077.689, 2888935.68, 726.0], [739033.253, 2888924.78, 726.0],
+    [738973.016, 2888907.82, 723.0], [739136.184, 2889025.65, 705.0], [739179.948, 2888631.85, 702.0],
+    [739140.769, 2888574.49, 702.0], [739312.871, 2888549.50, 720.0], [739249.159, 2888541.79, 707.0]])
+TESTPRO_K_PIXELS = np.array([
+    [582, 296], [402, 301], [272, 314], [1440, 467], [965, 296], [666, 265], [392, 283], [1583, 319],
+    [729, 606], [169, 696], [1804, 672], [885, 824]], dtype=np.float64)
+TESTPRO_K_FOCALS = [90, 100, 120, 150, 180, 210, 240, 300, 360]
+TESTPRO_K_SENSORS = [(102, 127), (127, 178), (203, 254)]
+TESTPRO_K_IMAGE = (2142, 1620)
+TESTPRO_K_ORIGIN = np.array([739424.6, 2888281.18, 770.0])
+
+
+def testpro_k_candidates():
+    """The 27 intrinsics of the K sweep (testpro-K.py:58-70), in loop order."""
+    out = []
+    for f in TESTPRO_K_FOCALS:
+        for (sw, sh) in TESTPRO_K_SENSORS:
+            fx = f / (sw / TESTPRO_K_IMAGE[0])
+            fy = f / (sh / TESTPRO_K_IMAGE[1])
+            out.append(np.array([[fx, 0, TESTPRO_K_IMAGE[0] / 2], [0, fy, TESTPRO_K_IMAGE[1] / 2], [0, 0, 1.0]]))
+    return out

@@ -1,0 +1,179 @@
+/*
+ * rsac.h -- C ABI of the MI355X RANSAC engine (librsac.so).
+ *
+ * Drop-in boundary for the reference's RANSAC hot path.  The reference calls
+ * OpenCV through the cv2 Python binding:
+ *
+ *   cv2.solvePnPRansac(objectPoints, imagePoints, K, dist, iterationsCount,
+ *                      reprojectionError, confidence) -> retval, rvec, tvec, inliers
+ *        main_v1.py:497-502, testpro-K.py:72-75, testpro.py:536-541, test_pro.py:515-520
+ *   cv2.findHomography(src, dst, cv2.RANSAC, ransacReprojThreshold) -> H, mask
+ *        main_v1.py:312, process.py:200, test02.py:263, testpro.py:350, test_pro.py:351
+ *   Python loop of findHomography over candidate locations
+ *        main_v1.py:274-284 (find_homographies), process.py:147-185
+ *   K sweep of solvePnPRansac over 27 intrinsics
+ *        testpro-K.py:58-75 (estimate_camera_orientation)
+ *
+ * Each entry point below replaces one of those.  Plain pointers and sizes
+ * only; the Python layer (rsac/, ctypes) mirrors the cv2 signatures on top.
+ *
+ * Conventions
+ *   - returns RSAC_OK (model found), RSAC_NO_MODEL (retval=False in cv2
+ *     terms), or a negative RSAC_E* code; rsac_last_error() gives the text
+ *     (thread-local).
+ *   - host inputs: float64, array-of-structs exactly as numpy holds them
+ *     (points3d N x 3, points2d N x 2), converted to float32 like OpenCV does.
+ *     With RSAC_F_DEVICE_IN the same layout lives in device memory.
+ *     With RSAC_F_DEVICE_SOA the inputs are already device float32
+ *     structure-of-arrays: pts3d = X[N] Y[N] Z[N], pts2d = U[N] V[N].
+ *   - inlier masks are RANSAC-phase masks (uint8, one per point), as OpenCV
+ *     returns them; host memory unless RSAC_F_DEVICE_OUT.
+ *   - work is enqueued on `stream` (hipStream_t, NULL = the context stream);
+ *     calls on one context are serialised; contexts are independent.
+ */
+#ifndef RSAC_H
+#define RSAC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSAC_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define RSAC_EXPORT __attribute__((visibility("default")))
+#else
+#define RSAC_EXPORT
+#endif
+
+/* status codes */
+#define RSAC_OK 0
+#define RSAC_NO_MODEL 1
+#define RSAC_EINVAL (-1)
+#define RSAC_ETOOFEW (-2) /* fewer than 4 correspondences (cv2 raises) */
+#define RSAC_EHIP (-3)
+#define RSAC_ENOMEM (-4)
+#define RSAC_ENODEV (-5)
+
+/* flags */
+#define RSAC_F_SAMPLER_OPENCV (1u << 0) /* OpenCV MWC getSubset sequence (host-generated) instead of Philox */
+#define RSAC_F_ADAPTIVE (1u << 1)       /* RANSACUpdateNumIters early termination, evaluated in rounds */
+#define RSAC_F_REFINE (1u << 2)         /* non-minimal refit on the inliers (LM) -> R,t / H */
+#define RSAC_F_DEVICE_IN (1u << 3)      /* inputs are device pointers (float64 AoS) */
+#define RSAC_F_DEVICE_SOA (1u << 4)     /* inputs are device float32 SoA (implies device) */
+#define RSAC_F_DEVICE_OUT (1u << 5)     /* inlier mask output is a device pointer */
+#define RSAC_F_EXACT_ONLY (1u << 6)     /* disable the float32 pre-filter in scoring (A/B and tests) */
+
+typedef struct rsac_ctx rsac_ctx;
+
+/* per-call diagnostics (all optional) */
+typedef struct rsac_stats {
+    int64_t best_hyp;      /* index of the winning hypothesis (-1 none) */
+    int64_t iters;         /* RANSAC iterations consumed (OpenCV `iter` at exit) */
+    int64_t hyps_scored;   /* hypotheses evaluated on the GPU (>= iters) */
+    int32_t n_inliers;     /* RANSAC-phase inlier count of the winner */
+    int32_t rounds;        /* launches of the solve+score pair */
+    double gpu_ms;         /* device time of solve+score (events), summed over rounds */
+    double solve_ms;       /* ... of which the sample+minimal-solve kernel */
+    double score_ms;       /* ... of which the scoring kernel */
+} rsac_stats;
+
+RSAC_EXPORT int rsac_create(int device, rsac_ctx **out);
+RSAC_EXPORT void rsac_destroy(rsac_ctx *ctx);
+RSAC_EXPORT const char *rsac_last_error(void);
+RSAC_EXPORT int rsac_abi_version(void);
+RSAC_EXPORT int rsac_device_count(void);
+RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
+
+/* cv2.solvePnPRansac (main_v1.py:497).  K: 3x3 row-major f64.  Minimal
+ * solver: P3P (Lambda Twist) on 4 points.  n_iters = iterationsCount cap,
+ * reproj_thresh in px, confidence as in OpenCV.  Outputs R (3x3 row-major),
+ * t (3), mask (n). */
+RSAC_EXPORT int rsac_pnp_ransac(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                    int32_t n_iters, double reproj_thresh, double confidence, uint64_t seed, uint32_t flags,
+                    double R_out[9], double t_out[3], uint8_t *inlier_mask_out, rsac_stats *stats, void *stream);
+
+/* Batched PnP: P independent problems, problem p owns points
+ * [offsets[p], offsets[p+1]) and intrinsics K[9p..9p+8] (the K sweep of
+ * testpro-K.py:58 is P problems sharing points; pass repeated rows).
+ * Outputs per problem: R (9), t (3), status (RSAC_OK/RSAC_NO_MODEL),
+ * n_inliers, mask (total points). */
+RSAC_EXPORT int rsac_pnp_ransac_batched(rsac_ctx *ctx, const void *pts3d, const void *pts2d, const int64_t *offsets,
+                            int32_t n_problems, const double *K, int32_t n_iters, double reproj_thresh,
+                            double confidence, uint64_t seed, uint32_t flags, double *R_out, double *t_out,
+                            int32_t *status_out, int32_t *n_inliers_out, uint8_t *inlier_mask_out, void *stream);
+
+/* cv2.findHomography(src, dst, cv2.RANSAC, thr) (main_v1.py:312):
+ * src, dst N x 2.  Defaults of OpenCV: max_iters 2000, confidence 0.995. */
+RSAC_EXPORT int rsac_homography_ransac(rsac_ctx *ctx, const void *src, const void *dst, int32_t n, int32_t max_iters,
+                           double thresh, double confidence, uint64_t seed, uint32_t flags, double H_out[9],
+                           uint8_t *mask_out, rsac_stats *stats, void *stream);
+
+/* The location-search loop of find_homographies (main_v1.py:274-284) as one
+ * call: P problems with point ranges given by offsets. */
+RSAC_EXPORT int rsac_homography_ransac_batched(rsac_ctx *ctx, const void *src, const void *dst, const int64_t *offsets,
+                                   int32_t n_problems, int32_t max_iters, double thresh, double confidence,
+                                   uint64_t seed, uint32_t flags, double *H_out, int32_t *status_out,
+                                   int32_t *n_inliers_out, uint8_t *mask_out, void *stream);
+
+/* Minimal slice: inlier counts of given poses (H x [R 9, t 3] f64, host)
+ * under the reprojection test of PnPRansacCallback::computeError. */
+RSAC_EXPORT int rsac_score_poses(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                     const double *poses, int32_t n_poses, double reproj_thresh, uint32_t flags, int32_t *counts_out,
+                     void *stream);
+
+/* Hypothesis-range evaluation for sharding one problem over ranks
+ * (SURVEY.md §8e): evaluates hypotheses [hyp_begin, hyp_begin + n_hyps) of
+ * the Philox stream and returns the packed key
+ * (count << 32) | (0xFFFFFFFF - local_best_index) of the best one
+ * (lowest index among ties) and that hypothesis' model (R, t).  Ranks
+ * all-reduce(MAX) the key. */
+RSAC_EXPORT int rsac_pnp_evaluate_range(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                            int64_t hyp_begin, int64_t n_hyps, double reproj_thresh, uint64_t seed, uint32_t flags,
+                            int64_t *key_out, double model_out[12], rsac_stats *stats, void *stream);
+
+/* Raw hot-path outputs for hypotheses [hyp_begin, hyp_begin + n_hyps) of
+ * one problem: per-hypothesis status (1 model, 0 solver failed, -1 no
+ * subset), inlier count and model (16 f64: R 9, t 3 | H 9; then valid).
+ * subsets (host int32 n_hyps x 4, optional) replaces the Philox draw, e.g.
+ * with OpenCV's MWC sequence.  This is what the parity tests compare with
+ * the CPU restatement hypothesis by hypothesis. */
+RSAC_EXPORT int rsac_pnp_hypotheses(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                                    int64_t hyp_begin, int32_t n_hyps, double reproj_thresh, uint64_t seed,
+                                    uint32_t flags, const int32_t *subsets, int32_t *counts_out, int8_t *status_out,
+                                    double *models_out, void *stream);
+RSAC_EXPORT int rsac_homography_hypotheses(rsac_ctx *ctx, const void *src, const void *dst, int32_t n,
+                                           int64_t hyp_begin, int32_t n_hyps, double thresh, uint64_t seed,
+                                           uint32_t flags, const int32_t *subsets, int32_t *counts_out,
+                                           int8_t *status_out, double *models_out, void *stream);
+
+/* Mask of a given pose under the RANSAC test (used after a sharded run). */
+RSAC_EXPORT int rsac_pnp_mask(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                  const double model[12], double reproj_thresh, uint32_t flags, uint8_t *mask_out,
+                  int32_t *count_out, void *stream);
+
+/* Host-side non-minimal fits (no GPU needed), f64 AoS host inputs rounded
+ * to f32 like the RANSAC path.  mask may be NULL (= all points).
+ * rsac_pnp_refine: LM on (R, t) in place, cv2.solvePnPRefineLM
+ *   (main_v1.py:508, testpro-K.py:122); returns iterations used.
+ * rsac_homography_fit: normalised least-squares DLT + 10 LM iterations,
+ *   findHomography's method-0 / final polish (main_v1.py:312). */
+RSAC_EXPORT int rsac_pnp_refine(const double *pts3d, const double *pts2d, int32_t n, const double K[9],
+                                const uint8_t *mask, double R[9], double t[3], int32_t max_iter);
+RSAC_EXPORT int rsac_homography_fit(const double *src, const double *dst, int32_t n, const uint8_t *mask,
+                                    double H_out[9]);
+
+/* Rodrigues (cv2.Rodrigues, main_v1.py:895): vector <-> matrix. */
+RSAC_EXPORT void rsac_rodrigues_v2m(const double r[3], double R[9]);
+RSAC_EXPORT void rsac_rodrigues_m2v(const double R[9], double r[3]);
+
+/* RANSACUpdateNumIters (OpenCV ptsetreg.cpp) */
+RSAC_EXPORT int rsac_update_num_iters(double p, double ep, int model_points, int max_iters);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RSAC_H */

@@ -1,0 +1,1080 @@
+/*
+ * rsac_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's RANSAC hot path.  Only tests/, the
+ * cpu_baseline leg of bench.py and __graft_entry__.smoke() may load this
+ * library, and only as the checker / the timed CPU baseline.  The product
+ * (code-reproduction-ransac_amd/csrc) never links or calls it.
+ *
+ * What it restates
+ * ----------------
+ * The reference (Mendel0408/Code-Reproduction-RANSAC) contains no RANSAC
+ * arithmetic of its own: it calls OpenCV (third party, NOT vendored under
+ * /root/reference, version not pinned; semantics below follow the public
+ * OpenCV 4.x calib3d sources: ptsetreg.cpp, fundam.cpp, solvepnp.cpp,
+ * calibration.cpp):
+ *   - cv2.solvePnPRansac   main_v1.py:497-502, testpro-K.py:72-75,
+ *                          testpro.py:536-541, test_pro.py:515-520
+ *   - cv2.findHomography   main_v1.py:312, process.py:200, test02.py:263,
+ *                          testpro.py:350, test_pro.py:351
+ *   - cv2.projectPoints    testpro-K.py:33 (compute_reprojection_error)
+ *   - cv2.solvePnPRefineLM main_v1.py:508-509, testpro-K.py:122-125
+ *   - cv2.Rodrigues        main_v1.py:895, testpro-K.py:84
+ * and re-scores in Python (main_v1.py:332-348, 419).
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - homography RANSAC (MWC sampler, OpenCV getSubset/checkSubset, f32 error,
+ *     RANSAC-phase mask) is pinned against the 24 complete findHomography
+ *     blocks recorded in the reference's debug.log (tests/golden/);
+ *   - PnP: OpenCV's default EPnP kernel is not restated; the north-star P3P
+ *     kernel (Lambda Twist, Persson & Nordberg, ECCV 2018) is.  PnP parity vs
+ *     OpenCV is therefore *unpinned* except for the loose known-answer camera
+ *     origin of testpro-K.py:234; GPU parity is against this restatement.
+ *
+ * Numerics contract shared with the HIP path (bit-exact on counts/masks):
+ *   compile with -ffp-contract=off, no -ffast-math; only + - * / sqrt in any
+ *   quantity that decides a count; f64 projection of f32-rounded inputs,
+ *   rounded to f32, f32 squared error, `err <= (float)(thr*thr)`.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+
+#define ORC_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------ */
+/* RNG 1: OpenCV cv::RNG, multiply-with-carry, seeded (uint64)-1 in         */
+/* RANSACPointSetRegistrator::run (ptsetreg.cpp) -- behind every cv2.* call  */
+/* listed above.                                                             */
+/* ------------------------------------------------------------------------ */
+ORC_API uint32_t orc_mwc_next(uint64_t *st) {
+    *st = (uint64_t)(uint32_t)(*st) * 4164903690u + (*st >> 32);
+    return (uint32_t)(*st);
+}
+
+ORC_API int orc_mwc_uniform(uint64_t *st, int a, int b) {
+    if (a == b) return a;
+    uint32_t r = orc_mwc_next(st);
+    return (int)(r % (uint32_t)(b - a) + (uint32_t)a);
+}
+
+/* ------------------------------------------------------------------------ */
+/* RNG 2: Philox-4x32-10 (Salmon et al., SC'11), the counter-based sampler  */
+/* the north star asks for.  key = seed, counter = (hyp_lo, hyp_hi,          */
+/* problem, block).                                                          */
+/* ------------------------------------------------------------------------ */
+ORC_API void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+typedef struct {
+    uint32_t key[2], ctr[4], buf[4];
+    int pos;
+} orc_stream;
+
+static void stream_init(orc_stream *s, uint64_t seed, uint32_t problem, uint64_t hyp) {
+    s->key[0] = (uint32_t)seed; s->key[1] = (uint32_t)(seed >> 32);
+    s->ctr[0] = (uint32_t)hyp; s->ctr[1] = (uint32_t)(hyp >> 32);
+    s->ctr[2] = problem; s->ctr[3] = 0;
+    s->pos = 4;
+}
+
+static uint32_t stream_next(orc_stream *s) {
+    if (s->pos == 4) {
+        orc_philox4x32_10(s->ctr, s->key, s->buf);
+        s->ctr[3] += 1u;
+        s->pos = 0;
+    }
+    return s->buf[s->pos++];
+}
+
+/* multiply-shift range reduction: floor(r * n / 2^32) */
+static int stream_index(orc_stream *s, int n) {
+    return (int)(((uint64_t)stream_next(s) * (uint64_t)(uint32_t)n) >> 32);
+}
+
+#define ORC_MAX_DRAWS_PER_SUBSET 256
+#define ORC_MAX_SUBSET_ATTEMPTS 10000 /* getSubset(..., rng, 10000) in RANSACPointSetRegistrator::run */
+
+/* draw s distinct indices from the hypothesis' stream; -1 on exhaustion */
+static int stream_subset(orc_stream *st, int n, int s, int32_t *idx) {
+    int draws = 0;
+    for (int i = 0; i < s; ++i) {
+        for (;;) {
+            if (draws++ >= ORC_MAX_DRAWS_PER_SUBSET) return -1;
+            int r = stream_index(st, n);
+            int dup = 0;
+            for (int j = 0; j < i; ++j) dup |= (idx[j] == r);
+            if (!dup) { idx[i] = r; break; }
+        }
+    }
+    return 0;
+}
+
+ORC_API int orc_philox_subset(uint64_t seed, uint32_t problem, uint64_t hyp, int n, int s, int32_t *idx) {
+    if (n < s) return -1;
+    orc_stream st;
+    stream_init(&st, seed, problem, hyp);
+    return stream_subset(&st, n, s, idx);
+}
+
+/* ------------------------------------------------------------------------ */
+/* RANSACUpdateNumIters (ptsetreg.cpp), used after every new best model.     */
+/* ------------------------------------------------------------------------ */
+static int cv_round(double v) { return (int)lrint(v); }
+
+ORC_API int orc_update_num_iters(double p, double ep, int model_points, int max_iters) {
+    if (model_points <= 0) return -1;
+    p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
+    double num = 1. - p; if (num < DBL_MIN) num = DBL_MIN;
+    double denom = 1. - pow(1. - ep, model_points);
+    if (denom < DBL_MIN) return 0;
+    num = log(num);
+    denom = log(denom);
+    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : cv_round(num / denom);
+}
+
+/* Sequential best-model selection of RANSACPointSetRegistrator::run:
+ * iterate hypotheses in index order while iter < niters; status<0 = subset
+ * not found (break; failure if at iter 0), status==0 = kernel produced no
+ * model (continue), else a model whose count replaces the best iff
+ * count > max(best, model_points-1); niters shrinks on each new best. */
+ORC_API int64_t orc_scan(const int32_t *counts, const int8_t *status, int64_t H, int n, int model_points,
+                         double confidence, int max_iters, int32_t *best_count_out, int64_t *iters_out) {
+    int64_t niters = max_iters > 1 ? max_iters : 1;
+    int64_t best = -1, i;
+    int32_t max_good = 0;
+    for (i = 0; i < H && i < niters; ++i) {
+        if (status[i] < 0) { if (i == 0) best = -1; break; }
+        if (status[i] == 0) continue;
+        int32_t c = counts[i];
+        int32_t floor_c = max_good > model_points - 1 ? max_good : model_points - 1;
+        if (c > floor_c) {
+            best = i; max_good = c;
+            niters = orc_update_num_iters(confidence, (double)(n - c) / n, model_points, (int)niters);
+        }
+    }
+    if (best_count_out) *best_count_out = max_good;
+    if (iters_out) *iters_out = i;
+    return best;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Projection + error (PnPRansacCallback::computeError -> projectPoints with */
+/* zero distortion, calibration.cpp), the formula of testpro-K.py:32-36.     */
+/* Inputs are the f32-rounded points (solvePnPRansac converts to CV_32F).    */
+/* ------------------------------------------------------------------------ */
+ORC_API float orc_pnp_err(const double R[9], const double t[3], const double cam[4],
+                          float Xf, float Yf, float Zf, float uf, float vf) {
+    double X = Xf, Y = Yf, Z = Zf;
+    double x = R[0] * X + R[1] * Y; x = x + R[2] * Z; x = x + t[0];
+    double y = R[3] * X + R[4] * Y; y = y + R[5] * Z; y = y + t[1];
+    double z = R[6] * X + R[7] * Y; z = z + R[8] * Z; z = z + t[2];
+    double iz = (z != 0.0) ? 1.0 / z : 1.0;
+    x = x * iz; y = y * iz;
+    double pu = x * cam[0] + cam[2];
+    double pv = y * cam[1] + cam[3];
+    float dx = uf - (float)pu;
+    float dy = vf - (float)pv;
+    float e1 = dx * dx, e2 = dy * dy;
+    return e1 + e2;
+}
+
+ORC_API float orc_thr2(double thr) { return (float)(thr * thr); }
+
+ORC_API int32_t orc_pnp_count(const double R[9], const double t[3], const double cam[4],
+                              const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                              int n, float thr2, uint8_t *mask) {
+    int32_t c = 0;
+    for (int i = 0; i < n; ++i) {
+        float e = orc_pnp_err(R, t, cam, X[i], Y[i], Z[i], U[i], V[i]);
+        int f = e <= thr2;
+        if (mask) mask[i] = (uint8_t)f;
+        c += f;
+    }
+    return c;
+}
+
+/* ------------------------------------------------------------------------ */
+/* P3P: Lambda Twist (Persson & Nordberg 2018), restated.  3 bearings y_k    */
+/* (unit), 3 world points x_k -> up to 4 (R, t) with y_k ~ R x_k + t.        */
+/* ------------------------------------------------------------------------ */
+static void root2real(double b, double c, double *r1, double *r2, int *ok) {
+    double v = b * b - 4.0 * c;
+    if (v < 0.0) { *r1 = 0.5 * b; *r2 = 0.5 * b; *ok = 0; return; }
+    double y = sqrt(v);
+    if (b < 0.0) { *r1 = 0.5 * (-b + y); *r2 = 2.0 * c / (-b + y); }
+    else { *r1 = 2.0 * c / (-b - y); *r2 = 0.5 * (-b - y); }
+    *ok = 1;
+}
+
+/* one real root of g^3 + b g^2 + c g + d: start near the sharpest root, then
+ * Newton (at most 50 steps, stop once |f| <= 1e-13 after the 7th) */
+static double cubic_root(double b, double c, double d) {
+    double r0;
+    if (b * b >= 3.0 * c) {
+        double v = sqrt(b * b - 3.0 * c);
+        double t1 = (-b - v) / 3.0;
+        double k = ((t1 + b) * t1 + c) * t1 + d;
+        if (k > 0.0) {
+            r0 = t1 - sqrt(-k / (3.0 * t1 + b));
+        } else {
+            double t2 = (-b + v) / 3.0;
+            k = ((t2 + b) * t2 + c) * t2 + d;
+            r0 = t2 + sqrt(-k / (3.0 * t2 + b));
+        }
+    } else {
+        r0 = -b / 3.0;
+        if (fabs((3.0 * r0 + 2.0 * b) * r0 + c) < 1e-4) r0 = r0 + 1.0;
+    }
+    for (int it = 0; it < 50; ++it) {
+        double fx = ((r0 + b) * r0 + c) * r0 + d;
+        if (it >= 7 && !(fabs(fx) > 1e-13)) break;
+        double fpx = (3.0 * r0 + 2.0 * b) * r0 + c;
+        r0 = r0 - fx / fpx;
+    }
+    return r0;
+}
+
+/* eigenvectors of the two non-zero eigenvalues of a symmetric 3x3 A whose
+ * third eigenvalue is known to be 0; columns: v1 (|e1|>=|e2|), v2 */
+static void eig_known0(const double A[9], double v1[3], double v2[3], double *e1o, double *e2o) {
+    double a00 = A[0], a01 = A[1], a02 = A[2], a11 = A[4], a12 = A[5], a22 = A[8];
+    double a01sq = a01 * a01;
+    double b = -a00 - a11 - a22;
+    double c = -a01sq - a02 * a02 - a12 * a12 + a00 * (a11 + a22) + a11 * a22;
+    double e1, e2; int ok;
+    root2real(b, c, &e1, &e2, &ok);
+    if (fabs(e1) < fabs(e2)) { double tmp = e1; e1 = e2; e2 = tmp; }
+    double m0011 = -a00 * a11;
+    double pr0 = a01 * a12 - a02 * a11;
+    double pr1 = a01 * a02 - a00 * a12;
+    {
+        double e = e1;
+        double tmp = 1.0 / (e * (a00 + a11) + m0011 - e * e + a01sq);
+        double q1 = -(e * a02 + pr0) * tmp;
+        double q2 = -(e * a12 + pr1) * tmp;
+        double rn = 1.0 / sqrt(q1 * q1 + q2 * q2 + 1.0);
+        v1[0] = q1 * rn; v1[1] = q2 * rn; v1[2] = rn;
+    }
+    {
+        double e = e2;
+        double tmp = 1.0 / (e * (a00 + a11) + m0011 - e * e + a01sq);
+        double q1 = -(e * a02 + pr0) * tmp;
+        double q2 = -(e * a12 + pr1) * tmp;
+        double rn = 1.0 / sqrt(q1 * q1 + q2 * q2 + 1.0);
+        v2[0] = q1 * rn; v2[1] = q2 * rn; v2[2] = rn;
+    }
+    *e1o = e1; *e2o = e2;
+}
+
+static double lt_resid(const double L[3], double a12, double a13, double a23, double b12, double b13, double b23,
+                       double r[3]) {
+    double l1 = L[0], l2 = L[1], l3 = L[2];
+    r[0] = l1 * l1 + l2 * l2 + b12 * l1 * l2 - a12;
+    r[1] = l1 * l1 + l3 * l3 + b13 * l1 * l3 - a13;
+    r[2] = l2 * l2 + l3 * l3 + b23 * l2 * l3 - a23;
+    return fabs(r[0]) + fabs(r[1]) + fabs(r[2]);
+}
+
+static void lt_refine(double L[3], double a12, double a13, double a23, double b12, double b13, double b23) {
+    for (int it = 0; it < 5; ++it) {
+        double r[3];
+        double s0 = lt_resid(L, a12, a13, a23, b12, b13, b23, r);
+        if (s0 < 1e-10) break;
+        double l1 = L[0], l2 = L[1], l3 = L[2];
+        double j0 = 2.0 * l1 + b12 * l2;  /* dr1/dl1 */
+        double j1 = 2.0 * l2 + b12 * l1;  /* dr1/dl2 */
+        double j3 = 2.0 * l1 + b13 * l3;  /* dr2/dl1 */
+        double j5 = 2.0 * l3 + b13 * l1;  /* dr2/dl3 */
+        double j7 = 2.0 * l2 + b23 * l3;  /* dr3/dl2 */
+        double j8 = 2.0 * l3 + b23 * l2;  /* dr3/dl3 */
+        double det = 1.0 / (-j0 * j5 * j7 - j1 * j3 * j8);
+        double d0 = -j5 * j7 * r[0] + -j1 * j8 * r[1] + j1 * j5 * r[2];
+        double d1 = -j3 * j8 * r[0] + j0 * j8 * r[1] + -j0 * j5 * r[2];
+        double d2 = j3 * j7 * r[0] + -j0 * j7 * r[1] + -j1 * j3 * r[2];
+        double Ln[3];
+        Ln[0] = l1 - det * d0; Ln[1] = l2 - det * d1; Ln[2] = l3 - det * d2;
+        double rn[3];
+        double s1 = lt_resid(Ln, a12, a13, a23, b12, b13, b23, rn);
+        if (s1 > s0) break;
+        L[0] = Ln[0]; L[1] = Ln[1]; L[2] = Ln[2];
+    }
+}
+
+static void cross3(const double a[3], const double b[3], double c[3]) {
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+/* inverse of the 3x3 (row-major) by the adjugate; 0 if singular */
+static int inv3(const double M[9], double I[9]) {
+    double c00 = M[4] * M[8] - M[5] * M[7];
+    double c01 = M[5] * M[6] - M[3] * M[8];
+    double c02 = M[3] * M[7] - M[4] * M[6];
+    double det = M[0] * c00 + M[1] * c01 + M[2] * c02;
+    if (det == 0.0 || !isfinite(det)) return 0;
+    double id = 1.0 / det;
+    I[0] = c00 * id; I[1] = (M[2] * M[7] - M[1] * M[8]) * id; I[2] = (M[1] * M[5] - M[2] * M[4]) * id;
+    I[3] = c01 * id; I[4] = (M[0] * M[8] - M[2] * M[6]) * id; I[5] = (M[2] * M[3] - M[0] * M[5]) * id;
+    I[6] = c02 * id; I[7] = (M[1] * M[6] - M[0] * M[7]) * id; I[8] = (M[0] * M[4] - M[1] * M[3]) * id;
+    return 1;
+}
+
+/* y: 3 unit bearings (row k = bearing k); x: 3 world points.  Returns the
+ * number of solutions written to Rs (k*9) / ts (k*3). */
+ORC_API int orc_p3p(const double y[9], const double x[9], double Rs[36], double ts[12]) {
+    const double *y1 = y, *y2 = y + 3, *y3 = y + 6;
+    const double *x1 = x, *x2 = x + 3, *x3 = x + 6;
+    double b12 = -2.0 * (y1[0] * y2[0] + y1[1] * y2[1] + y1[2] * y2[2]);
+    double b13 = -2.0 * (y1[0] * y3[0] + y1[1] * y3[1] + y1[2] * y3[2]);
+    double b23 = -2.0 * (y2[0] * y3[0] + y2[1] * y3[1] + y2[2] * y3[2]);
+    double d12[3], d13[3], d23[3], d12xd13[3];
+    for (int k = 0; k < 3; ++k) { d12[k] = x1[k] - x2[k]; d13[k] = x1[k] - x3[k]; d23[k] = x2[k] - x3[k]; }
+    cross3(d12, d13, d12xd13);
+    double a12 = d12[0] * d12[0] + d12[1] * d12[1] + d12[2] * d12[2];
+    double a13 = d13[0] * d13[0] + d13[1] * d13[1] + d13[2] * d13[2];
+    double a23 = d23[0] * d23[0] + d23[1] * d23[1] + d23[2] * d23[2];
+
+    double c31 = -0.5 * b13, c23 = -0.5 * b23, c12 = -0.5 * b12;
+    double blob = c12 * c23 * c31 - 1.0;
+    double s31 = 1.0 - c31 * c31, s23 = 1.0 - c23 * c23, s12 = 1.0 - c12 * c12;
+
+    double p3 = a13 * (a23 * s31 - a13 * s23);
+    double p2 = 2.0 * blob * a23 * a13 + a13 * (2.0 * a12 + a13) * s23 + a23 * (a23 - a12) * s31;
+    double p1 = a23 * (a13 - a23) * s12 - a12 * a12 * s23 - 2.0 * a12 * (blob * a23 + a13 * s23);
+    double p0 = a12 * (a12 * s23 - a23 * s12);
+    if (p3 == 0.0 || !isfinite(p3)) return 0;
+    double ip3 = 1.0 / p3;
+    p2 = p2 * ip3; p1 = p1 * ip3; p0 = p0 * ip3;
+    double g = cubic_root(p2, p1, p0);
+
+    double A[9];
+    A[0] = a23 * (1.0 - g);
+    A[1] = (a23 * b12) * 0.5;
+    A[2] = (a23 * b13 * g) * (-0.5);
+    A[4] = a23 - a12 + a13 * g;
+    A[5] = b23 * (a13 * g - a12) * 0.5;
+    A[8] = g * (a13 - a23) - a12;
+    A[3] = A[1]; A[6] = A[2]; A[7] = A[5];
+
+    double v1[3], v2[3], e1, e2;
+    eig_known0(A, v1, v2, &e1, &e2);
+    double vq = -e2 / e1;
+    double v = sqrt(vq > 0.0 ? vq : 0.0);
+
+    double Ls[4][3];
+    int valid = 0;
+    for (int sgn = 0; sgn < 2; ++sgn) {
+        double s = sgn == 0 ? v : -v;
+        double w2 = 1.0 / (s * v2[0] - v1[0]);
+        double w0 = (v1[1] - s * v2[1]) * w2;
+        double w1 = (v1[2] - s * v2[2]) * w2;
+        double a = 1.0 / ((a13 - a12) * w1 * w1 - a12 * b13 * w1 - a12);
+        double b = (a13 * b12 * w1 - a12 * b13 * w0 - 2.0 * w0 * w1 * (a12 - a13)) * a;
+        double c = ((a13 - a12) * w0 * w0 + a13 * b12 * w0 + a13) * a;
+        if (b * b - 4.0 * c >= 0.0) {
+            double tau[2]; int ok;
+            root2real(b, c, &tau[0], &tau[1], &ok);
+            for (int q = 0; q < 2; ++q) {
+                if (tau[q] > 0.0) {
+                    double tq = tau[q];
+                    double d = a23 / (tq * (b23 + tq) + 1.0);
+                    if (d > 0.0) {
+                        double l2 = sqrt(d);
+                        double l3 = tq * l2;
+                        double l1 = w0 * l2 + w1 * l3;
+                        if (l1 >= 0.0) { Ls[valid][0] = l1; Ls[valid][1] = l2; Ls[valid][2] = l3; ++valid; }
+                    }
+                }
+            }
+        }
+    }
+    for (int i = 0; i < valid; ++i) lt_refine(Ls[i], a12, a13, a23, b12, b13, b23);
+
+    double Xm[9] = {d12[0], d13[0], d12xd13[0], d12[1], d13[1], d12xd13[1], d12[2], d13[2], d12xd13[2]};
+    double Xi[9];
+    if (!inv3(Xm, Xi)) return 0;
+    int nout = 0;
+    for (int i = 0; i < valid; ++i) {
+        double ry1[3], ry2[3], ry3[3], yd1[3], yd2[3], yd1xd2[3];
+        for (int k = 0; k < 3; ++k) { ry1[k] = y1[k] * Ls[i][0]; ry2[k] = y2[k] * Ls[i][1]; ry3[k] = y3[k] * Ls[i][2]; }
+        for (int k = 0; k < 3; ++k) { yd1[k] = ry1[k] - ry2[k]; yd2[k] = ry1[k] - ry3[k]; }
+        cross3(yd1, yd2, yd1xd2);
+        double Ym[9] = {yd1[0], yd2[0], yd1xd2[0], yd1[1], yd2[1], yd1xd2[1], yd1[2], yd2[2], yd1xd2[2]};
+        double *R = Rs + 9 * nout, *t = ts + 3 * nout;
+        for (int r = 0; r < 3; ++r)
+            for (int cc = 0; cc < 3; ++cc)
+                R[3 * r + cc] = Ym[3 * r] * Xi[cc] + Ym[3 * r + 1] * Xi[3 + cc] + Ym[3 * r + 2] * Xi[6 + cc];
+        int fin = 1;
+        for (int r = 0; r < 3; ++r) {
+            double rx = R[3 * r] * x1[0] + R[3 * r + 1] * x1[1] + R[3 * r + 2] * x1[2];
+            t[r] = ry1[r] - rx;
+            fin &= isfinite(t[r]) != 0;
+        }
+        for (int k = 0; k < 9; ++k) fin &= isfinite(R[k]) != 0;
+        if (fin) ++nout;
+    }
+    return nout;
+}
+
+/* bearing of pixel (u, v): K^-1 [u v 1]^T normalised (skew ignored, as in
+ * cvProjectPoints2Internal which reads only fx, fy, cx, cy) */
+static void bearing(const double cam[4], float uf, float vf, double out[3]) {
+    double xn = ((double)uf - cam[2]) / cam[0];
+    double yn = ((double)vf - cam[3]) / cam[1];
+    double nrm = sqrt(xn * xn + yn * yn + 1.0);
+    out[0] = xn / nrm; out[1] = yn / nrm; out[2] = 1.0 / nrm;
+}
+
+/* 4-point minimal PnP kernel (as OpenCV's SOLVEPNP_P3P with 4 points: solve
+ * on the first three, keep the solution that reprojects the fourth best).
+ * Returns 1 and (R, t) when a model exists, 0 otherwise. */
+ORC_API int orc_pnp_minimal(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                            const int32_t idx[4], const double cam[4], double R[9], double t[3]) {
+    double yb[9], xw[9];
+    for (int k = 0; k < 3; ++k) {
+        int i = idx[k];
+        bearing(cam, U[i], V[i], yb + 3 * k);
+        xw[3 * k] = X[i]; xw[3 * k + 1] = Y[i]; xw[3 * k + 2] = Z[i];
+    }
+    double Rs[36], ts[12];
+    int ns = orc_p3p(yb, xw, Rs, ts);
+    if (ns == 0) return 0;
+    int i4 = idx[3];
+    double X4 = X[i4], Y4 = Y[i4], Z4 = Z[i4];
+    int best = -1;
+    double best_e = 0.0;
+    for (int s = 0; s < ns; ++s) {
+        const double *Rk = Rs + 9 * s, *tk = ts + 3 * s;
+        double x = Rk[0] * X4 + Rk[1] * Y4; x = x + Rk[2] * Z4; x = x + tk[0];
+        double y = Rk[3] * X4 + Rk[4] * Y4; y = y + Rk[5] * Z4; y = y + tk[1];
+        double z = Rk[6] * X4 + Rk[7] * Y4; z = z + Rk[8] * Z4; z = z + tk[2];
+        double iz = (z != 0.0) ? 1.0 / z : 1.0;
+        double du = (x * iz) * cam[0] + cam[2] - (double)U[i4];
+        double dv = (y * iz) * cam[1] + cam[3] - (double)V[i4];
+        double e = du * du + dv * dv;
+        if (!(e == e)) continue;
+        if (best < 0 || e < best_e) { best = s; best_e = e; }
+    }
+    if (best < 0) return 0;
+    memcpy(R, Rs + 9 * best, 9 * sizeof(double));
+    memcpy(t, ts + 3 * best, 3 * sizeof(double));
+    return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Homography (HomographyEstimatorCallback, fundam.cpp) for findHomography   */
+/* at main_v1.py:312 / process.py:200.                                       */
+/* ------------------------------------------------------------------------ */
+
+/* haveCollinearPoints(m, count): only the last point against every pair */
+static int have_collinear(const float *px, const float *py, const int32_t *idx, int count) {
+    int i = count - 1;
+    for (int j = 0; j < i; ++j) {
+        double dx1 = (double)(px[idx[j]] - px[idx[i]]);
+        double dy1 = (double)(py[idx[j]] - py[idx[i]]);
+        for (int k = 0; k < j; ++k) {
+            double dx2 = (double)(px[idx[k]] - px[idx[i]]);
+            double dy2 = (double)(py[idx[k]] - py[idx[i]]);
+            if (fabs(dx2 * dy1 - dy2 * dx1) <= FLT_EPSILON * (fabs(dx1) + fabs(dy1) + fabs(dx2) + fabs(dy2)))
+                return 1;
+        }
+    }
+    return 0;
+}
+
+static double det3_rows(double a0, double a1, double b0, double b1, double c0, double c1) {
+    /* Matx33d determinant of [[a0 a1 1],[b0 b1 1],[c0 c1 1]] (OpenCV's expansion) */
+    return a0 * (b1 * 1. - c1 * 1.) - a1 * (b0 * 1. - c0 * 1.) + 1. * (b0 * c1 - c0 * b1);
+}
+
+/* checkSubset(ms1, ms2, 4): collinearity in src and dst, then the
+ * orientation-consistency test of Marquez-Neila et al. */
+ORC_API int orc_hom_check_subset(const float *sx, const float *sy, const float *dx, const float *dy,
+                                 const int32_t idx[4]) {
+    if (have_collinear(sx, sy, idx, 4) || have_collinear(dx, dy, idx, 4)) return 0;
+    static const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
+    int negative = 0;
+    for (int i = 0; i < 4; ++i) {
+        const int *q = tt[i];
+        int p0 = idx[q[0]], p1 = idx[q[1]], p2 = idx[q[2]];
+        double dA = det3_rows(sx[p0], sy[p0], sx[p1], sy[p1], sx[p2], sy[p2]);
+        double dB = det3_rows(dx[p0], dy[p0], dx[p1], dy[p1], dx[p2], dy[p2]);
+        negative += dA * dB < 0;
+    }
+    return negative == 0 || negative == 4;
+}
+
+/* normalisation of HomographyEstimatorCallback::runKernel */
+typedef struct { double cMx, cMy, cmx, cmy, sMx, sMy, smx, smy; } hnorm;
+
+static int hom_norm(const float *sx, const float *sy, const float *dx, const float *dy, const int32_t *idx,
+                    int count, hnorm *h) {
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+    for (int i = 0; i < count; ++i) {
+        int p = idx ? idx[i] : i;
+        cmx += dx[p]; cmy += dy[p];
+        cMx += sx[p]; cMy += sy[p];
+    }
+    cmx /= count; cmy /= count; cMx /= count; cMy /= count;
+    for (int i = 0; i < count; ++i) {
+        int p = idx ? idx[i] : i;
+        smx += fabs(dx[p] - cmx); smy += fabs(dy[p] - cmy);
+        sMx += fabs(sx[p] - cMx); sMy += fabs(sy[p] - cMy);
+    }
+    if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON || fabs(sMy) < DBL_EPSILON)
+        return 0;
+    h->smx = count / smx; h->smy = count / smy; h->sMx = count / sMx; h->sMy = count / sMy;
+    h->cmx = cmx; h->cmy = cmy; h->cMx = cMx; h->cMy = cMy;
+    return 1;
+}
+
+static void mat3mul(const double A[9], const double B[9], double C[9]) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+/* H = invHnorm * Hn * Hnorm2, then scaled by 1/H22 (convertTo) */
+static void hom_denorm(const hnorm *h, const double Hn[9], double H[9]) {
+    double invHnorm[9] = {1. / h->smx, 0, h->cmx, 0, 1. / h->smy, h->cmy, 0, 0, 1};
+    double Hnorm2[9] = {h->sMx, 0, -h->cMx * h->sMx, 0, h->sMy, -h->cMy * h->sMy, 0, 0, 1};
+    double T[9], H0[9];
+    mat3mul(invHnorm, Hn, T);
+    mat3mul(T, Hnorm2, H0);
+    double sc = 1. / H0[8];
+    for (int k = 0; k < 9; ++k) H[k] = H0[k] * sc;
+}
+
+/* Minimal 4-point kernel of this build: the normalised DLT of runKernel,
+ * solved as the 8x8 system with h22 = 1 by Gaussian elimination with
+ * partial pivoting (first max on ties).  Exactly determined for 4 points,
+ * so it is the same model as OpenCV's LtL null vector up to rounding. */
+ORC_API int orc_hom_minimal(const float *sx, const float *sy, const float *dx, const float *dy,
+                            const int32_t idx[4], double H[9]) {
+    hnorm nm;
+    if (!hom_norm(sx, sy, dx, dy, idx, 4, &nm)) return 0;
+    double A[8][9];
+    for (int i = 0; i < 4; ++i) {
+        int p = idx[i];
+        double x = (dx[p] - nm.cmx) * nm.smx, y = (dy[p] - nm.cmy) * nm.smy;
+        double X = (sx[p] - nm.cMx) * nm.sMx, Y = (sy[p] - nm.cMy) * nm.sMy;
+        double *r0 = A[2 * i], *r1 = A[2 * i + 1];
+        r0[0] = X; r0[1] = Y; r0[2] = 1; r0[3] = 0; r0[4] = 0; r0[5] = 0; r0[6] = -x * X; r0[7] = -x * Y; r0[8] = x;
+        r1[0] = 0; r1[1] = 0; r1[2] = 0; r1[3] = X; r1[4] = Y; r1[5] = 1; r1[6] = -y * X; r1[7] = -y * Y; r1[8] = y;
+    }
+    for (int k = 0; k < 8; ++k) {
+        int piv = k;
+        double pm = fabs(A[k][k]);
+        for (int r = k + 1; r < 8; ++r) {
+            double v = fabs(A[r][k]);
+            if (v > pm) { pm = v; piv = r; }
+        }
+        if (!(pm > 1e-10)) return 0;
+        if (piv != k)
+            for (int j = 0; j < 9; ++j) { double tmp = A[k][j]; A[k][j] = A[piv][j]; A[piv][j] = tmp; }
+        for (int r = k + 1; r < 8; ++r) {
+            double f = A[r][k] / A[k][k];
+            for (int j = k + 1; j < 9; ++j) A[r][j] = A[r][j] - f * A[k][j];
+        }
+    }
+    double h[8];
+    for (int k = 7; k >= 0; --k) {
+        double s = A[k][8];
+        for (int j = k + 1; j < 8; ++j) s = s - A[k][j] * h[j];
+        h[k] = s / A[k][k];
+    }
+    double Hn[9] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], 1.0};
+    hom_denorm(&nm, Hn, H);
+    for (int k = 0; k < 9; ++k) if (!isfinite(H[k])) return 0;
+    return 1;
+}
+
+/* HomographyEstimatorCallback::computeError, all in f32 */
+ORC_API float orc_hom_err(const double H[9], float x, float y, float u, float v) {
+    float h0 = (float)H[0], h1 = (float)H[1], h2 = (float)H[2], h3 = (float)H[3];
+    float h4 = (float)H[4], h5 = (float)H[5], h6 = (float)H[6], h7 = (float)H[7];
+    float ww = 1.f / (h6 * x + h7 * y + 1.f);
+    float ex = (h0 * x + h1 * y + h2) * ww - u;
+    float ey = (h3 * x + h4 * y + h5) * ww - v;
+    float e1 = ex * ex, e2 = ey * ey;
+    return e1 + e2;
+}
+
+ORC_API int32_t orc_hom_count(const double H[9], const float *sx, const float *sy, const float *dx, const float *dy,
+                              int n, float thr2, uint8_t *mask) {
+    int32_t c = 0;
+    for (int i = 0; i < n; ++i) {
+        int f = orc_hom_err(H, sx[i], sy[i], dx[i], dy[i]) <= thr2;
+        if (mask) mask[i] = (uint8_t)f;
+        c += f;
+    }
+    return c;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Subset generation                                                          */
+/* ------------------------------------------------------------------------ */
+
+/* OpenCV getSubset(m1, m2, ms1, ms2, rng, 10000) with checkPartialSubsets ==
+ * false, run sequentially for H hypotheses sharing one MWC state.  For the
+ * homography model the checkSubset test is applied (pass sx..dy), for PnP
+ * pass NULL (PnPRansacCallback has no checkSubset).  status[h] = 1 found,
+ * -1 not found (the RANSAC loop then stops). */
+ORC_API void orc_mwc_subsets(uint64_t *state, int n, int s, int64_t H, const float *sx, const float *sy,
+                             const float *dx, const float *dy, int32_t *out, int8_t *status) {
+    for (int64_t h = 0; h < H; ++h) {
+        int32_t *idx = out + s * h;
+        int found = 0;
+        for (int att = 0; att < ORC_MAX_SUBSET_ATTEMPTS; ++att) {
+            for (int i = 0; i < s; ++i) {
+                int r;
+                for (;;) {
+                    r = orc_mwc_uniform(state, 0, n);
+                    int dup = 0;
+                    for (int j = 0; j < i; ++j) dup |= (idx[j] == r);
+                    if (!dup) break;
+                }
+                idx[i] = r;
+            }
+            if (sx && !orc_hom_check_subset(sx, sy, dx, dy, idx)) continue;
+            found = 1;
+            break;
+        }
+        status[h] = found ? 1 : -1;
+        if (!found) {
+            for (int64_t g = h + 1; g < H; ++g) status[g] = -1;
+            return;
+        }
+    }
+}
+
+/* Philox subsets for the homography model: attempts until checkSubset
+ * passes, all drawn from the hypothesis' own stream. */
+static int philox_hom_subset(orc_stream *st, int n, const float *sx, const float *sy, const float *dx,
+                             const float *dy, int32_t idx[4]) {
+    for (int att = 0; att < ORC_MAX_SUBSET_ATTEMPTS; ++att) {
+        if (stream_subset(st, n, 4, idx) < 0) return -1;
+        if (orc_hom_check_subset(sx, sy, dx, dy, idx)) return 0;
+    }
+    return -1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Per-hypothesis evaluation (what the GPU computes): status, count, model.  */
+/* subsets == NULL -> Philox sampler (seed, problem, hyp0 + h).              */
+/* models: H x 16 doubles (R 9, t 3, pad); may be NULL.                      */
+/* ------------------------------------------------------------------------ */
+ORC_API void orc_pnp_hypotheses(const float *X, const float *Y, const float *Z, const float *U, const float *V, int n,
+                                const double cam[4], float thr2, uint64_t seed, uint32_t problem, int64_t hyp0,
+                                int64_t H, const int32_t *subsets, const int8_t *sub_status, int32_t *counts,
+                                int8_t *status, double *models) {
+    for (int64_t h = 0; h < H; ++h) {
+        int32_t idx[4];
+        double R[9] = {0}, t[3] = {0};
+        int8_t st;
+        if (subsets) {
+            st = sub_status ? sub_status[h] : 1;
+            memcpy(idx, subsets + 4 * h, sizeof(idx));
+        } else {
+            st = orc_philox_subset(seed, problem, (uint64_t)(hyp0 + h), n, 4, idx) < 0 ? -1 : 1;
+        }
+        int32_t c = 0;
+        if (st > 0) {
+            st = (int8_t)orc_pnp_minimal(X, Y, Z, U, V, idx, cam, R, t);
+            if (st) c = orc_pnp_count(R, t, cam, X, Y, Z, U, V, n, thr2, NULL);
+        }
+        counts[h] = c;
+        status[h] = st;
+        if (models) {
+            double *m = models + 16 * h;
+            memset(m, 0, 16 * sizeof(double));
+            memcpy(m, R, 9 * sizeof(double));
+            memcpy(m + 9, t, 3 * sizeof(double));
+        }
+    }
+}
+
+ORC_API void orc_hom_hypotheses(const float *sx, const float *sy, const float *dx, const float *dy, int n,
+                                float thr2, uint64_t seed, uint32_t problem, int64_t hyp0, int64_t H,
+                                const int32_t *subsets, const int8_t *sub_status, int32_t *counts, int8_t *status,
+                                double *models) {
+    for (int64_t h = 0; h < H; ++h) {
+        int32_t idx[4];
+        double Hm[9] = {0};
+        int8_t st;
+        if (subsets) {
+            st = sub_status ? sub_status[h] : 1;
+            memcpy(idx, subsets + 4 * h, sizeof(idx));
+        } else {
+            orc_stream s;
+            stream_init(&s, seed, problem, (uint64_t)(hyp0 + h));
+            st = (n >= 4 && philox_hom_subset(&s, n, sx, sy, dx, dy, idx) == 0) ? 1 : -1;
+        }
+        int32_t c = 0;
+        if (st > 0) {
+            st = (int8_t)orc_hom_minimal(sx, sy, dx, dy, idx, Hm);
+            if (st) c = orc_hom_count(Hm, sx, sy, dx, dy, n, thr2, NULL);
+        }
+        counts[h] = c;
+        status[h] = st;
+        if (models) {
+            double *m = models + 16 * h;
+            memset(m, 0, 16 * sizeof(double));
+            memcpy(m, Hm, 9 * sizeof(double));
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Rodrigues (cv::Rodrigues, main_v1.py:895)                                  */
+/* ------------------------------------------------------------------------ */
+ORC_API void orc_rodrigues_v2m(const double r[3], double R[9]) {
+    double th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    if (th < DBL_EPSILON) {
+        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    double c = cos(th), s = sin(th), c1 = 1. - c, it = 1. / th;
+    double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+    R[0] = c + c1 * x * x;     R[1] = c1 * x * y - s * z; R[2] = c1 * x * z + s * y;
+    R[3] = c1 * x * y + s * z; R[4] = c + c1 * y * y;     R[5] = c1 * y * z - s * x;
+    R[6] = c1 * x * z - s * y; R[7] = c1 * y * z + s * x; R[8] = c + c1 * z * z;
+}
+
+ORC_API void orc_rodrigues_m2v(const double R[9], double r[3]) {
+    /* rotation angle/axis from the antisymmetric part, with the theta ~ pi
+     * branch taken from the symmetric part (as cv::Rodrigues does) */
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double th = acos(c);
+    if (s < 1e-5) {
+        if (c > 0) { r[0] = r[1] = r[2] = 0; return; }
+        double t;
+        t = (R[0] + 1) * 0.5; rx = sqrt(t > 0 ? t : 0);
+        t = (R[4] + 1) * 0.5; ry = sqrt(t > 0 ? t : 0) * (R[1] < 0 ? -1. : 1.);
+        t = (R[8] + 1) * 0.5; rz = sqrt(t > 0 ? t : 0) * (R[2] < 0 ? -1. : 1.);
+        if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+        double n = sqrt(rx * rx + ry * ry + rz * rz);
+        th = th / n;
+        r[0] = rx * th; r[1] = ry * th; r[2] = rz * th;
+        return;
+    }
+    double vth = 1 / (2 * s) * th;
+    r[0] = rx * vth; r[1] = ry * vth; r[2] = rz * vth;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Final refits (non-minimal solve on the RANSAC inliers).                   */
+/* ------------------------------------------------------------------------ */
+
+/* Solve the n x n SPD system (A + lam*diag(A)) x = b by Cholesky. */
+static int chol_solve(int n, const double *A, double lam, const double *b, double *x) {
+    double L[81];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double s = A[i * n + j];
+            if (i == j) s = s + lam * A[i * n + i];
+            for (int k = 0; k < j; ++k) s = s - L[i * n + k] * L[j * n + k];
+            if (i == j) {
+                if (!(s > 0)) return 0;
+                L[i * n + i] = sqrt(s);
+            } else {
+                L[i * n + j] = s / L[j * n + j];
+            }
+        }
+    double y[9];
+    for (int i = 0; i < n; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s = s - L[i * n + k] * y[k];
+        y[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double s = y[i];
+        for (int k = i + 1; k < n; ++k) s = s - L[k * n + i] * x[k];
+        x[i] = s / L[i * n + i];
+    }
+    return 1;
+}
+
+static double pnp_cost(const double R[9], const double t[3], const double cam[4], const float *X, const float *Y,
+                       const float *Z, const float *U, const float *V, const uint8_t *mask, int n) {
+    double cost = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!mask[i]) continue;
+        double Xd = X[i], Yd = Y[i], Zd = Z[i];
+        double x = R[0] * Xd + R[1] * Yd + R[2] * Zd + t[0];
+        double y = R[3] * Xd + R[4] * Yd + R[5] * Zd + t[1];
+        double z = R[6] * Xd + R[7] * Yd + R[8] * Zd + t[2];
+        double iz = 1.0 / z;
+        double ru = cam[0] * x * iz + cam[2] - U[i];
+        double rv = cam[1] * y * iz + cam[3] - V[i];
+        cost += ru * ru + rv * rv;
+    }
+    return cost;
+}
+
+/* Levenberg-Marquardt on the masked points, R <- Exp(w) R, t <- t + dt
+ * (the role of solvePnPRefineLM / the ITERATIVE final solvePnP,
+ * main_v1.py:508, testpro-K.py:122).  Returns iterations used. */
+ORC_API int orc_pnp_refine(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                           const uint8_t *mask, int n, const double cam[4], double R[9], double t[3], int max_iter) {
+    double lam = 1e-3;
+    double cost = pnp_cost(R, t, cam, X, Y, Z, U, V, mask, n);
+    int it;
+    for (it = 0; it < max_iter; ++it) {
+        double A[36] = {0}, g[6] = {0};
+        for (int i = 0; i < n; ++i) {
+            if (!mask[i]) continue;
+            double Xd = X[i], Yd = Y[i], Zd = Z[i];
+            double px = R[0] * Xd + R[1] * Yd + R[2] * Zd;
+            double py = R[3] * Xd + R[4] * Yd + R[5] * Zd;
+            double pz = R[6] * Xd + R[7] * Yd + R[8] * Zd;
+            double cx = px + t[0], cy = py + t[1], cz = pz + t[2];
+            double iz = 1.0 / cz;
+            double ru = cam[0] * cx * iz + cam[2] - U[i];
+            double rv = cam[1] * cy * iz + cam[3] - V[i];
+            double dux = cam[0] * iz, duz = -cam[0] * cx * iz * iz;
+            double dvy = cam[1] * iz, dvz = -cam[1] * cy * iz * iz;
+            /* d(c)/dw = -[p]x : rows (0, pz, -py), (-pz, 0, px), (py, -px, 0) */
+            double Ju[6], Jv[6];
+            Ju[0] = duz * py;            Ju[1] = dux * pz - duz * px; Ju[2] = -dux * py;
+            Jv[0] = -dvy * pz + dvz * py; Jv[1] = -dvz * px;           Jv[2] = dvy * px;
+            Ju[3] = dux; Ju[4] = 0; Ju[5] = duz;
+            Jv[3] = 0; Jv[4] = dvy; Jv[5] = dvz;
+            for (int a = 0; a < 6; ++a) {
+                g[a] += Ju[a] * ru + Jv[a] * rv;
+                for (int b = 0; b <= a; ++b) A[a * 6 + b] += Ju[a] * Ju[b] + Jv[a] * Jv[b];
+            }
+        }
+        for (int a = 0; a < 6; ++a)
+            for (int b = a + 1; b < 6; ++b) A[a * 6 + b] = A[b * 6 + a];
+        int accepted = 0;
+        while (!accepted) {
+            double d[6], mg[6];
+            for (int a = 0; a < 6; ++a) mg[a] = -g[a];
+            if (!chol_solve(6, A, lam, mg, d)) { lam *= 10; if (lam > 1e10) return it; continue; }
+            double Rw[9], Rn[9], tn[3];
+            orc_rodrigues_v2m(d, Rw);
+            mat3mul(Rw, R, Rn);
+            for (int k = 0; k < 3; ++k) tn[k] = t[k] + d[3 + k];
+            double cn = pnp_cost(Rn, tn, cam, X, Y, Z, U, V, mask, n);
+            if (cn < cost) {
+                double rel = (cost - cn) / (cost > 1e-300 ? cost : 1e-300);
+                memcpy(R, Rn, sizeof(Rn)); memcpy(t, tn, sizeof(tn));
+                cost = cn;
+                lam = lam * 0.1 > 1e-12 ? lam * 0.1 : 1e-12;
+                accepted = 1;
+                if (rel < 1e-12) return it + 1;
+            } else {
+                lam *= 10;
+                if (lam > 1e10) return it;
+            }
+        }
+    }
+    return it;
+}
+
+/* Symmetric eigen-decomposition (cyclic Jacobi) -> eigenvector of the
+ * smallest eigenvalue; used by the least-squares homography on inliers. */
+static void jacobi_min_evec(int n, double *A, double *v_out) {
+    double V[81];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0;
+        for (int i = 0; i < n; ++i)
+            for (int j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
+        if (off < 1e-300) break;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                double apq = A[p * n + q];
+                if (fabs(apq) < 1e-300) continue;
+                double app = A[p * n + p], aqq = A[q * n + q];
+                double theta = (aqq - app) / (2.0 * apq);
+                double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
+                for (int k = 0; k < n; ++k) {
+                    double akp = A[k * n + p], akq = A[k * n + q];
+                    A[k * n + p] = c * akp - s * akq;
+                    A[k * n + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double apk = A[p * n + k], aqk = A[q * n + k];
+                    A[p * n + k] = c * apk - s * aqk;
+                    A[q * n + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double vkp = V[k * n + p], vkq = V[k * n + q];
+                    V[k * n + p] = c * vkp - s * vkq;
+                    V[k * n + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    int mi = 0;
+    for (int i = 1; i < n; ++i)
+        if (A[i * n + i] < A[mi * n + mi]) mi = i;
+    for (int k = 0; k < n; ++k) v_out[k] = V[k * n + mi];
+}
+
+static double hom_cost(const double h[9], const float *sx, const float *sy, const float *dx, const float *dy,
+                       const uint8_t *mask, int n) {
+    double c = 0;
+    for (int i = 0; i < n; ++i) {
+        if (mask && !mask[i]) continue;
+        double x = sx[i], y = sy[i];
+        double ww = 1. / (h[6] * x + h[7] * y + 1.);
+        double ex = (h[0] * x + h[1] * y + h[2]) * ww - dx[i];
+        double ey = (h[3] * x + h[4] * y + h[5]) * ww - dy[i];
+        c += ex * ex + ey * ey;
+    }
+    return c;
+}
+
+/* non-minimal refit of findHomography (fundam.cpp): least-squares
+ * normalised DLT on the inliers, then 10 LM iterations on the
+ * reprojection error (HomographyRefineCallback). */
+ORC_API int orc_hom_refine(const float *sx, const float *sy, const float *dx, const float *dy, const uint8_t *mask,
+                           int n, double H[9]) {
+    int32_t *idx = (int32_t *)malloc(sizeof(int32_t) * (n > 0 ? n : 1));
+    int m = 0;
+    for (int i = 0; i < n; ++i) if (mask[i]) idx[m++] = i;
+    if (m < 4) { free(idx); return 0; }
+    hnorm nm;
+    if (!hom_norm(sx, sy, dx, dy, idx, m, &nm)) { free(idx); return 0; }
+    double LtL[81] = {0};
+    for (int i = 0; i < m; ++i) {
+        int p = idx[i];
+        double x = (dx[p] - nm.cmx) * nm.smx, y = (dy[p] - nm.cmy) * nm.smy;
+        double X = (sx[p] - nm.cMx) * nm.sMx, Y = (sy[p] - nm.cMy) * nm.sMy;
+        double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
+        double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
+        for (int j = 0; j < 9; ++j)
+            for (int k = j; k < 9; ++k) LtL[j * 9 + k] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+    }
+    for (int j = 0; j < 9; ++j)
+        for (int k = 0; k < j; ++k) LtL[j * 9 + k] = LtL[k * 9 + j];
+    free(idx);
+    double hv[9];
+    jacobi_min_evec(9, LtL, hv);
+    hom_denorm(&nm, hv, H);
+    /* LM, 10 iterations, 8 parameters (h22 fixed at 1) */
+    double lam = 1e-3;
+    double cost = hom_cost(H, sx, sy, dx, dy, mask, n);
+    for (int it = 0; it < 10; ++it) {
+        double A[64] = {0}, g[8] = {0};
+        for (int i = 0; i < n; ++i) {
+            if (!mask[i]) continue;
+            double x = sx[i], y = sy[i];
+            double den = H[6] * x + H[7] * y + 1.;
+            double ww = 1. / den;
+            double Xi = (H[0] * x + H[1] * y + H[2]) * ww;
+            double Yi = (H[3] * x + H[4] * y + H[5]) * ww;
+            double ex = Xi - dx[i], ey = Yi - dy[i];
+            double Jx[8] = {x * ww, y * ww, ww, 0, 0, 0, -Xi * x * ww, -Xi * y * ww};
+            double Jy[8] = {0, 0, 0, x * ww, y * ww, ww, -Yi * x * ww, -Yi * y * ww};
+            for (int a = 0; a < 8; ++a) {
+                g[a] += Jx[a] * ex + Jy[a] * ey;
+                for (int b = 0; b <= a; ++b) A[a * 8 + b] += Jx[a] * Jx[b] + Jy[a] * Jy[b];
+            }
+        }
+        for (int a = 0; a < 8; ++a)
+            for (int b = a + 1; b < 8; ++b) A[a * 8 + b] = A[b * 8 + a];
+        double d[8], mg[8];
+        for (int a = 0; a < 8; ++a) mg[a] = -g[a];
+        if (!chol_solve(8, A, lam, mg, d)) { lam *= 10; continue; }
+        double Hn[9];
+        for (int a = 0; a < 8; ++a) Hn[a] = H[a] + d[a];
+        Hn[8] = 1.0;
+        double cn = hom_cost(Hn, sx, sy, dx, dy, mask, n);
+        if (cn < cost) { memcpy(H, Hn, sizeof(Hn)); cost = cn; lam *= 0.1; }
+        else lam *= 10;
+    }
+    return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Whole loops (what cv2.solvePnPRansac / cv2.findHomography run).           */
+/* sampler: 0 = Philox (seed, problem 0), 1 = OpenCV MWC (seed ignored).     */
+/* Returns best hypothesis index (<0: no model); mask = RANSAC-phase mask.   */
+/* ------------------------------------------------------------------------ */
+ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, const float *U, const float *V, int n,
+                               const double cam[4], double thr, double confidence, int max_iters, uint64_t seed,
+                               int sampler, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
+                               int64_t *iters_used) {
+    int64_t H = max_iters > 1 ? max_iters : 1;
+    int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * H);
+    int8_t *status = (int8_t *)malloc(H);
+    double *models = (double *)malloc(sizeof(double) * 16 * H);
+    int32_t *subs = NULL;
+    int8_t *sst = NULL;
+    if (sampler == 1) {
+        subs = (int32_t *)malloc(sizeof(int32_t) * 4 * H);
+        sst = (int8_t *)malloc(H);
+        uint64_t st = ~(uint64_t)0;
+        orc_mwc_subsets(&st, n, 4, H, NULL, NULL, NULL, NULL, subs, sst);
+    }
+    float thr2 = orc_thr2(thr);
+    orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, 0, H, subs, sst, counts, status, models);
+    int32_t good = 0;
+    int64_t best = orc_scan(counts, status, H, n, 4, confidence, max_iters, &good, iters_used);
+    if (best >= 0) {
+        memcpy(R, models + 16 * best, 9 * sizeof(double));
+        memcpy(t, models + 16 * best + 9, 3 * sizeof(double));
+        orc_pnp_count(R, t, cam, X, Y, Z, U, V, n, thr2, mask);
+    } else if (mask) {
+        memset(mask, 0, n);
+    }
+    if (n_inliers) *n_inliers = good;
+    free(counts); free(status); free(models); free(subs); free(sst);
+    return best;
+}
+
+ORC_API int64_t orc_hom_ransac(const float *sx, const float *sy, const float *dx, const float *dy, int n, double thr,
+                               double confidence, int max_iters, uint64_t seed, int sampler, double Hout[9],
+                               uint8_t *mask, int32_t *n_inliers, int64_t *iters_used) {
+    int64_t H = max_iters > 1 ? max_iters : 1;
+    int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * H);
+    int8_t *status = (int8_t *)malloc(H);
+    double *models = (double *)malloc(sizeof(double) * 16 * H);
+    int32_t *subs = NULL;
+    int8_t *sst = NULL;
+    if (sampler == 1) {
+        subs = (int32_t *)malloc(sizeof(int32_t) * 4 * H);
+        sst = (int8_t *)malloc(H);
+        uint64_t st = ~(uint64_t)0;
+        orc_mwc_subsets(&st, n, 4, H, sx, sy, dx, dy, subs, sst);
+    }
+    float thr2 = orc_thr2(thr);
+    orc_hom_hypotheses(sx, sy, dx, dy, n, thr2, seed, 0, 0, H, subs, sst, counts, status, models);
+    int32_t good = 0;
+    int64_t best = orc_scan(counts, status, H, n, 4, confidence, max_iters, &good, iters_used);
+    if (best >= 0) {
+        memcpy(Hout, models + 16 * best, 9 * sizeof(double));
+        orc_hom_count(Hout, sx, sy, dx, dy, n, thr2, mask);
+    } else if (mask) {
+        memset(mask, 0, n);
+    }
+    if (n_inliers) *n_inliers = good;
+    free(counts); free(status); free(models); free(subs); free(sst);
+    return best;
+}

@@ -1,0 +1,238 @@
+"""GPU parity: librsac.so (HIP, gfx950) against the CPU restatement (oracle/).
+
+Bar (DESIGN.md "Parity"): per-hypothesis status and inlier counts, the models
+themselves (bitwise, float64) and the RANSAC-phase masks are identical to the
+oracle for the same seed; refined R, t agree within 1e-4.  Small cases are
+checked exhaustively, the BASELINE.json size (10k points, 100k hypotheses)
+through a random sample of hypotheses plus size-independent properties.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+import rsac
+from rsac import synth
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "debuglog_homography.json")
+
+
+def _bits_equal(a, b):
+    return np.array_equal(np.asarray(a, np.float64).view(np.uint64), np.asarray(b, np.float64).view(np.uint64))
+
+
+def _pnp_case(n, outl, seed):
+    pr = synth.pnp_problem(n, outl, seed=seed)
+    return pr, O.soa_pnp(pr["points3d"], pr["points2d"]), O.cam_from_K(pr["K"])
+
+
+@pytest.mark.parametrize("n,outl,seed,H", [(4, 0.0, 1, 256), (5, 0.2, 2, 256), (12, 0.3, 3, 512),
+                                           (100, 0.5, 4, 1000), (1000, 0.5, 5, 700), (2999, 0.6, 6, 333)])
+def test_pnp_hypotheses_bit_exact_philox(n, outl, seed, H):
+    pr, soa, cam = _pnp_case(n, outl, seed)
+    st, cnt, mdl = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 17, H, 30.0, seed=seed)
+    oc, os_, om = O.pnp_hypotheses(soa, cam, 30.0, seed, H, hyp0=17, models=True)
+    np.testing.assert_array_equal(st, os_)
+    np.testing.assert_array_equal(cnt, oc)
+    assert _bits_equal(mdl[:, :12], om[:, :12])
+
+
+def test_pnp_hypotheses_bit_exact_opencv_subsets():
+    pr, soa, cam = _pnp_case(500, 0.5, 7)
+    subs, sst = O.mwc_subsets(500, 800)
+    st, cnt, mdl = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, 800, 30.0, subsets=subs)
+    oc, os_, om = O.pnp_hypotheses(soa, cam, 30.0, 0, 800, subsets=subs, sub_status=sst, models=True)
+    np.testing.assert_array_equal(st, os_)
+    np.testing.assert_array_equal(cnt, oc)
+    assert _bits_equal(mdl[:, :12], om[:, :12])
+
+
+@pytest.mark.parametrize("ki", [0, 7, 13, 16, 19, 26])
+def test_testpro_k_points_bit_exact(ki):
+    K = synth.testpro_k_candidates()[ki]
+    soa = O.soa_pnp(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS)
+    cam = O.cam_from_K(K)
+    st, cnt, mdl = rsac.hypotheses("pnp", synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, K, 0, 2048, 30.0)
+    oc, os_, om = O.pnp_hypotheses(soa, cam, 30.0, 0x5EED, 2048, models=True)
+    np.testing.assert_array_equal(st, os_)
+    np.testing.assert_array_equal(cnt, oc)
+    assert _bits_equal(mdl[:, :12], om[:, :12])
+
+
+def _debuglog():
+    d = json.load(open(GOLD))
+    out = []
+    for b in d["blocks"]:
+        if not b["complete"]:
+            continue
+        M = np.array(b["M"])
+        pp2 = np.array(b["pp2"])
+        hs = np.c_[pp2, np.ones(len(pp2))] @ M.T
+        out.append((hs[:, :2] / hs[:, 2:3], np.array(b["p1"], np.float64), np.array(b["mask"], bool)))
+    return out, d["threshold"]
+
+
+def test_homography_hypotheses_bit_exact_debuglog():
+    blocks, thr = _debuglog()
+    for src, dst, _ in blocks:
+        soa = O.soa_hom(src, dst)
+        subs, sst = O.mwc_subsets(12, 300, hom=soa)
+        st, cnt, mdl = rsac.hypotheses("homography", src, dst, None, 0, 300, thr, subsets=subs)
+        oc, os_, om = O.hom_hypotheses(soa, thr, 0, 300, subsets=subs, sub_status=sst, models=True)
+        np.testing.assert_array_equal(st, os_)
+        np.testing.assert_array_equal(cnt, oc)
+        assert _bits_equal(mdl[:, :9], om[:, :9])
+
+
+def test_homography_ransac_reproduces_reference_masks():
+    """The GPU path reproduces the masks OpenCV recorded in the reference's debug.log."""
+    blocks, thr = _debuglog()
+    for src, dst, mref in blocks:
+        H, m = rsac.homography_ransac(src, dst, thr, max_iters=2000, confidence=0.995, sampler="opencv")
+        assert H is not None
+        np.testing.assert_array_equal(m, mref)
+
+
+def test_homography_batched_location_search_equals_singles():
+    blocks, thr = _debuglog()
+    srcs = [b[0] for b in blocks]
+    dsts = [b[1] for b in blocks]
+    batched = rsac.homography_ransac_batched(srcs, dsts, thr)
+    for (src, dst, mref), (Hb, mb, nb) in zip(blocks, batched):
+        np.testing.assert_array_equal(mb, mref)
+        Hs, ms = rsac.homography_ransac(src, dst, thr)
+        np.testing.assert_allclose(Hb, Hs, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_homography_philox_bit_exact(seed):
+    pr = synth.homography_problem(3000, 0.4, seed=seed)
+    soa = O.soa_hom(pr["src"], pr["dst"])
+    st, cnt, mdl = rsac.hypotheses("homography", pr["src"], pr["dst"], None, 5, 900, 4.0, seed=seed)
+    oc, os_, om = O.hom_hypotheses(soa, 4.0, seed, 900, hyp0=5, models=True)
+    np.testing.assert_array_equal(st, os_)
+    np.testing.assert_array_equal(cnt, oc)
+    assert _bits_equal(mdl[:, :9], om[:, :9])
+
+
+@pytest.mark.parametrize("sampler", ["philox", "opencv"])
+def test_pnp_ransac_end_to_end_vs_oracle(sampler):
+    pr, soa, cam = _pnp_case(4000, 0.5, 21)
+    R, t, m, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0, sampler=sampler,
+                                    refine=False, return_info=True)
+    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000, 0x5EED, sampler=sampler)
+    assert info.best_hyp == ref["best"]
+    assert info.n_inliers == ref["n_inliers"]
+    assert info.iters == ref["iters"]
+    np.testing.assert_array_equal(m, ref["mask"])
+    assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+    # refined pose: LM on the same inliers from the same start
+    R2, t2, m2 = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0, sampler=sampler, refine=True)
+    Ro, to, _ = O.pnp_refine(soa, ref["mask"].astype(np.uint8), cam, ref["R"], ref["t"])
+    np.testing.assert_array_equal(m2, ref["mask"])
+    assert np.abs(R2 - Ro).max() < 1e-4
+    assert np.abs(t2 - to).max() < 1e-4 * max(1.0, np.abs(to).max())
+    assert np.abs(R2 - pr["R"]).max() < 2e-3
+
+
+def test_pnp_ransac_non_adaptive_equals_adaptive_prefix():
+    pr, soa, cam = _pnp_case(3000, 0.5, 22)
+    _, _, m1, i1 = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 3000, 30.0, adaptive=True,
+                                   refine=False, return_info=True)
+    _, _, m2, i2 = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 3000, 30.0, adaptive=False,
+                                   refine=False, return_info=True)
+    assert i1.best_hyp == i2.best_hyp and i1.iters == i2.iters
+    assert i2.hyps_scored == 3000
+    np.testing.assert_array_equal(m1, m2)
+
+
+def test_pnp_batched_ragged_equals_singles():
+    probs = [synth.pnp_problem(n, 0.4, seed=30 + i) for i, n in enumerate([4, 9, 64, 65, 700, 2049])]
+    out = rsac.pnp_ransac_batched([p["points2d"] for p in probs], [p["points3d"] for p in probs],
+                                  [p["K"] for p in probs], 2000, 30.0, refine=False)
+    for p, (R, t, m, ni) in zip(probs, out):
+        ref = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 0.99, 2000, 0x5EED)
+        if ref["best"] < 0:
+            assert R is None
+            continue
+        assert ni == ref["n_inliers"]
+        np.testing.assert_array_equal(m, ref["mask"])
+        assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+
+
+def test_k_sweep_batched():
+    """testpro-K.py:58-75 as one batched call over the 27 intrinsics."""
+    Ks = synth.testpro_k_candidates()
+    out = rsac.pnp_ransac_batched([synth.TESTPRO_K_PIXELS] * 27, [synth.TESTPRO_K_POS3D] * 27, Ks, 5000, 30.0,
+                                  refine=False)
+    for K, (R, t, m, ni) in zip(Ks, out):
+        ref = O.pnp_ransac(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, K, 30.0, 0.99, 5000, 0x5EED)
+        assert ni == ref["n_inliers"]
+        np.testing.assert_array_equal(m, ref["mask"])
+
+
+def test_device_inputs_match_host_inputs():
+    import torch
+    pr, soa, cam = _pnp_case(5000, 0.5, 40)
+    R, t, m = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=False)
+    p2 = torch.from_numpy(pr["points2d"]).cuda()
+    p3 = torch.from_numpy(pr["points3d"]).cuda()
+    Rd, td, md = rsac.pnp_ransac(p2, p3, pr["K"], 2000, 30.0, refine=False)
+    assert md.is_cuda
+    np.testing.assert_array_equal(md.cpu().numpy(), m)
+    assert _bits_equal(Rd, R) and _bits_equal(td, t)
+
+
+def test_score_poses_vs_oracle_counts():
+    pr, soa, cam = _pnp_case(7000, 0.5, 41)
+    rng = np.random.default_rng(0)
+    poses = []
+    for k in range(40):
+        R = pr["R"] if k % 2 == 0 else synth.random_rotation(rng)
+        t = pr["t"] + rng.normal(size=3) * (0.0 if k == 0 else 0.5)
+        poses.append(np.concatenate([R.reshape(9), t]))
+    poses = np.array(poses)
+    cnt = rsac.score_poses(pr["points2d"], pr["points3d"], pr["K"], poses, 30.0)
+    ref = [O.pnp_count(p[:9].reshape(3, 3), p[9:], soa, cam, 30.0) for p in poses]
+    np.testing.assert_array_equal(cnt, ref)
+
+
+def test_baseline_size_sampled_parity_and_properties():
+    """BASELINE.json config 2 size: 10k correspondences, 50% outliers, 100k hypotheses."""
+    pr, soa, cam = _pnp_case(10000, 0.5, 0)
+    H = 100_000
+    st, cnt, mdl = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, H, 30.0)
+    rng = np.random.default_rng(123)
+    sample = np.sort(rng.choice(H, 600, replace=False))
+    for h in sample[:600]:
+        oc, os_ = O.pnp_hypotheses(soa, cam, 30.0, 0x5EED, 1, hyp0=int(h))
+        assert st[h] == os_[0] and cnt[h] == oc[0], h
+    # the best model's mask has exactly its count of inliers
+    best = int(np.argmax(np.where(st > 0, cnt, -1)))
+    m, c = rsac.pose_mask(pr["points2d"], pr["points3d"], pr["K"], mdl[best, :12], 30.0)
+    assert c == cnt[best] == int(m.sum())
+    assert (m == pr["inlier"]).mean() > 0.99
+    # sharded evaluation over two halves gives the same global best (key all-reduce MAX)
+    k0, _ = rsac.evaluate_range(pr["points2d"], pr["points3d"], pr["K"], 0, H // 2, 30.0)
+    k1, _ = rsac.evaluate_range(pr["points2d"], pr["points3d"], pr["K"], H // 2, H // 2, 30.0)
+    kmax = max(k0, k1)
+    assert (kmax >> 32) == cnt[best]
+    assert 0xFFFFFFFF - (kmax & 0xFFFFFFFF) == best
+
+
+def test_degenerate_inputs():
+    # all points identical -> every minimal solve fails -> no model, mask all False
+    P3 = np.tile(np.array([[739000.0, 2888500.0, 700.0]]), (50, 1))
+    P2 = np.tile(np.array([[100.0, 200.0]]), (50, 1))
+    R, t, m = rsac.pnp_ransac(P2, P3, synth.main_v1_K(), 500, 30.0)
+    assert R is None and not m.any()
+    with pytest.raises(rsac.RsacError):
+        rsac.pnp_ransac(P2[:3], P3[:3], synth.main_v1_K(), 500, 30.0)
+    # collinear homography input: checkSubset rejects every subset
+    s = np.c_[np.arange(20.0), 2 * np.arange(20.0)]
+    H, m = rsac.homography_ransac(s, s * 3, 3.0)
+    assert H is None and not m.any()
