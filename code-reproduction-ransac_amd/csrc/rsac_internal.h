@@ -11,8 +11,10 @@ namespace rsac {
 // offsets[p+1]) of the SoA arrays; its hypothesis records live at
 // [p * hyp_stride, p * hyp_stride + H).
 // Hypothesis h of problem p (h counted from the start of the call) is record
-// p * hyp_stride + h; its Philox counter is rng_base + h, so a shard of one
-// problem's hypothesis space is selected by rng_base.
+// p * hyp_stride + h; its Philox counter is (rng_base + h, stream), so a
+// shard of one problem's hypothesis space is selected by rng_base.  Every
+// problem of a batch uses the same stream (0): a batched call equals the loop
+// of single calls it replaces, as each cv2 call restarts OpenCV's RNG.
 struct PnpArgs {
     const float *X, *Y, *Z, *U, *V;
     const int64_t *offsets;  // P + 1

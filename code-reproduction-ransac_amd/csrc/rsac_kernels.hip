@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
         for (int j = 0; j < 4; ++j) idx[j] = a.subsets[rec * 4 + j];
     } else {
         Philox rng;
-        rng.init(a.seed, (uint32_t)prob, (uint64_t)(a.rng_base + h));
+        rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
         st = (n >= 4 && rng.subset<4>(n, idx) == 0) ? 1 : -1;
     }
     double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void k_hom_solve(HomArgs a, int64_t hyp_begin,
         st = -1;
     } else {
         Philox rng;
-        rng.init(a.seed, (uint32_t)prob, (uint64_t)(a.rng_base + h));
+        rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
         st = -1;
         for (int att = 0; att < kMaxSubsetAttempts; ++att) {
             int32_t idx[4];

@@ -84,6 +84,27 @@ class RsacError(RuntimeError):
         self.code = code
 
 
+def _share_hip_runtime_with_torch():
+    """Make librsac bind to the HIP runtime torch uses, whatever the import order.
+
+    torch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7) and loads it
+    as ``libamdhip64.so`` from its lib/ directory; librsac needs
+    ``libamdhip64.so.7``.  Loading torch's copy first (RTLD_GLOBAL) makes both
+    resolve to ONE runtime, so torch tensors' device pointers and streams are
+    valid in librsac and torch can still initialise after us.
+    """
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+    except Exception:
+        spec = None
+    if spec is None or not spec.origin:
+        return
+    hip = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        C.CDLL(hip, mode=C.RTLD_GLOBAL)
+
+
 def lib():
     """Load librsac.so (raises if it has not been built)."""
     global _lib
@@ -95,6 +116,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
                               f"g.build()'` (make -C code-reproduction-ransac_amd/csrc)")
+        _share_hip_runtime_with_torch()
         L = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             f = getattr(L, name)

@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, smoke, a short bench.  Every GPU step has its
+# own time limit; a crash/timeout stops the script (no further GPU work).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 1 = test failures (no fault)
+timeout -k 10 420 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -25 gpurun_out/pytest_gpu.log
+ok_rc $rc || exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -5 gpurun_out/smoke.log
+ok_rc $rc || exit $rc
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
+exit $rc
