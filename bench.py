@@ -151,7 +151,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32+f64",
             "data": "synthetic (rsac.synth.pnp_problem seed 0: UTM-scale points, main_v1.py K, N(0,1px) noise)",
             "config": {"workload": "C2: 10k 2D-3D correspondences, 50% outliers, P3P, thr 30 px, "
                                    f"{H} hypotheses per GPU per step, global best via RCCL all-reduce(MAX)",

@@ -98,6 +98,7 @@ struct rsac_ctx {
     int64_t round_size = 4096;
     // device scratch
     DevBuf pts, offsets, cams, thr2, models, status, counts, subsets, substatus, best, bestmodels, mask;
+    DevBuf centred, bounds_ws, frame, fconst, fmodels;  // float32 pre-filter state (PnP)
     // pinned host staging
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask;
 };
@@ -214,6 +215,7 @@ int ensure_hyp_buffers(rsac_ctx *c, int P, int64_t stride, bool subsets) {
     if (recs * kModelStride * sizeof(double) > kMaxModelBytes)
         return fail(RSAC_ENOMEM, "%lld hypothesis records exceed the resident budget", (long long)recs);
     HIPCHK(c->models.ensure(recs * kModelStride * sizeof(double)));
+    HIPCHK(c->fmodels.ensure(recs * kFModelStride * sizeof(float)));
     HIPCHK(c->status.ensure(recs));
     HIPCHK(c->counts.ensure(recs * sizeof(int32_t)));
     HIPCHK(c->best.ensure(sizeof(int64_t) * P));
@@ -230,6 +232,43 @@ int ensure_hyp_buffers(rsac_ctx *c, int P, int64_t stride, bool subsets) {
 }
 
 hipStream_t pick_stream(rsac_ctx *c, void *stream) { return stream ? (hipStream_t)stream : c->stream; }
+
+// PnpArgs for a staged problem set, with the float32 pre-filter frame built
+// on the device (unless RSAC_F_EXACT_ONLY).  Call after stage_tables and
+// ensure_hyp_buffers.
+int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64_t stride, int64_t rng_base,
+             hipStream_t s, PnpArgs &a) {
+    a = PnpArgs{};
+    a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
+    a.offsets = c->offsets.as<int64_t>();
+    a.cams = c->cams.as<double>();
+    a.thr2 = c->thr2.as<float>();
+    a.models = c->models.as<double>();
+    a.status = c->status.as<int8_t>();
+    a.hyp_stride = stride;
+    a.rng_base = rng_base;
+    a.seed = seed;
+    if (flags & RSAC_F_EXACT_ONLY) {
+        a.exact_only = 1;
+        return RSAC_OK;
+    }
+    const int P = st.P;
+    const int64_t N = st.total;
+    HIPCHK(c->centred.ensure(sizeof(float) * 3 * std::max<int64_t>(N, 1)));
+    HIPCHK(c->bounds_ws.ensure(sizeof(int32_t) * 6 * P));
+    HIPCHK(c->frame.ensure(sizeof(double) * kFrameStride * P));
+    HIPCHK(c->fconst.ensure(sizeof(float) * kFconstStride * P));
+    float *C = c->centred.as<float>();
+    int32_t max_n = 0;
+    for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
+    HIPCHK(launch_pnp_frame(a, P, max_n, c->bounds_ws.as<int32_t>(), C, C + N, C + 2 * N, c->frame.as<double>(),
+                            c->fconst.as<float>(), s));
+    a.XC = C; a.YC = C + N; a.ZC = C + 2 * N;
+    a.frame = c->frame.as<double>();
+    a.fconst = c->fconst.as<float>();
+    a.fmodels = c->fmodels.as<float>();
+    return RSAC_OK;
+}
 
 enum class Model { PnP, Hom };
 
@@ -409,17 +448,15 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     if (r) return r;
     r = stage_tables(c, st, K, thr, s);
     if (r) return r;
-    PnpArgs a{};
-    a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
-    a.offsets = c->offsets.as<int64_t>();
-    a.cams = c->cams.as<double>();
-    a.thr2 = c->thr2.as<float>();
-    a.seed = seed;
-    a.rng_base = 0;
+    const int64_t stride = std::max(n_iters, 1);
+    r = ensure_hyp_buffers(c, P, stride, (flags & RSAC_F_SAMPLER_OPENCV) != 0);
+    if (r) return r;
+    PnpArgs a;
+    r = pnp_args(c, st, flags, seed, stride, 0, s, a);
+    if (r) return r;
     LoopOut lo;
     r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo);
     if (r) return r;
-    const int64_t stride = std::max(n_iters, 1);
     r = finish_masks(c, Model::PnP, st, &a, lo, stride, mask_out, flags, s);
     if (r) return r;
     const double *bm = c->h_bestmodels.as<double>();
@@ -567,8 +604,10 @@ void rsac_destroy(rsac_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf *dev[] = {&c->pts, &c->offsets, &c->cams, &c->thr2, &c->models, &c->status, &c->counts,
-                     &c->subsets, &c->substatus, &c->best, &c->bestmodels, &c->mask};
+    DevBuf *dev[] = {&c->pts,       &c->offsets,    &c->cams,  &c->thr2,      &c->models,
+                     &c->status,    &c->counts,     &c->subsets, &c->substatus, &c->best,
+                     &c->bestmodels, &c->mask,      &c->centred, &c->bounds_ws, &c->frame,
+                     &c->fconst,    &c->fmodels};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};
@@ -642,15 +681,12 @@ int rsac_score_poses(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t 
         rec[(size_t)h * kModelStride + kValidSlot] = 1.0;
     }
     HIPCHK(hipMemcpyAsync(c->models.p, rec.data(), rec.size() * sizeof(double), hipMemcpyHostToDevice, s));
-    PnpArgs a{};
-    a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
-    a.offsets = c->offsets.as<int64_t>();
-    a.cams = c->cams.as<double>();
-    a.thr2 = c->thr2.as<float>();
-    a.models = c->models.as<double>();
-    a.status = c->status.as<int8_t>();
-    a.hyp_stride = n_poses;
+    PnpArgs a;
+    r = pnp_args(c, st, flags, 0, n_poses, 0, s, a);
+    if (r) return r;
+    if (a.fmodels) HIPCHK(launch_pnp_fmodels(a, 1, n_poses, s));
     HIPCHK(launch_pnp_score(a, 1, 0, n_poses, c->counts.as<int32_t>(), s));
+    HIPCHK(hipStreamSynchronize(s));  // rec (host vector) must outlive the async copy
     HIPCHK(hipMemcpyAsync(counts_out, c->counts.p, sizeof(int32_t) * n_poses, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return RSAC_OK;
@@ -671,54 +707,44 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
     if (r) return r;
     r = ensure_hyp_buffers(c, 1, n_hyps, false);
     if (r) return r;
-    PnpArgs a{};
-    a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
-    a.offsets = c->offsets.as<int64_t>();
-    a.cams = c->cams.as<double>();
-    a.thr2 = c->thr2.as<float>();
-    a.models = c->models.as<double>();
-    a.status = c->status.as<int8_t>();
-    a.hyp_stride = n_hyps;
-    a.rng_base = hyp_begin;
-    a.seed = seed;
+    PnpArgs a;
+    r = pnp_args(c, st, flags, seed, n_hyps, hyp_begin, s, a);
+    if (r) return r;
     const int32_t H = (int32_t)n_hyps;
     HIPCHK(hipEventRecord(c->ev0, s));
     HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
     HIPCHK(hipEventRecord(c->ev1, s));
     HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
     HIPCHK(hipEventRecord(c->ev2, s));
-    HIPCHK(c->h_counts.ensure(sizeof(int32_t) * H));
-    HIPCHK(c->h_status.ensure(H));
-    HIPCHK(hipMemcpyAsync(c->h_counts.p, c->counts.p, sizeof(int32_t) * H, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(c->h_status.p, c->status.p, H, hipMemcpyDeviceToHost, s));
+    // device-side argmax: only the 8-byte key and the winner's record cross PCIe
+    unsigned long long *dkey = (unsigned long long *)c->best.p;
+    HIPCHK(launch_best_key(c->counts.as<int32_t>(), c->status.as<int8_t>(), H, hyp_begin, dkey,
+                           c->models.as<double>(), c->bestmodels.as<double>(), s));
+    HIPCHK(c->h_bestmodels.ensure(sizeof(double) * (kModelStride + 2)));
+    double *hb = c->h_bestmodels.as<double>();
+    HIPCHK(hipMemcpyAsync(hb, c->bestmodels.p, sizeof(double) * kModelStride, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hb + kModelStride, dkey, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    unsigned long long key;
+    memcpy(&key, hb + kModelStride, sizeof key);
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         add_times(c, stats->gpu_ms, stats->solve_ms, stats->score_ms);
         stats->hyps_scored = H;
         stats->rounds = 1;
     }
-    const int32_t *cnt = c->h_counts.as<int32_t>();
-    const int8_t *sts = c->h_status.as<int8_t>();
-    int64_t best = -1;
-    int32_t bc = -1;
-    for (int32_t h = 0; h < H; ++h)
-        if (sts[h] > 0 && cnt[h] > bc) { bc = cnt[h]; best = h; }
-    if (best < 0) {
+    if (key == 0) {
         *key_out = -1;
+        if (stats) stats->best_hyp = -1;
         return RSAC_NO_MODEL;
     }
+    *key_out = (int64_t)key;
     if (stats) {
-        stats->best_hyp = hyp_begin + best;
-        stats->n_inliers = bc;
+        const uint64_t low = 0xFFFFFFFFull - (key & 0xFFFFFFFFull);
+        stats->best_hyp = (int64_t)(((uint64_t)hyp_begin & ~0xFFFFFFFFull) | low);
+        stats->n_inliers = (int32_t)(key >> 32);
     }
-    const uint64_t gidx = (uint64_t)(hyp_begin + best);
-    *key_out = (int64_t)(((uint64_t)(uint32_t)bc << 32) | (0xFFFFFFFFull - (gidx & 0xFFFFFFFFull)));
-    if (model_out) {
-        double m[kModelStride];
-        HIPCHK(hipMemcpy(m, c->models.as<double>() + best * kModelStride, sizeof m, hipMemcpyDeviceToHost));
-        memcpy(model_out, m, 12 * sizeof(double));
-    }
+    if (model_out) memcpy(model_out, hb, 12 * sizeof(double));
     return RSAC_OK;
 }
 
@@ -751,18 +777,11 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
         HIPCHK(hipMemcpyAsync(c->substatus.p, hss, H, hipMemcpyHostToDevice, s));
     }
     if (model == Model::PnP) {
-        PnpArgs a{};
-        a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
-        a.offsets = c->offsets.as<int64_t>();
-        a.cams = c->cams.as<double>();
-        a.thr2 = c->thr2.as<float>();
-        a.models = c->models.as<double>();
-        a.status = c->status.as<int8_t>();
+        PnpArgs a;
+        r = pnp_args(c, st, flags, seed, H, hyp_begin, s, a);
+        if (r) return r;
         a.subsets = subsets ? c->subsets.as<int32_t>() : nullptr;
         a.sub_status = subsets ? c->substatus.as<int8_t>() : nullptr;
-        a.hyp_stride = H;
-        a.rng_base = hyp_begin;
-        a.seed = seed;
         HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
         HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
     } else {

@@ -27,7 +27,19 @@ struct PnpArgs {
     int64_t hyp_stride;
     int64_t rng_base;
     uint64_t seed;
+    // float32 pre-filter (DESIGN.md "Scoring"): centred coordinates, per-problem
+    // frame / constants, per-hypothesis float32 records.  fmodels == nullptr
+    // (or exact_only) selects the all-f64 scoring kernel.
+    const float *XC, *YC, *ZC;
+    const double *frame;  // P x kFrameStride: c0 c1 c2 B rho cmax
+    const float *fconst;  // P x kFconstStride
+    float *fmodels;       // P x hyp_stride x kFModelStride
+    int exact_only;
 };
+
+constexpr int kFrameStride = 8;
+constexpr int kFconstStride = 16;
+constexpr int kFModelStride = 16;
 
 struct HomArgs {
     const float *SX, *SY, *DX, *DY;
@@ -42,9 +54,20 @@ struct HomArgs {
     uint64_t seed;
 };
 
+// best packed key of counts[0, H) (+ its model record -> model_out[16]);
+// key = 0 when no hypothesis has a model with >= 1 inlier
+hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t H, int64_t hyp_begin,
+                           unsigned long long *key, const double *models, double *model_out, hipStream_t s);
+
 // copy model records rec[p] (<0: zero) into out[p][16]
 hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s);
 
+// frame of every problem (centre, bounds, f32 constants) + centred coords:
+// bounds_ws is a P x 6 int workspace.
+hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *bounds_ws, float *XC, float *YC,
+                            float *ZC, double *frame, float *fconst, hipStream_t s);
+// f32 records for H given f64 models (rsac_score_poses / rsac_pnp_mask)
+hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_t s);
 hipError_t launch_pnp_prepare(const double *p3, const double *p2, int64_t n, float *X, float *Y, float *Z, float *U,
                               float *V, hipStream_t s);
 hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, float *SX, float *SY, float *DX,

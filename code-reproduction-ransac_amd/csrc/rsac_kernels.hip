@@ -48,6 +48,135 @@ __global__ void k_hom_prepare(const double *__restrict__ s, const double *__rest
 }
 
 // ---------------------------------------------------------------------------
+// PnP frame for the float32 pre-filter (DESIGN.md "Scoring").
+// Each problem is re-centred on the midpoint c of its bounding box; points
+// are kept as f32 offsets XC = fl32(Xf - c).  B bounds |XC|, rho the rounding
+// of XC.  fconst holds the per-problem f32 constants of the error bound.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int f2ord(float f) {
+    int i = __float_as_int(f);
+    return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
+
+constexpr double kU32 = 5.9604644775390625e-08;  // 2^-24, unit roundoff of float32
+
+// ws: [0, 3P) mins, [3P, 6P) maxes (ordered-int encoding), pre-set by memset
+__global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *__restrict__ ws) {
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float v[3] = {a.X[p0 + i], a.Y[p0 + i], a.Z[p0 + i]};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { lo[k] = fminf(lo[k], v[k]); hi[k] = fmaxf(hi[k], v[k]); }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
+        }
+    }
+    if ((threadIdx.x & 63) == 0 && n > 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            atomicMin(ws + 3 * prob + k, f2ord(lo[k]));
+            atomicMax(ws + 3 * P + 3 * prob + k, f2ord(hi[k]));
+        }
+    }
+}
+
+__global__ void k_pnp_frame(PnpArgs a, int32_t P, const int *__restrict__ ws, double *__restrict__ frame,
+                            float *__restrict__ fconst) {
+    const int prob = blockIdx.x * blockDim.x + threadIdx.x;
+    if (prob >= P) return;
+    const int n = (int)(a.offsets[prob + 1] - a.offsets[prob]);
+    double c[3] = {0, 0, 0}, B = 0;
+    if (n > 0) {
+        for (int k = 0; k < 3; ++k) {
+            const double lo = ord2f(ws[3 * prob + k]), hi = ord2f(ws[3 * P + 3 * prob + k]);
+            c[k] = (lo + hi) * 0.5;
+            B = fmax(B, (hi - lo) * 0.5);
+        }
+    }
+    B = B * (1.0 + 4.0 * kU32) + 1e-30;
+    double *f = frame + (int64_t)prob * kFrameStride;
+    f[0] = c[0]; f[1] = c[1]; f[2] = c[2];
+    f[3] = B;
+    f[4] = 2.0 * kU32 * B;                                           // rho: rounding of XC
+    f[5] = fmax(fmax(fabs(c[0]), fabs(c[1])), fabs(c[2])) + B;      // max |Xf|
+    f[6] = f[7] = 0;
+    const double *cm = a.cams + 4 * prob;
+    const double T = a.thr2[prob];
+    float *q = fconst + (int64_t)prob * kFconstStride;
+    q[0] = (float)cm[0]; q[1] = (float)cm[1]; q[2] = (float)cm[2]; q[3] = (float)cm[3];
+    q[4] = (float)(10.1 * kU32 * (fabs(cm[2]) + fabs(cm[3])) + 1e-6);  // C0
+    q[5] = (float)(10.1 * kU32 * fabs(cm[0]));                        // C1x
+    q[6] = (float)(10.1 * kU32 * fabs(cm[1]));                        // C1y
+    q[7] = (float)T;
+    q[8] = (float)(2.002 * sqrt(T));                                  // 2 sqrt(T) with slack
+    q[9] = (float)(1e-6 * T + 1e-30);                                 // relative rounding of e
+    for (int k = 10; k < kFconstStride; ++k) q[k] = 0.f;
+}
+
+__global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, const double *__restrict__ frame,
+                                                    float *__restrict__ XC, float *__restrict__ YC,
+                                                    float *__restrict__ ZC) {
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const double *f = frame + (int64_t)prob * kFrameStride;
+    const double c0 = f[0], c1 = f[1], c2 = f[2];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int64_t q = p0 + i;
+        XC[q] = (float)((double)a.X[q] - c0);
+        YC[q] = (float)((double)a.Y[q] - c1);
+        ZC[q] = (float)((double)a.Z[q] - c2);
+    }
+}
+
+// float32 record of one pose: R (9), t' = R c + t (3), error-bound constants
+// A0, A1x, A1y and the depth guard zg (zg < 0: no model).
+__device__ __forceinline__ void write_fmodel(const double *R, const double *t, bool valid, const double *frame,
+                                             const double *cam, float *fm) {
+    if (!valid) {
+#pragma unroll
+        for (int q = 0; q < kFModelStride; ++q) fm[q] = 0.f;
+        fm[15] = -1.f;
+        return;
+    }
+    const double B = frame[3], rho = frame[4], cmax = frame[5];
+    double eps[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const double tp = R[3 * r] * frame[0] + R[3 * r + 1] * frame[1] + R[3 * r + 2] * frame[2] + t[r];
+        const double r1 = fabs(R[3 * r]) + fabs(R[3 * r + 1]) + fabs(R[3 * r + 2]);
+        eps[r] = 6.0 * kU32 * (r1 * B + fabs(tp)) + r1 * rho + 4e-15 * (r1 * cmax + fabs(t[r]));
+        fm[9 + r] = (float)tp;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) fm[q] = (float)R[q];
+    const double fx = fabs(cam[0]), fy = fabs(cam[1]);
+    fm[12] = (float)(2.01 * (fx * eps[0] + fy * eps[1]));
+    fm[13] = (float)(2.01 * fx * eps[2]);
+    fm[14] = (float)(2.01 * fy * eps[2]);
+    fm[15] = (float)(2.02 * eps[2] + 1e-30);
+}
+
+__global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
+    const int prob = blockIdx.y;
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= H) return;
+    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
+    const double *m = a.models + rec * kModelStride;
+    write_fmodel(m, m + 9, m[kValidSlot] != 0.0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+                 a.fmodels + rec * kFModelStride);
+}
+
+// ---------------------------------------------------------------------------
 // PnP: sample + minimal solve, one lane per hypothesis
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin, int32_t H) {
@@ -88,6 +217,107 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
     m[kValidSlot] = st > 0 ? 1.0 : 0.0;
     a.status[rec] = st;
+    if (a.fmodels)
+        write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+                     a.fmodels + rec * kFModelStride);
+}
+
+// ---------------------------------------------------------------------------
+// PnP scoring, float32 pre-filter + exact fallback.  Same tiling as the
+// exact kernel below; per pair the f32 projection of the centred point gives
+// e' and a rigorous bound M on |e' - e| (e = the exact f64-projection error
+// of the oracle).  |e' - T| > M decides the pair; otherwise (and for
+// NaN/near-zero depth) the lane recomputes the exact f64 error.  Counts are
+// therefore bit-identical to the exact kernel.
+// ---------------------------------------------------------------------------
+template <int P, int HB>
+__global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_begin, int32_t H,
+                                                       int32_t *__restrict__ counts) {
+    static_assert(HB <= 64, "one lane per hypothesis of the block");
+    __shared__ int red[4][HB];
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t h0 = hyp_begin + (int64_t)blockIdx.x * HB;
+    const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
+    const float fx = fc[0], fy = fc[1], cx = fc[2], cy = fc[3];
+    const float C0 = fc[4], C1x = fc[5], C1y = fc[6], T = fc[7], sqT2 = fc[8], Trel = fc[9];
+    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+    const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
+    const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
+    const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
+
+    int cnt = 0;
+    for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
+        float px[P], py[P], pz[P], pu[P], pv[P];
+        bool in[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int i = base + j * 64 + lane;
+            in[j] = i < n;
+            const int ii = in[j] ? i : 0;
+            px[j] = XC[ii]; py[j] = YC[ii]; pz[j] = ZC[ii];
+            pu[j] = U[ii]; pv[j] = V[ii];
+        }
+        for (int h = 0; h < nh; ++h) {
+            const float *__restrict__ m = fmb + h * kFModelStride;
+            const float zg = m[15];
+            if (zg < 0.f) continue;
+            const float r0 = m[0], r1 = m[1], r2 = m[2], r3 = m[3], r4 = m[4], r5 = m[5], r6 = m[6], r7 = m[7],
+                        r8 = m[8], t0 = m[9], t1 = m[10], t2 = m[11], A0 = m[12], A1x = m[13], A1y = m[14];
+            uint64_t m_in = 0;
+            int und = 0;  // bit j: this lane's point j is not decided by the f32 bound
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const float x = __builtin_fmaf(r0, px[j], __builtin_fmaf(r1, py[j], __builtin_fmaf(r2, pz[j], t0)));
+                const float y = __builtin_fmaf(r3, px[j], __builtin_fmaf(r4, py[j], __builtin_fmaf(r5, pz[j], t1)));
+                const float z = __builtin_fmaf(r6, px[j], __builtin_fmaf(r7, py[j], __builtin_fmaf(r8, pz[j], t2)));
+                const float iz = __builtin_amdgcn_rcpf(z);
+                const float ax = x * iz, ay = y * iz;
+                const float dx = pu[j] - __builtin_fmaf(fx, ax, cx);
+                const float dy = pv[j] - __builtin_fmaf(fy, ay, cy);
+                const float e = __builtin_fmaf(dx, dx, dy * dy);
+                const float aax = __builtin_fabsf(ax), aay = __builtin_fabsf(ay);
+                const float D = __builtin_fmaf(__builtin_fmaf(A1x, aax, __builtin_fmaf(A1y, aay, A0)),
+                                               __builtin_fabsf(iz),
+                                               __builtin_fmaf(C1x, aax, __builtin_fmaf(C1y, aay, C0)));
+                const float M = __builtin_fmaf(__builtin_fmaf(D, 1.001f, sqT2), D, Trel);
+                // written so that NaN anywhere leaves the pair undecided
+                const bool decided = (__builtin_fabsf(e - T) > M) && (__builtin_fabsf(z) > zg);
+                m_in |= __ballot(in[j] && decided && e < T);
+                und |= (in[j] && !decided) ? (1 << j) : 0;
+            }
+            int cc = __popcll(m_in);
+            if (__ballot(und != 0)) {
+                // exact f64 error (pnp_err, the oracle's formula) for the undecided pairs
+                const double *md = a.models + (rec0 + h) * kModelStride;
+                const double *cm = a.cams + 4 * prob;
+                const Cam k{cm[0], cm[1], cm[2], cm[3]};
+                const float thr2 = a.thr2[prob];
+                uint64_t m_ex = 0;
+                for (int j = 0; j < P; ++j) {
+                    bool ex = false;
+                    if ((und >> j) & 1) {
+                        const int64_t q = p0 + base + j * 64 + lane;
+                        ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], pu[j], pv[j]) <=
+                             thr2;
+                    }
+                    m_ex |= __ballot(ex);
+                }
+                cc += __popcll(m_ex);
+            }
+            cnt += (lane == h) ? cc : 0;
+        }
+    }
+    if (lane < HB) red[wave][lane] = cnt;
+    __syncthreads();
+    if (threadIdx.x < nh) {
+        const int s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        counts[(int64_t)prob * a.hyp_stride + h0 + threadIdx.x] = s;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -293,6 +523,39 @@ __global__ void k_gather_models(const double *__restrict__ models, const int64_t
     out[i] = r >= 0 ? models[r * kModelStride + q] : 0.0;
 }
 
+// packed key of the best hypothesis of a range (count desc, index asc):
+// (count << 32) | (0xFFFFFFFF - (hyp_begin + h)); *key must be 0 on entry.
+__global__ __launch_bounds__(256) void k_best_key(const int32_t *__restrict__ counts,
+                                                  const int8_t *__restrict__ status, int32_t H, int64_t hyp_begin,
+                                                  unsigned long long *__restrict__ key) {
+    unsigned long long best = 0;
+    for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x) {
+        if (status[h] > 0 && counts[h] > 0) {
+            const uint64_t g = (uint64_t)(hyp_begin + h);
+            const unsigned long long k =
+                ((unsigned long long)(uint32_t)counts[h] << 32) | (0xFFFFFFFFull - (g & 0xFFFFFFFFull));
+            best = k > best ? k : best;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long other = __shfl_xor(best, o);
+        best = other > best ? other : best;
+    }
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(key, best);
+}
+
+// model record of the key's hypothesis -> out[16] (zeros when key == 0)
+__global__ void k_key_model(const double *__restrict__ models, const unsigned long long *__restrict__ key,
+                            int64_t hyp_begin, double *__restrict__ out) {
+    const int q = threadIdx.x;
+    if (q >= kModelStride) return;
+    const unsigned long long k = *key;
+    if (k == 0) { out[q] = 0.0; return; }
+    const uint64_t low = 0xFFFFFFFFull - (k & 0xFFFFFFFFull);
+    const int64_t h = (int64_t)((low - ((uint64_t)hyp_begin & 0xFFFFFFFFull)) & 0xFFFFFFFFull);
+    out[q] = models[h * kModelStride + q];
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
@@ -319,6 +582,27 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
     return hipGetLastError();
 }
 
+hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
+                            double *frame, float *fconst, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(ws, 0x7F, sizeof(int32_t) * 3 * P, s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(ws + 3 * P, 0x80, sizeof(int32_t) * 3 * P, s);
+    if (e != hipSuccess) return e;
+    unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
+    if (g > 64) g = 64;
+    hipLaunchKernelGGL(k_pnp_bounds, dim3(g, P), dim3(256), 0, s, a, P, ws);
+    hipLaunchKernelGGL(k_pnp_frame, dim3(cdiv(P, 64)), dim3(64), 0, s, a, P, ws, frame, fconst);
+    unsigned g2 = cdiv(max_n > 0 ? max_n : 1, 256);
+    if (g2 > 1024) g2 = 1024;
+    hipLaunchKernelGGL(k_pnp_center, dim3(g2, P), dim3(256), 0, s, a, frame, XC, YC, ZC);
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_t s) {
+    hipLaunchKernelGGL(k_pnp_fmodels, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, H);
+    return hipGetLastError();
+}
+
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     hipLaunchKernelGGL(k_pnp_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H);
     return hipGetLastError();
@@ -326,8 +610,12 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    hipLaunchKernelGGL((k_pnp_score<kScoreP, kScoreHB>), dim3(cdiv(H, kScoreHB), P), dim3(256), 0, s, a, hyp_begin, H,
-                       counts);
+    if (a.fmodels && !a.exact_only)
+        hipLaunchKernelGGL((k_pnp_score_f32<kScoreP, kScoreHB>), dim3(cdiv(H, kScoreHB), P), dim3(256), 0, s, a,
+                           hyp_begin, H, counts);
+    else
+        hipLaunchKernelGGL((k_pnp_score<kScoreP, kScoreHB>), dim3(cdiv(H, kScoreHB), P), dim3(256), 0, s, a,
+                           hyp_begin, H, counts);
     return hipGetLastError();
 }
 
@@ -362,6 +650,17 @@ hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int
 hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s) {
     hipLaunchKernelGGL(k_gather_models, dim3(cdiv((int64_t)P * kModelStride, 256)), dim3(256), 0, s, models, rec, P,
                        out);
+    return hipGetLastError();
+}
+
+hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t H, int64_t hyp_begin,
+                           unsigned long long *key, const double *models, double *model_out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(key, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    unsigned g = cdiv(H, 256);
+    if (g > 512) g = 512;
+    hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts, status, H, hyp_begin, key);
+    hipLaunchKernelGGL(k_key_model, dim3(1), dim3(64), 0, s, models, key, hyp_begin, model_out);
     return hipGetLastError();
 }
 

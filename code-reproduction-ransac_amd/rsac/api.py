@@ -120,7 +120,7 @@ def _K9(K) -> np.ndarray:
 
 def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
                confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox", adaptive: bool = True,
-               refine: bool = True, device=None, return_info: bool = False):
+               refine: bool = True, device=None, return_info: bool = False, exact_only: bool = False):
     """RANSAC PnP on the GPU: (points2D, points3D, K, n_iters, reproj_thresh) -> (R, t, inlier_mask).
 
     Defaults follow the reference call (iterationsCount=5000, reprojectionError=30,
@@ -136,7 +136,7 @@ def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float 
         raise ValueError("points3D and points2D must both be host arrays or both GPU tensors")
     n = p3.n
     ctx = L.context(_device_of(p3, device))
-    flags = _flags(adaptive, refine, sampler)
+    flags = _flags(adaptive, refine, sampler, exact_only)
     if p3.device:
         flags |= L.F_DEVICE_IN
     K9 = _K9(K)
@@ -260,7 +260,7 @@ def homography_ransac_batched(src_list, dst_list, reproj_thresh: float = 3.0, *,
     return out
 
 
-def score_poses(points2D, points3D, K, poses, reproj_thresh: float = 30.0, device=None):
+def score_poses(points2D, points3D, K, poses, reproj_thresh: float = 30.0, device=None, exact_only: bool = False):
     """Inlier counts of given poses ((H, 3, 4) [R | t] or (H, 12)) -- the minimal scoring slice."""
     p3 = _In(points3D, 3)
     p2 = _In(points2D, 2)
@@ -269,7 +269,7 @@ def score_poses(points2D, points3D, K, poses, reproj_thresh: float = 30.0, devic
         poses = np.concatenate([poses[:, :, :3].reshape(-1, 9), poses[:, :, 3]], axis=1)
     poses = np.ascontiguousarray(poses.reshape(-1, 12))
     ctx = L.context(_device_of(p3, device))
-    flags = L.F_DEVICE_IN if p3.device else 0
+    flags = (L.F_DEVICE_IN if p3.device else 0) | (L.F_EXACT_ONLY if exact_only else 0)
     counts = np.zeros(poses.shape[0], np.int32)
     K9 = _K9(K)
     with ctx.lock:
@@ -280,7 +280,7 @@ def score_poses(points2D, points3D, K, poses, reproj_thresh: float = 30.0, devic
 
 
 def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_thresh: float = 30.0, *,
-                   seed: int = 0x5EED, device=None, return_info: bool = False):
+                   seed: int = 0x5EED, device=None, return_info: bool = False, exact_only: bool = False):
     """Evaluate Philox hypotheses [hyp_begin, hyp_begin + n_hyps) of one problem.
 
     Returns (key, model12) where key = (count << 32) | (0xFFFFFFFF - best_index) (or -1).
@@ -289,7 +289,7 @@ def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_th
     p3 = _In(points3D, 3)
     p2 = _In(points2D, 2)
     ctx = L.context(_device_of(p3, device))
-    flags = L.F_DEVICE_IN if p3.device else 0
+    flags = (L.F_DEVICE_IN if p3.device else 0) | (L.F_EXACT_ONLY if exact_only else 0)
     key = C.c_int64(-1)
     model = np.zeros(12)
     K9 = _K9(K)
@@ -306,7 +306,7 @@ def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_th
 
 
 def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024, reproj_thresh: float = 30.0, *,
-               seed: int = 0x5EED, subsets=None, device=None):
+               seed: int = 0x5EED, subsets=None, device=None, exact_only: bool = False):
     """Raw per-hypothesis (status, counts, models) of the GPU hot path for one problem.
 
     model "pnp": a = points3D (N,3), b = points2D (N,2), K required.
@@ -317,7 +317,7 @@ def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024,
     A = _In(a, 3 if pnp else 2)
     B = _In(b, 2)
     ctx = L.context(_device_of(A, device))
-    flags = L.F_DEVICE_IN if A.device else 0
+    flags = (L.F_DEVICE_IN if A.device else 0) | (L.F_EXACT_ONLY if exact_only else 0)
     counts = np.zeros(n_hyps, np.int32)
     status = np.zeros(n_hyps, np.int8)
     models = np.zeros((n_hyps, 16))

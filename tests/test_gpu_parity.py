@@ -236,3 +236,75 @@ def test_degenerate_inputs():
     s = np.c_[np.arange(20.0), 2 * np.arange(20.0)]
     H, m = rsac.homography_ransac(s, s * 3, 3.0)
     assert H is None and not m.any()
+
+
+# ---------------------------------------------------------------------------------------------
+# float32 pre-filter: must never change a decision (DESIGN.md "Scoring")
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,seed", [(10000, 0), (4097, 3), (777, 9)])
+def test_f32_prefilter_equals_exact_kernel(n, seed):
+    pr, soa, cam = _pnp_case(n, 0.5, seed)
+    st_f, c_f, _ = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, 20000, 30.0)
+    st_e, c_e, _ = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, 20000, 30.0, exact_only=True)
+    np.testing.assert_array_equal(st_f, st_e)
+    np.testing.assert_array_equal(c_f, c_e)
+
+
+def _boundary_case(seed, n=6000, thr=30.0):
+    """Pixels placed at distance ~thr from the exact projection of the true pose, so that e ~ T to
+    within float32 rounding: every pair lands in (or next to) the pre-filter's undecided band."""
+    pr = synth.pnp_problem(n, 0.0, seed=seed, noise_px=0.0)
+    soa = O.soa_pnp(pr["points3d"], pr["points2d"])
+    cam = O.cam_from_K(pr["K"])
+    R, t = pr["R"], pr["t"]
+    X = np.stack(soa[:3], axis=1).astype(np.float64)
+    pc = X @ R.T + t
+    iz = 1.0 / pc[:, 2]
+    pu = (pc[:, 0] * iz) * cam[0] + cam[2]
+    pv = (pc[:, 1] * iz) * cam[1] + cam[3]
+    rng = np.random.default_rng(seed)
+    ang = rng.uniform(0, 2 * np.pi, n)
+    rad = thr * (1.0 + rng.choice([-1, 1], n) * rng.choice([0.0, 1e-8, 3e-8, 1e-7, 1e-6, 1e-5, 1e-3], n))
+    px = np.stack([pu + rad * np.cos(ang), pv + rad * np.sin(ang)], axis=1)
+    return pr["points3d"], px, pr["K"], np.concatenate([R.reshape(9), t])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_f32_prefilter_threshold_boundary(seed):
+    P3, P2, K, pose = _boundary_case(seed)
+    soa = O.soa_pnp(P3, P2)
+    cam = O.cam_from_K(K)
+    rng = np.random.default_rng(seed)
+    poses = [pose]
+    for _ in range(15):  # small perturbations of the pose keep most pairs near the boundary
+        p = pose.copy()
+        p[9:] += rng.normal(size=3) * 1e-3
+        poses.append(p)
+    poses = np.array(poses)
+    fast = rsac.score_poses(P2, P3, K, poses, 30.0)
+    exact = rsac.score_poses(P2, P3, K, poses, 30.0, exact_only=True)
+    ref = [O.pnp_count(p[:9].reshape(3, 3), p[9:], soa, cam, 30.0) for p in poses]
+    np.testing.assert_array_equal(exact, ref)
+    np.testing.assert_array_equal(fast, ref)
+    assert 0 < ref[0] < len(P3)  # the construction really straddles the threshold
+
+
+def test_f32_prefilter_points_behind_and_on_camera_plane():
+    pr = synth.pnp_problem(3000, 0.3, seed=44)
+    R, t = pr["R"], pr["t"]
+    C = -R.T @ t
+    rng = np.random.default_rng(1)
+    # points on the camera plane (z_cam = 0), behind the camera, and right at the centre
+    extra_c = np.concatenate([np.c_[rng.normal(size=(200, 2)) * 50, np.zeros(200)],
+                              np.c_[rng.normal(size=(200, 2)) * 50, -rng.uniform(1, 500, 200)],
+                              np.zeros((3, 3))])
+    extra_w = (extra_c - t) @ R
+    P3 = np.concatenate([pr["points3d"], extra_w, C[None, :]])
+    P2 = np.concatenate([pr["points2d"], rng.uniform(0, 2000, size=(len(extra_w) + 1, 2))])
+    soa = O.soa_pnp(P3, P2)
+    cam = O.cam_from_K(pr["K"])
+    poses = np.array([np.concatenate([R.reshape(9), t])] +
+                     [np.concatenate([synth.random_rotation(rng).reshape(9), t + rng.normal(size=3)]) for _ in range(7)])
+    fast = rsac.score_poses(P2, P3, pr["K"], poses, 30.0)
+    ref = [O.pnp_count(p[:9].reshape(3, 3), p[9:], soa, cam, 30.0) for p in poses]
+    np.testing.assert_array_equal(fast, ref)
