@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
             if (zg < 0.f) continue;
             const float r0 = m[0], r1 = m[1], r2 = m[2], r3 = m[3], r4 = m[4], r5 = m[5], r6 = m[6], r7 = m[7],
                         r8 = m[8], t0 = m[9], t1 = m[10], t2 = m[11], A0 = m[12], A1x = m[13], A1y = m[14];
-            uint64_t m_in = 0;
+            int cc = 0;
             int und = 0;  // bit j: this lane's point j is not decided by the f32 bound
 #pragma unroll
             for (int j = 0; j < P; ++j) {
@@ -287,17 +287,15 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
                 const float M = __builtin_fmaf(__builtin_fmaf(D, 1.001f, sqT2), D, Trel);
                 // written so that NaN anywhere leaves the pair undecided
                 const bool decided = (__builtin_fabsf(e - T) > M) && (__builtin_fabsf(z) > zg);
-                m_in |= __ballot(in[j] && decided && e < T);
+                cc += __popcll(__ballot(in[j] && decided && e < T));
                 und |= (in[j] && !decided) ? (1 << j) : 0;
             }
-            int cc = __popcll(m_in);
             if (__ballot(und != 0)) {
                 // exact f64 error (pnp_err, the oracle's formula) for the undecided pairs
                 const double *md = a.models + (rec0 + h) * kModelStride;
                 const double *cm = a.cams + 4 * prob;
                 const Cam k{cm[0], cm[1], cm[2], cm[3]};
                 const float thr2 = a.thr2[prob];
-                uint64_t m_ex = 0;
                 for (int j = 0; j < P; ++j) {
                     bool ex = false;
                     if ((und >> j) & 1) {
@@ -305,9 +303,8 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
                         ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], pu[j], pv[j]) <=
                              thr2;
                     }
-                    m_ex |= __ballot(ex);
+                    cc += __popcll(__ballot(ex));
                 }
-                cc += __popcll(m_ex);
             }
             cnt += (lane == h) ? cc : 0;
         }
