@@ -255,7 +255,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     const int P = st.P;
     const int64_t N = st.total;
     HIPCHK(c->centred.ensure(sizeof(float) * 3 * std::max<int64_t>(N, 1)));
-    HIPCHK(c->bounds_ws.ensure(sizeof(int32_t) * 6 * P));
+    HIPCHK(c->bounds_ws.ensure(sizeof(int32_t) * 10 * P));
     HIPCHK(c->frame.ensure(sizeof(double) * kFrameStride * P));
     HIPCHK(c->fconst.ensure(sizeof(float) * kFconstStride * P));
     float *C = c->centred.as<float>();

@@ -31,7 +31,7 @@ struct PnpArgs {
     // frame / constants, per-hypothesis float32 records.  fmodels == nullptr
     // (or exact_only) selects the all-f64 scoring kernel.
     const float *XC, *YC, *ZC;
-    const double *frame;  // P x kFrameStride: c0 c1 c2 B rho cmax
+    const double *frame;  // P x kFrameStride: c0 c1 c2 B rho cmax wmax
     const float *fconst;  // P x kFconstStride
     float *fmodels;       // P x hyp_stride x kFModelStride
     int exact_only;
@@ -63,7 +63,7 @@ hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t 
 hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s);
 
 // frame of every problem (centre, bounds, f32 constants) + centred coords:
-// bounds_ws is a P x 6 int workspace.
+// bounds_ws is a P x 10 int workspace.
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *bounds_ws, float *XC, float *YC,
                             float *ZC, double *frame, float *fconst, hipStream_t s);
 // f32 records for H given f64 models (rsac_score_poses / rsac_pnp_mask)

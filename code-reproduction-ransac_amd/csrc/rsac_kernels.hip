@@ -61,20 +61,21 @@ __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i
 
 constexpr double kU32 = 5.9604644775390625e-08;  // 2^-24, unit roundoff of float32
 
-// ws: [0, 3P) mins, [3P, 6P) maxes (ordered-int encoding), pre-set by memset
+// ws: [0, 5P) mins, [5P, 10P) maxes of X Y Z U V (ordered-int encoding), pre-set by memset
 __global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *__restrict__ ws) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
-    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const float v[3] = {a.X[p0 + i], a.Y[p0 + i], a.Z[p0 + i]};
+    float lo[5], hi[5];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { lo[k] = fminf(lo[k], v[k]); hi[k] = fmaxf(hi[k], v[k]); }
+    for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float v[5] = {a.X[p0 + i], a.Y[p0 + i], a.Z[p0 + i], a.U[p0 + i], a.V[p0 + i]};
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { lo[k] = fminf(lo[k], v[k]); hi[k] = fmaxf(hi[k], v[k]); }
     }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 5; ++k) {
         for (int o = 32; o > 0; o >>= 1) {
             lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
             hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
@@ -82,44 +83,55 @@ __global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *_
     }
     if ((threadIdx.x & 63) == 0 && n > 0) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            atomicMin(ws + 3 * prob + k, f2ord(lo[k]));
-            atomicMax(ws + 3 * P + 3 * prob + k, f2ord(hi[k]));
+        for (int k = 0; k < 5; ++k) {
+            atomicMin(ws + 5 * prob + k, f2ord(lo[k]));
+            atomicMax(ws + 5 * P + 5 * prob + k, f2ord(hi[k]));
         }
     }
 }
 
+// Per problem: frame = {c0 c1 c2 (bbox centre), B >= |XC|inf, rho >= |XC - (Xf - c)|,
+// max|Xf|, wmax (bound on |x/z| of any projection within thr of a pixel), 0};
+// fconst = {fx fy cx cy T 2.002 sqrt(T) 1e-6 T thr 2/fx 2/fy cu cv cc0} (see the scoring kernel).
 __global__ void k_pnp_frame(PnpArgs a, int32_t P, const int *__restrict__ ws, double *__restrict__ frame,
                             float *__restrict__ fconst) {
     const int prob = blockIdx.x * blockDim.x + threadIdx.x;
     if (prob >= P) return;
     const int n = (int)(a.offsets[prob + 1] - a.offsets[prob]);
-    double c[3] = {0, 0, 0}, B = 0;
+    const double *cm = a.cams + 4 * prob;
+    const double fx = fabs(cm[0]), fy = fabs(cm[1]), cx = cm[2], cy = cm[3];
+    const double T = a.thr2[prob];
+    const double thr = sqrt(T);
+    double c[3] = {0, 0, 0}, B = 0, du = 0, dv = 0;
     if (n > 0) {
         for (int k = 0; k < 3; ++k) {
-            const double lo = ord2f(ws[3 * prob + k]), hi = ord2f(ws[3 * P + 3 * prob + k]);
+            const double lo = ord2f(ws[5 * prob + k]), hi = ord2f(ws[5 * P + 5 * prob + k]);
             c[k] = (lo + hi) * 0.5;
             B = fmax(B, (hi - lo) * 0.5);
         }
+        du = fmax(fabs(ord2f(ws[5 * prob + 3]) - cx), fabs(ord2f(ws[5 * P + 5 * prob + 3]) - cx));
+        dv = fmax(fabs(ord2f(ws[5 * prob + 4]) - cy), fabs(ord2f(ws[5 * P + 5 * prob + 4]) - cy));
     }
     B = B * (1.0 + 4.0 * kU32) + 1e-30;
     double *f = frame + (int64_t)prob * kFrameStride;
     f[0] = c[0]; f[1] = c[1]; f[2] = c[2];
     f[3] = B;
-    f[4] = 2.0 * kU32 * B;                                           // rho: rounding of XC
-    f[5] = fmax(fmax(fabs(c[0]), fabs(c[1])), fabs(c[2])) + B;      // max |Xf|
-    f[6] = f[7] = 0;
-    const double *cm = a.cams + 4 * prob;
-    const double T = a.thr2[prob];
+    f[4] = 2.0 * kU32 * B;
+    f[5] = fmax(fmax(fabs(c[0]), fabs(c[1])), fabs(c[2])) + B;
+    f[6] = fmax(2.0 * (du + thr) / fx, 2.0 * (dv + thr) / fy) + 2e-3;  // wmax (>= every per-point wa, wb)
+    f[7] = 0;
     float *q = fconst + (int64_t)prob * kFconstStride;
-    q[0] = (float)cm[0]; q[1] = (float)cm[1]; q[2] = (float)cm[2]; q[3] = (float)cm[3];
-    q[4] = (float)(10.1 * kU32 * (fabs(cm[2]) + fabs(cm[3])) + 1e-6);  // C0
-    q[5] = (float)(10.1 * kU32 * fabs(cm[0]));                        // C1x
-    q[6] = (float)(10.1 * kU32 * fabs(cm[1]));                        // C1y
-    q[7] = (float)T;
-    q[8] = (float)(2.002 * sqrt(T));                                  // 2 sqrt(T) with slack
-    q[9] = (float)(1e-6 * T + 1e-30);                                 // relative rounding of e
-    for (int k = 10; k < kFconstStride; ++k) q[k] = 0.f;
+    q[0] = (float)cm[0]; q[1] = (float)cm[1]; q[2] = (float)cx; q[3] = (float)cy;
+    q[4] = (float)T;
+    q[5] = (float)(2.002 * thr);
+    q[6] = (float)(1e-6 * T + 1e-30);
+    q[7] = (float)thr;
+    q[8] = (float)(2.0 / fx);
+    q[9] = (float)(2.0 / fy);
+    q[10] = (float)(10.1 * kU32 * fx);
+    q[11] = (float)(10.1 * kU32 * fy);
+    q[12] = (float)(10.1 * kU32 * (fabs(cx) + fabs(cy) + 0.01 * (fx + fy)) + 1e-6);
+    for (int k = 13; k < kFconstStride; ++k) q[k] = 0.f;
 }
 
 __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, const double *__restrict__ frame,
@@ -138,17 +150,18 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, const double *__r
     }
 }
 
-// float32 record of one pose: R (9), t' = R c + t (3), error-bound constants
-// A0, A1x, A1y and the depth guard zg (zg < 0: no model).
+// float32 record of one pose: R (9), t' = R c + t (3), G0 = 1.01 (fx ex + fy ey),
+// G1 = 1.01 ez, zg (depth guard; < 0: no model).  ex, ey, ez bound |x' - x| etc.,
+// the camera-frame error of the f32 evaluation against the real-number one.
 __device__ __forceinline__ void write_fmodel(const double *R, const double *t, bool valid, const double *frame,
                                              const double *cam, float *fm) {
     if (!valid) {
 #pragma unroll
         for (int q = 0; q < kFModelStride; ++q) fm[q] = 0.f;
-        fm[15] = -1.f;
+        fm[14] = -1.f;
         return;
     }
-    const double B = frame[3], rho = frame[4], cmax = frame[5];
+    const double B = frame[3], rho = frame[4], cmax = frame[5], wmax = frame[6];
     double eps[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -160,10 +173,11 @@ __device__ __forceinline__ void write_fmodel(const double *R, const double *t, b
 #pragma unroll
     for (int q = 0; q < 9; ++q) fm[q] = (float)R[q];
     const double fx = fabs(cam[0]), fy = fabs(cam[1]);
-    fm[12] = (float)(2.01 * (fx * eps[0] + fy * eps[1]));
-    fm[13] = (float)(2.01 * fx * eps[2]);
-    fm[14] = (float)(2.01 * fy * eps[2]);
-    fm[15] = (float)(2.02 * eps[2] + 1e-30);
+    fm[12] = (float)(1.01 * (fx * eps[0] + fy * eps[1]));
+    fm[13] = (float)(1.01 * eps[2]);
+    // |z'| above zg keeps |x'/z' - x/z| <= 0.01 for every projection the bound is used on
+    fm[14] = (float)(100.0 * (fmax(eps[0], eps[1]) + wmax * eps[2]) + 2.02 * eps[2] + 1e-30);
+    fm[15] = 0.f;
 }
 
 __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
@@ -223,12 +237,17 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 }
 
 // ---------------------------------------------------------------------------
-// PnP scoring, float32 pre-filter + exact fallback.  Same tiling as the
-// exact kernel below; per pair the f32 projection of the centred point gives
-// e' and a rigorous bound M on |e' - e| (e = the exact f64-projection error
-// of the oracle).  |e' - T| > M decides the pair; otherwise (and for
-// NaN/near-zero depth) the lane recomputes the exact f64 error.  Counts are
-// therefore bit-identical to the exact kernel.
+// PnP scoring, float32 pre-filter + exact fallback.  Same tiling as the exact
+// kernel below.  Per pair, the f32 projection of the centred point gives e';
+// D bounds |pu' - pu| + |pv' - pv| (pu, pv: the oracle's f64 projection
+// rounded to f32) for every pair whose exact or f32 error is within the
+// threshold, so M = (2 sqrt(T) + D) D + 1e-6 T bounds |e' - e| there:
+//   D = (G0_h + G1_h W_i) |1/z'| + C_i
+// (G from the hypothesis' camera-frame error bound, W_i, C_i from the pixel
+// of point i).  |e' - T| > M with |z'| > zg decides the pair; otherwise the
+// lane recomputes the exact f64 error.  Counts are bit-identical to the
+// exact kernel (tests/test_gpu_parity.py, including threshold-straddling and
+// behind-camera cases).  Derivation: DESIGN.md "Scoring".
 // ---------------------------------------------------------------------------
 template <int P, int HB>
 __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_begin, int32_t H,
@@ -243,8 +262,7 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
-    const float fx = fc[0], fy = fc[1], cx = fc[2], cy = fc[3];
-    const float C0 = fc[4], C1x = fc[5], C1y = fc[6], T = fc[7], sqT2 = fc[8], Trel = fc[9];
+    const float fx = fc[0], fy = fc[1], cx = fc[2], cy = fc[3], T = fc[4], sqT2 = fc[5], Trel = fc[6];
     const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
     const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
     const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
@@ -252,54 +270,70 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
 
     int cnt = 0;
     for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
-        float px[P], py[P], pz[P], pu[P], pv[P];
-        bool in[P];
+        float px[P], py[P], pz[P], pu[P], pv[P], pw[P], pc[P];
+        {
+            const float thr = fc[7], ifx2 = fc[8], ify2 = fc[9], cu = fc[10], cv = fc[11], cc0 = fc[12];
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int i = base + j * 64 + lane;
-            in[j] = i < n;
-            const int ii = in[j] ? i : 0;
-            px[j] = XC[ii]; py[j] = YC[ii]; pz[j] = ZC[ii];
-            pu[j] = U[ii]; pv[j] = V[ii];
+            for (int j = 0; j < P; ++j) {
+                const int i = base + j * 64 + lane;
+                const bool in = i < n;
+                const int ii = in ? i : 0;
+                px[j] = XC[ii]; py[j] = YC[ii]; pz[j] = ZC[ii];
+                const float u = U[ii], v = V[ii];
+                const float wa = __builtin_fmaf(__builtin_fabsf(u - cx) + thr, ifx2, 1e-3f);
+                const float wb = __builtin_fmaf(__builtin_fabsf(v - cy) + thr, ify2, 1e-3f);
+                pw[j] = __builtin_fmaf(fx, wa, fy * wb);
+                pc[j] = __builtin_fmaf(cu, wa, __builtin_fmaf(cv, wb, cc0));
+                // out-of-range lanes: a pixel at 3e38 makes e' = inf, a decided outlier
+                pu[j] = in ? u : 3.0e38f;
+                pv[j] = in ? v : 3.0e38f;
+            }
         }
         for (int h = 0; h < nh; ++h) {
             const float *__restrict__ m = fmb + h * kFModelStride;
-            const float zg = m[15];
+            const float zg = m[14];
             if (zg < 0.f) continue;
             const float r0 = m[0], r1 = m[1], r2 = m[2], r3 = m[3], r4 = m[4], r5 = m[5], r6 = m[6], r7 = m[7],
-                        r8 = m[8], t0 = m[9], t1 = m[10], t2 = m[11], A0 = m[12], A1x = m[13], A1y = m[14];
+                        r8 = m[8], t0 = m[9], t1 = m[10], t2 = m[11], G0 = m[12], G1 = m[13];
             int cc = 0;
-            int und = 0;  // bit j: this lane's point j is not decided by the f32 bound
+            uint64_t und = 0;
 #pragma unroll
             for (int j = 0; j < P; ++j) {
                 const float x = __builtin_fmaf(r0, px[j], __builtin_fmaf(r1, py[j], __builtin_fmaf(r2, pz[j], t0)));
                 const float y = __builtin_fmaf(r3, px[j], __builtin_fmaf(r4, py[j], __builtin_fmaf(r5, pz[j], t1)));
                 const float z = __builtin_fmaf(r6, px[j], __builtin_fmaf(r7, py[j], __builtin_fmaf(r8, pz[j], t2)));
                 const float iz = __builtin_amdgcn_rcpf(z);
-                const float ax = x * iz, ay = y * iz;
-                const float dx = pu[j] - __builtin_fmaf(fx, ax, cx);
-                const float dy = pv[j] - __builtin_fmaf(fy, ay, cy);
+                const float dx = pu[j] - __builtin_fmaf(fx, x * iz, cx);
+                const float dy = pv[j] - __builtin_fmaf(fy, y * iz, cy);
                 const float e = __builtin_fmaf(dx, dx, dy * dy);
-                const float aax = __builtin_fabsf(ax), aay = __builtin_fabsf(ay);
-                const float D = __builtin_fmaf(__builtin_fmaf(A1x, aax, __builtin_fmaf(A1y, aay, A0)),
-                                               __builtin_fabsf(iz),
-                                               __builtin_fmaf(C1x, aax, __builtin_fmaf(C1y, aay, C0)));
+                const float D = __builtin_fmaf(__builtin_fmaf(G1, pw[j], G0), __builtin_fabsf(iz), pc[j]);
                 const float M = __builtin_fmaf(__builtin_fmaf(D, 1.001f, sqT2), D, Trel);
-                // written so that NaN anywhere leaves the pair undecided
+                // written so that a NaN anywhere leaves the pair undecided
                 const bool decided = (__builtin_fabsf(e - T) > M) && (__builtin_fabsf(z) > zg);
-                cc += __popcll(__ballot(in[j] && decided && e < T));
-                und |= (in[j] && !decided) ? (1 << j) : 0;
+                cc += __popcll(__ballot(decided && e < T));
+                und |= __ballot(!decided);
             }
-            if (__ballot(und != 0)) {
+            if (und) {
                 // exact f64 error (pnp_err, the oracle's formula) for the undecided pairs
                 const double *md = a.models + (rec0 + h) * kModelStride;
                 const double *cm = a.cams + 4 * prob;
                 const Cam k{cm[0], cm[1], cm[2], cm[3]};
                 const float thr2 = a.thr2[prob];
                 for (int j = 0; j < P; ++j) {
+                    const float x = __builtin_fmaf(r0, px[j], __builtin_fmaf(r1, py[j], __builtin_fmaf(r2, pz[j], t0)));
+                    const float y = __builtin_fmaf(r3, px[j], __builtin_fmaf(r4, py[j], __builtin_fmaf(r5, pz[j], t1)));
+                    const float z = __builtin_fmaf(r6, px[j], __builtin_fmaf(r7, py[j], __builtin_fmaf(r8, pz[j], t2)));
+                    const float iz = __builtin_amdgcn_rcpf(z);
+                    const float dx = pu[j] - __builtin_fmaf(fx, x * iz, cx);
+                    const float dy = pv[j] - __builtin_fmaf(fy, y * iz, cy);
+                    const float e = __builtin_fmaf(dx, dx, dy * dy);
+                    const float D = __builtin_fmaf(__builtin_fmaf(G1, pw[j], G0), __builtin_fabsf(iz), pc[j]);
+                    const float M = __builtin_fmaf(__builtin_fmaf(D, 1.001f, sqT2), D, Trel);
+                    const bool decided = (__builtin_fabsf(e - T) > M) && (__builtin_fabsf(z) > zg);
+                    const int i = base + j * 64 + lane;
                     bool ex = false;
-                    if ((und >> j) & 1) {
-                        const int64_t q = p0 + base + j * 64 + lane;
+                    if (!decided && i < n) {
+                        const int64_t q = p0 + i;
                         ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], pu[j], pv[j]) <=
                              thr2;
                     }
@@ -581,9 +615,9 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
                             double *frame, float *fconst, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ws, 0x7F, sizeof(int32_t) * 3 * P, s);
+    hipError_t e = hipMemsetAsync(ws, 0x7F, sizeof(int32_t) * 5 * P, s);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(ws + 3 * P, 0x80, sizeof(int32_t) * 3 * P, s);
+    e = hipMemsetAsync(ws + 5 * P, 0x80, sizeof(int32_t) * 5 * P, s);
     if (e != hipSuccess) return e;
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g > 64) g = 64;
