@@ -619,6 +619,12 @@ void rsac_destroy(rsac_ctx *c) {
     delete c;
 }
 
+int rsac_set_score_variant(int variant) {
+    if (variant < 0 || variant > 6) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
+    set_score_variant(variant);
+    return RSAC_OK;
+}
+
 int rsac_set_round_size(rsac_ctx *c, int64_t hyps) {
     if (!c || hyps <= 0) return fail(RSAC_EINVAL, "bad round size");
     c->round_size = hyps;

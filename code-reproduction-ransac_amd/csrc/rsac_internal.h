@@ -74,6 +74,7 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
                               float *DY, hipStream_t s);
 // solve / score hypotheses [hyp_begin, hyp_begin + H) of every problem
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
+void set_score_variant(int v);  // tuning knob (rsac_set_score_variant)
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,

@@ -314,27 +314,22 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
                 und |= __ballot(!decided);
             }
             if (und) {
-                // exact f64 error (pnp_err, the oracle's formula) for the undecided pairs
+                // Some pair of this tile is undecided: recount the whole tile for this
+                // hypothesis with the exact f64 error (pnp_err, the oracle's formula).
+                // Rare; operands are re-read from memory so no register array is
+                // indexed and the f64 code does not raise the kernel's VGPR budget.
                 const double *md = a.models + (rec0 + h) * kModelStride;
                 const double *cm = a.cams + 4 * prob;
                 const Cam k{cm[0], cm[1], cm[2], cm[3]};
                 const float thr2 = a.thr2[prob];
+                cc = 0;
+#pragma unroll 1
                 for (int j = 0; j < P; ++j) {
-                    const float x = __builtin_fmaf(r0, px[j], __builtin_fmaf(r1, py[j], __builtin_fmaf(r2, pz[j], t0)));
-                    const float y = __builtin_fmaf(r3, px[j], __builtin_fmaf(r4, py[j], __builtin_fmaf(r5, pz[j], t1)));
-                    const float z = __builtin_fmaf(r6, px[j], __builtin_fmaf(r7, py[j], __builtin_fmaf(r8, pz[j], t2)));
-                    const float iz = __builtin_amdgcn_rcpf(z);
-                    const float dx = pu[j] - __builtin_fmaf(fx, x * iz, cx);
-                    const float dy = pv[j] - __builtin_fmaf(fy, y * iz, cy);
-                    const float e = __builtin_fmaf(dx, dx, dy * dy);
-                    const float D = __builtin_fmaf(__builtin_fmaf(G1, pw[j], G0), __builtin_fabsf(iz), pc[j]);
-                    const float M = __builtin_fmaf(__builtin_fmaf(D, 1.001f, sqT2), D, Trel);
-                    const bool decided = (__builtin_fabsf(e - T) > M) && (__builtin_fabsf(z) > zg);
                     const int i = base + j * 64 + lane;
                     bool ex = false;
-                    if (!decided && i < n) {
+                    if (i < n) {
                         const int64_t q = p0 + i;
-                        ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], pu[j], pv[j]) <=
+                        ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <=
                              thr2;
                     }
                     cc += __popcll(__ballot(ex));
@@ -639,12 +634,28 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     return hipGetLastError();
 }
 
+// scoring-kernel variants (points per lane, hypotheses per block); 0 = default
+static int g_score_variant = 0;
+void set_score_variant(int v) { g_score_variant = v; }
+
+template <int PP, int HB>
+static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
+    hipLaunchKernelGGL((k_pnp_score_f32<PP, HB>), dim3(cdiv(H, HB), P), dim3(256), 0, s, a, hyp_begin, H, counts);
+}
+
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    if (a.fmodels && !a.exact_only)
-        hipLaunchKernelGGL((k_pnp_score_f32<kScoreP, kScoreHB>), dim3(cdiv(H, kScoreHB), P), dim3(256), 0, s, a,
-                           hyp_begin, H, counts);
-    else
+    if (a.fmodels && !a.exact_only) {
+        switch (g_score_variant) {
+            case 1: launch_f32<4, 32>(a, P, hyp_begin, H, counts, s); break;
+            case 2: launch_f32<8, 64>(a, P, hyp_begin, H, counts, s); break;
+            case 3: launch_f32<16, 32>(a, P, hyp_begin, H, counts, s); break;
+            case 4: launch_f32<6, 32>(a, P, hyp_begin, H, counts, s); break;
+            case 5: launch_f32<8, 16>(a, P, hyp_begin, H, counts, s); break;
+            case 6: launch_f32<4, 64>(a, P, hyp_begin, H, counts, s); break;
+            default: launch_f32<kScoreP, kScoreHB>(a, P, hyp_begin, H, counts, s); break;
+        }
+    } else
         hipLaunchKernelGGL((k_pnp_score<kScoreP, kScoreHB>), dim3(cdiv(H, kScoreHB), P), dim3(256), 0, s, a,
                            hyp_begin, H, counts);
     return hipGetLastError();

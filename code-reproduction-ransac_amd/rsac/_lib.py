@@ -51,6 +51,7 @@ SIGNATURES = [
     ("rsac_abi_version", C.c_int, []),
     ("rsac_device_count", C.c_int, []),
     ("rsac_set_round_size", C.c_int, [_vp, _i64]),
+    ("rsac_set_score_variant", C.c_int, [C.c_int]),
     ("rsac_pnp_ransac", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
                                   C.POINTER(Stats), _vp]),
     ("rsac_pnp_ransac_batched", C.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,

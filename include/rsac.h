@@ -86,6 +86,9 @@ RSAC_EXPORT const char *rsac_last_error(void);
 RSAC_EXPORT int rsac_abi_version(void);
 RSAC_EXPORT int rsac_device_count(void);
 RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
+/* tuning knob: PnP scoring-kernel tiling (0 default; 1..6 alternative points-per-lane x
+ * hypotheses-per-block instantiations, process-wide).  Results never depend on it. */
+RSAC_EXPORT int rsac_set_score_variant(int variant);
 
 /* cv2.solvePnPRansac (main_v1.py:497).  K: 3x3 row-major f64.  Minimal
  * solver: P3P (Lambda Twist) on 4 points.  n_iters = iterationsCount cap,
