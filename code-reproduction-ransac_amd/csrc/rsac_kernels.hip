@@ -124,13 +124,13 @@ __global__ void k_pnp_frame(PnpArgs a, int32_t P, const int *__restrict__ ws, do
     q[0] = (float)cm[0]; q[1] = (float)cm[1]; q[2] = (float)cx; q[3] = (float)cy;
     q[4] = (float)T;
     q[5] = (float)(2.002 * thr);
-    q[6] = (float)(1e-6 * T + 1e-30);
+    q[6] = (float)(4e-6 * T + 1e-30);
     q[7] = (float)thr;
     q[8] = (float)(2.0 / fx);
     q[9] = (float)(2.0 / fy);
-    q[10] = (float)(10.1 * kU32 * fx);
-    q[11] = (float)(10.1 * kU32 * fy);
-    q[12] = (float)(10.1 * kU32 * (fabs(cx) + fabs(cy) + 0.01 * (fx + fy)) + 1e-6);
+    q[10] = (float)(2.5 * kU32);                                            // kc
+    q[11] = (float)(2.5 * kU32 * (fabs(cx) + fabs(cy) + 2.0 * thr + 2.0) + 1e-6);  // kc0
+    q[12] = 0.f;
     for (int k = 13; k < kFconstStride; ++k) q[k] = 0.f;
 }
 
@@ -150,9 +150,11 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, const double *__r
     }
 }
 
-// float32 record of one pose: R (9), t' = R c + t (3), G0 = 1.01 (fx ex + fy ey),
-// G1 = 1.01 ez, zg (depth guard; < 0: no model).  ex, ey, ez bound |x' - x| etc.,
-// the camera-frame error of the f32 evaluation against the real-number one.
+// float32 record of one pose, division-free form of the test:
+//   { -fx R0 -fx R1 -fx R2 | -fy R3 -fy R4 -fy R5 | R6 R7 R8 | -fx t'x -fy t'y t'z | G0 G1 zg 0 }
+// with t' = R c + t.  ex, ey bound |xs' - fx x|/fx, |ys' - fy y|/fy and ez |z' - z| (camera
+// frame, f32 evaluation vs real numbers); G0 = 1.01 (fx ex + fy ey), G1 = 1.01 ez; zg is the
+// depth guard (< 0: no model).
 __device__ __forceinline__ void write_fmodel(const double *R, const double *t, bool valid, const double *frame,
                                              const double *cam, float *fm) {
     if (!valid) {
@@ -162,17 +164,18 @@ __device__ __forceinline__ void write_fmodel(const double *R, const double *t, b
         return;
     }
     const double B = frame[3], rho = frame[4], cmax = frame[5], wmax = frame[6];
+    const double fx = fabs(cam[0]), fy = fabs(cam[1]);
+    const double sc[3] = {-cam[0], -cam[1], 1.0};
     double eps[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const double tp = R[3 * r] * frame[0] + R[3 * r + 1] * frame[1] + R[3 * r + 2] * frame[2] + t[r];
         const double r1 = fabs(R[3 * r]) + fabs(R[3 * r + 1]) + fabs(R[3 * r + 2]);
-        eps[r] = 6.0 * kU32 * (r1 * B + fabs(tp)) + r1 * rho + 4e-15 * (r1 * cmax + fabs(t[r]));
-        fm[9 + r] = (float)tp;
-    }
+        eps[r] = 8.0 * kU32 * (r1 * B + fabs(tp)) + r1 * rho + 4e-15 * (r1 * cmax + fabs(t[r]));
 #pragma unroll
-    for (int q = 0; q < 9; ++q) fm[q] = (float)R[q];
-    const double fx = fabs(cam[0]), fy = fabs(cam[1]);
+        for (int q = 0; q < 3; ++q) fm[3 * r + q] = (float)(sc[r] * R[3 * r + q]);
+        fm[9 + r] = (float)(sc[r] * tp);
+    }
     fm[12] = (float)(1.01 * (fx * eps[0] + fy * eps[1]));
     fm[13] = (float)(1.01 * eps[2]);
     // |z'| above zg keeps |x'/z' - x/z| <= 0.01 for every projection the bound is used on
@@ -237,16 +240,17 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 }
 
 // ---------------------------------------------------------------------------
-// PnP scoring, float32 pre-filter + exact fallback.  Same tiling as the exact
-// kernel below.  Per pair, the f32 projection of the centred point gives e';
-// D bounds |pu' - pu| + |pv' - pv| (pu, pv: the oracle's f64 projection
-// rounded to f32) for every pair whose exact or f32 error is within the
-// threshold, so M = (2 sqrt(T) + D) D + 1e-6 T bounds |e' - e| there:
-//   D = (G0_h + G1_h W_i) |1/z'| + C_i
-// (G from the hypothesis' camera-frame error bound, W_i, C_i from the pixel
-// of point i).  |e' - T| > M with |z'| > zg decides the pair; otherwise the
-// lane recomputes the exact f64 error.  Counts are bit-identical to the
-// exact kernel (tests/test_gpu_parity.py, including threshold-straddling and
+// PnP scoring, float32 pre-filter + exact fallback (division-free).  Same
+// tiling as the exact kernel below.  Per pair (point i, hypothesis h), with
+// the point centred (XC) and the pixel taken relative to the principal point
+// (uc, vc):
+//   q1 = uc z - fx x,  q2 = vc z - fy y          (= z (u - pu), z (v - pv))
+//   E  = q1^2 + q2^2,  diff = E - T z^2          (sign(diff) = sign(e - T))
+//   Dz = (G0_h + G1_h W_i) + C_i |z|             (D |z|, D: pixel-error bound)
+//   Mz = (2 sqrt(T) |z| + Dz) Dz + 4e-6 T z^2    (M z^2, M: bound on |e' - e|)
+// |diff| > Mz and |z| > zg_h decide the pair; otherwise the tile is recounted
+// for this hypothesis with the exact f64 error.  Counts are bit-identical to
+// the exact kernel (tests/test_gpu_parity.py: threshold-straddling and
 // behind-camera cases).  Derivation: DESIGN.md "Scoring".
 // ---------------------------------------------------------------------------
 template <int P, int HB>
@@ -262,7 +266,7 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
-    const float fx = fc[0], fy = fc[1], cx = fc[2], cy = fc[3], T = fc[4], sqT2 = fc[5], Trel = fc[6];
+    const float T = fc[4], sqT2 = fc[5], Trel = fc[6];
     const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
     const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
     const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
@@ -272,21 +276,23 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
     for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
         float px[P], py[P], pz[P], pu[P], pv[P], pw[P], pc[P];
         {
-            const float thr = fc[7], ifx2 = fc[8], ify2 = fc[9], cu = fc[10], cv = fc[11], cc0 = fc[12];
+            const float fx = fc[0], fy = fc[1], cx = fc[2], cy = fc[3], thr = fc[7], ifx2 = fc[8], ify2 = fc[9];
+            const float kc = fc[10], kc0 = fc[11];
 #pragma unroll
             for (int j = 0; j < P; ++j) {
                 const int i = base + j * 64 + lane;
                 const bool in = i < n;
                 const int ii = in ? i : 0;
                 px[j] = XC[ii]; py[j] = YC[ii]; pz[j] = ZC[ii];
-                const float u = U[ii], v = V[ii];
-                const float wa = __builtin_fmaf(__builtin_fabsf(u - cx) + thr, ifx2, 1e-3f);
-                const float wb = __builtin_fmaf(__builtin_fabsf(v - cy) + thr, ify2, 1e-3f);
+                const float uc = U[ii] - cx, vc = V[ii] - cy;
+                const float au = __builtin_fabsf(uc), av = __builtin_fabsf(vc);
+                const float wa = __builtin_fmaf(au + thr, ifx2, 1e-3f);
+                const float wb = __builtin_fmaf(av + thr, ify2, 1e-3f);
                 pw[j] = __builtin_fmaf(fx, wa, fy * wb);
-                pc[j] = __builtin_fmaf(cu, wa, __builtin_fmaf(cv, wb, cc0));
-                // out-of-range lanes: a pixel at 3e38 makes e' = inf, a decided outlier
-                pu[j] = in ? u : 3.0e38f;
-                pv[j] = in ? v : 3.0e38f;
+                pc[j] = __builtin_fmaf(kc, au + av, kc0);
+                // out-of-range lanes: a pixel at 3e38 makes the pair a decided outlier
+                pu[j] = in ? uc : 3.0e38f;
+                pv[j] = in ? vc : 3.0e38f;
             }
         }
         for (int h = 0; h < nh; ++h) {
@@ -299,19 +305,22 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
             uint64_t und = 0;
 #pragma unroll
             for (int j = 0; j < P; ++j) {
-                const float x = __builtin_fmaf(r0, px[j], __builtin_fmaf(r1, py[j], __builtin_fmaf(r2, pz[j], t0)));
-                const float y = __builtin_fmaf(r3, px[j], __builtin_fmaf(r4, py[j], __builtin_fmaf(r5, pz[j], t1)));
+                const float xs = __builtin_fmaf(r0, px[j], __builtin_fmaf(r1, py[j], __builtin_fmaf(r2, pz[j], t0)));
+                const float ys = __builtin_fmaf(r3, px[j], __builtin_fmaf(r4, py[j], __builtin_fmaf(r5, pz[j], t1)));
                 const float z = __builtin_fmaf(r6, px[j], __builtin_fmaf(r7, py[j], __builtin_fmaf(r8, pz[j], t2)));
-                const float iz = __builtin_amdgcn_rcpf(z);
-                const float dx = pu[j] - __builtin_fmaf(fx, x * iz, cx);
-                const float dy = pv[j] - __builtin_fmaf(fy, y * iz, cy);
-                const float e = __builtin_fmaf(dx, dx, dy * dy);
-                const float D = __builtin_fmaf(__builtin_fmaf(G1, pw[j], G0), __builtin_fabsf(iz), pc[j]);
-                const float M = __builtin_fmaf(__builtin_fmaf(D, 1.001f, sqT2), D, Trel);
-                // written so that a NaN anywhere leaves the pair undecided
-                const bool decided = (__builtin_fabsf(e - T) > M) && (__builtin_fabsf(z) > zg);
-                cc += __popcll(__ballot(decided && e < T));
-                und |= __ballot(!decided);
+                const float q1 = __builtin_fmaf(pu[j], z, xs);
+                const float q2 = __builtin_fmaf(pv[j], z, ys);
+                const float z2 = z * z;
+                const float diff = __builtin_fmaf(-T, z2, __builtin_fmaf(q1, q1, q2 * q2));
+                const float az = __builtin_fabsf(z);
+                const float Dz = __builtin_fmaf(pc[j], az, __builtin_fmaf(G1, pw[j], G0));
+                const float Mz = __builtin_fmaf(__builtin_fmaf(sqT2, az, Dz), Dz, Trel * z2);
+                // one v_cmp per mask; a NaN anywhere leaves the pair undecided
+                const uint64_t mz = __ballot(az > zg);
+                const uint64_t mi = __ballot(diff < -Mz);
+                const uint64_t mo = __ballot(diff > Mz);
+                cc += __popcll(mi & mz);
+                und |= ~((mi | mo) & mz);
             }
             if (und) {
                 // Some pair of this tile is undecided: recount the whole tile for this
