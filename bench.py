@@ -77,19 +77,26 @@ def main():
     solve_ms = []
 
     def step():
-        key, model, info = rsac.evaluate_range(p2, p3, K, base, H, args.thr, return_info=True, device=local)
+        key, model, mask, info = rsac.evaluate_range(p2, p3, K, base, H, args.thr, return_info=True,
+                                                     with_mask=True, device=local)
         score_ms.append(info.score_ms)
         solve_ms.append(info.solve_ms)
-        if dist is not None:
-            kt = torch.tensor([key], dtype=torch.int64, device=dev)
-            dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-            gkey = int(kt.item())
-            gidx = 0xFFFFFFFF - (gkey & 0xFFFFFFFF)
+        if dist is None:
+            return key >> 32
+        kt = torch.tensor([key], dtype=torch.int64, device=dev)
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+        gkey = int(kt.item())
+        owner = min((0xFFFFFFFF - (gkey & 0xFFFFFFFF)) // H, world - 1)
+        if owner != rank or gkey != key:
+            # the winner lives on another rank: take its model, recompute the mask here
             mt = torch.from_numpy(model).to(dev)
-            dist.broadcast(mt, src=min(gidx // H, world - 1))
-            model = mt.cpu().numpy()
-        mask, cnt = rsac.pose_mask(p2, p3, K, model, args.thr, device=local)
-        return cnt
+            dist.broadcast(mt, src=owner)
+            if rank == 0:
+                mask, _ = rsac.pose_mask(p2, p3, K, mt.cpu().numpy(), args.thr, device=local)
+        else:
+            mt = torch.from_numpy(model).to(dev)
+            dist.broadcast(mt, src=owner)
+        return gkey >> 32
 
     for _ in range(args.warmup):
         step()

@@ -97,7 +97,10 @@ struct rsac_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     int64_t round_size = 4096;
     // device scratch
-    DevBuf pts, offsets, cams, thr2, models, status, counts, subsets, substatus, best, bestmodels, mask;
+    DevBuf pts, tables, models, status, counts, subsets, substatus, best, bestmodels, mask;
+    int64_t *d_off = nullptr;  // views into `tables`: offsets (P+1), cams (P x 4), thr2 (P)
+    double *d_cams = nullptr;
+    float *d_thr2 = nullptr;
     DevBuf centred, bounds_ws, frame, fconst, fmodels;  // float32 pre-filter state (PnP)
     // pinned host staging
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask;
@@ -182,16 +185,17 @@ int ensure_host_points(Staged &st, int nc, hipStream_t s) {
     return RSAC_OK;
 }
 
-// small per-problem tables: offsets (int64), cams (4 f64), thr2 (f32)
+// small per-problem tables, one H2D copy: offsets (int64 P+1), cams (P x fx fy cx cy, f64),
+// thr2 (f32, findInliers' float t = (float)(thresh*thresh))
 int stage_tables(rsac_ctx *c, const Staged &st, const double *K, double thresh, hipStream_t s) {
     const int P = st.P;
-    const size_t off_b = sizeof(int64_t) * (P + 1), cam_b = sizeof(double) * 4 * P, thr_b = sizeof(float) * P;
-    HIPCHK(c->offsets.ensure(off_b));
-    HIPCHK(c->cams.ensure(std::max<size_t>(cam_b, 32)));
-    HIPCHK(c->thr2.ensure(thr_b));
-    HIPCHK(c->h_small.ensure(off_b + cam_b + thr_b + 64));
+    auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+    const size_t off_b = al(sizeof(int64_t) * (P + 1)), cam_b = al(sizeof(double) * 4 * P), thr_b = al(sizeof(float) * P);
+    const size_t tot = off_b + cam_b + thr_b;
+    HIPCHK(c->tables.ensure(tot));
+    HIPCHK(c->h_small.ensure(tot));
     char *hs = c->h_small.as<char>();
-    memcpy(hs, st.off.data(), off_b);
+    memcpy(hs, st.off.data(), sizeof(int64_t) * (P + 1));
     double *hc = (double *)(hs + off_b);
     for (int p = 0; p < P; ++p) {
         if (K) {
@@ -202,11 +206,13 @@ int stage_tables(rsac_ctx *c, const Staged &st, const double *K, double thresh, 
         }
     }
     float *ht = (float *)(hs + off_b + cam_b);
-    const float t2 = (float)(thresh * thresh);  // findInliers: float t = (float)(thresh*thresh)
+    const float t2 = (float)(thresh * thresh);
     for (int p = 0; p < P; ++p) ht[p] = t2;
-    HIPCHK(hipMemcpyAsync(c->offsets.p, hs, off_b, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->cams.p, hs + off_b, cam_b, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->thr2.p, hs + off_b + cam_b, thr_b, hipMemcpyHostToDevice, s));
+    char *d = c->tables.as<char>();
+    HIPCHK(hipMemcpyAsync(d, hs, tot, hipMemcpyHostToDevice, s));
+    c->d_off = (int64_t *)d;
+    c->d_cams = (double *)(d + off_b);
+    c->d_thr2 = (float *)(d + off_b + cam_b);
     return RSAC_OK;
 }
 
@@ -240,9 +246,9 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
              hipStream_t s, PnpArgs &a) {
     a = PnpArgs{};
     a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
-    a.offsets = c->offsets.as<int64_t>();
-    a.cams = c->cams.as<double>();
-    a.thr2 = c->thr2.as<float>();
+    a.offsets = c->d_off;
+    a.cams = c->d_cams;
+    a.thr2 = c->d_thr2;
     a.models = c->models.as<double>();
     a.status = c->status.as<int8_t>();
     a.hyp_stride = stride;
@@ -518,8 +524,8 @@ int hom_core(rsac_ctx *c, const void *src, const void *dst, const int64_t *offse
     }
     HomArgs a{};
     a.SX = st.d[0]; a.SY = st.d[1]; a.DX = st.d[2]; a.DY = st.d[3];
-    a.offsets = c->offsets.as<int64_t>();
-    a.thr2 = c->thr2.as<float>();
+    a.offsets = c->d_off;
+    a.thr2 = c->d_thr2;
     a.seed = seed;
     a.rng_base = 0;
     LoopOut lo;
@@ -604,10 +610,9 @@ void rsac_destroy(rsac_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf *dev[] = {&c->pts,       &c->offsets,    &c->cams,  &c->thr2,      &c->models,
-                     &c->status,    &c->counts,     &c->subsets, &c->substatus, &c->best,
-                     &c->bestmodels, &c->mask,      &c->centred, &c->bounds_ws, &c->frame,
-                     &c->fconst,    &c->fmodels};
+    DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
+                     &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
+                     &c->frame, &c->fconst,   &c->fmodels};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};
@@ -700,7 +705,8 @@ int rsac_score_poses(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t 
 
 int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
                             int64_t hyp_begin, int64_t n_hyps, double thr, uint64_t seed, uint32_t flags,
-                            int64_t *key_out, double model_out[12], rsac_stats *stats, void *stream) {
+                            int64_t *key_out, double model_out[12], uint8_t *mask_out, rsac_stats *stats,
+                            void *stream) {
     int r = check_device(c);
     if (r) return r;
     if (n < 4) return fail(RSAC_ETOOFEW, "need >= 4 correspondences");
@@ -717,20 +723,37 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
     r = pnp_args(c, st, flags, seed, n_hyps, hyp_begin, s, a);
     if (r) return r;
     const int32_t H = (int32_t)n_hyps;
+    // the best key is reduced inside the scoring kernel; only 8 bytes + the
+    // winner's record (+ its mask, computed on the device) leave the GPU
+    unsigned long long *dkey = (unsigned long long *)c->best.p;
+    a.best_key = dkey;
+    HIPCHK(hipMemsetAsync(dkey, 0, sizeof(unsigned long long), s));
     HIPCHK(hipEventRecord(c->ev0, s));
     HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
     HIPCHK(hipEventRecord(c->ev1, s));
     HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
     HIPCHK(hipEventRecord(c->ev2, s));
-    // device-side argmax: only the 8-byte key and the winner's record cross PCIe
-    unsigned long long *dkey = (unsigned long long *)c->best.p;
-    HIPCHK(launch_best_key(c->counts.as<int32_t>(), c->status.as<int8_t>(), H, hyp_begin, dkey,
-                           c->models.as<double>(), c->bestmodels.as<double>(), s));
+    HIPCHK(launch_key_model(c->models.as<double>(), dkey, hyp_begin, c->bestmodels.as<double>(), s));
+    uint8_t *hmask_dev = nullptr;
+    if (mask_out) {
+        if (flags & RSAC_F_DEVICE_OUT) {
+            hmask_dev = mask_out;
+        } else {
+            HIPCHK(c->mask.ensure(std::max(n, 1)));
+            hmask_dev = c->mask.as<uint8_t>();
+        }
+        HIPCHK(launch_pnp_mask_key(a, n, dkey, hmask_dev, s));
+    }
     HIPCHK(c->h_bestmodels.ensure(sizeof(double) * (kModelStride + 2)));
     double *hb = c->h_bestmodels.as<double>();
     HIPCHK(hipMemcpyAsync(hb, c->bestmodels.p, sizeof(double) * kModelStride, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(hb + kModelStride, dkey, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if (mask_out && !(flags & RSAC_F_DEVICE_OUT)) {
+        HIPCHK(c->h_mask.ensure(std::max(n, 1)));
+        HIPCHK(hipMemcpyAsync(c->h_mask.p, hmask_dev, n, hipMemcpyDeviceToHost, s));
+    }
     HIPCHK(hipStreamSynchronize(s));
+    if (mask_out && !(flags & RSAC_F_DEVICE_OUT)) memcpy(mask_out, c->h_mask.p, n);
     unsigned long long key;
     memcpy(&key, hb + kModelStride, sizeof key);
     if (stats) {
@@ -793,8 +816,8 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
     } else {
         HomArgs a{};
         a.SX = st.d[0]; a.SY = st.d[1]; a.DX = st.d[2]; a.DY = st.d[3];
-        a.offsets = c->offsets.as<int64_t>();
-        a.thr2 = c->thr2.as<float>();
+        a.offsets = c->d_off;
+        a.thr2 = c->d_thr2;
         a.models = c->models.as<double>();
         a.status = c->status.as<int8_t>();
         a.subsets = subsets ? c->subsets.as<int32_t>() : nullptr;
@@ -850,9 +873,9 @@ int rsac_pnp_mask(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, 
     HIPCHK(hipMemcpyAsync(c->best.p, &zero, sizeof zero, hipMemcpyHostToDevice, s));
     PnpArgs a{};
     a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
-    a.offsets = c->offsets.as<int64_t>();
-    a.cams = c->cams.as<double>();
-    a.thr2 = c->thr2.as<float>();
+    a.offsets = c->d_off;
+    a.cams = c->d_cams;
+    a.thr2 = c->d_thr2;
     a.models = c->models.as<double>();
     uint8_t *dmask;
     if (flags & RSAC_F_DEVICE_OUT) {

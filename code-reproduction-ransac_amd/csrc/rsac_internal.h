@@ -35,6 +35,9 @@ struct PnpArgs {
     const float *fconst;  // P x kFconstStride
     float *fmodels;       // P x hyp_stride x kFModelStride
     int exact_only;
+    // optional fused reduction (single problem): max over the scored hypotheses of
+    // (count << 32) | (0xFFFFFFFF - low32(rng_base + h)), atomically into *best_key
+    unsigned long long *best_key;
 };
 
 constexpr int kFrameStride = 8;
@@ -53,6 +56,13 @@ struct HomArgs {
     int64_t rng_base;
     uint64_t seed;
 };
+
+// mask of the hypothesis a packed key names (problem 0, records at hyp 0..)
+hipError_t launch_pnp_mask_key(const PnpArgs &a, int32_t n, const unsigned long long *key, uint8_t *mask,
+                               hipStream_t s);
+// record of the hypothesis a packed key names -> out[16] (zeros when key == 0)
+hipError_t launch_key_model(const double *models, const unsigned long long *key, int64_t rng_base, double *out,
+                            hipStream_t s);
 
 // best packed key of counts[0, H) (+ its model record -> model_out[16]);
 // key = 0 when no hypothesis has a model with >= 1 inlier

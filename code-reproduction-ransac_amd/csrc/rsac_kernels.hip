@@ -63,6 +63,7 @@ constexpr double kU32 = 5.9604644775390625e-08;  // 2^-24, unit roundoff of floa
 
 // ws: [0, 5P) mins, [5P, 10P) maxes of X Y Z U V (ordered-int encoding), pre-set by memset
 __global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *__restrict__ ws) {
+    __shared__ float sl[4][5], sh[4][5];
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
@@ -81,12 +82,18 @@ __global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *_
             hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
         }
     }
-    if ((threadIdx.x & 63) == 0 && n > 0) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            atomicMin(ws + 5 * prob + k, f2ord(lo[k]));
-            atomicMax(ws + 5 * P + 5 * prob + k, f2ord(hi[k]));
-        }
+        for (int k = 0; k < 5; ++k) { sl[wave][k] = lo[k]; sh[wave][k] = hi[k]; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 5 && n > 0) {
+        const int k = threadIdx.x;
+        const float l = fminf(fminf(sl[0][k], sl[1][k]), fminf(sl[2][k], sl[3][k]));
+        const float h = fmaxf(fmaxf(sh[0][k], sh[1][k]), fmaxf(sh[2][k], sh[3][k]));
+        atomicMin(ws + 5 * prob + k, f2ord(l));
+        atomicMax(ws + 5 * P + 5 * prob + k, f2ord(h));
     }
 }
 
@@ -253,6 +260,30 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 // the exact kernel (tests/test_gpu_parity.py: threshold-straddling and
 // behind-camera cases).  Derivation: DESIGN.md "Scoring".
 // ---------------------------------------------------------------------------
+// counts of the block's hypotheses (sum of the 4 waves' partials) and, when
+// a.best_key is set, one atomicMax of the block's best packed key
+template <int HB>
+__device__ __forceinline__ void pnp_score_epilogue(const PnpArgs &a, const int (&red)[4][HB], int prob, int64_t h0,
+                                                   int nh, int lane, int32_t *__restrict__ counts) {
+    int s = 0;
+    if (lane < nh) {
+        s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+        counts[(int64_t)prob * a.hyp_stride + h0 + lane] = s;
+    }
+    if (a.best_key) {
+        unsigned long long k = 0;
+        if (lane < nh && s > 0) {
+            const uint64_t g = (uint64_t)(a.rng_base + h0 + lane);
+            k = ((unsigned long long)(uint32_t)s << 32) | (0xFFFFFFFFull - (g & 0xFFFFFFFFull));
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long other = __shfl_xor(k, o);
+            k = other > k ? other : k;
+        }
+        if (lane == 0 && k) atomicMax(a.best_key, k);
+    }
+}
+
 template <int P, int HB>
 __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_begin, int32_t H,
                                                        int32_t *__restrict__ counts) {
@@ -349,10 +380,7 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
     }
     if (lane < HB) red[wave][lane] = cnt;
     __syncthreads();
-    if (threadIdx.x < nh) {
-        const int s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-        counts[(int64_t)prob * a.hyp_stride + h0 + threadIdx.x] = s;
-    }
+    if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
 }
 
 // ---------------------------------------------------------------------------
@@ -410,10 +438,7 @@ __global__ __launch_bounds__(256) void k_pnp_score(PnpArgs a, int64_t hyp_begin,
     }
     if (lane < HB) red[wave][lane] = cnt;
     __syncthreads();
-    if (threadIdx.x < nh) {
-        const int s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-        counts[(int64_t)prob * a.hyp_stride + h0 + threadIdx.x] = s;
-    }
+    if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
 }
 
 // mask of one model per problem (best[prob] indexes the models buffer; <0 = none)
@@ -434,6 +459,24 @@ __global__ void k_pnp_mask(PnpArgs a, const int64_t *__restrict__ best, uint8_t 
         }
         mask[p0 + i] = f;
     }
+}
+
+// mask of the hypothesis named by a packed key (problem 0, records from hypothesis 0)
+__global__ void k_pnp_mask_key(PnpArgs a, int32_t n, const unsigned long long *__restrict__ key,
+                               uint8_t *__restrict__ mask) {
+    const unsigned long long k = *key;
+    const double *c = a.cams;
+    const Cam cam{c[0], c[1], c[2], c[3]};
+    const float thr2 = a.thr2[0];
+    const double *m = nullptr;
+    if (k) {
+        const uint64_t low = 0xFFFFFFFFull - (k & 0xFFFFFFFFull);
+        const int64_t h = (int64_t)((low - ((uint64_t)a.rng_base & 0xFFFFFFFFull)) & 0xFFFFFFFFull);
+        m = a.models + h * kModelStride;
+    }
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        mask[i] = m ? (pnp_err(m, m + 9, cam, (double)a.X[i], (double)a.Y[i], (double)a.Z[i], a.U[i], a.V[i]) <= thr2)
+                    : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -623,8 +666,8 @@ hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t 
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(ws + 5 * P, 0x80, sizeof(int32_t) * 5 * P, s);
     if (e != hipSuccess) return e;
-    unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
-    if (g > 64) g = 64;
+    unsigned g = cdiv(max_n > 0 ? max_n : 1, 2048);
+    if (g > 32) g = 32;
     hipLaunchKernelGGL(k_pnp_bounds, dim3(g, P), dim3(256), 0, s, a, P, ws);
     hipLaunchKernelGGL(k_pnp_frame, dim3(cdiv(P, 64)), dim3(64), 0, s, a, P, ws, frame, fconst);
     unsigned g2 = cdiv(max_n > 0 ? max_n : 1, 256);
@@ -701,6 +744,20 @@ hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int
 hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s) {
     hipLaunchKernelGGL(k_gather_models, dim3(cdiv((int64_t)P * kModelStride, 256)), dim3(256), 0, s, models, rec, P,
                        out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_mask_key(const PnpArgs &a, int32_t n, const unsigned long long *key, uint8_t *mask,
+                               hipStream_t s) {
+    unsigned g = cdiv(n > 0 ? n : 1, 256);
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_pnp_mask_key, dim3(g), dim3(256), 0, s, a, n, key, mask);
+    return hipGetLastError();
+}
+
+hipError_t launch_key_model(const double *models, const unsigned long long *key, int64_t rng_base, double *out,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_key_model, dim3(1), dim3(64), 0, s, models, key, rng_base, out);
     return hipGetLastError();
 }
 

@@ -62,7 +62,7 @@ SIGNATURES = [
                                                  _vp, _vp]),
     ("rsac_score_poses", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _i32, _d, _u32, _vp, _vp]),
     ("rsac_pnp_evaluate_range", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i64, _i64, _d, _u64, _u32,
-                                          C.POINTER(_i64), _vp, C.POINTER(Stats), _vp]),
+                                          C.POINTER(_i64), _vp, _vp, C.POINTER(Stats), _vp]),
     ("rsac_pnp_hypotheses", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i64, _i32, _d, _u64, _u32, _vp, _vp, _vp, _vp,
                                       _vp]),
     ("rsac_homography_hypotheses", C.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _d, _u64, _u32, _vp, _vp, _vp, _vp,

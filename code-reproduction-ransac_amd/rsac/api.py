@@ -91,7 +91,8 @@ def _mask_buffer(inp: _In, n: int):
 
 
 def _finish_mask(m, n):
-    return m[:n].bool() if _is_torch(m) else m[:n].astype(bool)
+    # uint8 0/1 -> bool without a copy (torch: reinterpret the bytes)
+    return m[:n].view(dtype=__import__("torch").bool) if _is_torch(m) else m[:n].view(np.bool_)
 
 
 @dataclass
@@ -280,11 +281,13 @@ def score_poses(points2D, points3D, K, poses, reproj_thresh: float = 30.0, devic
 
 
 def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_thresh: float = 30.0, *,
-                   seed: int = 0x5EED, device=None, return_info: bool = False, exact_only: bool = False):
+                   seed: int = 0x5EED, device=None, return_info: bool = False, exact_only: bool = False,
+                   with_mask: bool = False):
     """Evaluate Philox hypotheses [hyp_begin, hyp_begin + n_hyps) of one problem.
 
-    Returns (key, model12) where key = (count << 32) | (0xFFFFFFFF - best_index) (or -1).
-    The sharded driver (rsac.parallel) all-reduces the key with MAX.
+    Returns (key, model12[, mask][, info]) where key = (count << 32) | (0xFFFFFFFF - best_index)
+    (or -1) and mask is the best hypothesis' RANSAC-phase mask (with_mask=True; on the GPU for
+    GPU inputs).  The sharded driver (rsac.parallel) all-reduces the key with MAX.
     """
     p3 = _In(points3D, 3)
     p2 = _In(points2D, 2)
@@ -294,15 +297,23 @@ def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_th
     model = np.zeros(12)
     K9 = _K9(K)
     st = L.Stats()
+    mask = mptr = None
+    if with_mask:
+        mask, mptr, mflag = _mask_buffer(p3, p3.n)
+        flags |= mflag
     with ctx.lock:
         code = L.check(L.lib().rsac_pnp_evaluate_range(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n,
                                                        K9.ctypes.data, int(hyp_begin), int(n_hyps),
                                                        float(reproj_thresh), int(seed) & (2**64 - 1), flags,
-                                                       C.byref(key), model.ctypes.data, C.byref(st),
+                                                       C.byref(key), model.ctypes.data,
+                                                       C.c_void_p(mptr) if with_mask else None, C.byref(st),
                                                        _stream_of(p3)))
+    out = (int(key.value), model)
+    if with_mask:
+        out = out + (_finish_mask(mask, p3.n),)
     if return_info:
-        return int(key.value), model, _info(code, st)
-    return int(key.value), model
+        out = out + (_info(code, st),)
+    return out
 
 
 def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024, reproj_thresh: float = 30.0, *,

@@ -130,12 +130,14 @@ RSAC_EXPORT int rsac_score_poses(rsac_ctx *ctx, const void *pts3d, const void *p
 /* Hypothesis-range evaluation for sharding one problem over ranks
  * (SURVEY.md §8e): evaluates hypotheses [hyp_begin, hyp_begin + n_hyps) of
  * the Philox stream and returns the packed key
- * (count << 32) | (0xFFFFFFFF - local_best_index) of the best one
- * (lowest index among ties) and that hypothesis' model (R, t).  Ranks
- * all-reduce(MAX) the key. */
+ * (count << 32) | (0xFFFFFFFF - low32(global index)) of the best one (lowest
+ * index among ties), that hypothesis' model (R, t) and, if mask_out is
+ * given, its RANSAC-phase mask (device pointer with RSAC_F_DEVICE_OUT).
+ * Ranks all-reduce(MAX) the key. */
 RSAC_EXPORT int rsac_pnp_evaluate_range(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
                             int64_t hyp_begin, int64_t n_hyps, double reproj_thresh, uint64_t seed, uint32_t flags,
-                            int64_t *key_out, double model_out[12], rsac_stats *stats, void *stream);
+                            int64_t *key_out, double model_out[12], uint8_t *mask_out, rsac_stats *stats,
+                            void *stream);
 
 /* Raw hot-path outputs for hypotheses [hyp_begin, hyp_begin + n_hyps) of
  * one problem: per-hypothesis status (1 model, 0 solver failed, -1 no

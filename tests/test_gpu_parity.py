@@ -217,11 +217,15 @@ def test_baseline_size_sampled_parity_and_properties():
     assert c == cnt[best] == int(m.sum())
     assert (m == pr["inlier"]).mean() > 0.99
     # sharded evaluation over two halves gives the same global best (key all-reduce MAX)
-    k0, _ = rsac.evaluate_range(pr["points2d"], pr["points3d"], pr["K"], 0, H // 2, 30.0)
-    k1, _ = rsac.evaluate_range(pr["points2d"], pr["points3d"], pr["K"], H // 2, H // 2, 30.0)
+    k0, m0, mk0 = rsac.evaluate_range(pr["points2d"], pr["points3d"], pr["K"], 0, H // 2, 30.0, with_mask=True)
+    k1, m1, mk1 = rsac.evaluate_range(pr["points2d"], pr["points3d"], pr["K"], H // 2, H // 2, 30.0, with_mask=True)
     kmax = max(k0, k1)
     assert (kmax >> 32) == cnt[best]
     assert 0xFFFFFFFF - (kmax & 0xFFFFFFFF) == best
+    np.testing.assert_array_equal(mk0 if k0 > k1 else mk1, m)
+    for k, mk in ((k0, mk0), (k1, mk1)):
+        h = 0xFFFFFFFF - (k & 0xFFFFFFFF)
+        assert (k >> 32) == cnt[h] == int(mk.sum())
 
 
 def test_degenerate_inputs():
