@@ -101,7 +101,7 @@ struct rsac_ctx {
     int64_t *d_off = nullptr;  // views into `tables`: offsets (P+1), cams (P x 4), thr2 (P)
     double *d_cams = nullptr;
     float *d_thr2 = nullptr;
-    DevBuf centred, bounds_ws, frame, fconst, fmodels;  // float32 pre-filter state (PnP)
+    DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
     // pinned host staging
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask;
 };
@@ -243,7 +243,7 @@ hipStream_t pick_stream(rsac_ctx *c, void *stream) { return stream ? (hipStream_
 // on the device (unless RSAC_F_EXACT_ONLY).  Call after stage_tables and
 // ensure_hyp_buffers.
 int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64_t stride, int64_t rng_base,
-             hipStream_t s, PnpArgs &a) {
+             hipStream_t s, PnpArgs &a, unsigned long long *best_key = nullptr) {
     a = PnpArgs{};
     a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
     a.offsets = c->d_off;
@@ -254,25 +254,28 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     a.hyp_stride = stride;
     a.rng_base = rng_base;
     a.seed = seed;
-    if (flags & RSAC_F_EXACT_ONLY) {
-        a.exact_only = 1;
-        return RSAC_OK;
-    }
+    a.best_key = best_key;
     const int P = st.P;
     const int64_t N = st.total;
+    HIPCHK(c->queue.ensure(64));
     HIPCHK(c->centred.ensure(sizeof(float) * 3 * std::max<int64_t>(N, 1)));
     HIPCHK(c->bounds_ws.ensure(sizeof(int32_t) * 10 * P));
     HIPCHK(c->frame.ensure(sizeof(double) * kFrameStride * P));
     HIPCHK(c->fconst.ensure(sizeof(float) * kFconstStride * P));
+    a.queue = c->queue.as<int>();
+    a.exact_only = (flags & RSAC_F_EXACT_ONLY) ? 1 : 0;
     float *C = c->centred.as<float>();
     int32_t max_n = 0;
     for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
+    // resets best_key and the queue, then builds the frame (also in exact mode: cheap)
     HIPCHK(launch_pnp_frame(a, P, max_n, c->bounds_ws.as<int32_t>(), C, C + N, C + 2 * N, c->frame.as<double>(),
                             c->fconst.as<float>(), s));
-    a.XC = C; a.YC = C + N; a.ZC = C + 2 * N;
-    a.frame = c->frame.as<double>();
-    a.fconst = c->fconst.as<float>();
-    a.fmodels = c->fmodels.as<float>();
+    if (!a.exact_only) {
+        a.XC = C; a.YC = C + N; a.ZC = C + 2 * N;
+        a.frame = c->frame.as<double>();
+        a.fconst = c->fconst.as<float>();
+        a.fmodels = c->fmodels.as<float>();
+    }
     return RSAC_OK;
 }
 
@@ -612,7 +615,7 @@ void rsac_destroy(rsac_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
-                     &c->frame, &c->fconst,   &c->fmodels};
+                     &c->frame, &c->fconst,   &c->fmodels, &c->queue};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};
@@ -719,15 +722,13 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
     if (r) return r;
     r = ensure_hyp_buffers(c, 1, n_hyps, false);
     if (r) return r;
-    PnpArgs a;
-    r = pnp_args(c, st, flags, seed, n_hyps, hyp_begin, s, a);
-    if (r) return r;
-    const int32_t H = (int32_t)n_hyps;
     // the best key is reduced inside the scoring kernel; only 8 bytes + the
     // winner's record (+ its mask, computed on the device) leave the GPU
     unsigned long long *dkey = (unsigned long long *)c->best.p;
-    a.best_key = dkey;
-    HIPCHK(hipMemsetAsync(dkey, 0, sizeof(unsigned long long), s));
+    PnpArgs a;
+    r = pnp_args(c, st, flags, seed, n_hyps, hyp_begin, s, a, dkey);
+    if (r) return r;
+    const int32_t H = (int32_t)n_hyps;
     HIPCHK(hipEventRecord(c->ev0, s));
     HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
     HIPCHK(hipEventRecord(c->ev1, s));

@@ -38,6 +38,7 @@ struct PnpArgs {
     // optional fused reduction (single problem): max over the scored hypotheses of
     // (count << 32) | (0xFFFFFFFF - low32(rng_base + h)), atomically into *best_key
     unsigned long long *best_key;
+    int *queue;  // work-queue counter of the f32 scoring kernel (reset by launch_pnp_frame)
 };
 
 constexpr int kFrameStride = 8;
@@ -72,8 +73,8 @@ hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t 
 // copy model records rec[p] (<0: zero) into out[p][16]
 hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s);
 
-// frame of every problem (centre, bounds, f32 constants) + centred coords:
-// bounds_ws is a P x 10 int workspace.
+// frame of every problem (centre, bounds, f32 constants) + centred coords;
+// also resets a.best_key (if set) and a.queue.  bounds_ws: P x 10 ints.
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *bounds_ws, float *XC, float *YC,
                             float *ZC, double *frame, float *fconst, hipStream_t s);
 // f32 records for H given f64 models (rsac_score_poses / rsac_pnp_mask)

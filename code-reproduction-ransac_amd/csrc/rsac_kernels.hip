@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "rsac_internal.h"
 #include "rsac_math.h"
 
@@ -132,12 +134,9 @@ __global__ void k_pnp_frame(PnpArgs a, int32_t P, const int *__restrict__ ws, do
     q[4] = (float)T;
     q[5] = (float)(2.002 * thr);
     q[6] = (float)(4e-6 * T + 1e-30);
-    q[7] = (float)thr;
-    q[8] = (float)(2.0 / fx);
-    q[9] = (float)(2.0 / fy);
-    q[10] = (float)(2.5 * kU32);                                            // kc
-    q[11] = (float)(2.5 * kU32 * (fabs(cx) + fabs(cy) + 2.0 * thr + 2.0) + 1e-6);  // kc0
-    q[12] = 0.f;
+    // Cmax >= C_i = 2.5u (|u_i - cx| + |v_i - cy| + |cx| + |cy| + 2 thr + 2), the rounding part of D
+    q[7] = (float)(2.5 * kU32 * (du + dv + fabs(cx) + fabs(cy) + 2.0 * thr + 3.0) + 1e-6);
+    q[8] = q[9] = q[10] = q[11] = q[12] = 0.f;
     for (int k = 13; k < kFconstStride; ++k) q[k] = 0.f;
 }
 
@@ -158,9 +157,9 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, const double *__r
 }
 
 // float32 record of one pose, division-free form of the test:
-//   { -fx R0 -fx R1 -fx R2 | -fy R3 -fy R4 -fy R5 | R6 R7 R8 | -fx t'x -fy t'y t'z | G0 G1 zg 0 }
+//   { -fx R0 -fx R1 -fx R2 | -fy R3 -fy R4 -fy R5 | R6 R7 R8 | -fx t'x -fy t'y t'z | Dz0 0 zg 0 }
 // with t' = R c + t.  ex, ey bound |xs' - fx x|/fx, |ys' - fy y|/fy and ez |z' - z| (camera
-// frame, f32 evaluation vs real numbers); G0 = 1.01 (fx ex + fy ey), G1 = 1.01 ez; zg is the
+// frame, f32 evaluation vs real numbers); Dz0 is the hypothesis' part of D |z|; zg is the
 // depth guard (< 0: no model).
 __device__ __forceinline__ void write_fmodel(const double *R, const double *t, bool valid, const double *frame,
                                              const double *cam, float *fm) {
@@ -183,8 +182,9 @@ __device__ __forceinline__ void write_fmodel(const double *R, const double *t, b
         for (int q = 0; q < 3; ++q) fm[3 * r + q] = (float)(sc[r] * R[3 * r + q]);
         fm[9 + r] = (float)(sc[r] * tp);
     }
-    fm[12] = (float)(1.01 * (fx * eps[0] + fy * eps[1]));
-    fm[13] = (float)(1.01 * eps[2]);
+    // Dz0 = 1.01 (fx ex + fy ey + ez Wmax), Wmax = (fx + fy) wmax >= fx wa_i + fy wb_i of any point
+    fm[12] = (float)(1.01 * (fx * eps[0] + fy * eps[1] + eps[2] * (fx + fy) * wmax));
+    fm[13] = 0.f;
     // |z'| above zg keeps |x'/z' - x/z| <= 0.01 for every projection the bound is used on
     fm[14] = (float)(100.0 * (fmax(eps[0], eps[1]) + wmax * eps[2]) + 2.02 * eps[2] + 1e-30);
     fm[15] = 0.f;
@@ -247,18 +247,26 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 }
 
 // ---------------------------------------------------------------------------
-// PnP scoring, float32 pre-filter + exact fallback (division-free).  Same
-// tiling as the exact kernel below.  Per pair (point i, hypothesis h), with
-// the point centred (XC) and the pixel taken relative to the principal point
-// (uc, vc):
+// PnP scoring, float32 pre-filter + exact fallback (division-free).
+//
+// Work: units of HB consecutive hypotheses of one problem x all its points,
+// pulled from a queue (one atomicAdd per unit) by a grid sized to the
+// resident capacity, so the tail is at most one unit.  The 4 waves of a
+// block split the unit's points in tiles of 64*P; each lane keeps P centred
+// points in registers and runs every hypothesis of the unit over them (the
+// hypothesis' f32 record is wave-uniform: scalar loads, SGPRs).
+//
+// Per pair (point i, hypothesis h), pixel relative to the principal point:
 //   q1 = uc z - fx x,  q2 = vc z - fy y          (= z (u - pu), z (v - pv))
-//   E  = q1^2 + q2^2,  diff = E - T z^2          (sign(diff) = sign(e - T))
-//   Dz = (G0_h + G1_h W_i) + C_i |z|             (D |z|, D: pixel-error bound)
-//   Mz = (2 sqrt(T) |z| + Dz) Dz + 4e-6 T z^2    (M z^2, M: bound on |e' - e|)
+//   diff = q1^2 + q2^2 - T z^2                   (sign(diff) = sign(e - T))
+//   Dz = Dz0_h + Cmax |z|                        (D |z|; D bounds the pixel error
+//                                                 of the f32 evaluation)
+//   Mz = (2 sqrt(T) |z| + Dz) Dz + 4e-6 T z^2    (M z^2; M bounds |e' - e|)
 // |diff| > Mz and |z| > zg_h decide the pair; otherwise the tile is recounted
-// for this hypothesis with the exact f64 error.  Counts are bit-identical to
-// the exact kernel (tests/test_gpu_parity.py: threshold-straddling and
-// behind-camera cases).  Derivation: DESIGN.md "Scoring".
+// for this hypothesis with the exact f64 error (pnp_err, the oracle's
+// formula).  Counts are bit-identical to the exact kernel
+// (tests/test_gpu_parity.py: threshold-straddling and behind-camera cases).
+// Derivation: DESIGN.md "Scoring".
 // ---------------------------------------------------------------------------
 // counts of the block's hypotheses (sum of the 4 waves' partials) and, when
 // a.best_key is set, one atomicMax of the block's best packed key
@@ -285,102 +293,102 @@ __device__ __forceinline__ void pnp_score_epilogue(const PnpArgs &a, const int (
 }
 
 template <int P, int HB>
-__global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_begin, int32_t H,
-                                                       int32_t *__restrict__ counts) {
+__global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
+                                                       int *__restrict__ queue, int32_t *__restrict__ counts) {
     static_assert(HB <= 64, "one lane per hypothesis of the block");
     __shared__ int red[4][HB];
-    const int prob = blockIdx.y;
-    const int64_t p0 = a.offsets[prob];
-    const int n = (int)(a.offsets[prob + 1] - p0);
-    const int64_t h0 = hyp_begin + (int64_t)blockIdx.x * HB;
-    const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+    __shared__ int unit_s;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
-    const float T = fc[4], sqT2 = fc[5], Trel = fc[6];
-    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-    const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
-    const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
-    const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
+    const int units_per_prob = (H + HB - 1) / HB;
+    const int n_units = units_per_prob * n_prob;
+    for (;;) {
+        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
+        __syncthreads();
+        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
+        if (unit >= n_units) break;  // uniform: every wave of every block reaches it
+        const int prob = unit / units_per_prob;
+        const int64_t h0 = hyp_begin + (int64_t)(unit % units_per_prob) * HB;
+        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+        const int64_t p0 = a.offsets[prob];
+        const int n = (int)(a.offsets[prob + 1] - p0);
+        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
+        const float cx = fc[2], cy = fc[3], T = fc[4], sqT2 = fc[5], Trel = fc[6], Cmax = fc[7];
+        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+        const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
+        const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
+        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
 
-    int cnt = 0;
-    for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
-        float px[P], py[P], pz[P], pu[P], pv[P], pw[P], pc[P];
-        {
-            const float fx = fc[0], fy = fc[1], cx = fc[2], cy = fc[3], thr = fc[7], ifx2 = fc[8], ify2 = fc[9];
-            const float kc = fc[10], kc0 = fc[11];
+        int cnt = 0;
+        for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
+            float px[P], py[P], pz[P], pu[P], pv[P];
 #pragma unroll
             for (int j = 0; j < P; ++j) {
                 const int i = base + j * 64 + lane;
                 const bool in = i < n;
                 const int ii = in ? i : 0;
                 px[j] = XC[ii]; py[j] = YC[ii]; pz[j] = ZC[ii];
-                const float uc = U[ii] - cx, vc = V[ii] - cy;
-                const float au = __builtin_fabsf(uc), av = __builtin_fabsf(vc);
-                const float wa = __builtin_fmaf(au + thr, ifx2, 1e-3f);
-                const float wb = __builtin_fmaf(av + thr, ify2, 1e-3f);
-                pw[j] = __builtin_fmaf(fx, wa, fy * wb);
-                pc[j] = __builtin_fmaf(kc, au + av, kc0);
                 // out-of-range lanes: a pixel at 3e38 makes the pair a decided outlier
-                pu[j] = in ? uc : 3.0e38f;
-                pv[j] = in ? vc : 3.0e38f;
+                pu[j] = in ? U[ii] - cx : 3.0e38f;
+                pv[j] = in ? V[ii] - cy : 3.0e38f;
             }
-        }
-        for (int h = 0; h < nh; ++h) {
-            const float *__restrict__ m = fmb + h * kFModelStride;
-            const float zg = m[14];
-            if (zg < 0.f) continue;
-            const float r0 = m[0], r1 = m[1], r2 = m[2], r3 = m[3], r4 = m[4], r5 = m[5], r6 = m[6], r7 = m[7],
-                        r8 = m[8], t0 = m[9], t1 = m[10], t2 = m[11], G0 = m[12], G1 = m[13];
-            int cc = 0;
-            uint64_t und = 0;
+            for (int h = 0; h < nh; ++h) {
+                const float *__restrict__ m = fmb + h * kFModelStride;
+                const float zg = m[14];
+                if (zg < 0.f) continue;
+                const float r0 = m[0], r1 = m[1], r2 = m[2], r3 = m[3], r4 = m[4], r5 = m[5], r6 = m[6], r7 = m[7],
+                            r8 = m[8], t0 = m[9], t1 = m[10], t2 = m[11], Dz0 = m[12];
+                int cc = 0;
+                uint64_t und = 0;
 #pragma unroll
-            for (int j = 0; j < P; ++j) {
-                const float xs = __builtin_fmaf(r0, px[j], __builtin_fmaf(r1, py[j], __builtin_fmaf(r2, pz[j], t0)));
-                const float ys = __builtin_fmaf(r3, px[j], __builtin_fmaf(r4, py[j], __builtin_fmaf(r5, pz[j], t1)));
-                const float z = __builtin_fmaf(r6, px[j], __builtin_fmaf(r7, py[j], __builtin_fmaf(r8, pz[j], t2)));
-                const float q1 = __builtin_fmaf(pu[j], z, xs);
-                const float q2 = __builtin_fmaf(pv[j], z, ys);
-                const float z2 = z * z;
-                const float diff = __builtin_fmaf(-T, z2, __builtin_fmaf(q1, q1, q2 * q2));
-                const float az = __builtin_fabsf(z);
-                const float Dz = __builtin_fmaf(pc[j], az, __builtin_fmaf(G1, pw[j], G0));
-                const float Mz = __builtin_fmaf(__builtin_fmaf(sqT2, az, Dz), Dz, Trel * z2);
-                // one v_cmp per mask; a NaN anywhere leaves the pair undecided
-                const uint64_t mz = __ballot(az > zg);
-                const uint64_t mi = __ballot(diff < -Mz);
-                const uint64_t mo = __ballot(diff > Mz);
-                cc += __popcll(mi & mz);
-                und |= ~((mi | mo) & mz);
-            }
-            if (und) {
-                // Some pair of this tile is undecided: recount the whole tile for this
-                // hypothesis with the exact f64 error (pnp_err, the oracle's formula).
-                // Rare; operands are re-read from memory so no register array is
-                // indexed and the f64 code does not raise the kernel's VGPR budget.
-                const double *md = a.models + (rec0 + h) * kModelStride;
-                const double *cm = a.cams + 4 * prob;
-                const Cam k{cm[0], cm[1], cm[2], cm[3]};
-                const float thr2 = a.thr2[prob];
-                cc = 0;
-#pragma unroll 1
                 for (int j = 0; j < P; ++j) {
-                    const int i = base + j * 64 + lane;
-                    bool ex = false;
-                    if (i < n) {
-                        const int64_t q = p0 + i;
-                        ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <=
-                             thr2;
-                    }
-                    cc += __popcll(__ballot(ex));
+                    const float xs = __builtin_fmaf(r0, px[j], __builtin_fmaf(r1, py[j], __builtin_fmaf(r2, pz[j], t0)));
+                    const float ys = __builtin_fmaf(r3, px[j], __builtin_fmaf(r4, py[j], __builtin_fmaf(r5, pz[j], t1)));
+                    const float z = __builtin_fmaf(r6, px[j], __builtin_fmaf(r7, py[j], __builtin_fmaf(r8, pz[j], t2)));
+                    const float q1 = __builtin_fmaf(pu[j], z, xs);
+                    const float q2 = __builtin_fmaf(pv[j], z, ys);
+                    const float z2 = z * z;
+                    const float diff = __builtin_fmaf(-T, z2, __builtin_fmaf(q1, q1, q2 * q2));
+                    const float az = __builtin_fabsf(z);
+                    const float Dz = __builtin_fmaf(Cmax, az, Dz0);
+                    const float Mz = __builtin_fmaf(__builtin_fmaf(sqT2, az, Dz), Dz, Trel * z2);
+                    // one v_cmp per mask; a NaN anywhere leaves the pair undecided
+                    const uint64_t mz = __ballot(az > zg);
+                    const uint64_t mi = __ballot(diff < -Mz);
+                    const uint64_t mo = __ballot(diff > Mz);
+                    cc += __popcll(mi & mz);
+                    und |= ~((mi | mo) & mz);
                 }
+                if (und) {
+                    // Some pair of this tile is undecided: recount the tile for this
+                    // hypothesis with the exact f64 error.  Rare; operands are re-read
+                    // from memory so no register array is indexed and the f64 code does
+                    // not raise the kernel's VGPR budget.
+                    const double *md = a.models + (rec0 + h) * kModelStride;
+                    const double *cm = a.cams + 4 * prob;
+                    const Cam k{cm[0], cm[1], cm[2], cm[3]};
+                    const float thr2 = a.thr2[prob];
+                    cc = 0;
+#pragma unroll 1
+                    for (int j = 0; j < P; ++j) {
+                        const int i = base + j * 64 + lane;
+                        bool ex = false;
+                        if (i < n) {
+                            const int64_t q = p0 + i;
+                            ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q],
+                                         a.V[q]) <= thr2;
+                        }
+                        cc += __popcll(__ballot(ex));
+                    }
+                }
+                cnt += (lane == h) ? cc : 0;
             }
-            cnt += (lane == h) ? cc : 0;
         }
+        if (lane < HB) red[wave][lane] = cnt;
+        __syncthreads();
+        if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
+        __syncthreads();  // red and unit_s are rewritten by the next unit
     }
-    if (lane < HB) red[wave][lane] = cnt;
-    __syncthreads();
-    if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
 }
 
 // ---------------------------------------------------------------------------
@@ -477,6 +485,16 @@ __global__ void k_pnp_mask_key(PnpArgs a, int32_t n, const unsigned long long *_
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
         mask[i] = m ? (pnp_err(m, m + 9, cam, (double)a.X[i], (double)a.Y[i], (double)a.Z[i], a.U[i], a.V[i]) <= thr2)
                     : 0;
+}
+
+// per-call state reset in one launch: bounds sentinels, best key, work-queue counter
+__global__ void k_pnp_init(int32_t P, int *__restrict__ ws, unsigned long long *__restrict__ key,
+                           int *__restrict__ queue) {
+    for (int i = threadIdx.x; i < 10 * P; i += blockDim.x) ws[i] = i < 5 * P ? 0x7F7F7F7F : (int)0x80808080;
+    if (threadIdx.x == 0) {
+        if (key) *key = 0ull;
+        *queue = 0;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -662,10 +680,7 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
                             double *frame, float *fconst, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ws, 0x7F, sizeof(int32_t) * 5 * P, s);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(ws + 5 * P, 0x80, sizeof(int32_t) * 5 * P, s);
-    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pnp_init, dim3(1), dim3(256), 0, s, P, ws, a.best_key, a.queue);
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 2048);
     if (g > 32) g = 32;
     hipLaunchKernelGGL(k_pnp_bounds, dim3(g, P), dim3(256), 0, s, a, P, ws);
@@ -692,7 +707,17 @@ void set_score_variant(int v) { g_score_variant = v; }
 
 template <int PP, int HB>
 static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
-    hipLaunchKernelGGL((k_pnp_score_f32<PP, HB>), dim3(cdiv(H, HB), P), dim3(256), 0, s, a, hyp_begin, H, counts);
+    static int resident = 0;  // blocks the whole GPU keeps resident for this instantiation
+    if (resident == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pnp_score_f32<PP, HB>, 256, 0);
+        resident = std::max(1, cus) * std::max(1, per_cu);
+    }
+    const int64_t units = (int64_t)P * ((H + HB - 1) / HB);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
+    hipLaunchKernelGGL((k_pnp_score_f32<PP, HB>), dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, a.queue, counts);
 }
 
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
