@@ -296,8 +296,10 @@ template <int P, int HB>
 __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
                                                        int *__restrict__ queue, int32_t *__restrict__ counts) {
     static_assert(HB <= 64, "one lane per hypothesis of the block");
+    static_assert(HB * kFModelStride % 256 == 0 || HB * kFModelStride < 256, "model staging");
     __shared__ int red[4][HB];
     __shared__ int unit_s;
+    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];  // the unit's f32 records
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int units_per_prob = (H + HB - 1) / HB;
@@ -315,7 +317,14 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
         const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
         const float cx = fc[2], cy = fc[3], T = fc[4], sqT2 = fc[5], Trel = fc[6], Cmax = fc[7];
         const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-        const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
+        {
+            // stage the unit's records in LDS: every wave then reads a record with
+            // broadcast ds_reads instead of a global-latency load per hypothesis
+            const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
+            for (int q = threadIdx.x; q < HB * kFModelStride; q += 256)
+                mlds[q] = q < nh * kFModelStride ? fmb[q] : -1.f;
+        }
+        __syncthreads();
         const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
         const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
 
@@ -333,11 +342,12 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
                 pv[j] = in ? V[ii] - cy : 3.0e38f;
             }
             for (int h = 0; h < nh; ++h) {
-                const float *__restrict__ m = fmb + h * kFModelStride;
-                const float zg = m[14];
+                const float4 *m4 = reinterpret_cast<const float4 *>(mlds + h * kFModelStride);
+                const float4 ma = m4[0], mb = m4[1], mc = m4[2], md4 = m4[3];
+                const float zg = md4.z;
                 if (zg < 0.f) continue;
-                const float r0 = m[0], r1 = m[1], r2 = m[2], r3 = m[3], r4 = m[4], r5 = m[5], r6 = m[6], r7 = m[7],
-                            r8 = m[8], t0 = m[9], t1 = m[10], t2 = m[11], Dz0 = m[12];
+                const float r0 = ma.x, r1 = ma.y, r2 = ma.z, r3 = ma.w, r4 = mb.x, r5 = mb.y, r6 = mb.z, r7 = mb.w,
+                            r8 = mc.x, t0 = mc.y, t1 = mc.z, t2 = mc.w, Dz0 = md4.x;
                 int cc = 0;
                 uint64_t und = 0;
 #pragma unroll
