@@ -401,6 +401,121 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
     }
 }
 
+// Packed variant of k_pnp_score_f32: the same arithmetic, bit for bit, on two
+// points per instruction (v_pk_fma_f32 / v_pk_mul_f32: two f32 lanes per VGPR
+// pair).  Each lane holds P points as P/2 pairs.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 bc(float v) { return f2{v, v}; }
+
+template <int P, int HB>
+__global__ __launch_bounds__(256) void k_pnp_score_pk(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
+                                                      int *__restrict__ queue, int32_t *__restrict__ counts) {
+    static_assert(HB <= 64 && P % 2 == 0, "tiling");
+    constexpr int Q = P / 2;
+    __shared__ int red[4][HB];
+    __shared__ int unit_s;
+    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int units_per_prob = (H + HB - 1) / HB;
+    const int n_units = units_per_prob * n_prob;
+    for (;;) {
+        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
+        __syncthreads();
+        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
+        if (unit >= n_units) break;
+        const int prob = unit / units_per_prob;
+        const int64_t h0 = hyp_begin + (int64_t)(unit % units_per_prob) * HB;
+        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+        const int64_t p0 = a.offsets[prob];
+        const int n = (int)(a.offsets[prob + 1] - p0);
+        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
+        const float cx = fc[2], cy = fc[3], T = fc[4], sqT2 = fc[5], Trel = fc[6], Cmax = fc[7];
+        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+        {
+            const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
+            for (int q = threadIdx.x; q < HB * kFModelStride; q += 256)
+                mlds[q] = q < nh * kFModelStride ? fmb[q] : -1.f;
+        }
+        __syncthreads();
+        const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
+        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
+
+        int cnt = 0;
+        for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
+            f2 px[Q], py[Q], pz[Q], pu[Q], pv[Q];
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const int i = base + j * 64 + lane;
+                const bool in = i < n;
+                const int ii = in ? i : 0;
+                const float u = in ? U[ii] - cx : 3.0e38f, v = in ? V[ii] - cy : 3.0e38f;
+                if (j < Q) {
+                    px[j].x = XC[ii]; py[j].x = YC[ii]; pz[j].x = ZC[ii]; pu[j].x = u; pv[j].x = v;
+                } else {
+                    px[j - Q].y = XC[ii]; py[j - Q].y = YC[ii]; pz[j - Q].y = ZC[ii]; pu[j - Q].y = u;
+                    pv[j - Q].y = v;
+                }
+            }
+            for (int h = 0; h < nh; ++h) {
+                const float4 *m4 = reinterpret_cast<const float4 *>(mlds + h * kFModelStride);
+                const float4 ma = m4[0], mb = m4[1], mc = m4[2], md4 = m4[3];
+                const float zg = md4.z;
+                if (zg < 0.f) continue;
+                int cc = 0;
+                uint64_t und = 0;
+#pragma unroll
+                for (int j = 0; j < Q; ++j) {
+                    const f2 xs = pfma(bc(ma.x), px[j], pfma(bc(ma.y), py[j], pfma(bc(ma.z), pz[j], bc(mc.y))));
+                    const f2 ys = pfma(bc(ma.w), px[j], pfma(bc(mb.x), py[j], pfma(bc(mb.y), pz[j], bc(mc.z))));
+                    const f2 z = pfma(bc(mb.z), px[j], pfma(bc(mb.w), py[j], pfma(bc(mc.x), pz[j], bc(mc.w))));
+                    const f2 q1 = pfma(pu[j], z, xs);
+                    const f2 q2 = pfma(pv[j], z, ys);
+                    const f2 z2 = z * z;
+                    const f2 diff = pfma(bc(-T), z2, pfma(q1, q1, q2 * q2));
+                    const f2 az = f2{__builtin_fabsf(z.x), __builtin_fabsf(z.y)};
+                    const f2 Dz = pfma(bc(Cmax), az, bc(md4.x));
+                    const f2 Mz = pfma(pfma(bc(sqT2), az, Dz), Dz, bc(Trel) * z2);
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const float d = hh ? diff.y : diff.x, mzv = hh ? Mz.y : Mz.x, azv = hh ? az.y : az.x;
+                        const uint64_t mz = __ballot(azv > zg);
+                        const uint64_t mi = __ballot(d < -mzv);
+                        const uint64_t mo = __ballot(d > mzv);
+                        cc += __popcll(mi & mz);
+                        und |= ~((mi | mo) & mz);
+                    }
+                }
+                if (und) {
+                    const double *md = a.models + (rec0 + h) * kModelStride;
+                    const double *cm = a.cams + 4 * prob;
+                    const Cam k{cm[0], cm[1], cm[2], cm[3]};
+                    const float thr2 = a.thr2[prob];
+                    cc = 0;
+#pragma unroll 1
+                    for (int j = 0; j < P; ++j) {
+                        const int i = base + j * 64 + lane;
+                        bool ex = false;
+                        if (i < n) {
+                            const int64_t q = p0 + i;
+                            ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q],
+                                         a.V[q]) <= thr2;
+                        }
+                        cc += __popcll(__ballot(ex));
+                    }
+                }
+                cnt += (lane == h) ? cc : 0;
+            }
+        }
+        if (lane < HB) red[wave][lane] = cnt;
+        __syncthreads();
+        if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // PnP scoring.  Block = 4 waves; a block owns HB consecutive hypotheses of
 // one problem, its waves split that problem's points (tiles of 64*P per
@@ -666,6 +781,7 @@ __global__ void k_key_model(const double *__restrict__ models, const unsigned lo
 // launchers
 // ---------------------------------------------------------------------------
 static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+static_assert(true, "");
 
 constexpr int kScoreP = 8;
 constexpr int kScoreHB = 32;
@@ -715,19 +831,20 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 static int g_score_variant = 0;
 void set_score_variant(int v) { g_score_variant = v; }
 
-template <int PP, int HB>
+template <int PP, int HB, bool PK = false>
 static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
+    auto kern = PK ? k_pnp_score_pk<PP, HB> : k_pnp_score_f32<PP, HB>;
     static int resident = 0;  // blocks the whole GPU keeps resident for this instantiation
     if (resident == 0) {
         int dev = 0, cus = 0, per_cu = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pnp_score_f32<PP, HB>, 256, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
         resident = std::max(1, cus) * std::max(1, per_cu);
     }
     const int64_t units = (int64_t)P * ((H + HB - 1) / HB);
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
-    hipLaunchKernelGGL((k_pnp_score_f32<PP, HB>), dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, a.queue, counts);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, a.queue, counts);
 }
 
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
@@ -740,6 +857,10 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 4: launch_f32<6, 32>(a, P, hyp_begin, H, counts, s); break;
             case 5: launch_f32<8, 16>(a, P, hyp_begin, H, counts, s); break;
             case 6: launch_f32<4, 64>(a, P, hyp_begin, H, counts, s); break;
+            case 7: launch_f32<4, 32, true>(a, P, hyp_begin, H, counts, s); break;
+            case 8: launch_f32<8, 32, true>(a, P, hyp_begin, H, counts, s); break;
+            case 9: launch_f32<4, 16, true>(a, P, hyp_begin, H, counts, s); break;
+            case 10: launch_f32<6, 32, true>(a, P, hyp_begin, H, counts, s); break;
             default: launch_f32<kScoreP, kScoreHB>(a, P, hyp_begin, H, counts, s); break;
         }
     } else
