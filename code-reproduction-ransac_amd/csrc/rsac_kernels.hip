@@ -157,12 +157,12 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, const double *__r
 }
 
 // float32 record of one pose, division-free form of the test:
-//   { -fx R0 -fx R1 -fx R2 | -fy R3 -fy R4 -fy R5 | R6 R7 R8 | -fx t'x -fy t'y t'z | Dz0 0 zg 0 }
+//   { -fx R0 -fx R1 -fx R2 | -fy R3 -fy R4 -fy R5 | R6 R7 R8 | -fx t'x -fy t'y t'z | Dz0 beta zg alpha }
 // with t' = R c + t.  ex, ey bound |xs' - fx x|/fx, |ys' - fy y|/fy and ez |z' - z| (camera
 // frame, f32 evaluation vs real numbers); Dz0 is the hypothesis' part of D |z|; zg is the
 // depth guard (< 0: no model).
 __device__ __forceinline__ void write_fmodel(const double *R, const double *t, bool valid, const double *frame,
-                                             const double *cam, float *fm) {
+                                             const double *cam, const float *fconst, float *fm) {
     if (!valid) {
 #pragma unroll
         for (int q = 0; q < kFModelStride; ++q) fm[q] = 0.f;
@@ -183,11 +183,17 @@ __device__ __forceinline__ void write_fmodel(const double *R, const double *t, b
         fm[9 + r] = (float)(sc[r] * tp);
     }
     // Dz0 = 1.01 (fx ex + fy ey + ez Wmax), Wmax = (fx + fy) wmax >= fx wa_i + fy wb_i of any point
-    fm[12] = (float)(1.01 * (fx * eps[0] + fy * eps[1] + eps[2] * (fx + fy) * wmax));
-    fm[13] = 0.f;
+    const double D0 = 1.01 * (fx * eps[0] + fy * eps[1] + eps[2] * (fx + fy) * wmax);
+    fm[12] = (float)(D0 * (1.0 + 1e-6));
     // |z'| above zg keeps |x'/z' - x/z| <= 0.01 for every projection the bound is used on
     fm[14] = (float)(100.0 * (fmax(eps[0], eps[1]) + wmax * eps[2]) + 2.02 * eps[2] + 1e-30);
-    fm[15] = 0.f;
+    // Mz = (sqT2 |z| + Dz) Dz + Trel z^2 with Dz = D0 + Cmax |z| is at most alpha z^2 + beta:
+    // |z| <= z^2 / (2w) + w / 2 for any w > 0 (taken as the hypothesis' depth of the centre).
+    const double sqT2 = fconst[5], Trel = fconst[6], Cmax = fconst[7];
+    const double Bc = sqT2 * D0 + 2.0 * D0 * Cmax;
+    const double w = fmax(fabs((double)fm[11]), 1.0);
+    fm[13] = (float)(1.01 * (D0 * D0 + Bc * w * 0.5));                                // beta
+    fm[15] = (float)(1.01 * (sqT2 * Cmax + Cmax * Cmax + Trel + Bc / (2.0 * w)));    // alpha
 }
 
 __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
@@ -197,7 +203,7 @@ __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
     const double *m = a.models + rec * kModelStride;
     write_fmodel(m, m + 9, m[kValidSlot] != 0.0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                 a.fmodels + rec * kFModelStride);
+                 a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride);
 }
 
 // ---------------------------------------------------------------------------
@@ -243,7 +249,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     a.status[rec] = st;
     if (a.fmodels)
         write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                     a.fmodels + rec * kFModelStride);
+                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride);
 }
 
 // ---------------------------------------------------------------------------
@@ -513,6 +519,163 @@ __global__ __launch_bounds__(256) void k_pnp_score_pk(PnpArgs a, int64_t hyp_beg
         __syncthreads();
         if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
         __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// PnP scoring on the matrix cores.  The camera-frame coordinates of 4
+// hypotheses x 16 points are one v_mfma_f32_16x16x4_f32:
+//   A (16 x 4): rows 4g + i (hypothesis g of the set, i = xs, ys, z, pad),
+//               columns the scaled rotation coefficients of X, Y, Z (4th = 0)
+//   B (4 x 16): X, Y, Z, 0 of 16 centred points        (one VGPR per lane)
+//   C (16 x 16): the translations t' (row i of hypothesis g)
+// so lane l receives xs, ys, z of hypothesis l >> 4 and point l & 15, as an
+// exact f32 fma chain (cdna_hip_programming.md §3), inside the same error
+// bound as the VALU kernels.  The VALU then forms
+//   E = (uc z + xs)^2 + (vc z + ys)^2                 (= z^2 e')
+// and decides E < (T - alpha) z^2 - beta (inlier) or E > (T + alpha) z^2 + beta
+// (outlier), alpha z^2 + beta >= Mz of k_pnp_score_f32; everything else goes
+// to the exact f64 error, lane by lane.  Matrix and vector pipes run side by
+// side.  Counts are bit-identical to the exact kernel.
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int HB, int TC>
+__global__ __launch_bounds__(256) void k_pnp_score_mfma(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
+                                                        int *__restrict__ queue, int32_t *__restrict__ counts) {
+    static_assert(HB % 4 == 0 && HB <= 64, "sets of 4 hypotheses");
+    constexpr int S = HB / 4;
+    __shared__ int red[4][HB];
+    __shared__ int unit_s;
+    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
+    __shared__ int xcnt[HB];  // inliers found by the exact fallback
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, col = lane & 15;
+    if (threadIdx.x < HB) xcnt[threadIdx.x] = 0;
+    const int units_per_prob = (H + HB - 1) / HB;
+    const int n_units = units_per_prob * n_prob;
+    for (;;) {
+        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
+        __syncthreads();
+        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
+        if (unit >= n_units) break;  // uniform: every wave of every block reaches it
+        const int prob = unit / units_per_prob;
+        const int64_t h0 = hyp_begin + (int64_t)(unit % units_per_prob) * HB;
+        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+        const int64_t p0 = a.offsets[prob];
+        const int n = (int)(a.offsets[prob + 1] - p0);
+        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
+        const float cx = fc[2], cy = fc[3], T = fc[4];
+        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+        {
+            const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
+            for (int q = threadIdx.x; q < HB * kFModelStride; q += 256) {
+                const int hq = q / kFModelStride, fq = q % kFModelStride;
+                mlds[q] = hq < nh ? fmb[q] : (fq == 14 ? -1.f : 0.f);
+            }
+        }
+        __syncthreads();
+        // per set s: the A operand, the C operand and the decision constants of
+        // hypothesis 4s + g (this lane's output rows)
+        float Aop[S], tlo[S], thi[S], bet[S], zgs[S];
+        f32x4 Cop[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const float *ma = mlds + (4 * s + (col >> 2)) * kFModelStride;
+            const int i = col & 3;
+            Aop[s] = (i < 3 && g < 3) ? ma[3 * i + g] : 0.f;
+            const float *mc = mlds + (4 * s + g) * kFModelStride;
+            const bool valid = mc[14] >= 0.f;
+            // an absent/invalid hypothesis (zero record): z = 1, thresholds -inf, so
+            // every pair is a decided outlier
+            Cop[s] = valid ? f32x4{mc[9], mc[10], mc[11], 0.f} : f32x4{0.f, 0.f, 1.f, 0.f};
+            tlo[s] = valid ? T - mc[15] : -__builtin_inff();
+            thi[s] = valid ? T + mc[15] : -__builtin_inff();
+            bet[s] = valid ? mc[13] : 0.f;
+            zgs[s] = valid ? mc[14] : -1.f;
+        }
+        const float *__restrict__ Pk = g == 0 ? a.XC + p0 : g == 1 ? a.YC + p0 : a.ZC + p0;
+        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
+
+        int cnt[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) cnt[s] = 0;
+        for (int base = wave * 16 * TC; base < n; base += 4 * 16 * TC) {
+            static_assert(S * TC <= 32, "undecided bits");
+            uint32_t und = 0;
+            float Bop[TC], uc[TC], vc[TC];
+#pragma unroll
+            for (int t = 0; t < TC; ++t) {
+                const int pt = base + t * 16 + col;
+                const bool in = pt < n;
+                const int pp = in ? pt : 0;
+                const float b = Pk[pp];
+                Bop[t] = (in && g < 3) ? b : 0.f;
+                // out-of-range points: a pixel at 3e38 makes every pair a decided outlier
+                uc[t] = in ? U[pp] - cx : 3.0e38f;
+                vc[t] = in ? V[pp] - cy : 3.0e38f;
+            }
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+#pragma unroll
+                for (int t = 0; t < TC; ++t) {
+                    const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(Aop[s], Bop[t], Cop[s], 0, 0, 0);
+                    const float z = d[2];
+                    const float q1 = __builtin_fmaf(uc[t], z, d[0]);
+                    const float q2 = __builtin_fmaf(vc[t], z, d[1]);
+                    const float z2 = z * z;
+                    const float E = __builtin_fmaf(q1, q1, q2 * q2);
+                    const float lo = __builtin_fmaf(tlo[s], z2, -bet[s]);
+                    const float hi = __builtin_fmaf(thi[s], z2, bet[s]);
+                    // a NaN anywhere leaves the pair undecided (and not a decided inlier)
+                    const bool zok = __builtin_fabsf(z) > zgs[s];
+                    cnt[s] += (zok && E < lo) ? 1 : 0;
+                    const bool dec = zok && (E < lo || E > hi);
+                    und |= dec ? 0u : (1u << (s * TC + t));
+                }
+            }
+            if (__ballot(und != 0)) {
+                // rare: the exact f64 error (pnp_err, the oracle's formula) of the
+                // undecided pairs, one rolled loop for all of them
+                const double *cm = a.cams + 4 * prob;
+                const Cam k{cm[0], cm[1], cm[2], cm[3]};
+#pragma unroll 1
+                while (und) {
+                    const int b = __builtin_ctz(und);
+                    und &= und - 1;
+                    const int hs = 4 * (b / TC) + g;
+                    const int pt = base + (b % TC) * 16 + col;
+                    if (pt < n && hs < nh) {
+                        const double *md = a.models + (rec0 + hs) * kModelStride;
+                        const int64_t q = p0 + pt;
+                        if (md[kValidSlot] != 0.0 &&
+                            pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <=
+                                a.thr2[prob])
+                            atomicAdd(&xcnt[hs], 1);
+                    }
+                }
+            }
+        }
+        // counts of hypothesis 4s + g: sum over the 16 lanes of group g, then over waves
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            int v = cnt[s];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            if (col == 0) red[wave][4 * s + g] = v;
+        }
+        __syncthreads();  // also orders every wave's fallback atomics before xcnt is read
+        if (wave == 0) {
+            if (lane < HB) {
+                red[0][lane] += xcnt[lane];
+                xcnt[lane] = 0;
+            }
+            pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
+        }
+        __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
     }
 }
 
@@ -828,12 +991,17 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
-static int g_score_variant = 0;
-void set_score_variant(int v) { g_score_variant = v; }
+constexpr int kDefaultScoreVariant = 1;  // fastest measured on MI355X
+static int g_score_variant = kDefaultScoreVariant;
+void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
 
-template <int PP, int HB, bool PK = false>
+template <int PP, int HB, int KIND = 0>  // KIND 0 VALU f32, 1 packed f32, 2 MFMA (PP = point chunks of 16)
 static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
-    auto kern = PK ? k_pnp_score_pk<PP, HB> : k_pnp_score_f32<PP, HB>;
+    auto kern = [] {
+        if constexpr (KIND == 2) return k_pnp_score_mfma<HB, PP>;
+        else if constexpr (KIND == 1) return k_pnp_score_pk<PP, HB>;
+        else return k_pnp_score_f32<PP, HB>;
+    }();
     static int resident = 0;  // blocks the whole GPU keeps resident for this instantiation
     if (resident == 0) {
         int dev = 0, cus = 0, per_cu = 0;
@@ -857,10 +1025,15 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 4: launch_f32<6, 32>(a, P, hyp_begin, H, counts, s); break;
             case 5: launch_f32<8, 16>(a, P, hyp_begin, H, counts, s); break;
             case 6: launch_f32<4, 64>(a, P, hyp_begin, H, counts, s); break;
-            case 7: launch_f32<4, 32, true>(a, P, hyp_begin, H, counts, s); break;
-            case 8: launch_f32<8, 32, true>(a, P, hyp_begin, H, counts, s); break;
-            case 9: launch_f32<4, 16, true>(a, P, hyp_begin, H, counts, s); break;
-            case 10: launch_f32<6, 32, true>(a, P, hyp_begin, H, counts, s); break;
+            case 7: launch_f32<4, 32, 1>(a, P, hyp_begin, H, counts, s); break;
+            case 8: launch_f32<8, 32, 1>(a, P, hyp_begin, H, counts, s); break;
+            case 9: launch_f32<4, 16, 1>(a, P, hyp_begin, H, counts, s); break;
+            case 10: launch_f32<6, 32, 1>(a, P, hyp_begin, H, counts, s); break;
+            case 11: launch_f32<4, 16, 2>(a, P, hyp_begin, H, counts, s); break;
+            case 12: launch_f32<2, 16, 2>(a, P, hyp_begin, H, counts, s); break;
+            case 13: launch_f32<4, 32, 2>(a, P, hyp_begin, H, counts, s); break;
+            case 14: launch_f32<8, 16, 2>(a, P, hyp_begin, H, counts, s); break;
+            case 15: launch_f32<2, 32, 2>(a, P, hyp_begin, H, counts, s); break;
             default: launch_f32<kScoreP, kScoreHB>(a, P, hyp_begin, H, counts, s); break;
         }
     } else

@@ -86,8 +86,9 @@ RSAC_EXPORT const char *rsac_last_error(void);
 RSAC_EXPORT int rsac_abi_version(void);
 RSAC_EXPORT int rsac_device_count(void);
 RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
-/* tuning knob: PnP scoring-kernel tiling (0 default; 1..6 alternative points-per-lane x
- * hypotheses-per-block instantiations, process-wide).  Results never depend on it. */
+/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default;
+ * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 MFMA tilings).  Counts,
+ * masks and models never depend on it. */
 RSAC_EXPORT int rsac_set_score_variant(int variant);
 
 /* cv2.solvePnPRansac (main_v1.py:497).  K: 3x3 row-major f64.  Minimal

@@ -1,0 +1,79 @@
+"""Turn rocprofv3 outputs under gpurun_out/prof into the committed summaries under profiles/.
+
+    python scripts/summarize_profiles.py TAG [--points 10000 --hyps 100000]
+
+Writes
+  profiles/TAG_kernel_stats.csv      -- the --kernel-trace --stats summary of the bench command
+  profiles/TAG_summary.md            -- per-kernel table + the scoring kernel's average duration
+  profiles/pmc_score_kernel.json     -- HBM bytes per scoring launch (FETCH_SIZE x 2 per
+                                        MI355X_MICROARCH.md "HBM", + WRITE_SIZE), read by bench.py
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import shutil
+import statistics
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "gpurun_out", "prof")
+OUT = os.path.join(ROOT, "profiles")
+SCORE = "k_pnp_score"
+
+
+def counter(path, name):
+    vals = []
+    if not os.path.exists(path):
+        return None
+    for row in csv.DictReader(open(path)):
+        if SCORE in row["Kernel_Name"] and row["Counter_Name"] == name:
+            vals.append(float(row["Counter_Value"]))
+    return vals or None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--points", type=int, default=10_000)
+    ap.add_argument("--hyps", type=int, default=100_000)
+    args = ap.parse_args()
+    os.makedirs(OUT, exist_ok=True)
+    stats = os.path.join(PROF, "kt", "run_kernel_stats.csv")
+    dst = os.path.join(OUT, f"{args.tag}_kernel_stats.csv")
+    shutil.copyfile(stats, dst)
+    rows = list(csv.DictReader(open(stats)))
+    lines = [f"# rocprofv3 --kernel-trace --stats, `python3 bench.py --steps 10 --warmup 3` ({args.tag})", "",
+             "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
+    score_avg = None
+    for r in rows:
+        lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
+                     f"{float(r['Percentage']):.2f} |")
+        if SCORE in r["Name"] and score_avg is None:
+            score_avg = float(r["AverageNs"]) / 1e3
+    fetch = counter(os.path.join(PROF, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = counter(os.path.join(PROF, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    algo = args.points * 20 * args.hyps
+    pmc = None
+    if fetch:
+        fk = statistics.median(fetch)
+        wk = statistics.median(write) if write else 0.0
+        hbm = (2.0 * fk + wk) * 1024.0  # counters in KiB; FETCH_SIZE reads half on gfx950
+        pmc = {"kernel": SCORE, "points": args.points, "hyps": args.hyps, "fetch_size_kib": fk,
+               "write_size_kib": wk, "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": algo,
+               "launches": len(fetch),
+               "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (HBM); the 200 kB point set is re-read "
+                       "from L2/MALL by every hypothesis, so HBM traffic is far below the algorithmic bytes"}
+        json.dump(pmc, open(os.path.join(OUT, "pmc_score_kernel.json"), "w"), indent=1)
+    lines += ["", f"scoring kernel average: {score_avg:.1f} us" if score_avg else "scoring kernel not found"]
+    if pmc:
+        lines += [f"scoring kernel HBM bytes/launch (PMC): {pmc['hbm_bytes_per_launch'] / 1e6:.2f} MB "
+                  f"(FETCH_SIZE {pmc['fetch_size_kib']:.0f} KiB x2 + WRITE_SIZE {pmc['write_size_kib']:.0f} KiB); "
+                  f"algorithmic {algo / 1e9:.1f} GB"]
+    open(os.path.join(OUT, f"{args.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()

@@ -243,10 +243,22 @@ def test_degenerate_inputs():
 
 
 # ---------------------------------------------------------------------------------------------
-# float32 pre-filter: must never change a decision (DESIGN.md "Scoring")
+# float32 pre-filter: must never change a decision (DESIGN.md "Scoring").  Every scoring-kernel
+# variant (VALU f32, packed f32, MFMA) is checked, then the default is restored.
 # ---------------------------------------------------------------------------------------------
+SCORE_VARIANTS = [0, 1, 7, 11, 12, 13, 14, 15]
+
+
+@pytest.fixture(params=SCORE_VARIANTS)
+def score_variant(request):
+    from rsac import _lib as L
+    L.check(L.lib().rsac_set_score_variant(request.param))
+    yield request.param
+    L.check(L.lib().rsac_set_score_variant(-1))
+
+
 @pytest.mark.parametrize("n,seed", [(10000, 0), (4097, 3), (777, 9)])
-def test_f32_prefilter_equals_exact_kernel(n, seed):
+def test_f32_prefilter_equals_exact_kernel(n, seed, score_variant):
     pr, soa, cam = _pnp_case(n, 0.5, seed)
     st_f, c_f, _ = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, 20000, 30.0)
     st_e, c_e, _ = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, 20000, 30.0, exact_only=True)
@@ -274,7 +286,7 @@ def _boundary_case(seed, n=6000, thr=30.0):
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_f32_prefilter_threshold_boundary(seed):
+def test_f32_prefilter_threshold_boundary(seed, score_variant):
     P3, P2, K, pose = _boundary_case(seed)
     soa = O.soa_pnp(P3, P2)
     cam = O.cam_from_K(K)
@@ -293,7 +305,7 @@ def test_f32_prefilter_threshold_boundary(seed):
     assert 0 < ref[0] < len(P3)  # the construction really straddles the threshold
 
 
-def test_f32_prefilter_points_behind_and_on_camera_plane():
+def test_f32_prefilter_points_behind_and_on_camera_plane(score_variant):
     pr = synth.pnp_problem(3000, 0.3, seed=44)
     R, t = pr["R"], pr["t"]
     C = -R.T @ t
