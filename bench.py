@@ -8,7 +8,9 @@ problem, 10 000 2D-3D correspondences shaped like the reference's UTM scene,
 in HBM.  A step = sample -> P3P -> score all 10k points for every hypothesis
 of this rank's shard, global best by all-reduce(MAX) of the packed key
 (count << 32 | ~index) over RCCL, then the winner's RANSAC-phase mask.
-Weak scaling: rank r owns hypotheses [r*H, (r+1)*H) of the same Philox stream.
+Weak scaling: rank r owns hypotheses [r*H, (r+1)*H) of the same Philox stream; the
+exchange is rsac.parallel's all-reduce(MAX) of one int64 key; a rank that lost re-derives
+the winner's model from its index (no broadcast).
 
 Also reported: ms-to-best-model (adaptive termination on, LM refit on, wall
 time of the full rsac.pnp_ransac call), the scoring kernel's roofline, and
@@ -33,6 +35,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import rsac  # noqa: E402
+from rsac import parallel as par  # noqa: E402
 from rsac import synth  # noqa: E402
 
 METRIC = "RANSAC hypotheses/sec + ms-to-best-model, 10k pts 50% outliers, 1/2/4/8 GPU"
@@ -69,33 +72,26 @@ def main():
 
     pr = synth.pnp_problem(args.points, 0.5, seed=0)
     K = pr["K"]
-    p3 = torch.from_numpy(pr["points3d"]).to(dev)
-    p2 = torch.from_numpy(pr["points2d"]).to(dev)
     H = args.hyps
     base = rank * H
     score_ms = []
     solve_ms = []
 
+    ev = par.PnPShard(pr["points2d"], pr["points3d"], K, args.thr, device=local)
+
     def step():
-        key, model, mask, info = rsac.evaluate_range(p2, p3, K, base, H, args.thr, return_info=True,
+        key, model, mask, info = rsac.evaluate_range(ev.p2, ev.p3, K, base, H, args.thr, return_info=True,
                                                      with_mask=True, device=local)
         score_ms.append(info.score_ms)
         solve_ms.append(info.solve_ms)
         if dist is None:
             return key >> 32
-        kt = torch.tensor([key], dtype=torch.int64, device=dev)
-        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-        gkey = int(kt.item())
-        owner = min((0xFFFFFFFF - (gkey & 0xFFFFFFFF)) // H, world - 1)
-        if owner != rank or gkey != key:
-            # the winner lives on another rank: take its model, recompute the mask here
-            mt = torch.from_numpy(model).to(dev)
-            dist.broadcast(mt, src=owner)
-            if rank == 0:
-                mask, _ = rsac.pose_mask(p2, p3, K, mt.cpu().numpy(), args.thr, device=local)
-        else:
-            mt = torch.from_numpy(model).to(dev)
-            dist.broadcast(mt, src=owner)
+        gkey = par.all_reduce_max_key(max(key, 0))
+        if gkey != key:
+            # the winner lives on another rank: re-derive its model from the hypothesis index
+            # (Philox counter, one P3P solve) and its mask on this rank -- no broadcast
+            _, idx = par.unpack_key(gkey)
+            mask, _ = rsac.pose_mask(ev.p2, ev.p3, K, ev.model(idx), args.thr, device=local)
         return gkey >> 32
 
     for _ in range(args.warmup):
@@ -138,7 +134,7 @@ def main():
             walls = []
             for i in range(23):
                 t = time.perf_counter()
-                R, t_, m, info = rsac.pnp_ransac(p2, p3, K, 5000, args.thr, confidence=0.99, adaptive=True,
+                R, t_, m, info = rsac.pnp_ransac(ev.p2, ev.p3, K, 5000, args.thr, confidence=0.99, adaptive=True,
                                                  refine=True, return_info=True, device=local)
                 torch.cuda.synchronize()
                 if i >= 3:

@@ -935,4 +935,22 @@ int rsac_update_num_iters(double p, double ep, int model_points, int max_iters) 
     return update_num_iters(p, ep, model_points, max_iters);
 }
 
+void rsac_scan_init(rsac_scan_state *st, int32_t max_iters) {
+    if (!st) return;
+    ScanState s;
+    s.reset(max_iters);
+    *st = rsac_scan_state{s.niters, s.best, s.iter, s.max_good, 0};
+}
+
+int rsac_scan(rsac_scan_state *st, const int32_t *counts, const int8_t *status, int64_t count, int32_t n,
+              int32_t model_points, double confidence) {
+    if (!st || count < 0 || n <= 0 || (count > 0 && (!counts || !status)))
+        return fail(RSAC_EINVAL, "rsac_scan: bad arguments");
+    ScanState s;
+    s.niters = st->niters; s.best = st->best; s.iter = st->iter; s.max_good = st->max_good; s.done = st->done != 0;
+    scan_step(s, counts, status, count, n, model_points, confidence);
+    *st = rsac_scan_state{s.niters, s.best, s.iter, s.max_good, s.done ? 1 : 0};
+    return RSAC_OK;
+}
+
 }  // extern "C"

@@ -42,6 +42,12 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class ScanState(C.Structure):
+    """rsac_scan_state of include/rsac.h"""
+    _fields_ = [("niters", C.c_int64), ("best", C.c_int64), ("iter", C.c_int64), ("max_good", C.c_int32),
+                ("done", C.c_int32)]
+
+
 # (name, restype, argtypes) -- one row per declaration of include/rsac.h
 _vp, _i32, _i64, _u32, _u64, _d = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
 SIGNATURES = [
@@ -73,6 +79,8 @@ SIGNATURES = [
     ("rsac_rodrigues_v2m", None, [_vp, _vp]),
     ("rsac_rodrigues_m2v", None, [_vp, _vp]),
     ("rsac_update_num_iters", C.c_int, [_d, _d, C.c_int, C.c_int]),
+    ("rsac_scan_init", None, [_vp, _i32]),
+    ("rsac_scan", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d]),
 ]
 
 _lib = None

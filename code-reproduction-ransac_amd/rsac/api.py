@@ -410,3 +410,30 @@ def rodrigues(src):
 def update_num_iters(p: float, ep: float, model_points: int, max_iters: int) -> int:
     """RANSACUpdateNumIters of OpenCV, as the driver applies it after every new best model."""
     return int(L.lib().rsac_update_num_iters(float(p), float(ep), int(model_points), int(max_iters)))
+
+
+class Scan:
+    """OpenCV's sequential best-model scan (rsac_scan of include/rsac.h) over counts produced
+    elsewhere -- the multi-GPU driver feeds it each round's gathered counts."""
+
+    def __init__(self, max_iters: int, n_points: int, confidence: float = 0.99, model_points: int = 4):
+        self.st = L.ScanState()
+        L.lib().rsac_scan_init(C.byref(self.st), int(max_iters))
+        self.n = int(n_points)
+        self.conf = float(confidence)
+        self.s = int(model_points)
+
+    def step(self, counts, status):
+        c = np.ascontiguousarray(counts, np.int32)
+        st = np.ascontiguousarray(status, np.int8)
+        if c.shape != st.shape:
+            raise ValueError("counts and status differ in length")
+        L.check(L.lib().rsac_scan(C.byref(self.st), c.ctypes.data, st.ctypes.data, c.size, self.n, self.s, self.conf))
+        return self
+
+    done = property(lambda self: bool(self.st.done))
+    best = property(lambda self: int(self.st.best))
+    max_good = property(lambda self: int(self.st.max_good))
+    iters = property(lambda self: int(self.st.iter))
+    niters = property(lambda self: int(self.st.niters))
+

@@ -178,6 +178,24 @@ RSAC_EXPORT void rsac_rodrigues_m2v(const double R[9], double r[3]);
 /* RANSACUpdateNumIters (OpenCV ptsetreg.cpp) */
 RSAC_EXPORT int rsac_update_num_iters(double p, double ep, int model_points, int max_iters);
 
+/* The sequential best-model scan of OpenCV's RANSAC loop (ptsetreg.cpp run(): "count >
+ * max(maxGoodCount, modelPoints - 1)" replaces the best, then RANSACUpdateNumIters), over
+ * per-hypothesis (status, count) in hypothesis order.  rsac_pnp_ransac runs it internally;
+ * it is exported for drivers that produce the counts elsewhere, e.g. the multi-GPU loop of
+ * rsac/parallel.py, which gathers each round's counts from every rank and scans them
+ * identically everywhere.  Host-only, no device work. */
+typedef struct rsac_scan_state {
+    int64_t niters;   /* current iteration budget (starts at max_iters) */
+    int64_t best;     /* index of the best hypothesis so far, -1 = none */
+    int64_t iter;     /* hypotheses consumed */
+    int32_t max_good; /* inliers of the best */
+    int32_t done;     /* budget reached or sampler exhausted */
+} rsac_scan_state;
+RSAC_EXPORT void rsac_scan_init(rsac_scan_state *st, int32_t max_iters);
+/* consume hypotheses [st->iter, st->iter + count); status < 0 = sampler gave up (ends the scan) */
+RSAC_EXPORT int rsac_scan(rsac_scan_state *st, const int32_t *counts, const int8_t *status, int64_t count, int32_t n,
+                          int32_t model_points, double confidence);
+
 #ifdef __cplusplus
 }
 #endif

@@ -324,3 +324,23 @@ def test_f32_prefilter_points_behind_and_on_camera_plane(score_variant):
     fast = rsac.score_poses(P2, P3, pr["K"], poses, 30.0)
     ref = [O.pnp_count(p[:9].reshape(3, 3), p[9:], soa, cam, 30.0) for p in poses]
     np.testing.assert_array_equal(fast, ref)
+
+
+# ---------------------------------------------------------------------------------------------
+# multi-GPU driver on one rank (the gloo tests in test_parallel_gloo.py cover world_size 2)
+# ---------------------------------------------------------------------------------------------
+def test_parallel_driver_single_rank_equals_pnp_ransac():
+    from rsac import parallel as par
+    pr = synth.pnp_problem(3000, 0.6, seed=12)
+    ev = par.PnPShard(pr["points2d"], pr["points3d"], pr["K"], 30.0, device=0)
+    ada = par.sharded_ransac(ev, 5000, 0.99, round_size=512)
+    R, t, mask, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0, refine=False,
+                                       return_info=True)
+    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
+    assert (ada.best, ada.n_inliers, ada.iters) == (info.best_hyp, info.n_inliers, info.iters)
+    assert (ada.best, ada.n_inliers, ada.iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    np.testing.assert_array_equal(ada.model[:9].reshape(3, 3), ref["R"])
+    np.testing.assert_array_equal(ev.mask(ada.model), ref["mask"])
+    fixed = par.sharded_best(ev, 20000)
+    st, cn = ev.hypotheses(0, 20000)
+    assert par.pack_key(fixed.n_inliers, fixed.best) == par.best_key_of(cn, st, 0)

@@ -1,0 +1,149 @@
+"""Multi-rank driver (rsac/parallel.py) on CPU: world_size 2 over gloo, with an evaluator backed by
+the CPU restatement (the GPU evaluator PnPShard is exercised in test_gpu_parity.py).
+
+Checks that hypothesis sharding + all-reduce(MAX) of the packed key, the gathered adaptive scan,
+and the problem-sharded all-gather give exactly the single-process results.
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import pyoracle as O
+from rsac import parallel as par
+from rsac import synth
+
+
+class OracleShard:
+    """Evaluator with PnPShard's interface, computed by oracle/ (test infrastructure)."""
+
+    def __init__(self, pr, thr=30.0, seed=0x5EED):
+        self.soa = O.soa_pnp(pr["points3d"], pr["points2d"])
+        self.cam = O.cam_from_K(pr["K"])
+        self.thr, self.seed = thr, seed
+        self.n = len(self.soa[0])
+
+    def hypotheses(self, begin, count):
+        counts, status = O.pnp_hypotheses(self.soa, self.cam, self.thr, self.seed, count, hyp0=begin)
+        return status, counts
+
+    def range_key(self, begin, count):
+        st, cn = self.hypotheses(begin, count)
+        return par.best_key_of(cn, st, begin)
+
+    def model(self, index):
+        _, _, m = O.pnp_hypotheses(self.soa, self.cam, self.thr, self.seed, 1, hyp0=index, models=True)
+        return m[0, :12].copy()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pr = synth.pnp_problem(600, 0.6, seed=21)
+        ev = OracleShard(pr)
+        best = par.sharded_best(ev, 3001)
+        ada = par.sharded_ransac(ev, 5000, 0.99, round_size=100)
+        # problem sharding: 5 problems over the ranks, rows computed locally from the restatement
+        probs = [synth.pnp_problem(300, 0.4, seed=s) for s in range(5)]
+
+        def run_local(b, c):
+            rows = np.zeros((c, 3))
+            for i in range(c):
+                p = probs[b + i]
+                r = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 0.99, 400)
+                rows[i] = (b + i, r["best"], r["n_inliers"])
+            return rows
+
+        rows = par.sharded_batched(run_local, len(probs))
+        res = {"best": [best.best, best.n_inliers, best.model.tolist()],
+               "ada": [ada.best, ada.n_inliers, ada.iters, ada.model.tolist()],
+               "rows": rows.tolist()}
+        json.dump(res, open(os.path.join(out_dir, f"rank{rank}.json"), "w"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def gloo_results(tmp_path_factory):
+    d = tmp_path_factory.mktemp("gloo")
+    mp.spawn(_worker, args=(2, _free_port(), str(d)), nprocs=2, join=True)
+    return [json.load(open(d / f"rank{r}.json")) for r in range(2)]
+
+
+def test_ranks_agree(gloo_results):
+    assert gloo_results[0] == gloo_results[1]
+
+
+def test_sharded_best_equals_single_process(gloo_results):
+    pr = synth.pnp_problem(600, 0.6, seed=21)
+    ev = OracleShard(pr)
+    st, cn = ev.hypotheses(0, 3001)
+    key = par.best_key_of(cn, st, 0)
+    cnt, idx = par.unpack_key(key)
+    b, n, model = gloo_results[0]["best"]
+    assert (b, n) == (idx, cnt)
+    # lowest index among the maxima (OpenCV's first strictly-greater winner)
+    good = np.where(st > 0, cn, 0)
+    assert idx == int(np.flatnonzero(good == good.max())[0])
+    np.testing.assert_array_equal(model, ev.model(idx))
+
+
+def test_sharded_adaptive_equals_sequential_loop(gloo_results):
+    pr = synth.pnp_problem(600, 0.6, seed=21)
+    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
+    b, n, iters, model = gloo_results[0]["ada"]
+    assert (b, n, iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    np.testing.assert_array_equal(np.array(model[:9]).reshape(3, 3), ref["R"])
+    np.testing.assert_array_equal(model[9:], ref["t"])
+
+
+def test_problem_shards_gather_in_order(gloo_results):
+    rows = np.array(gloo_results[0]["rows"])
+    assert rows[:, 0].tolist() == list(range(5))
+    for i in range(5):
+        p = synth.pnp_problem(300, 0.4, seed=i)
+        r = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 0.99, 400)
+        assert rows[i, 1:].tolist() == [r["best"], r["n_inliers"]]
+
+
+@pytest.mark.parametrize("n,world", [(0, 2), (1, 2), (7, 3), (4096, 8), (100001, 8)])
+def test_shard_partition(n, world):
+    parts = [par.shard(n, r, world) for r in range(world)]
+    assert sum(c for _, c in parts) == n
+    pos = 0
+    for b, c in parts:
+        assert b == pos
+        pos += c
+    assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+
+
+def test_key_packing_orders_like_sequential_scan():
+    assert par.pack_key(10, 5) > par.pack_key(10, 6) > par.pack_key(9, 0) > par.pack_key(0, 0) == 0
+    assert par.unpack_key(par.pack_key(1234, 98765)) == (1234, 98765)
+
+
+def test_scan_matches_restatement():
+    rng = np.random.default_rng(5)
+    counts = rng.integers(0, 500, 3000).astype(np.int32)
+    status = rng.choice(np.array([0, 1], np.int8), 3000, p=[0.2, 0.8])
+    ref = O.scan(counts, status, 1000, 4, 0.99, 3000)
+    import rsac
+    sc = rsac.Scan(3000, 1000, 0.99, 4)
+    for b in range(0, 3000, 700):  # round boundaries must not matter
+        if sc.done:
+            break
+        sc.step(counts[b:b + 700], status[b:b + 700])
+    assert (sc.best, sc.max_good, sc.iters) == ref
