@@ -4,9 +4,10 @@
 //                 conversion of solvePnPRansac (main_v1.py:497)
 //   pnp_solve     one LANE per hypothesis: Philox subset (or a host-made
 //                 OpenCV subset), P3P in registers, 4th-point pick
-//   pnp_score     hypotheses x points tile: points held in registers per
-//                 lane, models in SGPRs (uniform scalar loads), inlier
-//                 counts by ballot + popcount, block-reduced through LDS
+//   pnp_score     work queue of 32-hypothesis units x all points: f32 records
+//                 staged in LDS, points in registers per lane, division-free
+//                 f32 test with exact f64 fallback, counts by ballot +
+//                 popcount, block-reduced through LDS (+ fused best key)
 //   pnp_mask      RANSAC-phase mask of the winners
 //   hom_*         the same skeleton for cv2.findHomography (main_v1.py:312)
 //
