@@ -102,6 +102,7 @@ struct rsac_ctx {
     double *d_cams = nullptr;
     float *d_thr2 = nullptr;
     DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
+    DevBuf loc;                                                // location search: inputs, pos2, H, err
     // pinned host staging
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask;
 };
@@ -673,6 +674,63 @@ int rsac_homography_ransac_batched(rsac_ctx *c, const void *src, const void *dst
     if (!offsets) return fail(RSAC_EINVAL, "offsets required");
     return hom_core(c, src, dst, offsets, P, 0, max_iters, thr, conf, seed, flags, H_out, status_out, ninl_out,
                     mask_out, nullptr, pick_stream(c, stream));
+}
+
+int rsac_location_search(rsac_ctx *c, const double *pos3d, const double *pixels, int32_t n, const double *locations,
+                         int32_t L, double thr, int32_t max_iters, double conf, uint32_t flags, double *H_out,
+                         double *err_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out,
+                         int32_t *n_good_out, void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (!pos3d || !pixels || !locations || !err_out || n <= 0 || L <= 0)
+        return fail(RSAC_EINVAL, "rsac_location_search: bad arguments");
+    if (flags & (RSAC_F_DEVICE_IN | RSAC_F_DEVICE_SOA | RSAC_F_DEVICE_OUT))
+        return fail(RSAC_EINVAL, "rsac_location_search takes host arrays");
+    hipStream_t s = pick_stream(c, stream);
+    // features noted on the image: pixel != (0, 0) (main_v1.py:304)
+    std::vector<double> in;
+    in.reserve((size_t)5 * n + 3 * L);
+    int32_t ng = 0;
+    for (int32_t i = 0; i < n; ++i)
+        if (pixels[2 * i] != 0.0 || pixels[2 * i + 1] != 0.0) {
+            in.insert(in.end(), pos3d + 3 * i, pos3d + 3 * i + 3);
+            ++ng;
+        }
+    for (int32_t i = 0; i < n; ++i)
+        if (pixels[2 * i] != 0.0 || pixels[2 * i + 1] != 0.0) in.insert(in.end(), pixels + 2 * i, pixels + 2 * i + 2);
+    in.insert(in.end(), locations, locations + 3 * (size_t)L);
+    if (n_good_out) *n_good_out = ng;
+    if (ng < 4) return fail(RSAC_ETOOFEW, "findHomography needs >= 4 noted features (got %d)", ng);
+    const size_t pairs = (size_t)L * ng;
+    // device layout (f64): p3 [3 ng] px [2 ng] locs [3 L] src [2 L ng] dst [2 L ng] H [9 L] err [2 L], ok [L] i32
+    const size_t nd = in.size() + 4 * pairs + 11 * (size_t)L;
+    HIPCHK(c->loc.ensure(nd * sizeof(double) + sizeof(int32_t) * L));
+    double *d_p3 = c->loc.as<double>(), *d_px = d_p3 + 3 * ng, *d_locs = d_px + 2 * ng, *d_src = d_locs + 3 * L;
+    double *d_dst = d_src + 2 * pairs, *d_H = d_dst + 2 * pairs, *d_err = d_H + 9 * (size_t)L;
+    int32_t *d_ok = (int32_t *)(d_err + 2 * (size_t)L);
+    HIPCHK(hipMemcpyAsync(d_p3, in.data(), in.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(launch_loc_pos2(d_p3, d_px, ng, d_locs, L, d_src, d_dst, s));
+    std::vector<int64_t> off((size_t)L + 1);
+    for (int32_t l = 0; l <= L; ++l) off[l] = (int64_t)l * ng;
+    std::vector<double> H((size_t)9 * L);
+    std::vector<int32_t> st(L), ninl(L);
+    std::vector<uint8_t> m(pairs);
+    r = hom_core(c, d_src, d_dst, off.data(), L, 0, max_iters, thr, conf, 0, flags | RSAC_F_DEVICE_IN, H.data(),
+                 st.data(), ninl.data(), m.data(), nullptr, s);
+    if (r < 0) return r;
+    // hom_core left the RANSAC-phase masks of every location in c->mask
+    std::vector<int32_t> ok(L);
+    for (int32_t l = 0; l < L; ++l) ok[l] = st[l] == RSAC_OK;
+    HIPCHK(hipMemcpyAsync(d_H, H.data(), H.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_ok, ok.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_loc_score(d_src, d_dst, c->mask.as<uint8_t>(), d_H, d_ok, L, ng, thr <= 0 ? 3.0 : thr, d_err, s));
+    HIPCHK(hipMemcpyAsync(err_out, d_err, sizeof(double) * 2 * L, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (H_out) memcpy(H_out, H.data(), H.size() * sizeof(double));
+    if (status_out) memcpy(status_out, st.data(), sizeof(int32_t) * L);
+    if (ninl_out) memcpy(ninl_out, ninl.data(), sizeof(int32_t) * L);
+    if (mask_out) memcpy(mask_out, m.data(), pairs);
+    return r;
 }
 
 int rsac_score_poses(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],

@@ -261,18 +261,166 @@ static void jacobi_min_evec(int n, double *A, double *v_out) {
     for (int k = 0; k < n; ++k) v_out[k] = V[k * n + mi];
 }
 
-static double hom_cost(const double h[9], const float *sx, const float *sy, const float *dx, const float *dy,
-                       const uint8_t *mask, int n) {
-    double c = 0;
+// Residuals of HomographyRefineCallback::compute (OpenCV fundam.cpp) over the
+// inliers: projection - dst (x, y interleaved); Jacobian w.r.t. h0..h7 (h8 = 1).
+static void hom_residuals(const double *h, const float *sx, const float *sy, const float *dx, const float *dy,
+                          const uint8_t *mask, int n, double *r, double *J) {
+    int q = 0;
     for (int i = 0; i < n; ++i) {
         if (!mask[i]) continue;
-        double x = sx[i], y = sy[i];
-        double ww = 1. / (h[6] * x + h[7] * y + 1.);
-        double ex = (h[0] * x + h[1] * y + h[2]) * ww - dx[i];
-        double ey = (h[3] * x + h[4] * y + h[5]) * ww - dy[i];
-        c += ex * ex + ey * ey;
+        const double Mx = sx[i], My = sy[i];
+        double ww = h[6] * Mx + h[7] * My + 1.;
+        ww = fabs(ww) > DBL_EPSILON ? 1. / ww : 0;
+        const double xi = (h[0] * Mx + h[1] * My + h[2]) * ww;
+        const double yi = (h[3] * Mx + h[4] * My + h[5]) * ww;
+        r[2 * q] = xi - dx[i];
+        r[2 * q + 1] = yi - dy[i];
+        if (J) {
+            double *jx = J + 16 * q, *jy = jx + 8;
+            jx[0] = Mx * ww; jx[1] = My * ww; jx[2] = ww; jx[3] = jx[4] = jx[5] = 0.;
+            jx[6] = -Mx * ww * xi; jx[7] = -My * ww * xi;
+            jy[0] = jy[1] = jy[2] = 0.; jy[3] = Mx * ww; jy[4] = My * ww; jy[5] = ww;
+            jy[6] = -Mx * ww * yi; jy[7] = -My * ww * yi;
+        }
+        ++q;
     }
-    return c;
+}
+
+// A = J^T J, v = J^T r for m residuals and 8 parameters
+static void normal_eqs(const double *J, const double *r, int m, double *A, double *v) {
+    std::fill(A, A + 64, 0.0);
+    std::fill(v, v + 8, 0.0);
+    for (int k = 0; k < m; ++k) {
+        const double *jr = J + 8 * k;
+        for (int a = 0; a < 8; ++a) {
+            v[a] += jr[a] * r[k];
+            for (int b = 0; b < 8; ++b) A[a * 8 + b] += jr[a] * jr[b];
+        }
+    }
+}
+
+// x = A^+ b through the symmetric eigen-decomposition (cv::solve DECOMP_EIG):
+// cyclic Jacobi, eigenvalues |w| <= 8 eps max|w| dropped
+static void solve_eig8(const double *A, const double *b, double *x) {
+    double W[64], V[64];
+    std::copy(A, A + 64, W);
+    for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j) V[i * 8 + j] = (i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0;
+        for (int i = 0; i < 8; ++i)
+            for (int j = i + 1; j < 8; ++j) off += W[i * 8 + j] * W[i * 8 + j];
+        if (off < 1e-300) break;
+        for (int p = 0; p < 8; ++p)
+            for (int q = p + 1; q < 8; ++q) {
+                const double apq = W[p * 8 + q];
+                if (fabs(apq) < 1e-300) continue;
+                const double theta = (W[q * 8 + q] - W[p * 8 + p]) / (2.0 * apq);
+                const double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
+                for (int k = 0; k < 8; ++k) {
+                    const double akp = W[k * 8 + p], akq = W[k * 8 + q];
+                    W[k * 8 + p] = c * akp - s * akq;
+                    W[k * 8 + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 8; ++k) {
+                    const double apk = W[p * 8 + k], aqk = W[q * 8 + k];
+                    W[p * 8 + k] = c * apk - s * aqk;
+                    W[q * 8 + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 8; ++k) {
+                    const double vkp = V[k * 8 + p], vkq = V[k * 8 + q];
+                    V[k * 8 + p] = c * vkp - s * vkq;
+                    V[k * 8 + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    double wmax = 0;
+    for (int i = 0; i < 8; ++i) wmax = fmax(wmax, fabs(W[i * 8 + i]));
+    const double tol = wmax * 8 * DBL_EPSILON;
+    std::fill(x, x + 8, 0.0);
+    for (int e = 0; e < 8; ++e) {
+        const double w = W[e * 8 + e];
+        if (fabs(w) <= tol) continue;
+        double c = 0;
+        for (int k = 0; k < 8; ++k) c += V[k * 8 + e] * b[k];
+        c /= w;
+        for (int k = 0; k < 8; ++k) x[k] += c * V[k * 8 + e];
+    }
+}
+
+// cv::LMSolver::run of OpenCV 4.x (levmarq.cpp, LMSolverImpl) on h0..h7:
+// damping lambda * diag(J^T J at the start), gain-ratio schedule (0.25 / 0.75),
+// lambda -> 0 below lc and restart from 1 / max diag(A^-1), at most max_iters
+// iterations, stop when |d|inf or |r|inf < FLT_EPSILON.
+static int hom_lm(const float *sx, const float *sy, const float *dx, const float *dy, const uint8_t *mask, int n,
+                  double H[9], int max_iters) {
+    int m = 0;
+    for (int i = 0; i < n; ++i) m += mask[i] != 0;
+    if (m == 0) return 0;
+    m *= 2;
+    std::vector<double> r(m), rd(m), J((size_t)m * 8);
+    double x[9], xd[9], A[64], Ap[64], v[8], D[8], d[8];
+    std::copy(H, H + 9, x);
+    std::copy(H, H + 9, xd);
+    hom_residuals(x, sx, sy, dx, dy, mask, n, r.data(), J.data());
+    double S = 0;
+    for (int k = 0; k < m; ++k) S += r[k] * r[k];
+    normal_eqs(J.data(), r.data(), m, A, v);
+    for (int a = 0; a < 8; ++a) D[a] = A[a * 8 + a];
+    const double Rlo = 0.25, Rhi = 0.75;
+    double lambda = 1, lc = 0.75;
+    int iter = 0;
+    for (;;) {
+        std::copy(A, A + 64, Ap);
+        for (int a = 0; a < 8; ++a) Ap[a * 8 + a] += lambda * D[a];
+        solve_eig8(Ap, v, d);
+        for (int a = 0; a < 8; ++a) xd[a] = x[a] - d[a];
+        hom_residuals(xd, sx, sy, dx, dy, mask, n, rd.data(), nullptr);
+        double Sd = 0;
+        for (int k = 0; k < m; ++k) Sd += rd[k] * rd[k];
+        double dS = 0;  // d . (2 v - A d)
+        for (int a = 0; a < 8; ++a) {
+            double ad = 0;
+            for (int b = 0; b < 8; ++b) ad += A[a * 8 + b] * d[b];
+            dS += d[a] * (2 * v[a] - ad);
+        }
+        const double R = (S - Sd) / (fabs(dS) > DBL_EPSILON ? dS : 1);
+        if (R > Rhi) {
+            lambda *= 0.5;
+            if (lambda < lc) lambda = 0;
+        } else if (R < Rlo) {
+            double t = 0;
+            for (int a = 0; a < 8; ++a) t += d[a] * v[a];
+            double nu = (Sd - S) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
+            nu = fmin(fmax(nu, 2.), 10.);
+            if (lambda == 0) {
+                double e[8], col[8], maxval = DBL_EPSILON;
+                for (int c = 0; c < 8; ++c) {
+                    for (int a = 0; a < 8; ++a) e[a] = a == c;
+                    solve_eig8(A, e, col);
+                    maxval = fmax(maxval, fabs(col[c]));
+                }
+                lambda = lc = 1. / maxval;
+                nu *= 0.5;
+            }
+            lambda *= nu;
+        }
+        if (Sd < S) {
+            S = Sd;
+            std::copy(xd, xd + 8, x);
+            hom_residuals(x, sx, sy, dx, dy, mask, n, r.data(), J.data());
+            normal_eqs(J.data(), r.data(), m, A, v);
+        }
+        iter++;
+        double dinf = 0, rinf = 0;
+        for (int a = 0; a < 8; ++a) dinf = fmax(dinf, fabs(d[a]));
+        for (int k = 0; k < m; ++k) rinf = fmax(rinf, fabs(r[k]));
+        if (!(iter < max_iters && dinf >= FLT_EPSILON && rinf >= FLT_EPSILON)) break;
+    }
+    std::copy(x, x + 8, H);
+    H[8] = 1.0;
+    return iter;
 }
 
 bool hom_refine(const float *sx, const float *sy, const float *dx, const float *dy, const uint8_t *mask, int n,
@@ -317,37 +465,7 @@ bool hom_refine(const float *sx, const float *sy, const float *dx, const float *
     mat3mul(T, Hnorm2, H0);
     double sc = 1. / H0[8];
     for (int k = 0; k < 9; ++k) H[k] = H0[k] * sc;
-    double lam = 1e-3;
-    double cost = hom_cost(H, sx, sy, dx, dy, mask, n);
-    for (int it = 0; it < 10; ++it) {
-        double A[64] = {0}, g[8] = {0};
-        for (int i = 0; i < n; ++i) {
-            if (!mask[i]) continue;
-            double x = sx[i], y = sy[i];
-            double den = H[6] * x + H[7] * y + 1.;
-            double ww = 1. / den;
-            double Xi = (H[0] * x + H[1] * y + H[2]) * ww;
-            double Yi = (H[3] * x + H[4] * y + H[5]) * ww;
-            double ex = Xi - dx[i], ey = Yi - dy[i];
-            double Jx[8] = {x * ww, y * ww, ww, 0, 0, 0, -Xi * x * ww, -Xi * y * ww};
-            double Jy[8] = {0, 0, 0, x * ww, y * ww, ww, -Yi * x * ww, -Yi * y * ww};
-            for (int a = 0; a < 8; ++a) {
-                g[a] += Jx[a] * ex + Jy[a] * ey;
-                for (int b = 0; b <= a; ++b) A[a * 8 + b] += Jx[a] * Jx[b] + Jy[a] * Jy[b];
-            }
-        }
-        for (int a = 0; a < 8; ++a)
-            for (int b = a + 1; b < 8; ++b) A[a * 8 + b] = A[b * 8 + a];
-        double d[8], mg[8];
-        for (int a = 0; a < 8; ++a) mg[a] = -g[a];
-        if (!chol_solve(8, A, lam, mg, d)) { lam *= 10; continue; }
-        double Hn[9];
-        for (int a = 0; a < 8; ++a) Hn[a] = H[a] + d[a];
-        Hn[8] = 1.0;
-        double cn = hom_cost(Hn, sx, sy, dx, dy, mask, n);
-        if (cn < cost) { memcpy(H, Hn, sizeof(Hn)); cost = cn; lam *= 0.1; }
-        else lam *= 10;
-    }
+    hom_lm(sx, sy, dx, dy, mask, n, H, 10);
     return true;
 }
 

@@ -96,4 +96,11 @@ hipError_t launch_hom_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int3
 hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
                            hipStream_t s);
 
+// camera-location search (main_v1.py:254-348): pos2 of every (location, feature) pair, then
+// err1 / err2 of every location's homography
+hipError_t launch_loc_pos2(const double *p3, const double *px, int32_t n, const double *locs, int32_t L, double *src,
+                           double *dst, hipStream_t s);
+hipError_t launch_loc_score(const double *src, const double *dst, const uint8_t *mask, const double *H,
+                            const int32_t *ok, int32_t L, int32_t n, double thr, double *err, hipStream_t s);
+
 }  // namespace rsac

@@ -1102,4 +1102,95 @@ hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Camera-location search (find_homographies / find_homography, main_v1.py:254-348)
+// ---------------------------------------------------------------------------
+// pos2 of every (location l, noted feature i): p = pos3d_i - loc_l, reordered
+// (p2, p1, p0) and divided by p0 (main_v1.py:305-308), f64 as numpy; dst = the
+// feature's pixel.  Output AoS, problem l = rows [l n, (l + 1) n).
+__global__ void k_loc_pos2(const double *__restrict__ p3, const double *__restrict__ px, int32_t n,
+                           const double *__restrict__ locs, int32_t L, double *__restrict__ src,
+                           double *__restrict__ dst) {
+    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (k >= (int64_t)L * n) return;
+    const int l = (int)(k / n), i = (int)(k % n);
+    const double d0 = p3[3 * i] - locs[3 * l];
+    const double d1 = p3[3 * i + 1] - locs[3 * l + 1];
+    const double d2 = p3[3 * i + 2] - locs[3 * l + 2];
+    src[2 * k] = d2 / d0;
+    src[2 * k + 1] = d1 / d0;
+    dst[2 * k] = px[2 * i];
+    dst[2 * k + 1] = px[2 * i + 1];
+}
+
+// 3x3 inverse by the adjugate (numpy.linalg.inv's LU differs only by rounding)
+__device__ __forceinline__ void inv3(const double *A, double *B) {
+    const double c0 = A[4] * A[8] - A[5] * A[7];
+    const double c1 = A[5] * A[6] - A[3] * A[8];
+    const double c2 = A[3] * A[7] - A[4] * A[6];
+    const double id = 1.0 / (A[0] * c0 + A[1] * c1 + A[2] * c2);
+    B[0] = c0 * id; B[1] = (A[2] * A[7] - A[1] * A[8]) * id; B[2] = (A[1] * A[5] - A[2] * A[4]) * id;
+    B[3] = c1 * id; B[4] = (A[0] * A[8] - A[2] * A[6]) * id; B[5] = (A[2] * A[3] - A[0] * A[5]) * id;
+    B[6] = c2 * id; B[7] = (A[1] * A[6] - A[0] * A[7]) * id; B[8] = (A[0] * A[4] - A[1] * A[3]) * id;
+}
+
+__device__ __forceinline__ double proj_dist(const double *A, double x, double y, double u, double v) {
+    const double w = A[6] * x + A[7] * y + A[8];
+    const double px = (A[0] * x + A[1] * y + A[2]) / w, py = (A[3] * x + A[4] * y + A[5]) / w;
+    return sqrt((u - px) * (u - px) + (v - py) * (v - py));
+}
+
+// One wave per location.  With H = findHomography's result and M = inv(H) (main_v1.py:314):
+//   err1 = sum_{mask} |p1 - dehom(inv(M) pos2)|     (main_v1.py:333-347)
+//   err2 = sum_{mask} |pos2 - dehom(M p1)| + (#not mask) * thr   (main_v1.py:347, 419)
+// Locations without a model get (0, 0), which the driver maps to 1e6 (main_v1.py:864).
+__global__ __launch_bounds__(64) void k_loc_score(const double *__restrict__ src, const double *__restrict__ dst,
+                                                  const uint8_t *__restrict__ mask, const double *__restrict__ H,
+                                                  const int32_t *__restrict__ ok, int32_t n, double thr,
+                                                  double *__restrict__ err) {
+    const int l = blockIdx.x, lane = threadIdx.x;
+    if (!ok[l]) {
+        if (lane == 0) err[2 * l] = err[2 * l + 1] = 0.0;
+        return;
+    }
+    double M[9], Mi[9];
+    inv3(H + 9 * l, M);
+    inv3(M, Mi);
+    double e1 = 0.0, e2 = 0.0;
+    int nout = 0;
+    for (int i = lane; i < n; i += 64) {
+        const int64_t k = (int64_t)l * n + i;
+        const double sx = src[2 * k], sy = src[2 * k + 1], u = dst[2 * k], v = dst[2 * k + 1];
+        if (mask[k]) {
+            e1 += proj_dist(Mi, sx, sy, u, v);
+            e2 += proj_dist(M, u, v, sx, sy);
+        } else {
+            ++nout;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        e1 += __shfl_xor(e1, o);
+        e2 += __shfl_xor(e2, o);
+        nout += __shfl_xor(nout, o);
+    }
+    if (lane == 0) {
+        err[2 * l] = e1;
+        err[2 * l + 1] = e2 + (double)nout * thr;
+    }
+}
+
+hipError_t launch_loc_pos2(const double *p3, const double *px, int32_t n, const double *locs, int32_t L, double *src,
+                           double *dst, hipStream_t s) {
+    const int64_t total = (int64_t)L * n;
+    hipLaunchKernelGGL(k_loc_pos2, dim3(cdiv(total > 0 ? total : 1, 256)), dim3(256), 0, s, p3, px, n, locs, L, src,
+                       dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_loc_score(const double *src, const double *dst, const uint8_t *mask, const double *H,
+                            const int32_t *ok, int32_t L, int32_t n, double thr, double *err, hipStream_t s) {
+    hipLaunchKernelGGL(k_loc_score, dim3(L), dim3(64), 0, s, src, dst, mask, H, ok, n, thr, err);
+    return hipGetLastError();
+}
+
 }  // namespace rsac

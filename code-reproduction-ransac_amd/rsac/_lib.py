@@ -79,6 +79,8 @@ SIGNATURES = [
     ("rsac_rodrigues_v2m", None, [_vp, _vp]),
     ("rsac_rodrigues_m2v", None, [_vp, _vp]),
     ("rsac_update_num_iters", C.c_int, [_d, _d, C.c_int, C.c_int]),
+    ("rsac_location_search", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _d, _i32, _d, _u32, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _vp]),
     ("rsac_scan_init", None, [_vp, _i32]),
     ("rsac_scan", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d]),
 ]

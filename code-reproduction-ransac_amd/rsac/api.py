@@ -412,6 +412,58 @@ def update_num_iters(p: float, ep: float, model_points: int, max_iters: int) -> 
     return int(L.lib().rsac_update_num_iters(float(p), float(ep), int(model_points), int(max_iters)))
 
 
+@dataclass
+class LocationResult:
+    """Outputs of rsac.location_search, one row per candidate camera location."""
+    err: np.ndarray  # (L, 2) f64: err1, err2 (num_matches of main_v1.py:273; (0, 0) = no model)
+    H: np.ndarray  # (L, 3, 3) findHomography's H (main_v1.py:312; M = inv(H) at :314)
+    ok: np.ndarray  # (L,) bool
+    n_inliers: np.ndarray  # (L,) int32
+    mask: np.ndarray  # (L, n_good) bool, RANSAC-phase
+    n_good: int  # features noted on the image
+
+    @property
+    def best(self) -> int:
+        """argmin of err2 with 0 -> 1e6, as main_v1.py:863-866 picks the camera location."""
+        e2 = self.err[:, 1].copy()
+        e2[e2 == 0] = 1000000
+        return int(np.argmin(e2))
+
+
+def location_search(pos3d, pixels, locations, ransacbound: float = 75.0, *, max_iters: int = 2000,
+                    confidence: float = 0.995, sampler: str = "opencv", adaptive: bool = True, refine: bool = True,
+                    device: int = 0) -> LocationResult:
+    """The camera-location search of find_homographies (main_v1.py:254-297) in one call.
+
+    pos3d (N,3) feature positions, pixels (N,2) (rows (0,0) = not noted on the image,
+    main_v1.py:304), locations (L,3) candidate camera positions.  For every location the
+    homography RANSAC of find_homography (main_v1.py:300-312) and its err1/err2 score
+    (main_v1.py:332-348, 419) run on the GPU.
+    """
+    P3 = np.ascontiguousarray(np.asarray(pos3d, np.float64).reshape(-1, 3))
+    P2 = np.ascontiguousarray(np.asarray(pixels, np.float64).reshape(-1, 2))
+    LC = np.ascontiguousarray(np.asarray(locations, np.float64).reshape(-1, 3))
+    if P3.shape[0] != P2.shape[0]:
+        raise ValueError("pos3d and pixels differ in length")
+    L_, n = LC.shape[0], P3.shape[0]
+    n_good_max = int(np.count_nonzero((P2[:, 0] != 0) | (P2[:, 1] != 0)))
+    err = np.zeros((L_, 2))
+    H = np.zeros((L_, 9))
+    st = np.zeros(L_, np.int32)
+    ninl = np.zeros(L_, np.int32)
+    mask = np.zeros(max(L_ * n_good_max, 1), np.uint8)
+    ng = C.c_int32(0)
+    ctx = L.context(device)
+    with ctx.lock:
+        L.check(L.lib().rsac_location_search(ctx.handle, P3.ctypes.data, P2.ctypes.data, n, LC.ctypes.data, L_,
+                                             float(ransacbound), int(max_iters), float(confidence),
+                                             _flags(adaptive, refine, sampler), H.ctypes.data, err.ctypes.data,
+                                             st.ctypes.data, ninl.ctypes.data, mask.ctypes.data, C.byref(ng), None))
+    g = int(ng.value)
+    return LocationResult(err=err, H=H.reshape(L_, 3, 3), ok=st == L.OK, n_inliers=ninl,
+                          mask=mask[:L_ * g].reshape(L_, g).astype(bool), n_good=g)
+
+
 class Scan:
     """OpenCV's sequential best-model scan (rsac_scan of include/rsac.h) over counts produced
     elsewhere -- the multi-GPU driver feeds it each round's gathered counts."""

@@ -106,3 +106,34 @@ def testpro_k_candidates():
             fy = f / (sh / TESTPRO_K_IMAGE[1])
             out.append(np.array([[fx, 0, TESTPRO_K_IMAGE[0] / 2], [0, fy, TESTPRO_K_IMAGE[1] / 2], [0, 0, 1.0]]))
     return out
+
+
+def location_problem(n_features: int = 13, n_locations: int = 458, n_outliers: int = 2, n_unnoted: int = 1,
+                     seed: int = 0, noise_px: float = 2.0, spacing: float = 150.0):
+    """Camera-location search scene shaped like main_v1.py's (12 noted features, 458 candidate
+    locations, main_v1.py:274, 862).
+
+    Features lie 2-9 km ahead (first coordinate) of the true camera position.  From that position
+    the direction ratios pos2 = (dz/dx, dy/dx) of main_v1.py:305-308 map to pixels by a homography
+    (a rotating camera), plus noise; ``n_outliers`` pixels are random, ``n_unnoted`` are (0, 0).
+    Candidates are a grid of ``spacing`` m around the true position, which is one of them."""
+    rng = np.random.default_rng(seed)
+    T = np.array([2888281.18, 739424.6, 770.0])
+    pos3d = T + np.c_[rng.uniform(2000, 9000, n_features), rng.uniform(-4000, 4000, n_features),
+                      rng.uniform(-200, 600, n_features)]
+    d = pos3d - T
+    ray = np.c_[d[:, 2] / d[:, 0], d[:, 1] / d[:, 0]]
+    H = np.array([[0.0, 600.0, 1071.0], [-2500.0, 0.0, 900.0], [0.05, 0.02, 1.0]])
+    H = H + rng.normal(size=(3, 3)) * np.array([[20, 20, 20], [20, 20, 20], [0.01, 0.01, 0]])
+    hs = np.c_[ray, np.ones(n_features)] @ H.T
+    pixels = hs[:, :2] / hs[:, 2:3] + rng.normal(0, noise_px, (n_features, 2))
+    perm = rng.permutation(n_features)
+    pixels[perm[:n_outliers]] = rng.uniform([0, 0], [IMAGE_W, IMAGE_H], (n_outliers, 2))
+    pixels[perm[n_outliers:n_outliers + n_unnoted]] = 0.0
+    side = int(np.ceil(np.sqrt(n_locations)))
+    gi, gj = np.meshgrid(np.arange(side) - side // 2, np.arange(side) - side // 2, indexing="ij")
+    grid = np.c_[gi.ravel(), gj.ravel()][:n_locations] * spacing
+    locations = np.c_[T[0] + grid[:, 0], T[1] + grid[:, 1], T[2] + 30.0 * np.sin(grid[:, 0] / 700.0)]
+    true_index = int(np.flatnonzero((grid[:, 0] == 0) & (grid[:, 1] == 0))[0])
+    locations[true_index] = T
+    return dict(pos3d=pos3d, pixels=pixels, locations=locations, true_index=true_index, H=H / H[2, 2])

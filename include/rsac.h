@@ -122,6 +122,26 @@ RSAC_EXPORT int rsac_homography_ransac_batched(rsac_ctx *ctx, const void *src, c
                                    uint64_t seed, uint32_t flags, double *H_out, int32_t *status_out,
                                    int32_t *n_inliers_out, uint8_t *mask_out, void *stream);
 
+/* The camera-location search of find_homographies / find_homography
+ * (main_v1.py:254-348, 419; driver main_v1.py:862-866) as one call.
+ * For every candidate location l (locations: L x 3 f64) and every feature i
+ * noted on the image (pixels[i] != (0,0), main_v1.py:304):
+ *   pos2 = (dz/dx, dy/dx) of pos3d[i] - loc[l]              (main_v1.py:305-308)
+ *   H, mask = findHomography(pos2, pixels, RANSAC, thr)     (main_v1.py:312)
+ *   err1 = sum_{mask} |pixel - H pos2|,  err2 = sum_{mask} |pos2 - H^-1 pixel|
+ *          + (#outliers) * thr                              (main_v1.py:332-348, 419)
+ * Host f64 arrays (pos3d n x 3, pixels n x 2).  Outputs: err_out L x 2
+ * (err1, err2; (0, 0) where no model, which the driver maps to 1e6), and
+ * optionally H_out L x 9 (findHomography's H = inv(M) of main_v1.py:314),
+ * status_out L, n_inliers_out L, mask_out L x n_good (RANSAC-phase),
+ * n_good_out.  flags: as rsac_homography_ransac (OpenCV sampler + adaptive +
+ * refine reproduce cv2.findHomography). */
+RSAC_EXPORT int rsac_location_search(rsac_ctx *ctx, const double *pos3d, const double *pixels, int32_t n,
+                                     const double *locations, int32_t n_locations, double thresh, int32_t max_iters,
+                                     double confidence, uint32_t flags, double *H_out, double *err_out,
+                                     int32_t *status_out, int32_t *n_inliers_out, uint8_t *mask_out,
+                                     int32_t *n_good_out, void *stream);
+
 /* Minimal slice: inlier counts of given poses (H x [R 9, t 3] f64, host)
  * under the reprojection test of PnPRansacCallback::computeError. */
 RSAC_EXPORT int rsac_score_poses(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],

@@ -305,3 +305,62 @@ def rodrigues_m2v(R):
     r = np.zeros(3)
     lib().orc_rodrigues_m2v(np.ascontiguousarray(R, np.float64).reshape(9), r)
     return r
+
+
+# ----------------------------------------------------------------------------------------------
+# camera-location search (main_v1.py:254-348, 419, 862-866), numpy restatement, literal loops
+# ----------------------------------------------------------------------------------------------
+def location_pos2(pos3ds, camera_location):
+    """main_v1.py:301-308: pos2 and the `good` (noted-pixel) flags are computed per feature."""
+    pos2 = np.zeros((len(pos3ds), 2))
+    for i in range(len(pos3ds)):
+        p = pos3ds[i, :] - camera_location
+        p = np.array([p[2], p[1], p[0]])
+        p = p / p[2]
+        pos2[i, :] = p[0:2]
+    return pos2
+
+
+def location_errors(pos2_good, pixels_good, M, mask, ransacbound):
+    """main_v1.py:332-348 + 419: err1, err2 of one location given M = inv(H) and the RANSAC mask."""
+    err1 = 0.0
+    err2 = 0.0
+    mask = np.asarray(mask).reshape(-1).astype(np.uint8)
+    for i in range(pos2_good.shape[0]):
+        p1 = pixels_good[i, :]
+        pp = np.array([pos2_good[i, 0], pos2_good[i, 1], 1.0])
+        pp2 = np.matmul(np.linalg.inv(M), pp)
+        pp2 = pp2 / pp2[2]
+        P1 = np.array([p1[0], p1[1], 1.0])
+        PP2 = np.matmul(M, P1)
+        PP2 = PP2 / PP2[2]
+        P2 = pos2_good[i, :]
+        if mask[i] == 1:
+            err1 += np.linalg.norm(p1 - pp2[0:2])
+            err2 += np.linalg.norm(P2 - PP2[0:2])
+    err2 += np.sum(1 - mask) * ransacbound
+    return err1, err2
+
+
+def find_homography(pixels, pos3ds, camera_location, ransacbound):
+    """main_v1.py:300-348, 419 with cv2.findHomography restated (hom_ransac, OpenCV sampler + refit).
+
+    -> dict(M, err1, err2, mask, H); no model -> err (0, 0), which the driver maps to 1e6 (the
+    reference itself would raise at np.linalg.inv(None))."""
+    pixels = np.asarray(pixels, np.float64)
+    good = (pixels[:, 0] != 0) | (pixels[:, 1] != 0)
+    pos2 = location_pos2(np.asarray(pos3ds, np.float64), np.asarray(camera_location, np.float64))
+    res = hom_ransac(pos2[good], pixels[good], ransacbound, 0.995, 2000, sampler="opencv", refine=True)
+    if res["best"] < 0:
+        return dict(M=None, H=None, err1=0.0, err2=0.0, mask=res["mask"])
+    H = res["H_refined"] if res["H_refined"] is not None else res["H"]
+    M = np.linalg.inv(H)
+    e1, e2 = location_errors(pos2[good], pixels[good], M, res["mask"], ransacbound)
+    return dict(M=M, H=H, err1=e1, err2=e2, mask=res["mask"])
+
+
+def best_location(num_matches):
+    """main_v1.py:863-866"""
+    e2 = np.array(num_matches, np.float64)[:, 1].copy()
+    e2[e2 == 0] = 1000000
+    return int(np.argmin(e2))

@@ -936,18 +936,176 @@ static void jacobi_min_evec(int n, double *A, double *v_out) {
     for (int k = 0; k < n; ++k) v_out[k] = V[k * n + mi];
 }
 
-static double hom_cost(const double h[9], const float *sx, const float *sy, const float *dx, const float *dy,
-                       const uint8_t *mask, int n) {
-    double c = 0;
+/* HomographyRefineCallback::compute (fundam.cpp): residuals proj - dst over the
+ * inliers (x2), Jacobian w.r.t. h0..h7 (h8 = 1). */
+static void hom_lm_compute(const double *h, const float *sx, const float *sy, const float *dx, const float *dy,
+                           const uint8_t *mask, int n, double *r, double *J) {
+    int q = 0;
     for (int i = 0; i < n; ++i) {
-        if (mask && !mask[i]) continue;
-        double x = sx[i], y = sy[i];
-        double ww = 1. / (h[6] * x + h[7] * y + 1.);
-        double ex = (h[0] * x + h[1] * y + h[2]) * ww - dx[i];
-        double ey = (h[3] * x + h[4] * y + h[5]) * ww - dy[i];
-        c += ex * ex + ey * ey;
+        if (!mask[i]) continue;
+        double Mx = sx[i], My = sy[i];
+        double ww = h[6] * Mx + h[7] * My + 1.;
+        ww = fabs(ww) > DBL_EPSILON ? 1. / ww : 0;
+        double xi = (h[0] * Mx + h[1] * My + h[2]) * ww;
+        double yi = (h[3] * Mx + h[4] * My + h[5]) * ww;
+        r[2 * q] = xi - dx[i];
+        r[2 * q + 1] = yi - dy[i];
+        if (J) {
+            double *j0 = J + 16 * q, *j1 = j0 + 8;
+            j0[0] = Mx * ww; j0[1] = My * ww; j0[2] = ww; j0[3] = j0[4] = j0[5] = 0.;
+            j0[6] = -Mx * ww * xi; j0[7] = -My * ww * xi;
+            j1[0] = j1[1] = j1[2] = 0.; j1[3] = Mx * ww; j1[4] = My * ww; j1[5] = ww;
+            j1[6] = -Mx * ww * yi; j1[7] = -My * ww * yi;
+        }
+        ++q;
     }
-    return c;
+}
+
+/* A = J^T J, v = J^T r (m residuals, 8 parameters) */
+static void lm_normal(const double *J, const double *r, int m, double *A, double *v) {
+    for (int a = 0; a < 8; ++a) {
+        v[a] = 0;
+        for (int b = 0; b < 8; ++b) A[a * 8 + b] = 0;
+    }
+    for (int k = 0; k < m; ++k) {
+        const double *jr = J + 8 * k;
+        for (int a = 0; a < 8; ++a) {
+            v[a] += jr[a] * r[k];
+            for (int b = 0; b < 8; ++b) A[a * 8 + b] += jr[a] * jr[b];
+        }
+    }
+}
+
+/* x = A^-1 b for symmetric A by its eigen-decomposition (cv::solve DECOMP_EIG):
+ * eigenvalues <= DBL_EPSILON * max are dropped. */
+static void sym_solve_eig(const double *A, const double *b, double *x) {
+    double W[64], V[64];
+    memcpy(W, A, sizeof W);
+    for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j) V[i * 8 + j] = (i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0;
+        for (int i = 0; i < 8; ++i)
+            for (int j = i + 1; j < 8; ++j) off += W[i * 8 + j] * W[i * 8 + j];
+        if (off < 1e-300) break;
+        for (int p = 0; p < 8; ++p)
+            for (int q = p + 1; q < 8; ++q) {
+                double apq = W[p * 8 + q];
+                if (fabs(apq) < 1e-300) continue;
+                double theta = (W[q * 8 + q] - W[p * 8 + p]) / (2.0 * apq);
+                double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
+                for (int k = 0; k < 8; ++k) {
+                    double akp = W[k * 8 + p], akq = W[k * 8 + q];
+                    W[k * 8 + p] = c * akp - s * akq;
+                    W[k * 8 + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 8; ++k) {
+                    double apk = W[p * 8 + k], aqk = W[q * 8 + k];
+                    W[p * 8 + k] = c * apk - s * aqk;
+                    W[q * 8 + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 8; ++k) {
+                    double vkp = V[k * 8 + p], vkq = V[k * 8 + q];
+                    V[k * 8 + p] = c * vkp - s * vkq;
+                    V[k * 8 + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    double wmax = 0;
+    for (int i = 0; i < 8; ++i) wmax = fmax(wmax, fabs(W[i * 8 + i]));
+    double tol = wmax * 8 * DBL_EPSILON;
+    for (int i = 0; i < 8; ++i) x[i] = 0;
+    for (int e = 0; e < 8; ++e) {
+        double w = W[e * 8 + e];
+        if (fabs(w) <= tol) continue;
+        double c = 0;
+        for (int k = 0; k < 8; ++k) c += V[k * 8 + e] * b[k];
+        c /= w;
+        for (int k = 0; k < 8; ++k) x[k] += c * V[k * 8 + e];
+    }
+}
+
+/* cv::LMSolver::run (levmarq.cpp, OpenCV 4.x LMSolverImpl): damping lambda * diag(A0)
+ * with A0 = J^T J at the start, gain-ratio schedule Rlo 0.25 / Rhi 0.75, lambda -> 0
+ * below lc, restart from 1/max diag(A^-1); stop after maxIters or when |d|inf <
+ * FLT_EPSILON or |r|inf < FLT_EPSILON.  Parameters h0..h7. */
+static int hom_lm_opencv(const float *sx, const float *sy, const float *dx, const float *dy, const uint8_t *mask,
+                         int n, double H[9], int max_iters) {
+    int m = 0;
+    for (int i = 0; i < n; ++i) m += mask[i] != 0;
+    if (m == 0) return 0;
+    m *= 2;
+    double *r = (double *)malloc(sizeof(double) * m * 2);
+    double *rd = r + m;
+    double *J = (double *)malloc(sizeof(double) * m * 8);
+    double x[9], xd[9], A[64], Ap[64], v[8], D[8], d[8], tmp[8];
+    memcpy(x, H, sizeof x);
+    memcpy(xd, H, sizeof xd);
+    hom_lm_compute(x, sx, sy, dx, dy, mask, n, r, J);
+    double S = 0;
+    for (int k = 0; k < m; ++k) S += r[k] * r[k];
+    lm_normal(J, r, m, A, v);
+    for (int a = 0; a < 8; ++a) D[a] = A[a * 8 + a];
+    const double Rlo = 0.25, Rhi = 0.75;
+    double lambda = 1, lc = 0.75;
+    int iter = 0;
+    for (;;) {
+        memcpy(Ap, A, sizeof Ap);
+        for (int a = 0; a < 8; ++a) Ap[a * 8 + a] += lambda * D[a];
+        sym_solve_eig(Ap, v, d);
+        for (int a = 0; a < 8; ++a) xd[a] = x[a] - d[a];
+        hom_lm_compute(xd, sx, sy, dx, dy, mask, n, rd, NULL);
+        double Sd = 0;
+        for (int k = 0; k < m; ++k) Sd += rd[k] * rd[k];
+        /* temp_d = 2 v - A d ; dS = d . temp_d */
+        double dS = 0;
+        for (int a = 0; a < 8; ++a) {
+            double ad = 0;
+            for (int b = 0; b < 8; ++b) ad += A[a * 8 + b] * d[b];
+            tmp[a] = 2 * v[a] - ad;
+            dS += d[a] * tmp[a];
+        }
+        double R = (S - Sd) / (fabs(dS) > DBL_EPSILON ? dS : 1);
+        if (R > Rhi) {
+            lambda *= 0.5;
+            if (lambda < lc) lambda = 0;
+        } else if (R < Rlo) {
+            double t = 0;
+            for (int a = 0; a < 8; ++a) t += d[a] * v[a];
+            double nu = (Sd - S) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
+            nu = fmin(fmax(nu, 2.), 10.);
+            if (lambda == 0) {
+                /* lc = 1 / max |diag(A^-1)| */
+                double Ai[64], e[8], col[8], maxval = DBL_EPSILON;
+                for (int c = 0; c < 8; ++c) {
+                    for (int a = 0; a < 8; ++a) e[a] = a == c;
+                    sym_solve_eig(A, e, col);
+                    for (int a = 0; a < 8; ++a) Ai[a * 8 + c] = col[a];
+                }
+                for (int a = 0; a < 8; ++a) maxval = fmax(maxval, fabs(Ai[a * 8 + a]));
+                lambda = lc = 1. / maxval;
+                nu *= 0.5;
+            }
+            lambda *= nu;
+        }
+        if (Sd < S) {
+            S = Sd;
+            memcpy(x, xd, 8 * sizeof(double));
+            hom_lm_compute(x, sx, sy, dx, dy, mask, n, r, J);
+            lm_normal(J, r, m, A, v);
+        }
+        iter++;
+        double dinf = 0, rinf = 0;
+        for (int a = 0; a < 8; ++a) dinf = fmax(dinf, fabs(d[a]));
+        for (int k = 0; k < m; ++k) rinf = fmax(rinf, fabs(r[k]));
+        if (!(iter < max_iters && dinf >= FLT_EPSILON && rinf >= FLT_EPSILON)) break;
+    }
+    memcpy(H, x, 8 * sizeof(double));
+    H[8] = 1.0;
+    free(r);
+    free(J);
+    return iter;
 }
 
 /* non-minimal refit of findHomography (fundam.cpp): least-squares
@@ -977,38 +1135,7 @@ ORC_API int orc_hom_refine(const float *sx, const float *sy, const float *dx, co
     double hv[9];
     jacobi_min_evec(9, LtL, hv);
     hom_denorm(&nm, hv, H);
-    /* LM, 10 iterations, 8 parameters (h22 fixed at 1) */
-    double lam = 1e-3;
-    double cost = hom_cost(H, sx, sy, dx, dy, mask, n);
-    for (int it = 0; it < 10; ++it) {
-        double A[64] = {0}, g[8] = {0};
-        for (int i = 0; i < n; ++i) {
-            if (!mask[i]) continue;
-            double x = sx[i], y = sy[i];
-            double den = H[6] * x + H[7] * y + 1.;
-            double ww = 1. / den;
-            double Xi = (H[0] * x + H[1] * y + H[2]) * ww;
-            double Yi = (H[3] * x + H[4] * y + H[5]) * ww;
-            double ex = Xi - dx[i], ey = Yi - dy[i];
-            double Jx[8] = {x * ww, y * ww, ww, 0, 0, 0, -Xi * x * ww, -Xi * y * ww};
-            double Jy[8] = {0, 0, 0, x * ww, y * ww, ww, -Yi * x * ww, -Yi * y * ww};
-            for (int a = 0; a < 8; ++a) {
-                g[a] += Jx[a] * ex + Jy[a] * ey;
-                for (int b = 0; b <= a; ++b) A[a * 8 + b] += Jx[a] * Jx[b] + Jy[a] * Jy[b];
-            }
-        }
-        for (int a = 0; a < 8; ++a)
-            for (int b = a + 1; b < 8; ++b) A[a * 8 + b] = A[b * 8 + a];
-        double d[8], mg[8];
-        for (int a = 0; a < 8; ++a) mg[a] = -g[a];
-        if (!chol_solve(8, A, lam, mg, d)) { lam *= 10; continue; }
-        double Hn[9];
-        for (int a = 0; a < 8; ++a) Hn[a] = H[a] + d[a];
-        Hn[8] = 1.0;
-        double cn = hom_cost(Hn, sx, sy, dx, dy, mask, n);
-        if (cn < cost) { memcpy(H, Hn, sizeof(Hn)); cost = cn; lam *= 0.1; }
-        else lam *= 10;
-    }
+    hom_lm_opencv(sx, sy, dx, dy, mask, n, H, 10);
     return 1;
 }
 

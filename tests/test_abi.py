@@ -71,3 +71,23 @@ def test_create_without_device_fails_cleanly():
     import rsac
     with pytest.raises(rsac.RsacError):
         rsac.pnp_ransac(np.zeros((10, 2)), np.zeros((10, 3)), np.eye(3))
+
+
+def test_host_homography_refit_matches_oracle_bitwise():
+    """findHomography's refit (runKernel DLT on the inliers + OpenCV's LMSolver, 10 iterations) is
+    host C++ in librsac; it must equal the restatement bit for bit (same IEEE operation order)."""
+    import json
+    import os
+
+    import pyoracle as O
+    import rsac
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "debuglog_homography.json")))
+    for b in [b for b in d["blocks"] if b["complete"]]:
+        M = np.array(b["M"])
+        pp2 = np.array(b["pp2"])
+        hs = np.c_[pp2, np.ones(len(pp2))] @ M.T
+        src, dst = hs[:, :2] / hs[:, 2:3], np.array(b["p1"], np.float64)
+        mask = np.array(b["mask"], np.uint8)
+        H = rsac.homography_fit(src, dst, mask)
+        Ho = O.hom_refine(O.soa_hom(src, dst), mask, np.eye(3))
+        np.testing.assert_array_equal(H, Ho)

@@ -344,3 +344,58 @@ def test_parallel_driver_single_rank_equals_pnp_ransac():
     fixed = par.sharded_best(ev, 20000)
     st, cn = ev.hypotheses(0, 20000)
     assert par.pack_key(fixed.n_inliers, fixed.best) == par.best_key_of(cn, st, 0)
+
+
+# ---------------------------------------------------------------------------------------------
+# camera-location search (main_v1.py:254-348, 419, 862-866)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed,thr", [(0, 75.0), (1, 120.0), (2, 75.0)])
+def test_location_search_matches_restatement(seed, thr):
+    pr = synth.location_problem(seed=seed)
+    res = rsac.location_search(pr["pos3d"], pr["pixels"], pr["locations"], thr)
+    assert res.n_good == int(np.count_nonzero(np.any(pr["pixels"] != 0, axis=1)))
+    ref = [O.find_homography(pr["pixels"], pr["pos3d"], loc, thr) for loc in pr["locations"]]
+    for l, r in enumerate(ref):
+        assert res.ok[l] == (r["M"] is not None)
+        np.testing.assert_array_equal(res.mask[l], r["mask"])
+        if r["M"] is not None:
+            np.testing.assert_array_equal(res.H[l], r["H"])  # RANSAC + host refit are bit-exact
+    err = np.array([[r["err1"], r["err2"]] for r in ref])
+    np.testing.assert_allclose(res.err, err, rtol=1e-9, atol=1e-9)
+    assert res.best == O.best_location(err)
+
+
+def test_location_search_reference_shaped_driver():
+    from rsac.location import best_location, find_homographies
+    pr = synth.location_problem(seed=3, n_locations=60)
+    recs = [{"pixel": p, "pos3d": q, "symbol": str(i)} for i, (p, q) in enumerate(zip(pr["pixels"], pr["pos3d"]))]
+    grid = np.arange(60) % 7 - 1  # grid_code -1 locations are skipped (main_v1.py:276-282)
+    locs = [{"grid_code": g, "pos3d": q} for g, q in zip(grid, pr["locations"])]
+    nm = find_homographies(recs, locs, 75.0)
+    assert np.all(nm[grid < 0] == 0)
+    for l in np.flatnonzero(grid >= 0)[:10]:
+        r = O.find_homography(pr["pixels"], pr["pos3d"], pr["locations"][l], 75.0)
+        np.testing.assert_allclose(nm[l], [r["err1"], r["err2"]], rtol=1e-9)
+    assert best_location(nm) == O.best_location(nm)
+
+
+def test_location_search_debuglog_masks():
+    """Each debug.log findHomography call as a one-location search: pos3d = (1, sy, sx) makes pos2 =
+    src exactly, so the search must reproduce the logged RANSAC masks (thr 120)."""
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "debuglog_homography.json")))
+    for b in [b for b in d["blocks"] if b["complete"]]:
+        M = np.array(b["M"])
+        pp2 = np.array(b["pp2"])
+        hs = np.c_[pp2, np.ones(len(pp2))] @ M.T
+        src = hs[:, :2] / hs[:, 2:3]
+        pos3d = np.c_[np.ones(len(src)), src[:, 1], src[:, 0]]
+        res = rsac.location_search(pos3d, np.array(b["p1"]), np.zeros((1, 3)), d["threshold"])
+        np.testing.assert_array_equal(res.mask[0], np.array(b["mask"], bool))
+
+
+def test_location_search_too_few_noted_features():
+    pr = synth.location_problem(seed=4)
+    px = pr["pixels"].copy()
+    px[3:] = 0
+    with pytest.raises(rsac.RsacError):
+        rsac.location_search(pr["pos3d"], px, pr["locations"][:5], 75.0)

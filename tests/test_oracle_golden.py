@@ -59,19 +59,34 @@ def test_debuglog_threshold_75_does_not_reproduce():
     assert agree < 12
 
 
-def test_debuglog_refit_not_worse_than_logged_on_most_blocks():
+def test_debuglog_refit_close_to_logged_reprojections():
+    """findHomography's refit (runKernel DLT on the inliers + LMSolver, 10 iterations) is NOT pinned:
+    src is recovered through the logged M (cond ~1.8e7) and the OpenCV version is unknown, so the
+    logged H is matched only loosely -- the refit's reprojections of the inliers agree with the
+    logged ones (pp2) to a median within thr/4 on all but the 3 near-degenerate 7-inlier blocks."""
     blocks, thr = _blocks()
-    better = 0
+    close = 0
     for b in blocks:
         src, dst = _src_dst(b)
         res = O.hom_ransac(src, dst, thr, 0.995, 2000, sampler="opencv")
         m = res["mask"]
         pr = np.c_[src, np.ones(len(src))] @ res["H_refined"].T
         pr = pr[:, :2] / pr[:, 2:3]
-        mine = (np.linalg.norm(pr - dst, axis=1)[m] ** 2).sum()
-        ref = (np.linalg.norm(np.array(b["pp2"]) - dst, axis=1)[m] ** 2).sum()
-        better += mine <= ref * 1.001
-    assert better >= 20
+        close += np.median(np.linalg.norm(pr - np.array(b["pp2"]), axis=1)[m]) <= thr / 4
+    assert close >= 21
+
+
+def test_debuglog_location_errors_reproduced():
+    """err1 of find_homography (main_v1.py:332-347) from the logged M and mask equals the sum of the
+    logged per-feature distances (test02.py's log lines) -- pins the scorer's formula."""
+    blocks, thr = _blocks()
+    for b in blocks:
+        src, dst = _src_dst(b)
+        mask = np.array(b["mask"])
+        e1, e2 = O.location_errors(src, dst, np.array(b["M"]), mask, thr)
+        ref = float(np.sum(np.array(b["distance"])[mask == 1]))
+        assert abs(e1 - ref) <= 1e-8 * ref
+        assert e2 >= np.sum(1 - mask) * thr
 
 
 def test_philox_known_answers():
