@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--cpu-hyps", type=int, default=150_000, help="CPU baseline sample (hypotheses, 1 thread)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ms-to-best", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C3 batch and location-search lines")
     return ap.parse_args()
 
 
@@ -151,6 +152,7 @@ def main():
             if i >= 2:
                 host_ms.append((time.perf_counter() - t) * 1e3)
         pcie_rate = H / (statistics.median(host_ms) * 1e-3)
+        extras = {} if args.no_extras else extra_workloads(local, args)
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(pr, args)
@@ -179,11 +181,46 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_pnp_score", "algorithmic_bytes_per_launch": args.points * BYTES_PER_POINT * H},
             "cpu_baseline": cpu,
+            "extras": extras,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return out
+
+
+def extra_workloads(local, args):
+    """Secondary lines (not `value`): C3 of BASELINE.json (1024 problems x 2000 points, 1024
+    hypotheses each, one batched call) and the 458-location search of main_v1.py:274/862."""
+    out = {}
+    probs = [synth.pnp_problem(2000, 0.5, seed=s) for s in range(1, 1025)]
+    p2 = [p["points2d"] for p in probs]
+    p3 = [p["points3d"] for p in probs]
+    Ks = [p["K"] for p in probs]
+    walls = []
+    for i in range(4):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        rsac.pnp_ransac_batched(p2, p3, Ks, 1024, args.thr, adaptive=False, refine=False, device=local)
+        torch.cuda.synchronize()
+        if i >= 1:
+            walls.append(time.perf_counter() - t)
+    w = statistics.median(walls)
+    out["c3_batched"] = {"problems": 1024, "points": 2000, "hyps_per_problem": 1024, "ms": w * 1e3,
+                         "hyp_s": 1024 * 1024 / w,
+                         "note": "host f64 inputs, per-problem winners + masks, adaptive off, no refit"}
+    lp = synth.location_problem(seed=0)
+    walls = []
+    for i in range(6):
+        t = time.perf_counter()
+        rsac.location_search(lp["pos3d"], lp["pixels"], lp["locations"], 75.0, device=local)
+        if i >= 1:
+            walls.append(time.perf_counter() - t)
+    out["location_search"] = {"locations": len(lp["locations"]), "features": len(lp["pos3d"]),
+                              "ms": statistics.median(walls) * 1e3,
+                              "note": "find_homographies of main_v1.py:254-297 (OpenCV-sampler RANSAC + LM refit + "
+                                      "err1/err2) for every candidate, one call"}
     return out
 
 

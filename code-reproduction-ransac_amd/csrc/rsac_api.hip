@@ -12,7 +12,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rsac.h"
@@ -42,6 +44,25 @@ static int fail(int code, const char *fmt, ...) {
     } while (0)
 
 namespace {
+
+// Run f(p) for p in [0, P) on up to 16 host threads (the per-problem refits of a
+// batch are independent; each writes only its own outputs).
+template <class F>
+void parallel_for(int P, F f) {
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nt = std::min({hw, 16, (P + 7) / 8});
+    if (nt <= 1) {
+        for (int p = 0; p < P; ++p) f(p);
+        return;
+    }
+    std::atomic<int> next{0};
+    std::vector<std::thread> pool;
+    for (int k = 0; k < nt; ++k)
+        pool.emplace_back([&] {
+            for (int p; (p = next.fetch_add(1)) < P;) f(p);
+        });
+    for (auto &t : pool) t.join();
+}
 
 struct DevBuf {
     void *p = nullptr;
@@ -116,6 +137,11 @@ struct Staged {
     int P = 0;
     int64_t total = 0;
     std::vector<int64_t> off;
+    int32_t max_n() const {
+        int64_t m = 0;
+        for (size_t p = 0; p + 1 < off.size(); ++p) m = std::max(m, off[p + 1] - off[p]);
+        return (int32_t)m;
+    }
     const float *d[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // device SoA
     std::vector<float> hbuf;                                            // host SoA copy (refits, MWC check)
     const float *h[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -248,6 +274,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     a = PnpArgs{};
     a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
     a.offsets = c->d_off;
+    a.max_n = st.max_n();
     a.cams = c->d_cams;
     a.thr2 = c->d_thr2;
     a.models = c->models.as<double>();
@@ -323,28 +350,13 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
     SETARG(subsets, (const int32_t *)nullptr);
     SETARG(sub_status, (const int8_t *)nullptr);
 
-    if (flags & RSAC_F_SAMPLER_OPENCV) {
-        // OpenCV's subset sequence is sequential in one MWC state per call:
-        // generate the whole budget on the host (cheap), upload once.
-        int32_t *hs = c->h_subsets.as<int32_t>();
-        int8_t *hss = c->h_substatus.as<int8_t>();
-        for (int p = 0; p < P; ++p) {
-            const int np = (int)(st.off[p + 1] - st.off[p]);
-            Mwc rng;
-            int32_t *o = hs + (size_t)p * stride * 4;
-            int8_t *os = hss + (size_t)p * stride;
-            if (np < 4) {
-                memset(os, -1, stride);
-                continue;
-            }
-            const float *hom[4];
-            if (model == Model::Hom) {
-                for (int k = 0; k < 4; ++k) hom[k] = st.h[k] + st.off[p];
-            }
-            mwc_subsets(rng, np, stride, model == Model::Hom ? hom : nullptr, o, os);
-        }
-        HIPCHK(hipMemcpyAsync(c->subsets.p, hs, sizeof(int32_t) * 4 * P * stride, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(c->substatus.p, hss, (size_t)P * stride, hipMemcpyHostToDevice, s));
+    // OpenCV's subset sequence is sequential in one MWC state per problem and call: the
+    // states persist across rounds, each round's slice is drawn on the host (problems in
+    // parallel) and uploaded before its solve
+    const bool opencv = (flags & RSAC_F_SAMPLER_OPENCV) != 0;
+    std::vector<Mwc> rngs;
+    if (opencv) {
+        rngs.assign(P, Mwc());
         SETARG(subsets, c->subsets.as<int32_t>());
         SETARG(sub_status, c->substatus.as<int8_t>());
     }
@@ -352,8 +364,33 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
 
     out.scan.assign(P, ScanState());
     for (auto &sc : out.scan) sc.reset((int)H);
-    for (int64_t hb = 0; hb < H; hb += round) {
-        const int32_t Hr = (int32_t)std::min<int64_t>(round, H - hb);
+    // adaptive: the first round is short (most runs stop within it), later ones double
+    int64_t cur = adaptive ? std::min<int64_t>(round, 256) : round;
+    for (int64_t hb = 0, Hr = 0; hb < H; hb += Hr) {
+        Hr = std::min<int64_t>(cur, H - hb);
+        cur = std::min<int64_t>(cur * 2, round);
+        if (opencv) {
+            int32_t *hs = c->h_subsets.as<int32_t>();
+            int8_t *hss = c->h_substatus.as<int8_t>();
+            parallel_for(P, [&](int p) {
+                int8_t *os = hss + (size_t)p * stride + hb;
+                const int np = (int)(st.off[p + 1] - st.off[p]);
+                if (np < 4 || out.scan[p].done) {  // nothing to draw: the solve skips status < 0
+                    memset(os, -1, Hr);
+                    return;
+                }
+                const float *hom[4];
+                if (model == Model::Hom)
+                    for (int k = 0; k < 4; ++k) hom[k] = st.h[k] + st.off[p];
+                mwc_subsets(rngs[p], np, Hr, model == Model::Hom ? hom : nullptr, hs + ((size_t)p * stride + hb) * 4,
+                            os);
+            });
+            HIPCHK(hipMemcpy2DAsync(c->subsets.as<int32_t>() + hb * 4, sizeof(int32_t) * 4 * stride, hs + hb * 4,
+                                    sizeof(int32_t) * 4 * stride, sizeof(int32_t) * 4 * Hr, P, hipMemcpyHostToDevice,
+                                    s));
+            HIPCHK(hipMemcpy2DAsync(c->substatus.as<int8_t>() + hb, stride, hss + hb, stride, Hr, P,
+                                    hipMemcpyHostToDevice, s));
+        }
         HIPCHK(hipEventRecord(c->ev0, s));
         if (pa) {
             HIPCHK(launch_pnp_solve(*pa, P, hb, Hr, s));
@@ -478,8 +515,7 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         r = host_mask(c, st, mask_out, flags, s, tmpmask, &hm);
         if (r) return r;
     }
-    int any = 0;
-    for (int p = 0; p < P; ++p) {
+    parallel_for(P, [&](int p) {
         const ScanState &sc = lo.scan[p];
         double R[9], t[3];
         memcpy(R, bm + kModelStride * p, sizeof R);
@@ -495,8 +531,9 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         if (t_out) memcpy(t_out + 3 * p, t, sizeof t);
         if (status_out) status_out[p] = ok ? RSAC_OK : RSAC_NO_MODEL;
         if (ninl_out) ninl_out[p] = sc.max_good;
-        any |= ok;
-    }
+    });
+    int any = 0;
+    for (int p = 0; p < P; ++p) any |= lo.scan[p].best >= 0;
     if (stats) {
         stats->best_hyp = lo.scan[0].best;
         stats->iters = lo.scan[0].iter;
@@ -529,6 +566,7 @@ int hom_core(rsac_ctx *c, const void *src, const void *dst, const int64_t *offse
     HomArgs a{};
     a.SX = st.d[0]; a.SY = st.d[1]; a.DX = st.d[2]; a.DY = st.d[3];
     a.offsets = c->d_off;
+    a.max_n = st.max_n();
     a.thr2 = c->d_thr2;
     a.seed = seed;
     a.rng_base = 0;
@@ -545,8 +583,7 @@ int hom_core(rsac_ctx *c, const void *src, const void *dst, const int64_t *offse
         r = host_mask(c, st, mask_out, flags, s, tmpmask, &hm);
         if (r) return r;
     }
-    int any = 0;
-    for (int p = 0; p < P; ++p) {
+    parallel_for(P, [&](int p) {
         const ScanState &sc = lo.scan[p];
         double Hm[9];
         memcpy(Hm, bm + kModelStride * p, sizeof Hm);
@@ -560,8 +597,9 @@ int hom_core(rsac_ctx *c, const void *src, const void *dst, const int64_t *offse
         if (H_out) memcpy(H_out + 9 * p, Hm, sizeof Hm);
         if (status_out) status_out[p] = ok ? RSAC_OK : RSAC_NO_MODEL;
         if (ninl_out) ninl_out[p] = sc.max_good;
-        any |= ok;
-    }
+    });
+    int any = 0;
+    for (int p = 0; p < P; ++p) any |= lo.scan[p].best >= 0;
     if (stats) {
         stats->best_hyp = lo.scan[0].best;
         stats->iters = lo.scan[0].iter;
@@ -876,6 +914,7 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
         HomArgs a{};
         a.SX = st.d[0]; a.SY = st.d[1]; a.DX = st.d[2]; a.DY = st.d[3];
         a.offsets = c->d_off;
+        a.max_n = st.max_n();
         a.thr2 = c->d_thr2;
         a.models = c->models.as<double>();
         a.status = c->status.as<int8_t>();
@@ -933,6 +972,7 @@ int rsac_pnp_mask(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, 
     PnpArgs a{};
     a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
     a.offsets = c->d_off;
+    a.max_n = st.max_n();
     a.cams = c->d_cams;
     a.thr2 = c->d_thr2;
     a.models = c->models.as<double>();

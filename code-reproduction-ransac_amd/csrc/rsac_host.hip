@@ -221,40 +221,49 @@ int pnp_refine_lm(const float *X, const float *Y, const float *Z, const float *U
     return it;
 }
 
-static void jacobi_min_evec(int n, double *A, double *v_out) {
-    double V[81];
+// Symmetric eigen-decomposition by cyclic Jacobi (cv::eigen's method): A (n x n,
+// destroyed) -> eigenvalues on the diagonal, eigenvectors in the columns of V.
+// Stops when the off-diagonal mass is below 1e-32 of the matrix's.
+static void jacobi_sym(int n, double *A, double *V) {
+    double frob = 0;
+    for (int i = 0; i < n * n; ++i) frob += A[i] * A[i];
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; ++sweep) {
         double off = 0;
         for (int i = 0; i < n; ++i)
             for (int j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
-        if (off < 1e-300) break;
+        if (off <= 1e-32 * frob || off < 1e-300) break;
         for (int p = 0; p < n; ++p)
             for (int q = p + 1; q < n; ++q) {
-                double apq = A[p * n + q];
+                const double apq = A[p * n + q];
                 if (fabs(apq) < 1e-300) continue;
-                double app = A[p * n + p], aqq = A[q * n + q];
-                double theta = (aqq - app) / (2.0 * apq);
-                double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
+                const double app = A[p * n + p], aqq = A[q * n + q];
+                const double theta = (aqq - app) / (2.0 * apq);
+                const double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
                 for (int k = 0; k < n; ++k) {
-                    double akp = A[k * n + p], akq = A[k * n + q];
+                    const double akp = A[k * n + p], akq = A[k * n + q];
                     A[k * n + p] = c * akp - s * akq;
                     A[k * n + q] = s * akp + c * akq;
                 }
                 for (int k = 0; k < n; ++k) {
-                    double apk = A[p * n + k], aqk = A[q * n + k];
+                    const double apk = A[p * n + k], aqk = A[q * n + k];
                     A[p * n + k] = c * apk - s * aqk;
                     A[q * n + k] = s * apk + c * aqk;
                 }
                 for (int k = 0; k < n; ++k) {
-                    double vkp = V[k * n + p], vkq = V[k * n + q];
+                    const double vkp = V[k * n + p], vkq = V[k * n + q];
                     V[k * n + p] = c * vkp - s * vkq;
                     V[k * n + q] = s * vkp + c * vkq;
                 }
             }
     }
+}
+
+static void jacobi_min_evec(int n, double *A, double *v_out) {
+    double V[81];
+    jacobi_sym(n, A, V);
     int mi = 0;
     for (int i = 1; i < n; ++i)
         if (A[i * n + i] < A[mi * n + mi]) mi = i;
@@ -299,54 +308,44 @@ static void normal_eqs(const double *J, const double *r, int m, double *A, doubl
     }
 }
 
-// x = A^+ b through the symmetric eigen-decomposition (cv::solve DECOMP_EIG):
-// cyclic Jacobi, eigenvalues |w| <= 8 eps max|w| dropped
-static void solve_eig8(const double *A, const double *b, double *x) {
-    double W[64], V[64];
+// 8x8 symmetric A -> eigenvalues W (diagonal), vectors V; |w| <= 8 eps max|w|
+// zeroed, as cv::solve / cv::invert with DECOMP_EIG drop them
+static void eig8(const double *A, double *W, double *V) {
     std::copy(A, A + 64, W);
-    for (int i = 0; i < 8; ++i)
-        for (int j = 0; j < 8; ++j) V[i * 8 + j] = (i == j) ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 60; ++sweep) {
-        double off = 0;
-        for (int i = 0; i < 8; ++i)
-            for (int j = i + 1; j < 8; ++j) off += W[i * 8 + j] * W[i * 8 + j];
-        if (off < 1e-300) break;
-        for (int p = 0; p < 8; ++p)
-            for (int q = p + 1; q < 8; ++q) {
-                const double apq = W[p * 8 + q];
-                if (fabs(apq) < 1e-300) continue;
-                const double theta = (W[q * 8 + q] - W[p * 8 + p]) / (2.0 * apq);
-                const double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
-                for (int k = 0; k < 8; ++k) {
-                    const double akp = W[k * 8 + p], akq = W[k * 8 + q];
-                    W[k * 8 + p] = c * akp - s * akq;
-                    W[k * 8 + q] = s * akp + c * akq;
-                }
-                for (int k = 0; k < 8; ++k) {
-                    const double apk = W[p * 8 + k], aqk = W[q * 8 + k];
-                    W[p * 8 + k] = c * apk - s * aqk;
-                    W[q * 8 + k] = s * apk + c * aqk;
-                }
-                for (int k = 0; k < 8; ++k) {
-                    const double vkp = V[k * 8 + p], vkq = V[k * 8 + q];
-                    V[k * 8 + p] = c * vkp - s * vkq;
-                    V[k * 8 + q] = s * vkp + c * vkq;
-                }
-            }
-    }
+    jacobi_sym(8, W, V);
     double wmax = 0;
     for (int i = 0; i < 8; ++i) wmax = fmax(wmax, fabs(W[i * 8 + i]));
     const double tol = wmax * 8 * DBL_EPSILON;
+    for (int i = 0; i < 8; ++i)
+        if (fabs(W[i * 8 + i]) <= tol) W[i * 8 + i] = 0;
+}
+
+// x = A^+ b (cv::solve DECOMP_EIG)
+static void solve_eig8(const double *A, const double *b, double *x) {
+    double W[64], V[64];
+    eig8(A, W, V);
     std::fill(x, x + 8, 0.0);
     for (int e = 0; e < 8; ++e) {
         const double w = W[e * 8 + e];
-        if (fabs(w) <= tol) continue;
+        if (w == 0) continue;
         double c = 0;
         for (int k = 0; k < 8; ++k) c += V[k * 8 + e] * b[k];
         c /= w;
         for (int k = 0; k < 8; ++k) x[k] += c * V[k * 8 + e];
     }
+}
+
+// max_a |(A^+)_aa| (cv::invert DECOMP_EIG, diagonal only)
+static double max_diag_pinv(const double *A) {
+    double W[64], V[64], maxval = DBL_EPSILON;
+    eig8(A, W, V);
+    for (int a = 0; a < 8; ++a) {
+        double d = 0;
+        for (int e = 0; e < 8; ++e)
+            if (W[e * 8 + e] != 0) d += V[a * 8 + e] * V[a * 8 + e] / W[e * 8 + e];
+        maxval = fmax(maxval, fabs(d));
+    }
+    return maxval;
 }
 
 // cv::LMSolver::run of OpenCV 4.x (levmarq.cpp, LMSolverImpl) on h0..h7:
@@ -395,12 +394,7 @@ static int hom_lm(const float *sx, const float *sy, const float *dx, const float
             double nu = (Sd - S) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
             nu = fmin(fmax(nu, 2.), 10.);
             if (lambda == 0) {
-                double e[8], col[8], maxval = DBL_EPSILON;
-                for (int c = 0; c < 8; ++c) {
-                    for (int a = 0; a < 8; ++a) e[a] = a == c;
-                    solve_eig8(A, e, col);
-                    maxval = fmax(maxval, fabs(col[c]));
-                }
+                const double maxval = max_diag_pinv(A);
                 lambda = lc = 1. / maxval;
                 nu *= 0.5;
             }

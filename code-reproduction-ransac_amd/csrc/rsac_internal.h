@@ -39,6 +39,7 @@ struct PnpArgs {
     // (count << 32) | (0xFFFFFFFF - low32(rng_base + h)), atomically into *best_key
     unsigned long long *best_key;
     int *queue;  // work-queue counter of the f32 scoring kernel (reset by launch_pnp_frame)
+    int32_t max_n;  // largest problem (points); small problems score one lane per hypothesis
 };
 
 constexpr int kFrameStride = 8;
@@ -56,7 +57,12 @@ struct HomArgs {
     int64_t hyp_stride;
     int64_t rng_base;
     uint64_t seed;
+    int32_t max_n;  // largest problem (points)
 };
+
+// problems with at most this many points are scored one lane per hypothesis
+// (all points staged in LDS) instead of the points-across-lanes tiles
+constexpr int kLanePts = 256;
 
 // mask of the hypothesis a packed key names (problem 0, records at hyp 0..)
 hipError_t launch_pnp_mask_key(const PnpArgs &a, int32_t n, const unsigned long long *key, uint8_t *mask,

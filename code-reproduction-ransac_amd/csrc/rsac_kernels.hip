@@ -200,6 +200,7 @@ __device__ __forceinline__ void write_fmodel(const double *R, const double *t, b
 __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
     const int prob = blockIdx.y;
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a.queue && h == 0 && prob == 0) *a.queue = 0;  // the scoring launch that follows starts its queue at 0
     if (h >= H) return;
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
     const double *m = a.models + rec * kModelStride;
@@ -213,6 +214,8 @@ __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
 __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
     const int hl = blockIdx.x * blockDim.x + threadIdx.x;
+    // every round's scoring launch follows a solve on the same stream: reset its work queue here
+    if (a.queue && hl == 0 && prob == 0) *a.queue = 0;
     if (hl >= H) return;
     const int64_t h = hyp_begin + hl;
     const int64_t p0 = a.offsets[prob];
@@ -879,6 +882,76 @@ __global__ __launch_bounds__(256) void k_hom_score(HomArgs a, int64_t hyp_begin,
     }
 }
 
+// Small problems (<= kLanePts points: the 12-feature scenes of main_v1.py and
+// testpro-K.py): one lane per hypothesis over all of the problem's points,
+// staged once per block in LDS.  The tile kernels would leave most lanes idle.
+__global__ __launch_bounds__(256) void k_hom_score_lane(HomArgs a, int64_t hyp_begin, int32_t H,
+                                                        int32_t *__restrict__ counts) {
+    __shared__ float sp[4][kLanePts];
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    for (int i = threadIdx.x; i < n; i += 256) {
+        sp[0][i] = a.SX[p0 + i]; sp[1][i] = a.SY[p0 + i]; sp[2][i] = a.DX[p0 + i]; sp[3][i] = a.DY[p0 + i];
+    }
+    __syncthreads();
+    const int hl = blockIdx.x * 256 + threadIdx.x;
+    if (hl >= H) return;
+    const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
+    const double *__restrict__ m = a.models + rec * kModelStride;
+    int cnt = 0;
+    if (m[kValidSlot] != 0.0) {
+        const float thr2 = a.thr2[prob];
+        float hf[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) hf[q] = (float)m[q];
+        for (int i = 0; i < n; ++i) cnt += hom_err(hf, sp[0][i], sp[1][i], sp[2][i], sp[3][i]) <= thr2;
+    }
+    counts[rec] = cnt;
+}
+
+// PnP twin: the exact f64 error (pnp_err, the oracle's formula) per pair -- at
+// these sizes the f32 pre-filter buys nothing.  Optional fused best key.
+__global__ __launch_bounds__(256) void k_pnp_score_lane(PnpArgs a, int64_t hyp_begin, int32_t H,
+                                                        int32_t *__restrict__ counts) {
+    __shared__ float sp[5][kLanePts];
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    for (int i = threadIdx.x; i < n; i += 256) {
+        sp[0][i] = a.X[p0 + i]; sp[1][i] = a.Y[p0 + i]; sp[2][i] = a.Z[p0 + i];
+        sp[3][i] = a.U[p0 + i]; sp[4][i] = a.V[p0 + i];
+    }
+    __syncthreads();
+    const int hl = blockIdx.x * 256 + threadIdx.x;
+    int cnt = 0;
+    if (hl < H) {
+        const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
+        const double *__restrict__ m = a.models + rec * kModelStride;
+        if (m[kValidSlot] != 0.0) {
+            const double *cm = a.cams + 4 * prob;
+            const Cam k{cm[0], cm[1], cm[2], cm[3]};
+            const float thr2 = a.thr2[prob];
+            for (int i = 0; i < n; ++i)
+                cnt += pnp_err(m, m + 9, k, (double)sp[0][i], (double)sp[1][i], (double)sp[2][i], sp[3][i],
+                               sp[4][i]) <= thr2;
+        }
+        counts[rec] = cnt;
+    }
+    if (a.best_key) {
+        unsigned long long key = 0;
+        if (hl < H && cnt > 0) {
+            const uint64_t g = (uint64_t)(a.rng_base + hyp_begin + hl);
+            key = ((unsigned long long)(uint32_t)cnt << 32) | (0xFFFFFFFFull - (g & 0xFFFFFFFFull));
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long other = __shfl_xor(key, o);
+            key = other > key ? other : key;
+        }
+        if ((threadIdx.x & 63) == 0 && key) atomicMax(a.best_key, key);
+    }
+}
+
 __global__ void k_hom_mask(HomArgs a, const int64_t *__restrict__ best, uint8_t *__restrict__ mask) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
@@ -1018,7 +1091,9 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
 
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    if (a.fmodels && !a.exact_only) {
+    if (a.max_n > 0 && a.max_n <= kLanePts) {
+        hipLaunchKernelGGL(k_pnp_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
+    } else if (a.fmodels && !a.exact_only) {
         switch (g_score_variant) {
             case 1: launch_f32<4, 32>(a, P, hyp_begin, H, counts, s); break;
             case 2: launch_f32<8, 64>(a, P, hyp_begin, H, counts, s); break;
@@ -1058,8 +1133,11 @@ hipError_t launch_hom_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int3
 
 hipError_t launch_hom_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    hipLaunchKernelGGL((k_hom_score<kScoreP, kScoreHB>), dim3(cdiv(H, kScoreHB), P), dim3(256), 0, s, a, hyp_begin, H,
-                       counts);
+    if (a.max_n > 0 && a.max_n <= kLanePts)
+        hipLaunchKernelGGL(k_hom_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
+    else
+        hipLaunchKernelGGL((k_hom_score<kScoreP, kScoreHB>), dim3(cdiv(H, kScoreHB), P), dim3(256), 0, s, a, hyp_begin,
+                           H, counts);
     return hipGetLastError();
 }
 

@@ -31,7 +31,8 @@ def _pnp_case(n, outl, seed):
 
 
 @pytest.mark.parametrize("n,outl,seed,H", [(4, 0.0, 1, 256), (5, 0.2, 2, 256), (12, 0.3, 3, 512),
-                                           (100, 0.5, 4, 1000), (1000, 0.5, 5, 700), (2999, 0.6, 6, 333)])
+                                           (100, 0.5, 4, 1000), (256, 0.5, 8, 300), (257, 0.5, 8, 300),
+                                           (1000, 0.5, 5, 700), (2999, 0.6, 6, 333)])
 def test_pnp_hypotheses_bit_exact_philox(n, outl, seed, H):
     pr, soa, cam = _pnp_case(n, outl, seed)
     st, cnt, mdl = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 17, H, 30.0, seed=seed)
@@ -399,3 +400,23 @@ def test_location_search_too_few_noted_features():
     px[3:] = 0
     with pytest.raises(rsac.RsacError):
         rsac.location_search(pr["pos3d"], px, pr["locations"][:5], 75.0)
+
+
+@pytest.mark.parametrize("sampler", ["philox", "opencv"])
+def test_many_rounds_equal_sequential_loop(sampler):
+    """Adaptive runs over many rounds (first round 64, doubling) must give the sequential loop's
+    best, count and iteration count: every round's scoring launch starts a fresh work queue and
+    the OpenCV MWC state carries over between rounds."""
+    from rsac import _lib as L
+    pr = synth.pnp_problem(1500, 0.85, seed=77)
+    ctx = L.context(0)
+    L.check(L.lib().rsac_set_round_size(ctx.handle, 64))
+    try:
+        R, t, m, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 3000, 30.0, sampler=sampler,
+                                        refine=False, return_info=True)
+    finally:
+        L.check(L.lib().rsac_set_round_size(ctx.handle, 4096))
+    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 3000, 0x5EED, sampler=sampler)
+    assert info.rounds > 3
+    assert (info.best_hyp, info.n_inliers, info.iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    np.testing.assert_array_equal(m, ref["mask"])
