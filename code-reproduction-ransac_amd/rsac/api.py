@@ -232,6 +232,41 @@ def pnp_ransac_batched(points2D_list, points3D_list, K_list, n_iters: int = 5000
     return out
 
 
+def pnp_ransac_batched_flat(points2D, points3D, offsets, Ks, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
+                            confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox",
+                            adaptive: bool = True, refine: bool = True, device=None):
+    """Batched PnP over problems already concatenated: points2D (N,2), points3D (N,3) f64 (numpy,
+    or torch cuda tensors that stay on the device), offsets (P+1) int64, Ks (P,3,3).
+
+    Returns (R (P,3,3), t (P,3), ok (P,) bool, n_inliers (P,), mask (N,) bool -- on the device
+    for device inputs).  Same results as pnp_ransac_batched on the split lists.
+    """
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    off = np.ascontiguousarray(np.asarray(offsets, np.int64).reshape(-1))
+    P = off.size - 1
+    if P < 1 or off[0] != 0 or off[-1] != p3.n or p2.n != p3.n:
+        raise ValueError("offsets must run from 0 to the number of points")
+    if np.diff(off).min() < 4:
+        raise ValueError("every problem needs >= 4 correspondences")
+    Kf = np.ascontiguousarray(np.asarray(Ks, np.float64).reshape(P, 9))
+    ctx = L.context(_device_of(p3, device))
+    flags = _flags(adaptive, refine, sampler) | (L.F_DEVICE_IN if p3.device else 0)
+    mask, mptr, mflag = _mask_buffer(p3, p3.n)
+    flags |= mflag
+    R = np.zeros((P, 9))
+    t = np.zeros((P, 3))
+    status = np.zeros(P, np.int32)
+    ninl = np.zeros(P, np.int32)
+    with ctx.lock:
+        L.check(L.lib().rsac_pnp_ransac_batched(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), off.ctypes.data, P,
+                                                Kf.ctypes.data, int(n_iters), float(reproj_thresh), float(confidence),
+                                                int(seed) & (2**64 - 1), flags, R.ctypes.data, t.ctypes.data,
+                                                status.ctypes.data, ninl.ctypes.data, C.c_void_p(mptr),
+                                                _stream_of(p3)))
+    return R.reshape(P, 3, 3), t, status == L.OK, ninl, _finish_mask(mask, p3.n)
+
+
 def homography_ransac_batched(src_list, dst_list, reproj_thresh: float = 3.0, *, max_iters: int = 2000,
                               confidence: float = 0.995, seed: int = 0x5EED, sampler: str = "opencv",
                               adaptive: bool = True, refine: bool = True, device: int = 0):

@@ -420,3 +420,22 @@ def test_many_rounds_equal_sequential_loop(sampler):
     assert info.rounds > 3
     assert (info.best_hyp, info.n_inliers, info.iters) == (ref["best"], ref["n_inliers"], ref["iters"])
     np.testing.assert_array_equal(m, ref["mask"])
+
+
+def test_batched_flat_device_inputs_equal_lists():
+    import torch
+    probs = [synth.pnp_problem(n, 0.5, seed=90 + i) for i, n in enumerate([300, 2000, 40, 1200])]
+    lists = rsac.pnp_ransac_batched([p["points2d"] for p in probs], [p["points3d"] for p in probs],
+                                    [p["K"] for p in probs], 600, 30.0, adaptive=False, refine=False)
+    off = np.r_[0, np.cumsum([len(p["points3d"]) for p in probs])]
+    p2 = torch.from_numpy(np.concatenate([p["points2d"] for p in probs])).cuda()
+    p3 = torch.from_numpy(np.concatenate([p["points3d"] for p in probs])).cuda()
+    R, t, ok, ninl, mask = rsac.pnp_ransac_batched_flat(p2, p3, off, np.stack([p["K"] for p in probs]), 600, 30.0,
+                                                        adaptive=False, refine=False)
+    assert mask.is_cuda
+    mask = mask.cpu().numpy()
+    for i, (Rl, tl, ml, nl) in enumerate(lists):
+        assert ok[i] == (Rl is not None) and ninl[i] == nl
+        np.testing.assert_array_equal(R[i], Rl)
+        np.testing.assert_array_equal(t[i], tl)
+        np.testing.assert_array_equal(mask[off[i]:off[i + 1]], ml)
