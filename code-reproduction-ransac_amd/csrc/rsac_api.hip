@@ -506,32 +506,22 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     if (r) return r;
     r = finish_masks(c, Model::PnP, st, &a, lo, stride, mask_out, flags, s);
     if (r) return r;
-    const double *bm = c->h_bestmodels.as<double>();
-    std::vector<uint8_t> tmpmask;
-    const uint8_t *hm = nullptr;
     if (flags & RSAC_F_REFINE) {
-        r = ensure_host_points(st, 5, s);
-        if (r) return r;
-        r = host_mask(c, st, mask_out, flags, s, tmpmask, &hm);
-        if (r) return r;
+        // final refit on the device, one block per problem, on the RANSAC-phase inliers
+        const uint8_t *dmask = (flags & RSAC_F_DEVICE_OUT) && mask_out ? mask_out : c->mask.as<uint8_t>();
+        HIPCHK(launch_pnp_refine(a, P, dmask, c->bestmodels.as<double>(), nullptr, s));
+        HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
     }
-    parallel_for(P, [&](int p) {
-        const ScanState &sc = lo.scan[p];
-        double R[9], t[3];
-        memcpy(R, bm + kModelStride * p, sizeof R);
-        memcpy(t, bm + kModelStride * p + 9, sizeof t);
-        const bool ok = sc.best >= 0;
-        if (ok && (flags & RSAC_F_REFINE)) {
-            const int64_t o = st.off[p];
-            const int np = (int)(st.off[p + 1] - o);
-            const double cam[4] = {K[9 * p], K[9 * p + 4], K[9 * p + 2], K[9 * p + 5]};
-            pnp_refine_lm(st.h[0] + o, st.h[1] + o, st.h[2] + o, st.h[3] + o, st.h[4] + o, hm + o, np, cam, R, t, 20);
-        }
-        if (R_out) memcpy(R_out + 9 * p, R, sizeof R);
-        if (t_out) memcpy(t_out + 3 * p, t, sizeof t);
+    const double *bm = c->h_bestmodels.as<double>();
+    for (int p = 0; p < P; ++p) {
+        const bool ok = lo.scan[p].best >= 0;
+        if (R_out) memcpy(R_out + 9 * p, bm + kModelStride * p, 9 * sizeof(double));
+        if (t_out) memcpy(t_out + 3 * p, bm + kModelStride * p + 9, 3 * sizeof(double));
         if (status_out) status_out[p] = ok ? RSAC_OK : RSAC_NO_MODEL;
-        if (ninl_out) ninl_out[p] = sc.max_good;
-    });
+        if (ninl_out) ninl_out[p] = lo.scan[p].max_good;
+    }
     int any = 0;
     for (int p = 0; p < P; ++p) any |= lo.scan[p].best >= 0;
     if (stats) {

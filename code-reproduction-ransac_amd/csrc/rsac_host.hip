@@ -114,110 +114,41 @@ void rodrigues_m2v(const double R[9], double r[3]) {
     r[0] = rx * vth; r[1] = ry * vth; r[2] = rz * vth;
 }
 
-// (A + lam diag(A)) x = b, A n x n SPD (row-major), Cholesky
-static bool chol_solve(int n, const double *A, double lam, const double *b, double *x) {
-    double L[81], y[9];
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j <= i; ++j) {
-            double s = A[i * n + j];
-            if (i == j) s = s + lam * A[i * n + i];
-            for (int k = 0; k < j; ++k) s = s - L[i * n + k] * L[j * n + k];
-            if (i == j) {
-                if (!(s > 0)) return false;
-                L[i * n + i] = sqrt(s);
-            } else {
-                L[i * n + j] = s / L[j * n + j];
-            }
-        }
-    for (int i = 0; i < n; ++i) {
-        double s = b[i];
-        for (int k = 0; k < i; ++k) s = s - L[i * n + k] * y[k];
-        y[i] = s / L[i * n + i];
-    }
-    for (int i = n - 1; i >= 0; --i) {
-        double s = y[i];
-        for (int k = i + 1; k < n; ++k) s = s - L[k * n + i] * x[k];
-        x[i] = s / L[i * n + i];
-    }
-    return true;
-}
+namespace {
 
-static double pnp_cost(const double R[9], const double t[3], const double cam[4], const float *X, const float *Y,
-                       const float *Z, const float *U, const float *V, const uint8_t *mask, int n) {
-    double cost = 0;
-    for (int i = 0; i < n; ++i) {
-        if (!mask[i]) continue;
-        double Xd = X[i], Yd = Y[i], Zd = Z[i];
-        double x = R[0] * Xd + R[1] * Yd + R[2] * Zd + t[0];
-        double y = R[3] * Xd + R[4] * Yd + R[5] * Zd + t[1];
-        double z = R[6] * Xd + R[7] * Yd + R[8] * Zd + t[2];
-        double iz = 1.0 / z;
-        double ru = cam[0] * x * iz + cam[2] - U[i];
-        double rv = cam[1] * y * iz + cam[3] - V[i];
-        cost += ru * ru + rv * rv;
+// host reducer of pnp_lm_refine: the GPU kernel's summation order (rsac_math.h)
+struct HostLmReducer {
+    const float *X, *Y, *Z, *U, *V;
+    const uint8_t *mask;
+    int n;
+    Cam k;
+    double c[3];  // centre of the refit frame
+    std::vector<double> part = std::vector<double>((size_t)kLmThreads * kLmTerms);
+    void normal(const double *R, const double *t, double *acc) {
+        lm_reduce_host(n, mask, kLmTerms, part.data(), acc, [&](int i, double *a) {
+            pnp_lm_point(R, t, k, (double)X[i] - c[0], (double)Y[i] - c[1], (double)Z[i] - c[2], (double)U[i],
+                         (double)V[i], a);
+        });
     }
-    return cost;
-}
+    double cost(const double *R, const double *t) {
+        double s;
+        lm_reduce_host(n, mask, 1, part.data(), &s, [&](int i, double *a) {
+            a[0] += pnp_lm_cost_point(R, t, k, (double)X[i] - c[0], (double)Y[i] - c[1], (double)Z[i] - c[2],
+                                      (double)U[i], (double)V[i]);
+        });
+        return s;
+    }
+};
+
+}  // namespace
 
 int pnp_refine_lm(const float *X, const float *Y, const float *Z, const float *U, const float *V, const uint8_t *mask,
                   int n, const double cam[4], double R[9], double t[3], int max_iter) {
-    double lam = 1e-3;
-    double cost = pnp_cost(R, t, cam, X, Y, Z, U, V, mask, n);
-    int it;
-    for (it = 0; it < max_iter; ++it) {
-        double A[36] = {0}, g[6] = {0};
-        for (int i = 0; i < n; ++i) {
-            if (!mask[i]) continue;
-            double Xd = X[i], Yd = Y[i], Zd = Z[i];
-            double px = R[0] * Xd + R[1] * Yd + R[2] * Zd;
-            double py = R[3] * Xd + R[4] * Yd + R[5] * Zd;
-            double pz = R[6] * Xd + R[7] * Yd + R[8] * Zd;
-            double cx = px + t[0], cy = py + t[1], cz = pz + t[2];
-            double iz = 1.0 / cz;
-            double ru = cam[0] * cx * iz + cam[2] - U[i];
-            double rv = cam[1] * cy * iz + cam[3] - V[i];
-            double dux = cam[0] * iz, duz = -cam[0] * cx * iz * iz;
-            double dvy = cam[1] * iz, dvz = -cam[1] * cy * iz * iz;
-            double Ju[6], Jv[6];
-            Ju[0] = duz * py;             Ju[1] = dux * pz - duz * px; Ju[2] = -dux * py;
-            Jv[0] = -dvy * pz + dvz * py; Jv[1] = -dvz * px;           Jv[2] = dvy * px;
-            Ju[3] = dux; Ju[4] = 0; Ju[5] = duz;
-            Jv[3] = 0; Jv[4] = dvy; Jv[5] = dvz;
-            for (int a = 0; a < 6; ++a) {
-                g[a] += Ju[a] * ru + Jv[a] * rv;
-                for (int b = 0; b <= a; ++b) A[a * 6 + b] += Ju[a] * Ju[b] + Jv[a] * Jv[b];
-            }
-        }
-        for (int a = 0; a < 6; ++a)
-            for (int b = a + 1; b < 6; ++b) A[a * 6 + b] = A[b * 6 + a];
-        bool accepted = false;
-        while (!accepted) {
-            double d[6], mg[6];
-            for (int a = 0; a < 6; ++a) mg[a] = -g[a];
-            if (!chol_solve(6, A, lam, mg, d)) {
-                lam *= 10;
-                if (lam > 1e10) return it;
-                continue;
-            }
-            double Rw[9], Rn[9], tn[3];
-            rodrigues_v2m(d, Rw);
-            mat3mul(Rw, R, Rn);
-            for (int k = 0; k < 3; ++k) tn[k] = t[k] + d[3 + k];
-            double cn = pnp_cost(Rn, tn, cam, X, Y, Z, U, V, mask, n);
-            if (cn < cost) {
-                double rel = (cost - cn) / (cost > 1e-300 ? cost : 1e-300);
-                memcpy(R, Rn, sizeof(Rn));
-                memcpy(t, tn, sizeof(tn));
-                cost = cn;
-                lam = lam * 0.1 > 1e-12 ? lam * 0.1 : 1e-12;
-                accepted = true;
-                if (rel < 1e-12) return it + 1;
-            } else {
-                lam *= 10;
-                if (lam > 1e10) return it;
-            }
-        }
-    }
+    if (n <= 0) return 0;
+    HostLmReducer red{X, Y, Z, U, V, mask, n, Cam{cam[0], cam[1], cam[2], cam[3]}, {(double)X[0], (double)Y[0], (double)Z[0]}};
+    lm_to_centred(R, red.c, t);
+    const int it = pnp_lm_refine(red, R, t, max_iter);
+    lm_from_centred(R, red.c, t);
     return it;
 }
 

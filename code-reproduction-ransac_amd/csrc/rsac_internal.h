@@ -102,6 +102,11 @@ hipError_t launch_hom_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int3
 hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
                            hipStream_t s);
 
+// LM refit of every problem's model record (models: P x kModelStride, R 9, t 3, valid)
+// on the inliers of mask (concatenated points), one block per problem
+hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
+                             hipStream_t s);
+
 // camera-location search (main_v1.py:254-348): pos2 of every (location, feature) pair, then
 // err1 / err2 of every location's homography
 hipError_t launch_loc_pos2(const double *p3, const double *px, int32_t n, const double *locs, int32_t L, double *src,

@@ -1271,4 +1271,86 @@ hipError_t launch_loc_score(const double *src, const double *dst, const uint8_t 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Final pose refit of every problem's winner on its RANSAC inliers (LM of
+// rsac_math.h, the final solvePnP step), one block per problem.  The block's
+// reductions use the summation order the host (rsac_pnp_refine) and the oracle
+// mirror, so the refined pose is bit-identical on every backend.
+// ---------------------------------------------------------------------------
+struct GpuLmReducer {
+    const float *X, *Y, *Z, *U, *V;
+    const uint8_t *mask;
+    int n;
+    Cam k;
+    double c0, c1, c2;  // centre of the refit frame
+    double (*wsum)[kLmTerms];  // LDS [kLmThreads / 64][kLmTerms]
+
+    __device__ void reduce(double *a, int nv, double *out) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        for (int q = 0; q < nv; ++q) {
+            for (int o = 32; o > 0; o >>= 1) a[q] = a[q] + __shfl_xor(a[q], o);
+            if (lane == 0) wsum[wave][q] = a[q];
+        }
+        __syncthreads();
+        for (int q = 0; q < nv; ++q) {
+            double s = wsum[0][q];
+            for (int w = 1; w < kLmThreads / 64; ++w) s = s + wsum[w][q];
+            out[q] = s;
+        }
+        __syncthreads();  // wsum is reused by the next reduction
+    }
+    __device__ void normal(const double *R, const double *t, double *acc) {
+        double a[kLmTerms];
+        for (int q = 0; q < kLmTerms; ++q) a[q] = 0.0;
+        for (int i = threadIdx.x; i < n; i += kLmThreads)
+            if (mask[i])
+                pnp_lm_point(R, t, k, (double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i],
+                             (double)V[i], a);
+        reduce(a, kLmTerms, acc);
+    }
+    __device__ double cost(const double *R, const double *t) {
+        double a = 0.0, out;
+        for (int i = threadIdx.x; i < n; i += kLmThreads)
+            if (mask[i])
+                a += pnp_lm_cost_point(R, t, k, (double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i],
+                                       (double)V[i]);
+        reduce(&a, 1, &out);
+        return out;
+    }
+};
+
+__global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint8_t *__restrict__ mask,
+                                                           double *__restrict__ models, int32_t *__restrict__ iters) {
+    __shared__ double wsum[kLmThreads / 64][kLmTerms];
+    const int prob = blockIdx.x;
+    double *m = models + (int64_t)prob * kModelStride;
+    if (m[kValidSlot] == 0.0) {  // no model: block-uniform exit
+        if (threadIdx.x == 0 && iters) iters[prob] = 0;
+        return;
+    }
+    const int64_t p0 = a.offsets[prob];
+    const double *cm = a.cams + 4 * prob;
+    const double c[3] = {(double)a.X[p0], (double)a.Y[p0], (double)a.Z[p0]};
+    GpuLmReducer red{a.X + p0, a.Y + p0, a.Z + p0, a.U + p0, a.V + p0, mask + p0,
+                     (int)(a.offsets[prob + 1] - p0), Cam{cm[0], cm[1], cm[2], cm[3]}, c[0], c[1], c[2], wsum};
+    double R[9], t[3];
+    for (int j = 0; j < 9; ++j) R[j] = m[j];
+    for (int j = 0; j < 3; ++j) t[j] = m[9 + j];
+    lm_to_centred(R, c, t);
+    const int it = pnp_lm_refine(red, R, t, kLmMaxIter);
+    lm_from_centred(R, c, t);
+    __syncthreads();  // every thread has read m before thread 0 overwrites it
+    if (threadIdx.x == 0) {
+        for (int j = 0; j < 9; ++j) m[j] = R[j];
+        for (int j = 0; j < 3; ++j) m[9 + j] = t[j];
+        if (iters) iters[prob] = it;
+    }
+}
+
+hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(k_pnp_refine, dim3(P), dim3(kLmThreads), 0, s, a, mask, models, iters);
+    return hipGetLastError();
+}
+
 }  // namespace rsac

@@ -472,4 +472,182 @@ RSAC_HD float hom_err(const float *h, float x, float y, float u, float v) {
     return e1 + e2;
 }
 
+// ---------------------------------------------------------------------------
+// Pose refinement: Levenberg-Marquardt on the reprojection error of the
+// inliers (the final solvePnP / solvePnPRefineLM step, main_v1.py:508-509,
+// testpro-K.py:122-125).  Parameters: a rotation increment d[0..2] applied as
+// R <- Cay(d) R (Cayley map: + - * / only, so every backend rounds the same)
+// and a translation increment d[3..5].  The pose is refined in a frame centred
+// on the problem's first point c (X - c exact in f64; t' = R c + t): UTM-scale
+// coordinates would otherwise couple rotation and translation badly.
+//
+// One summation order on every backend (GPU kernel k_pnp_refine, host
+// rsac_pnp_refine, oracle orc_pnp_refine): kLmThreads strided per-thread
+// partials (point i to thread i % kLmThreads, ascending), a 64-lane butterfly
+// per wave (x += x[lane ^ o], o = 32 .. 1), then the wave sums left to right.
+// ---------------------------------------------------------------------------
+constexpr int kLmThreads = 512;
+constexpr int kLmTerms = 27;  // J^T J lower triangle (21, row-major packed), J^T r (6)
+constexpr int kLmMaxIter = 20;
+
+// adds point (X, Y, Z) -> (u, v)'s terms of J^T J and J^T r to acc
+RSAC_HD void pnp_lm_point(const double *R, const double *t, const Cam &k, double Xd, double Yd, double Zd, double u,
+                          double v, double *acc) {
+    const double px = R[0] * Xd + R[1] * Yd + R[2] * Zd;
+    const double py = R[3] * Xd + R[4] * Yd + R[5] * Zd;
+    const double pz = R[6] * Xd + R[7] * Yd + R[8] * Zd;
+    const double cx = px + t[0], cy = py + t[1], cz = pz + t[2];
+    const double iz = 1.0 / cz;
+    const double ru = k.fx * cx * iz + k.cx - u;
+    const double rv = k.fy * cy * iz + k.cy - v;
+    const double dux = k.fx * iz, duz = -k.fx * cx * iz * iz;
+    const double dvy = k.fy * iz, dvz = -k.fy * cy * iz * iz;
+    double Ju[6], Jv[6];
+    Ju[0] = duz * py;             Ju[1] = dux * pz - duz * px; Ju[2] = -dux * py;
+    Jv[0] = -dvy * pz + dvz * py; Jv[1] = -dvz * px;           Jv[2] = dvy * px;
+    Ju[3] = dux; Ju[4] = 0; Ju[5] = duz;
+    Jv[3] = 0; Jv[4] = dvy; Jv[5] = dvz;
+    int q = 0;
+    for (int a = 0; a < 6; ++a)
+        for (int b = 0; b <= a; ++b, ++q) acc[q] += Ju[a] * Ju[b] + Jv[a] * Jv[b];
+    for (int a = 0; a < 6; ++a) acc[21 + a] += Ju[a] * ru + Jv[a] * rv;
+}
+
+RSAC_HD double pnp_lm_cost_point(const double *R, const double *t, const Cam &k, double Xd, double Yd, double Zd,
+                                 double u, double v) {
+    const double x = R[0] * Xd + R[1] * Yd + R[2] * Zd + t[0];
+    const double y = R[3] * Xd + R[4] * Yd + R[5] * Zd + t[1];
+    const double z = R[6] * Xd + R[7] * Yd + R[8] * Zd + t[2];
+    const double iz = 1.0 / z;
+    const double ru = k.fx * x * iz + k.cx - u;
+    const double rv = k.fy * y * iz + k.cy - v;
+    return ru * ru + rv * rv;
+}
+
+// (A + lam diag(A)) x = b, A 6 x 6 SPD row-major; false if not positive definite
+RSAC_HD bool chol6_solve(const double *A, double lam, const double *b, double *x) {
+    double L[36], y[6];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double s = A[i * 6 + j];
+            if (i == j) s = s + lam * A[i * 6 + i];
+            for (int q = 0; q < j; ++q) s = s - L[i * 6 + q] * L[j * 6 + q];
+            if (i == j) {
+                if (!(s > 0)) return false;
+                L[i * 6 + i] = dsqrt(s);
+            } else {
+                L[i * 6 + j] = s / L[j * 6 + j];
+            }
+        }
+    for (int i = 0; i < 6; ++i) {
+        double s = b[i];
+        for (int q = 0; q < i; ++q) s = s - L[i * 6 + q] * y[q];
+        y[i] = s / L[i * 6 + i];
+    }
+    for (int i = 5; i >= 0; --i) {
+        double s = y[i];
+        for (int q = i + 1; q < 6; ++q) s = s - L[q * 6 + i] * x[q];
+        x[i] = s / L[i * 6 + i];
+    }
+    return true;
+}
+
+// Rn = Cay(d) R, Cay(d) = the rotation of the quaternion (1, d/2) (first order: I + [d]x)
+RSAC_HD void cayley_apply(const double *d, const double *R, double *Rn) {
+    const double w0 = 0.5 * d[0], w1 = 0.5 * d[1], w2 = 0.5 * d[2];
+    const double a = w0 * w0, b = w1 * w1, c = w2 * w2;
+    const double is = 1.0 / (1.0 + a + b + c);
+    double Q[9];
+    Q[0] = (1.0 + a - b - c) * is;       Q[1] = 2.0 * (w0 * w1 - w2) * is; Q[2] = 2.0 * (w0 * w2 + w1) * is;
+    Q[3] = 2.0 * (w0 * w1 + w2) * is;    Q[4] = (1.0 - a + b - c) * is;   Q[5] = 2.0 * (w1 * w2 - w0) * is;
+    Q[6] = 2.0 * (w0 * w2 - w1) * is;    Q[7] = 2.0 * (w1 * w2 + w0) * is; Q[8] = (1.0 - a - b + c) * is;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Rn[3 * i + j] = Q[3 * i] * R[j] + Q[3 * i + 1] * R[3 + j] + Q[3 * i + 2] * R[6 + j];
+}
+
+// The LM loop.  Red provides normal(R, t, acc[27]) and cost(R, t), reduced in the
+// order above; on the GPU every thread of the block runs this loop in lockstep
+// (all decisions depend on reduced, block-uniform values).  Returns iterations.
+template <class Red>
+RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
+    double lam = 1e-3;
+    double cost = red.cost(R, t);
+    int it;
+    for (it = 0; it < max_iter; ++it) {
+        double acc[kLmTerms];
+        red.normal(R, t, acc);
+        double A[36], g[6];
+        int q = 0;
+        for (int a = 0; a < 6; ++a)
+            for (int b = 0; b <= a; ++b, ++q) A[a * 6 + b] = A[b * 6 + a] = acc[q];
+        for (int a = 0; a < 6; ++a) g[a] = -acc[21 + a];
+        bool accepted = false;
+        while (!accepted) {
+            double d[6];
+            if (!chol6_solve(A, lam, g, d)) {
+                lam *= 10;
+                if (lam > 1e10) return it;
+                continue;
+            }
+            double Rn[9], tn[3];
+            cayley_apply(d, R, Rn);
+            for (int j = 0; j < 3; ++j) tn[j] = t[j] + d[3 + j];
+            const double cn = red.cost(Rn, tn);
+            if (cn < cost) {
+                const double rel = (cost - cn) / (cost > 1e-300 ? cost : 1e-300);
+                for (int j = 0; j < 9; ++j) R[j] = Rn[j];
+                for (int j = 0; j < 3; ++j) t[j] = tn[j];
+                cost = cn;
+                lam = lam * 0.1 > 1e-12 ? lam * 0.1 : 1e-12;
+                accepted = true;
+                // converged: negligible cost decrease, or a step below FLT_EPSILON relative to
+                // the pose (CvLevMarq's criterion for solvePnP, on |d| / (|t| + 1))
+                double dd = 0, tt = 0;
+                for (int j = 0; j < 6; ++j) dd += d[j] * d[j];
+                for (int j = 0; j < 3; ++j) tt += t[j] * t[j];
+                if (rel < 1e-12 || dsqrt(dd) < 1.1920928955078125e-07 * (dsqrt(tt) + 1.0)) return it + 1;
+            } else {
+                lam *= 10;
+                if (lam > 1e10) return it;
+            }
+        }
+    }
+    return it;
+}
+
+// t' = R c + t and back (the centred frame of the refit)
+RSAC_HD void lm_to_centred(const double *R, const double *c, double *t) {
+    for (int j = 0; j < 3; ++j) t[j] = R[3 * j] * c[0] + R[3 * j + 1] * c[1] + R[3 * j + 2] * c[2] + t[j];
+}
+RSAC_HD void lm_from_centred(const double *R, const double *c, double *t) {
+    for (int j = 0; j < 3; ++j) t[j] = t[j] - (R[3 * j] * c[0] + R[3 * j + 1] * c[1] + R[3 * j + 2] * c[2]);
+}
+
+// Host/oracle-side mirror of the GPU reduction: sum f(i, acc) over points with
+// mask[i] != 0 in the kLmThreads-strided, wave-butterfly order.  part: scratch of
+// kLmThreads * nv doubles.
+template <class F>
+inline void lm_reduce_host(int n, const uint8_t *mask, int nv, double *part, double *out, F f) {
+    for (int q = 0; q < kLmThreads * nv; ++q) part[q] = 0.0;
+    for (int tid = 0; tid < kLmThreads; ++tid)
+        for (int i = tid; i < n; i += kLmThreads)
+            if (mask[i]) f(i, part + tid * nv);
+    double wsum[kLmThreads / 64][kLmTerms];
+    double v[64], w[64];
+    for (int wv = 0; wv < kLmThreads / 64; ++wv)
+        for (int q = 0; q < nv; ++q) {
+            for (int l = 0; l < 64; ++l) v[l] = part[(wv * 64 + l) * nv + q];
+            for (int o = 32; o > 0; o >>= 1) {
+                for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
+                for (int l = 0; l < 64; ++l) v[l] = w[l];
+            }
+            wsum[wv][q] = v[0];
+        }
+    for (int q = 0; q < nv; ++q) {
+        double s = wsum[0][q];
+        for (int wv = 1; wv < kLmThreads / 64; ++wv) s = s + wsum[wv][q];
+        out[q] = s;
+    }
+}
+
 }  // namespace rsac

@@ -787,110 +787,171 @@ ORC_API void orc_rodrigues_m2v(const double R[9], double r[3]) {
 /* Final refits (non-minimal solve on the RANSAC inliers).                   */
 /* ------------------------------------------------------------------------ */
 
-/* Solve the n x n SPD system (A + lam*diag(A)) x = b by Cholesky. */
-static int chol_solve(int n, const double *A, double lam, const double *b, double *x) {
-    double L[81];
-    for (int i = 0; i < n; ++i)
+/* Pose LM (final solvePnP / solvePnPRefineLM, main_v1.py:508-509,
+ * testpro-K.py:122-125): increments d = (rotation 3, translation 3), R <- Cay(d) R
+ * (Cayley map), damping lam*diag(J^T J), lam x0.1 on success / x10 on failure,
+ * at most 20 iterations, stop when the relative cost decrease < 1e-12 or
+ * |d| < FLT_EPSILON (|t| + 1) (CvLevMarq's step criterion of solvePnP).
+ * The pose is refined in the frame centred on the first point c (t' = R c + t).
+ * Sums use the GPU kernel's order: 512 strided per-thread partials, a 64-lane
+ * butterfly per wave (x += x[lane ^ o], o = 32..1), then the 8 wave sums left to right --
+ * so the HIP kernel k_pnp_refine reproduces this bit for bit. */
+#define LM_THREADS 512
+#define LM_TERMS 27
+
+typedef struct { const float *X, *Y, *Z, *U, *V; const uint8_t *mask; int n; double cam[4]; double *part; double c[3]; } lmctx;
+
+static void lm_point(const lmctx *c, const double *R, const double *t, int i, double *acc) {
+    double Xd = (double)c->X[i] - c->c[0], Yd = (double)c->Y[i] - c->c[1], Zd = (double)c->Z[i] - c->c[2];
+    double u = c->U[i], v = c->V[i];
+    double px = R[0] * Xd + R[1] * Yd + R[2] * Zd;
+    double py = R[3] * Xd + R[4] * Yd + R[5] * Zd;
+    double pz = R[6] * Xd + R[7] * Yd + R[8] * Zd;
+    double cx = px + t[0], cy = py + t[1], cz = pz + t[2];
+    double iz = 1.0 / cz;
+    double ru = c->cam[0] * cx * iz + c->cam[2] - u;
+    double rv = c->cam[1] * cy * iz + c->cam[3] - v;
+    double dux = c->cam[0] * iz, duz = -c->cam[0] * cx * iz * iz;
+    double dvy = c->cam[1] * iz, dvz = -c->cam[1] * cy * iz * iz;
+    double Ju[6], Jv[6];
+    Ju[0] = duz * py;             Ju[1] = dux * pz - duz * px; Ju[2] = -dux * py;
+    Jv[0] = -dvy * pz + dvz * py; Jv[1] = -dvz * px;           Jv[2] = dvy * px;
+    Ju[3] = dux; Ju[4] = 0; Ju[5] = duz;
+    Jv[3] = 0; Jv[4] = dvy; Jv[5] = dvz;
+    int q = 0;
+    for (int a = 0; a < 6; ++a)
+        for (int b = 0; b <= a; ++b, ++q) acc[q] += Ju[a] * Ju[b] + Jv[a] * Jv[b];
+    for (int a = 0; a < 6; ++a) acc[21 + a] += Ju[a] * ru + Jv[a] * rv;
+}
+
+static double lm_cost_point(const lmctx *c, const double *R, const double *t, int i) {
+    double Xd = (double)c->X[i] - c->c[0], Yd = (double)c->Y[i] - c->c[1], Zd = (double)c->Z[i] - c->c[2];
+    double u = c->U[i], v = c->V[i];
+    double x = R[0] * Xd + R[1] * Yd + R[2] * Zd + t[0];
+    double y = R[3] * Xd + R[4] * Yd + R[5] * Zd + t[1];
+    double z = R[6] * Xd + R[7] * Yd + R[8] * Zd + t[2];
+    double iz = 1.0 / z;
+    double ru = c->cam[0] * x * iz + c->cam[2] - u;
+    double rv = c->cam[1] * y * iz + c->cam[3] - v;
+    return ru * ru + rv * rv;
+}
+
+/* nv = LM_TERMS: normal equations; nv = 1: cost */
+static void lm_reduce(lmctx *c, const double *R, const double *t, int nv, double *out) {
+    double *part = c->part;
+    for (int q = 0; q < LM_THREADS * nv; ++q) part[q] = 0.0;
+    for (int tid = 0; tid < LM_THREADS; ++tid)
+        for (int i = tid; i < c->n; i += LM_THREADS) {
+            if (!c->mask[i]) continue;
+            if (nv == 1) part[tid] += lm_cost_point(c, R, t, i);
+            else lm_point(c, R, t, i, part + tid * nv);
+        }
+    double wsum[LM_THREADS / 64][LM_TERMS], v[64], w[64];
+    for (int wv = 0; wv < LM_THREADS / 64; ++wv)
+        for (int q = 0; q < nv; ++q) {
+            for (int l = 0; l < 64; ++l) v[l] = part[(wv * 64 + l) * nv + q];
+            for (int o = 32; o > 0; o >>= 1) {
+                for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
+                for (int l = 0; l < 64; ++l) v[l] = w[l];
+            }
+            wsum[wv][q] = v[0];
+        }
+    for (int q = 0; q < nv; ++q) {
+        double s = wsum[0][q];
+        for (int wv = 1; wv < LM_THREADS / 64; ++wv) s = s + wsum[wv][q];
+        out[q] = s;
+    }
+}
+
+/* (A + lam diag(A)) x = b, A 6x6 SPD, Cholesky */
+static int chol6(const double *A, double lam, const double *b, double *x) {
+    double L[36], y[6];
+    for (int i = 0; i < 6; ++i)
         for (int j = 0; j <= i; ++j) {
-            double s = A[i * n + j];
-            if (i == j) s = s + lam * A[i * n + i];
-            for (int k = 0; k < j; ++k) s = s - L[i * n + k] * L[j * n + k];
+            double s = A[i * 6 + j];
+            if (i == j) s = s + lam * A[i * 6 + i];
+            for (int k = 0; k < j; ++k) s = s - L[i * 6 + k] * L[j * 6 + k];
             if (i == j) {
                 if (!(s > 0)) return 0;
-                L[i * n + i] = sqrt(s);
+                L[i * 6 + i] = sqrt(s);
             } else {
-                L[i * n + j] = s / L[j * n + j];
+                L[i * 6 + j] = s / L[j * 6 + j];
             }
         }
-    double y[9];
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < 6; ++i) {
         double s = b[i];
-        for (int k = 0; k < i; ++k) s = s - L[i * n + k] * y[k];
-        y[i] = s / L[i * n + i];
+        for (int k = 0; k < i; ++k) s = s - L[i * 6 + k] * y[k];
+        y[i] = s / L[i * 6 + i];
     }
-    for (int i = n - 1; i >= 0; --i) {
+    for (int i = 5; i >= 0; --i) {
         double s = y[i];
-        for (int k = i + 1; k < n; ++k) s = s - L[k * n + i] * x[k];
-        x[i] = s / L[i * n + i];
+        for (int k = i + 1; k < 6; ++k) s = s - L[k * 6 + i] * x[k];
+        x[i] = s / L[i * 6 + i];
     }
     return 1;
 }
 
-static double pnp_cost(const double R[9], const double t[3], const double cam[4], const float *X, const float *Y,
-                       const float *Z, const float *U, const float *V, const uint8_t *mask, int n) {
-    double cost = 0;
-    for (int i = 0; i < n; ++i) {
-        if (!mask[i]) continue;
-        double Xd = X[i], Yd = Y[i], Zd = Z[i];
-        double x = R[0] * Xd + R[1] * Yd + R[2] * Zd + t[0];
-        double y = R[3] * Xd + R[4] * Yd + R[5] * Zd + t[1];
-        double z = R[6] * Xd + R[7] * Yd + R[8] * Zd + t[2];
-        double iz = 1.0 / z;
-        double ru = cam[0] * x * iz + cam[2] - U[i];
-        double rv = cam[1] * y * iz + cam[3] - V[i];
-        cost += ru * ru + rv * rv;
-    }
-    return cost;
+/* Rn = Cay(d) R: the rotation of the quaternion (1, d/2) */
+static void cayley(const double *d, const double *R, double *Rn) {
+    double w0 = 0.5 * d[0], w1 = 0.5 * d[1], w2 = 0.5 * d[2];
+    double a = w0 * w0, b = w1 * w1, c = w2 * w2;
+    double is = 1.0 / (1.0 + a + b + c);
+    double Q[9];
+    Q[0] = (1.0 + a - b - c) * is;       Q[1] = 2.0 * (w0 * w1 - w2) * is; Q[2] = 2.0 * (w0 * w2 + w1) * is;
+    Q[3] = 2.0 * (w0 * w1 + w2) * is;    Q[4] = (1.0 - a + b - c) * is;   Q[5] = 2.0 * (w1 * w2 - w0) * is;
+    Q[6] = 2.0 * (w0 * w2 - w1) * is;    Q[7] = 2.0 * (w1 * w2 + w0) * is; Q[8] = (1.0 - a - b + c) * is;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Rn[3 * i + j] = Q[3 * i] * R[j] + Q[3 * i + 1] * R[3 + j] + Q[3 * i + 2] * R[6 + j];
 }
 
-/* Levenberg-Marquardt on the masked points, R <- Exp(w) R, t <- t + dt
- * (the role of solvePnPRefineLM / the ITERATIVE final solvePnP,
- * main_v1.py:508, testpro-K.py:122).  Returns iterations used. */
 ORC_API int orc_pnp_refine(const float *X, const float *Y, const float *Z, const float *U, const float *V,
                            const uint8_t *mask, int n, const double cam[4], double R[9], double t[3], int max_iter) {
-    double lam = 1e-3;
-    double cost = pnp_cost(R, t, cam, X, Y, Z, U, V, mask, n);
+    if (n <= 0) return 0;
+    lmctx c = {X, Y, Z, U, V, mask, n, {cam[0], cam[1], cam[2], cam[3]}, NULL, {X[0], Y[0], Z[0]}};
+    c.part = (double *)malloc(sizeof(double) * LM_THREADS * LM_TERMS);
+    /* refit frame centred on the first point: t' = R c + t */
+    for (int j = 0; j < 3; ++j) t[j] = R[3 * j] * c.c[0] + R[3 * j + 1] * c.c[1] + R[3 * j + 2] * c.c[2] + t[j];
+    double lam = 1e-3, cost, acc[LM_TERMS];
+    lm_reduce(&c, R, t, 1, &cost);
     int it;
     for (it = 0; it < max_iter; ++it) {
-        double A[36] = {0}, g[6] = {0};
-        for (int i = 0; i < n; ++i) {
-            if (!mask[i]) continue;
-            double Xd = X[i], Yd = Y[i], Zd = Z[i];
-            double px = R[0] * Xd + R[1] * Yd + R[2] * Zd;
-            double py = R[3] * Xd + R[4] * Yd + R[5] * Zd;
-            double pz = R[6] * Xd + R[7] * Yd + R[8] * Zd;
-            double cx = px + t[0], cy = py + t[1], cz = pz + t[2];
-            double iz = 1.0 / cz;
-            double ru = cam[0] * cx * iz + cam[2] - U[i];
-            double rv = cam[1] * cy * iz + cam[3] - V[i];
-            double dux = cam[0] * iz, duz = -cam[0] * cx * iz * iz;
-            double dvy = cam[1] * iz, dvz = -cam[1] * cy * iz * iz;
-            /* d(c)/dw = -[p]x : rows (0, pz, -py), (-pz, 0, px), (py, -px, 0) */
-            double Ju[6], Jv[6];
-            Ju[0] = duz * py;            Ju[1] = dux * pz - duz * px; Ju[2] = -dux * py;
-            Jv[0] = -dvy * pz + dvz * py; Jv[1] = -dvz * px;           Jv[2] = dvy * px;
-            Ju[3] = dux; Ju[4] = 0; Ju[5] = duz;
-            Jv[3] = 0; Jv[4] = dvy; Jv[5] = dvz;
-            for (int a = 0; a < 6; ++a) {
-                g[a] += Ju[a] * ru + Jv[a] * rv;
-                for (int b = 0; b <= a; ++b) A[a * 6 + b] += Ju[a] * Ju[b] + Jv[a] * Jv[b];
-            }
-        }
+        double A[36], g[6];
+        lm_reduce(&c, R, t, LM_TERMS, acc);
+        int q = 0;
         for (int a = 0; a < 6; ++a)
-            for (int b = a + 1; b < 6; ++b) A[a * 6 + b] = A[b * 6 + a];
+            for (int b = 0; b <= a; ++b, ++q) A[a * 6 + b] = A[b * 6 + a] = acc[q];
+        for (int a = 0; a < 6; ++a) g[a] = -acc[21 + a];
         int accepted = 0;
         while (!accepted) {
-            double d[6], mg[6];
-            for (int a = 0; a < 6; ++a) mg[a] = -g[a];
-            if (!chol_solve(6, A, lam, mg, d)) { lam *= 10; if (lam > 1e10) return it; continue; }
-            double Rw[9], Rn[9], tn[3];
-            orc_rodrigues_v2m(d, Rw);
-            mat3mul(Rw, R, Rn);
-            for (int k = 0; k < 3; ++k) tn[k] = t[k] + d[3 + k];
-            double cn = pnp_cost(Rn, tn, cam, X, Y, Z, U, V, mask, n);
+            double d[6], Rn[9], tn[3], cn;
+            if (!chol6(A, lam, g, d)) {
+                lam *= 10;
+                if (lam > 1e10) goto done;
+                continue;
+            }
+            cayley(d, R, Rn);
+            for (int j = 0; j < 3; ++j) tn[j] = t[j] + d[3 + j];
+            lm_reduce(&c, Rn, tn, 1, &cn);
             if (cn < cost) {
                 double rel = (cost - cn) / (cost > 1e-300 ? cost : 1e-300);
-                memcpy(R, Rn, sizeof(Rn)); memcpy(t, tn, sizeof(tn));
+                memcpy(R, Rn, sizeof(Rn));
+                memcpy(t, tn, sizeof(tn));
                 cost = cn;
                 lam = lam * 0.1 > 1e-12 ? lam * 0.1 : 1e-12;
                 accepted = 1;
-                if (rel < 1e-12) return it + 1;
+                double dd = 0, tt = 0;
+                for (int j = 0; j < 6; ++j) dd += d[j] * d[j];
+                for (int j = 0; j < 3; ++j) tt += t[j] * t[j];
+                if (rel < 1e-12 || sqrt(dd) < 1.1920928955078125e-07 * (sqrt(tt) + 1.0)) { it = it + 1; goto done; }
             } else {
                 lam *= 10;
-                if (lam > 1e10) return it;
+                if (lam > 1e10) goto done;
             }
         }
     }
+done:
+    for (int j = 0; j < 3; ++j) t[j] = t[j] - (R[3 * j] * c.c[0] + R[3 * j + 1] * c.c[1] + R[3 * j + 2] * c.c[2]);
+    free(c.part);
     return it;
 }
 
