@@ -124,6 +124,7 @@ struct rsac_ctx {
     float *d_thr2 = nullptr;
     DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
     DevBuf loc;                                                // location search: inputs, pos2, H, err
+    DevBuf lo;                                                 // LO-RANSAC: 2 model records, 2 counts, 2 masks
     // pinned host staging
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask;
 };
@@ -317,7 +318,53 @@ struct LoopOut {
     int rounds = 0;
     int64_t scored = 0;
     double gpu_ms = 0, solve_ms = 0, score_ms = 0;
+    int32_t lo_improvements = 0;
 };
+
+// LO-RANSAC local optimisation of the new best of problem 0 (DESIGN.md "LO-RANSAC";
+// the oracle's orc_pnp_ransac_lo): up to 4 rounds of LM refit on the current inliers +
+// recount, kept while the count rises.  An improved model replaces the best
+// hypothesis' record, so the final mask / gather / refit see it.
+constexpr int kLoSteps = 4;
+
+int local_opt(rsac_ctx *c, const PnpArgs &a, int32_t n, ScanState &sc, double confidence, hipStream_t s,
+              int32_t &improvements) {
+    const size_t rec_bytes = sizeof(double) * kModelStride;
+    HIPCHK(c->lo.ensure(2 * rec_bytes + 64 + 2 * (size_t)std::max(n, 1)));
+    double *rec[2] = {c->lo.as<double>(), c->lo.as<double>() + kModelStride};
+    int32_t *cnt = (int32_t *)(rec[1] + kModelStride);
+    uint8_t *mk[2] = {(uint8_t *)(cnt + 16), (uint8_t *)(cnt + 16) + std::max(n, 1)};
+    double *best_rec = a.models + sc.best * kModelStride;  // problem 0: record index = hypothesis
+    HIPCHK(hipMemcpyAsync(rec[0], best_rec, rec_bytes, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), s));
+    HIPCHK(launch_pnp_model_count(a, n, rec[0], mk[0], cnt, s));
+    int32_t cur = sc.max_good;
+    bool better = false;
+    for (int step = 0; step < kLoSteps; ++step) {
+        HIPCHK(hipMemcpyAsync(rec[1], rec[0], rec_bytes, hipMemcpyDeviceToDevice, s));
+        HIPCHK(launch_pnp_refine(a, 1, mk[0], rec[1], nullptr, s));
+        HIPCHK(hipMemsetAsync(cnt + 1, 0, sizeof(int32_t), s));
+        HIPCHK(launch_pnp_model_count(a, n, rec[1], mk[1], cnt + 1, s));
+        int32_t c2 = 0;
+        HIPCHK(hipMemcpyAsync(&c2, cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (c2 <= cur) break;
+        std::swap(rec[0], rec[1]);
+        std::swap(mk[0], mk[1]);
+        cur = c2;
+        better = true;
+        ++improvements;
+    }
+    if (better) {
+        HIPCHK(hipMemcpyAsync(best_rec, rec[0], rec_bytes, hipMemcpyDeviceToDevice, s));
+        if (cur > sc.max_good) {
+            sc.max_good = cur;
+            sc.niters = update_num_iters(confidence, (double)(n - cur) / n, 4, (int)sc.niters);
+            if (sc.iter >= sc.niters) sc.done = true;
+        }
+    }
+    return RSAC_OK;
+}
 
 void add_times(rsac_ctx *c, double &gpu, double &solve, double &score) {
     float a = 0, b = 0;
@@ -331,6 +378,7 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
     const int P = st.P;
     const int64_t H = std::max(max_iters, 1);
     const bool adaptive = (flags & RSAC_F_ADAPTIVE) != 0;
+    const bool lo = (flags & RSAC_F_LO) != 0 && model == Model::PnP && P == 1;
     const int64_t round = adaptive ? std::min<int64_t>(std::max<int64_t>(c->round_size, 64), H) : H;
     const int64_t stride = H;
     int r = ensure_hyp_buffers(c, P, stride, (flags & RSAC_F_SAMPLER_OPENCV) != 0);
@@ -413,10 +461,21 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
         bool all_done = true;
         for (int p = 0; p < P; ++p) {
             ScanState &sc = out.scan[p];
-            if (!sc.done) {
-                const int np = (int)(st.off[p + 1] - st.off[p]);
-                scan_step(sc, c->h_counts.as<int32_t>() + (size_t)p * Hr, c->h_status.as<int8_t>() + (size_t)p * Hr,
-                          Hr, np, 4, confidence);
+            const int np = (int)(st.off[p + 1] - st.off[p]);
+            const int32_t *cr = c->h_counts.as<int32_t>() + (size_t)p * Hr;
+            const int8_t *sr = c->h_status.as<int8_t>() + (size_t)p * Hr;
+            if (lo) {
+                // stop at every new best, optimise it locally, continue with the raised floor
+                while (!sc.done && sc.iter < hb + Hr) {
+                    scan_step(sc, cr + (sc.iter - hb), sr + (sc.iter - hb), hb + Hr - sc.iter, np, 4, confidence, true);
+                    if (sc.improved) {
+                        sc.improved = false;
+                        int rr = local_opt(c, *pa, np, sc, confidence, s, out.lo_improvements);
+                        if (rr) return rr;
+                    }
+                }
+            } else if (!sc.done) {
+                scan_step(sc, cr, sr, Hr, np, 4, confidence);
             }
             all_done = all_done && sc.done;
         }
@@ -533,6 +592,7 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         stats->gpu_ms = lo.gpu_ms;
         stats->solve_ms = lo.solve_ms;
         stats->score_ms = lo.score_ms;
+        stats->lo_improvements = lo.lo_improvements;
     }
     return any ? RSAC_OK : RSAC_NO_MODEL;
 }
@@ -599,6 +659,7 @@ int hom_core(rsac_ctx *c, const void *src, const void *dst, const int64_t *offse
         stats->gpu_ms = lo.gpu_ms;
         stats->solve_ms = lo.solve_ms;
         stats->score_ms = lo.score_ms;
+        stats->lo_improvements = 0;
     }
     return any ? RSAC_OK : RSAC_NO_MODEL;
 }

@@ -38,15 +38,17 @@ struct ScanState {
     int32_t max_good = 0;
     int64_t iter = 0;
     bool done = false;
+    bool improved = false;  // set by scan_step(stop_on_improve) when it stopped at a new best
     void reset(int max_iters) {
         niters = max_iters > 1 ? max_iters : 1;
-        best = -1; max_good = 0; iter = 0; done = false;
+        best = -1; max_good = 0; iter = 0; done = false; improved = false;
     }
 };
 
 // consume hypotheses [s.iter, s.iter + count) (counts/status indexed from 0)
+// stop_on_improve: return right after a new best (s.improved set, s.iter = its index + 1)
 void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_t count, int n, int model_points,
-               double confidence);
+               double confidence, bool stop_on_improve = false);
 
 void rodrigues_v2m(const double r[3], double R[9]);
 void rodrigues_m2v(const double R[9], double r[3]);

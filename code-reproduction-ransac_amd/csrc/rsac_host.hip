@@ -58,7 +58,7 @@ int update_num_iters(double p, double ep, int model_points, int max_iters) {
 }
 
 void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_t count, int n, int model_points,
-               double confidence) {
+               double confidence, bool stop_on_improve) {
     if (s.done) return;
     const int64_t begin = s.iter;
     int64_t i = begin;
@@ -73,6 +73,11 @@ void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_
             s.best = i;
             s.max_good = c;
             s.niters = update_num_iters(confidence, (double)(n - c) / n, model_points, (int)s.niters);
+            if (stop_on_improve) {
+                s.improved = true;
+                ++i;
+                break;
+            }
         }
     }
     s.iter = i;

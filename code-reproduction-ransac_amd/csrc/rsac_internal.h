@@ -107,6 +107,10 @@ hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
                              hipStream_t s);
 
+// mask + inlier count (atomically into *count, zeroed by the caller) of one model record, problem 0
+hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, int32_t *count,
+                                  hipStream_t s);
+
 // camera-location search (main_v1.py:254-348): pos2 of every (location, feature) pair, then
 // err1 / err2 of every location's homography
 hipError_t launch_loc_pos2(const double *p3, const double *px, int32_t n, const double *locs, int32_t L, double *src,

@@ -1353,4 +1353,33 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
     return hipGetLastError();
 }
 
+// RANSAC-test mask and inlier count of one model record (problem 0): the
+// local-optimisation step of LO-RANSAC.  *count must be zero on entry.
+__global__ __launch_bounds__(256) void k_pnp_model_count(PnpArgs a, const double *__restrict__ m,
+                                                         uint8_t *__restrict__ mask, int32_t *__restrict__ count) {
+    const int64_t p0 = a.offsets[0];
+    const int n = (int)(a.offsets[1] - p0);
+    const Cam k{a.cams[0], a.cams[1], a.cams[2], a.cams[3]};
+    const float thr2 = a.thr2[0];
+    const bool valid = m[kValidSlot] != 0.0;
+    int local = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int64_t q = p0 + i;
+        const bool f = valid && pnp_err(m, m + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <=
+                                    thr2;
+        mask[q] = f;
+        local += f;
+    }
+    for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(count, local);
+}
+
+hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, int32_t *count,
+                                  hipStream_t s) {
+    unsigned g = cdiv(n > 0 ? n : 1, 256);
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_pnp_model_count, dim3(g), dim3(256), 0, s, a, model, mask, count);
+    return hipGetLastError();
+}
+
 }  // namespace rsac

@@ -29,6 +29,7 @@ F_DEVICE_IN = 1 << 3
 F_DEVICE_SOA = 1 << 4
 F_DEVICE_OUT = 1 << 5
 F_EXACT_ONLY = 1 << 6
+F_LO = 1 << 7
 
 ABI_VERSION = 1
 
@@ -36,7 +37,7 @@ ABI_VERSION = 1
 class Stats(C.Structure):
     _fields_ = [("best_hyp", C.c_int64), ("iters", C.c_int64), ("hyps_scored", C.c_int64),
                 ("n_inliers", C.c_int32), ("rounds", C.c_int32), ("gpu_ms", C.c_double), ("solve_ms", C.c_double),
-                ("score_ms", C.c_double)]
+                ("score_ms", C.c_double), ("lo_improvements", C.c_int32), ("reserved", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

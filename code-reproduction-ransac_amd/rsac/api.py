@@ -106,12 +106,13 @@ class RansacInfo:
     gpu_ms: float
     solve_ms: float
     score_ms: float
+    lo_improvements: int = 0
 
 
 def _info(code, st: L.Stats) -> RansacInfo:
     return RansacInfo(ok=code == L.OK, n_inliers=st.n_inliers, best_hyp=st.best_hyp, iters=st.iters,
                       hyps_scored=st.hyps_scored, rounds=st.rounds, gpu_ms=st.gpu_ms, solve_ms=st.solve_ms,
-                      score_ms=st.score_ms)
+                      score_ms=st.score_ms, lo_improvements=st.lo_improvements)
 
 
 def _K9(K) -> np.ndarray:
@@ -121,13 +122,15 @@ def _K9(K) -> np.ndarray:
 
 def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
                confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox", adaptive: bool = True,
-               refine: bool = True, device=None, return_info: bool = False, exact_only: bool = False):
+               refine: bool = True, device=None, return_info: bool = False, exact_only: bool = False,
+               lo: bool = False):
     """RANSAC PnP on the GPU: (points2D, points3D, K, n_iters, reproj_thresh) -> (R, t, inlier_mask).
 
     Defaults follow the reference call (iterationsCount=5000, reprojectionError=30,
     confidence=0.99; main_v1.py:497-502).  ``R`` is 3x3, ``t`` (3,) with
     x_cam = R X + t; ``inlier_mask`` is the RANSAC-phase mask (OpenCV's
     convention).  On failure R and t are None and the mask is all False.
+    lo=True runs LO-RANSAC (local optimisation at every new best; BASELINE.json C5).
     """
     p3 = _In(points3D, 3)
     p2 = _In(points2D, 2)
@@ -137,7 +140,7 @@ def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float 
         raise ValueError("points3D and points2D must both be host arrays or both GPU tensors")
     n = p3.n
     ctx = L.context(_device_of(p3, device))
-    flags = _flags(adaptive, refine, sampler, exact_only)
+    flags = _flags(adaptive, refine, sampler, exact_only) | (L.F_LO if lo else 0)
     if p3.device:
         flags |= L.F_DEVICE_IN
     K9 = _K9(K)

@@ -65,6 +65,8 @@ extern "C" {
 #define RSAC_F_DEVICE_SOA (1u << 4)     /* inputs are device float32 SoA (implies device) */
 #define RSAC_F_DEVICE_OUT (1u << 5)     /* inlier mask output is a device pointer */
 #define RSAC_F_EXACT_ONLY (1u << 6)     /* disable the float32 pre-filter in scoring (A/B and tests) */
+#define RSAC_F_LO (1u << 7)             /* LO-RANSAC (PnP, one problem): local optimisation at every new best,
+                                           BASELINE.json configs[4]; see DESIGN.md "LO-RANSAC" */
 
 typedef struct rsac_ctx rsac_ctx;
 
@@ -78,6 +80,8 @@ typedef struct rsac_stats {
     double gpu_ms;         /* device time of solve+score (events), summed over rounds */
     double solve_ms;       /* ... of which the sample+minimal-solve kernel */
     double score_ms;       /* ... of which the scoring kernel */
+    int32_t lo_improvements; /* LO-RANSAC: refits that raised the best count */
+    int32_t reserved;
 } rsac_stats;
 
 RSAC_EXPORT int rsac_create(int device, rsac_ctx **out);

@@ -96,6 +96,10 @@ def lib():
                                  C.c_int, C.c_uint64, C.c_int, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
                                  C.POINTER(C.c_int64)]
     L.orc_pnp_ransac.restype = C.c_int64
+    L.orc_pnp_ransac_lo.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
+                                    C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
+                                    C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
+    L.orc_pnp_ransac_lo.restype = C.c_int64
     L.orc_hom_ransac.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_double, C.c_double, C.c_int,
                                  C.c_uint64, C.c_int, _f64p, _u8p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     L.orc_hom_ransac.restype = C.c_int64
@@ -229,6 +233,23 @@ def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000,
                                 mask, C.byref(good), C.byref(iters))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value))
+
+
+def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED):
+    """LO-RANSAC restatement (orc_pnp_ransac_lo): local optimisation at every new best."""
+    soa = soa_pnp(points3d, points2d)
+    n = len(soa[0])
+    cam = cam_from_K(K)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    mask = np.zeros(n, np.uint8)
+    good = C.c_int32(0)
+    iters = C.c_int64(0)
+    nlo = C.c_int32(0)
+    best = lib().orc_pnp_ransac_lo(*soa, n, cam, thr, confidence, max_iters, seed, R, t, mask, C.byref(good),
+                                   C.byref(iters), C.byref(nlo))
+    return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
+                iters=int(iters.value), lo_improvements=int(nlo.value))
 
 
 def pnp_refine(soa, mask, cam, R, t, max_iter=20):

@@ -1230,6 +1230,77 @@ ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, c
     return best;
 }
 
+/* LO-RANSAC (BASELINE.json configs[4], C5; Chum et al. 2003, simple LO):
+ * the OpenCV loop above, except that whenever hypothesis i becomes the best
+ * (count > max(best, 3)) a local optimisation runs before hypothesis i+1:
+ *     M, c = model_i, count_i
+ *     repeat at most 4 times:
+ *         M' = orc_pnp_refine(M, inliers(M))   (the final-refit LM)
+ *         c' = count(M');  if c' <= c: stop;  M, c = M', c'
+ *     best := (M, c);  niters := RANSACUpdateNumIters(conf, (n - c)/n, 4, niters)
+ * Returns the seeding hypothesis; R, t = the best (locally optimised) model,
+ * mask = its RANSAC-test inliers, *n_inliers = c. */
+#define LO_STEPS 4
+ORC_API int64_t orc_pnp_ransac_lo(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                  int n, const double cam[4], double thr, double confidence, int max_iters,
+                                  uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
+                                  int64_t *iters_used, int32_t *lo_improvements) {
+    int64_t H = max_iters > 1 ? max_iters : 1;
+    int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * H);
+    int8_t *status = (int8_t *)malloc(H);
+    double *models = (double *)malloc(sizeof(double) * 16 * H);
+    uint8_t *m0 = (uint8_t *)malloc(n > 0 ? n : 1), *m1 = (uint8_t *)malloc(n > 0 ? n : 1);
+    float thr2 = orc_thr2(thr);
+    orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, 0, H, NULL, NULL, counts, status, models);
+    int64_t niters = H, best = -1, i;
+    int32_t max_good = 0, nlo = 0;
+    double BR[9] = {0}, Bt[3] = {0};
+    for (i = 0; i < H && i < niters; ++i) {
+        if (status[i] < 0) break;
+        if (status[i] == 0) continue;
+        int32_t c = counts[i];
+        int32_t floor_c = max_good > 3 ? max_good : 3;
+        if (c <= floor_c) continue;
+        best = i; max_good = c;
+        niters = orc_update_num_iters(confidence, (double)(n - c) / n, 4, (int)niters);
+        double MR[9], Mt[3];
+        memcpy(MR, models + 16 * i, sizeof MR);
+        memcpy(Mt, models + 16 * i + 9, sizeof Mt);
+        orc_pnp_count(MR, Mt, cam, X, Y, Z, U, V, n, thr2, m0);
+        for (int step = 0; step < LO_STEPS; ++step) {
+            double NR[9], Nt[3];
+            memcpy(NR, MR, sizeof NR);
+            memcpy(Nt, Mt, sizeof Nt);
+            orc_pnp_refine(X, Y, Z, U, V, m0, n, cam, NR, Nt, 20);
+            int32_t c2 = orc_pnp_count(NR, Nt, cam, X, Y, Z, U, V, n, thr2, m1);
+            if (c2 <= c) break;
+            memcpy(MR, NR, sizeof MR);
+            memcpy(Mt, Nt, sizeof Mt);
+            c = c2;
+            uint8_t *tm = m0; m0 = m1; m1 = tm;
+            ++nlo;
+        }
+        if (c > max_good) {
+            max_good = c;
+            niters = orc_update_num_iters(confidence, (double)(n - c) / n, 4, (int)niters);
+        }
+        memcpy(BR, MR, sizeof BR);
+        memcpy(Bt, Mt, sizeof Bt);
+    }
+    if (best >= 0) {
+        memcpy(R, BR, sizeof BR);
+        memcpy(t, Bt, sizeof Bt);
+        orc_pnp_count(R, t, cam, X, Y, Z, U, V, n, thr2, mask);
+    } else if (mask) {
+        memset(mask, 0, n);
+    }
+    if (n_inliers) *n_inliers = max_good;
+    if (iters_used) *iters_used = i;
+    if (lo_improvements) *lo_improvements = nlo;
+    free(counts); free(status); free(models); free(m0); free(m1);
+    return best;
+}
+
 ORC_API int64_t orc_hom_ransac(const float *sx, const float *sy, const float *dx, const float *dy, int n, double thr,
                                double confidence, int max_iters, uint64_t seed, int sampler, double Hout[9],
                                uint8_t *mask, int32_t *n_inliers, int64_t *iters_used) {

@@ -451,3 +451,18 @@ def test_batched_refit_bit_exact_per_problem():
         Ro, to, _ = O.pnp_refine(soa, ref["mask"].astype(np.uint8), O.cam_from_K(p["K"]), ref["R"], ref["t"])
         np.testing.assert_array_equal(m, ref["mask"])
         assert _bits_equal(R, Ro) and _bits_equal(t, to)
+
+
+# ---------------------------------------------------------------------------------------------
+# LO-RANSAC (BASELINE.json configs[4])
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,outl,seed", [(3000, 0.8, 5), (20000, 0.7, 5), (5000, 0.5, 9), (100000, 0.5, 3)])
+def test_lo_ransac_matches_restatement(n, outl, seed):
+    pr = synth.pnp_problem(n, outl, seed=seed)
+    R, t, m, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0, refine=False, lo=True,
+                                    return_info=True)
+    ref = O.pnp_ransac_lo(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
+    assert (info.best_hyp, info.n_inliers, info.iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    assert info.lo_improvements == ref["lo_improvements"]
+    assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+    np.testing.assert_array_equal(m, ref["mask"])
