@@ -219,6 +219,22 @@ def extra_workloads(local, args):
                          "hyp_s": 1024 * 1024 / w, "host_inputs_ms": wh * 1e3, "host_inputs_hyp_s": 1024 * 1024 / wh,
                          "note": "inputs resident in HBM (and, second figure, handed over as host f64 arrays); "
                                  "per-problem winners + RANSAC masks, adaptive off, no refit"}
+    # C5 (BASELINE.json configs[4]): LO-RANSAC, 100k correspondences, adaptive, inputs in HBM
+    p5 = synth.pnp_problem(100_000, 0.5, seed=3)
+    q2 = torch.from_numpy(p5["points2d"]).to(dev)
+    q3 = torch.from_numpy(p5["points3d"]).to(dev)
+    walls = []
+    for i in range(6):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        _, _, _, info = rsac.pnp_ransac(q2, q3, p5["K"], 5000, args.thr, lo=True, refine=True, return_info=True,
+                                        device=local)
+        torch.cuda.synchronize()
+        if i >= 1:
+            walls.append(time.perf_counter() - t)
+    out["c5_lo_ransac"] = {"points": 100_000, "outlier_ratio": 0.5, "ms_to_best": statistics.median(walls) * 1e3,
+                           "iters": info.iters, "n_inliers": info.n_inliers, "lo_improvements": info.lo_improvements,
+                           "note": "1 GPU; the multi-GPU form is rsac.parallel.sharded_ransac(lo=True)"}
     lp = synth.location_problem(seed=0)
     walls = []
     for i in range(6):

@@ -822,6 +822,50 @@ int rsac_location_search(rsac_ctx *c, const double *pos3d, const double *pixels,
     return r;
 }
 
+int rsac_pnp_local_opt(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                       const double model_in[12], double thr, uint32_t flags, double model_out[12], int32_t *count_out,
+                       int32_t *steps_out, void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (!K || !model_in || !model_out || n < 1) return fail(RSAC_EINVAL, "bad arguments");
+    hipStream_t s = pick_stream(c, stream);
+    Staged st;
+    r = stage_points(c, pts3d, pts2d, 3, nullptr, 1, n, flags & (RSAC_F_DEVICE_IN | RSAC_F_DEVICE_SOA), s, st);
+    if (r) return r;
+    r = stage_tables(c, st, K, thr, s);
+    if (r) return r;
+    r = ensure_hyp_buffers(c, 1, 1, false);
+    if (r) return r;
+    PnpArgs a;
+    r = pnp_args(c, st, flags | RSAC_F_EXACT_ONLY, 0, 1, 0, s, a);
+    if (r) return r;
+    double rec[kModelStride] = {0};
+    memcpy(rec, model_in, 12 * sizeof(double));
+    rec[kValidSlot] = 1.0;
+    HIPCHK(hipMemcpyAsync(c->models.p, rec, sizeof rec, hipMemcpyHostToDevice, s));
+    // the model's own count starts the chain (local_opt recounts it on the device)
+    HIPCHK(c->lo.ensure(2 * sizeof(double) * kModelStride + 64 + 2 * (size_t)n));
+    int32_t *cnt = (int32_t *)(c->lo.as<double>() + 2 * kModelStride);
+    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(int32_t), s));
+    HIPCHK(launch_pnp_model_count(a, n, c->models.as<double>(), (uint8_t *)(cnt + 16), cnt, s));
+    int32_t c0 = 0;
+    HIPCHK(hipMemcpyAsync(&c0, cnt, sizeof c0, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ScanState sc;
+    sc.reset(1 << 30);
+    sc.best = 0;
+    sc.max_good = c0;
+    int32_t steps = 0;
+    r = local_opt(c, a, n, sc, 0.99, s, steps);
+    if (r) return r;
+    HIPCHK(hipMemcpyAsync(rec, c->models.p, sizeof rec, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memcpy(model_out, rec, 12 * sizeof(double));
+    if (count_out) *count_out = sc.max_good;
+    if (steps_out) *steps_out = steps;
+    return RSAC_OK;
+}
+
 int rsac_score_poses(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
                      const double *poses, int32_t n_poses, double thr, uint32_t flags, int32_t *counts_out,
                      void *stream) {
@@ -1082,6 +1126,28 @@ void rsac_rodrigues_v2m(const double r[3], double R[9]) { rodrigues_v2m(r, R); }
 void rsac_rodrigues_m2v(const double R[9], double r[3]) { rodrigues_m2v(R, r); }
 int rsac_update_num_iters(double p, double ep, int model_points, int max_iters) {
     return update_num_iters(p, ep, model_points, max_iters);
+}
+
+int rsac_scan_until_best(rsac_scan_state *st, const int32_t *counts, const int8_t *status, int64_t count, int32_t n,
+                         int32_t model_points, double confidence, int32_t *improved) {
+    if (!st || count < 0 || n <= 0 || (count > 0 && (!counts || !status)))
+        return fail(RSAC_EINVAL, "rsac_scan_until_best: bad arguments");
+    ScanState s;
+    s.niters = st->niters; s.best = st->best; s.iter = st->iter; s.max_good = st->max_good; s.done = st->done != 0;
+    scan_step(s, counts, status, count, n, model_points, confidence, true);
+    *st = rsac_scan_state{s.niters, s.best, s.iter, s.max_good, s.done ? 1 : 0};
+    if (improved) *improved = s.improved ? 1 : 0;
+    return RSAC_OK;
+}
+
+int rsac_scan_raise(rsac_scan_state *st, int32_t count, int32_t n, int32_t model_points, double confidence) {
+    if (!st || n <= 0) return fail(RSAC_EINVAL, "rsac_scan_raise: bad arguments");
+    if (count > st->max_good) {  // as local_opt applies it
+        st->max_good = count;
+        st->niters = update_num_iters(confidence, (double)(n - count) / n, model_points, (int)st->niters);
+        if (st->iter >= st->niters) st->done = 1;
+    }
+    return RSAC_OK;
 }
 
 void rsac_scan_init(rsac_scan_state *st, int32_t max_iters) {

@@ -83,6 +83,9 @@ SIGNATURES = [
     ("rsac_location_search", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _d, _i32, _d, _u32, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp]),
     ("rsac_scan_init", None, [_vp, _i32]),
+    ("rsac_scan_until_best", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d, _vp]),
+    ("rsac_scan_raise", C.c_int, [_vp, _i32, _i32, _i32, _d]),
+    ("rsac_pnp_local_opt", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _d, _u32, _vp, _vp, _vp, _vp]),
     ("rsac_scan", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d]),
 ]
 

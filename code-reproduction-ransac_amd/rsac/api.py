@@ -502,6 +502,24 @@ def location_search(pos3d, pixels, locations, ransacbound: float = 75.0, *, max_
                           mask=mask[:L_ * g].reshape(L_, g).astype(bool), n_good=g)
 
 
+def local_opt(points2D, points3D, K, model12, reproj_thresh: float = 30.0, device=None):
+    """One LO-RANSAC local optimisation of a pose -> (model12, inlier count, steps)."""
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    ctx = L.context(_device_of(p3, device))
+    m_in = np.ascontiguousarray(np.asarray(model12, np.float64).reshape(12))
+    m_out = np.zeros(12)
+    cnt = C.c_int32(0)
+    steps = C.c_int32(0)
+    K9 = _K9(K)
+    with ctx.lock:
+        L.check(L.lib().rsac_pnp_local_opt(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n, K9.ctypes.data,
+                                           m_in.ctypes.data, float(reproj_thresh),
+                                           L.F_DEVICE_IN if p3.device else 0, m_out.ctypes.data, C.byref(cnt),
+                                           C.byref(steps), _stream_of(p3)))
+    return m_out, int(cnt.value), int(steps.value)
+
+
 class Scan:
     """OpenCV's sequential best-model scan (rsac_scan of include/rsac.h) over counts produced
     elsewhere -- the multi-GPU driver feeds it each round's gathered counts."""
@@ -520,6 +538,22 @@ class Scan:
             raise ValueError("counts and status differ in length")
         L.check(L.lib().rsac_scan(C.byref(self.st), c.ctypes.data, st.ctypes.data, c.size, self.n, self.s, self.conf))
         return self
+
+    def step_until_best(self, counts, status) -> int:
+        """Scan until a new best (LO-RANSAC); returns how many entries were consumed (the
+        new best is the last of them when ``improved``)."""
+        c = np.ascontiguousarray(counts, np.int32)
+        st = np.ascontiguousarray(status, np.int8)
+        before = self.iters
+        imp = C.c_int32(0)
+        L.check(L.lib().rsac_scan_until_best(C.byref(self.st), c.ctypes.data, st.ctypes.data, c.size, self.n, self.s,
+                                             self.conf, C.byref(imp)))
+        self.improved = bool(imp.value)
+        return self.iters - before
+
+    def raise_count(self, count: int):
+        """Apply a locally optimised inlier count."""
+        L.check(L.lib().rsac_scan_raise(C.byref(self.st), int(count), self.n, self.s, self.conf))
 
     done = property(lambda self: bool(self.st.done))
     best = property(lambda self: int(self.st.best))

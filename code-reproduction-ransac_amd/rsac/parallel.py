@@ -128,6 +128,11 @@ class PnPShard:
         _, _, m = api.hypotheses("pnp", self.p3, self.p2, self.K, index, 1, self.thr, seed=self.seed)
         return m[0, :12].copy()
 
+    def local_opt(self, model12, count: int):
+        """LO-RANSAC step on this rank's copy of the points (identical on every rank)."""
+        m, c, _ = api.local_opt(self.p2, self.p3, self.K, model12, self.thr)
+        return m, c
+
     def mask(self, model12) -> np.ndarray:
         m, _ = api.pose_mask(self.p2, self.p3, self.K, model12, self.thr)
         return np.asarray(m.cpu() if torch.is_tensor(m) else m, bool)
@@ -154,11 +159,17 @@ def sharded_best(ev, n_total: int, group=None) -> ShardedResult:
 
 
 def sharded_ransac(ev, max_iters: int, confidence: float = 0.99, round_size: int = 4096, group=None,
-                   model_points: int = 4) -> ShardedResult:
-    """Adaptive RANSAC (OpenCV iteration semantics) with each round's hypotheses split over ranks."""
+                   model_points: int = 4, lo: bool = False) -> ShardedResult:
+    """Adaptive RANSAC (OpenCV iteration semantics) with each round's hypotheses split over ranks.
+
+    lo=True: LO-RANSAC (BASELINE.json configs[4]); the scan stops at every new best, every rank
+    runs the same (deterministic) local optimisation on its copy of the points, and the scan
+    continues with the raised count -- the single-GPU rsac.pnp_ransac(lo=True) result.
+    """
     rank, world = _rank_world(group)
     scan = api.Scan(max_iters, ev.n, confidence, model_points)
     hb = 0
+    best_model = None
     while not scan.done and hb < max_iters:
         hr = min(int(round_size), max_iters - hb, scan.niters - hb)
         b, c = shard(hr, rank, world)
@@ -167,11 +178,21 @@ def sharded_ransac(ev, max_iters: int, confidence: float = 0.99, round_size: int
         rows[:, 0] = st
         rows[:, 1] = cn
         full = np.concatenate(_all_gather_rows(rows, group))  # rank order = hypothesis order
-        scan.step(full[:, 1], full[:, 0].astype(np.int8))
+        if not lo:
+            scan.step(full[:, 1], full[:, 0].astype(np.int8))
+        else:
+            pos = 0
+            while not scan.done and pos < hr:
+                pos += scan.step_until_best(full[pos:, 1], full[pos:, 0].astype(np.int8))
+                if scan.improved:
+                    m, cnt = ev.local_opt(ev.model(scan.best), scan.max_good)
+                    best_model = m if cnt > scan.max_good else ev.model(scan.best)
+                    scan.raise_count(cnt)
         hb += hr
     if scan.best < 0:
         return ShardedResult(-1, 0, scan.iters, None)
-    return ShardedResult(scan.best, scan.max_good, scan.iters, ev.model(scan.best))
+    model = best_model if lo else ev.model(scan.best)
+    return ShardedResult(scan.best, scan.max_good, scan.iters, model)
 
 
 def sharded_batched(run_local, n_problems: int, group=None):

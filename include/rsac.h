@@ -219,6 +219,20 @@ RSAC_EXPORT void rsac_scan_init(rsac_scan_state *st, int32_t max_iters);
 /* consume hypotheses [st->iter, st->iter + count); status < 0 = sampler gave up (ends the scan) */
 RSAC_EXPORT int rsac_scan(rsac_scan_state *st, const int32_t *counts, const int8_t *status, int64_t count, int32_t n,
                           int32_t model_points, double confidence);
+/* LO-RANSAC drivers: as rsac_scan, but return right after a new best (*improved = 1,
+ * st->iter = its index + 1) so that it can be optimised locally before the scan goes on */
+RSAC_EXPORT int rsac_scan_until_best(rsac_scan_state *st, const int32_t *counts, const int8_t *status, int64_t count,
+                                     int32_t n, int32_t model_points, double confidence, int32_t *improved);
+/* apply a locally optimised inlier count: raises max_good and lowers the iteration bound */
+RSAC_EXPORT int rsac_scan_raise(rsac_scan_state *st, int32_t count, int32_t n, int32_t model_points, double confidence);
+
+/* One LO-RANSAC local optimisation (RSAC_F_LO's step) of a pose on the device: up to 4
+ * rounds of LM refit on the current RANSAC inliers + recount, kept while the count rises.
+ * model_in / model_out: R 9 row-major, t 3.  *count_out = the final inlier count (>= the
+ * model's own count), *steps_out = refits that raised it.  flags: RSAC_F_DEVICE_IN. */
+RSAC_EXPORT int rsac_pnp_local_opt(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                                   const double model_in[12], double thresh, uint32_t flags, double model_out[12],
+                                   int32_t *count_out, int32_t *steps_out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -100,6 +100,9 @@ def lib():
                                     C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
                                     C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
     L.orc_pnp_ransac_lo.restype = C.c_int64
+    L.orc_pnp_local_opt.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_float, _f64p, _f64p,
+                                    C.c_int32, C.POINTER(C.c_int32)]
+    L.orc_pnp_local_opt.restype = C.c_int32
     L.orc_hom_ransac.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_double, C.c_double, C.c_int,
                                  C.c_uint64, C.c_int, _f64p, _u8p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     L.orc_hom_ransac.restype = C.c_int64
@@ -250,6 +253,15 @@ def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=50
                                    C.byref(iters), C.byref(nlo))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value), lo_improvements=int(nlo.value))
+
+
+def pnp_local_opt(soa, cam, thr, R, t, count):
+    """One LO-RANSAC local optimisation -> (R, t, count, steps)."""
+    R = np.ascontiguousarray(R, np.float64).reshape(9).copy()
+    t = np.ascontiguousarray(t, np.float64).copy()
+    steps = C.c_int32(0)
+    c = lib().orc_pnp_local_opt(*soa, len(soa[0]), cam, thr2(thr), R, t, int(count), C.byref(steps))
+    return R.reshape(3, 3), t, int(c), int(steps.value)
 
 
 def pnp_refine(soa, mask, cam, R, t, max_iter=20):

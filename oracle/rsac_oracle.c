@@ -1241,6 +1241,33 @@ ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, c
  * Returns the seeding hypothesis; R, t = the best (locally optimised) model,
  * mask = its RANSAC-test inliers, *n_inliers = c. */
 #define LO_STEPS 4
+/* the local optimisation of one new best (R, t with `count` inliers), in place;
+ * returns the final count, *steps = refits that raised it */
+ORC_API int32_t orc_pnp_local_opt(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                  int n, const double cam[4], float thr2, double R[9], double t[3], int32_t count,
+                                  int32_t *steps) {
+    uint8_t *m0 = (uint8_t *)malloc(n > 0 ? n : 1), *m1 = (uint8_t *)malloc(n > 0 ? n : 1);
+    int32_t c = count, k = 0;
+    orc_pnp_count(R, t, cam, X, Y, Z, U, V, n, thr2, m0);
+    for (int step = 0; step < LO_STEPS; ++step) {
+        double NR[9], Nt[3];
+        memcpy(NR, R, sizeof NR);
+        memcpy(Nt, t, sizeof Nt);
+        orc_pnp_refine(X, Y, Z, U, V, m0, n, cam, NR, Nt, 20);
+        int32_t c2 = orc_pnp_count(NR, Nt, cam, X, Y, Z, U, V, n, thr2, m1);
+        if (c2 <= c) break;
+        memcpy(R, NR, sizeof NR);
+        memcpy(t, Nt, sizeof Nt);
+        c = c2;
+        uint8_t *tm = m0; m0 = m1; m1 = tm;
+        ++k;
+    }
+    if (steps) *steps = k;
+    free(m0);
+    free(m1);
+    return c;
+}
+
 ORC_API int64_t orc_pnp_ransac_lo(const float *X, const float *Y, const float *Z, const float *U, const float *V,
                                   int n, const double cam[4], double thr, double confidence, int max_iters,
                                   uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
@@ -1249,7 +1276,6 @@ ORC_API int64_t orc_pnp_ransac_lo(const float *X, const float *Y, const float *Z
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * H);
     int8_t *status = (int8_t *)malloc(H);
     double *models = (double *)malloc(sizeof(double) * 16 * H);
-    uint8_t *m0 = (uint8_t *)malloc(n > 0 ? n : 1), *m1 = (uint8_t *)malloc(n > 0 ? n : 1);
     float thr2 = orc_thr2(thr);
     orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, 0, H, NULL, NULL, counts, status, models);
     int64_t niters = H, best = -1, i;
@@ -1266,20 +1292,9 @@ ORC_API int64_t orc_pnp_ransac_lo(const float *X, const float *Y, const float *Z
         double MR[9], Mt[3];
         memcpy(MR, models + 16 * i, sizeof MR);
         memcpy(Mt, models + 16 * i + 9, sizeof Mt);
-        orc_pnp_count(MR, Mt, cam, X, Y, Z, U, V, n, thr2, m0);
-        for (int step = 0; step < LO_STEPS; ++step) {
-            double NR[9], Nt[3];
-            memcpy(NR, MR, sizeof NR);
-            memcpy(Nt, Mt, sizeof Nt);
-            orc_pnp_refine(X, Y, Z, U, V, m0, n, cam, NR, Nt, 20);
-            int32_t c2 = orc_pnp_count(NR, Nt, cam, X, Y, Z, U, V, n, thr2, m1);
-            if (c2 <= c) break;
-            memcpy(MR, NR, sizeof MR);
-            memcpy(Mt, Nt, sizeof Mt);
-            c = c2;
-            uint8_t *tm = m0; m0 = m1; m1 = tm;
-            ++nlo;
-        }
+        int32_t steps = 0;
+        c = orc_pnp_local_opt(X, Y, Z, U, V, n, cam, thr2, MR, Mt, c, &steps);
+        nlo += steps;
         if (c > max_good) {
             max_good = c;
             niters = orc_update_num_iters(confidence, (double)(n - c) / n, 4, (int)niters);
@@ -1297,7 +1312,7 @@ ORC_API int64_t orc_pnp_ransac_lo(const float *X, const float *Y, const float *Z
     if (n_inliers) *n_inliers = max_good;
     if (iters_used) *iters_used = i;
     if (lo_improvements) *lo_improvements = nlo;
-    free(counts); free(status); free(models); free(m0); free(m1);
+    free(counts); free(status); free(models);
     return best;
 }
 

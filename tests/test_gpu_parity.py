@@ -466,3 +466,14 @@ def test_lo_ransac_matches_restatement(n, outl, seed):
     assert info.lo_improvements == ref["lo_improvements"]
     assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
     np.testing.assert_array_equal(m, ref["mask"])
+
+
+def test_parallel_driver_lo_single_rank_equals_pnp_ransac_lo():
+    from rsac import parallel as par
+    pr = synth.pnp_problem(8000, 0.75, seed=31)
+    ev = par.PnPShard(pr["points2d"], pr["points3d"], pr["K"], 30.0, device=0)
+    res = par.sharded_ransac(ev, 5000, 0.99, round_size=333, lo=True)
+    R, t, m, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0, refine=False, lo=True,
+                                    return_info=True)
+    assert (res.best, res.n_inliers, res.iters) == (info.best_hyp, info.n_inliers, info.iters)
+    assert _bits_equal(res.model[:9].reshape(3, 3), R) and _bits_equal(res.model[9:], t)

@@ -41,6 +41,10 @@ class OracleShard:
         _, _, m = O.pnp_hypotheses(self.soa, self.cam, self.thr, self.seed, 1, hyp0=index, models=True)
         return m[0, :12].copy()
 
+    def local_opt(self, model12, count):
+        R, t, c, _ = O.pnp_local_opt(self.soa, self.cam, self.thr, model12[:9], model12[9:12], count)
+        return np.concatenate([R.reshape(9), t]), c
+
 
 def _free_port():
     with socket.socket() as s:
@@ -56,6 +60,7 @@ def _worker(rank, world, port, out_dir):
         ev = OracleShard(pr)
         best = par.sharded_best(ev, 3001)
         ada = par.sharded_ransac(ev, 5000, 0.99, round_size=100)
+        lo = par.sharded_ransac(OracleShard(synth.pnp_problem(1500, 0.8, seed=8)), 5000, 0.99, round_size=97, lo=True)
         # problem sharding: 5 problems over the ranks, rows computed locally from the restatement
         probs = [synth.pnp_problem(300, 0.4, seed=s) for s in range(5)]
 
@@ -70,6 +75,7 @@ def _worker(rank, world, port, out_dir):
         rows = par.sharded_batched(run_local, len(probs))
         res = {"best": [best.best, best.n_inliers, best.model.tolist()],
                "ada": [ada.best, ada.n_inliers, ada.iters, ada.model.tolist()],
+               "lo": [lo.best, lo.n_inliers, lo.iters, lo.model.tolist()],
                "rows": rows.tolist()}
         json.dump(res, open(os.path.join(out_dir, f"rank{rank}.json"), "w"))
     finally:
@@ -105,6 +111,15 @@ def test_sharded_adaptive_equals_sequential_loop(gloo_results):
     pr = synth.pnp_problem(600, 0.6, seed=21)
     ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
     b, n, iters, model = gloo_results[0]["ada"]
+    assert (b, n, iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    np.testing.assert_array_equal(np.array(model[:9]).reshape(3, 3), ref["R"])
+    np.testing.assert_array_equal(model[9:], ref["t"])
+
+
+def test_sharded_lo_ransac_equals_sequential_loop(gloo_results):
+    pr = synth.pnp_problem(1500, 0.8, seed=8)
+    ref = O.pnp_ransac_lo(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
+    b, n, iters, model = gloo_results[0]["lo"]
     assert (b, n, iters) == (ref["best"], ref["n_inliers"], ref["iters"])
     np.testing.assert_array_equal(np.array(model[:9]).reshape(3, 3), ref["R"])
     np.testing.assert_array_equal(model[9:], ref["t"])
