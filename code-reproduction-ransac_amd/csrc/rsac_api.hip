@@ -308,7 +308,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     return RSAC_OK;
 }
 
-enum class Model { PnP, Hom };
+enum class Model { PnP, Hom, Fm };  // Fm: fundamental matrix on the HomArgs block
 
 // The RANSAC loop of RANSACPointSetRegistrator::run for P problems at once:
 // rounds of `round` hypotheses are solved + scored on the GPU, then every
@@ -387,7 +387,8 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
     HIPCHK(c->h_status.ensure((size_t)P * round));
 
     PnpArgs *pa = model == Model::PnP ? (PnpArgs *)args : nullptr;
-    HomArgs *ha = model == Model::Hom ? (HomArgs *)args : nullptr;
+    HomArgs *ha = model != Model::PnP ? (HomArgs *)args : nullptr;
+    const int model_points = model == Model::Fm ? 8 : 4;
 #define SETARG(field, val) \
     do {                   \
         if (pa) pa->field = (val); else ha->field = (val); \
@@ -444,6 +445,10 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
             HIPCHK(launch_pnp_solve(*pa, P, hb, Hr, s));
             HIPCHK(hipEventRecord(c->ev1, s));
             HIPCHK(launch_pnp_score(*pa, P, hb, Hr, c->counts.as<int32_t>(), s));
+        } else if (model == Model::Fm) {
+            HIPCHK(launch_fm_solve(*ha, P, hb, Hr, s));
+            HIPCHK(hipEventRecord(c->ev1, s));
+            HIPCHK(launch_fm_score(*ha, P, hb, Hr, c->counts.as<int32_t>(), s));
         } else {
             HIPCHK(launch_hom_solve(*ha, P, hb, Hr, s));
             HIPCHK(hipEventRecord(c->ev1, s));
@@ -467,7 +472,8 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
             if (lo) {
                 // stop at every new best, optimise it locally, continue with the raised floor
                 while (!sc.done && sc.iter < hb + Hr) {
-                    scan_step(sc, cr + (sc.iter - hb), sr + (sc.iter - hb), hb + Hr - sc.iter, np, 4, confidence, true);
+                    scan_step(sc, cr + (sc.iter - hb), sr + (sc.iter - hb), hb + Hr - sc.iter, np, model_points,
+                              confidence, true);
                     if (sc.improved) {
                         sc.improved = false;
                         int rr = local_opt(c, *pa, np, sc, confidence, s, out.lo_improvements);
@@ -475,7 +481,7 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
                     }
                 }
             } else if (!sc.done) {
-                scan_step(sc, cr, sr, Hr, np, 4, confidence);
+                scan_step(sc, cr, sr, Hr, np, model_points, confidence);
             }
             all_done = all_done && sc.done;
         }
@@ -507,6 +513,8 @@ int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const L
     if (N > 0) {
         if (model == Model::PnP)
             HIPCHK(launch_pnp_mask(*(PnpArgs *)args, P, max_n, c->best.as<int64_t>(), dmask, s));
+        else if (model == Model::Fm)
+            HIPCHK(launch_fm_mask(*(HomArgs *)args, P, max_n, c->best.as<int64_t>(), dmask, s));
         else
             HIPCHK(launch_hom_mask(*(HomArgs *)args, P, max_n, c->best.as<int64_t>(), dmask, s));
     }
@@ -977,6 +985,7 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
     if (r) return r;
     if (H <= 0 || !counts_out || !status_out) return fail(RSAC_EINVAL, "bad arguments");
     if (model == Model::PnP && !K) return fail(RSAC_EINVAL, "K required");
+    if (model == Model::Fm && subsets) return fail(RSAC_EINVAL, "the fundamental-matrix sampler is Philox only");
     hipStream_t s = pick_stream(c, stream);
     Staged st;
     r = stage_points(c, a_pts, b_pts, model == Model::PnP ? 3 : 2, nullptr, 1, n, flags, s, st);
@@ -1018,8 +1027,13 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
         a.hyp_stride = H;
         a.rng_base = hyp_begin;
         a.seed = seed;
-        HIPCHK(launch_hom_solve(a, 1, 0, H, s));
-        HIPCHK(launch_hom_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
+        if (model == Model::Fm) {
+            HIPCHK(launch_fm_solve(a, 1, 0, H, s));
+            HIPCHK(launch_fm_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
+        } else {
+            HIPCHK(launch_hom_solve(a, 1, 0, H, s));
+            HIPCHK(launch_hom_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
+        }
     }
     HIPCHK(hipMemcpyAsync(counts_out, c->counts.p, sizeof(int32_t) * H, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(status_out, c->status.p, H, hipMemcpyDeviceToHost, s));
@@ -1042,6 +1056,56 @@ int rsac_homography_hypotheses(rsac_ctx *c, const void *src, const void *dst, in
                                int32_t *counts_out, int8_t *status_out, double *models_out, void *stream) {
     return hypotheses_core(c, Model::Hom, src, dst, n, nullptr, hyp_begin, n_hyps, thr, seed, flags, subsets,
                            counts_out, status_out, models_out, stream);
+}
+
+int rsac_fundamental_hypotheses(rsac_ctx *c, const void *pts1, const void *pts2, int32_t n, int64_t hyp_begin,
+                                int32_t n_hyps, double thr, uint64_t seed, uint32_t flags, int32_t *counts_out,
+                                int8_t *status_out, double *models_out, void *stream) {
+    return hypotheses_core(c, Model::Fm, pts1, pts2, n, nullptr, hyp_begin, n_hyps, thr, seed, flags, nullptr,
+                           counts_out, status_out, models_out, stream);
+}
+
+int rsac_fundamental_ransac(rsac_ctx *c, const void *pts1, const void *pts2, int32_t n, int32_t max_iters,
+                            double thr, double conf, uint64_t seed, uint32_t flags, double F_out[9],
+                            uint8_t *mask_out, rsac_stats *stats, void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (n < 8) return fail(RSAC_ETOOFEW, "the 8-point fundamental matrix needs >= 8 correspondences (got %d)", n);
+    if (flags & (RSAC_F_SAMPLER_OPENCV | RSAC_F_REFINE | RSAC_F_LO))
+        return fail(RSAC_EINVAL, "fundamental matrix: Philox sampler only, no refit / LO");
+    hipStream_t s = pick_stream(c, stream);
+    Staged st;
+    r = stage_points(c, pts1, pts2, 2, nullptr, 1, n, flags, s, st);
+    if (r) return r;
+    r = stage_tables(c, st, nullptr, thr, s);
+    if (r) return r;
+    HomArgs a{};
+    a.SX = st.d[0]; a.SY = st.d[1]; a.DX = st.d[2]; a.DY = st.d[3];
+    a.offsets = c->d_off;
+    a.max_n = st.max_n();
+    a.thr2 = c->d_thr2;
+    a.seed = seed;
+    a.rng_base = 0;
+    LoopOut lo;
+    r = run_loop(c, Model::Fm, st, &a, max_iters, conf, flags, s, lo);
+    if (r) return r;
+    const int64_t stride = std::max(max_iters, 1);
+    r = finish_masks(c, Model::Fm, st, &a, lo, stride, mask_out, flags, s);
+    if (r) return r;
+    const ScanState &sc = lo.scan[0];
+    if (F_out) memcpy(F_out, c->h_bestmodels.as<double>(), 9 * sizeof(double));
+    if (stats) {
+        stats->best_hyp = sc.best;
+        stats->iters = sc.iter;
+        stats->hyps_scored = lo.scored;
+        stats->n_inliers = sc.max_good;
+        stats->rounds = lo.rounds;
+        stats->gpu_ms = lo.gpu_ms;
+        stats->solve_ms = lo.solve_ms;
+        stats->score_ms = lo.score_ms;
+        stats->lo_improvements = 0;
+    }
+    return sc.best >= 0 ? RSAC_OK : RSAC_NO_MODEL;
 }
 
 int rsac_pnp_mask(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],

@@ -102,6 +102,12 @@ hipError_t launch_hom_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int3
 hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
                            hipStream_t s);
 
+// fundamental matrix (8-point + Sampson) on the homography argument block
+hipError_t launch_fm_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
+hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s);
+hipError_t launch_fm_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
+                          hipStream_t s);
+
 // LM refit of every problem's model record (models: P x kModelStride, R 9, t 3, valid)
 // on the inliers of mask (concatenated points), one block per problem
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,

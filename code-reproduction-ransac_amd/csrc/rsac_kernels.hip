@@ -1382,4 +1382,145 @@ hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *mod
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Fundamental matrix RANSAC (BASELINE.json configs[3]): the homography skeleton
+// with an 8-point sample, the normalised 8-point solver and the Sampson test
+// (rsac_math.h).  HomArgs: SX SY = image-1 points, DX DY = image-2 points.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fm_solve(HomArgs a, int64_t hyp_begin, int32_t H) {
+    const int prob = blockIdx.y;
+    const int hl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (hl >= H) return;
+    const int64_t h = hyp_begin + hl;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
+    double *m = a.models + rec * kModelStride;
+    int8_t st = -1;
+    double F[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (n >= 8) {
+        Philox rng;
+        rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
+        int32_t idx[8];
+        if (rng.subset<8>(n, idx) == 0) {
+            float x1[8], y1[8], x2[8], y2[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int64_t i = p0 + idx[j];
+                x1[j] = a.SX[i]; y1[j] = a.SY[i]; x2[j] = a.DX[i]; y2[j] = a.DY[i];
+            }
+            st = fm_minimal8(x1, y1, x2, y2, F) ? 1 : 0;
+            if (st == 0)
+                for (int q = 0; q < 9; ++q) F[q] = 0.0;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) m[q] = F[q];
+    m[kValidSlot] = st > 0 ? 1.0 : 0.0;
+    a.status[rec] = st;
+}
+
+// hypotheses x points tiles (points in registers, hypothesis wave-uniform), exact f64 test
+template <int P, int HB>
+__global__ __launch_bounds__(256) void k_fm_score(HomArgs a, int64_t hyp_begin, int32_t H, int32_t *__restrict__ counts) {
+    __shared__ int red[4][HB];
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t h0 = hyp_begin + (int64_t)blockIdx.x * HB;
+    const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const double T = (double)a.thr2[prob];
+    const double *__restrict__ mb = a.models + ((int64_t)prob * a.hyp_stride + h0) * kModelStride;
+    const float *__restrict__ SX = a.SX + p0, *__restrict__ SY = a.SY + p0;
+    const float *__restrict__ DX = a.DX + p0, *__restrict__ DY = a.DY + p0;
+    int cnt = 0;
+    for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
+        double x1[P], y1[P], x2[P], y2[P];
+        bool in[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int i = base + j * 64 + lane;
+            in[j] = i < n;
+            const int ii = in[j] ? i : 0;
+            x1[j] = SX[ii]; y1[j] = SY[ii]; x2[j] = DX[ii]; y2[j] = DY[ii];
+        }
+        for (int h = 0; h < nh; ++h) {
+            const double *__restrict__ m = mb + h * kModelStride;
+            if (m[kValidSlot] == 0.0) continue;
+            double F[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) F[q] = m[q];
+            int cc = 0;
+#pragma unroll
+            for (int j = 0; j < P; ++j) cc += __popcll(__ballot(in[j] && fm_inlier(F, x1[j], y1[j], x2[j], y2[j], T)));
+            cnt += (lane == h) ? cc : 0;
+        }
+    }
+    if (lane < HB) red[wave][lane] = cnt;
+    __syncthreads();
+    if (threadIdx.x < nh) {
+        const int s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        counts[(int64_t)prob * a.hyp_stride + h0 + threadIdx.x] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fm_score_lane(HomArgs a, int64_t hyp_begin, int32_t H,
+                                                       int32_t *__restrict__ counts) {
+    __shared__ float sp[4][kLanePts];
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    for (int i = threadIdx.x; i < n; i += 256) {
+        sp[0][i] = a.SX[p0 + i]; sp[1][i] = a.SY[p0 + i]; sp[2][i] = a.DX[p0 + i]; sp[3][i] = a.DY[p0 + i];
+    }
+    __syncthreads();
+    const int hl = blockIdx.x * 256 + threadIdx.x;
+    if (hl >= H) return;
+    const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
+    const double *__restrict__ m = a.models + rec * kModelStride;
+    int cnt = 0;
+    if (m[kValidSlot] != 0.0) {
+        const double T = (double)a.thr2[prob];
+        double F[9];
+        for (int q = 0; q < 9; ++q) F[q] = m[q];
+        for (int i = 0; i < n; ++i) cnt += fm_inlier(F, sp[0][i], sp[1][i], sp[2][i], sp[3][i], T);
+    }
+    counts[rec] = cnt;
+}
+
+__global__ void k_fm_mask(HomArgs a, const int64_t *__restrict__ best, uint8_t *__restrict__ mask) {
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t b = best[prob];
+    const double T = (double)a.thr2[prob];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int64_t q = p0 + i;
+        mask[q] = b >= 0 && fm_inlier(a.models + b * kModelStride, a.SX[q], a.SY[q], a.DX[q], a.DY[q], T);
+    }
+}
+
+hipError_t launch_fm_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
+    hipLaunchKernelGGL(k_fm_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H);
+    return hipGetLastError();
+}
+
+hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
+    if (a.max_n > 0 && a.max_n <= kLanePts)
+        hipLaunchKernelGGL(k_fm_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
+    else
+        hipLaunchKernelGGL((k_fm_score<4, 32>), dim3(cdiv(H, 32), P), dim3(256), 0, s, a, hyp_begin, H, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_fm_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
+                          hipStream_t s) {
+    unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_fm_mask, dim3(g, P), dim3(256), 0, s, a, best, mask);
+    return hipGetLastError();
+}
+
 }  // namespace rsac

@@ -473,6 +473,155 @@ RSAC_HD float hom_err(const float *h, float x, float y, float u, float v) {
 }
 
 // ---------------------------------------------------------------------------
+// Fundamental matrix (BASELINE.json configs[3]; no reference implementation
+// exists -- SURVEY.md §8d -- so this restatement defines the semantics):
+//   minimal solver: normalised 8-point DLT (Hartley: centroid, mean distance
+//   sqrt 2), null vector by Gauss-Jordan with full pivoting, rank 2 by removing
+//   the smallest right-singular direction (Jacobi on F^T F), denormalised, unit
+//   Frobenius norm;
+//   inlier test: Sampson distance r^2 / (a^2 + b^2 + a'^2 + b'^2) <= thr^2,
+//   evaluated division-free as r^2 <= T (a^2 + b^2 + a'^2 + b'^2) in f64 with
+//   explicit fma (bit-identical on every backend).
+// ---------------------------------------------------------------------------
+RSAC_HD double dfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+RSAC_HD bool fm_norm8(const float (&x)[8], const float (&y)[8], double &cx, double &cy, double &s) {
+    cx = 0.0;
+    cy = 0.0;
+    for (int i = 0; i < 8; ++i) {
+        cx = cx + (double)x[i];
+        cy = cy + (double)y[i];
+    }
+    cx = cx * 0.125;
+    cy = cy * 0.125;
+    double d = 0.0;
+    for (int i = 0; i < 8; ++i) {
+        const double dx = (double)x[i] - cx, dy = (double)y[i] - cy;
+        d = d + dsqrt(dx * dx + dy * dy);
+    }
+    d = d * 0.125;
+    if (!(d > 1e-300)) return false;
+    s = 1.4142135623730951 / d;
+    return true;
+}
+
+// eigenvector of the smallest eigenvalue of a symmetric 3x3 (cyclic Jacobi, 12 sweeps max)
+RSAC_HD void sym3_min_evec(double (&A)[9], double (&v)[3]) {
+    double V[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    for (int sweep = 0; sweep < 12; ++sweep) {
+        const double off = A[1] * A[1] + A[2] * A[2] + A[5] * A[5];
+        const double dia = A[0] * A[0] + A[4] * A[4] + A[8] * A[8];
+        if (off <= 1e-34 * dia || off < 1e-300) break;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                const double apq = A[p * 3 + q];
+                if (dabs(apq) < 1e-300) continue;
+                const double theta = (A[q * 3 + q] - A[p * 3 + p]) / (2.0 * apq);
+                const double tt = (theta >= 0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
+                const double c = 1.0 / dsqrt(tt * tt + 1.0), sn = tt * c;
+                for (int k = 0; k < 3; ++k) {
+                    const double akp = A[k * 3 + p], akq = A[k * 3 + q];
+                    A[k * 3 + p] = c * akp - sn * akq;
+                    A[k * 3 + q] = sn * akp + c * akq;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    const double apk = A[p * 3 + k], aqk = A[q * 3 + k];
+                    A[p * 3 + k] = c * apk - sn * aqk;
+                    A[q * 3 + k] = sn * apk + c * aqk;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    const double vkp = V[k * 3 + p], vkq = V[k * 3 + q];
+                    V[k * 3 + p] = c * vkp - sn * vkq;
+                    V[k * 3 + q] = sn * vkp + c * vkq;
+                }
+            }
+    }
+    int mi = 0;
+    if (A[4] < A[mi * 4]) mi = 1;
+    if (A[8] < A[mi * 4]) mi = 2;
+    v[0] = V[mi];
+    v[1] = V[3 + mi];
+    v[2] = V[6 + mi];
+}
+
+// x1,y1 -> x2,y2 (x2^T F x1 = 0); F row-major 3x3.  false for degenerate samples.
+RSAC_HD bool fm_minimal8(const float (&x1)[8], const float (&y1)[8], const float (&x2)[8], const float (&y2)[8],
+                         double *F) {
+    double c1x, c1y, s1, c2x, c2y, s2;
+    if (!fm_norm8(x1, y1, c1x, c1y, s1) || !fm_norm8(x2, y2, c2x, c2y, s2)) return false;
+    double A[8][9];
+    double amax = 0.0;
+    for (int i = 0; i < 8; ++i) {
+        const double u1 = ((double)x1[i] - c1x) * s1, v1 = ((double)y1[i] - c1y) * s1;
+        const double u2 = ((double)x2[i] - c2x) * s2, v2 = ((double)y2[i] - c2y) * s2;
+        A[i][0] = u2 * u1; A[i][1] = u2 * v1; A[i][2] = u2;
+        A[i][3] = v2 * u1; A[i][4] = v2 * v1; A[i][5] = v2;
+        A[i][6] = u1;      A[i][7] = v1;      A[i][8] = 1.0;
+        for (int j = 0; j < 9; ++j) amax = dabs(A[i][j]) > amax ? dabs(A[i][j]) : amax;
+    }
+    int perm[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8};
+    for (int r = 0; r < 8; ++r) {
+        int pr = r, pc = r;
+        double best = -1.0;
+        for (int i = r; i < 8; ++i)
+            for (int j = r; j < 9; ++j)
+                if (dabs(A[i][j]) > best) { best = dabs(A[i][j]); pr = i; pc = j; }
+        if (!(best > 1e-12 * amax)) return false;
+        if (pr != r)
+            for (int j = 0; j < 9; ++j) { const double tmp = A[r][j]; A[r][j] = A[pr][j]; A[pr][j] = tmp; }
+        if (pc != r) {
+            for (int i = 0; i < 8; ++i) { const double tmp = A[i][r]; A[i][r] = A[i][pc]; A[i][pc] = tmp; }
+            const int tp = perm[r]; perm[r] = perm[pc]; perm[pc] = tp;
+        }
+        const double ip = 1.0 / A[r][r];
+        for (int i = 0; i < 8; ++i) {
+            if (i == r) continue;
+            const double f = A[i][r] * ip;
+            if (f == 0.0) continue;
+            for (int j = r; j < 9; ++j) A[i][j] = A[i][j] - f * A[r][j];
+        }
+    }
+    double f[9];
+    f[perm[8]] = 1.0;
+    for (int r = 0; r < 8; ++r) f[perm[r]] = -A[r][8] / A[r][r];
+    // rank 2: Fn (I - v v^T), v the smallest right-singular vector of Fn
+    double M[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) M[3 * i + j] = f[i] * f[j] + f[3 + i] * f[3 + j] + f[6 + i] * f[6 + j];
+    double v[3];
+    sym3_min_evec(M, v);
+    double Fr[9];
+    for (int i = 0; i < 3; ++i) {
+        const double w = f[3 * i] * v[0] + f[3 * i + 1] * v[1] + f[3 * i + 2] * v[2];
+        for (int j = 0; j < 3; ++j) Fr[3 * i + j] = f[3 * i + j] - w * v[j];
+    }
+    // F = T2^T Fr T1, T = [[s, 0, -s cx], [0, s, -s cy], [0, 0, 1]]
+    const double T1[9] = {s1, 0.0, -s1 * c1x, 0.0, s1, -s1 * c1y, 0.0, 0.0, 1.0};
+    const double T2t[9] = {s2, 0.0, 0.0, 0.0, s2, 0.0, -s2 * c2x, -s2 * c2y, 1.0};
+    double tmp[9];
+    mat3mul(T2t, Fr, tmp);
+    mat3mul(tmp, T1, F);
+    double nrm = 0.0;
+    for (int k = 0; k < 9; ++k) nrm = nrm + F[k] * F[k];
+    if (!(nrm > 1e-300) || !dfinite(nrm)) return false;
+    const double in = 1.0 / dsqrt(nrm);
+    for (int k = 0; k < 9; ++k) F[k] = F[k] * in;
+    return true;
+}
+
+// Sampson test, division-free
+RSAC_HD bool fm_inlier(const double *F, double x1, double y1, double x2, double y2, double T) {
+    const double a = dfma(F[0], x1, dfma(F[1], y1, F[2]));
+    const double b = dfma(F[3], x1, dfma(F[4], y1, F[5]));
+    const double c = dfma(F[6], x1, dfma(F[7], y1, F[8]));
+    const double a2 = dfma(F[0], x2, dfma(F[3], y2, F[6]));
+    const double b2 = dfma(F[1], x2, dfma(F[4], y2, F[7]));
+    const double r = dfma(x2, a, dfma(y2, b, c));
+    const double den = dfma(a, a, dfma(b, b, dfma(a2, a2, b2 * b2)));
+    return r * r <= T * den;
+}
+
+// ---------------------------------------------------------------------------
 // Pose refinement: Levenberg-Marquardt on the reprojection error of the
 // inliers (the final solvePnP / solvePnPRefineLM step, main_v1.py:508-509,
 // testpro-K.py:122-125).  Parameters: a rotation increment d[0..2] applied as

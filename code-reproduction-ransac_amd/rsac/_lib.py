@@ -82,6 +82,8 @@ SIGNATURES = [
     ("rsac_update_num_iters", C.c_int, [_d, _d, C.c_int, C.c_int]),
     ("rsac_location_search", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _d, _i32, _d, _u32, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp]),
+    ("rsac_fundamental_ransac", C.c_int, [_vp, _vp, _vp, _i32, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp, _vp]),
+    ("rsac_fundamental_hypotheses", C.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _d, _u64, _u32, _vp, _vp, _vp, _vp]),
     ("rsac_scan_init", None, [_vp, _i32]),
     ("rsac_scan_until_best", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d, _vp]),
     ("rsac_scan_raise", C.c_int, [_vp, _i32, _i32, _i32, _d]),

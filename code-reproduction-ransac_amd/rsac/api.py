@@ -191,6 +191,33 @@ def homography_ransac(src, dst, reproj_thresh: float = 3.0, *, max_iters: int = 
     return out + (_info(code, st),) if return_info else out
 
 
+def fundamental_ransac(pts1, pts2, reproj_thresh: float = 1.5, *, max_iters: int = 100_000,
+                       confidence: float = 0.99, seed: int = 0x5EED, adaptive: bool = True, device=None,
+                       return_info: bool = False, exact_only: bool = False):
+    """Fundamental matrix RANSAC (BASELINE.json configs[3]): 8-point samples, Sampson test.
+
+    pts1, pts2 (N,2) with x2^T F x1 = 0.  Returns (F (3,3) unit Frobenius norm or None, mask).
+    """
+    a = _In(pts1, 2)
+    b = _In(pts2, 2)
+    if a.n != b.n:
+        raise ValueError("pts1 and pts2 differ in length")
+    ctx = L.context(_device_of(a, device))
+    flags = _flags(adaptive, False, "philox", exact_only) | (L.F_DEVICE_IN if a.device else 0)
+    mask, mptr, mflag = _mask_buffer(a, a.n)
+    flags |= mflag
+    F = np.zeros(9)
+    st = L.Stats()
+    with ctx.lock:
+        code = L.check(L.lib().rsac_fundamental_ransac(ctx.handle, C.c_void_p(a.ptr), C.c_void_p(b.ptr), a.n,
+                                                       int(max_iters), float(reproj_thresh), float(confidence),
+                                                       int(seed) & (2**64 - 1), flags, F.ctypes.data,
+                                                       C.c_void_p(mptr), C.byref(st), _stream_of(a)))
+    m = _finish_mask(mask, a.n)
+    out = (F.reshape(3, 3) if code == L.OK else None, m)
+    return out + (_info(code, st),) if return_info else out
+
+
 def _concat(parts, cols):
     arrs = [np.asarray(p, dtype=np.float64).reshape(-1, cols) for p in parts]
     off = np.zeros(len(arrs) + 1, np.int64)
@@ -360,9 +387,12 @@ def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024,
 
     model "pnp": a = points3D (N,3), b = points2D (N,2), K required.
     model "homography": a = src (N,2), b = dst (N,2).
+    model "fundamental": a = pts1 (N,2), b = pts2 (N,2).
     subsets: optional (n_hyps, 4) int32 index table replacing the Philox draw.
     """
     pnp = model == "pnp"
+    if model not in ("pnp", "homography", "fundamental"):
+        raise ValueError(f"unknown model {model!r}")
     A = _In(a, 3 if pnp else 2)
     B = _In(b, 2)
     ctx = L.context(_device_of(A, device))
@@ -379,6 +409,11 @@ def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024,
                                                 int(seed) & (2**64 - 1), flags,
                                                 None if sub is None else sub.ctypes.data, counts.ctypes.data,
                                                 status.ctypes.data, models.ctypes.data, _stream_of(A)))
+        elif model == "fundamental":
+            L.check(L.lib().rsac_fundamental_hypotheses(ctx.handle, C.c_void_p(A.ptr), C.c_void_p(B.ptr), A.n,
+                                                        int(hyp_begin), int(n_hyps), float(reproj_thresh),
+                                                        int(seed) & (2**64 - 1), flags, counts.ctypes.data,
+                                                        status.ctypes.data, models.ctypes.data, _stream_of(A)))
         else:
             L.check(L.lib().rsac_homography_hypotheses(ctx.handle, C.c_void_p(A.ptr), C.c_void_p(B.ptr), A.n,
                                                        int(hyp_begin), int(n_hyps), float(reproj_thresh),

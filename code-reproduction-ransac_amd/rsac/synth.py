@@ -137,3 +137,38 @@ def location_problem(n_features: int = 13, n_locations: int = 458, n_outliers: i
     true_index = int(np.flatnonzero((grid[:, 0] == 0) & (grid[:, 1] == 0))[0])
     locations[true_index] = T
     return dict(pos3d=pos3d, pixels=pixels, locations=locations, true_index=true_index, H=H / H[2, 2])
+
+
+def fundamental_problem(n: int = 50_000, outlier_ratio: float = 0.8, seed: int = 2, noise_px: float = 0.5):
+    """Two synthetic views of a 3D scene (BASELINE.json configs[3]: 50k matches, 80 % outliers, seed 2).
+
+    Returns dict(pts1, pts2 (N,2) pixels, F (3,3) ground truth, x2^T F x1 = 0, unit norm, inlier (N,) bool)."""
+    rng = np.random.default_rng(seed)
+    K = np.array([[1200.0, 0, 960.0], [0, 1200.0, 540.0], [0, 0, 1]])
+    X = np.c_[rng.uniform(-30, 30, n), rng.uniform(-20, 20, n), rng.uniform(40, 120, n)]
+    R2 = random_rotation(rng)
+    # keep the second view close to the first: a small rotation
+    w = rng.normal(size=3) * 0.08
+    th = np.linalg.norm(w)
+    k = w / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    R2 = np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+    t2 = np.array([4.0, 0.5, 0.3]) + rng.normal(size=3) * 0.2
+    x1 = X @ K.T
+    x1 = x1[:, :2] / x1[:, 2:3]
+    X2 = X @ R2.T + t2
+    x2 = X2 @ K.T
+    x2 = x2[:, :2] / x2[:, 2:3]
+    x1 = x1 + rng.normal(0, noise_px, x1.shape)
+    x2 = x2 + rng.normal(0, noise_px, x2.shape)
+    n_out = int(round(outlier_ratio * n))
+    out = rng.permutation(n)[:n_out]
+    inlier = np.ones(n, bool)
+    inlier[out] = False
+    x2[out] = rng.uniform([0, 0], [1920, 1080], (n_out, 2))
+    tx = np.array([[0, -t2[2], t2[1]], [t2[2], 0, -t2[0]], [-t2[1], t2[0], 0]])
+    Ki = np.linalg.inv(K)
+    F = Ki.T @ tx @ R2 @ Ki
+    F = F / np.linalg.norm(F)
+    return dict(pts1=x1, pts2=x2, F=F, inlier=inlier)
+

@@ -146,6 +146,21 @@ RSAC_EXPORT int rsac_location_search(rsac_ctx *ctx, const double *pos3d, const d
                                      int32_t *status_out, int32_t *n_inliers_out, uint8_t *mask_out,
                                      int32_t *n_good_out, void *stream);
 
+/* Fundamental-matrix RANSAC (BASELINE.json configs[3]; the reference has no
+ * implementation -- SURVEY.md §8d -- so DESIGN.md "Fundamental matrix" defines it):
+ * 8-point samples (Philox), normalised 8-point DLT + rank 2, Sampson test
+ * r^2 <= thr^2 (a^2 + b^2 + a'^2 + b'^2) in f64, adaptive RANSACUpdateNumIters with
+ * 8 model points.  pts1, pts2: N x 2 (x2^T F x1 = 0).  Flags: ADAPTIVE, DEVICE_IN,
+ * DEVICE_SOA, DEVICE_OUT, EXACT_ONLY. */
+RSAC_EXPORT int rsac_fundamental_ransac(rsac_ctx *ctx, const void *pts1, const void *pts2, int32_t n, int32_t max_iters,
+                                        double thresh, double confidence, uint64_t seed, uint32_t flags,
+                                        double F_out[9], uint8_t *mask_out, rsac_stats *stats, void *stream);
+/* per-hypothesis probe (status, counts, models) of the fundamental-matrix path */
+RSAC_EXPORT int rsac_fundamental_hypotheses(rsac_ctx *ctx, const void *pts1, const void *pts2, int32_t n,
+                                            int64_t hyp_begin, int32_t n_hyps, double thresh, uint64_t seed,
+                                            uint32_t flags, int32_t *counts_out, int8_t *status_out,
+                                            double *models_out, void *stream);
+
 /* Minimal slice: inlier counts of given poses (H x [R 9, t 3] f64, host)
  * under the reprojection test of PnPRansacCallback::computeError. */
 RSAC_EXPORT int rsac_score_poses(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],

@@ -106,6 +106,16 @@ def lib():
     L.orc_hom_ransac.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_double, C.c_double, C.c_int,
                                  C.c_uint64, C.c_int, _f64p, _u8p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     L.orc_hom_ransac.restype = C.c_int64
+    L.orc_fm_minimal8.argtypes = [_f32p, _f32p, _f32p, _f32p, _f64p]
+    L.orc_fm_minimal8.restype = C.c_int
+    L.orc_fm_count.argtypes = [_f64p, _f32p, _f32p, _f32p, _f32p, C.c_int, C.c_float, C.c_void_p]
+    L.orc_fm_count.restype = C.c_int32
+    L.orc_fm_hypotheses.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_float, C.c_uint64, C.c_int64,
+                                    C.c_int64, _i32p, _i8p, C.c_void_p]
+    L.orc_fm_hypotheses.restype = None
+    L.orc_fm_ransac.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_double, C.c_double, C.c_int, C.c_uint64,
+                                _f64p, _u8p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
+    L.orc_fm_ransac.restype = C.c_int64
     _lib = L
     return L
 
@@ -397,3 +407,41 @@ def best_location(num_matches):
     e2 = np.array(num_matches, np.float64)[:, 1].copy()
     e2[e2 == 0] = 1000000
     return int(np.argmin(e2))
+
+
+# ----------------------------------------------------------------------------------------------
+# fundamental matrix (BASELINE.json configs[3]; semantics defined by the restatement)
+# ----------------------------------------------------------------------------------------------
+def fm_minimal(soa, idx):
+    F = np.zeros(9)
+    sub = [np.ascontiguousarray(a[np.asarray(idx)], np.float32) for a in soa]
+    ok = lib().orc_fm_minimal8(*sub, F)
+    return bool(ok), F.reshape(3, 3)
+
+
+def fm_count(F, soa, thr, mask=False):
+    m = np.zeros(len(soa[0]), np.uint8) if mask else None
+    c = lib().orc_fm_count(np.ascontiguousarray(F, np.float64).reshape(9), *soa, len(soa[0]), thr2(thr), _ptr(m))
+    return (int(c), m.astype(bool)) if mask else int(c)
+
+
+def fm_hypotheses(soa, thr, seed, H, hyp0=0, models=False):
+    n = len(soa[0])
+    counts = np.zeros(H, np.int32)
+    status = np.zeros(H, np.int8)
+    mdl = np.zeros((H, 16)) if models else None
+    lib().orc_fm_hypotheses(*soa, n, thr2(thr), seed, hyp0, H, counts, status, _ptr(mdl))
+    return (counts, status, mdl) if models else (counts, status)
+
+
+def fm_ransac(pts1, pts2, thr=1.5, confidence=0.99, max_iters=100000, seed=0x5EED):
+    soa = soa_hom(pts1, pts2)
+    n = len(soa[0])
+    F = np.zeros(9)
+    mask = np.zeros(n, np.uint8)
+    good = C.c_int32(0)
+    iters = C.c_int64(0)
+    best = lib().orc_fm_ransac(*soa, n, thr, confidence, max_iters, seed, F, mask, C.byref(good), C.byref(iters))
+    return dict(best=int(best), F=F.reshape(3, 3), mask=mask.astype(bool), n_inliers=int(good.value),
+                iters=int(iters.value))
+

@@ -477,3 +477,27 @@ def test_parallel_driver_lo_single_rank_equals_pnp_ransac_lo():
                                     return_info=True)
     assert (res.best, res.n_inliers, res.iters) == (info.best_hyp, info.n_inliers, info.iters)
     assert _bits_equal(res.model[:9].reshape(3, 3), R) and _bits_equal(res.model[9:], t)
+
+
+# ---------------------------------------------------------------------------------------------
+# fundamental matrix (BASELINE.json configs[3]): bit-exact against the restatement
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,outl,H", [(8, 0.0, 64), (60, 0.5, 700), (3000, 0.8, 1500), (20000, 0.8, 600)])
+def test_fundamental_hypotheses_bit_exact(n, outl, H):
+    pr = synth.fundamental_problem(n, outl, seed=n)
+    soa = O.soa_hom(pr["pts1"], pr["pts2"])
+    st, cnt, mdl = rsac.hypotheses("fundamental", pr["pts1"], pr["pts2"], None, 11, H, 1.5, seed=7)
+    oc, os_, om = O.fm_hypotheses(soa, 1.5, 7, H, hyp0=11, models=True)
+    np.testing.assert_array_equal(st, os_)
+    np.testing.assert_array_equal(cnt, oc)
+    assert _bits_equal(mdl[:, :9], om[:, :9])
+
+
+@pytest.mark.parametrize("n,outl", [(5000, 0.5), (50000, 0.8)])
+def test_fundamental_ransac_matches_restatement(n, outl):
+    pr = synth.fundamental_problem(n, outl, seed=2)
+    F, m, info = rsac.fundamental_ransac(pr["pts1"], pr["pts2"], 1.5, max_iters=3000, return_info=True)
+    ref = O.fm_ransac(pr["pts1"], pr["pts2"], 1.5, 0.99, 3000)
+    assert (info.best_hyp, info.n_inliers, info.iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    assert _bits_equal(F, ref["F"])
+    np.testing.assert_array_equal(m, ref["mask"])

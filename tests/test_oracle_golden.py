@@ -183,3 +183,22 @@ def test_scan_semantics_first_strictly_greater():
     status[0] = -1
     best, good, iters = O.scan(counts, status, 100, 4, 0.99, 7)
     assert best == -1 and iters == 0
+
+
+def test_fundamental_minimal_recovers_noise_free_geometry():
+    """The 8-point restatement (no reference implementation exists) recovers the
+    ground-truth F of a noise-free synthetic two-view scene from any 8 inliers."""
+    pr = synth.fundamental_problem(400, 0.0, seed=4, noise_px=0.0)
+    soa = O.soa_hom(pr["pts1"], pr["pts2"])
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        ok, F = O.fm_minimal(soa, rng.choice(400, 8, replace=False))
+        assert ok
+        assert min(np.abs(F - pr["F"]).max(), np.abs(F + pr["F"]).max()) < 1e-5  # f32-rounded pixels
+    assert O.fm_count(pr["F"], soa, 0.1) == 400
+
+
+def test_fundamental_degenerate_sample_rejected():
+    pts = np.c_[np.arange(8.0), 2 * np.arange(8.0)]  # collinear in both images
+    ok, _ = O.fm_minimal(O.soa_hom(pts, pts * 3 + 1), np.arange(8))
+    assert not ok
