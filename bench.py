@@ -235,6 +235,24 @@ def extra_workloads(local, args):
     out["c5_lo_ransac"] = {"points": 100_000, "outlier_ratio": 0.5, "ms_to_best": statistics.median(walls) * 1e3,
                            "iters": info.iters, "n_inliers": info.n_inliers, "lo_improvements": info.lo_improvements,
                            "note": "1 GPU; the multi-GPU form is rsac.parallel.sharded_ransac(lo=True)"}
+    # C4 (BASELINE.json configs[3]): fundamental matrix, 50k matches, 80 % outliers, 100k hypotheses
+    p4 = synth.fundamental_problem(50_000, 0.8, seed=2)
+    f1 = torch.from_numpy(p4["pts1"]).to(dev)
+    f2 = torch.from_numpy(p4["pts2"]).to(dev)
+    walls = []
+    for i in range(4):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        _, _, info4 = rsac.fundamental_ransac(f1, f2, 1.5, max_iters=100_000, adaptive=False, return_info=True,
+                                              device=local)
+        torch.cuda.synchronize()
+        if i >= 1:
+            walls.append(time.perf_counter() - t)
+    w4 = statistics.median(walls)
+    out["c4_fundamental"] = {"matches": 50_000, "outlier_ratio": 0.8, "hyps": 100_000, "ms": w4 * 1e3,
+                             "hyp_s": 100_000 / w4, "n_inliers": info4.n_inliers, "score_ms": info4.score_ms,
+                             "solve_ms": info4.solve_ms,
+                             "note": "8-point + Sampson (f64), inputs in HBM, fixed budget (adaptive off)"}
     lp = synth.location_problem(seed=0)
     walls = []
     for i in range(6):
