@@ -411,6 +411,172 @@ __global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_be
     }
 }
 
+// Variant of k_pnp_score_f32 with a cheaper band and no per-hypothesis branch.
+//   * band: alpha z^2 + beta >= Mz (the MFMA kernel's majorant), so a pair is
+//     decided by E < (T - alpha) z^2 - beta or E > (T + alpha) z^2 + beta, two
+//     fma instead of five operations;
+//   * the unit's records are staged in LDS already transformed (T - alpha,
+//     T + alpha; invalid records rewritten to z = 1 with -inf thresholds, i.e.
+//     decided outliers), so the hypothesis loop has no branch;
+//   * undecided pairs only set a per-lane bit per hypothesis; the exact f64
+//     recount of those pairs runs once per tile, after the hypothesis loop.
+// Counts are bit-identical to the exact kernel (same tests as k_pnp_score_f32).
+// the three tests of one pair: |z| > zg, E < lo (inlier side), E > hi (outlier side)
+struct AbTest {
+    bool zok, lt, gt;
+};
+
+__device__ __forceinline__ AbTest ab_test(const float *m, float x, float y, float zc, float u, float v) {
+    const float xs = __builtin_fmaf(m[0], x, __builtin_fmaf(m[1], y, __builtin_fmaf(m[2], zc, m[9])));
+    const float ys = __builtin_fmaf(m[3], x, __builtin_fmaf(m[4], y, __builtin_fmaf(m[5], zc, m[10])));
+    const float z = __builtin_fmaf(m[6], x, __builtin_fmaf(m[7], y, __builtin_fmaf(m[8], zc, m[11])));
+    const float q1 = __builtin_fmaf(u, z, xs);
+    const float q2 = __builtin_fmaf(v, z, ys);
+    const float z2 = z * z;
+    const float E = __builtin_fmaf(q1, q1, q2 * q2);
+    const float lo = __builtin_fmaf(m[12], z2, -m[13]);
+    const float hi = __builtin_fmaf(m[15], z2, m[13]);
+    return AbTest{__builtin_fabsf(z) > m[14], E < lo, E > hi};
+}
+
+// The exact f64 recount of a tile's undecided pairs (rare).  Returns this
+// lane's share of the hypotheses' counts (lane h: hypothesis h's inliers).
+template <int P>
+__device__ __forceinline__ int ab_fallback(const PnpArgs &a, int prob, int64_t p0, int n, int64_t rec0,
+                                                     int base, int lane, uint32_t wund, uint32_t undm,
+                                                     const float *mlds, const float (&px)[P], const float (&py)[P],
+                                                     const float (&pz)[P], const float (&pu)[P],
+                                                     const float (&pv)[P]) {
+    const double *cm = a.cams + 4 * prob;
+    const Cam k{cm[0], cm[1], cm[2], cm[3]};
+    const float thr2 = a.thr2[prob];
+    int cnt = 0;
+#pragma unroll 1
+    while (wund) {
+        const int h = __builtin_ctz(wund);
+        wund &= wund - 1;
+        const float *m = mlds + h * kFModelStride;
+        const double *md = a.models + (rec0 + h) * kModelStride;
+        int cc = 0;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int i = base + j * 64 + lane;
+            bool ex = false;
+            if ((undm >> h) & 1u) {
+                const AbTest r = ab_test(m, px[j], py[j], pz[j], pu[j], pv[j]);
+                const bool dec = r.zok & (r.lt | r.gt);
+                if (!dec && i < n) {
+                    const int64_t q = p0 + i;
+                    ex = md[kValidSlot] != 0.0 &&
+                         pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <=
+                             thr2;
+                }
+            }
+            cc += __popcll(__ballot(ex));
+        }
+        cnt += (lane == h) ? cc : 0;
+    }
+    return cnt;
+}
+
+template <int P, int HB, int W = 4>  // W: minimum waves per SIMD the register budget must allow
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_ab(
+    PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts) {
+    static_assert(HB <= 32, "undecided bits per lane");
+    __shared__ int red[4][HB];
+    __shared__ int unit_s;
+    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int units_per_prob = (H + HB - 1) / HB;
+    const int n_units = units_per_prob * n_prob;
+    for (;;) {
+        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
+        __syncthreads();
+        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
+        if (unit >= n_units) break;  // uniform: every wave of every block reaches it
+        const int prob = unit / units_per_prob;
+        const int64_t h0 = hyp_begin + (int64_t)(unit % units_per_prob) * HB;
+        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+        const int64_t p0 = a.offsets[prob];
+        const int n = (int)(a.offsets[prob + 1] - p0);
+        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
+        const float cx = fc[2], cy = fc[3], T = fc[4];
+        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+        if (threadIdx.x < HB) {
+            // one thread per record: copy and transform (slots 12 / 15 -> T -+ alpha)
+            const int hq = threadIdx.x;
+            float *dst = mlds + hq * kFModelStride;
+            const float *src = a.fmodels + (rec0 + hq) * kFModelStride;
+            const bool valid = hq < nh && src[14] >= 0.f;
+            if (valid) {
+#pragma unroll
+                for (int q = 0; q < 12; ++q) dst[q] = src[q];
+                dst[12] = T - src[15];
+                dst[13] = src[13];
+                dst[14] = src[14];
+                dst[15] = T + src[15];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 12; ++q) dst[q] = 0.f;
+                dst[11] = 1.f;  // z = 1
+                dst[12] = -__builtin_inff();
+                dst[13] = 0.f;
+                dst[14] = -1.f;
+                dst[15] = -__builtin_inff();
+            }
+        }
+        __syncthreads();
+        const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
+        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
+
+        int cnt = 0;
+        for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
+            float px[P], py[P], pz[P], pu[P], pv[P];
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const int i = base + j * 64 + lane;
+                const bool in = i < n;
+                const int ii = in ? i : 0;
+                px[j] = XC[ii]; py[j] = YC[ii]; pz[j] = ZC[ii];
+                const float uu = U[ii], vv = V[ii];  // unconditional loads (clamped index): no branch
+                // out-of-range lanes: a pixel at 3e38 makes the pair a decided outlier
+                pu[j] = in ? uu - cx : 3.0e38f;
+                pv[j] = in ? vv - cy : 3.0e38f;
+            }
+            uint32_t undm = 0;  // bit h: this lane has an undecided pair with hypothesis h
+#pragma unroll 2
+            for (int h = 0; h < nh; ++h) {
+                const float *m = mlds + h * kFModelStride;
+                int cc = 0;
+                uint64_t und = 0;
+#pragma unroll
+                for (int j = 0; j < P; ++j) {
+                    const AbTest r = ab_test(m, px[j], py[j], pz[j], pu[j], pv[j]);
+                    // one v_cmp per mask, combined on the scalar unit; NaN leaves a pair undecided
+                    const uint64_t mz = __ballot(r.zok);
+                    const uint64_t mi = __ballot(r.lt);
+                    const uint64_t mo = __ballot(r.gt);
+                    cc += __popcll(mi & mz);
+                    und |= ~((mi | mo) & mz);
+                }
+                cnt += (lane == h) ? cc : 0;
+                undm |= __builtin_amdgcn_inverse_ballot_w64(und) ? (1u << h) : 0u;
+            }
+            // exact f64 error (pnp_err, the oracle's formula) for the undecided pairs only
+            uint32_t wund = undm;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) wund |= (uint32_t)__shfl_xor((int)wund, o);
+            wund = __builtin_amdgcn_readfirstlane(wund);
+            if (wund) cnt += ab_fallback<P>(a, prob, p0, n, rec0, base, lane, wund, undm, mlds, px, py, pz, pu, pv);
+        }
+        if (lane < HB) red[wave][lane] = cnt;
+        __syncthreads();
+        if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
+        __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
+    }
+}
+
 // Packed variant of k_pnp_score_f32: the same arithmetic, bit for bit, on two
 // points per instruction (v_pk_fma_f32 / v_pk_mul_f32: two f32 lanes per VGPR
 // pair).  Each lane holds P points as P/2 pairs.
@@ -1065,14 +1231,15 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
-constexpr int kDefaultScoreVariant = 1;  // fastest measured on MI355X
+constexpr int kDefaultScoreVariant = 23;  // fastest measured on MI355X
 static int g_score_variant = kDefaultScoreVariant;
 void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
 
-template <int PP, int HB, int KIND = 0>  // KIND 0 VALU f32, 1 packed f32, 2 MFMA (PP = point chunks of 16)
+template <int PP, int HB, int KIND = 0, int W = 4>  // KIND 0 VALU f32, 1 packed f32, 2 MFMA (PP = point chunks of 16), 3 alpha-beta (W waves/SIMD)
 static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
     auto kern = [] {
-        if constexpr (KIND == 2) return k_pnp_score_mfma<HB, PP>;
+        if constexpr (KIND == 3) return k_pnp_score_ab<PP, HB, W>;
+        else if constexpr (KIND == 2) return k_pnp_score_mfma<HB, PP>;
         else if constexpr (KIND == 1) return k_pnp_score_pk<PP, HB>;
         else return k_pnp_score_f32<PP, HB>;
     }();
@@ -1110,6 +1277,15 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 13: launch_f32<4, 32, 2>(a, P, hyp_begin, H, counts, s); break;
             case 14: launch_f32<8, 16, 2>(a, P, hyp_begin, H, counts, s); break;
             case 15: launch_f32<2, 32, 2>(a, P, hyp_begin, H, counts, s); break;
+            case 16: launch_f32<4, 32, 3>(a, P, hyp_begin, H, counts, s); break;
+            case 17: launch_f32<4, 16, 3>(a, P, hyp_begin, H, counts, s); break;
+            case 18: launch_f32<8, 32, 3>(a, P, hyp_begin, H, counts, s); break;
+            case 19: launch_f32<2, 32, 3>(a, P, hyp_begin, H, counts, s); break;
+            case 20: launch_f32<6, 32, 3>(a, P, hyp_begin, H, counts, s); break;
+            case 21: launch_f32<4, 32, 3, 5>(a, P, hyp_begin, H, counts, s); break;
+            case 22: launch_f32<4, 32, 3, 6>(a, P, hyp_begin, H, counts, s); break;
+            case 23: launch_f32<8, 32, 3, 5>(a, P, hyp_begin, H, counts, s); break;
+            case 24: launch_f32<2, 32, 3, 6>(a, P, hyp_begin, H, counts, s); break;
             default: launch_f32<kScoreP, kScoreHB>(a, P, hyp_begin, H, counts, s); break;
         }
     } else

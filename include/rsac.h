@@ -91,7 +91,8 @@ RSAC_EXPORT int rsac_abi_version(void);
 RSAC_EXPORT int rsac_device_count(void);
 RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
 /* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default;
- * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 MFMA tilings).  Counts,
+ * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 MFMA tilings, 16..20 the
+ * branch-free alpha-beta band tilings).  Counts,
  * masks and models never depend on it. */
 RSAC_EXPORT int rsac_set_score_variant(int variant);
 
