@@ -545,7 +545,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
                 pv[j] = in ? vv - cy : 3.0e38f;
             }
             uint32_t undm = 0;  // bit h: this lane has an undecided pair with hypothesis h
-#pragma unroll 2
             for (int h = 0; h < nh; ++h) {
                 const float *m = mlds + h * kFModelStride;
                 int cc = 0;

@@ -179,7 +179,47 @@ RSAC_HD void lt_refine(double &L0, double &L1, double &L2, double a12, double a1
 
 // y: 3 unit bearings (row-major 3x3), x: 3 world points.  Writes up to 4
 // (R, t); returns the count.
-RSAC_HD int p3p_lambdatwist(const double *y, const double *x, double *Rs, double *ts) {
+// One candidate (lambda1..3) of the Lambda Twist solver: Gauss-Newton refine, then
+// the pose from the scaled bearings; emitted if finite.  Returns 1 if emitted.
+template <class Emit>
+RSAC_HD int p3p_pose(double l1, double l2, double l3, double a12, double a13, double a23, double b12, double b13,
+                     double b23, const double *y1, const double *y2, const double *y3, const double *x1,
+                     const double *Xi, Emit &emit) {
+    lt_refine(l1, l2, l3, a12, a13, a23, b12, b13, b23);
+    double ry1[3], ry2[3], ry3[3], yd1[3], yd2[3], yc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { ry1[k] = y1[k] * l1; ry2[k] = y2[k] * l2; ry3[k] = y3[k] * l3; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { yd1[k] = ry1[k] - ry2[k]; yd2[k] = ry1[k] - ry3[k]; }
+    yc[0] = yd1[1] * yd2[2] - yd1[2] * yd2[1];
+    yc[1] = yd1[2] * yd2[0] - yd1[0] * yd2[2];
+    yc[2] = yd1[0] * yd2[1] - yd1[1] * yd2[0];
+    const double Y[9] = {yd1[0], yd2[0], yc[0], yd1[1], yd2[1], yc[1], yd1[2], yd2[2], yc[2]};
+    double R[9], t[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc)
+            R[3 * r + cc] = Y[3 * r] * Xi[cc] + Y[3 * r + 1] * Xi[3 + cc] + Y[3 * r + 2] * Xi[6 + cc];
+    bool fin = true;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const double rx = R[3 * r] * x1[0] + R[3 * r + 1] * x1[1] + R[3 * r + 2] * x1[2];
+        t[r] = ry1[r] - rx;
+        fin = fin && dfinite(t[r]);
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) fin = fin && dfinite(R[k]);
+    if (!fin) return 0;
+    emit(R, t);
+    return 1;
+}
+
+// Every solution (R, t), in the order of the restatement's solution list, is
+// handed to emit(R, t) as it is built: no solution arrays, so the GPU solver
+// keeps everything in registers.  Returns the number of solutions.
+template <class Emit>
+RSAC_HD int p3p_lambdatwist(const double *y, const double *x, Emit &&emit) {
     const double *y1 = y, *y2 = y + 3, *y3 = y + 6;
     const double *x1 = x, *x2 = x + 3, *x3 = x + 6;
     double b12 = -2.0 * (y1[0] * y2[0] + y1[1] * y2[1] + y1[2] * y2[2]);
@@ -245,8 +285,21 @@ RSAC_HD int p3p_lambdatwist(const double *y, const double *x, double *Rs, double
     double vq = -e2 / e1;
     double v = dsqrt(vq > 0.0 ? vq : 0.0);
 
-    double Ls[4][3];
-    int valid = 0;
+    // X = [d12 d13 d12xd13] (columns), its inverse by the adjugate
+    double M[9] = {d12[0], d13[0], d12xd13[0], d12[1], d13[1], d12xd13[1], d12[2], d13[2], d12xd13[2]};
+    double Xi[9];
+    {
+        double c00 = M[4] * M[8] - M[5] * M[7];
+        double c01 = M[5] * M[6] - M[3] * M[8];
+        double c02 = M[3] * M[7] - M[4] * M[6];
+        double det = M[0] * c00 + M[1] * c01 + M[2] * c02;
+        if (det == 0.0 || !dfinite(det)) return 0;
+        double id = 1.0 / det;
+        Xi[0] = c00 * id; Xi[1] = (M[2] * M[7] - M[1] * M[8]) * id; Xi[2] = (M[1] * M[5] - M[2] * M[4]) * id;
+        Xi[3] = c01 * id; Xi[4] = (M[0] * M[8] - M[2] * M[6]) * id; Xi[5] = (M[2] * M[3] - M[0] * M[5]) * id;
+        Xi[6] = c02 * id; Xi[7] = (M[1] * M[6] - M[0] * M[7]) * id; Xi[8] = (M[0] * M[4] - M[1] * M[3]) * id;
+    }
+    int nout = 0;
     for (int sgn = 0; sgn < 2; ++sgn) {
         double s = sgn == 0 ? v : -v;
         double w2 = 1.0 / (s * v2[0] - v1[0]);
@@ -266,56 +319,13 @@ RSAC_HD int p3p_lambdatwist(const double *y, const double *x, double *Rs, double
                         double l2 = dsqrt(d);
                         double l3 = tq * l2;
                         double l1 = w0 * l2 + w1 * l3;
-                        if (l1 >= 0.0) { Ls[valid][0] = l1; Ls[valid][1] = l2; Ls[valid][2] = l3; ++valid; }
+                        if (l1 >= 0.0) nout += p3p_pose(l1, l2, l3, a12, a13, a23, b12, b13, b23, y1, y2, y3, x1, Xi, emit);
                     }
                 }
             }
         }
     }
-    for (int i = 0; i < valid; ++i) lt_refine(Ls[i][0], Ls[i][1], Ls[i][2], a12, a13, a23, b12, b13, b23);
 
-    // X = [d12 d13 d12xd13] (columns), its inverse by the adjugate
-    double M[9] = {d12[0], d13[0], d12xd13[0], d12[1], d13[1], d12xd13[1], d12[2], d13[2], d12xd13[2]};
-    double Xi[9];
-    {
-        double c00 = M[4] * M[8] - M[5] * M[7];
-        double c01 = M[5] * M[6] - M[3] * M[8];
-        double c02 = M[3] * M[7] - M[4] * M[6];
-        double det = M[0] * c00 + M[1] * c01 + M[2] * c02;
-        if (det == 0.0 || !dfinite(det)) return 0;
-        double id = 1.0 / det;
-        Xi[0] = c00 * id; Xi[1] = (M[2] * M[7] - M[1] * M[8]) * id; Xi[2] = (M[1] * M[5] - M[2] * M[4]) * id;
-        Xi[3] = c01 * id; Xi[4] = (M[0] * M[8] - M[2] * M[6]) * id; Xi[5] = (M[2] * M[3] - M[0] * M[5]) * id;
-        Xi[6] = c02 * id; Xi[7] = (M[1] * M[6] - M[0] * M[7]) * id; Xi[8] = (M[0] * M[4] - M[1] * M[3]) * id;
-    }
-    int nout = 0;
-    for (int i = 0; i < valid; ++i) {
-        double ry1[3], ry2[3], ry3[3], yd1[3], yd2[3], yc[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { ry1[k] = y1[k] * Ls[i][0]; ry2[k] = y2[k] * Ls[i][1]; ry3[k] = y3[k] * Ls[i][2]; }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { yd1[k] = ry1[k] - ry2[k]; yd2[k] = ry1[k] - ry3[k]; }
-        yc[0] = yd1[1] * yd2[2] - yd1[2] * yd2[1];
-        yc[1] = yd1[2] * yd2[0] - yd1[0] * yd2[2];
-        yc[2] = yd1[0] * yd2[1] - yd1[1] * yd2[0];
-        double Y[9] = {yd1[0], yd2[0], yc[0], yd1[1], yd2[1], yc[1], yd1[2], yd2[2], yc[2]};
-        double *R = Rs + 9 * nout, *t = ts + 3 * nout;
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int cc = 0; cc < 3; ++cc)
-                R[3 * r + cc] = Y[3 * r] * Xi[cc] + Y[3 * r + 1] * Xi[3 + cc] + Y[3 * r + 2] * Xi[6 + cc];
-        bool fin = true;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            double rx = R[3 * r] * x1[0] + R[3 * r + 1] * x1[1] + R[3 * r + 2] * x1[2];
-            t[r] = ry1[r] - rx;
-            fin = fin && dfinite(t[r]);
-        }
-#pragma unroll
-        for (int k = 0; k < 9; ++k) fin = fin && dfinite(R[k]);
-        if (fin) ++nout;
-    }
     return nout;
 }
 
@@ -336,29 +346,29 @@ RSAC_HD bool pnp_minimal(const float (&X)[4], const float (&Y)[4], const float (
         bearing(k, U[j], V[j], yb + 3 * j);
         xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
     }
-    double Rs[36], ts[12];
-    int ns = p3p_lambdatwist(yb, xw, Rs, ts);
-    if (ns == 0) return false;
-    double X4 = X[3], Y4 = Y[3], Z4 = Z[3];
-    int best = -1;
+    const double X4 = X[3], Y4 = Y[3], Z4 = Z[3];
+    bool have = false;
     double best_e = 0.0;
-    for (int s = 0; s < ns; ++s) {
-        const double *Rk = Rs + 9 * s, *tk = ts + 3 * s;
+    // the 4th point picks the solution: smallest reprojection error, first one on ties
+    const int ns = p3p_lambdatwist(yb, xw, [&](const double *Rk, const double *tk) {
         double x = Rk[0] * X4 + Rk[1] * Y4; x = x + Rk[2] * Z4; x = x + tk[0];
         double y = Rk[3] * X4 + Rk[4] * Y4; y = y + Rk[5] * Z4; y = y + tk[1];
         double z = Rk[6] * X4 + Rk[7] * Y4; z = z + Rk[8] * Z4; z = z + tk[2];
-        double iz = (z != 0.0) ? 1.0 / z : 1.0;
-        double du = (x * iz) * k.fx + k.cx - (double)U[3];
-        double dv = (y * iz) * k.fy + k.cy - (double)V[3];
-        double e = du * du + dv * dv;
-        if (!(e == e)) continue;
-        if (best < 0 || e < best_e) { best = s; best_e = e; }
-    }
-    if (best < 0) return false;
+        const double iz = (z != 0.0) ? 1.0 / z : 1.0;
+        const double du = (x * iz) * k.fx + k.cx - (double)U[3];
+        const double dv = (y * iz) * k.fy + k.cy - (double)V[3];
+        const double e = du * du + dv * dv;
+        if (!(e == e)) return;
+        if (!have || e < best_e) {
+            have = true;
+            best_e = e;
 #pragma unroll
-    for (int q = 0; q < 9; ++q) R[q] = Rs[9 * best + q];
+            for (int q = 0; q < 9; ++q) R[q] = Rk[q];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) t[q] = ts[3 * best + q];
+            for (int q = 0; q < 3; ++q) t[q] = tk[q];
+        }
+    });
+    if (ns == 0 || !have) return false;
     return true;
 }
 
