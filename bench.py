@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--cpu-hyps", type=int, default=150_000, help="CPU baseline sample (hypotheses, 1 thread)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ms-to-best", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the C3 batch and location-search lines")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C3/C4/C5 and location-search lines")
+    ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo only to rehearse "
+                                                       "the N>1 path on fewer GPUs than ranks)")
     return ap.parse_args()
 
 
@@ -64,10 +66,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if args.backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())  # rehearsal: ranks may share a GPU
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -110,7 +117,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        et = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        et = torch.tensor([elapsed], dtype=torch.float64, device=par._comm_device(None))
         dist.all_reduce(et, op=dist.ReduceOp.MAX)
         elapsed = float(et.item())
 
@@ -152,7 +159,7 @@ def main():
             if i >= 2:
                 host_ms.append((time.perf_counter() - t) * 1e3)
         pcie_rate = H / (statistics.median(host_ms) * 1e-3)
-        extras = {} if args.no_extras else extra_workloads(local, args)
+        extras = {} if (args.no_extras or world > 1) else extra_workloads(local, args)
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(pr, args)
