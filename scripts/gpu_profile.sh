@@ -7,15 +7,15 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
 TAG=${TAG:-r01}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o run --output-format csv -- \
-    python3 bench.py --steps 10 --warmup 3 --no-cpu --no-ms-to-best > gpurun_out/prof/bench_under_rocprof.log 2>&1
+    python3 bench.py --steps 10 --warmup 3 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/bench_under_rocprof.log 2>&1
 rc=$?; echo "rocprof kernel-trace rc=$rc"; tail -2 gpurun_out/prof/bench_under_rocprof.log
 [ $rc -eq 0 ] || exit $rc
 if [ -n "$PMC" ]; then
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/pmc_fetch -o run --output-format csv -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best > gpurun_out/prof/pmc_fetch.log 2>&1
+      python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/pmc_fetch.log 2>&1
   rc=$?; echo "rocprof pmc FETCH_SIZE rc=$rc"; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/pmc_write -o run --output-format csv -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best > gpurun_out/prof/pmc_write.log 2>&1
+      python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/pmc_write.log 2>&1
   rc=$?; echo "rocprof pmc WRITE_SIZE rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 find gpurun_out/prof -name "*.csv" | head -20
