@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) wund |= (uint32_t)__shfl_xor((int)wund, o);
             wund = __builtin_amdgcn_readfirstlane(wund);
-            if (wund) cnt += ab_fallback<P>(a, prob, p0, n, rec0, base, lane, wund, undm, mlds, px, py, pz, pu, pv);
+            if (__builtin_expect(wund != 0, 0)) cnt += ab_fallback<P>(a, prob, p0, n, rec0, base, lane, wund, undm, mlds, px, py, pz, pu, pv);
         }
         if (lane < HB) red[wave][lane] = cnt;
         __syncthreads();
