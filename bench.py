@@ -86,32 +86,34 @@ def main():
     solve_ms = []
 
     ev = par.PnPShard(pr["points2d"], pr["points3d"], K, args.thr, device=local)
+    nccl = dist is not None and args.backend == "nccl"
 
     def step():
-        key, model, mask, info = rsac.evaluate_range(ev.p2, ev.p3, K, base, H, args.thr, return_info=True,
-                                                     with_mask=True, device=local)
-        score_ms.append(info.score_ms)
-        solve_ms.append(info.solve_ms)
+        # one pass over the batch, asynchronous end to end: solve + score + fused best key + the
+        # winner's mask stay on the device; for N > 1 the key is all-reduced (RCCL, MAX) and every
+        # rank re-derives the global winner's model and mask from it (rsac_pnp_winner), so no
+        # step waits for the host
+        key_t, model_t, mask = rsac.evaluate_range(ev.p2, ev.p3, K, base, H, args.thr, with_mask=True,
+                                                   device_result=True)
         if dist is None:
-            return key >> 32
-        gkey = par.all_reduce_max_key(max(key, 0))
-        if gkey != key:
-            # the winner lives on another rank: re-derive its model from the hypothesis index
-            # (Philox counter, one P3P solve) and its mask on this rank -- no broadcast
-            _, idx = par.unpack_key(gkey)
-            mask, _ = rsac.pose_mask(ev.p2, ev.p3, K, ev.model(idx), args.thr, device=local)
-        return gkey >> 32
+            return key_t
+        if nccl:
+            dist.all_reduce(key_t, op=dist.ReduceOp.MAX)
+        else:  # gloo rehearsal: host round trip
+            kc = key_t.cpu()
+            dist.all_reduce(kc, op=dist.ReduceOp.MAX)
+            key_t.copy_(kc)
+        rsac.winner(ev.p2, ev.p3, K, key_t, args.thr)
+        return key_t
 
     for _ in range(args.warmup):
         step()
-    score_ms.clear()
-    solve_ms.clear()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        cnt = step()
+        key_t = step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -120,6 +122,13 @@ def main():
         et = torch.tensor([elapsed], dtype=torch.float64, device=par._comm_device(None))
         dist.all_reduce(et, op=dist.ReduceOp.MAX)
         elapsed = float(et.item())
+
+    cnt = int(key_t.item()) >> 32
+    # kernel times of the same call, from the HIP events of a synchronous run (outside the timed loop)
+    for _ in range(3):
+        _, _, info = rsac.evaluate_range(ev.p2, ev.p3, K, base, H, args.thr, return_info=True, device=local)
+        score_ms.append(info.score_ms)
+        solve_ms.append(info.solve_ms)
 
     out = None
     if rank == 0:

@@ -116,6 +116,9 @@ struct rsac_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    // the last async copy out of h_pts / h_small: the host waits on it before rewriting the
+    // buffer (calls may return before their copies ran, RSAC_F_ASYNC)
+    hipEvent_t ev_pts = nullptr, ev_small = nullptr;
     int64_t round_size = 4096;
     // device scratch
     DevBuf pts, tables, models, status, counts, subsets, substatus, best, bestmodels, mask;
@@ -125,6 +128,7 @@ struct rsac_ctx {
     DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
     DevBuf loc;                                                // location search: inputs, pos2, H, err
     DevBuf lo;                                                 // LO-RANSAC: 2 model records, 2 counts, 2 masks
+    DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     // pinned host staging
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask;
 };
@@ -185,6 +189,7 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
         return RSAC_OK;
     }
     // host float64 AoS -> float32 SoA (the CV_32F conversion of OpenCV), pinned, one H2D copy
+    HIPCHK(hipEventSynchronize(c->ev_pts));
     HIPCHK(c->h_pts.ensure(sizeof(float) * nc * std::max<int64_t>(N, 1)));
     float *H = c->h_pts.as<float>();
     const double *A = (const double *)a, *B = (const double *)b;
@@ -194,6 +199,7 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
         H[(ncomp_a + 1) * N + i] = (float)B[2 * i + 1];
     }
     HIPCHK(hipMemcpyAsync(D, H, sizeof(float) * nc * N, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(c->ev_pts, s));
     for (int k = 0; k < nc; ++k) st.h[k] = H + k * N;
     st.host_ready = true;
     return RSAC_OK;
@@ -221,6 +227,7 @@ int stage_tables(rsac_ctx *c, const Staged &st, const double *K, double thresh, 
     const size_t off_b = al(sizeof(int64_t) * (P + 1)), cam_b = al(sizeof(double) * 4 * P), thr_b = al(sizeof(float) * P);
     const size_t tot = off_b + cam_b + thr_b;
     HIPCHK(c->tables.ensure(tot));
+    HIPCHK(hipEventSynchronize(c->ev_small));
     HIPCHK(c->h_small.ensure(tot));
     char *hs = c->h_small.as<char>();
     memcpy(hs, st.off.data(), sizeof(int64_t) * (P + 1));
@@ -238,6 +245,7 @@ int stage_tables(rsac_ctx *c, const Staged &st, const double *K, double thresh, 
     for (int p = 0; p < P; ++p) ht[p] = t2;
     char *d = c->tables.as<char>();
     HIPCHK(hipMemcpyAsync(d, hs, tot, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(c->ev_small, s));
     c->d_off = (int64_t *)d;
     c->d_cams = (double *)(d + off_b);
     c->d_thr2 = (float *)(d + off_b + cam_b);
@@ -699,7 +707,9 @@ int rsac_create(int device, rsac_ctx **out) {
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ev2) != hipSuccess) {
+        hipEventCreate(&c->ev2) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_pts, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_small, hipEventDisableTiming) != hipSuccess) {
         rsac_destroy(c);
         return fail(RSAC_EHIP, "stream/event creation failed");
     }
@@ -713,7 +723,7 @@ void rsac_destroy(rsac_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
-                     &c->frame, &c->fconst,   &c->fmodels, &c->queue};
+                     &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};
@@ -721,6 +731,8 @@ void rsac_destroy(rsac_ctx *c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
+    if (c->ev_pts) (void)hipEventDestroy(c->ev_pts);
+    if (c->ev_small) (void)hipEventDestroy(c->ev_small);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -830,6 +842,27 @@ int rsac_location_search(rsac_ctx *c, const double *pos3d, const double *pixels,
     return r;
 }
 
+int rsac_pnp_winner(rsac_ctx *c, const double *pts3d, const double *pts2d, int32_t n, const double K[9], double thr,
+                    uint64_t seed, const int64_t *key, double *model_out, uint8_t *mask_out, void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (!pts3d || !pts2d || !K || !key || n < 4) return fail(RSAC_EINVAL, "bad arguments");
+    hipStream_t s = pick_stream(c, stream);
+    HIPCHK(c->win.ensure(sizeof(double) * (kModelStride + 8)));
+    double *rec = c->win.as<double>();
+    double *cam = rec + kModelStride;
+    const double cm[4] = {K[0], K[4], K[2], K[5]};
+    HIPCHK(c->h_small.ensure(64));
+    HIPCHK(hipEventSynchronize(c->ev_small));
+    double *hc = c->h_small.as<double>();
+    memcpy(hc, cm, sizeof cm);
+    hc[4] = (double)(float)(thr * thr);
+    HIPCHK(hipMemcpyAsync(cam, hc, 5 * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(c->ev_small, s));
+    HIPCHK(launch_pnp_winner(pts3d, pts2d, n, cam, seed, key, rec, model_out, mask_out, s));
+    return RSAC_OK;
+}
+
 int rsac_pnp_local_opt(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
                        const double model_in[12], double thr, uint32_t flags, double model_out[12], int32_t *count_out,
                        int32_t *steps_out, void *stream) {
@@ -913,6 +946,8 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
     if (r) return r;
     if (n < 4) return fail(RSAC_ETOOFEW, "need >= 4 correspondences");
     if (n_hyps <= 0 || n_hyps > INT32_MAX || !K || !key_out) return fail(RSAC_EINVAL, "bad arguments");
+    if ((flags & RSAC_F_ASYNC) && mask_out && !(flags & RSAC_F_DEVICE_OUT))
+        return fail(RSAC_EINVAL, "RSAC_F_ASYNC needs a device mask (RSAC_F_DEVICE_OUT)");
     hipStream_t s = pick_stream(c, stream);
     Staged st;
     r = stage_points(c, pts3d, pts2d, 3, nullptr, 1, n, flags & ~RSAC_F_SAMPLER_OPENCV, s, st);
@@ -943,6 +978,15 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
             hmask_dev = c->mask.as<uint8_t>();
         }
         HIPCHK(launch_pnp_mask_key(a, n, dkey, hmask_dev, s));
+    }
+    if (flags & RSAC_F_ASYNC) {
+        // results stay on the device, nothing waits: the packed key (0 = no model) and the
+        // winner's R, t are copied to the caller's device buffers in stream order
+        HIPCHK(hipMemcpyAsync(key_out, dkey, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        if (model_out)
+            HIPCHK(hipMemcpyAsync(model_out, c->bestmodels.p, 12 * sizeof(double), hipMemcpyDeviceToDevice, s));
+        if (stats) memset(stats, 0, sizeof(*stats));
+        return RSAC_OK;
     }
     HIPCHK(c->h_bestmodels.ensure(sizeof(double) * (kModelStride + 2)));
     double *hb = c->h_bestmodels.as<double>();

@@ -117,6 +117,10 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
 hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, int32_t *count,
                                   hipStream_t s);
 
+// re-solve the hypothesis named by a device packed key (+ its mask); cam = fx fy cx cy thr2
+hipError_t launch_pnp_winner(const double *p3, const double *p2, int32_t n, const double *cam, uint64_t seed,
+                             const int64_t *key, double *rec, double *model_out, uint8_t *mask, hipStream_t s);
+
 // camera-location search (main_v1.py:254-348): pos2 of every (location, feature) pair, then
 // err1 / err2 of every location's homography
 hipError_t launch_loc_pos2(const double *p3, const double *px, int32_t n, const double *locs, int32_t L, double *src,

@@ -1698,4 +1698,63 @@ hipError_t launch_fm_mask(const HomArgs &a, int32_t P, int32_t max_n, const int6
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Winner re-derivation (rsac_pnp_winner): the hypothesis named by a device-
+// resident packed key is re-solved from its Philox counter (the same draw and
+// P3P as k_pnp_solve, from the f64 AoS inputs rounded to f32 exactly as
+// k_pnp_prepare rounds them), then its RANSAC-test mask.  No host round trip.
+// cam: fx fy cx cy thr2 (f64).
+// ---------------------------------------------------------------------------
+__global__ void k_pnp_winner_solve(const double *__restrict__ p3, const double *__restrict__ p2, int32_t n,
+                                   const double *__restrict__ cam, uint64_t seed, const int64_t *__restrict__ key,
+                                   double *__restrict__ rec, double *__restrict__ model_out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const unsigned long long kk = (unsigned long long)*key;
+    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
+    bool ok = false;
+    if (kk != 0 && n >= 4) {
+        const uint64_t idx = 0xFFFFFFFFull - (kk & 0xFFFFFFFFull);
+        Philox rng;
+        rng.init(seed, 0u, idx);
+        int32_t id[4];
+        if (rng.subset<4>(n, id) == 0) {
+            float X[4], Y[4], Z[4], U[4], V[4];
+            for (int j = 0; j < 4; ++j) {
+                X[j] = (float)p3[3 * id[j]]; Y[j] = (float)p3[3 * id[j] + 1]; Z[j] = (float)p3[3 * id[j] + 2];
+                U[j] = (float)p2[2 * id[j]]; V[j] = (float)p2[2 * id[j] + 1];
+            }
+            const Cam k{cam[0], cam[1], cam[2], cam[3]};
+            ok = pnp_minimal(X, Y, Z, U, V, k, R, t);
+        }
+    }
+    for (int q = 0; q < 9; ++q) rec[q] = ok ? R[q] : 0.0;
+    for (int q = 0; q < 3; ++q) rec[9 + q] = ok ? t[q] : 0.0;
+    rec[kValidSlot] = ok ? 1.0 : 0.0;
+    if (model_out)
+        for (int q = 0; q < 12; ++q) model_out[q] = rec[q];
+}
+
+__global__ void k_pnp_winner_mask(const double *__restrict__ p3, const double *__restrict__ p2, int32_t n,
+                                  const double *__restrict__ cam, const double *__restrict__ rec,
+                                  uint8_t *__restrict__ mask) {
+    const Cam k{cam[0], cam[1], cam[2], cam[3]};
+    const float thr2 = (float)cam[4];
+    const bool valid = rec[kValidSlot] != 0.0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const double X = (float)p3[3 * i], Y = (float)p3[3 * i + 1], Z = (float)p3[3 * i + 2];
+        mask[i] = valid && pnp_err(rec, rec + 9, k, X, Y, Z, (float)p2[2 * i], (float)p2[2 * i + 1]) <= thr2;
+    }
+}
+
+hipError_t launch_pnp_winner(const double *p3, const double *p2, int32_t n, const double *cam, uint64_t seed,
+                             const int64_t *key, double *rec, double *model_out, uint8_t *mask, hipStream_t s) {
+    hipLaunchKernelGGL(k_pnp_winner_solve, dim3(1), dim3(64), 0, s, p3, p2, n, cam, seed, key, rec, model_out);
+    if (mask) {
+        unsigned g = cdiv(n > 0 ? n : 1, 256);
+        if (g > 1024) g = 1024;
+        hipLaunchKernelGGL(k_pnp_winner_mask, dim3(g), dim3(256), 0, s, p3, p2, n, cam, rec, mask);
+    }
+    return hipGetLastError();
+}
+
 }  // namespace rsac

@@ -30,6 +30,7 @@ F_DEVICE_SOA = 1 << 4
 F_DEVICE_OUT = 1 << 5
 F_EXACT_ONLY = 1 << 6
 F_LO = 1 << 7
+F_ASYNC = 1 << 8
 
 ABI_VERSION = 1
 
@@ -84,6 +85,7 @@ SIGNATURES = [
                                        _vp, _vp]),
     ("rsac_fundamental_ransac", C.c_int, [_vp, _vp, _vp, _i32, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp, _vp]),
     ("rsac_fundamental_hypotheses", C.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _d, _u64, _u32, _vp, _vp, _vp, _vp]),
+    ("rsac_pnp_winner", C.c_int, [_vp, _vp, _vp, _i32, _vp, _d, _u64, _vp, _vp, _vp, _vp]),
     ("rsac_scan_init", None, [_vp, _i32]),
     ("rsac_scan_until_best", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d, _vp]),
     ("rsac_scan_raise", C.c_int, [_vp, _i32, _i32, _i32, _d]),

@@ -347,25 +347,46 @@ def score_poses(points2D, points3D, K, poses, reproj_thresh: float = 30.0, devic
 
 def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_thresh: float = 30.0, *,
                    seed: int = 0x5EED, device=None, return_info: bool = False, exact_only: bool = False,
-                   with_mask: bool = False):
+                   with_mask: bool = False, device_result: bool = False):
     """Evaluate Philox hypotheses [hyp_begin, hyp_begin + n_hyps) of one problem.
 
     Returns (key, model12[, mask][, info]) where key = (count << 32) | (0xFFFFFFFF - best_index)
     (or -1) and mask is the best hypothesis' RANSAC-phase mask (with_mask=True; on the GPU for
     GPU inputs).  The sharded driver (rsac.parallel) all-reduces the key with MAX.
+
+    device_result=True (GPU tensor inputs): nothing waits for the GPU; key is a 1-element int64
+    tensor (raw packed key, 0 = no model) and model12 a float64 tensor, both on the device.
     """
     p3 = _In(points3D, 3)
     p2 = _In(points2D, 2)
+    if device_result and not p3.device:
+        raise ValueError("device_result needs GPU tensor inputs")
     ctx = L.context(_device_of(p3, device))
     flags = (L.F_DEVICE_IN if p3.device else 0) | (L.F_EXACT_ONLY if exact_only else 0)
-    key = C.c_int64(-1)
-    model = np.zeros(12)
     K9 = _K9(K)
     st = L.Stats()
     mask = mptr = None
     if with_mask:
         mask, mptr, mflag = _mask_buffer(p3, p3.n)
         flags |= mflag
+    if device_result:
+        import torch
+        dev = p3.keep.device
+        key_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        model_t = torch.zeros(12, dtype=torch.float64, device=dev)
+        with ctx.lock:
+            L.check(L.lib().rsac_pnp_evaluate_range(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n,
+                                                    K9.ctypes.data, int(hyp_begin), int(n_hyps),
+                                                    float(reproj_thresh), int(seed) & (2**64 - 1),
+                                                    flags | L.F_ASYNC,
+                                                    C.cast(key_t.data_ptr(), C.POINTER(C.c_int64)),
+                                                    C.c_void_p(model_t.data_ptr()),
+                                                    C.c_void_p(mptr) if with_mask else None, C.byref(st),
+                                                    _stream_of(p3)))
+        out = (key_t, model_t)
+        return out + (_finish_mask(mask, p3.n),) if with_mask else out
+    key = C.c_int64(-1)
+    model = np.zeros(12)
     with ctx.lock:
         code = L.check(L.lib().rsac_pnp_evaluate_range(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n,
                                                        K9.ctypes.data, int(hyp_begin), int(n_hyps),
@@ -379,6 +400,27 @@ def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_th
     if return_info:
         out = out + (_info(code, st),)
     return out
+
+
+def winner(points2D, points3D, K, key, reproj_thresh: float = 30.0, *, seed: int = 0x5EED, with_mask: bool = True):
+    """Re-derive the hypothesis named by a device packed key (e.g. after an all-reduce) on this
+    GPU: (model12 tensor, mask tensor) without a host round trip (rsac_pnp_winner)."""
+    import torch
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    if not p3.device:
+        raise ValueError("winner() needs GPU tensor inputs")
+    ctx = L.context(_device_of(p3, None))
+    dev = p3.keep.device
+    model_t = torch.zeros(12, dtype=torch.float64, device=dev)
+    mask_t = torch.empty(max(p3.n, 1), dtype=torch.uint8, device=dev) if with_mask else None
+    K9 = _K9(K)
+    with ctx.lock:
+        L.check(L.lib().rsac_pnp_winner(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n, K9.ctypes.data,
+                                        float(reproj_thresh), int(seed) & (2**64 - 1), C.c_void_p(key.data_ptr()),
+                                        C.c_void_p(model_t.data_ptr()),
+                                        C.c_void_p(mask_t.data_ptr()) if with_mask else None, _stream_of(p3)))
+    return model_t, (_finish_mask(mask_t, p3.n) if with_mask else None)
 
 
 def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024, reproj_thresh: float = 30.0, *,

@@ -65,6 +65,7 @@ extern "C" {
 #define RSAC_F_DEVICE_SOA (1u << 4)     /* inputs are device float32 SoA (implies device) */
 #define RSAC_F_DEVICE_OUT (1u << 5)     /* inlier mask output is a device pointer */
 #define RSAC_F_EXACT_ONLY (1u << 6)     /* disable the float32 pre-filter in scoring (A/B and tests) */
+#define RSAC_F_ASYNC (1u << 8)          /* rsac_pnp_evaluate_range: device outputs, no host wait (see there) */
 #define RSAC_F_LO (1u << 7)             /* LO-RANSAC (PnP, one problem): local optimisation at every new best,
                                            BASELINE.json configs[4]; see DESIGN.md "LO-RANSAC" */
 
@@ -162,6 +163,16 @@ RSAC_EXPORT int rsac_fundamental_hypotheses(rsac_ctx *ctx, const void *pts1, con
                                             uint32_t flags, int32_t *counts_out, int8_t *status_out,
                                             double *models_out, void *stream);
 
+/* The winner of a sharded run, re-derived on every rank without a host round trip
+ * ("the winning model is re-derivable from hyp_idx on every rank"):
+ * key = device pointer to the all-reduced packed key (count << 32 | ~index; 0 = none);
+ * pts3d / pts2d = device f64 AoS; writes the hypothesis' R 9, t 3 to model_out
+ * (device, 12 doubles; zeros for key 0) and its RANSAC-test mask to mask_out (device,
+ * n bytes, optional).  Asynchronous on `stream`. */
+RSAC_EXPORT int rsac_pnp_winner(rsac_ctx *ctx, const double *pts3d, const double *pts2d, int32_t n, const double K[9],
+                                double thresh, uint64_t seed, const int64_t *key, double *model_out,
+                                uint8_t *mask_out, void *stream);
+
 /* Minimal slice: inlier counts of given poses (H x [R 9, t 3] f64, host)
  * under the reprojection test of PnPRansacCallback::computeError. */
 RSAC_EXPORT int rsac_score_poses(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
@@ -174,7 +185,10 @@ RSAC_EXPORT int rsac_score_poses(rsac_ctx *ctx, const void *pts3d, const void *p
  * (count << 32) | (0xFFFFFFFF - low32(global index)) of the best one (lowest
  * index among ties), that hypothesis' model (R, t) and, if mask_out is
  * given, its RANSAC-phase mask (device pointer with RSAC_F_DEVICE_OUT).
- * Ranks all-reduce(MAX) the key. */
+ * Ranks all-reduce(MAX) the key.
+ * RSAC_F_ASYNC: key_out (one int64, the raw packed key, 0 = no model) and model_out
+ * (12 doubles) are DEVICE pointers, mask_out must be a device pointer too; the call only
+ * enqueues work on `stream` and returns RSAC_OK without waiting (no stats). */
 RSAC_EXPORT int rsac_pnp_evaluate_range(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
                             int64_t hyp_begin, int64_t n_hyps, double reproj_thresh, uint64_t seed, uint32_t flags,
                             int64_t *key_out, double model_out[12], uint8_t *mask_out, rsac_stats *stats,

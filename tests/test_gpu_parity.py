@@ -501,3 +501,36 @@ def test_fundamental_ransac_matches_restatement(n, outl):
     assert (info.best_hyp, info.n_inliers, info.iters) == (ref["best"], ref["n_inliers"], ref["iters"])
     assert _bits_equal(F, ref["F"])
     np.testing.assert_array_equal(m, ref["mask"])
+
+
+# ---------------------------------------------------------------------------------------------
+# asynchronous device-result path (bench step) and the on-device winner re-derivation
+# ---------------------------------------------------------------------------------------------
+def test_async_evaluate_range_and_winner_match_sync():
+    import torch
+    pr = synth.pnp_problem(6000, 0.5, seed=61)
+    p2 = torch.from_numpy(pr["points2d"]).cuda()
+    p3 = torch.from_numpy(pr["points3d"]).cuda()
+    # back-to-back async calls with different thresholds / ranges on one context: the pinned
+    # staging buffers must not be overwritten before their copies ran
+    outs = [rsac.evaluate_range(p2, p3, pr["K"], b, 3000, thr, with_mask=True, device_result=True)
+            for b, thr in [(0, 30.0), (3000, 12.0), (6000, 30.0), (9000, 50.0)]]
+    torch.cuda.synchronize()
+    for (key_t, model_t, mask_t), (b, thr) in zip(outs, [(0, 30.0), (3000, 12.0), (6000, 30.0), (9000, 50.0)]):
+        key, model, mask = rsac.evaluate_range(pr["points2d"], pr["points3d"], pr["K"], b, 3000, thr, with_mask=True)
+        assert int(key_t.item()) == key
+        assert _bits_equal(model_t.cpu().numpy(), model)
+        np.testing.assert_array_equal(mask_t.cpu().numpy(), mask)
+        # the winner re-derived from the key alone (what a losing rank does)
+        wm, wmask = rsac.winner(p2, p3, pr["K"], key_t, thr)
+        assert _bits_equal(wm.cpu().numpy(), model)
+        np.testing.assert_array_equal(wmask.cpu().numpy(), mask)
+
+
+def test_winner_of_empty_key_is_zero():
+    import torch
+    pr = synth.pnp_problem(500, 0.5, seed=62)
+    p2 = torch.from_numpy(pr["points2d"]).cuda()
+    p3 = torch.from_numpy(pr["points3d"]).cuda()
+    wm, wmask = rsac.winner(p2, p3, pr["K"], torch.zeros(1, dtype=torch.int64, device="cuda"), 30.0)
+    assert not wm.cpu().numpy().any() and not wmask.cpu().numpy().any()
