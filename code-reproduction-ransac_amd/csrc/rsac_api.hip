@@ -968,7 +968,6 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
     HIPCHK(hipEventRecord(c->ev1, s));
     HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
     HIPCHK(hipEventRecord(c->ev2, s));
-    HIPCHK(launch_key_model(c->models.as<double>(), dkey, hyp_begin, c->bestmodels.as<double>(), s));
     uint8_t *hmask_dev = nullptr;
     if (mask_out) {
         if (flags & RSAC_F_DEVICE_OUT) {
@@ -977,14 +976,13 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
             HIPCHK(c->mask.ensure(std::max(n, 1)));
             hmask_dev = c->mask.as<uint8_t>();
         }
-        HIPCHK(launch_pnp_mask_key(a, n, dkey, hmask_dev, s));
     }
-    if (flags & RSAC_F_ASYNC) {
-        // results stay on the device, nothing waits: the packed key (0 = no model) and the
-        // winner's R, t are copied to the caller's device buffers in stream order
-        HIPCHK(hipMemcpyAsync(key_out, dkey, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-        if (model_out)
-            HIPCHK(hipMemcpyAsync(model_out, c->bestmodels.p, 12 * sizeof(double), hipMemcpyDeviceToDevice, s));
+    const bool async = (flags & RSAC_F_ASYNC) != 0;
+    HIPCHK(launch_pnp_key_finish(a, n, dkey, hmask_dev, c->bestmodels.as<double>(), async ? model_out : nullptr,
+                                 async ? key_out : nullptr, s));
+    if (async) {
+        // results stay on the device and nothing waits: the raw packed key (0 = no model) and
+        // the winner's R, t were written to the caller's device buffers in stream order
         if (stats) memset(stats, 0, sizeof(*stats));
         return RSAC_OK;
     }

@@ -67,6 +67,10 @@ constexpr int kLanePts = 256;
 // mask of the hypothesis a packed key names (problem 0, records at hyp 0..)
 hipError_t launch_pnp_mask_key(const PnpArgs &a, int32_t n, const unsigned long long *key, uint8_t *mask,
                                hipStream_t s);
+// evaluate_range's epilogue in one launch: record named by the key -> rec16 (+ model12, the raw
+// key -> key_out, when non-null) and its mask (when non-null); problem 0
+hipError_t launch_pnp_key_finish(const PnpArgs &a, int32_t n, const unsigned long long *key, uint8_t *mask,
+                                 double *rec16, double *model12, int64_t *key_out, hipStream_t s);
 // record of the hypothesis a packed key names -> out[16] (zeros when key == 0)
 hipError_t launch_key_model(const double *models, const unsigned long long *key, int64_t rng_base, double *out,
                             hipStream_t s);

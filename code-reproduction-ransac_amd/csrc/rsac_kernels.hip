@@ -103,10 +103,8 @@ __global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *_
 // Per problem: frame = {c0 c1 c2 (bbox centre), B >= |XC|inf, rho >= |XC - (Xf - c)|,
 // max|Xf|, wmax (bound on |x/z| of any projection within thr of a pixel), 0};
 // fconst = {fx fy cx cy T 2.002 sqrt(T) 1e-6 T thr 2/fx 2/fy cu cv cc0} (see the scoring kernel).
-__global__ void k_pnp_frame(PnpArgs a, int32_t P, const int *__restrict__ ws, double *__restrict__ frame,
-                            float *__restrict__ fconst) {
-    const int prob = blockIdx.x * blockDim.x + threadIdx.x;
-    if (prob >= P) return;
+__device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *__restrict__ ws,
+                              double *__restrict__ frame, float *__restrict__ fconst) {
     const int n = (int)(a.offsets[prob + 1] - a.offsets[prob]);
     const double *cm = a.cams + 4 * prob;
     const double fx = fabs(cm[0]), fy = fabs(cm[1]), cx = cm[2], cy = cm[3];
@@ -141,14 +139,22 @@ __global__ void k_pnp_frame(PnpArgs a, int32_t P, const int *__restrict__ ws, do
     for (int k = 13; k < kFconstStride; ++k) q[k] = 0.f;
 }
 
-__global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, const double *__restrict__ frame,
+// centred coordinates; block 0 of each problem also writes the problem's frame and
+// constants (one launch instead of two).  The centre is recomputed from the bounds
+// in every block with the frame's own arithmetic.
+__global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const int *__restrict__ ws,
+                                                    double *__restrict__ frame, float *__restrict__ fconst,
                                                     float *__restrict__ XC, float *__restrict__ YC,
                                                     float *__restrict__ ZC) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
-    const double *f = frame + (int64_t)prob * kFrameStride;
-    const double c0 = f[0], c1 = f[1], c2 = f[2];
+    if (blockIdx.x == 0 && threadIdx.x == 0) pnp_frame_one(a, P, prob, ws, frame, fconst);
+    double cc[3] = {0, 0, 0};
+    if (n > 0)
+        for (int k = 0; k < 3; ++k)
+            cc[k] = ((double)ord2f(ws[5 * prob + k]) + (double)ord2f(ws[5 * P + 5 * prob + k])) * 0.5;
+    const double c0 = cc[0], c1 = cc[1], c2 = cc[2];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int64_t q = p0 + i;
         XC[q] = (float)((double)a.X[q] - c0);
@@ -944,6 +950,35 @@ __global__ void k_pnp_mask_key(PnpArgs a, int32_t n, const unsigned long long *_
                     : 0;
 }
 
+// The end of an evaluate_range call in one launch: the record named by the packed key
+// -> rec16 (and R, t -> model12, the raw key -> key_out, when given) and its
+// RANSAC-test mask (when given).
+__global__ void k_pnp_key_finish(PnpArgs a, int32_t n, const unsigned long long *__restrict__ key,
+                                 uint8_t *__restrict__ mask, double *__restrict__ rec16, double *__restrict__ model12,
+                                 int64_t *__restrict__ key_out) {
+    const unsigned long long k = *key;
+    const double *m = nullptr;
+    if (k) {
+        const uint64_t low = 0xFFFFFFFFull - (k & 0xFFFFFFFFull);
+        const int64_t h = (int64_t)((low - ((uint64_t)a.rng_base & 0xFFFFFFFFull)) & 0xFFFFFFFFull);
+        m = a.models + h * kModelStride;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < kModelStride) {
+        const int q = threadIdx.x;
+        const double v = m ? m[q] : 0.0;
+        rec16[q] = v;
+        if (model12 && q < 12) model12[q] = v;
+        if (key_out && q == 0) *key_out = (int64_t)k;
+    }
+    if (!mask) return;
+    const double *c = a.cams;
+    const Cam cam{c[0], c[1], c[2], c[3]};
+    const float thr2 = a.thr2[0];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        mask[i] = m ? (pnp_err(m, m + 9, cam, (double)a.X[i], (double)a.Y[i], (double)a.Z[i], a.U[i], a.V[i]) <= thr2)
+                    : 0;
+}
+
 // per-call state reset in one launch: bounds sentinels, best key, work-queue counter
 __global__ void k_pnp_init(int32_t P, int *__restrict__ ws, unsigned long long *__restrict__ key,
                            int *__restrict__ queue) {
@@ -1212,10 +1247,9 @@ hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t 
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 2048);
     if (g > 32) g = 32;
     hipLaunchKernelGGL(k_pnp_bounds, dim3(g, P), dim3(256), 0, s, a, P, ws);
-    hipLaunchKernelGGL(k_pnp_frame, dim3(cdiv(P, 64)), dim3(64), 0, s, a, P, ws, frame, fconst);
     unsigned g2 = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g2 > 1024) g2 = 1024;
-    hipLaunchKernelGGL(k_pnp_center, dim3(g2, P), dim3(256), 0, s, a, frame, XC, YC, ZC);
+    hipLaunchKernelGGL(k_pnp_center, dim3(g2, P), dim3(256), 0, s, a, P, ws, frame, fconst, XC, YC, ZC);
     return hipGetLastError();
 }
 
@@ -1335,6 +1369,14 @@ hipError_t launch_pnp_mask_key(const PnpArgs &a, int32_t n, const unsigned long 
     unsigned g = cdiv(n > 0 ? n : 1, 256);
     if (g > 1024) g = 1024;
     hipLaunchKernelGGL(k_pnp_mask_key, dim3(g), dim3(256), 0, s, a, n, key, mask);
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_key_finish(const PnpArgs &a, int32_t n, const unsigned long long *key, uint8_t *mask,
+                                 double *rec16, double *model12, int64_t *key_out, hipStream_t s) {
+    unsigned g = mask ? cdiv(n > 0 ? n : 1, 256) : 1;
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_pnp_key_finish, dim3(g), dim3(256), 0, s, a, n, key, mask, rec16, model12, key_out);
     return hipGetLastError();
 }
 
