@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--cpu-hyps", type=int, default=150_000, help="CPU baseline sample (hypotheses, 1 thread)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ms-to-best", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the C3/C4/C5 and location-search lines")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C3/C4/C5, location-search and DEM-march lines")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo only to rehearse "
                                                        "the N>1 path on fewer GPUs than ranks)")
     return ap.parse_args()
@@ -172,6 +172,8 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(pr, args)
+            if "dem_ray_march" in extras:
+                extras["dem_ray_march"]["cpu_baseline"] = cpu_baseline_dem(args)
         out = {
             "metric": METRIC,
             "value": value,
@@ -280,7 +282,55 @@ def extra_workloads(local, args):
                               "ms": statistics.median(walls) * 1e3,
                               "note": "find_homographies of main_v1.py:254-297 (OpenCV-sampler RANSAC + LM refit + "
                                       "err1/err2) for every candidate, one call"}
+    out["dem_ray_march"] = dem_workload(local)
     return out
+
+
+def dem_workload(local, n_rays=4096):
+    """pixel_to_geo's march (main_v1.py:635-684) for n_rays pixels of a synthetic 577x577 SRTM-like
+    DEM (rsac.synth.dem_problem), inputs in HBM, one call; kernel time by HIP events."""
+    from rsac import dem
+    pr = synth.dem_problem(n_rays, seed=0)
+    g = dem.DemGrid.from_geotransform(pr["z"], pr["gt"])
+    e, n = dem.wgs84_to_utm(pr["origin_lonlat"][None], device=local)[0]
+    origin = np.array([e, n, pr["origin_height"]])
+    dev = torch.device("cuda", local)
+    d = torch.from_numpy(pr["dirs"]).to(dev)
+    ms = []
+    for i in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        hits, st = dem.ray_intersect_dem(origin, d, g)
+        b.record()
+        torch.cuda.synchronize()
+        if i >= 1:
+            ms.append(a.elapsed_time(b))
+    st = st.cpu().numpy()
+    h = hits.cpu().numpy()
+    w = statistics.median(ms)
+    steps_hit = np.rint(np.linalg.norm(h[st == 0] - origin, axis=1)) + 1
+    return {"rays": n_rays, "ms": w, "rays_s": n_rays / w * 1e3, "hit": int((st == 0).sum()),
+            "no_hit": int((st == 1).sum()), "off_dem": int((st == 2).sum()),
+            "mean_steps_of_hits": float(steps_hit.mean()) if steps_hit.size else None,
+            "note": "1 m steps, <=10000 per ray, UTM->WGS84 + bilinear DEM per step (f64); inputs in HBM"}
+
+
+def cpu_baseline_dem(args, n_rays=3):
+    """CPU leg for the DEM march: the literal per-ray loop of oracle/dem_oracle.py (numpy scalar
+    steps + scipy RegularGridInterpolator, as main_v1.py:635-656) on a few rays of the same scene."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import dem_oracle as D
+    pr = synth.dem_problem(n_rays, seed=0)
+    gt = pr["gt"]
+    e, n = D.wgs84_to_utm(*pr["origin_lonlat"])
+    o = np.array([e, n, pr["origin_height"]])
+    interp = D.make_interpolator(pr["z"], gt[3], gt[5], gt[0], gt[1])
+    t = time.perf_counter()
+    for i in range(n_rays):
+        D.ray_intersect_dem(o, pr["dirs"][i], interp)
+    dt = time.perf_counter() - t
+    return {"value": n_rays / dt, "unit": "rays/s", "cores": 1, "kind": "port",
+            "sample": f"{n_rays} rays of the dem_ray_march scene, literal Python loop, {dt:.1f} s"}
 
 
 def cpu_baseline(pr, args):

@@ -129,6 +129,7 @@ struct rsac_ctx {
     DevBuf loc;                                                // location search: inputs, pos2, H, err
     DevBuf lo;                                                 // LO-RANSAC: 2 model records, 2 counts, 2 masks
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
+    DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
     // pinned host staging
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask;
 };
@@ -723,7 +724,7 @@ void rsac_destroy(rsac_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
-                     &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win};
+                     &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};
@@ -840,6 +841,70 @@ int rsac_location_search(rsac_ctx *c, const double *pos3d, const double *pixels,
     if (ninl_out) memcpy(ninl_out, ninl.data(), sizeof(int32_t) * L);
     if (mask_out) memcpy(mask_out, m.data(), pairs);
     return r;
+}
+
+int rsac_utm_convert(rsac_ctx *c, int inverse, const double *in, int64_t n, int32_t zone, int32_t south,
+                     uint32_t flags, double *out, void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (!in || !out || n < 0 || zone < 1 || zone > 60) return fail(RSAC_EINVAL, "bad arguments");
+    if (n == 0) return RSAC_OK;
+    hipStream_t s = pick_stream(c, stream);
+    const bool dev = (flags & RSAC_F_DEVICE_IN) != 0;
+    const double *din = in;
+    double *dout = out;
+    if (!dev) {
+        HIPCHK(c->geo.ensure(sizeof(double) * 4 * (size_t)n));
+        double *b = c->geo.as<double>();
+        HIPCHK(hipMemcpyAsync(b, in, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
+        din = b;
+        dout = b + 2 * n;
+    }
+    HIPCHK(launch_utm(inverse != 0, din, n, zone, south != 0, dout, s));
+    if (!dev) {
+        HIPCHK(hipMemcpyAsync(out, dout, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return RSAC_OK;
+}
+
+int rsac_dem_ray_intersect(rsac_ctx *c, const double *origins, const double *dirs, int32_t n_rays, const double *dem,
+                           int32_t ny, int32_t nx, double y0, double dy, double x0, double dx, int32_t zone,
+                           int32_t south, double max_search_dist, double step, int32_t min_steps, uint32_t flags,
+                           double *hits_out, int8_t *status_out, void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (!origins || !dirs || !dem || !hits_out || !status_out || n_rays < 0 || ny < 2 || nx < 2 || dy == 0.0 ||
+        dx == 0.0 || !(step > 0.0) || zone < 1 || zone > 60)
+        return fail(RSAC_EINVAL, "bad arguments");
+    if (n_rays == 0) return RSAC_OK;
+    // int(max_search_dist / step) of the reference's range()
+    const double q = max_search_dist / step;
+    const int32_t n_steps = q >= 2147483647.0 ? 2147483647 : (q > 0 ? (int32_t)q : 0);
+    hipStream_t s = pick_stream(c, stream);
+    const bool dev = (flags & RSAC_F_DEVICE_IN) != 0;
+    const size_t cells = (size_t)ny * nx;
+    const double *d_o = origins, *d_d = dirs, *d_dem = dem;
+    double *d_hits = hits_out;
+    int8_t *d_st = status_out;
+    if (!dev) {
+        HIPCHK(c->geo.ensure(sizeof(double) * (9 * (size_t)n_rays + cells) + (size_t)n_rays + 64));
+        double *b = c->geo.as<double>();
+        double *bo = b, *bd = b + 3 * (size_t)n_rays, *bh = bd + 3 * (size_t)n_rays, *bz = bh + 3 * (size_t)n_rays;
+        int8_t *bs = (int8_t *)(bz + cells);
+        HIPCHK(hipMemcpyAsync(bo, origins, sizeof(double) * 3 * n_rays, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(bd, dirs, sizeof(double) * 3 * n_rays, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(bz, dem, sizeof(double) * cells, hipMemcpyHostToDevice, s));
+        d_o = bo; d_d = bd; d_dem = bz; d_hits = bh; d_st = bs;
+    }
+    HIPCHK(launch_dem_march(d_o, d_d, n_rays, d_dem, ny, nx, y0, dy, x0, dx, zone, south != 0, n_steps, step,
+                            min_steps, d_hits, d_st, s));
+    if (!dev) {
+        HIPCHK(hipMemcpyAsync(hits_out, d_hits, sizeof(double) * 3 * n_rays, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(status_out, d_st, n_rays, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return RSAC_OK;
 }
 
 int rsac_pnp_winner(rsac_ctx *c, const double *pts3d, const double *pts2d, int32_t n, const double K[9], double thr,

@@ -125,6 +125,12 @@ hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *mod
 hipError_t launch_pnp_winner(const double *p3, const double *p2, int32_t n, const double *cam, uint64_t seed,
                              const int64_t *key, double *rec, double *model_out, uint8_t *mask, hipStream_t s);
 
+// UTM <-> WGS84 (lon, lat degrees / easting, northing), and the DEM ray march (rsac_geo.h)
+hipError_t launch_utm(bool inverse, const double *in, int64_t n, int zone, bool south, double *out, hipStream_t s);
+hipError_t launch_dem_march(const double *o, const double *d, int32_t n, const double *dem, int32_t ny, int32_t nx,
+                            double y0, double dy, double x0, double dx, int zone, bool south, int32_t n_steps,
+                            double step, int32_t min_steps, double *hits, int8_t *status, hipStream_t s);
+
 // camera-location search (main_v1.py:254-348): pos2 of every (location, feature) pair, then
 // err1 / err2 of every location's homography
 hipError_t launch_loc_pos2(const double *p3, const double *px, int32_t n, const double *locs, int32_t L, double *src,

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 
+#include "rsac_geo.h"
 #include "rsac_internal.h"
 #include "rsac_math.h"
 
@@ -1796,6 +1797,58 @@ hipError_t launch_pnp_winner(const double *p3, const double *p2, int32_t n, cons
         if (g > 1024) g = 1024;
         hipLaunchKernelGGL(k_pnp_winner_mask, dim3(g), dim3(256), 0, s, p3, p2, n, cam, rec, mask);
     }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Geodesy and the DEM ray march (rsac_geo.h): one lane per point / ray
+// ---------------------------------------------------------------------------
+__global__ void k_utm_inverse(const double *__restrict__ en, int64_t n, TmConst k, UtmZone z,
+                              double *__restrict__ lonlat) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        utm_inverse(k, z, en[2 * i], en[2 * i + 1], lonlat[2 * i], lonlat[2 * i + 1]);
+}
+
+__global__ void k_utm_forward(const double *__restrict__ lonlat, int64_t n, TmConst k, UtmZone z,
+                              double *__restrict__ en) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        utm_forward(k, z, lonlat[2 * i], lonlat[2 * i + 1], en[2 * i], en[2 * i + 1]);
+}
+
+__global__ __launch_bounds__(64) void k_dem_march(const double *__restrict__ o, const double *__restrict__ d, int32_t n,
+                                                  DemGrid g, TmConst k, UtmZone z, int32_t n_steps, double step,
+                                                  int32_t min_steps, double *__restrict__ hits,
+                                                  int8_t *__restrict__ status) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double nan = __builtin_nan("");
+    double pos[3] = {nan, nan, nan};  // no hit: NaN (the reference's None)
+    const int st = dem_march(k, z, g, o + 3 * i, d + 3 * i, n_steps, step, min_steps, pos);
+    hits[3 * i] = pos[0];
+    hits[3 * i + 1] = pos[1];
+    hits[3 * i + 2] = pos[2];
+    status[i] = (int8_t)st;
+}
+
+hipError_t launch_utm(bool inverse, const double *in, int64_t n, int zone, bool south, double *out, hipStream_t s) {
+    const TmConst k = tm_const();
+    const UtmZone z = utm_zone(zone, south);
+    unsigned g = cdiv(n > 0 ? n : 1, 256);
+    if (g > 4096) g = 4096;
+    if (inverse)
+        hipLaunchKernelGGL(k_utm_inverse, dim3(g), dim3(256), 0, s, in, n, k, z, out);
+    else
+        hipLaunchKernelGGL(k_utm_forward, dim3(g), dim3(256), 0, s, in, n, k, z, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_dem_march(const double *o, const double *d, int32_t n, const double *dem, int32_t ny, int32_t nx,
+                            double y0, double dy, double x0, double dx, int zone, bool south, int32_t n_steps,
+                            double step, int32_t min_steps, double *hits, int8_t *status, hipStream_t s) {
+    const DemGrid g{dem, ny, nx, y0, dy, x0, dx};
+    // small blocks: rays march for different numbers of steps, so waves retire independently
+    hipLaunchKernelGGL(k_dem_march, dim3(cdiv(n > 0 ? n : 1, 64)), dim3(64), 0, s, o, d, n, g, tm_const(),
+                       utm_zone(zone, south), n_steps, step, min_steps, hits, status);
     return hipGetLastError();
 }
 

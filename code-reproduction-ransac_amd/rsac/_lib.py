@@ -86,6 +86,9 @@ SIGNATURES = [
     ("rsac_fundamental_ransac", C.c_int, [_vp, _vp, _vp, _i32, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp, _vp]),
     ("rsac_fundamental_hypotheses", C.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _d, _u64, _u32, _vp, _vp, _vp, _vp]),
     ("rsac_pnp_winner", C.c_int, [_vp, _vp, _vp, _i32, _vp, _d, _u64, _vp, _vp, _vp, _vp]),
+    ("rsac_utm_convert", C.c_int, [_vp, C.c_int, _vp, _i64, _i32, _i32, _u32, _vp, _vp]),
+    ("rsac_dem_ray_intersect", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _i32, _d, _d, _d, _d, _i32, _i32, _d, _d,
+                                         _i32, _u32, _vp, _vp, _vp]),
     ("rsac_scan_init", None, [_vp, _i32]),
     ("rsac_scan_until_best", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d, _vp]),
     ("rsac_scan_raise", C.c_int, [_vp, _i32, _i32, _i32, _d]),

@@ -172,3 +172,49 @@ def fundamental_problem(n: int = 50_000, outlier_ratio: float = 0.8, seed: int =
     F = F / np.linalg.norm(F)
     return dict(pts1=x1, pts2=x2, F=F, inlier=inlier)
 
+
+
+KULIANG_LONLAT = (119.3906, 26.0936)   # potential_camera_locations.csv area, UTM zone 50N
+
+
+def camera_rotation(azimuth_deg: float, tilt_deg: float) -> np.ndarray:
+    """R (UTM -> camera, x right, y down, z forward) of a camera looking at the azimuth (from
+    north, clockwise) and tilted down by tilt_deg, as pixel_to_ray uses it (main_v1.py:569)."""
+    az, tl = np.radians(azimuth_deg), np.radians(tilt_deg)
+    z = np.array([np.sin(az) * np.cos(tl), np.cos(az) * np.cos(tl), -np.sin(tl)])
+    x = np.array([np.cos(az), -np.sin(az), 0.0])
+    y = np.cross(z, x)
+    return np.stack([x, y, z])
+
+
+def dem_problem(n_rays: int = 4096, seed: int = 0, half_extent_deg: float = 0.08, cell_deg: float = 1.0 / 3600,
+                n_hills: int = 14, azimuth_deg: float = 40.0, tilt_deg: float = 0.0, height_above: float = 300.0):
+    """A DEM scene for the ray march (main_v1.py:635-684; the reference's dem_data.tif is not shipped).
+
+    DEM: north-up grid (GDAL geotransform gt = (x0, dx, 0, y0, 0, dy), dy < 0) of
+    ``cell_deg`` cells (SRTM 1" by default) spanning +-half_extent_deg around Kuliang, smooth
+    hills of 100-600 m over a 300 m plain.  Camera: at the centre, ``height_above`` m above the
+    terrain, pose from ``camera_rotation``; rays = pixels uniform over the image, so a share of
+    them points above the horizon (no hit, or off the DEM).
+
+    Returns dict(z (ny,nx) f64, gt (6,), K, R, pixels (n,2), dirs (n,3), origin_lonlat (2,),
+    origin_height); the caller projects origin_lonlat to UTM (rsac.dem.wgs84_to_utm)."""
+    from .dem import pixel_to_ray
+    rng = np.random.default_rng(seed)
+    lon0, lat0 = KULIANG_LONLAT
+    n = int(round(2 * half_extent_deg / cell_deg)) + 1
+    gt = (lon0 - half_extent_deg, cell_deg, 0.0, lat0 + half_extent_deg, 0.0, -cell_deg)
+    lat = np.arange(n) * gt[5] + gt[3]
+    lon = np.arange(n) * gt[1] + gt[0]
+    LA, LO = np.meshgrid(lat, lon, indexing="ij")
+    z = np.full((n, n), 300.0)
+    for _ in range(n_hills):
+        cy, cx = lat0 + rng.uniform(-1, 1) * half_extent_deg, lon0 + rng.uniform(-1, 1) * half_extent_deg
+        s = rng.uniform(0.004, 0.02)
+        z += rng.uniform(100, 600) * np.exp(-((LA - cy) ** 2 + (LO - cx) ** 2) / (2 * s * s))
+    K = main_v1_K()
+    R = camera_rotation(azimuth_deg, tilt_deg)
+    pixels = rng.uniform([0, 0], [IMAGE_W, IMAGE_H], (n_rays, 2))
+    dirs = pixel_to_ray(pixels, K, R)
+    return dict(z=z, gt=np.array(gt), K=K, R=R, pixels=pixels, dirs=dirs, origin_lonlat=np.array([lon0, lat0]),
+                origin_height=float(z[n // 2, n // 2]) + height_above)

@@ -173,6 +173,29 @@ RSAC_EXPORT int rsac_pnp_winner(rsac_ctx *ctx, const double *pts3d, const double
                                 double thresh, uint64_t seed, const int64_t *key, double *model_out,
                                 uint8_t *mask_out, void *stream);
 
+/* GeoCoordTransformer (main_v1.py:36-57, pyproj EPSG:4326 <-> EPSG:326zz/327zz):
+ * inverse != 0: (easting, northing) -> (lon, lat) degrees; inverse == 0: the reverse.
+ * in, out: n x 2 f64 (host, or device with RSAC_F_DEVICE_IN: enqueued on `stream`, no wait).
+ * Krueger's series to 6th order (DESIGN.md "DEM ray march"). */
+RSAC_EXPORT int rsac_utm_convert(rsac_ctx *ctx, int inverse, const double *in, int64_t n, int32_t zone, int32_t south,
+                                 uint32_t flags, double *out, void *stream);
+
+/* ray_intersect_dem (main_v1.py:635-656) for n_rays rays at once: from origins[i] (UTM
+ * easting, northing, height) march along dirs[i] in `step` m steps, int(max_search_dist /
+ * step) times; a ray hits at the first position, from step index min_steps (150 in the
+ * reference) on, not above the DEM.  The DEM is the reference's RegularGridInterpolator over
+ * (lat, lon): dem ny x nx f64 row-major, lat_i = i * dy + y0, lon_j = j * dx + x0 (GDAL
+ * geotransform: y0 = gt[3], dy = gt[5], x0 = gt[0], dx = gt[1]); each step's UTM position is
+ * converted with the zone's inverse projection.  Outputs: hits_out n x 3 (NaN without a hit), status_out n:
+ * 0 hit, 1 no hit within the distance (None), 2 left the DEM (the reference's caught
+ * interpolation error, None).  Host arrays, or device with RSAC_F_DEVICE_IN (all of them; the
+ * call then only enqueues on `stream` and returns without waiting). */
+RSAC_EXPORT int rsac_dem_ray_intersect(rsac_ctx *ctx, const double *origins, const double *dirs, int32_t n_rays,
+                                       const double *dem, int32_t ny, int32_t nx, double y0, double dy, double x0,
+                                       double dx, int32_t zone, int32_t south, double max_search_dist, double step,
+                                       int32_t min_steps, uint32_t flags, double *hits_out, int8_t *status_out,
+                                       void *stream);
+
 /* Minimal slice: inlier counts of given poses (H x [R 9, t 3] f64, host)
  * under the reprojection test of PnPRansacCallback::computeError. */
 RSAC_EXPORT int rsac_score_poses(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
