@@ -308,10 +308,22 @@ def dem_workload(local, n_rays=4096):
     st = st.cpu().numpy()
     h = hits.cpu().numpy()
     w = statistics.median(ms)
+    # polygon-sized call (one 1898.json object's outline): latency, a block per ray
+    d64 = d[:64].contiguous()
+    ms64 = []
+    for i in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        dem.ray_intersect_dem(origin, d64, g)
+        b.record()
+        torch.cuda.synchronize()
+        if i >= 1:
+            ms64.append(a.elapsed_time(b))
     steps_hit = np.rint(np.linalg.norm(h[st == 0] - origin, axis=1)) + 1
     return {"rays": n_rays, "ms": w, "rays_s": n_rays / w * 1e3, "hit": int((st == 0).sum()),
             "no_hit": int((st == 1).sum()), "off_dem": int((st == 2).sum()),
             "mean_steps_of_hits": float(steps_hit.mean()) if steps_hit.size else None,
+            "rays64_ms": statistics.median(ms64),
             "note": "1 m steps, <=10000 per ray, UTM->WGS84 + bilinear DEM per step (f64); inputs in HBM"}
 
 

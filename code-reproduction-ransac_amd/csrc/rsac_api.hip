@@ -706,7 +706,10 @@ int rsac_create(int device, rsac_ctx **out) {
     HIPCHK(hipSetDevice(device));
     rsac_ctx *c = new rsac_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    // blocking stream: ordered with the legacy null stream, which is torch's default stream
+    // (handle 0, indistinguishable from stream = NULL at the C-ABI), so device inputs written by
+    // torch before a call, and device outputs read by torch after it, need no extra sync
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev2) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_pts, hipEventDisableTiming) != hipSuccess ||

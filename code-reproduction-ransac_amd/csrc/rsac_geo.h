@@ -129,6 +129,76 @@ RSAC_HD void utm_forward(const TmConst &k, const UtmZone &z, double lon, double 
     E = kUtmFE + kUtmK0 * k.A * (etap + si);
 }
 
+// sinh and cosh from one expm1 (accurate near 0 as well)
+RSAC_HD void dsinhcosh(double x, double &sh, double &ch) {
+    const double em1 = expm1(x), e = 1.0 + em1;
+    sh = 0.5 * (em1 + em1 / e);
+    ch = 0.5 * (e + 1.0 / e);
+}
+
+// utm_inverse with the transcendental calls shared: one sincos + one expm1 per
+// Clenshaw argument, sin/cos(2 chi) from sin chi.  Same series; differs from
+// utm_inverse only by rounding (~1e-15 deg).  Used by the ray march.
+RSAC_HD void utm_inverse_fast(const TmConst &k, const UtmZone &z, double E, double N, double &lon, double &lat) {
+    const double kDeg = 57.29577951308232;
+    const double xi = (N - z.fn) / (kUtmK0 * k.A);
+    const double eta = (E - kUtmFE) / (kUtmK0 * k.A);
+    double s2, c2, sh2, ch2;
+    sincos(2.0 * xi, &s2, &c2);
+    dsinhcosh(2.0 * eta, sh2, ch2);
+    const double ar = 2.0 * c2 * ch2, ai = -2.0 * s2 * sh2;
+    double y1r = 0.0, y1i = 0.0, y2r = 0.0, y2i = 0.0;
+    for (int j = 5; j >= 0; --j) {
+        const double yr = ar * y1r - ai * y1i - y2r + k.beta[j];
+        const double yi = ar * y1i + ai * y1r - y2i;
+        y2r = y1r; y2i = y1i;
+        y1r = yr; y1i = yi;
+    }
+    const double br = s2 * ch2, bi = c2 * sh2;
+    const double xip = xi - (y1r * br - y1i * bi), etap = eta - (y1r * bi + y1i * br);
+    double sx, cx, she, che;
+    sincos(xip, &sx, &cx);
+    dsinhcosh(etap, she, che);
+    const double sc = sx / che;                  // sin chi
+    const double cc = dsqrt((1.0 - sc) * (1.0 + sc));  // cos chi >= 0
+    const double chi = atan2(sc, cc);
+    // delta series at chi: sum d_j sin(2 j chi), a = 2 cos(2 chi)
+    const double a = 2.0 * (cc - sc) * (cc + sc);
+    double y1 = 0.0, y2 = 0.0;
+    for (int j = 5; j >= 0; --j) {
+        const double y = a * y1 - y2 + k.delta[j];
+        y2 = y1;
+        y1 = y;
+    }
+    lat = (chi + y1 * (2.0 * sc * cc)) * kDeg;
+    lon = (z.lon0 + atan2(she, cx)) * kDeg;
+}
+
+// The reference advances the ray by repeated addition, x_{s+1} = fl(x_s + c),
+// c = fl(step * d) (main_v1.py:652-654).  Inside one binade, away from its
+// ends, every such sum rounds onto the same grid u = ulp(x), so
+// x_{s+j} = x_s + j * delta exactly, delta = fl(x_s + c) - x_s, unless the
+// rounding of c onto the grid is a tie (then the even-rule alternates).
+// stride_closed_form checks that for steps [0, W] from x and returns delta;
+// false means the caller must add step by step.
+RSAC_HD bool stride_closed_form(double x, double c, int W, double &delta) {
+    if (x == 0.0 || !dfinite(x) || !dfinite(c)) return false;
+    int ex;
+    frexp(x, &ex);  // |x| in [2^(ex-1), 2^ex)
+    const double lo = ldexp(1.0, ex - 1), hi = ldexp(1.0, ex), u = ldexp(1.0, ex - 53);
+    const double ac = dabs(c);
+    const double in_lo = lo + ac + 2.0 * u, in_hi = hi - ac - 2.0 * u;
+    const double ax = dabs(x);
+    if (!(ax >= in_lo && ax <= in_hi)) return false;
+    const double d = (x + c) - x;      // exact: both in the binade
+    if (dabs(c - d) == 0.5 * u) return false;  // tie: parity-dependent rounding
+    const double end = x + (double)W * d;      // exact while inside the binade
+    const double ae = dabs(end);
+    if ((end < 0.0) != (x < 0.0) || !(ae >= in_lo && ae <= in_hi)) return false;
+    delta = d;
+    return true;
+}
+
 // A regular (lat, lon) grid as load_dem_data builds it (main_v1.py:430-433):
 // lat_i = i * dy + y0, lon_j = j * dx + x0 (dy < 0 for north-up GDAL rasters).
 struct DemGrid {

@@ -1815,19 +1815,92 @@ __global__ void k_utm_forward(const double *__restrict__ lonlat, int64_t n, TmCo
         utm_forward(k, z, lonlat[2 * i], lonlat[2 * i + 1], en[2 * i], en[2 * i + 1]);
 }
 
-__global__ __launch_bounds__(64) void k_dem_march(const double *__restrict__ o, const double *__restrict__ d, int32_t n,
-                                                  DemGrid g, TmConst k, UtmZone z, int32_t n_steps, double step,
-                                                  int32_t min_steps, double *__restrict__ hits,
-                                                  int8_t *__restrict__ status) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// Position of step base + t of one coordinate: closed form when the stride is
+// exact (stride_closed_form), else the reference's additions one by one with
+// thread t keeping the value at its step.  Returns the position at base + W.
+template <int W>
+__device__ __forceinline__ double stride_positions(double x, double c, int t, double &xt) {
+    double delta;
+    if (stride_closed_form(x, c, W, delta)) {
+        xt = x + (double)t * delta;
+        return x + (double)W * delta;
+    }
+    xt = x;
+#pragma unroll 4
+    for (int j = 0; j < W; ++j) {
+        if (j == t) xt = x;
+        x = x + c;
+    }
+    return x;
+}
+
+// ray_intersect_dem (main_v1.py:635-656), WPR waves per ray.  The block's
+// W = 64 * WPR threads evaluate W consecutive steps of one ray at a time
+// (thread t: step base + t); the ray's positions follow the reference's
+// sequential additions exactly (stride_positions).  The first step, in order,
+// that leaves the DEM (status 2) or hits (status 0) ends the ray.
+template <int WPR>
+__global__ __launch_bounds__(256) void k_dem_march(const double *__restrict__ o, const double *__restrict__ d,
+                                                   int32_t n, DemGrid g, TmConst k, UtmZone z, int32_t n_steps,
+                                                   double step, int32_t min_steps, double *__restrict__ hits,
+                                                   int8_t *__restrict__ status) {
+    static_assert(WPR == 1 || WPR == 4, "barriers assume one ray per block when WPR > 1");
+    constexpr int W = 64 * WPR;
+    constexpr int kRaysPerBlock = 4 / WPR;
+    __shared__ int first[2][WPR];
+    const int t = threadIdx.x % W;
+    const int slot = threadIdx.x / W;
+    const int ray = blockIdx.x * kRaysPerBlock + slot;
+    const int lane = threadIdx.x & 63, wave = t >> 6;
+    const bool live = ray < n;  // uniform per ray group; dead groups still join the barriers
+    const int r = live ? ray : 0;
+    double p0 = o[3 * r], p1 = o[3 * r + 1], p2 = o[3 * r + 2];
+    const double c0 = step * d[3 * r], c1 = step * d[3 * r + 1], c2 = step * d[3 * r + 2];
+    int found = -1;  // the chunk thread whose step ended the ray (uniform per ray)
+    bool found_off = false;
+    double q0 = 0.0, q1 = 0.0, q2 = 0.0;
+    int parity = 0;
+    for (int base = 0; base < n_steps; base += W) {
+        p0 = stride_positions<W>(p0, c0, t, q0);
+        p1 = stride_positions<W>(p1, c1, t, q1);
+        p2 = stride_positions<W>(p2, c2, t, q2);
+        const int s = base + t;
+        bool ev = false;
+        if (live && s < n_steps) {
+            double lon, lat, elev;
+            utm_inverse_fast(k, z, q0, q1, lon, lat);
+            found_off = !dem_interp(g, lat, lon, elev);
+            ev = found_off || (s >= min_steps && q2 <= elev);
+        }
+        const unsigned long long m = __ballot(ev);
+        int f = m ? (wave * 64 + __builtin_ctzll(m)) : W;
+        if constexpr (WPR > 1) {
+            if (lane == 0) first[parity][wave] = f;
+            __syncthreads();
+            f = W;
+            for (int w = 0; w < WPR; ++w) f = min(f, first[parity][w]);
+            parity ^= 1;
+        }
+        if (f < W) {
+            found = f;
+            break;
+        }
+    }
+    if (!live) return;
     const double nan = __builtin_nan("");
-    double pos[3] = {nan, nan, nan};  // no hit: NaN (the reference's None)
-    const int st = dem_march(k, z, g, o + 3 * i, d + 3 * i, n_steps, step, min_steps, pos);
-    hits[3 * i] = pos[0];
-    hits[3 * i + 1] = pos[1];
-    hits[3 * i + 2] = pos[2];
-    status[i] = (int8_t)st;
+    if (found < 0) {
+        if (t == 0) {
+            hits[3 * ray] = nan;
+            hits[3 * ray + 1] = nan;
+            hits[3 * ray + 2] = nan;
+            status[ray] = 1;
+        }
+    } else if (t == found) {
+        hits[3 * ray] = found_off ? nan : q0;
+        hits[3 * ray + 1] = found_off ? nan : q1;
+        hits[3 * ray + 2] = found_off ? nan : q2;
+        status[ray] = found_off ? 2 : 0;
+    }
 }
 
 hipError_t launch_utm(bool inverse, const double *in, int64_t n, int zone, bool south, double *out, hipStream_t s) {
@@ -1846,9 +1919,16 @@ hipError_t launch_dem_march(const double *o, const double *d, int32_t n, const d
                             double y0, double dy, double x0, double dx, int zone, bool south, int32_t n_steps,
                             double step, int32_t min_steps, double *hits, int8_t *status, hipStream_t s) {
     const DemGrid g{dem, ny, nx, y0, dy, x0, dx};
-    // small blocks: rays march for different numbers of steps, so waves retire independently
-    hipLaunchKernelGGL(k_dem_march, dim3(cdiv(n > 0 ? n : 1, 64)), dim3(64), 0, s, o, d, n, g, tm_const(),
-                       utm_zone(zone, south), n_steps, step, min_steps, hits, status);
+    const TmConst k = tm_const();
+    const UtmZone z = utm_zone(zone, south);
+    // few rays: a whole block (4 waves, 256 steps per pass) per ray for latency; many rays: a
+    // wave per ray (64 steps per pass, less overshoot past the hit), 4 rays per block
+    if (n < 4 * 256)
+        hipLaunchKernelGGL(k_dem_march<4>, dim3(n > 0 ? n : 1), dim3(256), 0, s, o, d, n, g, k, z, n_steps, step,
+                           min_steps, hits, status);
+    else
+        hipLaunchKernelGGL(k_dem_march<1>, dim3(cdiv(n, 4)), dim3(256), 0, s, o, d, n, g, k, z, n_steps, step,
+                           min_steps, hits, status);
     return hipGetLastError();
 }
 

@@ -28,7 +28,8 @@
  *     structure-of-arrays: pts3d = X[N] Y[N] Z[N], pts2d = U[N] V[N].
  *   - inlier masks are RANSAC-phase masks (uint8, one per point), as OpenCV
  *     returns them; host memory unless RSAC_F_DEVICE_OUT.
- *   - work is enqueued on `stream` (hipStream_t, NULL = the context stream);
+ *   - work is enqueued on `stream` (hipStream_t; NULL = the context stream, a blocking stream
+ *     ordered with the device null stream, i.e. with torch's default stream);
  *     calls on one context are serialised; contexts are independent.
  */
 #ifndef RSAC_H
