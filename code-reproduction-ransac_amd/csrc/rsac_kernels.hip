@@ -1921,14 +1921,11 @@ hipError_t launch_dem_march(const double *o, const double *d, int32_t n, const d
     const DemGrid g{dem, ny, nx, y0, dy, x0, dx};
     const TmConst k = tm_const();
     const UtmZone z = utm_zone(zone, south);
-    // few rays: a whole block (4 waves, 256 steps per pass) per ray for latency; many rays: a
-    // wave per ray (64 steps per pass, less overshoot past the hit), 4 rays per block
-    if (n < 4 * 256)
-        hipLaunchKernelGGL(k_dem_march<4>, dim3(n > 0 ? n : 1), dim3(256), 0, s, o, d, n, g, k, z, n_steps, step,
-                           min_steps, hits, status);
-    else
-        hipLaunchKernelGGL(k_dem_march<1>, dim3(cdiv(n, 4)), dim3(256), 0, s, o, d, n, g, k, z, n_steps, step,
-                           min_steps, hits, status);
+    // a block (4 waves, 256 steps per pass) per ray: measured faster than a wave per ray at every
+    // batch size (64 / 1024 / 4096 rays: 0.20 / 0.38 / 0.85 ms vs 0.46 / 0.53 / 1.09 ms) -- the
+    // rays' lengths differ by 10x, and per-ray blocks keep every SIMD busy to the end
+    hipLaunchKernelGGL(k_dem_march<4>, dim3(n > 0 ? n : 1), dim3(256), 0, s, o, d, n, g, k, z, n_steps, step,
+                       min_steps, hits, status);
     return hipGetLastError();
 }
 

@@ -372,8 +372,8 @@ def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_th
     if device_result:
         import torch
         dev = p3.keep.device
-        key_t = torch.zeros(1, dtype=torch.int64, device=dev)
-        model_t = torch.zeros(12, dtype=torch.float64, device=dev)
+        key_t = torch.empty(1, dtype=torch.int64, device=dev)  # written by the call (no fill launch)
+        model_t = torch.empty(12, dtype=torch.float64, device=dev)
         with ctx.lock:
             L.check(L.lib().rsac_pnp_evaluate_range(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n,
                                                     K9.ctypes.data, int(hyp_begin), int(n_hyps),

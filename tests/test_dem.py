@@ -142,7 +142,7 @@ def test_gpu_utm_matches_oracle():
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,n_rays,kw", [(1, 300, {}), (2, 257, dict(tilt_deg=3.0, height_above=120.0)),
                                             (3, 64, dict(half_extent_deg=0.03, azimuth_deg=200.0)),
-                                            (4, 2048, dict(tilt_deg=1.0))])  # >= 1024 rays: a wave per ray
+                                            (4, 2048, dict(tilt_deg=1.0))])
 def test_gpu_ray_march_matches_oracle(seed, n_rays, kw):
     from rsac import dem
     pr = _scene(n_rays, seed=seed, **kw)
