@@ -582,10 +582,12 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     if (r) return r;
     r = finish_masks(c, Model::PnP, st, &a, lo, stride, mask_out, flags, s);
     if (r) return r;
-    if (flags & RSAC_F_REFINE) {
-        // final refit on the device, one block per problem, on the RANSAC-phase inliers
+    if (flags & (RSAC_F_REFINE | RSAC_F_EPNP)) {
+        // final solve on the device, one block per problem, on the RANSAC-phase inliers:
+        // EPnP (solvePnPRansac with SOLVEPNP_P3P), then / or LM (solvePnPRefineLM)
         const uint8_t *dmask = (flags & RSAC_F_DEVICE_OUT) && mask_out ? mask_out : c->mask.as<uint8_t>();
-        HIPCHK(launch_pnp_refine(a, P, dmask, c->bestmodels.as<double>(), nullptr, s));
+        if (flags & RSAC_F_EPNP) HIPCHK(launch_pnp_epnp(a, P, dmask, c->bestmodels.as<double>(), s));
+        if (flags & RSAC_F_REFINE) HIPCHK(launch_pnp_refine(a, P, dmask, c->bestmodels.as<double>(), nullptr, s));
         HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
                               hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -1181,7 +1183,7 @@ int rsac_fundamental_ransac(rsac_ctx *c, const void *pts1, const void *pts2, int
     int r = check_device(c);
     if (r) return r;
     if (n < 8) return fail(RSAC_ETOOFEW, "the 8-point fundamental matrix needs >= 8 correspondences (got %d)", n);
-    if (flags & (RSAC_F_SAMPLER_OPENCV | RSAC_F_REFINE | RSAC_F_LO))
+    if (flags & (RSAC_F_SAMPLER_OPENCV | RSAC_F_REFINE | RSAC_F_LO | RSAC_F_EPNP))
         return fail(RSAC_EINVAL, "fundamental matrix: Philox sampler only, no refit / LO");
     hipStream_t s = pick_stream(c, stream);
     Staged st;
@@ -1279,6 +1281,22 @@ int rsac_pnp_refine(const double *pts3d, const double *pts2d, int32_t n, const d
     const double cam[4] = {K[0], K[4], K[2], K[5]};
     const float *b = soa.data();
     return pnp_refine_lm(b, b + n, b + 2 * n, b + 3 * n, b + 4 * n, m.data(), n, cam, R, t, max_iter);
+}
+
+int rsac_pnp_epnp(const double *pts3d, const double *pts2d, int32_t n, const double K[9], const uint8_t *mask,
+                  double R[9], double t[3]) {
+    if (n < 4 || !pts3d || !pts2d || !K || !R || !t) return fail(RSAC_EINVAL, "bad arguments");
+    std::vector<float> soa((size_t)5 * n);
+    for (int32_t i = 0; i < n; ++i) {
+        for (int k = 0; k < 3; ++k) soa[(size_t)k * n + i] = (float)pts3d[3 * i + k];
+        soa[(size_t)3 * n + i] = (float)pts2d[2 * i];
+        soa[(size_t)4 * n + i] = (float)pts2d[2 * i + 1];
+    }
+    std::vector<uint8_t> m(n, 1);
+    if (mask) memcpy(m.data(), mask, n);
+    const double cam[4] = {K[0], K[4], K[2], K[5]};
+    const float *b = soa.data();
+    return pnp_epnp_host(b, b + n, b + 2 * n, b + 3 * n, b + 4 * n, m.data(), n, cam, R, t) ? RSAC_OK : RSAC_NO_MODEL;
 }
 
 int rsac_homography_fit(const double *src, const double *dst, int32_t n, const uint8_t *mask, double H_out[9]) {

@@ -53,6 +53,11 @@ void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_
 void rodrigues_v2m(const double r[3], double R[9]);
 void rodrigues_m2v(const double R[9], double r[3]);
 
+// EPnP on the masked points (the final solve of solvePnPRansac with SOLVEPNP_P3P),
+// bit-identical to k_pnp_epnp; false for < 4 inliers or a degenerate cloud.
+bool pnp_epnp_host(const float *X, const float *Y, const float *Z, const float *U, const float *V, const uint8_t *mask,
+                   int n, const double cam[4], double R[9], double t[3]);
+
 // LM over (R, t) on masked correspondences (f32 SoA); returns iterations
 int pnp_refine_lm(const float *X, const float *Y, const float *Z, const float *U, const float *V, const uint8_t *mask,
                   int n, const double cam[4], double R[9], double t[3], int max_iter);

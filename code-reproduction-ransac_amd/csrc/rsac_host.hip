@@ -5,6 +5,8 @@
 #include <string.h>
 
 #include <cfloat>
+#include <memory>
+#include <vector>
 
 #include "rsac_math.h"
 
@@ -145,7 +147,48 @@ struct HostLmReducer {
     }
 };
 
+struct HostEpnpReducer {
+    const float *X, *Y, *Z, *U, *V;
+    const uint8_t *mask;
+    int n;
+    double c[3];
+    std::vector<double> part = std::vector<double>((size_t)kLmThreads * kRedMax);
+    EpnpShared sh;
+    template <int NV, class F>
+    void sum(F f, double *out) {
+        lm_reduce_host(n, mask, NV, part.data(), out, [&](int i, double *a) {
+            f((double)X[i] - c[0], (double)Y[i] - c[1], (double)Z[i] - c[2], (double)U[i], (double)V[i], a);
+        });
+    }
+    bool first(double *p) {
+        for (int i = 0; i < n; ++i)
+            if (mask[i]) {
+                p[0] = (double)X[i] - c[0];
+                p[1] = (double)Y[i] - c[1];
+                p[2] = (double)Z[i] - c[2];
+                return true;
+            }
+        return false;
+    }
+    EpnpShared *shared() { return &sh; }
+    bool leader() const { return true; }
+    void sync() {}
+};
+
 }  // namespace
+
+bool pnp_epnp_host(const float *X, const float *Y, const float *Z, const float *U, const float *V, const uint8_t *mask,
+                   int n, const double cam[4], double R[9], double t[3]) {
+    if (n <= 0) return false;
+    auto red = std::make_unique<HostEpnpReducer>();
+    *red = HostEpnpReducer{X, Y, Z, U, V, mask, n, {(double)X[0], (double)Y[0], (double)Z[0]}};
+    double Rn[9], tn[3];
+    if (!pnp_epnp(*red, Cam{cam[0], cam[1], cam[2], cam[3]}, Rn, tn)) return false;
+    lm_from_centred(Rn, red->c, tn);
+    for (int j = 0; j < 9; ++j) R[j] = Rn[j];
+    for (int j = 0; j < 3; ++j) t[j] = tn[j];
+    return true;
+}
 
 int pnp_refine_lm(const float *X, const float *Y, const float *Z, const float *U, const float *V, const uint8_t *mask,
                   int n, const double cam[4], double R[9], double t[3], int max_iter) {

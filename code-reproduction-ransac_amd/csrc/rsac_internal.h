@@ -114,6 +114,7 @@ hipError_t launch_fm_mask(const HomArgs &a, int32_t P, int32_t max_n, const int6
 
 // LM refit of every problem's model record (models: P x kModelStride, R 9, t 3, valid)
 // on the inliers of mask (concatenated points), one block per problem
+hipError_t launch_pnp_epnp(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, hipStream_t s);
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
                              hipStream_t s);
 

@@ -1565,6 +1565,90 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     }
 }
 
+// EPnP of every problem's winner on its RANSAC inliers (rsac_math.h pnp_epnp),
+// one block per problem; the same summation order as the host (pnp_epnp_host).
+struct GpuEpnpReducer {
+    const float *X, *Y, *Z, *U, *V;
+    const uint8_t *mask;
+    int n;
+    double c0, c1, c2;
+    double (*wsum)[kRedMax];  // LDS [kLmThreads / 64][kRedMax]
+    EpnpShared *sh;           // LDS
+    int *wmin;                // LDS [kLmThreads / 64]
+
+    template <int NV, class F>
+    __device__ void sum(F f, double *out) {
+        double a[NV];
+        for (int q = 0; q < NV; ++q) a[q] = 0.0;
+        for (int i = threadIdx.x; i < n; i += kLmThreads)
+            if (mask[i])
+                f((double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i], (double)V[i], a);
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        for (int q = 0; q < NV; ++q) {
+            double v = a[q];
+            for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o);
+            if (lane == 0) wsum[wave][q] = v;
+        }
+        __syncthreads();
+        for (int q = 0; q < NV; ++q) {
+            double v = wsum[0][q];
+            for (int w = 1; w < kLmThreads / 64; ++w) v = v + wsum[w][q];
+            out[q] = v;
+        }
+        __syncthreads();
+    }
+    __device__ bool first(double *p) {
+        int m = 0x7fffffff;
+        for (int i = threadIdx.x; i < n; i += kLmThreads)
+            if (mask[i]) {
+                m = i;
+                break;
+            }
+        for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
+        if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = m;
+        __syncthreads();
+        m = wmin[0];
+        for (int w = 1; w < kLmThreads / 64; ++w) m = min(m, wmin[w]);
+        __syncthreads();
+        if (m == 0x7fffffff) return false;
+        p[0] = (double)X[m] - c0;
+        p[1] = (double)Y[m] - c1;
+        p[2] = (double)Z[m] - c2;
+        return true;
+    }
+    __device__ EpnpShared *shared() { return sh; }
+    __device__ bool leader() const { return threadIdx.x == 0; }
+    __device__ void sync() { __syncthreads(); }
+};
+
+__global__ __launch_bounds__(kLmThreads) void k_pnp_epnp(PnpArgs a, const uint8_t *__restrict__ mask,
+                                                         double *__restrict__ models) {
+    __shared__ double wsum[kLmThreads / 64][kRedMax];
+    __shared__ EpnpShared sh;
+    __shared__ int wmin[kLmThreads / 64];
+    const int prob = blockIdx.x;
+    double *m = models + (int64_t)prob * kModelStride;
+    if (m[kValidSlot] == 0.0) return;  // no model: block-uniform exit
+    const int64_t p0 = a.offsets[prob];
+    const double *cm = a.cams + 4 * prob;
+    const double c[3] = {(double)a.X[p0], (double)a.Y[p0], (double)a.Z[p0]};
+    GpuEpnpReducer red{a.X + p0, a.Y + p0, a.Z + p0, a.U + p0, a.V + p0, mask + p0,
+                       (int)(a.offsets[prob + 1] - p0), c[0], c[1], c[2], wsum, &sh, wmin};
+    double R[9], t[3];
+    const bool ok = pnp_epnp(red, Cam{cm[0], cm[1], cm[2], cm[3]}, R, t);
+    __syncthreads();  // every thread has read m before thread 0 overwrites it
+    if (ok && threadIdx.x == 0) {
+        lm_from_centred(R, c, t);
+        for (int j = 0; j < 9; ++j) m[j] = R[j];
+        for (int j = 0; j < 3; ++j) m[9 + j] = t[j];
+    }
+}
+
+hipError_t launch_pnp_epnp(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, hipStream_t s) {
+    hipLaunchKernelGGL(k_pnp_epnp, dim3(P), dim3(kLmThreads), 0, s, a, mask, models);
+    return hipGetLastError();
+}
+
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
                              hipStream_t s) {
     hipLaunchKernelGGL(k_pnp_refine, dim3(P), dim3(kLmThreads), 0, s, a, mask, models, iters);

@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #define RSAC_HD __host__ __device__ __forceinline__
+#define RSAC_NOINLINE __host__ __device__ __attribute__((noinline)) inline
 
 namespace rsac {
 
@@ -648,6 +649,7 @@ RSAC_HD bool fm_inlier(const double *F, double x1, double y1, double x2, double 
 constexpr int kLmThreads = 512;
 constexpr int kLmTerms = 27;  // J^T J lower triangle (21, row-major packed), J^T r (6)
 constexpr int kLmMaxIter = 20;
+constexpr int kRedMax = 40;   // widest reduction (EPnP's pair sums)
 
 // adds point (X, Y, Z) -> (u, v)'s terms of J^T J and J^T r to acc
 RSAC_HD void pnp_lm_point(const double *R, const double *t, const Cam &k, double Xd, double Yd, double Zd, double u,
@@ -791,7 +793,7 @@ inline void lm_reduce_host(int n, const uint8_t *mask, int nv, double *part, dou
     for (int tid = 0; tid < kLmThreads; ++tid)
         for (int i = tid; i < n; i += kLmThreads)
             if (mask[i]) f(i, part + tid * nv);
-    double wsum[kLmThreads / 64][kLmTerms];
+    double wsum[kLmThreads / 64][kRedMax];
     double v[64], w[64];
     for (int wv = 0; wv < kLmThreads / 64; ++wv)
         for (int q = 0; q < nv; ++q) {
@@ -807,6 +809,443 @@ inline void lm_reduce_host(int n, const uint8_t *mask, int nv, double *part, dou
         for (int wv = 1; wv < kLmThreads / 64; ++wv) s = s + wsum[wv][q];
         out[q] = s;
     }
+}
+
+// ---------------------------------------------------------------------------
+// EPnP (Lepetit, Moreno-Noguer, Fua, IJCV 2009) on the inliers: the
+// non-minimal final solve of cv2.solvePnPRansac when its minimal solver is
+// P3P (OpenCV re-solves the inliers with SOLVEPNP_EPNP, main_v1.py:497 with
+// flags=SOLVEPNP_P3P).  Steps as OpenCV's epnp.cpp:
+// control points from the centroid and principal axes, barycentric alphas,
+// M^T M (12 x 12), its 4 smallest eigenvectors, the L 6x10 / rho system,
+// beta approximations 1, 2, 3 each polished by 5 Gauss-Newton steps, the pose
+// of each by the SVD of the centred cross-covariance, the one with the lowest
+// mean reprojection error wins.  Own numerics (no OpenCV to pin against):
+// Jacobi eigen-decompositions, Householder least squares, and the frame
+// centred on the problem's first point, as the LM refit.  The O(n) sums go
+// through Red (the summation order of lm_reduce_host / GpuLmReducer).
+// ---------------------------------------------------------------------------
+constexpr int kEpnpPairSums = 40;  // 10 control-point pairs x 4 sums
+
+// Cyclic Jacobi of a symmetric N x N matrix (row-major, destroyed): d[k]
+// eigenvalues, V[i * N + k] the k-th eigenvector.  Fixed rotation order.
+template <int N>
+RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
+    for (int i = 0; i < N * N; ++i) V[i] = 0.0;
+    for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0, diag = 0.0;
+        for (int p = 0; p < N; ++p) {
+            diag = diag + A[p * N + p] * A[p * N + p];
+            for (int q = p + 1; q < N; ++q) off = off + A[p * N + q] * A[p * N + q];
+        }
+        if (!(off > 1e-32 * diag)) break;
+        for (int p = 0; p < N - 1; ++p)
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = A[p * N + q];
+                if (apq == 0.0) continue;
+                const double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
+                const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
+                const double c = 1.0 / dsqrt(tt * tt + 1.0), sn = tt * c;
+                for (int k = 0; k < N; ++k) {
+                    const double akp = A[k * N + p], akq = A[k * N + q];
+                    A[k * N + p] = c * akp - sn * akq;
+                    A[k * N + q] = sn * akp + c * akq;
+                }
+                for (int k = 0; k < N; ++k) {
+                    const double apk = A[p * N + k], aqk = A[q * N + k];
+                    A[p * N + k] = c * apk - sn * aqk;
+                    A[q * N + k] = sn * apk + c * aqk;
+                }
+                for (int k = 0; k < N; ++k) {
+                    const double vkp = V[k * N + p], vkq = V[k * N + q];
+                    V[k * N + p] = c * vkp - sn * vkq;
+                    V[k * N + q] = sn * vkp + c * vkq;
+                }
+            }
+    }
+    for (int k = 0; k < N; ++k) d[k] = A[k * N + k];
+}
+
+// order[] = eigenvalue indices by decreasing value (ties: lower index first)
+template <int N>
+RSAC_HD void eig_order_desc(const double *d, int *order) {
+    for (int i = 0; i < N; ++i) order[i] = i;
+    for (int i = 1; i < N; ++i) {
+        const int k = order[i];
+        int j = i - 1;
+        while (j >= 0 && d[order[j]] < d[k]) {
+            order[j + 1] = order[j];
+            --j;
+        }
+        order[j + 1] = k;
+    }
+}
+
+// Least squares min |A x - b|, A M x N row-major (M >= N), by Householder QR;
+// A and b are destroyed.  A vanishing pivot gives x_k = 0.
+template <int M, int N>
+RSAC_HD void householder_ls(double *A, double *b, double *x) {
+    for (int k = 0; k < N; ++k) {
+        double nrm = 0.0;
+        for (int i = k; i < M; ++i) nrm = nrm + A[i * N + k] * A[i * N + k];
+        nrm = dsqrt(nrm);
+        if (nrm == 0.0) continue;
+        const double alpha = A[k * N + k] > 0.0 ? -nrm : nrm;
+        double v[M];
+        for (int i = k; i < M; ++i) v[i] = A[i * N + k];
+        v[k] = v[k] - alpha;
+        double vv = 0.0;
+        for (int i = k; i < M; ++i) vv = vv + v[i] * v[i];
+        if (vv == 0.0) continue;
+        for (int j = k; j < N; ++j) {
+            double sdot = 0.0;
+            for (int i = k; i < M; ++i) sdot = sdot + v[i] * A[i * N + j];
+            const double f = 2.0 * sdot / vv;
+            for (int i = k; i < M; ++i) A[i * N + j] = A[i * N + j] - f * v[i];
+        }
+        double sdot = 0.0;
+        for (int i = k; i < M; ++i) sdot = sdot + v[i] * b[i];
+        const double f = 2.0 * sdot / vv;
+        for (int i = k; i < M; ++i) b[i] = b[i] - f * v[i];
+    }
+    for (int k = N - 1; k >= 0; --k) {
+        double sacc = b[k];
+        for (int j = k + 1; j < N; ++j) sacc = sacc - A[k * N + j] * x[j];
+        const double rkk = A[k * N + k];
+        x[k] = dabs(rkk) > 1e-300 ? sacc / rkk : 0.0;
+    }
+}
+
+struct EpnpFrame {
+    double cw[4][3];   // control points (centred frame)
+    double ci[9];      // inverse of [cw1 - cw0, cw2 - cw0, cw3 - cw0] (columns)
+};
+
+// what the barycentric coordinates need: cw0 and the inverse (kept small for the sums' registers)
+struct EpnpAlpha {
+    double c[3], ci[9];
+};
+
+RSAC_HD EpnpAlpha epnp_alpha_frame(const EpnpFrame &f) {
+    EpnpAlpha a;
+    for (int j = 0; j < 3; ++j) a.c[j] = f.cw[0][j];
+    for (int j = 0; j < 9; ++j) a.ci[j] = f.ci[j];
+    return a;
+}
+
+RSAC_HD void epnp_alphas(const EpnpAlpha &f, double X, double Y, double Z, double *a) {
+    const double dx = X - f.c[0], dy = Y - f.c[1], dz = Z - f.c[2];
+    for (int j = 0; j < 3; ++j) a[1 + j] = f.ci[3 * j] * dx + f.ci[3 * j + 1] * dy + f.ci[3 * j + 2] * dz;
+    a[0] = 1.0 - a[1] - a[2] - a[3];
+}
+
+// the 6 x 10 L matrix of the betas' quadratic forms (OpenCV compute_L_6x10)
+RSAC_HD void epnp_l6x10(const double *const v[4], double *L) {
+    int a = 0, b = 1;
+    for (int i = 0; i < 6; ++i) {
+        double dv[4][3];
+        for (int p = 0; p < 4; ++p)
+            for (int q = 0; q < 3; ++q) dv[p][q] = v[p][3 * a + q] - v[p][3 * b + q];
+        ++b;
+        if (b > 3) {
+            ++a;
+            b = a + 1;
+        }
+        double *r = L + 10 * i;
+        auto dot = [&](int p, int q) { return dv[p][0] * dv[q][0] + dv[p][1] * dv[q][1] + dv[p][2] * dv[q][2]; };
+        r[0] = dot(0, 0);
+        r[1] = 2.0 * dot(0, 1);
+        r[2] = dot(1, 1);
+        r[3] = 2.0 * dot(0, 2);
+        r[4] = 2.0 * dot(1, 2);
+        r[5] = dot(2, 2);
+        r[6] = 2.0 * dot(0, 3);
+        r[7] = 2.0 * dot(1, 3);
+        r[8] = 2.0 * dot(2, 3);
+        r[9] = dot(3, 3);
+    }
+}
+
+// 5 Gauss-Newton steps on the betas (OpenCV gauss_newton)
+RSAC_HD void epnp_gauss_newton(const double *L, const double *rho, double *be) {
+    for (int it = 0; it < 5; ++it) {
+        double A[24], b[6], x[4];
+        for (int i = 0; i < 6; ++i) {
+            const double *r = L + 10 * i;
+            A[4 * i + 0] = 2.0 * r[0] * be[0] + r[1] * be[1] + r[3] * be[2] + r[6] * be[3];
+            A[4 * i + 1] = r[1] * be[0] + 2.0 * r[2] * be[1] + r[4] * be[2] + r[7] * be[3];
+            A[4 * i + 2] = r[3] * be[0] + r[4] * be[1] + 2.0 * r[5] * be[2] + r[8] * be[3];
+            A[4 * i + 3] = r[6] * be[0] + r[7] * be[1] + r[8] * be[2] + 2.0 * r[9] * be[3];
+            b[i] = rho[i] - (r[0] * be[0] * be[0] + r[1] * be[0] * be[1] + r[2] * be[1] * be[1] +
+                             r[3] * be[0] * be[2] + r[4] * be[1] * be[2] + r[5] * be[2] * be[2] +
+                             r[6] * be[0] * be[3] + r[7] * be[1] * be[3] + r[8] * be[2] * be[3] +
+                             r[9] * be[3] * be[3]);
+        }
+        householder_ls<6, 4>(A, b, x);
+        for (int j = 0; j < 4; ++j) be[j] = be[j] + x[j];
+    }
+}
+
+// R = U V^T of the 3 x 3 cross-covariance H = sum (pc - pc0)(pw - pw0)^T, with
+// OpenCV's determinant fix (negate the last row); false if H has rank < 2
+RSAC_HD bool epnp_rotation(const double *H, double *R) {
+    double B[9], V[9], d[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) B[3 * i + j] = H[i] * H[j] + H[3 + i] * H[3 + j] + H[6 + i] * H[6 + j];
+    jacobi_eig<3>(B, V, d);
+    int o[3];
+    eig_order_desc<3>(d, o);
+    double v[3][3], u[3][3];
+    for (int k = 0; k < 3; ++k)
+        for (int i = 0; i < 3; ++i) v[k][i] = V[3 * i + o[k]];
+    const double s0 = dsqrt(d[o[0]] > 0.0 ? d[o[0]] : 0.0);
+    if (!(s0 > 0.0)) return false;
+    for (int k = 0; k < 3; ++k) {
+        const double sk = dsqrt(d[o[k]] > 0.0 ? d[o[k]] : 0.0);
+        if (k < 2 || sk > 1e-10 * s0) {
+            if (!(sk > 1e-10 * s0)) return false;
+            for (int i = 0; i < 3; ++i) u[k][i] = (H[3 * i] * v[k][0] + H[3 * i + 1] * v[k][1] + H[3 * i + 2] * v[k][2]) / sk;
+        } else {  // rank 2: complete U by the cross product
+            u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
+            u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
+            u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
+        }
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = u[0][i] * v[0][j] + u[1][i] * v[1][j] + u[2][i] * v[2][j];
+    const double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                       R[2] * (R[3] * R[7] - R[4] * R[6]);
+    if (det < 0.0)
+        for (int j = 0; j < 3; ++j) R[6 + j] = -R[6 + j];
+    return true;
+}
+
+// The serial middle of EPnP (M^T M's eigenvectors, L, rho, the three beta
+// estimates) runs on one thread (Red::leader) in this scratch -- LDS on the GPU.
+struct EpnpShared {
+    double A[144], V[144], d[12];
+    double ut[4][12];  // eigenvectors of the 4 smallest eigenvalues, smallest first
+    double L[60], rho[6];
+    double be[3][4];
+    int valid[3];
+};
+
+// The serial middle of EPnP (leader thread): M^T M from the pair sums, its
+// eigenvectors, L and rho, the three beta estimates with Gauss-Newton.  Not
+// inlined on the GPU so its registers do not add to the O(n) sums'.
+RSAC_NOINLINE void epnp_serial(EpnpShared *sh, const double *pairs, const Cam &k, const EpnpFrame &f) {
+    int q = 0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = i; j < 4; ++j, q += 4) {
+            const double s0 = pairs[q], su = pairs[q + 1], sv = pairs[q + 2], sw = pairs[q + 3];
+            const double blk[9] = {k.fx * k.fx * s0, 0.0, k.fx * su, 0.0, k.fy * k.fy * s0, k.fy * sv,
+                                   k.fx * su, k.fy * sv, sw};
+            for (int p = 0; p < 3; ++p)
+                for (int r = 0; r < 3; ++r) {
+                    sh->A[12 * (3 * i + p) + 3 * j + r] = blk[3 * p + r];
+                    sh->A[12 * (3 * j + r) + 3 * i + p] = blk[3 * p + r];
+                }
+        }
+    jacobi_eig<12>(sh->A, sh->V, sh->d);
+    int o[12];
+    eig_order_desc<12>(sh->d, o);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 12; ++j) sh->ut[i][j] = sh->V[12 * j + o[11 - i]];
+    const double *vv[4] = {sh->ut[0], sh->ut[1], sh->ut[2], sh->ut[3]};
+    epnp_l6x10(vv, sh->L);
+    q = 0;
+    for (int a = 0; a < 4; ++a)
+        for (int b = a + 1; b < 4; ++b, ++q) {
+            const double dx = f.cw[a][0] - f.cw[b][0], dy = f.cw[a][1] - f.cw[b][1], dz = f.cw[a][2] - f.cw[b][2];
+            sh->rho[q] = dx * dx + dy * dy + dz * dz;
+        }
+    for (int approx = 1; approx <= 3; ++approx) {
+        double *be = sh->be[approx - 1];
+        for (int j = 0; j < 4; ++j) be[j] = 0.0;
+        double b[6];
+        for (int i = 0; i < 6; ++i) b[i] = sh->rho[i];
+        bool ok = true;
+        if (approx == 1) {  // columns 0 1 3 6: beta1^2, b1 b2, b1 b3, b1 b4
+            const int cols[4] = {0, 1, 3, 6};
+            double A[24], x[4];
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 4; ++j) A[4 * i + j] = sh->L[10 * i + cols[j]];
+            householder_ls<6, 4>(A, b, x);
+            const double sg = x[0] < 0.0 ? -1.0 : 1.0;
+            be[0] = dsqrt(sg * x[0]);
+            ok = be[0] != 0.0;
+            if (ok)
+                for (int j = 1; j < 4; ++j) be[j] = sg * x[j] / be[0];
+        } else if (approx == 2) {  // columns 0 1 2: beta1^2, b1 b2, b2^2
+            double A[18], x[3];
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 3; ++j) A[3 * i + j] = sh->L[10 * i + j];
+            householder_ls<6, 3>(A, b, x);
+            if (x[0] < 0.0) {
+                be[0] = dsqrt(-x[0]);
+                be[1] = x[2] < 0.0 ? dsqrt(-x[2]) : 0.0;
+            } else {
+                be[0] = dsqrt(x[0]);
+                be[1] = x[2] > 0.0 ? dsqrt(x[2]) : 0.0;
+            }
+            if (x[1] < 0.0) be[0] = -be[0];
+        } else {  // columns 0..4: beta1^2, b1 b2, b2^2, b1 b3, b2 b3
+            double A[30], x[5];
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 5; ++j) A[5 * i + j] = sh->L[10 * i + j];
+            householder_ls<6, 5>(A, b, x);
+            if (x[0] < 0.0) {
+                be[0] = dsqrt(-x[0]);
+                be[1] = x[2] < 0.0 ? dsqrt(-x[2]) : 0.0;
+            } else {
+                be[0] = dsqrt(x[0]);
+                be[1] = x[2] > 0.0 ? dsqrt(x[2]) : 0.0;
+            }
+            if (x[1] < 0.0) be[0] = -be[0];
+            ok = be[0] != 0.0;
+            if (ok) be[2] = x[3] / be[0];
+        }
+        if (ok) epnp_gauss_newton(sh->L, sh->rho, be);
+        sh->valid[approx - 1] = ok;
+    }
+    }
+
+// Red provides:
+//   template <int NV, class F> void sum(F f, double *out): out[q] = sum over the inliers of
+//     f(X, Y, Z, u, v, acc) (acc[NV]; coordinates in the centred frame), in the fixed order;
+//   bool first(double *p): the first inlier's centred coordinates;
+//   EpnpShared *shared(), bool leader(), void sync(): the serial part's scratch and barrier.
+// Every thread runs this function; values are block-uniform.  Returns false (pose
+// untouched) for < 4 inliers or a degenerate (e.g. planar) configuration.
+template <class Red>
+RSAC_HD bool pnp_epnp(Red &red, const Cam &k, double *R_out, double *t_out) {
+    double s4[4];
+    red.template sum<4>([](double X, double Y, double Z, double, double, double *acc) {
+        acc[0] += X; acc[1] += Y; acc[2] += Z; acc[3] += 1.0;
+    }, s4);
+    const double n = s4[3];
+    if (!(n >= 4.0)) return false;
+    EpnpFrame f;
+    for (int j = 0; j < 3; ++j) f.cw[0][j] = s4[j] / n;
+    const double c0x = f.cw[0][0], c0y = f.cw[0][1], c0z = f.cw[0][2];
+    double cov[6];
+    red.template sum<6>([=](double X, double Y, double Z, double, double, double *acc) {
+        const double x = X - c0x, y = Y - c0y, z = Z - c0z;
+        acc[0] += x * x; acc[1] += x * y; acc[2] += x * z; acc[3] += y * y; acc[4] += y * z; acc[5] += z * z;
+    }, cov);
+    {
+        double A[9] = {cov[0], cov[1], cov[2], cov[1], cov[3], cov[4], cov[2], cov[4], cov[5]}, V[9], d[3];
+        jacobi_eig<3>(A, V, d);
+        int o[3];
+        eig_order_desc<3>(d, o);
+        for (int i = 1; i < 4; ++i) {
+            const double ev = d[o[i - 1]];
+            const double kk = dsqrt((ev > 0.0 ? ev : 0.0) / n);
+            for (int j = 0; j < 3; ++j) f.cw[i][j] = f.cw[0][j] + kk * V[3 * j + o[i - 1]];
+        }
+    }
+    {
+        double cc[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 1; j < 4; ++j) cc[3 * i + j - 1] = f.cw[j][i] - f.cw[0][i];
+        const double m00 = cc[4] * cc[8] - cc[5] * cc[7], m01 = cc[5] * cc[6] - cc[3] * cc[8],
+                     m02 = cc[3] * cc[7] - cc[4] * cc[6];
+        const double det = cc[0] * m00 + cc[1] * m01 + cc[2] * m02;
+        double nrm = 0.0;
+        for (int q = 0; q < 9; ++q) nrm = nrm + cc[q] * cc[q];
+        if (!(dabs(det) > 1e-12 * nrm * dsqrt(nrm))) return false;  // planar / degenerate cloud
+        const double id = 1.0 / det;
+        f.ci[0] = m00 * id;
+        f.ci[1] = (cc[2] * cc[7] - cc[1] * cc[8]) * id;
+        f.ci[2] = (cc[1] * cc[5] - cc[2] * cc[4]) * id;
+        f.ci[3] = m01 * id;
+        f.ci[4] = (cc[0] * cc[8] - cc[2] * cc[6]) * id;
+        f.ci[5] = (cc[2] * cc[3] - cc[0] * cc[5]) * id;
+        f.ci[6] = m02 * id;
+        f.ci[7] = (cc[1] * cc[6] - cc[0] * cc[7]) * id;
+        f.ci[8] = (cc[0] * cc[4] - cc[1] * cc[3]) * id;
+    }
+    // M^T M (12 x 12) = sum over points of kron(a a^T, G), G = m1 m1^T + m2 m2^T for the two rows
+    // m1 = (fx, 0, cx - u), m2 = (0, fy, cy - v) of fill_M: per control-point pair (i <= j)
+    // the sums of a_i a_j times 1, (cx - u), (cy - v), (cx - u)^2 + (cy - v)^2
+    const EpnpAlpha af = epnp_alpha_frame(f);
+    double pairs[kEpnpPairSums];
+    red.template sum<kEpnpPairSums>([=](double X, double Y, double Z, double u, double v, double *acc) {
+        double a[4];
+        epnp_alphas(af, X, Y, Z, a);
+        const double du = k.cx - u, dv = k.cy - v, w = du * du + dv * dv;
+        int q = 0;
+        for (int i = 0; i < 4; ++i)
+            for (int j = i; j < 4; ++j, q += 4) {
+                const double aa = a[i] * a[j];
+                acc[q] += aa;
+                acc[q + 1] += aa * du;
+                acc[q + 2] += aa * dv;
+                acc[q + 3] += aa * w;
+            }
+    }, pairs);
+    EpnpShared *sh = red.shared();
+    if (red.leader()) epnp_serial(sh, pairs, k, f);
+    red.sync();
+    double p1[3], a1[4];
+    if (!red.first(p1)) return false;
+    epnp_alphas(af, p1[0], p1[1], p1[2], a1);
+    double best_err = 0.0, bestR[9], bestt[3];
+    bool have = false;
+    for (int approx = 0; approx < 3; ++approx) {
+        if (!sh->valid[approx]) continue;
+        const double *be = sh->be[approx];
+        // control points in the camera frame, the sign from the first inlier's depth
+        double cc[4][3];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 3; ++j)
+                cc[i][j] = be[0] * sh->ut[0][3 * i + j] + be[1] * sh->ut[1][3 * i + j] +
+                           be[2] * sh->ut[2][3 * i + j] + be[3] * sh->ut[3][3 * i + j];
+        const double z1 = a1[0] * cc[0][2] + a1[1] * cc[1][2] + a1[2] * cc[2][2] + a1[3] * cc[3][2];
+        if (z1 < 0.0)
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 3; ++j) cc[i][j] = -cc[i][j];
+        double pc0[3];
+        red.template sum<3>([=](double X, double Y, double Z, double, double, double *acc) {
+            double a[4];
+            epnp_alphas(af, X, Y, Z, a);
+            for (int j = 0; j < 3; ++j) acc[j] += a[0] * cc[0][j] + a[1] * cc[1][j] + a[2] * cc[2][j] + a[3] * cc[3][j];
+        }, pc0);
+        for (int j = 0; j < 3; ++j) pc0[j] = pc0[j] / n;
+        double H[9];
+        red.template sum<9>([=](double X, double Y, double Z, double, double, double *acc) {
+            double a[4], pc[3];
+            epnp_alphas(af, X, Y, Z, a);
+            for (int j = 0; j < 3; ++j)
+                pc[j] = a[0] * cc[0][j] + a[1] * cc[1][j] + a[2] * cc[2][j] + a[3] * cc[3][j] - pc0[j];
+            const double pw[3] = {X - c0x, Y - c0y, Z - c0z};
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) acc[3 * i + j] += pc[i] * pw[j];
+        }, H);
+        double Rk[9], tk[3];
+        if (!epnp_rotation(H, Rk)) continue;
+        for (int i = 0; i < 3; ++i) tk[i] = pc0[i] - (Rk[3 * i] * c0x + Rk[3 * i + 1] * c0y + Rk[3 * i + 2] * c0z);
+        double es;
+        red.template sum<1>([=](double X, double Y, double Z, double u, double v, double *acc) {
+            const double x = Rk[0] * X + Rk[1] * Y + Rk[2] * Z + tk[0];
+            const double y = Rk[3] * X + Rk[4] * Y + Rk[5] * Z + tk[1];
+            const double iz = 1.0 / (Rk[6] * X + Rk[7] * Y + Rk[8] * Z + tk[2]);
+            const double du = u - (k.cx + k.fx * x * iz), dv = v - (k.cy + k.fy * y * iz);
+            acc[0] += dsqrt(du * du + dv * dv);
+        }, &es);
+        const double err = es / n;
+        if (!have || err < best_err) {
+            have = true;
+            best_err = err;
+            for (int j = 0; j < 9; ++j) bestR[j] = Rk[j];
+            for (int j = 0; j < 3; ++j) bestt[j] = tk[j];
+        }
+    }
+    if (!have) return false;
+    for (int j = 0; j < 9; ++j) R_out[j] = bestR[j];
+    for (int j = 0; j < 3; ++j) t_out[j] = bestt[j];
+    return true;
 }
 
 }  // namespace rsac

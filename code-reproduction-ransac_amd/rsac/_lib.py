@@ -31,6 +31,7 @@ F_DEVICE_OUT = 1 << 5
 F_EXACT_ONLY = 1 << 6
 F_LO = 1 << 7
 F_ASYNC = 1 << 8
+F_EPNP = 1 << 9
 
 ABI_VERSION = 1
 
@@ -76,6 +77,7 @@ SIGNATURES = [
     ("rsac_homography_hypotheses", C.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _d, _u64, _u32, _vp, _vp, _vp, _vp,
                                              _vp]),
     ("rsac_pnp_mask", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _d, _u32, _vp, C.POINTER(_i32), _vp]),
+    ("rsac_pnp_epnp", C.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     ("rsac_pnp_refine", C.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32]),
     ("rsac_homography_fit", C.c_int, [_vp, _vp, _i32, _vp, _vp]),
     ("rsac_rodrigues_v2m", None, [_vp, _vp]),

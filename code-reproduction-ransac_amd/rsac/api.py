@@ -70,8 +70,16 @@ def _flags(adaptive, refine, sampler, exact_only=False):
     f = 0
     if adaptive:
         f |= L.F_ADAPTIVE
-    if refine:
+    # refine: True / "lm" -> LM from the minimal model; "epnp" -> EPnP on the inliers (solvePnPRansac
+    # with SOLVEPNP_P3P); "epnp+lm" -> EPnP, then LM from it
+    if refine is True or refine == "lm":
         f |= L.F_REFINE
+    elif refine == "epnp":
+        f |= L.F_EPNP
+    elif refine == "epnp+lm":
+        f |= L.F_EPNP | L.F_REFINE
+    elif refine not in (False, None):
+        raise ValueError(f"refine must be True/False, 'lm', 'epnp' or 'epnp+lm', got {refine!r}")
     if sampler == "opencv":
         f |= L.F_SAMPLER_OPENCV
     elif sampler != "philox":
@@ -495,6 +503,19 @@ def refine_pose(points2D, points3D, K, R, t, mask=None, max_iter: int = 20):
                                     None if m is None else m.ctypes.data, Rr.ctypes.data, tr.ctypes.data,
                                     int(max_iter)))
     return Rr.reshape(3, 3), tr
+
+
+def epnp_pose(points2D, points3D, K, mask=None):
+    """EPnP on all (or the masked) points, cv2.solvePnP(..., flags=SOLVEPNP_EPNP) -> (R, t) or
+    (None, None) for < 4 points / a planar cloud.  Host arrays; the same numbers as the device pass
+    of pnp_ransac(refine="epnp")."""
+    P3 = np.ascontiguousarray(np.asarray(points3D, np.float64).reshape(-1, 3))
+    P2 = np.ascontiguousarray(np.asarray(points2D, np.float64).reshape(-1, 2))
+    m = None if mask is None else np.ascontiguousarray(np.asarray(mask, np.uint8).reshape(-1))
+    R, t = np.zeros(9), np.zeros(3)
+    code = L.check(L.lib().rsac_pnp_epnp(P3.ctypes.data, P2.ctypes.data, P3.shape[0], _K9(K).ctypes.data,
+                                         None if m is None else m.ctypes.data, R.ctypes.data, t.ctypes.data))
+    return (R.reshape(3, 3), t) if code == L.OK else (None, None)
 
 
 def homography_fit(src, dst, mask=None):

@@ -50,8 +50,10 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
     """-> (retval, rvec (3,1), tvec (3,1), inliers (M,1) int32 or None).
 
     Minimal kernel: P3P on 4 points (the north star's kernel; OpenCV's default
-    would be EPnP on 5).  Final pose: LM on the RANSAC inliers started from
-    the best minimal model (what SOLVEPNP_ITERATIVE's final solvePnP does).
+    would be EPnP on 5).  Final pose on the RANSAC inliers as OpenCV's: for
+    SOLVEPNP_P3P / AP3P / EPNP, EPnP (OpenCV re-solves P3P's inliers with
+    EPnP); otherwise LM started from the best minimal model (what
+    SOLVEPNP_ITERATIVE's final solvePnP with the RANSAC guess does).
     """
     _check_dist(distCoeffs)
     P3 = np.asarray(objectPoints, np.float64).reshape(-1, 3)
@@ -60,8 +62,9 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
         raise error("objectPoints and imagePoints differ in length")
     if P3.shape[0] < 4:
         raise error("solvePnPRansac needs at least 4 points")
+    refine = "epnp" if flags in (SOLVEPNP_P3P, SOLVEPNP_AP3P, SOLVEPNP_EPNP) else "lm"
     R, t, mask = api.pnp_ransac(P2, P3, cameraMatrix, int(iterationsCount), float(reprojectionError),
-                                confidence=float(confidence), adaptive=True, refine=True)
+                                confidence=float(confidence), adaptive=True, refine=refine)
     if R is None:
         return False, (np.zeros((3, 1)) if rvec is None else rvec), (np.zeros((3, 1)) if tvec is None else tvec), None
     idx = np.flatnonzero(mask).astype(np.int32).reshape(-1, 1)

@@ -67,6 +67,8 @@ extern "C" {
 #define RSAC_F_DEVICE_OUT (1u << 5)     /* inlier mask output is a device pointer */
 #define RSAC_F_EXACT_ONLY (1u << 6)     /* disable the float32 pre-filter in scoring (A/B and tests) */
 #define RSAC_F_ASYNC (1u << 8)          /* rsac_pnp_evaluate_range: device outputs, no host wait (see there) */
+#define RSAC_F_EPNP (1u << 9)           /* PnP: EPnP on the inliers as the final solve (solvePnPRansac with
+                                           SOLVEPNP_P3P); with RSAC_F_REFINE, LM from the EPnP pose */
 #define RSAC_F_LO (1u << 7)             /* LO-RANSAC (PnP, one problem): local optimisation at every new best,
                                            BASELINE.json configs[4]; see DESIGN.md "LO-RANSAC" */
 
@@ -237,6 +239,14 @@ RSAC_EXPORT int rsac_homography_hypotheses(rsac_ctx *ctx, const void *src, const
 RSAC_EXPORT int rsac_pnp_mask(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
                   const double model[12], double reproj_thresh, uint32_t flags, uint8_t *mask_out,
                   int32_t *count_out, void *stream);
+
+/* cv2.solvePnP(..., flags=SOLVEPNP_EPNP) on the masked points (mask NULL = all), the
+ * final solve cv2.solvePnPRansac runs on its inliers when the minimal solver is P3P
+ * (main_v1.py:497).  Host arrays; the same computation as the device
+ * pass of RSAC_F_EPNP, bit for bit.  Returns RSAC_NO_MODEL for < 4 points or a degenerate
+ * (planar) cloud. */
+RSAC_EXPORT int rsac_pnp_epnp(const double *pts3d, const double *pts2d, int32_t n, const double K[9],
+                              const uint8_t *mask, double R_out[9], double t_out[3]);
 
 /* Host-side non-minimal fits (no GPU needed), f64 AoS host inputs rounded
  * to f32 like the RANSAC path.  mask may be NULL (= all points).

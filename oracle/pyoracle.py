@@ -90,6 +90,8 @@ def lib():
     L.orc_rodrigues_m2v.restype = None
     L.orc_pnp_refine.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, _u8p, C.c_int, _f64p, _f64p, _f64p, C.c_int]
     L.orc_pnp_refine.restype = C.c_int
+    L.orc_pnp_epnp.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, _u8p, C.c_int, _f64p, _f64p, _f64p]
+    L.orc_pnp_epnp.restype = C.c_int
     L.orc_hom_refine.argtypes = [_f32p, _f32p, _f32p, _f32p, _u8p, C.c_int, _f64p]
     L.orc_hom_refine.restype = C.c_int
     L.orc_pnp_ransac.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
@@ -279,6 +281,13 @@ def pnp_refine(soa, mask, cam, R, t, max_iter=20):
     t = np.ascontiguousarray(t, np.float64).copy()
     it = lib().orc_pnp_refine(*soa, np.ascontiguousarray(mask, np.uint8), len(soa[0]), cam, R, t, max_iter)
     return R.reshape(3, 3), t, it
+
+
+def pnp_epnp(soa, mask, cam):
+    """EPnP on the masked points -> (R, t) or (None, None)."""
+    R, t = np.zeros(9), np.zeros(3)
+    ok = lib().orc_pnp_epnp(*soa, np.ascontiguousarray(mask, np.uint8), len(soa[0]), cam, R, t)
+    return (R.reshape(3, 3), t) if ok else (None, None)
 
 
 # ----------------------------------------------------------------------------------------------

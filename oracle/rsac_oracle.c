@@ -1531,3 +1531,427 @@ ORC_API int64_t orc_hom_ransac(const float *sx, const float *sy, const float *dx
     free(counts); free(status); free(models); free(subs); free(sst);
     return best;
 }
+
+/* ------------------------------------------------------------------------
+ * EPnP on the inliers (Lepetit, Moreno-Noguer, Fua 2009): the final solve of
+ * cv2.solvePnPRansac when the minimal solver is P3P (OpenCV re-solves the
+ * inliers with SOLVEPNP_EPNP; main_v1.py:497).  The steps of
+ * OpenCV's epnp.cpp: control points from the centroid and the principal axes,
+ * barycentric alphas, M^T M, its 4 smallest eigenvectors, L 6x10 and rho, beta
+ * approximations 1-3 each + 5 Gauss-Newton steps, the pose by SVD of the
+ * cross-covariance, the lowest mean reprojection error wins.  Numerics of this
+ * project (no OpenCV here to pin them): cyclic Jacobi eigen-decompositions,
+ * Householder least squares, M^T M assembled from per-control-point-pair sums,
+ * the frame centred on the problem's first point, sums in the GPU order
+ * (LM_THREADS strided partials, 64-lane butterfly, wave sums in order).
+ * ------------------------------------------------------------------------ */
+#define EP_MAXV 40
+
+typedef struct { const float *X, *Y, *Z, *U, *V; const uint8_t *mask; int n; double cam[4]; double c[3]; double *part; } epctx;
+typedef void (*ep_fn)(const void *prm, double X, double Y, double Z, double u, double v, double *acc);
+
+static void ep_reduce(epctx *c, int nv, ep_fn f, const void *prm, double *out) {
+    double *part = c->part;
+    for (int q = 0; q < LM_THREADS * nv; ++q) part[q] = 0.0;
+    for (int tid = 0; tid < LM_THREADS; ++tid)
+        for (int i = tid; i < c->n; i += LM_THREADS)
+            if (c->mask[i])
+                f(prm, (double)c->X[i] - c->c[0], (double)c->Y[i] - c->c[1], (double)c->Z[i] - c->c[2],
+                  (double)c->U[i], (double)c->V[i], part + tid * nv);
+    double wsum[LM_THREADS / 64][EP_MAXV], v[64], w[64];
+    for (int wv = 0; wv < LM_THREADS / 64; ++wv)
+        for (int q = 0; q < nv; ++q) {
+            for (int l = 0; l < 64; ++l) v[l] = part[(wv * 64 + l) * nv + q];
+            for (int o = 32; o > 0; o >>= 1) {
+                for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
+                for (int l = 0; l < 64; ++l) v[l] = w[l];
+            }
+            wsum[wv][q] = v[0];
+        }
+    for (int q = 0; q < nv; ++q) {
+        double s = wsum[0][q];
+        for (int wv = 1; wv < LM_THREADS / 64; ++wv) s = s + wsum[wv][q];
+        out[q] = s;
+    }
+}
+
+/* cyclic Jacobi, symmetric N x N (destroyed): d eigenvalues, V[i*N+k] k-th eigenvector */
+static void ep_jacobi(int N, double *A, double *V, double *d) {
+    for (int i = 0; i < N * N; ++i) V[i] = 0.0;
+    for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0, diag = 0.0;
+        for (int p = 0; p < N; ++p) {
+            diag = diag + A[p * N + p] * A[p * N + p];
+            for (int q = p + 1; q < N; ++q) off = off + A[p * N + q] * A[p * N + q];
+        }
+        if (!(off > 1e-32 * diag)) break;
+        for (int p = 0; p < N - 1; ++p)
+            for (int q = p + 1; q < N; ++q) {
+                double apq = A[p * N + q];
+                if (apq == 0.0) continue;
+                double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
+                double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                double cs = 1.0 / sqrt(tt * tt + 1.0), sn = tt * cs;
+                for (int k = 0; k < N; ++k) {
+                    double akp = A[k * N + p], akq = A[k * N + q];
+                    A[k * N + p] = cs * akp - sn * akq;
+                    A[k * N + q] = sn * akp + cs * akq;
+                }
+                for (int k = 0; k < N; ++k) {
+                    double apk = A[p * N + k], aqk = A[q * N + k];
+                    A[p * N + k] = cs * apk - sn * aqk;
+                    A[q * N + k] = sn * apk + cs * aqk;
+                }
+                for (int k = 0; k < N; ++k) {
+                    double vkp = V[k * N + p], vkq = V[k * N + q];
+                    V[k * N + p] = cs * vkp - sn * vkq;
+                    V[k * N + q] = sn * vkp + cs * vkq;
+                }
+            }
+    }
+    for (int k = 0; k < N; ++k) d[k] = A[k * N + k];
+}
+
+/* eigenvalue indices by decreasing value, ties keep the lower index first (insertion sort) */
+static void ep_order(int N, const double *d, int *o) {
+    for (int i = 0; i < N; ++i) o[i] = i;
+    for (int i = 1; i < N; ++i) {
+        int k = o[i], j = i - 1;
+        while (j >= 0 && d[o[j]] < d[k]) { o[j + 1] = o[j]; --j; }
+        o[j + 1] = k;
+    }
+}
+
+/* min |A x - b|, A 6 x N (N <= 5), Householder QR; a vanishing pivot gives x_k = 0 */
+static void ep_lsq(int N, double *A, double *b, double *x) {
+    const int M = 6;
+    for (int k = 0; k < N; ++k) {
+        double nrm = 0.0, v[6], vv = 0.0, sdot, f;
+        for (int i = k; i < M; ++i) nrm = nrm + A[i * N + k] * A[i * N + k];
+        nrm = sqrt(nrm);
+        if (nrm == 0.0) continue;
+        double alpha = A[k * N + k] > 0.0 ? -nrm : nrm;
+        for (int i = k; i < M; ++i) v[i] = A[i * N + k];
+        v[k] = v[k] - alpha;
+        for (int i = k; i < M; ++i) vv = vv + v[i] * v[i];
+        if (vv == 0.0) continue;
+        for (int j = k; j < N; ++j) {
+            sdot = 0.0;
+            for (int i = k; i < M; ++i) sdot = sdot + v[i] * A[i * N + j];
+            f = 2.0 * sdot / vv;
+            for (int i = k; i < M; ++i) A[i * N + j] = A[i * N + j] - f * v[i];
+        }
+        sdot = 0.0;
+        for (int i = k; i < M; ++i) sdot = sdot + v[i] * b[i];
+        f = 2.0 * sdot / vv;
+        for (int i = k; i < M; ++i) b[i] = b[i] - f * v[i];
+    }
+    for (int k = N - 1; k >= 0; --k) {
+        double s = b[k];
+        for (int j = k + 1; j < N; ++j) s = s - A[k * N + j] * x[j];
+        double rkk = A[k * N + k];
+        x[k] = fabs(rkk) > 1e-300 ? s / rkk : 0.0;
+    }
+}
+
+typedef struct { double c[3], ci[9]; } ep_alpha;
+
+static void ep_alphas(const ep_alpha *f, double X, double Y, double Z, double *a) {
+    double dx = X - f->c[0], dy = Y - f->c[1], dz = Z - f->c[2];
+    for (int j = 0; j < 3; ++j) a[1 + j] = f->ci[3 * j] * dx + f->ci[3 * j + 1] * dy + f->ci[3 * j + 2] * dz;
+    a[0] = 1.0 - a[1] - a[2] - a[3];
+}
+
+static void ep_f_mean(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
+    acc[0] += X; acc[1] += Y; acc[2] += Z; acc[3] += 1.0;
+}
+static void ep_f_cov(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
+    const double *c0 = (const double *)prm;
+    double x = X - c0[0], y = Y - c0[1], z = Z - c0[2];
+    acc[0] += x * x; acc[1] += x * y; acc[2] += x * z; acc[3] += y * y; acc[4] += y * z; acc[5] += z * z;
+}
+typedef struct { ep_alpha af; double cam[4]; } ep_pair_prm;
+static void ep_f_pairs(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
+    const ep_pair_prm *p = (const ep_pair_prm *)prm;
+    double a[4];
+    ep_alphas(&p->af, X, Y, Z, a);
+    double du = p->cam[2] - u, dv = p->cam[3] - v, w = du * du + dv * dv;
+    int q = 0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = i; j < 4; ++j, q += 4) {
+            double aa = a[i] * a[j];
+            acc[q] += aa;
+            acc[q + 1] += aa * du;
+            acc[q + 2] += aa * dv;
+            acc[q + 3] += aa * w;
+        }
+}
+typedef struct { ep_alpha af; double cc[4][3]; double pc0[3]; double c0[3]; } ep_pose_prm;
+static void ep_f_pc0(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
+    const ep_pose_prm *p = (const ep_pose_prm *)prm;
+    double a[4];
+    ep_alphas(&p->af, X, Y, Z, a);
+    for (int j = 0; j < 3; ++j) acc[j] += a[0] * p->cc[0][j] + a[1] * p->cc[1][j] + a[2] * p->cc[2][j] + a[3] * p->cc[3][j];
+}
+static void ep_f_cross(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
+    const ep_pose_prm *p = (const ep_pose_prm *)prm;
+    double a[4], pc[3];
+    ep_alphas(&p->af, X, Y, Z, a);
+    for (int j = 0; j < 3; ++j)
+        pc[j] = a[0] * p->cc[0][j] + a[1] * p->cc[1][j] + a[2] * p->cc[2][j] + a[3] * p->cc[3][j] - p->pc0[j];
+    double pw[3] = {X - p->c0[0], Y - p->c0[1], Z - p->c0[2]};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) acc[3 * i + j] += pc[i] * pw[j];
+}
+typedef struct { double R[9], t[3], cam[4]; } ep_err_prm;
+static void ep_f_err(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
+    const ep_err_prm *p = (const ep_err_prm *)prm;
+    const double *R = p->R, *t = p->t;
+    double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    double iz = 1.0 / (R[6] * X + R[7] * Y + R[8] * Z + t[2]);
+    double du = u - (p->cam[2] + p->cam[0] * x * iz), dv = v - (p->cam[3] + p->cam[1] * y * iz);
+    acc[0] += sqrt(du * du + dv * dv);
+}
+
+/* R = U V^T of the cross-covariance H (SVD via the eigen-decomposition of H^T H), last row
+ * negated when det < 0 (OpenCV's estimate_R_and_t); 0 when H has rank < 2 */
+static int ep_rotation(const double *H, double *R) {
+    double B[9], V[9], d[3], v[3][3], u[3][3];
+    int o[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) B[3 * i + j] = H[i] * H[j] + H[3 + i] * H[3 + j] + H[6 + i] * H[6 + j];
+    ep_jacobi(3, B, V, d);
+    ep_order(3, d, o);
+    for (int k = 0; k < 3; ++k)
+        for (int i = 0; i < 3; ++i) v[k][i] = V[3 * i + o[k]];
+    double s0 = sqrt(d[o[0]] > 0.0 ? d[o[0]] : 0.0);
+    if (!(s0 > 0.0)) return 0;
+    for (int k = 0; k < 3; ++k) {
+        double sk = sqrt(d[o[k]] > 0.0 ? d[o[k]] : 0.0);
+        if (k < 2 || sk > 1e-10 * s0) {
+            if (!(sk > 1e-10 * s0)) return 0;
+            for (int i = 0; i < 3; ++i) u[k][i] = (H[3 * i] * v[k][0] + H[3 * i + 1] * v[k][1] + H[3 * i + 2] * v[k][2]) / sk;
+        } else {
+            u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
+            u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
+            u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
+        }
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = u[0][i] * v[0][j] + u[1][i] * v[1][j] + u[2][i] * v[2][j];
+    double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) + R[2] * (R[3] * R[7] - R[4] * R[6]);
+    if (det < 0.0)
+        for (int j = 0; j < 3; ++j) R[6 + j] = -R[6 + j];
+    return 1;
+}
+
+/* 5 Gauss-Newton steps on the betas */
+static void ep_gauss_newton(const double *L, const double *rho, double *be) {
+    for (int it = 0; it < 5; ++it) {
+        double A[24], b[6], x[4];
+        for (int i = 0; i < 6; ++i) {
+            const double *r = L + 10 * i;
+            A[4 * i + 0] = 2.0 * r[0] * be[0] + r[1] * be[1] + r[3] * be[2] + r[6] * be[3];
+            A[4 * i + 1] = r[1] * be[0] + 2.0 * r[2] * be[1] + r[4] * be[2] + r[7] * be[3];
+            A[4 * i + 2] = r[3] * be[0] + r[4] * be[1] + 2.0 * r[5] * be[2] + r[8] * be[3];
+            A[4 * i + 3] = r[6] * be[0] + r[7] * be[1] + r[8] * be[2] + 2.0 * r[9] * be[3];
+            b[i] = rho[i] - (r[0] * be[0] * be[0] + r[1] * be[0] * be[1] + r[2] * be[1] * be[1] +
+                             r[3] * be[0] * be[2] + r[4] * be[1] * be[2] + r[5] * be[2] * be[2] +
+                             r[6] * be[0] * be[3] + r[7] * be[1] * be[3] + r[8] * be[2] * be[3] +
+                             r[9] * be[3] * be[3]);
+        }
+        ep_lsq(4, A, b, x);
+        for (int j = 0; j < 4; ++j) be[j] = be[j] + x[j];
+    }
+}
+
+/* returns 1 and (R, t) in the input frame, or 0 (< 4 inliers / degenerate cloud; R, t untouched) */
+ORC_API int orc_pnp_epnp(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                         const uint8_t *mask, int n, const double cam[4], double R_out[9], double t_out[3]) {
+    if (n <= 0) return 0;
+    epctx c = {X, Y, Z, U, V, mask, n, {cam[0], cam[1], cam[2], cam[3]}, {X[0], Y[0], Z[0]}, NULL};
+    c.part = (double *)malloc(sizeof(double) * LM_THREADS * EP_MAXV);
+    int ok = 0;
+    double s4[4], cw[4][3], cov[6];
+    ep_reduce(&c, 4, ep_f_mean, NULL, s4);
+    double nn = s4[3];
+    if (!(nn >= 4.0)) goto out;
+    for (int j = 0; j < 3; ++j) cw[0][j] = s4[j] / nn;
+    ep_reduce(&c, 6, ep_f_cov, cw[0], cov);
+    {
+        double A[9] = {cov[0], cov[1], cov[2], cov[1], cov[3], cov[4], cov[2], cov[4], cov[5]}, Vv[9], d[3];
+        int o[3];
+        ep_jacobi(3, A, Vv, d);
+        ep_order(3, d, o);
+        for (int i = 1; i < 4; ++i) {
+            double ev = d[o[i - 1]];
+            double kk = sqrt((ev > 0.0 ? ev : 0.0) / nn);
+            for (int j = 0; j < 3; ++j) cw[i][j] = cw[0][j] + kk * Vv[3 * j + o[i - 1]];
+        }
+    }
+    ep_alpha af;
+    for (int j = 0; j < 3; ++j) af.c[j] = cw[0][j];
+    {
+        double cc[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 1; j < 4; ++j) cc[3 * i + j - 1] = cw[j][i] - cw[0][i];
+        double m00 = cc[4] * cc[8] - cc[5] * cc[7], m01 = cc[5] * cc[6] - cc[3] * cc[8], m02 = cc[3] * cc[7] - cc[4] * cc[6];
+        double det = cc[0] * m00 + cc[1] * m01 + cc[2] * m02;
+        double nrm = 0.0;
+        for (int q = 0; q < 9; ++q) nrm = nrm + cc[q] * cc[q];
+        if (!(fabs(det) > 1e-12 * nrm * sqrt(nrm))) goto out;
+        double id = 1.0 / det;
+        af.ci[0] = m00 * id;
+        af.ci[1] = (cc[2] * cc[7] - cc[1] * cc[8]) * id;
+        af.ci[2] = (cc[1] * cc[5] - cc[2] * cc[4]) * id;
+        af.ci[3] = m01 * id;
+        af.ci[4] = (cc[0] * cc[8] - cc[2] * cc[6]) * id;
+        af.ci[5] = (cc[2] * cc[3] - cc[0] * cc[5]) * id;
+        af.ci[6] = m02 * id;
+        af.ci[7] = (cc[1] * cc[6] - cc[0] * cc[7]) * id;
+        af.ci[8] = (cc[0] * cc[4] - cc[1] * cc[3]) * id;
+    }
+    double pairs[40];
+    {
+        ep_pair_prm pp;
+        pp.af = af;
+        memcpy(pp.cam, cam, sizeof(pp.cam));
+        ep_reduce(&c, 40, ep_f_pairs, &pp, pairs);
+    }
+    double ut[4][12], L[60], rho[6], be3[3][4];
+    int valid[3];
+    {
+        double A[144], Vv[144], d[12];
+        int o[12], q = 0;
+        const double fx = cam[0], fy = cam[1];
+        for (int i = 0; i < 4; ++i)
+            for (int j = i; j < 4; ++j, q += 4) {
+                double s0 = pairs[q], su = pairs[q + 1], sv = pairs[q + 2], sw = pairs[q + 3];
+                double blk[9] = {fx * fx * s0, 0.0, fx * su, 0.0, fy * fy * s0, fy * sv, fx * su, fy * sv, sw};
+                for (int p = 0; p < 3; ++p)
+                    for (int r = 0; r < 3; ++r) {
+                        A[12 * (3 * i + p) + 3 * j + r] = blk[3 * p + r];
+                        A[12 * (3 * j + r) + 3 * i + p] = blk[3 * p + r];
+                    }
+            }
+        ep_jacobi(12, A, Vv, d);
+        ep_order(12, d, o);
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 12; ++j) ut[i][j] = Vv[12 * j + o[11 - i]];
+        /* L 6x10 (compute_L_6x10) */
+        int a = 0, b = 1;
+        for (int i = 0; i < 6; ++i) {
+            double dv[4][3];
+            for (int p = 0; p < 4; ++p)
+                for (int qq = 0; qq < 3; ++qq) dv[p][qq] = ut[p][3 * a + qq] - ut[p][3 * b + qq];
+            ++b;
+            if (b > 3) { ++a; b = a + 1; }
+#define EPDOT(p, qd) (dv[p][0] * dv[qd][0] + dv[p][1] * dv[qd][1] + dv[p][2] * dv[qd][2])
+            double *r = L + 10 * i;
+            r[0] = EPDOT(0, 0);
+            r[1] = 2.0 * EPDOT(0, 1);
+            r[2] = EPDOT(1, 1);
+            r[3] = 2.0 * EPDOT(0, 2);
+            r[4] = 2.0 * EPDOT(1, 2);
+            r[5] = EPDOT(2, 2);
+            r[6] = 2.0 * EPDOT(0, 3);
+            r[7] = 2.0 * EPDOT(1, 3);
+            r[8] = 2.0 * EPDOT(2, 3);
+            r[9] = EPDOT(3, 3);
+#undef EPDOT
+        }
+        q = 0;
+        for (int i = 0; i < 4; ++i)
+            for (int j = i + 1; j < 4; ++j, ++q) {
+                double dx = cw[i][0] - cw[j][0], dy = cw[i][1] - cw[j][1], dz = cw[i][2] - cw[j][2];
+                rho[q] = dx * dx + dy * dy + dz * dz;
+            }
+        for (int ap = 1; ap <= 3; ++ap) {
+            double *be = be3[ap - 1], bb[6];
+            for (int j = 0; j < 4; ++j) be[j] = 0.0;
+            for (int i = 0; i < 6; ++i) bb[i] = rho[i];
+            int okk = 1;
+            if (ap == 1) {
+                static const int cols[4] = {0, 1, 3, 6};
+                double AA[24], x[4];
+                for (int i = 0; i < 6; ++i)
+                    for (int j = 0; j < 4; ++j) AA[4 * i + j] = L[10 * i + cols[j]];
+                ep_lsq(4, AA, bb, x);
+                double sg = x[0] < 0.0 ? -1.0 : 1.0;
+                be[0] = sqrt(sg * x[0]);
+                okk = be[0] != 0.0;
+                if (okk)
+                    for (int j = 1; j < 4; ++j) be[j] = sg * x[j] / be[0];
+            } else if (ap == 2) {
+                double AA[18], x[3];
+                for (int i = 0; i < 6; ++i)
+                    for (int j = 0; j < 3; ++j) AA[3 * i + j] = L[10 * i + j];
+                ep_lsq(3, AA, bb, x);
+                if (x[0] < 0.0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0.0 ? sqrt(-x[2]) : 0.0; }
+                else { be[0] = sqrt(x[0]); be[1] = x[2] > 0.0 ? sqrt(x[2]) : 0.0; }
+                if (x[1] < 0.0) be[0] = -be[0];
+            } else {
+                double AA[30], x[5];
+                for (int i = 0; i < 6; ++i)
+                    for (int j = 0; j < 5; ++j) AA[5 * i + j] = L[10 * i + j];
+                ep_lsq(5, AA, bb, x);
+                if (x[0] < 0.0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0.0 ? sqrt(-x[2]) : 0.0; }
+                else { be[0] = sqrt(x[0]); be[1] = x[2] > 0.0 ? sqrt(x[2]) : 0.0; }
+                if (x[1] < 0.0) be[0] = -be[0];
+                okk = be[0] != 0.0;
+                if (okk) be[2] = x[3] / be[0];
+            }
+            if (okk) ep_gauss_newton(L, rho, be);
+            valid[ap - 1] = okk;
+        }
+    }
+    int first = -1;
+    for (int i = 0; i < n; ++i)
+        if (mask[i]) { first = i; break; }
+    if (first < 0) goto out;
+    double a1[4];
+    ep_alphas(&af, (double)X[first] - c.c[0], (double)Y[first] - c.c[1], (double)Z[first] - c.c[2], a1);
+    double best = 0.0, bR[9], bt[3];
+    int have = 0;
+    for (int ap = 0; ap < 3; ++ap) {
+        if (!valid[ap]) continue;
+        const double *be = be3[ap];
+        ep_pose_prm pp;
+        pp.af = af;
+        for (int j = 0; j < 3; ++j) pp.c0[j] = cw[0][j];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 3; ++j)
+                pp.cc[i][j] = be[0] * ut[0][3 * i + j] + be[1] * ut[1][3 * i + j] + be[2] * ut[2][3 * i + j] + be[3] * ut[3][3 * i + j];
+        double z1 = a1[0] * pp.cc[0][2] + a1[1] * pp.cc[1][2] + a1[2] * pp.cc[2][2] + a1[3] * pp.cc[3][2];
+        if (z1 < 0.0)
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 3; ++j) pp.cc[i][j] = -pp.cc[i][j];
+        ep_reduce(&c, 3, ep_f_pc0, &pp, pp.pc0);
+        for (int j = 0; j < 3; ++j) pp.pc0[j] = pp.pc0[j] / nn;
+        double H[9];
+        ep_reduce(&c, 9, ep_f_cross, &pp, H);
+        ep_err_prm ep;
+        if (!ep_rotation(H, ep.R)) continue;
+        for (int i = 0; i < 3; ++i) ep.t[i] = pp.pc0[i] - (ep.R[3 * i] * cw[0][0] + ep.R[3 * i + 1] * cw[0][1] + ep.R[3 * i + 2] * cw[0][2]);
+        memcpy(ep.cam, cam, sizeof(ep.cam));
+        double es;
+        ep_reduce(&c, 1, ep_f_err, &ep, &es);
+        double err = es / nn;
+        if (!have || err < best) {
+            have = 1;
+            best = err;
+            memcpy(bR, ep.R, sizeof(bR));
+            memcpy(bt, ep.t, sizeof(bt));
+        }
+    }
+    if (!have) goto out;
+    for (int j = 0; j < 3; ++j) bt[j] = bt[j] - (bR[3 * j] * c.c[0] + bR[3 * j + 1] * c.c[1] + bR[3 * j + 2] * c.c[2]);
+    memcpy(R_out, bR, sizeof(bR));
+    memcpy(t_out, bt, sizeof(bt));
+    ok = 1;
+out:
+    free(c.part);
+    return ok;
+}
