@@ -283,6 +283,22 @@ def extra_workloads(local, args):
                               "note": "find_homographies of main_v1.py:254-297 (OpenCV-sampler RANSAC + LM refit + "
                                       "err1/err2) for every candidate, one call"}
     out["dem_ray_march"] = dem_workload(local)
+    # the final solve on the C2 problem's inliers: ms-to-best-model for each refit choice
+    p2c = synth.pnp_problem(args.points, 0.5, seed=0)
+    g2 = torch.from_numpy(p2c["points2d"]).to(dev)
+    g3 = torch.from_numpy(p2c["points3d"]).to(dev)
+    fin = {}
+    for mode in (False, "lm", "epnp", "epnp+lm"):
+        walls = []
+        for i in range(12):
+            t = time.perf_counter()
+            rsac.pnp_ransac(g2, g3, p2c["K"], 5000, args.thr, refine=mode, device=local)
+            torch.cuda.synchronize()
+            if i >= 2:
+                walls.append((time.perf_counter() - t) * 1e3)
+        fin[str(mode).lower()] = statistics.median(walls)
+    out["final_solve_ms_to_best"] = dict(fin, note="pnp_ransac wall time, adaptive, C2 problem; refine=False/lm/"
+                                                    "epnp (solvePnPRansac SOLVEPNP_P3P)/epnp+lm")
     return out
 
 

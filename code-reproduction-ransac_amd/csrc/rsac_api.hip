@@ -130,8 +130,9 @@ struct rsac_ctx {
     DevBuf lo;                                                 // LO-RANSAC: 2 model records, 2 counts, 2 masks
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
+    DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
     // pinned host staging
-    PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask;
+    PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask, h_epnp;
 };
 
 // ---------------------------------------------------------------------------
@@ -586,7 +587,25 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         // final solve on the device, one block per problem, on the RANSAC-phase inliers:
         // EPnP (solvePnPRansac with SOLVEPNP_P3P), then / or LM (solvePnPRefineLM)
         const uint8_t *dmask = (flags & RSAC_F_DEVICE_OUT) && mask_out ? mask_out : c->mask.as<uint8_t>();
-        if (flags & RSAC_F_EPNP) HIPCHK(launch_pnp_epnp(a, P, dmask, c->bestmodels.as<double>(), s));
+        if (flags & RSAC_F_EPNP) {
+            // stage 1 (sums) on the device, stage 2 (12 x 12 eigenvectors + betas, O(1)) on the
+            // host, stage 3 (pose candidates) on the device
+            const size_t b1 = sizeof(EpnpStage1) * P, b2 = sizeof(EpnpStage2) * P;
+            HIPCHK(c->epnp.ensure(b1 + b2));
+            HIPCHK(c->h_epnp.ensure(b1 + b2));
+            EpnpStage1 *d1 = c->epnp.as<EpnpStage1>(), *h1 = c->h_epnp.as<EpnpStage1>();
+            EpnpStage2 *d2 = (EpnpStage2 *)(d1 + P), *h2 = (EpnpStage2 *)(h1 + P);
+            HIPCHK(launch_pnp_epnp_s1(a, P, dmask, c->bestmodels.as<double>(), d1, s));
+            HIPCHK(hipMemcpyAsync(h1, d1, b1, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            parallel_for(P, [&](int p) {
+                const double *Kp = K + 9 * p;
+                if (h1[p].ok != 0.0) epnp_stage2(h1[p], Cam{Kp[0], Kp[4], Kp[2], Kp[5]}, h2[p]);
+                else memset(&h2[p], 0, sizeof(EpnpStage2));
+            });
+            HIPCHK(hipMemcpyAsync(d2, h2, b2, hipMemcpyHostToDevice, s));
+            HIPCHK(launch_pnp_epnp_s3(a, P, dmask, d1, d2, c->bestmodels.as<double>(), s));
+        }
         if (flags & RSAC_F_REFINE) HIPCHK(launch_pnp_refine(a, P, dmask, c->bestmodels.as<double>(), nullptr, s));
         HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
                               hipMemcpyDeviceToHost, s));

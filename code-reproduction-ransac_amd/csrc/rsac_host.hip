@@ -153,7 +153,6 @@ struct HostEpnpReducer {
     int n;
     double c[3];
     std::vector<double> part = std::vector<double>((size_t)kLmThreads * kRedMax);
-    EpnpShared sh;
     template <int NV, class F>
     void sum(F f, double *out) {
         lm_reduce_host(n, mask, NV, part.data(), out, [&](int i, double *a) {
@@ -170,9 +169,6 @@ struct HostEpnpReducer {
             }
         return false;
     }
-    EpnpShared *shared() { return &sh; }
-    bool leader() const { return true; }
-    void sync() {}
 };
 
 }  // namespace

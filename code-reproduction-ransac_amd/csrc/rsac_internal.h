@@ -7,6 +7,9 @@
 
 namespace rsac {
 
+struct EpnpStage1;
+struct EpnpStage2;
+
 // PnP problem set on the device.  Problem p owns points [offsets[p],
 // offsets[p+1]) of the SoA arrays; its hypothesis records live at
 // [p * hyp_stride, p * hyp_stride + H).
@@ -114,7 +117,10 @@ hipError_t launch_fm_mask(const HomArgs &a, int32_t P, int32_t max_n, const int6
 
 // LM refit of every problem's model record (models: P x kModelStride, R 9, t 3, valid)
 // on the inliers of mask (concatenated points), one block per problem
-hipError_t launch_pnp_epnp(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, hipStream_t s);
+hipError_t launch_pnp_epnp_s1(const PnpArgs &a, int32_t P, const uint8_t *mask, const double *models,
+                              EpnpStage1 *st1, hipStream_t s);
+hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, const EpnpStage1 *st1,
+                              const EpnpStage2 *st2, double *models, hipStream_t s);
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
                              hipStream_t s);
 

@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <utility>
 
 #include "rsac_geo.h"
 #include "rsac_internal.h"
@@ -1567,27 +1568,42 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
 
 // EPnP of every problem's winner on its RANSAC inliers (rsac_math.h pnp_epnp),
 // one block per problem; the same summation order as the host (pnp_epnp_host).
+constexpr int kEpThreads = 256;  // real threads; the sums keep kLmThreads (512) virtual ones
+
 struct GpuEpnpReducer {
     const float *X, *Y, *Z, *U, *V;
     const uint8_t *mask;
     int n;
     double c0, c1, c2;
     double (*wsum)[kRedMax];  // LDS [kLmThreads / 64][kRedMax]
-    EpnpShared *sh;           // LDS
-    int *wmin;                // LDS [kLmThreads / 64]
+    int *wmin;                // LDS [kEpThreads / 64]
 
+    // Thread t accumulates virtual threads t and t + 256 of the kLmThreads-strided order in
+    // separate partials, so the sums equal the 512-thread order bit for bit while each thread
+    // has twice the registers of a 512-thread block.
     template <int NV, class F>
     __device__ void sum(F f, double *out) {
-        double a[NV];
-        for (int q = 0; q < NV; ++q) a[q] = 0.0;
+        double a0[NV], a1[NV];
+        for (int q = 0; q < NV; ++q) a0[q] = a1[q] = 0.0;
+#pragma unroll 1
         for (int i = threadIdx.x; i < n; i += kLmThreads)
             if (mask[i])
-                f((double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i], (double)V[i], a);
+                f((double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i], (double)V[i], a0);
+#pragma unroll 1
+        for (int i = threadIdx.x + kEpThreads; i < n; i += kLmThreads)
+            if (mask[i])
+                f((double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i], (double)V[i], a1);
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         for (int q = 0; q < NV; ++q) {
-            double v = a[q];
-            for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o);
-            if (lane == 0) wsum[wave][q] = v;
+            double v0 = a0[q], v1 = a1[q];
+            for (int o = 32; o > 0; o >>= 1) {
+                v0 = v0 + __shfl_xor(v0, o);
+                v1 = v1 + __shfl_xor(v1, o);
+            }
+            if (lane == 0) {
+                wsum[wave][q] = v0;
+                wsum[wave + kEpThreads / 64][q] = v1;
+            }
         }
         __syncthreads();
         for (int q = 0; q < NV; ++q) {
@@ -1599,7 +1615,7 @@ struct GpuEpnpReducer {
     }
     __device__ bool first(double *p) {
         int m = 0x7fffffff;
-        for (int i = threadIdx.x; i < n; i += kLmThreads)
+        for (int i = threadIdx.x; i < n; i += kEpThreads)
             if (mask[i]) {
                 m = i;
                 break;
@@ -1608,7 +1624,7 @@ struct GpuEpnpReducer {
         if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = m;
         __syncthreads();
         m = wmin[0];
-        for (int w = 1; w < kLmThreads / 64; ++w) m = min(m, wmin[w]);
+        for (int w = 1; w < kEpThreads / 64; ++w) m = min(m, wmin[w]);
         __syncthreads();
         if (m == 0x7fffffff) return false;
         p[0] = (double)X[m] - c0;
@@ -1616,36 +1632,65 @@ struct GpuEpnpReducer {
         p[2] = (double)Z[m] - c2;
         return true;
     }
-    __device__ EpnpShared *shared() { return sh; }
-    __device__ bool leader() const { return threadIdx.x == 0; }
-    __device__ void sync() { __syncthreads(); }
 };
 
-__global__ __launch_bounds__(kLmThreads) void k_pnp_epnp(PnpArgs a, const uint8_t *__restrict__ mask,
-                                                         double *__restrict__ models) {
-    __shared__ double wsum[kLmThreads / 64][kRedMax];
-    __shared__ EpnpShared sh;
-    __shared__ int wmin[kLmThreads / 64];
-    const int prob = blockIdx.x;
-    double *m = models + (int64_t)prob * kModelStride;
-    if (m[kValidSlot] == 0.0) return;  // no model: block-uniform exit
+// EPnP stage 1 (sums -> frame + pair sums) and stage 3 (pose candidates) of every problem's
+// winner, one block per problem; stage 2 (12 x 12 eigenvectors, betas) runs on the host in
+// between (rsac_api.hip).  Problems without a model write s1.ok = 0.
+__device__ GpuEpnpReducer epnp_reducer(const PnpArgs &a, const uint8_t *mask, int prob, double (*wsum)[kRedMax],
+                                       int *wmin) {
     const int64_t p0 = a.offsets[prob];
+    return GpuEpnpReducer{a.X + p0, a.Y + p0, a.Z + p0, a.U + p0, a.V + p0, mask + p0,
+                          (int)(a.offsets[prob + 1] - p0), (double)a.X[p0], (double)a.Y[p0], (double)a.Z[p0],
+                          wsum, wmin};
+}
+
+__global__ __launch_bounds__(kEpThreads) void k_pnp_epnp_s1(PnpArgs a, const uint8_t *__restrict__ mask,
+                                                            const double *__restrict__ models, EpnpStage1 *st1) {
+    __shared__ double wsum[kLmThreads / 64][kRedMax];
+    __shared__ int wmin[kEpThreads / 64];
+    const int prob = blockIdx.x;
+    if (models[(int64_t)prob * kModelStride + kValidSlot] == 0.0) {  // no model: block-uniform exit
+        if (threadIdx.x == 0) st1[prob].ok = 0.0;
+        return;
+    }
     const double *cm = a.cams + 4 * prob;
-    const double c[3] = {(double)a.X[p0], (double)a.Y[p0], (double)a.Z[p0]};
-    GpuEpnpReducer red{a.X + p0, a.Y + p0, a.Z + p0, a.U + p0, a.V + p0, mask + p0,
-                       (int)(a.offsets[prob + 1] - p0), c[0], c[1], c[2], wsum, &sh, wmin};
+    GpuEpnpReducer red = epnp_reducer(a, mask, prob, wsum, wmin);
+    EpnpStage1 s1;
+    epnp_stage1(red, Cam{cm[0], cm[1], cm[2], cm[3]}, s1);
+    if (threadIdx.x == 0) st1[prob] = s1;
+}
+
+__global__ __launch_bounds__(kEpThreads) void k_pnp_epnp_s3(PnpArgs a, const uint8_t *__restrict__ mask,
+                                                            const EpnpStage1 *__restrict__ st1,
+                                                            const EpnpStage2 *__restrict__ st2,
+                                                            double *__restrict__ models) {
+    __shared__ double wsum[kLmThreads / 64][kRedMax];
+    __shared__ int wmin[kEpThreads / 64];
+    const int prob = blockIdx.x;
+    if (st1[prob].ok == 0.0) return;  // block-uniform
+    const double *cm = a.cams + 4 * prob;
+    GpuEpnpReducer red = epnp_reducer(a, mask, prob, wsum, wmin);
     double R[9], t[3];
-    const bool ok = pnp_epnp(red, Cam{cm[0], cm[1], cm[2], cm[3]}, R, t);
-    __syncthreads();  // every thread has read m before thread 0 overwrites it
+    const bool ok = epnp_stage3(red, Cam{cm[0], cm[1], cm[2], cm[3]}, st1[prob], st2[prob], R, t);
     if (ok && threadIdx.x == 0) {
+        const double c[3] = {red.c0, red.c1, red.c2};
         lm_from_centred(R, c, t);
+        double *m = models + (int64_t)prob * kModelStride;
         for (int j = 0; j < 9; ++j) m[j] = R[j];
         for (int j = 0; j < 3; ++j) m[9 + j] = t[j];
     }
 }
 
-hipError_t launch_pnp_epnp(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, hipStream_t s) {
-    hipLaunchKernelGGL(k_pnp_epnp, dim3(P), dim3(kLmThreads), 0, s, a, mask, models);
+hipError_t launch_pnp_epnp_s1(const PnpArgs &a, int32_t P, const uint8_t *mask, const double *models,
+                              EpnpStage1 *st1, hipStream_t s) {
+    hipLaunchKernelGGL(k_pnp_epnp_s1, dim3(P), dim3(kEpThreads), 0, s, a, mask, models, st1);
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, const EpnpStage1 *st1,
+                              const EpnpStage2 *st2, double *models, hipStream_t s) {
+    hipLaunchKernelGGL(k_pnp_epnp_s3, dim3(P), dim3(kEpThreads), 0, s, a, mask, st1, st2, models);
     return hipGetLastError();
 }
 

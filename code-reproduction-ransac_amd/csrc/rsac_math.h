@@ -940,6 +940,25 @@ RSAC_HD void epnp_alphas(const EpnpAlpha &f, double X, double Y, double Z, doubl
     a[0] = 1.0 - a[1] - a[2] - a[3];
 }
 
+// one point's terms of the control-point pair sums, pairs 5 H .. 5 H + 4 of (0,0) (0,1) (0,2)
+// (0,3) (1,1) (1,2) (1,3) (2,2) (2,3) (3,3): a_i a_j times 1, (cx - u), (cy - v), |(cx - u, cy - v)|^2
+template <int H>
+RSAC_HD void epnp_pair_acc(const EpnpAlpha &af, const Cam &k, double X, double Y, double Z, double u, double v,
+                           double *acc) {
+    constexpr int pi[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3}, pj[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
+    double a[4];
+    epnp_alphas(af, X, Y, Z, a);
+    const double du = k.cx - u, dv = k.cy - v, w = du * du + dv * dv;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+        const double aa = a[pi[5 * H + r]] * a[pj[5 * H + r]];
+        acc[4 * r] += aa;
+        acc[4 * r + 1] += aa * du;
+        acc[4 * r + 2] += aa * dv;
+        acc[4 * r + 3] += aa * w;
+    }
+}
+
 // the 6 x 10 L matrix of the betas' quadratic forms (OpenCV compute_L_6x10)
 RSAC_HD void epnp_l6x10(const double *const v[4], double *L) {
     int a = 0, b = 1;
@@ -1021,20 +1040,30 @@ RSAC_HD bool epnp_rotation(const double *H, double *R) {
     return true;
 }
 
-// The serial middle of EPnP (M^T M's eigenvectors, L, rho, the three beta
-// estimates) runs on one thread (Red::leader) in this scratch -- LDS on the GPU.
-struct EpnpShared {
-    double A[144], V[144], d[12];
-    double ut[4][12];  // eigenvectors of the 4 smallest eigenvalues, smallest first
-    double L[60], rho[6];
-    double be[3][4];
-    int valid[3];
+// Stage 1 -> stage 2 record (per problem; device memory between the GPU passes).
+struct EpnpStage1 {
+    EpnpFrame f;
+    double pairs[kEpnpPairSums];
+    double n;   // inlier count
+    double ok;  // 1: a frame exists (>= 4 inliers, non-degenerate)
 };
 
-// The serial middle of EPnP (leader thread): M^T M from the pair sums, its
-// eigenvectors, L and rho, the three beta estimates with Gauss-Newton.  Not
-// inlined on the GPU so its registers do not add to the O(n) sums'.
-RSAC_NOINLINE void epnp_serial(EpnpShared *sh, const double *pairs, const Cam &k, const EpnpFrame &f) {
+// Stage 2 -> stage 3 record: the serial middle's results.
+struct EpnpStage2 {
+    double ut[4][12];  // eigenvectors of M^T M's 4 smallest eigenvalues, smallest first
+    double be[3][4];   // betas of approximations 1, 2, 3 (after Gauss-Newton)
+    double valid[3];
+};
+
+// The serial middle's scratch.
+struct EpnpShared {
+    double A[144], V[144], d[12];
+    double L[60], rho[6];
+};
+
+// Stage 2, the serial middle of EPnP (O(1), on the host): M^T M from the pair
+// sums, its eigenvectors, L and rho, the three beta estimates with Gauss-Newton.
+RSAC_HD void epnp_mtm(EpnpShared *sh, const double *pairs, const Cam &k) {
     int q = 0;
     for (int i = 0; i < 4; ++i)
         for (int j = i; j < 4; ++j, q += 4) {
@@ -1047,12 +1076,20 @@ RSAC_NOINLINE void epnp_serial(EpnpShared *sh, const double *pairs, const Cam &k
                     sh->A[12 * (3 * j + r) + 3 * i + p] = blk[3 * p + r];
                 }
         }
+}
+
+inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, EpnpStage2 &s2) {
+    EpnpShared shm;
+    EpnpShared *sh = &shm;
+    const EpnpFrame &f = s1.f;
+    epnp_mtm(sh, s1.pairs, k);
     jacobi_eig<12>(sh->A, sh->V, sh->d);
+    int q = 0;
     int o[12];
     eig_order_desc<12>(sh->d, o);
     for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 12; ++j) sh->ut[i][j] = sh->V[12 * j + o[11 - i]];
-    const double *vv[4] = {sh->ut[0], sh->ut[1], sh->ut[2], sh->ut[3]};
+        for (int j = 0; j < 12; ++j) s2.ut[i][j] = sh->V[12 * j + o[11 - i]];
+    const double *vv[4] = {s2.ut[0], s2.ut[1], s2.ut[2], s2.ut[3]};
     epnp_l6x10(vv, sh->L);
     q = 0;
     for (int a = 0; a < 4; ++a)
@@ -1061,7 +1098,7 @@ RSAC_NOINLINE void epnp_serial(EpnpShared *sh, const double *pairs, const Cam &k
             sh->rho[q] = dx * dx + dy * dy + dz * dz;
         }
     for (int approx = 1; approx <= 3; ++approx) {
-        double *be = sh->be[approx - 1];
+        double *be = s2.be[approx - 1];
         for (int j = 0; j < 4; ++j) be[j] = 0.0;
         double b[6];
         for (int i = 0; i < 6; ++i) b[i] = sh->rho[i];
@@ -1107,26 +1144,30 @@ RSAC_NOINLINE void epnp_serial(EpnpShared *sh, const double *pairs, const Cam &k
             if (ok) be[2] = x[3] / be[0];
         }
         if (ok) epnp_gauss_newton(sh->L, sh->rho, be);
-        sh->valid[approx - 1] = ok;
+        s2.valid[approx - 1] = ok;
     }
     }
 
 // Red provides:
 //   template <int NV, class F> void sum(F f, double *out): out[q] = sum over the inliers of
 //     f(X, Y, Z, u, v, acc) (acc[NV]; coordinates in the centred frame), in the fixed order;
-//   bool first(double *p): the first inlier's centred coordinates;
-//   EpnpShared *shared(), bool leader(), void sync(): the serial part's scratch and barrier.
-// Every thread runs this function; values are block-uniform.  Returns false (pose
-// untouched) for < 4 inliers or a degenerate (e.g. planar) configuration.
+//   bool first(double *p): the first inlier's centred coordinates.
+// Every thread runs the stages; values are block-uniform.
+
+// Stage 1 (O(n) sums): the inlier count, centroid, principal axes -> control points and
+// the barycentric frame, the control-point pair sums of M^T M.  s1.ok = 0 for < 4 inliers or
+// a degenerate (e.g. planar) cloud.
 template <class Red>
-RSAC_HD bool pnp_epnp(Red &red, const Cam &k, double *R_out, double *t_out) {
+RSAC_HD void epnp_stage1(Red &red, const Cam &k, EpnpStage1 &s1) {
+    s1.ok = 0.0;
     double s4[4];
     red.template sum<4>([](double X, double Y, double Z, double, double, double *acc) {
         acc[0] += X; acc[1] += Y; acc[2] += Z; acc[3] += 1.0;
     }, s4);
     const double n = s4[3];
-    if (!(n >= 4.0)) return false;
-    EpnpFrame f;
+    s1.n = n;
+    if (!(n >= 4.0)) return;
+    EpnpFrame &f = s1.f;
     for (int j = 0; j < 3; ++j) f.cw[0][j] = s4[j] / n;
     const double c0x = f.cw[0][0], c0y = f.cw[0][1], c0z = f.cw[0][2];
     double cov[6];
@@ -1154,7 +1195,7 @@ RSAC_HD bool pnp_epnp(Red &red, const Cam &k, double *R_out, double *t_out) {
         const double det = cc[0] * m00 + cc[1] * m01 + cc[2] * m02;
         double nrm = 0.0;
         for (int q = 0; q < 9; ++q) nrm = nrm + cc[q] * cc[q];
-        if (!(dabs(det) > 1e-12 * nrm * dsqrt(nrm))) return false;  // planar / degenerate cloud
+        if (!(dabs(det) > 1e-12 * nrm * dsqrt(nrm))) return;  // planar / degenerate cloud
         const double id = 1.0 / det;
         f.ci[0] = m00 * id;
         f.ci[1] = (cc[2] * cc[7] - cc[1] * cc[8]) * id;
@@ -1168,40 +1209,40 @@ RSAC_HD bool pnp_epnp(Red &red, const Cam &k, double *R_out, double *t_out) {
     }
     // M^T M (12 x 12) = sum over points of kron(a a^T, G), G = m1 m1^T + m2 m2^T for the two rows
     // m1 = (fx, 0, cx - u), m2 = (0, fy, cy - v) of fill_M: per control-point pair (i <= j)
-    // the sums of a_i a_j times 1, (cx - u), (cy - v), (cx - u)^2 + (cy - v)^2
+    // the sums of a_i a_j times 1, (cx - u), (cy - v), (cx - u)^2 + (cy - v)^2; two passes of
+    // 5 pairs each (register pressure), each sum's order unchanged
     const EpnpAlpha af = epnp_alpha_frame(f);
-    double pairs[kEpnpPairSums];
-    red.template sum<kEpnpPairSums>([=](double X, double Y, double Z, double u, double v, double *acc) {
-        double a[4];
-        epnp_alphas(af, X, Y, Z, a);
-        const double du = k.cx - u, dv = k.cy - v, w = du * du + dv * dv;
-        int q = 0;
-        for (int i = 0; i < 4; ++i)
-            for (int j = i; j < 4; ++j, q += 4) {
-                const double aa = a[i] * a[j];
-                acc[q] += aa;
-                acc[q + 1] += aa * du;
-                acc[q + 2] += aa * dv;
-                acc[q + 3] += aa * w;
-            }
-    }, pairs);
-    EpnpShared *sh = red.shared();
-    if (red.leader()) epnp_serial(sh, pairs, k, f);
-    red.sync();
+    red.template sum<kEpnpPairSums / 2>([=](double X, double Y, double Z, double u, double v, double *acc) {
+        epnp_pair_acc<0>(af, k, X, Y, Z, u, v, acc);
+    }, s1.pairs);
+    red.template sum<kEpnpPairSums / 2>([=](double X, double Y, double Z, double u, double v, double *acc) {
+        epnp_pair_acc<1>(af, k, X, Y, Z, u, v, acc);
+    }, s1.pairs + kEpnpPairSums / 2);
+    s1.ok = 1.0;
+}
+
+// Stage 3 (O(n) sums): for each valid beta estimate, the camera-frame control points (sign from
+// the first inlier's depth), the pose by SVD of the centred cross-covariance, the mean
+// reprojection error; the lowest wins.  (R, t) in the centred frame; false if none.
+template <class Red>
+RSAC_HD bool epnp_stage3(Red &red, const Cam &k, const EpnpStage1 &s1, const EpnpStage2 &s2, double *R_out,
+                         double *t_out) {
+    const double n = s1.n;
+    const EpnpAlpha af = epnp_alpha_frame(s1.f);
+    const double c0x = s1.f.cw[0][0], c0y = s1.f.cw[0][1], c0z = s1.f.cw[0][2];
     double p1[3], a1[4];
     if (!red.first(p1)) return false;
     epnp_alphas(af, p1[0], p1[1], p1[2], a1);
     double best_err = 0.0, bestR[9], bestt[3];
     bool have = false;
     for (int approx = 0; approx < 3; ++approx) {
-        if (!sh->valid[approx]) continue;
-        const double *be = sh->be[approx];
-        // control points in the camera frame, the sign from the first inlier's depth
+        if (s2.valid[approx] == 0.0) continue;
+        const double *be = s2.be[approx];
         double cc[4][3];
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 3; ++j)
-                cc[i][j] = be[0] * sh->ut[0][3 * i + j] + be[1] * sh->ut[1][3 * i + j] +
-                           be[2] * sh->ut[2][3 * i + j] + be[3] * sh->ut[3][3 * i + j];
+                cc[i][j] = be[0] * s2.ut[0][3 * i + j] + be[1] * s2.ut[1][3 * i + j] + be[2] * s2.ut[2][3 * i + j] +
+                           be[3] * s2.ut[3][3 * i + j];
         const double z1 = a1[0] * cc[0][2] + a1[1] * cc[1][2] + a1[2] * cc[2][2] + a1[3] * cc[3][2];
         if (z1 < 0.0)
             for (int i = 0; i < 4; ++i)
@@ -1246,6 +1287,18 @@ RSAC_HD bool pnp_epnp(Red &red, const Cam &k, double *R_out, double *t_out) {
     for (int j = 0; j < 9; ++j) R_out[j] = bestR[j];
     for (int j = 0; j < 3; ++j) t_out[j] = bestt[j];
     return true;
+}
+
+// EPnP of one problem on the host: the three stages in a row (the GPU runs stages 1 and 3 as
+// kernels and stage 2 on the host, with the same functions).
+template <class Red>
+inline bool pnp_epnp(Red &red, const Cam &k, double *R_out, double *t_out) {
+    EpnpStage1 s1;
+    epnp_stage1(red, k, s1);
+    if (s1.ok == 0.0) return false;
+    EpnpStage2 s2;
+    epnp_stage2(s1, k, s2);
+    return epnp_stage3(red, k, s1, s2, R_out, t_out);
 }
 
 }  // namespace rsac
