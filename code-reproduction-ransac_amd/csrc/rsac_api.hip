@@ -110,6 +110,15 @@ struct PinBuf {
 
 constexpr size_t kMaxModelBytes = size_t(32) << 30;  // hypothesis records kept resident per call
 
+// hipMemcpy2DAsync, as one linear copy when the rows are contiguous (one problem): the 2-D path
+// costs tens of microseconds more per call on this runtime (measured in the adaptive loop)
+hipError_t copy_rows(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height,
+                     hipMemcpyKind kind, hipStream_t s) {
+    if (height == 1 || (dpitch == width && spitch == width))
+        return hipMemcpyAsync(dst, src, width * height, kind, s);
+    return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, kind, s);
+}
+
 }  // namespace
 
 struct rsac_ctx {
@@ -444,10 +453,10 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
                 mwc_subsets(rngs[p], np, Hr, model == Model::Hom ? hom : nullptr, hs + ((size_t)p * stride + hb) * 4,
                             os);
             });
-            HIPCHK(hipMemcpy2DAsync(c->subsets.as<int32_t>() + hb * 4, sizeof(int32_t) * 4 * stride, hs + hb * 4,
+            HIPCHK(copy_rows(c->subsets.as<int32_t>() + hb * 4, sizeof(int32_t) * 4 * stride, hs + hb * 4,
                                     sizeof(int32_t) * 4 * stride, sizeof(int32_t) * 4 * Hr, P, hipMemcpyHostToDevice,
                                     s));
-            HIPCHK(hipMemcpy2DAsync(c->substatus.as<int8_t>() + hb, stride, hss + hb, stride, Hr, P,
+            HIPCHK(copy_rows(c->substatus.as<int8_t>() + hb, stride, hss + hb, stride, Hr, P,
                                     hipMemcpyHostToDevice, s));
         }
         HIPCHK(hipEventRecord(c->ev0, s));
@@ -465,9 +474,9 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
             HIPCHK(launch_hom_score(*ha, P, hb, Hr, c->counts.as<int32_t>(), s));
         }
         HIPCHK(hipEventRecord(c->ev2, s));
-        HIPCHK(hipMemcpy2DAsync(c->h_counts.p, sizeof(int32_t) * Hr, c->counts.as<int32_t>() + hb,
+        HIPCHK(copy_rows(c->h_counts.p, sizeof(int32_t) * Hr, c->counts.as<int32_t>() + hb,
                                 sizeof(int32_t) * stride, sizeof(int32_t) * Hr, P, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpy2DAsync(c->h_status.p, Hr, c->status.as<int8_t>() + hb, stride, Hr, P,
+        HIPCHK(copy_rows(c->h_status.p, Hr, c->status.as<int8_t>() + hb, stride, Hr, P,
                                 hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
@@ -501,13 +510,17 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
 }
 
 // masks + winning models of every problem; records of winners -> c->best
+// defer_sync: leave the stream running (the caller enqueues more work, synchronises, then
+// calls finish_masks_host to copy a host mask out)
 int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const LoopOut &lo, int64_t stride,
-                 uint8_t *mask_out, uint32_t flags, hipStream_t s) {
+                 uint8_t *mask_out, uint32_t flags, hipStream_t s, bool defer_sync = false) {
     const int P = st.P;
     int64_t *hb = c->h_best.as<int64_t>();
     for (int p = 0; p < P; ++p) hb[p] = lo.scan[p].best >= 0 ? (int64_t)p * stride + lo.scan[p].best : -1;
-    HIPCHK(hipMemcpyAsync(c->best.p, hb, sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
-    HIPCHK(launch_gather_models(c->models.as<double>(), c->best.as<int64_t>(), P, c->bestmodels.as<double>(), s));
+    // one problem: the record index goes as a kernel argument (no upload)
+    const int64_t *dbest = P == 1 ? nullptr : c->best.as<int64_t>();
+    if (P > 1) HIPCHK(hipMemcpyAsync(c->best.p, hb, sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_gather_models(c->models.as<double>(), dbest, P, c->bestmodels.as<double>(), s, hb[0]));
     HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
                           hipMemcpyDeviceToHost, s));
     int32_t max_n = 0;
@@ -522,21 +535,27 @@ int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const L
     }
     if (N > 0) {
         if (model == Model::PnP)
-            HIPCHK(launch_pnp_mask(*(PnpArgs *)args, P, max_n, c->best.as<int64_t>(), dmask, s));
+            HIPCHK(launch_pnp_mask(*(PnpArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
         else if (model == Model::Fm)
-            HIPCHK(launch_fm_mask(*(HomArgs *)args, P, max_n, c->best.as<int64_t>(), dmask, s));
+            HIPCHK(launch_fm_mask(*(HomArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
         else
-            HIPCHK(launch_hom_mask(*(HomArgs *)args, P, max_n, c->best.as<int64_t>(), dmask, s));
+            HIPCHK(launch_hom_mask(*(HomArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
     }
     if (!(flags & RSAC_F_DEVICE_OUT) && mask_out && N > 0) {
         HIPCHK(c->h_mask.ensure(N));
         HIPCHK(hipMemcpyAsync(c->h_mask.p, dmask, N, hipMemcpyDeviceToHost, s));
+        if (defer_sync) return RSAC_OK;
         HIPCHK(hipStreamSynchronize(s));
         memcpy(mask_out, c->h_mask.p, N);
-    } else {
+    } else if (!defer_sync) {
         HIPCHK(hipStreamSynchronize(s));
     }
     return RSAC_OK;
+}
+
+// after a deferred finish_masks and a stream synchronisation: the host mask copy-out
+void finish_masks_host(rsac_ctx *c, const Staged &st, uint8_t *mask_out, uint32_t flags) {
+    if (!(flags & RSAC_F_DEVICE_OUT) && mask_out && st.total > 0) memcpy(mask_out, c->h_mask.p, st.total);
 }
 
 int check_device(rsac_ctx *c) {
@@ -581,9 +600,10 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     LoopOut lo;
     r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo);
     if (r) return r;
-    r = finish_masks(c, Model::PnP, st, &a, lo, stride, mask_out, flags, s);
+    const bool refit = (flags & (RSAC_F_REFINE | RSAC_F_EPNP)) != 0;
+    r = finish_masks(c, Model::PnP, st, &a, lo, stride, mask_out, flags, s, refit);
     if (r) return r;
-    if (flags & (RSAC_F_REFINE | RSAC_F_EPNP)) {
+    if (refit) {
         // final solve on the device, one block per problem, on the RANSAC-phase inliers:
         // EPnP (solvePnPRansac with SOLVEPNP_P3P), then / or LM (solvePnPRefineLM)
         const uint8_t *dmask = (flags & RSAC_F_DEVICE_OUT) && mask_out ? mask_out : c->mask.as<uint8_t>();
@@ -610,6 +630,7 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
                               hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        finish_masks_host(c, st, mask_out, flags);
     }
     const double *bm = c->h_bestmodels.as<double>();
     for (int p = 0; p < P; ++p) {

@@ -84,7 +84,9 @@ hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t 
                            unsigned long long *key, const double *models, double *model_out, hipStream_t s);
 
 // copy model records rec[p] (<0: zero) into out[p][16]
-hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s);
+// rec (device, P entries) or, with rec == nullptr, rec0 for the one problem
+hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s,
+                                int64_t rec0 = -1);
 
 // frame of every problem (centre, bounds, f32 constants) + centred coords;
 // also resets a.best_key (if set) and a.queue.  bounds_ws: P x 10 ints.
@@ -102,18 +104,18 @@ void set_score_variant(int v);  // tuning knob (rsac_set_score_variant)
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                           hipStream_t s);
+                           hipStream_t s, int64_t best0 = -1);
 hipError_t launch_hom_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
 hipError_t launch_hom_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
 hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                           hipStream_t s);
+                           hipStream_t s, int64_t best0 = -1);
 
 // fundamental matrix (8-point + Sampson) on the homography argument block
 hipError_t launch_fm_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
 hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s);
 hipError_t launch_fm_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                          hipStream_t s);
+                          hipStream_t s, int64_t best0 = -1);
 
 // LM refit of every problem's model record (models: P x kModelStride, R 9, t 3, valid)
 // on the inliers of mask (concatenated points), one block per problem

@@ -487,16 +487,22 @@ __device__ __forceinline__ int ab_fallback(const PnpArgs &a, int prob, int64_t p
     return cnt;
 }
 
+// split > 1 (small rounds, no fused best key): a unit is (problem, hypothesis tile, point
+// chunk) and the chunk's counts are atomically added into zeroed counts -- enough units to
+// fill the GPU when a round has only a few tiles (an adaptive run's first 256 hypotheses).
 template <int P, int HB, int W = 4>  // W: minimum waves per SIMD the register budget must allow
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_ab(
-    PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts) {
+    PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
+    int split) {
     static_assert(HB <= 32, "undecided bits per lane");
+    constexpr int kStride = 4 * 64 * P;  // points one pass of the block covers
     __shared__ int red[4][HB];
     __shared__ int unit_s;
     __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int units_per_prob = (H + HB - 1) / HB;
+    const int tiles_per_prob = (H + HB - 1) / HB;
+    const int units_per_prob = tiles_per_prob * split;
     const int n_units = units_per_prob * n_prob;
     for (;;) {
         if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
@@ -504,10 +510,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         const int unit = __builtin_amdgcn_readfirstlane(unit_s);
         if (unit >= n_units) break;  // uniform: every wave of every block reaches it
         const int prob = unit / units_per_prob;
-        const int64_t h0 = hyp_begin + (int64_t)(unit % units_per_prob) * HB;
+        const int rem = unit % units_per_prob;
+        const int chunk = rem % split;
+        const int64_t h0 = hyp_begin + (int64_t)(rem / split) * HB;
         const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
         const int64_t p0 = a.offsets[prob];
-        const int n = (int)(a.offsets[prob + 1] - p0);
+        const int n_all = (int)(a.offsets[prob + 1] - p0);
+        const int clen = ((n_all + split - 1) / split + kStride - 1) / kStride * kStride;
+        const int start = chunk * clen;
+        const int n = min(n_all, start + clen);  // this unit's points: [start, n)
         const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
         const float cx = fc[2], cy = fc[3], T = fc[4];
         const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
@@ -539,7 +550,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
 
         int cnt = 0;
-        for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
+        for (int base = start + wave * 64 * P; base < n; base += kStride) {
             float px[P], py[P], pz[P], pu[P], pv[P];
 #pragma unroll
             for (int j = 0; j < P; ++j) {
@@ -579,7 +590,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         }
         if (lane < HB) red[wave][lane] = cnt;
         __syncthreads();
-        if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
+        if (split == 1) {
+            if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
+        } else if (wave == 0 && lane < nh) {
+            const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+            if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
+        }
         __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
     }
 }
@@ -915,11 +931,11 @@ __global__ __launch_bounds__(256) void k_pnp_score(PnpArgs a, int64_t hyp_begin,
 }
 
 // mask of one model per problem (best[prob] indexes the models buffer; <0 = none)
-__global__ void k_pnp_mask(PnpArgs a, const int64_t *__restrict__ best, uint8_t *__restrict__ mask) {
+__global__ void k_pnp_mask(PnpArgs a, const int64_t *__restrict__ best, int64_t best0, uint8_t *__restrict__ mask) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
-    const int64_t b = best[prob];
+    const int64_t b = best ? best[prob] : best0;  // best0: the one problem's record, no upload
     const double *c = a.cams + 4 * prob;
     const Cam k{c[0], c[1], c[2], c[3]};
     const float thr2 = a.thr2[prob];
@@ -1154,11 +1170,11 @@ __global__ __launch_bounds__(256) void k_pnp_score_lane(PnpArgs a, int64_t hyp_b
     }
 }
 
-__global__ void k_hom_mask(HomArgs a, const int64_t *__restrict__ best, uint8_t *__restrict__ mask) {
+__global__ void k_hom_mask(HomArgs a, const int64_t *__restrict__ best, int64_t best0, uint8_t *__restrict__ mask) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
-    const int64_t b = best[prob];
+    const int64_t b = best ? best[prob] : best0;  // best0: the one problem's record, no upload
     const float thr2 = a.thr2[prob];
     float hf[8];
     if (b >= 0) {
@@ -1174,12 +1190,12 @@ __global__ void k_hom_mask(HomArgs a, const int64_t *__restrict__ best, uint8_t 
     }
 }
 
-__global__ void k_gather_models(const double *__restrict__ models, const int64_t *__restrict__ rec, int32_t P,
-                                double *__restrict__ out) {
+__global__ void k_gather_models(const double *__restrict__ models, const int64_t *__restrict__ rec, int64_t rec0,
+                                int32_t P, double *__restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P * kModelStride) return;
     const int p = i / kModelStride, q = i % kModelStride;
-    const int64_t r = rec[p];
+    const int64_t r = rec ? rec[p] : rec0;
     out[i] = r >= 0 ? models[r * kModelStride + q] : 0.0;
 }
 
@@ -1286,9 +1302,24 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
         resident = std::max(1, cus) * std::max(1, per_cu);
     }
-    const int64_t units = (int64_t)P * ((H + HB - 1) / HB);
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, a.queue, counts);
+    int64_t units = (int64_t)P * ((H + HB - 1) / HB);
+    if constexpr (KIND == 3) {
+        // few tiles and no fused best key: split the points too (counts accumulate atomically)
+        int split = 1;
+        const int64_t chunks = std::max<int64_t>(1, ((int64_t)a.max_n + 4 * 64 * PP - 1) / (4 * 64 * PP));
+        if (!a.best_key && units * 2 <= resident)
+            split = (int)std::min<int64_t>(chunks, (resident + units - 1) / units);
+        if (split > 1 && P == 1)
+            (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
+        else if (split > 1)
+            (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P, s);
+        units *= split;
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, a.queue, counts, split);
+    } else {
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, a.queue, counts);
+    }
 }
 
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
@@ -1330,10 +1361,10 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                           hipStream_t s) {
+                           hipStream_t s, int64_t best0) {
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g > 1024) g = 1024;
-    hipLaunchKernelGGL(k_pnp_mask, dim3(g, P), dim3(256), 0, s, a, best, mask);
+    hipLaunchKernelGGL(k_pnp_mask, dim3(g, P), dim3(256), 0, s, a, best, best0, mask);
     return hipGetLastError();
 }
 
@@ -1353,15 +1384,16 @@ hipError_t launch_hom_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                           hipStream_t s) {
+                           hipStream_t s, int64_t best0) {
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g > 1024) g = 1024;
-    hipLaunchKernelGGL(k_hom_mask, dim3(g, P), dim3(256), 0, s, a, best, mask);
+    hipLaunchKernelGGL(k_hom_mask, dim3(g, P), dim3(256), 0, s, a, best, best0, mask);
     return hipGetLastError();
 }
 
-hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_gather_models, dim3(cdiv((int64_t)P * kModelStride, 256)), dim3(256), 0, s, models, rec, P,
+hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s,
+                                int64_t rec0) {
+    hipLaunchKernelGGL(k_gather_models, dim3(cdiv((int64_t)P * kModelStride, 256)), dim3(256), 0, s, models, rec, rec0, P,
                        out);
     return hipGetLastError();
 }
@@ -1837,11 +1869,11 @@ __global__ __launch_bounds__(256) void k_fm_score_lane(HomArgs a, int64_t hyp_be
     counts[rec] = cnt;
 }
 
-__global__ void k_fm_mask(HomArgs a, const int64_t *__restrict__ best, uint8_t *__restrict__ mask) {
+__global__ void k_fm_mask(HomArgs a, const int64_t *__restrict__ best, int64_t best0, uint8_t *__restrict__ mask) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
-    const int64_t b = best[prob];
+    const int64_t b = best ? best[prob] : best0;  // best0: the one problem's record, no upload
     const double T = (double)a.thr2[prob];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int64_t q = p0 + i;
@@ -1863,10 +1895,10 @@ hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32
 }
 
 hipError_t launch_fm_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                          hipStream_t s) {
+                          hipStream_t s, int64_t best0) {
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g > 1024) g = 1024;
-    hipLaunchKernelGGL(k_fm_mask, dim3(g, P), dim3(256), 0, s, a, best, mask);
+    hipLaunchKernelGGL(k_fm_mask, dim3(g, P), dim3(256), 0, s, a, best, best0, mask);
     return hipGetLastError();
 }
 
