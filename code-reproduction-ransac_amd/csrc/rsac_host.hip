@@ -131,6 +131,7 @@ struct HostLmReducer {
     Cam k;
     double c[3];  // centre of the refit frame
     std::vector<double> part = std::vector<double>((size_t)kLmThreads * kLmTerms);
+    void mark(int) {}
     void normal(const double *R, const double *t, double *acc) {
         lm_reduce_host(n, mask, kLmTerms, part.data(), acc, [&](int i, double *a) {
             pnp_lm_point(R, t, k, (double)X[i] - c[0], (double)Y[i] - c[1], (double)Z[i] - c[2], (double)U[i],

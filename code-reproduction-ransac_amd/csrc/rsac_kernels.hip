@@ -1538,10 +1538,12 @@ struct GpuLmReducer {
 
     __device__ void reduce(double *a, int nv, double *out) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        for (int q = 0; q < nv; ++q) {
-            for (int o = 32; o > 0; o >>= 1) a[q] = a[q] + __shfl_xor(a[q], o);
-            if (lane == 0) wsum[wave][q] = a[q];
-        }
+        // levels outside, terms inside: the nv butterflies are independent, so their shuffles
+        // overlap (each term's additions are the same as term by term)
+        for (int o = 32; o > 0; o >>= 1)
+            for (int q = 0; q < nv; ++q) a[q] = a[q] + __shfl_xor(a[q], o);
+        if (lane == 0)
+            for (int q = 0; q < nv; ++q) wsum[wave][q] = a[q];
         __syncthreads();
         for (int q = 0; q < nv; ++q) {
             double s = wsum[0][q];
@@ -1553,14 +1555,36 @@ struct GpuLmReducer {
     __device__ void normal(const double *R, const double *t, double *acc) {
         double a[kLmTerms];
         for (int q = 0; q < kLmTerms; ++q) a[q] = 0.0;
+#pragma unroll 4
         for (int i = threadIdx.x; i < n; i += kLmThreads)
             if (mask[i])
                 pnp_lm_point(R, t, k, (double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i],
                              (double)V[i], a);
+#ifdef RSAC_TRACE
+        mark(20);
+#endif
         reduce(a, kLmTerms, acc);
     }
+#ifdef RSAC_TRACE
+    unsigned long long stamp[48];
+    int phase_of[48];
+    int ns = 0;
+    __device__ void mark(int phase) {
+        __syncthreads();
+        if (ns < 48) {
+            stamp[ns] = __builtin_amdgcn_s_memrealtime();
+            phase_of[ns++] = phase;
+        }
+    }
+    __device__ void dump() {
+        if (threadIdx.x == 0 && blockIdx.x == 0)
+            for (int i = 1; i < ns; ++i)
+                printf("trace %d->%d %llu ticks\n", phase_of[i - 1], phase_of[i], stamp[i] - stamp[i - 1]);
+    }
+#endif
     __device__ double cost(const double *R, const double *t) {
         double a = 0.0, out;
+#pragma unroll 4
         for (int i = threadIdx.x; i < n; i += kLmThreads)
             if (mask[i])
                 a += pnp_lm_cost_point(R, t, k, (double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i],
@@ -1589,6 +1613,10 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     for (int j = 0; j < 3; ++j) t[j] = m[9 + j];
     lm_to_centred(R, c, t);
     const int it = pnp_lm_refine(red, R, t, kLmMaxIter);
+#ifdef RSAC_TRACE
+    red.mark(99);
+    red.dump();
+#endif
     lm_from_centred(R, c, t);
     __syncthreads();  // every thread has read m before thread 0 overwrites it
     if (threadIdx.x == 0) {

@@ -16,6 +16,12 @@
 
 #define RSAC_HD __host__ __device__ __forceinline__
 #define RSAC_NOINLINE __host__ __device__ __attribute__((noinline)) inline
+// phase timestamps of block 0 (timing builds: -DRSAC_TRACE, scripts/trace_build.sh)
+#ifdef RSAC_TRACE
+#define RSAC_TRACE_MARK(red, phase) (red).mark(phase)
+#else
+#define RSAC_TRACE_MARK(red, phase) ((void)0)
+#endif
 
 namespace rsac {
 
@@ -685,10 +691,14 @@ RSAC_HD double pnp_lm_cost_point(const double *R, const double *t, const Cam &k,
     return ru * ru + rv * rv;
 }
 
-// (A + lam diag(A)) x = b, A 6 x 6 SPD row-major; false if not positive definite
+// (A + lam diag(A)) x = b, A 6 x 6 SPD row-major; false if not positive definite.
+// Divisions by the pivots are multiplications by their reciprocals (6 divisions, not 33:
+// the GPU refit runs this on every thread of the block, between two reductions).
 RSAC_HD bool chol6_solve(const double *A, double lam, const double *b, double *x) {
-    double L[36], y[6];
+    double L[36], y[6], inv[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i)
+#pragma unroll
         for (int j = 0; j <= i; ++j) {
             double s = A[i * 6 + j];
             if (i == j) s = s + lam * A[i * 6 + i];
@@ -696,19 +706,22 @@ RSAC_HD bool chol6_solve(const double *A, double lam, const double *b, double *x
             if (i == j) {
                 if (!(s > 0)) return false;
                 L[i * 6 + i] = dsqrt(s);
+                inv[i] = 1.0 / L[i * 6 + i];
             } else {
-                L[i * 6 + j] = s / L[j * 6 + j];
+                L[i * 6 + j] = s * inv[j];
             }
         }
+#pragma unroll
     for (int i = 0; i < 6; ++i) {
         double s = b[i];
         for (int q = 0; q < i; ++q) s = s - L[i * 6 + q] * y[q];
-        y[i] = s / L[i * 6 + i];
+        y[i] = s * inv[i];
     }
+#pragma unroll
     for (int i = 5; i >= 0; --i) {
         double s = y[i];
         for (int q = i + 1; q < 6; ++q) s = s - L[q * 6 + i] * x[q];
-        x[i] = s / L[i * 6 + i];
+        x[i] = s * inv[i];
     }
     return true;
 }
@@ -732,11 +745,14 @@ RSAC_HD void cayley_apply(const double *d, const double *R, double *Rn) {
 template <class Red>
 RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
     double lam = 1e-3;
+    RSAC_TRACE_MARK(red, 10);
     double cost = red.cost(R, t);
+    RSAC_TRACE_MARK(red, 11);
     int it;
     for (it = 0; it < max_iter; ++it) {
         double acc[kLmTerms];
         red.normal(R, t, acc);
+        RSAC_TRACE_MARK(red, 12);
         double A[36], g[6];
         int q = 0;
         for (int a = 0; a < 6; ++a)
@@ -753,7 +769,9 @@ RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
             double Rn[9], tn[3];
             cayley_apply(d, R, Rn);
             for (int j = 0; j < 3; ++j) tn[j] = t[j] + d[3 + j];
+            RSAC_TRACE_MARK(red, 13);
             const double cn = red.cost(Rn, tn);
+            RSAC_TRACE_MARK(red, 14);
             if (cn < cost) {
                 const double rel = (cost - cn) / (cost > 1e-300 ? cost : 1e-300);
                 for (int j = 0; j < 9; ++j) R[j] = Rn[j];

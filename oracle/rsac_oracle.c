@@ -1049,9 +1049,10 @@ static void lm_reduce(lmctx *c, const double *R, const double *t, int nv, double
     }
 }
 
-/* (A + lam diag(A)) x = b, A 6x6 SPD, Cholesky */
+/* (A + lam diag(A)) x = b, A 6x6 SPD, Cholesky; divisions by a pivot are multiplications
+ * by its reciprocal */
 static int chol6(const double *A, double lam, const double *b, double *x) {
-    double L[36], y[6];
+    double L[36], y[6], inv[6];
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j <= i; ++j) {
             double s = A[i * 6 + j];
@@ -1060,19 +1061,20 @@ static int chol6(const double *A, double lam, const double *b, double *x) {
             if (i == j) {
                 if (!(s > 0)) return 0;
                 L[i * 6 + i] = sqrt(s);
+                inv[i] = 1.0 / L[i * 6 + i];
             } else {
-                L[i * 6 + j] = s / L[j * 6 + j];
+                L[i * 6 + j] = s * inv[j];
             }
         }
     for (int i = 0; i < 6; ++i) {
         double s = b[i];
         for (int k = 0; k < i; ++k) s = s - L[i * 6 + k] * y[k];
-        y[i] = s / L[i * 6 + i];
+        y[i] = s * inv[i];
     }
     for (int i = 5; i >= 0; --i) {
         double s = y[i];
         for (int k = i + 1; k < 6; ++k) s = s - L[k * 6 + i] * x[k];
-        x[i] = s / L[i * 6 + i];
+        x[i] = s * inv[i];
     }
     return 1;
 }
