@@ -37,6 +37,15 @@ struct PnpArgs {
     const double *frame;  // P x kFrameStride: c0 c1 c2 B rho cmax wmax
     const float *fconst;  // P x kFconstStride
     float *fmodels;       // P x hyp_stride x kFModelStride
+    // MFMA scoring kernel (k_pnp_score_mx): f16 hi/lo point features (8 x f16 per point,
+    // built by k_pnp_center) and per-hypothesis MFMA records (kHModelStride floats);
+    // both nullptr unless an MFMA scoring variant is selected
+    const uint4 *PF;
+    float *hmodels;
+    struct MxUndecided *mx_list;   // tiles with undecided pairs, recounted by k_pnp_mx_fallback
+    int *mx_count;                 // records written (reset by the solve / fmodels kernels)
+    int mx_cap;
+    unsigned long long *mx_stats;  // diagnostics (RSAC_MX_STATS=1): fallback tiles, undecided pairs
     int exact_only;
     // optional fused reduction (single problem): max over the scored hypotheses of
     // (count << 32) | (0xFFFFFFFF - low32(rng_base + h)), atomically into *best_key
@@ -48,6 +57,17 @@ struct PnpArgs {
 constexpr int kFrameStride = 8;
 constexpr int kFconstStride = 16;
 constexpr int kFModelStride = 16;
+constexpr int kHModelStride = 32;
+constexpr int kMxMasks = 16;  // undecided masks per record: NT x 4 (NT <= 4)
+
+// one wave-tile of k_pnp_score_mx with undecided pairs: hypotheses rec + [0, nh) (the wave's),
+// points base + (lane & 31) (< n), mask m[4t + j]: lanes whose pair with hypothesis 8t + 2j +
+// (lane >> 5) is undecided
+struct MxUndecided {
+    int64_t rec;
+    int32_t prob, base, n, nh;
+    uint64_t m[kMxMasks];
+};
 
 struct HomArgs {
     const float *SX, *SY, *DX, *DY;
@@ -91,7 +111,7 @@ hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_
 // frame of every problem (centre, bounds, f32 constants) + centred coords;
 // also resets a.best_key (if set) and a.queue.  bounds_ws: P x 10 ints.
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *bounds_ws, float *XC, float *YC,
-                            float *ZC, double *frame, float *fconst, hipStream_t s);
+                            float *ZC, double *frame, float *fconst, hipStream_t s, uint4 *PF = nullptr);
 // f32 records for H given f64 models (rsac_score_poses / rsac_pnp_mask)
 hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_t s);
 hipError_t launch_pnp_prepare(const double *p3, const double *p2, int64_t n, float *X, float *Y, float *Z, float *U,
@@ -101,6 +121,7 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 // solve / score hypotheses [hyp_begin, hyp_begin + H) of every problem
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
 void set_score_variant(int v);  // tuning knob (rsac_set_score_variant)
+bool score_variant_mx();        // the selected variant is an MFMA one (needs PF + hmodels)
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,

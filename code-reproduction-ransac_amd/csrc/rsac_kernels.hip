@@ -18,7 +18,10 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <utility>
+#include <vector>
 
 #include "rsac_geo.h"
 #include "rsac_internal.h"
@@ -102,6 +105,62 @@ __global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *_
     }
 }
 
+// f16 hi + lo operands of the MFMA scoring path (write_hmodel has the error model)
+constexpr double kMxF1 = 4096.0;               // the constant feature (exact in f16)
+constexpr double kMxEps = 3.814697265625e-06;  // 2^-18
+constexpr float kMxFlush = 6.103515625e-05f;   // 2^-14, smallest normal f16
+
+// scale of the z row, fz = 2^k with fz <= fx < 2 fz: the three rows (-fx R0, -fy R1, fz R2) then
+// share one magnitude, so one per-hypothesis scale fits all of them into f16 (fconst[8] = 1 / fz
+// rescales the pixel offsets: q1 = (uc / fz) (fz z) + xs, all powers of 2, bit-identical rounding)
+__host__ __device__ __forceinline__ double mx_zscale(double fx) {
+    int e = 0;
+    (void)frexp(fx > 0 ? fx : 1.0, &e);
+    return ldexp(1.0, e - 1);
+}
+
+// feature scale fs = 2^-b with B fs < 2^13 (B bounds |XC|)
+__host__ __device__ __forceinline__ double mx_feature_scale(double B) {
+    int e = 0;
+    (void)frexp(B > 0 ? B : 1.0, &e);  // B < 2^e
+    return ldexp(1.0, 13 - e);
+}
+
+__device__ __forceinline__ void mx_split(float v, _Float16 &hi, _Float16 &lo) {
+    if (!(__builtin_fabsf(v) >= kMxFlush)) {  // tiny (or NaN: the caller never passes one)
+        hi = (_Float16)0.f;
+        lo = (_Float16)0.f;
+        return;
+    }
+    hi = (_Float16)v;
+    const float r = v - (float)hi;  // exact
+    lo = __builtin_fabsf(r) >= kMxFlush ? (_Float16)r : (_Float16)0.f;
+}
+
+// B-operand column of a point: Xh Yh Zh F1 Xl Yl Zl 0 (both lane halves read the same 16 B)
+__device__ __forceinline__ uint4 mx_point_features(float x, float y, float z) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    h8 f;
+    _Float16 hi, lo;
+    mx_split(x, hi, lo); f[0] = hi; f[4] = lo;
+    mx_split(y, hi, lo); f[1] = hi; f[5] = lo;
+    mx_split(z, hi, lo); f[2] = hi; f[6] = lo;
+    f[3] = (_Float16)(float)kMxF1;
+    f[7] = (_Float16)0.f;
+    return __builtin_bit_cast(uint4, f);
+}
+
+// B >= |XC|inf of problem prob (the frame's f[3]; recomputed identically wherever needed)
+__device__ __forceinline__ double frame_bound(const int *__restrict__ ws, int32_t P, int prob, int n) {
+    double B = 0;
+    if (n > 0)
+        for (int k = 0; k < 3; ++k) {
+            const double lo = ord2f(ws[5 * prob + k]), hi = ord2f(ws[5 * P + 5 * prob + k]);
+            B = fmax(B, (hi - lo) * 0.5);
+        }
+    return B * (1.0 + 4.0 * kU32) + 1e-30;
+}
+
 // Per problem: frame = {c0 c1 c2 (bbox centre), B >= |XC|inf, rho >= |XC - (Xf - c)|,
 // max|Xf|, wmax (bound on |x/z| of any projection within thr of a pixel), 0};
 // fconst = {fx fy cx cy T 2.002 sqrt(T) 1e-6 T thr 2/fx 2/fy cu cv cc0} (see the scoring kernel).
@@ -112,17 +171,13 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
     const double fx = fabs(cm[0]), fy = fabs(cm[1]), cx = cm[2], cy = cm[3];
     const double T = a.thr2[prob];
     const double thr = sqrt(T);
-    double c[3] = {0, 0, 0}, B = 0, du = 0, dv = 0;
+    double c[3] = {0, 0, 0}, du = 0, dv = 0;
     if (n > 0) {
-        for (int k = 0; k < 3; ++k) {
-            const double lo = ord2f(ws[5 * prob + k]), hi = ord2f(ws[5 * P + 5 * prob + k]);
-            c[k] = (lo + hi) * 0.5;
-            B = fmax(B, (hi - lo) * 0.5);
-        }
+        for (int k = 0; k < 3; ++k) c[k] = ((double)ord2f(ws[5 * prob + k]) + (double)ord2f(ws[5 * P + 5 * prob + k])) * 0.5;
         du = fmax(fabs(ord2f(ws[5 * prob + 3]) - cx), fabs(ord2f(ws[5 * P + 5 * prob + 3]) - cx));
         dv = fmax(fabs(ord2f(ws[5 * prob + 4]) - cy), fabs(ord2f(ws[5 * P + 5 * prob + 4]) - cy));
     }
-    B = B * (1.0 + 4.0 * kU32) + 1e-30;
+    const double B = frame_bound(ws, P, prob, n);
     double *f = frame + (int64_t)prob * kFrameStride;
     f[0] = c[0]; f[1] = c[1]; f[2] = c[2];
     f[3] = B;
@@ -137,7 +192,8 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
     q[6] = (float)(4e-6 * T + 1e-30);
     // Cmax >= C_i = 2.5u (|u_i - cx| + |v_i - cy| + |cx| + |cy| + 2 thr + 2), the rounding part of D
     q[7] = (float)(2.5 * kU32 * (du + dv + fabs(cx) + fabs(cy) + 2.0 * thr + 3.0) + 1e-6);
-    q[8] = q[9] = q[10] = q[11] = q[12] = 0.f;
+    q[8] = (float)(1.0 / mx_zscale(fx));  // the MFMA kernel's pixel-offset scale
+    q[9] = q[10] = q[11] = q[12] = 0.f;
     for (int k = 13; k < kFconstStride; ++k) q[k] = 0.f;
 }
 
@@ -147,7 +203,7 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
 __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const int *__restrict__ ws,
                                                     double *__restrict__ frame, float *__restrict__ fconst,
                                                     float *__restrict__ XC, float *__restrict__ YC,
-                                                    float *__restrict__ ZC) {
+                                                    float *__restrict__ ZC, uint4 *__restrict__ PF) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
@@ -157,12 +213,48 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const 
         for (int k = 0; k < 3; ++k)
             cc[k] = ((double)ord2f(ws[5 * prob + k]) + (double)ord2f(ws[5 * P + 5 * prob + k])) * 0.5;
     const double c0 = cc[0], c1 = cc[1], c2 = cc[2];
+    const float fs = PF ? (float)mx_feature_scale(frame_bound(ws, P, prob, n)) : 0.f;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int64_t q = p0 + i;
-        XC[q] = (float)((double)a.X[q] - c0);
-        YC[q] = (float)((double)a.Y[q] - c1);
-        ZC[q] = (float)((double)a.Z[q] - c2);
+        const float xc = (float)((double)a.X[q] - c0), yc = (float)((double)a.Y[q] - c1),
+                    zc = (float)((double)a.Z[q] - c2);
+        XC[q] = xc;
+        YC[q] = yc;
+        ZC[q] = zc;
+        if (PF) PF[q] = mx_point_features(xc * fs, yc * fs, zc * fs);  // power-of-2 scale: exact
     }
+}
+
+// Band of the division-free test from the evaluation error bounds eps (ex, ey, ez: DESIGN.md
+// "Scoring"); tz = the hypothesis' depth of the centre (any w > 0 is valid for the majorant).
+struct BandConsts {
+    double D0, beta, zg, alpha;
+};
+
+__device__ __forceinline__ BandConsts band_consts(const double (&eps)[3], double fx, double fy, double wmax, double tz,
+                                                  const float *fconst) {
+    BandConsts b;
+    // Dz0 = 1.01 (fx ex + fy ey + ez Wmax), Wmax = (fx + fy) wmax >= fx wa_i + fy wb_i of any point
+    b.D0 = 1.01 * (fx * eps[0] + fy * eps[1] + eps[2] * (fx + fy) * wmax);
+    // |z'| above zg keeps |x'/z' - x/z| <= 0.01 for every projection the bound is used on
+    b.zg = 100.0 * (fmax(eps[0], eps[1]) + wmax * eps[2]) + 2.02 * eps[2] + 1e-30;
+    // Mz = (sqT2 |z| + Dz) Dz + Trel z^2 with Dz = D0 + Cmax |z| is at most alpha z^2 + beta:
+    // |z| <= z^2 / (2w) + w / 2 for any w > 0 (taken as the hypothesis' depth of the centre).
+    const double sqT2 = fconst[5], Trel = fconst[6], Cmax = fconst[7];
+    const double Bc = sqT2 * b.D0 + 2.0 * b.D0 * Cmax;
+    const double w = fmax(fabs(tz), 1.0);
+    b.beta = 1.01 * (b.D0 * b.D0 + Bc * w * 0.5);
+    b.alpha = 1.01 * (sqT2 * Cmax + Cmax * Cmax + Trel + Bc / (2.0 * w));
+    // beta >= K and beta >= (T - alpha) zg^2 make the depth guard redundant (k_pnp_score_mx
+    // has none): E < lo then implies |z'| > zg, and for |z'| <= zg, E > hi >= K means
+    // |q| >= sqrt(E') - delta > sqrt(T) (zg + ez) >= sqrt(T) |z| (delta = D0 + Cmax (zg + ez)
+    // bounds |q' - q|, L1): the pair's reprojection distance exceeds thr, an outlier
+    const double T = fconst[4], ez = eps[2];
+    const double zr = b.zg + ez;
+    const double K = (1.0 + 1e-6) * (b.D0 + Cmax * zr + sqrt(T * 1.00001) * zr) * (b.D0 + Cmax * zr + sqrt(T * 1.00001) * zr);
+    b.beta = fmax(b.beta, K);
+    if (T > b.alpha) b.beta = fmax(b.beta, (T - b.alpha) * b.zg * b.zg * (1.0 + 1e-6));
+    return b;
 }
 
 // float32 record of one pose, division-free form of the test:
@@ -191,29 +283,118 @@ __device__ __forceinline__ void write_fmodel(const double *R, const double *t, b
         for (int q = 0; q < 3; ++q) fm[3 * r + q] = (float)(sc[r] * R[3 * r + q]);
         fm[9 + r] = (float)(sc[r] * tp);
     }
-    // Dz0 = 1.01 (fx ex + fy ey + ez Wmax), Wmax = (fx + fy) wmax >= fx wa_i + fy wb_i of any point
-    const double D0 = 1.01 * (fx * eps[0] + fy * eps[1] + eps[2] * (fx + fy) * wmax);
-    fm[12] = (float)(D0 * (1.0 + 1e-6));
-    // |z'| above zg keeps |x'/z' - x/z| <= 0.01 for every projection the bound is used on
-    fm[14] = (float)(100.0 * (fmax(eps[0], eps[1]) + wmax * eps[2]) + 2.02 * eps[2] + 1e-30);
-    // Mz = (sqT2 |z| + Dz) Dz + Trel z^2 with Dz = D0 + Cmax |z| is at most alpha z^2 + beta:
-    // |z| <= z^2 / (2w) + w / 2 for any w > 0 (taken as the hypothesis' depth of the centre).
-    const double sqT2 = fconst[5], Trel = fconst[6], Cmax = fconst[7];
-    const double Bc = sqT2 * D0 + 2.0 * D0 * Cmax;
-    const double w = fmax(fabs((double)fm[11]), 1.0);
-    fm[13] = (float)(1.01 * (D0 * D0 + Bc * w * 0.5));                                // beta
-    fm[15] = (float)(1.01 * (sqT2 * Cmax + Cmax * Cmax + Trel + Bc / (2.0 * w)));    // alpha
+    const BandConsts b = band_consts(eps, fx, fy, wmax, (double)fm[11], fconst);
+    fm[12] = (float)(b.D0 * (1.0 + 1e-6));
+    fm[13] = (float)b.beta;
+    fm[14] = (float)b.zg;
+    fm[15] = (float)b.alpha;
+}
+
+// ---------------------------------------------------------------------------
+// MFMA record (k_pnp_score_mx): the camera-frame coordinates (xs, ys, fz z) of
+// a pair are one v_mfma_f32_32x32x16_f16 output each.  Coefficients c (rows
+// -fx R0, -fy R1, fz R2 with t', per-hypothesis scale S = 2^g) and point features f (XC YC ZC
+// times fs = 2^-b, and the constant F1 = 2^12) are split into f16 hi + lo, and
+// K = 16 carries the four products hi*hi, hi*lo, lo*hi, lo*lo:
+//   A row (hyp, quantity r), lane half 0: c0h c1h c2h c3h c0h c1h c2h 0
+//                            lane half 1: c0l c1l c2l c3l c0l c1l c2l 0
+//   B column (point), both halves:        Xh  Yh  Zh  F1  Xl  Yl  Zl  0
+// so the output is sum_k (c_kh + c_kl)(f_kh + f_kl) in f32: S x the exact
+// coordinate up to the split (<= 2^-22 relative per operand + 2^-14 absolute:
+// pieces below the f16 normal range are flushed), the f32 rounding of the
+// record (2^-24) and the MFMA's f32 accumulation (<= 16 roundings, counted at
+// 2^-23 each).  eps = 2^-18 (r1 B + |t'|) + 3 / (S |sc|) bounds all of it; the
+// rest of the band (alpha, beta, zg) is the f32 kernel's, with the scale
+// folded in (the test is homogeneous: beta * S^2, zg * S fz, (T -+ alpha) / fz^2).
+// Record (32 floats): [0..24) the three A rows (2 halves x 8 f16 each),
+// 24 (T - alpha) / fz^2, 25 beta S^2, 26 (T + alpha) / fz^2, 27 zg S fz (not
+// tested: beta makes the depth guard redundant, band_consts), 28..31 unused.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void write_hmodel(const double *R, const double *t, bool valid, const double *frame,
+                                             const double *cam, const float *fconst, float *hm) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    h8 rows[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) rows[q] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+    float4 cst;
+    const double B = frame[3], rho = frame[4], cmax = frame[5], wmax = frame[6];
+    const double fs = mx_feature_scale(B);
+    const double fx = fabs(cam[0]), fy = fabs(cam[1]);
+    const double fz = mx_zscale(fx);
+    const double sc[3] = {-cam[0], -cam[1], fz};
+    double c[3][4], tp[3], r1[3], m = 0.0;
+    bool finite = valid;
+    if (valid) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            tp[r] = R[3 * r] * frame[0] + R[3 * r + 1] * frame[1] + R[3 * r + 2] * frame[2] + t[r];
+            r1[r] = fabs(R[3 * r]) + fabs(R[3 * r + 1]) + fabs(R[3 * r + 2]);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) c[r][k] = sc[r] * R[3 * r + k] / fs;
+            c[r][3] = sc[r] * tp[r] / kMxF1;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m = fmax(m, fabs(c[r][k]));
+            finite = finite && isfinite(tp[r]) && isfinite(r1[r]);
+        }
+        finite = finite && isfinite(m);
+    }
+    if (!valid) {
+        // decided outlier everywhere: z = F1 > 0, thresholds -inf
+        rows[4][3] = (_Float16)1.f;
+        cst = make_float4(-__builtin_inff(), 0.f, -__builtin_inff(), -1.f);
+    } else if (!finite) {
+        // every pair undecided (z = 0: E < -inf and E > NaN never hold): the exact f64 test decides
+        cst = make_float4(-__builtin_inff(), 0.f, __builtin_inff(), __builtin_inff());
+    } else {
+        int e = 0;
+        (void)frexp(m > 0 ? m : 1.0, &e);
+        const double S = ldexp(1.0, 12 - e);  // m S < 2^12
+        double eps[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                _Float16 hi, lo;
+                mx_split((float)(c[r][k] * S), hi, lo);
+                rows[2 * r][k] = hi;
+                rows[2 * r + 1][k] = lo;
+                if (k < 3) {
+                    rows[2 * r][4 + k] = hi;
+                    rows[2 * r + 1][4 + k] = lo;
+                }
+            }
+            eps[r] = kMxEps * (r1[r] * B + fabs(tp[r])) + 3.0 / (S * fabs(sc[r])) + r1[r] * rho +
+                     4e-15 * (r1[r] * cmax + fabs(t[r]));
+        }
+        const BandConsts b = band_consts(eps, fx, fy, wmax, tp[2], fconst);
+        const double T = fconst[4];
+        const double lo_c = T - b.alpha, hi_c = T + b.alpha;
+        const double ifz2 = 1.0 / (fz * fz);  // z' = fz S z: z'^2 carries fz^2
+        cst = make_float4((float)((lo_c - 1e-6 * fabs(lo_c)) * ifz2), (float)(b.beta * S * S * (1.0 + 1e-6)),
+                          (float)(hi_c * (1.0 + 1e-6) * ifz2), (float)(b.zg * S * fz * (1.0 + 1e-6)));
+    }
+    h8 *o = reinterpret_cast<h8 *>(hm);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) o[q] = rows[q];
+    reinterpret_cast<float4 *>(hm)[6] = cst;
+    reinterpret_cast<float4 *>(hm)[7] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
     const int prob = blockIdx.y;
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
-    if (a.queue && h == 0 && prob == 0) *a.queue = 0;  // the scoring launch that follows starts its queue at 0
+    if (h == 0 && prob == 0) {  // the scoring launch that follows starts its queue (and fallback list) at 0
+        if (a.queue) *a.queue = 0;
+        if (a.mx_count) *a.mx_count = 0;
+    }
     if (h >= H) return;
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
     const double *m = a.models + rec * kModelStride;
     write_fmodel(m, m + 9, m[kValidSlot] != 0.0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
                  a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride);
+    if (a.hmodels)
+        write_hmodel(m, m + 9, m[kValidSlot] != 0.0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+                     a.fconst + (int64_t)prob * kFconstStride, a.hmodels + rec * kHModelStride);
 }
 
 // ---------------------------------------------------------------------------
@@ -223,7 +404,10 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     const int prob = blockIdx.y;
     const int hl = blockIdx.x * blockDim.x + threadIdx.x;
     // every round's scoring launch follows a solve on the same stream: reset its work queue here
-    if (a.queue && hl == 0 && prob == 0) *a.queue = 0;
+    if (hl == 0 && prob == 0) {
+        if (a.queue) *a.queue = 0;
+        if (a.mx_count) *a.mx_count = 0;
+    }
     if (hl >= H) return;
     const int64_t h = hyp_begin + hl;
     const int64_t p0 = a.offsets[prob];
@@ -259,7 +443,10 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
     m[kValidSlot] = st > 0 ? 1.0 : 0.0;
     a.status[rec] = st;
-    if (a.fmodels)
+    if (a.hmodels)  // the MFMA scoring kernel reads only these
+        write_hmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+                     a.fconst + (int64_t)prob * kFconstStride, a.hmodels + rec * kHModelStride);
+    else if (a.fmodels)
         write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
                      a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride);
 }
@@ -597,6 +784,327 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
             if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
         }
         __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA scoring kernel.  The camera-frame coordinates (xs, ys, z) of 8
+// hypotheses x 32 points come out of one v_mfma_f32_32x32x16_f16 (record and
+// error model: write_hmodel); the VALU does the rest of the alpha-beta test of
+// k_pnp_score_ab, 10 operations per pair instead of 19.
+//   C/D map (gfx950): column = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+//   row 8j + 4h + q  <->  hypothesis 2j + h of the tile, quantity q (xs ys z, 3 unused)
+// so lane (column c, half h) holds xs ys z of hypothesis 2j + h at point c in
+// registers 4j .. 4j + 2: 4 hypotheses x 1 point per lane and MFMA.
+// A unit is (HB = 32 NT hypotheses, a chunk of the points).  Wave w owns NT
+// tiles (8 NT hypotheses; their A operands and band constants stay in
+// registers) and runs every 32-point tile of the chunk, so the 4 waves of a
+// block read the same points (L1 reuse) and need no count reduction.  Counts
+// are ballot popcounts (scalar unit); undecided pairs (the band, |z| <= zg,
+// NaN) are recounted with the exact f64 error after the tile, as in
+// k_pnp_score_ab, so counts equal the exact kernel's bit for bit.
+// ---------------------------------------------------------------------------
+typedef _Float16 mx_h8 __attribute__((ext_vector_type(8)));
+typedef float mx_f16 __attribute__((ext_vector_type(16)));
+
+// the test of one pair from an MFMA output (registers 4 jj .. 4 jj + 2: xs ys fz z, scaled):
+// E < lo decided inlier, E > hi decided outlier (no depth guard: beta covers it, band_consts);
+// a NaN anywhere leaves the pair undecided
+struct MxTest {
+    bool lt, gt;
+};
+__device__ __forceinline__ MxTest mx_test(const mx_f16 &acc, int jj, float4 k, float uc, float vc) {
+    const float xs = acc[4 * jj], ys = acc[4 * jj + 1], z = acc[4 * jj + 2];
+    const float q1 = __builtin_fmaf(uc, z, xs);
+    const float q2 = __builtin_fmaf(vc, z, ys);
+    const float z2 = z * z;
+    const float E = __builtin_fmaf(q1, q1, q2 * q2);
+    const float lo = __builtin_fmaf(k.x, z2, -k.y);
+    const float hi = __builtin_fmaf(k.z, z2, k.y);
+    return MxTest{E < lo, E > hi};
+}
+
+// the wave's A operands (this lane supplies row `col` of every tile: hypothesis 2j + hh, quantity
+// q; lane half = the hi (0) or lo (1) pieces) and band constants; hypotheses past nh are
+// decided outliers
+template <int NT>
+__device__ __forceinline__ void mx_load_operands(const float *__restrict__ hm, int hw0, int nh, int col, int half,
+                                                 mx_h8 (&A)[NT], float4 (&cs)[NT][4]) {
+    const int j = col >> 3, hh = (col >> 2) & 1, q = col & 3;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int hl = hw0 + t * 8 + 2 * j + hh;
+        mx_h8 v = mx_h8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (q < 3 && hl < nh)
+            v = *reinterpret_cast<const mx_h8 *>(hm + hl * kHModelStride + q * 8 + half * 4);
+        else if (q == 2 && half == 0)
+            v[3] = (_Float16)1.f;  // z = F1 > 0
+        A[t] = v;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int hc = hw0 + t * 8 + 2 * jj + half;
+            cs[t][jj] = hc < nh ? *reinterpret_cast<const float4 *>(hm + hc * kHModelStride + 24)
+                                : make_float4(-__builtin_inff(), 0.f, -__builtin_inff(), -1.f);
+        }
+    }
+}
+
+// CV: 0 inlier counts by ballot popcounts, 1 per-lane counts (VGPR), 2 per-lane counts and
+// all-VALU undecided detection; PD: tiles of point loads in flight
+template <int NT, int W, int CV, int PD, int EXP = 0>  // EXP != 0: timing experiments only (wrong counts)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_mx(
+    PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
+    int split) {
+    static_assert(NT * 4 <= kMxMasks, "undecided-tile record");
+    constexpr int HW = 8 * NT;  // hypotheses per wave
+    constexpr int HB = 4 * HW;  // per unit
+    __shared__ int unit_s;
+    __shared__ int scnt[HB];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int col = lane & 31, half = lane >> 5;
+    const int tiles_per_prob = (H + HB - 1) / HB;
+    const int units_per_prob = tiles_per_prob * split;
+    const int n_units = units_per_prob * n_prob;
+    for (;;) {
+        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
+        __syncthreads();
+        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
+        if (unit >= n_units) break;  // uniform: every wave of every block reaches it
+        const int prob = unit / units_per_prob;
+        const int rem = unit % units_per_prob;
+        const int chunk = rem % split;
+        const int64_t h0 = hyp_begin + (int64_t)(rem / split) * HB;
+        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+        const int64_t p0 = a.offsets[prob];
+        const int n_all = (int)(a.offsets[prob + 1] - p0);
+        const int clen = ((n_all + split - 1) / split + 31) / 32 * 32;
+        const int start = chunk * clen;
+        const int n = min(n_all, start + clen);  // this unit's points: [start, n)
+        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
+        const float cx = fc[2], cy = fc[3], ifz = fc[8];
+        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+        const int hw0 = wave * HW;  // the wave's first hypothesis in the unit
+        const float *__restrict__ hm = a.hmodels + rec0 * kHModelStride;
+
+        mx_h8 A[NT];
+        float4 cs[NT][4];
+        mx_load_operands<NT>(hm, hw0, nh, col, half, A, cs);
+        const uint4 *__restrict__ PF = a.PF + p0;
+        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
+        int cnt[NT][4][2];
+        int vcnt[NT][4];  // CV: this lane's inliers of hypothesis (t, jj, half)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) cnt[t][jj][0] = cnt[t][jj][1] = vcnt[t][jj] = 0;
+
+        // software pipeline: the next PD tiles' point loads are in flight while this tile computes
+        // (indices clamped to the unit's last point, so every load is in bounds)
+        uint4 pf_q[PD];
+        float uu_q[PD], vv_q[PD];
+#pragma unroll
+        for (int d = 0; d < PD; ++d) {
+            pf_q[d] = make_uint4(0, 0, 0, 0);
+            uu_q[d] = vv_q[d] = 0.f;
+            if (start < n) {
+                const int i0 = min(start + 32 * d + col, n - 1);
+                pf_q[d] = PF[i0];
+                uu_q[d] = U[i0];
+                vv_q[d] = V[i0];
+            }
+        }
+        mx_f16 acc0[NT];  // EXP 4 only
+        for (int base = start; base < n; base += 32) {
+            const int i = base + col;
+            const bool in = i < n;
+            const mx_h8 Bf = __builtin_bit_cast(mx_h8, pf_q[0]);
+            const float uu = uu_q[0], vv = vv_q[0];
+#pragma unroll
+            for (int d = 0; d + 1 < PD; ++d) {
+                pf_q[d] = pf_q[d + 1];
+                uu_q[d] = uu_q[d + 1];
+                vv_q[d] = vv_q[d + 1];
+            }
+            if constexpr (EXP != 3) {  // EXP 3: no loads in the loop (timing)
+                const int inx = min(base + 32 * PD + col, n - 1);
+                pf_q[PD - 1] = PF[inx];
+                uu_q[PD - 1] = U[inx];
+                vv_q[PD - 1] = V[inx];
+            }
+            // out-of-range lanes: a pixel at 3e38 makes the pair a decided outlier (or undecided)
+            const float uc = in ? (uu - cx) * ifz : 3.0e38f, vc = in ? (vv - cy) * ifz : 3.0e38f;
+            uint64_t und[NT][4];
+            uint64_t any = 0;
+            mx_f16 acc[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                if constexpr (EXP == 4) {  // MFMA once per unit (timing)
+                    if (base == start) acc0[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[t], Bf, mx_f16{}, 0, 0, 0);
+                    acc[t] = acc0[t];
+                } else if constexpr (EXP == 2) {  // no MFMA: operands as stand-in values
+                    const float4 bb = __builtin_bit_cast(float4, Bf);
+                    const float4 aa = __builtin_bit_cast(float4, A[t]);
+                    acc[t] = mx_f16{bb.x, bb.y, bb.z, bb.w, aa.x, aa.y, aa.z, aa.w, bb.x, aa.y, bb.z, aa.w, aa.x, bb.y, aa.z, bb.w};
+                } else {
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[t], Bf, mx_f16{}, 0, 0, 0);
+                }
+            }
+            if constexpr (EXP == 1) {  // no test: fold the outputs into one count
+                float sacc = 0.f;
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) sacc += acc[t][r];
+                cnt[0][0][0] += __popcll(__ballot(sacc > uc));
+                continue;
+            }
+            if constexpr (CV == 2) {
+                // all-VALU decisions: per-lane inlier counts and a per-lane count of decided pairs;
+                // the undecided masks are only formed (MFMA and test redone) when a lane of the
+                // tile has an undecided pair
+                int dec = 0;
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const MxTest r = mx_test(acc[t], jj, cs[t][jj], uc, vc);
+                        vcnt[t][jj] += r.lt ? 1 : 0;
+                        dec += r.lt ? 1 : 0;
+                        dec += r.gt ? 1 : 0;
+                    }
+                if (__builtin_expect(__ballot(dec != NT * 4) != 0, 0)) {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                        const mx_f16 ac = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[t], Bf, mx_f16{}, 0, 0, 0);
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) {
+                            const MxTest r = mx_test(ac, jj, cs[t][jj], uc, vc);
+                            und[t][jj] = ~(__ballot(r.lt) | __ballot(r.gt));
+                            any |= und[t][jj];
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const MxTest r = mx_test(acc[t], jj, cs[t][jj], uc, vc);
+                    const bool lt = r.lt;
+                    const uint64_t mi = __ballot(lt);
+                    const uint64_t mo = __ballot(r.gt);
+                    if constexpr (CV) {
+                        vcnt[t][jj] += lt ? 1 : 0;
+                    } else {
+                        cnt[t][jj][0] += __popc((uint32_t)mi);
+                        cnt[t][jj][1] += __popc((uint32_t)(mi >> 32));
+                    }
+                    und[t][jj] = ~(mi | mo);
+                    any |= und[t][jj];
+                }
+            }
+            }
+            if (__builtin_expect(any != 0, 0)) {
+                // defer the exact recount of the undecided pairs to k_pnp_mx_fallback: one record
+                // per tile, so this kernel carries no f64 code
+                int slot = 0;
+                if (lane == 0) slot = atomicAdd(a.mx_count, 1);
+                slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0));
+                if (slot < a.mx_cap && lane == 0) {
+                    MxUndecided &r = a.mx_list[slot];
+                    r.rec = rec0 + hw0;
+                    r.prob = prob;
+                    r.base = base;
+                    r.n = n;
+                    r.nh = nh - hw0;
+#pragma unroll
+                    for (int t = 0; t < NT; ++t)
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) r.m[t * 4 + jj] = und[t][jj];
+                }
+            }
+        }
+        if constexpr (CV) {
+            // sum each half's 32 lanes (hypotheses 2 jj and 2 jj + 1 of tile t)
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    int v = vcnt[t][jj];
+#pragma unroll
+                    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+                    cnt[t][jj][0] = __shfl(v, 0);
+                    cnt[t][jj][1] = __shfl(v, 32);
+                }
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    scnt[hw0 + t * 8 + 2 * jj] = cnt[t][jj][0];
+                    scnt[hw0 + t * 8 + 2 * jj + 1] = cnt[t][jj][1];
+                }
+        }
+        __syncthreads();
+        if (threadIdx.x < nh) {
+            const int sum = scnt[threadIdx.x];
+            if (split == 1)
+                counts[rec0 + threadIdx.x] = sum;
+            else if (sum)
+                atomicAdd(&counts[rec0 + threadIdx.x], sum);
+        }
+        __syncthreads();  // scnt and unit_s are rewritten by the next unit
+    }
+}
+
+// The exact f64 recount of the undecided pairs k_pnp_score_mx recorded (rare): one wave per
+// record, lanes laid out as in the scoring kernel (point base + (lane & 31), hypothesis pair
+// by lane half), inliers added atomically to the counts.
+__global__ __launch_bounds__(256) void k_pnp_mx_fallback(PnpArgs a, int nt, int32_t *__restrict__ counts) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = lane & 31, half = lane >> 5;
+    const int total = min(*a.mx_count, a.mx_cap);
+    for (int e = blockIdx.x * 4 + wave; e < total; e += gridDim.x * 4) {
+        const MxUndecided &r = a.mx_list[e];
+        const int prob = r.prob;
+        const int64_t p0 = a.offsets[prob];
+        const double *cm = a.cams + 4 * prob;
+        const Cam k{cm[0], cm[1], cm[2], cm[3]};
+        const float thr2 = a.thr2[prob];
+        const int i = r.base + col;
+        const bool in = i < r.n;
+        unsigned long long np = 0;
+        for (int tj = 0; tj < nt * 4; ++tj) {
+            const uint64_t u = r.m[tj];
+            if (!u) continue;  // uniform
+            const int hl0 = (tj >> 2) * 8 + 2 * (tj & 3);
+            const int hl = hl0 + half;
+            bool ex = false;
+            if (((u >> lane) & 1ull) && in && hl < r.nh) {
+                const double *md = a.models + (r.rec + hl) * kModelStride;
+                const int64_t q = p0 + i;
+                ex = md[kValidSlot] != 0.0 &&
+                     pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <= thr2;
+            }
+            const uint64_t b = __ballot(ex);
+            if (lane == 0) {
+                const int c0 = __popc((uint32_t)b), c1 = __popc((uint32_t)(b >> 32));
+                if (c0) atomicAdd(&counts[r.rec + hl0], c0);
+                if (c1) atomicAdd(&counts[r.rec + hl0 + 1], c1);
+                if (a.mx_stats && prob == 0) {  // diagnostics: undecided pairs per record index
+                    if (hl0 < r.nh) atomicAdd(a.mx_stats + 2 + (r.rec + hl0) % a.hyp_stride, (unsigned long long)__popc((uint32_t)u));
+                    if (hl0 + 1 < r.nh)
+                        atomicAdd(a.mx_stats + 2 + (r.rec + hl0 + 1) % a.hyp_stride, (unsigned long long)__popc((uint32_t)(u >> 32)));
+                }
+            }
+            np += __popcll(u);
+        }
+        if (a.mx_stats && lane == 0) {
+            atomicAdd(a.mx_stats, 1ull);
+            atomicAdd(a.mx_stats + 1, np);
+        }
     }
 }
 
@@ -1217,7 +1725,15 @@ __global__ __launch_bounds__(256) void k_best_key(const int32_t *__restrict__ co
         const unsigned long long other = __shfl_xor(best, o);
         best = other > best ? other : best;
     }
-    if ((threadIdx.x & 63) == 0 && best) atomicMax(key, best);
+    // one atomic per block: thousands of same-address atomics serialise in L2
+    __shared__ unsigned long long wbest[4];
+    if ((threadIdx.x & 63) == 0) wbest[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        best = wbest[0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = wbest[w] > best ? wbest[w] : best;
+        if (best) atomicMax(key, best);
+    }
 }
 
 // model record of the key's hypothesis -> out[16] (zeros when key == 0)
@@ -1260,14 +1776,14 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 }
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
-                            double *frame, float *fconst, hipStream_t s) {
+                            double *frame, float *fconst, hipStream_t s, uint4 *PF) {
     hipLaunchKernelGGL(k_pnp_init, dim3(1), dim3(256), 0, s, P, ws, a.best_key, a.queue);
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 2048);
     if (g > 32) g = 32;
     hipLaunchKernelGGL(k_pnp_bounds, dim3(g, P), dim3(256), 0, s, a, P, ws);
     unsigned g2 = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g2 > 1024) g2 = 1024;
-    hipLaunchKernelGGL(k_pnp_center, dim3(g2, P), dim3(256), 0, s, a, P, ws, frame, fconst, XC, YC, ZC);
+    hipLaunchKernelGGL(k_pnp_center, dim3(g2, P), dim3(256), 0, s, a, P, ws, frame, fconst, XC, YC, ZC, PF);
     return hipGetLastError();
 }
 
@@ -1322,10 +1838,87 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
     }
 }
 
+// MFMA variants (k_pnp_score_mx): units of 32 NT hypotheses x a point chunk, about 8 units per
+// resident block so that the work queue's tail (at most one unit) stays small; the counts of a
+// split unit accumulate atomically.  k_pnp_mx_fallback then adds the exact recount of the
+// undecided pairs, and k_best_key reduces the best key (single problem).
+template <int NT, int W, int CV, int PD, int EXP = 0>
+static void launch_mx(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
+    constexpr int HB = 32 * NT;
+    auto kern = k_pnp_score_mx<NT, W, CV, PD, EXP>;
+    static int resident = 0;
+    if (resident == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
+        resident = std::max(1, cus) * std::max(1, per_cu);
+    }
+    const int64_t tiles = (int64_t)P * ((H + HB - 1) / HB);
+    const int64_t chunks = std::max<int64_t>(1, ((int64_t)a.max_n + 255) / 256);  // chunks of >= 256 points
+    const int split = (int)std::min<int64_t>(chunks, std::max<int64_t>(1, (8 * (int64_t)resident + tiles - 1) / tiles));
+    if (split > 1 && P == 1)
+        (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
+    else if (split > 1)
+        (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P, s);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(tiles * split, resident));
+    static unsigned long long *stats = nullptr;
+    static size_t stats_cap = 0;
+    static const bool want_stats = getenv("RSAC_MX_STATS") != nullptr;
+    const size_t need = sizeof(unsigned long long) * (2 + (size_t)a.hyp_stride);
+    if (want_stats && stats_cap < need) {
+        if (stats) (void)hipFree(stats);
+        (void)hipMalloc(&stats, need);
+        stats_cap = need;
+    }
+    PnpArgs ka = a;
+    if (want_stats && stats) {
+        ka.mx_stats = stats;
+        (void)hipMemsetAsync(stats, 0, need, s);
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin, H, P, a.queue, counts, split);
+    // the record count is on the device: a grid of 16k waves, the idle ones exit at once
+    hipLaunchKernelGGL(k_pnp_mx_fallback, dim3(4096), dim3(256), 0, s, ka, NT, counts);
+    if (want_stats && stats) {
+        std::vector<unsigned long long> h(2 + (size_t)a.hyp_stride);
+        (void)hipMemcpyAsync(h.data(), stats, need, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        int nz = 0, over100 = 0;
+        unsigned long long top = 0;
+        for (int64_t q = 0; q < a.hyp_stride; ++q) {
+            nz += h[2 + q] > 0; over100 += h[2 + q] > 100;
+            top = std::max(top, h[2 + q]);
+        }
+        fprintf(stderr, "[mx] P=%d H=%d split=%d grid=%u: fallback wave-tiles %llu of %.4g, undecided pairs %llu;"
+                " hypotheses (problem 0) with any %d, >100 %d, max %llu\n",
+                P, H, split, grid, h[0], (double)P * ((H + 8 * NT - 1) / (8 * NT)) * ((a.max_n + 31) / 32), h[1], nz,
+                over100, top);
+    }
+    if (a.best_key) {
+        unsigned g = cdiv(H, 1024);
+        if (g > 128) g = 128;
+        hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
+                           a.rng_base + hyp_begin, a.best_key);
+    }
+}
+
+bool score_variant_mx() { return g_score_variant >= 30 && g_score_variant < 40; }
+
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
     if (a.max_n > 0 && a.max_n <= kLanePts) {
         hipLaunchKernelGGL(k_pnp_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
+    } else if (a.hmodels && a.PF && !a.exact_only && score_variant_mx()) {
+        switch (g_score_variant) {
+            case 31: launch_mx<1, 4, 0, 1>(a, P, hyp_begin, H, counts, s); break;
+            case 32: launch_mx<2, 4, 2, 1>(a, P, hyp_begin, H, counts, s); break;
+            case 33: launch_mx<1, 4, 2, 1>(a, P, hyp_begin, H, counts, s); break;
+            case 34: launch_mx<2, 5, 2, 1>(a, P, hyp_begin, H, counts, s); break;
+            case 35: launch_mx<2, 4, 0, 1, 1>(a, P, hyp_begin, H, counts, s); break;  // timing only
+            case 36: launch_mx<2, 4, 0, 1, 3>(a, P, hyp_begin, H, counts, s); break;  // timing only
+            case 37: launch_mx<2, 4, 0, 1, 4>(a, P, hyp_begin, H, counts, s); break;  // timing only
+            default: launch_mx<2, 4, 0, 1>(a, P, hyp_begin, H, counts, s); break;
+        }
     } else if (a.fmodels && !a.exact_only) {
         switch (g_score_variant) {
             case 1: launch_f32<4, 32>(a, P, hyp_begin, H, counts, s); break;
@@ -1424,8 +2017,8 @@ hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t 
                            unsigned long long *key, const double *models, double *model_out, hipStream_t s) {
     hipError_t e = hipMemsetAsync(key, 0, sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
-    unsigned g = cdiv(H, 256);
-    if (g > 512) g = 512;
+    unsigned g = cdiv(H, 1024);
+    if (g > 128) g = 128;
     hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts, status, H, hyp_begin, key);
     hipLaunchKernelGGL(k_key_model, dim3(1), dim3(64), 0, s, models, key, hyp_begin, model_out);
     return hipGetLastError();
