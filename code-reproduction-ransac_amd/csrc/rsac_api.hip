@@ -806,7 +806,7 @@ void rsac_destroy(rsac_ctx *c) {
 }
 
 int rsac_set_score_variant(int variant) {
-    if (variant < -1 || (variant > 24 && (variant < 30 || variant > 37))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
+    if (variant < -1 || (variant > 28 && (variant < 30 || variant > 37))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
     set_score_variant(variant);
     return RSAC_OK;
 }

@@ -636,7 +636,7 @@ __device__ __forceinline__ AbTest ab_test(const float *m, float x, float y, floa
 
 // The exact f64 recount of a tile's undecided pairs (rare).  Returns this
 // lane's share of the hypotheses' counts (lane h: hypothesis h's inliers).
-template <int P>
+template <int P, bool NZ>
 __device__ __forceinline__ int ab_fallback(const PnpArgs &a, int prob, int64_t p0, int n, int64_t rec0,
                                                      int base, int lane, uint32_t wund, uint32_t undm,
                                                      const float *mlds, const float (&px)[P], const float (&py)[P],
@@ -659,7 +659,7 @@ __device__ __forceinline__ int ab_fallback(const PnpArgs &a, int prob, int64_t p
             bool ex = false;
             if ((undm >> h) & 1u) {
                 const AbTest r = ab_test(m, px[j], py[j], pz[j], pu[j], pv[j]);
-                const bool dec = r.zok & (r.lt | r.gt);
+                const bool dec = (NZ || r.zok) & (r.lt | r.gt);
                 if (!dec && i < n) {
                     const int64_t q = p0 + i;
                     ex = md[kValidSlot] != 0.0 &&
@@ -677,7 +677,8 @@ __device__ __forceinline__ int ab_fallback(const PnpArgs &a, int prob, int64_t p
 // split > 1 (small rounds, no fused best key): a unit is (problem, hypothesis tile, point
 // chunk) and the chunk's counts are atomically added into zeroed counts -- enough units to
 // fill the GPU when a round has only a few tiles (an adaptive run's first 256 hypotheses).
-template <int P, int HB, int W = 4>  // W: minimum waves per SIMD the register budget must allow
+// NZ: no depth-guard test (beta makes it redundant, band_consts): one compare fewer per pair.
+template <int P, int HB, int W = 4, bool NZ = false>  // W: minimum waves per SIMD the register budget must allow
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_ab(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int split) {
@@ -759,11 +760,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
                 for (int j = 0; j < P; ++j) {
                     const AbTest r = ab_test(m, px[j], py[j], pz[j], pu[j], pv[j]);
                     // one v_cmp per mask, combined on the scalar unit; NaN leaves a pair undecided
-                    const uint64_t mz = __ballot(r.zok);
                     const uint64_t mi = __ballot(r.lt);
                     const uint64_t mo = __ballot(r.gt);
-                    cc += __popcll(mi & mz);
-                    und |= ~((mi | mo) & mz);
+                    if constexpr (NZ) {
+                        cc += __popcll(mi);
+                        und |= ~(mi | mo);
+                    } else {
+                        const uint64_t mz = __ballot(r.zok);
+                        cc += __popcll(mi & mz);
+                        und |= ~((mi | mo) & mz);
+                    }
                 }
                 cnt += (lane == h) ? cc : 0;
                 undm |= __builtin_amdgcn_inverse_ballot_w64(und) ? (1u << h) : 0u;
@@ -773,7 +779,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) wund |= (uint32_t)__shfl_xor((int)wund, o);
             wund = __builtin_amdgcn_readfirstlane(wund);
-            if (__builtin_expect(wund != 0, 0)) cnt += ab_fallback<P>(a, prob, p0, n, rec0, base, lane, wund, undm, mlds, px, py, pz, pu, pv);
+            if (__builtin_expect(wund != 0, 0)) cnt += ab_fallback<P, NZ>(a, prob, p0, n, rec0, base, lane, wund, undm, mlds, px, py, pz, pu, pv);
         }
         if (lane < HB) red[wave][lane] = cnt;
         __syncthreads();
@@ -1059,49 +1065,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     }
 }
 
-// The exact f64 recount of the undecided pairs k_pnp_score_mx recorded (rare): one wave per
-// record, lanes laid out as in the scoring kernel (point base + (lane & 31), hypothesis pair
-// by lane half), inliers added atomically to the counts.
+// The exact f64 recount of the undecided pairs k_pnp_score_mx recorded (rare, about one pair
+// per record): one thread per record walks its mask bits (bit b of mask 4t + j: point base +
+// (b & 31), hypothesis 8t + 2j + (b >> 5)); inliers are added atomically to the counts.
 __global__ __launch_bounds__(256) void k_pnp_mx_fallback(PnpArgs a, int nt, int32_t *__restrict__ counts) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int col = lane & 31, half = lane >> 5;
     const int total = min(*a.mx_count, a.mx_cap);
-    for (int e = blockIdx.x * 4 + wave; e < total; e += gridDim.x * 4) {
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
         const MxUndecided &r = a.mx_list[e];
         const int prob = r.prob;
         const int64_t p0 = a.offsets[prob];
         const double *cm = a.cams + 4 * prob;
         const Cam k{cm[0], cm[1], cm[2], cm[3]};
         const float thr2 = a.thr2[prob];
-        const int i = r.base + col;
-        const bool in = i < r.n;
         unsigned long long np = 0;
         for (int tj = 0; tj < nt * 4; ++tj) {
-            const uint64_t u = r.m[tj];
-            if (!u) continue;  // uniform
-            const int hl0 = (tj >> 2) * 8 + 2 * (tj & 3);
-            const int hl = hl0 + half;
-            bool ex = false;
-            if (((u >> lane) & 1ull) && in && hl < r.nh) {
+            uint64_t u = r.m[tj];
+            np += __popcll(u);
+            while (u) {
+                const int b = __builtin_ctzll(u);
+                u &= u - 1;
+                const int i = r.base + (b & 31);
+                const int hl = (tj >> 2) * 8 + 2 * (tj & 3) + (b >> 5);
+                if (i >= r.n || hl >= r.nh) continue;
+                if (a.mx_stats && prob == 0) atomicAdd(a.mx_stats + 2 + (r.rec + hl) % a.hyp_stride, 1ull);
                 const double *md = a.models + (r.rec + hl) * kModelStride;
                 const int64_t q = p0 + i;
-                ex = md[kValidSlot] != 0.0 &&
-                     pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <= thr2;
+                if (md[kValidSlot] != 0.0 &&
+                    pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <= thr2)
+                    atomicAdd(&counts[r.rec + hl], 1);
             }
-            const uint64_t b = __ballot(ex);
-            if (lane == 0) {
-                const int c0 = __popc((uint32_t)b), c1 = __popc((uint32_t)(b >> 32));
-                if (c0) atomicAdd(&counts[r.rec + hl0], c0);
-                if (c1) atomicAdd(&counts[r.rec + hl0 + 1], c1);
-                if (a.mx_stats && prob == 0) {  // diagnostics: undecided pairs per record index
-                    if (hl0 < r.nh) atomicAdd(a.mx_stats + 2 + (r.rec + hl0) % a.hyp_stride, (unsigned long long)__popc((uint32_t)u));
-                    if (hl0 + 1 < r.nh)
-                        atomicAdd(a.mx_stats + 2 + (r.rec + hl0 + 1) % a.hyp_stride, (unsigned long long)__popc((uint32_t)(u >> 32)));
-                }
-            }
-            np += __popcll(u);
         }
-        if (a.mx_stats && lane == 0) {
+        if (a.mx_stats) {
             atomicAdd(a.mx_stats, 1ull);
             atomicAdd(a.mx_stats + 1, np);
         }
@@ -1798,14 +1792,17 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
-constexpr int kDefaultScoreVariant = 23;  // fastest measured on MI355X
+constexpr int kDefaultScoreVariant = 25;  // fastest measured on MI355X
 static int g_score_variant = kDefaultScoreVariant;
 void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
 
-template <int PP, int HB, int KIND = 0, int W = 4>  // KIND 0 VALU f32, 1 packed f32, 2 MFMA (PP = point chunks of 16), 3 alpha-beta (W waves/SIMD)
+// KIND 0 VALU f32, 1 packed f32, 2 MFMA (PP = point chunks of 16), 3 alpha-beta (W waves/SIMD);
+// alpha-beta only: NZ no depth guard, BAL balanced point split (~8 units per resident block, the
+// best key then reduced by k_best_key after the scoring launch)
+template <int PP, int HB, int KIND = 0, int W = 4, bool NZ = false, bool BAL = false>
 static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
     auto kern = [] {
-        if constexpr (KIND == 3) return k_pnp_score_ab<PP, HB, W>;
+        if constexpr (KIND == 3) return k_pnp_score_ab<PP, HB, W, NZ>;
         else if constexpr (KIND == 2) return k_pnp_score_mfma<HB, PP>;
         else if constexpr (KIND == 1) return k_pnp_score_pk<PP, HB>;
         else return k_pnp_score_f32<PP, HB>;
@@ -1823,7 +1820,9 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
         // few tiles and no fused best key: split the points too (counts accumulate atomically)
         int split = 1;
         const int64_t chunks = std::max<int64_t>(1, ((int64_t)a.max_n + 4 * 64 * PP - 1) / (4 * 64 * PP));
-        if (!a.best_key && units * 2 <= resident)
+        if (BAL && (!a.best_key || P == 1))
+            split = (int)std::min<int64_t>(chunks, std::max<int64_t>(1, (8 * (int64_t)resident + units - 1) / units));
+        else if (!a.best_key && units * 2 <= resident)
             split = (int)std::min<int64_t>(chunks, (resident + units - 1) / units);
         if (split > 1 && P == 1)
             (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
@@ -1831,7 +1830,15 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
             (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P, s);
         units *= split;
         const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, a.queue, counts, split);
+        PnpArgs ka = a;
+        if (split > 1) ka.best_key = nullptr;  // reduced below from the complete counts
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin, H, P, a.queue, counts, split);
+        if (split > 1 && a.best_key) {
+            unsigned g = cdiv(H, 1024);
+            if (g > 128) g = 128;
+            hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
+                               a.rng_base + hyp_begin, a.best_key);
+        }
     } else {
         const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, a.queue, counts);
@@ -1856,7 +1863,9 @@ static void launch_mx(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H,
     }
     const int64_t tiles = (int64_t)P * ((H + HB - 1) / HB);
     const int64_t chunks = std::max<int64_t>(1, ((int64_t)a.max_n + 255) / 256);  // chunks of >= 256 points
-    const int split = (int)std::min<int64_t>(chunks, std::max<int64_t>(1, (8 * (int64_t)resident + tiles - 1) / tiles));
+    static const int64_t units_per_block = getenv("RSAC_MX_UNITS") ? atoi(getenv("RSAC_MX_UNITS")) : 8;
+    const int split = (int)std::min<int64_t>(
+        chunks, std::max<int64_t>(1, (units_per_block * (int64_t)resident + tiles - 1) / tiles));
     if (split > 1 && P == 1)
         (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
     else if (split > 1)
@@ -1877,8 +1886,8 @@ static void launch_mx(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H,
         (void)hipMemsetAsync(stats, 0, need, s);
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin, H, P, a.queue, counts, split);
-    // the record count is on the device: a grid of 16k waves, the idle ones exit at once
-    hipLaunchKernelGGL(k_pnp_mx_fallback, dim3(4096), dim3(256), 0, s, ka, NT, counts);
+    // the record count is on the device: a fixed grid, idle threads exit at once
+    hipLaunchKernelGGL(k_pnp_mx_fallback, dim3(512), dim3(256), 0, s, ka, NT, counts);
     if (want_stats && stats) {
         std::vector<unsigned long long> h(2 + (size_t)a.hyp_stride);
         (void)hipMemcpyAsync(h.data(), stats, need, hipMemcpyDeviceToHost, s);
@@ -1945,6 +1954,10 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 22: launch_f32<4, 32, 3, 6>(a, P, hyp_begin, H, counts, s); break;
             case 23: launch_f32<8, 32, 3, 5>(a, P, hyp_begin, H, counts, s); break;
             case 24: launch_f32<2, 32, 3, 6>(a, P, hyp_begin, H, counts, s); break;
+            case 25: launch_f32<8, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 26: launch_f32<8, 32, 3, 5, false, true>(a, P, hyp_begin, H, counts, s); break;
+            case 27: launch_f32<8, 32, 3, 5, true, false>(a, P, hyp_begin, H, counts, s); break;
+            case 28: launch_f32<4, 32, 3, 6, true, true>(a, P, hyp_begin, H, counts, s); break;
             default: launch_f32<kScoreP, kScoreHB>(a, P, hyp_begin, H, counts, s); break;
         }
     } else
