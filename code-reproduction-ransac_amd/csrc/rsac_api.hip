@@ -348,6 +348,17 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     return RSAC_OK;
 }
 
+// fundamental matrix: the f32 Sampson pre-filter's records and coordinate bounds (unless
+// RSAC_F_EXACT_ONLY, which keeps the all-f64 scoring kernel).  Call after ensure_hyp_buffers.
+int fm_prefilter(rsac_ctx *c, HomArgs &a, int32_t P, uint32_t flags, hipStream_t s) {
+    if (flags & RSAC_F_EXACT_ONLY) return RSAC_OK;
+    HIPCHK(c->bounds_ws.ensure(sizeof(int32_t) * 10 * P));  // >= 8 per problem
+    a.fmodels = c->fmodels.as<float>();
+    a.fbounds = c->bounds_ws.as<int>();
+    HIPCHK(launch_fm_bounds(a, P, a.max_n, c->bounds_ws.as<int>(), s));
+    return RSAC_OK;
+}
+
 enum class Model { PnP, Hom, Fm };  // Fm: fundamental matrix on the HomArgs block
 
 // The RANSAC loop of RANSACPointSetRegistrator::run for P problems at once:
@@ -1202,6 +1213,8 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
         a.rng_base = hyp_begin;
         a.seed = seed;
         if (model == Model::Fm) {
+            r = fm_prefilter(c, a, 1, flags, s);
+            if (r) return r;
             HIPCHK(launch_fm_solve(a, 1, 0, H, s));
             HIPCHK(launch_fm_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
         } else {
@@ -1260,6 +1273,10 @@ int rsac_fundamental_ransac(rsac_ctx *c, const void *pts1, const void *pts2, int
     a.thr2 = c->d_thr2;
     a.seed = seed;
     a.rng_base = 0;
+    r = ensure_hyp_buffers(c, 1, std::max(max_iters, 1), false);
+    if (r) return r;
+    r = fm_prefilter(c, a, 1, flags, s);
+    if (r) return r;
     LoopOut lo;
     r = run_loop(c, Model::Fm, st, &a, max_iters, conf, flags, s, lo);
     if (r) return r;

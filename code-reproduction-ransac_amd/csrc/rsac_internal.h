@@ -81,6 +81,11 @@ struct HomArgs {
     int64_t rng_base;
     uint64_t seed;
     int32_t max_n;  // largest problem (points)
+    // fundamental matrix only: float32 Sampson pre-filter (kernels k_fm_bounds / k_fm_score_f32),
+    // per-hypothesis records (kFModelStride floats) and per-problem coordinate bounds
+    // (min / max of x1 y1 x2 y2, ordered ints, k_fm_bounds); nullptr: the all-f64 kernel
+    float *fmodels;
+    const int *fbounds;
 };
 
 // problems with at most this many points are scored one lane per hypothesis
@@ -134,6 +139,8 @@ hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int
 
 // fundamental matrix (8-point + Sampson) on the homography argument block
 hipError_t launch_fm_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
+// coordinate bounds of every problem for the f32 Sampson pre-filter (ws: P x 8 ints)
+hipError_t launch_fm_bounds(const HomArgs &a, int32_t P, int32_t max_n, int *ws, hipStream_t s);
 hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s);
 hipError_t launch_fm_mask(const HomArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
                           hipStream_t s, int64_t best0 = -1);

@@ -2400,6 +2400,178 @@ hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *mod
 // with an 8-point sample, the normalised 8-point solver and the Sampson test
 // (rsac_math.h).  HomArgs: SX SY = image-1 points, DX DY = image-2 points.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Float32 Sampson pre-filter (BASELINE configs[3]).  The f32 test runs in a
+// normalised frame: x^ = (x - c) / s per image (c = the f32 midpoint of the
+// problem's bounding box, s a common power of 2 >= every half-range), so that
+// r = x2^T F x1 does not cancel between pixel-scale terms.  With
+// F^ = T2^T F T1 (T = [[s, 0, cx], [0, s, cy], [0, 0, 1]]): r^ = r,
+// (a^, b^) = s (a, b), (a2^, b2^) = s (a2, b2), so r^2 <= T den  <=>  r^2 <= (T / s^2) den^.
+// Per pair, in f32 with the f64 kernel's operation order:
+//   a b c = F^ (x1^ y1^ 1),  a2 b2 = F^T (x2^ y2^ 1) (first two),  r = x2^ a + y2^ b + c,
+//   den = a^2 + b^2 + a2^2 + b2^2,   decided inlier  r^2 < A den - beta1,
+//                                    decided outlier r^2 > C den + beta2,
+// otherwise the pair is recounted with the exact f64 test (fm_inlier, pixel frame), so the
+// counts equal the f64 kernel's bit for bit.  Error model per hypothesis (u = 2^-24; X^ Y^ bounds
+// of |x^| |y^|, exact x^ vs its f32 evaluation <= u |x^|; A^ B^ C^ A2^ B2^ absolute row / column
+// sums of F^ against the bounds, Rp the pixel-frame analogue for the f64 kernel's own rounding):
+//   |a32 - a^| <= e_a = 4.1u A^ + 1e-15 (A^ + s Ap),  likewise b c a2 b2;  e = max of them;
+//   |r32 - r|  <= e_r = 7.5u (X2^ A^ + Y2^ B^ + C^) + 1e-15 Rp;
+//   |den32 - den^| <= 4 e sqrt(den^) + 4 e^2 + 4.01u den32;
+// with 2|r| e_r <= eta r^2 + e_r^2 / eta and 4 e sqrt(den) <= eta den + 4 e^2 / eta (eta = 1e-3),
+// T^ = T / s^2:
+//   A = T^ (1 - 6u) / (1 + eta)^2,  beta1 = (1 + 1/eta)(e_r^2 + 4 T^ e^2) / (1 + eta)
+//   C = T^ (1 + 6u) / (1 - eta)^2,  beta2 = (e_r^2 / eta + 4 T^ e^2 (1 + 1/eta) / (1 - eta)) / (1 - eta)
+// each with 1e-6 slack for the f32 rounding of A den -+ beta and the f64 kernel's own rounding.
+// Record: F^ (9 f32), A, beta1, C, beta2; an invalid model is a decided outlier everywhere.
+// ---------------------------------------------------------------------------
+struct FmFrame {
+    float c[4];      // x1 y1 x2 y2 centres
+    float is;        // 1 / s
+    double s;        // power of 2
+    double hb[4];    // bounds of |x^| per coordinate
+    double pb[4];    // bounds of |x| (pixel frame)
+};
+
+// ws: per problem 4 ordered-int minima then 4 maxima (k_fm_bounds); identical in every kernel
+__device__ __forceinline__ FmFrame fm_frame(const int *ws, int prob) {
+    FmFrame f;
+    double half = 0;
+    for (int k = 0; k < 4; ++k) {
+        const float lo = ord2f(ws[8 * prob + k]), hi = ord2f(ws[8 * prob + 4 + k]);
+        f.c[k] = (lo <= hi) ? (lo + hi) * 0.5f : 0.f;  // empty problem: lo = +inf, hi = -inf
+        f.pb[k] = fmax(fabs((double)lo), fabs((double)hi));
+        half = fmax(half, fmax((double)hi - f.c[k], (double)f.c[k] - lo));
+    }
+    int e = 0;
+    (void)frexp(half > 0 && half < 1e30 ? half : 1.0, &e);
+    f.s = ldexp(1.0, e);  // >= half
+    f.is = (float)(1.0 / f.s);
+    for (int k = 0; k < 4; ++k) {
+        const float lo = ord2f(ws[8 * prob + k]), hi = ord2f(ws[8 * prob + 4 + k]);
+        f.hb[k] = fmax((double)hi - f.c[k], (double)f.c[k] - lo) * (1.0 + 1.2e-7) / f.s;
+    }
+    return f;
+}
+
+__device__ __forceinline__ void fm_write_record(const double *F, bool valid, const int *ws, int prob, double T,
+                                                float *rec) {
+    const FmFrame fr = fm_frame(ws, prob);
+    bool finite = valid;
+    for (int q = 0; q < 9; ++q) finite = finite && isfinite(F[q]);
+    if (!valid || !finite || !(fr.hb[0] == fr.hb[0]) || !(fr.pb[0] < 1e30) || !(fr.pb[2] < 1e30)) {
+#pragma unroll
+        for (int q = 0; q < kFModelStride; ++q) rec[q] = 0.f;
+        if (!valid) {
+            rec[10] = 1.f;   // lo = -1: never an inlier
+            rec[12] = -1.f;  // hi = -1 < r^2 = 0: an outlier
+        } else {
+            rec[9] = rec[11] = __builtin_nanf("");  // every pair undecided: the f64 test decides
+        }
+        return;
+    }
+    const double s = fr.s;
+    // F^ = T2^T F T1
+    double G[9];  // F T1
+    for (int i = 0; i < 3; ++i) {
+        G[3 * i] = F[3 * i] * s;
+        G[3 * i + 1] = F[3 * i + 1] * s;
+        G[3 * i + 2] = F[3 * i] * fr.c[0] + F[3 * i + 1] * fr.c[1] + F[3 * i + 2];
+    }
+    double Fh[9];
+    for (int j = 0; j < 3; ++j) {
+        Fh[j] = s * G[j];
+        Fh[3 + j] = s * G[3 + j];
+        Fh[6 + j] = fr.c[2] * G[j] + fr.c[3] * G[3 + j] + G[6 + j];
+    }
+    const double X1 = fr.hb[0], Y1 = fr.hb[1], X2 = fr.hb[2], Y2 = fr.hb[3];
+    const double Ar = fabs(Fh[0]) * X1 + fabs(Fh[1]) * Y1 + fabs(Fh[2]);
+    const double Br = fabs(Fh[3]) * X1 + fabs(Fh[4]) * Y1 + fabs(Fh[5]);
+    const double Cr = fabs(Fh[6]) * X1 + fabs(Fh[7]) * Y1 + fabs(Fh[8]);
+    const double A2 = fabs(Fh[0]) * X2 + fabs(Fh[3]) * Y2 + fabs(Fh[6]);
+    const double B2 = fabs(Fh[1]) * X2 + fabs(Fh[4]) * Y2 + fabs(Fh[7]);
+    // pixel-frame sums (the f64 kernel's rounding, ~1e-16 relative of these)
+    const double P1 = fr.pb[0], Q1 = fr.pb[1], P2 = fr.pb[2], Q2 = fr.pb[3];
+    const double Ap = fmax(fmax(fabs(F[0]) * P1 + fabs(F[1]) * Q1 + fabs(F[2]), fabs(F[3]) * P1 + fabs(F[4]) * Q1 + fabs(F[5])),
+                           fmax(fabs(F[0]) * P2 + fabs(F[3]) * Q2 + fabs(F[6]), fabs(F[1]) * P2 + fabs(F[4]) * Q2 + fabs(F[7])));
+    const double Rp = P2 * (fabs(F[0]) * P1 + fabs(F[1]) * Q1 + fabs(F[2])) +
+                      Q2 * (fabs(F[3]) * P1 + fabs(F[4]) * Q1 + fabs(F[5])) + fabs(F[6]) * P1 + fabs(F[7]) * Q1 + fabs(F[8]);
+    constexpr double u = 5.9604644775390625e-08, eta = 1e-3;
+    const double e = 4.1 * u * fmax(fmax(Ar, Br), fmax(fmax(A2, B2), Cr)) + 1e-15 * (fmax(fmax(Ar, Br), fmax(A2, B2)) + s * Ap);
+    const double er = 7.5 * u * (X2 * Ar + Y2 * Br + Cr) + 1e-15 * Rp;
+    const double Th = T / (s * s);
+    const double Alo = Th * (1.0 - 6.0 * u) / ((1.0 + eta) * (1.0 + eta)) * (1.0 - 1e-6);
+    const double b1 = (1.0 + 1.0 / eta) * (er * er + 4.0 * Th * e * e) / (1.0 + eta) * (1.0 + 1e-6);
+    const double Chi = Th * (1.0 + 6.0 * u) / ((1.0 - eta) * (1.0 - eta)) * (1.0 + 1e-6);
+    const double b2 = (er * er / eta + 4.0 * Th * e * e * (1.0 + 1.0 / eta) / (1.0 - eta)) / (1.0 - eta) * (1.0 + 1e-6);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) rec[q] = (float)Fh[q];
+    // A rounded down, the others up (float conversion rounds to nearest: nudge by 2^-23)
+    rec[9] = (float)(Alo * (1.0 - 1.2e-7));
+    rec[10] = (float)(b1 * (1.0 + 1.2e-7));
+    rec[11] = (float)(Chi * (1.0 + 1.2e-7));
+    rec[12] = (float)(b2 * (1.0 + 1.2e-7));
+    rec[13] = rec[14] = rec[15] = 0.f;
+}
+
+struct FmTest {
+    bool lt, gt;
+};
+__device__ __forceinline__ FmTest fm_test_f32(const float *m, float x1, float y1, float x2, float y2) {
+    const float a = __builtin_fmaf(m[0], x1, __builtin_fmaf(m[1], y1, m[2]));
+    const float b = __builtin_fmaf(m[3], x1, __builtin_fmaf(m[4], y1, m[5]));
+    const float c = __builtin_fmaf(m[6], x1, __builtin_fmaf(m[7], y1, m[8]));
+    const float a2 = __builtin_fmaf(m[0], x2, __builtin_fmaf(m[3], y2, m[6]));
+    const float b2 = __builtin_fmaf(m[1], x2, __builtin_fmaf(m[4], y2, m[7]));
+    const float r = __builtin_fmaf(x2, a, __builtin_fmaf(y2, b, c));
+    const float r2 = r * r;
+    const float den = __builtin_fmaf(a, a, __builtin_fmaf(b, b, __builtin_fmaf(a2, a2, b2 * b2)));
+    return FmTest{r2 < __builtin_fmaf(m[9], den, -m[10]), r2 > __builtin_fmaf(m[11], den, m[12])};
+}
+
+// min / max of x1 y1 x2 y2 of every problem (ordered-int encoding; ws: P x 8, preset to
+// +max / -max by launch_fm_bounds); a NaN coordinate poisons the problem's frame (all pairs
+// then fall back to the f64 test)
+__global__ __launch_bounds__(256) void k_fm_bounds(HomArgs a, int *__restrict__ ws) {
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    float lo[4], hi[4];
+    bool nan = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float v[4] = {a.SX[p0 + i], a.SY[p0 + i], a.DX[p0 + i], a.DY[p0 + i]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            lo[k] = fminf(lo[k], v[k]);
+            hi[k] = fmaxf(hi[k], v[k]);
+            nan = nan || v[k] != v[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
+        }
+    }
+    if (__ballot(nan)) { lo[0] = -__builtin_inff(); hi[0] = __builtin_inff(); }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            atomicMin(ws + 8 * prob + k, f2ord(lo[k]));
+            atomicMax(ws + 8 * prob + 4 + k, f2ord(hi[k]));
+        }
+    }
+}
+
+// ws preset: minima to INT_MAX, maxima to INT_MIN (ordered-int encoding)
+__global__ void k_fm_bounds_init(int32_t P, int *__restrict__ ws) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 8 * P; i += gridDim.x * blockDim.x)
+        ws[i] = (i % 8) < 4 ? 0x7FFFFFFF : (int)0x80000000;
+}
+
 __global__ __launch_bounds__(256) void k_fm_solve(HomArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
     const int hl = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2431,6 +2603,7 @@ __global__ __launch_bounds__(256) void k_fm_solve(HomArgs a, int64_t hyp_begin, 
     for (int q = 0; q < 9; ++q) m[q] = F[q];
     m[kValidSlot] = st > 0 ? 1.0 : 0.0;
     a.status[rec] = st;
+    if (a.fmodels) fm_write_record(F, st > 0, a.fbounds, prob, (double)a.thr2[prob], a.fmodels + rec * kFModelStride);
 }
 
 // hypotheses x points tiles (points in registers, hypothesis wave-uniform), exact f64 test
@@ -2503,6 +2676,96 @@ __global__ __launch_bounds__(256) void k_fm_score_lane(HomArgs a, int64_t hyp_be
     counts[rec] = cnt;
 }
 
+// f32 Sampson pre-filter (record: fm_write_record): hypotheses x points tiles as in k_fm_score,
+// the block's HB records staged in LDS; undecided pairs are recounted with the exact f64 test
+// after the hypothesis loop, once per tile.
+template <int P, int HB>
+__global__ __launch_bounds__(256) void k_fm_score_f32(HomArgs a, int64_t hyp_begin, int32_t H,
+                                                      int32_t *__restrict__ counts) {
+    static_assert(HB <= 32, "undecided bits per lane");
+    __shared__ int red[4][HB];
+    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
+    const int prob = blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t h0 = hyp_begin + (int64_t)blockIdx.x * HB;
+    const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+    for (int q = threadIdx.x; q < HB * kFModelStride; q += 256)
+        mlds[q] = q < nh * kFModelStride ? a.fmodels[rec0 * kFModelStride + q] : 0.f;
+    __syncthreads();
+    const float *__restrict__ SX = a.SX + p0, *__restrict__ SY = a.SY + p0;
+    const float *__restrict__ DX = a.DX + p0, *__restrict__ DY = a.DY + p0;
+    const FmFrame fr = fm_frame(a.fbounds, prob);
+    int cnt = 0;
+    for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
+        float x1[P], y1[P], x2[P], y2[P];  // normalised frame
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int i = base + j * 64 + lane;
+            const bool in = i < n;
+            const int ii = in ? i : 0;
+            x1[j] = (SX[ii] - fr.c[0]) * fr.is;
+            y1[j] = (SY[ii] - fr.c[1]) * fr.is;
+            x2[j] = (DX[ii] - fr.c[2]) * fr.is;
+            // out-of-range lanes: y2 = 3e38 makes the pair a decided outlier (or undecided)
+            y2[j] = in ? (DY[ii] - fr.c[3]) * fr.is : 3.0e38f;
+        }
+        uint32_t undm = 0;  // bit h: this lane has an undecided pair with hypothesis h
+        for (int h = 0; h < nh; ++h) {
+            const float *m = mlds + h * kFModelStride;
+            int cc = 0;
+            uint64_t und = 0;
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const FmTest r = fm_test_f32(m, x1[j], y1[j], x2[j], y2[j]);
+                const uint64_t mi = __ballot(r.lt);
+                const uint64_t mo = __ballot(r.gt);
+                cc += __popcll(mi);
+                und |= ~(mi | mo);
+            }
+            cnt += (lane == h) ? cc : 0;
+            undm |= __builtin_amdgcn_inverse_ballot_w64(und) ? (1u << h) : 0u;
+        }
+        uint32_t wund = undm;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) wund |= (uint32_t)__shfl_xor((int)wund, o);
+        wund = __builtin_amdgcn_readfirstlane(wund);
+        if (__builtin_expect(wund != 0, 0)) {
+            const double T = (double)a.thr2[prob];
+#pragma unroll 1
+            while (wund) {
+                const int h = __builtin_ctz(wund);
+                wund &= wund - 1;
+                const float *m = mlds + h * kFModelStride;
+                const double *md = a.models + (rec0 + h) * kModelStride;
+                int cc = 0;
+#pragma unroll 1
+                for (int j = 0; j < P; ++j) {
+                    const int i = base + j * 64 + lane;
+                    bool ex = false;
+                    if ((undm >> h) & 1u) {
+                        const FmTest r = fm_test_f32(m, x1[j], y1[j], x2[j], y2[j]);
+                        if (!(r.lt | r.gt) && i < n)
+                            ex = md[kValidSlot] != 0.0 && fm_inlier(md, (double)SX[i], (double)SY[i], (double)DX[i],
+                                                                    (double)DY[i], T);
+                    }
+                    cc += __popcll(__ballot(ex));
+                }
+                cnt += (lane == h) ? cc : 0;
+            }
+        }
+    }
+    if (lane < HB) red[wave][lane] = cnt;
+    __syncthreads();
+    if (threadIdx.x < nh) {
+        const int s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        counts[rec0 + threadIdx.x] = s;
+    }
+}
+
 __global__ void k_fm_mask(HomArgs a, const int64_t *__restrict__ best, int64_t best0, uint8_t *__restrict__ mask) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
@@ -2523,8 +2786,18 @@ hipError_t launch_fm_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32
 hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
     if (a.max_n > 0 && a.max_n <= kLanePts)
         hipLaunchKernelGGL(k_fm_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
+    else if (a.fmodels)
+        hipLaunchKernelGGL((k_fm_score_f32<8, 32>), dim3(cdiv(H, 32), P), dim3(256), 0, s, a, hyp_begin, H, counts);
     else
         hipLaunchKernelGGL((k_fm_score<4, 32>), dim3(cdiv(H, 32), P), dim3(256), 0, s, a, hyp_begin, H, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_fm_bounds(const HomArgs &a, int32_t P, int32_t max_n, int *ws, hipStream_t s) {
+    hipLaunchKernelGGL(k_fm_bounds_init, dim3(cdiv(8 * P, 256)), dim3(256), 0, s, P, ws);
+    unsigned g = cdiv(max_n > 0 ? max_n : 1, 2048);
+    if (g > 64) g = 64;
+    hipLaunchKernelGGL(k_fm_bounds, dim3(g, P), dim3(256), 0, s, a, ws);
     return hipGetLastError();
 }
 

@@ -493,6 +493,19 @@ def test_fundamental_hypotheses_bit_exact(n, outl, H):
     assert _bits_equal(mdl[:, :9], om[:, :9])
 
 
+@pytest.mark.parametrize("n,outl,thr", [(20000, 0.8, 1.5), (5000, 0.3, 0.4), (5000, 0.5, 6.0), (3001, 0.8, 60.0)])
+def test_fundamental_f32_prefilter_equals_exact_kernel(n, outl, thr):
+    # the f32 Sampson pre-filter (k_fm_score_f32) must never change a decision: counts equal the
+    # all-f64 kernel's, and the thresholds put many pairs inside the pre-filter's band
+    pr = synth.fundamental_problem(n, outl, seed=n + 5)
+    st_f, c_f, _ = rsac.hypotheses("fundamental", pr["pts1"], pr["pts2"], None, 0, 3000, thr, seed=3)
+    st_e, c_e, _ = rsac.hypotheses("fundamental", pr["pts1"], pr["pts2"], None, 0, 3000, thr, seed=3,
+                                   exact_only=True)
+    np.testing.assert_array_equal(st_f, st_e)
+    np.testing.assert_array_equal(c_f, c_e)
+    assert c_e.max() > 0
+
+
 @pytest.mark.parametrize("n,outl", [(5000, 0.5), (50000, 0.8)])
 def test_fundamental_ransac_matches_restatement(n, outl):
     pr = synth.fundamental_problem(n, outl, seed=2)
