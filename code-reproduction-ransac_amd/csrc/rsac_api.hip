@@ -142,6 +142,7 @@ struct rsac_ctx {
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
     DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
+    DevBuf lmscr;                                              // multi-block LM refit: barrier + wave sums
     // pinned host staging
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask, h_epnp;
 };
@@ -378,6 +379,15 @@ struct LoopOut {
 // hypothesis' record, so the final mask / gather / refit see it.
 constexpr int kLoSteps = 4;
 
+// the multi-block LM refit's scratch (rsac_internal.h kLmScratchDoubles; barrier counters zeroed)
+double *lm_scratch(rsac_ctx *c, hipStream_t s) {
+    if (!c->lmscr.p) {
+        if (c->lmscr.ensure(sizeof(double) * kLmScratchDoubles) != hipSuccess) return nullptr;
+        if (hipMemsetAsync(c->lmscr.p, 0, 64, s) != hipSuccess) return nullptr;
+    }
+    return c->lmscr.as<double>();
+}
+
 int local_opt(rsac_ctx *c, const PnpArgs &a, int32_t n, ScanState &sc, double confidence, hipStream_t s,
               int32_t &improvements) {
     const size_t rec_bytes = sizeof(double) * kModelStride;
@@ -393,7 +403,7 @@ int local_opt(rsac_ctx *c, const PnpArgs &a, int32_t n, ScanState &sc, double co
     bool better = false;
     for (int step = 0; step < kLoSteps; ++step) {
         HIPCHK(hipMemcpyAsync(rec[1], rec[0], rec_bytes, hipMemcpyDeviceToDevice, s));
-        HIPCHK(launch_pnp_refine(a, 1, mk[0], rec[1], nullptr, s));
+        HIPCHK(launch_pnp_refine(a, 1, mk[0], rec[1], nullptr, s, lm_scratch(c, s), nullptr));
         HIPCHK(hipMemsetAsync(cnt + 1, 0, sizeof(int32_t), s));
         HIPCHK(launch_pnp_model_count(a, n, rec[1], mk[1], cnt + 1, s));
         int32_t c2 = 0;
@@ -658,7 +668,9 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
             HIPCHK(hipMemcpyAsync(d2, h2, b2, hipMemcpyHostToDevice, s));
             HIPCHK(launch_pnp_epnp_s3(a, P, dmask, d1, d2, c->bestmodels.as<double>(), s));
         }
-        if (flags & RSAC_F_REFINE) HIPCHK(launch_pnp_refine(a, P, dmask, c->bestmodels.as<double>(), nullptr, s));
+        if (flags & RSAC_F_REFINE)
+            HIPCHK(launch_pnp_refine(a, P, dmask, c->bestmodels.as<double>(), nullptr, s, lm_scratch(c, s),
+                                     st.off.data()));
         HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
                               hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -802,7 +814,7 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist};
+                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};

@@ -151,8 +151,11 @@ hipError_t launch_pnp_epnp_s1(const PnpArgs &a, int32_t P, const uint8_t *mask, 
                               EpnpStage1 *st1, hipStream_t s);
 hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, const EpnpStage1 *st1,
                               const EpnpStage2 *st2, double *models, hipStream_t s);
+// scratch (problems > 4096 points): kLmScratchDoubles doubles, its first 8 bytes zeroed once
+// (the grid barrier's counters); host_off: the problems' offsets on the host (P + 1)
+constexpr size_t kLmScratchDoubles = 8 + 2 * (32768 / 64) * 27;
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
-                             hipStream_t s);
+                             hipStream_t s, double *scratch, const int64_t *host_off);
 
 // mask + inlier count (atomically into *count, zeroed by the caller) of one model record, problem 0
 hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, int32_t *count,

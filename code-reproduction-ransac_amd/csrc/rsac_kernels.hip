@@ -2141,6 +2141,31 @@ struct GpuLmReducer {
     Cam k;
     double c0, c1, c2;  // centre of the refit frame
     double (*wsum)[kLmTerms];  // LDS [kLmThreads / 64][kLmTerms]
+    // more than one block per problem (S = lm_slots(n) > 512): this block owns slots
+    // [512 b, 512 b + 512) of the S; wave sums go through global scratch (two alternating
+    // buffers of [S / 64][kLmTerms]) and a grid barrier (bar: arrivals, generation)
+    int S = kLmThreads, nb = 1;
+    double *gws = nullptr;
+    unsigned *bar = nullptr;
+    int parity = 0;
+
+    __device__ void grid_barrier() {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();  // release this block's wave sums
+            const unsigned gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (atomicAdd(bar, 1u) == (unsigned)nb - 1) {
+                __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __threadfence();
+                atomicAdd(bar + 1, 1u);
+            } else {
+                while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            __threadfence();  // acquire the other blocks' wave sums
+        }
+        __syncthreads();
+    }
 
     __device__ void reduce(double *a, int nv, double *out) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2148,21 +2173,49 @@ struct GpuLmReducer {
         // overlap (each term's additions are the same as term by term)
         for (int o = 32; o > 0; o >>= 1)
             for (int q = 0; q < nv; ++q) a[q] = a[q] + __shfl_xor(a[q], o);
-        if (lane == 0)
-            for (int q = 0; q < nv; ++q) wsum[wave][q] = a[q];
-        __syncthreads();
-        for (int q = 0; q < nv; ++q) {
-            double s = wsum[0][q];
-            for (int w = 1; w < kLmThreads / 64; ++w) s = s + wsum[w][q];
-            out[q] = s;
+        if (nb == 1) {
+            if (lane == 0)
+                for (int q = 0; q < nv; ++q) wsum[wave][q] = a[q];
+            __syncthreads();
+            for (int q = 0; q < nv; ++q) {
+                double s = wsum[0][q];
+                for (int w = 1; w < kLmThreads / 64; ++w) s = s + wsum[w][q];
+                out[q] = s;
+            }
+            __syncthreads();  // wsum is reused by the next reduction
+            return;
         }
-        __syncthreads();  // wsum is reused by the next reduction
+        double *g = gws + (size_t)parity * (S / 64) * kLmTerms;
+        parity ^= 1;  // the next reduction writes the other buffer (a block may run ahead by one)
+        if (lane == 0)
+            for (int q = 0; q < nv; ++q) g[(blockIdx.x * (kLmThreads / 64) + wave) * kLmTerms + q] = a[q];
+        grid_barrier();
+        // thread q < nv sums term q over the S / 64 wave sums, left to right.  Plain loads: the
+        // barrier's acquire fence invalidated this CU's L1; batches of 32 loads are in flight
+        // ahead of the (sequential) additions.
+        if (threadIdx.x < nv) {
+            const int q = threadIdx.x;
+            const int nw = S / 64;
+            double s = 0.0;
+            for (int w0 = 0; w0 < nw; w0 += 32) {
+                double v[32];
+#pragma unroll
+                for (int j = 0; j < 32; ++j) v[j] = w0 + j < nw ? g[(w0 + j) * kLmTerms + q] : 0.0;
+#pragma unroll
+                for (int j = 0; j < 32; ++j)
+                    if (w0 + j < nw) s = (w0 + j == 0) ? v[j] : s + v[j];
+            }
+            wsum[0][q] = s;
+        }
+        __syncthreads();
+        for (int q = 0; q < nv; ++q) out[q] = wsum[0][q];
+        __syncthreads();
     }
     __device__ void normal(const double *R, const double *t, double *acc) {
         double a[kLmTerms];
         for (int q = 0; q < kLmTerms; ++q) a[q] = 0.0;
 #pragma unroll 4
-        for (int i = threadIdx.x; i < n; i += kLmThreads)
+        for (int i = blockIdx.x * kLmThreads + threadIdx.x; i < n; i += S)
             if (mask[i])
                 pnp_lm_point(R, t, k, (double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i],
                              (double)V[i], a);
@@ -2191,7 +2244,7 @@ struct GpuLmReducer {
     __device__ double cost(const double *R, const double *t) {
         double a = 0.0, out;
 #pragma unroll 4
-        for (int i = threadIdx.x; i < n; i += kLmThreads)
+        for (int i = blockIdx.x * kLmThreads + threadIdx.x; i < n; i += S)
             if (mask[i])
                 a += pnp_lm_cost_point(R, t, k, (double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i],
                                        (double)V[i]);
@@ -2200,20 +2253,33 @@ struct GpuLmReducer {
     }
 };
 
+// one problem per blockIdx.y (prob_base + y); blocks x < lm_slots(n) / 512 of it take part
+// (x > 0 only when the problem has more than 4096 points).  Multi-block problems need all
+// their blocks co-resident: the launcher keeps them to one problem per launch (<= 64 blocks).
 __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint8_t *__restrict__ mask,
-                                                           double *__restrict__ models, int32_t *__restrict__ iters) {
+                                                           double *__restrict__ models, int32_t *__restrict__ iters,
+                                                           int prob_base, double *gws, unsigned *bar) {
     __shared__ double wsum[kLmThreads / 64][kLmTerms];
-    const int prob = blockIdx.x;
+    const int prob = prob_base + blockIdx.y;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int S = lm_slots(n);
+    const int nb = S / kLmThreads;
+    if ((int)blockIdx.x >= nb) return;  // block-uniform; this problem uses fewer blocks
+    if ((nb > 1) != (gws != nullptr)) return;  // the other launch's problem (launch_pnp_refine)
     double *m = models + (int64_t)prob * kModelStride;
     if (m[kValidSlot] == 0.0) {  // no model: block-uniform exit
-        if (threadIdx.x == 0 && iters) iters[prob] = 0;
+        if (threadIdx.x == 0 && blockIdx.x == 0 && iters) iters[prob] = 0;
         return;
     }
-    const int64_t p0 = a.offsets[prob];
     const double *cm = a.cams + 4 * prob;
     const double c[3] = {(double)a.X[p0], (double)a.Y[p0], (double)a.Z[p0]};
     GpuLmReducer red{a.X + p0, a.Y + p0, a.Z + p0, a.U + p0, a.V + p0, mask + p0,
-                     (int)(a.offsets[prob + 1] - p0), Cam{cm[0], cm[1], cm[2], cm[3]}, c[0], c[1], c[2], wsum};
+                     n, Cam{cm[0], cm[1], cm[2], cm[3]}, c[0], c[1], c[2], wsum};
+    red.S = S;
+    red.nb = nb;
+    red.gws = gws;
+    red.bar = bar;
     double R[9], t[3];
     for (int j = 0; j < 9; ++j) R[j] = m[j];
     for (int j = 0; j < 3; ++j) t[j] = m[9 + j];
@@ -2224,8 +2290,9 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     red.dump();
 #endif
     lm_from_centred(R, c, t);
+    if (nb > 1) red.grid_barrier();  // every block has read m before block 0 overwrites it
     __syncthreads();  // every thread has read m before thread 0 overwrites it
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
         for (int j = 0; j < 9; ++j) m[j] = R[j];
         for (int j = 0; j < 3; ++j) m[9 + j] = t[j];
         if (iters) iters[prob] = it;
@@ -2361,8 +2428,25 @@ hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, 
 }
 
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(k_pnp_refine, dim3(P), dim3(kLmThreads), 0, s, a, mask, models, iters);
+                             hipStream_t s, double *scratch, const int64_t *host_off) {
+    // every problem of up to 4096 points (and, with host_off unknown, every problem) in one
+    // launch, one block each; each larger problem in a launch of its own, lm_slots(n) / 512
+    // blocks (<= 64, all co-resident) that meet at grid barriers
+    const int nb_max = lm_slots(a.max_n) / kLmThreads;
+    hipLaunchKernelGGL(k_pnp_refine, dim3(1, P), dim3(kLmThreads), 0, s, a, mask, models, iters, 0,
+                       (double *)nullptr, (unsigned *)nullptr);
+    if (nb_max > 1) {
+        if (!scratch) return hipErrorInvalidValue;
+        unsigned *bar = (unsigned *)scratch;  // zeroed by the caller once; back to 0 after every barrier
+        double *gws = scratch + 8;
+        for (int p = 0; p < P; ++p) {
+            const int np = host_off ? (int)(host_off[p + 1] - host_off[p]) : a.max_n;
+            const int nb = lm_slots(np) / kLmThreads;
+            if (nb > 1)
+                hipLaunchKernelGGL(k_pnp_refine, dim3(nb, 1), dim3(kLmThreads), 0, s, a, mask, models, iters, p, gws,
+                                   bar);
+        }
+    }
     return hipGetLastError();
 }
 

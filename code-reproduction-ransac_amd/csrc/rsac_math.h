@@ -648,11 +648,19 @@ RSAC_HD bool fm_inlier(const double *F, double x1, double y1, double x2, double 
 // coordinates would otherwise couple rotation and translation badly.
 //
 // One summation order on every backend (GPU kernel k_pnp_refine, host
-// rsac_pnp_refine, oracle orc_pnp_refine): kLmThreads strided per-thread
-// partials (point i to thread i % kLmThreads, ascending), a 64-lane butterfly
-// per wave (x += x[lane ^ o], o = 32 .. 1), then the wave sums left to right.
+// rsac_pnp_refine, oracle orc_pnp_refine): S = lm_slots(n) strided per-slot
+// partials (point i to slot i % S, ascending), a 64-lane butterfly per wave of
+// 64 slots (x += x[lane ^ o], o = 32 .. 1), then the S / 64 wave sums left to
+// right.  S = 512 up to 4096 points; larger problems get more slots (at most 8
+// points each, S <= 32768), so the GPU spreads them over S / 512 blocks.
 // ---------------------------------------------------------------------------
 constexpr int kLmThreads = 512;
+constexpr int kLmMaxSlots = 32768;
+RSAC_HD int lm_slots(int n) {
+    int S = kLmThreads;
+    while (S < kLmMaxSlots && n > 8 * S) S *= 2;
+    return S;
+}
 constexpr int kLmTerms = 27;  // J^T J lower triangle (21, row-major packed), J^T r (6)
 constexpr int kLmMaxIter = 20;
 constexpr int kRedMax = 40;   // widest reduction (EPnP's pair sums)
@@ -805,28 +813,24 @@ RSAC_HD void lm_from_centred(const double *R, const double *c, double *t) {
 // Host/oracle-side mirror of the GPU reduction: sum f(i, acc) over points with
 // mask[i] != 0 in the kLmThreads-strided, wave-butterfly order.  part: scratch of
 // kLmThreads * nv doubles.
+// slots: S (lm_slots(n) for the LM refit, kLmThreads for EPnP); part: S * nv doubles.
 template <class F>
-inline void lm_reduce_host(int n, const uint8_t *mask, int nv, double *part, double *out, F f) {
-    for (int q = 0; q < kLmThreads * nv; ++q) part[q] = 0.0;
-    for (int tid = 0; tid < kLmThreads; ++tid)
-        for (int i = tid; i < n; i += kLmThreads)
+inline void lm_reduce_host(int n, const uint8_t *mask, int nv, double *part, double *out, F f, int slots = kLmThreads) {
+    for (int q = 0; q < slots * nv; ++q) part[q] = 0.0;
+    for (int tid = 0; tid < slots; ++tid)
+        for (int i = tid; i < n; i += slots)
             if (mask[i]) f(i, part + tid * nv);
-    double wsum[kLmThreads / 64][kRedMax];
     double v[64], w[64];
-    for (int wv = 0; wv < kLmThreads / 64; ++wv)
+    for (int q = 0; q < nv; ++q) out[q] = 0.0;
+    for (int wv = 0; wv < slots / 64; ++wv)
         for (int q = 0; q < nv; ++q) {
             for (int l = 0; l < 64; ++l) v[l] = part[(wv * 64 + l) * nv + q];
             for (int o = 32; o > 0; o >>= 1) {
                 for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
                 for (int l = 0; l < 64; ++l) v[l] = w[l];
             }
-            wsum[wv][q] = v[0];
+            out[q] = wv == 0 ? v[0] : out[q] + v[0];  // wave sums left to right
         }
-    for (int q = 0; q < nv; ++q) {
-        double s = wsum[0][q];
-        for (int wv = 1; wv < kLmThreads / 64; ++wv) s = s + wsum[wv][q];
-        out[q] = s;
-    }
 }
 
 // ---------------------------------------------------------------------------
