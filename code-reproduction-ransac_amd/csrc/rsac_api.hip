@@ -143,7 +143,9 @@ struct rsac_ctx {
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
     DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
     DevBuf lmscr;                                              // multi-block LM refit: barrier + wave sums
+    DevBuf scanrec;                                            // single-round scans: improvement records
     // pinned host staging
+    PinBuf h_scanrec;
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask, h_epnp;
 };
 
@@ -516,6 +518,43 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
             HIPCHK(launch_hom_score(*ha, P, hb, Hr, c->counts.as<int32_t>(), s));
         }
         HIPCHK(hipEventRecord(c->ev2, s));
+        // one round, no LO: the device lists each problem's scan improvements (prefix-maximum
+        // records) and the host replays the exact scan on them; otherwise every count comes back
+        std::vector<int> full;  // problems scanned from their full count / status rows
+        if (!adaptive && !lo && hb == 0 && Hr == H) {
+            HIPCHK(c->scanrec.ensure(sizeof(ScanRecords) * P));
+            HIPCHK(c->h_scanrec.ensure(sizeof(ScanRecords) * P));
+            HIPCHK(launch_scan_records(c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, P, (int32_t)Hr,
+                                       model_points, c->scanrec.as<ScanRecords>(), s));
+            HIPCHK(hipMemcpyAsync(c->h_scanrec.p, c->scanrec.p, sizeof(ScanRecords) * P, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            const ScanRecords *rec = c->h_scanrec.as<ScanRecords>();
+            for (int p = 0; p < P; ++p) {
+                if (rec[p].nrec < 0) {
+                    full.push_back(p);
+                    continue;
+                }
+                const int np = (int)(st.off[p + 1] - st.off[p]);
+                scan_records(out.scan[p], rec[p].idx, rec[p].cnt, rec[p].nrec, rec[p].first_neg, (int64_t)Hr, np,
+                             model_points, confidence);
+            }
+            if (!full.empty()) {
+                HIPCHK(copy_rows(c->h_counts.p, sizeof(int32_t) * Hr, c->counts.as<int32_t>() + hb,
+                                 sizeof(int32_t) * stride, sizeof(int32_t) * Hr, P, hipMemcpyDeviceToHost, s));
+                HIPCHK(copy_rows(c->h_status.p, Hr, c->status.as<int8_t>() + hb, stride, Hr, P, hipMemcpyDeviceToHost,
+                                 s));
+                HIPCHK(hipStreamSynchronize(s));
+                for (int p : full) {
+                    const int np = (int)(st.off[p + 1] - st.off[p]);
+                    scan_step(out.scan[p], c->h_counts.as<int32_t>() + (size_t)p * Hr,
+                              c->h_status.as<int8_t>() + (size_t)p * Hr, Hr, np, model_points, confidence);
+                }
+            }
+            add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
+            out.rounds++;
+            out.scored += (int64_t)Hr;
+            break;
+        }
         HIPCHK(copy_rows(c->h_counts.p, sizeof(int32_t) * Hr, c->counts.as<int32_t>() + hb,
                                 sizeof(int32_t) * stride, sizeof(int32_t) * Hr, P, hipMemcpyDeviceToHost, s));
         HIPCHK(copy_rows(c->h_status.p, Hr, c->status.as<int8_t>() + hb, stride, Hr, P,
@@ -814,7 +853,7 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr};
+                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr, &c->scanrec};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};

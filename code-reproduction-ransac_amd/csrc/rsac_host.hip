@@ -1,3 +1,4 @@
+#include <algorithm>
 // rsac_host.hip -- host-side sequential parts of the driver (see rsac_host.h).
 #include "rsac_host.h"
 
@@ -84,6 +85,21 @@ void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_
     }
     s.iter = i;
     if (i >= s.niters) s.done = true;
+}
+
+void scan_records(ScanState &s, const int32_t *idx, const int32_t *cnt, int nrec, int32_t first_neg, int64_t H, int n,
+                  int model_points, double confidence) {
+    // scan_step stops at the first index >= niters (niters only shrinks) or with status < 0;
+    // between records nothing changes
+    for (int r = 0; r < nrec; ++r) {
+        const int64_t stop = std::min<int64_t>(first_neg, s.niters);
+        if (idx[r] >= stop) break;
+        s.best = idx[r];
+        s.max_good = cnt[r];
+        s.niters = update_num_iters(confidence, (double)(n - cnt[r]) / n, model_points, (int)s.niters);
+    }
+    s.iter = std::min<int64_t>(std::min<int64_t>(first_neg, s.niters), H);
+    s.done = true;
 }
 
 void rodrigues_v2m(const double r[3], double R[9]) {

@@ -103,6 +103,19 @@ hipError_t launch_pnp_key_finish(const PnpArgs &a, int32_t n, const unsigned lon
 hipError_t launch_key_model(const double *models, const unsigned long long *key, int64_t rng_base, double *out,
                             hipStream_t s);
 
+// Single-round scan support (non-adaptive runs without LO): the scan's improvements are the
+// strict prefix maxima of the counts of valid hypotheses (status > 0) above model_points - 1,
+// up to the first status < 0.  k_scan_records lists them per problem, so the host runs the
+// exact scan (RANSACUpdateNumIters with the host's libm) on a few records instead of copying
+// every count.  nrec = -1: more than kScanRecs records (the caller falls back to all counts).
+constexpr int kScanRecs = 14;
+struct ScanRecords {
+    int32_t nrec, first_neg;  // first_neg = H when no status < 0
+    int32_t idx[kScanRecs], cnt[kScanRecs];
+};
+hipError_t launch_scan_records(const int32_t *counts, const int8_t *status, int64_t stride, int32_t P, int32_t H,
+                               int model_points, ScanRecords *out, hipStream_t s);
+
 // best packed key of counts[0, H) (+ its model record -> model_out[16]);
 // key = 0 when no hypothesis has a model with >= 1 inlier
 hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t H, int64_t hyp_begin,

@@ -1730,6 +1730,55 @@ __global__ __launch_bounds__(256) void k_best_key(const int32_t *__restrict__ co
     }
 }
 
+// one wave per problem: 64 hypotheses per step, the running maximum carried across steps
+__global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict__ counts,
+                                                      const int8_t *__restrict__ status, int64_t stride, int32_t P,
+                                                      int32_t H, int model_points, ScanRecords *__restrict__ out) {
+    const int prob = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (prob >= P) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int32_t *c = counts + (int64_t)prob * stride;
+    const int8_t *st = status + (int64_t)prob * stride;
+    int floor_c = model_points - 1;  // the scan's floor: max(s - 1, best count so far)
+    int nrec = 0, first_neg = H;
+    ScanRecords &o = out[prob];
+    for (int b = 0; b < H; b += 64) {
+        const int i = b + lane;
+        const int8_t sv = i < H ? st[i] : (int8_t)0;
+        const uint64_t neg = __ballot(sv < 0);
+        const int lim = neg ? b + __builtin_ctzll(neg) : H;  // hypotheses before the first status < 0
+        int v = (i < lim && sv > 0) ? c[i] : -1;
+        // candidates: above the floor; take them in order, each raising the floor
+        uint64_t cand = __ballot(v > floor_c);
+        while (cand) {
+            const int l = __builtin_ctzll(cand);
+            const int cv = __shfl(v, l);
+            if (nrec < kScanRecs && lane == 0) {
+                o.idx[nrec] = b + l;
+                o.cnt[nrec] = cv;
+            }
+            ++nrec;
+            floor_c = cv;
+            cand = __ballot(v > floor_c && lane > l);
+        }
+        if (neg) {
+            first_neg = lim;
+            break;
+        }
+    }
+    if (lane == 0) {
+        o.nrec = nrec <= kScanRecs ? nrec : -1;
+        o.first_neg = first_neg;
+    }
+}
+
+hipError_t launch_scan_records(const int32_t *counts, const int8_t *status, int64_t stride, int32_t P, int32_t H,
+                               int model_points, ScanRecords *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_records, dim3((P + 3) / 4), dim3(256), 0, s, counts, status, stride, P, H, model_points,
+                       out);
+    return hipGetLastError();
+}
+
 // model record of the key's hypothesis -> out[16] (zeros when key == 0)
 __global__ void k_key_model(const double *__restrict__ models, const unsigned long long *__restrict__ key,
                             int64_t hyp_begin, double *__restrict__ out) {
