@@ -46,6 +46,9 @@ struct PnpArgs {
     int *mx_count;                 // records written (reset by the solve / fmodels kernels)
     int mx_cap;
     unsigned long long *mx_stats;  // diagnostics (RSAC_MX_STATS=1): fallback tiles, undecided pairs
+    // set when the solve kernel precedes the scoring launch: the solve zeroes these counts, so a
+    // split scoring launch (atomic count accumulation) needs no memset
+    int32_t *counts_out;
     int exact_only;
     // optional fused reduction (single problem): max over the scored hypotheses of
     // (count << 32) | (0xFFFFFFFF - low32(rng_base + h)), atomically into *best_key

@@ -161,6 +161,45 @@ __device__ __forceinline__ double frame_bound(const int *__restrict__ ws, int32_
     return B * (1.0 + 4.0 * kU32) + 1e-30;
 }
 
+// k_pnp_bounds for one problem in one 1024-thread block: min / max written directly (the
+// encoding of k_pnp_init + atomics, identical values), best key and work queue reset
+__global__ __launch_bounds__(1024) void k_pnp_bounds1(PnpArgs a, int *__restrict__ ws) {
+    __shared__ float sl[16][5], sh[16][5];
+    const int64_t p0 = a.offsets[0];
+    const int n = (int)(a.offsets[1] - p0);
+    float lo[5], hi[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const float v[5] = {a.X[p0 + i], a.Y[p0 + i], a.Z[p0 + i], a.U[p0 + i], a.V[p0 + i]};
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { lo[k] = fminf(lo[k], v[k]); hi[k] = fmaxf(hi[k], v[k]); }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
+        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { sl[wave][k] = lo[k]; sh[wave][k] = hi[k]; }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        const int k = threadIdx.x;
+        float l = sl[0][k], h = sh[0][k];
+        for (int w = 1; w < 16; ++w) { l = fminf(l, sl[w][k]); h = fmaxf(h, sh[w][k]); }
+        // as k_pnp_init (0x7F7F7F7F / 0x80808080) then atomicMin / Max of f2ord
+        ws[k] = n > 0 ? min(0x7F7F7F7F, f2ord(l)) : 0x7F7F7F7F;
+        ws[5 + k] = n > 0 ? max((int)0x80808080, f2ord(h)) : (int)0x80808080;
+    }
+    if (threadIdx.x == 0) {
+        if (a.best_key) *a.best_key = 0ull;
+        *a.queue = 0;
+    }
+}
+
 // Per problem: frame = {c0 c1 c2 (bbox centre), B >= |XC|inf, rho >= |XC - (Xf - c)|,
 // max|Xf|, wmax (bound on |x/z| of any projection within thr of a pixel), 0};
 // fconst = {fx fy cx cy T 2.002 sqrt(T) 1e-6 T thr 2/fx 2/fy cu cv cc0} (see the scoring kernel).
@@ -443,6 +482,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
     m[kValidSlot] = st > 0 ? 1.0 : 0.0;
     a.status[rec] = st;
+    if (a.counts_out) a.counts_out[rec] = 0;  // the scoring launch that follows may accumulate
     if (a.hmodels)  // the MFMA scoring kernel reads only these
         write_hmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
                      a.fconst + (int64_t)prob * kFconstStride, a.hmodels + rec * kHModelStride);
@@ -785,9 +825,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         __syncthreads();
         if (split == 1) {
             if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
-        } else if (wave == 0 && lane < nh) {
-            const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-            if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
+        } else {
+            if (wave == 0 && lane < nh) {
+                const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+                if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
+            }
         }
         __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
     }
@@ -1820,10 +1862,15 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
                             double *frame, float *fconst, hipStream_t s, uint4 *PF) {
-    hipLaunchKernelGGL(k_pnp_init, dim3(1), dim3(256), 0, s, P, ws, a.best_key, a.queue);
-    unsigned g = cdiv(max_n > 0 ? max_n : 1, 2048);
-    if (g > 32) g = 32;
-    hipLaunchKernelGGL(k_pnp_bounds, dim3(g, P), dim3(256), 0, s, a, P, ws);
+    if (P == 1 && max_n <= 65536) {
+        // one block: no atomics, so no initialisation launch (it also resets the key and queue)
+        hipLaunchKernelGGL(k_pnp_bounds1, dim3(1), dim3(1024), 0, s, a, ws);
+    } else {
+        hipLaunchKernelGGL(k_pnp_init, dim3(1), dim3(256), 0, s, P, ws, a.best_key, a.queue);
+        unsigned g = cdiv(max_n > 0 ? max_n : 1, 2048);
+        if (g > 32) g = 32;
+        hipLaunchKernelGGL(k_pnp_bounds, dim3(g, P), dim3(256), 0, s, a, P, ws);
+    }
     unsigned g2 = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g2 > 1024) g2 = 1024;
     hipLaunchKernelGGL(k_pnp_center, dim3(g2, P), dim3(256), 0, s, a, P, ws, frame, fconst, XC, YC, ZC, PF);
@@ -1873,10 +1920,17 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
             split = (int)std::min<int64_t>(chunks, std::max<int64_t>(1, (8 * (int64_t)resident + units - 1) / units));
         else if (!a.best_key && units * 2 <= resident)
             split = (int)std::min<int64_t>(chunks, (resident + units - 1) / units);
-        if (split > 1 && P == 1)
-            (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
-        else if (split > 1)
-            (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P, s);
+        // counts already zeroed by the solve kernel (a.counts_out set): no memset.  The best key
+        // is reduced afterwards by k_best_key (a completion counter per tile would need a fence
+        // per unit, which costs more than the launch)
+        const bool zeroed = a.counts_out == counts;
+        if (split > 1 && !zeroed) {
+            if (P == 1)
+                (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
+            else
+                (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P,
+                                       s);
+        }
         units *= split;
         const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
         PnpArgs ka = a;
