@@ -47,16 +47,17 @@ def test_host_only_helpers():
     assert rsac.update_num_iters(0.99, 0.5, 4, 5000) == 71
 
 
-def test_host_refine_matches_oracle():
+@pytest.mark.parametrize("n", [500, 9000, 70000])  # 9000 / 70000: lm_slots(n) = 2048 / 16384 (multi-block order)
+def test_host_refine_matches_oracle(n):
     import pyoracle as O
     import rsac
     from rsac import synth
-    pr = synth.pnp_problem(500, 0.0, seed=5, noise_px=0.5)
+    pr = synth.pnp_problem(n, 0.0, seed=5, noise_px=0.5)
     R0 = synth.random_rotation(np.random.default_rng(9)) * 0 + pr["R"]
     t0 = pr["t"] + np.array([0.5, -0.3, 0.2])
     R, t = rsac.refine_pose(pr["points2d"], pr["points3d"], pr["K"], R0, t0)
     soa = O.soa_pnp(pr["points3d"], pr["points2d"])
-    Ro, to, _ = O.pnp_refine(soa, np.ones(500, np.uint8), O.cam_from_K(pr["K"]), R0, t0)
+    Ro, to, _ = O.pnp_refine(soa, np.ones(n, np.uint8), O.cam_from_K(pr["K"]), R0, t0)
     # same arithmetic and summation order (the GPU kernel's) on both sides: bit-identical
     np.testing.assert_array_equal(R, Ro)
     np.testing.assert_array_equal(t, to)
