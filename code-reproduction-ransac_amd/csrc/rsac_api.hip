@@ -10,6 +10,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <atomic>
@@ -528,10 +529,11 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
             HIPCHK(launch_hom_score(*ha, P, hb, Hr, c->counts.as<int32_t>(), s));
         }
         HIPCHK(hipEventRecord(c->ev2, s));
-        // one round, no LO: the device lists each problem's scan improvements (prefix-maximum
-        // records) and the host replays the exact scan on them; otherwise every count comes back
+        // the first round without LO: the device lists each problem's scan improvements
+        // (prefix-maximum records) and the host replays the exact scan on them; later rounds (and
+        // LO) copy every count
         std::vector<int> full;  // problems scanned from their full count / status rows
-        if (!adaptive && !lo && hb == 0 && Hr == H) {
+        if (!lo && hb == 0) {
             HIPCHK(c->scanrec.ensure(sizeof(ScanRecords) * P));
             HIPCHK(c->h_scanrec.ensure(sizeof(ScanRecords) * P));
             HIPCHK(launch_scan_records(c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, P, (int32_t)Hr,
@@ -546,7 +548,7 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
                 }
                 const int np = (int)(st.off[p + 1] - st.off[p]);
                 scan_records(out.scan[p], rec[p].idx, rec[p].cnt, rec[p].nrec, rec[p].first_neg, (int64_t)Hr, np,
-                             model_points, confidence);
+                             model_points, confidence);  // the first round: the scan starts at 0
             }
             if (!full.empty()) {
                 HIPCHK(copy_rows(c->h_counts.p, sizeof(int32_t) * Hr, c->counts.as<int32_t>() + hb,
@@ -563,7 +565,10 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
             add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
             out.rounds++;
             out.scored += (int64_t)Hr;
-            break;
+            bool all_done = true;
+            for (int p = 0; p < P; ++p) all_done = all_done && out.scan[p].done;
+            if (all_done) break;
+            continue;  // later rounds copy their counts
         }
         HIPCHK(copy_rows(c->h_counts.p, sizeof(int32_t) * Hr, c->counts.as<int32_t>() + hb,
                                 sizeof(int32_t) * stride, sizeof(int32_t) * Hr, P, hipMemcpyDeviceToHost, s));
@@ -611,12 +616,13 @@ int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const L
     // one problem: the record index goes as a kernel argument (no upload)
     const int64_t *dbest = P == 1 ? nullptr : c->best.as<int64_t>();
     if (P > 1) HIPCHK(hipMemcpyAsync(c->best.p, hb, sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
-    HIPCHK(launch_gather_models(c->models.as<double>(), dbest, P, c->bestmodels.as<double>(), s, hb[0]));
-    HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
-                          hipMemcpyDeviceToHost, s));
+    const int64_t N = st.total;
+    // PnP: the mask kernel also gathers the winners' records (one launch fewer)
+    const bool fused_gather = model == Model::PnP && N > 0;
+    if (!fused_gather)
+        HIPCHK(launch_gather_models(c->models.as<double>(), dbest, P, c->bestmodels.as<double>(), s, hb[0]));
     int32_t max_n = 0;
     for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
-    const int64_t N = st.total;
     uint8_t *dmask;
     if (flags & RSAC_F_DEVICE_OUT) {
         dmask = mask_out;
@@ -626,12 +632,16 @@ int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const L
     }
     if (N > 0) {
         if (model == Model::PnP)
-            HIPCHK(launch_pnp_mask(*(PnpArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
+            HIPCHK(launch_pnp_mask(*(PnpArgs *)args, P, max_n, dbest, dmask, s, hb[0], c->bestmodels.as<double>()));
         else if (model == Model::Fm)
             HIPCHK(launch_fm_mask(*(HomArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
         else
             HIPCHK(launch_hom_mask(*(HomArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
     }
+    // the winners' records for the host (a refit copies the refined ones instead)
+    if (!defer_sync)
+        HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
+                              hipMemcpyDeviceToHost, s));
     if (!(flags & RSAC_F_DEVICE_OUT) && mask_out && N > 0) {
         HIPCHK(c->h_mask.ensure(N));
         HIPCHK(hipMemcpyAsync(c->h_mask.p, dmask, N, hipMemcpyDeviceToHost, s));

@@ -50,7 +50,7 @@ struct ScanState {
 void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_t count, int n, int model_points,
                double confidence, bool stop_on_improve = false);
 
-// the scan of one whole round [0, H) from its improvement records (rsac_internal.h
+// the first round [0, H) of a fresh scan from its improvement records (rsac_internal.h
 // ScanRecords): identical to scan_step over the full rows
 void scan_records(ScanState &s, const int32_t *idx, const int32_t *cnt, int nrec, int32_t first_neg, int64_t H, int n,
                   int model_points, double confidence);

@@ -89,8 +89,8 @@ void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_
 
 void scan_records(ScanState &s, const int32_t *idx, const int32_t *cnt, int nrec, int32_t first_neg, int64_t H, int n,
                   int model_points, double confidence) {
-    // scan_step stops at the first index >= niters (niters only shrinks) or with status < 0;
-    // between records nothing changes
+    // the first round [0, H) of a fresh scan (s reset).  scan_step stops at the first index
+    // >= niters (niters only shrinks) or with status < 0; between records nothing changes
     for (int r = 0; r < nrec; ++r) {
         const int64_t stop = std::min<int64_t>(first_neg, s.niters);
         if (idx[r] >= stop) break;
@@ -98,8 +98,15 @@ void scan_records(ScanState &s, const int32_t *idx, const int32_t *cnt, int nrec
         s.max_good = cnt[r];
         s.niters = update_num_iters(confidence, (double)(n - cnt[r]) / n, model_points, (int)s.niters);
     }
-    s.iter = std::min<int64_t>(std::min<int64_t>(first_neg, s.niters), H);
-    s.done = true;
+    // as scan_step over [0, H): it stops at min(first_neg, niters) inside the round, else at H
+    const int64_t stop = std::min<int64_t>(first_neg, s.niters);
+    if (stop < H) {
+        s.iter = stop;
+        s.done = true;
+    } else {
+        s.iter = H;
+        s.done = H >= s.niters;
+    }
 }
 
 void rodrigues_v2m(const double r[3], double R[9]) {

@@ -146,7 +146,7 @@ bool score_variant_mx();        // the selected variant is an MFMA one (needs PF
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                           hipStream_t s, int64_t best0 = -1);
+                           hipStream_t s, int64_t best0 = -1, double *model_out = nullptr);
 hipError_t launch_hom_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
 hipError_t launch_hom_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
@@ -169,7 +169,7 @@ hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, 
                               const EpnpStage2 *st2, double *models, hipStream_t s);
 // scratch (problems > 4096 points): kLmScratchDoubles doubles, its first 8 bytes zeroed once
 // (the grid barrier's counters); host_off: the problems' offsets on the host (P + 1)
-constexpr size_t kLmScratchDoubles = 8 + 2 * (32768 / 64) * 27;
+constexpr size_t kLmScratchDoubles = 8 + 2 * (32768 / 64) * 28;
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
                              hipStream_t s, double *scratch, const int64_t *host_off);
 

@@ -1475,11 +1475,16 @@ __global__ __launch_bounds__(256) void k_pnp_score(PnpArgs a, int64_t hyp_begin,
 }
 
 // mask of one model per problem (best[prob] indexes the models buffer; <0 = none)
-__global__ void k_pnp_mask(PnpArgs a, const int64_t *__restrict__ best, int64_t best0, uint8_t *__restrict__ mask) {
+// model_out (optional): block 0 of every problem also copies the winner's record there
+// (k_gather_models' output, one launch fewer)
+__global__ void k_pnp_mask(PnpArgs a, const int64_t *__restrict__ best, int64_t best0, uint8_t *__restrict__ mask,
+                           double *__restrict__ model_out) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
     const int64_t b = best ? best[prob] : best0;  // best0: the one problem's record, no upload
+    if (model_out && blockIdx.x == 0 && threadIdx.x < kModelStride)
+        model_out[(int64_t)prob * kModelStride + threadIdx.x] = b >= 0 ? a.models[b * kModelStride + threadIdx.x] : 0.0;
     const double *c = a.cams + 4 * prob;
     const Cam k{c[0], c[1], c[2], c[3]};
     const float thr2 = a.thr2[prob];
@@ -2070,10 +2075,10 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                           hipStream_t s, int64_t best0) {
+                           hipStream_t s, int64_t best0, double *model_out) {
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g > 1024) g = 1024;
-    hipLaunchKernelGGL(k_pnp_mask, dim3(g, P), dim3(256), 0, s, a, best, best0, mask);
+    hipLaunchKernelGGL(k_pnp_mask, dim3(g, P), dim3(256), 0, s, a, best, best0, mask, model_out);
     return hipGetLastError();
 }
 
@@ -2237,16 +2242,19 @@ hipError_t launch_loc_score(const double *src, const double *dst, const uint8_t 
 // reductions use the summation order the host (rsac_pnp_refine) and the oracle
 // mirror, so the refined pose is bit-identical on every backend.
 // ---------------------------------------------------------------------------
+constexpr int kLmRed = kLmTerms + 1;  // widest LM reduction: normal equations + cost
+
 struct GpuLmReducer {
+    static constexpr bool kFused = true;  // cost_normal: one pass for a candidate (rsac_math.h)
     const float *X, *Y, *Z, *U, *V;
     const uint8_t *mask;
     int n;
     Cam k;
     double c0, c1, c2;  // centre of the refit frame
-    double (*wsum)[kLmTerms];  // LDS [kLmThreads / 64][kLmTerms]
+    double (*wsum)[kLmRed];  // LDS [kLmThreads / 64][kLmRed]
     // more than one block per problem (S = lm_slots(n) > 512): this block owns slots
     // [512 b, 512 b + 512) of the S; wave sums go through global scratch (two alternating
-    // buffers of [S / 64][kLmTerms]) and a grid barrier (bar: arrivals, generation)
+    // buffers of [S / 64][kLmRed]) and a grid barrier (bar: arrivals, generation)
     int S = kLmThreads, nb = 1;
     double *gws = nullptr;
     unsigned *bar = nullptr;
@@ -2288,10 +2296,10 @@ struct GpuLmReducer {
             __syncthreads();  // wsum is reused by the next reduction
             return;
         }
-        double *g = gws + (size_t)parity * (S / 64) * kLmTerms;
+        double *g = gws + (size_t)parity * (S / 64) * kLmRed;
         parity ^= 1;  // the next reduction writes the other buffer (a block may run ahead by one)
         if (lane == 0)
-            for (int q = 0; q < nv; ++q) g[(blockIdx.x * (kLmThreads / 64) + wave) * kLmTerms + q] = a[q];
+            for (int q = 0; q < nv; ++q) g[(blockIdx.x * (kLmThreads / 64) + wave) * kLmRed + q] = a[q];
         grid_barrier();
         // thread q < nv sums term q over the S / 64 wave sums, left to right.  Plain loads: the
         // barrier's acquire fence invalidated this CU's L1; batches of 32 loads are in flight
@@ -2303,7 +2311,7 @@ struct GpuLmReducer {
             for (int w0 = 0; w0 < nw; w0 += 32) {
                 double v[32];
 #pragma unroll
-                for (int j = 0; j < 32; ++j) v[j] = w0 + j < nw ? g[(w0 + j) * kLmTerms + q] : 0.0;
+                for (int j = 0; j < 32; ++j) v[j] = w0 + j < nw ? g[(w0 + j) * kLmRed + q] : 0.0;
 #pragma unroll
                 for (int j = 0; j < 32; ++j)
                     if (w0 + j < nw) s = (w0 + j == 0) ? v[j] : s + v[j];
@@ -2354,6 +2362,23 @@ struct GpuLmReducer {
         reduce(&a, 1, &out);
         return out;
     }
+    // cost(R, t) and normal(R, t) in one pass: per-slot partials and reductions are term by
+    // term the same as the separate passes'
+    __device__ double cost_normal(const double *R, const double *t, double *acc) {
+        double a[kLmRed];
+        for (int q = 0; q < kLmRed; ++q) a[q] = 0.0;
+#pragma unroll 2
+        for (int i = blockIdx.x * kLmThreads + threadIdx.x; i < n; i += S)
+            if (mask[i]) {
+                const double Xd = (double)X[i] - c0, Yd = (double)Y[i] - c1, Zd = (double)Z[i] - c2;
+                pnp_lm_point(R, t, k, Xd, Yd, Zd, (double)U[i], (double)V[i], a);
+                a[kLmTerms] += pnp_lm_cost_point(R, t, k, Xd, Yd, Zd, (double)U[i], (double)V[i]);
+            }
+        double out[kLmRed];
+        reduce(a, kLmRed, out);
+        for (int q = 0; q < kLmTerms; ++q) acc[q] = out[q];
+        return out[kLmTerms];
+    }
 };
 
 // one problem per blockIdx.y (prob_base + y); blocks x < lm_slots(n) / 512 of it take part
@@ -2362,7 +2387,7 @@ struct GpuLmReducer {
 __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint8_t *__restrict__ mask,
                                                            double *__restrict__ models, int32_t *__restrict__ iters,
                                                            int prob_base, double *gws, unsigned *bar) {
-    __shared__ double wsum[kLmThreads / 64][kLmTerms];
+    __shared__ double wsum[kLmThreads / 64][kLmRed];
     const int prob = prob_base + blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
@@ -2536,8 +2561,9 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
     // launch, one block each; each larger problem in a launch of its own, lm_slots(n) / 512
     // blocks (<= 64, all co-resident) that meet at grid barriers
     const int nb_max = lm_slots(a.max_n) / kLmThreads;
-    hipLaunchKernelGGL(k_pnp_refine, dim3(1, P), dim3(kLmThreads), 0, s, a, mask, models, iters, 0,
-                       (double *)nullptr, (unsigned *)nullptr);
+    if (!(P == 1 && nb_max > 1))  // (one large problem: only the multi-block launch has work)
+        hipLaunchKernelGGL(k_pnp_refine, dim3(1, P), dim3(kLmThreads), 0, s, a, mask, models, iters, 0,
+                           (double *)nullptr, (unsigned *)nullptr);
     if (nb_max > 1) {
         if (!scratch) return hipErrorInvalidValue;
         unsigned *bar = (unsigned *)scratch;  // zeroed by the caller once; back to 0 after every barrier

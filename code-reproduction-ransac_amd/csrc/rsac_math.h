@@ -750,16 +750,35 @@ RSAC_HD void cayley_apply(const double *d, const double *R, double *Rn) {
 // The LM loop.  Red provides normal(R, t, acc[27]) and cost(R, t), reduced in the
 // order above; on the GPU every thread of the block runs this loop in lockstep
 // (all decisions depend on reduced, block-uniform values).  Returns iterations.
+// A reducer with kFused = true also provides cost_normal(R, t, acc) = cost(R, t) with
+// normal(R, t, acc) in the same pass (each term reduced in the same order as alone): the
+// accepted candidate's normal equations are then not recomputed, one reduction per iteration.
+template <class Red, class = void>
+struct LmFused {
+    static constexpr bool value = false;
+};
+template <class Red>
+struct LmFused<Red, decltype((void)Red::kFused)> {
+    static constexpr bool value = Red::kFused;
+};
+
 template <class Red>
 RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
+    constexpr bool fused = LmFused<Red>::value;
     double lam = 1e-3;
     RSAC_TRACE_MARK(red, 10);
     double cost = red.cost(R, t);
     RSAC_TRACE_MARK(red, 11);
+    double acc_next[kLmTerms];
+    bool have_next = false;
     int it;
     for (it = 0; it < max_iter; ++it) {
         double acc[kLmTerms];
-        red.normal(R, t, acc);
+        if (fused && have_next) {
+            for (int q = 0; q < kLmTerms; ++q) acc[q] = acc_next[q];
+        } else {
+            red.normal(R, t, acc);
+        }
         RSAC_TRACE_MARK(red, 12);
         double A[36], g[6];
         int q = 0;
@@ -778,9 +797,12 @@ RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
             cayley_apply(d, R, Rn);
             for (int j = 0; j < 3; ++j) tn[j] = t[j] + d[3 + j];
             RSAC_TRACE_MARK(red, 13);
-            const double cn = red.cost(Rn, tn);
+            double cn;
+            if constexpr (fused) cn = red.cost_normal(Rn, tn, acc_next);
+            else cn = red.cost(Rn, tn);
             RSAC_TRACE_MARK(red, 14);
             if (cn < cost) {
+                have_next = true;
                 const double rel = (cost - cn) / (cost > 1e-300 ? cost : 1e-300);
                 for (int j = 0; j < 9; ++j) R[j] = Rn[j];
                 for (int j = 0; j < 3; ++j) t[j] = tn[j];
