@@ -143,7 +143,8 @@ struct rsac_ctx {
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
     DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
-    DevBuf lmscr;                                              // multi-block LM refit: barrier + wave sums
+    DevBuf lmscr;                                              // multi-block LM refit: tagged wave sums
+    LmScratch lm;                                              // ... and its launch counter
     DevBuf scanrec;                                            // single-round scans: improvement records
     std::vector<char> last_tables;                             // the tables last uploaded (stage_tables)
     void *last_tables_dev = nullptr;
@@ -392,13 +393,15 @@ struct LoopOut {
 // hypothesis' record, so the final mask / gather / refit see it.
 constexpr int kLoSteps = 4;
 
-// the multi-block LM refit's scratch (rsac_internal.h kLmScratchDoubles; barrier counters zeroed)
-double *lm_scratch(rsac_ctx *c, hipStream_t s) {
+// the multi-block LM refit's scratch (rsac_internal.h LmScratch; granules zeroed once here)
+LmScratch *lm_scratch(rsac_ctx *c, hipStream_t s) {
     if (!c->lmscr.p) {
-        if (c->lmscr.ensure(sizeof(double) * kLmScratchDoubles) != hipSuccess) return nullptr;
-        if (hipMemsetAsync(c->lmscr.p, 0, 64, s) != hipSuccess) return nullptr;
+        if (c->lmscr.ensure(kLmGranuleBytes) != hipSuccess) return nullptr;
+        if (hipMemsetAsync(c->lmscr.p, 0, kLmGranuleBytes, s) != hipSuccess) return nullptr;
+        c->lm.gran = (unsigned long long *)c->lmscr.p;
+        c->lm.launch = 0;
     }
-    return c->lmscr.as<double>();
+    return &c->lm;
 }
 
 int local_opt(rsac_ctx *c, const PnpArgs &a, int32_t n, ScanState &sc, double confidence, hipStream_t s,

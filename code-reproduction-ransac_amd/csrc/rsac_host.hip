@@ -153,21 +153,22 @@ struct HostLmReducer {
     int n;
     Cam k;
     double c[3];  // centre of the refit frame
-    int slots = lm_slots(n);
-    std::vector<double> part = std::vector<double>((size_t)lm_slots(n) * kLmTerms);
+    std::vector<double> part = std::vector<double>((size_t)lm_blocks(n) * kLmThreads * kLmTerms);
+    double accs[2][kLmTerms] = {};
+    double *acc_buf(int k) { return accs[k]; }
     void mark(int) {}
     void normal(const double *R, const double *t, double *acc) {
-        lm_reduce_host(n, mask, kLmTerms, part.data(), acc, [&](int i, double *a) {
+        lm_reduce_blocks_host(n, mask, kLmTerms, part.data(), acc, [&](int i, double *a) {
             pnp_lm_point(R, t, k, (double)X[i] - c[0], (double)Y[i] - c[1], (double)Z[i] - c[2], (double)U[i],
                          (double)V[i], a);
-        }, slots);
+        });
     }
     double cost(const double *R, const double *t) {
         double s;
-        lm_reduce_host(n, mask, 1, part.data(), &s, [&](int i, double *a) {
+        lm_reduce_blocks_host(n, mask, 1, part.data(), &s, [&](int i, double *a) {
             a[0] += pnp_lm_cost_point(R, t, k, (double)X[i] - c[0], (double)Y[i] - c[1], (double)Z[i] - c[2],
                                       (double)U[i], (double)V[i]);
-        }, slots);
+        });
         return s;
     }
 };
@@ -215,8 +216,6 @@ int pnp_refine_lm(const float *X, const float *Y, const float *Z, const float *U
                   int n, const double cam[4], double R[9], double t[3], int max_iter) {
     if (n <= 0) return 0;
     HostLmReducer red{X, Y, Z, U, V, mask, n, Cam{cam[0], cam[1], cam[2], cam[3]}, {(double)X[0], (double)Y[0], (double)Z[0]}};
-    red.slots = lm_slots(n);
-    red.part.assign((size_t)red.slots * kLmTerms, 0.0);
     lm_to_centred(R, red.c, t);
     const int it = pnp_lm_refine(red, R, t, max_iter);
     lm_from_centred(R, red.c, t);

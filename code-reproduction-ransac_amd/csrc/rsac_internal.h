@@ -167,11 +167,16 @@ hipError_t launch_pnp_epnp_s1(const PnpArgs &a, int32_t P, const uint8_t *mask, 
                               EpnpStage1 *st1, hipStream_t s);
 hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, const EpnpStage1 *st1,
                               const EpnpStage2 *st2, double *models, hipStream_t s);
-// scratch (problems > 4096 points): kLmScratchDoubles doubles, its first 8 bytes zeroed once
-// (the grid barrier's counters); host_off: the problems' offsets on the host (P + 1)
-constexpr size_t kLmScratchDoubles = 8 + 2 * (32768 / 64) * 28;
+// multi-block refit scratch (problems > 4096 points): the tagged wave-sum granules, two buffers
+// of [64 blocks * 8 waves][28 terms][2] u64, zeroed on allocation and whenever launch wraps;
+// launch: the per-context launch counter of the tags.  host_off: the problems' offsets (P + 1)
+constexpr size_t kLmGranuleBytes = 2ull * 64 * 8 * 28 * 2 * 8;
+struct LmScratch {
+    unsigned long long *gran = nullptr;
+    unsigned launch = 0;
+};
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
-                             hipStream_t s, double *scratch, const int64_t *host_off);
+                             hipStream_t s, LmScratch *scratch, const int64_t *host_off);
 
 // mask + inlier count (atomically into *count, zeroed by the caller) of one model record, problem 0
 hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, int32_t *count,

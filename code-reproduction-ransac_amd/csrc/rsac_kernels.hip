@@ -2244,6 +2244,19 @@ hipError_t launch_loc_score(const double *src, const double *dst, const uint8_t 
 // ---------------------------------------------------------------------------
 constexpr int kLmRed = kLmTerms + 1;  // widest LM reduction: normal equations + cost
 
+// LDS of k_pnp_refine: the staged points (SoA, [5][cap]; cap = 4096 points for one block,
+// 2048 for a range of a multi-block problem), then, multi-block only, the nb * 8 wave sums of a
+// reduction ([wave][kLmRed] doubles, at most 512 waves = 112 KB)
+constexpr int kLmStageOne = 8 * kLmThreads;
+constexpr int kLmStageMulti = 4 * kLmThreads;
+constexpr int kLmWaveSums = kLmMaxBlocks * (kLmThreads / 64);
+constexpr int kLmLdsBytes = 5 * kLmStageMulti * 4 + kLmWaveSums * kLmRed * 8;
+static_assert(5 * kLmStageOne * 4 <= kLmLdsBytes, "single-block stage fits");
+static_assert(kLmBlockPoints <= kLmStageMulti, "a range of ~2048 points fits one tile");
+
+typedef __attribute__((address_space(1))) unsigned long long lm_gu64;
+constexpr unsigned kLmSpinLimit = 1u << 20;  // ~1 s of polls: a block that never arrives ends the waits
+
 struct GpuLmReducer {
     static constexpr bool kFused = true;  // cost_normal: one pass for a candidate (rsac_math.h)
     const float *X, *Y, *Z, *U, *V;
@@ -2252,96 +2265,229 @@ struct GpuLmReducer {
     Cam k;
     double c0, c1, c2;  // centre of the refit frame
     double (*wsum)[kLmRed];  // LDS [kLmThreads / 64][kLmRed]
-    // more than one block per problem (S = lm_slots(n) > 512): this block owns slots
-    // [512 b, 512 b + 512) of the S; wave sums go through global scratch (two alternating
-    // buffers of [S / 64][kLmRed]) and a grid barrier (bar: arrivals, generation)
-    int S = kLmThreads, nb = 1;
-    double *gws = nullptr;
-    unsigned *bar = nullptr;
-    int parity = 0;
+    // this block's range [lo, hi) of the block-compacted order (rsac_math.h).  More than one
+    // block per problem (nb > 1): every reduction's wave sums are handed over as data-tagged
+    // granules (gran, below), no barrier
+    int nb = 1;
+    int lo = 0, hi = 0;
+    float *stage = nullptr;  // LDS [5][cap]: compacted X Y Z U V of the range
+    int cap = kLmStageOne;
+    int *scan = nullptr;     // LDS [kLmThreads / 64]: wave totals
+    int staged = -1;         // masked points of a range that fits one tile (staged once); -1: re-staged per pass
+    // multi-block hand-off (cdna_hip_programming.md Guideline 16, R2): each wave's sum of term q
+    // goes out as two 8-byte {tag, 32-bit half} granules, stored sc1 by lane q; every block
+    // sweeps all nb * 8 * nv * 2 granules with sc1 loads until each carries this reduction's tag
+    // (launch tag | reduction index: unique per launch, the host zeroes the granules on wrap),
+    // into LDS (wsums), and sums them left to right.  Two alternating granule buffers: a block
+    // overwrites buffer k % 2 only after every block has stored reduction k - 1, i.e. finished
+    // reading reduction k - 2.
+    lm_gu64 *gran = nullptr;  // [2][kLmWaveSums][kLmRed][2]
+    unsigned tag_base = 0;
+    int phase = 0;
+    double *wsums = nullptr;  // LDS [kLmWaveSums][kLmRed]
+    bool broken = false;
+    double (*accs)[kLmRed] = nullptr;  // LDS [2][kLmRed]: pnp_lm_refine's normal equations
+    double *res = nullptr;             // LDS [1]: a cost reduction's result
+    __device__ double *acc_buf(int k) { return accs[k]; }
 
-    __device__ void grid_barrier() {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();  // release this block's wave sums
-            const unsigned gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (atomicAdd(bar, 1u) == (unsigned)nb - 1) {
-                __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __threadfence();
-                atomicAdd(bar + 1, 1u);
-            } else {
-                while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen)
-                    __builtin_amdgcn_s_sleep(1);
-            }
-            __threadfence();  // acquire the other blocks' wave sums
+    // the masked points of [tlo, thi) (at most cap indices), ascending, into stage[.][0, cnt);
+    // returns cnt (block-uniform).  Thread t covers indices tlo + (cap / 512) t, ...
+    __device__ int stage_tile(int tlo, int thi) {
+        const int per = cap / kLmThreads;  // 8 or 4
+        const int base = tlo + per * (int)threadIdx.x;
+        unsigned bits = 0;
+        for (int k = 0; k < per; ++k)
+            if (base + k < thi && mask[base + k]) bits |= 1u << k;
+        const int cnt = __popc(bits);
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        int incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
         }
+        __syncthreads();  // the previous tile's readers are done with stage and scan
+        if (lane == 63) scan[wave] = incl;
         __syncthreads();
+        int pos = incl - cnt, tot = 0;
+        for (int w = 0; w < kLmThreads / 64; ++w) {
+            const int v = scan[w];
+            pos += w < wave ? v : 0;
+            tot += v;
+        }
+        for (int k = 0; k < per; ++k)
+            if (bits >> k & 1u) {
+                const int i = base + k;
+                stage[pos] = X[i];
+                stage[cap + pos] = Y[i];
+                stage[2 * cap + pos] = Z[i];
+                stage[3 * cap + pos] = U[i];
+                stage[4 * cap + pos] = V[i];
+                ++pos;
+            }
+        __syncthreads();
+        return tot;
+    }
+    __device__ void set_range(int b) {
+        const int C = lm_chunk(n);
+        lo = b * C;
+        hi = (int)min((int64_t)n, (int64_t)lo + C);
+        if (hi - lo <= cap) staged = stage_tile(lo, hi);
+    }
+    // f(Xd, Yd, Zd, u, v) over this thread's points: the range's masked points p = thread,
+    // thread + 512, ... of the compacted order
+    template <class F>
+    __device__ void for_points(F f) {
+        auto point = [&](int q) {
+            f((double)stage[q] - c0, (double)stage[cap + q] - c1, (double)stage[2 * cap + q] - c2,
+              (double)stage[3 * cap + q], (double)stage[4 * cap + q]);
+        };
+        if (staged >= 0) {
+            for (int q = threadIdx.x; q < staged; q += kLmThreads) point(q);
+            return;
+        }
+        int p0 = 0;  // compacted position of the tile's first point
+        for (int tlo = lo; tlo < hi; tlo += cap) {
+            const int cnt = stage_tile(tlo, min(hi, tlo + cap));
+            for (int q = ((int)threadIdx.x - p0 % kLmThreads + kLmThreads) % kLmThreads; q < cnt; q += kLmThreads)
+                point(q);
+            p0 += cnt;
+        }
     }
 
+    // a + (the value of lane l + o): lane l < o gets the pair (l, l ^ o) of the xor butterfly,
+    // so after o = 32, 16, ..., 1 lane 0 holds the butterfly's sum bit for bit (only lane 0's
+    // sum is used).  o = 32 / 16 cross rows: v_permlane32_swap / v_permlane16_swap; o <= 8 stay
+    // in a row of 16: DPP row_shl.  No LDS traffic (ds_bpermute was ~5 us for 27 terms).
+    template <int O>
+    __device__ static double add_down(double a) {
+        const int lo = __double2loint(a), hi = __double2hiint(a);
+        int dlo, dhi;
+        if constexpr (O == 32) {
+            dlo = __builtin_amdgcn_permlane32_swap(lo, lo, false, false)[1];
+            dhi = __builtin_amdgcn_permlane32_swap(hi, hi, false, false)[1];
+        } else if constexpr (O == 16) {
+            dlo = __builtin_amdgcn_permlane16_swap(lo, lo, false, false)[1];
+            dhi = __builtin_amdgcn_permlane16_swap(hi, hi, false, false)[1];
+        } else {
+            dlo = __builtin_amdgcn_update_dpp(0, lo, 0x100 + O, 0xf, 0xf, false);  // row_shl:O
+            dhi = __builtin_amdgcn_update_dpp(0, hi, 0x100 + O, 0xf, 0xf, false);
+        }
+        return a + __hiloint2double(dhi, dlo);
+    }
+
+    // sums a[0, nv) of every thread in the order of rsac_math.h into out[0, nv) (LDS, written by
+    // threads q < nv; complete when this returns)
     __device__ void reduce(double *a, int nv, double *out) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        // levels outside, terms inside: the nv butterflies are independent, so their shuffles
-        // overlap (each term's additions are the same as term by term)
-        for (int o = 32; o > 0; o >>= 1)
-            for (int q = 0; q < nv; ++q) a[q] = a[q] + __shfl_xor(a[q], o);
+        // levels outside, terms inside: the nv reductions are independent and overlap
+        for (int q = 0; q < nv; ++q) a[q] = add_down<32>(a[q]);
+        for (int q = 0; q < nv; ++q) a[q] = add_down<16>(a[q]);
+        for (int q = 0; q < nv; ++q) a[q] = add_down<8>(a[q]);
+        for (int q = 0; q < nv; ++q) a[q] = add_down<4>(a[q]);
+        for (int q = 0; q < nv; ++q) a[q] = add_down<2>(a[q]);
+        for (int q = 0; q < nv; ++q) a[q] = add_down<1>(a[q]);
+#ifdef RSAC_TRACE
+        mark(21);
+#endif
         if (nb == 1) {
             if (lane == 0)
                 for (int q = 0; q < nv; ++q) wsum[wave][q] = a[q];
             __syncthreads();
-            for (int q = 0; q < nv; ++q) {
+            if (threadIdx.x < nv) {
+                const int q = threadIdx.x;
                 double s = wsum[0][q];
                 for (int w = 1; w < kLmThreads / 64; ++w) s = s + wsum[w][q];
                 out[q] = s;
             }
-            __syncthreads();  // wsum is reused by the next reduction
+            __syncthreads();  // out is complete; wsum is free for the next reduction
             return;
         }
-        double *g = gws + (size_t)parity * (S / 64) * kLmRed;
-        parity ^= 1;  // the next reduction writes the other buffer (a block may run ahead by one)
-        if (lane == 0)
-            for (int q = 0; q < nv; ++q) g[(blockIdx.x * (kLmThreads / 64) + wave) * kLmRed + q] = a[q];
-        grid_barrier();
-        // thread q < nv sums term q over the S / 64 wave sums, left to right.  Plain loads: the
-        // barrier's acquire fence invalidated this CU's L1; batches of 32 loads are in flight
-        // ahead of the (sequential) additions.
-        if (threadIdx.x < nv) {
-            const int q = threadIdx.x;
-            const int nw = S / 64;
-            double s = 0.0;
-            for (int w0 = 0; w0 < nw; w0 += 32) {
-                double v[32];
-#pragma unroll
-                for (int j = 0; j < 32; ++j) v[j] = w0 + j < nw ? g[(w0 + j) * kLmRed + q] : 0.0;
-#pragma unroll
-                for (int j = 0; j < 32; ++j)
-                    if (w0 + j < nw) s = (w0 + j == 0) ? v[j] : s + v[j];
+        ++phase;
+        const unsigned long long tag = (unsigned long long)(tag_base | (unsigned)phase) << 32;
+        lm_gu64 *g = gran + (size_t)(phase & 1) * kLmWaveSums * kLmRed * 2;
+        // lane q < nv publishes term q of this wave (lane 0 holds the wave's sums)
+        unsigned mlo = 0, mhi = 0;
+        for (int q = 0; q < nv; ++q) {
+            const unsigned vlo = __builtin_amdgcn_readfirstlane(__double2loint(a[q]));
+            const unsigned vhi = __builtin_amdgcn_readfirstlane(__double2hiint(a[q]));
+            if (lane == q) {
+                mlo = vlo;
+                mhi = vhi;
             }
-            wsum[0][q] = s;
+        }
+        if (lane < nv) {
+            lm_gu64 *gw = g + ((size_t)(blockIdx.x * (kLmThreads / 64) + wave) * kLmRed + lane) * 2;
+            __hip_atomic_store(gw, tag | mlo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gw + 1, tag | mhi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#ifdef RSAC_TRACE
+        mark(22);
+#endif
+        // sweep: granule k = (wave w, term q, half h), k = (w nv + q) 2 + h, 16 per thread in
+        // flight per pass; a pass re-reads the ones whose tag is not yet this reduction's
+        const int nw = nb * (kLmThreads / 64), tot = nw * nv * 2;
+        unsigned *ws32 = (unsigned *)wsums;
+        for (int k0 = 0; k0 < tot; k0 += 16 * kLmThreads) {
+            unsigned pending = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (k0 + j * kLmThreads + (int)threadIdx.x < tot) pending |= 1u << j;
+            for (unsigned spins = 0; pending && !broken; ++spins) {
+                unsigned long long x[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int k = k0 + j * kLmThreads + threadIdx.x;
+                    const int w = k / (2 * nv), r = k - w * 2 * nv;
+                    x[j] = (pending >> j & 1u)
+                               ? __hip_atomic_load(g + (size_t)w * kLmRed * 2 + r, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : 0ull;
+                }
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    if (!(pending >> j & 1u) || (x[j] & 0xFFFFFFFF00000000ull) != tag) continue;
+                    const int k = k0 + j * kLmThreads + threadIdx.x;
+                    const int w = k / (2 * nv), r = k - w * 2 * nv;
+                    ws32[w * kLmRed * 2 + r] = (unsigned)x[j];
+                    pending &= ~(1u << j);
+                }
+                if (pending) {
+                    if (spins >= kLmSpinLimit) broken = true;  // a block never arrived: stop waiting (no hang)
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
         }
         __syncthreads();
-        for (int q = 0; q < nv; ++q) out[q] = wsum[0][q];
+#ifdef RSAC_TRACE
+        mark(23);
+#endif
+        // thread q < nv sums term q over the nb * 8 wave sums, left to right
+        if (threadIdx.x < nv) {
+            const int q = threadIdx.x;
+            double s = wsums[q];
+            for (int w = 1; w < nw; ++w) s = s + wsums[w * kLmRed + q];
+            out[q] = s;
+        }
         __syncthreads();
     }
     __device__ void normal(const double *R, const double *t, double *acc) {
         double a[kLmTerms];
         for (int q = 0; q < kLmTerms; ++q) a[q] = 0.0;
-#pragma unroll 4
-        for (int i = blockIdx.x * kLmThreads + threadIdx.x; i < n; i += S)
-            if (mask[i])
-                pnp_lm_point(R, t, k, (double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i],
-                             (double)V[i], a);
+        for_points([&](double Xd, double Yd, double Zd, double u, double v) {
+            pnp_lm_point(R, t, k, Xd, Yd, Zd, u, v, a);
+        });
 #ifdef RSAC_TRACE
         mark(20);
 #endif
         reduce(a, kLmTerms, acc);
     }
 #ifdef RSAC_TRACE
-    unsigned long long stamp[48];
-    int phase_of[48];
+    unsigned long long stamp[96];
+    int phase_of[96];
     int ns = 0;
     __device__ void mark(int phase) {
         __syncthreads();
-        if (ns < 48) {
+        if (ns < 96) {
             stamp[ns] = __builtin_amdgcn_s_memrealtime();
             phase_of[ns++] = phase;
         }
@@ -2353,48 +2499,43 @@ struct GpuLmReducer {
     }
 #endif
     __device__ double cost(const double *R, const double *t) {
-        double a = 0.0, out;
-#pragma unroll 4
-        for (int i = blockIdx.x * kLmThreads + threadIdx.x; i < n; i += S)
-            if (mask[i])
-                a += pnp_lm_cost_point(R, t, k, (double)X[i] - c0, (double)Y[i] - c1, (double)Z[i] - c2, (double)U[i],
-                                       (double)V[i]);
-        reduce(&a, 1, &out);
-        return out;
+        double a = 0.0;
+        for_points([&](double Xd, double Yd, double Zd, double u, double v) {
+            a += pnp_lm_cost_point(R, t, k, Xd, Yd, Zd, u, v);
+        });
+        reduce(&a, 1, res);
+        return res[0];
     }
     // cost(R, t) and normal(R, t) in one pass: per-slot partials and reductions are term by
     // term the same as the separate passes'
     __device__ double cost_normal(const double *R, const double *t, double *acc) {
         double a[kLmRed];
         for (int q = 0; q < kLmRed; ++q) a[q] = 0.0;
-#pragma unroll 2
-        for (int i = blockIdx.x * kLmThreads + threadIdx.x; i < n; i += S)
-            if (mask[i]) {
-                const double Xd = (double)X[i] - c0, Yd = (double)Y[i] - c1, Zd = (double)Z[i] - c2;
-                pnp_lm_point(R, t, k, Xd, Yd, Zd, (double)U[i], (double)V[i], a);
-                a[kLmTerms] += pnp_lm_cost_point(R, t, k, Xd, Yd, Zd, (double)U[i], (double)V[i]);
-            }
-        double out[kLmRed];
-        reduce(a, kLmRed, out);
-        for (int q = 0; q < kLmTerms; ++q) acc[q] = out[q];
-        return out[kLmTerms];
+        for_points([&](double Xd, double Yd, double Zd, double u, double v) {
+            pnp_lm_point(R, t, k, Xd, Yd, Zd, u, v, a);
+            a[kLmTerms] += pnp_lm_cost_point(R, t, k, Xd, Yd, Zd, u, v);
+        });
+        reduce(a, kLmRed, acc);  // acc: an acc_buf (kLmRed wide), the cost in its last slot
+        return acc[kLmTerms];
     }
 };
 
-// one problem per blockIdx.y (prob_base + y); blocks x < lm_slots(n) / 512 of it take part
-// (x > 0 only when the problem has more than 4096 points).  Multi-block problems need all
+// one problem per blockIdx.y (prob_base + y); blocks x < lm_blocks(n) of it take part, one
+// per range of the block-compacted order (x > 0 only when the problem has more than 4096 points).  Multi-block problems need all
 // their blocks co-resident: the launcher keeps them to one problem per launch (<= 64 blocks).
 __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint8_t *__restrict__ mask,
                                                            double *__restrict__ models, int32_t *__restrict__ iters,
-                                                           int prob_base, double *gws, unsigned *bar) {
+                                                           int prob_base, unsigned long long *gran, unsigned tag_base) {
     __shared__ double wsum[kLmThreads / 64][kLmRed];
+    __shared__ double accs[2][kLmRed], res[1];
+    __shared__ int scan[kLmThreads / 64];
+    __shared__ __attribute__((aligned(16))) char lds[kLmLdsBytes];  // 152 KB (gfx950: 160 KB per workgroup)
     const int prob = prob_base + blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
-    const int S = lm_slots(n);
-    const int nb = S / kLmThreads;
+    const int nb = lm_blocks(n);
     if ((int)blockIdx.x >= nb) return;  // block-uniform; this problem uses fewer blocks
-    if ((nb > 1) != (gws != nullptr)) return;  // the other launch's problem (launch_pnp_refine)
+    if ((nb > 1) != (gran != nullptr)) return;  // the other launch's problem (launch_pnp_refine)
     double *m = models + (int64_t)prob * kModelStride;
     if (m[kValidSlot] == 0.0) {  // no model: block-uniform exit
         if (threadIdx.x == 0 && blockIdx.x == 0 && iters) iters[prob] = 0;
@@ -2404,10 +2545,16 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     const double c[3] = {(double)a.X[p0], (double)a.Y[p0], (double)a.Z[p0]};
     GpuLmReducer red{a.X + p0, a.Y + p0, a.Z + p0, a.U + p0, a.V + p0, mask + p0,
                      n, Cam{cm[0], cm[1], cm[2], cm[3]}, c[0], c[1], c[2], wsum};
-    red.S = S;
     red.nb = nb;
-    red.gws = gws;
-    red.bar = bar;
+    red.stage = (float *)lds;
+    red.cap = nb == 1 ? kLmStageOne : kLmStageMulti;
+    red.scan = scan;
+    red.gran = (lm_gu64 *)gran;
+    red.tag_base = tag_base;
+    red.wsums = (double *)(lds + 5 * kLmStageMulti * 4);
+    red.accs = accs;
+    red.res = res;
+    red.set_range(blockIdx.x);
     double R[9], t[3];
     for (int j = 0; j < 9; ++j) R[j] = m[j];
     for (int j = 0; j < 3; ++j) t[j] = m[9 + j];
@@ -2418,8 +2565,9 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     red.dump();
 #endif
     lm_from_centred(R, c, t);
-    if (nb > 1) red.grid_barrier();  // every block has read m before block 0 overwrites it
-    __syncthreads();  // every thread has read m before thread 0 overwrites it
+    // every block read m before its first contribution, and block 0 got past the first
+    // reduction only with every block's: no barrier before block 0 overwrites m
+    __syncthreads();  // every thread of this block has read m before thread 0 overwrites it
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         for (int j = 0; j < 9; ++j) m[j] = R[j];
         for (int j = 0; j < 3; ++j) m[9 + j] = t[j];
@@ -2556,24 +2704,29 @@ hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, 
 }
 
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
-                             hipStream_t s, double *scratch, const int64_t *host_off) {
+                             hipStream_t s, LmScratch *scratch, const int64_t *host_off) {
     // every problem of up to 4096 points (and, with host_off unknown, every problem) in one
-    // launch, one block each; each larger problem in a launch of its own, lm_slots(n) / 512
-    // blocks (<= 64, all co-resident) that meet at grid barriers
-    const int nb_max = lm_slots(a.max_n) / kLmThreads;
+    // launch, one block each; each larger problem in a launch of its own, lm_blocks(n)
+    // blocks (<= 64, all co-resident) that hand their wave sums over as tagged granules
+    const int nb_max = lm_blocks(a.max_n);
     if (!(P == 1 && nb_max > 1))  // (one large problem: only the multi-block launch has work)
         hipLaunchKernelGGL(k_pnp_refine, dim3(1, P), dim3(kLmThreads), 0, s, a, mask, models, iters, 0,
-                           (double *)nullptr, (unsigned *)nullptr);
+                           (unsigned long long *)nullptr, 0u);
     if (nb_max > 1) {
-        if (!scratch) return hipErrorInvalidValue;
-        unsigned *bar = (unsigned *)scratch;  // zeroed by the caller once; back to 0 after every barrier
-        double *gws = scratch + 8;
+        if (!scratch || !scratch->gran) return hipErrorInvalidValue;
         for (int p = 0; p < P; ++p) {
             const int np = host_off ? (int)(host_off[p + 1] - host_off[p]) : a.max_n;
-            const int nb = lm_slots(np) / kLmThreads;
-            if (nb > 1)
-                hipLaunchKernelGGL(k_pnp_refine, dim3(nb, 1), dim3(kLmThreads), 0, s, a, mask, models, iters, p, gws,
-                                   bar);
+            const int nb = lm_blocks(np);
+            if (nb <= 1) continue;
+            // tag = launch (22 bits, never 0) << 10 | reduction index (< 1024): unique among the
+            // granules in memory, which are zeroed whenever the launch counter wraps
+            if (++scratch->launch >= (1u << 22)) {
+                const hipError_t e = hipMemsetAsync(scratch->gran, 0, kLmGranuleBytes, s);
+                if (e != hipSuccess) return e;
+                scratch->launch = 1;
+            }
+            hipLaunchKernelGGL(k_pnp_refine, dim3(nb, 1), dim3(kLmThreads), 0, s, a, mask, models, iters, p,
+                               scratch->gran, scratch->launch << 10);
         }
     }
     return hipGetLastError();

@@ -651,18 +651,26 @@ RSAC_HD bool fm_inlier(const double *F, double x1, double y1, double x2, double 
 // coordinates would otherwise couple rotation and translation badly.
 //
 // One summation order on every backend (GPU kernel k_pnp_refine, host
-// rsac_pnp_refine, oracle orc_pnp_refine): S = lm_slots(n) strided per-slot
-// partials (point i to slot i % S, ascending), a 64-lane butterfly per wave of
-// 64 slots (x += x[lane ^ o], o = 32 .. 1), then the S / 64 wave sums left to
-// right.  S = 512 up to 4096 points; larger problems get more slots (at most 8
-// points each, S <= 32768), so the GPU spreads them over S / 512 blocks.
+// rsac_pnp_refine, oracle orc_pnp_refine), "block-compacted": the points are cut
+// into nb = lm_blocks(n) contiguous ranges of lm_chunk(n) indices; within range b
+// the masked points, in ascending index order, are dealt round-robin to 512 slots
+// (the p-th masked point of the range to slot b * 512 + p % 512); each slot sums
+// its points in order, a 64-lane tree per wave of 64 slots (x += x[lane ^ o],
+// o = 32 .. 1), then the nb * 8 wave sums left to right.  The GPU runs one block
+// per range and stages the range's masked points in LDS once per refit, so every
+// thread gets ceil(inliers of the range / 512) points and no outlier costs a pass.
 // ---------------------------------------------------------------------------
 constexpr int kLmThreads = 512;
-constexpr int kLmMaxSlots = 32768;
-RSAC_HD int lm_slots(int n) {
-    int S = kLmThreads;
-    while (S < kLmMaxSlots && n > 8 * S) S *= 2;
-    return S;
+constexpr int kLmMaxBlocks = 64;
+constexpr int kLmBlockPoints = 2048;  // range length above 4096 points
+RSAC_HD int lm_blocks(int n) {
+    if (n <= 2 * kLmBlockPoints) return 1;
+    const int nb = (n + kLmBlockPoints - 1) / kLmBlockPoints;
+    return nb < kLmMaxBlocks ? nb : kLmMaxBlocks;
+}
+RSAC_HD int lm_chunk(int n) {
+    const int nb = lm_blocks(n);
+    return (int)(((int64_t)n + nb - 1) / nb);
 }
 constexpr int kLmTerms = 27;  // J^T J lower triangle (21, row-major packed), J^T r (6)
 constexpr int kLmMaxIter = 20;
@@ -702,17 +710,19 @@ RSAC_HD double pnp_lm_cost_point(const double *R, const double *t, const Cam &k,
     return ru * ru + rv * rv;
 }
 
-// (A + lam diag(A)) x = b, A 6 x 6 SPD row-major; false if not positive definite.
-// Divisions by the pivots are multiplications by their reciprocals (6 divisions, not 33:
-// the GPU refit runs this on every thread of the block, between two reductions).
-RSAC_HD bool chol6_solve(const double *A, double lam, const double *b, double *x) {
+// (A + lam diag(A)) x = b by Cholesky, A 6 x 6 SPD, on the packed normal equations of
+// pnp_lm_point (acc: J^T J lower triangle row-major, then J^T r): A[i][j] = acc[i (i + 1) / 2
+// + j], b = -J^T r; false if not positive definite.  Divisions by the pivots are
+// multiplications by their reciprocals (6 divisions, not 33: the GPU refit runs this on every
+// thread of the block, between two reductions, reading acc from LDS).
+RSAC_HD bool chol6_solve_packed(const double *acc, double lam, double *x) {
     double L[36], y[6], inv[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
         for (int j = 0; j <= i; ++j) {
-            double s = A[i * 6 + j];
-            if (i == j) s = s + lam * A[i * 6 + i];
+            double s = acc[i * (i + 1) / 2 + j];
+            if (i == j) s = s + lam * acc[i * (i + 1) / 2 + i];
             for (int q = 0; q < j; ++q) s = s - L[i * 6 + q] * L[j * 6 + q];
             if (i == j) {
                 if (!(s > 0)) return false;
@@ -724,7 +734,7 @@ RSAC_HD bool chol6_solve(const double *A, double lam, const double *b, double *x
         }
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-        double s = b[i];
+        double s = -acc[21 + i];
         for (int q = 0; q < i; ++q) s = s - L[i * 6 + q] * y[q];
         y[i] = s * inv[i];
     }
@@ -765,6 +775,8 @@ struct LmFused<Red, decltype((void)Red::kFused)> {
     static constexpr bool value = Red::kFused;
 };
 
+// Red::acc_buf(k), k = 0, 1: two buffers of kLmTerms doubles for the current and the next
+// normal equations (the GPU reducer's are in LDS, written by its reductions)
 template <class Red>
 RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
     constexpr bool fused = LmFused<Red>::value;
@@ -772,26 +784,22 @@ RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
     RSAC_TRACE_MARK(red, 10);
     double cost = red.cost(R, t);
     RSAC_TRACE_MARK(red, 11);
-    double acc_next[kLmTerms];
+    double *acc = red.acc_buf(0), *acc_next = red.acc_buf(1);
     bool have_next = false;
     int it;
     for (it = 0; it < max_iter; ++it) {
-        double acc[kLmTerms];
         if (fused && have_next) {
-            for (int q = 0; q < kLmTerms; ++q) acc[q] = acc_next[q];
+            double *tmp = acc;  // the accepted candidate's normal equations
+            acc = acc_next;
+            acc_next = tmp;
         } else {
             red.normal(R, t, acc);
         }
         RSAC_TRACE_MARK(red, 12);
-        double A[36], g[6];
-        int q = 0;
-        for (int a = 0; a < 6; ++a)
-            for (int b = 0; b <= a; ++b, ++q) A[a * 6 + b] = A[b * 6 + a] = acc[q];
-        for (int a = 0; a < 6; ++a) g[a] = -acc[21 + a];
         bool accepted = false;
         while (!accepted) {
             double d[6];
-            if (!chol6_solve(A, lam, g, d)) {
+            if (!chol6_solve_packed(acc, lam, d)) {
                 lam *= 10;
                 if (lam > 1e10) return it;
                 continue;
@@ -835,16 +843,8 @@ RSAC_HD void lm_from_centred(const double *R, const double *c, double *t) {
     for (int j = 0; j < 3; ++j) t[j] = t[j] - (R[3 * j] * c[0] + R[3 * j + 1] * c[1] + R[3 * j + 2] * c[2]);
 }
 
-// Host/oracle-side mirror of the GPU reduction: sum f(i, acc) over points with
-// mask[i] != 0 in the kLmThreads-strided, wave-butterfly order.  part: scratch of
-// kLmThreads * nv doubles.
-// slots: S (lm_slots(n) for the LM refit, kLmThreads for EPnP); part: S * nv doubles.
-template <class F>
-inline void lm_reduce_host(int n, const uint8_t *mask, int nv, double *part, double *out, F f, int slots = kLmThreads) {
-    for (int q = 0; q < slots * nv; ++q) part[q] = 0.0;
-    for (int tid = 0; tid < slots; ++tid)
-        for (int i = tid; i < n; i += slots)
-            if (mask[i]) f(i, part + tid * nv);
+// the wave trees and the left-to-right sum of the wave sums of slots part[slot * nv + q]
+inline void lm_tree_host(const double *part, int slots, int nv, double *out) {
     double v[64], w[64];
     for (int q = 0; q < nv; ++q) out[q] = 0.0;
     for (int wv = 0; wv < slots / 64; ++wv)
@@ -856,6 +856,32 @@ inline void lm_reduce_host(int n, const uint8_t *mask, int nv, double *part, dou
             }
             out[q] = wv == 0 ? v[0] : out[q] + v[0];  // wave sums left to right
         }
+}
+
+// Host/oracle-side mirror of the GPU EPnP reduction: sum f(i, acc) over points with
+// mask[i] != 0, point i to slot i % kLmThreads; part: kLmThreads * nv doubles.
+template <class F>
+inline void lm_reduce_host(int n, const uint8_t *mask, int nv, double *part, double *out, F f) {
+    for (int q = 0; q < kLmThreads * nv; ++q) part[q] = 0.0;
+    for (int tid = 0; tid < kLmThreads; ++tid)
+        for (int i = tid; i < n; i += kLmThreads)
+            if (mask[i]) f(i, part + tid * nv);
+    lm_tree_host(part, kLmThreads, nv, out);
+}
+
+// the LM refit's block-compacted order (above); part: lm_blocks(n) * kLmThreads * nv doubles
+template <class F>
+inline void lm_reduce_blocks_host(int n, const uint8_t *mask, int nv, double *part, double *out, F f) {
+    const int nb = lm_blocks(n), C = lm_chunk(n);
+    for (int q = 0; q < nb * kLmThreads * nv; ++q) part[q] = 0.0;
+    for (int b = 0; b < nb; ++b) {
+        const int64_t end = (int64_t)(b + 1) * C;
+        const int hi = end < n ? (int)end : n;
+        int p = 0;
+        for (int i = b * C; i < hi; ++i)
+            if (mask[i]) f(i, part + (b * kLmThreads + p++ % kLmThreads) * nv);
+    }
+    lm_tree_host(part, nb * kLmThreads, nv, out);
 }
 
 // ---------------------------------------------------------------------------

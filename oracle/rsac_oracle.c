@@ -982,18 +982,25 @@ ORC_API int64_t orc_fm_ransac(const float *x1, const float *y1, const float *x2,
  * at most 20 iterations, stop when the relative cost decrease < 1e-12 or
  * |d| < FLT_EPSILON (|t| + 1) (CvLevMarq's step criterion of solvePnP).
  * The pose is refined in the frame centred on the first point c (t' = R c + t).
- * Sums use the GPU kernel's order: S strided per-slot partials (S = lm_slots(n): 512 up to
- * 4096 points, then doubled while n > 8 S, at most 32768), a 64-lane butterfly per wave of
- * 64 slots (x += x[lane ^ o], o = 32..1), then the S/64 wave sums left to right -- so the
- * HIP kernel k_pnp_refine reproduces this bit for bit. */
+ * Sums use the GPU kernel's block-compacted order: nb = lm_blocks(n) contiguous ranges of
+ * lm_chunk(n) points (one range up to 4096 points, then ranges of ~2048, at most 64); the
+ * masked points of range b, ascending, dealt round-robin to slots b*512 + p%512; per-slot
+ * sums in order, a 64-lane butterfly per wave of 64 slots (x += x[lane ^ o], o = 32..1),
+ * then the nb*8 wave sums left to right -- so the HIP kernel k_pnp_refine reproduces this
+ * bit for bit. */
 #define LM_THREADS 512
-#define LM_MAX_SLOTS 32768
+#define LM_MAX_BLOCKS 64
+#define LM_BLOCK_POINTS 2048
 #define LM_TERMS 27
 
-static int lm_slots(int n) {
-    int S = LM_THREADS;
-    while (S < LM_MAX_SLOTS && n > 8 * S) S *= 2;
-    return S;
+static int lm_blocks(int n) {
+    if (n <= 2 * LM_BLOCK_POINTS) return 1;
+    int nb = (n + LM_BLOCK_POINTS - 1) / LM_BLOCK_POINTS;
+    return nb < LM_MAX_BLOCKS ? nb : LM_MAX_BLOCKS;
+}
+static int lm_chunk(int n) {
+    int nb = lm_blocks(n);
+    return (int)(((int64_t)n + nb - 1) / nb);
 }
 
 typedef struct { const float *X, *Y, *Z, *U, *V; const uint8_t *mask; int n; double cam[4]; double *part; double c[3]; } lmctx;
@@ -1036,14 +1043,17 @@ static double lm_cost_point(const lmctx *c, const double *R, const double *t, in
 /* nv = LM_TERMS: normal equations; nv = 1: cost */
 static void lm_reduce(lmctx *c, const double *R, const double *t, int nv, double *out) {
     double *part = c->part;
-    const int S = lm_slots(c->n);
+    const int nb = lm_blocks(c->n), C = lm_chunk(c->n), S = nb * LM_THREADS;
     for (int q = 0; q < S * nv; ++q) part[q] = 0.0;
-    for (int tid = 0; tid < S; ++tid)
-        for (int i = tid; i < c->n; i += S) {
+    for (int b = 0; b < nb; ++b) {
+        int hi = (int64_t)(b + 1) * C < c->n ? (b + 1) * C : c->n, p = 0;
+        for (int i = b * C; i < hi; ++i) {
             if (!c->mask[i]) continue;
-            if (nv == 1) part[tid] += lm_cost_point(c, R, t, i);
-            else lm_point(c, R, t, i, part + tid * nv);
+            const int slot = b * LM_THREADS + p++ % LM_THREADS;
+            if (nv == 1) part[slot] += lm_cost_point(c, R, t, i);
+            else lm_point(c, R, t, i, part + slot * nv);
         }
+    }
     double v[64], w[64];
     for (int wv = 0; wv < S / 64; ++wv)
         for (int q = 0; q < nv; ++q) {
@@ -1103,7 +1113,7 @@ ORC_API int orc_pnp_refine(const float *X, const float *Y, const float *Z, const
                            const uint8_t *mask, int n, const double cam[4], double R[9], double t[3], int max_iter) {
     if (n <= 0) return 0;
     lmctx c = {X, Y, Z, U, V, mask, n, {cam[0], cam[1], cam[2], cam[3]}, NULL, {X[0], Y[0], Z[0]}};
-    c.part = (double *)malloc(sizeof(double) * lm_slots(n) * LM_TERMS);
+    c.part = (double *)malloc(sizeof(double) * lm_blocks(n) * LM_THREADS * LM_TERMS);
     /* refit frame centred on the first point: t' = R c + t */
     for (int j = 0; j < 3; ++j) t[j] = R[3 * j] * c.c[0] + R[3 * j + 1] * c.c[1] + R[3 * j + 2] * c.c[2] + t[j];
     double lam = 1e-3, cost, acc[LM_TERMS];

@@ -47,17 +47,23 @@ def test_host_only_helpers():
     assert rsac.update_num_iters(0.99, 0.5, 4, 5000) == 71
 
 
-@pytest.mark.parametrize("n", [500, 9000, 70000])  # 9000 / 70000: lm_slots(n) = 2048 / 16384 (multi-block order)
-def test_host_refine_matches_oracle(n):
+# 9000 / 70000 / 300000: 5 / 35 / 64 ranges of the block-compacted order (the last one's ranges
+# exceed one LDS tile on the GPU); masked: every third point dropped, so ranges compact unevenly
+@pytest.mark.parametrize("n,masked", [(500, False), (4097, True), (9000, False), (9000, True), (70000, True),
+                                      (300000, True)])
+def test_host_refine_matches_oracle(n, masked):
     import pyoracle as O
     import rsac
     from rsac import synth
     pr = synth.pnp_problem(n, 0.0, seed=5, noise_px=0.5)
     R0 = synth.random_rotation(np.random.default_rng(9)) * 0 + pr["R"]
     t0 = pr["t"] + np.array([0.5, -0.3, 0.2])
-    R, t = rsac.refine_pose(pr["points2d"], pr["points3d"], pr["K"], R0, t0)
+    mask = np.ones(n, np.uint8)
+    if masked:
+        mask[np.random.default_rng(n).random(n) < 0.33] = 0
+    R, t = rsac.refine_pose(pr["points2d"], pr["points3d"], pr["K"], R0, t0, mask=mask if masked else None)
     soa = O.soa_pnp(pr["points3d"], pr["points2d"])
-    Ro, to, _ = O.pnp_refine(soa, np.ones(n, np.uint8), O.cam_from_K(pr["K"]), R0, t0)
+    Ro, to, _ = O.pnp_refine(soa, mask, O.cam_from_K(pr["K"]), R0, t0)
     # same arithmetic and summation order (the GPU kernel's) on both sides: bit-identical
     np.testing.assert_array_equal(R, Ro)
     np.testing.assert_array_equal(t, to)

@@ -453,6 +453,19 @@ def test_batched_refit_bit_exact_per_problem():
         assert _bits_equal(R, Ro) and _bits_equal(t, to)
 
 
+@pytest.mark.parametrize("n,outl", [(4096, 0.3), (4097, 0.6), (300000, 0.5)])
+def test_refit_block_ranges_bit_exact(n, outl):
+    # one range at 4096 points, two at 4097; 300000 points: 64 ranges of 4688 indices, each
+    # more than one LDS tile, so every pass re-stages its tiles (k_pnp_refine tile path)
+    pr = synth.pnp_problem(n, outl, seed=77)
+    R, t, m = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=True)
+    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 2000, 0x5EED)
+    np.testing.assert_array_equal(m, ref["mask"])
+    soa = O.soa_pnp(pr["points3d"], pr["points2d"])
+    Ro, to, _ = O.pnp_refine(soa, ref["mask"].astype(np.uint8), O.cam_from_K(pr["K"]), ref["R"], ref["t"])
+    assert _bits_equal(R, Ro) and _bits_equal(t, to)
+
+
 # ---------------------------------------------------------------------------------------------
 # LO-RANSAC (BASELINE.json configs[4])
 # ---------------------------------------------------------------------------------------------
