@@ -145,7 +145,6 @@ struct rsac_ctx {
     DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
     DevBuf lmscr;                                              // multi-block LM refit: tagged wave sums
     LmScratch lm;                                              // ... and its launch counter
-    DevBuf scanrec;                                            // single-round scans: improvement records
     std::vector<char> last_tables;                             // the tables last uploaded (stage_tables)
     void *last_tables_dev = nullptr;
     // pinned host staging
@@ -385,6 +384,10 @@ struct LoopOut {
     int64_t scored = 0;
     double gpu_ms = 0, solve_ms = 0, score_ms = 0;
     int32_t lo_improvements = 0;
+    // speculative first round (run_loop with a ScanDecide): the records are on their way to
+    // the host and the device has picked the winner; spec_resolve replays and verifies
+    bool spec_pending = false;
+    int64_t spec_H = 0;
 };
 
 // LO-RANSAC local optimisation of the new best of problem 0 (DESIGN.md "LO-RANSAC";
@@ -451,7 +454,7 @@ void add_times(rsac_ctx *c, double &gpu, double &solve, double &score) {
 }
 
 int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max_iters, double confidence,
-             uint32_t flags, hipStream_t s, LoopOut &out) {
+             uint32_t flags, hipStream_t s, LoopOut &out, const ScanDecide *spec = nullptr, bool resume = false) {
     const int P = st.P;
     const int64_t H = std::max(max_iters, 1);
     const bool adaptive = (flags & RSAC_F_ADAPTIVE) != 0;
@@ -488,11 +491,17 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
     }
 #undef SETARG
 
-    out.scan.assign(P, ScanState());
-    for (auto &sc : out.scan) sc.reset((int)H);
     // adaptive: the first round is short (most runs stop within it), later ones double
     int64_t cur = adaptive ? std::min<int64_t>(round, 256) : round;
-    for (int64_t hb = 0, Hr = 0; hb < H; hb += Hr) {
+    int64_t hb0 = 0;
+    if (resume) {  // after a verified speculative first round (philox: no sampler state to carry)
+        hb0 = out.spec_H;
+        cur = std::min<int64_t>(cur * 2, round);
+    } else {
+        out.scan.assign(P, ScanState());
+        for (auto &sc : out.scan) sc.reset((int)H);
+    }
+    for (int64_t hb = hb0, Hr = 0; hb < H; hb += Hr) {
         Hr = std::min<int64_t>(cur, H - hb);
         cur = std::min<int64_t>(cur * 2, round);
         if (opencv) {
@@ -537,11 +546,15 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
         // LO) copy every count
         std::vector<int> full;  // problems scanned from their full count / status rows
         if (!lo && hb == 0) {
-            HIPCHK(c->scanrec.ensure(sizeof(ScanRecords) * P));
             HIPCHK(c->h_scanrec.ensure(sizeof(ScanRecords) * P));
+            // the kernel writes the records straight into pinned host memory (no copy launch)
             HIPCHK(launch_scan_records(c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, P, (int32_t)Hr,
-                                       model_points, c->scanrec.as<ScanRecords>(), s));
-            HIPCHK(hipMemcpyAsync(c->h_scanrec.p, c->scanrec.p, sizeof(ScanRecords) * P, hipMemcpyDeviceToHost, s));
+                                       model_points, c->h_scanrec.as<ScanRecords>(), s, spec ? *spec : ScanDecide()));
+            if (spec) {  // no synchronisation: the caller enqueues the finish, then spec_resolve
+                out.spec_pending = true;
+                out.spec_H = Hr;
+                return RSAC_OK;
+            }
             HIPCHK(hipStreamSynchronize(s));
             const ScanRecords *rec = c->h_scanrec.as<ScanRecords>();
             for (int p = 0; p < P; ++p) {
@@ -608,17 +621,41 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
     return RSAC_OK;
 }
 
+// after the stream synchronised: the host's replay of a speculative first round (one problem).
+// ok: it ended the scan with the winner the device picked (the finish enqueued on the device's
+// pick is the result); otherwise the caller starts over without speculation.
+int spec_resolve(rsac_ctx *c, const Staged &st, LoopOut &out, int model_points, double confidence, bool &ok) {
+    const ScanRecords &rec = *c->h_scanrec.as<ScanRecords>();
+    out.spec_pending = false;
+    ok = false;
+    if (rec.nrec < 0) {  // more improvements than records: the caller runs the loop afresh
+        out.scan[0].reset((int)out.scan[0].niters);
+        out.spec_H = 0;
+        return RSAC_OK;
+    }
+    const int np = (int)(st.off[1] - st.off[0]);
+    scan_records(out.scan[0], rec.idx, rec.cnt, rec.nrec, rec.first_neg, out.spec_H, np, model_points, confidence);
+    add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
+    out.rounds = 1;
+    out.scored = out.spec_H;
+    ok = out.scan[0].done && rec.dev_done && out.scan[0].best == (int64_t)rec.dev_best;
+    return RSAC_OK;
+}
+
 // masks + winning models of every problem; records of winners -> c->best
 // defer_sync: leave the stream running (the caller enqueues more work, synchronises, then
 // calls finish_masks_host to copy a host mask out)
+// dev_best: the winners' record indices are already on the device (c->best, a speculative
+// first round), not in lo
 int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const LoopOut &lo, int64_t stride,
-                 uint8_t *mask_out, uint32_t flags, hipStream_t s, bool defer_sync = false) {
+                 uint8_t *mask_out, uint32_t flags, hipStream_t s, bool defer_sync = false, bool dev_best = false) {
     const int P = st.P;
     int64_t *hb = c->h_best.as<int64_t>();
     for (int p = 0; p < P; ++p) hb[p] = lo.scan[p].best >= 0 ? (int64_t)p * stride + lo.scan[p].best : -1;
     // one problem: the record index goes as a kernel argument (no upload)
-    const int64_t *dbest = P == 1 ? nullptr : c->best.as<int64_t>();
-    if (P > 1) HIPCHK(hipMemcpyAsync(c->best.p, hb, sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
+    const int64_t *dbest = P == 1 && !dev_best ? nullptr : c->best.as<int64_t>();
+    if (P > 1 && !dev_best)
+        HIPCHK(hipMemcpyAsync(c->best.p, hb, sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
     const int64_t N = st.total;
     // PnP: the mask kernel also gathers the winners' records (one launch fewer)
     const bool fused_gather = model == Model::PnP && N > 0;
@@ -634,15 +671,16 @@ int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const L
         dmask = c->mask.as<uint8_t>();
     }
     if (N > 0) {
-        if (model == Model::PnP)
-            HIPCHK(launch_pnp_mask(*(PnpArgs *)args, P, max_n, dbest, dmask, s, hb[0], c->bestmodels.as<double>()));
+        if (model == Model::PnP)  // without a refit the winners also go straight to the pinned host records
+            HIPCHK(launch_pnp_mask(*(PnpArgs *)args, P, max_n, dbest, dmask, s, hb[0], c->bestmodels.as<double>(),
+                                   defer_sync ? nullptr : c->h_bestmodels.as<double>()));
         else if (model == Model::Fm)
             HIPCHK(launch_fm_mask(*(HomArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
         else
             HIPCHK(launch_hom_mask(*(HomArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
     }
     // the winners' records for the host (a refit copies the refined ones instead)
-    if (!defer_sync)
+    if (!defer_sync && !(model == Model::PnP && N > 0))
         HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
                               hipMemcpyDeviceToHost, s));
     if (!(flags & RSAC_F_DEVICE_OUT) && mask_out && N > 0) {
@@ -683,6 +721,46 @@ int host_mask(rsac_ctx *c, const Staged &st, uint8_t *mask_out, uint32_t flags, 
     return RSAC_OK;
 }
 
+// the winners' masks, then the final solve on the device, one block per problem, on the
+// RANSAC-phase inliers: EPnP (solvePnPRansac with SOLVEPNP_P3P), then / or LM
+// (solvePnPRefineLM); returns with the stream synchronised and c->h_bestmodels filled.
+// dev_best: the winners come from the device's speculative replay (c->best)
+int pnp_finish(rsac_ctx *c, const Staged &st, const PnpArgs &a, const LoopOut &lo, int64_t stride, const double *K,
+               uint8_t *mask_out, uint32_t flags, hipStream_t s, bool refit, bool dev_best) {
+    const int P = st.P;
+    int r = finish_masks(c, Model::PnP, st, (void *)&a, lo, stride, mask_out, flags, s, refit, dev_best);
+    if (r || !refit) return r;
+    const uint8_t *dmask = (flags & RSAC_F_DEVICE_OUT) && mask_out ? mask_out : c->mask.as<uint8_t>();
+    if (flags & RSAC_F_EPNP) {
+        // stage 1 (sums) on the device, stage 2 (12 x 12 eigenvectors + betas, O(1)) on the
+        // host, stage 3 (pose candidates) on the device
+        const size_t b1 = sizeof(EpnpStage1) * P, b2 = sizeof(EpnpStage2) * P;
+        HIPCHK(c->epnp.ensure(b1 + b2));
+        HIPCHK(c->h_epnp.ensure(b1 + b2));
+        EpnpStage1 *d1 = c->epnp.as<EpnpStage1>(), *h1 = c->h_epnp.as<EpnpStage1>();
+        EpnpStage2 *d2 = (EpnpStage2 *)(d1 + P), *h2 = (EpnpStage2 *)(h1 + P);
+        HIPCHK(launch_pnp_epnp_s1(a, P, dmask, c->bestmodels.as<double>(), d1, s));
+        HIPCHK(hipMemcpyAsync(h1, d1, b1, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        parallel_for(P, [&](int p) {
+            const double *Kp = K + 9 * p;
+            if (h1[p].ok != 0.0) epnp_stage2(h1[p], Cam{Kp[0], Kp[4], Kp[2], Kp[5]}, h2[p]);
+            else memset(&h2[p], 0, sizeof(EpnpStage2));
+        });
+        HIPCHK(hipMemcpyAsync(d2, h2, b2, hipMemcpyHostToDevice, s));
+        HIPCHK(launch_pnp_epnp_s3(a, P, dmask, d1, d2, c->bestmodels.as<double>(), s));
+    }
+    if (flags & RSAC_F_REFINE)  // the refit also writes R, t into the pinned host records
+        HIPCHK(launch_pnp_refine(a, P, dmask, c->bestmodels.as<double>(), nullptr, s, lm_scratch(c, s),
+                                 st.off.data(), c->h_bestmodels.as<double>()));
+    else
+        HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
+                              hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    finish_masks_host(c, st, mask_out, flags);
+    return RSAC_OK;
+}
+
 int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *offsets, int32_t P, int32_t n,
              const double *K, int32_t n_iters, double thr, double conf, uint64_t seed, uint32_t flags, double *R_out,
              double *t_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out, rsac_stats *stats,
@@ -701,43 +779,40 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     PnpArgs a;
     r = pnp_args(c, st, flags, seed, stride, 0, s, a);
     if (r) return r;
+    // one adaptive problem: the device replays the first round's scan itself and the final mask
+    // and refit are enqueued behind it, so the call synchronises once; the host verifies the
+    // device's pick afterwards and redoes the call without speculation on a mismatch (a libm
+    // ulp in RANSACUpdateNumIters) or when the first round did not end the scan
+    const bool spec = P == 1 && (flags & RSAC_F_ADAPTIVE) && !(flags & (RSAC_F_LO | RSAC_F_SAMPLER_OPENCV)) &&
+                      st.total > 0;
+    ScanDecide dec;
+    if (spec) {
+        dec.best_out = c->best.as<int64_t>();
+        dec.n = (int32_t)st.total;
+        dec.max_iters = std::max(n_iters, 1);
+        dec.confidence = conf;
+    }
     LoopOut lo;
-    r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo);
+    r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, spec ? &dec : nullptr);
     if (r) return r;
     const bool refit = (flags & (RSAC_F_REFINE | RSAC_F_EPNP)) != 0;
-    r = finish_masks(c, Model::PnP, st, &a, lo, stride, mask_out, flags, s, refit);
+    r = pnp_finish(c, st, a, lo, stride, K, mask_out, flags, s, refit, lo.spec_pending);
     if (r) return r;
-    if (refit) {
-        // final solve on the device, one block per problem, on the RANSAC-phase inliers:
-        // EPnP (solvePnPRansac with SOLVEPNP_P3P), then / or LM (solvePnPRefineLM)
-        const uint8_t *dmask = (flags & RSAC_F_DEVICE_OUT) && mask_out ? mask_out : c->mask.as<uint8_t>();
-        if (flags & RSAC_F_EPNP) {
-            // stage 1 (sums) on the device, stage 2 (12 x 12 eigenvectors + betas, O(1)) on the
-            // host, stage 3 (pose candidates) on the device
-            const size_t b1 = sizeof(EpnpStage1) * P, b2 = sizeof(EpnpStage2) * P;
-            HIPCHK(c->epnp.ensure(b1 + b2));
-            HIPCHK(c->h_epnp.ensure(b1 + b2));
-            EpnpStage1 *d1 = c->epnp.as<EpnpStage1>(), *h1 = c->h_epnp.as<EpnpStage1>();
-            EpnpStage2 *d2 = (EpnpStage2 *)(d1 + P), *h2 = (EpnpStage2 *)(h1 + P);
-            HIPCHK(launch_pnp_epnp_s1(a, P, dmask, c->bestmodels.as<double>(), d1, s));
-            HIPCHK(hipMemcpyAsync(h1, d1, b1, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
-            parallel_for(P, [&](int p) {
-                const double *Kp = K + 9 * p;
-                if (h1[p].ok != 0.0) epnp_stage2(h1[p], Cam{Kp[0], Kp[4], Kp[2], Kp[5]}, h2[p]);
-                else memset(&h2[p], 0, sizeof(EpnpStage2));
-            });
-            HIPCHK(hipMemcpyAsync(d2, h2, b2, hipMemcpyHostToDevice, s));
-            HIPCHK(launch_pnp_epnp_s3(a, P, dmask, d1, d2, c->bestmodels.as<double>(), s));
+    if (lo.spec_pending) {
+        bool ok = false;
+        r = spec_resolve(c, st, lo, 4, conf, ok);
+        if (r) return r;
+        if (!ok) {
+            // the host's replay rules: later rounds if the scan goes on, then the finish again
+            if (!lo.scan[0].done) {
+                r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, nullptr, true);
+                if (r) return r;
+            }
+            r = pnp_finish(c, st, a, lo, stride, K, mask_out, flags, s, refit, false);
+            if (r) return r;
         }
-        if (flags & RSAC_F_REFINE)
-            HIPCHK(launch_pnp_refine(a, P, dmask, c->bestmodels.as<double>(), nullptr, s, lm_scratch(c, s),
-                                     st.off.data()));
-        HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
-                              hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        finish_masks_host(c, st, mask_out, flags);
     }
+
     const double *bm = c->h_bestmodels.as<double>();
     for (int p = 0; p < P; ++p) {
         const bool ok = lo.scan[p].best >= 0;
@@ -876,7 +951,7 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr, &c->scanrec};
+                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};

@@ -115,9 +115,19 @@ constexpr int kScanRecs = 14;
 struct ScanRecords {
     int32_t nrec, first_neg;  // first_neg = H when no status < 0
     int32_t idx[kScanRecs], cnt[kScanRecs];
+    int32_t dev_best, dev_done;  // the device's replay (ScanDecide), for the host to verify
+};
+// optional device replay of problem 0's first round (scan_records with the device's libm):
+// best record index (stride 0 problem: the hypothesis) -> *best_out, so the final mask and refit
+// can be enqueued before the host has seen the records; the host's own replay decides
+struct ScanDecide {
+    int64_t *best_out = nullptr;
+    int32_t n = 0;
+    int64_t max_iters = 0;
+    double confidence = 0;
 };
 hipError_t launch_scan_records(const int32_t *counts, const int8_t *status, int64_t stride, int32_t P, int32_t H,
-                               int model_points, ScanRecords *out, hipStream_t s);
+                               int model_points, ScanRecords *out, hipStream_t s, ScanDecide dec = ScanDecide());
 
 // best packed key of counts[0, H) (+ its model record -> model_out[16]);
 // key = 0 when no hypothesis has a model with >= 1 inlier
@@ -146,7 +156,8 @@ bool score_variant_mx();        // the selected variant is an MFMA one (needs PF
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                           hipStream_t s, int64_t best0 = -1, double *model_out = nullptr);
+                           hipStream_t s, int64_t best0 = -1, double *model_out = nullptr,
+                           double *host_model_out = nullptr);
 hipError_t launch_hom_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
 hipError_t launch_hom_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
@@ -176,7 +187,8 @@ struct LmScratch {
     unsigned launch = 0;
 };
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
-                             hipStream_t s, LmScratch *scratch, const int64_t *host_off);
+                             hipStream_t s, LmScratch *scratch, const int64_t *host_off,
+                             double *host_models = nullptr);  // pinned: R, t also written there
 
 // mask + inlier count (atomically into *count, zeroed by the caller) of one model record, problem 0
 hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, int32_t *count,

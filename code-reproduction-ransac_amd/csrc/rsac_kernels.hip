@@ -1478,13 +1478,16 @@ __global__ __launch_bounds__(256) void k_pnp_score(PnpArgs a, int64_t hyp_begin,
 // model_out (optional): block 0 of every problem also copies the winner's record there
 // (k_gather_models' output, one launch fewer)
 __global__ void k_pnp_mask(PnpArgs a, const int64_t *__restrict__ best, int64_t best0, uint8_t *__restrict__ mask,
-                           double *__restrict__ model_out) {
+                           double *__restrict__ model_out, double *__restrict__ host_model_out) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
     const int64_t b = best ? best[prob] : best0;  // best0: the one problem's record, no upload
-    if (model_out && blockIdx.x == 0 && threadIdx.x < kModelStride)
-        model_out[(int64_t)prob * kModelStride + threadIdx.x] = b >= 0 ? a.models[b * kModelStride + threadIdx.x] : 0.0;
+    if (model_out && blockIdx.x == 0 && threadIdx.x < kModelStride) {
+        const double v = b >= 0 ? a.models[b * kModelStride + threadIdx.x] : 0.0;
+        model_out[(int64_t)prob * kModelStride + threadIdx.x] = v;
+        if (host_model_out) host_model_out[(int64_t)prob * kModelStride + threadIdx.x] = v;  // pinned host copy
+    }
     const double *c = a.cams + 4 * prob;
     const Cam k{c[0], c[1], c[2], c[3]};
     const float thr2 = a.thr2[prob];
@@ -1778,12 +1781,30 @@ __global__ __launch_bounds__(256) void k_best_key(const int32_t *__restrict__ co
 }
 
 // one wave per problem: 64 hypotheses per step, the running maximum carried across steps
+// RANSACUpdateNumIters (rsac_host.hip update_num_iters) with the device's pow / log / lrint:
+// may differ from the host's in a last-ulp tie, which is why the host re-checks the decision
+__device__ int update_num_iters_dev(double p, double ep, int model_points, int max_iters) {
+    p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
+    double num = 1. - p;
+    if (num < 2.2250738585072014e-308) num = 2.2250738585072014e-308;
+    double denom = 1. - pow(1. - ep, model_points);
+    if (denom < 2.2250738585072014e-308) return 0;
+    num = log(num);
+    denom = log(denom);
+    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)lrint(num / denom);
+}
+
 __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict__ counts,
                                                       const int8_t *__restrict__ status, int64_t stride, int32_t P,
-                                                      int32_t H, int model_points, ScanRecords *__restrict__ out) {
+                                                      int32_t H, int model_points, ScanRecords *__restrict__ out,
+                                                      ScanDecide dec) {
+    // records kept in LDS and written out once: out may be pinned host memory (no copy back)
+    __shared__ int32_t sidx[4][kScanRecs], scnt[4][kScanRecs];
     const int prob = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (prob >= P) return;  // wave-uniform
     const int lane = threadIdx.x & 63;
+    int32_t *ridx = sidx[threadIdx.x >> 6], *rcnt = scnt[threadIdx.x >> 6];
     const int32_t *c = counts + (int64_t)prob * stride;
     const int8_t *st = status + (int64_t)prob * stride;
     int floor_c = model_points - 1;  // the scan's floor: max(s - 1, best count so far)
@@ -1801,8 +1822,8 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
             const int l = __builtin_ctzll(cand);
             const int cv = __shfl(v, l);
             if (nrec < kScanRecs && lane == 0) {
-                o.idx[nrec] = b + l;
-                o.cnt[nrec] = cv;
+                ridx[nrec] = b + l;
+                rcnt[nrec] = cv;
             }
             ++nrec;
             floor_c = cv;
@@ -1816,13 +1837,34 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
     if (lane == 0) {
         o.nrec = nrec <= kScanRecs ? nrec : -1;
         o.first_neg = first_neg;
+        for (int r = 0; r < nrec && r < kScanRecs; ++r) {
+            o.idx[r] = ridx[r];
+            o.cnt[r] = rcnt[r];
+        }
+    }
+    if (dec.best_out && prob == 0 && lane == 0) {
+        // scan_records (rsac_host.hip) on the records just written by this lane
+        int64_t niters = dec.max_iters > 1 ? dec.max_iters : 1, best = -1;
+        const int nr = nrec <= kScanRecs ? nrec : 0;
+        for (int r = 0; r < nr; ++r) {
+            const int64_t stop = first_neg < niters ? first_neg : niters;
+            if (ridx[r] >= stop) break;
+            best = ridx[r];
+            niters = update_num_iters_dev(dec.confidence, (double)(dec.n - rcnt[r]) / dec.n, model_points,
+                                          (int)niters);
+        }
+        const int64_t stop = first_neg < niters ? first_neg : niters;
+        const bool done = nrec <= kScanRecs && (stop < H || H >= niters);
+        *dec.best_out = done ? best : -1;  // not done: the speculative finish has no model (cheap no-op)
+        o.dev_best = (int32_t)best;
+        o.dev_done = done;
     }
 }
 
 hipError_t launch_scan_records(const int32_t *counts, const int8_t *status, int64_t stride, int32_t P, int32_t H,
-                               int model_points, ScanRecords *out, hipStream_t s) {
+                               int model_points, ScanRecords *out, hipStream_t s, ScanDecide dec) {
     hipLaunchKernelGGL(k_scan_records, dim3((P + 3) / 4), dim3(256), 0, s, counts, status, stride, P, H, model_points,
-                       out);
+                       out, dec);
     return hipGetLastError();
 }
 
@@ -2021,6 +2063,16 @@ static void launch_mx(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H,
 
 bool score_variant_mx() { return g_score_variant >= 30 && g_score_variant < 40; }
 
+// RSAC_SMALL_PP / RSAC_SMALL_TILES: tuning knobs of the small-round scoring instance
+static int small_round_pp() {
+    static const int v = [] { const char *e = getenv("RSAC_SMALL_PP"); return e ? atoi(e) : 2; }();
+    return v;
+}
+static int64_t small_round_tiles() {
+    static const int64_t v = [] { const char *e = getenv("RSAC_SMALL_TILES"); return e ? atoll(e) : 16; }();
+    return v;
+}
+
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
     if (a.max_n > 0 && a.max_n <= kLanePts) {
@@ -2062,7 +2114,20 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 22: launch_f32<4, 32, 3, 6>(a, P, hyp_begin, H, counts, s); break;
             case 23: launch_f32<8, 32, 3, 5>(a, P, hyp_begin, H, counts, s); break;
             case 24: launch_f32<2, 32, 3, 6>(a, P, hyp_begin, H, counts, s); break;
-            case 25: launch_f32<8, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 25:
+                // a round of only a few hypothesis tiles (an adaptive run's first 256): 2 points per
+                // lane, so the point split gives 4x the units and the GPU fills
+                if ((int64_t)P * ((H + 31) / 32) <= small_round_tiles())
+                    switch (small_round_pp()) {
+                        case 4: launch_f32<4, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+                        case 8: launch_f32<8, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+                        case 1: launch_f32<1, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+                        case 16: launch_f32<2, 16, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+                        default: launch_f32<2, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+                    }
+                else
+                    launch_f32<8, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s);
+                break;
             case 26: launch_f32<8, 32, 3, 5, false, true>(a, P, hyp_begin, H, counts, s); break;
             case 27: launch_f32<8, 32, 3, 5, true, false>(a, P, hyp_begin, H, counts, s); break;
             case 28: launch_f32<4, 32, 3, 6, true, true>(a, P, hyp_begin, H, counts, s); break;
@@ -2075,10 +2140,10 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
-                           hipStream_t s, int64_t best0, double *model_out) {
+                           hipStream_t s, int64_t best0, double *model_out, double *host_model_out) {
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g > 1024) g = 1024;
-    hipLaunchKernelGGL(k_pnp_mask, dim3(g, P), dim3(256), 0, s, a, best, best0, mask, model_out);
+    hipLaunchKernelGGL(k_pnp_mask, dim3(g, P), dim3(256), 0, s, a, best, best0, mask, model_out, host_model_out);
     return hipGetLastError();
 }
 
@@ -2525,7 +2590,8 @@ struct GpuLmReducer {
 // their blocks co-resident: the launcher keeps them to one problem per launch (<= 64 blocks).
 __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint8_t *__restrict__ mask,
                                                            double *__restrict__ models, int32_t *__restrict__ iters,
-                                                           int prob_base, unsigned long long *gran, unsigned tag_base) {
+                                                           int prob_base, unsigned long long *gran, unsigned tag_base,
+                                                           double *host_models) {
     __shared__ double wsum[kLmThreads / 64][kLmRed];
     __shared__ double accs[2][kLmRed], res[1];
     __shared__ int scan[kLmThreads / 64];
@@ -2539,6 +2605,8 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     double *m = models + (int64_t)prob * kModelStride;
     if (m[kValidSlot] == 0.0) {  // no model: block-uniform exit
         if (threadIdx.x == 0 && blockIdx.x == 0 && iters) iters[prob] = 0;
+        if (host_models && blockIdx.x == 0 && threadIdx.x < 12)
+            host_models[(int64_t)prob * kModelStride + threadIdx.x] = m[threadIdx.x];
         return;
     }
     const double *cm = a.cams + 4 * prob;
@@ -2572,6 +2640,11 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
         for (int j = 0; j < 9; ++j) m[j] = R[j];
         for (int j = 0; j < 3; ++j) m[9 + j] = t[j];
         if (iters) iters[prob] = it;
+        if (host_models) {  // pinned host memory: the result without a copy launch
+            double *h = host_models + (int64_t)prob * kModelStride;
+            for (int j = 0; j < 9; ++j) h[j] = R[j];
+            for (int j = 0; j < 3; ++j) h[9 + j] = t[j];
+        }
     }
 }
 
@@ -2704,14 +2777,14 @@ hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, 
 }
 
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
-                             hipStream_t s, LmScratch *scratch, const int64_t *host_off) {
+                             hipStream_t s, LmScratch *scratch, const int64_t *host_off, double *host_models) {
     // every problem of up to 4096 points (and, with host_off unknown, every problem) in one
     // launch, one block each; each larger problem in a launch of its own, lm_blocks(n)
     // blocks (<= 64, all co-resident) that hand their wave sums over as tagged granules
     const int nb_max = lm_blocks(a.max_n);
     if (!(P == 1 && nb_max > 1))  // (one large problem: only the multi-block launch has work)
         hipLaunchKernelGGL(k_pnp_refine, dim3(1, P), dim3(kLmThreads), 0, s, a, mask, models, iters, 0,
-                           (unsigned long long *)nullptr, 0u);
+                           (unsigned long long *)nullptr, 0u, host_models);
     if (nb_max > 1) {
         if (!scratch || !scratch->gran) return hipErrorInvalidValue;
         for (int p = 0; p < P; ++p) {
@@ -2726,7 +2799,7 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
                 scratch->launch = 1;
             }
             hipLaunchKernelGGL(k_pnp_refine, dim3(nb, 1), dim3(kLmThreads), 0, s, a, mask, models, iters, p,
-                               scratch->gran, scratch->launch << 10);
+                               scratch->gran, scratch->launch << 10, host_models);
         }
     }
     return hipGetLastError();

@@ -453,6 +453,24 @@ def test_batched_refit_bit_exact_per_problem():
         assert _bits_equal(R, Ro) and _bits_equal(t, to)
 
 
+@pytest.mark.parametrize("outl,refine", [(0.85, True), (0.85, False), (0.93, True)])
+def test_speculative_first_round_falls_back(outl, refine):
+    # the first round (256 hypotheses) cannot end these scans: the device's speculative finish is
+    # discarded and the loop resumes at round 2; results equal the restatement's
+    pr = synth.pnp_problem(3000, outl, seed=int(outl * 100))
+    R, t, m, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0, refine=refine,
+                                    return_info=True)
+    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000, 0x5EED)
+    assert info.rounds > 1
+    assert (info.best_hyp, info.n_inliers, info.iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    np.testing.assert_array_equal(m, ref["mask"])
+    if refine:
+        soa = O.soa_pnp(pr["points3d"], pr["points2d"])
+        ref["R"], ref["t"], _ = O.pnp_refine(soa, ref["mask"].astype(np.uint8), O.cam_from_K(pr["K"]), ref["R"],
+                                             ref["t"])
+    assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+
+
 @pytest.mark.parametrize("n,outl", [(4096, 0.3), (4097, 0.6), (300000, 0.5)])
 def test_refit_block_ranges_bit_exact(n, outl):
     # one range at 4096 points, two at 4097; 300000 points: 64 ranges of 4688 indices, each
