@@ -170,11 +170,14 @@ struct Staged {
     std::vector<float> hbuf;                                            // host SoA copy (refits, MWC check)
     const float *h[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     bool host_ready = false;
+    PnpPrepare prep;  // stage_points(defer): the conversion pnp_args fuses into its frame launch
 };
 
 // ncomp3 = 3 for PnP (pts3d N x 3, pts2d N x 2 -> X Y Z U V), 2 for 2D-2D (src, dst -> SX SY DX DY)
+// defer: one device-input PnP problem of <= 65536 points is converted by pnp_args' frame
+// launch (the caller must call pnp_args next)
 int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const int64_t *offsets, int32_t P, int32_t n,
-                 uint32_t flags, hipStream_t s, Staged &st) {
+                 uint32_t flags, hipStream_t s, Staged &st, bool defer = false) {
     st.P = P;
     st.off.resize(P + 1);
     if (offsets) {
@@ -200,6 +203,10 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
     float *D = c->pts.as<float>();
     for (int k = 0; k < nc; ++k) st.d[k] = D + k * N;
     if (flags & RSAC_F_DEVICE_IN) {
+        if (ncomp_a == 3 && defer && P == 1 && N > 0 && N <= 65536) {
+            st.prep = PnpPrepare{(const double *)a, (const double *)b, D, D + N, D + 2 * N, D + 3 * N, D + 4 * N};
+            return RSAC_OK;
+        }
         if (ncomp_a == 3)
             HIPCHK(launch_pnp_prepare((const double *)a, (const double *)b, N, D, D + N, D + 2 * N, D + 3 * N,
                                       D + 4 * N, s));
@@ -344,7 +351,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     }
     // resets best_key and the queue, then builds the frame (also in exact mode: cheap)
     HIPCHK(launch_pnp_frame(a, P, max_n, c->bounds_ws.as<int32_t>(), C, C + N, C + 2 * N, c->frame.as<double>(),
-                            c->fconst.as<float>(), s, PF));
+                            c->fconst.as<float>(), s, PF, &st.prep));
     if (!a.exact_only) {
         a.counts_out = c->counts.as<int32_t>();
         a.XC = C; a.YC = C + N; a.ZC = C + 2 * N;
@@ -769,7 +776,7 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     if (r) return r;
     if (P <= 0 || !K) return fail(RSAC_EINVAL, "bad problem count or K");
     Staged st;
-    r = stage_points(c, pts3d, pts2d, 3, offsets, P, n, flags, s, st);
+    r = stage_points(c, pts3d, pts2d, 3, offsets, P, n, flags, s, st, true);
     if (r) return r;
     r = stage_tables(c, st, K, thr, s);
     if (r) return r;

@@ -141,8 +141,15 @@ hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_
 
 // frame of every problem (centre, bounds, f32 constants) + centred coords;
 // also resets a.best_key (if set) and a.queue.  bounds_ws: P x 10 ints.
+// prep: a deferred device f64 -> f32 conversion of one problem (<= 65536 points) to fuse into
+// the frame launch (k_pnp_setup1); X .. V the staging SoA it fills
+struct PnpPrepare {
+    const double *p3 = nullptr, *p2 = nullptr;
+    float *X = nullptr, *Y = nullptr, *Z = nullptr, *U = nullptr, *V = nullptr;
+};
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *bounds_ws, float *XC, float *YC,
-                            float *ZC, double *frame, float *fconst, hipStream_t s, uint4 *PF = nullptr);
+                            float *ZC, double *frame, float *fconst, hipStream_t s, uint4 *PF = nullptr,
+                            const PnpPrepare *prep = nullptr);
 // f32 records for H given f64 models (rsac_score_poses / rsac_pnp_mask)
 hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_t s);
 hipError_t launch_pnp_prepare(const double *p3, const double *p2, int64_t n, float *X, float *Y, float *Z, float *U,

@@ -264,6 +264,72 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const 
     }
 }
 
+// One problem of up to 65536 points, inputs as device f64 AoS: k_pnp_prepare + k_pnp_bounds1 +
+// k_pnp_center in one 1024-thread block (one launch instead of three; the same values: the f32
+// conversion, the ordered-int bounds, the frame and the centred / MFMA coordinates)
+__global__ __launch_bounds__(1024) void k_pnp_setup1(const double *__restrict__ p3, const double *__restrict__ p2,
+                                                     PnpArgs a, float *__restrict__ X, float *__restrict__ Y,
+                                                     float *__restrict__ Z, float *__restrict__ U,
+                                                     float *__restrict__ V, int *__restrict__ ws,
+                                                     double *__restrict__ frame, float *__restrict__ fconst,
+                                                     float *__restrict__ XC, float *__restrict__ YC,
+                                                     float *__restrict__ ZC, uint4 *__restrict__ PF) {
+    __shared__ float sl[16][5], sh[16][5];
+    __shared__ int wsl[10];
+    const int n = (int)(a.offsets[1] - a.offsets[0]);  // offsets[0] = 0 (one problem)
+    float lo[5], hi[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
+#pragma unroll 4
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const float v[5] = {(float)p3[3 * i], (float)p3[3 * i + 1], (float)p3[3 * i + 2], (float)p2[2 * i],
+                            (float)p2[2 * i + 1]};
+        X[i] = v[0]; Y[i] = v[1]; Z[i] = v[2]; U[i] = v[3]; V[i] = v[4];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { lo[k] = fminf(lo[k], v[k]); hi[k] = fmaxf(hi[k], v[k]); }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
+        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { sl[wave][k] = lo[k]; sh[wave][k] = hi[k]; }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        const int k = threadIdx.x;
+        float l = sl[0][k], h = sh[0][k];
+        for (int w = 1; w < 16; ++w) { l = fminf(l, sl[w][k]); h = fmaxf(h, sh[w][k]); }
+        const int wl = n > 0 ? min(0x7F7F7F7F, f2ord(l)) : 0x7F7F7F7F;
+        const int wh = n > 0 ? max((int)0x80808080, f2ord(h)) : (int)0x80808080;
+        ws[k] = wl;
+        ws[5 + k] = wh;
+        wsl[k] = wl;
+        wsl[5 + k] = wh;
+    }
+    if (threadIdx.x == 0) {
+        if (a.best_key) *a.best_key = 0ull;
+        *a.queue = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) pnp_frame_one(a, 1, 0, wsl, frame, fconst);
+    double cc[3] = {0, 0, 0};
+    if (n > 0)
+        for (int k = 0; k < 3; ++k) cc[k] = ((double)ord2f(wsl[k]) + (double)ord2f(wsl[5 + k])) * 0.5;
+    const float fs = PF ? (float)mx_feature_scale(frame_bound(wsl, 1, 0, n)) : 0.f;
+    for (int i = threadIdx.x; i < n; i += 1024) {  // this thread's own stores above: visible
+        const float xc = (float)((double)X[i] - cc[0]), yc = (float)((double)Y[i] - cc[1]),
+                    zc = (float)((double)Z[i] - cc[2]);
+        XC[i] = xc;
+        YC[i] = yc;
+        ZC[i] = zc;
+        if (PF) PF[i] = mx_point_features(xc * fs, yc * fs, zc * fs);
+    }
+}
+
 // Band of the division-free test from the evaluation error bounds eps (ex, ey, ez: DESIGN.md
 // "Scoring"); tz = the hypothesis' depth of the centre (any w > 0 is valid for the majorant).
 struct BandConsts {
@@ -1908,7 +1974,13 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 }
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
-                            double *frame, float *fconst, hipStream_t s, uint4 *PF) {
+                            double *frame, float *fconst, hipStream_t s, uint4 *PF, const PnpPrepare *prep) {
+    if (prep && prep->p3) {  // the deferred f64 -> f32 conversion of one problem, fused
+        if (P != 1 || max_n > 65536) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_pnp_setup1, dim3(1), dim3(1024), 0, s, prep->p3, prep->p2, a, prep->X, prep->Y, prep->Z,
+                           prep->U, prep->V, ws, frame, fconst, XC, YC, ZC, PF);
+        return hipGetLastError();
+    }
     if (P == 1 && max_n <= 65536) {
         // one block: no atomics, so no initialisation launch (it also resets the key and queue)
         hipLaunchKernelGGL(k_pnp_bounds1, dim3(1), dim3(1024), 0, s, a, ws);

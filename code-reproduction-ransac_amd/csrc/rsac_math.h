@@ -782,10 +782,16 @@ RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
     constexpr bool fused = LmFused<Red>::value;
     double lam = 1e-3;
     RSAC_TRACE_MARK(red, 10);
-    double cost = red.cost(R, t);
-    RSAC_TRACE_MARK(red, 11);
     double *acc = red.acc_buf(0), *acc_next = red.acc_buf(1);
     bool have_next = false;
+    double cost;
+    if constexpr (fused) {  // the start's cost and normal equations in one pass
+        cost = red.cost_normal(R, t, acc_next);
+        have_next = true;
+    } else {
+        cost = red.cost(R, t);
+    }
+    RSAC_TRACE_MARK(red, 11);
     int it;
     for (it = 0; it < max_iter; ++it) {
         if (fused && have_next) {
