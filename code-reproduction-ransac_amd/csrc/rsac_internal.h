@@ -185,10 +185,10 @@ hipError_t launch_pnp_epnp_s1(const PnpArgs &a, int32_t P, const uint8_t *mask, 
                               EpnpStage1 *st1, hipStream_t s);
 hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, const EpnpStage1 *st1,
                               const EpnpStage2 *st2, double *models, hipStream_t s);
-// multi-block refit scratch (problems > 4096 points): the tagged wave-sum granules, two buffers
-// of [64 blocks * 8 waves][28 terms][2] u64, zeroed on allocation and whenever launch wraps;
+// multi-block refit scratch (problems > 4096 points): the tagged block-sum granules, two buffers
+// of [64 blocks][28 terms][2] u64, zeroed on allocation and whenever launch wraps;
 // launch: the per-context launch counter of the tags.  host_off: the problems' offsets (P + 1)
-constexpr size_t kLmGranuleBytes = 2ull * 64 * 8 * 28 * 2 * 8;
+constexpr size_t kLmGranuleBytes = 2ull * 64 * 28 * 2 * 8;
 struct LmScratch {
     unsigned long long *gran = nullptr;
     unsigned launch = 0;

@@ -2381,15 +2381,12 @@ hipError_t launch_loc_score(const double *src, const double *dst, const uint8_t 
 // ---------------------------------------------------------------------------
 constexpr int kLmRed = kLmTerms + 1;  // widest LM reduction: normal equations + cost
 
-// LDS of k_pnp_refine: the staged points (SoA, [5][cap]; cap = 4096 points for one block,
-// 2048 for a range of a multi-block problem), then, multi-block only, the nb * 8 wave sums of a
-// reduction ([wave][kLmRed] doubles, at most 512 waves = 112 KB)
-constexpr int kLmStageOne = 8 * kLmThreads;
-constexpr int kLmStageMulti = 4 * kLmThreads;
-constexpr int kLmWaveSums = kLmMaxBlocks * (kLmThreads / 64);
-constexpr int kLmLdsBytes = 5 * kLmStageMulti * 4 + kLmWaveSums * kLmRed * 8;
-static_assert(5 * kLmStageOne * 4 <= kLmLdsBytes, "single-block stage fits");
-static_assert(kLmBlockPoints <= kLmStageMulti, "a range of ~2048 points fits one tile");
+// LDS of k_pnp_refine: the staged points (SoA, [5][4096]: a range of up to 4096 points is
+// staged once), then, multi-block only, the nb block sums of a reduction ([block][kLmRed])
+constexpr int kLmStage = 8 * kLmThreads;
+constexpr int kLmLdsBytes = 5 * kLmStage * 4 + kLmMaxBlocks * kLmRed * 8;
+static_assert(kLmBlockPoints <= kLmStage, "a range of ~2048 points fits one tile");
+static_assert(kLmMaxBlocks * kLmRed * 2 <= 8 * kLmThreads, "one sweep pass covers every granule");
 
 typedef __attribute__((address_space(1))) unsigned long long lm_gu64;
 constexpr unsigned kLmSpinLimit = 1u << 20;  // ~1 s of polls: a block that never arrives ends the waits
@@ -2408,20 +2405,20 @@ struct GpuLmReducer {
     int nb = 1;
     int lo = 0, hi = 0;
     float *stage = nullptr;  // LDS [5][cap]: compacted X Y Z U V of the range
-    int cap = kLmStageOne;
+    int cap = kLmStage;
     int *scan = nullptr;     // LDS [kLmThreads / 64]: wave totals
     int staged = -1;         // masked points of a range that fits one tile (staged once); -1: re-staged per pass
-    // multi-block hand-off (cdna_hip_programming.md Guideline 16, R2): each wave's sum of term q
-    // goes out as two 8-byte {tag, 32-bit half} granules, stored sc1 by lane q; every block
-    // sweeps all nb * 8 * nv * 2 granules with sc1 loads until each carries this reduction's tag
+    // multi-block hand-off (cdna_hip_programming.md Guideline 16, R2): the block's sum of term q
+    // goes out as two 8-byte {tag, 32-bit half} granules, stored sc1 by thread q; every block
+    // sweeps all nb * nv * 2 granules with sc1 loads until each carries this reduction's tag
     // (launch tag | reduction index: unique per launch, the host zeroes the granules on wrap),
     // into LDS (wsums), and sums them left to right.  Two alternating granule buffers: a block
     // overwrites buffer k % 2 only after every block has stored reduction k - 1, i.e. finished
     // reading reduction k - 2.
-    lm_gu64 *gran = nullptr;  // [2][kLmWaveSums][kLmRed][2]
+    lm_gu64 *gran = nullptr;  // [2][kLmMaxBlocks][kLmRed][2]
     unsigned tag_base = 0;
     int phase = 0;
-    double *wsums = nullptr;  // LDS [kLmWaveSums][kLmRed]
+    double *wsums = nullptr;  // LDS [kLmMaxBlocks][kLmRed]: the blocks' sums
     bool broken = false;
     double (*accs)[kLmRed] = nullptr;  // LDS [2][kLmRed]: pnp_lm_refine's normal equations
     double *res = nullptr;             // LDS [1]: a cost reduction's result
@@ -2526,83 +2523,76 @@ struct GpuLmReducer {
 #ifdef RSAC_TRACE
         mark(21);
 #endif
+        // the block's sum of term q: its 8 wave sums left to right (thread q)
+        if (lane == 0)
+            for (int q = 0; q < nv; ++q) wsum[wave][q] = a[q];
+        __syncthreads();
+        double bsum = 0.0;
+        if (threadIdx.x < nv) {
+            const int q = threadIdx.x;
+            bsum = wsum[0][q];
+            for (int w = 1; w < kLmThreads / 64; ++w) bsum = bsum + wsum[w][q];
+        }
         if (nb == 1) {
-            if (lane == 0)
-                for (int q = 0; q < nv; ++q) wsum[wave][q] = a[q];
-            __syncthreads();
-            if (threadIdx.x < nv) {
-                const int q = threadIdx.x;
-                double s = wsum[0][q];
-                for (int w = 1; w < kLmThreads / 64; ++w) s = s + wsum[w][q];
-                out[q] = s;
-            }
+            if (threadIdx.x < nv) out[threadIdx.x] = bsum;
             __syncthreads();  // out is complete; wsum is free for the next reduction
             return;
         }
         ++phase;
         const unsigned long long tag = (unsigned long long)(tag_base | (unsigned)phase) << 32;
-        lm_gu64 *g = gran + (size_t)(phase & 1) * kLmWaveSums * kLmRed * 2;
-        // lane q < nv publishes term q of this wave (lane 0 holds the wave's sums)
-        unsigned mlo = 0, mhi = 0;
-        for (int q = 0; q < nv; ++q) {
-            const unsigned vlo = __builtin_amdgcn_readfirstlane(__double2loint(a[q]));
-            const unsigned vhi = __builtin_amdgcn_readfirstlane(__double2hiint(a[q]));
-            if (lane == q) {
-                mlo = vlo;
-                mhi = vhi;
-            }
-        }
-        if (lane < nv) {
-            lm_gu64 *gw = g + ((size_t)(blockIdx.x * (kLmThreads / 64) + wave) * kLmRed + lane) * 2;
-            __hip_atomic_store(gw, tag | mlo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gw + 1, tag | mhi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lm_gu64 *g = gran + (size_t)(phase & 1) * kLmMaxBlocks * kLmRed * 2;
+        // thread q < nv (wave 0) publishes the block's term q
+        if (threadIdx.x < nv) {
+            lm_gu64 *gw = g + ((size_t)blockIdx.x * kLmRed + threadIdx.x) * 2;
+            __hip_atomic_store(gw, tag | (unsigned)__double2loint(bsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gw + 1, tag | (unsigned)__double2hiint(bsum), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
 #ifdef RSAC_TRACE
         mark(22);
 #endif
-        // sweep: granule k = (wave w, term q, half h), k = (w nv + q) 2 + h, 16 per thread in
-        // flight per pass; a pass re-reads the ones whose tag is not yet this reduction's
-        const int nw = nb * (kLmThreads / 64), tot = nw * nv * 2;
+        // sweep: granule k = (block b, term q, half h), k = (b nv + q) 2 + h, at most 8 per thread
+        // (64 blocks x 28 terms x 2 = 3584 <= 8 x 512), all in flight; a pass re-reads the ones
+        // whose tag is not yet this reduction's
+        const int tot = nb * nv * 2;
         unsigned *ws32 = (unsigned *)wsums;
-        for (int k0 = 0; k0 < tot; k0 += 16 * kLmThreads) {
-            unsigned pending = 0;
+        unsigned pending = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (k0 + j * kLmThreads + (int)threadIdx.x < tot) pending |= 1u << j;
-            for (unsigned spins = 0; pending && !broken; ++spins) {
-                unsigned long long x[16];
+        for (int j = 0; j < 8; ++j)
+            if (j * kLmThreads + (int)threadIdx.x < tot) pending |= 1u << j;
+        for (unsigned spins = 0; pending && !broken; ++spins) {
+            unsigned long long x[8];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int k = k0 + j * kLmThreads + threadIdx.x;
-                    const int w = k / (2 * nv), r = k - w * 2 * nv;
-                    x[j] = (pending >> j & 1u)
-                               ? __hip_atomic_load(g + (size_t)w * kLmRed * 2 + r, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)
-                               : 0ull;
-                }
+            for (int j = 0; j < 8; ++j) {
+                const int k = j * kLmThreads + threadIdx.x;
+                const int bb = k / (2 * nv), r = k - bb * 2 * nv;
+                x[j] = (pending >> j & 1u)
+                           ? __hip_atomic_load(g + (size_t)bb * kLmRed * 2 + r, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : 0ull;
+            }
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    if (!(pending >> j & 1u) || (x[j] & 0xFFFFFFFF00000000ull) != tag) continue;
-                    const int k = k0 + j * kLmThreads + threadIdx.x;
-                    const int w = k / (2 * nv), r = k - w * 2 * nv;
-                    ws32[w * kLmRed * 2 + r] = (unsigned)x[j];
-                    pending &= ~(1u << j);
-                }
-                if (pending) {
-                    if (spins >= kLmSpinLimit) broken = true;  // a block never arrived: stop waiting (no hang)
-                    __builtin_amdgcn_s_sleep(1);
-                }
+            for (int j = 0; j < 8; ++j) {
+                if (!(pending >> j & 1u) || (x[j] & 0xFFFFFFFF00000000ull) != tag) continue;
+                const int k = j * kLmThreads + threadIdx.x;
+                const int bb = k / (2 * nv), r = k - bb * 2 * nv;
+                ws32[bb * kLmRed * 2 + r] = (unsigned)x[j];
+                pending &= ~(1u << j);
+            }
+            if (pending) {
+                if (spins >= kLmSpinLimit) broken = true;  // a block never arrived: stop waiting (no hang)
+                __builtin_amdgcn_s_sleep(1);
             }
         }
         __syncthreads();
 #ifdef RSAC_TRACE
         mark(23);
 #endif
-        // thread q < nv sums term q over the nb * 8 wave sums, left to right
+        // thread q < nv sums term q over the nb block sums, left to right
         if (threadIdx.x < nv) {
             const int q = threadIdx.x;
             double s = wsums[q];
-            for (int w = 1; w < nw; ++w) s = s + wsums[w * kLmRed + q];
+            for (int bb = 1; bb < nb; ++bb) s = s + wsums[bb * kLmRed + q];
             out[q] = s;
         }
         __syncthreads();
@@ -2667,7 +2657,7 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     __shared__ double wsum[kLmThreads / 64][kLmRed];
     __shared__ double accs[2][kLmRed], res[1];
     __shared__ int scan[kLmThreads / 64];
-    __shared__ __attribute__((aligned(16))) char lds[kLmLdsBytes];  // 152 KB (gfx950: 160 KB per workgroup)
+    __shared__ __attribute__((aligned(16))) char lds[kLmLdsBytes];  // 94 KB
     const int prob = prob_base + blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
@@ -2687,11 +2677,11 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
                      n, Cam{cm[0], cm[1], cm[2], cm[3]}, c[0], c[1], c[2], wsum};
     red.nb = nb;
     red.stage = (float *)lds;
-    red.cap = nb == 1 ? kLmStageOne : kLmStageMulti;
+    red.cap = kLmStage;
     red.scan = scan;
     red.gran = (lm_gu64 *)gran;
     red.tag_base = tag_base;
-    red.wsums = (double *)(lds + 5 * kLmStageMulti * 4);
+    red.wsums = (double *)(lds + 5 * kLmStage * 4);
     red.accs = accs;
     red.res = res;
     red.set_range(blockIdx.x);

@@ -656,9 +656,10 @@ RSAC_HD bool fm_inlier(const double *F, double x1, double y1, double x2, double 
 // the masked points, in ascending index order, are dealt round-robin to 512 slots
 // (the p-th masked point of the range to slot b * 512 + p % 512); each slot sums
 // its points in order, a 64-lane tree per wave of 64 slots (x += x[lane ^ o],
-// o = 32 .. 1), then the nb * 8 wave sums left to right.  The GPU runs one block
-// per range and stages the range's masked points in LDS once per refit, so every
-// thread gets ceil(inliers of the range / 512) points and no outlier costs a pass.
+// o = 32 .. 1), each range's 8 wave sums left to right, then the nb range sums left
+// to right.  The GPU runs one block per range and stages the range's masked points
+// in LDS once per refit, so every thread gets ceil(inliers of the range / 512)
+// points and no outlier costs a pass; the blocks exchange one sum per term.
 // ---------------------------------------------------------------------------
 constexpr int kLmThreads = 512;
 constexpr int kLmMaxBlocks = 64;
@@ -849,18 +850,23 @@ RSAC_HD void lm_from_centred(const double *R, const double *c, double *t) {
     for (int j = 0; j < 3; ++j) t[j] = t[j] - (R[3 * j] * c[0] + R[3 * j + 1] * c[1] + R[3 * j + 2] * c[2]);
 }
 
-// the wave trees and the left-to-right sum of the wave sums of slots part[slot * nv + q]
+// the wave trees of slots part[slot * nv + q], each block's 8 wave sums left to right, then
+// the block sums (kLmThreads slots each) left to right
 inline void lm_tree_host(const double *part, int slots, int nv, double *out) {
     double v[64], w[64];
     for (int q = 0; q < nv; ++q) out[q] = 0.0;
-    for (int wv = 0; wv < slots / 64; ++wv)
+    for (int b = 0; b < slots / kLmThreads; ++b)
         for (int q = 0; q < nv; ++q) {
-            for (int l = 0; l < 64; ++l) v[l] = part[(wv * 64 + l) * nv + q];
-            for (int o = 32; o > 0; o >>= 1) {
-                for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
-                for (int l = 0; l < 64; ++l) v[l] = w[l];
+            double bsum = 0.0;
+            for (int wv = 0; wv < kLmThreads / 64; ++wv) {
+                for (int l = 0; l < 64; ++l) v[l] = part[((b * kLmThreads / 64 + wv) * 64 + l) * nv + q];
+                for (int o = 32; o > 0; o >>= 1) {
+                    for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
+                    for (int l = 0; l < 64; ++l) v[l] = w[l];
+                }
+                bsum = wv == 0 ? v[0] : bsum + v[0];  // wave sums left to right
             }
-            out[q] = wv == 0 ? v[0] : out[q] + v[0];  // wave sums left to right
+            out[q] = b == 0 ? bsum : out[q] + bsum;  // block sums left to right
         }
 }
 

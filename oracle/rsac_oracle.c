@@ -986,7 +986,8 @@ ORC_API int64_t orc_fm_ransac(const float *x1, const float *y1, const float *x2,
  * lm_chunk(n) points (one range up to 4096 points, then ranges of ~2048, at most 64); the
  * masked points of range b, ascending, dealt round-robin to slots b*512 + p%512; per-slot
  * sums in order, a 64-lane butterfly per wave of 64 slots (x += x[lane ^ o], o = 32..1),
- * then the nb*8 wave sums left to right -- so the HIP kernel k_pnp_refine reproduces this
+ * each range's 8 wave sums left to right, then the nb range sums left to right -- so the
+ * HIP kernel k_pnp_refine (one block per range, one exchanged sum per term) reproduces this
  * bit for bit. */
 #define LM_THREADS 512
 #define LM_MAX_BLOCKS 64
@@ -1055,14 +1056,18 @@ static void lm_reduce(lmctx *c, const double *R, const double *t, int nv, double
         }
     }
     double v[64], w[64];
-    for (int wv = 0; wv < S / 64; ++wv)
+    for (int b = 0; b < nb; ++b)
         for (int q = 0; q < nv; ++q) {
-            for (int l = 0; l < 64; ++l) v[l] = part[(wv * 64 + l) * nv + q];
-            for (int o = 32; o > 0; o >>= 1) {
-                for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
-                for (int l = 0; l < 64; ++l) v[l] = w[l];
+            double bsum = 0.0;
+            for (int wv = 0; wv < LM_THREADS / 64; ++wv) {
+                for (int l = 0; l < 64; ++l) v[l] = part[((b * (LM_THREADS / 64) + wv) * 64 + l) * nv + q];
+                for (int o = 32; o > 0; o >>= 1) {
+                    for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
+                    for (int l = 0; l < 64; ++l) v[l] = w[l];
+                }
+                bsum = wv == 0 ? v[0] : bsum + v[0]; /* a range's 8 wave sums left to right */
             }
-            out[q] = wv == 0 ? v[0] : out[q] + v[0]; /* wave sums left to right */
+            out[q] = b == 0 ? bsum : out[q] + bsum; /* range sums left to right */
         }
 }
 
