@@ -139,7 +139,9 @@ struct rsac_ctx {
     DevBuf pfeat, hmodels, mxlist;                             // MFMA scoring: f16 point features, records,
                                                                // undecided-tile list (+ its counter)
     DevBuf loc;                                                // location search: inputs, pos2, H, err
-    DevBuf lo;                                                 // LO-RANSAC: 2 model records, 2 counts, 2 masks
+    DevBuf lo;                                                 // LO-RANSAC: 2 model records, chain state, 2 masks
+    const void *lo_state_base = nullptr;                       // the lo allocation whose LoState is zeroed
+    PinBuf h_lo;                                               // LO chain state, written by the device
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
     DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
@@ -414,41 +416,38 @@ LmScratch *lm_scratch(rsac_ctx *c, hipStream_t s) {
     return &c->lm;
 }
 
+// The kLoSteps steps are enqueued at once and decided on the device (k_pnp_lo_count): step k
+// refits record src_k on mask k into rec[(k + 1) % 2], recounts it, and either makes it the best
+// (copied over the best hypothesis' record) or ends the chain, after which the remaining
+// launches are no-ops.  One synchronisation per LO call; the state comes back in pinned memory.
 int local_opt(rsac_ctx *c, const PnpArgs &a, int32_t n, ScanState &sc, double confidence, hipStream_t s,
               int32_t &improvements) {
     const size_t rec_bytes = sizeof(double) * kModelStride;
     HIPCHK(c->lo.ensure(2 * rec_bytes + 64 + 2 * (size_t)std::max(n, 1)));
+    HIPCHK(c->h_lo.ensure(sizeof(LoState)));
     double *rec[2] = {c->lo.as<double>(), c->lo.as<double>() + kModelStride};
-    int32_t *cnt = (int32_t *)(rec[1] + kModelStride);
-    uint8_t *mk[2] = {(uint8_t *)(cnt + 16), (uint8_t *)(cnt + 16) + std::max(n, 1)};
-    double *best_rec = a.models + sc.best * kModelStride;  // problem 0: record index = hypothesis
-    HIPCHK(hipMemcpyAsync(rec[0], best_rec, rec_bytes, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), s));
-    HIPCHK(launch_pnp_model_count(a, n, rec[0], mk[0], cnt, s));
-    int32_t cur = sc.max_good;
-    bool better = false;
-    for (int step = 0; step < kLoSteps; ++step) {
-        HIPCHK(hipMemcpyAsync(rec[1], rec[0], rec_bytes, hipMemcpyDeviceToDevice, s));
-        HIPCHK(launch_pnp_refine(a, 1, mk[0], rec[1], nullptr, s, lm_scratch(c, s), nullptr));
-        HIPCHK(hipMemsetAsync(cnt + 1, 0, sizeof(int32_t), s));
-        HIPCHK(launch_pnp_model_count(a, n, rec[1], mk[1], cnt + 1, s));
-        int32_t c2 = 0;
-        HIPCHK(hipMemcpyAsync(&c2, cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        if (c2 <= cur) break;
-        std::swap(rec[0], rec[1]);
-        std::swap(mk[0], mk[1]);
-        cur = c2;
-        better = true;
-        ++improvements;
+    LoState *st = (LoState *)(rec[1] + kModelStride);
+    uint8_t *mk[2] = {(uint8_t *)st + 64, (uint8_t *)st + 64 + std::max(n, 1)};
+    if (c->lo_state_base != c->lo.p) {  // count and ticket must start at 0 (then self-resetting)
+        HIPCHK(hipMemsetAsync(st, 0, sizeof(LoState), s));
+        c->lo_state_base = c->lo.p;
     }
-    if (better) {
-        HIPCHK(hipMemcpyAsync(best_rec, rec[0], rec_bytes, hipMemcpyDeviceToDevice, s));
-        if (cur > sc.max_good) {
-            sc.max_good = cur;
-            sc.niters = update_num_iters(confidence, (double)(n - cur) / n, 4, (int)sc.niters);
-            if (sc.iter >= sc.niters) sc.done = true;
-        }
+    LoState *hst = c->h_lo.as<LoState>();
+    double *best_rec = a.models + sc.best * kModelStride;  // problem 0: record index = hypothesis
+    HIPCHK(launch_pnp_lo_count(a, n, best_rec, mk[0], st, -1, sc.max_good, nullptr, hst, s));
+    for (int step = 0; step < kLoSteps; ++step) {
+        const double *src = step == 0 ? best_rec : rec[step & 1];
+        double *dst = rec[(step + 1) & 1];
+        HIPCHK(launch_pnp_refine(a, 1, mk[step & 1], dst, nullptr, s, lm_scratch(c, s), nullptr, nullptr, src,
+                                 &st->stopped));
+        HIPCHK(launch_pnp_lo_count(a, n, dst, mk[(step + 1) & 1], st, step, 0, best_rec, hst, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    improvements += hst->improvements;
+    if (hst->improvements > 0 && hst->cur > sc.max_good) {
+        sc.max_good = hst->cur;
+        sc.niters = update_num_iters(confidence, (double)(n - hst->cur) / n, 4, (int)sc.niters);
+        if (sc.iter >= sc.niters) sc.done = true;
     }
     return RSAC_OK;
 }
@@ -961,8 +960,10 @@ void rsac_destroy(rsac_ctx *c) {
                      &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
-                     &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask};
+                     &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,
+                     &c->h_epnp};
     for (PinBuf *b : pin) b->release();
+    c->lo_state_base = nullptr;
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);

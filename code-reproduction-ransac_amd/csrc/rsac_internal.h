@@ -195,7 +195,15 @@ struct LmScratch {
 };
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
                              hipStream_t s, LmScratch *scratch, const int64_t *host_off,
-                             double *host_models = nullptr);  // pinned: R, t also written there
+                             double *host_models = nullptr,  // pinned: R, t also written there
+                             const double *src = nullptr,    // start records (else models)
+                             const int32_t *stop = nullptr); // nonzero: no-op (an ended LO chain)
+// device state of an LO-RANSAC chain (k_pnp_lo_count)
+struct LoState {
+    int32_t cur, stopped, best_buf, improvements, count, ticket, last_total, pad;
+};
+hipError_t launch_pnp_lo_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, LoState *st, int step,
+                               int32_t init_cur, double *best_out, LoState *host_st, hipStream_t s);
 
 // mask + inlier count (atomically into *count, zeroed by the caller) of one model record, problem 0
 hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, int32_t *count,

@@ -2653,7 +2653,8 @@ struct GpuLmReducer {
 __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint8_t *__restrict__ mask,
                                                            double *__restrict__ models, int32_t *__restrict__ iters,
                                                            int prob_base, unsigned long long *gran, unsigned tag_base,
-                                                           double *host_models) {
+                                                           double *host_models, const double *src,
+                                                           const int32_t *stop) {
     __shared__ double wsum[kLmThreads / 64][kLmRed];
     __shared__ double accs[2][kLmRed], res[1];
     __shared__ int scan[kLmThreads / 64];
@@ -2664,11 +2665,15 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     const int nb = lm_blocks(n);
     if ((int)blockIdx.x >= nb) return;  // block-uniform; this problem uses fewer blocks
     if ((nb > 1) != (gran != nullptr)) return;  // the other launch's problem (launch_pnp_refine)
+    if (stop && *stop) return;  // an LO chain that already ended (k_pnp_lo_count)
     double *m = models + (int64_t)prob * kModelStride;
-    if (m[kValidSlot] == 0.0) {  // no model: block-uniform exit
+    // src: the start record (else m itself); block 0 writes the whole record to m at the end
+    const double *ms = src ? src + (int64_t)prob * kModelStride : m;
+    if (ms[kValidSlot] == 0.0) {  // no model: block-uniform exit
         if (threadIdx.x == 0 && blockIdx.x == 0 && iters) iters[prob] = 0;
+        if (src && blockIdx.x == 0 && threadIdx.x < kModelStride) m[threadIdx.x] = ms[threadIdx.x];
         if (host_models && blockIdx.x == 0 && threadIdx.x < 12)
-            host_models[(int64_t)prob * kModelStride + threadIdx.x] = m[threadIdx.x];
+            host_models[(int64_t)prob * kModelStride + threadIdx.x] = ms[threadIdx.x];
         return;
     }
     const double *cm = a.cams + 4 * prob;
@@ -2686,8 +2691,8 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     red.res = res;
     red.set_range(blockIdx.x);
     double R[9], t[3];
-    for (int j = 0; j < 9; ++j) R[j] = m[j];
-    for (int j = 0; j < 3; ++j) t[j] = m[9 + j];
+    for (int j = 0; j < 9; ++j) R[j] = ms[j];
+    for (int j = 0; j < 3; ++j) t[j] = ms[9 + j];
     lm_to_centred(R, c, t);
     const int it = pnp_lm_refine(red, R, t, kLmMaxIter);
 #ifdef RSAC_TRACE
@@ -2699,6 +2704,8 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     // reduction only with every block's: no barrier before block 0 overwrites m
     __syncthreads();  // every thread of this block has read m before thread 0 overwrites it
     if (threadIdx.x == 0 && blockIdx.x == 0) {
+        if (src)
+            for (int j = 12; j < kModelStride; ++j) m[j] = ms[j];
         for (int j = 0; j < 9; ++j) m[j] = R[j];
         for (int j = 0; j < 3; ++j) m[9 + j] = t[j];
         if (iters) iters[prob] = it;
@@ -2839,14 +2846,15 @@ hipError_t launch_pnp_epnp_s3(const PnpArgs &a, int32_t P, const uint8_t *mask, 
 }
 
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
-                             hipStream_t s, LmScratch *scratch, const int64_t *host_off, double *host_models) {
+                             hipStream_t s, LmScratch *scratch, const int64_t *host_off, double *host_models,
+                             const double *src, const int32_t *stop) {
     // every problem of up to 4096 points (and, with host_off unknown, every problem) in one
     // launch, one block each; each larger problem in a launch of its own, lm_blocks(n)
     // blocks (<= 64, all co-resident) that hand their wave sums over as tagged granules
     const int nb_max = lm_blocks(a.max_n);
     if (!(P == 1 && nb_max > 1))  // (one large problem: only the multi-block launch has work)
         hipLaunchKernelGGL(k_pnp_refine, dim3(1, P), dim3(kLmThreads), 0, s, a, mask, models, iters, 0,
-                           (unsigned long long *)nullptr, 0u, host_models);
+                           (unsigned long long *)nullptr, 0u, host_models, src, stop);
     if (nb_max > 1) {
         if (!scratch || !scratch->gran) return hipErrorInvalidValue;
         for (int p = 0; p < P; ++p) {
@@ -2861,7 +2869,7 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
                 scratch->launch = 1;
             }
             hipLaunchKernelGGL(k_pnp_refine, dim3(nb, 1), dim3(kLmThreads), 0, s, a, mask, models, iters, p,
-                               scratch->gran, scratch->launch << 10, host_models);
+                               scratch->gran, scratch->launch << 10, host_models, src, stop);
         }
     }
     return hipGetLastError();
@@ -2886,6 +2894,83 @@ __global__ __launch_bounds__(256) void k_pnp_model_count(PnpArgs a, const double
     }
     for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o);
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(count, local);
+}
+
+// One LO-RANSAC step's recount (rsac_api.hip local_opt), decided on the device so that the
+// whole chain of steps is enqueued at once: the mask and count of record m; the block that
+// finishes last (ticket) compares the count with st->cur.  step < 0: the chain's start (st is
+// initialised with cur = init_cur).  step >= 0: a no-op once an earlier step stopped the
+// chain; a higher count makes m the best (st->best_buf = step's output buffer, improvements++)
+// and, when best_out is set, copies m there; otherwise the chain stops.  count / ticket go back
+// to 0, and the state is mirrored into pinned host memory (host_st).
+__global__ __launch_bounds__(256) void k_pnp_lo_count(PnpArgs a, const double *__restrict__ m,
+                                                      uint8_t *__restrict__ mask, LoState *st, int step,
+                                                      int32_t init_cur, double *best_out, LoState *host_st) {
+    __shared__ int wsum[4];
+    if (step >= 0 && st->stopped) return;  // block-uniform; written only by an earlier launch
+    const int64_t p0 = a.offsets[0];
+    const int n = (int)(a.offsets[1] - p0);
+    const Cam k{a.cams[0], a.cams[1], a.cams[2], a.cams[3]};
+    const float thr2 = a.thr2[0];
+    const bool valid = m[kValidSlot] != 0.0;
+    int local = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int64_t q = p0 + i;
+        const bool f = valid && pnp_err(m, m + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <=
+                                    thr2;
+        mask[q] = f;
+        local += f;
+    }
+    for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = local;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const int blk = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (blk) atomicAdd(&st->count, blk);
+    __threadfence();
+    if (atomicAdd(&st->ticket, 1) != (int)gridDim.x - 1) return;
+    // the last block: every block's count is in
+    const int total = __hip_atomic_load(&st->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    LoState v;
+    if (step < 0) {
+        v.cur = init_cur;
+        v.stopped = 0;
+        v.best_buf = 0;
+        v.improvements = 0;
+    } else {
+        v.cur = __hip_atomic_load(&st->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v.stopped = 0;
+        v.best_buf = __hip_atomic_load(&st->best_buf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v.improvements = __hip_atomic_load(&st->improvements, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (total > v.cur) {
+            v.cur = total;
+            v.best_buf = (step + 1) & 1;
+            ++v.improvements;
+            if (best_out)
+                for (int q = 0; q < kModelStride; ++q) best_out[q] = m[q];
+        } else {
+            v.stopped = 1;
+        }
+    }
+    v.count = 0;
+    v.ticket = 0;
+    v.last_total = total;
+    __hip_atomic_store(&st->cur, v.cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st->stopped, v.stopped, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st->best_buf, v.best_buf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st->improvements, v.improvements, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st->count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st->ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (host_st) *host_st = v;
+}
+
+hipError_t launch_pnp_lo_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, LoState *st, int step,
+                               int32_t init_cur, double *best_out, LoState *host_st, hipStream_t s) {
+    unsigned g = cdiv(n > 0 ? n : 1, 256);
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_pnp_lo_count, dim3(g), dim3(256), 0, s, a, model, mask, st, step, init_cur, best_out,
+                       host_st);
+    return hipGetLastError();
 }
 
 hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, int32_t *count,
