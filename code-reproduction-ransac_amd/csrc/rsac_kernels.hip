@@ -557,6 +557,107 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
                      a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride);
 }
 
+// Small rounds (an adaptive run's first 256 hypotheses: one block, every lane's latency is the
+// launch's): four lanes per hypothesis.  All four draw the sample and run lt_common; lane c
+// then takes candidate c = (sign, root) of the Lambda Twist solution list (lt_sign, lt_tau:
+// the operations of p3p_lambdatwist for that candidate) and its 4th-point error; the four
+// lanes pick the smallest error, the lowest candidate on ties (= pnp_minimal's first-one rule),
+// and the winner writes the record.  Results equal k_pnp_solve's bit for bit.
+__global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    const int prob = blockIdx.y;
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int hl = gt >> 2, cand = gt & 3;
+    if (gt == 0 && prob == 0) {
+        if (a.queue) *a.queue = 0;
+        if (a.mx_count) *a.mx_count = 0;
+    }
+    const bool live = hl < H;  // the 4 lanes of a hypothesis share it: shuffles stay in the group
+    const int64_t h = hyp_begin + hl;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
+    int32_t idx[4] = {0, 0, 0, 0};
+    int8_t st = -1;
+    if (live) {
+        if (a.subsets) {
+            st = a.sub_status[rec];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) idx[j] = a.subsets[rec * 4 + j];
+        } else {
+            Philox rng;
+            rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
+            st = (n >= 4 && rng.subset<4>(n, idx) == 0) ? 1 : -1;
+        }
+    }
+    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
+    double e = 0.0;
+    bool mine = false;  // this lane's candidate was emitted with a usable error
+    const Cam k{a.cams[4 * prob], a.cams[4 * prob + 1], a.cams[4 * prob + 2], a.cams[4 * prob + 3]};
+    if (st > 0) {
+        float X[4], Y[4], Z[4], U[4], V[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t i = p0 + idx[j];
+            X[j] = a.X[i]; Y[j] = a.Y[i]; Z[j] = a.Z[i]; U[j] = a.U[i]; V[j] = a.V[i];
+        }
+        double yb[9], xw[9];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            bearing(k, U[j], V[j], yb + 3 * j);
+            xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
+        }
+        LtCommon L;
+        double w0, w1, tau[2];
+        if (lt_common(yb, xw, L) && lt_sign(L, cand >> 1, w0, w1, tau)) {
+            auto emit = [&](const double *Rk, const double *tk) {
+                const double ek = pnp_fourth_error(Rk, tk, X, Y, Z, U, V, k);
+                if (!(ek == ek)) return;
+                mine = true;
+                e = ek;
+#pragma unroll
+                for (int q = 0; q < 9; ++q) R[q] = Rk[q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) t[q] = tk[q];
+            };
+            (void)lt_tau(L, w0, w1, tau[cand & 1], yb, xw, emit);
+        }
+    }
+    // the group's winner: smallest e, then the lowest candidate (all 4 lanes agree)
+    int win = mine ? cand : 4;
+    double we = mine ? e : 0.0;
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+        const int ow = __shfl_xor(win, o);
+        const double oe = __shfl_xor(we, o);
+        if (ow < 4 && (win == 4 || oe < we || (oe == we && ow < win))) {
+            win = ow;
+            we = oe;
+        }
+    }
+    if (!live) return;
+    const bool ok = win < 4;
+    if (ok ? cand != win : cand != 0) return;  // one writer per hypothesis
+    const int8_t sv = st > 0 ? (ok ? 1 : 0) : st;
+    double *m = a.models + rec * kModelStride;
+    if (!ok)
+        for (int q = 0; q < 9; ++q) R[q] = 0.0;
+    if (!ok)
+        for (int q = 0; q < 3; ++q) t[q] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) m[q] = R[q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
+    m[kValidSlot] = sv > 0 ? 1.0 : 0.0;
+    a.status[rec] = sv;
+    if (a.counts_out) a.counts_out[rec] = 0;
+    if (a.hmodels)
+        write_hmodel(R, t, sv > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+                     a.fconst + (int64_t)prob * kFconstStride, a.hmodels + rec * kHModelStride);
+    else if (a.fmodels)
+        write_fmodel(R, t, sv > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride);
+}
+
 // ---------------------------------------------------------------------------
 // PnP scoring, float32 pre-filter + exact fallback (division-free).
 //
@@ -1973,6 +2074,12 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
     return hipGetLastError();
 }
 
+// RSAC_SOLVE4_MAX: the largest round (problems x hypotheses) solved 4 lanes per hypothesis
+static int64_t solve4_max_hyps() {
+    static const int64_t v = [] { const char *e = getenv("RSAC_SOLVE4_MAX"); return e ? atoll(e) : 4096; }();
+    return v;
+}
+
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
                             double *frame, float *fconst, hipStream_t s, uint4 *PF, const PnpPrepare *prep) {
     if (prep && prep->p3) {  // the deferred f64 -> f32 conversion of one problem, fused
@@ -2002,7 +2109,11 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
 }
 
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
-    hipLaunchKernelGGL(k_pnp_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H);
+    // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
+    if ((int64_t)P * H <= solve4_max_hyps())
+        hipLaunchKernelGGL(k_pnp_solve4, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, a, hyp_begin, H);
+    else
+        hipLaunchKernelGGL(k_pnp_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H);
     return hipGetLastError();
 }
 

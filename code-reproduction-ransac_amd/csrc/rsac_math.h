@@ -225,11 +225,16 @@ RSAC_HD int p3p_pose(double l1, double l2, double l3, double a12, double a13, do
     return 1;
 }
 
-// Every solution (R, t), in the order of the restatement's solution list, is
-// handed to emit(R, t) as it is built: no solution arrays, so the GPU solver
-// keeps everything in registers.  Returns the number of solutions.
-template <class Emit>
-RSAC_HD int p3p_lambdatwist(const double *y, const double *x, Emit &&emit) {
+// The Lambda Twist solver in three pieces, so that the GPU can also run the (up to 4)
+// candidates of one sample on 4 lanes (k_pnp_solve4) with the same operations:
+//   lt_common: the cubic, the two eigenvectors, v and the inverse of [d12 d13 d12xd13]
+//   lt_sign:   for s = +v / -v: w0, w1 and the quadratic's roots tau (false: no real root)
+//   lt_tau:    one root: lambdas, Gauss-Newton refine, pose, emit (1 if emitted)
+struct LtCommon {
+    double a12, a13, a23, b12, b13, b23, v, v1[3], v2[3], Xi[9];
+};
+
+RSAC_HD bool lt_common(const double *y, const double *x, LtCommon &L) {
     const double *y1 = y, *y2 = y + 3, *y3 = y + 6;
     const double *x1 = x, *x2 = x + 3, *x3 = x + 6;
     double b12 = -2.0 * (y1[0] * y2[0] + y1[1] * y2[1] + y1[2] * y2[2]);
@@ -252,7 +257,7 @@ RSAC_HD int p3p_lambdatwist(const double *y, const double *x, Emit &&emit) {
     double p2 = 2.0 * blob * a23 * a13 + a13 * (2.0 * a12 + a13) * s23 + a23 * (a23 - a12) * s31;
     double p1 = a23 * (a13 - a23) * s12 - a12 * a12 * s23 - 2.0 * a12 * (blob * a23 + a13 * s23);
     double p0 = a12 * (a12 * s23 - a23 * s12);
-    if (p3 == 0.0 || !dfinite(p3)) return 0;
+    if (p3 == 0.0 || !dfinite(p3)) return false;
     double ip3 = 1.0 / p3;
     p2 = p2 * ip3; p1 = p1 * ip3; p0 = p0 * ip3;
     double g = cubic_root(p2, p1, p0);
@@ -265,7 +270,7 @@ RSAC_HD int p3p_lambdatwist(const double *y, const double *x, Emit &&emit) {
     double A22 = g * (a13 - a23) - a12;
 
     // eigenvectors of the two non-zero eigenvalues (the third is 0)
-    double v1[3], v2[3], e1, e2;
+    double e1, e2;
     {
         double a01sq = A01 * A01;
         double b = -A00 - A11 - A22;
@@ -281,7 +286,7 @@ RSAC_HD int p3p_lambdatwist(const double *y, const double *x, Emit &&emit) {
             double q1 = -(e * A02 + pr0) * tmp;
             double q2 = -(e * A12 + pr1) * tmp;
             double rn = 1.0 / dsqrt(q1 * q1 + q2 * q2 + 1.0);
-            v1[0] = q1 * rn; v1[1] = q2 * rn; v1[2] = rn;
+            L.v1[0] = q1 * rn; L.v1[1] = q2 * rn; L.v1[2] = rn;
         }
         {
             double e = e2;
@@ -289,53 +294,68 @@ RSAC_HD int p3p_lambdatwist(const double *y, const double *x, Emit &&emit) {
             double q1 = -(e * A02 + pr0) * tmp;
             double q2 = -(e * A12 + pr1) * tmp;
             double rn = 1.0 / dsqrt(q1 * q1 + q2 * q2 + 1.0);
-            v2[0] = q1 * rn; v2[1] = q2 * rn; v2[2] = rn;
+            L.v2[0] = q1 * rn; L.v2[1] = q2 * rn; L.v2[2] = rn;
         }
     }
     double vq = -e2 / e1;
-    double v = dsqrt(vq > 0.0 ? vq : 0.0);
+    L.v = dsqrt(vq > 0.0 ? vq : 0.0);
 
     // X = [d12 d13 d12xd13] (columns), its inverse by the adjugate
     double M[9] = {d12[0], d13[0], d12xd13[0], d12[1], d13[1], d12xd13[1], d12[2], d13[2], d12xd13[2]};
-    double Xi[9];
     {
         double c00 = M[4] * M[8] - M[5] * M[7];
         double c01 = M[5] * M[6] - M[3] * M[8];
         double c02 = M[3] * M[7] - M[4] * M[6];
         double det = M[0] * c00 + M[1] * c01 + M[2] * c02;
-        if (det == 0.0 || !dfinite(det)) return 0;
+        if (det == 0.0 || !dfinite(det)) return false;
         double id = 1.0 / det;
-        Xi[0] = c00 * id; Xi[1] = (M[2] * M[7] - M[1] * M[8]) * id; Xi[2] = (M[1] * M[5] - M[2] * M[4]) * id;
-        Xi[3] = c01 * id; Xi[4] = (M[0] * M[8] - M[2] * M[6]) * id; Xi[5] = (M[2] * M[3] - M[0] * M[5]) * id;
-        Xi[6] = c02 * id; Xi[7] = (M[1] * M[6] - M[0] * M[7]) * id; Xi[8] = (M[0] * M[4] - M[1] * M[3]) * id;
+        L.Xi[0] = c00 * id; L.Xi[1] = (M[2] * M[7] - M[1] * M[8]) * id; L.Xi[2] = (M[1] * M[5] - M[2] * M[4]) * id;
+        L.Xi[3] = c01 * id; L.Xi[4] = (M[0] * M[8] - M[2] * M[6]) * id; L.Xi[5] = (M[2] * M[3] - M[0] * M[5]) * id;
+        L.Xi[6] = c02 * id; L.Xi[7] = (M[1] * M[6] - M[0] * M[7]) * id; L.Xi[8] = (M[0] * M[4] - M[1] * M[3]) * id;
     }
+    L.a12 = a12; L.a13 = a13; L.a23 = a23; L.b12 = b12; L.b13 = b13; L.b23 = b23;
+    return true;
+}
+
+RSAC_HD bool lt_sign(const LtCommon &L, int sgn, double &w0, double &w1, double *tau) {
+    const double a12 = L.a12, a13 = L.a13, b12 = L.b12, b13 = L.b13;
+    double s = sgn == 0 ? L.v : -L.v;
+    double w2 = 1.0 / (s * L.v2[0] - L.v1[0]);
+    w0 = (L.v1[1] - s * L.v2[1]) * w2;
+    w1 = (L.v1[2] - s * L.v2[2]) * w2;
+    double a = 1.0 / ((a13 - a12) * w1 * w1 - a12 * b13 * w1 - a12);
+    double b = (a13 * b12 * w1 - a12 * b13 * w0 - 2.0 * w0 * w1 * (a12 - a13)) * a;
+    double c = ((a13 - a12) * w0 * w0 + a13 * b12 * w0 + a13) * a;
+    if (!(b * b - 4.0 * c >= 0.0)) return false;
+    root2real(b, c, tau[0], tau[1]);
+    return true;
+}
+
+template <class Emit>
+RSAC_HD int lt_tau(const LtCommon &L, double w0, double w1, double tq, const double *y, const double *x, Emit &emit) {
+    if (!(tq > 0.0)) return 0;
+    double d = L.a23 / (tq * (L.b23 + tq) + 1.0);
+    if (!(d > 0.0)) return 0;
+    double l2 = dsqrt(d);
+    double l3 = tq * l2;
+    double l1 = w0 * l2 + w1 * l3;
+    if (!(l1 >= 0.0)) return 0;
+    return p3p_pose(l1, l2, l3, L.a12, L.a13, L.a23, L.b12, L.b13, L.b23, y, y + 3, y + 6, x, L.Xi, emit);
+}
+
+// Every solution (R, t), in the order of the restatement's solution list, is
+// handed to emit(R, t) as it is built: no solution arrays, so the GPU solver
+// keeps everything in registers.  Returns the number of solutions.
+template <class Emit>
+RSAC_HD int p3p_lambdatwist(const double *y, const double *x, Emit &&emit) {
+    LtCommon L;
+    if (!lt_common(y, x, L)) return 0;
     int nout = 0;
     for (int sgn = 0; sgn < 2; ++sgn) {
-        double s = sgn == 0 ? v : -v;
-        double w2 = 1.0 / (s * v2[0] - v1[0]);
-        double w0 = (v1[1] - s * v2[1]) * w2;
-        double w1 = (v1[2] - s * v2[2]) * w2;
-        double a = 1.0 / ((a13 - a12) * w1 * w1 - a12 * b13 * w1 - a12);
-        double b = (a13 * b12 * w1 - a12 * b13 * w0 - 2.0 * w0 * w1 * (a12 - a13)) * a;
-        double c = ((a13 - a12) * w0 * w0 + a13 * b12 * w0 + a13) * a;
-        if (b * b - 4.0 * c >= 0.0) {
-            double tau[2];
-            root2real(b, c, tau[0], tau[1]);
-            for (int q = 0; q < 2; ++q) {
-                if (tau[q] > 0.0) {
-                    double tq = tau[q];
-                    double d = a23 / (tq * (b23 + tq) + 1.0);
-                    if (d > 0.0) {
-                        double l2 = dsqrt(d);
-                        double l3 = tq * l2;
-                        double l1 = w0 * l2 + w1 * l3;
-                        if (l1 >= 0.0) nout += p3p_pose(l1, l2, l3, a12, a13, a23, b12, b13, b23, y1, y2, y3, x1, Xi, emit);
-                    }
-                }
-            }
-        }
+        double w0, w1, tau[2];
+        if (lt_sign(L, sgn, w0, w1, tau))
+            for (int q = 0; q < 2; ++q) nout += lt_tau(L, w0, w1, tau[q], y, x, emit);
     }
-
     return nout;
 }
 
@@ -344,6 +364,19 @@ RSAC_HD void bearing(const Cam &k, float uf, float vf, double *out) {
     double yn = ((double)vf - k.cy) / k.fy;
     double nrm = dsqrt(xn * xn + yn * yn + 1.0);
     out[0] = xn / nrm; out[1] = yn / nrm; out[2] = 1.0 / nrm;
+}
+
+// squared reprojection error of the sample's 4th point under (R, t) (NaN: unusable)
+RSAC_HD double pnp_fourth_error(const double *Rk, const double *tk, const float (&X)[4], const float (&Y)[4],
+                                const float (&Z)[4], const float (&U)[4], const float (&V)[4], const Cam &k) {
+    const double X4 = X[3], Y4 = Y[3], Z4 = Z[3];
+    double x = Rk[0] * X4 + Rk[1] * Y4; x = x + Rk[2] * Z4; x = x + tk[0];
+    double y = Rk[3] * X4 + Rk[4] * Y4; y = y + Rk[5] * Z4; y = y + tk[1];
+    double z = Rk[6] * X4 + Rk[7] * Y4; z = z + Rk[8] * Z4; z = z + tk[2];
+    const double iz = (z != 0.0) ? 1.0 / z : 1.0;
+    const double du = (x * iz) * k.fx + k.cx - (double)U[3];
+    const double dv = (y * iz) * k.fy + k.cy - (double)V[3];
+    return du * du + dv * dv;
 }
 
 // 4-point minimal PnP: P3P on the first three, disambiguated by the fourth.
@@ -356,18 +389,11 @@ RSAC_HD bool pnp_minimal(const float (&X)[4], const float (&Y)[4], const float (
         bearing(k, U[j], V[j], yb + 3 * j);
         xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
     }
-    const double X4 = X[3], Y4 = Y[3], Z4 = Z[3];
     bool have = false;
     double best_e = 0.0;
     // the 4th point picks the solution: smallest reprojection error, first one on ties
     const int ns = p3p_lambdatwist(yb, xw, [&](const double *Rk, const double *tk) {
-        double x = Rk[0] * X4 + Rk[1] * Y4; x = x + Rk[2] * Z4; x = x + tk[0];
-        double y = Rk[3] * X4 + Rk[4] * Y4; y = y + Rk[5] * Z4; y = y + tk[1];
-        double z = Rk[6] * X4 + Rk[7] * Y4; z = z + Rk[8] * Z4; z = z + tk[2];
-        const double iz = (z != 0.0) ? 1.0 / z : 1.0;
-        const double du = (x * iz) * k.fx + k.cx - (double)U[3];
-        const double dv = (y * iz) * k.fy + k.cy - (double)V[3];
-        const double e = du * du + dv * dv;
+        const double e = pnp_fourth_error(Rk, tk, X, Y, Z, U, V, k);
         if (!(e == e)) return;
         if (!have || e < best_e) {
             have = true;
