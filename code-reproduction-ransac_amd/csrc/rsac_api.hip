@@ -146,6 +146,7 @@ struct rsac_ctx {
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
     DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
     DevBuf lmscr;                                              // multi-block LM refit: tagged wave sums
+    DevBuf setup_scr;                                          // k_pnp_setup_fc: ticket + per-block bounds
     LmScratch lm;                                              // ... and its launch counter
     std::vector<char> last_tables;                             // the tables last uploaded (stage_tables)
     void *last_tables_dev = nullptr;
@@ -207,6 +208,12 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
     if (flags & RSAC_F_DEVICE_IN) {
         if (ncomp_a == 3 && defer && P == 1 && N > 0 && N <= 65536) {
             st.prep = PnpPrepare{(const double *)a, (const double *)b, D, D + N, D + 2 * N, D + 3 * N, D + 4 * N};
+            if (!c->setup_scr.p) {  // the ticket must start at 0 (the kernel resets it)
+                HIPCHK(c->setup_scr.ensure(64 + sizeof(float) * 10 * kSetupMaxBlocks));
+                HIPCHK(hipMemsetAsync(c->setup_scr.p, 0, 64, s));
+            }
+            st.prep.ticket = c->setup_scr.as<int>();
+            st.prep.part = (float *)(c->setup_scr.as<char>() + 64);
             return RSAC_OK;
         }
         if (ncomp_a == 3)
@@ -957,7 +964,7 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr};
+                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr, &c->setup_scr};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,

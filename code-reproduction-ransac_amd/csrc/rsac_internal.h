@@ -146,7 +146,12 @@ hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_
 struct PnpPrepare {
     const double *p3 = nullptr, *p2 = nullptr;
     float *X = nullptr, *Y = nullptr, *Z = nullptr, *U = nullptr, *V = nullptr;
+    // k_pnp_setup_fc's scratch: per-block bounds (kSetupMaxBlocks x 10 floats) and its ticket
+    // (zero on allocation, reset by the kernel)
+    float *part = nullptr;
+    int *ticket = nullptr;
 };
+constexpr int kSetupMaxBlocks = 256;
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *bounds_ws, float *XC, float *YC,
                             float *ZC, double *frame, float *fconst, hipStream_t s, uint4 *PF = nullptr,
                             const PnpPrepare *prep = nullptr);

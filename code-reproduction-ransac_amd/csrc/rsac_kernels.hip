@@ -203,8 +203,11 @@ __global__ __launch_bounds__(1024) void k_pnp_bounds1(PnpArgs a, int *__restrict
 // Per problem: frame = {c0 c1 c2 (bbox centre), B >= |XC|inf, rho >= |XC - (Xf - c)|,
 // max|Xf|, wmax (bound on |x/z| of any projection within thr of a pixel), 0};
 // fconst = {fx fy cx cy T 2.002 sqrt(T) 1e-6 T thr 2/fx 2/fy cu cv cc0} (see the scoring kernel).
+// cgiven: the frame's centre (else the bounding box's midpoint); B then bounds |X - c| from the
+// bounds around that centre
 __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *__restrict__ ws,
-                              double *__restrict__ frame, float *__restrict__ fconst) {
+                              double *__restrict__ frame, float *__restrict__ fconst,
+                              const double *cgiven = nullptr) {
     const int n = (int)(a.offsets[prob + 1] - a.offsets[prob]);
     const double *cm = a.cams + 4 * prob;
     const double fx = fabs(cm[0]), fy = fabs(cm[1]), cx = cm[2], cy = cm[3];
@@ -216,7 +219,16 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
         du = fmax(fabs(ord2f(ws[5 * prob + 3]) - cx), fabs(ord2f(ws[5 * P + 5 * prob + 3]) - cx));
         dv = fmax(fabs(ord2f(ws[5 * prob + 4]) - cy), fabs(ord2f(ws[5 * P + 5 * prob + 4]) - cy));
     }
-    const double B = frame_bound(ws, P, prob, n);
+    double B = frame_bound(ws, P, prob, n);
+    if (cgiven) {
+        double Bg = 0;
+        for (int k = 0; k < 3; ++k) {
+            c[k] = cgiven[k];
+            if (n > 0)
+                Bg = fmax(Bg, fmax((double)ord2f(ws[5 * P + 5 * prob + k]) - c[k], c[k] - (double)ord2f(ws[5 * prob + k])));
+        }
+        B = Bg * (1.0 + 4.0 * kU32) + 1e-30;
+    }
     double *f = frame + (int64_t)prob * kFrameStride;
     f[0] = c[0]; f[1] = c[1]; f[2] = c[2];
     f[3] = B;
@@ -327,6 +339,83 @@ __global__ __launch_bounds__(1024) void k_pnp_setup1(const double *__restrict__ 
         YC[i] = yc;
         ZC[i] = zc;
         if (PF) PF[i] = mx_point_features(xc * fs, yc * fs, zc * fs);
+    }
+}
+
+// One problem, inputs as device f64 AoS, no MFMA features: conversion, centring and bounds in
+// one pass over a full grid (one point per thread).  The frame is centred on the first point
+// (known before any reduction, so every block centres its own points at once); the last block
+// to finish (ticket) reduces the blocks' bounds, writes the frame and resets the ticket.  The
+// pre-filter's bounds hold for any centre, so counts do not depend on the choice.
+__global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__ p3, const double *__restrict__ p2,
+                                                      PnpArgs a, float *__restrict__ X, float *__restrict__ Y,
+                                                      float *__restrict__ Z, float *__restrict__ U,
+                                                      float *__restrict__ V, int *__restrict__ ws,
+                                                      double *__restrict__ frame, float *__restrict__ fconst,
+                                                      float *__restrict__ XC, float *__restrict__ YC,
+                                                      float *__restrict__ ZC, float *part, int *ticket) {
+    __shared__ float sl[4][5], sh[4][5];
+    const int n = (int)(a.offsets[1] - a.offsets[0]);  // offsets[0] = 0 (one problem)
+    const double c[3] = {(double)(float)p3[0], (double)(float)p3[1], (double)(float)p3[2]};
+    float lo[5], hi[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const float v[5] = {(float)p3[3 * i], (float)p3[3 * i + 1], (float)p3[3 * i + 2], (float)p2[2 * i],
+                            (float)p2[2 * i + 1]};
+        X[i] = v[0]; Y[i] = v[1]; Z[i] = v[2]; U[i] = v[3]; V[i] = v[4];
+        XC[i] = (float)((double)v[0] - c[0]);
+        YC[i] = (float)((double)v[1] - c[1]);
+        ZC[i] = (float)((double)v[2] - c[2]);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { lo[k] = fminf(lo[k], v[k]); hi[k] = fmaxf(hi[k], v[k]); }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
+        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { sl[wave][k] = lo[k]; sh[wave][k] = hi[k]; }
+    __syncthreads();
+    __shared__ int last;
+    if (threadIdx.x < 5) {
+        const int k = threadIdx.x;
+        const float l = fminf(fminf(sl[0][k], sl[1][k]), fminf(sl[2][k], sl[3][k]));
+        const float h = fmaxf(fmaxf(sh[0][k], sh[1][k]), fmaxf(sh[2][k], sh[3][k]));
+        __hip_atomic_store(part + 10 * blockIdx.x + k, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part + 10 * blockIdx.x + 5 + k, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (sc1 stores)
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    // the last block: every block's bounds are in (sc1 stores drained before each ticket add)
+    __shared__ int wsl[10];
+    if (threadIdx.x < 5) {
+        const int k = threadIdx.x;
+        float l = __builtin_inff(), h = -__builtin_inff();
+        for (int b = 0; b < (int)gridDim.x; ++b) {
+            l = fminf(l, __hip_atomic_load(part + 10 * b + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            h = fmaxf(h, __hip_atomic_load(part + 10 * b + 5 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+        const int wl = n > 0 ? min(0x7F7F7F7F, f2ord(l)) : 0x7F7F7F7F;
+        const int wh = n > 0 ? max((int)0x80808080, f2ord(h)) : (int)0x80808080;
+        ws[k] = wl;
+        ws[5 + k] = wh;
+        wsl[k] = wl;
+        wsl[5 + k] = wh;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        pnp_frame_one(a, 1, 0, wsl, frame, fconst, c);
+        if (a.best_key) *a.best_key = 0ull;
+        *a.queue = 0;
+        *ticket = 0;  // for the next call (stream order)
     }
 }
 
@@ -2084,8 +2173,15 @@ hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t 
                             double *frame, float *fconst, hipStream_t s, uint4 *PF, const PnpPrepare *prep) {
     if (prep && prep->p3) {  // the deferred f64 -> f32 conversion of one problem, fused
         if (P != 1 || max_n > 65536) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_pnp_setup1, dim3(1), dim3(1024), 0, s, prep->p3, prep->p2, a, prep->X, prep->Y, prep->Z,
-                           prep->U, prep->V, ws, frame, fconst, XC, YC, ZC, PF);
+        if (!PF && prep->part && prep->ticket) {
+            unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
+            if (g > kSetupMaxBlocks) g = kSetupMaxBlocks;
+            hipLaunchKernelGGL(k_pnp_setup_fc, dim3(g), dim3(256), 0, s, prep->p3, prep->p2, a, prep->X, prep->Y,
+                               prep->Z, prep->U, prep->V, ws, frame, fconst, XC, YC, ZC, prep->part, prep->ticket);
+        } else {
+            hipLaunchKernelGGL(k_pnp_setup1, dim3(1), dim3(1024), 0, s, prep->p3, prep->p2, a, prep->X, prep->Y,
+                               prep->Z, prep->U, prep->V, ws, frame, fconst, XC, YC, ZC, PF);
+        }
         return hipGetLastError();
     }
     if (P == 1 && max_n <= 65536) {
