@@ -2037,20 +2037,6 @@ __global__ __launch_bounds__(256) void k_best_key(const int32_t *__restrict__ co
 }
 
 // one wave per problem: 64 hypotheses per step, the running maximum carried across steps
-// RANSACUpdateNumIters (rsac_host.hip update_num_iters) with the device's pow / log / lrint:
-// may differ from the host's in a last-ulp tie, which is why the host re-checks the decision
-__device__ int update_num_iters_dev(double p, double ep, int model_points, int max_iters) {
-    p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
-    ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
-    double num = 1. - p;
-    if (num < 2.2250738585072014e-308) num = 2.2250738585072014e-308;
-    double denom = 1. - pow(1. - ep, model_points);
-    if (denom < 2.2250738585072014e-308) return 0;
-    num = log(num);
-    denom = log(denom);
-    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)lrint(num / denom);
-}
-
 __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict__ counts,
                                                       const int8_t *__restrict__ status, int64_t stride, int32_t P,
                                                       int32_t H, int model_points, ScanRecords *__restrict__ out,
@@ -2098,22 +2084,43 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
             o.cnt[r] = rcnt[r];
         }
     }
-    if (dec.best_out && prob == 0 && lane == 0) {
-        // scan_records (rsac_host.hip) on the records just written by this lane
-        int64_t niters = dec.max_iters > 1 ? dec.max_iters : 1, best = -1;
+    if (dec.best_out && prob == 0) {  // wave-uniform
+        // scan_records (rsac_host.hip) on the records lane 0 just wrote.  update_num_iters'
+        // logarithms (the latency) for every record at once, lane r for record r; the
+        // sequential part on them is uniform across the wave.
+        __builtin_amdgcn_wave_barrier();
         const int nr = nrec <= kScanRecs ? nrec : 0;
+        double p = dec.confidence;
+        p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
+        double num = 1. - p;
+        if (num < 2.2250738585072014e-308) num = 2.2250738585072014e-308;
+        num = log(num);
+        double ldenom = 0.;
+        int zero = 0;  // update_num_iters returns 0 (denominator below DBL_MIN)
+        if (lane < nr) {
+            double ep = (double)(dec.n - rcnt[lane]) / dec.n;
+            ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
+            const double denom = 1. - pow(1. - ep, model_points);
+            if (denom < 2.2250738585072014e-308) zero = 1;
+            else ldenom = log(denom);
+        }
+        int64_t niters = dec.max_iters > 1 ? dec.max_iters : 1, best = -1;
         for (int r = 0; r < nr; ++r) {
+            const double ld = __shfl(ldenom, r);
+            const int z = __shfl(zero, r);
             const int64_t stop = first_neg < niters ? first_neg : niters;
             if (ridx[r] >= stop) break;
             best = ridx[r];
-            niters = update_num_iters_dev(dec.confidence, (double)(dec.n - rcnt[r]) / dec.n, model_points,
-                                          (int)niters);
+            const int mi = (int)niters;
+            niters = z ? 0 : ((ld >= 0 || -num >= mi * (-ld)) ? mi : (int)lrint(num / ld));
         }
         const int64_t stop = first_neg < niters ? first_neg : niters;
         const bool done = nrec <= kScanRecs && (stop < H || H >= niters);
-        *dec.best_out = done ? best : -1;  // not done: the speculative finish has no model (cheap no-op)
-        o.dev_best = (int32_t)best;
-        o.dev_done = done;
+        if (lane == 0) {
+            *dec.best_out = done ? best : -1;  // not done: the speculative finish has no model (cheap no-op)
+            o.dev_best = (int32_t)best;
+            o.dev_done = done;
+        }
     }
 }
 
