@@ -208,12 +208,6 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
     if (flags & RSAC_F_DEVICE_IN) {
         if (ncomp_a == 3 && defer && P == 1 && N > 0 && N <= 65536) {
             st.prep = PnpPrepare{(const double *)a, (const double *)b, D, D + N, D + 2 * N, D + 3 * N, D + 4 * N};
-            if (!c->setup_scr.p) {  // the ticket must start at 0 (the kernel resets it)
-                HIPCHK(c->setup_scr.ensure(64 + sizeof(float) * 10 * kSetupMaxBlocks));
-                HIPCHK(hipMemsetAsync(c->setup_scr.p, 0, 64, s));
-            }
-            st.prep.ticket = c->setup_scr.as<int>();
-            st.prep.part = (float *)(c->setup_scr.as<char>() + 64);
             return RSAC_OK;
         }
         if (ncomp_a == 3)
@@ -359,8 +353,18 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
         PF = c->pfeat.as<uint4>();
     }
     // resets best_key and the queue, then builds the frame (also in exact mode: cheap)
+    // one problem: k_pnp_setup_fc's scratch (its ticket starts at 0; the kernel resets it)
+    PnpPrepare prep = st.prep;
+    if (P == 1) {
+        if (!c->setup_scr.p) {
+            HIPCHK(c->setup_scr.ensure(64 + sizeof(float) * 10 * kSetupMaxBlocks));
+            HIPCHK(hipMemsetAsync(c->setup_scr.p, 0, 64, s));
+        }
+        prep.ticket = c->setup_scr.as<int>();
+        prep.part = (float *)(c->setup_scr.as<char>() + 64);
+    }
     HIPCHK(launch_pnp_frame(a, P, max_n, c->bounds_ws.as<int32_t>(), C, C + N, C + 2 * N, c->frame.as<double>(),
-                            c->fconst.as<float>(), s, PF, &st.prep));
+                            c->fconst.as<float>(), s, PF, &prep));
     if (!a.exact_only) {
         a.counts_out = c->counts.as<int32_t>();
         a.XC = C; a.YC = C + N; a.ZC = C + 2 * N;

@@ -347,6 +347,8 @@ __global__ __launch_bounds__(1024) void k_pnp_setup1(const double *__restrict__ 
 // (known before any reduction, so every block centres its own points at once); the last block
 // to finish (ticket) reduces the blocks' bounds, writes the frame and resets the ticket.  The
 // pre-filter's bounds hold for any centre, so counts do not depend on the choice.
+// CONVERT = false: the points are already the f32 SoA a.X .. a.V (p3, p2, X .. V unused)
+template <bool CONVERT>
 __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__ p3, const double *__restrict__ p2,
                                                       PnpArgs a, float *__restrict__ X, float *__restrict__ Y,
                                                       float *__restrict__ Z, float *__restrict__ U,
@@ -355,15 +357,27 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
                                                       float *__restrict__ XC, float *__restrict__ YC,
                                                       float *__restrict__ ZC, float *part, int *ticket) {
     __shared__ float sl[4][5], sh[4][5];
-    const int n = (int)(a.offsets[1] - a.offsets[0]);  // offsets[0] = 0 (one problem)
-    const double c[3] = {(double)(float)p3[0], (double)(float)p3[1], (double)(float)p3[2]};
+    const int64_t p0 = a.offsets[0];
+    const int n = (int)(a.offsets[1] - p0);
+    double c[3];
+    if constexpr (CONVERT) {
+        c[0] = (double)(float)p3[0]; c[1] = (double)(float)p3[1]; c[2] = (double)(float)p3[2];
+    } else {
+        c[0] = n > 0 ? (double)a.X[p0] : 0.0; c[1] = n > 0 ? (double)a.Y[p0] : 0.0; c[2] = n > 0 ? (double)a.Z[p0] : 0.0;
+    }
     float lo[5], hi[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        const float v[5] = {(float)p3[3 * i], (float)p3[3 * i + 1], (float)p3[3 * i + 2], (float)p2[2 * i],
-                            (float)p2[2 * i + 1]};
-        X[i] = v[0]; Y[i] = v[1]; Z[i] = v[2]; U[i] = v[3]; V[i] = v[4];
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+        const int64_t i = p0 + j;
+        float v[5];
+        if constexpr (CONVERT) {
+            v[0] = (float)p3[3 * i]; v[1] = (float)p3[3 * i + 1]; v[2] = (float)p3[3 * i + 2];
+            v[3] = (float)p2[2 * i]; v[4] = (float)p2[2 * i + 1];
+            X[i] = v[0]; Y[i] = v[1]; Z[i] = v[2]; U[i] = v[3]; V[i] = v[4];
+        } else {
+            v[0] = a.X[i]; v[1] = a.Y[i]; v[2] = a.Z[i]; v[3] = a.U[i]; v[4] = a.V[i];
+        }
         XC[i] = (float)((double)v[0] - c[0]);
         YC[i] = (float)((double)v[1] - c[1]);
         ZC[i] = (float)((double)v[2] - c[2]);
@@ -2183,12 +2197,23 @@ hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t 
         if (!PF && prep->part && prep->ticket) {
             unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
             if (g > kSetupMaxBlocks) g = kSetupMaxBlocks;
-            hipLaunchKernelGGL(k_pnp_setup_fc, dim3(g), dim3(256), 0, s, prep->p3, prep->p2, a, prep->X, prep->Y,
-                               prep->Z, prep->U, prep->V, ws, frame, fconst, XC, YC, ZC, prep->part, prep->ticket);
+            hipLaunchKernelGGL(k_pnp_setup_fc<true>, dim3(g), dim3(256), 0, s, prep->p3, prep->p2, a, prep->X,
+                               prep->Y, prep->Z, prep->U, prep->V, ws, frame, fconst, XC, YC, ZC, prep->part,
+                               prep->ticket);
         } else {
             hipLaunchKernelGGL(k_pnp_setup1, dim3(1), dim3(1024), 0, s, prep->p3, prep->p2, a, prep->X, prep->Y,
                                prep->Z, prep->U, prep->V, ws, frame, fconst, XC, YC, ZC, PF);
         }
+        return hipGetLastError();
+    }
+    if (P == 1 && !PF && prep && prep->part && prep->ticket) {
+        // one problem already in f32: bounds, frame and centring in one full-grid launch
+        unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
+        if (g > kSetupMaxBlocks) g = kSetupMaxBlocks;
+        hipLaunchKernelGGL(k_pnp_setup_fc<false>, dim3(g), dim3(256), 0, s, (const double *)nullptr,
+                           (const double *)nullptr, a, (float *)nullptr, (float *)nullptr, (float *)nullptr,
+                           (float *)nullptr, (float *)nullptr, ws, frame, fconst, XC, YC, ZC, prep->part,
+                           prep->ticket);
         return hipGetLastError();
     }
     if (P == 1 && max_n <= 65536) {
