@@ -151,6 +151,7 @@ struct rsac_ctx {
     std::vector<char> last_tables;                             // the tables last uploaded (stage_tables)
     void *last_tables_dev = nullptr;
     // pinned host staging
+    DevBuf scanrec;                                            // first-round improvement records (P > 1)
     PinBuf h_scanrec;
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask, h_epnp;
 };
@@ -564,9 +565,21 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
         std::vector<int> full;  // problems scanned from their full count / status rows
         if (!lo && hb == 0) {
             HIPCHK(c->h_scanrec.ensure(sizeof(ScanRecords) * P));
-            // the kernel writes the records straight into pinned host memory (no copy launch)
-            HIPCHK(launch_scan_records(c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, P, (int32_t)Hr,
-                                       model_points, c->h_scanrec.as<ScanRecords>(), s, spec ? *spec : ScanDecide()));
+            // one problem: the kernel writes its record straight into pinned host memory (no copy
+            // launch); many problems: device records and one copy (thousands of scattered 4-byte
+            // writes over PCIe cost more than the copy)
+            if (P == 1) {
+                HIPCHK(launch_scan_records(c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, P, (int32_t)Hr,
+                                           model_points, c->h_scanrec.as<ScanRecords>(), s,
+                                           spec ? *spec : ScanDecide()));
+            } else {
+                HIPCHK(c->scanrec.ensure(sizeof(ScanRecords) * P));
+                HIPCHK(launch_scan_records(c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, P, (int32_t)Hr,
+                                           model_points, c->scanrec.as<ScanRecords>(), s,
+                                           spec ? *spec : ScanDecide()));
+                HIPCHK(hipMemcpyAsync(c->h_scanrec.p, c->scanrec.p, sizeof(ScanRecords) * P, hipMemcpyDeviceToHost,
+                                      s));
+            }
             if (spec) {  // no synchronisation: the caller enqueues the finish, then spec_resolve
                 out.spec_pending = true;
                 out.spec_H = Hr;
@@ -968,7 +981,7 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr, &c->setup_scr};
+                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr, &c->setup_scr, &c->scanrec};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,
