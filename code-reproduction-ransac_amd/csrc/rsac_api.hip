@@ -409,6 +409,7 @@ struct LoopOut {
     // the host and the device has picked the winner; spec_resolve replays and verifies
     bool spec_pending = false;
     int64_t spec_H = 0;
+    bool timing = true;  // HIP events around solve / score (the caller wants rsac_stats)
 };
 
 // LO-RANSAC local optimisation of the new best of problem 0 (DESIGN.md "LO-RANSAC";
@@ -544,21 +545,21 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
             HIPCHK(copy_rows(c->substatus.as<int8_t>() + hb, stride, hss + hb, stride, Hr, P,
                                     hipMemcpyHostToDevice, s));
         }
-        HIPCHK(hipEventRecord(c->ev0, s));
+        if (out.timing) HIPCHK(hipEventRecord(c->ev0, s));
         if (pa) {
             HIPCHK(launch_pnp_solve(*pa, P, hb, Hr, s));
-            HIPCHK(hipEventRecord(c->ev1, s));
+            if (out.timing) HIPCHK(hipEventRecord(c->ev1, s));
             HIPCHK(launch_pnp_score(*pa, P, hb, Hr, c->counts.as<int32_t>(), s));
         } else if (model == Model::Fm) {
             HIPCHK(launch_fm_solve(*ha, P, hb, Hr, s));
-            HIPCHK(hipEventRecord(c->ev1, s));
+            if (out.timing) HIPCHK(hipEventRecord(c->ev1, s));
             HIPCHK(launch_fm_score(*ha, P, hb, Hr, c->counts.as<int32_t>(), s));
         } else {
             HIPCHK(launch_hom_solve(*ha, P, hb, Hr, s));
-            HIPCHK(hipEventRecord(c->ev1, s));
+            if (out.timing) HIPCHK(hipEventRecord(c->ev1, s));
             HIPCHK(launch_hom_score(*ha, P, hb, Hr, c->counts.as<int32_t>(), s));
         }
-        HIPCHK(hipEventRecord(c->ev2, s));
+        if (out.timing) HIPCHK(hipEventRecord(c->ev2, s));
         // the first round without LO: the device lists each problem's scan improvements
         // (prefix-maximum records) and the host replays the exact scan on them; later rounds (and
         // LO) copy every count
@@ -608,7 +609,7 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
                               c->h_status.as<int8_t>() + (size_t)p * Hr, Hr, np, model_points, confidence);
                 }
             }
-            add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
+            if (out.timing) add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
             out.rounds++;
             out.scored += (int64_t)Hr;
             bool all_done = true;
@@ -621,7 +622,7 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
         HIPCHK(copy_rows(c->h_status.p, Hr, c->status.as<int8_t>() + hb, stride, Hr, P,
                                 hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
+        if (out.timing) add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
         out.rounds++;
         out.scored += (int64_t)Hr;
         bool all_done = true;
@@ -665,7 +666,7 @@ int spec_resolve(rsac_ctx *c, const Staged &st, LoopOut &out, int model_points, 
     }
     const int np = (int)(st.off[1] - st.off[0]);
     scan_records(out.scan[0], rec.idx, rec.cnt, rec.nrec, rec.first_neg, out.spec_H, np, model_points, confidence);
-    add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
+    if (out.timing) add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
     out.rounds = 1;
     out.scored = out.spec_H;
     ok = out.scan[0].done && rec.dev_done && out.scan[0].best == (int64_t)rec.dev_best;
@@ -823,6 +824,7 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         dec.confidence = conf;
     }
     LoopOut lo;
+    lo.timing = stats != nullptr;
     r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, spec ? &dec : nullptr);
     if (r) return r;
     const bool refit = (flags & (RSAC_F_REFINE | RSAC_F_EPNP)) != 0;

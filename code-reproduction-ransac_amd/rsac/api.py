@@ -35,7 +35,10 @@ class _In:
         if _is_torch(a):
             import torch
             self.torch = True
-            t = a.reshape(-1, cols).to(torch.float64).contiguous()
+            if a.dtype == torch.float64 and a.dim() == 2 and a.shape[1] == cols and a.is_contiguous():
+                t = a  # already the (n, cols) float64 layout: no view or copy (the common GPU call)
+            else:
+                t = a.reshape(-1, cols).to(torch.float64).contiguous()
             self.device = t.is_cuda
             if not self.device:
                 t = t.numpy()
@@ -100,7 +103,10 @@ def _mask_buffer(inp: _In, n: int):
 
 def _finish_mask(m, n):
     # uint8 0/1 -> bool without a copy (torch: reinterpret the bytes)
-    return m[:n].view(dtype=__import__("torch").bool) if _is_torch(m) else m[:n].view(np.bool_)
+    if _is_torch(m):
+        import torch
+        return (m if m.shape[0] == n else m[:n]).view(dtype=torch.bool)
+    return m[:n].view(np.bool_)
 
 
 @dataclass
@@ -161,7 +167,8 @@ def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float 
         code = L.check(L.lib().rsac_pnp_ransac(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), n,
                                                K9.ctypes.data, int(n_iters), float(reproj_thresh),
                                                float(confidence), int(seed) & (2**64 - 1), flags, R.ctypes.data,
-                                               t.ctypes.data, C.c_void_p(mptr), C.byref(st), _stream_of(p3)))
+                                               t.ctypes.data, C.c_void_p(mptr),
+                                               C.byref(st) if return_info else None, _stream_of(p3)))
     m = _finish_mask(mask, n)
     out = (R.reshape(3, 3), t, m) if code == L.OK else (None, None, m)
     return out + (_info(code, st),) if return_info else out
