@@ -74,7 +74,7 @@ extern "C" {
 
 typedef struct rsac_ctx rsac_ctx;
 
-/* per-call diagnostics (all optional) */
+/* per-call diagnostics (all optional; without them no HIP timing events are recorded) */
 typedef struct rsac_stats {
     int64_t best_hyp;      /* index of the winning hypothesis (-1 none) */
     int64_t iters;         /* RANSAC iterations consumed (OpenCV `iter` at exit) */
@@ -94,10 +94,10 @@ RSAC_EXPORT const char *rsac_last_error(void);
 RSAC_EXPORT int rsac_abi_version(void);
 RSAC_EXPORT int rsac_device_count(void);
 RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
-/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default;
- * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 MFMA tilings, 16..20 the
- * branch-free alpha-beta band tilings).  Counts,
- * masks and models never depend on it. */
+/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 25;
+ * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 MFMA tilings, 16..28 the
+ * branch-free alpha-beta band tilings, 30..34 the f16-split MFMA kernel; 35..37 are timing
+ * experiments whose counts are wrong).  Counts, masks and models never depend on 0..34. */
 RSAC_EXPORT int rsac_set_score_variant(int variant);
 
 /* cv2.solvePnPRansac (main_v1.py:497).  K: 3x3 row-major f64.  Minimal
