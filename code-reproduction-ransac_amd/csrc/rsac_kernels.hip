@@ -408,15 +408,32 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
     if (threadIdx.x == 0) last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
     __syncthreads();
     if (!last) return;
-    // the last block: every block's bounds are in (sc1 stores drained before each ticket add)
+    // the last block: every block's bounds are in (sc1 stores drained before each ticket add);
+    // thread b loads block b's (all in flight at once), then min / max across the block
     __shared__ int wsl[10];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
+    if (threadIdx.x < gridDim.x)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            lo[k] = __hip_atomic_load(part + 10 * threadIdx.x + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi[k] = __hip_atomic_load(part + 10 * threadIdx.x + 5 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
+        }
+    __syncthreads();  // sl / sh are rewritten
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { sl[wave][k] = lo[k]; sh[wave][k] = hi[k]; }
+    __syncthreads();
     if (threadIdx.x < 5) {
         const int k = threadIdx.x;
-        float l = __builtin_inff(), h = -__builtin_inff();
-        for (int b = 0; b < (int)gridDim.x; ++b) {
-            l = fminf(l, __hip_atomic_load(part + 10 * b + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            h = fmaxf(h, __hip_atomic_load(part + 10 * b + 5 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        }
+        const float l = fminf(fminf(sl[0][k], sl[1][k]), fminf(sl[2][k], sl[3][k]));
+        const float h = fmaxf(fmaxf(sh[0][k], sh[1][k]), fmaxf(sh[2][k], sh[3][k]));
         const int wl = n > 0 ? min(0x7F7F7F7F, f2ord(l)) : 0x7F7F7F7F;
         const int wh = n > 0 ? max((int)0x80808080, f2ord(h)) : (int)0x80808080;
         ws[k] = wl;
