@@ -2641,7 +2641,7 @@ constexpr int kLmRed = kLmTerms + 1;  // widest LM reduction: normal equations +
 // staged once), then, multi-block only, the nb block sums of a reduction ([block][kLmRed])
 constexpr int kLmStage = 8 * kLmThreads;
 constexpr int kLmLdsBytes = 5 * kLmStage * 4 + kLmMaxBlocks * kLmRed * 8;
-static_assert(kLmBlockPoints <= kLmStage, "a range of ~2048 points fits one tile");
+static_assert(kLmBlockPoints <= kLmStage, "a range of ~1024 points fits one tile");
 static_assert(kLmMaxBlocks * kLmRed * 2 <= 8 * kLmThreads, "one sweep pass covers every granule");
 
 typedef __attribute__((address_space(1))) unsigned long long lm_gu64;

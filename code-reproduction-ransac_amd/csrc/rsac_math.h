@@ -689,9 +689,10 @@ RSAC_HD bool fm_inlier(const double *F, double x1, double y1, double x2, double 
 // ---------------------------------------------------------------------------
 constexpr int kLmThreads = 512;
 constexpr int kLmMaxBlocks = 64;
-constexpr int kLmBlockPoints = 2048;  // range length above 4096 points
+constexpr int kLmOneBlock = 4096;     // one range up to this many points
+constexpr int kLmBlockPoints = 1024;  // range length above it: ~2 inliers per thread at 50 %
 RSAC_HD int lm_blocks(int n) {
-    if (n <= 2 * kLmBlockPoints) return 1;
+    if (n <= kLmOneBlock) return 1;
     const int nb = (n + kLmBlockPoints - 1) / kLmBlockPoints;
     return nb < kLmMaxBlocks ? nb : kLmMaxBlocks;
 }

@@ -983,7 +983,7 @@ ORC_API int64_t orc_fm_ransac(const float *x1, const float *y1, const float *x2,
  * |d| < FLT_EPSILON (|t| + 1) (CvLevMarq's step criterion of solvePnP).
  * The pose is refined in the frame centred on the first point c (t' = R c + t).
  * Sums use the GPU kernel's block-compacted order: nb = lm_blocks(n) contiguous ranges of
- * lm_chunk(n) points (one range up to 4096 points, then ranges of ~2048, at most 64); the
+ * lm_chunk(n) points (one range up to 4096 points, then ranges of ~1024, at most 64); the
  * masked points of range b, ascending, dealt round-robin to slots b*512 + p%512; per-slot
  * sums in order, a 64-lane butterfly per wave of 64 slots (x += x[lane ^ o], o = 32..1),
  * each range's 8 wave sums left to right, then the nb range sums left to right -- so the
@@ -991,11 +991,12 @@ ORC_API int64_t orc_fm_ransac(const float *x1, const float *y1, const float *x2,
  * bit for bit. */
 #define LM_THREADS 512
 #define LM_MAX_BLOCKS 64
-#define LM_BLOCK_POINTS 2048
+#define LM_ONE_BLOCK 4096
+#define LM_BLOCK_POINTS 1024
 #define LM_TERMS 27
 
 static int lm_blocks(int n) {
-    if (n <= 2 * LM_BLOCK_POINTS) return 1;
+    if (n <= LM_ONE_BLOCK) return 1;
     int nb = (n + LM_BLOCK_POINTS - 1) / LM_BLOCK_POINTS;
     return nb < LM_MAX_BLOCKS ? nb : LM_MAX_BLOCKS;
 }
