@@ -47,7 +47,7 @@ def test_host_only_helpers():
     assert rsac.update_num_iters(0.99, 0.5, 4, 5000) == 71
 
 
-# 9000 / 70000 / 300000: 5 / 35 / 64 ranges of the block-compacted order (the last one's ranges
+# 9000 / 70000 / 300000: 9 / 64 / 64 ranges of the block-compacted order (the last one's ranges
 # exceed one LDS tile on the GPU); masked: every third point dropped, so ranges compact unevenly
 @pytest.mark.parametrize("n,masked", [(500, False), (4097, True), (9000, False), (9000, True), (70000, True),
                                       (300000, True)])
