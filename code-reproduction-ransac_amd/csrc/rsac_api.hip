@@ -142,6 +142,8 @@ struct rsac_ctx {
     DevBuf lo;                                                 // LO-RANSAC: 2 model records, chain state, 2 masks
     const void *lo_state_base = nullptr;                       // the lo allocation whose LoState is zeroed
     PinBuf h_lo;                                               // LO chain state, written by the device
+    PinBuf h_lmfail;                                           // multi-block refit failure word (device-written)
+    int dbg_refit_max_blocks = 0;                              // RSAC_DBG_REFIT_MAX_BLOCKS (0: device limit)
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
     DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
@@ -418,15 +420,36 @@ struct LoopOut {
 // hypothesis' record, so the final mask / gather / refit see it.
 constexpr int kLoSteps = 4;
 
-// the multi-block LM refit's scratch (rsac_internal.h LmScratch; granules zeroed once here)
+// the multi-block LM refit's scratch (rsac_internal.h LmScratch; granules zeroed once here),
+// the device's co-resident block limit for it, and the pinned failure word
 LmScratch *lm_scratch(rsac_ctx *c, hipStream_t s) {
     if (!c->lmscr.p) {
         if (c->lmscr.ensure(kLmGranuleBytes) != hipSuccess) return nullptr;
         if (hipMemsetAsync(c->lmscr.p, 0, kLmGranuleBytes, s) != hipSuccess) return nullptr;
+        if (c->h_lmfail.ensure(sizeof(int32_t)) != hipSuccess) return nullptr;
+        *c->h_lmfail.as<int32_t>() = 0;
         c->lm.gran = (unsigned long long *)c->lmscr.p;
+        c->lm.fail = c->h_lmfail.as<int32_t>();
         c->lm.launch = 0;
+        c->lm.max_blocks = 0;
+    }
+    if (c->lm.max_blocks == 0) {
+        c->lm.max_blocks = pnp_refine_coresident(c->device);
+        if (c->dbg_refit_max_blocks > 0) c->lm.max_blocks = std::min(c->lm.max_blocks, c->dbg_refit_max_blocks);
     }
     return &c->lm;
+}
+
+// after the synchronisation that follows refits: a multi-block refit whose range sums never
+// all arrived (its blocks were not co-resident) kept the start pose and set the failure word
+int lm_check(rsac_ctx *c) {
+    int32_t *f = c->h_lmfail.as<int32_t>();
+    if (f && __atomic_load_n(f, __ATOMIC_ACQUIRE)) {
+        *f = 0;
+        return fail(RSAC_EHIP, "pose refit: the cooperating blocks of a multi-block LM refit were not all resident "
+                               "(a range's sums never arrived); the RANSAC pose was kept");
+    }
+    return RSAC_OK;
 }
 
 // The kLoSteps steps are enqueued at once and decided on the device (k_pnp_lo_count): step k
@@ -456,6 +479,7 @@ int local_opt(rsac_ctx *c, const PnpArgs &a, int32_t n, ScanState &sc, double co
         HIPCHK(launch_pnp_lo_count(a, n, dst, mk[(step + 1) & 1], st, step, 0, best_rec, hst, s));
     }
     HIPCHK(hipStreamSynchronize(s));
+    if (int r = lm_check(c)) return r;
     improvements += hst->improvements;
     if (hst->improvements > 0 && hst->cur > sc.max_good) {
         sc.max_good = hst->cur;
@@ -788,6 +812,8 @@ int pnp_finish(rsac_ctx *c, const Staged &st, const PnpArgs &a, const LoopOut &l
         HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,
                               hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (flags & RSAC_F_REFINE)
+        if (int r = lm_check(c)) return r;
     finish_masks_host(c, st, mask_out, flags);
     return RSAC_OK;
 }
@@ -985,7 +1011,7 @@ void rsac_destroy(rsac_ctx *c) {
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
                      &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr, &c->setup_scr, &c->scanrec};
     for (DevBuf *b : dev) b->release();
-    PinBuf *pin[] = {&c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
+    PinBuf *pin[] = {&c->h_lmfail, &c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,
                      &c->h_epnp};
     for (PinBuf *b : pin) b->release();
@@ -1002,6 +1028,34 @@ void rsac_destroy(rsac_ctx *c) {
 int rsac_set_score_variant(int variant) {
     if (variant < -1 || (variant > 28 && (variant < 30 || variant > 37))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
     set_score_variant(variant);
+    return RSAC_OK;
+}
+
+int rsac_debug_set(rsac_ctx *c, int32_t key, int64_t value) {
+    if (!c) return fail(RSAC_EINVAL, "null context");
+    switch (key) {
+    case RSAC_DBG_REFIT_MAX_BLOCKS:
+        if (value < 0) return fail(RSAC_EINVAL, "bad block cap");
+        c->dbg_refit_max_blocks = (int)std::min<int64_t>(value, kLmMaxBlocks);
+        c->lm.max_blocks = 0;  // recomputed by the next refit
+        return RSAC_OK;
+    case RSAC_DBG_REFIT_DROP_BLOCK:
+        c->lm.drop_block = value != 0;
+        return RSAC_OK;
+    default:
+        return fail(RSAC_EINVAL, "unknown debug key %d", key);
+    }
+}
+
+int rsac_refit_blocks(rsac_ctx *c, int32_t n, int32_t *ranges, int32_t *blocks) {
+    if (!c || n < 0) return fail(RSAC_EINVAL, "bad arguments");
+    int r = check_device(c);
+    if (r) return r;
+    LmScratch *lm = lm_scratch(c, c->stream);
+    if (!lm) return fail(RSAC_ENOMEM, "refit scratch");
+    const int nb = lm_blocks(n);
+    if (ranges) *ranges = nb;
+    if (blocks) *blocks = nb > 1 ? std::min(nb, lm->max_blocks) : 1;
     return RSAC_OK;
 }
 

@@ -197,7 +197,12 @@ constexpr size_t kLmGranuleBytes = 2ull * 64 * 28 * 2 * 8;
 struct LmScratch {
     unsigned long long *gran = nullptr;
     unsigned launch = 0;
+    int max_blocks = 0;        // blocks of one problem that can run at once (pnp_refine_coresident)
+    int drop_block = 0;        // test hook RSAC_DBG_REFIT_DROP_BLOCK
+    int32_t *fail = nullptr;   // pinned host word: a refit's range sums never arrived
 };
+// co-resident k_pnp_refine blocks on `device` (occupancy x CUs, capped at kLmMaxBlocks; >= 1)
+int pnp_refine_coresident(int device);
 hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, double *models, int32_t *iters,
                              hipStream_t s, LmScratch *scratch, const int64_t *host_off,
                              double *host_models = nullptr,  // pinned: R, t also written there

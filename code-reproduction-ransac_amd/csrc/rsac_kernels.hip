@@ -2637,15 +2637,21 @@ hipError_t launch_loc_score(const double *src, const double *dst, const uint8_t 
 // ---------------------------------------------------------------------------
 constexpr int kLmRed = kLmTerms + 1;  // widest LM reduction: normal equations + cost
 
-// LDS of k_pnp_refine: the staged points (SoA, [5][4096]: a range of up to 4096 points is
-// staged once), then, multi-block only, the nb block sums of a reduction ([block][kLmRed])
+// LDS of k_pnp_refine: the staged points (SoA, [5][kLmStage]), then, multi-range only, the nb
+// range sums of a reduction ([range][kLmRed]).  Ranges are one of up to 4096 points, else
+// ~1024 points (lm_blocks / lm_chunk of rsac_math.h: lm_chunk(n) <= kLmStage for every
+// n <= kLmMaxBlocks * kLmStage = 262144, checked in tests/test_abi.py).  A block stages the
+// masked points of all the ranges it owns once per refit when their indices fit one tile
+// (always, when it owns one range and n <= 262144); otherwise every pass re-stages each range
+// tile by tile in the same order.
 constexpr int kLmStage = 8 * kLmThreads;
 constexpr int kLmLdsBytes = 5 * kLmStage * 4 + kLmMaxBlocks * kLmRed * 8;
 static_assert(kLmBlockPoints <= kLmStage, "a range of ~1024 points fits one tile");
+static_assert(kLmOneBlock <= kLmStage, "a one-range problem of up to 4096 points fits one tile");
 static_assert(kLmMaxBlocks * kLmRed * 2 <= 8 * kLmThreads, "one sweep pass covers every granule");
 
 typedef __attribute__((address_space(1))) unsigned long long lm_gu64;
-constexpr unsigned kLmSpinLimit = 1u << 20;  // ~1 s of polls: a block that never arrives ends the waits
+constexpr unsigned kLmSpinLimit = 1u << 20;  // ~1 s of polls: a range whose sums never arrive ends the waits
 
 struct GpuLmReducer {
     static constexpr bool kFused = true;  // cost_normal: one pass for a candidate (rsac_math.h)
@@ -2655,39 +2661,51 @@ struct GpuLmReducer {
     Cam k;
     double c0, c1, c2;  // centre of the refit frame
     double (*wsum)[kLmRed];  // LDS [kLmThreads / 64][kLmRed]
-    // this block's range [lo, hi) of the block-compacted order (rsac_math.h).  More than one
-    // block per problem (nb > 1): every reduction's wave sums are handed over as data-tagged
-    // granules (gran, below), no barrier
+    // the nb ranges of the block-compacted order (rsac_math.h).  The problem's G blocks share
+    // them: block x owns ranges x, x + G, x + 2G, ... (G = nb unless the device cannot hold nb
+    // blocks at once; launch_pnp_refine).  Every reduction yields one sum per range and term;
+    // with G > 1 they are handed over as data-tagged granules (gran, below), no barrier
     int nb = 1;
-    int lo = 0, hi = 0;
-    float *stage = nullptr;  // LDS [5][cap]: compacted X Y Z U V of the range
+    int first = 0, G = 1, nown = 1;  // this block's first range, the range stride, ranges owned
+    float *stage = nullptr;  // LDS [5][cap]: compacted X Y Z U V of the owned ranges
     int cap = kLmStage;
     int *scan = nullptr;     // LDS [kLmThreads / 64]: wave totals
-    int staged = -1;         // masked points of a range that fits one tile (staged once); -1: re-staged per pass
-    // multi-block hand-off (cdna_hip_programming.md Guideline 16, R2): the block's sum of term q
-    // goes out as two 8-byte {tag, 32-bit half} granules, stored sc1 by thread q; every block
-    // sweeps all nb * nv * 2 granules with sc1 loads until each carries this reduction's tag
-    // (launch tag | reduction index: unique per launch, the host zeroes the granules on wrap),
-    // into LDS (wsums), and sums them left to right.  Two alternating granule buffers: a block
-    // overwrites buffer k % 2 only after every block has stored reduction k - 1, i.e. finished
-    // reading reduction k - 2.
+    int *rbase = nullptr;    // LDS [kLmMaxBlocks]: owned range k's staged points start at stage[rbase[k]] ...
+    int *rcnt = nullptr;     // LDS [kLmMaxBlocks]: ... and number rcnt[k]
+    int staged = -1;         // masked points staged once for the whole refit; -1: re-staged per pass
+    // multi-block hand-off (cdna_hip_programming.md Guideline 16, R2): range r's sum of term q
+    // goes out as two 8-byte {tag, 32-bit half} granules, stored sc1 by thread q of the owning
+    // block; every block sweeps all nb * nv * 2 granules with sc1 loads until each carries this
+    // reduction's tag (launch tag | reduction index: unique per launch, the host zeroes the
+    // granules on wrap), into LDS (wsums), and sums them left to right.  Two alternating granule
+    // buffers: a block overwrites buffer k % 2 only after every block has stored reduction
+    // k - 1, i.e. finished reading reduction k - 2.
     lm_gu64 *gran = nullptr;  // [2][kLmMaxBlocks][kLmRed][2]
     unsigned tag_base = 0;
     int phase = 0;
-    double *wsums = nullptr;  // LDS [kLmMaxBlocks][kLmRed]: the blocks' sums
+    double *wsums = nullptr;  // LDS [kLmMaxBlocks][kLmRed]: the ranges' sums
+    // block-uniform: a reduction's sums never all arrived (a block that was never resident);
+    // the remaining reductions return NaN without waiting and the kernel reports the failure
     bool broken = false;
     double (*accs)[kLmRed] = nullptr;  // LDS [2][kLmRed]: pnp_lm_refine's normal equations
     double *res = nullptr;             // LDS [1]: a cost reduction's result
     __device__ double *acc_buf(int k) { return accs[k]; }
 
-    // the masked points of [tlo, thi) (at most cap indices), ascending, into stage[.][0, cnt);
-    // returns cnt (block-uniform).  Thread t covers indices tlo + (cap / 512) t, ...
-    __device__ int stage_tile(int tlo, int thi) {
+    __device__ void range_of(int r, int &lo, int &hi) const {
+        const int C = lm_chunk(n);
+        lo = r * C;
+        hi = (int)min((int64_t)n, (int64_t)lo + C);
+    }
+
+    // the masked points of [tlo, thi) (at most cap - base indices), ascending, into
+    // stage[.][base, base + cnt); returns cnt (block-uniform).  Thread t covers indices
+    // tlo + (cap / 512) t, ...
+    __device__ int stage_tile(int tlo, int thi, int base) {
         const int per = cap / kLmThreads;  // 8 or 4
-        const int base = tlo + per * (int)threadIdx.x;
+        const int first_i = tlo + per * (int)threadIdx.x;
         unsigned bits = 0;
-        for (int k = 0; k < per; ++k)
-            if (base + k < thi && mask[base + k]) bits |= 1u << k;
+        for (int j = 0; j < per; ++j)
+            if (first_i + j < thi && mask[first_i + j]) bits |= 1u << j;
         const int cnt = __popc(bits);
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         int incl = cnt;
@@ -2698,15 +2716,15 @@ struct GpuLmReducer {
         __syncthreads();  // the previous tile's readers are done with stage and scan
         if (lane == 63) scan[wave] = incl;
         __syncthreads();
-        int pos = incl - cnt, tot = 0;
+        int pos = base + incl - cnt, tot = 0;
         for (int w = 0; w < kLmThreads / 64; ++w) {
             const int v = scan[w];
             pos += w < wave ? v : 0;
             tot += v;
         }
-        for (int k = 0; k < per; ++k)
-            if (bits >> k & 1u) {
-                const int i = base + k;
+        for (int j = 0; j < per; ++j)
+            if (bits >> j & 1u) {
+                const int i = first_i + j;
                 stage[pos] = X[i];
                 stage[cap + pos] = Y[i];
                 stage[2 * cap + pos] = Z[i];
@@ -2717,27 +2735,50 @@ struct GpuLmReducer {
         __syncthreads();
         return tot;
     }
-    __device__ void set_range(int b) {
-        const int C = lm_chunk(n);
-        lo = b * C;
-        hi = (int)min((int64_t)n, (int64_t)lo + C);
-        if (hi - lo <= cap) staged = stage_tile(lo, hi);
+    // block b0 of a problem whose ranges are shared by `stride` blocks
+    __device__ void set_ranges(int b0, int stride) {
+        first = b0;
+        G = stride;
+        nown = (nb - b0 + G - 1) / G;
+        int span = 0;
+        for (int r = b0; r < nb; r += G) {
+            int lo, hi;
+            range_of(r, lo, hi);
+            span += hi - lo;
+        }
+        if (span > cap) return;  // staged = -1: tiles per pass
+        int base = 0;
+        for (int kk = 0, r = b0; r < nb; r += G, ++kk) {
+            int lo, hi;
+            range_of(r, lo, hi);
+            const int cnt = stage_tile(lo, hi, base);
+            if (threadIdx.x == 0) {
+                rbase[kk] = base;
+                rcnt[kk] = cnt;
+            }
+            base += cnt;
+        }
+        __syncthreads();
+        staged = base;
     }
-    // f(Xd, Yd, Zd, u, v) over this thread's points: the range's masked points p = thread,
-    // thread + 512, ... of the compacted order
+    // f(Xd, Yd, Zd, u, v) over this thread's points of owned range kk: the range's masked
+    // points p = thread, thread + 512, ... of the compacted order
     template <class F>
-    __device__ void for_points(F f) {
+    __device__ void for_points(int kk, F f) {
         auto point = [&](int q) {
             f((double)stage[q] - c0, (double)stage[cap + q] - c1, (double)stage[2 * cap + q] - c2,
               (double)stage[3 * cap + q], (double)stage[4 * cap + q]);
         };
         if (staged >= 0) {
-            for (int q = threadIdx.x; q < staged; q += kLmThreads) point(q);
+            const int b = rbase[kk], cnt = rcnt[kk];
+            for (int q = threadIdx.x; q < cnt; q += kLmThreads) point(b + q);
             return;
         }
+        int lo, hi;
+        range_of(first + kk * G, lo, hi);
         int p0 = 0;  // compacted position of the tile's first point
         for (int tlo = lo; tlo < hi; tlo += cap) {
-            const int cnt = stage_tile(tlo, min(hi, tlo + cap));
+            const int cnt = stage_tile(tlo, min(hi, tlo + cap), 0);
             for (int q = ((int)threadIdx.x - p0 % kLmThreads + kLmThreads) % kLmThreads; q < cnt; q += kLmThreads)
                 point(q);
             p0 += cnt;
@@ -2765,9 +2806,9 @@ struct GpuLmReducer {
         return a + __hiloint2double(dhi, dlo);
     }
 
-    // sums a[0, nv) of every thread in the order of rsac_math.h into out[0, nv) (LDS, written by
-    // threads q < nv; complete when this returns)
-    __device__ void reduce(double *a, int nv, double *out) {
+    // the range sum of every term of a[0, nv): the wave trees, then the 8 wave sums left to
+    // right; the result is valid in thread q < nv (returns 0 elsewhere)
+    __device__ double range_sum(double *a, int nv) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         // levels outside, terms inside: the nv reductions are independent and overlap
         for (int q = 0; q < nv; ++q) a[q] = add_down<32>(a[q]);
@@ -2779,7 +2820,6 @@ struct GpuLmReducer {
 #ifdef RSAC_TRACE
         mark(21);
 #endif
-        // the block's sum of term q: its 8 wave sums left to right (thread q)
         if (lane == 0)
             for (int q = 0; q < nv; ++q) wsum[wave][q] = a[q];
         __syncthreads();
@@ -2789,80 +2829,105 @@ struct GpuLmReducer {
             bsum = wsum[0][q];
             for (int w = 1; w < kLmThreads / 64; ++w) bsum = bsum + wsum[w][q];
         }
-        if (nb == 1) {
-            if (threadIdx.x < nv) out[threadIdx.x] = bsum;
-            __syncthreads();  // out is complete; wsum is free for the next reduction
-            return;
-        }
-        ++phase;
+        return bsum;
+    }
+
+    // sums f's terms a[0, NV) over the masked points in the order of rsac_math.h into
+    // out[0, NV) (LDS, written by threads q < NV; complete when this returns)
+    template <int NV, class F>
+    __device__ void sum_terms(F f, double *out) {
+        if (nb > 1 && G > 1) ++phase;
         const unsigned long long tag = (unsigned long long)(tag_base | (unsigned)phase) << 32;
         lm_gu64 *g = gran + (size_t)(phase & 1) * kLmMaxBlocks * kLmRed * 2;
-        // thread q < nv (wave 0) publishes the block's term q
-        if (threadIdx.x < nv) {
-            lm_gu64 *gw = g + ((size_t)blockIdx.x * kLmRed + threadIdx.x) * 2;
-            __hip_atomic_store(gw, tag | (unsigned)__double2loint(bsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gw + 1, tag | (unsigned)__double2hiint(bsum), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        for (int kk = 0; kk < nown; ++kk) {
+            double a[NV];
+            for (int q = 0; q < NV; ++q) a[q] = 0.0;
+            for_points(kk, [&](double Xd, double Yd, double Zd, double u, double v) { f(Xd, Yd, Zd, u, v, a); });
+#ifdef RSAC_TRACE
+            mark(20);
+#endif
+            const double bsum = range_sum(a, NV);
+            const int r = first + kk * G;
+            if (threadIdx.x < NV) {
+                const int q = threadIdx.x;
+                if (nb == 1) {
+                    out[q] = bsum;
+                } else if (G == 1) {
+                    wsums[r * kLmRed + q] = bsum;  // every range in this block: straight to LDS
+                } else {  // thread q (wave 0) publishes range r's term q
+                    lm_gu64 *gw = g + ((size_t)r * kLmRed + q) * 2;
+                    __hip_atomic_store(gw, tag | (unsigned)__double2loint(bsum), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(gw + 1, tag | (unsigned)__double2hiint(bsum), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (kk + 1 < nown) __syncthreads();  // this range's readers of wsum are done
+        }
+        if (nb == 1) {
+            __syncthreads();  // out is complete; wsum is free for the next reduction
+            return;
         }
 #ifdef RSAC_TRACE
         mark(22);
 #endif
-        // sweep: granule k = (block b, term q, half h), k = (b nv + q) 2 + h, at most 8 per thread
-        // (64 blocks x 28 terms x 2 = 3584 <= 8 x 512), all in flight; a pass re-reads the ones
-        // whose tag is not yet this reduction's
-        const int tot = nb * nv * 2;
-        unsigned *ws32 = (unsigned *)wsums;
-        unsigned pending = 0;
+        if (G > 1) {
+            // sweep: granule j = (range b, term q, half h), j = (b NV + q) 2 + h, at most 8 per
+            // thread (64 ranges x 28 terms x 2 = 3584 <= 8 x 512), all in flight; a pass re-reads
+            // the ones whose tag is not yet this reduction's
+            const int tot = nb * NV * 2;
+            unsigned *ws32 = (unsigned *)wsums;
+            unsigned pending = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j * kLmThreads + (int)threadIdx.x < tot) pending |= 1u << j;
-        for (unsigned spins = 0; pending && !broken; ++spins) {
-            unsigned long long x[8];
+            for (int j = 0; j < 8; ++j)
+                if (j * kLmThreads + (int)threadIdx.x < tot) pending |= 1u << j;
+            bool late = false;
+            for (unsigned spins = 0; pending && !broken; ++spins) {
+                unsigned long long x[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = j * kLmThreads + threadIdx.x;
-                const int bb = k / (2 * nv), r = k - bb * 2 * nv;
-                x[j] = (pending >> j & 1u)
-                           ? __hip_atomic_load(g + (size_t)bb * kLmRed * 2 + r, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT)
-                           : 0ull;
-            }
+                for (int j = 0; j < 8; ++j) {
+                    const int i = j * kLmThreads + threadIdx.x;
+                    const int bb = i / (2 * NV), rr = i - bb * 2 * NV;
+                    x[j] = (pending >> j & 1u) ? __hip_atomic_load(g + (size_t)bb * kLmRed * 2 + rr, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT)
+                                               : 0ull;
+                }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (!(pending >> j & 1u) || (x[j] & 0xFFFFFFFF00000000ull) != tag) continue;
-                const int k = j * kLmThreads + threadIdx.x;
-                const int bb = k / (2 * nv), r = k - bb * 2 * nv;
-                ws32[bb * kLmRed * 2 + r] = (unsigned)x[j];
-                pending &= ~(1u << j);
+                for (int j = 0; j < 8; ++j) {
+                    if (!(pending >> j & 1u) || (x[j] & 0xFFFFFFFF00000000ull) != tag) continue;
+                    const int i = j * kLmThreads + threadIdx.x;
+                    const int bb = i / (2 * NV), rr = i - bb * 2 * NV;
+                    ws32[bb * kLmRed * 2 + rr] = (unsigned)x[j];
+                    pending &= ~(1u << j);
+                }
+                if (pending) {
+                    if (spins >= kLmSpinLimit) {  // a range's sums never arrived: stop waiting (no hang)
+                        late = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
             }
-            if (pending) {
-                if (spins >= kLmSpinLimit) broken = true;  // a block never arrived: stop waiting (no hang)
-                __builtin_amdgcn_s_sleep(1);
-            }
+            broken = __syncthreads_or(broken || late) != 0;  // block-uniform from here on
+        } else {
+            __syncthreads();
         }
-        __syncthreads();
 #ifdef RSAC_TRACE
         mark(23);
 #endif
-        // thread q < nv sums term q over the nb block sums, left to right
-        if (threadIdx.x < nv) {
+        // thread q < NV sums term q over the nb range sums, left to right
+        if (threadIdx.x < NV) {
             const int q = threadIdx.x;
             double s = wsums[q];
             for (int bb = 1; bb < nb; ++bb) s = s + wsums[bb * kLmRed + q];
-            out[q] = s;
+            out[q] = broken ? __builtin_nan("") : s;
         }
         __syncthreads();
     }
     __device__ void normal(const double *R, const double *t, double *acc) {
-        double a[kLmTerms];
-        for (int q = 0; q < kLmTerms; ++q) a[q] = 0.0;
-        for_points([&](double Xd, double Yd, double Zd, double u, double v) {
-            pnp_lm_point(R, t, k, Xd, Yd, Zd, u, v, a);
-        });
-#ifdef RSAC_TRACE
-        mark(20);
-#endif
-        reduce(a, kLmTerms, acc);
+        sum_terms<kLmTerms>([&](double Xd, double Yd, double Zd, double u, double v,
+                                double *a) { pnp_lm_point(R, t, k, Xd, Yd, Zd, u, v, a); },
+                            acc);
     }
 #ifdef RSAC_TRACE
     unsigned long long stamp[96];
@@ -2882,38 +2947,38 @@ struct GpuLmReducer {
     }
 #endif
     __device__ double cost(const double *R, const double *t) {
-        double a = 0.0;
-        for_points([&](double Xd, double Yd, double Zd, double u, double v) {
-            a += pnp_lm_cost_point(R, t, k, Xd, Yd, Zd, u, v);
-        });
-        reduce(&a, 1, res);
+        sum_terms<1>([&](double Xd, double Yd, double Zd, double u, double v,
+                         double *a) { a[0] += pnp_lm_cost_point(R, t, k, Xd, Yd, Zd, u, v); },
+                     res);
         return res[0];
     }
     // cost(R, t) and normal(R, t) in one pass: per-slot partials and reductions are term by
     // term the same as the separate passes'
     __device__ double cost_normal(const double *R, const double *t, double *acc) {
-        double a[kLmRed];
-        for (int q = 0; q < kLmRed; ++q) a[q] = 0.0;
-        for_points([&](double Xd, double Yd, double Zd, double u, double v) {
-            pnp_lm_point(R, t, k, Xd, Yd, Zd, u, v, a);
-            a[kLmTerms] += pnp_lm_cost_point(R, t, k, Xd, Yd, Zd, u, v);
-        });
-        reduce(a, kLmRed, acc);  // acc: an acc_buf (kLmRed wide), the cost in its last slot
+        sum_terms<kLmRed>(
+            [&](double Xd, double Yd, double Zd, double u, double v, double *a) {
+                pnp_lm_point(R, t, k, Xd, Yd, Zd, u, v, a);
+                a[kLmTerms] += pnp_lm_cost_point(R, t, k, Xd, Yd, Zd, u, v);
+            },
+            acc);  // acc: an acc_buf (kLmRed wide), the cost in its last slot
         return acc[kLmTerms];
     }
 };
 
-// one problem per blockIdx.y (prob_base + y); blocks x < lm_blocks(n) of it take part, one
-// per range of the block-compacted order (x > 0 only when the problem has more than 4096 points).  Multi-block problems need all
-// their blocks co-resident: the launcher keeps them to one problem per launch (<= 64 blocks).
+// one problem per blockIdx.y (prob_base + y).  A problem of nb = lm_blocks(n) > 1 ranges runs in
+// a launch of its own with G <= nb blocks (stride, = gridDim.x unless a test drops a block),
+// block x owning ranges x, x + G, ...; all G blocks must be co-resident (launch_pnp_refine caps
+// G at the device's limit).  fail (pinned host word): set when a reduction's sums never arrived;
+// block 0 then writes the start pose back instead of a refined one.
 __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint8_t *__restrict__ mask,
                                                            double *__restrict__ models, int32_t *__restrict__ iters,
                                                            int prob_base, unsigned long long *gran, unsigned tag_base,
                                                            double *host_models, const double *src,
-                                                           const int32_t *stop) {
+                                                           const int32_t *stop, int stride, int32_t *fail) {
     __shared__ double wsum[kLmThreads / 64][kLmRed];
     __shared__ double accs[2][kLmRed], res[1];
     __shared__ int scan[kLmThreads / 64];
+    __shared__ int rtab[2][kLmMaxBlocks];
     __shared__ __attribute__((aligned(16))) char lds[kLmLdsBytes];  // 94 KB
     const int prob = prob_base + blockIdx.y;
     const int64_t p0 = a.offsets[prob];
@@ -2940,22 +3005,30 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     red.stage = (float *)lds;
     red.cap = kLmStage;
     red.scan = scan;
+    red.rbase = rtab[0];
+    red.rcnt = rtab[1];
     red.gran = (lm_gu64 *)gran;
     red.tag_base = tag_base;
     red.wsums = (double *)(lds + 5 * kLmStage * 4);
     red.accs = accs;
     red.res = res;
-    red.set_range(blockIdx.x);
+    red.set_ranges(blockIdx.x, nb > 1 ? stride : 1);
     double R[9], t[3];
     for (int j = 0; j < 9; ++j) R[j] = ms[j];
     for (int j = 0; j < 3; ++j) t[j] = ms[9 + j];
     lm_to_centred(R, c, t);
-    const int it = pnp_lm_refine(red, R, t, kLmMaxIter);
+    int it = pnp_lm_refine(red, R, t, kLmMaxIter);
 #ifdef RSAC_TRACE
     red.mark(99);
     red.dump();
 #endif
     lm_from_centred(R, c, t);
+    if (red.broken) {  // block-uniform: report, and keep the start pose
+        if (threadIdx.x == 0 && fail) __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int j = 0; j < 9; ++j) R[j] = ms[j];
+        for (int j = 0; j < 3; ++j) t[j] = ms[9 + j];
+        it = 0;
+    }
     // every block read m before its first contribution, and block 0 got past the first
     // reduction only with every block's: no barrier before block 0 overwrites m
     __syncthreads();  // every thread of this block has read m before thread 0 overwrites it
@@ -2971,6 +3044,14 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
             for (int j = 0; j < 3; ++j) h[9 + j] = t[j];
         }
     }
+}
+
+int pnp_refine_coresident(int device) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pnp_refine, kLmThreads, 0) != hipSuccess) return 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 1;
+    const int64_t lim = (int64_t)per_cu * cus;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(lim, kLmMaxBlocks));
 }
 
 // EPnP of every problem's winner on its RANSAC inliers (rsac_math.h pnp_epnp),
@@ -3105,18 +3186,22 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
                              hipStream_t s, LmScratch *scratch, const int64_t *host_off, double *host_models,
                              const double *src, const int32_t *stop) {
     // every problem of up to 4096 points (and, with host_off unknown, every problem) in one
-    // launch, one block each; each larger problem in a launch of its own, lm_blocks(n)
-    // blocks (<= 64, all co-resident) that hand their wave sums over as tagged granules
+    // launch, one block each; each larger problem in a launch of its own: G = min(lm_blocks(n),
+    // the co-resident limit) blocks share its ranges and hand their range sums over as tagged
+    // granules (G = 1: one block walks all the ranges, same order, no exchange)
     const int nb_max = lm_blocks(a.max_n);
     if (!(P == 1 && nb_max > 1))  // (one large problem: only the multi-block launch has work)
         hipLaunchKernelGGL(k_pnp_refine, dim3(1, P), dim3(kLmThreads), 0, s, a, mask, models, iters, 0,
-                           (unsigned long long *)nullptr, 0u, host_models, src, stop);
+                           (unsigned long long *)nullptr, 0u, host_models, src, stop, 1, (int32_t *)nullptr);
     if (nb_max > 1) {
-        if (!scratch || !scratch->gran) return hipErrorInvalidValue;
+        if (!scratch || !scratch->gran || scratch->max_blocks < 1) return hipErrorInvalidValue;
         for (int p = 0; p < P; ++p) {
             const int np = host_off ? (int)(host_off[p + 1] - host_off[p]) : a.max_n;
             const int nb = lm_blocks(np);
             if (nb <= 1) continue;
+            const int G = std::min(nb, scratch->max_blocks);
+            // test hook (RSAC_DBG_REFIT_DROP_BLOCK): one block of the stride is never launched
+            const int launched = scratch->drop_block && G > 1 ? G - 1 : G;
             // tag = launch (22 bits, never 0) << 10 | reduction index (< 1024): unique among the
             // granules in memory, which are zeroed whenever the launch counter wraps
             if (++scratch->launch >= (1u << 22)) {
@@ -3124,8 +3209,8 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
                 if (e != hipSuccess) return e;
                 scratch->launch = 1;
             }
-            hipLaunchKernelGGL(k_pnp_refine, dim3(nb, 1), dim3(kLmThreads), 0, s, a, mask, models, iters, p,
-                               scratch->gran, scratch->launch << 10, host_models, src, stop);
+            hipLaunchKernelGGL(k_pnp_refine, dim3(launched, 1), dim3(kLmThreads), 0, s, a, mask, models, iters, p,
+                               scratch->gran, scratch->launch << 10, host_models, src, stop, G, scratch->fail);
         }
     }
     return hipGetLastError();

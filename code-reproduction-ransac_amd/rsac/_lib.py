@@ -33,6 +33,9 @@ F_LO = 1 << 7
 F_ASYNC = 1 << 8
 F_EPNP = 1 << 9
 
+DBG_REFIT_MAX_BLOCKS = 1
+DBG_REFIT_DROP_BLOCK = 2
+
 ABI_VERSION = 1
 
 
@@ -61,6 +64,8 @@ SIGNATURES = [
     ("rsac_device_count", C.c_int, []),
     ("rsac_set_round_size", C.c_int, [_vp, _i64]),
     ("rsac_set_score_variant", C.c_int, [C.c_int]),
+    ("rsac_refit_blocks", C.c_int, [_vp, _i32, C.POINTER(_i32), C.POINTER(_i32)]),
+    ("rsac_debug_set", C.c_int, [_vp, _i32, _i64]),
     ("rsac_pnp_ransac", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
                                   C.POINTER(Stats), _vp]),
     ("rsac_pnp_ransac_batched", C.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
@@ -174,6 +179,16 @@ class Context:
 
     def set_round_size(self, n: int):
         check(lib().rsac_set_round_size(self._h, int(n)))
+
+    def refit_blocks(self, n: int) -> tuple[int, int]:
+        """(ranges of the refit's summation order, cooperating blocks on this device) for n points"""
+        r, b = _i32(), _i32()
+        check(lib().rsac_refit_blocks(self._h, int(n), C.byref(r), C.byref(b)))
+        return r.value, b.value
+
+    def debug_set(self, key: int, value: int):
+        """test hooks of include/rsac.h (DBG_REFIT_MAX_BLOCKS, DBG_REFIT_DROP_BLOCK)"""
+        check(lib().rsac_debug_set(self._h, int(key), int(value)))
 
     def close(self):
         if self._h:

@@ -100,6 +100,20 @@ RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* a
  * experiments whose counts are wrong).  Counts, masks and models never depend on 0..34. */
 RSAC_EXPORT int rsac_set_score_variant(int variant);
 
+/* The pose refit (solvePnPRefineLM, main_v1.py:508-509) of a problem above 4096 points runs
+ * on several cooperating blocks that must be resident at once.  rsac_refit_blocks reports, for
+ * an n-point problem, the ranges of its summation order (lm_blocks) and the blocks that share
+ * them on this device (the co-resident limit; fewer blocks walk more ranges each, same order,
+ * same bits).  A refit whose blocks were not all resident returns RSAC_EHIP and keeps the
+ * RANSAC pose. */
+RSAC_EXPORT int rsac_refit_blocks(rsac_ctx *ctx, int32_t n, int32_t *ranges, int32_t *blocks);
+/* Test hooks, not for production use.  RSAC_DBG_REFIT_MAX_BLOCKS: cap the refit's
+ * cooperating blocks (0 = the device limit).  RSAC_DBG_REFIT_DROP_BLOCK (nonzero): launch one
+ * block fewer than the ranges' stride, so one range's sums never arrive. */
+#define RSAC_DBG_REFIT_MAX_BLOCKS 1
+#define RSAC_DBG_REFIT_DROP_BLOCK 2
+RSAC_EXPORT int rsac_debug_set(rsac_ctx *ctx, int32_t key, int64_t value);
+
 /* cv2.solvePnPRansac (main_v1.py:497).  K: 3x3 row-major f64.  Minimal
  * solver: P3P (Lambda Twist) on 4 points.  n_iters = iterationsCount cap,
  * reproj_thresh in px, confidence as in OpenCV.  Outputs R (3x3 row-major),

@@ -100,3 +100,26 @@ def test_host_homography_refit_matches_oracle_bitwise():
         H = rsac.homography_fit(src, dst, mask)
         Ho = O.hom_refine(O.soa_hom(src, dst), mask, np.eye(3))
         np.testing.assert_array_equal(H, Ho)
+
+
+def _lm_blocks(n):  # rsac_math.h lm_blocks (= oracle/rsac_oracle.c lm_blocks)
+    return 1 if n <= 4096 else min(64, -(-n // 1024))
+
+
+def _lm_chunk(n):  # rsac_math.h lm_chunk
+    nb = _lm_blocks(n)
+    return -(-n // nb)
+
+
+def test_refit_ranges_fit_one_tile_up_to_262144_points():
+    # k_pnp_refine stages a range's masked points once per refit when the range has at most
+    # kLmStage = 4096 indices: that holds for every n <= kLmMaxBlocks * kLmStage = 262144, and
+    # the tile-by-tile path is taken only above it.  Every range is non-empty.
+    for n in list(range(1, 70000, 7)) + list(range(262000, 262145)):
+        nb, c = _lm_blocks(n), _lm_chunk(n)
+        assert c <= 4096, n
+        assert (nb - 1) * c < n <= nb * c, n
+    assert _lm_chunk(262145) == 4097
+    assert (_lm_blocks(4097), _lm_chunk(4097)) == (5, 820)
+    assert (_lm_blocks(65536), _lm_chunk(65536)) == (64, 1024)
+    assert (_lm_blocks(65537), _lm_chunk(65537)) == (64, 1025)

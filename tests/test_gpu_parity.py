@@ -14,6 +14,7 @@ import pytest
 
 import pyoracle as O
 import rsac
+from rsac import _lib as L
 from rsac import synth
 
 pytestmark = pytest.mark.gpu
@@ -471,16 +472,67 @@ def test_speculative_first_round_falls_back(outl, refine):
     assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
 
 
-@pytest.mark.parametrize("n,outl", [(4096, 0.3), (4097, 0.6), (300000, 0.5)])
-def test_refit_block_ranges_bit_exact(n, outl):
-    # one range at 4096 points, two at 4097; 300000 points: 64 ranges of 4688 indices, each
-    # more than one LDS tile, so every pass re-stages its tiles (k_pnp_refine tile path)
-    pr = synth.pnp_problem(n, outl, seed=77)
-    R, t, m = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=True)
+def _refit_case(n, outl, seed=77):
+    pr = synth.pnp_problem(n, outl, seed=seed)
     ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 2000, 0x5EED)
-    np.testing.assert_array_equal(m, ref["mask"])
     soa = O.soa_pnp(pr["points3d"], pr["points2d"])
     Ro, to, _ = O.pnp_refine(soa, ref["mask"].astype(np.uint8), O.cam_from_K(pr["K"]), ref["R"], ref["t"])
+    return pr, ref, Ro, to
+
+
+@pytest.mark.parametrize("n,outl", [(4096, 0.3), (4097, 0.6), (65536, 0.5), (65537, 0.5), (300000, 0.5)])
+def test_refit_block_ranges_bit_exact(n, outl):
+    # one range at 4096 points, 5 ranges of 820 indices at 4097; 65536: 64 ranges of exactly
+    # 1024 (the block count saturates), 65537: 64 ranges of 1025 (still one tile each);
+    # 300000 points: 64 ranges of 4688 indices, each more than one LDS tile, so every pass
+    # re-stages its tiles (k_pnp_refine tile path)
+    pr, ref, Ro, to = _refit_case(n, outl)
+    ranges, _ = rsac.context().refit_blocks(n)
+    assert ranges == (1 if n <= 4096 else min(64, -(-n // 1024)))
+    R, t, m = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=True)
+    np.testing.assert_array_equal(m, ref["mask"])
+    assert _bits_equal(R, Ro) and _bits_equal(t, to)
+
+
+@pytest.mark.parametrize("cap", [1, 3, 7])
+@pytest.mark.parametrize("n", [20000, 65537, 300000])
+def test_refit_fewer_blocks_than_ranges_bit_exact(n, cap):
+    # a device that cannot hold lm_blocks(n) blocks at once: G = cap blocks walk the ranges
+    # x, x + G, ... each (staged once when their indices fit one tile, else tile by tile);
+    # the summation order, and so the pose, is unchanged
+    ctx = rsac.context()
+    pr, ref, Ro, to = _refit_case(n, 0.5)
+    try:
+        ctx.debug_set(L.DBG_REFIT_MAX_BLOCKS, cap)
+        ranges, blocks = ctx.refit_blocks(n)
+        assert blocks == min(cap, ranges)
+        R, t, m = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=True)
+        R2, t2, _, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0, refine=False,
+                                          lo=True, return_info=True)
+    finally:
+        ctx.debug_set(L.DBG_REFIT_MAX_BLOCKS, 0)
+    np.testing.assert_array_equal(m, ref["mask"])
+    assert _bits_equal(R, Ro) and _bits_equal(t, to)
+    lo = O.pnp_ransac_lo(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
+    assert info.lo_improvements == lo["lo_improvements"]
+    assert _bits_equal(R2, lo["R"]) and _bits_equal(t2, lo["t"])
+
+
+def test_refit_missing_block_raises():
+    # one block of the refit's stride is never launched (test hook): the others stop waiting
+    # after ~1 s, the call fails with EHIP instead of returning a pose from stale sums, and the
+    # context keeps working
+    ctx = rsac.context()
+    pr, ref, Ro, to = _refit_case(20000, 0.5)
+    try:
+        ctx.debug_set(L.DBG_REFIT_DROP_BLOCK, 1)
+        with pytest.raises(rsac.RsacError) as ei:
+            rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=True)
+        assert ei.value.code == L.EHIP and "resident" in str(ei.value)
+    finally:
+        ctx.debug_set(L.DBG_REFIT_DROP_BLOCK, 0)
+    R, t, m = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=True)
+    np.testing.assert_array_equal(m, ref["mask"])
     assert _bits_equal(R, Ro) and _bits_equal(t, to)
 
 
