@@ -431,7 +431,6 @@ LmScratch *lm_scratch(rsac_ctx *c, hipStream_t s) {
         c->lm.gran = (unsigned long long *)c->lmscr.p;
         c->lm.fail = c->h_lmfail.as<int32_t>();
         c->lm.launch = 0;
-        c->lm.max_blocks = 0;
     }
     if (c->lm.max_blocks == 0) {
         c->lm.max_blocks = pnp_refine_coresident(c->device);
@@ -1026,7 +1025,7 @@ void rsac_destroy(rsac_ctx *c) {
 }
 
 int rsac_set_score_variant(int variant) {
-    if (variant < -1 || (variant > 28 && (variant < 30 || variant > 37))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
+    if (variant < -1 || (variant > 28 && (variant < 30 || variant > 37) && (variant < 40 || variant > 48))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
     set_score_variant(variant);
     return RSAC_OK;
 }
@@ -1037,7 +1036,8 @@ int rsac_debug_set(rsac_ctx *c, int32_t key, int64_t value) {
     case RSAC_DBG_REFIT_MAX_BLOCKS:
         if (value < 0) return fail(RSAC_EINVAL, "bad block cap");
         c->dbg_refit_max_blocks = (int)std::min<int64_t>(value, kLmMaxBlocks);
-        c->lm.max_blocks = 0;  // recomputed by the next refit
+        c->lm.max_blocks = pnp_refine_coresident(c->device);
+        if (c->dbg_refit_max_blocks > 0) c->lm.max_blocks = std::min(c->lm.max_blocks, c->dbg_refit_max_blocks);
         return RSAC_OK;
     case RSAC_DBG_REFIT_DROP_BLOCK:
         c->lm.drop_block = value != 0;

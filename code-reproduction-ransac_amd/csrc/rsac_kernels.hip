@@ -1005,7 +1005,11 @@ __device__ __forceinline__ int ab_fallback(const PnpArgs &a, int prob, int64_t p
 // chunk) and the chunk's counts are atomically added into zeroed counts -- enough units to
 // fill the GPU when a round has only a few tiles (an adaptive run's first 256 hypotheses).
 // NZ: no depth-guard test (beta makes it redundant, band_consts): one compare fewer per pair.
-template <int P, int HB, int W = 4, bool NZ = false>  // W: minimum waves per SIMD the register budget must allow
+// LEAN: the hypothesis loop runs all HB staged records (the ones past the round are decided
+// outliers), keeps its counter in an SGPR, writes hypothesis h's tile count into lane h
+// (v_writelane) and its undecided flag into bit h of an SGPR mask: ~2 vector instructions per
+// hypothesis besides the pairs' 18, instead of ~10.
+template <int P, int HB, int W = 4, bool NZ = false, bool LEAN = false>  // W: minimum waves per SIMD the register budget must allow
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_ab(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int split) {
@@ -1077,6 +1081,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
                 // out-of-range lanes: a pixel at 3e38 makes the pair a decided outlier
                 pu[j] = in ? uu - cx : 3.0e38f;
                 pv[j] = in ? vv - cy : 3.0e38f;
+            }
+            if constexpr (LEAN) {
+                static_assert(NZ, "the lean loop has no depth-guard test");
+                int ccl = 0;        // lane h: hypothesis h's decided inliers of this tile
+                uint32_t wund = 0;  // bit h: hypothesis h has an undecided pair (wave-uniform)
+#pragma unroll 4
+                for (int h = 0; h < HB; ++h) {
+                    const float *m = mlds + h * kFModelStride;
+                    int cc = 0;
+                    uint64_t und = 0;
+#pragma unroll
+                    for (int j = 0; j < P; ++j) {
+                        const AbTest r = ab_test(m, px[j], py[j], pz[j], pu[j], pv[j]);
+                        const uint64_t mi = __ballot(r.lt);
+                        const uint64_t mo = __ballot(r.gt);
+                        cc += __popcll(mi);
+                        und |= ~(mi | mo);
+                    }
+                    // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
+                    // operands would exceed the constant bus); cc and h are SALU results: no hazard
+                    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
+                    wund |= und ? (1u << h) : 0u;
+                }
+                cnt += ccl;
+                if (__builtin_expect(wund != 0, 0))
+                    cnt += ab_fallback<P, NZ>(a, prob, p0, n, rec0, base, lane, wund, 0xFFFFFFFFu, mlds, px, py, pz,
+                                              pu, pv);
+                continue;
             }
             uint32_t undm = 0;  // bit h: this lane has an undecided pair with hypothesis h
             for (int h = 0; h < nh; ++h) {
@@ -2263,7 +2295,7 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
-constexpr int kDefaultScoreVariant = 25;  // fastest measured on MI355X
+constexpr int kDefaultScoreVariant = 48;  // fastest measured on MI355X
 static int g_score_variant = kDefaultScoreVariant;
 void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
 
@@ -2273,7 +2305,8 @@ void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant :
 template <int PP, int HB, int KIND = 0, int W = 4, bool NZ = false, bool BAL = false>
 static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
     auto kern = [] {
-        if constexpr (KIND == 3) return k_pnp_score_ab<PP, HB, W, NZ>;
+        if constexpr (KIND == 4) return k_pnp_score_ab<PP, HB, W, true, true>;
+        else if constexpr (KIND == 3) return k_pnp_score_ab<PP, HB, W, NZ>;
         else if constexpr (KIND == 2) return k_pnp_score_mfma<HB, PP>;
         else if constexpr (KIND == 1) return k_pnp_score_pk<PP, HB>;
         else return k_pnp_score_f32<PP, HB>;
@@ -2287,7 +2320,7 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
         resident = std::max(1, cus) * std::max(1, per_cu);
     }
     int64_t units = (int64_t)P * ((H + HB - 1) / HB);
-    if constexpr (KIND == 3) {
+    if constexpr (KIND == 3 || KIND == 4) {
         // few tiles and no fused best key: split the points too (counts accumulate atomically)
         int split = 1;
         const int64_t chunks = std::max<int64_t>(1, ((int64_t)a.max_n + 4 * 64 * PP - 1) / (4 * 64 * PP));
@@ -2447,6 +2480,9 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
                 // lane, so the point split gives 4x the units and the GPU fills
                 if ((int64_t)P * ((H + 31) / 32) <= small_round_tiles())
                     switch (small_round_pp()) {
+                        case 102: launch_f32<2, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
+                        case 105: launch_f32<2, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+                        case 104: launch_f32<4, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
                         case 4: launch_f32<4, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
                         case 8: launch_f32<8, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
                         case 1: launch_f32<1, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
@@ -2459,6 +2495,22 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 26: launch_f32<8, 32, 3, 5, false, true>(a, P, hyp_begin, H, counts, s); break;
             case 27: launch_f32<8, 32, 3, 5, true, false>(a, P, hyp_begin, H, counts, s); break;
             case 28: launch_f32<4, 32, 3, 6, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 48:
+                // default: the lean hypothesis loop (k_pnp_score_ab LEAN); small rounds (an adaptive
+                // run's first 256 hypotheses) with 2 points per lane so the point split fills the GPU
+                if ((int64_t)P * ((H + 31) / 32) <= small_round_tiles())
+                    launch_f32<2, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s);
+                else
+                    launch_f32<8, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s);
+                break;
+            case 40: launch_f32<8, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 41: launch_f32<4, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 42: launch_f32<8, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 43: launch_f32<6, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 44: launch_f32<8, 32, 4, 3, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 45: launch_f32<12, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 46: launch_f32<8, 16, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 47: launch_f32<6, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
             default: launch_f32<kScoreP, kScoreHB>(a, P, hyp_begin, H, counts, s); break;
         }
     } else

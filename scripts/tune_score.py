@@ -18,7 +18,7 @@ p2 = torch.from_numpy(pr["points2d"]).cuda()
 H = 100_000
 res = {v: [] for v in variants}
 keys = {}
-for rnd in range(6):
+for rnd in range(int(os.environ.get("ROUNDS", "6"))):
     for v in variants:
         L.check(L.lib().rsac_set_score_variant(v))
         key, model, info = rsac.evaluate_range(p2, p3, pr["K"], 0, H, 30.0, return_info=True)

@@ -248,7 +248,8 @@ def test_degenerate_inputs():
 # float32 pre-filter: must never change a decision (DESIGN.md "Scoring").  Every scoring-kernel
 # variant (VALU f32, packed f32, MFMA) is checked, then the default is restored.
 # ---------------------------------------------------------------------------------------------
-SCORE_VARIANTS = [0, 1, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 30, 31, 32, 33, 34]
+SCORE_VARIANTS = [0, 1, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 30, 31, 32, 33, 34,
+                  40, 41, 42, 43, 44, 45, 46, 47, 48]
 
 
 @pytest.fixture(params=SCORE_VARIANTS)
