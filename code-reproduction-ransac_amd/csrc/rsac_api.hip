@@ -136,8 +136,6 @@ struct rsac_ctx {
     double *d_cams = nullptr;
     float *d_thr2 = nullptr;
     DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
-    DevBuf pfeat, hmodels, mxlist;                             // MFMA scoring: f16 point features, records,
-                                                               // undecided-tile list (+ its counter)
     DevBuf loc;                                                // location search: inputs, pos2, H, err
     DevBuf lo;                                                 // LO-RANSAC: 2 model records, chain state, 2 masks
     const void *lo_state_base = nullptr;                       // the lo allocation whose LoState is zeroed
@@ -343,18 +341,6 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     float *C = c->centred.as<float>();
     int32_t max_n = 0;
     for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
-    uint4 *PF = nullptr;
-    // MFMA scoring: the undecided-tile list is sized for the worst case (every wave-tile of every
-    // problem, 8-hypothesis tiles), so it cannot overflow; past 4 GB the f32 kernel is used instead
-    int64_t list_cap = (int64_t)P * ((std::max<int64_t>(stride, 1) + 7) / 8) * ((max_n + 31) / 32);
-    const bool mx = !a.exact_only && score_variant_mx() && max_n > kLanePts &&
-                    list_cap * (int64_t)sizeof(MxUndecided) <= (4ll << 30) && list_cap < (1ll << 31) - 64;
-    if (mx) {
-        HIPCHK(c->pfeat.ensure(sizeof(uint4) * std::max<int64_t>(N, 1)));
-        HIPCHK(c->hmodels.ensure(sizeof(float) * kHModelStride * (size_t)P * (size_t)std::max<int64_t>(stride, 1)));
-        HIPCHK(c->mxlist.ensure(64 + sizeof(MxUndecided) * (size_t)list_cap));
-        PF = c->pfeat.as<uint4>();
-    }
     // resets best_key and the queue, then builds the frame (also in exact mode: cheap)
     // one problem: k_pnp_setup_fc's scratch (its ticket starts at 0; the kernel resets it)
     PnpPrepare prep = st.prep;
@@ -367,20 +353,14 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
         prep.part = (float *)(c->setup_scr.as<char>() + 64);
     }
     HIPCHK(launch_pnp_frame(a, P, max_n, c->bounds_ws.as<int32_t>(), C, C + N, C + 2 * N, c->frame.as<double>(),
-                            c->fconst.as<float>(), s, PF, &prep));
+                            c->fconst.as<float>(), s, &prep));
     if (!a.exact_only) {
         a.counts_out = c->counts.as<int32_t>();
         a.XC = C; a.YC = C + N; a.ZC = C + 2 * N;
         a.frame = c->frame.as<double>();
         a.fconst = c->fconst.as<float>();
         a.fmodels = c->fmodels.as<float>();
-        if (mx) {
-            a.PF = PF;
-            a.hmodels = c->hmodels.as<float>();
-            a.mx_count = c->mxlist.as<int>();
-            a.mx_list = (MxUndecided *)(c->mxlist.as<char>() + 64);
-            a.mx_cap = (int)list_cap;
-        }
+        a.fform = score_record_form();
     }
     return RSAC_OK;
 }
@@ -1008,7 +988,7 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->pfeat, &c->hmodels, &c->mxlist, &c->lmscr, &c->setup_scr, &c->scanrec};
+                     &c->epnp, &c->lmscr, &c->setup_scr, &c->scanrec};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_lmfail, &c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,
@@ -1025,7 +1005,7 @@ void rsac_destroy(rsac_ctx *c) {
 }
 
 int rsac_set_score_variant(int variant) {
-    if (variant < -1 || (variant > 28 && (variant < 30 || variant > 37) && (variant < 40 || variant > 48))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
+    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 52))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
     set_score_variant(variant);
     return RSAC_OK;
 }

@@ -37,15 +37,6 @@ struct PnpArgs {
     const double *frame;  // P x kFrameStride: c0 c1 c2 B rho cmax wmax
     const float *fconst;  // P x kFconstStride
     float *fmodels;       // P x hyp_stride x kFModelStride
-    // MFMA scoring kernel (k_pnp_score_mx): f16 hi/lo point features (8 x f16 per point,
-    // built by k_pnp_center) and per-hypothesis MFMA records (kHModelStride floats);
-    // both nullptr unless an MFMA scoring variant is selected
-    const uint4 *PF;
-    float *hmodels;
-    struct MxUndecided *mx_list;   // tiles with undecided pairs, recounted by k_pnp_mx_fallback
-    int *mx_count;                 // records written (reset by the solve / fmodels kernels)
-    int mx_cap;
-    unsigned long long *mx_stats;  // diagnostics (RSAC_MX_STATS=1): fallback tiles, undecided pairs
     // set when the solve kernel precedes the scoring launch: the solve zeroes these counts, so a
     // split scoring launch (atomic count accumulation) needs no memset
     int32_t *counts_out;
@@ -55,22 +46,12 @@ struct PnpArgs {
     unsigned long long *best_key;
     int *queue;  // work-queue counter of the f32 scoring kernel (reset by launch_pnp_frame)
     int32_t max_n;  // largest problem (points); small problems score one lane per hypothesis
+    int fform = 0;  // f32 record form: 0 write_fmodel, 1 the scaled form of k_pnp_score_sc
 };
 
 constexpr int kFrameStride = 8;
 constexpr int kFconstStride = 16;
 constexpr int kFModelStride = 16;
-constexpr int kHModelStride = 32;
-constexpr int kMxMasks = 16;  // undecided masks per record: NT x 4 (NT <= 4)
-
-// one wave-tile of k_pnp_score_mx with undecided pairs: hypotheses rec + [0, nh) (the wave's),
-// points base + (lane & 31) (< n), mask m[4t + j]: lanes whose pair with hypothesis 8t + 2j +
-// (lane >> 5) is undecided
-struct MxUndecided {
-    int64_t rec;
-    int32_t prob, base, n, nh;
-    uint64_t m[kMxMasks];
-};
 
 struct HomArgs {
     const float *SX, *SY, *DX, *DY;
@@ -153,7 +134,7 @@ struct PnpPrepare {
 };
 constexpr int kSetupMaxBlocks = 256;
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *bounds_ws, float *XC, float *YC,
-                            float *ZC, double *frame, float *fconst, hipStream_t s, uint4 *PF = nullptr,
+                            float *ZC, double *frame, float *fconst, hipStream_t s,
                             const PnpPrepare *prep = nullptr);
 // f32 records for H given f64 models (rsac_score_poses / rsac_pnp_mask)
 hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_t s);
@@ -164,7 +145,7 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 // solve / score hypotheses [hyp_begin, hyp_begin + H) of every problem
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
 void set_score_variant(int v);  // tuning knob (rsac_set_score_variant)
-bool score_variant_mx();        // the selected variant is an MFMA one (needs PF + hmodels)
+int score_record_form();        // f32 record form the selected variant reads (PnpArgs::fform)
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,

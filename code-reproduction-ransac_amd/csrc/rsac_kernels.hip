@@ -105,51 +105,6 @@ __global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *_
     }
 }
 
-// f16 hi + lo operands of the MFMA scoring path (write_hmodel has the error model)
-constexpr double kMxF1 = 4096.0;               // the constant feature (exact in f16)
-constexpr double kMxEps = 3.814697265625e-06;  // 2^-18
-constexpr float kMxFlush = 6.103515625e-05f;   // 2^-14, smallest normal f16
-
-// scale of the z row, fz = 2^k with fz <= fx < 2 fz: the three rows (-fx R0, -fy R1, fz R2) then
-// share one magnitude, so one per-hypothesis scale fits all of them into f16 (fconst[8] = 1 / fz
-// rescales the pixel offsets: q1 = (uc / fz) (fz z) + xs, all powers of 2, bit-identical rounding)
-__host__ __device__ __forceinline__ double mx_zscale(double fx) {
-    int e = 0;
-    (void)frexp(fx > 0 ? fx : 1.0, &e);
-    return ldexp(1.0, e - 1);
-}
-
-// feature scale fs = 2^-b with B fs < 2^13 (B bounds |XC|)
-__host__ __device__ __forceinline__ double mx_feature_scale(double B) {
-    int e = 0;
-    (void)frexp(B > 0 ? B : 1.0, &e);  // B < 2^e
-    return ldexp(1.0, 13 - e);
-}
-
-__device__ __forceinline__ void mx_split(float v, _Float16 &hi, _Float16 &lo) {
-    if (!(__builtin_fabsf(v) >= kMxFlush)) {  // tiny (or NaN: the caller never passes one)
-        hi = (_Float16)0.f;
-        lo = (_Float16)0.f;
-        return;
-    }
-    hi = (_Float16)v;
-    const float r = v - (float)hi;  // exact
-    lo = __builtin_fabsf(r) >= kMxFlush ? (_Float16)r : (_Float16)0.f;
-}
-
-// B-operand column of a point: Xh Yh Zh F1 Xl Yl Zl 0 (both lane halves read the same 16 B)
-__device__ __forceinline__ uint4 mx_point_features(float x, float y, float z) {
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-    h8 f;
-    _Float16 hi, lo;
-    mx_split(x, hi, lo); f[0] = hi; f[4] = lo;
-    mx_split(y, hi, lo); f[1] = hi; f[5] = lo;
-    mx_split(z, hi, lo); f[2] = hi; f[6] = lo;
-    f[3] = (_Float16)(float)kMxF1;
-    f[7] = (_Float16)0.f;
-    return __builtin_bit_cast(uint4, f);
-}
-
 // B >= |XC|inf of problem prob (the frame's f[3]; recomputed identically wherever needed)
 __device__ __forceinline__ double frame_bound(const int *__restrict__ ws, int32_t P, int prob, int n) {
     double B = 0;
@@ -243,8 +198,9 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
     q[6] = (float)(4e-6 * T + 1e-30);
     // Cmax >= C_i = 2.5u (|u_i - cx| + |v_i - cy| + |cx| + |cy| + 2 thr + 2), the rounding part of D
     q[7] = (float)(2.5 * kU32 * (du + dv + fabs(cx) + fabs(cy) + 2.0 * thr + 3.0) + 1e-6);
-    q[8] = (float)(1.0 / mx_zscale(fx));  // the MFMA kernel's pixel-offset scale
-    q[9] = q[10] = q[11] = q[12] = 0.f;
+    q[8] = 0.f;
+    q[9] = (T > 1e-12 && T < 1e30) ? (float)(1.0 / thr) : 1.f;  // k_pnp_score_sc: u' = (u - cx) / sqrt(T)
+    q[10] = q[11] = q[12] = 0.f;
     for (int k = 13; k < kFconstStride; ++k) q[k] = 0.f;
 }
 
@@ -254,7 +210,7 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
 __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const int *__restrict__ ws,
                                                     double *__restrict__ frame, float *__restrict__ fconst,
                                                     float *__restrict__ XC, float *__restrict__ YC,
-                                                    float *__restrict__ ZC, uint4 *__restrict__ PF) {
+                                                    float *__restrict__ ZC) {
     const int prob = blockIdx.y;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
@@ -264,7 +220,6 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const 
         for (int k = 0; k < 3; ++k)
             cc[k] = ((double)ord2f(ws[5 * prob + k]) + (double)ord2f(ws[5 * P + 5 * prob + k])) * 0.5;
     const double c0 = cc[0], c1 = cc[1], c2 = cc[2];
-    const float fs = PF ? (float)mx_feature_scale(frame_bound(ws, P, prob, n)) : 0.f;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int64_t q = p0 + i;
         const float xc = (float)((double)a.X[q] - c0), yc = (float)((double)a.Y[q] - c1),
@@ -272,7 +227,6 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const 
         XC[q] = xc;
         YC[q] = yc;
         ZC[q] = zc;
-        if (PF) PF[q] = mx_point_features(xc * fs, yc * fs, zc * fs);  // power-of-2 scale: exact
     }
 }
 
@@ -285,7 +239,7 @@ __global__ __launch_bounds__(1024) void k_pnp_setup1(const double *__restrict__ 
                                                      float *__restrict__ V, int *__restrict__ ws,
                                                      double *__restrict__ frame, float *__restrict__ fconst,
                                                      float *__restrict__ XC, float *__restrict__ YC,
-                                                     float *__restrict__ ZC, uint4 *__restrict__ PF) {
+                                                     float *__restrict__ ZC) {
     __shared__ float sl[16][5], sh[16][5];
     __shared__ int wsl[10];
     const int n = (int)(a.offsets[1] - a.offsets[0]);  // offsets[0] = 0 (one problem)
@@ -331,14 +285,12 @@ __global__ __launch_bounds__(1024) void k_pnp_setup1(const double *__restrict__ 
     double cc[3] = {0, 0, 0};
     if (n > 0)
         for (int k = 0; k < 3; ++k) cc[k] = ((double)ord2f(wsl[k]) + (double)ord2f(wsl[5 + k])) * 0.5;
-    const float fs = PF ? (float)mx_feature_scale(frame_bound(wsl, 1, 0, n)) : 0.f;
     for (int i = threadIdx.x; i < n; i += 1024) {  // this thread's own stores above: visible
         const float xc = (float)((double)X[i] - cc[0]), yc = (float)((double)Y[i] - cc[1]),
                     zc = (float)((double)Z[i] - cc[2]);
         XC[i] = xc;
         YC[i] = yc;
         ZC[i] = zc;
-        if (PF) PF[i] = mx_point_features(xc * fs, yc * fs, zc * fs);
     }
 }
 
@@ -487,8 +439,15 @@ __device__ __forceinline__ BandConsts band_consts(const double (&eps)[3], double
 // with t' = R c + t.  ex, ey bound |xs' - fx x|/fx, |ys' - fy y|/fy and ez |z' - z| (camera
 // frame, f32 evaluation vs real numbers); Dz0 is the hypothesis' part of D |z|; zg is the
 // depth guard (< 0: no model).
+__device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t, bool valid, const double *frame,
+                                                const double *cam, const float *fconst, float *fm);
+
 __device__ __forceinline__ void write_fmodel(const double *R, const double *t, bool valid, const double *frame,
-                                             const double *cam, const float *fconst, float *fm) {
+                                             const double *cam, const float *fconst, float *fm, int form = 0) {
+    if (form == 1) {
+        write_fmodel_sc(R, t, valid, frame, cam, fconst, fm);
+        return;
+    }
     if (!valid) {
 #pragma unroll
         for (int q = 0; q < kFModelStride; ++q) fm[q] = 0.f;
@@ -515,111 +474,77 @@ __device__ __forceinline__ void write_fmodel(const double *R, const double *t, b
     fm[15] = (float)b.alpha;
 }
 
-// ---------------------------------------------------------------------------
-// MFMA record (k_pnp_score_mx): the camera-frame coordinates (xs, ys, fz z) of
-// a pair are one v_mfma_f32_32x32x16_f16 output each.  Coefficients c (rows
-// -fx R0, -fy R1, fz R2 with t', per-hypothesis scale S = 2^g) and point features f (XC YC ZC
-// times fs = 2^-b, and the constant F1 = 2^12) are split into f16 hi + lo, and
-// K = 16 carries the four products hi*hi, hi*lo, lo*hi, lo*lo:
-//   A row (hyp, quantity r), lane half 0: c0h c1h c2h c3h c0h c1h c2h 0
-//                            lane half 1: c0l c1l c2l c3l c0l c1l c2l 0
-//   B column (point), both halves:        Xh  Yh  Zh  F1  Xl  Yl  Zl  0
-// so the output is sum_k (c_kh + c_kl)(f_kh + f_kl) in f32: S x the exact
-// coordinate up to the split (<= 2^-22 relative per operand + 2^-14 absolute:
-// pieces below the f16 normal range are flushed), the f32 rounding of the
-// record (2^-24) and the MFMA's f32 accumulation (<= 16 roundings, counted at
-// 2^-23 each).  eps = 2^-18 (r1 B + |t'|) + 3 / (S |sc|) bounds all of it; the
-// rest of the band (alpha, beta, zg) is the f32 kernel's, with the scale
-// folded in (the test is homogeneous: beta * S^2, zg * S fz, (T -+ alpha) / fz^2).
-// Record (32 floats): [0..24) the three A rows (2 halves x 8 f16 each),
-// 24 (T - alpha) / fz^2, 25 beta S^2, 26 (T + alpha) / fz^2, 27 zg S fz (not
-// tested: beta makes the depth guard redundant, band_consts), 28..31 unused.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void write_hmodel(const double *R, const double *t, bool valid, const double *frame,
-                                             const double *cam, const float *fconst, float *hm) {
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-    h8 rows[6];
+// Scaled record (k_pnp_score_sc, DESIGN.md "Scoring: scaled form").  The z row is multiplied
+// by s = sqrt(T) and the kernel's pixel offsets by 1/s (u' = (u - cx) / s), so that
+//   q1 = u' z' + xs,  q2 = v' z' + ys,  D = q1^2 + q2^2 - z'^2   (z' = s z)
+// has the sign of e - T with no T z^2 term, and the band is linear in |z'|: a pair is decided
+// when |D| - a |z'| > b.  Bound (zeta = z' / s, the computed depth in z units): the f32 kernel's
+//   Mz = (2.002 s |zeta| + Dz) Dz + Trel' zeta^2,  Dz = D0 + C' |zeta|,
+// with C' = 2 Cmax (u' carries three roundings instead of one) and Trel' = Trel + 1e-6 T (the
+// rounding of D itself), and zeta^2 <= Zeta |zeta| for |zeta| <= Zeta = (r1 B + |t'z|) + ez, the
+// largest depth of any point of the problem.  b also covers the depth guard (b >= K and
+// b >= T zg^2: an inlier verdict implies |zeta| > zg; for |zeta| <= zg an outlier verdict
+// implies |q| > sqrt(T) |z|), as band_consts does for beta.
+//   { -fx R0 -fx R1 -fx R2 | -fy R3 -fy R4 -fy R5 | s R6 s R7 s R8 | -fx t'x -fy t'y s t'z | a b zg 0 }
+// b = +inf (every pair recounted exactly) when T or the coordinate magnitudes leave the range
+// where the f32 evaluation cannot overflow.
+__device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t, bool valid, const double *frame,
+                                                const double *cam, const float *fconst, float *fm) {
+    if (!valid) {  // already the kernel's decided-outlier form: z' = 0, xs = 1 (D = 1), b = -inf
 #pragma unroll
-    for (int q = 0; q < 6; ++q) rows[q] = h8{0, 0, 0, 0, 0, 0, 0, 0};
-    float4 cst;
+        for (int q = 0; q < kFModelStride; ++q) fm[q] = 0.f;
+        fm[9] = 1.f;
+        fm[13] = -__builtin_inff();
+        fm[14] = -1.f;
+        return;
+    }
     const double B = frame[3], rho = frame[4], cmax = frame[5], wmax = frame[6];
-    const double fs = mx_feature_scale(B);
     const double fx = fabs(cam[0]), fy = fabs(cam[1]);
-    const double fz = mx_zscale(fx);
-    const double sc[3] = {-cam[0], -cam[1], fz};
-    double c[3][4], tp[3], r1[3], m = 0.0;
-    bool finite = valid;
-    if (valid) {
+    const double T = fconst[4];
+    const bool t_ok = T > 1e-12 && T < 1e30;
+    const double s = t_ok ? sqrt(T) : 1.0;
+    const double sc[3] = {-cam[0], -cam[1], s};
+    double eps[3], mag[3];
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            tp[r] = R[3 * r] * frame[0] + R[3 * r + 1] * frame[1] + R[3 * r + 2] * frame[2] + t[r];
-            r1[r] = fabs(R[3 * r]) + fabs(R[3 * r + 1]) + fabs(R[3 * r + 2]);
+    for (int r = 0; r < 3; ++r) {
+        const double tp = R[3 * r] * frame[0] + R[3 * r + 1] * frame[1] + R[3 * r + 2] * frame[2] + t[r];
+        const double r1 = fabs(R[3 * r]) + fabs(R[3 * r + 1]) + fabs(R[3 * r + 2]);
+        eps[r] = 8.0 * kU32 * (r1 * B + fabs(tp)) + r1 * rho + 4e-15 * (r1 * cmax + fabs(t[r]));
+        mag[r] = r1 * B + fabs(tp);  // bound on |camera-frame coordinate r| over the problem
 #pragma unroll
-            for (int k = 0; k < 3; ++k) c[r][k] = sc[r] * R[3 * r + k] / fs;
-            c[r][3] = sc[r] * tp[r] / kMxF1;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) m = fmax(m, fabs(c[r][k]));
-            finite = finite && isfinite(tp[r]) && isfinite(r1[r]);
-        }
-        finite = finite && isfinite(m);
+        for (int q = 0; q < 3; ++q) fm[3 * r + q] = (float)(sc[r] * R[3 * r + q]);
+        fm[9 + r] = (float)(sc[r] * tp);
     }
-    if (!valid) {
-        // decided outlier everywhere: z = F1 > 0, thresholds -inf
-        rows[4][3] = (_Float16)1.f;
-        cst = make_float4(-__builtin_inff(), 0.f, -__builtin_inff(), -1.f);
-    } else if (!finite) {
-        // every pair undecided (z = 0: E < -inf and E > NaN never hold): the exact f64 test decides
-        cst = make_float4(-__builtin_inff(), 0.f, __builtin_inff(), __builtin_inff());
-    } else {
-        int e = 0;
-        (void)frexp(m > 0 ? m : 1.0, &e);
-        const double S = ldexp(1.0, 12 - e);  // m S < 2^12
-        double eps[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                _Float16 hi, lo;
-                mx_split((float)(c[r][k] * S), hi, lo);
-                rows[2 * r][k] = hi;
-                rows[2 * r + 1][k] = lo;
-                if (k < 3) {
-                    rows[2 * r][4 + k] = hi;
-                    rows[2 * r + 1][4 + k] = lo;
-                }
-            }
-            eps[r] = kMxEps * (r1[r] * B + fabs(tp[r])) + 3.0 / (S * fabs(sc[r])) + r1[r] * rho +
-                     4e-15 * (r1[r] * cmax + fabs(t[r]));
-        }
-        const BandConsts b = band_consts(eps, fx, fy, wmax, tp[2], fconst);
-        const double T = fconst[4];
-        const double lo_c = T - b.alpha, hi_c = T + b.alpha;
-        const double ifz2 = 1.0 / (fz * fz);  // z' = fz S z: z'^2 carries fz^2
-        cst = make_float4((float)((lo_c - 1e-6 * fabs(lo_c)) * ifz2), (float)(b.beta * S * S * (1.0 + 1e-6)),
-                          (float)(hi_c * (1.0 + 1e-6) * ifz2), (float)(b.zg * S * fz * (1.0 + 1e-6)));
-    }
-    h8 *o = reinterpret_cast<h8 *>(hm);
-#pragma unroll
-    for (int q = 0; q < 6; ++q) o[q] = rows[q];
-    reinterpret_cast<float4 *>(hm)[6] = cst;
-    reinterpret_cast<float4 *>(hm)[7] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const double D0 = 1.01 * (fx * eps[0] + fy * eps[1] + eps[2] * (fx + fy) * wmax);
+    const double zg = 100.0 * (fmax(eps[0], eps[1]) + wmax * eps[2]) + 2.02 * eps[2] + 1e-30;
+    const double Cp = 2.0 * (double)fconst[7], Trelp = (double)fconst[6] + 1e-6 * T;
+    const double c1 = Cp / s;                     // Dz = D0 + c1 |z'|
+    const double Zp = s * (mag[2] + eps[2]) * (1.0 + 1e-6);  // >= |z'| of every point
+    double a = 1.01 * (D0 * (2.002 + 2.0 * c1) + (c1 * (2.002 + c1) + Trelp / T) * Zp);
+    double b = 1.01 * D0 * D0;
+    const double zr = zg + eps[2];
+    const double Kq = D0 + Cp * zr + sqrt(T * 1.00001) * zr;
+    b = fmax(b, (1.0 + 1e-6) * Kq * Kq);
+    b = fmax(b, T * zg * zg * (1.0 + 1e-5));
+    // q, z' and D stay far below the f32 range: |q| <= fx|x| + fy|y| + |u - cx| |z| (+ the band)
+    const double umax = (double)fconst[7] / (2.5 * kU32);  // >= |u - cx| + |v - cy| (pnp_frame_one)
+    const double qmax = fx * mag[0] + fy * mag[1] + umax * (mag[2] + eps[2]) + D0;
+    const bool fits = t_ok && qmax < 1e17 && Zp < 1e17 && a * Zp < 1e30 && b < 1e30;
+    fm[12] = fits ? (float)a : 0.f;
+    fm[13] = fits ? (float)b : __builtin_inff();
+    fm[14] = (float)zg;
+    fm[15] = 0.f;
 }
 
 __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
     const int prob = blockIdx.y;
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
-    if (h == 0 && prob == 0) {  // the scoring launch that follows starts its queue (and fallback list) at 0
-        if (a.queue) *a.queue = 0;
-        if (a.mx_count) *a.mx_count = 0;
-    }
+    if (h == 0 && prob == 0 && a.queue) *a.queue = 0;  // the scoring launch that follows starts its queue at 0
     if (h >= H) return;
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
     const double *m = a.models + rec * kModelStride;
     write_fmodel(m, m + 9, m[kValidSlot] != 0.0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                 a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride);
-    if (a.hmodels)
-        write_hmodel(m, m + 9, m[kValidSlot] != 0.0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                     a.fconst + (int64_t)prob * kFconstStride, a.hmodels + rec * kHModelStride);
+                 a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
 }
 
 // ---------------------------------------------------------------------------
@@ -631,7 +556,6 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     // every round's scoring launch follows a solve on the same stream: reset its work queue here
     if (hl == 0 && prob == 0) {
         if (a.queue) *a.queue = 0;
-        if (a.mx_count) *a.mx_count = 0;
     }
     if (hl >= H) return;
     const int64_t h = hyp_begin + hl;
@@ -669,12 +593,9 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     m[kValidSlot] = st > 0 ? 1.0 : 0.0;
     a.status[rec] = st;
     if (a.counts_out) a.counts_out[rec] = 0;  // the scoring launch that follows may accumulate
-    if (a.hmodels)  // the MFMA scoring kernel reads only these
-        write_hmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                     a.fconst + (int64_t)prob * kFconstStride, a.hmodels + rec * kHModelStride);
-    else if (a.fmodels)
+    if (a.fmodels)
         write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride);
+                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
 }
 
 // Small rounds (an adaptive run's first 256 hypotheses: one block, every lane's latency is the
@@ -689,7 +610,6 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
     const int hl = gt >> 2, cand = gt & 3;
     if (gt == 0 && prob == 0) {
         if (a.queue) *a.queue = 0;
-        if (a.mx_count) *a.mx_count = 0;
     }
     const bool live = hl < H;  // the 4 lanes of a hypothesis share it: shuffles stay in the group
     const int64_t h = hyp_begin + hl;
@@ -770,12 +690,9 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
     m[kValidSlot] = sv > 0 ? 1.0 : 0.0;
     a.status[rec] = sv;
     if (a.counts_out) a.counts_out[rec] = 0;
-    if (a.hmodels)
-        write_hmodel(R, t, sv > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                     a.fconst + (int64_t)prob * kFconstStride, a.hmodels + rec * kHModelStride);
-    else if (a.fmodels)
+    if (a.fmodels)
         write_fmodel(R, t, sv > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride);
+                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
 }
 
 // ---------------------------------------------------------------------------
@@ -1155,81 +1072,82 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
 }
 
 // ---------------------------------------------------------------------------
-// MFMA scoring kernel.  The camera-frame coordinates (xs, ys, z) of 8
-// hypotheses x 32 points come out of one v_mfma_f32_32x32x16_f16 (record and
-// error model: write_hmodel); the VALU does the rest of the alpha-beta test of
-// k_pnp_score_ab, 10 operations per pair instead of 19.
-//   C/D map (gfx950): column = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
-//   row 8j + 4h + q  <->  hypothesis 2j + h of the tile, quantity q (xs ys z, 3 unused)
-// so lane (column c, half h) holds xs ys z of hypothesis 2j + h at point c in
-// registers 4j .. 4j + 2: 4 hypotheses x 1 point per lane and MFMA.
-// A unit is (HB = 32 NT hypotheses, a chunk of the points).  Wave w owns NT
-// tiles (8 NT hypotheses; their A operands and band constants stay in
-// registers) and runs every 32-point tile of the chunk, so the 4 waves of a
-// block read the same points (L1 reuse) and need no count reduction.  Counts
-// are ballot popcounts (scalar unit); undecided pairs (the band, |z| <= zg,
-// NaN) are recounted with the exact f64 error after the tile, as in
-// k_pnp_score_ab, so counts equal the exact kernel's bit for bit.
+// Scaled-form scoring kernel (records of write_fmodel_sc).  Per (hypothesis, point) pair:
+//   xs, ys, z' = record rows . (XC, YC, ZC) + t'        9 FMA
+//   q1 = u' z' + xs, q2 = v' z' + ys                    2 FMA  (u' = (u - cx) / sqrt(T))
+//   D = q1^2 + q2^2 - z'^2                              3      (sign of e - T)
+//   t = |D| - a |z'|                                    1 FMA  (abs source modifiers)
+//   inlier count: ballot(D < 0)                         1 compare
+//   undecided: min3 of the t's over the lane's points   1/2 per pair, then one compare per
+//                                                      hypothesis: !(min t > b)
+// 16.5 vector instructions per pair against 18 for k_pnp_score_ab.  The fast count takes D < 0
+// for every pair; for a hypothesis with an undecided pair on the tile, sc_fallback recomputes
+// the tile's pairs (same operations, same bits) and replaces the fast verdict of each undecided
+// pair by the exact f64 test.  Points with a non-finite coordinate are staged as decided
+// outliers (the exact test says outlier for them: NaN / inf error), so D is never NaN.
 // ---------------------------------------------------------------------------
-typedef _Float16 mx_h8 __attribute__((ext_vector_type(8)));
-typedef float mx_f16 __attribute__((ext_vector_type(16)));
-
-// the test of one pair from an MFMA output (registers 4 jj .. 4 jj + 2: xs ys fz z, scaled):
-// E < lo decided inlier, E > hi decided outlier (no depth guard: beta covers it, band_consts);
-// a NaN anywhere leaves the pair undecided
-struct MxTest {
-    bool lt, gt;
+struct ScPair {
+    float D, t;
 };
-__device__ __forceinline__ MxTest mx_test(const mx_f16 &acc, int jj, float4 k, float uc, float vc) {
-    const float xs = acc[4 * jj], ys = acc[4 * jj + 1], z = acc[4 * jj + 2];
-    const float q1 = __builtin_fmaf(uc, z, xs);
-    const float q2 = __builtin_fmaf(vc, z, ys);
-    const float z2 = z * z;
-    const float E = __builtin_fmaf(q1, q1, q2 * q2);
-    const float lo = __builtin_fmaf(k.x, z2, -k.y);
-    const float hi = __builtin_fmaf(k.z, z2, k.y);
-    return MxTest{E < lo, E > hi};
+
+__device__ __forceinline__ ScPair sc_pair(const float *m, float x, float y, float zc, float u, float v) {
+    const float xs = __builtin_fmaf(m[0], x, __builtin_fmaf(m[1], y, __builtin_fmaf(m[2], zc, m[9])));
+    const float ys = __builtin_fmaf(m[3], x, __builtin_fmaf(m[4], y, __builtin_fmaf(m[5], zc, m[10])));
+    const float z = __builtin_fmaf(m[6], x, __builtin_fmaf(m[7], y, __builtin_fmaf(m[8], zc, m[11])));
+    const float q1 = __builtin_fmaf(u, z, xs);
+    const float q2 = __builtin_fmaf(v, z, ys);
+    const float D = __builtin_fmaf(-z, z, __builtin_fmaf(q1, q1, q2 * q2));
+    const float tt = __builtin_fmaf(-m[12], __builtin_fabsf(z), __builtin_fabsf(D));
+    return ScPair{D, tt};
 }
 
-// the wave's A operands (this lane supplies row `col` of every tile: hypothesis 2j + hh, quantity
-// q; lane half = the hi (0) or lo (1) pieces) and band constants; hypotheses past nh are
-// decided outliers
-template <int NT>
-__device__ __forceinline__ void mx_load_operands(const float *__restrict__ hm, int hw0, int nh, int col, int half,
-                                                 mx_h8 (&A)[NT], float4 (&cs)[NT][4]) {
-    const int j = col >> 3, hh = (col >> 2) & 1, q = col & 3;
+// exact recount of the undecided pairs of the flagged hypotheses (wund) on this lane's points:
+// returns this lane's share of the count corrections (lane h: hypothesis h's)
+template <int P>
+__device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p0, int n, int64_t rec0, int base,
+                                           int lane, uint32_t wund, const float *mlds, const float (&px)[P],
+                                           const float (&py)[P], const float (&pz)[P], const float (&pu)[P],
+                                           const float (&pv)[P]) {
+    const double *cm = a.cams + 4 * prob;
+    const Cam k{cm[0], cm[1], cm[2], cm[3]};
+    const float thr2 = a.thr2[prob];
+    int cnt = 0;
+#pragma unroll 1
+    while (wund) {
+        const int h = __builtin_ctz(wund);
+        wund &= wund - 1;
+        const float *m = mlds + h * kFModelStride;
+        const double *md = a.models + (rec0 + h) * kModelStride;
+        int cc = 0;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int hl = hw0 + t * 8 + 2 * j + hh;
-        mx_h8 v = mx_h8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (q < 3 && hl < nh)
-            v = *reinterpret_cast<const mx_h8 *>(hm + hl * kHModelStride + q * 8 + half * 4);
-        else if (q == 2 && half == 0)
-            v[3] = (_Float16)1.f;  // z = F1 > 0
-        A[t] = v;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int hc = hw0 + t * 8 + 2 * jj + half;
-            cs[t][jj] = hc < nh ? *reinterpret_cast<const float4 *>(hm + hc * kHModelStride + 24)
-                                : make_float4(-__builtin_inff(), 0.f, -__builtin_inff(), -1.f);
+        for (int j = 0; j < P; ++j) {
+            const int i = base + j * 64 + lane;
+            const ScPair r = sc_pair(m, px[j], py[j], pz[j], pu[j], pv[j]);
+            const bool und = !(r.t > m[13]);
+            bool ex = false;
+            if (und && i < n) {
+                const int64_t q = p0 + i;
+                ex = md[kValidSlot] != 0.0 &&
+                     pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <= thr2;
+            }
+            cc += __popcll(__ballot(und && ex)) - __popcll(__ballot(und && r.D < 0.f));
         }
+        cnt += (lane == h) ? cc : 0;
     }
+    return cnt;
 }
 
-// CV: 0 inlier counts by ballot popcounts, 1 per-lane counts (VGPR), 2 per-lane counts and
-// all-VALU undecided detection; PD: tiles of point loads in flight
-template <int NT, int W, int CV, int PD, int EXP = 0>  // EXP != 0: timing experiments only (wrong counts)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_mx(
+template <int P, int HB, int W = 4>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_sc(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int split) {
-    static_assert(NT * 4 <= kMxMasks, "undecided-tile record");
-    constexpr int HW = 8 * NT;  // hypotheses per wave
-    constexpr int HB = 4 * HW;  // per unit
+    static_assert(HB <= 32, "undecided bits per wave");
+    constexpr int kStride = 4 * 64 * P;  // points one pass of the block covers
+    __shared__ int red[4][HB];
     __shared__ int unit_s;
-    __shared__ int scnt[HB];
+    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int col = lane & 31, half = lane >> 5;
     const int tiles_per_prob = (H + HB - 1) / HB;
     const int units_per_prob = tiles_per_prob * split;
     const int n_units = units_per_prob * n_prob;
@@ -1245,221 +1163,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
         const int64_t p0 = a.offsets[prob];
         const int n_all = (int)(a.offsets[prob + 1] - p0);
-        const int clen = ((n_all + split - 1) / split + 31) / 32 * 32;
+        const int clen = ((n_all + split - 1) / split + kStride - 1) / kStride * kStride;
         const int start = chunk * clen;
         const int n = min(n_all, start + clen);  // this unit's points: [start, n)
         const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
-        const float cx = fc[2], cy = fc[3], ifz = fc[8];
+        const float cx = fc[2], cy = fc[3], inv_s = fc[9];
         const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-        const int hw0 = wave * HW;  // the wave's first hypothesis in the unit
-        const float *__restrict__ hm = a.hmodels + rec0 * kHModelStride;
-
-        mx_h8 A[NT];
-        float4 cs[NT][4];
-        mx_load_operands<NT>(hm, hw0, nh, col, half, A, cs);
-        const uint4 *__restrict__ PF = a.PF + p0;
-        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
-        int cnt[NT][4][2];
-        int vcnt[NT][4];  // CV: this lane's inliers of hypothesis (t, jj, half)
+        if (threadIdx.x < HB) {
+            // one thread per record; past the round or no model: z' = 0, xs = 1 (D = 1 > 0, a
+            // decided outlier) and b = -inf (never undecided)
+            const int hq = threadIdx.x;
+            float *dst = mlds + hq * kFModelStride;
+            const float *src = a.fmodels + (rec0 + hq) * kFModelStride;
+            const bool valid = hq < nh && src[14] >= 0.f;
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) cnt[t][jj][0] = cnt[t][jj][1] = vcnt[t][jj] = 0;
-
-        // software pipeline: the next PD tiles' point loads are in flight while this tile computes
-        // (indices clamped to the unit's last point, so every load is in bounds)
-        uint4 pf_q[PD];
-        float uu_q[PD], vv_q[PD];
-#pragma unroll
-        for (int d = 0; d < PD; ++d) {
-            pf_q[d] = make_uint4(0, 0, 0, 0);
-            uu_q[d] = vv_q[d] = 0.f;
-            if (start < n) {
-                const int i0 = min(start + 32 * d + col, n - 1);
-                pf_q[d] = PF[i0];
-                uu_q[d] = U[i0];
-                vv_q[d] = V[i0];
+            for (int q = 0; q < 14; ++q) dst[q] = valid ? src[q] : 0.f;
+            if (!valid) {
+                dst[9] = 1.f;
+                dst[13] = -__builtin_inff();
             }
-        }
-        mx_f16 acc0[NT];  // EXP 4 only
-        for (int base = start; base < n; base += 32) {
-            const int i = base + col;
-            const bool in = i < n;
-            const mx_h8 Bf = __builtin_bit_cast(mx_h8, pf_q[0]);
-            const float uu = uu_q[0], vv = vv_q[0];
-#pragma unroll
-            for (int d = 0; d + 1 < PD; ++d) {
-                pf_q[d] = pf_q[d + 1];
-                uu_q[d] = uu_q[d + 1];
-                vv_q[d] = vv_q[d + 1];
-            }
-            if constexpr (EXP != 3) {  // EXP 3: no loads in the loop (timing)
-                const int inx = min(base + 32 * PD + col, n - 1);
-                pf_q[PD - 1] = PF[inx];
-                uu_q[PD - 1] = U[inx];
-                vv_q[PD - 1] = V[inx];
-            }
-            // out-of-range lanes: a pixel at 3e38 makes the pair a decided outlier (or undecided)
-            const float uc = in ? (uu - cx) * ifz : 3.0e38f, vc = in ? (vv - cy) * ifz : 3.0e38f;
-            uint64_t und[NT][4];
-            uint64_t any = 0;
-            mx_f16 acc[NT];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                if constexpr (EXP == 4) {  // MFMA once per unit (timing)
-                    if (base == start) acc0[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[t], Bf, mx_f16{}, 0, 0, 0);
-                    acc[t] = acc0[t];
-                } else if constexpr (EXP == 2) {  // no MFMA: operands as stand-in values
-                    const float4 bb = __builtin_bit_cast(float4, Bf);
-                    const float4 aa = __builtin_bit_cast(float4, A[t]);
-                    acc[t] = mx_f16{bb.x, bb.y, bb.z, bb.w, aa.x, aa.y, aa.z, aa.w, bb.x, aa.y, bb.z, aa.w, aa.x, bb.y, aa.z, bb.w};
-                } else {
-                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[t], Bf, mx_f16{}, 0, 0, 0);
-                }
-            }
-            if constexpr (EXP == 1) {  // no test: fold the outputs into one count
-                float sacc = 0.f;
-#pragma unroll
-                for (int t = 0; t < NT; ++t)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) sacc += acc[t][r];
-                cnt[0][0][0] += __popcll(__ballot(sacc > uc));
-                continue;
-            }
-            if constexpr (CV == 2) {
-                // all-VALU decisions: per-lane inlier counts and a per-lane count of decided pairs;
-                // the undecided masks are only formed (MFMA and test redone) when a lane of the
-                // tile has an undecided pair
-                int dec = 0;
-#pragma unroll
-                for (int t = 0; t < NT; ++t)
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const MxTest r = mx_test(acc[t], jj, cs[t][jj], uc, vc);
-                        vcnt[t][jj] += r.lt ? 1 : 0;
-                        dec += r.lt ? 1 : 0;
-                        dec += r.gt ? 1 : 0;
-                    }
-                if (__builtin_expect(__ballot(dec != NT * 4) != 0, 0)) {
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) {
-                        const mx_f16 ac = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[t], Bf, mx_f16{}, 0, 0, 0);
-#pragma unroll
-                        for (int jj = 0; jj < 4; ++jj) {
-                            const MxTest r = mx_test(ac, jj, cs[t][jj], uc, vc);
-                            und[t][jj] = ~(__ballot(r.lt) | __ballot(r.gt));
-                            any |= und[t][jj];
-                        }
-                    }
-                }
-            } else {
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const MxTest r = mx_test(acc[t], jj, cs[t][jj], uc, vc);
-                    const bool lt = r.lt;
-                    const uint64_t mi = __ballot(lt);
-                    const uint64_t mo = __ballot(r.gt);
-                    if constexpr (CV) {
-                        vcnt[t][jj] += lt ? 1 : 0;
-                    } else {
-                        cnt[t][jj][0] += __popc((uint32_t)mi);
-                        cnt[t][jj][1] += __popc((uint32_t)(mi >> 32));
-                    }
-                    und[t][jj] = ~(mi | mo);
-                    any |= und[t][jj];
-                }
-            }
-            }
-            if (__builtin_expect(any != 0, 0)) {
-                // defer the exact recount of the undecided pairs to k_pnp_mx_fallback: one record
-                // per tile, so this kernel carries no f64 code
-                int slot = 0;
-                if (lane == 0) slot = atomicAdd(a.mx_count, 1);
-                slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0));
-                if (slot < a.mx_cap && lane == 0) {
-                    MxUndecided &r = a.mx_list[slot];
-                    r.rec = rec0 + hw0;
-                    r.prob = prob;
-                    r.base = base;
-                    r.n = n;
-                    r.nh = nh - hw0;
-#pragma unroll
-                    for (int t = 0; t < NT; ++t)
-#pragma unroll
-                        for (int jj = 0; jj < 4; ++jj) r.m[t * 4 + jj] = und[t][jj];
-                }
-            }
-        }
-        if constexpr (CV) {
-            // sum each half's 32 lanes (hypotheses 2 jj and 2 jj + 1 of tile t)
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    int v = vcnt[t][jj];
-#pragma unroll
-                    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
-                    cnt[t][jj][0] = __shfl(v, 0);
-                    cnt[t][jj][1] = __shfl(v, 32);
-                }
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    scnt[hw0 + t * 8 + 2 * jj] = cnt[t][jj][0];
-                    scnt[hw0 + t * 8 + 2 * jj + 1] = cnt[t][jj][1];
-                }
         }
         __syncthreads();
-        if (threadIdx.x < nh) {
-            const int sum = scnt[threadIdx.x];
-            if (split == 1)
-                counts[rec0 + threadIdx.x] = sum;
-            else if (sum)
-                atomicAdd(&counts[rec0 + threadIdx.x], sum);
-        }
-        __syncthreads();  // scnt and unit_s are rewritten by the next unit
-    }
-}
+        const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
+        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
 
-// The exact f64 recount of the undecided pairs k_pnp_score_mx recorded (rare, about one pair
-// per record): one thread per record walks its mask bits (bit b of mask 4t + j: point base +
-// (b & 31), hypothesis 8t + 2j + (b >> 5)); inliers are added atomically to the counts.
-__global__ __launch_bounds__(256) void k_pnp_mx_fallback(PnpArgs a, int nt, int32_t *__restrict__ counts) {
-    const int total = min(*a.mx_count, a.mx_cap);
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-        const MxUndecided &r = a.mx_list[e];
-        const int prob = r.prob;
-        const int64_t p0 = a.offsets[prob];
-        const double *cm = a.cams + 4 * prob;
-        const Cam k{cm[0], cm[1], cm[2], cm[3]};
-        const float thr2 = a.thr2[prob];
-        unsigned long long np = 0;
-        for (int tj = 0; tj < nt * 4; ++tj) {
-            uint64_t u = r.m[tj];
-            np += __popcll(u);
-            while (u) {
-                const int b = __builtin_ctzll(u);
-                u &= u - 1;
-                const int i = r.base + (b & 31);
-                const int hl = (tj >> 2) * 8 + 2 * (tj & 3) + (b >> 5);
-                if (i >= r.n || hl >= r.nh) continue;
-                if (a.mx_stats && prob == 0) atomicAdd(a.mx_stats + 2 + (r.rec + hl) % a.hyp_stride, 1ull);
-                const double *md = a.models + (r.rec + hl) * kModelStride;
-                const int64_t q = p0 + i;
-                if (md[kValidSlot] != 0.0 &&
-                    pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <= thr2)
-                    atomicAdd(&counts[r.rec + hl], 1);
+        int cnt = 0;
+        for (int base = start + wave * 64 * P; base < n; base += kStride) {
+            float px[P], py[P], pz[P], pu[P], pv[P];
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const int i = base + j * 64 + lane;
+                const bool in = i < n;
+                const int ii = in ? i : 0;
+                const float x = XC[ii], y = YC[ii], z = ZC[ii], uu = U[ii], vv = V[ii];
+                // out of range or a non-finite coordinate: a pixel at 3e38 at the centre's depth
+                // makes the pair a decided outlier (or D = xs^2 + ys^2 >= 0 when z' = 0)
+                const bool ok = in && __builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z) &&
+                                __builtin_isfinite(uu) && __builtin_isfinite(vv);
+                px[j] = ok ? x : 0.f;
+                py[j] = ok ? y : 0.f;
+                pz[j] = ok ? z : 0.f;
+                pu[j] = ok ? (uu - cx) * inv_s : 3.0e38f;
+                pv[j] = ok ? (vv - cy) * inv_s : 3.0e38f;
+            }
+            int ccl = 0;        // lane h: hypothesis h's fast count (D < 0) of this tile
+            uint32_t wund = 0;  // bit h: hypothesis h has an undecided pair (wave-uniform)
+#pragma unroll 4
+            for (int h = 0; h < HB; ++h) {
+                const float *m = mlds + h * kFModelStride;
+                int cc = 0;
+                float tmin = __builtin_inff();
+#pragma unroll
+                for (int j = 0; j < P; ++j) {
+                    const ScPair r = sc_pair(m, px[j], py[j], pz[j], pu[j], pv[j]);
+                    cc += __popcll(__ballot(r.D < 0.f));
+                    tmin = __builtin_fminf(tmin, r.t);
+                }
+                const uint64_t und = __ballot(!(tmin > m[13]));
+                // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
+                // operands would exceed the constant bus); cc and h are SALU results: no hazard
+                asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
+                wund |= und ? (1u << h) : 0u;
+            }
+            cnt += ccl;
+            if (__builtin_expect(wund != 0, 0))
+                cnt += sc_fallback<P>(a, prob, p0, n, rec0, base, lane, wund, mlds, px, py, pz, pu, pv);
+        }
+        if (lane < HB) red[wave][lane] = cnt;
+        __syncthreads();
+        if (split == 1) {
+            if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
+        } else {
+            if (wave == 0 && lane < nh) {
+                const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+                if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
             }
         }
-        if (a.mx_stats) {
-            atomicAdd(a.mx_stats, 1ull);
-            atomicAdd(a.mx_stats + 1, np);
-        }
+        __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
     }
 }
 
@@ -2240,10 +2020,10 @@ static int64_t solve4_max_hyps() {
 }
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
-                            double *frame, float *fconst, hipStream_t s, uint4 *PF, const PnpPrepare *prep) {
+                            double *frame, float *fconst, hipStream_t s, const PnpPrepare *prep) {
     if (prep && prep->p3) {  // the deferred f64 -> f32 conversion of one problem, fused
         if (P != 1 || max_n > 65536) return hipErrorInvalidValue;
-        if (!PF && prep->part && prep->ticket) {
+        if (prep->part && prep->ticket) {
             unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
             if (g > kSetupMaxBlocks) g = kSetupMaxBlocks;
             hipLaunchKernelGGL(k_pnp_setup_fc<true>, dim3(g), dim3(256), 0, s, prep->p3, prep->p2, a, prep->X,
@@ -2251,11 +2031,11 @@ hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t 
                                prep->ticket);
         } else {
             hipLaunchKernelGGL(k_pnp_setup1, dim3(1), dim3(1024), 0, s, prep->p3, prep->p2, a, prep->X, prep->Y,
-                               prep->Z, prep->U, prep->V, ws, frame, fconst, XC, YC, ZC, PF);
+                               prep->Z, prep->U, prep->V, ws, frame, fconst, XC, YC, ZC);
         }
         return hipGetLastError();
     }
-    if (P == 1 && !PF && prep && prep->part && prep->ticket) {
+    if (P == 1 && prep && prep->part && prep->ticket) {
         // one problem already in f32: bounds, frame and centring in one full-grid launch
         unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
         if (g > kSetupMaxBlocks) g = kSetupMaxBlocks;
@@ -2276,7 +2056,7 @@ hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t 
     }
     unsigned g2 = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g2 > 1024) g2 = 1024;
-    hipLaunchKernelGGL(k_pnp_center, dim3(g2, P), dim3(256), 0, s, a, P, ws, frame, fconst, XC, YC, ZC, PF);
+    hipLaunchKernelGGL(k_pnp_center, dim3(g2, P), dim3(256), 0, s, a, P, ws, frame, fconst, XC, YC, ZC);
     return hipGetLastError();
 }
 
@@ -2295,7 +2075,7 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
-constexpr int kDefaultScoreVariant = 48;  // fastest measured on MI355X
+constexpr int kDefaultScoreVariant = 49;  // fastest measured on MI355X
 static int g_score_variant = kDefaultScoreVariant;
 void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
 
@@ -2305,7 +2085,8 @@ void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant :
 template <int PP, int HB, int KIND = 0, int W = 4, bool NZ = false, bool BAL = false>
 static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
     auto kern = [] {
-        if constexpr (KIND == 4) return k_pnp_score_ab<PP, HB, W, true, true>;
+        if constexpr (KIND == 5) return k_pnp_score_sc<PP, HB, W>;
+        else if constexpr (KIND == 4) return k_pnp_score_ab<PP, HB, W, true, true>;
         else if constexpr (KIND == 3) return k_pnp_score_ab<PP, HB, W, NZ>;
         else if constexpr (KIND == 2) return k_pnp_score_mfma<HB, PP>;
         else if constexpr (KIND == 1) return k_pnp_score_pk<PP, HB>;
@@ -2320,7 +2101,7 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
         resident = std::max(1, cus) * std::max(1, per_cu);
     }
     int64_t units = (int64_t)P * ((H + HB - 1) / HB);
-    if constexpr (KIND == 3 || KIND == 4) {
+    if constexpr (KIND >= 3) {
         // few tiles and no fused best key: split the points too (counts accumulate atomically)
         int split = 1;
         const int64_t chunks = std::max<int64_t>(1, ((int64_t)a.max_n + 4 * 64 * PP - 1) / (4 * 64 * PP));
@@ -2356,73 +2137,7 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
     }
 }
 
-// MFMA variants (k_pnp_score_mx): units of 32 NT hypotheses x a point chunk, about 8 units per
-// resident block so that the work queue's tail (at most one unit) stays small; the counts of a
-// split unit accumulate atomically.  k_pnp_mx_fallback then adds the exact recount of the
-// undecided pairs, and k_best_key reduces the best key (single problem).
-template <int NT, int W, int CV, int PD, int EXP = 0>
-static void launch_mx(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
-    constexpr int HB = 32 * NT;
-    auto kern = k_pnp_score_mx<NT, W, CV, PD, EXP>;
-    static int resident = 0;
-    if (resident == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
-        resident = std::max(1, cus) * std::max(1, per_cu);
-    }
-    const int64_t tiles = (int64_t)P * ((H + HB - 1) / HB);
-    const int64_t chunks = std::max<int64_t>(1, ((int64_t)a.max_n + 255) / 256);  // chunks of >= 256 points
-    static const int64_t units_per_block = getenv("RSAC_MX_UNITS") ? atoi(getenv("RSAC_MX_UNITS")) : 8;
-    const int split = (int)std::min<int64_t>(
-        chunks, std::max<int64_t>(1, (units_per_block * (int64_t)resident + tiles - 1) / tiles));
-    if (split > 1 && P == 1)
-        (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
-    else if (split > 1)
-        (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P, s);
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(tiles * split, resident));
-    static unsigned long long *stats = nullptr;
-    static size_t stats_cap = 0;
-    static const bool want_stats = getenv("RSAC_MX_STATS") != nullptr;
-    const size_t need = sizeof(unsigned long long) * (2 + (size_t)a.hyp_stride);
-    if (want_stats && stats_cap < need) {
-        if (stats) (void)hipFree(stats);
-        (void)hipMalloc(&stats, need);
-        stats_cap = need;
-    }
-    PnpArgs ka = a;
-    if (want_stats && stats) {
-        ka.mx_stats = stats;
-        (void)hipMemsetAsync(stats, 0, need, s);
-    }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin, H, P, a.queue, counts, split);
-    // the record count is on the device: a fixed grid, idle threads exit at once
-    hipLaunchKernelGGL(k_pnp_mx_fallback, dim3(512), dim3(256), 0, s, ka, NT, counts);
-    if (want_stats && stats) {
-        std::vector<unsigned long long> h(2 + (size_t)a.hyp_stride);
-        (void)hipMemcpyAsync(h.data(), stats, need, hipMemcpyDeviceToHost, s);
-        (void)hipStreamSynchronize(s);
-        int nz = 0, over100 = 0;
-        unsigned long long top = 0;
-        for (int64_t q = 0; q < a.hyp_stride; ++q) {
-            nz += h[2 + q] > 0; over100 += h[2 + q] > 100;
-            top = std::max(top, h[2 + q]);
-        }
-        fprintf(stderr, "[mx] P=%d H=%d split=%d grid=%u: fallback wave-tiles %llu of %.4g, undecided pairs %llu;"
-                " hypotheses (problem 0) with any %d, >100 %d, max %llu\n",
-                P, H, split, grid, h[0], (double)P * ((H + 8 * NT - 1) / (8 * NT)) * ((a.max_n + 31) / 32), h[1], nz,
-                over100, top);
-    }
-    if (a.best_key) {
-        unsigned g = cdiv(H, 1024);
-        if (g > 128) g = 128;
-        hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
-                           a.rng_base + hyp_begin, a.best_key);
-    }
-}
-
-bool score_variant_mx() { return g_score_variant >= 30 && g_score_variant < 40; }
+int score_record_form() { return g_score_variant >= 49 && g_score_variant <= 52 ? 1 : 0; }
 
 // RSAC_SMALL_PP / RSAC_SMALL_TILES: tuning knobs of the small-round scoring instance
 static int small_round_pp() {
@@ -2438,17 +2153,6 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
                             hipStream_t s) {
     if (a.max_n > 0 && a.max_n <= kLanePts) {
         hipLaunchKernelGGL(k_pnp_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
-    } else if (a.hmodels && a.PF && !a.exact_only && score_variant_mx()) {
-        switch (g_score_variant) {
-            case 31: launch_mx<1, 4, 0, 1>(a, P, hyp_begin, H, counts, s); break;
-            case 32: launch_mx<2, 4, 2, 1>(a, P, hyp_begin, H, counts, s); break;
-            case 33: launch_mx<1, 4, 2, 1>(a, P, hyp_begin, H, counts, s); break;
-            case 34: launch_mx<2, 5, 2, 1>(a, P, hyp_begin, H, counts, s); break;
-            case 35: launch_mx<2, 4, 0, 1, 1>(a, P, hyp_begin, H, counts, s); break;  // timing only
-            case 36: launch_mx<2, 4, 0, 1, 3>(a, P, hyp_begin, H, counts, s); break;  // timing only
-            case 37: launch_mx<2, 4, 0, 1, 4>(a, P, hyp_begin, H, counts, s); break;  // timing only
-            default: launch_mx<2, 4, 0, 1>(a, P, hyp_begin, H, counts, s); break;
-        }
     } else if (a.fmodels && !a.exact_only) {
         switch (g_score_variant) {
             case 1: launch_f32<4, 32>(a, P, hyp_begin, H, counts, s); break;
@@ -2503,6 +2207,16 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
                 else
                     launch_f32<8, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s);
                 break;
+            case 49:
+                // the scaled form (k_pnp_score_sc): records written by write_fmodel_sc (fform 1)
+                if ((int64_t)P * ((H + 31) / 32) <= small_round_tiles())
+                    launch_f32<2, 32, 5, 5, true, true>(a, P, hyp_begin, H, counts, s);
+                else
+                    launch_f32<8, 32, 5, 4, true, true>(a, P, hyp_begin, H, counts, s);
+                break;
+            case 50: launch_f32<8, 32, 5, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 51: launch_f32<4, 32, 5, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 52: launch_f32<6, 32, 5, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
             case 40: launch_f32<8, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
             case 41: launch_f32<4, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
             case 42: launch_f32<8, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;

@@ -94,12 +94,11 @@ RSAC_EXPORT const char *rsac_last_error(void);
 RSAC_EXPORT int rsac_abi_version(void);
 RSAC_EXPORT int rsac_device_count(void);
 RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
-/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 48;
- * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 MFMA tilings, 16..28 the
- * branch-free alpha-beta band tilings, 30..34 the f16-split MFMA kernel; 35..37 are timing
- * experiments whose counts are wrong; 40..47 the alpha-beta band with the lean hypothesis
- * loop, 48 = 42 with the small-round instance).  Counts, masks and models never depend on
- * 0..34 or 40..48. */
+/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 49;
+ * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 f32 MFMA tilings, 16..28 the
+ * branch-free alpha-beta band tilings, 40..48 the alpha-beta band with the lean hypothesis
+ * loop (48 = 42 with the small-round instance), 49..52 the scaled form (k_pnp_score_sc; 49
+ * with the small-round instance)).  Counts, masks and models never depend on the variant. */
 RSAC_EXPORT int rsac_set_score_variant(int variant);
 
 /* The pose refit (solvePnPRefineLM, main_v1.py:508-509) of a problem above 4096 points runs

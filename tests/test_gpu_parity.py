@@ -248,8 +248,8 @@ def test_degenerate_inputs():
 # float32 pre-filter: must never change a decision (DESIGN.md "Scoring").  Every scoring-kernel
 # variant (VALU f32, packed f32, MFMA) is checked, then the default is restored.
 # ---------------------------------------------------------------------------------------------
-SCORE_VARIANTS = [0, 1, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 30, 31, 32, 33, 34,
-                  40, 41, 42, 43, 44, 45, 46, 47, 48]
+SCORE_VARIANTS = [0, 1, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28,
+                  40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52]
 
 
 @pytest.fixture(params=SCORE_VARIANTS)
@@ -306,6 +306,34 @@ def test_f32_prefilter_threshold_boundary(seed, score_variant):
     np.testing.assert_array_equal(exact, ref)
     np.testing.assert_array_equal(fast, ref)
     assert 0 < ref[0] < len(P3)  # the construction really straddles the threshold
+
+
+def test_f32_prefilter_nonfinite_and_huge_coordinates(score_variant):
+    # NaN / inf coordinates (the exact test: an outlier) and a scene scaled by 1e15 (beyond the
+    # range where the f32 evaluation is safe: every pair goes to the exact recount)
+    pr = synth.pnp_problem(3000, 0.3, seed=45)
+    P3, P2 = pr["points3d"].copy(), pr["points2d"].copy()
+    rng = np.random.default_rng(3)
+    bad = rng.choice(len(P3), 40, replace=False)
+    P3[bad[:10], 0] = np.nan
+    P3[bad[10:20], 2] = np.inf
+    P2[bad[20:30], 0] = -np.inf
+    P2[bad[30:], 1] = np.nan
+    R, t = pr["R"], pr["t"]
+    poses = np.array([np.concatenate([R.reshape(9), t])] +
+                     [np.concatenate([R.reshape(9), t + rng.normal(size=3) * 0.05]) for _ in range(5)])
+    cam = O.cam_from_K(pr["K"])
+    fast = rsac.score_poses(P2, P3, pr["K"], poses, 30.0)
+    ref = [O.pnp_count(p[:9].reshape(3, 3), p[9:], O.soa_pnp(P3, P2), cam, 30.0) for p in poses]
+    np.testing.assert_array_equal(fast, ref)
+    assert ref[0] > 1000
+    s = 1e15
+    P3h = pr["points3d"] * s
+    poses_h = poses.copy()
+    poses_h[:, 9:] *= s
+    fast = rsac.score_poses(pr["points2d"], P3h, pr["K"], poses_h, 30.0)
+    ref = [O.pnp_count(p[:9].reshape(3, 3), p[9:], O.soa_pnp(P3h, pr["points2d"]), cam, 30.0) for p in poses_h]
+    np.testing.assert_array_equal(fast, ref)
 
 
 def test_f32_prefilter_points_behind_and_on_camera_plane(score_variant):
