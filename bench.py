@@ -41,6 +41,9 @@ from rsac import synth  # noqa: E402
 METRIC = "RANSAC hypotheses/sec + ms-to-best-model, 10k pts 50% outliers, 1/2/4/8 GPU"
 BYTES_PER_POINT = 20  # f32 X, Y, Z, u, v
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, f32 vector peak
+VALU_ISSUE_PEAK = 1024 * 0.5 * 2.4e9  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each, 2.4 GHz
+FLOP_PER_PAIR = 31  # k_pnp_score_sc: 16.5 vector instructions per pair, 14.5 of them FMAs
 
 
 def parse():
@@ -146,6 +149,28 @@ def main():
                     traffic = d.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        # the issue-side roofline of the same launch: VALU wave-instructions per second (PMC count
+        # of a profiled run of this command, profiles/pmc_score_valu.json) against the wave64
+        # issue peak, 1024 SIMDs x 1 instruction / 2 cycles at the 2.4 GHz peak clock; and the
+        # algorithmic f32 flops (31 per pair: the 16.5 instructions, FMAs counted twice) against
+        # the 157.3 TFLOP/s vector peak
+        roof_valu = None
+        pv = os.path.join(ROOT, "profiles", "pmc_score_valu.json")
+        pairs = args.points * H
+        tflops = pairs * FLOP_PER_PAIR / (score_avg * 1e-3) / 1e12
+        roof_valu = {"bound": "valu", "flop_per_pair": FLOP_PER_PAIR, "achieved_tflops": tflops,
+                     "peak_tflops": VALU_PEAK_TFLOPS, "frac_flops": tflops / VALU_PEAK_TFLOPS}
+        if os.path.exists(pv):
+            try:
+                d = json.load(open(pv))
+                if d.get("points") == args.points and d.get("hyps") == H:
+                    ips = d["valu_instr_per_launch"] / (score_avg * 1e-3)
+                    roof_valu.update({"achieved": ips / 1e9, "peak": VALU_ISSUE_PEAK / 1e9, "unit": "G wave-instr/s",
+                                      "frac": ips / VALU_ISSUE_PEAK,
+                                      "valu_instr_per_launch": d["valu_instr_per_launch"],
+                                      "effective_clock_ghz_profiled": d.get("effective_clock_ghz")})
+            except Exception:
+                pass
         ms_to_best = None
         if not args.no_ms_to_best:
             walls = []
@@ -199,6 +224,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_pnp_score", "algorithmic_bytes_per_launch": args.points * BYTES_PER_POINT * H},
+            "roofline_valu": roof_valu,
             "cpu_baseline": cpu,
             "extras": extras,
         }

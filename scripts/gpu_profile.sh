@@ -17,5 +17,11 @@ if [ -n "$PMC" ]; then
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/pmc_write -o run --output-format csv -- \
       python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/pmc_write.log 2>&1
   rc=$?; echo "rocprof pmc WRITE_SIZE rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  # issue side of the same command: VALU / SALU instructions, wave-cycle split, clock
+  timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
+      SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT \
+      -d gpurun_out/prof/pmc_valu -o run --output-format csv -- \
+      python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/pmc_valu.log 2>&1
+  rc=$?; echo "rocprof pmc VALU rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 find gpurun_out/prof -name "*.csv" | head -20

@@ -7,6 +7,8 @@ Writes
   profiles/TAG_summary.md            -- per-kernel table + the scoring kernel's average duration
   profiles/pmc_score_kernel.json     -- HBM bytes per scoring launch (FETCH_SIZE x 2 per
                                         MI355X_MICROARCH.md "HBM", + WRITE_SIZE), read by bench.py
+  profiles/pmc_score_valu.json       -- VALU instructions per scoring launch and the issue-side
+                                        counters (SQ_*, GRBM_GUI_ACTIVE), read by bench.py
 """
 from __future__ import annotations
 
@@ -24,13 +26,39 @@ SCORE = "k_pnp_score"
 
 
 def counter(path, name):
-    vals = []
+    """per-launch values of counter `name` for the scoring kernel (summed over the counter's
+    instances / dimensions of one dispatch)"""
     if not os.path.exists(path):
         return None
+    per = {}
     for row in csv.DictReader(open(path)):
         if SCORE in row["Kernel_Name"] and row["Counter_Name"] == name:
-            vals.append(float(row["Counter_Value"]))
-    return vals or None
+            per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+    return list(per.values()) or None
+
+
+def valu_summary(path, points, hyps):
+    names = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY",
+             "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"]
+    vals = {n: counter(path, n) for n in names}
+    if not vals["SQ_INSTS_VALU"]:
+        return None
+    dur = []
+    for row in csv.DictReader(open(path)):
+        if SCORE in row["Kernel_Name"] and row.get("Start_Timestamp"):
+            dur.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+    m = {n: statistics.median(v) for n, v in vals.items() if v}
+    out = {"kernel": SCORE, "points": points, "hyps": hyps, "launches": len(vals["SQ_INSTS_VALU"]),
+           "valu_instr_per_launch": m["SQ_INSTS_VALU"], "salu_instr_per_launch": m.get("SQ_INSTS_SALU"),
+           "counters_median": m,
+           "note": "SQ_WAVE_CYCLES / WAIT / ACTIVE count quad-cycles; GRBM_GUI_ACTIVE sums the 8 XCDs"}
+    if dur and "GRBM_GUI_ACTIVE" in m:
+        wall = statistics.median(dur)
+        clk = m["GRBM_GUI_ACTIVE"] / 8 / wall
+        out["wall_s_profiled"] = wall
+        out["effective_clock_ghz"] = clk / 1e9
+        out["valu_per_simd_cycle"] = m["SQ_INSTS_VALU"] / (1024 * m["GRBM_GUI_ACTIVE"] / 8)
+    return out
 
 
 def main():
@@ -66,7 +94,14 @@ def main():
                "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (HBM); the 200 kB point set is re-read "
                        "from L2/MALL by every hypothesis, so HBM traffic is far below the algorithmic bytes"}
         json.dump(pmc, open(os.path.join(OUT, "pmc_score_kernel.json"), "w"), indent=1)
+    valu = valu_summary(os.path.join(PROF, "pmc_valu", "run_counter_collection.csv"), args.points, args.hyps)
+    if valu:
+        json.dump(valu, open(os.path.join(OUT, "pmc_score_valu.json"), "w"), indent=1)
     lines += ["", f"scoring kernel average: {score_avg:.1f} us" if score_avg else "scoring kernel not found"]
+    if valu:
+        lines += [f"scoring kernel VALU instructions/launch (PMC): {valu['valu_instr_per_launch']:.4g}; "
+                  f"effective clock {valu.get('effective_clock_ghz', float('nan')):.3f} GHz; "
+                  f"{valu.get('valu_per_simd_cycle', float('nan')):.3f} VALU wave-instr per SIMD-cycle (peak 0.5)"]
     if pmc:
         lines += [f"scoring kernel HBM bytes/launch (PMC): {pmc['hbm_bytes_per_launch'] / 1e6:.2f} MB "
                   f"(FETCH_SIZE {pmc['fetch_size_kib']:.0f} KiB x2 + WRITE_SIZE {pmc['write_size_kib']:.0f} KiB); "
