@@ -1018,7 +1018,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
                     }
                     // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
                     // operands would exceed the constant bus); cc and h are SALU results: no hazard
-                    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
+                    asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
                     wund |= und ? (1u << h) : 0u;
                 }
                 cnt += ccl;
@@ -1137,35 +1137,49 @@ __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p
     return cnt;
 }
 
+// Work units (launch_sc): the tiles (problem, 32 hypotheses) are numbered problem-major; the
+// first tb of them are one unit each (all their points, one pass of the block per cell of
+// 64 x 4 x P points), the rest one unit per cell, so the queue ends with cell-sized units that
+// even out the blocks' finishing times.  Counts are added atomically into zeroed counts.
 template <int P, int HB, int W = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_sc(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
-    int split) {
+    int tb, int cells) {
     static_assert(HB <= 32, "undecided bits per wave");
-    constexpr int kStride = 4 * 64 * P;  // points one pass of the block covers
+    constexpr int kStride = 4 * 64 * P;  // points one pass of the block covers: one cell
     __shared__ int red[4][HB];
     __shared__ int unit_s;
     __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tiles_per_prob = (H + HB - 1) / HB;
-    const int units_per_prob = tiles_per_prob * split;
-    const int n_units = units_per_prob * n_prob;
+    const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
     for (;;) {
         if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
         __syncthreads();
         const int unit = __builtin_amdgcn_readfirstlane(unit_s);
         if (unit >= n_units) break;  // uniform: every wave of every block reaches it
-        const int prob = unit / units_per_prob;
-        const int rem = unit % units_per_prob;
-        const int chunk = rem % split;
-        const int64_t h0 = hyp_begin + (int64_t)(rem / split) * HB;
+        int tile, c0, c1;             // the unit's tile and cells [c0, c1)
+        if (unit < tb) {
+            tile = unit;
+            c0 = 0;
+            c1 = cells;
+        } else {
+            tile = tb + (unit - tb) / cells;
+            c0 = (unit - tb) % cells;
+            c1 = c0 + 1;
+        }
+        const int prob = tile / tiles_per_prob;
+        const int64_t h0 = hyp_begin + (int64_t)(tile % tiles_per_prob) * HB;
         const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
         const int64_t p0 = a.offsets[prob];
         const int n_all = (int)(a.offsets[prob + 1] - p0);
-        const int clen = ((n_all + split - 1) / split + kStride - 1) / kStride * kStride;
-        const int start = chunk * clen;
-        const int n = min(n_all, start + clen);  // this unit's points: [start, n)
+        const int start = c0 * kStride;
+        const int n = min(n_all, c1 * kStride);  // this unit's points: [start, n)
+        if (start >= n_all) {  // a cell past a short problem of a batch (uniform)
+            __syncthreads();   // every thread has read unit_s before it is rewritten
+            continue;
+        }
         const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
         const float cx = fc[2], cy = fc[3], inv_s = fc[9];
         const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
@@ -1222,7 +1236,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
                 const uint64_t und = __ballot(!(tmin > m[13]));
                 // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
                 // operands would exceed the constant bus); cc and h are SALU results: no hazard
-                asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
+                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
                 wund |= und ? (1u << h) : 0u;
             }
             cnt += ccl;
@@ -1231,13 +1245,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         }
         if (lane < HB) red[wave][lane] = cnt;
         __syncthreads();
-        if (split == 1) {
-            if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
-        } else {
-            if (wave == 0 && lane < nh) {
-                const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-                if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
-            }
+        if (wave == 0 && lane < nh) {
+            const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+            if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
         }
         __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
     }
@@ -2075,6 +2085,7 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 }
 
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
+static const int64_t g_sc_cell_tiles = [] { const char *e = getenv("RSAC_SC_CELL_TILES"); return e ? atoll(e) : 0; }();
 constexpr int kDefaultScoreVariant = 49;  // fastest measured on MI355X
 static int g_score_variant = kDefaultScoreVariant;
 void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
@@ -2085,8 +2096,7 @@ void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant :
 template <int PP, int HB, int KIND = 0, int W = 4, bool NZ = false, bool BAL = false>
 static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
     auto kern = [] {
-        if constexpr (KIND == 5) return k_pnp_score_sc<PP, HB, W>;
-        else if constexpr (KIND == 4) return k_pnp_score_ab<PP, HB, W, true, true>;
+        if constexpr (KIND == 4) return k_pnp_score_ab<PP, HB, W, true, true>;
         else if constexpr (KIND == 3) return k_pnp_score_ab<PP, HB, W, NZ>;
         else if constexpr (KIND == 2) return k_pnp_score_mfma<HB, PP>;
         else if constexpr (KIND == 1) return k_pnp_score_pk<PP, HB>;
@@ -2138,6 +2148,45 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
 }
 
 int score_record_form() { return g_score_variant >= 49 && g_score_variant <= 52 ? 1 : 0; }
+
+// k_pnp_score_sc: whole-tile units for all but the last `resident` tiles, which go as one unit
+// per cell (64 x 4 x P points): the cells even out the blocks' finishing times (the queue's
+// tail is one cell, against a whole split unit before).  Counts are zeroed (by the solve kernel,
+// else here) and added atomically; the best key is reduced afterwards.
+template <int P, int W>
+static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
+    auto kern = k_pnp_score_sc<P, 32, W>;
+    static int resident = 0;
+    if (resident == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
+        resident = std::max(1, cus) * std::max(1, per_cu);
+    }
+    const int64_t cells = std::max<int64_t>(1, ((int64_t)a.max_n + 256 * P - 1) / (256 * P));
+    const int64_t tiles = (int64_t)P_ * ((H + 31) / 32);
+    const int64_t cell_tiles = std::min<int64_t>(tiles, g_sc_cell_tiles > 0 ? g_sc_cell_tiles : resident);
+    const int64_t tb = tiles - cell_tiles;
+    const int64_t units = tb + cell_tiles * cells;
+    if (a.counts_out != counts) {
+        if (P_ == 1)
+            (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
+        else
+            (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P_, s);
+    }
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
+    PnpArgs ka = a;
+    ka.best_key = nullptr;  // reduced below from the complete counts
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin, H, P_, a.queue, counts, (int)tb,
+                       (int)cells);
+    if (a.best_key) {
+        unsigned g = cdiv(H, 1024);
+        if (g > 128) g = 128;
+        hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
+                           a.rng_base + hyp_begin, a.best_key);
+    }
+}
 
 // RSAC_SMALL_PP / RSAC_SMALL_TILES: tuning knobs of the small-round scoring instance
 static int small_round_pp() {
@@ -2210,13 +2259,13 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 49:
                 // the scaled form (k_pnp_score_sc): records written by write_fmodel_sc (fform 1)
                 if ((int64_t)P * ((H + 31) / 32) <= small_round_tiles())
-                    launch_f32<2, 32, 5, 5, true, true>(a, P, hyp_begin, H, counts, s);
+                    launch_sc<2, 5>(a, P, hyp_begin, H, counts, s);
                 else
-                    launch_f32<8, 32, 5, 4, true, true>(a, P, hyp_begin, H, counts, s);
+                    launch_sc<8, 4>(a, P, hyp_begin, H, counts, s);
                 break;
-            case 50: launch_f32<8, 32, 5, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 51: launch_f32<4, 32, 5, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 52: launch_f32<6, 32, 5, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
+            case 50: launch_sc<8, 5>(a, P, hyp_begin, H, counts, s); break;
+            case 51: launch_sc<4, 4>(a, P, hyp_begin, H, counts, s); break;
+            case 52: launch_sc<6, 4>(a, P, hyp_begin, H, counts, s); break;
             case 40: launch_f32<8, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
             case 41: launch_f32<4, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
             case 42: launch_f32<8, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
