@@ -1005,7 +1005,7 @@ void rsac_destroy(rsac_ctx *c) {
 }
 
 int rsac_set_score_variant(int variant) {
-    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 52))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
+    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 53))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
     set_score_variant(variant);
     return RSAC_OK;
 }

@@ -496,6 +496,7 @@ __device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t
         fm[9] = 1.f;
         fm[13] = -__builtin_inff();
         fm[14] = -1.f;
+        fm[15] = -__builtin_inff();
         return;
     }
     const double B = frame[3], rho = frame[4], cmax = frame[5], wmax = frame[6];
@@ -533,7 +534,7 @@ __device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t
     fm[12] = fits ? (float)a : 0.f;
     fm[13] = fits ? (float)b : __builtin_inff();
     fm[14] = (float)zg;
-    fm[15] = 0.f;
+    fm[15] = fits ? (float)((b + a * Zp) * (1.0 + 1e-6)) : __builtin_inff();  // constant band (CB kernels)
 }
 
 __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
@@ -1103,7 +1104,7 @@ __device__ __forceinline__ ScPair sc_pair(const float *m, float x, float y, floa
 
 // exact recount of the undecided pairs of the flagged hypotheses (wund) on this lane's points:
 // returns this lane's share of the count corrections (lane h: hypothesis h's)
-template <int P>
+template <int P, bool CB = false>
 __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p0, int n, int64_t rec0, int base,
                                            int lane, uint32_t wund, const float *mlds, const float (&px)[P],
                                            const float (&py)[P], const float (&pz)[P], const float (&pu)[P],
@@ -1123,7 +1124,7 @@ __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p
         for (int j = 0; j < P; ++j) {
             const int i = base + j * 64 + lane;
             const ScPair r = sc_pair(m, px[j], py[j], pz[j], pu[j], pv[j]);
-            const bool und = !(r.t > m[13]);
+            const bool und = CB ? !(__builtin_fabsf(r.D) > m[15]) : !(r.t > m[13]);
             bool ex = false;
             if (und && i < n) {
                 const int64_t q = p0 + i;
@@ -1141,7 +1142,9 @@ __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p
 // first tb of them are one unit each (all their points, one pass of the block per cell of
 // 64 x 4 x P points), the rest one unit per cell, so the queue ends with cell-sized units that
 // even out the blocks' finishing times.  Counts are added atomically into zeroed counts.
-template <int P, int HB, int W = 4>
+// CB: the constant band of record slot 15 (b + a Zmax) instead of a |z'| + b: no t per pair, the
+// minimum is taken over |D| directly (more pairs undecided where |z'| is well below Zmax).
+template <int P, int HB, int W = 4, bool CB = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_sc(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int tb, int cells) {
@@ -1191,10 +1194,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
             const float *src = a.fmodels + (rec0 + hq) * kFModelStride;
             const bool valid = hq < nh && src[14] >= 0.f;
 #pragma unroll
-            for (int q = 0; q < 14; ++q) dst[q] = valid ? src[q] : 0.f;
+            for (int q = 0; q < 16; ++q) dst[q] = valid ? src[q] : 0.f;
             if (!valid) {
                 dst[9] = 1.f;
                 dst[13] = -__builtin_inff();
+                dst[15] = -__builtin_inff();
             }
         }
         __syncthreads();
@@ -1231,9 +1235,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
                 for (int j = 0; j < P; ++j) {
                     const ScPair r = sc_pair(m, px[j], py[j], pz[j], pu[j], pv[j]);
                     cc += __popcll(__ballot(r.D < 0.f));
-                    tmin = __builtin_fminf(tmin, r.t);
+                    tmin = __builtin_fminf(tmin, CB ? __builtin_fabsf(r.D) : r.t);
                 }
-                const uint64_t und = __ballot(!(tmin > m[13]));
+                const uint64_t und = __ballot(!(tmin > m[CB ? 15 : 13]));
                 // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
                 // operands would exceed the constant bus); cc and h are SALU results: no hazard
                 asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
@@ -1241,7 +1245,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
             }
             cnt += ccl;
             if (__builtin_expect(wund != 0, 0))
-                cnt += sc_fallback<P>(a, prob, p0, n, rec0, base, lane, wund, mlds, px, py, pz, pu, pv);
+                cnt += sc_fallback<P, CB>(a, prob, p0, n, rec0, base, lane, wund, mlds, px, py, pz, pu, pv);
         }
         if (lane < HB) red[wave][lane] = cnt;
         __syncthreads();
@@ -2147,15 +2151,15 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
     }
 }
 
-int score_record_form() { return g_score_variant >= 49 && g_score_variant <= 52 ? 1 : 0; }
+int score_record_form() { return g_score_variant >= 49 && g_score_variant <= 53 ? 1 : 0; }
 
 // k_pnp_score_sc: whole-tile units for all but the last `resident` tiles, which go as one unit
 // per cell (64 x 4 x P points): the cells even out the blocks' finishing times (the queue's
 // tail is one cell, against a whole split unit before).  Counts are zeroed (by the solve kernel,
 // else here) and added atomically; the best key is reduced afterwards.
-template <int P, int W>
+template <int P, int W, bool CB = false>
 static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
-    auto kern = k_pnp_score_sc<P, 32, W>;
+    auto kern = k_pnp_score_sc<P, 32, W, CB>;
     static int resident = 0;
     if (resident == 0) {
         int dev = 0, cus = 0, per_cu = 0;
@@ -2266,6 +2270,7 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 50: launch_sc<8, 5>(a, P, hyp_begin, H, counts, s); break;
             case 51: launch_sc<4, 4>(a, P, hyp_begin, H, counts, s); break;
             case 52: launch_sc<6, 4>(a, P, hyp_begin, H, counts, s); break;
+            case 53: launch_sc<8, 4, true>(a, P, hyp_begin, H, counts, s); break;
             case 40: launch_f32<8, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
             case 41: launch_f32<4, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
             case 42: launch_f32<8, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;

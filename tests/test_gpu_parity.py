@@ -249,7 +249,7 @@ def test_degenerate_inputs():
 # variant (VALU f32, packed f32, MFMA) is checked, then the default is restored.
 # ---------------------------------------------------------------------------------------------
 SCORE_VARIANTS = [0, 1, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28,
-                  40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52]
+                  40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53]
 
 
 @pytest.fixture(params=SCORE_VARIANTS)
