@@ -372,6 +372,8 @@ int fm_prefilter(rsac_ctx *c, HomArgs &a, int32_t P, uint32_t flags, hipStream_t
     HIPCHK(c->bounds_ws.ensure(sizeof(int32_t) * 10 * P));  // >= 8 per problem
     a.fmodels = c->fmodels.as<float>();
     a.fbounds = c->bounds_ws.as<int>();
+    HIPCHK(c->queue.ensure(64));
+    a.fm_queue = c->queue.as<int>() + 8;  // its own counter (the PnP kernels use word 0)
     HIPCHK(launch_fm_bounds(a, P, a.max_n, c->bounds_ws.as<int>(), s));
     return RSAC_OK;
 }

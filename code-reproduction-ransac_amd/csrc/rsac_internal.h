@@ -70,6 +70,7 @@ struct HomArgs {
     // (min / max of x1 y1 x2 y2, ordered ints, k_fm_bounds); nullptr: the all-f64 kernel
     float *fmodels;
     const int *fbounds;
+    int *fm_queue = nullptr;  // work-queue counter of k_fm_score_q (zeroed before each launch)
 };
 
 // problems with at most this many points are scored one lane per hypothesis

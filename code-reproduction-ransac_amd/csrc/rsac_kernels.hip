@@ -3423,93 +3423,128 @@ __global__ __launch_bounds__(256) void k_fm_score_lane(HomArgs a, int64_t hyp_be
     counts[rec] = cnt;
 }
 
-// f32 Sampson pre-filter (record: fm_write_record): hypotheses x points tiles as in k_fm_score,
-// the block's HB records staged in LDS; undecided pairs are recounted with the exact f64 test
-// after the hypothesis loop, once per tile.
-template <int P, int HB>
-__global__ __launch_bounds__(256) void k_fm_score_f32(HomArgs a, int64_t hyp_begin, int32_t H,
-                                                      int32_t *__restrict__ counts) {
-    static_assert(HB <= 32, "undecided bits per lane");
+// f32 Sampson pre-filter (record: fm_write_record) on a work queue (the layout of
+// k_pnp_score_sc; undecided pairs recounted with the exact f64 test): tiles of 32 hypotheses,
+// whole-tile units for all but the last `resident` tiles, which go one unit per cell of
+// 64 x 4 x P points; the lean hypothesis loop (all 32 staged records, counts by v_writelane,
+// undecided flags in an SGPR mask); counts added atomically into zeroed counts.
+template <int P>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_fm_score_q(
+    HomArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int32_t *__restrict__ counts, int tb, int cells) {
+    constexpr int HB = 32;
+    constexpr int kStride = 4 * 64 * P;
     __shared__ int red[4][HB];
+    __shared__ int unit_s;
     __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
-    const int prob = blockIdx.y;
-    const int64_t p0 = a.offsets[prob];
-    const int n = (int)(a.offsets[prob + 1] - p0);
-    const int64_t h0 = hyp_begin + (int64_t)blockIdx.x * HB;
-    const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-    for (int q = threadIdx.x; q < HB * kFModelStride; q += 256)
-        mlds[q] = q < nh * kFModelStride ? a.fmodels[rec0 * kFModelStride + q] : 0.f;
-    __syncthreads();
-    const float *__restrict__ SX = a.SX + p0, *__restrict__ SY = a.SY + p0;
-    const float *__restrict__ DX = a.DX + p0, *__restrict__ DY = a.DY + p0;
-    const FmFrame fr = fm_frame(a.fbounds, prob);
-    int cnt = 0;
-    for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
-        float x1[P], y1[P], x2[P], y2[P];  // normalised frame
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int i = base + j * 64 + lane;
-            const bool in = i < n;
-            const int ii = in ? i : 0;
-            x1[j] = (SX[ii] - fr.c[0]) * fr.is;
-            y1[j] = (SY[ii] - fr.c[1]) * fr.is;
-            x2[j] = (DX[ii] - fr.c[2]) * fr.is;
-            // out-of-range lanes: y2 = 3e38 makes the pair a decided outlier (or undecided)
-            y2[j] = in ? (DY[ii] - fr.c[3]) * fr.is : 3.0e38f;
+    const int tiles_per_prob = (H + HB - 1) / HB;
+    const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
+    for (;;) {
+        if (threadIdx.x == 0) unit_s = atomicAdd(a.fm_queue, 1);
+        __syncthreads();
+        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
+        if (unit >= n_units) break;  // uniform
+        int tile, c0, c1;
+        if (unit < tb) {
+            tile = unit;
+            c0 = 0;
+            c1 = cells;
+        } else {
+            tile = tb + (unit - tb) / cells;
+            c0 = (unit - tb) % cells;
+            c1 = c0 + 1;
         }
-        uint32_t undm = 0;  // bit h: this lane has an undecided pair with hypothesis h
-        for (int h = 0; h < nh; ++h) {
-            const float *m = mlds + h * kFModelStride;
-            int cc = 0;
-            uint64_t und = 0;
+        const int prob = tile / tiles_per_prob;
+        const int64_t h0 = hyp_begin + (int64_t)(tile % tiles_per_prob) * HB;
+        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+        const int64_t p0 = a.offsets[prob];
+        const int n_all = (int)(a.offsets[prob + 1] - p0);
+        const int start = c0 * kStride;
+        const int n = min(n_all, c1 * kStride);
+        if (start >= n_all) {
+            __syncthreads();
+            continue;
+        }
+        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+        if (threadIdx.x < HB) {  // past the round: fm_write_record's "no model" form (decided outlier)
+            const int hq = threadIdx.x;
+            float *dst = mlds + hq * kFModelStride;
+            const float *src = a.fmodels + (rec0 + hq) * kFModelStride;
+            const bool in = hq < nh;
+#pragma unroll
+            for (int q = 0; q < kFModelStride; ++q) dst[q] = in ? src[q] : 0.f;
+            if (!in) {
+                dst[10] = 1.f;
+                dst[12] = -1.f;
+            }
+        }
+        __syncthreads();
+        const float *__restrict__ SX = a.SX + p0, *__restrict__ SY = a.SY + p0;
+        const float *__restrict__ DX = a.DX + p0, *__restrict__ DY = a.DY + p0;
+        const FmFrame fr = fm_frame(a.fbounds, prob);
+        int cnt = 0;
+        for (int base = start + wave * 64 * P; base < n; base += kStride) {
+            float x1[P], y1[P], x2[P], y2[P];  // normalised frame
 #pragma unroll
             for (int j = 0; j < P; ++j) {
-                const FmTest r = fm_test_f32(m, x1[j], y1[j], x2[j], y2[j]);
-                const uint64_t mi = __ballot(r.lt);
-                const uint64_t mo = __ballot(r.gt);
-                cc += __popcll(mi);
-                und |= ~(mi | mo);
+                const int i = base + j * 64 + lane;
+                const bool in = i < n;
+                const int ii = in ? i : 0;
+                x1[j] = (SX[ii] - fr.c[0]) * fr.is;
+                y1[j] = (SY[ii] - fr.c[1]) * fr.is;
+                x2[j] = (DX[ii] - fr.c[2]) * fr.is;
+                // out-of-range lanes: y2 = 3e38 makes the pair a decided outlier (or undecided)
+                y2[j] = in ? (DY[ii] - fr.c[3]) * fr.is : 3.0e38f;
             }
-            cnt += (lane == h) ? cc : 0;
-            undm |= __builtin_amdgcn_inverse_ballot_w64(und) ? (1u << h) : 0u;
-        }
-        uint32_t wund = undm;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) wund |= (uint32_t)__shfl_xor((int)wund, o);
-        wund = __builtin_amdgcn_readfirstlane(wund);
-        if (__builtin_expect(wund != 0, 0)) {
-            const double T = (double)a.thr2[prob];
-#pragma unroll 1
-            while (wund) {
-                const int h = __builtin_ctz(wund);
-                wund &= wund - 1;
+            int ccl = 0;
+            uint32_t wund = 0;
+#pragma unroll 4
+            for (int h = 0; h < HB; ++h) {
                 const float *m = mlds + h * kFModelStride;
-                const double *md = a.models + (rec0 + h) * kModelStride;
                 int cc = 0;
-#pragma unroll 1
+                uint64_t und = 0;
+#pragma unroll
                 for (int j = 0; j < P; ++j) {
-                    const int i = base + j * 64 + lane;
-                    bool ex = false;
-                    if ((undm >> h) & 1u) {
-                        const FmTest r = fm_test_f32(m, x1[j], y1[j], x2[j], y2[j]);
-                        if (!(r.lt | r.gt) && i < n)
-                            ex = md[kValidSlot] != 0.0 && fm_inlier(md, (double)SX[i], (double)SY[i], (double)DX[i],
-                                                                    (double)DY[i], T);
-                    }
-                    cc += __popcll(__ballot(ex));
+                    const FmTest r = fm_test_f32(m, x1[j], y1[j], x2[j], y2[j]);
+                    const uint64_t mi = __ballot(r.lt);
+                    const uint64_t mo = __ballot(r.gt);
+                    cc += __popcll(mi);
+                    und |= ~(mi | mo);
                 }
-                cnt += (lane == h) ? cc : 0;
+                // v_writelane_b32 (no clang builtin); lane select through M0; SALU operands
+                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
+                wund |= und ? (1u << h) : 0u;
+            }
+            cnt += ccl;
+            if (__builtin_expect(wund != 0, 0)) {
+                const double T = (double)a.thr2[prob];
+#pragma unroll 1
+                while (wund) {
+                    const int h = __builtin_ctz(wund);
+                    wund &= wund - 1;
+                    const float *m = mlds + h * kFModelStride;
+                    const double *md = a.models + (rec0 + h) * kModelStride;
+                    int cc = 0;
+#pragma unroll 1
+                    for (int j = 0; j < P; ++j) {
+                        const int i = base + j * 64 + lane;
+                        const FmTest r = fm_test_f32(m, x1[j], y1[j], x2[j], y2[j]);
+                        const bool ex = !(r.lt | r.gt) && i < n && md[kValidSlot] != 0.0 &&
+                                        fm_inlier(md, (double)SX[i], (double)SY[i], (double)DX[i], (double)DY[i], T);
+                        cc += __popcll(__ballot(ex));
+                    }
+                    cnt += (lane == h) ? cc : 0;
+                }
             }
         }
-    }
-    if (lane < HB) red[wave][lane] = cnt;
-    __syncthreads();
-    if (threadIdx.x < nh) {
-        const int s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-        counts[rec0 + threadIdx.x] = s;
+        if (lane < HB) red[wave][lane] = cnt;
+        __syncthreads();
+        if (wave == 0 && lane < nh) {
+            const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+            if (sum) atomicAdd(&counts[rec0 + lane], sum);
+        }
+        __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
     }
 }
 
@@ -3533,9 +3568,33 @@ hipError_t launch_fm_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32
 hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
     if (a.max_n > 0 && a.max_n <= kLanePts)
         hipLaunchKernelGGL(k_fm_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
-    else if (a.fmodels)
-        hipLaunchKernelGGL((k_fm_score_f32<8, 32>), dim3(cdiv(H, 32), P), dim3(256), 0, s, a, hyp_begin, H, counts);
-    else
+    else if (a.fmodels && a.fm_queue) {
+        // k_fm_score_q: whole-tile units, then the last `resident` tiles by cells (launch_sc)
+        constexpr int FP = 8;
+        static int resident = 0;
+        if (resident == 0) {
+            int dev = 0, cus = 0, per_cu = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fm_score_q<FP>, 256, 0);
+            resident = std::max(1, cus) * std::max(1, per_cu);
+        }
+        const int64_t cells = std::max<int64_t>(1, ((int64_t)a.max_n + 256 * FP - 1) / (256 * FP));
+        const int64_t tiles = (int64_t)P * ((H + 31) / 32);
+        const int64_t cell_tiles = std::min<int64_t>(tiles, resident);
+        const int64_t tb = tiles - cell_tiles, units = tb + cell_tiles * cells;
+        hipError_t e = hipMemsetAsync(a.fm_queue, 0, sizeof(int), s);
+        if (e == hipSuccess) {
+            if (P == 1)
+                e = hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
+            else
+                e = hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P, s);
+        }
+        if (e != hipSuccess) return e;
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
+        hipLaunchKernelGGL(k_fm_score_q<FP>, dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, counts, (int)tb,
+                           (int)cells);
+    } else
         hipLaunchKernelGGL((k_fm_score<4, 32>), dim3(cdiv(H, 32), P), dim3(256), 0, s, a, hyp_begin, H, counts);
     return hipGetLastError();
 }
