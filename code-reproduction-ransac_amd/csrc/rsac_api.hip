@@ -136,6 +136,8 @@ struct rsac_ctx {
     double *d_cams = nullptr;
     float *d_thr2 = nullptr;
     DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
+    DevBuf mxpts;                                              // MFMA point operands (PF, UV: 40 B / point)
+    DevBuf mflist;                                             // MFMA scorer's flagged-iteration records
     DevBuf loc;                                                // location search: inputs, pos2, H, err
     DevBuf lo;                                                 // LO-RANSAC: 2 model records, chain state, 2 masks
     const void *lo_state_base = nullptr;                       // the lo allocation whose LoState is zeroed
@@ -343,6 +345,16 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
     // resets best_key and the queue, then builds the frame (also in exact mode: cheap)
     // one problem: k_pnp_setup_fc's scratch (its ticket starts at 0; the kernel resets it)
+    const int fform = score_record_form();
+    if (!a.exact_only && fform == 2) {  // the MFMA scorer's point operands, written with the centring
+        HIPCHK(c->mxpts.ensure(40 * std::max<int64_t>(N, 1)));
+        a.PF = c->mxpts.as<uint4>();
+        a.UV = reinterpret_cast<float2 *>(c->mxpts.as<char>() + 32 * std::max<int64_t>(N, 1));
+        constexpr int64_t kMfCap = 1 << 21;  // 64 MB of records; larger launches are split (launch_mf)
+        HIPCHK(c->mflist.ensure(sizeof(MfFlag) * kMfCap));
+        a.mf_list = c->mflist.as<MfFlag>();
+        a.mf_cap = kMfCap;
+    }
     PnpPrepare prep = st.prep;
     if (P == 1) {
         if (!c->setup_scr.p) {
@@ -360,7 +372,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
         a.frame = c->frame.as<double>();
         a.fconst = c->fconst.as<float>();
         a.fmodels = c->fmodels.as<float>();
-        a.fform = score_record_form();
+        a.fform = fform;
     }
     return RSAC_OK;
 }
@@ -990,7 +1002,7 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->lmscr, &c->setup_scr, &c->scanrec};
+                     &c->epnp, &c->lmscr, &c->setup_scr, &c->scanrec, &c->mxpts, &c->mflist};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_lmfail, &c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,
@@ -1007,7 +1019,8 @@ void rsac_destroy(rsac_ctx *c) {
 }
 
 int rsac_set_score_variant(int variant) {
-    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 53))) return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
+    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 53) && (variant < 60 || variant > 73)))
+        return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
     set_score_variant(variant);
     return RSAC_OK;
 }

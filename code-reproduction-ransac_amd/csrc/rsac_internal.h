@@ -10,6 +10,15 @@ namespace rsac {
 struct EpnpStage1;
 struct EpnpStage2;
 
+// one flagged check window of k_pnp_score_mf (a wave's iterations of 2 x 32 points from `base` x
+// the 32 hypotheses of work unit `unit`, with an undecided pair in the slots of fl), recounted
+// exactly afterwards (k_pnp_mf_recount)
+struct MfFlag {
+    int32_t unit, base;  // base: the window's first iteration (its points base + [0, 64))
+    uint32_t fl;         // bit 4t + g: slot g of MFMA group t (hypotheses 8t + 2g, 8t + 2g + 1)
+    int32_t iters;       // iterations in the window (the next ones at base + 256 k)
+};
+
 // PnP problem set on the device.  Problem p owns points [offsets[p],
 // offsets[p+1]) of the SoA arrays; its hypothesis records live at
 // [p * hyp_stride, p * hyp_stride + H).
@@ -44,9 +53,18 @@ struct PnpArgs {
     // optional fused reduction (single problem): max over the scored hypotheses of
     // (count << 32) | (0xFFFFFFFF - low32(rng_base + h)), atomically into *best_key
     unsigned long long *best_key;
-    int *queue;  // work-queue counter of the f32 scoring kernel (reset by launch_pnp_frame)
+    int *queue;  // counters of the f32 scoring kernels, words 0..3 (reset by the frame and solve kernels)
     int32_t max_n;  // largest problem (points); small problems score one lane per hypothesis
-    int fform = 0;  // f32 record form: 0 write_fmodel, 1 the scaled form of k_pnp_score_sc
+    int fform = 0;  // f32 record form: 0 write_fmodel, 1 the scaled form of k_pnp_score_sc, 2 the MFMA
+                    // form of k_pnp_score_mf (form 1 for problems outside its operand range)
+    // MFMA scoring operands per point (fform 2; written with the centred coordinates): PF = two
+    // uint4 per point, f16 {hi XC, hi YC, hi ZC, 1, lo XC, lo YC, lo ZC, 0} and the same x 2^-11
+    // (the B operand of the lanes that hold the hypotheses' lo parts x 2^11);
+    // UV = (u - cx, v - cy) / sqrt(T)
+    uint4 *PF = nullptr;
+    float2 *UV = nullptr;
+    MfFlag *mf_list = nullptr;  // flagged-iteration records (capacity mf_cap) of k_pnp_score_mf
+    int64_t mf_cap = 0;
 };
 
 constexpr int kFrameStride = 8;

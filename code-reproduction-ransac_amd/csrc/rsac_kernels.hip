@@ -69,6 +69,15 @@ __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i
 
 constexpr double kU32 = 5.9604644775390625e-08;  // 2^-24, unit roundoff of float32
 
+// the PnP scoring launch's counters (PnpArgs::queue, words 0..3): unit queue, units finished,
+// flagged-iteration records appended, records taken (k_pnp_score_mf); reset before each launch
+__device__ __forceinline__ void reset_pnp_queue(int *q) {
+    q[0] = 0;
+    q[1] = 0;
+    q[2] = 0;
+    q[3] = 0;
+}
+
 // ws: [0, 5P) mins, [5P, 10P) maxes of X Y Z U V (ordered-int encoding), pre-set by memset
 __global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *__restrict__ ws) {
     __shared__ float sl[4][5], sh[4][5];
@@ -151,7 +160,7 @@ __global__ __launch_bounds__(1024) void k_pnp_bounds1(PnpArgs a, int *__restrict
     }
     if (threadIdx.x == 0) {
         if (a.best_key) *a.best_key = 0ull;
-        *a.queue = 0;
+        reset_pnp_queue(a.queue);
     }
 }
 
@@ -200,8 +209,52 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
     q[7] = (float)(2.5 * kU32 * (du + dv + fabs(cx) + fabs(cy) + 2.0 * thr + 3.0) + 1e-6);
     q[8] = 0.f;
     q[9] = (T > 1e-12 && T < 1e30) ? (float)(1.0 / thr) : 1.f;  // k_pnp_score_sc: u' = (u - cx) / sqrt(T)
-    q[10] = q[11] = q[12] = 0.f;
+    q[10] = 0.f;
+    // k_pnp_score_mf: the centred coordinates are MFMA operands as they are (f16 hi + lo), so
+    // |XC| <= B must stay inside the f16 range; small scenes would spend the band on the f16
+    // subnormal floor (the form-1 kernel path takes both)
+    q[11] = (B <= 32768.0 && B >= 0.015625) ? 1.f : 0.f;
+    q[12] = 0.f;
     for (int k = 13; k < kFconstStride; ++k) q[k] = 0.f;
+}
+
+// MFMA point operands (PnpArgs::PF / UV, k_pnp_score_mf) of one point from its centred
+// coordinates and pixel: f16 hi + lo of XC YC ZC (hi = RN(x), lo = RN(x - hi): |x - hi - lo| <=
+// 2^-22 |x| + 2^-25), the constant feature 1, the same four pairs x 2^-11 (exact: powers of 2,
+// the B operand facing the hypotheses' lo parts x 2^11), and the scaled pixel offsets u' v' of
+// k_pnp_score_sc.  A non-finite coordinate stages the decided-outlier point of k_pnp_score_sc
+// (the origin, pixel at 3e38).
+struct MxPixel {
+    float cx, cy, inv_s;
+};
+__device__ __forceinline__ MxPixel mx_pixel(const PnpArgs &a, int prob) {
+    const double T = a.thr2[prob];
+    const float inv_s = (T > 1e-12 && T < 1e30) ? (float)(1.0 / sqrt(T)) : 1.f;  // = fconst[9]
+    return MxPixel{(float)a.cams[4 * prob + 2], (float)a.cams[4 * prob + 3], inv_s};
+}
+__device__ __forceinline__ uint32_t mx_pack2(_Float16 lo16, _Float16 hi16) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo16) | ((uint32_t)__builtin_bit_cast(uint16_t, hi16) << 16);
+}
+constexpr float kMxLoScale = 0x1p-11f;  // B x 2^-11 faces A_lo x 2^11
+__device__ __forceinline__ void mx_point(const PnpArgs &a, int64_t q, float xc, float yc, float zc, float uu,
+                                         float vv, const MxPixel &k) {
+    const bool ok = __builtin_isfinite(xc) && __builtin_isfinite(yc) && __builtin_isfinite(zc) &&
+                    __builtin_isfinite(uu) && __builtin_isfinite(vv);
+    uint4 f = make_uint4(0u, 0x3C000000u, 0u, 0u);  // {0, 0, 0, 1 | 0, 0, 0, 0}
+    uint4 g = make_uint4(0u, mx_pack2((_Float16)0.0f, (_Float16)kMxLoScale), 0u, 0u);
+    float2 uv = make_float2(3.0e38f, 3.0e38f);
+    if (ok) {
+        const _Float16 hx = (_Float16)xc, hy = (_Float16)yc, hz = (_Float16)zc;
+        const _Float16 lx = (_Float16)(xc - (float)hx), ly = (_Float16)(yc - (float)hy), lz = (_Float16)(zc - (float)hz);
+        f = make_uint4(mx_pack2(hx, hy), mx_pack2(hz, (_Float16)1.0f), mx_pack2(lx, ly), mx_pack2(lz, (_Float16)0.0f));
+        const _Float16 k11 = (_Float16)kMxLoScale;
+        g = make_uint4(mx_pack2(hx * k11, hy * k11), mx_pack2(hz * k11, k11), mx_pack2(lx * k11, ly * k11),
+                       mx_pack2(lz * k11, (_Float16)0.0f));
+        uv = make_float2((uu - k.cx) * k.inv_s, (vv - k.cy) * k.inv_s);
+    }
+    a.PF[2 * q] = f;
+    a.PF[2 * q + 1] = g;
+    a.UV[q] = uv;
 }
 
 // centred coordinates; block 0 of each problem also writes the problem's frame and
@@ -220,6 +273,7 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const 
         for (int k = 0; k < 3; ++k)
             cc[k] = ((double)ord2f(ws[5 * prob + k]) + (double)ord2f(ws[5 * P + 5 * prob + k])) * 0.5;
     const double c0 = cc[0], c1 = cc[1], c2 = cc[2];
+    const MxPixel mk = mx_pixel(a, prob);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int64_t q = p0 + i;
         const float xc = (float)((double)a.X[q] - c0), yc = (float)((double)a.Y[q] - c1),
@@ -227,6 +281,7 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const 
         XC[q] = xc;
         YC[q] = yc;
         ZC[q] = zc;
+        if (a.PF) mx_point(a, q, xc, yc, zc, a.U[q], a.V[q], mk);
     }
 }
 
@@ -278,19 +333,21 @@ __global__ __launch_bounds__(1024) void k_pnp_setup1(const double *__restrict__ 
     }
     if (threadIdx.x == 0) {
         if (a.best_key) *a.best_key = 0ull;
-        *a.queue = 0;
+        reset_pnp_queue(a.queue);
     }
     __syncthreads();
     if (threadIdx.x == 0) pnp_frame_one(a, 1, 0, wsl, frame, fconst);
     double cc[3] = {0, 0, 0};
     if (n > 0)
         for (int k = 0; k < 3; ++k) cc[k] = ((double)ord2f(wsl[k]) + (double)ord2f(wsl[5 + k])) * 0.5;
+    const MxPixel mk = mx_pixel(a, 0);
     for (int i = threadIdx.x; i < n; i += 1024) {  // this thread's own stores above: visible
         const float xc = (float)((double)X[i] - cc[0]), yc = (float)((double)Y[i] - cc[1]),
                     zc = (float)((double)Z[i] - cc[2]);
         XC[i] = xc;
         YC[i] = yc;
         ZC[i] = zc;
+        if (a.PF) mx_point(a, i, xc, yc, zc, U[i], V[i], mk);
     }
 }
 
@@ -318,6 +375,7 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
         c[0] = n > 0 ? (double)a.X[p0] : 0.0; c[1] = n > 0 ? (double)a.Y[p0] : 0.0; c[2] = n > 0 ? (double)a.Z[p0] : 0.0;
     }
     float lo[5], hi[5];
+    const MxPixel mk = mx_pixel(a, 0);
 #pragma unroll
     for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
     for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
@@ -330,9 +388,12 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
         } else {
             v[0] = a.X[i]; v[1] = a.Y[i]; v[2] = a.Z[i]; v[3] = a.U[i]; v[4] = a.V[i];
         }
-        XC[i] = (float)((double)v[0] - c[0]);
-        YC[i] = (float)((double)v[1] - c[1]);
-        ZC[i] = (float)((double)v[2] - c[2]);
+        const float xc = (float)((double)v[0] - c[0]), yc = (float)((double)v[1] - c[1]),
+                    zc = (float)((double)v[2] - c[2]);
+        XC[i] = xc;
+        YC[i] = yc;
+        ZC[i] = zc;
+        if (a.PF) mx_point(a, i, xc, yc, zc, v[3], v[4], mk);
 #pragma unroll
         for (int k = 0; k < 5; ++k) { lo[k] = fminf(lo[k], v[k]); hi[k] = fmaxf(hi[k], v[k]); }
     }
@@ -397,7 +458,7 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
     if (threadIdx.x == 0) {
         pnp_frame_one(a, 1, 0, wsl, frame, fconst, c);
         if (a.best_key) *a.best_key = 0ull;
-        *a.queue = 0;
+        reset_pnp_queue(a.queue);
         *ticket = 0;  // for the next call (stream order)
     }
 }
@@ -442,9 +503,16 @@ __device__ __forceinline__ BandConsts band_consts(const double (&eps)[3], double
 __device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t, bool valid, const double *frame,
                                                 const double *cam, const float *fconst, float *fm);
 
+__device__ __forceinline__ void write_fmodel_mx(const double *R, const double *t, bool valid, const double *frame,
+                                                const double *cam, const float *fconst, float *fm);
+
 __device__ __forceinline__ void write_fmodel(const double *R, const double *t, bool valid, const double *frame,
                                              const double *cam, const float *fconst, float *fm, int form = 0) {
-    if (form == 1) {
+    if (form == 2 && fconst[11] != 0.f) {
+        write_fmodel_mx(R, t, valid, frame, cam, fconst, fm);
+        return;
+    }
+    if (form >= 1) {
         write_fmodel_sc(R, t, valid, frame, cam, fconst, fm);
         return;
     }
@@ -537,10 +605,125 @@ __device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t
     fm[15] = fits ? (float)((b + a * Zp) * (1.0 + 1e-6)) : __builtin_inff();  // constant band (CB kernels)
 }
 
+// The band constants of the scaled form (write_fmodel_sc) from the camera-frame evaluation error
+// bounds eps (rows x y z) and the row magnitudes mag: {a, b, zg, b + a Zp}; fits = false when a
+// quantity of the test could leave the f32 range (then b = +inf: every pair recounted exactly)
+struct ScBand {
+    double a, b, zg, bcb, Zp, qmax;
+};
+__device__ __forceinline__ ScBand sc_band(const double (&eps)[3], const double (&mag)[3], double fx, double fy,
+                                          double wmax, double T, double s, const float *fconst) {
+    ScBand r;
+    const double D0 = 1.01 * (fx * eps[0] + fy * eps[1] + eps[2] * (fx + fy) * wmax);
+    r.zg = 100.0 * (fmax(eps[0], eps[1]) + wmax * eps[2]) + 2.02 * eps[2] + 1e-30;
+    const double Cp = 2.0 * (double)fconst[7], Trelp = (double)fconst[6] + 1e-6 * T;
+    const double c1 = Cp / s;
+    r.Zp = s * (mag[2] + eps[2]) * (1.0 + 1e-6);
+    r.a = 1.01 * (D0 * (2.002 + 2.0 * c1) + (c1 * (2.002 + c1) + Trelp / T) * r.Zp);
+    r.b = 1.01 * D0 * D0;
+    const double zr = r.zg + eps[2];
+    const double Kq = D0 + Cp * zr + sqrt(T * 1.00001) * zr;
+    r.b = fmax(r.b, (1.0 + 1e-6) * Kq * Kq);
+    r.b = fmax(r.b, T * r.zg * r.zg * (1.0 + 1e-5));
+    const double umax = (double)fconst[7] / (2.5 * kU32);
+    r.qmax = fx * mag[0] + fy * mag[1] + umax * (mag[2] + eps[2]) + D0;
+    r.bcb = (r.b + r.a * r.Zp) * (1.0 + 1e-6);
+    return r;
+}
+
+// MFMA record (k_pnp_score_mf, DESIGN.md "Scoring: MFMA form").  The three rows of the scaled
+// form, (xs, ys, z') = sc_r (R_r . XC + t'_r) with sc = (-fx, -fy, sqrt(T)), are the A operands of
+// v_mfma_f32_32x32x16_f16: per row the coefficients of XC, YC, ZC and of the constant feature
+// (sc_r t'_r), all of one hypothesis scaled by lambda = 2^k so that the largest lies in
+// (2^14, 2^15], split into f16 hi = RN(A) and lo = RN(A - hi) (stored x 2^11).  The kernel forms
+// sum_k (hi_k + lo_k)(Bhi_k + Blo_k) with the point operands of mx_point; the test then runs on
+// lambda-scaled quantities, exactly as on the unscaled ones (powers of 2), with a' = lambda a and
+// b' = lambda^2 b.  Error of one row's output (lambda units), per feature k:
+//   |dA_k| |B~_k| + |A_k| |dB_k|   (dA_k: this hypothesis' exact split error, plus the f16
+//                                   subnormal operands in case the matrix core flushes them; lo
+//                                   is stored x 2^11 and faces B x 2^-11 (mx_point), so it is
+//                                   normal unless |A_k| < 2^-14; dB_k <= 2^-21 |B_k| + 2^-13 with
+//                                   the same allowance for both copies of B)
+//   + 2^-20 sum_k |A~_k| |B~_k|     (16 exact f32 products summed in round-to-nearest f32 in
+//                                   any order: gamma_15 < 16u)
+// in camera units eps_r = that / (lambda |sc_r|) + the centring and f64 terms of write_fmodel_sc,
+// about 3x its 8u (r1 B + |t'|).  Layout: f16 hi rows 0..2 (4 each: XC YC ZC 1) | f16 lo x 2^11
+// rows | f32 { a', b', zg, b'_cb }.
+__device__ __forceinline__ void write_fmodel_mx(const double *R, const double *t, bool valid, const double *frame,
+                                                const double *cam, const float *fconst, float *fm) {
+    _Float16 *hm = reinterpret_cast<_Float16 *>(fm);
+    if (!valid) {  // the kernel's decided-outlier form: xs = 1 (D = 1), b' = -inf
+#pragma unroll
+        for (int q = 0; q < kFModelStride; ++q) fm[q] = 0.f;
+        hm[3] = (_Float16)1.0f;
+        fm[13] = -__builtin_inff();
+        fm[14] = -1.f;
+        fm[15] = -__builtin_inff();
+        return;
+    }
+    const double B = frame[3], rho = frame[4], cmax = frame[5], wmax = frame[6];
+    const double fx = fabs(cam[0]), fy = fabs(cam[1]);
+    const double T = fconst[4];
+    const bool t_ok = T > 1e-12 && T < 1e30;
+    const double s = t_ok ? sqrt(T) : 1.0;
+    const double sc[3] = {-cam[0], -cam[1], s};
+    double A[3][4], r1[3], mag[3], tp[3];
+    double M = 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        tp[r] = R[3 * r] * frame[0] + R[3 * r + 1] * frame[1] + R[3 * r + 2] * frame[2] + t[r];
+        r1[r] = fabs(R[3 * r]) + fabs(R[3 * r + 1]) + fabs(R[3 * r + 2]);
+        mag[r] = r1[r] * B + fabs(tp[r]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) A[r][k] = sc[r] * R[3 * r + k];
+        A[r][3] = sc[r] * tp[r];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) M = fmax(M, fabs(A[r][k]));
+    }
+    int e = 0;
+    (void)frexp(M, &e);  // M = m 2^e, m in [0.5, 1)
+    const int kx = min(120, max(-120, 15 - e));
+    const double lam = ldexp(1.0, kx);
+    const double Bs = B * (1.0 + 0x1p-20) + 0x1p-14;  // >= |B~_k| of every point (k < 3)
+    double eps[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        double dA = 0.0, SA = 0.0, AB = 0.0;  // sum dA_k Bmax_k, sum_{k<3} |A_k|, sum |A_k| Bmax_k
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double v = A[r][k] * lam;
+            const _Float16 hi = (_Float16)(float)v;
+            const _Float16 lo = (_Float16)(float)((v - (double)hi) * 0x1p11);  // lo x 2^11: normal unless v is tiny
+            hm[4 * r + k] = hi;
+            hm[12 + 4 * r + k] = lo;
+            const double h = (double)hi, l = (double)lo * 0x1p-11;
+            double d = fabs(v - h - l);
+            if (fabs(h) < 0x1p-14) d += fabs(h);  // subnormal operands: allow for a flush to zero
+            if (fabs((double)lo) < 0x1p-14) d += fabs(l);
+            const double bm = k < 3 ? Bs : 1.0;
+            dA += d * bm;
+            AB += fabs(v) * bm;
+            if (k < 3) SA += fabs(v);
+        }
+        // A side + B side (2^-21 relative on XC YC ZC, 2^-13 absolute) + the accumulation (16u: 16
+        // exact products summed in round-to-nearest f32, any order)
+        const double err = 1.001 * (dA + 0x1p-21 * AB + 0x1p-13 * SA + 0x1p-20 * (AB + dA + 0x1p-13 * SA + 1.0));
+        eps[r] = err / (lam * fabs(sc[r])) + r1[r] * rho + 4e-15 * (r1[r] * cmax + fabs(t[r]));
+    }
+    ScBand bd = sc_band(eps, mag, fx, fy, wmax, T, s, fconst);
+    const double ap = bd.a * lam, bp = bd.b * lam * lam, cbp = bd.bcb * lam * lam;
+    const bool fits = t_ok && M > 0.0 && bd.qmax * lam < 1e17 && bd.Zp * lam < 1e17 && ap * bd.Zp * lam < 1e30 &&
+                      bp < 1e30 && cbp < 1e30 && bp > 1e-30;
+    fm[12] = fits ? (float)ap : 0.f;
+    fm[13] = fits ? (float)bp : __builtin_inff();
+    fm[14] = (float)bd.zg;
+    fm[15] = fits ? (float)cbp : __builtin_inff();
+}
+
 __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
     const int prob = blockIdx.y;
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
-    if (h == 0 && prob == 0 && a.queue) *a.queue = 0;  // the scoring launch that follows starts its queue at 0
+    if (h == 0 && prob == 0 && a.queue) reset_pnp_queue(a.queue);  // the scoring launch that follows starts at 0
     if (h >= H) return;
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
     const double *m = a.models + rec * kModelStride;
@@ -556,7 +739,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     const int hl = blockIdx.x * blockDim.x + threadIdx.x;
     // every round's scoring launch follows a solve on the same stream: reset its work queue here
     if (hl == 0 && prob == 0) {
-        if (a.queue) *a.queue = 0;
+        if (a.queue) reset_pnp_queue(a.queue);
     }
     if (hl >= H) return;
     const int64_t h = hyp_begin + hl;
@@ -610,7 +793,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
     const int hl = gt >> 2, cand = gt & 3;
     if (gt == 0 && prob == 0) {
-        if (a.queue) *a.queue = 0;
+        if (a.queue) reset_pnp_queue(a.queue);
     }
     const bool live = hl < H;  // the 4 lanes of a hypothesis share it: shuffles stay in the group
     const int64_t h = hyp_begin + hl;
@@ -1138,6 +1321,86 @@ __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p
     return cnt;
 }
 
+// One work unit of the scaled-form kernel: hypotheses [h0, h0 + nh) of problem prob (records at
+// rec0) over the points [start, n) of the problem (p0 its first point).  The unit's HB records are
+// staged in mlds; the counts are added atomically into zeroed counts.  Shared with
+// k_pnp_score_mf, which runs its problems outside the f16 operand range through it.
+template <int P, int HB, bool CB = false>
+__device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
+                                        int lane, int wave, int (*red)[HB], float *mlds, int32_t *__restrict__ counts) {
+    constexpr int kStride = 4 * 64 * P;  // points one pass of the block covers: one cell
+    const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
+    const float cx = fc[2], cy = fc[3], inv_s = fc[9];
+    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+    if (threadIdx.x < HB) {
+        // one thread per record; past the round or no model: z' = 0, xs = 1 (D = 1 > 0, a
+        // decided outlier) and b = -inf (never undecided)
+        const int hq = threadIdx.x;
+        float *dst = mlds + hq * kFModelStride;
+        const float *src = a.fmodels + (rec0 + hq) * kFModelStride;
+        const bool valid = hq < nh && src[14] >= 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dst[q] = valid ? src[q] : 0.f;
+        if (!valid) {
+            dst[9] = 1.f;
+            dst[13] = -__builtin_inff();
+            dst[15] = -__builtin_inff();
+        }
+    }
+    __syncthreads();
+    const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
+    const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
+
+    int cnt = 0;
+    for (int base = start + wave * 64 * P; base < n; base += kStride) {
+        float px[P], py[P], pz[P], pu[P], pv[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int i = base + j * 64 + lane;
+            const bool in = i < n;
+            const int ii = in ? i : 0;
+            const float x = XC[ii], y = YC[ii], z = ZC[ii], uu = U[ii], vv = V[ii];
+            // out of range or a non-finite coordinate: a pixel at 3e38 at the centre's depth
+            // makes the pair a decided outlier (or D = xs^2 + ys^2 >= 0 when z' = 0)
+            const bool ok = in && __builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z) &&
+                            __builtin_isfinite(uu) && __builtin_isfinite(vv);
+            px[j] = ok ? x : 0.f;
+            py[j] = ok ? y : 0.f;
+            pz[j] = ok ? z : 0.f;
+            pu[j] = ok ? (uu - cx) * inv_s : 3.0e38f;
+            pv[j] = ok ? (vv - cy) * inv_s : 3.0e38f;
+        }
+        int ccl = 0;        // lane h: hypothesis h's fast count (D < 0) of this tile
+        uint32_t wund = 0;  // bit h: hypothesis h has an undecided pair (wave-uniform)
+#pragma unroll 4
+        for (int h = 0; h < HB; ++h) {
+            const float *m = mlds + h * kFModelStride;
+            int cc = 0;
+            float tmin = __builtin_inff();
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const ScPair r = sc_pair(m, px[j], py[j], pz[j], pu[j], pv[j]);
+                cc += __popcll(__ballot(r.D < 0.f));
+                tmin = __builtin_fminf(tmin, CB ? __builtin_fabsf(r.D) : r.t);
+            }
+            const uint64_t und = __ballot(!(tmin > m[CB ? 15 : 13]));
+            // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
+            // operands would exceed the constant bus); cc and h are SALU results: no hazard
+            asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
+            wund |= und ? (1u << h) : 0u;
+        }
+        cnt += ccl;
+        if (__builtin_expect(wund != 0, 0))
+            cnt += sc_fallback<P, CB>(a, prob, p0, n, rec0, base, lane, wund, mlds, px, py, pz, pu, pv);
+    }
+    if (lane < HB) red[wave][lane] = cnt;
+    __syncthreads();
+    if (wave == 0 && lane < nh) {
+        const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+        if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
+    }
+}
+
 // Work units (launch_sc): the tiles (problem, 32 hypotheses) are numbered problem-major; the
 // first tb of them are one unit each (all their points, one pass of the block per cell of
 // 64 x 4 x P points), the rest one unit per cell, so the queue ends with cell-sized units that
@@ -1179,81 +1442,451 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         const int n_all = (int)(a.offsets[prob + 1] - p0);
         const int start = c0 * kStride;
         const int n = min(n_all, c1 * kStride);  // this unit's points: [start, n)
-        if (start >= n_all) {  // a cell past a short problem of a batch (uniform)
-            __syncthreads();   // every thread has read unit_s before it is rewritten
-            continue;
-        }
-        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
-        const float cx = fc[2], cy = fc[3], inv_s = fc[9];
-        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-        if (threadIdx.x < HB) {
-            // one thread per record; past the round or no model: z' = 0, xs = 1 (D = 1 > 0, a
-            // decided outlier) and b = -inf (never undecided)
-            const int hq = threadIdx.x;
-            float *dst = mlds + hq * kFModelStride;
-            const float *src = a.fmodels + (rec0 + hq) * kFModelStride;
-            const bool valid = hq < nh && src[14] >= 0.f;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) dst[q] = valid ? src[q] : 0.f;
-            if (!valid) {
-                dst[9] = 1.f;
-                dst[13] = -__builtin_inff();
-                dst[15] = -__builtin_inff();
-            }
-        }
-        __syncthreads();
-        const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
-        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
-
-        int cnt = 0;
-        for (int base = start + wave * 64 * P; base < n; base += kStride) {
-            float px[P], py[P], pz[P], pu[P], pv[P];
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-                const int i = base + j * 64 + lane;
-                const bool in = i < n;
-                const int ii = in ? i : 0;
-                const float x = XC[ii], y = YC[ii], z = ZC[ii], uu = U[ii], vv = V[ii];
-                // out of range or a non-finite coordinate: a pixel at 3e38 at the centre's depth
-                // makes the pair a decided outlier (or D = xs^2 + ys^2 >= 0 when z' = 0)
-                const bool ok = in && __builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z) &&
-                                __builtin_isfinite(uu) && __builtin_isfinite(vv);
-                px[j] = ok ? x : 0.f;
-                py[j] = ok ? y : 0.f;
-                pz[j] = ok ? z : 0.f;
-                pu[j] = ok ? (uu - cx) * inv_s : 3.0e38f;
-                pv[j] = ok ? (vv - cy) * inv_s : 3.0e38f;
-            }
-            int ccl = 0;        // lane h: hypothesis h's fast count (D < 0) of this tile
-            uint32_t wund = 0;  // bit h: hypothesis h has an undecided pair (wave-uniform)
-#pragma unroll 4
-            for (int h = 0; h < HB; ++h) {
-                const float *m = mlds + h * kFModelStride;
-                int cc = 0;
-                float tmin = __builtin_inff();
-#pragma unroll
-                for (int j = 0; j < P; ++j) {
-                    const ScPair r = sc_pair(m, px[j], py[j], pz[j], pu[j], pv[j]);
-                    cc += __popcll(__ballot(r.D < 0.f));
-                    tmin = __builtin_fminf(tmin, CB ? __builtin_fabsf(r.D) : r.t);
-                }
-                const uint64_t und = __ballot(!(tmin > m[CB ? 15 : 13]));
-                // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
-                // operands would exceed the constant bus); cc and h are SALU results: no hazard
-                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
-                wund |= und ? (1u << h) : 0u;
-            }
-            cnt += ccl;
-            if (__builtin_expect(wund != 0, 0))
-                cnt += sc_fallback<P, CB>(a, prob, p0, n, rec0, base, lane, wund, mlds, px, py, pz, pu, pv);
-        }
-        if (lane < HB) red[wave][lane] = cnt;
-        __syncthreads();
-        if (wave == 0 && lane < nh) {
-            const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-            if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
-        }
+        if (start < n_all)  // else a cell past a short problem of a batch (uniform)
+            sc_unit<P, HB, CB>(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
         __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA scoring kernel (variant 60; records of write_fmodel_mx, points of mx_point).
+//
+// xs, ys, z' of 8 hypotheses x 32 points come out of one v_mfma_f32_32x32x16_f16: the A operand
+// (32 rows x K 16) holds row r of hypothesis 8t + i/4 in row i (i % 4 = r; r = 3 unused) as
+// [hi x4 | hi x4] (lanes 0-31, K 0-7) and [lo x4 | lo x4] (lanes 32-63, K 8-15); the B operand
+// (K 16 x 32 points) is every point's PF record [hi XC YC ZC 1 | lo XC YC ZC 0] in both halves,
+// so the sum over K is (hi + lo)(Bhi + Blo) for each feature (the four products of a feature are
+// exact in f32).  Output map (gfx950): column = lane & 31, row = (reg & 3) + 8 (reg >> 2) +
+// 4 (lane >> 5), so lane (c, half) holds xs ys z' of hypotheses 8t + 2g + half (g = 0..3) at
+// point c in registers 4g .. 4g + 2.  The VALU then runs the scaled-form test of
+// k_pnp_score_sc on them (q1 q2 D: 5, t: 1, count: 1, band minimum: 0.5 per pair):
+//   count: the sign bit of D (D is never -0 or NaN: D = -z'^2 + X with X = q1^2 + q2^2 >= +0,
+//          and the staged operands are finite), two tiles' bits as 0xFF bytes (v_perm_b32)
+//          summed into 255 x the count (v_sad_u8);
+//   band:  min3 of the t's of both tiles per slot, compared with b' every CHK iterations.
+// A wave runs 2 x 32 points per iteration over all 32 hypotheses of the unit (4 MFMA groups);
+// a flagged (slot, window) is recomputed (the same MFMA, the same VALU bits) and its undecided
+// pairs take the exact f64 test (pnp_err), as sc_fallback does, so counts equal the exact
+// kernel's.  Problems whose centred coordinates leave the f16 range (fconst[11] = 0) carry
+// form-1 records and run the sc_unit body.
+// ---------------------------------------------------------------------------
+typedef _Float16 mf_h8 __attribute__((ext_vector_type(8)));
+typedef float mf_f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float mf_min3(float a, float b, float c) {
+    float d;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));  // no canonicalising v_max
+    return d;
+}
+__device__ __forceinline__ uint32_t mf_sgn(float x) { return __float_as_uint(x) >> 31; }
+// c + 255 ([a < 0] + [b < 0]) in two instructions: v_perm_b32 gathers the two sign bits as 0x00 /
+// 0xFF bytes (selectors 9, 11: a byte of copies of bit 31 of src1, src0; 12: zero) and v_sad_u8
+// adds the bytes (sum of |byte - 0|) to c
+__device__ __forceinline__ uint32_t mf_cnt255(uint32_t c, float a, float b) {
+    return __builtin_amdgcn_sad_u8(__builtin_amdgcn_perm(__float_as_uint(a), __float_as_uint(b), 0x0C0C0B09u), 0u, c);
+}
+
+struct MfPair {
+    float D, t;
+};
+// the test quantities of slot g of an MFMA output (lambda units; the expressions of sc_pair)
+__device__ __forceinline__ MfPair mf_pair(const mf_f16v &x, int g, float2 uv, float ag) {
+    const float z = x[4 * g + 2];
+    const float q1 = __builtin_fmaf(uv.x, z, x[4 * g]);
+    const float q2 = __builtin_fmaf(uv.y, z, x[4 * g + 1]);
+    const float D = __builtin_fmaf(-z, z, __builtin_fmaf(q1, q1, q2 * q2));
+    const float tt = __builtin_fmaf(-ag, __builtin_fabsf(z), __builtin_fabsf(D));
+    return MfPair{D, tt};
+}
+
+
+// global-memory view of a pointer: the kernel's PnpArgs also reaches an out-of-line function by
+// reference, after which the compiler no longer infers the address space of its pointer fields
+// and would issue flat loads (counted in lgkmcnt with the LDS reads of the hot loop)
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *gview(const T *p) {
+    return (const __attribute__((address_space(1))) T *)p;
+}
+
+// one iteration's point operands (tiles [base, base + 32) and [base + 32, base + 64) of the unit)
+typedef uint32_t mf_u4 __attribute__((ext_vector_type(4)));
+typedef float mf_f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t mf_u2 __attribute__((ext_vector_type(2)));
+// (lanes 0-31 load a point's first PF record, lanes 32-63 its x 2^-11 copy: hf = lane >> 5)
+__device__ __forceinline__ void mf_load_full(const uint4 *__restrict__ PFg, const float2 *__restrict__ UVg, int base,
+                                             int col, int hf, mf_h8 &Ba, mf_h8 &Bb, float2 &ua, float2 &ub) {
+    const auto PF = gview(reinterpret_cast<const mf_u4 *>(PFg));
+    const auto UV = gview(reinterpret_cast<const mf_f2 *>(UVg));
+    const int ia = base + col, ib = ia + 32;
+    const mf_u4 pa = PF[2 * ia + hf], pb = PF[2 * ib + hf];
+    const mf_f2 va = UV[ia], vb = UV[ib];
+    Ba = __builtin_bit_cast(mf_h8, pa);
+    Bb = __builtin_bit_cast(mf_h8, pb);
+    ua = make_float2(va.x, va.y);
+    ub = make_float2(vb.x, vb.y);
+}
+__device__ __forceinline__ void mf_load_part(const uint4 *__restrict__ PFg, const float2 *__restrict__ UVg, int base,
+                                             int n, int col, int hf, mf_h8 &Ba, mf_h8 &Bb, float2 &ua, float2 &ub) {
+    const auto PF = gview(reinterpret_cast<const mf_u4 *>(PFg));
+    const auto UV = gview(reinterpret_cast<const mf_f2 *>(UVg));
+    const int ia = base + col, ib = ia + 32;
+    // the origin with its constant feature (1, or 2^-11 in the scaled copy)
+    const mf_u4 none = {0u, hf ? 0x10000000u : 0x3C000000u, 0u, 0u};
+    const mf_f2 far = {3.0e38f, 3.0e38f};
+    const mf_u4 pa = ia < n ? PF[2 * ia + hf] : none, pb = ib < n ? PF[2 * ib + hf] : none;
+    const mf_f2 va = ia < n ? UV[ia] : far, vb = ib < n ? UV[ib] : far;
+    Ba = __builtin_bit_cast(mf_h8, pa);
+    Bb = __builtin_bit_cast(mf_h8, pb);
+    ua = make_float2(va.x, va.y);
+    ub = make_float2(vb.x, vb.y);
+}
+__device__ __forceinline__ void mf_load(const uint4 *__restrict__ PF, const float2 *__restrict__ UV, int base, int n,
+                                        int col, int hf, mf_h8 &Ba, mf_h8 &Bb, float2 &ua, float2 &ub) {
+    if (base + 64 <= n)
+        mf_load_full(PF, UV, base, col, hf, Ba, Bb, ua, ub);
+    else
+        mf_load_part(PF, UV, base, n, col, hf, Ba, Bb, ua, ub);
+}
+
+// the A operand of MFMA group t for this lane (row col & 31: hypothesis 8t + (col >> 2), row
+// col & 3; hi in lanes 0-31, lo in 32-63); past the round: xs = 1 (D = 1, a decided outlier)
+__device__ __forceinline__ mf_h8 mf_operand(const float *__restrict__ recs, int t, int col, int half, int nh) {
+    const int r = col & 3, j = 8 * t + (col >> 2);
+    mf_u2 w = {0u, 0u};
+    if (r < 3 && j < nh)
+        w = *gview(reinterpret_cast<const mf_u2 *>(reinterpret_cast<const char *>(recs + j * kFModelStride) +
+                                                   half * 24 + r * 8));
+    else if (r == 0 && half == 0 && j >= nh)
+        w.y = 0x3C000000u;
+    const mf_u4 v = {w.x, w.y, w.x, w.y};
+    return __builtin_bit_cast(mf_h8, v);
+}
+
+// work unit -> (problem, first hypothesis, hypotheses, point range) of a k_pnp_score_mf launch
+struct MfUnit {
+    int prob, nh, start, n;
+    int64_t h0, p0;
+};
+__device__ __forceinline__ MfUnit mf_decode(const PnpArgs &a, int unit, int64_t hyp_begin, int32_t H, int tb, int cells,
+                                            int cell_pts) {
+    constexpr int HB = 32;
+    const int tiles_per_prob = (H + HB - 1) / HB;
+    int tile, c0, c1;
+    if (unit < tb) {
+        tile = unit;
+        c0 = 0;
+        c1 = cells;
+    } else {
+        tile = tb + (unit - tb) / cells;
+        c0 = (unit - tb) % cells;
+        c1 = c0 + 1;
+    }
+    MfUnit u;
+    u.prob = tile / tiles_per_prob;
+    u.h0 = hyp_begin + (int64_t)(tile % tiles_per_prob) * HB;
+    u.nh = (int)min((int64_t)HB, hyp_begin + H - u.h0);
+    u.p0 = a.offsets[u.prob];
+    const int n_all = (int)(a.offsets[u.prob + 1] - u.p0);
+    u.start = c0 * cell_pts;
+    u.n = min(n_all, c1 * cell_pts);
+    return u;
+}
+
+// exact recount of one flagged iteration (one wave): the MFMA and the VALU test of the flagged
+// slots are redone (same operands, same bits) and each undecided pair's fast verdict (D < 0) is
+// replaced by the exact f64 test (pnp_err); the corrections are added to the counts
+__device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfUnit &u, int base, uint32_t fl, int col, int half,
+                                           int32_t *__restrict__ counts) {
+    const int64_t p0 = u.p0, rec0 = (int64_t)u.prob * a.hyp_stride + u.h0;
+    const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
+    mf_h8 Ba, Bb;
+    float2 ua, ub;
+    mf_load(a.PF + 2 * p0, a.UV + p0, base, u.n, col, half, Ba, Bb, ua, ub);
+    const double *cm = a.cams + 4 * u.prob;
+    const Cam k{cm[0], cm[1], cm[2], cm[3]};
+    const float thr2 = a.thr2[u.prob];
+#pragma unroll 1
+    for (int t = 0; t < 4; ++t) {
+        const uint32_t ft = (fl >> (4 * t)) & 15u;
+        if (!ft) continue;
+        const mf_h8 At = mf_operand(recs, t, col, half, u.nh);
+        const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
+        const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            if (!((ft >> g) & 1u)) continue;  // uniform
+            const int j = 8 * t + 2 * g + half;  // this lane's hypothesis
+            const bool live = j < u.nh;
+            const float ag = live ? recs[j * kFModelStride + 12] : 0.f;
+            const float bg = live ? recs[j * kFModelStride + 13] : -__builtin_inff();
+            const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
+            const int ia = base + col, ib = ia + 32;
+            const bool wa = !(ra.t > bg) && ia < u.n, wb = !(rb.t > bg) && ib < u.n;
+            if (wa || wb) {
+                const double *md = a.models + (rec0 + j) * kModelStride;
+                const bool mv = md[kValidSlot] != 0.0;
+                int c = 0;
+#pragma unroll 1
+                for (int tile = 0; tile < 2; ++tile) {
+                    if (!(tile ? wb : wa)) continue;
+                    const int64_t q = p0 + (tile ? ib : ia);
+                    const bool ex = mv && pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q],
+                                                  a.U[q], a.V[q]) <= thr2;
+                    c += (ex ? 1 : 0) - ((tile ? rb.D : ra.D) < 0.f ? 1 : 0);
+                }
+                if (c) atomicAdd(&counts[rec0 + j], c);
+            }
+        }
+    }
+}
+
+// the form-1 body for problems outside the f16 operand range (rare: kept out of line, so its
+// registers do not constrain the MFMA loop's)
+__device__ __attribute__((noinline)) void mf_sc_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0,
+                                                     int start, int n, int lane, int wave, int (*red)[32], float *mlds,
+                                                     int32_t *__restrict__ counts) {
+    sc_unit<8, 32>(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
+}
+
+constexpr int kWrec = 64;  // flagged-window list of a wave (k_pnp_score_mf)
+
+// CHK: iterations (2 x 32 points per wave) per check window of the band minimum
+template <bool FB, int CHK, int PD, bool RA>
+__device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, int64_t h0, int nh, int64_t p0, int start,
+                                        int n, int lane, int wave, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
+                                        mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *wcnt,
+                                        int32_t *__restrict__ counts) {
+    constexpr int HB = 32;
+    const int col = lane & 31, half = lane >> 5;
+    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+    const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
+    if (threadIdx.x < HB) {
+        // a' and b' of slot (t, g, half) = hypothesis 8t + 2g + half; past the round: b' = -inf
+        // (records without a model carry a' = 0, b' = -inf themselves)
+        const int j = threadIdx.x;
+        const bool v = j < nh;
+        ab[0][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 12] : 0.f;
+        ab[1][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 13] : -__builtin_inff();
+    }
+    {  // the unit's A operands (the same for the 4 waves): thread (t, lane) stages group t's
+        const int tl = threadIdx.x & 63;
+        alds[threadIdx.x >> 6][tl] = mf_operand(recs, threadIdx.x >> 6, tl & 31, tl >> 5, nh);
+    }
+    __syncthreads();
+    const uint4 *__restrict__ PF = a.PF + 2 * p0;
+    const float2 *__restrict__ UV = a.UV + p0;
+    uint32_t vc[4][4];
+    float tm[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            vc[t][g] = 0u;
+            tm[t][g] = __builtin_inff();
+        }
+    int nw = 0;  // flagged windows in the wave's list (uniform)
+    int it = 0;  // iterations in the current window
+    // Per iteration: counts and the band minimum (min3 of both tiles per slot).  At the end of a
+    // window (CHK iterations, or the wave's last) the minima are compared with b'; a window with
+    // a flagged slot is recorded for k_pnp_mf_recount (FB = false: timing experiments only, no
+    // check at all).  Full iterations run without bounds checks; a partial one follows the loop.
+    const int b0 = start + wave * 64;
+    const int iters = n > b0 ? (n - b0 + 255) / 256 : 0;
+    // the point operands of iteration i, loaded PD iterations ahead (PD = 0: at its start)
+    // RA: the A operands and slopes a' in registers for the whole unit (else read from LDS per
+    // iteration, fewer registers)
+    mf_h8 Ar[4];
+    float4 avr[4];
+    if constexpr (RA) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            Ar[t] = alds[t][lane];
+            avr[t] = *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
+        }
+    }
+    auto body = [&](int i, const mf_h8 &Ba, const mf_h8 &Bb, const float2 &ua, const float2 &ub)
+        __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const mf_h8 At = RA ? Ar[t] : alds[t][lane];
+            const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
+            const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
+            const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
+                const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
+                vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
+                if (FB) tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
+            }
+        }
+        if (FB && (++it == CHK || i == iters - 1)) {  // end of a check window (uniform)
+            uint32_t fl = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
+                    fl |= __ballot(!(tm[t][g] > bg)) ? (1u << (4 * t + g)) : 0u;
+                    tm[t][g] = __builtin_inff();
+                }
+            }
+            if (__builtin_expect(fl != 0, 0)) {
+                // kept in the wave's LDS list (first iteration, window length in bits 24..),
+                // appended to a.mf_list with the unit's (one atomic per block), or at once by the
+                // wave when its list is full
+                if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)(i + 1 - it) | ((uint32_t)it << 24), fl);
+                if (++nw == kWrec) {
+                    __builtin_amdgcn_wave_barrier();
+                    int slot = 0;
+                    if (lane == 0) slot = atomicAdd(a.queue + 2, kWrec);
+                    slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0));
+                    if (slot + lane < a.mf_cap) {
+                        const uint2 w = wrec[wave][lane];
+                        a.mf_list[slot + lane] = MfFlag{unit, b0 + 256 * (int)(w.x & 0xFFFFFFu), w.y, (int)(w.x >> 24)};
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    nw = 0;
+                }
+            }
+            it = 0;
+        }
+    };
+    const int full = n >= b0 + 64 ? (n - b0 - 64) / 256 + 1 : 0;  // iterations with 64 points in range
+    if constexpr (PD == 0) {
+        for (int i = 0; i < full; ++i) {
+            mf_h8 Ba, Bb;
+            float2 ua, ub;
+            mf_load_full(PF, UV, b0 + 256 * i, col, half, Ba, Bb, ua, ub);
+            body(i, Ba, Bb, ua, ub);
+        }
+    } else {  // one iteration ahead: the next operands are in flight while this one computes
+        mf_h8 Ba, Bb, Na, Nb;
+        float2 ua, ub, na, nb;
+        if (full > 0) mf_load_full(PF, UV, b0, col, half, Ba, Bb, ua, ub);
+        for (int i = 0; i < full; ++i) {
+            if (i + 1 < full) mf_load_full(PF, UV, b0 + 256 * (i + 1), col, half, Na, Nb, na, nb);
+            body(i, Ba, Bb, ua, ub);
+            Ba = Na;
+            Bb = Nb;
+            ua = na;
+            ub = nb;
+        }
+    }
+    if (full < iters) {
+        mf_h8 Ba, Bb;
+        float2 ua, ub;
+        mf_load_part(PF, UV, b0 + 256 * full, n, col, half, Ba, Bb, ua, ub);
+        body(full, Ba, Bb, ua, ub);
+    }
+    if (lane == 0) wcnt[wave] = nw;
+    // counts: lane (c, half) of wave w holds slot (t, g)'s count over its points; hypothesis j =
+    // 8t + 2g + half sums 4 waves x 32 lanes (8 threads of 16 values each, then a shuffle tree)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) cl[wave][4 * t + g][lane] = vc[t][g];
+    __syncthreads();
+    {
+        const int j = threadIdx.x >> 3, p = threadIdx.x & 7;
+        const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + 4 * p;
+        uint32_t sum = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) sum += cl[w][slot][l0 + l];
+        sum += __shfl_xor(sum, 1);
+        sum += __shfl_xor(sum, 2);
+        sum += __shfl_xor(sum, 4);
+        if (p == 0 && j < nh && sum) atomicAdd(&counts[rec0 + j], (int)(sum / 255u));
+    }
+    if (FB) {  // the waves' flagged iterations: one atomic for the block, then a store per record
+        if (threadIdx.x == 0) {
+            const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+            wcnt[4] = tot ? atomicAdd(a.queue + 2, tot) : 0;
+        }
+        __syncthreads();
+        int off = wcnt[4];
+        for (int w = 0; w < wave; ++w) off += wcnt[w];
+        if (lane < wcnt[wave] && off + lane < a.mf_cap) {
+            const uint2 w = wrec[wave][lane];
+            a.mf_list[off + lane] = MfFlag{unit, b0 + 256 * (int)(w.x & 0xFFFFFFu), w.y, (int)(w.x >> 24)};
+        }
+    }
+}
+
+// Phase 1: units from the queue (a.queue[0]); a unit's flagged iterations are appended to
+// a.mf_list (count a.queue[2]) and the unit is counted finished (a.queue[1]).  Phase 2, once the
+// unit queue is empty: every wave takes flagged records (a.queue[3]) after all units have
+// finished (their records are then complete) and recounts them.  A block only waits once every
+// unit has been taken by a running block, so the wait always ends.
+// W: minimum waves per SIMD the register budget must allow; PD: point operands loaded 0 / 1
+// iterations ahead
+template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_mf(
+    PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
+    int tb, int cells, int cell_pts) {
+    constexpr int HB = 32;
+    __shared__ int unit_s;
+    __shared__ uint32_t cl[4][16][64];
+    __shared__ __attribute__((aligned(16))) float ab[2][2][4][4];
+    __shared__ uint2 wrec[4][kWrec];
+    __shared__ int wcnt[5];
+    __shared__ mf_h8 alds[4][64];
+    __shared__ int red[4][HB];                                                 // sc_unit
+    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];  // sc_unit
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tiles_per_prob = (H + HB - 1) / HB;
+    const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
+    for (;;) {
+        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
+        __syncthreads();
+        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
+        if (unit >= n_units) break;  // uniform: every wave of every block reaches it
+        int tile, c0, c1;
+        if (unit < tb) {
+            tile = unit;
+            c0 = 0;
+            c1 = cells;
+        } else {
+            tile = tb + (unit - tb) / cells;
+            c0 = (unit - tb) % cells;
+            c1 = c0 + 1;
+        }
+        const int prob = tile / tiles_per_prob;
+        const int64_t h0 = hyp_begin + (int64_t)(tile % tiles_per_prob) * HB;
+        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+        const int64_t p0 = a.offsets[prob];
+        const int n_all = (int)(a.offsets[prob + 1] - p0);
+        const int start = c0 * cell_pts;
+        const int n = min(n_all, c1 * cell_pts);
+        if (start < n_all) {
+            if (a.fconst[(int64_t)prob * kFconstStride + 11] != 0.f)
+                mf_unit<FB, CHK, PD, RA>(a, unit, prob, h0, nh, p0, start, n, lane, wave, cl, ab, alds, wrec, wcnt, counts);
+            else
+                mf_sc_unit(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
+        }
+        __syncthreads();  // the unit's LDS and unit_s are rewritten by the next unit
+    }
+}
+
+// The exact recount of k_pnp_score_mf's flagged iterations (a.mf_list, count a.queue[2]): one
+// wave per record, grid-stride; the corrections are added to the counts.
+__global__ __launch_bounds__(256) void k_pnp_mf_recount(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
+                                                        int32_t *__restrict__ counts, int tb, int cells, int cell_pts) {
+    const int lane = threadIdx.x & 63;
+    const int col = lane & 31, half = lane >> 5;
+    const int nrec = (int)min((int64_t)a.queue[2], a.mf_cap);
+    const int tiles_per_prob = (H + 31) / 32;
+    const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
+    for (int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < nrec; r += (gridDim.x * blockDim.x) >> 6) {
+        const MfFlag f = a.mf_list[r];
+        if (f.unit < 0 || f.unit >= n_units) continue;  // a record always names a unit of the launch
+        const MfUnit u = mf_decode(a, f.unit, hyp_begin, H, tb, cells, cell_pts);
+        if (f.base < u.start || f.base >= u.n || f.iters < 1 || f.iters > 4) continue;
+        for (int w = 0; w < f.iters && f.base + 256 * w < u.n; ++w) mf_recount(a, u, f.base + 256 * w, f.fl, col, half, counts);
     }
 }
 
@@ -1668,7 +2301,7 @@ __global__ void k_pnp_init(int32_t P, int *__restrict__ ws, unsigned long long *
     for (int i = threadIdx.x; i < 10 * P; i += blockDim.x) ws[i] = i < 5 * P ? 0x7F7F7F7F : (int)0x80808080;
     if (threadIdx.x == 0) {
         if (key) *key = 0ull;
-        *queue = 0;
+        reset_pnp_queue(queue);
     }
 }
 
@@ -2151,7 +2784,10 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
     }
 }
 
-int score_record_form() { return g_score_variant >= 49 && g_score_variant <= 53 ? 1 : 0; }
+int score_record_form() {
+    if (g_score_variant >= 60 && g_score_variant <= 73) return 2;
+    return g_score_variant >= 49 && g_score_variant <= 53 ? 1 : 0;
+}
 
 // k_pnp_score_sc: whole-tile units for all but the last `resident` tiles, which go as one unit
 // per cell (64 x 4 x P points): the cells even out the blocks' finishing times (the queue's
@@ -2190,6 +2826,84 @@ static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H
         hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
                            a.rng_base + hyp_begin, a.best_key);
     }
+}
+
+// k_pnp_score_mf: whole-tile units, then one unit per cell for the last `resident` tiles (as
+// launch_sc); cells of 2048 points, halved (down to 256, one iteration per wave) while the units
+// would not fill the resident grid (an adaptive run's first rounds).  Every wave-iteration
+// appends at most one flagged record, so a launch whose bound exceeds a.mf_cap is split into
+// hypothesis chunks (counters reset before each).
+template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false>
+static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
+                            hipStream_t s) {
+    auto kern = k_pnp_score_mf<FB, CHK, W, PD, RA>;
+    static int resident = 0;
+    if (resident == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
+        resident = std::max(1, cus) * std::max(1, per_cu);
+    }
+    if (a.counts_out != counts) {
+        if (P_ == 1)
+            (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
+        else
+            (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P_, s);
+    }
+    const int64_t max_n = std::max<int64_t>(1, a.max_n);
+    auto plan = [&](int64_t Hc, int64_t &cell_pts, int64_t &cells, int64_t &tb, int64_t &units, int64_t &bound) {
+        const int64_t tiles = (int64_t)P_ * ((Hc + 31) / 32);
+        cell_pts = 2048;
+        while (cell_pts > 256 && tiles * ((max_n + cell_pts - 1) / cell_pts) < resident) cell_pts /= 2;
+        cells = (max_n + cell_pts - 1) / cell_pts;
+        const int64_t cell_tiles = std::min<int64_t>(tiles, g_sc_cell_tiles > 0 ? g_sc_cell_tiles : resident);
+        tb = tiles - cell_tiles;
+        units = tb + cell_tiles * cells;
+        bound = tb * ((max_n + 63) / 64 + 3) + cell_tiles * cells * ((cell_pts + 63) / 64 + 3);
+    };
+    int64_t cell_pts, cells, tb, units, bound;
+    plan(H, cell_pts, cells, tb, units, bound);
+    int64_t Hc = H;
+    if (FB && bound > a.mf_cap) {
+        const int64_t per_tile = (int64_t)P_ * std::max<int64_t>((max_n + 63) / 64 + 3, cells * ((256 + 63) / 64 + 3) +
+                                                                                           (max_n + 63) / 64);
+        const int64_t tiles_c = a.mf_cap / std::max<int64_t>(1, per_tile);
+        if (tiles_c < 1) return hipErrorOutOfMemory;  // one 32-hypothesis tile per problem exceeds the list
+        Hc = 32 * tiles_c;
+    }
+    PnpArgs ka = a;
+    ka.best_key = nullptr;  // reduced below from the complete counts
+    for (int64_t h = 0; h < H; h += Hc) {
+        const int32_t Hh = (int32_t)std::min<int64_t>(Hc, H - h);
+        if (Hc < H) {
+            plan(Hh, cell_pts, cells, tb, units, bound);
+            hipError_t e = hipMemsetAsync(a.queue, 0, 4 * sizeof(int), s);
+            if (e != hipSuccess) return e;
+        }
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, a.queue, counts, (int)tb,
+                           (int)cells, (int)cell_pts);
+        if (FB) {
+            static const bool dbg = getenv("RSAC_DBG_MF") != nullptr;  // diagnostics: flagged records per launch
+            if (dbg) {
+                int q[4] = {0, 0, 0, 0};
+                (void)hipMemcpyAsync(q, a.queue, sizeof q, hipMemcpyDeviceToHost, s);
+                (void)hipStreamSynchronize(s);
+                fprintf(stderr, "rsac mf: units %lld records %d of bound %lld (H %d, cells %lld x %lld)\n",
+                        (long long)units, q[2], (long long)bound, Hh, (long long)cells, (long long)cell_pts);
+            }
+            hipLaunchKernelGGL(k_pnp_mf_recount, dim3(std::max(1, resident / 2)), dim3(256), 0, s, ka, hyp_begin + h, Hh,
+                               P_, counts, (int)tb, (int)cells, (int)cell_pts);
+        }
+    }
+    if (a.best_key) {
+        unsigned g = cdiv(H, 1024);
+        if (g > 128) g = 128;
+        hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
+                           a.rng_base + hyp_begin, a.best_key);
+    }
+    return hipGetLastError();
 }
 
 // RSAC_SMALL_PP / RSAC_SMALL_TILES: tuning knobs of the small-round scoring instance
@@ -2267,6 +2981,20 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
                 else
                     launch_sc<8, 4>(a, P, hyp_begin, H, counts, s);
                 break;
+            case 60: return launch_mf<true, 2>(a, P, hyp_begin, H, counts, s);
+            case 61: return launch_mf<false, 1>(a, P, hyp_begin, H, counts, s);  // timing only: no recount
+            case 62: return launch_mf<true, 1>(a, P, hyp_begin, H, counts, s);
+            case 63: return launch_mf<true, 4>(a, P, hyp_begin, H, counts, s);
+            case 64: return launch_mf<true, 2, 3>(a, P, hyp_begin, H, counts, s);
+            case 65: return launch_mf<true, 4, 3>(a, P, hyp_begin, H, counts, s);
+            case 66: return launch_mf<true, 1, 3>(a, P, hyp_begin, H, counts, s);
+            case 67: return launch_mf<true, 2, 3, 1>(a, P, hyp_begin, H, counts, s);
+            case 68: return launch_mf<false, 1, 3, 1>(a, P, hyp_begin, H, counts, s);  // timing only
+            case 69: return launch_mf<true, 2, 2, 1>(a, P, hyp_begin, H, counts, s);
+            case 70: return launch_mf<true, 2, 3, 0, true>(a, P, hyp_begin, H, counts, s);
+            case 71: return launch_mf<true, 4, 3, 0, true>(a, P, hyp_begin, H, counts, s);
+            case 72: return launch_mf<false, 1, 3, 0, true>(a, P, hyp_begin, H, counts, s);  // timing only
+            case 73: return launch_mf<true, 2, 3, 1, true>(a, P, hyp_begin, H, counts, s);
             case 50: launch_sc<8, 5>(a, P, hyp_begin, H, counts, s); break;
             case 51: launch_sc<4, 4>(a, P, hyp_begin, H, counts, s); break;
             case 52: launch_sc<6, 4>(a, P, hyp_begin, H, counts, s); break;

@@ -97,8 +97,13 @@ RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* a
 /* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 49;
  * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 f32 MFMA tilings, 16..28 the
  * branch-free alpha-beta band tilings, 40..48 the alpha-beta band with the lean hypothesis
- * loop (48 = 42 with the small-round instance), 49..52 the scaled form (k_pnp_score_sc; 49
- * with the small-round instance)).  Counts, masks and models never depend on the variant. */
+ * loop (48 = 42 with the small-round instance), 49..53 the scaled form (k_pnp_score_sc; 49
+ * with the small-round instance), 60..73 the MFMA form (k_pnp_score_mf: xs ys z' by
+ * v_mfma_f32_32x32x16_f16 on f16 hi/lo operands; the band checked every 2 iterations; 61 and 68
+ * without the exact recount, timing only; 62, 63 checked every 1, 4 iterations; 64..66 = 60, 63,
+ * 62 at 3 waves per SIMD; 67 (68, 69) = 64 (61, 64 at 2 waves) with the point operands loaded one
+ * iteration ahead; 70..73 = 64, 65, 68 (timing only), 67 with the A operands and slopes in
+ * registers)).  Counts, masks and models never depend on the variant (61, 68, 72 excepted). */
 RSAC_EXPORT int rsac_set_score_variant(int variant);
 
 /* The pose refit (solvePnPRefineLM, main_v1.py:508-509) of a problem above 4096 points runs

@@ -166,6 +166,31 @@ def test_pnp_batched_ragged_equals_singles():
         assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
 
 
+@pytest.mark.parametrize("variant", [49, 60])
+def test_pnp_batched_mixed_scales_equals_oracle(variant):
+    # one batch, problems inside and outside the MFMA scorer's f16 operand range (centred
+    # coordinates above 2^15 or below 1/64 run the form-1 path of k_pnp_score_mf)
+    from rsac import _lib as L
+    base = [synth.pnp_problem(n, 0.4, seed=70 + i) for i, n in enumerate([3000, 1500, 2500, 800])]
+    scales = [1.0, 1e3, 1e-5, 1.0]
+    probs = []
+    for p, sc in zip(base, scales):
+        q = dict(p)
+        q["points3d"] = p["points3d"] * sc
+        probs.append(q)
+    L.check(L.lib().rsac_set_score_variant(variant))
+    try:
+        out = rsac.pnp_ransac_batched([p["points2d"] for p in probs], [p["points3d"] for p in probs],
+                                      [p["K"] for p in probs], 1500, 30.0, refine=False)
+    finally:
+        L.check(L.lib().rsac_set_score_variant(-1))
+    for p, (R, t, m, ni) in zip(probs, out):
+        ref = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 0.99, 1500, 0x5EED)
+        assert ni == ref["n_inliers"]
+        np.testing.assert_array_equal(m, ref["mask"])
+        assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+
+
 def test_k_sweep_batched():
     """testpro-K.py:58-75 as one batched call over the 27 intrinsics."""
     Ks = synth.testpro_k_candidates()
@@ -249,7 +274,7 @@ def test_degenerate_inputs():
 # variant (VALU f32, packed f32, MFMA) is checked, then the default is restored.
 # ---------------------------------------------------------------------------------------------
 SCORE_VARIANTS = [0, 1, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28,
-                  40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53]
+                  40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 60, 62, 63, 64, 65, 66, 67, 69, 70, 71, 73]
 
 
 @pytest.fixture(params=SCORE_VARIANTS)
