@@ -1326,7 +1326,8 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
         return fail(RSAC_EINVAL, "RSAC_F_ASYNC needs a device mask (RSAC_F_DEVICE_OUT)");
     hipStream_t s = pick_stream(c, stream);
     Staged st;
-    r = stage_points(c, pts3d, pts2d, 3, nullptr, 1, n, flags & ~RSAC_F_SAMPLER_OPENCV, s, st);
+    // device f64 inputs: the f32 conversion is fused into the frame launch of pnp_args
+    r = stage_points(c, pts3d, pts2d, 3, nullptr, 1, n, flags & ~RSAC_F_SAMPLER_OPENCV, s, st, true);
     if (r) return r;
     r = stage_tables(c, st, K, thr, s);
     if (r) return r;
@@ -1339,11 +1340,15 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
     r = pnp_args(c, st, flags, seed, n_hyps, hyp_begin, s, a, dkey);
     if (r) return r;
     const int32_t H = (int32_t)n_hyps;
-    HIPCHK(hipEventRecord(c->ev0, s));
+    const bool async = (flags & RSAC_F_ASYNC) != 0;
+    // timing events only for a synchronous call that reports stats: each event record in the
+    // stream costs a gap of several microseconds between the kernels around it
+    const bool timed = stats != nullptr && !async;
+    if (timed) HIPCHK(hipEventRecord(c->ev0, s));
     HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
-    HIPCHK(hipEventRecord(c->ev1, s));
+    if (timed) HIPCHK(hipEventRecord(c->ev1, s));
     HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
-    HIPCHK(hipEventRecord(c->ev2, s));
+    if (timed) HIPCHK(hipEventRecord(c->ev2, s));
     uint8_t *hmask_dev = nullptr;
     if (mask_out) {
         if (flags & RSAC_F_DEVICE_OUT) {
@@ -1353,7 +1358,6 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
             hmask_dev = c->mask.as<uint8_t>();
         }
     }
-    const bool async = (flags & RSAC_F_ASYNC) != 0;
     HIPCHK(launch_pnp_key_finish(a, n, dkey, hmask_dev, c->bestmodels.as<double>(), async ? model_out : nullptr,
                                  async ? key_out : nullptr, s));
     if (async) {
