@@ -11,12 +11,15 @@ struct EpnpStage1;
 struct EpnpStage2;
 
 // one flagged check window of k_pnp_score_mf (a wave's iterations of 2 x 32 points from `base` x
-// the 32 hypotheses of work unit `unit`, with an undecided pair in the slots of fl), recounted
-// exactly afterwards (k_pnp_mf_recount)
+// the 32 hypotheses of a work unit, with an undecided pair in the slots of fl), recounted exactly
+// afterwards (k_pnp_mf_recount)
 struct MfFlag {
-    int32_t unit, base;  // base: the window's first iteration (its points base + [0, 64))
-    uint32_t fl;         // bit 4t + g: slot g of MFMA group t (hypotheses 8t + 2g, 8t + 2g + 1)
-    int32_t iters;       // iterations in the window (the next ones at base + 256 k)
+    int64_t rec0, p0;  // the unit's first hypothesis record and its problem's first point
+    int32_t base;      // the window's first iteration (its points base + [0, 64))
+    int32_t n;         // the unit's point range ends at n
+    uint32_t fl;       // bit 4t + g: slot g of MFMA group t (hypotheses 8t + 2g, 8t + 2g + 1)
+    int16_t nh;        // hypotheses of the unit
+    int16_t iters;     // iterations in the window (the next ones at base + 256 k)
 };
 
 // PnP problem set on the device.  Problem p owns points [offsets[p],

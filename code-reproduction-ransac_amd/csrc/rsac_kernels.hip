@@ -1562,66 +1562,38 @@ __device__ __forceinline__ mf_h8 mf_operand(const float *__restrict__ recs, int 
     return __builtin_bit_cast(mf_h8, v);
 }
 
-// work unit -> (problem, first hypothesis, hypotheses, point range) of a k_pnp_score_mf launch
-struct MfUnit {
-    int prob, nh, start, n;
-    int64_t h0, p0;
-};
-__device__ __forceinline__ MfUnit mf_decode(const PnpArgs &a, int unit, int64_t hyp_begin, int32_t H, int tb, int cells,
-                                            int cell_pts) {
-    constexpr int HB = 32;
-    const int tiles_per_prob = (H + HB - 1) / HB;
-    int tile, c0, c1;
-    if (unit < tb) {
-        tile = unit;
-        c0 = 0;
-        c1 = cells;
-    } else {
-        tile = tb + (unit - tb) / cells;
-        c0 = (unit - tb) % cells;
-        c1 = c0 + 1;
-    }
-    MfUnit u;
-    u.prob = tile / tiles_per_prob;
-    u.h0 = hyp_begin + (int64_t)(tile % tiles_per_prob) * HB;
-    u.nh = (int)min((int64_t)HB, hyp_begin + H - u.h0);
-    u.p0 = a.offsets[u.prob];
-    const int n_all = (int)(a.offsets[u.prob + 1] - u.p0);
-    u.start = c0 * cell_pts;
-    u.n = min(n_all, c1 * cell_pts);
-    return u;
-}
-
 // exact recount of one flagged iteration (one wave): the MFMA and the VALU test of the flagged
 // slots are redone (same operands, same bits) and each undecided pair's fast verdict (D < 0) is
 // replaced by the exact f64 test (pnp_err); the corrections are added to the counts
-__device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfUnit &u, int base, uint32_t fl, int col, int half,
+__device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfFlag &f, int base, int col, int half,
                                            int32_t *__restrict__ counts) {
-    const int64_t p0 = u.p0, rec0 = (int64_t)u.prob * a.hyp_stride + u.h0;
+    const int64_t p0 = f.p0, rec0 = f.rec0;
+    const uint32_t fl = f.fl;
+    const int prob = (int)(rec0 / a.hyp_stride);
     const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
     mf_h8 Ba, Bb;
     float2 ua, ub;
-    mf_load(a.PF + 2 * p0, a.UV + p0, base, u.n, col, half, Ba, Bb, ua, ub);
-    const double *cm = a.cams + 4 * u.prob;
+    mf_load(a.PF + 2 * p0, a.UV + p0, base, f.n, col, half, Ba, Bb, ua, ub);
+    const double *cm = a.cams + 4 * prob;
     const Cam k{cm[0], cm[1], cm[2], cm[3]};
-    const float thr2 = a.thr2[u.prob];
+    const float thr2 = a.thr2[prob];
 #pragma unroll 1
     for (int t = 0; t < 4; ++t) {
         const uint32_t ft = (fl >> (4 * t)) & 15u;
         if (!ft) continue;
-        const mf_h8 At = mf_operand(recs, t, col, half, u.nh);
+        const mf_h8 At = mf_operand(recs, t, col, half, f.nh);
         const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
         const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             if (!((ft >> g) & 1u)) continue;  // uniform
             const int j = 8 * t + 2 * g + half;  // this lane's hypothesis
-            const bool live = j < u.nh;
+            const bool live = j < f.nh;
             const float ag = live ? recs[j * kFModelStride + 12] : 0.f;
             const float bg = live ? recs[j * kFModelStride + 13] : -__builtin_inff();
             const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
             const int ia = base + col, ib = ia + 32;
-            const bool wa = !(ra.t > bg) && ia < u.n, wb = !(rb.t > bg) && ib < u.n;
+            const bool wa = !(ra.t > bg) && ia < f.n, wb = !(rb.t > bg) && ib < f.n;
             if (wa || wb) {
                 const double *md = a.models + (rec0 + j) * kModelStride;
                 const bool mv = md[kValidSlot] != 0.0;
@@ -1744,7 +1716,8 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
                     slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0));
                     if (slot + lane < a.mf_cap) {
                         const uint2 w = wrec[wave][lane];
-                        a.mf_list[slot + lane] = MfFlag{unit, b0 + 256 * (int)(w.x & 0xFFFFFFu), w.y, (int)(w.x >> 24)};
+                        a.mf_list[slot + lane] = MfFlag{rec0, p0, b0 + 256 * (int)(w.x & 0xFFFFFFu), n, w.y, (int16_t)nh,
+                                                     (int16_t)(w.x >> 24)};
                     }
                     __builtin_amdgcn_wave_barrier();
                     nw = 0;
@@ -1811,7 +1784,8 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
         for (int w = 0; w < wave; ++w) off += wcnt[w];
         if (lane < wcnt[wave] && off + lane < a.mf_cap) {
             const uint2 w = wrec[wave][lane];
-            a.mf_list[off + lane] = MfFlag{unit, b0 + 256 * (int)(w.x & 0xFFFFFFu), w.y, (int)(w.x >> 24)};
+            a.mf_list[off + lane] = MfFlag{rec0, p0, b0 + 256 * (int)(w.x & 0xFFFFFFu), n, w.y, (int16_t)nh,
+                                          (int16_t)(w.x >> 24)};
         }
     }
 }
@@ -1879,14 +1853,20 @@ __global__ __launch_bounds__(256) void k_pnp_mf_recount(PnpArgs a, int64_t hyp_b
     const int lane = threadIdx.x & 63;
     const int col = lane & 31, half = lane >> 5;
     const int nrec = (int)min((int64_t)a.queue[2], a.mf_cap);
-    const int tiles_per_prob = (H + 31) / 32;
-    const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
-    for (int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < nrec; r += (gridDim.x * blockDim.x) >> 6) {
-        const MfFlag f = a.mf_list[r];
-        if (f.unit < 0 || f.unit >= n_units) continue;  // a record always names a unit of the launch
-        const MfUnit u = mf_decode(a, f.unit, hyp_begin, H, tb, cells, cell_pts);
-        if (f.base < u.start || f.base >= u.n || f.iters < 1 || f.iters > 4) continue;
-        for (int w = 0; w < f.iters && f.base + 256 * w < u.n; ++w) mf_recount(a, u, f.base + 256 * w, f.fl, col, half, counts);
+    const int step = (gridDim.x * blockDim.x) >> 6;
+    int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    MfFlag f;
+    if (r < nrec) f = a.mf_list[r];
+    for (; r < nrec; r += step) {
+        const MfFlag cur = f;
+        if (r + step < nrec) f = a.mf_list[r + step];  // the next record in flight meanwhile
+        // a record always names a unit of this launch; the checks only keep a corrupted list from
+        // addressing outside the problem set
+        if (cur.rec0 < 0 || cur.nh < 1 || cur.nh > 32 || cur.iters < 1 || cur.iters > 4 || cur.base < 0 ||
+            cur.n < cur.base || cur.rec0 / a.hyp_stride >= n_prob)
+            continue;
+        for (int w = 0; w < cur.iters && cur.base + 256 * w < cur.n; ++w)
+            mf_recount(a, cur, cur.base + 256 * w, col, half, counts);
     }
 }
 
@@ -2707,23 +2687,36 @@ hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t 
     return hipGetLastError();
 }
 
+static int64_t small_round_tiles();
+
+// a round of at most small_round_tiles() hypothesis tiles (an adaptive run's first 256) is
+// scored by the scaled-form small-round instance even under the MFMA variants: the records of
+// such a round are written in form 1 (the solve and the scoring launch apply the same rule)
+static bool small_round(int32_t P, int32_t H) { return (int64_t)P * ((H + 31) / 32) <= small_round_tiles(); }
+static PnpArgs round_args(const PnpArgs &a, int32_t P, int32_t H) {
+    PnpArgs ka = a;
+    if (ka.fform == 2 && small_round(P, H)) ka.fform = 1;
+    return ka;
+}
+
 hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_t s) {
-    hipLaunchKernelGGL(k_pnp_fmodels, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, H);
+    hipLaunchKernelGGL(k_pnp_fmodels, dim3(cdiv(H, 256), P), dim3(256), 0, s, round_args(a, P, H), H);
     return hipGetLastError();
 }
 
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
+    const PnpArgs ka = round_args(a, P, H);
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     if ((int64_t)P * H <= solve4_max_hyps())
-        hipLaunchKernelGGL(k_pnp_solve4, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, a, hyp_begin, H);
+        hipLaunchKernelGGL(k_pnp_solve4, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     else
-        hipLaunchKernelGGL(k_pnp_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H);
+        hipLaunchKernelGGL(k_pnp_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     return hipGetLastError();
 }
 
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
 static const int64_t g_sc_cell_tiles = [] { const char *e = getenv("RSAC_SC_CELL_TILES"); return e ? atoll(e) : 0; }();
-constexpr int kDefaultScoreVariant = 49;  // fastest measured on MI355X
+constexpr int kDefaultScoreVariant = 73;  // fastest measured on MI355X
 static int g_score_variant = kDefaultScoreVariant;
 void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
 
@@ -2893,8 +2886,10 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
                 fprintf(stderr, "rsac mf: units %lld records %d of bound %lld (H %d, cells %lld x %lld)\n",
                         (long long)units, q[2], (long long)bound, Hh, (long long)cells, (long long)cell_pts);
             }
-            hipLaunchKernelGGL(k_pnp_mf_recount, dim3(std::max(1, resident / 2)), dim3(256), 0, s, ka, hyp_begin + h, Hh,
-                               P_, counts, (int)tb, (int)cells, (int)cell_pts);
+            // one wave per record, records latency-bound (a chain of dependent loads): a wide grid
+            // (blocks past the record count exit at once)
+            hipLaunchKernelGGL(k_pnp_mf_recount, dim3(2048), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, counts,
+                               (int)tb, (int)cells, (int)cell_pts);
         }
     }
     if (a.best_key) {
@@ -2921,6 +2916,10 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     if (a.max_n > 0 && a.max_n <= kLanePts) {
         hipLaunchKernelGGL(k_pnp_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
     } else if (a.fmodels && !a.exact_only) {
+        if (a.fform == 2 && small_round(P, H)) {  // form-1 records (round_args): the small-round instance
+            launch_sc<2, 5>(a, P, hyp_begin, H, counts, s);
+            return hipGetLastError();
+        }
         switch (g_score_variant) {
             case 1: launch_f32<4, 32>(a, P, hyp_begin, H, counts, s); break;
             case 2: launch_f32<8, 64>(a, P, hyp_begin, H, counts, s); break;

@@ -94,7 +94,7 @@ RSAC_EXPORT const char *rsac_last_error(void);
 RSAC_EXPORT int rsac_abi_version(void);
 RSAC_EXPORT int rsac_device_count(void);
 RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
-/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 49;
+/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 73;
  * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 f32 MFMA tilings, 16..28 the
  * branch-free alpha-beta band tilings, 40..48 the alpha-beta band with the lean hypothesis
  * loop (48 = 42 with the small-round instance), 49..53 the scaled form (k_pnp_score_sc; 49
