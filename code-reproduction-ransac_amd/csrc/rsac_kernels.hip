@@ -1613,10 +1613,19 @@ __device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfFlag &f, in
 }
 
 // the form-1 body for problems outside the f16 operand range (rare: kept out of line, so its
-// registers do not constrain the MFMA loop's)
-__device__ __attribute__((noinline)) void mf_sc_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0,
+// registers do not constrain the MFMA loop's).  The arguments are read from the kernel's argument
+// segment (PnpArgs is the first kernel argument, offset 0): passing the kernel parameter by
+// reference would give it an address, and the compiler then copies all of PnpArgs to scratch
+// in every wave and reads every field in the hot kernel from there (≈50 MB of scratch writes per
+// C2 launch)
+typedef const __attribute__((address_space(4))) PnpArgs *KernargPnp;
+__device__ __forceinline__ KernargPnp kernarg_pnp() {
+    return (KernargPnp)__builtin_amdgcn_kernarg_segment_ptr();
+}
+__device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, int64_t h0, int nh, int64_t p0,
                                                      int start, int n, int lane, int wave, int (*red)[32], float *mlds,
                                                      int32_t *__restrict__ counts) {
+    const PnpArgs a = *(const PnpArgs *)ka;  // generic view (the host pass has no address spaces)
     sc_unit<8, 32>(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
 }
 
@@ -1840,7 +1849,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
             if (a.fconst[(int64_t)prob * kFconstStride + 11] != 0.f)
                 mf_unit<FB, CHK, PD, RA>(a, unit, prob, h0, nh, p0, start, n, lane, wave, cl, ab, alds, wrec, wcnt, counts);
             else
-                mf_sc_unit(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
+                mf_sc_unit(kernarg_pnp(), prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
         }
         __syncthreads();  // the unit's LDS and unit_s are rewritten by the next unit
     }
