@@ -333,7 +333,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     a.best_key = best_key;
     const int P = st.P;
     const int64_t N = st.total;
-    HIPCHK(c->queue.ensure(64));
+    HIPCHK(c->queue.ensure(4096));  // kQWords ints (rsac_kernels.hip)
     HIPCHK(c->centred.ensure(sizeof(float) * 3 * std::max<int64_t>(N, 1)));
     HIPCHK(c->bounds_ws.ensure(sizeof(int32_t) * 10 * P));
     HIPCHK(c->frame.ensure(sizeof(double) * kFrameStride * P));
@@ -384,7 +384,7 @@ int fm_prefilter(rsac_ctx *c, HomArgs &a, int32_t P, uint32_t flags, hipStream_t
     HIPCHK(c->bounds_ws.ensure(sizeof(int32_t) * 10 * P));  // >= 8 per problem
     a.fmodels = c->fmodels.as<float>();
     a.fbounds = c->bounds_ws.as<int>();
-    HIPCHK(c->queue.ensure(64));
+    HIPCHK(c->queue.ensure(4096));  // kQWords ints (rsac_kernels.hip)
     a.fm_queue = c->queue.as<int>() + 8;  // its own counter (the PnP kernels use word 0)
     HIPCHK(launch_fm_bounds(a, P, a.max_n, c->bounds_ws.as<int>(), s));
     return RSAC_OK;
@@ -1019,7 +1019,7 @@ void rsac_destroy(rsac_ctx *c) {
 }
 
 int rsac_set_score_variant(int variant) {
-    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 53) && (variant < 60 || variant > 73)))
+    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 53) && (variant < 60 || variant > 79)))
         return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
     set_score_variant(variant);
     return RSAC_OK;

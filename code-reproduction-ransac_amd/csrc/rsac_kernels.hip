@@ -71,11 +71,25 @@ constexpr double kU32 = 5.9604644775390625e-08;  // 2^-24, unit roundoff of floa
 
 // the PnP scoring launch's counters (PnpArgs::queue, words 0..3): unit queue, units finished,
 // flagged-iteration records appended, records taken (k_pnp_score_mf); reset before each launch
+// Split work queue (k_pnp_score_mw): kQSub unit counters and kQSub flagged-record counters, one
+// 128-byte line each.  Atomics on one address serialise (≈10 ns each on MI355X, measured: a
+// single counter for 62 500 wave units cost ≈0.45 ms), so block b draws its units from counter
+// b % kQSub (units u ≡ b mod kQSub) and appends its flagged records to segment b % kQSub.
+constexpr int kQSub = 8;
+constexpr int kQWords = 32 + 64 * kQSub;  // ints of the queue buffer used by the PnP kernels
+__device__ __forceinline__ int *unit_queue(int *q, int k) { return q + 32 + 32 * k; }
+__device__ __forceinline__ int *rec_queue(int *q, int k) { return q + 32 + 32 * kQSub + 32 * k; }
+
 __device__ __forceinline__ void reset_pnp_queue(int *q) {
     q[0] = 0;
     q[1] = 0;
     q[2] = 0;
     q[3] = 0;
+#pragma unroll
+    for (int k = 0; k < kQSub; ++k) {
+        *unit_queue(q, k) = 0;
+        *rec_queue(q, k) = 0;
+    }
 }
 
 // ws: [0, 5P) mins, [5P, 10P) maxes of X Y Z U V (ordered-int encoding), pre-set by memset
@@ -1721,11 +1735,13 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
                 if (++nw == kWrec) {
                     __builtin_amdgcn_wave_barrier();
                     int slot = 0;
-                    if (lane == 0) slot = atomicAdd(a.queue + 2, kWrec);
+                    const int qk = blockIdx.x % kQSub;
+                    const int64_t seg = a.mf_cap / kQSub;
+                    if (lane == 0) slot = atomicAdd(rec_queue(a.queue, qk), kWrec);
                     slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0));
-                    if (slot + lane < a.mf_cap) {
+                    if (slot + lane < seg) {
                         const uint2 w = wrec[wave][lane];
-                        a.mf_list[slot + lane] = MfFlag{rec0, p0, b0 + 256 * (int)(w.x & 0xFFFFFFu), n, w.y, (int16_t)nh,
+                        a.mf_list[qk * seg + slot + lane] = MfFlag{rec0, p0, b0 + 256 * (int)(w.x & 0xFFFFFFu), n, w.y, (int16_t)nh,
                                                      (int16_t)(w.x >> 24)};
                     }
                     __builtin_amdgcn_wave_barrier();
@@ -1786,14 +1802,15 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
     if (FB) {  // the waves' flagged iterations: one atomic for the block, then a store per record
         if (threadIdx.x == 0) {
             const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-            wcnt[4] = tot ? atomicAdd(a.queue + 2, tot) : 0;
+            wcnt[4] = tot ? atomicAdd(rec_queue(a.queue, blockIdx.x % kQSub), tot) : 0;
         }
         __syncthreads();
         int off = wcnt[4];
         for (int w = 0; w < wave; ++w) off += wcnt[w];
-        if (lane < wcnt[wave] && off + lane < a.mf_cap) {
+        const int64_t seg = a.mf_cap / kQSub;
+        if (lane < wcnt[wave] && off + lane < seg) {
             const uint2 w = wrec[wave][lane];
-            a.mf_list[off + lane] = MfFlag{rec0, p0, b0 + 256 * (int)(w.x & 0xFFFFFFu), n, w.y, (int16_t)nh,
+            a.mf_list[blockIdx.x % kQSub * seg + off + lane] = MfFlag{rec0, p0, b0 + 256 * (int)(w.x & 0xFFFFFFu), n, w.y, (int16_t)nh,
                                           (int16_t)(w.x >> 24)};
         }
     }
@@ -1824,7 +1841,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     const int tiles_per_prob = (H + HB - 1) / HB;
     const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
     for (;;) {
-        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
+        if (threadIdx.x == 0) unit_s = blockIdx.x % kQSub + kQSub * atomicAdd(unit_queue(queue, blockIdx.x % kQSub), 1);
         __syncthreads();
         const int unit = __builtin_amdgcn_readfirstlane(unit_s);
         if (unit >= n_units) break;  // uniform: every wave of every block reaches it
@@ -1857,25 +1874,317 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
 
 // The exact recount of k_pnp_score_mf's flagged iterations (a.mf_list, count a.queue[2]): one
 // wave per record, grid-stride; the corrections are added to the counts.
+// segs = kQSub: the records of k_pnp_score_mw, in kQSub segments of a.mf_cap / kQSub (record r
+// of the concatenation maps to its segment through the counts); 0: one list (k_pnp_score_mf)
+__device__ __forceinline__ int64_t mf_rec_index(const int *cnt, int segs, int64_t seg, int r) {
+    if (!segs) return r;
+    int k = 0;
+    while (k < segs - 1 && r >= cnt[k]) r -= cnt[k++];
+    return k * seg + r;
+}
 __global__ __launch_bounds__(256) void k_pnp_mf_recount(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
-                                                        int32_t *__restrict__ counts, int tb, int cells, int cell_pts) {
+                                                        int32_t *__restrict__ counts, int segs, int, int) {
     const int lane = threadIdx.x & 63;
     const int col = lane & 31, half = lane >> 5;
-    const int nrec = (int)min((int64_t)a.queue[2], a.mf_cap);
+    const int64_t seg = segs ? a.mf_cap / segs : a.mf_cap;
+    int cnt[kQSub];
+    int nrec = 0;
+    if (segs) {
+#pragma unroll
+        for (int k = 0; k < kQSub; ++k) {
+            cnt[k] = (int)min((int64_t)*rec_queue(a.queue, k), seg);
+            nrec += cnt[k];
+        }
+    } else
+        nrec = (int)min((int64_t)a.queue[2], a.mf_cap);
     const int step = (gridDim.x * blockDim.x) >> 6;
     int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     MfFlag f;
-    if (r < nrec) f = a.mf_list[r];
+    if (r < nrec) f = a.mf_list[mf_rec_index(cnt, segs, seg, r)];
     for (; r < nrec; r += step) {
         const MfFlag cur = f;
-        if (r + step < nrec) f = a.mf_list[r + step];  // the next record in flight meanwhile
+        if (r + step < nrec) f = a.mf_list[mf_rec_index(cnt, segs, seg, r + step)];  // the next record in flight
         // a record always names a unit of this launch; the checks only keep a corrupted list from
         // addressing outside the problem set
         if (cur.rec0 < 0 || cur.nh < 1 || cur.nh > 32 || cur.iters < 1 || cur.iters > 4 || cur.base < 0 ||
             cur.n < cur.base || cur.rec0 / a.hyp_stride >= n_prob)
             continue;
-        for (int w = 0; w < cur.iters && cur.base + 256 * w < cur.n; ++w)
-            mf_recount(a, cur, cur.base + 256 * w, col, half, counts);
+        // window iterations are 256 points apart (k_pnp_score_mf: 4 waves x 64), or 64 apart
+        // (k_pnp_score_mw: bits 16.. of fl = 1)
+        const int stride = (cur.fl >> 16) ? 64 : 256;
+        for (int w = 0; w < cur.iters && cur.base + stride * w < cur.n; ++w)
+            mf_recount(a, cur, cur.base + stride * w, col, half, counts);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-autonomous MFMA scoring kernel (variant 74): the arithmetic, operands, records and
+// flagged-window recount of k_pnp_score_mf, but every wave pulls its own work units (32
+// hypotheses x one cell of points) from the queue.  No block barrier anywhere: in the block form
+// the 4 waves of a block (on 4 SIMDs, each shared with other blocks' waves) met at 4-5 barriers
+// per unit, and each unit also waited on its queue atomic, its record staging and its record
+// append in turn (≈3 µs per unit, measured by the cell-count sweep).  Here the next unit's
+// atomic is issued when the current unit starts, the unit's A operands and slopes go straight
+// from the records into registers, its band constants b' into the wave's own LDS, and the
+// counts are transposed through the wave's LDS; a wave waiting on a load leaves its SIMD to the
+// other two waves.  An iteration covers 2 x 32 consecutive points (base, base + 32), so a
+// flagged window's iterations are 64 points apart (fl bit 16 tells k_pnp_mf_recount).
+// Units: tiles [0, ta) in cb cells of cbig points, then the remaining tiles in cs cells of
+// csmall points (the queue's tail).  Problems outside the f16 operand range (fconst[11] = 0)
+// are counted with the exact f64 test, one lane per point (never at C2-C5 scales).
+// ---------------------------------------------------------------------------
+constexpr int kMwWaves = 4;  // waves per block (blocks only group waves for the launch)
+
+// the A operand of MFMA group t (mf_operand's values) from an unconditional load: the index is
+// clamped into the unit and the value replaced afterwards, so the unit's loads issue together
+// instead of one conditional load (and wait) after another
+__device__ __forceinline__ mf_h8 mw_operand(const float *__restrict__ recs, int t, int col, int half, int nh) {
+    const int r = col & 3, j = 8 * t + (col >> 2);
+    const int jj = min(j, nh - 1), rr = min(r, 2);
+    mf_u2 w = *gview(reinterpret_cast<const mf_u2 *>(reinterpret_cast<const char *>(recs + jj * kFModelStride) +
+                                                     half * 24 + rr * 8));
+    if (!(r < 3 && j < nh)) {
+        w.x = 0u;
+        w.y = (r == 0 && half == 0 && j >= nh) ? 0x3C000000u : 0u;
+    }
+    const mf_u4 v = {w.x, w.y, w.x, w.y};
+    return __builtin_bit_cast(mf_h8, v);
+}
+
+// the wave's flagged windows (LDS, full records) to segment qk of a.mf_list (a.mf_cap / kQSub
+// records each): one atomic for the slots
+__device__ __forceinline__ void mw_flush(const PnpArgs &a, int qk, const MfFlag *lst, int nw, int lane) {
+    const int64_t seg = a.mf_cap / kQSub;
+    int slot = 0;
+    if (lane == 0) slot = atomicAdd(rec_queue(a.queue, qk), nw);
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    if (lane < nw && slot + lane < seg) a.mf_list[qk * seg + slot + lane] = lst[lane];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the list is rewritten after this
+}
+
+template <int CHK, int PD, int XP = 0>
+__device__ __forceinline__ void mw_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
+                                        int lane, int qk, uint32_t (*cw)[64], float (*bl)[2][16], MfFlag *lst,
+                                        int &nw, int32_t *__restrict__ counts) {
+    const int col = lane & 31, half = lane >> 5;
+    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+    const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
+    const uint4 *__restrict__ PF = a.PF + 2 * p0;
+    const float2 *__restrict__ UV = a.UV + p0;
+    const int iters = (n - start + 63) / 64;
+    const int full = (n - start) / 64;  // iterations with 64 points in range
+    // the unit's loads, issued together: A operands, a' / b', the first point operands
+    mf_h8 Ar[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) Ar[t] = mw_operand(recs, t, col, half, nh);
+    const int j = col;  // a' (lanes 0-31) and b' (lanes 32-63) of hypothesis j
+    float abv = gview(recs)[min(j, nh - 1) * kFModelStride + 12 + half];
+    mf_h8 Ba, Bb;
+    float2 ua, ub;
+    if (full > 0)
+        mf_load_full(PF, UV, start, col, half, Ba, Bb, ua, ub);
+    else
+        mf_load_part(PF, UV, start, n, col, half, Ba, Bb, ua, ub);
+    bl[half][j & 1][4 * (j >> 3) + ((j >> 1) & 3)] = j < nh ? abv : (half ? -__builtin_inff() : 0.f);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t vc[4][4];
+    float tm[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            vc[t][g] = 0u;
+            tm[t][g] = __builtin_inff();
+        }
+    int it = 0;  // iterations in the current window
+    auto body = [&](int i, const mf_h8 &Ba, const mf_h8 &Bb, const float2 &ua, const float2 &ub)
+        __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float4 av = *reinterpret_cast<const float4 *>(&bl[0][half][4 * t]);
+            const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Ba, mf_f16v{}, 0, 0, 0);
+            const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Bb, mf_f16v{}, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
+                const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
+                vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
+                tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
+            }
+        }
+        if (++it == CHK || i == iters - 1) {  // end of a check window (uniform)
+            uint32_t fl = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float4 bv = *reinterpret_cast<const float4 *>(&bl[1][half][4 * t]);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
+                    fl |= __ballot(!(tm[t][g] > bg)) ? (1u << (4 * t + g)) : 0u;
+                    tm[t][g] = __builtin_inff();
+                }
+            }
+            if (__builtin_expect(fl != 0, 0)) {
+                if (lane == 0)
+                    lst[nw] = MfFlag{rec0, p0, start + 64 * (i + 1 - it), n, fl | (1u << 16), (int16_t)nh, (int16_t)it};
+                if (++nw == kWrec) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    mw_flush(a, qk, lst, nw, lane);
+                    nw = 0;
+                }
+            }
+            it = 0;
+        }
+    };
+    if constexpr (PD == 0) {
+        for (int i = 0; i < full; ++i) {
+            if (i > 0) mf_load_full(PF, UV, start + 64 * i, col, half, Ba, Bb, ua, ub);
+            body(i, Ba, Bb, ua, ub);
+        }
+    } else {  // one iteration ahead
+        mf_h8 Na, Nb;
+        float2 na, nb;
+        for (int i = 0; i < full; ++i) {
+            if (i + 1 < full) mf_load_full(PF, UV, start + 64 * (i + 1), col, half, Na, Nb, na, nb);
+            body(i, Ba, Bb, ua, ub);
+            Ba = Na;
+            Bb = Nb;
+            ua = na;
+            ub = nb;
+        }
+    }
+    if (full < iters) {
+        if (full > 0) mf_load_part(PF, UV, start + 64 * full, n, col, half, Ba, Bb, ua, ub);
+        body(full, Ba, Bb, ua, ub);
+    }
+    // counts: lane (c, half) holds slot (t, g)'s count of hypothesis 8t + 2g + half over its
+    // points; transposed through the wave's LDS, lane pair (2j, 2j + 1) sums hypothesis j's 32
+    // columns (16 each, then one shuffle)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) cw[4 * t + g][lane] = vc[t][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    {
+        const int jh = lane >> 1, p = lane & 1;
+        const int slot = 4 * (jh >> 3) + ((jh >> 1) & 3), c0 = (jh & 1) * 32 + 16 * p;
+        const uint4 *src = reinterpret_cast<const uint4 *>(&cw[slot][c0]);
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = src[q];
+            sum += v.x + v.y + v.z + v.w;
+        }
+        sum += __shfl_xor(sum, 1);
+        if (XP & 2) {  // timing experiment: no count atomics
+            if (p == 0 && jh < nh && sum == 0xFFFFFFFFu) counts[rec0 + jh] = 0;
+        } else if (p == 0 && jh < nh && sum)
+            atomicAdd(&counts[rec0 + jh], (int)(sum / 255u));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // cw and bl are rewritten by the next unit
+}
+
+// the exact f64 count of one unit, one lane per point (problems outside the f16 operand range)
+__device__ __forceinline__ void mw_exact_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start,
+                                              int n, int lane, int32_t *__restrict__ counts) {
+    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+    const double *cm = a.cams + 4 * prob;
+    const Cam k{cm[0], cm[1], cm[2], cm[3]};
+    const float thr2 = a.thr2[prob];
+#pragma unroll 1
+    for (int j = 0; j < nh; ++j) {
+        const double *md = a.models + (rec0 + j) * kModelStride;
+        if (md[kValidSlot] == 0.0) continue;  // uniform
+        int c = 0;
+#pragma unroll 1
+        for (int i = start + lane; i < n; i += 64) {
+            const int64_t q = p0 + i;
+            c += pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <= thr2 ? 1 : 0;
+        }
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+        if (lane == 0 && c) atomicAdd(&counts[rec0 + j], c);
+    }
+}
+
+// XP: timing experiments only (counts wrong): bit 0 static unit assignment (no queue atomics),
+// bit 1 no count atomics
+template <int CHK, int PD, int XP = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_pnp_score_mw(
+    PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
+    int ta, int cb, int cbig, int cs, int csmall) {
+    constexpr int HB = 32;
+    __shared__ __attribute__((aligned(16))) uint32_t cw[kMwWaves][16][64];
+    __shared__ __attribute__((aligned(16))) float bl[kMwWaves][2][2][16];  // a' / b' [half][slot]
+    __shared__ MfFlag lst[kMwWaves][kWrec];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tpp = (H + HB - 1) / HB;
+    const int tiles = tpp * n_prob;
+    const int ua = ta * cb;
+    const int n_units = ua + (tiles - ta) * cs;
+    int nw = 0;  // the wave's flagged windows not yet appended to a.mf_list
+    // this block's share of the units: u = qk + kQSub i, i drawn from counter qk
+    const int qk = blockIdx.x % kQSub;
+    const int nq = n_units > qk ? (n_units - qk + kQSub - 1) / kQSub : 0;
+    int *const uq = unit_queue(queue, qk);
+    int ci = 0;
+    const int gw = blockIdx.x / kQSub * kMwWaves + wave;                              // XP & 1: static
+    const int nwq = ((int)gridDim.x - qk + kQSub - 1) / kQSub * kMwWaves;           // waves sharing qk
+    if (XP & 1)
+        ci = gw;
+    else {
+        if (lane == 0) ci = atomicAdd(uq, 1);
+        ci = __builtin_amdgcn_readfirstlane(ci);
+    }
+    int last_prob = -1, n_all = 0;
+    int64_t p0 = 0;
+    bool in_range = false;
+    while (ci < nq) {  // uniform per wave: every wave reaches the end of its queue
+        const int cur = qk + kQSub * ci;
+        // the next unit's index, in flight while this unit runs (no atomic optimizer here: its
+        // per-lane fix-up would wait for the result at once); waited for below
+        int nx = ci + nwq;
+        if (!(XP & 1) && lane == 0)
+            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "+v"(nx) : "v"(uq), "v"(1) : "memory");
+        int tile, start, len;
+        if (cur < ua) {
+            tile = cur / cb;
+            start = (cur % cb) * cbig;
+            len = cbig;
+        } else {
+            tile = ta + (cur - ua) / cs;
+            start = ((cur - ua) % cs) * csmall;
+            len = csmall;
+        }
+        const int prob = tile / tpp;
+        const int64_t h0 = hyp_begin + (int64_t)(tile % tpp) * HB;
+        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
+        if (prob != last_prob) {  // uniform; once per call for one problem
+            p0 = a.offsets[prob];
+            n_all = (int)(a.offsets[prob + 1] - p0);
+            in_range = a.fconst[(int64_t)prob * kFconstStride + 11] != 0.f;
+            last_prob = prob;
+        }
+        const int n = min(n_all, start + len);
+        if (start < n_all) {  // else a cell past a short problem of a batch
+            if (in_range)
+                mw_unit<CHK, PD, XP>(a, prob, h0, nh, p0, start, n, lane, qk, cw[wave], bl[wave], lst[wave], nw,
+                                     counts);
+            else
+                mw_exact_unit(a, prob, h0, nh, p0, start, n, lane, counts);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(nx)::"memory");
+        ci = __builtin_amdgcn_readfirstlane(nx);
+    }
+    if (nw) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        mw_flush(a, qk, lst[wave], nw, lane);
     }
 }
 
@@ -2787,7 +3096,7 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
 }
 
 int score_record_form() {
-    if (g_score_variant >= 60 && g_score_variant <= 73) return 2;
+    if (g_score_variant >= 60 && g_score_variant <= 79) return 2;
     return g_score_variant >= 49 && g_score_variant <= 53 ? 1 : 0;
 }
 
@@ -2867,10 +3176,12 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
     int64_t cell_pts, cells, tb, units, bound;
     plan(H, cell_pts, cells, tb, units, bound);
     int64_t Hc = H;
-    if (FB && bound > a.mf_cap) {
+    // a block's records go to segment blockIdx % kQSub of a.mf_list: bound each by its share
+    const int64_t seg = a.mf_cap / kQSub;
+    if (FB && (bound + kQSub - 1) / kQSub + 2 * ((max_n + 63) / 64 + 3) > seg) {
         const int64_t per_tile = (int64_t)P_ * std::max<int64_t>((max_n + 63) / 64 + 3, cells * ((256 + 63) / 64 + 3) +
                                                                                            (max_n + 63) / 64);
-        const int64_t tiles_c = a.mf_cap / std::max<int64_t>(1, per_tile);
+        const int64_t tiles_c = seg / std::max<int64_t>(1, per_tile);
         if (tiles_c < 1) return hipErrorOutOfMemory;  // one 32-hypothesis tile per problem exceeds the list
         Hc = 32 * tiles_c;
     }
@@ -2880,7 +3191,7 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
         const int32_t Hh = (int32_t)std::min<int64_t>(Hc, H - h);
         if (Hc < H) {
             plan(Hh, cell_pts, cells, tb, units, bound);
-            hipError_t e = hipMemsetAsync(a.queue, 0, 4 * sizeof(int), s);
+            hipError_t e = hipMemsetAsync(a.queue + 32, 0, (kQWords - 32) * sizeof(int), s);
             if (e != hipSuccess) return e;
         }
         const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
@@ -2889,17 +3200,116 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
         if (FB) {
             static const bool dbg = getenv("RSAC_DBG_MF") != nullptr;  // diagnostics: flagged records per launch
             if (dbg) {
-                int q[4] = {0, 0, 0, 0};
+                int q[kQWords];
                 (void)hipMemcpyAsync(q, a.queue, sizeof q, hipMemcpyDeviceToHost, s);
                 (void)hipStreamSynchronize(s);
+                q[2] = 0;
+                for (int k = 0; k < kQSub; ++k) q[2] += q[32 + 32 * kQSub + 32 * k];
                 fprintf(stderr, "rsac mf: units %lld records %d of bound %lld (H %d, cells %lld x %lld)\n",
                         (long long)units, q[2], (long long)bound, Hh, (long long)cells, (long long)cell_pts);
             }
             // one wave per record, records latency-bound (a chain of dependent loads): a wide grid
             // (blocks past the record count exit at once)
-            hipLaunchKernelGGL(k_pnp_mf_recount, dim3(2048), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, counts,
-                               (int)tb, (int)cells, (int)cell_pts);
+            hipLaunchKernelGGL(k_pnp_mf_recount, dim3(2048), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, counts, kQSub,
+                               0, 0);
         }
+    }
+    if (a.best_key) {
+        unsigned g = cdiv(H, 1024);
+        if (g > 128) g = 128;
+        hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
+                           a.rng_base + hyp_begin, a.best_key);
+    }
+    return hipGetLastError();
+}
+
+// k_pnp_score_mw: units of 32 hypotheses x a cell, big cells (cbig points) for all but the last
+// `tail` tiles, small cells (csmall) for those, so the queue ends on short units.  Cells halve
+// (down to 64 points) while the units would not give every resident wave work (an adaptive run's
+// first rounds).  A unit appends at most one flagged record per iteration, so a launch whose
+// bound exceeds a.mf_cap is split into hypothesis chunks (counters reset before each).
+// RSAC_MW_BIG / RSAC_MW_SMALL / RSAC_MW_TAIL: tuning knobs (points, points, tiles).
+static int64_t env_i64(const char *name, int64_t dflt) {
+    const char *e = getenv(name);
+    return e ? atoll(e) : dflt;
+}
+template <int CHK, int PD, int XP = 0>
+static hipError_t launch_mw(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
+                            hipStream_t s) {
+    auto kern = k_pnp_score_mw<CHK, PD, XP>;
+    static int resident = 0;  // resident blocks of 4 waves
+    if (resident == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
+        resident = std::max(1, cus) * std::max(1, per_cu);
+    }
+    static const int64_t big0 = std::max<int64_t>(64, env_i64("RSAC_MW_BIG", 2048) / 64 * 64);
+    static const int64_t small0 = std::max<int64_t>(64, env_i64("RSAC_MW_SMALL", 512) / 64 * 64);
+    static const int64_t tail0 = env_i64("RSAC_MW_TAIL", -1);
+    if (a.counts_out != counts) {
+        if (P_ == 1)
+            (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
+        else
+            (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P_, s);
+    }
+    const int64_t max_n = std::max<int64_t>(1, a.max_n);
+    const int64_t waves = 4 * (int64_t)resident;
+    struct Plan {
+        int64_t ta, cb, cbig, cs, csmall, units, bound;
+    };
+    auto plan = [&](int64_t Hc) {
+        Plan p;
+        const int64_t tiles = (int64_t)P_ * ((Hc + 31) / 32);
+        p.cbig = std::min<int64_t>(big0, (max_n + 63) / 64 * 64);
+        while (p.cbig > 64 && tiles * ((max_n + p.cbig - 1) / p.cbig) < waves) p.cbig /= 2;
+        p.csmall = std::min(p.cbig, small0);
+        p.cb = (max_n + p.cbig - 1) / p.cbig;
+        p.cs = (max_n + p.csmall - 1) / p.csmall;
+        const int64_t tail = std::min<int64_t>(tiles, tail0 >= 0 ? tail0 : waves / 8);
+        p.ta = tiles - tail;
+        p.units = p.ta * p.cb + tail * p.cs;
+        p.bound = p.ta * p.cb * ((p.cbig + 63) / 64) + tail * p.cs * ((p.csmall + 63) / 64);
+        return p;
+    };
+    Plan pl = plan(H);
+    int64_t Hc = H;
+    // a block's records go to segment blockIdx % kQSub: bound each segment by its units' share
+    const int64_t seg = a.mf_cap / kQSub;
+    auto seg_bound = [&](const Plan &p) { return (p.bound + kQSub - 1) / kQSub + 2 * ((std::max(p.cbig, p.csmall) + 63) / 64); };
+    if (seg_bound(pl) > seg) {
+        const int64_t per_tile = (int64_t)P_ * std::max(pl.cb * ((pl.cbig + 63) / 64), pl.cs * ((pl.csmall + 63) / 64));
+        const int64_t tiles_c = seg / std::max<int64_t>(1, per_tile);
+        if (tiles_c < 1) return hipErrorOutOfMemory;  // one 32-hypothesis tile per problem exceeds the list
+        Hc = 32 * tiles_c;
+    }
+    PnpArgs ka = a;
+    ka.best_key = nullptr;  // reduced below from the complete counts
+    for (int64_t h = 0; h < H; h += Hc) {
+        const int32_t Hh = (int32_t)std::min<int64_t>(Hc, H - h);
+        if (Hc < H) {
+            pl = plan(Hh);
+            hipError_t e = hipMemsetAsync(a.queue + 32, 0, (kQWords - 32) * sizeof(int), s);
+            if (e != hipSuccess) return e;
+        }
+        if (pl.units > INT32_MAX) return hipErrorInvalidValue;
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((pl.units + 3) / 4, resident));
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, a.queue, counts, (int)pl.ta,
+                           (int)pl.cb, (int)pl.cbig, (int)pl.cs, (int)pl.csmall);
+        static const bool dbg = getenv("RSAC_DBG_MF") != nullptr;  // diagnostics: flagged records per launch
+        if (dbg) {
+            int q[kQWords];
+            (void)hipMemcpyAsync(q, a.queue, sizeof q, hipMemcpyDeviceToHost, s);
+            (void)hipStreamSynchronize(s);
+            q[2] = 0;
+            for (int k = 0; k < kQSub; ++k) q[2] += q[32 + 32 * kQSub + 32 * k];
+            fprintf(stderr, "rsac mw: units %lld records %d of bound %lld (H %d, %lld x %lld big, %lld x %lld small)\n",
+                    (long long)pl.units, q[2], (long long)pl.bound, Hh, (long long)pl.cb, (long long)pl.cbig,
+                    (long long)pl.cs, (long long)pl.csmall);
+        }
+        hipLaunchKernelGGL(k_pnp_mf_recount, dim3(2048), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, counts, kQSub, 0,
+                           0);
     }
     if (a.best_key) {
         unsigned g = cdiv(H, 1024);
@@ -3003,6 +3413,12 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 71: return launch_mf<true, 4, 3, 0, true>(a, P, hyp_begin, H, counts, s);
             case 72: return launch_mf<false, 1, 3, 0, true>(a, P, hyp_begin, H, counts, s);  // timing only
             case 73: return launch_mf<true, 2, 3, 1, true>(a, P, hyp_begin, H, counts, s);
+            case 74: return launch_mw<2, 1>(a, P, hyp_begin, H, counts, s);
+            case 75: return launch_mw<2, 0>(a, P, hyp_begin, H, counts, s);
+            case 76: return launch_mw<1, 1>(a, P, hyp_begin, H, counts, s);
+            case 77: return launch_mw<2, 1, 1>(a, P, hyp_begin, H, counts, s);  // timing only
+            case 78: return launch_mw<2, 1, 2>(a, P, hyp_begin, H, counts, s);  // timing only
+            case 79: return launch_mw<2, 1, 3>(a, P, hyp_begin, H, counts, s);  // timing only
             case 50: launch_sc<8, 5>(a, P, hyp_begin, H, counts, s); break;
             case 51: launch_sc<4, 4>(a, P, hyp_begin, H, counts, s); break;
             case 52: launch_sc<6, 4>(a, P, hyp_begin, H, counts, s); break;

@@ -166,7 +166,7 @@ def test_pnp_batched_ragged_equals_singles():
         assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
 
 
-@pytest.mark.parametrize("variant", [49, 73])
+@pytest.mark.parametrize("variant", [49, 73, 74])
 def test_pnp_batched_mixed_scales_equals_oracle(variant):
     # one batch, problems inside and outside the MFMA scorer's f16 operand range (centred
     # coordinates above 2^15 or below 1/64 run the form-1 path of k_pnp_score_mf)
@@ -274,7 +274,7 @@ def test_degenerate_inputs():
 # variant (VALU f32, packed f32, MFMA) is checked, then the default is restored.
 # ---------------------------------------------------------------------------------------------
 SCORE_VARIANTS = [0, 1, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28,
-                  40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 60, 62, 63, 64, 65, 66, 67, 69, 70, 71, 73]
+                  40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 60, 62, 63, 64, 65, 66, 67, 69, 70, 71, 73, 74, 75, 76]
 
 
 @pytest.fixture(params=SCORE_VARIANTS)
