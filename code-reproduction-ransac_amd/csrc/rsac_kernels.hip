@@ -1576,50 +1576,75 @@ __device__ __forceinline__ mf_h8 mf_operand(const float *__restrict__ recs, int 
     return __builtin_bit_cast(mf_h8, v);
 }
 
+// the A operand of MFMA group t (mf_operand's values) from an unconditional load: the index is
+// clamped into the unit and the value replaced afterwards, so the unit's loads issue together
+// instead of one conditional load (and wait) after another
+__device__ __forceinline__ mf_h8 mw_operand(const float *__restrict__ recs, int t, int col, int half, int nh) {
+    const int r = col & 3, j = 8 * t + (col >> 2);
+    const int jj = min(j, nh - 1), rr = min(r, 2);
+    mf_u2 w = *gview(reinterpret_cast<const mf_u2 *>(reinterpret_cast<const char *>(recs + jj * kFModelStride) +
+                                                     half * 24 + rr * 8));
+    if (!(r < 3 && j < nh)) {
+        w.x = 0u;
+        w.y = (r == 0 && half == 0 && j >= nh) ? 0x3C000000u : 0u;
+    }
+    const mf_u4 v = {w.x, w.y, w.x, w.y};
+    return __builtin_bit_cast(mf_h8, v);
+}
+
 // exact recount of one flagged iteration (one wave): the MFMA and the VALU test of the flagged
 // slots are redone (same operands, same bits) and each undecided pair's fast verdict (D < 0) is
-// replaced by the exact f64 test (pnp_err); the corrections are added to the counts
+// replaced by the exact f64 test (pnp_err); the corrections are added to the counts.  Every load
+// that does not depend on the test (point operands, the slopes and bands of the 32 hypotheses,
+// the lane's two points in f32) is issued up front; per flagged group the A operand, per slot
+// with an undecided pair its model.
 __device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfFlag &f, int base, int col, int half,
                                            int32_t *__restrict__ counts) {
     const int64_t p0 = f.p0, rec0 = f.rec0;
     const uint32_t fl = f.fl;
+    const int nh = f.nh;
     const int prob = (int)(rec0 / a.hyp_stride);
     const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
     mf_h8 Ba, Bb;
     float2 ua, ub;
     mf_load(a.PF + 2 * p0, a.UV + p0, base, f.n, col, half, Ba, Bb, ua, ub);
+    // lane c < 32: a' and b' of hypothesis c (read by the others through a lane shuffle)
+    const int jc = min(col, nh - 1);
+    const float a_c = gview(recs)[jc * kFModelStride + 12], b_c = gview(recs)[jc * kFModelStride + 13];
+    const int ia = base + col, ib = ia + 32;
+    const int64_t qa = p0 + min(ia, f.n - 1), qb = p0 + min(ib, f.n - 1);
+    const float Xa = a.X[qa], Ya = a.Y[qa], Za = a.Z[qa], Uxa = a.U[qa], Vxa = a.V[qa];
+    const float Xb = a.X[qb], Yb = a.Y[qb], Zb = a.Z[qb], Uxb = a.U[qb], Vxb = a.V[qb];
     const double *cm = a.cams + 4 * prob;
     const Cam k{cm[0], cm[1], cm[2], cm[3]};
     const float thr2 = a.thr2[prob];
 #pragma unroll 1
     for (int t = 0; t < 4; ++t) {
         const uint32_t ft = (fl >> (4 * t)) & 15u;
-        if (!ft) continue;
-        const mf_h8 At = mf_operand(recs, t, col, half, f.nh);
+        if (!ft) continue;  // uniform
+        const mf_h8 At = mw_operand(recs, t, col, half, nh);
         const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
         const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             if (!((ft >> g) & 1u)) continue;  // uniform
             const int j = 8 * t + 2 * g + half;  // this lane's hypothesis
-            const bool live = j < f.nh;
-            const float ag = live ? recs[j * kFModelStride + 12] : 0.f;
-            const float bg = live ? recs[j * kFModelStride + 13] : -__builtin_inff();
+            const bool live = j < nh;
+            const float aj = __shfl(a_c, j), bj = __shfl(b_c, j);
+            const float ag = live ? aj : 0.f;
+            const float bg = live ? bj : -__builtin_inff();
             const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
-            const int ia = base + col, ib = ia + 32;
             const bool wa = !(ra.t > bg) && ia < f.n, wb = !(rb.t > bg) && ib < f.n;
             if (wa || wb) {
                 const double *md = a.models + (rec0 + j) * kModelStride;
                 const bool mv = md[kValidSlot] != 0.0;
                 int c = 0;
-#pragma unroll 1
-                for (int tile = 0; tile < 2; ++tile) {
-                    if (!(tile ? wb : wa)) continue;
-                    const int64_t q = p0 + (tile ? ib : ia);
-                    const bool ex = mv && pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q],
-                                                  a.U[q], a.V[q]) <= thr2;
-                    c += (ex ? 1 : 0) - ((tile ? rb.D : ra.D) < 0.f ? 1 : 0);
-                }
+                if (wa)
+                    c += (mv && pnp_err(md, md + 9, k, (double)Xa, (double)Ya, (double)Za, Uxa, Vxa) <= thr2 ? 1 : 0) -
+                         (ra.D < 0.f ? 1 : 0);
+                if (wb)
+                    c += (mv && pnp_err(md, md + 9, k, (double)Xb, (double)Yb, (double)Zb, Uxb, Vxb) <= thr2 ? 1 : 0) -
+                         (rb.D < 0.f ? 1 : 0);
                 if (c) atomicAdd(&counts[rec0 + j], c);
             }
         }
@@ -1645,12 +1670,27 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 
 constexpr int kWrec = 64;  // flagged-window list of a wave (k_pnp_score_mf)
 
+// s_memtime phase totals of k_pnp_score_mf's timing instance (variant 84, diagnostics only):
+// [0] kernel, [1] unit prologue (staging), [2] point loop, [3] epilogue, [4] between units
+// (barrier + queue), [5] waves, [6] units
+__device__ unsigned long long g_mf_timing[8];
+struct MfTimes {
+    unsigned long long pro = 0, loop = 0, epi = 0;
+};
+__device__ __forceinline__ unsigned long long mf_clock() {
+    unsigned long long t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the stamp has arrived
+    return t;
+}
+
 // CHK: iterations (2 x 32 points per wave) per check window of the band minimum
-template <bool FB, int CHK, int PD, bool RA>
+template <bool FB, int CHK, int PD, bool RA, bool PIPE = false, bool TM = false, bool INL = false>
 __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, int64_t h0, int nh, int64_t p0, int start,
-                                        int n, int lane, int wave, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
-                                        mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *wcnt,
+                                        int n, int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
+                                        mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *wcnt, MfTimes &tms,
                                         int32_t *__restrict__ counts) {
+    unsigned long long ts0 = 0, ts1 = 0;
+    if constexpr (TM) ts0 = mf_clock();
     constexpr int HB = 32;
     const int col = lane & 31, half = lane >> 5;
     const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
@@ -1701,18 +1741,44 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
     }
     auto body = [&](int i, const mf_h8 &Ba, const mf_h8 &Bb, const float2 &ua, const float2 &ub)
         __attribute__((always_inline)) {
+        if constexpr (PIPE) {
+            // software-pipelined: group t + 1's MFMAs are issued before group t's vector work, so
+            // the matrix latency hides behind this wave's own VALU (two output sets live)
+            mf_f16v xa[2], xb[2];
+            xa[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(RA ? Ar[0] : alds[0][lane], Ba, mf_f16v{}, 0, 0, 0);
+            xb[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(RA ? Ar[0] : alds[0][lane], Bb, mf_f16v{}, 0, 0, 0);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const mf_h8 At = RA ? Ar[t] : alds[t][lane];
-            const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
-            const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
-            const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
+            for (int t = 0; t < 4; ++t) {
+                if (t < 3) {
+                    const mf_h8 An = RA ? Ar[t + 1] : alds[t + 1][lane];
+                    xa[(t + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(An, Ba, mf_f16v{}, 0, 0, 0);
+                    xb[(t + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(An, Bb, mf_f16v{}, 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
-                const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
-                vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
-                if (FB) tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
+                for (int g = 0; g < 4; ++g) {
+                    const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
+                    const MfPair ra = mf_pair(xa[t & 1], g, ua, ag), rb = mf_pair(xb[t & 1], g, ub, ag);
+                    vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
+                    if (FB) tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const mf_h8 At = RA ? Ar[t] : alds[t][lane];
+                const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
+                const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
+                const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
+                    const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
+                    vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
+                    if (FB) tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
+                }
             }
         }
         if (FB && (++it == CHK || i == iters - 1)) {  // end of a check window (uniform)
@@ -1732,7 +1798,9 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
                 // appended to a.mf_list with the unit's (one atomic per block), or at once by the
                 // wave when its list is full
                 if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)(i + 1 - it) | ((uint32_t)it << 24), fl);
-                if (++nw == kWrec) {
+                if (INL)
+                    ++nw;  // INL: at most kWrec windows per wave and unit (the launcher checks)
+                else if (++nw == kWrec) {
                     __builtin_amdgcn_wave_barrier();
                     int slot = 0;
                     const int qk = blockIdx.x % kQSub;
@@ -1752,6 +1820,11 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
         }
     };
     const int full = n >= b0 + 64 ? (n - b0 - 64) / 256 + 1 : 0;  // iterations with 64 points in range
+    if constexpr (TM) {
+        ts1 = mf_clock();
+        tms.pro += ts1 - ts0;
+        ts0 = ts1;
+    }
     if constexpr (PD == 0) {
         for (int i = 0; i < full; ++i) {
             mf_h8 Ba, Bb;
@@ -1778,6 +1851,26 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
         mf_load_part(PF, UV, b0 + 256 * full, n, col, half, Ba, Bb, ua, ub);
         body(full, Ba, Bb, ua, ub);
     }
+    if constexpr (INL) {
+        // the wave's flagged windows recounted here (no records, no recount launch): the wave's
+        // exact-test latency overlaps the other blocks' waves on its SIMD
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+        for (int k = 0; k < nw; ++k) {
+            const uint2 w = wrec[wave][k];
+            const int base = b0 + 256 * (int)(w.x & 0xFFFFFFu), wi = (int)(w.x >> 24);
+            const MfFlag f{rec0, p0, base, n, w.y, (int16_t)nh, (int16_t)wi};
+#pragma unroll 1
+            for (int iw = 0; iw < wi && base + 256 * iw < n; ++iw) mf_recount(a, f, base + 256 * iw, col, half, counts);
+        }
+        nw = 0;
+    }
+    if constexpr (TM) {
+        ts1 = mf_clock();
+        tms.loop += ts1 - ts0;
+        ts0 = ts1;
+    }
     if (lane == 0) wcnt[wave] = nw;
     // counts: lane (c, half) of wave w holds slot (t, g)'s count over its points; hypothesis j =
     // 8t + 2g + half sums 4 waves x 32 lanes (8 threads of 16 values each, then a shuffle tree)
@@ -1786,6 +1879,18 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
 #pragma unroll
         for (int g = 0; g < 4; ++g) cl[wave][4 * t + g][lane] = vc[t][g];
     __syncthreads();
+    // the waves' flagged iterations: one atomic for the block (in flight during the count
+    // reduction; inline asm, as the atomic optimizer's fix-up would wait for it at once), then a
+    // store per record
+    int roff = 0, rtot = 0;
+    if (FB && threadIdx.x == 0) {
+        rtot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        if (rtot)
+            asm volatile("global_atomic_add %0, %1, %2, off sc0"
+                         : "+v"(roff)
+                         : "v"(rec_queue(a.queue, blockIdx.x % kQSub)), "v"(rtot)
+                         : "memory");
+    }
     {
         const int j = threadIdx.x >> 3, p = threadIdx.x & 7;
         const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + 4 * p;
@@ -1797,13 +1902,22 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
         sum += __shfl_xor(sum, 1);
         sum += __shfl_xor(sum, 2);
         sum += __shfl_xor(sum, 4);
-        if (p == 0 && j < nh && sum) atomicAdd(&counts[rec0 + j], (int)(sum / 255u));
-    }
-    if (FB) {  // the waves' flagged iterations: one atomic for the block, then a store per record
-        if (threadIdx.x == 0) {
-            const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-            wcnt[4] = tot ? atomicAdd(rec_queue(a.queue, blockIdx.x % kQSub), tot) : 0;
+        // thread 0 takes its record offset first, so its wait does not cover a count atomic
+        if (FB && threadIdx.x == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(roff)::"memory");
+            wcnt[4] = rtot ? roff : 0;
         }
+        // a unit over all of its problem's points is the only writer of its counts: a store
+        // (an atomic is acknowledged by the device's coherence point, and every later wait of
+        // the wave would wait for it)
+        if (p == 0 && j < nh) {
+            if (start == 0 && n == n_all_pts)
+                counts[rec0 + j] = (int)(sum / 255u);
+            else if (sum)
+                atomicAdd(&counts[rec0 + j], (int)(sum / 255u));
+        }
+    }
+    if (FB) {
         __syncthreads();
         int off = wcnt[4];
         for (int w = 0; w < wave; ++w) off += wcnt[w];
@@ -1814,6 +1928,197 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
                                           (int16_t)(w.x >> 24)};
         }
     }
+    if constexpr (TM) tms.epi += mf_clock() - ts0;
+}
+
+// Dynamic form of mf_unit (variants 85, 86): the block's 4 waves take pairs of consecutive
+// iterations (2 x 64 points) from an LDS counter instead of a fixed 256-point stride, so they
+// reach the epilogue barrier within one pair of each other.  With the fixed stride the waves of
+// a block (each on a SIMD shared with other blocks' waves) drifted apart, and the first ones
+// waited at that barrier for 20 % of the kernel (s_memtime phases, variant 84).  A pair is one
+// check window; its record is {base, 1 or 2 iterations, 64 points apart}.  The next pair's index
+// is taken one pair ahead, so the point operands are loaded one iteration ahead throughout.
+template <bool RA, bool TM>
+__device__ __forceinline__ void mfd_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
+                                         int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
+                                         mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *wcnt, int *pctr, MfTimes &tms,
+                                         int32_t *__restrict__ counts) {
+    unsigned long long ts0 = 0, ts1 = 0;
+    if constexpr (TM) ts0 = mf_clock();
+    constexpr int HB = 32;
+    const int col = lane & 31, half = lane >> 5;
+    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
+    const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
+    if (threadIdx.x < HB) {
+        const int j = threadIdx.x;
+        const bool v = j < nh;
+        ab[0][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 12] : 0.f;
+        ab[1][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 13] : -__builtin_inff();
+    }
+    {
+        const int tl = threadIdx.x & 63;
+        alds[threadIdx.x >> 6][tl] = mf_operand(recs, threadIdx.x >> 6, tl & 31, tl >> 5, nh);
+    }
+    if (threadIdx.x == 0) *pctr = 0;
+    __syncthreads();
+    const uint4 *__restrict__ PF = a.PF + 2 * p0;
+    const float2 *__restrict__ UV = a.UV + p0;
+    uint32_t vc[4][4];
+    float tm[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            vc[t][g] = 0u;
+            tm[t][g] = __builtin_inff();
+        }
+    int nw = 0;
+    mf_h8 Ar[4];
+    float4 avr[4];
+    if constexpr (RA) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            Ar[t] = alds[t][lane];
+            avr[t] = *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
+        }
+    }
+    auto body = [&](const mf_h8 &Ba, const mf_h8 &Bb, const float2 &ua, const float2 &ub)
+        __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const mf_h8 At = RA ? Ar[t] : alds[t][lane];
+            const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
+            const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
+            const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
+                const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
+                vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
+                tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
+            }
+        }
+    };
+    auto grab = [&]() __attribute__((always_inline)) {
+        int g = 0;
+        if (lane == 0) g = __hip_atomic_fetch_add(pctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __builtin_amdgcn_readfirstlane(g);
+    };
+    auto load = [&](int base, mf_h8 &Ba, mf_h8 &Bb, float2 &ua, float2 &ub) __attribute__((always_inline)) {
+        if (base + 64 <= n)
+            mf_load_full(PF, UV, base, col, half, Ba, Bb, ua, ub);
+        else
+            mf_load_part(PF, UV, base, n, col, half, Ba, Bb, ua, ub);
+    };
+    const int npairs = (n - start + 127) / 128;
+    int g = grab();
+    mf_h8 Ba, Bb, Na, Nb;
+    float2 ua, ub, na, nb;
+    if (g < npairs) load(start + 128 * g, Ba, Bb, ua, ub);
+    while (g < npairs) {  // uniform
+        const int gn = grab();
+        const int base = start + 128 * g;
+        const bool two = base + 64 < n;
+        if (two)
+            load(base + 64, Na, Nb, na, nb);
+        else if (gn < npairs)
+            load(start + 128 * gn, Na, Nb, na, nb);
+        body(Ba, Bb, ua, ub);
+        Ba = Na;
+        Bb = Nb;
+        ua = na;
+        ub = nb;
+        if (two) {
+            if (gn < npairs) load(start + 128 * gn, Na, Nb, na, nb);
+            body(Ba, Bb, ua, ub);
+            Ba = Na;
+            Bb = Nb;
+            ua = na;
+            ub = nb;
+        }
+        uint32_t fl = 0;  // the pair's check window
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float bg = q == 0 ? bv.x : q == 1 ? bv.y : q == 2 ? bv.z : bv.w;
+                fl |= __ballot(!(tm[t][q] > bg)) ? (1u << (4 * t + q)) : 0u;
+                tm[t][q] = __builtin_inff();
+            }
+        }
+        if (__builtin_expect(fl != 0, 0)) {
+            if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)base, fl | (1u << 16) | ((two ? 2u : 1u) << 24));
+            if (++nw == kWrec) {
+                __builtin_amdgcn_wave_barrier();
+                int slot = 0;
+                const int qk = blockIdx.x % kQSub;
+                const int64_t seg = a.mf_cap / kQSub;
+                if (lane == 0) slot = atomicAdd(rec_queue(a.queue, qk), kWrec);
+                slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0));
+                if (slot + lane < seg) {
+                    const uint2 w = wrec[wave][lane];
+                    a.mf_list[qk * seg + slot + lane] =
+                        MfFlag{rec0, p0, (int32_t)w.x, n, w.y & 0x1FFFFu, (int16_t)nh, (int16_t)(w.y >> 24)};
+                }
+                __builtin_amdgcn_wave_barrier();
+                nw = 0;
+            }
+        }
+        g = gn;
+    }
+    if constexpr (TM) {
+        ts1 = mf_clock();
+        tms.loop += ts1 - ts0;
+        ts0 = ts1;
+    }
+    if (lane == 0) wcnt[wave] = nw;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cl[wave][4 * t + q][lane] = vc[t][q];
+    __syncthreads();
+    int roff = 0, rtot = 0;
+    if (threadIdx.x == 0) {
+        rtot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        if (rtot)
+            asm volatile("global_atomic_add %0, %1, %2, off sc0"
+                         : "+v"(roff)
+                         : "v"(rec_queue(a.queue, blockIdx.x % kQSub)), "v"(rtot)
+                         : "memory");
+    }
+    {
+        const int j = threadIdx.x >> 3, p = threadIdx.x & 7;
+        const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + 4 * p;
+        uint32_t sum = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) sum += cl[w][slot][l0 + l];
+        sum += __shfl_xor(sum, 1);
+        sum += __shfl_xor(sum, 2);
+        sum += __shfl_xor(sum, 4);
+        if (threadIdx.x == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(roff)::"memory");
+            wcnt[4] = rtot ? roff : 0;
+        }
+        if (p == 0 && j < nh) {
+            if (start == 0 && n == n_all_pts)
+                counts[rec0 + j] = (int)(sum / 255u);
+            else if (sum)
+                atomicAdd(&counts[rec0 + j], (int)(sum / 255u));
+        }
+    }
+    __syncthreads();
+    int off = wcnt[4];
+    for (int w = 0; w < wave; ++w) off += wcnt[w];
+    const int64_t seg = a.mf_cap / kQSub;
+    if (lane < wcnt[wave] && off + lane < seg) {
+        const uint2 w = wrec[wave][lane];
+        a.mf_list[blockIdx.x % kQSub * seg + off + lane] =
+            MfFlag{rec0, p0, (int32_t)w.x, n, w.y & 0x1FFFFu, (int16_t)nh, (int16_t)(w.y >> 24)};
+    }
+    if constexpr (TM) tms.epi += mf_clock() - ts0;
 }
 
 // Phase 1: units from the queue (a.queue[0]); a unit's flagged iterations are appended to
@@ -1823,7 +2128,8 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
 // unit has been taken by a running block, so the wait always ends.
 // W: minimum waves per SIMD the register budget must allow; PD: point operands loaded 0 / 1
 // iterations ahead
-template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false>
+template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false, bool PIPE = false, bool TM = false,
+          bool DYN = false, bool INL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_mf(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int tb, int cells, int cell_pts) {
@@ -1833,6 +2139,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     __shared__ __attribute__((aligned(16))) float ab[2][2][4][4];
     __shared__ uint2 wrec[4][kWrec];
     __shared__ int wcnt[5];
+    __shared__ int pctr;  // DYN: the unit's next iteration pair
     __shared__ mf_h8 alds[4][64];
     __shared__ int red[4][HB];                                                 // sc_unit
     __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];  // sc_unit
@@ -1840,11 +2147,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tiles_per_prob = (H + HB - 1) / HB;
     const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
+    MfTimes tms;
+    unsigned long long tk0 = 0, tb0 = 0, tbar = 0, nunits = 0;
+    if constexpr (TM) tk0 = mf_clock();
+    const int qk = blockIdx.x % kQSub;  // this block's units: qk + kQSub i, i from counter qk
+    int *const uq = unit_queue(queue, qk);
+    if (threadIdx.x == 0) unit_s = qk + kQSub * atomicAdd(uq, 1);
+    __syncthreads();
+    int last_prob = -1, n_all = 0;
+    int64_t p0 = 0;
+    bool in_range = false;
     for (;;) {
-        if (threadIdx.x == 0) unit_s = blockIdx.x % kQSub + kQSub * atomicAdd(unit_queue(queue, blockIdx.x % kQSub), 1);
-        __syncthreads();
         const int unit = __builtin_amdgcn_readfirstlane(unit_s);
         if (unit >= n_units) break;  // uniform: every wave of every block reaches it
+        // the next unit's index, in flight while this unit runs (inline asm: the atomic
+        // optimizer's fix-up would wait for the result at once); waited for at the unit's end
+        int nx = 0;
+        if (threadIdx.x == 0)
+            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "+v"(nx) : "v"(uq), "v"(1) : "memory");
         int tile, c0, c1;
         if (unit < tb) {
             tile = unit;
@@ -1858,17 +2178,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         const int prob = tile / tiles_per_prob;
         const int64_t h0 = hyp_begin + (int64_t)(tile % tiles_per_prob) * HB;
         const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
-        const int64_t p0 = a.offsets[prob];
-        const int n_all = (int)(a.offsets[prob + 1] - p0);
+        if (prob != last_prob) {  // uniform; once per call for one problem
+            p0 = a.offsets[prob];
+            n_all = (int)(a.offsets[prob + 1] - p0);
+            in_range = a.fconst[(int64_t)prob * kFconstStride + 11] != 0.f;
+            last_prob = prob;
+        }
         const int start = c0 * cell_pts;
         const int n = min(n_all, c1 * cell_pts);
         if (start < n_all) {
-            if (a.fconst[(int64_t)prob * kFconstStride + 11] != 0.f)
-                mf_unit<FB, CHK, PD, RA>(a, unit, prob, h0, nh, p0, start, n, lane, wave, cl, ab, alds, wrec, wcnt, counts);
+            if (in_range)
+                if constexpr (DYN)
+                    mfd_unit<RA, TM>(a, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds, wrec, wcnt, &pctr, tms,
+                                     counts);
+                else
+                    mf_unit<FB, CHK, PD, RA, PIPE, TM, INL>(a, unit, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds,
+                                                       wrec, wcnt, tms, counts);
             else
                 mf_sc_unit(kernarg_pnp(), prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
         }
+        if constexpr (TM) {
+            tb0 = mf_clock();
+            ++nunits;
+        }
+        if (threadIdx.x == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(nx)::"memory");
+            unit_s = qk + kQSub * nx;  // every thread read unit_s before the unit's barriers
+        }
         __syncthreads();  // the unit's LDS and unit_s are rewritten by the next unit
+        if constexpr (TM) tbar += mf_clock() - tb0;
+    }
+    if constexpr (TM) {
+        if (lane == 0) {
+            atomicAdd(&g_mf_timing[0], mf_clock() - tk0);
+            atomicAdd(&g_mf_timing[1], tms.pro);
+            atomicAdd(&g_mf_timing[2], tms.loop);
+            atomicAdd(&g_mf_timing[3], tms.epi);
+            atomicAdd(&g_mf_timing[4], tbar);
+            atomicAdd(&g_mf_timing[5], 1ull);
+            atomicAdd(&g_mf_timing[6], nunits);
+        }
     }
 }
 
@@ -1934,22 +2283,6 @@ __global__ __launch_bounds__(256) void k_pnp_mf_recount(PnpArgs a, int64_t hyp_b
 // are counted with the exact f64 test, one lane per point (never at C2-C5 scales).
 // ---------------------------------------------------------------------------
 constexpr int kMwWaves = 4;  // waves per block (blocks only group waves for the launch)
-
-// the A operand of MFMA group t (mf_operand's values) from an unconditional load: the index is
-// clamped into the unit and the value replaced afterwards, so the unit's loads issue together
-// instead of one conditional load (and wait) after another
-__device__ __forceinline__ mf_h8 mw_operand(const float *__restrict__ recs, int t, int col, int half, int nh) {
-    const int r = col & 3, j = 8 * t + (col >> 2);
-    const int jj = min(j, nh - 1), rr = min(r, 2);
-    mf_u2 w = *gview(reinterpret_cast<const mf_u2 *>(reinterpret_cast<const char *>(recs + jj * kFModelStride) +
-                                                     half * 24 + rr * 8));
-    if (!(r < 3 && j < nh)) {
-        w.x = 0u;
-        w.y = (r == 0 && half == 0 && j >= nh) ? 0x3C000000u : 0u;
-    }
-    const mf_u4 v = {w.x, w.y, w.x, w.y};
-    return __builtin_bit_cast(mf_h8, v);
-}
 
 // the wave's flagged windows (LDS, full records) to segment qk of a.mf_list (a.mf_cap / kQSub
 // records each): one atomic for the slots
@@ -3096,7 +3429,7 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
 }
 
 int score_record_form() {
-    if (g_score_variant >= 60 && g_score_variant <= 79) return 2;
+    if (g_score_variant >= 60 && g_score_variant <= 89) return 2;
     return g_score_variant >= 49 && g_score_variant <= 53 ? 1 : 0;
 }
 
@@ -3144,10 +3477,15 @@ static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H
 // would not fill the resident grid (an adaptive run's first rounds).  Every wave-iteration
 // appends at most one flagged record, so a launch whose bound exceeds a.mf_cap is split into
 // hypothesis chunks (counters reset before each).
-template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false>
+template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false, bool PIPE = false, bool TM = false,
+          bool DYN = false, bool INL = false>
 static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    auto kern = k_pnp_score_mf<FB, CHK, W, PD, RA>;
+    auto kern = k_pnp_score_mf<FB, CHK, W, PD, RA, PIPE, TM, DYN, INL>;
+    if (TM) {
+        unsigned long long z[8] = {};
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mf_timing), z, sizeof z, 0, hipMemcpyHostToDevice, s);
+    }
     static int resident = 0;
     if (resident == 0) {
         int dev = 0, cus = 0, per_cu = 0;
@@ -3210,8 +3548,9 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
             }
             // one wave per record, records latency-bound (a chain of dependent loads): a wide grid
             // (blocks past the record count exit at once)
-            hipLaunchKernelGGL(k_pnp_mf_recount, dim3(2048), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, counts, kQSub,
-                               0, 0);
+            if (!INL)
+                hipLaunchKernelGGL(k_pnp_mf_recount, dim3(2048), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, counts,
+                                   kQSub, 0, 0);
         }
     }
     if (a.best_key) {
@@ -3419,6 +3758,34 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 77: return launch_mw<2, 1, 1>(a, P, hyp_begin, H, counts, s);  // timing only
             case 78: return launch_mw<2, 1, 2>(a, P, hyp_begin, H, counts, s);  // timing only
             case 79: return launch_mw<2, 1, 3>(a, P, hyp_begin, H, counts, s);  // timing only
+            case 80: return launch_mf<true, 2, 2, 1, true, true>(a, P, hyp_begin, H, counts, s);
+            case 81: return launch_mf<true, 2, 3, 1, true, true>(a, P, hyp_begin, H, counts, s);
+            case 82: return launch_mf<true, 2, 2, 1, false, true>(a, P, hyp_begin, H, counts, s);
+            case 83: return launch_mf<true, 2, 3, 0, false, true>(a, P, hyp_begin, H, counts, s);
+            case 85: return launch_mf<true, 2, 3, 1, true, false, false, true>(a, P, hyp_begin, H, counts, s);
+            case 88:  // 73 with the flagged windows recounted inside the unit (no recount launch):
+                      // at most kWrec windows per wave and unit, so problems up to 32768 points
+                if (a.max_n <= 2 * 256 * kWrec)
+                    return launch_mf<true, 2, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
+                return launch_mf<true, 2, 3, 1, true>(a, P, hyp_begin, H, counts, s);
+            case 89:
+                if (a.max_n <= 256 * kWrec)
+                    return launch_mf<true, 1, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
+                return launch_mf<true, 2, 3, 1, true>(a, P, hyp_begin, H, counts, s);
+            case 86: return launch_mf<true, 2, 3, 1, false, false, false, true>(a, P, hyp_begin, H, counts, s);
+            case 84:
+            case 87: {  // 73 / 85 with s_memtime phase totals (diagnostics)
+                hipError_t e = g_score_variant == 84
+                                   ? launch_mf<true, 2, 3, 1, true, false, true>(a, P, hyp_begin, H, counts, s)
+                                   : launch_mf<true, 2, 3, 1, true, false, true, true>(a, P, hyp_begin, H, counts, s);
+                unsigned long long t[8];
+                (void)hipMemcpyFromSymbolAsync(t, HIP_SYMBOL(g_mf_timing), sizeof t, 0, hipMemcpyDeviceToHost, s);
+                (void)hipStreamSynchronize(s);
+                const double w = t[5] ? (double)t[5] : 1.0;
+                fprintf(stderr, "rsac mf timing per wave (memtime ticks): kernel %.0f pro %.0f loop %.0f epi %.0f between %.0f units %.2f\n",
+                        t[0] / w, t[1] / w, t[2] / w, t[3] / w, t[4] / w, t[6] / w);
+                return e;
+            }
             case 50: launch_sc<8, 5>(a, P, hyp_begin, H, counts, s); break;
             case 51: launch_sc<4, 4>(a, P, hyp_begin, H, counts, s); break;
             case 52: launch_sc<6, 4>(a, P, hyp_begin, H, counts, s); break;
