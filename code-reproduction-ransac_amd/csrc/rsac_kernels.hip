@@ -79,6 +79,9 @@ constexpr int kQSub = 8;
 constexpr int kQWords = 32 + 64 * kQSub;  // ints of the queue buffer used by the PnP kernels
 __device__ __forceinline__ int *unit_queue(int *q, int k) { return q + 32 + 32 * k; }
 __device__ __forceinline__ int *rec_queue(int *q, int k) { return q + 32 + 32 * kQSub + 32 * k; }
+// k_fm_score_q's counters (HomArgs::fm_queue = queue + 8): words kQWords + 32 k of the buffer
+constexpr int kFmQOff = kQWords - 8;
+__device__ __forceinline__ int *fm_unit_queue(int *fq, int k) { return fq + kFmQOff + 32 * k; }
 
 __device__ __forceinline__ void reset_pnp_queue(int *q) {
     q[0] = 0;
@@ -4959,8 +4962,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tiles_per_prob = (H + HB - 1) / HB;
     const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
+    // split queue (as k_pnp_score_mf): block b takes units b % kQSub + kQSub i from counter b % kQSub
+    int *const uq = fm_unit_queue(a.fm_queue, blockIdx.x % kQSub);
     for (;;) {
-        if (threadIdx.x == 0) unit_s = atomicAdd(a.fm_queue, 1);
+        if (threadIdx.x == 0) unit_s = blockIdx.x % kQSub + kQSub * atomicAdd(uq, 1);
         __syncthreads();
         const int unit = __builtin_amdgcn_readfirstlane(unit_s);
         if (unit >= n_units) break;  // uniform
@@ -5102,7 +5107,7 @@ hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32
         const int64_t tiles = (int64_t)P * ((H + 31) / 32);
         const int64_t cell_tiles = std::min<int64_t>(tiles, resident);
         const int64_t tb = tiles - cell_tiles, units = tb + cell_tiles * cells;
-        hipError_t e = hipMemsetAsync(a.fm_queue, 0, sizeof(int), s);
+        hipError_t e = hipMemsetAsync(a.fm_queue + kFmQOff, 0, 32 * kQSub * sizeof(int), s);
         if (e == hipSuccess) {
             if (P == 1)
                 e = hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
