@@ -294,6 +294,23 @@ def test_f32_prefilter_equals_exact_kernel(n, seed, score_variant):
     np.testing.assert_array_equal(c_f, c_e)
 
 
+@pytest.mark.parametrize("variant", [73, 74])
+def test_f32_prefilter_record_list_chunks(variant):
+    # 100k points x 50k hypotheses: the flagged-record bound of one launch exceeds a record
+    # segment (a.mf_cap / 8), so the launch is split into hypothesis chunks (queue counters reset
+    # before each); counts must still equal the exact kernel's
+    from rsac import _lib as L
+    pr = synth.pnp_problem(100_000, 0.5, seed=11)
+    L.check(L.lib().rsac_set_score_variant(variant))
+    try:
+        st_f, c_f, _ = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, 50_000, 30.0)
+    finally:
+        L.check(L.lib().rsac_set_score_variant(-1))
+    st_e, c_e, _ = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, 50_000, 30.0, exact_only=True)
+    np.testing.assert_array_equal(st_f, st_e)
+    np.testing.assert_array_equal(c_f, c_e)
+
+
 def _boundary_case(seed, n=6000, thr=30.0):
     """Pixels placed at distance ~thr from the exact projection of the true pose, so that e ~ T to
     within float32 rounding: every pair lands in (or next to) the pre-filter's undecided band."""
