@@ -43,7 +43,9 @@ BYTES_PER_POINT = 20  # f32 X, Y, Z, u, v
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
 VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, f32 vector peak
 VALU_ISSUE_PEAK = 1024 * 0.5 * 2.4e9  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each, 2.4 GHz
-FLOP_PER_PAIR = 31  # k_pnp_score_sc: 16.5 vector instructions per pair, 14.5 of them FMAs
+FLOP_PER_PAIR = 11  # k_pnp_score_mf: the VALU test per pair (q1, q2, D, t: 5 FMAs + 1 multiply)
+MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, dense f16 matrix peak
+MFMA_FLOP_PER_PAIR = 32 * 32 * 16 * 2 / 256  # one v_mfma_f32_32x32x16_f16 per 8 hypotheses x 32 points
 
 
 def parse():
@@ -223,8 +225,14 @@ def main():
             "kernels_ms": {"pnp_solve": solve_avg, "pnp_score": score_avg},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_pnp_score", "algorithmic_bytes_per_launch": args.points * BYTES_PER_POINT * H},
+                         "kernel": "scoring stage (HIP events): k_pnp_score_mf + k_pnp_mf_recount + k_best_key",
+                         "algorithmic_bytes_per_launch": args.points * BYTES_PER_POINT * H},
             "roofline_valu": roof_valu,
+            "roofline_mfma": {"bound": "mfma", "flop_per_pair": MFMA_FLOP_PER_PAIR,
+                              "achieved": pairs * MFMA_FLOP_PER_PAIR / (score_avg * 1e-3) / 1e12,
+                              "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": pairs * MFMA_FLOP_PER_PAIR / (score_avg * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS,
+                              "note": "f16 matrix flops of the projection (hi/lo operands), dense peak"},
             "cpu_baseline": cpu,
             "extras": extras,
         }
