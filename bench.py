@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -41,6 +42,7 @@ from rsac import synth  # noqa: E402
 METRIC = "RANSAC hypotheses/sec + ms-to-best-model, 10k pts 50% outliers, 1/2/4/8 GPU"
 BYTES_PER_POINT = 20  # f32 X, Y, Z, u, v
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+WARMUP_MIN_S = 0.25  # minimum wall time of the untimed warmup steps (clock ramp)
 VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, f32 vector peak
 VALU_ISSUE_PEAK = 1024 * 0.5 * 2.4e9  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each, 2.4 GHz
 FLOP_PER_PAIR = 11  # k_pnp_score_mf: the VALU test per pair (q1, q2, D, t: 5 FMAs + 1 multiply)
@@ -111,8 +113,24 @@ def main():
         rsac.winner(ev.p2, ev.p3, K, key_t, args.thr)
         return key_t
 
-    for _ in range(args.warmup):
+    # W untimed warmup steps, continued until at least WARMUP_MIN_S of them have run: the GPU's
+    # clock ramps up under sustained load, and 10 steps after 3 warmup steps ran 13 % slower than
+    # at steady state (0.367 vs 0.325 ms/step on one box); the timed region is still exactly K steps
+    # (the extra count is agreed over the ranks, so every rank runs the same number of steps)
+    t_w = time.perf_counter()
+    for _ in range(max(1, args.warmup)):
         step()
+    torch.cuda.synchronize()
+    spent = time.perf_counter() - t_w
+    extra = max(0, math.ceil((WARMUP_MIN_S - spent) / (spent / max(1, args.warmup))))
+    if dist is not None:
+        ex = torch.tensor([extra], dtype=torch.int64, device=par._comm_device(None))
+        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+        extra = int(ex.item())
+    for i in range(extra):
+        step()
+        if i % 16 == 15:
+            torch.cuda.synchronize()  # keep the host within a few steps of the GPU
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
