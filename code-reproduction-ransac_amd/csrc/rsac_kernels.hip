@@ -1687,7 +1687,7 @@ __device__ __forceinline__ unsigned long long mf_clock() {
 }
 
 // CHK: iterations (2 x 32 points per wave) per check window of the band minimum
-template <bool FB, int CHK, int PD, bool RA, bool PIPE = false, bool TM = false, bool INL = false>
+template <bool FB, int CHK, int PD, bool RA, bool PIPE = false, bool TM = false, bool INL = false, int PRIO = 0>
 __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, int64_t h0, int nh, int64_t p0, int start,
                                         int n, int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
                                         mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *wcnt, MfTimes &tms,
@@ -1773,8 +1773,10 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
             for (int t = 0; t < 4; ++t) {
                 const mf_h8 At = RA ? Ar[t] : alds[t][lane];
                 const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
+                if (PRIO == 1) __builtin_amdgcn_s_setprio(1);  // PRIO 1: priority around the MFMA pair
                 const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
                 const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
+                if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
@@ -1914,7 +1916,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
         // (an atomic is acknowledged by the device's coherence point, and every later wait of
         // the wave would wait for it)
         if (p == 0 && j < nh) {
-            if (start == 0 && n == n_all_pts)
+            if (!INL && start == 0 && n == n_all_pts)  // INL: its corrections are already in
                 counts[rec0 + j] = (int)(sum / 255u);
             else if (sum)
                 atomicAdd(&counts[rec0 + j], (int)(sum / 255u));
@@ -2132,7 +2134,7 @@ __device__ __forceinline__ void mfd_unit(const PnpArgs &a, int prob, int64_t h0,
 // W: minimum waves per SIMD the register budget must allow; PD: point operands loaded 0 / 1
 // iterations ahead
 template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false, bool PIPE = false, bool TM = false,
-          bool DYN = false, bool INL = false>
+          bool DYN = false, bool INL = false, int PRIO = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_mf(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int tb, int cells, int cell_pts) {
@@ -2150,6 +2152,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tiles_per_prob = (H + HB - 1) / HB;
     const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
+    if (PRIO == 2 && wave >= 2) __builtin_amdgcn_s_setprio(1);  // PRIO 2: static priority, younger half
+    if (PRIO == 3 && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);  // PRIO 3: every other block
     MfTimes tms;
     unsigned long long tk0 = 0, tb0 = 0, tbar = 0, nunits = 0;
     if constexpr (TM) tk0 = mf_clock();
@@ -2195,7 +2199,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
                     mfd_unit<RA, TM>(a, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds, wrec, wcnt, &pctr, tms,
                                      counts);
                 else
-                    mf_unit<FB, CHK, PD, RA, PIPE, TM, INL>(a, unit, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds,
+                    mf_unit<FB, CHK, PD, RA, PIPE, TM, INL, PRIO>(a, unit, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds,
                                                        wrec, wcnt, tms, counts);
             else
                 mf_sc_unit(kernarg_pnp(), prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
@@ -3370,7 +3374,7 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
 static const int64_t g_sc_cell_tiles = [] { const char *e = getenv("RSAC_SC_CELL_TILES"); return e ? atoll(e) : 0; }();
-constexpr int kDefaultScoreVariant = 73;  // fastest measured on MI355X
+constexpr int kDefaultScoreVariant = 89;  // fastest measured on MI355X
 static int g_score_variant = kDefaultScoreVariant;
 void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
 
@@ -3432,7 +3436,7 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
 }
 
 int score_record_form() {
-    if (g_score_variant >= 60 && g_score_variant <= 89) return 2;
+    if (g_score_variant >= 60 && g_score_variant <= 94) return 2;
     return g_score_variant >= 49 && g_score_variant <= 53 ? 1 : 0;
 }
 
@@ -3481,10 +3485,10 @@ static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H
 // appends at most one flagged record, so a launch whose bound exceeds a.mf_cap is split into
 // hypothesis chunks (counters reset before each).
 template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false, bool PIPE = false, bool TM = false,
-          bool DYN = false, bool INL = false>
+          bool DYN = false, bool INL = false, int PRIO = 0>
 static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    auto kern = k_pnp_score_mf<FB, CHK, W, PD, RA, PIPE, TM, DYN, INL>;
+    auto kern = k_pnp_score_mf<FB, CHK, W, PD, RA, PIPE, TM, DYN, INL, PRIO>;
     if (TM) {
         unsigned long long z[8] = {};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mf_timing), z, sizeof z, 0, hipMemcpyHostToDevice, s);
@@ -3766,6 +3770,17 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 82: return launch_mf<true, 2, 2, 1, false, true>(a, P, hyp_begin, H, counts, s);
             case 83: return launch_mf<true, 2, 3, 0, false, true>(a, P, hyp_begin, H, counts, s);
             case 85: return launch_mf<true, 2, 3, 1, true, false, false, true>(a, P, hyp_begin, H, counts, s);
+            case 90: return launch_mf<true, 2, 3, 1, true, false, false, false, false, 1>(a, P, hyp_begin, H, counts, s);
+            case 93:  // 89 + 90
+                if (a.max_n <= 256 * kWrec)
+                    return launch_mf<true, 1, 3, 1, true, false, false, false, true, 1>(a, P, hyp_begin, H, counts, s);
+                return launch_mf<true, 2, 3, 1, true, false, false, false, false, 1>(a, P, hyp_begin, H, counts, s);
+            case 94:  // 88 + 90
+                if (a.max_n <= 2 * 256 * kWrec)
+                    return launch_mf<true, 2, 3, 1, true, false, false, false, true, 1>(a, P, hyp_begin, H, counts, s);
+                return launch_mf<true, 2, 3, 1, true, false, false, false, false, 1>(a, P, hyp_begin, H, counts, s);
+            case 91: return launch_mf<true, 2, 3, 1, true, false, false, false, false, 2>(a, P, hyp_begin, H, counts, s);
+            case 92: return launch_mf<true, 2, 3, 1, true, false, false, false, false, 3>(a, P, hyp_begin, H, counts, s);
             case 88:  // 73 with the flagged windows recounted inside the unit (no recount launch):
                       // at most kWrec windows per wave and unit, so problems up to 32768 points
                 if (a.max_n <= 2 * 256 * kWrec)

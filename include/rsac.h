@@ -94,7 +94,7 @@ RSAC_EXPORT const char *rsac_last_error(void);
 RSAC_EXPORT int rsac_abi_version(void);
 RSAC_EXPORT int rsac_device_count(void);
 RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
-/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 73;
+/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 89;
  * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 f32 MFMA tilings, 16..28 the
  * branch-free alpha-beta band tilings, 40..48 the alpha-beta band with the lean hypothesis
  * loop (48 = 42 with the small-round instance), 49..53 the scaled form (k_pnp_score_sc; 49
@@ -103,7 +103,12 @@ RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* a
  * without the exact recount, timing only; 62, 63 checked every 1, 4 iterations; 64..66 = 60, 63,
  * 62 at 3 waves per SIMD; 67 (68, 69) = 64 (61, 64 at 2 waves) with the point operands loaded one
  * iteration ahead; 70..73 = 64, 65, 68 (timing only), 67 with the A operands and slopes in
- * registers)).  Counts, masks and models never depend on the variant (61, 68, 72 excepted). */
+ * registers); 74..79 the wave-autonomous MFMA kernel (k_pnp_score_mw; 77..79 timing
+ * experiments); 80..83 software-pipelined MFMA groups; 84, 87 s_memtime phase totals
+ * (diagnostics); 85, 86 dynamic iteration pairs; 88, 89 = 73 with the flagged windows recounted
+ * inside the unit (89: checked every iteration; problems up to 16384 points, else 73);
+ * 90..92 s_setprio forms; 93, 94 = 89, 88 + 90).  Counts, masks and models never depend on the
+ * variant (61, 68, 72, 78, 79 excepted). */
 RSAC_EXPORT int rsac_set_score_variant(int variant);
 
 /* The pose refit (solvePnPRefineLM, main_v1.py:508-509) of a problem above 4096 points runs
