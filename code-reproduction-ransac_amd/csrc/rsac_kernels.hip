@@ -3512,8 +3512,18 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
         const int64_t tiles = (int64_t)P_ * ((Hc + 31) / 32);
         cell_pts = 2048;
         while (cell_pts > 256 && tiles * ((max_n + cell_pts - 1) / cell_pts) < resident) cell_pts /= 2;
+        int64_t cell_tiles = std::min<int64_t>(tiles, g_sc_cell_tiles > 0 ? g_sc_cell_tiles : resident);
+        // INL: a wave lists at most kWrec windows per unit, so problems longer than that many
+        // windows run every tile by cells (of up to that length; shorter while the units would
+        // not give each resident block four)
+        constexpr int64_t win_pts = 256 * CHK * kWrec;
+        if (INL && max_n > win_pts) {
+            int64_t cp = win_pts;
+            while (cp > cell_pts && tiles * ((max_n + cp - 1) / cp) < 4 * resident) cp /= 2;
+            cell_pts = cp;
+            cell_tiles = tiles;
+        }
         cells = (max_n + cell_pts - 1) / cell_pts;
-        const int64_t cell_tiles = std::min<int64_t>(tiles, g_sc_cell_tiles > 0 ? g_sc_cell_tiles : resident);
         tb = tiles - cell_tiles;
         units = tb + cell_tiles * cells;
         bound = tb * ((max_n + 63) / 64 + 3) + cell_tiles * cells * ((cell_pts + 63) / 64 + 3);
@@ -3771,25 +3781,14 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 83: return launch_mf<true, 2, 3, 0, false, true>(a, P, hyp_begin, H, counts, s);
             case 85: return launch_mf<true, 2, 3, 1, true, false, false, true>(a, P, hyp_begin, H, counts, s);
             case 90: return launch_mf<true, 2, 3, 1, true, false, false, false, false, 1>(a, P, hyp_begin, H, counts, s);
-            case 93:  // 89 + 90
-                if (a.max_n <= 256 * kWrec)
-                    return launch_mf<true, 1, 3, 1, true, false, false, false, true, 1>(a, P, hyp_begin, H, counts, s);
-                return launch_mf<true, 2, 3, 1, true, false, false, false, false, 1>(a, P, hyp_begin, H, counts, s);
-            case 94:  // 88 + 90
-                if (a.max_n <= 2 * 256 * kWrec)
-                    return launch_mf<true, 2, 3, 1, true, false, false, false, true, 1>(a, P, hyp_begin, H, counts, s);
-                return launch_mf<true, 2, 3, 1, true, false, false, false, false, 1>(a, P, hyp_begin, H, counts, s);
+            case 93: return launch_mf<true, 1, 3, 1, true, false, false, false, true, 1>(a, P, hyp_begin, H, counts, s);
+            case 94: return launch_mf<true, 2, 3, 1, true, false, false, false, true, 1>(a, P, hyp_begin, H, counts, s);
             case 91: return launch_mf<true, 2, 3, 1, true, false, false, false, false, 2>(a, P, hyp_begin, H, counts, s);
             case 92: return launch_mf<true, 2, 3, 1, true, false, false, false, false, 3>(a, P, hyp_begin, H, counts, s);
-            case 88:  // 73 with the flagged windows recounted inside the unit (no recount launch):
-                      // at most kWrec windows per wave and unit, so problems up to 32768 points
-                if (a.max_n <= 2 * 256 * kWrec)
-                    return launch_mf<true, 2, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
-                return launch_mf<true, 2, 3, 1, true>(a, P, hyp_begin, H, counts, s);
-            case 89:
-                if (a.max_n <= 256 * kWrec)
-                    return launch_mf<true, 1, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
-                return launch_mf<true, 2, 3, 1, true>(a, P, hyp_begin, H, counts, s);
+            case 88:  // 73 with the flagged windows recounted inside the unit (no recount launch)
+                return launch_mf<true, 2, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
+            case 89:  // the same, band checked every iteration (default)
+                return launch_mf<true, 1, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
             case 86: return launch_mf<true, 2, 3, 1, false, false, false, true>(a, P, hyp_begin, H, counts, s);
             case 84:
             case 87: {  // 73 / 85 with s_memtime phase totals (diagnostics)

@@ -106,7 +106,7 @@ RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* a
  * registers); 74..79 the wave-autonomous MFMA kernel (k_pnp_score_mw; 77..79 timing
  * experiments); 80..83 software-pipelined MFMA groups; 84, 87 s_memtime phase totals
  * (diagnostics); 85, 86 dynamic iteration pairs; 88, 89 = 73 with the flagged windows recounted
- * inside the unit (89: checked every iteration; problems up to 16384 points, else 73);
+ * inside the unit (89: checked every iteration; long problems by cells of <= 16384 points);
  * 90..92 s_setprio forms; 93, 94 = 89, 88 + 90).  Counts, masks and models never depend on the
  * variant (61, 68, 72, 78, 79 excepted). */
 RSAC_EXPORT int rsac_set_score_variant(int variant);

@@ -296,7 +296,7 @@ def test_f32_prefilter_equals_exact_kernel(n, seed, H, score_variant):
     np.testing.assert_array_equal(c_f, c_e)
 
 
-@pytest.mark.parametrize("variant", [73, 74])
+@pytest.mark.parametrize("variant", [73, 74, 89])
 def test_f32_prefilter_record_list_chunks(variant):
     # 100k points x 50k hypotheses: the flagged-record bound of one launch exceeds a record
     # segment (a.mf_cap / 8), so the launch is split into hypothesis chunks (queue counters reset
