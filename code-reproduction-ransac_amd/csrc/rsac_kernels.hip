@@ -805,6 +805,106 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 // the operations of p3p_lambdatwist for that candidate) and its 4th-point error; the four
 // lanes pick the smallest error, the lowest candidate on ties (= pnp_minimal's first-one rule),
 // and the winner writes the record.  Results equal k_pnp_solve's bit for bit.
+// Two lanes per hypothesis (rounds above solve4_max_hyps, up to solve2_max_hyps): lane s runs
+// the Lambda Twist sign branch s and both of its tau candidates (candidates 2s and 2s + 1, in
+// that order), so the common part is done twice instead of four times and a SIMD holds twice
+// the waves of the one-lane kernel.  The pick is the serial solver's: the smallest 4th-point
+// error, the lowest candidate on a tie.
+__global__ __launch_bounds__(256) void k_pnp_solve2(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    const int prob = blockIdx.y;
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int hl = gt >> 1, sgn = gt & 1;
+    if (gt == 0 && prob == 0) {
+        if (a.queue) reset_pnp_queue(a.queue);
+    }
+    const bool live = hl < H;  // the 2 lanes of a hypothesis share it: shuffles stay in the pair
+    const int64_t h = hyp_begin + hl;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
+    int32_t idx[4] = {0, 0, 0, 0};
+    int8_t st = -1;
+    if (live) {
+        if (a.subsets) {
+            st = a.sub_status[rec];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) idx[j] = a.subsets[rec * 4 + j];
+        } else {
+            Philox rng;
+            rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
+            st = (n >= 4 && rng.subset<4>(n, idx) == 0) ? 1 : -1;
+        }
+    }
+    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
+    double e = 0.0;
+    int mine = 4;  // this lane's kept candidate (4: none)
+    const Cam k{a.cams[4 * prob], a.cams[4 * prob + 1], a.cams[4 * prob + 2], a.cams[4 * prob + 3]};
+    if (st > 0) {
+        float X[4], Y[4], Z[4], U[4], V[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t i = p0 + idx[j];
+            X[j] = a.X[i]; Y[j] = a.Y[i]; Z[j] = a.Z[i]; U[j] = a.U[i]; V[j] = a.V[i];
+        }
+        double yb[9], xw[9];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            bearing(k, U[j], V[j], yb + 3 * j);
+            xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
+        }
+        LtCommon L;
+        double w0, w1, tau[2];
+        if (lt_common(yb, xw, L) && lt_sign(L, sgn, w0, w1, tau)) {
+#pragma unroll 1
+            for (int ti = 0; ti < 2; ++ti) {
+                const int cand = 2 * sgn + ti;
+                auto emit = [&](const double *Rk, const double *tk) {
+                    const double ek = pnp_fourth_error(Rk, tk, X, Y, Z, U, V, k);
+                    if (!(ek == ek)) return;
+                    if (mine < 4 && !(ek < e)) return;  // the first smallest error wins
+                    mine = cand;
+                    e = ek;
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) R[q] = Rk[q];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) t[q] = tk[q];
+                };
+                (void)lt_tau(L, w0, w1, tau[ti], yb, xw, emit);
+            }
+        }
+    }
+    // the pair's winner: smallest e, then the lowest candidate
+    int win = mine;
+    double we = mine < 4 ? e : 0.0;
+    {
+        const int ow = __shfl_xor(win, 1);
+        const double oe = __shfl_xor(we, 1);
+        if (ow < 4 && (win == 4 || oe < we || (oe == we && ow < win))) {
+            win = ow;
+            we = oe;
+        }
+    }
+    if (!live) return;
+    const bool ok = win < 4;
+    if (ok ? mine != win : sgn != 0) return;  // one writer per hypothesis
+    const int8_t sv = st > 0 ? (ok ? 1 : 0) : st;
+    double *m = a.models + rec * kModelStride;
+    if (!ok)
+        for (int q = 0; q < 9; ++q) R[q] = 0.0;
+    if (!ok)
+        for (int q = 0; q < 3; ++q) t[q] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) m[q] = R[q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
+    m[kValidSlot] = sv > 0 ? 1.0 : 0.0;
+    a.status[rec] = sv;
+    if (a.counts_out) a.counts_out[rec] = 0;
+    if (a.fmodels)
+        write_fmodel(R, t, sv > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
+}
+
 __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3303,6 +3403,12 @@ static int64_t solve4_max_hyps() {
     static const int64_t v = [] { const char *e = getenv("RSAC_SOLVE4_MAX"); return e ? atoll(e) : 4096; }();
     return v;
 }
+// RSAC_SOLVE2_MAX: rounds up to this many hypotheses (above solve4_max_hyps) solve on two lanes
+// per hypothesis (k_pnp_solve2), larger ones on one
+static int64_t solve2_max_hyps() {
+    static const int64_t v = [] { const char *e = getenv("RSAC_SOLVE2_MAX"); return e ? atoll(e) : 0; }();
+    return v;
+}
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
                             double *frame, float *fconst, hipStream_t s, const PnpPrepare *prep) {
@@ -3367,6 +3473,8 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     if ((int64_t)P * H <= solve4_max_hyps())
         hipLaunchKernelGGL(k_pnp_solve4, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+    else if ((int64_t)P * H <= solve2_max_hyps())
+        hipLaunchKernelGGL(k_pnp_solve2, dim3(cdiv(2 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     else
         hipLaunchKernelGGL(k_pnp_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     return hipGetLastError();
