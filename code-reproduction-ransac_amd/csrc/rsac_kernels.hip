@@ -1984,17 +1984,11 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
 #pragma unroll
         for (int g = 0; g < 4; ++g) cl[wave][4 * t + g][lane] = vc[t][g];
     __syncthreads();
-    // the waves' flagged iterations: one atomic for the block (in flight during the count
-    // reduction; inline asm, as the atomic optimizer's fix-up would wait for it at once), then a
-    // store per record
-    int roff = 0, rtot = 0;
+    // the waves' flagged iterations: one atomic for the block (taken before thread 0's count
+    // atomic, so its wait does not cover that), then a store per record
     if (FB && threadIdx.x == 0) {
-        rtot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        if (rtot)
-            asm volatile("global_atomic_add %0, %1, %2, off sc0"
-                         : "+v"(roff)
-                         : "v"(rec_queue(a.queue, blockIdx.x % kQSub)), "v"(rtot)
-                         : "memory");
+        const int rtot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        wcnt[4] = rtot ? atomicAdd(rec_queue(a.queue, blockIdx.x % kQSub), rtot) : 0;
     }
     {
         const int j = threadIdx.x >> 3, p = threadIdx.x & 7;
@@ -2007,11 +2001,6 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
         sum += __shfl_xor(sum, 1);
         sum += __shfl_xor(sum, 2);
         sum += __shfl_xor(sum, 4);
-        // thread 0 takes its record offset first, so its wait does not cover a count atomic
-        if (FB && threadIdx.x == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(roff)::"memory");
-            wcnt[4] = rtot ? roff : 0;
-        }
         // a unit over all of its problem's points is the only writer of its counts: a store
         // (an atomic is acknowledged by the device's coherence point, and every later wait of
         // the wave would wait for it)
@@ -2183,14 +2172,9 @@ __device__ __forceinline__ void mfd_unit(const PnpArgs &a, int prob, int64_t h0,
 #pragma unroll
         for (int q = 0; q < 4; ++q) cl[wave][4 * t + q][lane] = vc[t][q];
     __syncthreads();
-    int roff = 0, rtot = 0;
     if (threadIdx.x == 0) {
-        rtot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        if (rtot)
-            asm volatile("global_atomic_add %0, %1, %2, off sc0"
-                         : "+v"(roff)
-                         : "v"(rec_queue(a.queue, blockIdx.x % kQSub)), "v"(rtot)
-                         : "memory");
+        const int rtot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        wcnt[4] = rtot ? atomicAdd(rec_queue(a.queue, blockIdx.x % kQSub), rtot) : 0;
     }
     {
         const int j = threadIdx.x >> 3, p = threadIdx.x & 7;
@@ -2203,10 +2187,6 @@ __device__ __forceinline__ void mfd_unit(const PnpArgs &a, int prob, int64_t h0,
         sum += __shfl_xor(sum, 1);
         sum += __shfl_xor(sum, 2);
         sum += __shfl_xor(sum, 4);
-        if (threadIdx.x == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(roff)::"memory");
-            wcnt[4] = rtot ? roff : 0;
-        }
         if (p == 0 && j < nh) {
             if (start == 0 && n == n_all_pts)
                 counts[rec0 + j] = (int)(sum / 255u);
@@ -2267,11 +2247,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     for (;;) {
         const int unit = __builtin_amdgcn_readfirstlane(unit_s);
         if (unit >= n_units) break;  // uniform: every wave of every block reaches it
-        // the next unit's index, in flight while this unit runs (inline asm: the atomic
-        // optimizer's fix-up would wait for the result at once); waited for at the unit's end
-        int nx = 0;
-        if (threadIdx.x == 0)
-            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "+v"(nx) : "v"(uq), "v"(1) : "memory");
         int tile, c0, c1;
         if (unit < tb) {
             tile = unit;
@@ -2308,10 +2283,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
             tb0 = mf_clock();
             ++nunits;
         }
-        if (threadIdx.x == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(nx)::"memory");
-            unit_s = qk + kQSub * nx;  // every thread read unit_s before the unit's barriers
-        }
+        // the next unit (every thread read unit_s before the unit's barriers).  Taking it one
+        // unit ahead with an inline-asm atomic measured the same, and a register allocator that
+        // spills the asm result before it arrives would read a stale unit index
+        if (threadIdx.x == 0) unit_s = qk + kQSub * atomicAdd(uq, 1);
         __syncthreads();  // the unit's LDS and unit_s are rewritten by the next unit
         if constexpr (TM) tbar += mf_clock() - tb0;
     }
@@ -2586,11 +2561,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
     bool in_range = false;
     while (ci < nq) {  // uniform per wave: every wave reaches the end of its queue
         const int cur = qk + kQSub * ci;
-        // the next unit's index, in flight while this unit runs (no atomic optimizer here: its
-        // per-lane fix-up would wait for the result at once); waited for below
-        int nx = ci + nwq;
-        if (!(XP & 1) && lane == 0)
-            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "+v"(nx) : "v"(uq), "v"(1) : "memory");
+
         int tile, start, len;
         if (cur < ua) {
             tile = cur / cb;
@@ -2618,8 +2589,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
             else
                 mw_exact_unit(a, prob, h0, nh, p0, start, n, lane, counts);
         }
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(nx)::"memory");
-        ci = __builtin_amdgcn_readfirstlane(nx);
+        int nx = ci + nwq;  // XP & 1: static assignment
+        if (!(XP & 1)) {
+            if (lane == 0) nx = atomicAdd(uq, 1);
+            nx = __builtin_amdgcn_readfirstlane(nx);
+        }
+        ci = nx;
     }
     if (nw) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -3544,7 +3519,7 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
 }
 
 int score_record_form() {
-    if (g_score_variant >= 60 && g_score_variant <= 94) return 2;
+    if (g_score_variant >= 60 && g_score_variant <= 98) return 2;
     return g_score_variant >= 49 && g_score_variant <= 53 ? 1 : 0;
 }
 
@@ -3897,6 +3872,10 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
                 return launch_mf<true, 2, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
             case 89:  // the same, band checked every iteration (default)
                 return launch_mf<true, 1, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
+            case 95: return launch_mf<true, 1, 4, 1, false, false, false, false, true>(a, P, hyp_begin, H, counts, s);
+            case 96: return launch_mf<true, 1, 4, 0, false, false, false, false, true>(a, P, hyp_begin, H, counts, s);
+            case 97: return launch_mf<true, 1, 3, 1, false, false, false, false, true>(a, P, hyp_begin, H, counts, s);
+            case 98: return launch_mf<true, 1, 3, 0, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
             case 86: return launch_mf<true, 2, 3, 1, false, false, false, true>(a, P, hyp_begin, H, counts, s);
             case 84:
             case 87: {  // 73 / 85 with s_memtime phase totals (diagnostics)
