@@ -3457,7 +3457,7 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
 static const int64_t g_sc_cell_tiles = [] { const char *e = getenv("RSAC_SC_CELL_TILES"); return e ? atoll(e) : 0; }();
-constexpr int kDefaultScoreVariant = 89;  // fastest measured on MI355X
+constexpr int kDefaultScoreVariant = 98;  // fastest measured on MI355X
 static int g_score_variant = kDefaultScoreVariant;
 void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
 

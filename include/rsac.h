@@ -94,7 +94,7 @@ RSAC_EXPORT const char *rsac_last_error(void);
 RSAC_EXPORT int rsac_abi_version(void);
 RSAC_EXPORT int rsac_device_count(void);
 RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
-/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 89;
+/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 98;
  * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 f32 MFMA tilings, 16..28 the
  * branch-free alpha-beta band tilings, 40..48 the alpha-beta band with the lean hypothesis
  * loop (48 = 42 with the small-round instance), 49..53 the scaled form (k_pnp_score_sc; 49
@@ -107,7 +107,8 @@ RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* a
  * experiments); 80..83 software-pipelined MFMA groups; 84, 87 s_memtime phase totals
  * (diagnostics); 85, 86 dynamic iteration pairs; 88, 89 = 73 with the flagged windows recounted
  * inside the unit (89: checked every iteration; long problems by cells of <= 16384 points);
- * 90..92 s_setprio forms; 93, 94 = 89, 88 + 90).  Counts, masks and models never depend on the
+ * 90..92 s_setprio forms; 93, 94 = 89, 88 + 90; 95..97 = 89 at 4 waves / A operands from LDS;
+ * 98 = 89 without the point-operand prefetch, the default).  Counts, masks and models never depend on the
  * variant (61, 68, 72, 78, 79 excepted). */
 RSAC_EXPORT int rsac_set_score_variant(int variant);
 
