@@ -1701,8 +1701,10 @@ __device__ __forceinline__ mf_h8 mw_operand(const float *__restrict__ recs, int 
 // that does not depend on the test (point operands, the slopes and bands of the 32 hypotheses,
 // the lane's two points in f32) is issued up front; per flagged group the A operand, per slot
 // with an undecided pair its model.
+// lcorr (inline recount): the corrections go to the unit's LDS array (index: hypothesis within
+// the unit) instead of global atomics; the unit's epilogue folds them into its counts
 __device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfFlag &f, int base, int col, int half,
-                                           int32_t *__restrict__ counts) {
+                                           int32_t *__restrict__ counts, int *lcorr = nullptr) {
     const int64_t p0 = f.p0, rec0 = f.rec0;
     const uint32_t fl = f.fl;
     const int nh = f.nh;
@@ -1748,7 +1750,12 @@ __device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfFlag &f, in
                 if (wb)
                     c += (mv && pnp_err(md, md + 9, k, (double)Xb, (double)Yb, (double)Zb, Uxb, Vxb) <= thr2 ? 1 : 0) -
                          (rb.D < 0.f ? 1 : 0);
-                if (c) atomicAdd(&counts[rec0 + j], c);
+                if (c) {
+                    if (lcorr)
+                        atomicAdd(&lcorr[j], c);
+                    else
+                        atomicAdd(&counts[rec0 + j], c);
+                }
             }
         }
     }
@@ -1791,13 +1798,14 @@ template <bool FB, int CHK, int PD, bool RA, bool PIPE = false, bool TM = false,
 __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, int64_t h0, int nh, int64_t p0, int start,
                                         int n, int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
                                         mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *wcnt, MfTimes &tms,
-                                        int32_t *__restrict__ counts) {
+                                        int32_t *__restrict__ counts, int *lcorr = nullptr) {
     unsigned long long ts0 = 0, ts1 = 0;
     if constexpr (TM) ts0 = mf_clock();
     constexpr int HB = 32;
     const int col = lane & 31, half = lane >> 5;
     const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
     const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
+    if (INL && threadIdx.x < HB) lcorr[threadIdx.x] = 0;  // the unit's corrections (before the barrier)
     if (threadIdx.x < HB) {
         // a' and b' of slot (t, g, half) = hypothesis 8t + 2g + half; past the round: b' = -inf
         // (records without a model carry a' = 0, b' = -inf themselves)
@@ -1967,7 +1975,8 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
             const int base = b0 + 256 * (int)(w.x & 0xFFFFFFu), wi = (int)(w.x >> 24);
             const MfFlag f{rec0, p0, base, n, w.y, (int16_t)nh, (int16_t)wi};
 #pragma unroll 1
-            for (int iw = 0; iw < wi && base + 256 * iw < n; ++iw) mf_recount(a, f, base + 256 * iw, col, half, counts);
+            for (int iw = 0; iw < wi && base + 256 * iw < n; ++iw)
+                mf_recount(a, f, base + 256 * iw, col, half, counts, lcorr);
         }
         nw = 0;
     }
@@ -2005,10 +2014,12 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
         // (an atomic is acknowledged by the device's coherence point, and every later wait of
         // the wave would wait for it)
         if (p == 0 && j < nh) {
-            if (!INL && start == 0 && n == n_all_pts)  // INL: its corrections are already in
-                counts[rec0 + j] = (int)(sum / 255u);
-            else if (sum)
-                atomicAdd(&counts[rec0 + j], (int)(sum / 255u));
+            // INL: + the unit's corrections (in LDS, complete at the barrier above)
+            const int cj = (int)(sum / 255u) + (INL ? lcorr[j] : 0);
+            if (start == 0 && n == n_all_pts)
+                counts[rec0 + j] = cj;
+            else if (cj)
+                atomicAdd(&counts[rec0 + j], cj);
         }
     }
     if (FB) {
@@ -2224,6 +2235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     __shared__ __attribute__((aligned(16))) float ab[2][2][4][4];
     __shared__ uint2 wrec[4][kWrec];
     __shared__ int wcnt[5];
+    __shared__ int lcorr[32];  // INL: the unit's exact-recount corrections
     __shared__ int pctr;  // DYN: the unit's next iteration pair
     __shared__ mf_h8 alds[4][64];
     __shared__ int red[4][HB];                                                 // sc_unit
@@ -2275,7 +2287,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
                                      counts);
                 else
                     mf_unit<FB, CHK, PD, RA, PIPE, TM, INL, PRIO>(a, unit, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds,
-                                                       wrec, wcnt, tms, counts);
+                                                       wrec, wcnt, tms, counts, lcorr);
             else
                 mf_sc_unit(kernarg_pnp(), prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
         }
