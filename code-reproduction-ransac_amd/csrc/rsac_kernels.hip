@@ -1895,17 +1895,34 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
             }
         }
         if (FB && (++it == CHK || i == iters - 1)) {  // end of a check window (uniform)
-            uint32_t fl = 0;
+            // one OR of the 16 slots' ballots (a compare and a scalar OR per slot); the slot
+            // bits only when some slot is flagged (rare)
+            uint64_t any = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
-                    fl |= __ballot(!(tm[t][g] > bg)) ? (1u << (4 * t + g)) : 0u;
-                    tm[t][g] = __builtin_inff();
+                    any |= __ballot(!(tm[t][g] > bg));
                 }
             }
+            uint32_t fl = 0;
+            if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
+                        fl |= __ballot(!(tm[t][g] > bg)) ? (1u << (4 * t + g)) : 0u;
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) tm[t][g] = __builtin_inff();
             if (__builtin_expect(fl != 0, 0)) {
                 // kept in the wave's LDS list (first iteration, window length in bits 24..),
                 // appended to a.mf_list with the unit's (one atomic per block), or at once by the
