@@ -1019,7 +1019,7 @@ void rsac_destroy(rsac_ctx *c) {
 }
 
 int rsac_set_score_variant(int variant) {
-    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 53) && (variant < 60 || variant > 98)))
+    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 53) && (variant < 60 || variant > 99)))
         return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
     set_score_variant(variant);
     return RSAC_OK;

@@ -1876,6 +1876,37 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
+        } else if constexpr (PRIO == 4) {
+            // the count and band minimum of group t - 1 are issued right behind group t's MFMAs
+            // (they fill the matrix shadow instead of waiting behind the next pair's FMAs)
+            MfPair pa[4], pb[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const mf_h8 At = RA ? Ar[t] : alds[t][lane];
+                const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
+                const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
+                const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (t > 0) {
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        vc[t - 1][g] = mf_cnt255(vc[t - 1][g], pa[g].D, pb[g].D);
+                        if (FB) tm[t - 1][g] = mf_min3(tm[t - 1][g], pa[g].t, pb[g].t);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
+                    pa[g] = mf_pair(xa, g, ua, ag);
+                    pb[g] = mf_pair(xb, g, ub, ag);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                vc[3][g] = mf_cnt255(vc[3][g], pa[g].D, pb[g].D);
+                if (FB) tm[3][g] = mf_min3(tm[3][g], pa[g].t, pb[g].t);
+            }
         } else {
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -3548,7 +3579,7 @@ static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H
 }
 
 int score_record_form() {
-    if (g_score_variant >= 60 && g_score_variant <= 98) return 2;
+    if (g_score_variant >= 60 && g_score_variant <= 99) return 2;
     return g_score_variant >= 49 && g_score_variant <= 53 ? 1 : 0;
 }
 
@@ -3905,6 +3936,8 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             case 96: return launch_mf<true, 1, 4, 0, false, false, false, false, true>(a, P, hyp_begin, H, counts, s);
             case 97: return launch_mf<true, 1, 3, 1, false, false, false, false, true>(a, P, hyp_begin, H, counts, s);
             case 98: return launch_mf<true, 1, 3, 0, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
+            case 99:  // 98 with the count / band minimum of a group issued behind the next group's MFMAs
+                return launch_mf<true, 1, 3, 0, true, false, false, false, true, 4>(a, P, hyp_begin, H, counts, s);
             case 86: return launch_mf<true, 2, 3, 1, false, false, false, true>(a, P, hyp_begin, H, counts, s);
             case 84:
             case 87: {  // 73 / 85 with s_memtime phase totals (diagnostics)

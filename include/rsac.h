@@ -108,7 +108,8 @@ RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* a
  * (diagnostics); 85, 86 dynamic iteration pairs; 88, 89 = 73 with the flagged windows recounted
  * inside the unit (89: checked every iteration; long problems by cells of <= 16384 points);
  * 90..92 s_setprio forms; 93, 94 = 89, 88 + 90; 95..97 = 89 at 4 waves / A operands from LDS;
- * 98 = 89 without the point-operand prefetch, the default).  Counts, masks and models never depend on the
+ * 98 = 89 without the point-operand prefetch, the default; 99 = 98 with the count of a group
+ * issued behind the next group's MFMAs).  Counts, masks and models never depend on the
  * variant (61, 68, 72, 78, 79 excepted). */
 RSAC_EXPORT int rsac_set_score_variant(int variant);
 

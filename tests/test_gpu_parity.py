@@ -274,7 +274,7 @@ def test_degenerate_inputs():
 # variant (VALU f32, packed f32, MFMA) is checked, then the default is restored.
 # ---------------------------------------------------------------------------------------------
 SCORE_VARIANTS = [0, 1, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28,
-                  40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 60, 62, 63, 64, 65, 66, 67, 69, 70, 71, 73, 74, 75, 76, 80, 81, 82, 83, 85, 86, 88, 89, 90, 92, 93, 94, 95, 96, 97, 98]
+                  40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 60, 62, 63, 64, 65, 66, 67, 69, 70, 71, 73, 74, 75, 76, 80, 81, 82, 83, 85, 86, 88, 89, 90, 92, 93, 94, 95, 96, 97, 98, 99]
 
 
 @pytest.fixture(params=SCORE_VARIANTS)
