@@ -243,7 +243,7 @@ def main():
             "kernels_ms": {"pnp_solve": solve_avg, "pnp_score": score_avg},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "scoring stage (HIP events): k_pnp_score_mf + k_pnp_mf_recount + k_best_key",
+                         "kernel": "scoring stage (HIP events): k_pnp_score_mf (flagged windows recounted inside, variant 98) + k_best_key",
                          "algorithmic_bytes_per_launch": args.points * BYTES_PER_POINT * H},
             "roofline_valu": roof_valu,
             "roofline_mfma": {"bound": "mfma", "flop_per_pair": MFMA_FLOP_PER_PAIR,
