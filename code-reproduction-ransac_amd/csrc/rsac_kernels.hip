@@ -3504,7 +3504,10 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
 }
 
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
-    const PnpArgs ka = round_args(a, P, H);
+    PnpArgs ka = round_args(a, P, H);
+    // RSAC_DBG_SOLVE_NO_RECORDS: timing experiment only (the scoring records go stale)
+    static const bool no_rec = getenv("RSAC_DBG_SOLVE_NO_RECORDS") != nullptr;
+    if (no_rec) ka.fmodels = nullptr;
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     if ((int64_t)P * H <= solve4_max_hyps())
         hipLaunchKernelGGL(k_pnp_solve4, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
