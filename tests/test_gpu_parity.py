@@ -166,7 +166,7 @@ def test_pnp_batched_ragged_equals_singles():
         assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
 
 
-@pytest.mark.parametrize("variant", [49, 73, 74])
+@pytest.mark.parametrize("variant", [49, 73, 74, 98])
 def test_pnp_batched_mixed_scales_equals_oracle(variant):
     # one batch, problems inside and outside the MFMA scorer's f16 operand range (centred
     # coordinates above 2^15 or below 1/64 run the form-1 path of k_pnp_score_mf)
@@ -296,7 +296,7 @@ def test_f32_prefilter_equals_exact_kernel(n, seed, H, score_variant):
     np.testing.assert_array_equal(c_f, c_e)
 
 
-@pytest.mark.parametrize("variant", [73, 74, 89])
+@pytest.mark.parametrize("variant", [73, 74, 89, 98])
 def test_f32_prefilter_record_list_chunks(variant):
     # 100k points x 50k hypotheses: the flagged-record bound of one launch exceeds a record
     # segment (a.mf_cap / 8), so the launch is split into hypothesis chunks (queue counters reset
