@@ -1798,7 +1798,8 @@ template <bool FB, int CHK, int PD, bool RA, bool PIPE = false, bool TM = false,
 __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, int64_t h0, int nh, int64_t p0, int start,
                                         int n, int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
                                         mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *wcnt, MfTimes &tms,
-                                        int32_t *__restrict__ counts, int *lcorr = nullptr) {
+                                        int32_t *__restrict__ counts, int *lcorr = nullptr,
+                                        unsigned long long *blk_best = nullptr) {
     unsigned long long ts0 = 0, ts1 = 0;
     if constexpr (TM) ts0 = mf_clock();
     constexpr int HB = 32;
@@ -2061,6 +2062,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
         // a unit over all of its problem's points is the only writer of its counts: a store
         // (an atomic is acknowledged by the device's coherence point, and every later wait of
         // the wave would wait for it)
+        unsigned long long kj = 0;
         if (p == 0 && j < nh) {
             // INL: + the unit's corrections (in LDS, complete at the barrier above)
             const int cj = (int)(sum / 255u) + (INL ? lcorr[j] : 0);
@@ -2068,6 +2070,20 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
                 counts[rec0 + j] = cj;
             else if (cj)
                 atomicAdd(&counts[rec0 + j], cj);
+            // fused best key (INL, every unit over its whole problem: the counts are final here):
+            // k_best_key's packed key of hypothesis h0 + j
+            if (INL && blk_best && cj > 0 && a.status[rec0 + j] > 0) {
+                const uint64_t g = (uint64_t)(a.rng_base + h0 + j);
+                kj = ((unsigned long long)(uint32_t)cj << 32) | (0xFFFFFFFFull - (g & 0xFFFFFFFFull));
+            }
+        }
+        if (INL && blk_best) {  // uniform: the wave's maximum into the block's (LDS)
+#pragma unroll
+            for (int o = 8; o < 64; o <<= 1) {
+                const unsigned long long other = __shfl_xor(kj, o);
+                kj = other > kj ? other : kj;
+            }
+            if (lane == 0 && kj) atomicMax(blk_best, kj);
         }
     }
     if (FB) {
@@ -2284,6 +2300,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     __shared__ uint2 wrec[4][kWrec];
     __shared__ int wcnt[5];
     __shared__ int lcorr[32];  // INL: the unit's exact-recount corrections
+    __shared__ unsigned long long blk_best;  // INL with a.best_key: the block's best packed key
     __shared__ int pctr;  // DYN: the unit's next iteration pair
     __shared__ mf_h8 alds[4][64];
     __shared__ int red[4][HB];                                                 // sc_unit
@@ -2292,6 +2309,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tiles_per_prob = (H + HB - 1) / HB;
     const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
+    // INL with a.best_key (the launcher passes it only when every unit covers its whole problem):
+    // the best key is reduced here, one atomic per block at the end (no k_best_key launch)
+    const bool fuse_key = INL && a.best_key != nullptr;
+    if (threadIdx.x == 0) blk_best = 0;
     if (PRIO == 2 && wave >= 2) __builtin_amdgcn_s_setprio(1);  // PRIO 2: static priority, younger half
     if (PRIO == 3 && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);  // PRIO 3: every other block
     MfTimes tms;
@@ -2335,7 +2356,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
                                      counts);
                 else
                     mf_unit<FB, CHK, PD, RA, PIPE, TM, INL, PRIO>(a, unit, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds,
-                                                       wrec, wcnt, tms, counts, lcorr);
+                                                       wrec, wcnt, tms, counts, lcorr,
+                                                       fuse_key ? &blk_best : nullptr);
             else
                 mf_sc_unit(kernarg_pnp(), prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
         }
@@ -2350,6 +2372,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         __syncthreads();  // the unit's LDS and unit_s are rewritten by the next unit
         if constexpr (TM) tbar += mf_clock() - tb0;
     }
+    if (fuse_key && threadIdx.x == 0 && blk_best) atomicMax(a.best_key, blk_best);  // after the last barrier
     if constexpr (TM) {
         if (lane == 0) {
             atomicAdd(&g_mf_timing[0], mf_clock() - tk0);
@@ -3654,11 +3677,19 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
             (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P_, s);
     }
     const int64_t max_n = std::max<int64_t>(1, a.max_n);
+    // fused best key (RSAC_FUSE_KEY=1; INL, one problem, every tile a whole-problem unit, at
+    // least one tile per resident block): the kernel reduces the key from its final counts, no
+    // k_best_key launch.  Off by default: without the tail's cells the C2 step is 4 % slower
+    // (0.312 vs 0.298 ms, scripts/fuse_key_ab.sh) than with them and the separate launch.
+    static const bool fuse_env = [] { const char *e = getenv("RSAC_FUSE_KEY"); return e && atoi(e) != 0; }();
+    const bool fuse = INL && fuse_env && a.best_key && P_ == 1 && max_n <= 256 * CHK * kWrec &&
+                      (int64_t)((H + 31) / 32) >= resident;
     auto plan = [&](int64_t Hc, int64_t &cell_pts, int64_t &cells, int64_t &tb, int64_t &units, int64_t &bound) {
         const int64_t tiles = (int64_t)P_ * ((Hc + 31) / 32);
         cell_pts = 2048;
         while (cell_pts > 256 && tiles * ((max_n + cell_pts - 1) / cell_pts) < resident) cell_pts /= 2;
         int64_t cell_tiles = std::min<int64_t>(tiles, g_sc_cell_tiles > 0 ? g_sc_cell_tiles : resident);
+        if (fuse) cell_tiles = 0;
         // INL: a wave lists at most kWrec windows per unit, so problems longer than that many
         // windows run every tile by cells (of up to that length; shorter while the units would
         // not give each resident block four)
@@ -3687,7 +3718,7 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
         Hc = 32 * tiles_c;
     }
     PnpArgs ka = a;
-    ka.best_key = nullptr;  // reduced below from the complete counts
+    if (!fuse) ka.best_key = nullptr;  // reduced below from the complete counts
     for (int64_t h = 0; h < H; h += Hc) {
         const int32_t Hh = (int32_t)std::min<int64_t>(Hc, H - h);
         if (Hc < H) {
@@ -3716,7 +3747,7 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
                                    kQSub, 0, 0);
         }
     }
-    if (a.best_key) {
+    if (a.best_key && !fuse) {
         unsigned g = cdiv(H, 1024);
         if (g > 128) g = 128;
         hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
