@@ -3541,6 +3541,11 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     return hipGetLastError();
 }
 
+static int64_t env_i64(const char *name, int64_t dflt) {
+    const char *e = getenv(name);
+    return e ? atoll(e) : dflt;
+}
+
 // scoring-kernel variants (points per lane, hypotheses per block); 0 = default
 static const int64_t g_sc_cell_tiles = [] { const char *e = getenv("RSAC_SC_CELL_TILES"); return e ? atoll(e) : 0; }();
 constexpr int kDefaultScoreVariant = 98;  // fastest measured on MI355X
@@ -3686,7 +3691,8 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
                       (int64_t)((H + 31) / 32) >= resident;
     auto plan = [&](int64_t Hc, int64_t &cell_pts, int64_t &cells, int64_t &tb, int64_t &units, int64_t &bound) {
         const int64_t tiles = (int64_t)P_ * ((Hc + 31) / 32);
-        cell_pts = 2048;
+        static const int64_t cell0 = std::max<int64_t>(256, env_i64("RSAC_MF_CELL_PTS", 2048) / 256 * 256);
+        cell_pts = cell0;
         while (cell_pts > 256 && tiles * ((max_n + cell_pts - 1) / cell_pts) < resident) cell_pts /= 2;
         int64_t cell_tiles = std::min<int64_t>(tiles, g_sc_cell_tiles > 0 ? g_sc_cell_tiles : resident);
         if (fuse) cell_tiles = 0;
@@ -3762,10 +3768,6 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
 // first rounds).  A unit appends at most one flagged record per iteration, so a launch whose
 // bound exceeds a.mf_cap is split into hypothesis chunks (counters reset before each).
 // RSAC_MW_BIG / RSAC_MW_SMALL / RSAC_MW_TAIL: tuning knobs (points, points, tiles).
-static int64_t env_i64(const char *name, int64_t dflt) {
-    const char *e = getenv(name);
-    return e ? atoll(e) : dflt;
-}
 template <int CHK, int PD, int XP = 0>
 static hipError_t launch_mw(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
