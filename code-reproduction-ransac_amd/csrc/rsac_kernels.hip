@@ -2328,6 +2328,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     for (;;) {
         const int unit = __builtin_amdgcn_readfirstlane(unit_s);
         if (unit >= n_units) break;  // uniform: every wave of every block reaches it
+        // the next unit's index, in flight while this unit runs: the atomic optimizer is off for
+        // this file (Makefile), so the compiler waits for the result only where it is used, at
+        // the unit's end (and a spill of the pending register waits for it too)
+        int nx = 0;
+        if (threadIdx.x == 0) nx = atomicAdd(uq, 1);
         int tile, c0, c1;
         if (unit < tb) {
             tile = unit;
@@ -2365,10 +2370,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
             tb0 = mf_clock();
             ++nunits;
         }
-        // the next unit (every thread read unit_s before the unit's barriers).  Taking it one
-        // unit ahead with an inline-asm atomic measured the same, and a register allocator that
-        // spills the asm result before it arrives would read a stale unit index
-        if (threadIdx.x == 0) unit_s = qk + kQSub * atomicAdd(uq, 1);
+        // the next unit (every thread read unit_s before the unit's barriers); the empty asm keeps
+        // the arithmetic on nx (and so the wait for it) here
+        if (threadIdx.x == 0) {
+            asm volatile("" : "+v"(nx));
+            unit_s = qk + kQSub * nx;
+        }
         __syncthreads();  // the unit's LDS and unit_s are rewritten by the next unit
         if constexpr (TM) tbar += mf_clock() - tb0;
     }
