@@ -191,6 +191,22 @@ def test_pnp_batched_mixed_scales_equals_oracle(variant):
         assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
 
 
+def test_pnp_batched_long_problem_cells_equals_oracle():
+    # a batch with a problem longer than one inline-recount unit (16 384 points): every tile of
+    # the batch then runs by cells, and the short problem's cells past its end are skipped.  90 %
+    # outliers keep the adaptive bound above the budget, so the rounds grow past the small-round
+    # instance (16 tiles) into the MFMA scorer
+    base = [synth.pnp_problem(n, 0.9, seed=90 + i) for i, n in enumerate([20000, 3000])]
+    out = rsac.pnp_ransac_batched([p["points2d"] for p in base], [p["points3d"] for p in base],
+                                  [p["K"] for p in base], 2048, 30.0, refine=False)
+    for p, (R, t, m, ni) in zip(base, out):
+        ref = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 0.99, 2048, 0x5EED)
+        assert ref["iters"] == 2048
+        assert ni == ref["n_inliers"]
+        np.testing.assert_array_equal(m, ref["mask"])
+        assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+
+
 def test_k_sweep_batched():
     """testpro-K.py:58-75 as one batched call over the 27 intrinsics."""
     Ks = synth.testpro_k_candidates()
