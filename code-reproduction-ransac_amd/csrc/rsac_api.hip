@@ -28,6 +28,14 @@ using namespace rsac;
 static thread_local std::string g_err;
 
 static int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static bool solve_overlap() {
+    static const bool on = [] {
+        const char *v = getenv("RSAC_SOLVE_OVERLAP");
+        return v && atoi(v) > 0;
+    }();
+    return on;
+}
+
 static int fail(int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;
@@ -129,6 +137,10 @@ struct rsac_ctx {
     // the last async copy out of h_pts / h_small: the host waits on it before rewriting the
     // buffer (calls may return before their copies ran, RSAC_F_ASYNC)
     hipEvent_t ev_pts = nullptr, ev_small = nullptr;
+    // RSAC_SOLVE_OVERLAP: a side stream solves the second half of a fixed-budget range while
+    // the main stream scores the first (created on first use)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int64_t round_size = 4096;
     // device scratch
     DevBuf pts, tables, models, status, counts, subsets, substatus, best, bestmodels, mask;
@@ -1014,6 +1026,9 @@ void rsac_destroy(rsac_ctx *c) {
     if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->ev_pts) (void)hipEventDestroy(c->ev_pts);
     if (c->ev_small) (void)hipEventDestroy(c->ev_small);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1345,9 +1360,34 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
     // stream costs a gap of several microseconds between the kernels around it
     const bool timed = stats != nullptr && !async;
     if (timed) HIPCHK(hipEventRecord(c->ev0, s));
-    HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
-    if (timed) HIPCHK(hipEventRecord(c->ev1, s));
-    HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
+    // RSAC_SOLVE_OVERLAP=1: two halves; the second half's solve runs on a side stream beside the
+    // first half's scoring (the solve fills 1.5 waves per SIMD).  Counts and the best key are the
+    // same; only the order of the launches changes.  Timed: solve_ms is the first half's solve.
+    const int64_t H0 = solve_overlap() && H >= 16384 ? (H / 2) & ~int64_t(1023) : 0;
+    if (H0 > 0) {
+        if (!c->side) {
+            HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+        }
+        const int32_t H1 = (int32_t)(H - H0);
+        PnpArgs a1 = a;
+        a1.queue = nullptr;  // the first half's scoring launch owns the queue meanwhile
+        HIPCHK(launch_pnp_solve(a, 1, 0, (int32_t)H0, s));
+        if (timed) HIPCHK(hipEventRecord(c->ev1, s));
+        HIPCHK(hipEventRecord(c->ev_fork, s));
+        HIPCHK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+        HIPCHK(launch_pnp_solve(a1, 1, H0, H1, c->side));
+        HIPCHK(hipEventRecord(c->ev_join, c->side));
+        HIPCHK(launch_pnp_score(a, 1, 0, (int32_t)H0, c->counts.as<int32_t>(), s));
+        HIPCHK(reset_pnp_queue_async(a.queue, s));
+        HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
+        HIPCHK(launch_pnp_score(a, 1, H0, H1, c->counts.as<int32_t>(), s));
+    } else {
+        HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
+        if (timed) HIPCHK(hipEventRecord(c->ev1, s));
+        HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
+    }
     if (timed) HIPCHK(hipEventRecord(c->ev2, s));
     uint8_t *hmask_dev = nullptr;
     if (mask_out) {

@@ -166,6 +166,7 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
                               float *DY, hipStream_t s);
 // solve / score hypotheses [hyp_begin, hyp_begin + H) of every problem
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
+hipError_t reset_pnp_queue_async(int *queue, hipStream_t s);
 void set_score_variant(int v);  // tuning knob (rsac_set_score_variant)
 int score_record_form();        // f32 record form the selected variant reads (PnpArgs::fform)
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,

@@ -3548,6 +3548,12 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     return hipGetLastError();
 }
 
+// zero every counter of the PnP scoring launch (the solve kernel does it too; this is for a
+// scoring launch whose solve ran on another stream and could not)
+hipError_t reset_pnp_queue_async(int *queue, hipStream_t s) {
+    return hipMemsetAsync(queue, 0, kQWords * sizeof(int), s);
+}
+
 static int64_t env_i64(const char *name, int64_t dflt) {
     const char *e = getenv(name);
     return e ? atoll(e) : dflt;
