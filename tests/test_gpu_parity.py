@@ -719,3 +719,29 @@ def test_winner_of_empty_key_is_zero():
     p3 = torch.from_numpy(pr["points3d"]).cuda()
     wm, wmask = rsac.winner(p2, p3, pr["K"], torch.zeros(1, dtype=torch.int64, device="cuda"), 30.0)
     assert not wm.cpu().numpy().any() and not wmask.cpu().numpy().any()
+
+
+def test_solve_overlap_knob_matches_default():
+    # RSAC_SOLVE_OVERLAP=1 (read once per process, so a child process): the second half's solve
+    # on a side stream beside the first half's scoring must give the same key, model and mask
+    import subprocess
+    import sys
+    pr = synth.pnp_problem(10000, 0.5, seed=63)
+    H, base = 40000, 5000
+    key, model, mask = rsac.evaluate_range(pr["points2d"], pr["points3d"], pr["K"], base, H, 30.0, with_mask=True)
+    code = (
+        "import sys, numpy as np, rsac; from rsac import synth\n"
+        "pr = synth.pnp_problem(10000, 0.5, seed=63)\n"
+        f"k, m, s = rsac.evaluate_range(pr['points2d'], pr['points3d'], pr['K'], {base}, {H}, 30.0, with_mask=True)\n"
+        "np.savez(sys.argv[1], k=np.int64(k), m=np.asarray(m, np.float64), s=np.asarray(s))\n")
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"rsac_overlap_{os.getpid()}.npz")
+    env = dict(os.environ, RSAC_SOLVE_OVERLAP="1")
+    env["PYTHONPATH"] = os.pathsep.join(sys.path)
+    subprocess.run([sys.executable, "-c", code, out], env=env, check=True, timeout=90)
+    try:
+        got = np.load(out)
+        assert int(got["k"]) == key
+        assert _bits_equal(got["m"], model)
+        np.testing.assert_array_equal(got["s"], mask)
+    finally:
+        os.remove(out)
