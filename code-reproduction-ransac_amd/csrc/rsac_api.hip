@@ -28,13 +28,6 @@ using namespace rsac;
 static thread_local std::string g_err;
 
 static int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
-static bool solve_overlap() {
-    static const bool on = [] {
-        const char *v = getenv("RSAC_SOLVE_OVERLAP");
-        return v && atoi(v) > 0;
-    }();
-    return on;
-}
 
 static int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -137,10 +130,6 @@ struct rsac_ctx {
     // the last async copy out of h_pts / h_small: the host waits on it before rewriting the
     // buffer (calls may return before their copies ran, RSAC_F_ASYNC)
     hipEvent_t ev_pts = nullptr, ev_small = nullptr;
-    // RSAC_SOLVE_OVERLAP: a side stream solves the second half of a fixed-budget range while
-    // the main stream scores the first (created on first use)
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int64_t round_size = 4096;
     // device scratch
     DevBuf pts, tables, models, status, counts, subsets, substatus, best, bestmodels, mask;
@@ -149,7 +138,6 @@ struct rsac_ctx {
     float *d_thr2 = nullptr;
     DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
     DevBuf mxpts;                                              // MFMA point operands (PF, UV: 40 B / point)
-    DevBuf mflist;                                             // MFMA scorer's flagged-iteration records
     DevBuf loc;                                                // location search: inputs, pos2, H, err
     DevBuf lo;                                                 // LO-RANSAC: 2 model records, chain state, 2 masks
     const void *lo_state_base = nullptr;                       // the lo allocation whose LoState is zeroed
@@ -157,6 +145,7 @@ struct rsac_ctx {
     PinBuf h_lmfail;                                           // multi-block refit failure word (device-written)
     int dbg_refit_max_blocks = 0;                              // RSAC_DBG_REFIT_MAX_BLOCKS (0: device limit)
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
+    DevBuf reproj;                                             // reprojection errors / the K sweep's inputs
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
     DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
     DevBuf lmscr;                                              // multi-block LM refit: tagged wave sums
@@ -357,15 +346,10 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
     // resets best_key and the queue, then builds the frame (also in exact mode: cheap)
     // one problem: k_pnp_setup_fc's scratch (its ticket starts at 0; the kernel resets it)
-    const int fform = score_record_form();
-    if (!a.exact_only && fform == 2) {  // the MFMA scorer's point operands, written with the centring
+    if (!a.exact_only) {  // the MFMA scorer's point operands, written with the centring
         HIPCHK(c->mxpts.ensure(40 * std::max<int64_t>(N, 1)));
         a.PF = c->mxpts.as<uint4>();
         a.UV = reinterpret_cast<float2 *>(c->mxpts.as<char>() + 32 * std::max<int64_t>(N, 1));
-        constexpr int64_t kMfCap = 1 << 21;  // 64 MB of records; larger launches are split (launch_mf)
-        HIPCHK(c->mflist.ensure(sizeof(MfFlag) * kMfCap));
-        a.mf_list = c->mflist.as<MfFlag>();
-        a.mf_cap = kMfCap;
     }
     PnpPrepare prep = st.prep;
     if (P == 1) {
@@ -384,7 +368,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
         a.frame = c->frame.as<double>();
         a.fconst = c->fconst.as<float>();
         a.fmodels = c->fmodels.as<float>();
-        a.fform = fform;
+        a.fform = 2;  // MFMA records (form 1 for small rounds and out-of-f16-range problems)
     }
     return RSAC_OK;
 }
@@ -446,15 +430,33 @@ LmScratch *lm_scratch(rsac_ctx *c, hipStream_t s) {
 }
 
 // after the synchronisation that follows refits: a multi-block refit whose range sums never
-// all arrived (its blocks were not co-resident) kept the start pose and set the failure word
+// all arrived (its blocks were not all co-resident: other work held the CUs for longer than the
+// kernel's ~1 s wait) kept the start pose and set the failure word.  The caller then redoes the
+// call with one block per refit (with_one_refit_block), which needs no co-residency and gives
+// the same bits.
+constexpr int kRetryOneBlock = -1000;  // internal: not an RSAC_* code, never returned to callers
 int lm_check(rsac_ctx *c) {
     int32_t *f = c->h_lmfail.as<int32_t>();
     if (f && __atomic_load_n(f, __ATOMIC_ACQUIRE)) {
         *f = 0;
-        return fail(RSAC_EHIP, "pose refit: the cooperating blocks of a multi-block LM refit were not all resident "
-                               "(a range's sums never arrived); the RANSAC pose was kept");
+        if (c->lm.max_blocks > 1) return kRetryOneBlock;
+        return fail(RSAC_EHIP, "pose refit: a single-block LM refit lost its own range sums");
     }
     return RSAC_OK;
+}
+
+// run `call` (an API body); when one of its multi-block refits failed for lack of co-residency,
+// run it again with every refit on one block
+template <class F>
+int with_one_refit_block(rsac_ctx *c, F call) {
+    int r = call();
+    if (r != kRetryOneBlock) return r;
+    const int saved = c->lm.max_blocks;
+    c->lm.max_blocks = 1;
+    c->lo_state_base = nullptr;  // an LO chain's device state starts from zero again
+    r = call();
+    c->lm.max_blocks = saved;
+    return r == kRetryOneBlock ? fail(RSAC_EHIP, "pose refit failed with one block") : r;
 }
 
 // The kLoSteps steps are enqueued at once and decided on the device (k_pnp_lo_count): step k
@@ -1014,7 +1016,7 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->lmscr, &c->setup_scr, &c->scanrec, &c->mxpts, &c->mflist};
+                     &c->epnp, &c->lmscr, &c->setup_scr, &c->scanrec, &c->mxpts, &c->reproj};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_lmfail, &c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,
@@ -1026,18 +1028,8 @@ void rsac_destroy(rsac_ctx *c) {
     if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->ev_pts) (void)hipEventDestroy(c->ev_pts);
     if (c->ev_small) (void)hipEventDestroy(c->ev_small);
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
-}
-
-int rsac_set_score_variant(int variant) {
-    if (variant < -1 || (variant > 28 && (variant < 40 || variant > 53) && (variant < 60 || variant > 99)))
-        return fail(RSAC_EINVAL, "unknown scoring variant %d", variant);
-    set_score_variant(variant);
-    return RSAC_OK;
 }
 
 int rsac_debug_set(rsac_ctx *c, int32_t key, int64_t value) {
@@ -1080,8 +1072,10 @@ int rsac_pnp_ransac(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n
                     uint8_t *mask_out, rsac_stats *stats, void *stream) {
     if (n < 4) return fail(RSAC_ETOOFEW, "solvePnPRansac needs >= 4 correspondences (got %d)", n);
     int32_t status = 0, ninl = 0;
-    return pnp_core(c, pts3d, pts2d, nullptr, 1, n, K, n_iters, thr, conf, seed, flags, R_out, t_out, &status, &ninl,
-                    mask_out, stats, pick_stream(c, stream));
+    return with_one_refit_block(c, [&] {
+        return pnp_core(c, pts3d, pts2d, nullptr, 1, n, K, n_iters, thr, conf, seed, flags, R_out, t_out, &status,
+                        &ninl, mask_out, stats, pick_stream(c, stream));
+    });
 }
 
 int rsac_pnp_ransac_batched(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *offsets, int32_t P,
@@ -1089,8 +1083,10 @@ int rsac_pnp_ransac_batched(rsac_ctx *c, const void *pts3d, const void *pts2d, c
                             double *R_out, double *t_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out,
                             void *stream) {
     if (!offsets) return fail(RSAC_EINVAL, "offsets required");
-    return pnp_core(c, pts3d, pts2d, offsets, P, 0, K, n_iters, thr, conf, seed, flags, R_out, t_out, status_out,
-                    ninl_out, mask_out, nullptr, pick_stream(c, stream));
+    return with_one_refit_block(c, [&] {
+        return pnp_core(c, pts3d, pts2d, offsets, P, 0, K, n_iters, thr, conf, seed, flags, R_out, t_out, status_out,
+                        ninl_out, mask_out, nullptr, pick_stream(c, stream));
+    });
 }
 
 int rsac_homography_ransac(rsac_ctx *c, const void *src, const void *dst, int32_t n, int32_t max_iters, double thr,
@@ -1283,17 +1279,197 @@ int rsac_pnp_local_opt(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_
     HIPCHK(hipMemcpyAsync(&c0, cnt, sizeof c0, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     ScanState sc;
-    sc.reset(1 << 30);
-    sc.best = 0;
-    sc.max_good = c0;
     int32_t steps = 0;
-    r = local_opt(c, a, n, sc, 0.99, s, steps);
+    r = with_one_refit_block(c, [&] {
+        // from the input model each time (a failed chain may have replaced the record)
+        HIPCHK(hipMemcpyAsync(c->models.p, rec, sizeof rec, hipMemcpyHostToDevice, s));
+        sc.reset(1 << 30);
+        sc.best = 0;
+        sc.max_good = c0;
+        steps = 0;
+        return local_opt(c, a, n, sc, 0.99, s, steps);
+    });
     if (r) return r;
     HIPCHK(hipMemcpyAsync(rec, c->models.p, sizeof rec, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     memcpy(model_out, rec, 12 * sizeof(double));
     if (count_out) *count_out = sc.max_good;
     if (steps_out) *steps_out = steps;
+    return RSAC_OK;
+}
+
+// LM on (R, t) from the given start over the masked points (NULL = all), on the device: one
+// problem's k_pnp_refine, the bits of rsac_pnp_refine (host) and orc_pnp_refine.  Host f64 AoS.
+static int refine_on_device(rsac_ctx *c, const double *pts3d, const double *pts2d, int32_t n, const double K[9],
+                            const uint8_t *mask, double R[9], double t[3], hipStream_t s) {
+    Staged st;
+    int r = stage_points(c, pts3d, pts2d, 3, nullptr, 1, n, 0, s, st);
+    if (r) return r;
+    r = stage_tables(c, st, K, 1.0, s);
+    if (r) return r;
+    r = ensure_hyp_buffers(c, 1, 1, false);
+    if (r) return r;
+    PnpArgs a;
+    r = pnp_args(c, st, RSAC_F_EXACT_ONLY, 0, 1, 0, s, a);
+    if (r) return r;
+    HIPCHK(c->h_bestmodels.ensure(sizeof(double) * kModelStride));
+    HIPCHK(c->h_mask.ensure(std::max(n, 1)));
+    double *hrec = c->h_bestmodels.as<double>();
+    memset(hrec, 0, sizeof(double) * kModelStride);
+    memcpy(hrec, R, 9 * sizeof(double));
+    memcpy(hrec + 9, t, 3 * sizeof(double));
+    hrec[kValidSlot] = 1.0;
+    uint8_t *hm = c->h_mask.as<uint8_t>();
+    if (mask)
+        memcpy(hm, mask, n);
+    else
+        memset(hm, 1, n);
+    HIPCHK(c->mask.ensure(std::max(n, 1)));
+    HIPCHK(hipMemcpyAsync(c->bestmodels.p, hrec, sizeof(double) * kModelStride, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->mask.p, hm, n, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_pnp_refine(a, 1, c->mask.as<uint8_t>(), c->bestmodels.as<double>(), nullptr, s, lm_scratch(c, s),
+                             st.off.data(), hrec));  // R, t also written to the pinned record
+    HIPCHK(hipStreamSynchronize(s));
+    if (int e = lm_check(c)) return e;
+    memcpy(R, hrec, 9 * sizeof(double));
+    memcpy(t, hrec + 9, 3 * sizeof(double));
+    return RSAC_OK;
+}
+
+int rsac_pnp_refine_lm(rsac_ctx *c, const double *pts3d, const double *pts2d, int32_t n, const double K[9],
+                       const uint8_t *mask, double R[9], double t[3], void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (n < 3 || !pts3d || !pts2d || !K || !R || !t) return fail(RSAC_EINVAL, "bad arguments");
+    const double R0[9] = {R[0], R[1], R[2], R[3], R[4], R[5], R[6], R[7], R[8]}, t0[3] = {t[0], t[1], t[2]};
+    return with_one_refit_block(c, [&] {
+        memcpy(R, R0, sizeof R0);
+        memcpy(t, t0, sizeof t0);
+        return refine_on_device(c, pts3d, pts2d, n, K, mask, R, t, pick_stream(c, stream));
+    });
+}
+
+int rsac_pnp_reprojection_errors(rsac_ctx *c, const double *pts3d, const double *pts2d, int32_t n, const double K[9],
+                                 const double R[9], const double t[3], uint32_t flags, double *proj_out,
+                                 double *err_out, void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (n < 0 || !pts3d || !pts2d || !K || !R || !t) return fail(RSAC_EINVAL, "bad arguments");
+    if (n == 0) return RSAC_OK;
+    hipStream_t s = pick_stream(c, stream);
+    PoseCam pc;
+    memcpy(pc.R, R, sizeof pc.R);
+    memcpy(pc.t, t, sizeof pc.t);
+    pc.cam[0] = K[0]; pc.cam[1] = K[4]; pc.cam[2] = K[2]; pc.cam[3] = K[5];
+    if (flags & RSAC_F_DEVICE_IN)  // device inputs and outputs: enqueue only
+        return launch_pnp_reproj(pts3d, pts2d, n, pc, proj_out, err_out, s) == hipSuccess
+                   ? RSAC_OK
+                   : fail(RSAC_EHIP, "reprojection launch failed");
+    const size_t N = (size_t)n;
+    HIPCHK(c->reproj.ensure(sizeof(double) * 8 * N));
+    double *d3 = c->reproj.as<double>(), *d2 = d3 + 3 * N, *dp = d2 + 2 * N, *de = dp + 2 * N;
+    HIPCHK(hipMemcpyAsync(d3, pts3d, sizeof(double) * 3 * N, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d2, pts2d, sizeof(double) * 2 * N, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_pnp_reproj(d3, d2, n, pc, proj_out ? dp : nullptr, err_out ? de : nullptr, s));
+    if (proj_out) HIPCHK(hipMemcpyAsync(proj_out, dp, sizeof(double) * 2 * N, hipMemcpyDeviceToHost, s));
+    if (err_out) HIPCHK(hipMemcpyAsync(err_out, de, sizeof(double) * N, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return RSAC_OK;
+}
+
+int rsac_pnp_orientation_sweep(rsac_ctx *c, const double *pts3d, const double *pts2d, int32_t n, const double *Ks,
+                               int32_t n_k, int32_t n_iters, double thr, double conf, uint64_t seed, uint32_t flags,
+                               int32_t min_inliers, int32_t *best_out, double *mean_err_out, double *models_out,
+                               int32_t *status_out, int32_t *n_inliers_out, uint8_t *masks_out, double R_out[9],
+                               double t_out[3], void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (n < 4) return fail(RSAC_ETOOFEW, "solvePnPRansac needs >= 4 correspondences (got %d)", n);
+    if (n_k < 1 || !pts3d || !pts2d || !Ks || !best_out) return fail(RSAC_EINVAL, "bad arguments");
+    if (flags & (RSAC_F_DEVICE_IN | RSAC_F_DEVICE_SOA | RSAC_F_DEVICE_OUT | RSAC_F_LO | RSAC_F_ASYNC))
+        return fail(RSAC_EINVAL, "the K sweep takes host arrays (no device, LO or async flags)");
+    hipStream_t s = pick_stream(c, stream);
+    const size_t N = (size_t)n, P = (size_t)n_k;
+    // 1. the loop over the intrinsics (testpro-K.py:58-75) as one batched call: problem k is the
+    //    point set with K_k
+    std::vector<double> p3(3 * N * P), p2(2 * N * P);
+    std::vector<int64_t> off(P + 1);
+    for (size_t k = 0; k < P; ++k) {
+        memcpy(&p3[3 * N * k], pts3d, sizeof(double) * 3 * N);
+        memcpy(&p2[2 * N * k], pts2d, sizeof(double) * 2 * N);
+        off[k] = (int64_t)(N * k);
+    }
+    off[P] = (int64_t)(N * P);
+    std::vector<double> R(9 * P), t(3 * P);
+    std::vector<int32_t> status(P), ninl(P);
+    std::vector<uint8_t> masks(N * P);
+    r = rsac_pnp_ransac_batched(c, p3.data(), p2.data(), off.data(), n_k, Ks, n_iters, thr, conf, seed, flags, R.data(),
+                                t.data(), status.data(), ninl.data(), masks.data(), stream);
+    if (r < 0) return r;
+    // 2. the gate (testpro-K.py:77) and each pose as projectPoints sees it: the shim returns
+    //    rvec = Rodrigues(R), and projectPoints rotates by Rodrigues(rvec)
+    std::vector<double> poses(12 * P, 0.0), cams(4 * P);
+    std::vector<uint8_t> pass(P);
+    for (size_t k = 0; k < P; ++k) {
+        pass[k] = status[k] == RSAC_OK && ninl[k] >= min_inliers;
+        double rv[3];
+        rodrigues_m2v(&R[9 * k], rv);
+        rodrigues_v2m(rv, &poses[12 * k]);
+        memcpy(&poses[12 * k + 9], &t[3 * k], 3 * sizeof(double));
+        const double *Kk = Ks + 9 * k;
+        cams[4 * k] = Kk[0]; cams[4 * k + 1] = Kk[4]; cams[4 * k + 2] = Kk[2]; cams[4 * k + 3] = Kk[5];
+    }
+    // 3. the mean inlier reprojection error of every K on the device (testpro-K.py:80-82)
+    HIPCHK(c->reproj.ensure(sizeof(double) * (5 * N + 16 * P + 2 * P) + N * P));
+    double *d3 = c->reproj.as<double>(), *d2 = d3 + 3 * N, *dposes = d2 + 2 * N, *dcams = dposes + 12 * P,
+           *dout = dcams + 4 * P;
+    uint8_t *dmasks = (uint8_t *)(dout + 2 * P);
+    HIPCHK(hipMemcpyAsync(d3, pts3d, sizeof(double) * 3 * N, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d2, pts2d, sizeof(double) * 2 * N, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dposes, poses.data(), sizeof(double) * 12 * P, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dcams, cams.data(), sizeof(double) * 4 * P, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dmasks, masks.data(), N * P, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_pnp_reproj_mean(d3, d2, n, n_k, dposes, dcams, dmasks, dout, s));
+    std::vector<double> sums(2 * P);
+    HIPCHK(hipMemcpyAsync(sums.data(), dout, sizeof(double) * 2 * P, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    // 4. the first K with the strictly smallest mean (testpro-K.py:90-97)
+    int best = -1;
+    double best_err = __builtin_inf();
+    for (size_t k = 0; k < P; ++k) {
+        const double mean = sums[2 * k] / sums[2 * k + 1];
+        if (mean_err_out) mean_err_out[k] = pass[k] ? mean : __builtin_nan("");
+        if (pass[k] && mean < best_err) {
+            best_err = mean;
+            best = (int)k;
+        }
+    }
+    *best_out = best;
+    for (size_t k = 0; k < P; ++k) {
+        if (models_out) {
+            memcpy(models_out + 12 * k, &R[9 * k], 9 * sizeof(double));
+            memcpy(models_out + 12 * k + 9, &t[3 * k], 3 * sizeof(double));
+        }
+        if (status_out) status_out[k] = pass[k] ? RSAC_OK : RSAC_NO_MODEL;
+        if (n_inliers_out) n_inliers_out[k] = ninl[k];
+    }
+    if (masks_out) memcpy(masks_out, masks.data(), N * P);
+    if (best < 0) return RSAC_NO_MODEL;
+    // 5. solvePnPRefineLM on the winner's inliers from its pose (testpro-K.py:122-125): the
+    //    reference passes the inlier subset, in index order, and the rvec of step 2
+    std::vector<double> s3, s2;
+    for (size_t i = 0; i < N; ++i)
+        if (masks[N * best + i]) {
+            s3.insert(s3.end(), pts3d + 3 * i, pts3d + 3 * i + 3);
+            s2.insert(s2.end(), pts2d + 2 * i, pts2d + 2 * i + 2);
+        }
+    double Rr[9], tr[3];
+    memcpy(Rr, &poses[12 * best], sizeof Rr);
+    memcpy(tr, &poses[12 * best + 9], sizeof tr);
+    r = rsac_pnp_refine_lm(c, s3.data(), s2.data(), (int32_t)(s3.size() / 3), Ks + 9 * best, nullptr, Rr, tr, stream);
+    if (r < 0) return r;
+    if (R_out) memcpy(R_out, Rr, sizeof Rr);
+    if (t_out) memcpy(t_out, tr, sizeof tr);
     return RSAC_OK;
 }
 
@@ -1360,35 +1536,17 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
     // stream costs a gap of several microseconds between the kernels around it
     const bool timed = stats != nullptr && !async;
     if (timed) HIPCHK(hipEventRecord(c->ev0, s));
-    // RSAC_SOLVE_OVERLAP=1: two halves; the second half's solve runs on a side stream beside the
-    // first half's scoring (the solve fills 1.5 waves per SIMD).  Counts and the best key are the
-    // same; only the order of the launches changes.  Timed: solve_ms is the first half's solve.
-    const int64_t H0 = solve_overlap() && H >= 16384 ? (H / 2) & ~int64_t(1023) : 0;
-    if (H0 > 0) {
-        if (!c->side) {
-            HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-        }
-        const int32_t H1 = (int32_t)(H - H0);
-        PnpArgs a1 = a;
-        a1.queue = nullptr;  // the first half's scoring launch owns the queue meanwhile
-        HIPCHK(launch_pnp_solve(a, 1, 0, (int32_t)H0, s));
-        if (timed) HIPCHK(hipEventRecord(c->ev1, s));
-        HIPCHK(hipEventRecord(c->ev_fork, s));
-        HIPCHK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-        HIPCHK(launch_pnp_solve(a1, 1, H0, H1, c->side));
-        HIPCHK(hipEventRecord(c->ev_join, c->side));
-        HIPCHK(launch_pnp_score(a, 1, 0, (int32_t)H0, c->counts.as<int32_t>(), s));
-        HIPCHK(reset_pnp_queue_async(a.queue, s));
-        HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
-        HIPCHK(launch_pnp_score(a, 1, H0, H1, c->counts.as<int32_t>(), s));
+    HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
+    if (timed) HIPCHK(hipEventRecord(c->ev1, s));
+    if (timed) {  // score_ms = the scoring kernel alone (ev1 -> ev2), then the key's reduction
+        PnpArgs ak = a;
+        ak.best_key = nullptr;
+        HIPCHK(launch_pnp_score(ak, 1, 0, H, c->counts.as<int32_t>(), s));
+        HIPCHK(hipEventRecord(c->ev2, s));
+        HIPCHK(launch_pnp_best_key(a, 0, H, c->counts.as<int32_t>(), s));
     } else {
-        HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
-        if (timed) HIPCHK(hipEventRecord(c->ev1, s));
         HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
     }
-    if (timed) HIPCHK(hipEventRecord(c->ev2, s));
     uint8_t *hmask_dev = nullptr;
     if (mask_out) {
         if (flags & RSAC_F_DEVICE_OUT) {

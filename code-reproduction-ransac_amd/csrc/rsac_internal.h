@@ -10,18 +10,6 @@ namespace rsac {
 struct EpnpStage1;
 struct EpnpStage2;
 
-// one flagged check window of k_pnp_score_mf (a wave's iterations of 2 x 32 points from `base` x
-// the 32 hypotheses of a work unit, with an undecided pair in the slots of fl), recounted exactly
-// afterwards (k_pnp_mf_recount)
-struct MfFlag {
-    int64_t rec0, p0;  // the unit's first hypothesis record and its problem's first point
-    int32_t base;      // the window's first iteration (its points base + [0, 64))
-    int32_t n;         // the unit's point range ends at n
-    uint32_t fl;       // bit 4t + g: slot g of MFMA group t (hypotheses 8t + 2g, 8t + 2g + 1)
-    int16_t nh;        // hypotheses of the unit
-    int16_t iters;     // iterations in the window (the next ones at base + 256 k)
-};
-
 // PnP problem set on the device.  Problem p owns points [offsets[p],
 // offsets[p+1]) of the SoA arrays; its hypothesis records live at
 // [p * hyp_stride, p * hyp_stride + H).
@@ -58,7 +46,7 @@ struct PnpArgs {
     unsigned long long *best_key;
     int *queue;  // counters of the f32 scoring kernels, words 0..3 (reset by the frame and solve kernels)
     int32_t max_n;  // largest problem (points); small problems score one lane per hypothesis
-    int fform = 0;  // f32 record form: 0 write_fmodel, 1 the scaled form of k_pnp_score_sc, 2 the MFMA
+    int fform = 2;  // f32 record form: 1 the scaled form of k_pnp_score_sc (small rounds), 2 the MFMA
                     // form of k_pnp_score_mf (form 1 for problems outside its operand range)
     // MFMA scoring operands per point (fform 2; written with the centred coordinates): PF = two
     // uint4 per point, f16 {hi XC, hi YC, hi ZC, 1, lo XC, lo YC, lo ZC, 0} and the same x 2^-11
@@ -66,8 +54,6 @@ struct PnpArgs {
     // UV = (u - cx, v - cy) / sqrt(T)
     uint4 *PF = nullptr;
     float2 *UV = nullptr;
-    MfFlag *mf_list = nullptr;  // flagged-iteration records (capacity mf_cap) of k_pnp_score_mf
-    int64_t mf_cap = 0;
 };
 
 constexpr int kFrameStride = 8;
@@ -166,11 +152,11 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
                               float *DY, hipStream_t s);
 // solve / score hypotheses [hyp_begin, hyp_begin + H) of every problem
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
-hipError_t reset_pnp_queue_async(int *queue, hipStream_t s);
-void set_score_variant(int v);  // tuning knob (rsac_set_score_variant)
-int score_record_form();        // f32 record form the selected variant reads (PnpArgs::fform)
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
+// the packed best key of counts [hyp_begin, hyp_begin + H) of one problem into *a.best_key (no-op
+// without it); launch_pnp_score does this itself when a.best_key is set
+hipError_t launch_pnp_best_key(const PnpArgs &a, int64_t hyp_begin, int32_t H, const int32_t *counts, hipStream_t s);
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
                            hipStream_t s, int64_t best0 = -1, double *model_out = nullptr,
                            double *host_model_out = nullptr);
@@ -226,6 +212,16 @@ hipError_t launch_pnp_model_count(const PnpArgs &a, int32_t n, const double *mod
 // re-solve the hypothesis named by a device packed key (+ its mask); cam = fx fy cx cy thr2
 hipError_t launch_pnp_winner(const double *p3, const double *p2, int32_t n, const double *cam, uint64_t seed,
                              const int64_t *key, double *rec, double *model_out, uint8_t *mask, hipStream_t s);
+
+// compute_reprojection_error (testpro-K.py:32-36): one pose's projections / errors over f64
+// AoS device points, and the mean inlier error of P poses over one shared point set
+struct PoseCam {
+    double R[9], t[3], cam[4];
+};
+hipError_t launch_pnp_reproj(const double *p3, const double *p2, int32_t n, const PoseCam &pc, double *proj,
+                             double *err, hipStream_t s);
+hipError_t launch_pnp_reproj_mean(const double *p3, const double *p2, int32_t n, int32_t P, const double *poses,
+                                  const double *cams, const uint8_t *masks, double *out, hipStream_t s);
 
 // UTM <-> WGS84 (lon, lat degrees / easting, northing), and the DEM ray march (rsac_geo.h)
 hipError_t launch_utm(bool inverse, const double *in, int64_t n, int zone, bool south, double *out, hipStream_t s);

@@ -78,7 +78,6 @@ constexpr double kU32 = 5.9604644775390625e-08;  // 2^-24, unit roundoff of floa
 constexpr int kQSub = 8;
 constexpr int kQWords = 32 + 64 * kQSub;  // ints of the queue buffer used by the PnP kernels
 __device__ __forceinline__ int *unit_queue(int *q, int k) { return q + 32 + 32 * k; }
-__device__ __forceinline__ int *rec_queue(int *q, int k) { return q + 32 + 32 * kQSub + 32 * k; }
 // k_fm_score_q's counters (HomArgs::fm_queue = queue + 8): words kQWords + 32 k of the buffer
 constexpr int kFmQOff = kQWords - 8;
 __device__ __forceinline__ int *fm_unit_queue(int *fq, int k) { return fq + kFmQOff + 32 * k; }
@@ -91,7 +90,6 @@ __device__ __forceinline__ void reset_pnp_queue(int *q) {
 #pragma unroll
     for (int k = 0; k < kQSub; ++k) {
         *unit_queue(q, k) = 0;
-        *rec_queue(q, k) = 0;
     }
 }
 
@@ -480,43 +478,10 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
     }
 }
 
-// Band of the division-free test from the evaluation error bounds eps (ex, ey, ez: DESIGN.md
-// "Scoring"); tz = the hypothesis' depth of the centre (any w > 0 is valid for the majorant).
-struct BandConsts {
-    double D0, beta, zg, alpha;
-};
-
-__device__ __forceinline__ BandConsts band_consts(const double (&eps)[3], double fx, double fy, double wmax, double tz,
-                                                  const float *fconst) {
-    BandConsts b;
-    // Dz0 = 1.01 (fx ex + fy ey + ez Wmax), Wmax = (fx + fy) wmax >= fx wa_i + fy wb_i of any point
-    b.D0 = 1.01 * (fx * eps[0] + fy * eps[1] + eps[2] * (fx + fy) * wmax);
-    // |z'| above zg keeps |x'/z' - x/z| <= 0.01 for every projection the bound is used on
-    b.zg = 100.0 * (fmax(eps[0], eps[1]) + wmax * eps[2]) + 2.02 * eps[2] + 1e-30;
-    // Mz = (sqT2 |z| + Dz) Dz + Trel z^2 with Dz = D0 + Cmax |z| is at most alpha z^2 + beta:
-    // |z| <= z^2 / (2w) + w / 2 for any w > 0 (taken as the hypothesis' depth of the centre).
-    const double sqT2 = fconst[5], Trel = fconst[6], Cmax = fconst[7];
-    const double Bc = sqT2 * b.D0 + 2.0 * b.D0 * Cmax;
-    const double w = fmax(fabs(tz), 1.0);
-    b.beta = 1.01 * (b.D0 * b.D0 + Bc * w * 0.5);
-    b.alpha = 1.01 * (sqT2 * Cmax + Cmax * Cmax + Trel + Bc / (2.0 * w));
-    // beta >= K and beta >= (T - alpha) zg^2 make the depth guard redundant (k_pnp_score_mx
-    // has none): E < lo then implies |z'| > zg, and for |z'| <= zg, E > hi >= K means
-    // |q| >= sqrt(E') - delta > sqrt(T) (zg + ez) >= sqrt(T) |z| (delta = D0 + Cmax (zg + ez)
-    // bounds |q' - q|, L1): the pair's reprojection distance exceeds thr, an outlier
-    const double T = fconst[4], ez = eps[2];
-    const double zr = b.zg + ez;
-    const double K = (1.0 + 1e-6) * (b.D0 + Cmax * zr + sqrt(T * 1.00001) * zr) * (b.D0 + Cmax * zr + sqrt(T * 1.00001) * zr);
-    b.beta = fmax(b.beta, K);
-    if (T > b.alpha) b.beta = fmax(b.beta, (T - b.alpha) * b.zg * b.zg * (1.0 + 1e-6));
-    return b;
-}
-
-// float32 record of one pose, division-free form of the test:
-//   { -fx R0 -fx R1 -fx R2 | -fy R3 -fy R4 -fy R5 | R6 R7 R8 | -fx t'x -fy t'y t'z | Dz0 beta zg alpha }
-// with t' = R c + t.  ex, ey bound |xs' - fx x|/fx, |ys' - fy y|/fy and ez |z' - z| (camera
-// frame, f32 evaluation vs real numbers); Dz0 is the hypothesis' part of D |z|; zg is the
-// depth guard (< 0: no model).
+// f32 record of one pose for the pre-filter, in the form the scoring launch reads (PnpArgs::fform):
+// 2 = the MFMA record of k_pnp_score_mf (write_fmodel_mx) when the problem's centred coordinates
+// fit the f16 operands (fconst[11] != 0), else 1 = the scaled record of k_pnp_score_sc
+// (write_fmodel_sc; also every small round, round_args)
 __device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t, bool valid, const double *frame,
                                                 const double *cam, const float *fconst, float *fm);
 
@@ -524,39 +489,11 @@ __device__ __forceinline__ void write_fmodel_mx(const double *R, const double *t
                                                 const double *cam, const float *fconst, float *fm);
 
 __device__ __forceinline__ void write_fmodel(const double *R, const double *t, bool valid, const double *frame,
-                                             const double *cam, const float *fconst, float *fm, int form = 0) {
-    if (form == 2 && fconst[11] != 0.f) {
+                                             const double *cam, const float *fconst, float *fm, int form) {
+    if (form == 2 && fconst[11] != 0.f)
         write_fmodel_mx(R, t, valid, frame, cam, fconst, fm);
-        return;
-    }
-    if (form >= 1) {
+    else
         write_fmodel_sc(R, t, valid, frame, cam, fconst, fm);
-        return;
-    }
-    if (!valid) {
-#pragma unroll
-        for (int q = 0; q < kFModelStride; ++q) fm[q] = 0.f;
-        fm[14] = -1.f;
-        return;
-    }
-    const double B = frame[3], rho = frame[4], cmax = frame[5], wmax = frame[6];
-    const double fx = fabs(cam[0]), fy = fabs(cam[1]);
-    const double sc[3] = {-cam[0], -cam[1], 1.0};
-    double eps[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const double tp = R[3 * r] * frame[0] + R[3 * r + 1] * frame[1] + R[3 * r + 2] * frame[2] + t[r];
-        const double r1 = fabs(R[3 * r]) + fabs(R[3 * r + 1]) + fabs(R[3 * r + 2]);
-        eps[r] = 8.0 * kU32 * (r1 * B + fabs(tp)) + r1 * rho + 4e-15 * (r1 * cmax + fabs(t[r]));
-#pragma unroll
-        for (int q = 0; q < 3; ++q) fm[3 * r + q] = (float)(sc[r] * R[3 * r + q]);
-        fm[9 + r] = (float)(sc[r] * tp);
-    }
-    const BandConsts b = band_consts(eps, fx, fy, wmax, (double)fm[11], fconst);
-    fm[12] = (float)(b.D0 * (1.0 + 1e-6));
-    fm[13] = (float)b.beta;
-    fm[14] = (float)b.zg;
-    fm[15] = (float)b.alpha;
 }
 
 // Scaled record (k_pnp_score_sc, DESIGN.md "Scoring: scaled form").  The z row is multiplied
@@ -619,7 +556,7 @@ __device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t
     fm[12] = fits ? (float)a : 0.f;
     fm[13] = fits ? (float)b : __builtin_inff();
     fm[14] = (float)zg;
-    fm[15] = fits ? (float)((b + a * Zp) * (1.0 + 1e-6)) : __builtin_inff();  // constant band (CB kernels)
+    fm[15] = fits ? (float)((b + a * Zp) * (1.0 + 1e-6)) : __builtin_inff();  // constant band b + a Zmax
 }
 
 // The band constants of the scaled form (write_fmodel_sc) from the camera-frame evaluation error
@@ -805,105 +742,6 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 // the operations of p3p_lambdatwist for that candidate) and its 4th-point error; the four
 // lanes pick the smallest error, the lowest candidate on ties (= pnp_minimal's first-one rule),
 // and the winner writes the record.  Results equal k_pnp_solve's bit for bit.
-// Two lanes per hypothesis (rounds above solve4_max_hyps, up to solve2_max_hyps): lane s runs
-// the Lambda Twist sign branch s and both of its tau candidates (candidates 2s and 2s + 1, in
-// that order), so the common part is done twice instead of four times and a SIMD holds twice
-// the waves of the one-lane kernel.  The pick is the serial solver's: the smallest 4th-point
-// error, the lowest candidate on a tie.
-__global__ __launch_bounds__(256) void k_pnp_solve2(PnpArgs a, int64_t hyp_begin, int32_t H) {
-    const int prob = blockIdx.y;
-    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-    const int hl = gt >> 1, sgn = gt & 1;
-    if (gt == 0 && prob == 0) {
-        if (a.queue) reset_pnp_queue(a.queue);
-    }
-    const bool live = hl < H;  // the 2 lanes of a hypothesis share it: shuffles stay in the pair
-    const int64_t h = hyp_begin + hl;
-    const int64_t p0 = a.offsets[prob];
-    const int n = (int)(a.offsets[prob + 1] - p0);
-    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
-    int32_t idx[4] = {0, 0, 0, 0};
-    int8_t st = -1;
-    if (live) {
-        if (a.subsets) {
-            st = a.sub_status[rec];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) idx[j] = a.subsets[rec * 4 + j];
-        } else {
-            Philox rng;
-            rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
-            st = (n >= 4 && rng.subset<4>(n, idx) == 0) ? 1 : -1;
-        }
-    }
-    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
-    double e = 0.0;
-    int mine = 4;  // this lane's kept candidate (4: none)
-    const Cam k{a.cams[4 * prob], a.cams[4 * prob + 1], a.cams[4 * prob + 2], a.cams[4 * prob + 3]};
-    if (st > 0) {
-        float X[4], Y[4], Z[4], U[4], V[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int64_t i = p0 + idx[j];
-            X[j] = a.X[i]; Y[j] = a.Y[i]; Z[j] = a.Z[i]; U[j] = a.U[i]; V[j] = a.V[i];
-        }
-        double yb[9], xw[9];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            bearing(k, U[j], V[j], yb + 3 * j);
-            xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
-        }
-        LtCommon L;
-        double w0, w1, tau[2];
-        if (lt_common(yb, xw, L) && lt_sign(L, sgn, w0, w1, tau)) {
-#pragma unroll 1
-            for (int ti = 0; ti < 2; ++ti) {
-                const int cand = 2 * sgn + ti;
-                auto emit = [&](const double *Rk, const double *tk) {
-                    const double ek = pnp_fourth_error(Rk, tk, X, Y, Z, U, V, k);
-                    if (!(ek == ek)) return;
-                    if (mine < 4 && !(ek < e)) return;  // the first smallest error wins
-                    mine = cand;
-                    e = ek;
-#pragma unroll
-                    for (int q = 0; q < 9; ++q) R[q] = Rk[q];
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) t[q] = tk[q];
-                };
-                (void)lt_tau(L, w0, w1, tau[ti], yb, xw, emit);
-            }
-        }
-    }
-    // the pair's winner: smallest e, then the lowest candidate
-    int win = mine;
-    double we = mine < 4 ? e : 0.0;
-    {
-        const int ow = __shfl_xor(win, 1);
-        const double oe = __shfl_xor(we, 1);
-        if (ow < 4 && (win == 4 || oe < we || (oe == we && ow < win))) {
-            win = ow;
-            we = oe;
-        }
-    }
-    if (!live) return;
-    const bool ok = win < 4;
-    if (ok ? mine != win : sgn != 0) return;  // one writer per hypothesis
-    const int8_t sv = st > 0 ? (ok ? 1 : 0) : st;
-    double *m = a.models + rec * kModelStride;
-    if (!ok)
-        for (int q = 0; q < 9; ++q) R[q] = 0.0;
-    if (!ok)
-        for (int q = 0; q < 3; ++q) t[q] = 0.0;
-#pragma unroll
-    for (int q = 0; q < 9; ++q) m[q] = R[q];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
-    m[kValidSlot] = sv > 0 ? 1.0 : 0.0;
-    a.status[rec] = sv;
-    if (a.counts_out) a.counts_out[rec] = 0;
-    if (a.fmodels)
-        write_fmodel(R, t, sv > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
-}
 
 __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
@@ -997,27 +835,12 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
 }
 
 // ---------------------------------------------------------------------------
-// PnP scoring, float32 pre-filter + exact fallback (division-free).
-//
-// Work: units of HB consecutive hypotheses of one problem x all its points,
-// pulled from a queue (one atomicAdd per unit) by a grid sized to the
-// resident capacity, so the tail is at most one unit.  The 4 waves of a
-// block split the unit's points in tiles of 64*P; each lane keeps P centred
-// points in registers and runs every hypothesis of the unit over them (the
-// hypothesis' f32 record is wave-uniform: scalar loads, SGPRs).
-//
-// Per pair (point i, hypothesis h), pixel relative to the principal point:
-//   q1 = uc z - fx x,  q2 = vc z - fy y          (= z (u - pu), z (v - pv))
-//   diff = q1^2 + q2^2 - T z^2                   (sign(diff) = sign(e - T))
-//   Dz = Dz0_h + Cmax |z|                        (D |z|; D bounds the pixel error
-//                                                 of the f32 evaluation)
-//   Mz = (2 sqrt(T) |z| + Dz) Dz + 4e-6 T z^2    (M z^2; M bounds |e' - e|)
-// |diff| > Mz and |z| > zg_h decide the pair; otherwise the tile is recounted
-// for this hypothesis with the exact f64 error (pnp_err, the oracle's
-// formula).  Counts are bit-identical to the exact kernel
-// (tests/test_gpu_parity.py: threshold-straddling and behind-camera cases).
-// Derivation: DESIGN.md "Scoring".
+// PnP scoring.  The product path is the MFMA kernel k_pnp_score_mf (its small-round and
+// out-of-f16-range forms run the scaled-form body sc_unit); RSAC_F_EXACT_ONLY selects the
+// all-f64 kernel k_pnp_score, whose counts the pre-filter kernels must reproduce bit for bit.
 // ---------------------------------------------------------------------------
+// counts of the block's hypotheses (sum of the 4 waves' partials) and, when
+// a.best_key is set, one atomicMax of the block's best packed key
 // counts of the block's hypotheses (sum of the 4 waves' partials) and, when
 // a.best_key is set, one atomicMax of the block's best packed key
 template <int HB>
@@ -1042,335 +865,6 @@ __device__ __forceinline__ void pnp_score_epilogue(const PnpArgs &a, const int (
     }
 }
 
-template <int P, int HB>
-__global__ __launch_bounds__(256) void k_pnp_score_f32(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
-                                                       int *__restrict__ queue, int32_t *__restrict__ counts) {
-    static_assert(HB <= 64, "one lane per hypothesis of the block");
-    static_assert(HB * kFModelStride % 256 == 0 || HB * kFModelStride < 256, "model staging");
-    __shared__ int red[4][HB];
-    __shared__ int unit_s;
-    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];  // the unit's f32 records
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int units_per_prob = (H + HB - 1) / HB;
-    const int n_units = units_per_prob * n_prob;
-    for (;;) {
-        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
-        __syncthreads();
-        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
-        if (unit >= n_units) break;  // uniform: every wave of every block reaches it
-        const int prob = unit / units_per_prob;
-        const int64_t h0 = hyp_begin + (int64_t)(unit % units_per_prob) * HB;
-        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
-        const int64_t p0 = a.offsets[prob];
-        const int n = (int)(a.offsets[prob + 1] - p0);
-        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
-        const float cx = fc[2], cy = fc[3], T = fc[4], sqT2 = fc[5], Trel = fc[6], Cmax = fc[7];
-        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-        {
-            // stage the unit's records in LDS: every wave then reads a record with
-            // broadcast ds_reads instead of a global-latency load per hypothesis
-            const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
-            for (int q = threadIdx.x; q < HB * kFModelStride; q += 256)
-                mlds[q] = q < nh * kFModelStride ? fmb[q] : -1.f;
-        }
-        __syncthreads();
-        const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
-        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
-
-        int cnt = 0;
-        for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
-            float px[P], py[P], pz[P], pu[P], pv[P];
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-                const int i = base + j * 64 + lane;
-                const bool in = i < n;
-                const int ii = in ? i : 0;
-                px[j] = XC[ii]; py[j] = YC[ii]; pz[j] = ZC[ii];
-                // out-of-range lanes: a pixel at 3e38 makes the pair a decided outlier
-                pu[j] = in ? U[ii] - cx : 3.0e38f;
-                pv[j] = in ? V[ii] - cy : 3.0e38f;
-            }
-            for (int h = 0; h < nh; ++h) {
-                const float4 *m4 = reinterpret_cast<const float4 *>(mlds + h * kFModelStride);
-                const float4 ma = m4[0], mb = m4[1], mc = m4[2], md4 = m4[3];
-                const float zg = md4.z;
-                if (zg < 0.f) continue;
-                const float r0 = ma.x, r1 = ma.y, r2 = ma.z, r3 = ma.w, r4 = mb.x, r5 = mb.y, r6 = mb.z, r7 = mb.w,
-                            r8 = mc.x, t0 = mc.y, t1 = mc.z, t2 = mc.w, Dz0 = md4.x;
-                int cc = 0;
-                uint64_t und = 0;
-#pragma unroll
-                for (int j = 0; j < P; ++j) {
-                    const float xs = __builtin_fmaf(r0, px[j], __builtin_fmaf(r1, py[j], __builtin_fmaf(r2, pz[j], t0)));
-                    const float ys = __builtin_fmaf(r3, px[j], __builtin_fmaf(r4, py[j], __builtin_fmaf(r5, pz[j], t1)));
-                    const float z = __builtin_fmaf(r6, px[j], __builtin_fmaf(r7, py[j], __builtin_fmaf(r8, pz[j], t2)));
-                    const float q1 = __builtin_fmaf(pu[j], z, xs);
-                    const float q2 = __builtin_fmaf(pv[j], z, ys);
-                    const float z2 = z * z;
-                    const float diff = __builtin_fmaf(-T, z2, __builtin_fmaf(q1, q1, q2 * q2));
-                    const float az = __builtin_fabsf(z);
-                    const float Dz = __builtin_fmaf(Cmax, az, Dz0);
-                    const float Mz = __builtin_fmaf(__builtin_fmaf(sqT2, az, Dz), Dz, Trel * z2);
-                    // one v_cmp per mask; a NaN anywhere leaves the pair undecided
-                    const uint64_t mz = __ballot(az > zg);
-                    const uint64_t mi = __ballot(diff < -Mz);
-                    const uint64_t mo = __ballot(diff > Mz);
-                    cc += __popcll(mi & mz);
-                    und |= ~((mi | mo) & mz);
-                }
-                if (und) {
-                    // Some pair of this tile is undecided: recount the tile for this
-                    // hypothesis with the exact f64 error.  Rare; operands are re-read
-                    // from memory so no register array is indexed and the f64 code does
-                    // not raise the kernel's VGPR budget.
-                    const double *md = a.models + (rec0 + h) * kModelStride;
-                    const double *cm = a.cams + 4 * prob;
-                    const Cam k{cm[0], cm[1], cm[2], cm[3]};
-                    const float thr2 = a.thr2[prob];
-                    cc = 0;
-#pragma unroll 1
-                    for (int j = 0; j < P; ++j) {
-                        const int i = base + j * 64 + lane;
-                        bool ex = false;
-                        if (i < n) {
-                            const int64_t q = p0 + i;
-                            ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q],
-                                         a.V[q]) <= thr2;
-                        }
-                        cc += __popcll(__ballot(ex));
-                    }
-                }
-                cnt += (lane == h) ? cc : 0;
-            }
-        }
-        if (lane < HB) red[wave][lane] = cnt;
-        __syncthreads();
-        if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
-        __syncthreads();  // red and unit_s are rewritten by the next unit
-    }
-}
-
-// Variant of k_pnp_score_f32 with a cheaper band and no per-hypothesis branch.
-//   * band: alpha z^2 + beta >= Mz (the MFMA kernel's majorant), so a pair is
-//     decided by E < (T - alpha) z^2 - beta or E > (T + alpha) z^2 + beta, two
-//     fma instead of five operations;
-//   * the unit's records are staged in LDS already transformed (T - alpha,
-//     T + alpha; invalid records rewritten to z = 1 with -inf thresholds, i.e.
-//     decided outliers), so the hypothesis loop has no branch;
-//   * undecided pairs only set a per-lane bit per hypothesis; the exact f64
-//     recount of those pairs runs once per tile, after the hypothesis loop.
-// Counts are bit-identical to the exact kernel (same tests as k_pnp_score_f32).
-// the three tests of one pair: |z| > zg, E < lo (inlier side), E > hi (outlier side)
-struct AbTest {
-    bool zok, lt, gt;
-};
-
-__device__ __forceinline__ AbTest ab_test(const float *m, float x, float y, float zc, float u, float v) {
-    const float xs = __builtin_fmaf(m[0], x, __builtin_fmaf(m[1], y, __builtin_fmaf(m[2], zc, m[9])));
-    const float ys = __builtin_fmaf(m[3], x, __builtin_fmaf(m[4], y, __builtin_fmaf(m[5], zc, m[10])));
-    const float z = __builtin_fmaf(m[6], x, __builtin_fmaf(m[7], y, __builtin_fmaf(m[8], zc, m[11])));
-    const float q1 = __builtin_fmaf(u, z, xs);
-    const float q2 = __builtin_fmaf(v, z, ys);
-    const float z2 = z * z;
-    const float E = __builtin_fmaf(q1, q1, q2 * q2);
-    const float lo = __builtin_fmaf(m[12], z2, -m[13]);
-    const float hi = __builtin_fmaf(m[15], z2, m[13]);
-    return AbTest{__builtin_fabsf(z) > m[14], E < lo, E > hi};
-}
-
-// The exact f64 recount of a tile's undecided pairs (rare).  Returns this
-// lane's share of the hypotheses' counts (lane h: hypothesis h's inliers).
-template <int P, bool NZ>
-__device__ __forceinline__ int ab_fallback(const PnpArgs &a, int prob, int64_t p0, int n, int64_t rec0,
-                                                     int base, int lane, uint32_t wund, uint32_t undm,
-                                                     const float *mlds, const float (&px)[P], const float (&py)[P],
-                                                     const float (&pz)[P], const float (&pu)[P],
-                                                     const float (&pv)[P]) {
-    const double *cm = a.cams + 4 * prob;
-    const Cam k{cm[0], cm[1], cm[2], cm[3]};
-    const float thr2 = a.thr2[prob];
-    int cnt = 0;
-#pragma unroll 1
-    while (wund) {
-        const int h = __builtin_ctz(wund);
-        wund &= wund - 1;
-        const float *m = mlds + h * kFModelStride;
-        const double *md = a.models + (rec0 + h) * kModelStride;
-        int cc = 0;
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int i = base + j * 64 + lane;
-            bool ex = false;
-            if ((undm >> h) & 1u) {
-                const AbTest r = ab_test(m, px[j], py[j], pz[j], pu[j], pv[j]);
-                const bool dec = (NZ || r.zok) & (r.lt | r.gt);
-                if (!dec && i < n) {
-                    const int64_t q = p0 + i;
-                    ex = md[kValidSlot] != 0.0 &&
-                         pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <=
-                             thr2;
-                }
-            }
-            cc += __popcll(__ballot(ex));
-        }
-        cnt += (lane == h) ? cc : 0;
-    }
-    return cnt;
-}
-
-// split > 1 (small rounds, no fused best key): a unit is (problem, hypothesis tile, point
-// chunk) and the chunk's counts are atomically added into zeroed counts -- enough units to
-// fill the GPU when a round has only a few tiles (an adaptive run's first 256 hypotheses).
-// NZ: no depth-guard test (beta makes it redundant, band_consts): one compare fewer per pair.
-// LEAN: the hypothesis loop runs all HB staged records (the ones past the round are decided
-// outliers), keeps its counter in an SGPR, writes hypothesis h's tile count into lane h
-// (v_writelane) and its undecided flag into bit h of an SGPR mask: ~2 vector instructions per
-// hypothesis besides the pairs' 18, instead of ~10.
-template <int P, int HB, int W = 4, bool NZ = false, bool LEAN = false>  // W: minimum waves per SIMD the register budget must allow
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_ab(
-    PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
-    int split) {
-    static_assert(HB <= 32, "undecided bits per lane");
-    constexpr int kStride = 4 * 64 * P;  // points one pass of the block covers
-    __shared__ int red[4][HB];
-    __shared__ int unit_s;
-    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int tiles_per_prob = (H + HB - 1) / HB;
-    const int units_per_prob = tiles_per_prob * split;
-    const int n_units = units_per_prob * n_prob;
-    for (;;) {
-        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
-        __syncthreads();
-        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
-        if (unit >= n_units) break;  // uniform: every wave of every block reaches it
-        const int prob = unit / units_per_prob;
-        const int rem = unit % units_per_prob;
-        const int chunk = rem % split;
-        const int64_t h0 = hyp_begin + (int64_t)(rem / split) * HB;
-        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
-        const int64_t p0 = a.offsets[prob];
-        const int n_all = (int)(a.offsets[prob + 1] - p0);
-        const int clen = ((n_all + split - 1) / split + kStride - 1) / kStride * kStride;
-        const int start = chunk * clen;
-        const int n = min(n_all, start + clen);  // this unit's points: [start, n)
-        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
-        const float cx = fc[2], cy = fc[3], T = fc[4];
-        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-        if (threadIdx.x < HB) {
-            // one thread per record: copy and transform (slots 12 / 15 -> T -+ alpha)
-            const int hq = threadIdx.x;
-            float *dst = mlds + hq * kFModelStride;
-            const float *src = a.fmodels + (rec0 + hq) * kFModelStride;
-            const bool valid = hq < nh && src[14] >= 0.f;
-            if (valid) {
-#pragma unroll
-                for (int q = 0; q < 12; ++q) dst[q] = src[q];
-                dst[12] = T - src[15];
-                dst[13] = src[13];
-                dst[14] = src[14];
-                dst[15] = T + src[15];
-            } else {
-#pragma unroll
-                for (int q = 0; q < 12; ++q) dst[q] = 0.f;
-                dst[11] = 1.f;  // z = 1
-                dst[12] = -__builtin_inff();
-                dst[13] = 0.f;
-                dst[14] = -1.f;
-                dst[15] = -__builtin_inff();
-            }
-        }
-        __syncthreads();
-        const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
-        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
-
-        int cnt = 0;
-        for (int base = start + wave * 64 * P; base < n; base += kStride) {
-            float px[P], py[P], pz[P], pu[P], pv[P];
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-                const int i = base + j * 64 + lane;
-                const bool in = i < n;
-                const int ii = in ? i : 0;
-                px[j] = XC[ii]; py[j] = YC[ii]; pz[j] = ZC[ii];
-                const float uu = U[ii], vv = V[ii];  // unconditional loads (clamped index): no branch
-                // out-of-range lanes: a pixel at 3e38 makes the pair a decided outlier
-                pu[j] = in ? uu - cx : 3.0e38f;
-                pv[j] = in ? vv - cy : 3.0e38f;
-            }
-            if constexpr (LEAN) {
-                static_assert(NZ, "the lean loop has no depth-guard test");
-                int ccl = 0;        // lane h: hypothesis h's decided inliers of this tile
-                uint32_t wund = 0;  // bit h: hypothesis h has an undecided pair (wave-uniform)
-#pragma unroll 4
-                for (int h = 0; h < HB; ++h) {
-                    const float *m = mlds + h * kFModelStride;
-                    int cc = 0;
-                    uint64_t und = 0;
-#pragma unroll
-                    for (int j = 0; j < P; ++j) {
-                        const AbTest r = ab_test(m, px[j], py[j], pz[j], pu[j], pv[j]);
-                        const uint64_t mi = __ballot(r.lt);
-                        const uint64_t mo = __ballot(r.gt);
-                        cc += __popcll(mi);
-                        und |= ~(mi | mo);
-                    }
-                    // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
-                    // operands would exceed the constant bus); cc and h are SALU results: no hazard
-                    asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
-                    wund |= und ? (1u << h) : 0u;
-                }
-                cnt += ccl;
-                if (__builtin_expect(wund != 0, 0))
-                    cnt += ab_fallback<P, NZ>(a, prob, p0, n, rec0, base, lane, wund, 0xFFFFFFFFu, mlds, px, py, pz,
-                                              pu, pv);
-                continue;
-            }
-            uint32_t undm = 0;  // bit h: this lane has an undecided pair with hypothesis h
-            for (int h = 0; h < nh; ++h) {
-                const float *m = mlds + h * kFModelStride;
-                int cc = 0;
-                uint64_t und = 0;
-#pragma unroll
-                for (int j = 0; j < P; ++j) {
-                    const AbTest r = ab_test(m, px[j], py[j], pz[j], pu[j], pv[j]);
-                    // one v_cmp per mask, combined on the scalar unit; NaN leaves a pair undecided
-                    const uint64_t mi = __ballot(r.lt);
-                    const uint64_t mo = __ballot(r.gt);
-                    if constexpr (NZ) {
-                        cc += __popcll(mi);
-                        und |= ~(mi | mo);
-                    } else {
-                        const uint64_t mz = __ballot(r.zok);
-                        cc += __popcll(mi & mz);
-                        und |= ~((mi | mo) & mz);
-                    }
-                }
-                cnt += (lane == h) ? cc : 0;
-                undm |= __builtin_amdgcn_inverse_ballot_w64(und) ? (1u << h) : 0u;
-            }
-            // exact f64 error (pnp_err, the oracle's formula) for the undecided pairs only
-            uint32_t wund = undm;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) wund |= (uint32_t)__shfl_xor((int)wund, o);
-            wund = __builtin_amdgcn_readfirstlane(wund);
-            if (__builtin_expect(wund != 0, 0)) cnt += ab_fallback<P, NZ>(a, prob, p0, n, rec0, base, lane, wund, undm, mlds, px, py, pz, pu, pv);
-        }
-        if (lane < HB) red[wave][lane] = cnt;
-        __syncthreads();
-        if (split == 1) {
-            if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
-        } else {
-            if (wave == 0 && lane < nh) {
-                const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-                if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
-            }
-        }
-        __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Scaled-form scoring kernel (records of write_fmodel_sc).  Per (hypothesis, point) pair:
@@ -1404,7 +898,7 @@ __device__ __forceinline__ ScPair sc_pair(const float *m, float x, float y, floa
 
 // exact recount of the undecided pairs of the flagged hypotheses (wund) on this lane's points:
 // returns this lane's share of the count corrections (lane h: hypothesis h's)
-template <int P, bool CB = false>
+template <int P>
 __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p0, int n, int64_t rec0, int base,
                                            int lane, uint32_t wund, const float *mlds, const float (&px)[P],
                                            const float (&py)[P], const float (&pz)[P], const float (&pu)[P],
@@ -1424,7 +918,7 @@ __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p
         for (int j = 0; j < P; ++j) {
             const int i = base + j * 64 + lane;
             const ScPair r = sc_pair(m, px[j], py[j], pz[j], pu[j], pv[j]);
-            const bool und = CB ? !(__builtin_fabsf(r.D) > m[15]) : !(r.t > m[13]);
+            const bool und = !(r.t > m[13]);
             bool ex = false;
             if (und && i < n) {
                 const int64_t q = p0 + i;
@@ -1442,7 +936,7 @@ __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p
 // rec0) over the points [start, n) of the problem (p0 its first point).  The unit's HB records are
 // staged in mlds; the counts are added atomically into zeroed counts.  Shared with
 // k_pnp_score_mf, which runs its problems outside the f16 operand range through it.
-template <int P, int HB, bool CB = false>
+template <int P, int HB>
 __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
                                         int lane, int wave, int (*red)[HB], float *mlds, int32_t *__restrict__ counts) {
     constexpr int kStride = 4 * 64 * P;  // points one pass of the block covers: one cell
@@ -1498,9 +992,9 @@ __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, 
             for (int j = 0; j < P; ++j) {
                 const ScPair r = sc_pair(m, px[j], py[j], pz[j], pu[j], pv[j]);
                 cc += __popcll(__ballot(r.D < 0.f));
-                tmin = __builtin_fminf(tmin, CB ? __builtin_fabsf(r.D) : r.t);
+                tmin = __builtin_fminf(tmin, r.t);
             }
-            const uint64_t und = __ballot(!(tmin > m[CB ? 15 : 13]));
+            const uint64_t und = __ballot(!(tmin > m[13]));
             // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
             // operands would exceed the constant bus); cc and h are SALU results: no hazard
             asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
@@ -1508,7 +1002,7 @@ __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, 
         }
         cnt += ccl;
         if (__builtin_expect(wund != 0, 0))
-            cnt += sc_fallback<P, CB>(a, prob, p0, n, rec0, base, lane, wund, mlds, px, py, pz, pu, pv);
+            cnt += sc_fallback<P>(a, prob, p0, n, rec0, base, lane, wund, mlds, px, py, pz, pu, pv);
     }
     if (lane < HB) red[wave][lane] = cnt;
     __syncthreads();
@@ -1522,9 +1016,7 @@ __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, 
 // first tb of them are one unit each (all their points, one pass of the block per cell of
 // 64 x 4 x P points), the rest one unit per cell, so the queue ends with cell-sized units that
 // even out the blocks' finishing times.  Counts are added atomically into zeroed counts.
-// CB: the constant band of record slot 15 (b + a Zmax) instead of a |z'| + b: no t per pair, the
-// minimum is taken over |D| directly (more pairs undecided where |z'| is well below Zmax).
-template <int P, int HB, int W = 4, bool CB = false>
+template <int P, int HB, int W = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_sc(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int tb, int cells) {
@@ -1560,7 +1052,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         const int start = c0 * kStride;
         const int n = min(n_all, c1 * kStride);  // this unit's points: [start, n)
         if (start < n_all)  // else a cell past a short problem of a batch (uniform)
-            sc_unit<P, HB, CB>(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
+            sc_unit<P, HB>(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
         __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
     }
 }
@@ -1695,29 +1187,26 @@ __device__ __forceinline__ mf_h8 mw_operand(const float *__restrict__ recs, int 
     return __builtin_bit_cast(mf_h8, v);
 }
 
-// exact recount of one flagged iteration (one wave): the MFMA and the VALU test of the flagged
-// slots are redone (same operands, same bits) and each undecided pair's fast verdict (D < 0) is
-// replaced by the exact f64 test (pnp_err); the corrections are added to the counts.  Every load
-// that does not depend on the test (point operands, the slopes and bands of the 32 hypotheses,
-// the lane's two points in f32) is issued up front; per flagged group the A operand, per slot
-// with an undecided pair its model.
-// lcorr (inline recount): the corrections go to the unit's LDS array (index: hypothesis within
-// the unit) instead of global atomics; the unit's epilogue folds them into its counts
-__device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfFlag &f, int base, int col, int half,
-                                           int32_t *__restrict__ counts, int *lcorr = nullptr) {
-    const int64_t p0 = f.p0, rec0 = f.rec0;
-    const uint32_t fl = f.fl;
-    const int nh = f.nh;
+// exact recount of one flagged iteration of a unit (one wave; hypotheses rec0 .. rec0 + nh of the
+// problem whose points start at p0 and whose unit ends at point n): the MFMA and the VALU test of
+// the flagged slots fl are redone (same operands, same bits) and each undecided pair's fast
+// verdict (D < 0) is replaced by the exact f64 test (pnp_err); the corrections go to the unit's
+// LDS array lcorr (index: hypothesis within the unit), which the epilogue folds into the counts.
+// Every load that does not depend on the test (point operands, the slopes and bands of the 32
+// hypotheses, the lane's two points in f32) is issued up front; per flagged group the A
+// operand, per slot with an undecided pair its model.
+__device__ __forceinline__ void mf_recount(const PnpArgs &a, int64_t rec0, int64_t p0, int n, uint32_t fl, int nh,
+                                           int base, int col, int half, int *lcorr) {
     const int prob = (int)(rec0 / a.hyp_stride);
     const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
     mf_h8 Ba, Bb;
     float2 ua, ub;
-    mf_load(a.PF + 2 * p0, a.UV + p0, base, f.n, col, half, Ba, Bb, ua, ub);
+    mf_load(a.PF + 2 * p0, a.UV + p0, base, n, col, half, Ba, Bb, ua, ub);
     // lane c < 32: a' and b' of hypothesis c (read by the others through a lane shuffle)
     const int jc = min(col, nh - 1);
     const float a_c = gview(recs)[jc * kFModelStride + 12], b_c = gview(recs)[jc * kFModelStride + 13];
     const int ia = base + col, ib = ia + 32;
-    const int64_t qa = p0 + min(ia, f.n - 1), qb = p0 + min(ib, f.n - 1);
+    const int64_t qa = p0 + min(ia, n - 1), qb = p0 + min(ib, n - 1);
     const float Xa = a.X[qa], Ya = a.Y[qa], Za = a.Z[qa], Uxa = a.U[qa], Vxa = a.V[qa];
     const float Xb = a.X[qb], Yb = a.Y[qb], Zb = a.Z[qb], Uxb = a.U[qb], Vxb = a.V[qb];
     const double *cm = a.cams + 4 * prob;
@@ -1739,7 +1228,7 @@ __device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfFlag &f, in
             const float ag = live ? aj : 0.f;
             const float bg = live ? bj : -__builtin_inff();
             const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
-            const bool wa = !(ra.t > bg) && ia < f.n, wb = !(rb.t > bg) && ib < f.n;
+            const bool wa = !(ra.t > bg) && ia < n, wb = !(rb.t > bg) && ib < n;
             if (wa || wb) {
                 const double *md = a.models + (rec0 + j) * kModelStride;
                 const bool mv = md[kValidSlot] != 0.0;
@@ -1750,12 +1239,7 @@ __device__ __forceinline__ void mf_recount(const PnpArgs &a, const MfFlag &f, in
                 if (wb)
                     c += (mv && pnp_err(md, md + 9, k, (double)Xb, (double)Yb, (double)Zb, Uxb, Vxb) <= thr2 ? 1 : 0) -
                          (rb.D < 0.f ? 1 : 0);
-                if (c) {
-                    if (lcorr)
-                        atomicAdd(&lcorr[j], c);
-                    else
-                        atomicAdd(&counts[rec0 + j], c);
-                }
+                if (c) atomicAdd(&lcorr[j], c);
             }
         }
     }
@@ -1778,36 +1262,26 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
     sc_unit<8, 32>(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
 }
 
-constexpr int kWrec = 64;  // flagged-window list of a wave (k_pnp_score_mf)
 
-// s_memtime phase totals of k_pnp_score_mf's timing instance (variant 84, diagnostics only):
-// [0] kernel, [1] unit prologue (staging), [2] point loop, [3] epilogue, [4] between units
-// (barrier + queue), [5] waves, [6] units
-__device__ unsigned long long g_mf_timing[8];
-struct MfTimes {
-    unsigned long long pro = 0, loop = 0, epi = 0;
-};
-__device__ __forceinline__ unsigned long long mf_clock() {
-    unsigned long long t = __builtin_amdgcn_s_memtime();
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the stamp has arrived
-    return t;
-}
+// One unit of k_pnp_score_mf: hypotheses [h0, h0 + nh) of problem prob (records at rec0) over
+// the points [start, n) of the problem (p0 its first point, n_all_pts its length).  Per
+// iteration a wave takes 2 x 32 points: 4 MFMA groups x 2 tiles, the counts (255 x, v_sad_u8)
+// and the band minimum per slot; after every iteration the 16 slot minima are compared with b'
+// and a flagged iteration goes to the wave's LDS list (at most kWrec: the launcher bounds a
+// unit's points by 256 kWrec).  After its point loop the wave recounts its listed iterations
+// exactly (mf_recount) into the unit's LDS corrections, which the epilogue adds to the counts.
+constexpr int kWrec = 64;  // flagged iterations a wave lists per unit (k_pnp_score_mf)
 
-// CHK: iterations (2 x 32 points per wave) per check window of the band minimum
-template <bool FB, int CHK, int PD, bool RA, bool PIPE = false, bool TM = false, bool INL = false, int PRIO = 0>
-__device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, int64_t h0, int nh, int64_t p0, int start,
-                                        int n, int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
-                                        mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *wcnt, MfTimes &tms,
-                                        int32_t *__restrict__ counts, int *lcorr = nullptr,
-                                        unsigned long long *blk_best = nullptr) {
-    unsigned long long ts0 = 0, ts1 = 0;
-    if constexpr (TM) ts0 = mf_clock();
+__device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
+                                        int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64],
+                                        float (*ab)[2][4][4], mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *lcorr,
+                                        int32_t *__restrict__ counts) {
     constexpr int HB = 32;
     const int col = lane & 31, half = lane >> 5;
     const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
     const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
-    if (INL && threadIdx.x < HB) lcorr[threadIdx.x] = 0;  // the unit's corrections (before the barrier)
     if (threadIdx.x < HB) {
+        lcorr[threadIdx.x] = 0;  // the unit's corrections (before the barrier)
         // a' and b' of slot (t, g, half) = hypothesis 8t + 2g + half; past the round: b' = -inf
         // (records without a model carry a' = 0, b' = -inf themselves)
         const int j = threadIdx.x;
@@ -1831,334 +1305,24 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int unit, int prob, in
             vc[t][g] = 0u;
             tm[t][g] = __builtin_inff();
         }
-    int nw = 0;  // flagged windows in the wave's list (uniform)
-    int it = 0;  // iterations in the current window
-    // Per iteration: counts and the band minimum (min3 of both tiles per slot).  At the end of a
-    // window (CHK iterations, or the wave's last) the minima are compared with b'; a window with
-    // a flagged slot is recorded for k_pnp_mf_recount (FB = false: timing experiments only, no
-    // check at all).  Full iterations run without bounds checks; a partial one follows the loop.
+    int nw = 0;  // flagged iterations in the wave's list (uniform)
     const int b0 = start + wave * 64;
     const int iters = n > b0 ? (n - b0 + 255) / 256 : 0;
-    // the point operands of iteration i, loaded PD iterations ahead (PD = 0: at its start)
-    // RA: the A operands and slopes a' in registers for the whole unit (else read from LDS per
-    // iteration, fewer registers)
+    // the A operands and slopes a' in registers for the whole unit
     mf_h8 Ar[4];
     float4 avr[4];
-    if constexpr (RA) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            Ar[t] = alds[t][lane];
-            avr[t] = *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
-        }
+    for (int t = 0; t < 4; ++t) {
+        Ar[t] = alds[t][lane];
+        avr[t] = *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
     }
     auto body = [&](int i, const mf_h8 &Ba, const mf_h8 &Bb, const float2 &ua, const float2 &ub)
         __attribute__((always_inline)) {
-        if constexpr (PIPE) {
-            // software-pipelined: group t + 1's MFMAs are issued before group t's vector work, so
-            // the matrix latency hides behind this wave's own VALU (two output sets live)
-            mf_f16v xa[2], xb[2];
-            xa[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(RA ? Ar[0] : alds[0][lane], Ba, mf_f16v{}, 0, 0, 0);
-            xb[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(RA ? Ar[0] : alds[0][lane], Bb, mf_f16v{}, 0, 0, 0);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                if (t < 3) {
-                    const mf_h8 An = RA ? Ar[t + 1] : alds[t + 1][lane];
-                    xa[(t + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(An, Ba, mf_f16v{}, 0, 0, 0);
-                    xb[(t + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(An, Bb, mf_f16v{}, 0, 0, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
-                    const MfPair ra = mf_pair(xa[t & 1], g, ua, ag), rb = mf_pair(xb[t & 1], g, ub, ag);
-                    vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
-                    if (FB) tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else if constexpr (PRIO == 4) {
-            // the count and band minimum of group t - 1 are issued right behind group t's MFMAs
-            // (they fill the matrix shadow instead of waiting behind the next pair's FMAs)
-            MfPair pa[4], pb[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const mf_h8 At = RA ? Ar[t] : alds[t][lane];
-                const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
-                const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
-                const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (t > 0) {
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        vc[t - 1][g] = mf_cnt255(vc[t - 1][g], pa[g].D, pb[g].D);
-                        if (FB) tm[t - 1][g] = mf_min3(tm[t - 1][g], pa[g].t, pb[g].t);
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
-                    pa[g] = mf_pair(xa, g, ua, ag);
-                    pb[g] = mf_pair(xb, g, ub, ag);
-                }
-            }
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                vc[3][g] = mf_cnt255(vc[3][g], pa[g].D, pb[g].D);
-                if (FB) tm[3][g] = mf_min3(tm[3][g], pa[g].t, pb[g].t);
-            }
-        } else {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const mf_h8 At = RA ? Ar[t] : alds[t][lane];
-                const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
-                if (PRIO == 1) __builtin_amdgcn_s_setprio(1);  // PRIO 1: priority around the MFMA pair
-                const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
-                const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
-                if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
-                    const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
-                    vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
-                    if (FB) tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
-                }
-            }
-        }
-        if (FB && (++it == CHK || i == iters - 1)) {  // end of a check window (uniform)
-            // one OR of the 16 slots' ballots (a compare and a scalar OR per slot); the slot
-            // bits only when some slot is flagged (rare)
-            uint64_t any = 0;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
-                    any |= __ballot(!(tm[t][g] > bg));
-                }
-            }
-            uint32_t fl = 0;
-            if (__builtin_expect(any != 0, 0)) {
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
-                        fl |= __ballot(!(tm[t][g] > bg)) ? (1u << (4 * t + g)) : 0u;
-                    }
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) tm[t][g] = __builtin_inff();
-            if (__builtin_expect(fl != 0, 0)) {
-                // kept in the wave's LDS list (first iteration, window length in bits 24..),
-                // appended to a.mf_list with the unit's (one atomic per block), or at once by the
-                // wave when its list is full
-                if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)(i + 1 - it) | ((uint32_t)it << 24), fl);
-                if (INL)
-                    ++nw;  // INL: at most kWrec windows per wave and unit (the launcher checks)
-                else if (++nw == kWrec) {
-                    __builtin_amdgcn_wave_barrier();
-                    int slot = 0;
-                    const int qk = blockIdx.x % kQSub;
-                    const int64_t seg = a.mf_cap / kQSub;
-                    if (lane == 0) slot = atomicAdd(rec_queue(a.queue, qk), kWrec);
-                    slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0));
-                    if (slot + lane < seg) {
-                        const uint2 w = wrec[wave][lane];
-                        a.mf_list[qk * seg + slot + lane] = MfFlag{rec0, p0, b0 + 256 * (int)(w.x & 0xFFFFFFu), n, w.y, (int16_t)nh,
-                                                     (int16_t)(w.x >> 24)};
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    nw = 0;
-                }
-            }
-            it = 0;
-        }
-    };
-    const int full = n >= b0 + 64 ? (n - b0 - 64) / 256 + 1 : 0;  // iterations with 64 points in range
-    if constexpr (TM) {
-        ts1 = mf_clock();
-        tms.pro += ts1 - ts0;
-        ts0 = ts1;
-    }
-    if constexpr (PD == 0) {
-        for (int i = 0; i < full; ++i) {
-            mf_h8 Ba, Bb;
-            float2 ua, ub;
-            mf_load_full(PF, UV, b0 + 256 * i, col, half, Ba, Bb, ua, ub);
-            body(i, Ba, Bb, ua, ub);
-        }
-    } else {  // one iteration ahead: the next operands are in flight while this one computes
-        mf_h8 Ba, Bb, Na, Nb;
-        float2 ua, ub, na, nb;
-        if (full > 0) mf_load_full(PF, UV, b0, col, half, Ba, Bb, ua, ub);
-        for (int i = 0; i < full; ++i) {
-            if (i + 1 < full) mf_load_full(PF, UV, b0 + 256 * (i + 1), col, half, Na, Nb, na, nb);
-            body(i, Ba, Bb, ua, ub);
-            Ba = Na;
-            Bb = Nb;
-            ua = na;
-            ub = nb;
-        }
-    }
-    if (full < iters) {
-        mf_h8 Ba, Bb;
-        float2 ua, ub;
-        mf_load_part(PF, UV, b0 + 256 * full, n, col, half, Ba, Bb, ua, ub);
-        body(full, Ba, Bb, ua, ub);
-    }
-    if constexpr (INL) {
-        // the wave's flagged windows recounted here (no records, no recount launch): the wave's
-        // exact-test latency overlaps the other blocks' waves on its SIMD
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll 1
-        for (int k = 0; k < nw; ++k) {
-            const uint2 w = wrec[wave][k];
-            const int base = b0 + 256 * (int)(w.x & 0xFFFFFFu), wi = (int)(w.x >> 24);
-            const MfFlag f{rec0, p0, base, n, w.y, (int16_t)nh, (int16_t)wi};
-#pragma unroll 1
-            for (int iw = 0; iw < wi && base + 256 * iw < n; ++iw)
-                mf_recount(a, f, base + 256 * iw, col, half, counts, lcorr);
-        }
-        nw = 0;
-    }
-    if constexpr (TM) {
-        ts1 = mf_clock();
-        tms.loop += ts1 - ts0;
-        ts0 = ts1;
-    }
-    if (lane == 0) wcnt[wave] = nw;
-    // counts: lane (c, half) of wave w holds slot (t, g)'s count over its points; hypothesis j =
-    // 8t + 2g + half sums 4 waves x 32 lanes (8 threads of 16 values each, then a shuffle tree)
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) cl[wave][4 * t + g][lane] = vc[t][g];
-    __syncthreads();
-    // the waves' flagged iterations: one atomic for the block (taken before thread 0's count
-    // atomic, so its wait does not cover that), then a store per record
-    if (FB && threadIdx.x == 0) {
-        const int rtot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        wcnt[4] = rtot ? atomicAdd(rec_queue(a.queue, blockIdx.x % kQSub), rtot) : 0;
-    }
-    {
-        const int j = threadIdx.x >> 3, p = threadIdx.x & 7;
-        const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + 4 * p;
-        uint32_t sum = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-#pragma unroll
-            for (int l = 0; l < 4; ++l) sum += cl[w][slot][l0 + l];
-        sum += __shfl_xor(sum, 1);
-        sum += __shfl_xor(sum, 2);
-        sum += __shfl_xor(sum, 4);
-        // a unit over all of its problem's points is the only writer of its counts: a store
-        // (an atomic is acknowledged by the device's coherence point, and every later wait of
-        // the wave would wait for it)
-        unsigned long long kj = 0;
-        if (p == 0 && j < nh) {
-            // INL: + the unit's corrections (in LDS, complete at the barrier above)
-            const int cj = (int)(sum / 255u) + (INL ? lcorr[j] : 0);
-            if (start == 0 && n == n_all_pts)
-                counts[rec0 + j] = cj;
-            else if (cj)
-                atomicAdd(&counts[rec0 + j], cj);
-            // fused best key (INL, every unit over its whole problem: the counts are final here):
-            // k_best_key's packed key of hypothesis h0 + j
-            if (INL && blk_best && cj > 0 && a.status[rec0 + j] > 0) {
-                const uint64_t g = (uint64_t)(a.rng_base + h0 + j);
-                kj = ((unsigned long long)(uint32_t)cj << 32) | (0xFFFFFFFFull - (g & 0xFFFFFFFFull));
-            }
-        }
-        if (INL && blk_best) {  // uniform: the wave's maximum into the block's (LDS)
-#pragma unroll
-            for (int o = 8; o < 64; o <<= 1) {
-                const unsigned long long other = __shfl_xor(kj, o);
-                kj = other > kj ? other : kj;
-            }
-            if (lane == 0 && kj) atomicMax(blk_best, kj);
-        }
-    }
-    if (FB) {
-        __syncthreads();
-        int off = wcnt[4];
-        for (int w = 0; w < wave; ++w) off += wcnt[w];
-        const int64_t seg = a.mf_cap / kQSub;
-        if (lane < wcnt[wave] && off + lane < seg) {
-            const uint2 w = wrec[wave][lane];
-            a.mf_list[blockIdx.x % kQSub * seg + off + lane] = MfFlag{rec0, p0, b0 + 256 * (int)(w.x & 0xFFFFFFu), n, w.y, (int16_t)nh,
-                                          (int16_t)(w.x >> 24)};
-        }
-    }
-    if constexpr (TM) tms.epi += mf_clock() - ts0;
-}
-
-// Dynamic form of mf_unit (variants 85, 86): the block's 4 waves take pairs of consecutive
-// iterations (2 x 64 points) from an LDS counter instead of a fixed 256-point stride, so they
-// reach the epilogue barrier within one pair of each other.  With the fixed stride the waves of
-// a block (each on a SIMD shared with other blocks' waves) drifted apart, and the first ones
-// waited at that barrier for 20 % of the kernel (s_memtime phases, variant 84).  A pair is one
-// check window; its record is {base, 1 or 2 iterations, 64 points apart}.  The next pair's index
-// is taken one pair ahead, so the point operands are loaded one iteration ahead throughout.
-template <bool RA, bool TM>
-__device__ __forceinline__ void mfd_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
-                                         int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
-                                         mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *wcnt, int *pctr, MfTimes &tms,
-                                         int32_t *__restrict__ counts) {
-    unsigned long long ts0 = 0, ts1 = 0;
-    if constexpr (TM) ts0 = mf_clock();
-    constexpr int HB = 32;
-    const int col = lane & 31, half = lane >> 5;
-    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-    const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
-    if (threadIdx.x < HB) {
-        const int j = threadIdx.x;
-        const bool v = j < nh;
-        ab[0][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 12] : 0.f;
-        ab[1][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 13] : -__builtin_inff();
-    }
-    {
-        const int tl = threadIdx.x & 63;
-        alds[threadIdx.x >> 6][tl] = mf_operand(recs, threadIdx.x >> 6, tl & 31, tl >> 5, nh);
-    }
-    if (threadIdx.x == 0) *pctr = 0;
-    __syncthreads();
-    const uint4 *__restrict__ PF = a.PF + 2 * p0;
-    const float2 *__restrict__ UV = a.UV + p0;
-    uint32_t vc[4][4];
-    float tm[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            vc[t][g] = 0u;
-            tm[t][g] = __builtin_inff();
-        }
-    int nw = 0;
-    mf_h8 Ar[4];
-    float4 avr[4];
-    if constexpr (RA) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            Ar[t] = alds[t][lane];
-            avr[t] = *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
-        }
-    }
-    auto body = [&](const mf_h8 &Ba, const mf_h8 &Bb, const float2 &ua, const float2 &ub)
-        __attribute__((always_inline)) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const mf_h8 At = RA ? Ar[t] : alds[t][lane];
-            const float4 av = RA ? avr[t] : *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
-            const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Ba, mf_f16v{}, 0, 0, 0);
-            const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(At, Bb, mf_f16v{}, 0, 0, 0);
+            const float4 av = avr[t];
+            const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Ba, mf_f16v{}, 0, 0, 0);
+            const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Bb, mf_f16v{}, 0, 0, 0);
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
@@ -2167,141 +1331,107 @@ __device__ __forceinline__ void mfd_unit(const PnpArgs &a, int prob, int64_t h0,
                 tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
             }
         }
-    };
-    auto grab = [&]() __attribute__((always_inline)) {
-        int g = 0;
-        if (lane == 0) g = __hip_atomic_fetch_add(pctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return __builtin_amdgcn_readfirstlane(g);
-    };
-    auto load = [&](int base, mf_h8 &Ba, mf_h8 &Bb, float2 &ua, float2 &ub) __attribute__((always_inline)) {
-        if (base + 64 <= n)
-            mf_load_full(PF, UV, base, col, half, Ba, Bb, ua, ub);
-        else
-            mf_load_part(PF, UV, base, n, col, half, Ba, Bb, ua, ub);
-    };
-    const int npairs = (n - start + 127) / 128;
-    int g = grab();
-    mf_h8 Ba, Bb, Na, Nb;
-    float2 ua, ub, na, nb;
-    if (g < npairs) load(start + 128 * g, Ba, Bb, ua, ub);
-    while (g < npairs) {  // uniform
-        const int gn = grab();
-        const int base = start + 128 * g;
-        const bool two = base + 64 < n;
-        if (two)
-            load(base + 64, Na, Nb, na, nb);
-        else if (gn < npairs)
-            load(start + 128 * gn, Na, Nb, na, nb);
-        body(Ba, Bb, ua, ub);
-        Ba = Na;
-        Bb = Nb;
-        ua = na;
-        ub = nb;
-        if (two) {
-            if (gn < npairs) load(start + 128 * gn, Na, Nb, na, nb);
-            body(Ba, Bb, ua, ub);
-            Ba = Na;
-            Bb = Nb;
-            ua = na;
-            ub = nb;
-        }
-        uint32_t fl = 0;  // the pair's check window
+        // one OR of the 16 slots' ballots (a compare and a scalar OR per slot); the slot bits
+        // only when some slot is flagged (rare)
+        uint64_t any = 0;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float bg = q == 0 ? bv.x : q == 1 ? bv.y : q == 2 ? bv.z : bv.w;
-                fl |= __ballot(!(tm[t][q] > bg)) ? (1u << (4 * t + q)) : 0u;
-                tm[t][q] = __builtin_inff();
+            for (int g = 0; g < 4; ++g) {
+                const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
+                any |= __ballot(!(tm[t][g] > bg));
             }
         }
-        if (__builtin_expect(fl != 0, 0)) {
-            if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)base, fl | (1u << 16) | ((two ? 2u : 1u) << 24));
-            if (++nw == kWrec) {
-                __builtin_amdgcn_wave_barrier();
-                int slot = 0;
-                const int qk = blockIdx.x % kQSub;
-                const int64_t seg = a.mf_cap / kQSub;
-                if (lane == 0) slot = atomicAdd(rec_queue(a.queue, qk), kWrec);
-                slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0));
-                if (slot + lane < seg) {
-                    const uint2 w = wrec[wave][lane];
-                    a.mf_list[qk * seg + slot + lane] =
-                        MfFlag{rec0, p0, (int32_t)w.x, n, w.y & 0x1FFFFu, (int16_t)nh, (int16_t)(w.y >> 24)};
+        uint32_t fl = 0;
+        if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
+                    fl |= __ballot(!(tm[t][g] > bg)) ? (1u << (4 * t + g)) : 0u;
                 }
-                __builtin_amdgcn_wave_barrier();
-                nw = 0;
             }
         }
-        g = gn;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) tm[t][g] = __builtin_inff();
+        if (__builtin_expect(fl != 0, 0)) {
+            if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)i, fl);
+            ++nw;
+        }
+    };
+    const int full = n >= b0 + 64 ? (n - b0 - 64) / 256 + 1 : 0;  // iterations with 64 points in range
+    for (int i = 0; i < full; ++i) {
+        mf_h8 Ba, Bb;
+        float2 ua, ub;
+        mf_load_full(PF, UV, b0 + 256 * i, col, half, Ba, Bb, ua, ub);
+        body(i, Ba, Bb, ua, ub);
     }
-    if constexpr (TM) {
-        ts1 = mf_clock();
-        tms.loop += ts1 - ts0;
-        ts0 = ts1;
+    if (full < iters) {
+        mf_h8 Ba, Bb;
+        float2 ua, ub;
+        mf_load_part(PF, UV, b0 + 256 * full, n, col, half, Ba, Bb, ua, ub);
+        body(full, Ba, Bb, ua, ub);
     }
-    if (lane == 0) wcnt[wave] = nw;
+    // the wave's flagged iterations recounted here: the wave's exact-test latency overlaps the
+    // other blocks' waves on its SIMD
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (int k = 0; k < nw; ++k) {
+        const uint2 w = wrec[wave][k];
+        mf_recount(a, rec0, p0, n, w.y, nh, b0 + 256 * (int)w.x, col, half, lcorr);
+    }
+    // counts: lane (c, half) of wave w holds slot (t, g)'s count over its points; hypothesis j =
+    // 8t + 2g + half sums 4 waves x 32 lanes (8 threads of 16 values each, then a shuffle tree)
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cl[wave][4 * t + q][lane] = vc[t][q];
+        for (int g = 0; g < 4; ++g) cl[wave][4 * t + g][lane] = vc[t][g];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const int rtot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        wcnt[4] = rtot ? atomicAdd(rec_queue(a.queue, blockIdx.x % kQSub), rtot) : 0;
-    }
-    {
-        const int j = threadIdx.x >> 3, p = threadIdx.x & 7;
-        const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + 4 * p;
-        uint32_t sum = 0;
+    const int j = threadIdx.x >> 3, p = threadIdx.x & 7;
+    const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + 4 * p;
+    uint32_t sum = 0;
 #pragma unroll
-        for (int w = 0; w < 4; ++w)
+    for (int w = 0; w < 4; ++w)
 #pragma unroll
-            for (int l = 0; l < 4; ++l) sum += cl[w][slot][l0 + l];
-        sum += __shfl_xor(sum, 1);
-        sum += __shfl_xor(sum, 2);
-        sum += __shfl_xor(sum, 4);
-        if (p == 0 && j < nh) {
-            if (start == 0 && n == n_all_pts)
-                counts[rec0 + j] = (int)(sum / 255u);
-            else if (sum)
-                atomicAdd(&counts[rec0 + j], (int)(sum / 255u));
-        }
+        for (int l = 0; l < 4; ++l) sum += cl[w][slot][l0 + l];
+    sum += __shfl_xor(sum, 1);
+    sum += __shfl_xor(sum, 2);
+    sum += __shfl_xor(sum, 4);
+    if (p == 0 && j < nh) {
+        // + the unit's corrections (in LDS, complete at the barrier above).  A unit over all of
+        // its problem's points is the only writer of its counts: a store (an atomic is
+        // acknowledged by the device's coherence point, and every later wait of the wave would
+        // wait for it); cells add theirs
+        const int cj = (int)(sum / 255u) + lcorr[j];
+        if (start == 0 && n == n_all_pts)
+            counts[rec0 + j] = cj;
+        else if (cj)
+            atomicAdd(&counts[rec0 + j], cj);
     }
-    __syncthreads();
-    int off = wcnt[4];
-    for (int w = 0; w < wave; ++w) off += wcnt[w];
-    const int64_t seg = a.mf_cap / kQSub;
-    if (lane < wcnt[wave] && off + lane < seg) {
-        const uint2 w = wrec[wave][lane];
-        a.mf_list[blockIdx.x % kQSub * seg + off + lane] =
-            MfFlag{rec0, p0, (int32_t)w.x, n, w.y & 0x1FFFFu, (int16_t)nh, (int16_t)(w.y >> 24)};
-    }
-    if constexpr (TM) tms.epi += mf_clock() - ts0;
 }
 
-// Phase 1: units from the queue (a.queue[0]); a unit's flagged iterations are appended to
-// a.mf_list (count a.queue[2]) and the unit is counted finished (a.queue[1]).  Phase 2, once the
-// unit queue is empty: every wave takes flagged records (a.queue[3]) after all units have
-// finished (their records are then complete) and recounts them.  A block only waits once every
-// unit has been taken by a running block, so the wait always ends.
-// W: minimum waves per SIMD the register budget must allow; PD: point operands loaded 0 / 1
-// iterations ahead
-template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false, bool PIPE = false, bool TM = false,
-          bool DYN = false, bool INL = false, int PRIO = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_pnp_score_mf(
+// Units from the split queue: block b takes units b % kQSub + kQSub i from counter b % kQSub.
+// Unit numbering as k_pnp_score_sc (the first tb tiles whole, then one unit per cell of cell_pts
+// points).  Problems whose centred coordinates leave the f16 operand range (fconst[11] = 0) carry
+// form-1 records and run the sc_unit body.  3 waves per SIMD (168 VGPRs).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_pnp_score_mf(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int tb, int cells, int cell_pts) {
     constexpr int HB = 32;
-    __shared__ int unit_s;
+    // the unit index, double-buffered by iteration parity: thread 0 writes the next unit's slot
+    // while the other waves may still be reading this one's (a skipped cell runs no barrier
+    // between the read at the loop's top and that write)
+    __shared__ int unit_s[2];
     __shared__ uint32_t cl[4][16][64];
     __shared__ __attribute__((aligned(16))) float ab[2][2][4][4];
     __shared__ uint2 wrec[4][kWrec];
-    __shared__ int wcnt[5];
-    __shared__ int lcorr[32];  // INL: the unit's exact-recount corrections
-    __shared__ unsigned long long blk_best;  // INL with a.best_key: the block's best packed key
-    __shared__ int pctr;  // DYN: the unit's next iteration pair
+    __shared__ int lcorr[32];  // the unit's exact-recount corrections
     __shared__ mf_h8 alds[4][64];
     __shared__ int red[4][HB];                                                 // sc_unit
     __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];  // sc_unit
@@ -2309,28 +1439,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tiles_per_prob = (H + HB - 1) / HB;
     const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
-    // INL with a.best_key (the launcher passes it only when every unit covers its whole problem):
-    // the best key is reduced here, one atomic per block at the end (no k_best_key launch)
-    const bool fuse_key = INL && a.best_key != nullptr;
-    if (threadIdx.x == 0) blk_best = 0;
-    if (PRIO == 2 && wave >= 2) __builtin_amdgcn_s_setprio(1);  // PRIO 2: static priority, younger half
-    if (PRIO == 3 && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);  // PRIO 3: every other block
-    MfTimes tms;
-    unsigned long long tk0 = 0, tb0 = 0, tbar = 0, nunits = 0;
-    if constexpr (TM) tk0 = mf_clock();
     const int qk = blockIdx.x % kQSub;  // this block's units: qk + kQSub i, i from counter qk
     int *const uq = unit_queue(queue, qk);
-    if (threadIdx.x == 0) unit_s = qk + kQSub * atomicAdd(uq, 1);
+    if (threadIdx.x == 0) unit_s[0] = qk + kQSub * atomicAdd(uq, 1);
     __syncthreads();
     int last_prob = -1, n_all = 0;
     int64_t p0 = 0;
     bool in_range = false;
-    for (;;) {
-        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
+    for (int par = 0;; par ^= 1) {
+        const int unit = __builtin_amdgcn_readfirstlane(unit_s[par]);
         if (unit >= n_units) break;  // uniform: every wave of every block reaches it
-        // the next unit's index, in flight while this unit runs: the atomic optimizer is off for
-        // this file (Makefile), so the compiler waits for the result only where it is used, at
-        // the unit's end (and a spill of the pending register waits for it too)
+        // the next unit's index, in flight while this unit runs: the library is built with the
+        // atomic optimizer off (Makefile), so the compiler waits for the result only where it is
+        // used, at the unit's end
         int nx = 0;
         if (threadIdx.x == 0) nx = atomicAdd(uq, 1);
         int tile, c0, c1;
@@ -2354,614 +1475,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) voi
         }
         const int start = c0 * cell_pts;
         const int n = min(n_all, c1 * cell_pts);
-        if (start < n_all) {
+        if (start < n_all) {  // else a cell past a short problem of a batch (uniform)
             if (in_range)
-                if constexpr (DYN)
-                    mfd_unit<RA, TM>(a, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds, wrec, wcnt, &pctr, tms,
-                                     counts);
-                else
-                    mf_unit<FB, CHK, PD, RA, PIPE, TM, INL, PRIO>(a, unit, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds,
-                                                       wrec, wcnt, tms, counts, lcorr,
-                                                       fuse_key ? &blk_best : nullptr);
+                mf_unit(a, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds, wrec, lcorr, counts);
             else
                 mf_sc_unit(kernarg_pnp(), prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
         }
-        if constexpr (TM) {
-            tb0 = mf_clock();
-            ++nunits;
-        }
-        // the next unit (every thread read unit_s before the unit's barriers); the empty asm keeps
-        // the arithmetic on nx (and so the wait for it) here
+        // the next unit (the other slot); the empty asm keeps the arithmetic on nx (and so the
+        // wait for it) here
         if (threadIdx.x == 0) {
             asm volatile("" : "+v"(nx));
-            unit_s = qk + kQSub * nx;
+            unit_s[par ^ 1] = qk + kQSub * nx;
         }
-        __syncthreads();  // the unit's LDS and unit_s are rewritten by the next unit
-        if constexpr (TM) tbar += mf_clock() - tb0;
-    }
-    if (fuse_key && threadIdx.x == 0 && blk_best) atomicMax(a.best_key, blk_best);  // after the last barrier
-    if constexpr (TM) {
-        if (lane == 0) {
-            atomicAdd(&g_mf_timing[0], mf_clock() - tk0);
-            atomicAdd(&g_mf_timing[1], tms.pro);
-            atomicAdd(&g_mf_timing[2], tms.loop);
-            atomicAdd(&g_mf_timing[3], tms.epi);
-            atomicAdd(&g_mf_timing[4], tbar);
-            atomicAdd(&g_mf_timing[5], 1ull);
-            atomicAdd(&g_mf_timing[6], nunits);
-        }
-    }
-}
-
-// The exact recount of k_pnp_score_mf's flagged iterations (a.mf_list, count a.queue[2]): one
-// wave per record, grid-stride; the corrections are added to the counts.
-// segs = kQSub: the records of k_pnp_score_mw, in kQSub segments of a.mf_cap / kQSub (record r
-// of the concatenation maps to its segment through the counts); 0: one list (k_pnp_score_mf)
-__device__ __forceinline__ int64_t mf_rec_index(const int *cnt, int segs, int64_t seg, int r) {
-    if (!segs) return r;
-    int k = 0;
-    while (k < segs - 1 && r >= cnt[k]) r -= cnt[k++];
-    return k * seg + r;
-}
-__global__ __launch_bounds__(256) void k_pnp_mf_recount(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
-                                                        int32_t *__restrict__ counts, int segs, int, int) {
-    const int lane = threadIdx.x & 63;
-    const int col = lane & 31, half = lane >> 5;
-    const int64_t seg = segs ? a.mf_cap / segs : a.mf_cap;
-    int cnt[kQSub];
-    int nrec = 0;
-    if (segs) {
-#pragma unroll
-        for (int k = 0; k < kQSub; ++k) {
-            cnt[k] = (int)min((int64_t)*rec_queue(a.queue, k), seg);
-            nrec += cnt[k];
-        }
-    } else
-        nrec = (int)min((int64_t)a.queue[2], a.mf_cap);
-    const int step = (gridDim.x * blockDim.x) >> 6;
-    int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    MfFlag f;
-    if (r < nrec) f = a.mf_list[mf_rec_index(cnt, segs, seg, r)];
-    for (; r < nrec; r += step) {
-        const MfFlag cur = f;
-        if (r + step < nrec) f = a.mf_list[mf_rec_index(cnt, segs, seg, r + step)];  // the next record in flight
-        // a record always names a unit of this launch; the checks only keep a corrupted list from
-        // addressing outside the problem set
-        if (cur.rec0 < 0 || cur.nh < 1 || cur.nh > 32 || cur.iters < 1 || cur.iters > 4 || cur.base < 0 ||
-            cur.n < cur.base || cur.rec0 / a.hyp_stride >= n_prob)
-            continue;
-        // window iterations are 256 points apart (k_pnp_score_mf: 4 waves x 64), or 64 apart
-        // (k_pnp_score_mw: bits 16.. of fl = 1)
-        const int stride = (cur.fl >> 16) ? 64 : 256;
-        for (int w = 0; w < cur.iters && cur.base + stride * w < cur.n; ++w)
-            mf_recount(a, cur, cur.base + stride * w, col, half, counts);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Wave-autonomous MFMA scoring kernel (variant 74): the arithmetic, operands, records and
-// flagged-window recount of k_pnp_score_mf, but every wave pulls its own work units (32
-// hypotheses x one cell of points) from the queue.  No block barrier anywhere: in the block form
-// the 4 waves of a block (on 4 SIMDs, each shared with other blocks' waves) met at 4-5 barriers
-// per unit, and each unit also waited on its queue atomic, its record staging and its record
-// append in turn (≈3 µs per unit, measured by the cell-count sweep).  Here the next unit's
-// atomic is issued when the current unit starts, the unit's A operands and slopes go straight
-// from the records into registers, its band constants b' into the wave's own LDS, and the
-// counts are transposed through the wave's LDS; a wave waiting on a load leaves its SIMD to the
-// other two waves.  An iteration covers 2 x 32 consecutive points (base, base + 32), so a
-// flagged window's iterations are 64 points apart (fl bit 16 tells k_pnp_mf_recount).
-// Units: tiles [0, ta) in cb cells of cbig points, then the remaining tiles in cs cells of
-// csmall points (the queue's tail).  Problems outside the f16 operand range (fconst[11] = 0)
-// are counted with the exact f64 test, one lane per point (never at C2-C5 scales).
-// ---------------------------------------------------------------------------
-constexpr int kMwWaves = 4;  // waves per block (blocks only group waves for the launch)
-
-// the wave's flagged windows (LDS, full records) to segment qk of a.mf_list (a.mf_cap / kQSub
-// records each): one atomic for the slots
-__device__ __forceinline__ void mw_flush(const PnpArgs &a, int qk, const MfFlag *lst, int nw, int lane) {
-    const int64_t seg = a.mf_cap / kQSub;
-    int slot = 0;
-    if (lane == 0) slot = atomicAdd(rec_queue(a.queue, qk), nw);
-    slot = __builtin_amdgcn_readfirstlane(slot);
-    if (lane < nw && slot + lane < seg) a.mf_list[qk * seg + slot + lane] = lst[lane];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();  // the list is rewritten after this
-}
-
-template <int CHK, int PD, int XP = 0>
-__device__ __forceinline__ void mw_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
-                                        int lane, int qk, uint32_t (*cw)[64], float (*bl)[2][16], MfFlag *lst,
-                                        int &nw, int32_t *__restrict__ counts) {
-    const int col = lane & 31, half = lane >> 5;
-    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-    const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
-    const uint4 *__restrict__ PF = a.PF + 2 * p0;
-    const float2 *__restrict__ UV = a.UV + p0;
-    const int iters = (n - start + 63) / 64;
-    const int full = (n - start) / 64;  // iterations with 64 points in range
-    // the unit's loads, issued together: A operands, a' / b', the first point operands
-    mf_h8 Ar[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) Ar[t] = mw_operand(recs, t, col, half, nh);
-    const int j = col;  // a' (lanes 0-31) and b' (lanes 32-63) of hypothesis j
-    float abv = gview(recs)[min(j, nh - 1) * kFModelStride + 12 + half];
-    mf_h8 Ba, Bb;
-    float2 ua, ub;
-    if (full > 0)
-        mf_load_full(PF, UV, start, col, half, Ba, Bb, ua, ub);
-    else
-        mf_load_part(PF, UV, start, n, col, half, Ba, Bb, ua, ub);
-    bl[half][j & 1][4 * (j >> 3) + ((j >> 1) & 3)] = j < nh ? abv : (half ? -__builtin_inff() : 0.f);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    uint32_t vc[4][4];
-    float tm[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            vc[t][g] = 0u;
-            tm[t][g] = __builtin_inff();
-        }
-    int it = 0;  // iterations in the current window
-    auto body = [&](int i, const mf_h8 &Ba, const mf_h8 &Bb, const float2 &ua, const float2 &ub)
-        __attribute__((always_inline)) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const float4 av = *reinterpret_cast<const float4 *>(&bl[0][half][4 * t]);
-            const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Ba, mf_f16v{}, 0, 0, 0);
-            const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Bb, mf_f16v{}, 0, 0, 0);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
-                const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
-                vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
-                tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
-            }
-        }
-        if (++it == CHK || i == iters - 1) {  // end of a check window (uniform)
-            uint32_t fl = 0;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float4 bv = *reinterpret_cast<const float4 *>(&bl[1][half][4 * t]);
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
-                    fl |= __ballot(!(tm[t][g] > bg)) ? (1u << (4 * t + g)) : 0u;
-                    tm[t][g] = __builtin_inff();
-                }
-            }
-            if (__builtin_expect(fl != 0, 0)) {
-                if (lane == 0)
-                    lst[nw] = MfFlag{rec0, p0, start + 64 * (i + 1 - it), n, fl | (1u << 16), (int16_t)nh, (int16_t)it};
-                if (++nw == kWrec) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    mw_flush(a, qk, lst, nw, lane);
-                    nw = 0;
-                }
-            }
-            it = 0;
-        }
-    };
-    if constexpr (PD == 0) {
-        for (int i = 0; i < full; ++i) {
-            if (i > 0) mf_load_full(PF, UV, start + 64 * i, col, half, Ba, Bb, ua, ub);
-            body(i, Ba, Bb, ua, ub);
-        }
-    } else {  // one iteration ahead
-        mf_h8 Na, Nb;
-        float2 na, nb;
-        for (int i = 0; i < full; ++i) {
-            if (i + 1 < full) mf_load_full(PF, UV, start + 64 * (i + 1), col, half, Na, Nb, na, nb);
-            body(i, Ba, Bb, ua, ub);
-            Ba = Na;
-            Bb = Nb;
-            ua = na;
-            ub = nb;
-        }
-    }
-    if (full < iters) {
-        if (full > 0) mf_load_part(PF, UV, start + 64 * full, n, col, half, Ba, Bb, ua, ub);
-        body(full, Ba, Bb, ua, ub);
-    }
-    // counts: lane (c, half) holds slot (t, g)'s count of hypothesis 8t + 2g + half over its
-    // points; transposed through the wave's LDS, lane pair (2j, 2j + 1) sums hypothesis j's 32
-    // columns (16 each, then one shuffle)
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) cw[4 * t + g][lane] = vc[t][g];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    {
-        const int jh = lane >> 1, p = lane & 1;
-        const int slot = 4 * (jh >> 3) + ((jh >> 1) & 3), c0 = (jh & 1) * 32 + 16 * p;
-        const uint4 *src = reinterpret_cast<const uint4 *>(&cw[slot][c0]);
-        uint32_t sum = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4 v = src[q];
-            sum += v.x + v.y + v.z + v.w;
-        }
-        sum += __shfl_xor(sum, 1);
-        if (XP & 2) {  // timing experiment: no count atomics
-            if (p == 0 && jh < nh && sum == 0xFFFFFFFFu) counts[rec0 + jh] = 0;
-        } else if (p == 0 && jh < nh && sum)
-            atomicAdd(&counts[rec0 + jh], (int)(sum / 255u));
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();  // cw and bl are rewritten by the next unit
-}
-
-// the exact f64 count of one unit, one lane per point (problems outside the f16 operand range)
-__device__ __forceinline__ void mw_exact_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start,
-                                              int n, int lane, int32_t *__restrict__ counts) {
-    const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-    const double *cm = a.cams + 4 * prob;
-    const Cam k{cm[0], cm[1], cm[2], cm[3]};
-    const float thr2 = a.thr2[prob];
-#pragma unroll 1
-    for (int j = 0; j < nh; ++j) {
-        const double *md = a.models + (rec0 + j) * kModelStride;
-        if (md[kValidSlot] == 0.0) continue;  // uniform
-        int c = 0;
-#pragma unroll 1
-        for (int i = start + lane; i < n; i += 64) {
-            const int64_t q = p0 + i;
-            c += pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <= thr2 ? 1 : 0;
-        }
-        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
-        if (lane == 0 && c) atomicAdd(&counts[rec0 + j], c);
-    }
-}
-
-// XP: timing experiments only (counts wrong): bit 0 static unit assignment (no queue atomics),
-// bit 1 no count atomics
-template <int CHK, int PD, int XP = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_pnp_score_mw(
-    PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
-    int ta, int cb, int cbig, int cs, int csmall) {
-    constexpr int HB = 32;
-    __shared__ __attribute__((aligned(16))) uint32_t cw[kMwWaves][16][64];
-    __shared__ __attribute__((aligned(16))) float bl[kMwWaves][2][2][16];  // a' / b' [half][slot]
-    __shared__ MfFlag lst[kMwWaves][kWrec];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int tpp = (H + HB - 1) / HB;
-    const int tiles = tpp * n_prob;
-    const int ua = ta * cb;
-    const int n_units = ua + (tiles - ta) * cs;
-    int nw = 0;  // the wave's flagged windows not yet appended to a.mf_list
-    // this block's share of the units: u = qk + kQSub i, i drawn from counter qk
-    const int qk = blockIdx.x % kQSub;
-    const int nq = n_units > qk ? (n_units - qk + kQSub - 1) / kQSub : 0;
-    int *const uq = unit_queue(queue, qk);
-    int ci = 0;
-    const int gw = blockIdx.x / kQSub * kMwWaves + wave;                              // XP & 1: static
-    const int nwq = ((int)gridDim.x - qk + kQSub - 1) / kQSub * kMwWaves;           // waves sharing qk
-    if (XP & 1)
-        ci = gw;
-    else {
-        if (lane == 0) ci = atomicAdd(uq, 1);
-        ci = __builtin_amdgcn_readfirstlane(ci);
-    }
-    int last_prob = -1, n_all = 0;
-    int64_t p0 = 0;
-    bool in_range = false;
-    while (ci < nq) {  // uniform per wave: every wave reaches the end of its queue
-        const int cur = qk + kQSub * ci;
-
-        int tile, start, len;
-        if (cur < ua) {
-            tile = cur / cb;
-            start = (cur % cb) * cbig;
-            len = cbig;
-        } else {
-            tile = ta + (cur - ua) / cs;
-            start = ((cur - ua) % cs) * csmall;
-            len = csmall;
-        }
-        const int prob = tile / tpp;
-        const int64_t h0 = hyp_begin + (int64_t)(tile % tpp) * HB;
-        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
-        if (prob != last_prob) {  // uniform; once per call for one problem
-            p0 = a.offsets[prob];
-            n_all = (int)(a.offsets[prob + 1] - p0);
-            in_range = a.fconst[(int64_t)prob * kFconstStride + 11] != 0.f;
-            last_prob = prob;
-        }
-        const int n = min(n_all, start + len);
-        if (start < n_all) {  // else a cell past a short problem of a batch
-            if (in_range)
-                mw_unit<CHK, PD, XP>(a, prob, h0, nh, p0, start, n, lane, qk, cw[wave], bl[wave], lst[wave], nw,
-                                     counts);
-            else
-                mw_exact_unit(a, prob, h0, nh, p0, start, n, lane, counts);
-        }
-        int nx = ci + nwq;  // XP & 1: static assignment
-        if (!(XP & 1)) {
-            if (lane == 0) nx = atomicAdd(uq, 1);
-            nx = __builtin_amdgcn_readfirstlane(nx);
-        }
-        ci = nx;
-    }
-    if (nw) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        mw_flush(a, qk, lst[wave], nw, lane);
-    }
-}
-
-// Packed variant of k_pnp_score_f32: the same arithmetic, bit for bit, on two
-// points per instruction (v_pk_fma_f32 / v_pk_mul_f32: two f32 lanes per VGPR
-// pair).  Each lane holds P points as P/2 pairs.
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 bc(float v) { return f2{v, v}; }
-
-template <int P, int HB>
-__global__ __launch_bounds__(256) void k_pnp_score_pk(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
-                                                      int *__restrict__ queue, int32_t *__restrict__ counts) {
-    static_assert(HB <= 64 && P % 2 == 0, "tiling");
-    constexpr int Q = P / 2;
-    __shared__ int red[4][HB];
-    __shared__ int unit_s;
-    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int units_per_prob = (H + HB - 1) / HB;
-    const int n_units = units_per_prob * n_prob;
-    for (;;) {
-        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
-        __syncthreads();
-        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
-        if (unit >= n_units) break;
-        const int prob = unit / units_per_prob;
-        const int64_t h0 = hyp_begin + (int64_t)(unit % units_per_prob) * HB;
-        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
-        const int64_t p0 = a.offsets[prob];
-        const int n = (int)(a.offsets[prob + 1] - p0);
-        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
-        const float cx = fc[2], cy = fc[3], T = fc[4], sqT2 = fc[5], Trel = fc[6], Cmax = fc[7];
-        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-        {
-            const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
-            for (int q = threadIdx.x; q < HB * kFModelStride; q += 256)
-                mlds[q] = q < nh * kFModelStride ? fmb[q] : -1.f;
-        }
-        __syncthreads();
-        const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
-        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
-
-        int cnt = 0;
-        for (int base = wave * 64 * P; base < n; base += 4 * 64 * P) {
-            f2 px[Q], py[Q], pz[Q], pu[Q], pv[Q];
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-                const int i = base + j * 64 + lane;
-                const bool in = i < n;
-                const int ii = in ? i : 0;
-                const float u = in ? U[ii] - cx : 3.0e38f, v = in ? V[ii] - cy : 3.0e38f;
-                if (j < Q) {
-                    px[j].x = XC[ii]; py[j].x = YC[ii]; pz[j].x = ZC[ii]; pu[j].x = u; pv[j].x = v;
-                } else {
-                    px[j - Q].y = XC[ii]; py[j - Q].y = YC[ii]; pz[j - Q].y = ZC[ii]; pu[j - Q].y = u;
-                    pv[j - Q].y = v;
-                }
-            }
-            for (int h = 0; h < nh; ++h) {
-                const float4 *m4 = reinterpret_cast<const float4 *>(mlds + h * kFModelStride);
-                const float4 ma = m4[0], mb = m4[1], mc = m4[2], md4 = m4[3];
-                const float zg = md4.z;
-                if (zg < 0.f) continue;
-                int cc = 0;
-                uint64_t und = 0;
-#pragma unroll
-                for (int j = 0; j < Q; ++j) {
-                    const f2 xs = pfma(bc(ma.x), px[j], pfma(bc(ma.y), py[j], pfma(bc(ma.z), pz[j], bc(mc.y))));
-                    const f2 ys = pfma(bc(ma.w), px[j], pfma(bc(mb.x), py[j], pfma(bc(mb.y), pz[j], bc(mc.z))));
-                    const f2 z = pfma(bc(mb.z), px[j], pfma(bc(mb.w), py[j], pfma(bc(mc.x), pz[j], bc(mc.w))));
-                    const f2 q1 = pfma(pu[j], z, xs);
-                    const f2 q2 = pfma(pv[j], z, ys);
-                    const f2 z2 = z * z;
-                    const f2 diff = pfma(bc(-T), z2, pfma(q1, q1, q2 * q2));
-                    const f2 az = f2{__builtin_fabsf(z.x), __builtin_fabsf(z.y)};
-                    const f2 Dz = pfma(bc(Cmax), az, bc(md4.x));
-                    const f2 Mz = pfma(pfma(bc(sqT2), az, Dz), Dz, bc(Trel) * z2);
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const float d = hh ? diff.y : diff.x, mzv = hh ? Mz.y : Mz.x, azv = hh ? az.y : az.x;
-                        const uint64_t mz = __ballot(azv > zg);
-                        const uint64_t mi = __ballot(d < -mzv);
-                        const uint64_t mo = __ballot(d > mzv);
-                        cc += __popcll(mi & mz);
-                        und |= ~((mi | mo) & mz);
-                    }
-                }
-                if (und) {
-                    const double *md = a.models + (rec0 + h) * kModelStride;
-                    const double *cm = a.cams + 4 * prob;
-                    const Cam k{cm[0], cm[1], cm[2], cm[3]};
-                    const float thr2 = a.thr2[prob];
-                    cc = 0;
-#pragma unroll 1
-                    for (int j = 0; j < P; ++j) {
-                        const int i = base + j * 64 + lane;
-                        bool ex = false;
-                        if (i < n) {
-                            const int64_t q = p0 + i;
-                            ex = pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q],
-                                         a.V[q]) <= thr2;
-                        }
-                        cc += __popcll(__ballot(ex));
-                    }
-                }
-                cnt += (lane == h) ? cc : 0;
-            }
-        }
-        if (lane < HB) red[wave][lane] = cnt;
-        __syncthreads();
-        if (wave == 0) pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
-        __syncthreads();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// PnP scoring on the matrix cores.  The camera-frame coordinates of 4
-// hypotheses x 16 points are one v_mfma_f32_16x16x4_f32:
-//   A (16 x 4): rows 4g + i (hypothesis g of the set, i = xs, ys, z, pad),
-//               columns the scaled rotation coefficients of X, Y, Z (4th = 0)
-//   B (4 x 16): X, Y, Z, 0 of 16 centred points        (one VGPR per lane)
-//   C (16 x 16): the translations t' (row i of hypothesis g)
-// so lane l receives xs, ys, z of hypothesis l >> 4 and point l & 15, as an
-// exact f32 fma chain (cdna_hip_programming.md §3), inside the same error
-// bound as the VALU kernels.  The VALU then forms
-//   E = (uc z + xs)^2 + (vc z + ys)^2                 (= z^2 e')
-// and decides E < (T - alpha) z^2 - beta (inlier) or E > (T + alpha) z^2 + beta
-// (outlier), alpha z^2 + beta >= Mz of k_pnp_score_f32; everything else goes
-// to the exact f64 error, lane by lane.  Matrix and vector pipes run side by
-// side.  Counts are bit-identical to the exact kernel.
-// ---------------------------------------------------------------------------
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-template <int HB, int TC>
-__global__ __launch_bounds__(256) void k_pnp_score_mfma(PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob,
-                                                        int *__restrict__ queue, int32_t *__restrict__ counts) {
-    static_assert(HB % 4 == 0 && HB <= 64, "sets of 4 hypotheses");
-    constexpr int S = HB / 4;
-    __shared__ int red[4][HB];
-    __shared__ int unit_s;
-    __shared__ __attribute__((aligned(16))) float mlds[HB * kFModelStride];
-    __shared__ int xcnt[HB];  // inliers found by the exact fallback
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int g = lane >> 4, col = lane & 15;
-    if (threadIdx.x < HB) xcnt[threadIdx.x] = 0;
-    const int units_per_prob = (H + HB - 1) / HB;
-    const int n_units = units_per_prob * n_prob;
-    for (;;) {
-        if (threadIdx.x == 0) unit_s = atomicAdd(queue, 1);
-        __syncthreads();
-        const int unit = __builtin_amdgcn_readfirstlane(unit_s);
-        if (unit >= n_units) break;  // uniform: every wave of every block reaches it
-        const int prob = unit / units_per_prob;
-        const int64_t h0 = hyp_begin + (int64_t)(unit % units_per_prob) * HB;
-        const int nh = (int)min((int64_t)HB, hyp_begin + H - h0);
-        const int64_t p0 = a.offsets[prob];
-        const int n = (int)(a.offsets[prob + 1] - p0);
-        const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
-        const float cx = fc[2], cy = fc[3], T = fc[4];
-        const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
-        {
-            const float *__restrict__ fmb = a.fmodels + rec0 * kFModelStride;
-            for (int q = threadIdx.x; q < HB * kFModelStride; q += 256) {
-                const int hq = q / kFModelStride, fq = q % kFModelStride;
-                mlds[q] = hq < nh ? fmb[q] : (fq == 14 ? -1.f : 0.f);
-            }
-        }
-        __syncthreads();
-        // per set s: the A operand, the C operand and the decision constants of
-        // hypothesis 4s + g (this lane's output rows)
-        float Aop[S], tlo[S], thi[S], bet[S], zgs[S];
-        f32x4 Cop[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const float *ma = mlds + (4 * s + (col >> 2)) * kFModelStride;
-            const int i = col & 3;
-            Aop[s] = (i < 3 && g < 3) ? ma[3 * i + g] : 0.f;
-            const float *mc = mlds + (4 * s + g) * kFModelStride;
-            const bool valid = mc[14] >= 0.f;
-            // an absent/invalid hypothesis (zero record): z = 1, thresholds -inf, so
-            // every pair is a decided outlier
-            Cop[s] = valid ? f32x4{mc[9], mc[10], mc[11], 0.f} : f32x4{0.f, 0.f, 1.f, 0.f};
-            tlo[s] = valid ? T - mc[15] : -__builtin_inff();
-            thi[s] = valid ? T + mc[15] : -__builtin_inff();
-            bet[s] = valid ? mc[13] : 0.f;
-            zgs[s] = valid ? mc[14] : -1.f;
-        }
-        const float *__restrict__ Pk = g == 0 ? a.XC + p0 : g == 1 ? a.YC + p0 : a.ZC + p0;
-        const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
-
-        int cnt[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) cnt[s] = 0;
-        for (int base = wave * 16 * TC; base < n; base += 4 * 16 * TC) {
-            static_assert(S * TC <= 32, "undecided bits");
-            uint32_t und = 0;
-            float Bop[TC], uc[TC], vc[TC];
-#pragma unroll
-            for (int t = 0; t < TC; ++t) {
-                const int pt = base + t * 16 + col;
-                const bool in = pt < n;
-                const int pp = in ? pt : 0;
-                const float b = Pk[pp];
-                Bop[t] = (in && g < 3) ? b : 0.f;
-                // out-of-range points: a pixel at 3e38 makes every pair a decided outlier
-                uc[t] = in ? U[pp] - cx : 3.0e38f;
-                vc[t] = in ? V[pp] - cy : 3.0e38f;
-            }
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-#pragma unroll
-                for (int t = 0; t < TC; ++t) {
-                    const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(Aop[s], Bop[t], Cop[s], 0, 0, 0);
-                    const float z = d[2];
-                    const float q1 = __builtin_fmaf(uc[t], z, d[0]);
-                    const float q2 = __builtin_fmaf(vc[t], z, d[1]);
-                    const float z2 = z * z;
-                    const float E = __builtin_fmaf(q1, q1, q2 * q2);
-                    const float lo = __builtin_fmaf(tlo[s], z2, -bet[s]);
-                    const float hi = __builtin_fmaf(thi[s], z2, bet[s]);
-                    // a NaN anywhere leaves the pair undecided (and not a decided inlier)
-                    const bool zok = __builtin_fabsf(z) > zgs[s];
-                    cnt[s] += (zok && E < lo) ? 1 : 0;
-                    const bool dec = zok && (E < lo || E > hi);
-                    und |= dec ? 0u : (1u << (s * TC + t));
-                }
-            }
-            if (__ballot(und != 0)) {
-                // rare: the exact f64 error (pnp_err, the oracle's formula) of the
-                // undecided pairs, one rolled loop for all of them
-                const double *cm = a.cams + 4 * prob;
-                const Cam k{cm[0], cm[1], cm[2], cm[3]};
-#pragma unroll 1
-                while (und) {
-                    const int b = __builtin_ctz(und);
-                    und &= und - 1;
-                    const int hs = 4 * (b / TC) + g;
-                    const int pt = base + (b % TC) * 16 + col;
-                    if (pt < n && hs < nh) {
-                        const double *md = a.models + (rec0 + hs) * kModelStride;
-                        const int64_t q = p0 + pt;
-                        if (md[kValidSlot] != 0.0 &&
-                            pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <=
-                                a.thr2[prob])
-                            atomicAdd(&xcnt[hs], 1);
-                    }
-                }
-            }
-        }
-        // counts of hypothesis 4s + g: sum over the 16 lanes of group g, then over waves
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            int v = cnt[s];
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
-            v += __shfl_xor(v, 8);
-            if (col == 0) red[wave][4 * s + g] = v;
-        }
-        __syncthreads();  // also orders every wave's fallback atomics before xcnt is read
-        if (wave == 0) {
-            if (lane < HB) {
-                red[0][lane] += xcnt[lane];
-                xcnt[lane] = 0;
-            }
-            pnp_score_epilogue<HB>(a, red, prob, h0, nh, lane, counts);
-        }
-        __syncthreads();  // red, mlds and unit_s are rewritten by the next unit
+        __syncthreads();  // the unit's LDS and the slot are rewritten by the next unit
     }
 }
 
@@ -3463,17 +1989,9 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
     return hipGetLastError();
 }
 
-// RSAC_SOLVE4_MAX: the largest round (problems x hypotheses) solved 4 lanes per hypothesis
-static int64_t solve4_max_hyps() {
-    static const int64_t v = [] { const char *e = getenv("RSAC_SOLVE4_MAX"); return e ? atoll(e) : 4096; }();
-    return v;
-}
-// RSAC_SOLVE2_MAX: rounds up to this many hypotheses (above solve4_max_hyps) solve on two lanes
-// per hypothesis (k_pnp_solve2), larger ones on one
-static int64_t solve2_max_hyps() {
-    static const int64_t v = [] { const char *e = getenv("RSAC_SOLVE2_MAX"); return e ? atoll(e) : 0; }();
-    return v;
-}
+// rounds of at most this many hypotheses (problems x hypotheses) are solved 4 lanes per
+// hypothesis (k_pnp_solve4); larger ones one lane per hypothesis (k_pnp_solve)
+constexpr int64_t kSolve4MaxHyps = 4096;
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
                             double *frame, float *fconst, hipStream_t s, const PnpPrepare *prep) {
@@ -3516,12 +2034,13 @@ hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t 
     return hipGetLastError();
 }
 
-static int64_t small_round_tiles();
+// a round of at most kSmallRoundTiles hypothesis tiles (an adaptive run's first 256
+// hypotheses) is scored by the scaled-form small-round instance (2 points per lane, so the cells
+// fill the GPU); its records are written in form 1 (the solve and the scoring launch apply the
+// same rule)
+constexpr int64_t kSmallRoundTiles = 16;
 
-// a round of at most small_round_tiles() hypothesis tiles (an adaptive run's first 256) is
-// scored by the scaled-form small-round instance even under the MFMA variants: the records of
-// such a round are written in form 1 (the solve and the scoring launch apply the same rule)
-static bool small_round(int32_t P, int32_t H) { return (int64_t)P * ((H + 31) / 32) <= small_round_tiles(); }
+static bool small_round(int32_t P, int32_t H) { return (int64_t)P * ((H + 31) / 32) <= kSmallRoundTiles; }
 static PnpArgs round_args(const PnpArgs &a, int32_t P, int32_t H) {
     PnpArgs ka = a;
     if (ka.fform == 2 && small_round(P, H)) ka.fform = 1;
@@ -3535,347 +2054,104 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
 
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
-    // RSAC_DBG_SOLVE_NO_RECORDS: timing experiment only (the scoring records go stale)
-    static const bool no_rec = getenv("RSAC_DBG_SOLVE_NO_RECORDS") != nullptr;
-    if (no_rec) ka.fmodels = nullptr;
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
-    if ((int64_t)P * H <= solve4_max_hyps())
+    if ((int64_t)P * H <= kSolve4MaxHyps)
         hipLaunchKernelGGL(k_pnp_solve4, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-    else if ((int64_t)P * H <= solve2_max_hyps())
-        hipLaunchKernelGGL(k_pnp_solve2, dim3(cdiv(2 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     else
         hipLaunchKernelGGL(k_pnp_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     return hipGetLastError();
 }
 
-// zero every counter of the PnP scoring launch (the solve kernel does it too; this is for a
-// scoring launch whose solve ran on another stream and could not)
-hipError_t reset_pnp_queue_async(int *queue, hipStream_t s) {
-    return hipMemsetAsync(queue, 0, kQWords * sizeof(int), s);
+// blocks of `kern` (256 threads) the whole GPU keeps resident
+template <class Kern>
+static int resident_blocks(Kern kern) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
+    return std::max(1, cus) * std::max(1, per_cu);
 }
 
-static int64_t env_i64(const char *name, int64_t dflt) {
-    const char *e = getenv(name);
-    return e ? atoll(e) : dflt;
+// grid of a split-queue launch (block b takes the units = b mod kQSub): enough blocks for every
+// residue class that has units, else at most the resident blocks
+static unsigned queue_grid(int64_t units, int resident) {
+    const int64_t g = std::max<int64_t>(std::min<int64_t>(units, resident), std::min<int64_t>(units, kQSub));
+    return (unsigned)std::max<int64_t>(1, g);
 }
 
-// scoring-kernel variants (points per lane, hypotheses per block); 0 = default
-static const int64_t g_sc_cell_tiles = [] { const char *e = getenv("RSAC_SC_CELL_TILES"); return e ? atoll(e) : 0; }();
-constexpr int kDefaultScoreVariant = 98;  // fastest measured on MI355X
-static int g_score_variant = kDefaultScoreVariant;
-void set_score_variant(int v) { g_score_variant = v < 0 ? kDefaultScoreVariant : v; }
-
-// KIND 0 VALU f32, 1 packed f32, 2 MFMA (PP = point chunks of 16), 3 alpha-beta (W waves/SIMD);
-// alpha-beta only: NZ no depth guard, BAL balanced point split (~8 units per resident block, the
-// best key then reduced by k_best_key after the scoring launch)
-template <int PP, int HB, int KIND = 0, int W = 4, bool NZ = false, bool BAL = false>
-static void launch_f32(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
-    auto kern = [] {
-        if constexpr (KIND == 4) return k_pnp_score_ab<PP, HB, W, true, true>;
-        else if constexpr (KIND == 3) return k_pnp_score_ab<PP, HB, W, NZ>;
-        else if constexpr (KIND == 2) return k_pnp_score_mfma<HB, PP>;
-        else if constexpr (KIND == 1) return k_pnp_score_pk<PP, HB>;
-        else return k_pnp_score_f32<PP, HB>;
-    }();
-    static int resident = 0;  // blocks the whole GPU keeps resident for this instantiation
-    if (resident == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
-        resident = std::max(1, cus) * std::max(1, per_cu);
-    }
-    int64_t units = (int64_t)P * ((H + HB - 1) / HB);
-    if constexpr (KIND >= 3) {
-        // few tiles and no fused best key: split the points too (counts accumulate atomically)
-        int split = 1;
-        const int64_t chunks = std::max<int64_t>(1, ((int64_t)a.max_n + 4 * 64 * PP - 1) / (4 * 64 * PP));
-        if (BAL && (!a.best_key || P == 1))
-            split = (int)std::min<int64_t>(chunks, std::max<int64_t>(1, (8 * (int64_t)resident + units - 1) / units));
-        else if (!a.best_key && units * 2 <= resident)
-            split = (int)std::min<int64_t>(chunks, (resident + units - 1) / units);
-        // counts already zeroed by the solve kernel (a.counts_out set): no memset.  The best key
-        // is reduced afterwards by k_best_key (a completion counter per tile would need a fence
-        // per unit, which costs more than the launch)
-        const bool zeroed = a.counts_out == counts;
-        if (split > 1 && !zeroed) {
-            if (P == 1)
-                (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
-            else
-                (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P,
-                                       s);
-        }
-        units *= split;
-        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
-        PnpArgs ka = a;
-        if (split > 1) ka.best_key = nullptr;  // reduced below from the complete counts
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin, H, P, a.queue, counts, split);
-        if (split > 1 && a.best_key) {
-            unsigned g = cdiv(H, 1024);
-            if (g > 128) g = 128;
-            hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
-                               a.rng_base + hyp_begin, a.best_key);
-        }
-    } else {
-        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, a.queue, counts);
-    }
+static void zero_counts(int32_t *counts, int64_t hyp_begin, int32_t H, int32_t P, int64_t stride, hipStream_t s) {
+    if (P == 1)
+        (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
+    else
+        (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * stride, 0, sizeof(int32_t) * H, P, s);
 }
 
-int score_record_form() {
-    if (g_score_variant >= 60 && g_score_variant <= 99) return 2;
-    return g_score_variant >= 49 && g_score_variant <= 53 ? 1 : 0;
+static void launch_best_key_of(const PnpArgs &a, int64_t hyp_begin, int32_t H, const int32_t *counts, hipStream_t s) {
+    unsigned g = cdiv(H, 1024);
+    if (g > 128) g = 128;
+    hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
+                       a.rng_base + hyp_begin, a.best_key);
 }
 
-// k_pnp_score_sc: whole-tile units for all but the last `resident` tiles, which go as one unit
-// per cell (64 x 4 x P points): the cells even out the blocks' finishing times (the queue's
-// tail is one cell, against a whole split unit before).  Counts are zeroed (by the solve kernel,
-// else here) and added atomically; the best key is reduced afterwards.
-template <int P, int W, bool CB = false>
+hipError_t launch_pnp_best_key(const PnpArgs &a, int64_t hyp_begin, int32_t H, const int32_t *counts, hipStream_t s) {
+    if (a.best_key) launch_best_key_of(a, hyp_begin, H, counts, s);
+    return hipGetLastError();
+}
+
+// k_pnp_score_sc (small rounds, form-1 records): whole-tile units for all but the last
+// `resident` tiles, which go as one unit per cell (64 x 4 x P points): the cells even out the
+// blocks' finishing times.  Counts are zeroed (by the solve kernel, else here) and added
+// atomically; the best key is reduced afterwards.
+template <int P, int W>
 static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
-    auto kern = k_pnp_score_sc<P, 32, W, CB>;
-    static int resident = 0;
-    if (resident == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
-        resident = std::max(1, cus) * std::max(1, per_cu);
-    }
+    auto kern = k_pnp_score_sc<P, 32, W>;
+    static const int resident = resident_blocks(kern);
     const int64_t cells = std::max<int64_t>(1, ((int64_t)a.max_n + 256 * P - 1) / (256 * P));
     const int64_t tiles = (int64_t)P_ * ((H + 31) / 32);
-    const int64_t cell_tiles = std::min<int64_t>(tiles, g_sc_cell_tiles > 0 ? g_sc_cell_tiles : resident);
+    const int64_t cell_tiles = std::min<int64_t>(tiles, resident);
     const int64_t tb = tiles - cell_tiles;
     const int64_t units = tb + cell_tiles * cells;
-    if (a.counts_out != counts) {
-        if (P_ == 1)
-            (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
-        else
-            (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P_, s);
-    }
+    if (a.counts_out != counts) zero_counts(counts, hyp_begin, H, P_, a.hyp_stride, s);
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
     PnpArgs ka = a;
     ka.best_key = nullptr;  // reduced below from the complete counts
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin, H, P_, a.queue, counts, (int)tb,
                        (int)cells);
-    if (a.best_key) {
-        unsigned g = cdiv(H, 1024);
-        if (g > 128) g = 128;
-        hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
-                           a.rng_base + hyp_begin, a.best_key);
-    }
+    if (a.best_key) launch_best_key_of(a, hyp_begin, H, counts, s);
 }
 
 // k_pnp_score_mf: whole-tile units, then one unit per cell for the last `resident` tiles (as
 // launch_sc); cells of 2048 points, halved (down to 256, one iteration per wave) while the units
-// would not fill the resident grid (an adaptive run's first rounds).  Every wave-iteration
-// appends at most one flagged record, so a launch whose bound exceeds a.mf_cap is split into
-// hypothesis chunks (counters reset before each).
-template <bool FB, int CHK, int W = 4, int PD = 0, bool RA = false, bool PIPE = false, bool TM = false,
-          bool DYN = false, bool INL = false, int PRIO = 0>
+// would not fill the resident grid (an adaptive run's first rounds).  A wave lists at most kWrec
+// flagged iterations per unit, so problems longer than 256 kWrec points run every tile by cells
+// (of up to that length; shorter while the units would not give each resident block four).
+// Returns hipErrorInvalidValue only for launches past the int32 unit space.
 static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    auto kern = k_pnp_score_mf<FB, CHK, W, PD, RA, PIPE, TM, DYN, INL, PRIO>;
-    if (TM) {
-        unsigned long long z[8] = {};
-        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mf_timing), z, sizeof z, 0, hipMemcpyHostToDevice, s);
-    }
-    static int resident = 0;
-    if (resident == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
-        resident = std::max(1, cus) * std::max(1, per_cu);
-    }
-    if (a.counts_out != counts) {
-        if (P_ == 1)
-            (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
-        else
-            (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P_, s);
-    }
+    static const int resident = resident_blocks(k_pnp_score_mf);
+    if (a.counts_out != counts) zero_counts(counts, hyp_begin, H, P_, a.hyp_stride, s);
     const int64_t max_n = std::max<int64_t>(1, a.max_n);
-    // fused best key (RSAC_FUSE_KEY=1; INL, one problem, every tile a whole-problem unit, at
-    // least one tile per resident block): the kernel reduces the key from its final counts, no
-    // k_best_key launch.  Off by default: without the tail's cells the C2 step is 4 % slower
-    // (0.312 vs 0.298 ms, scripts/fuse_key_ab.sh) than with them and the separate launch.
-    static const bool fuse_env = [] { const char *e = getenv("RSAC_FUSE_KEY"); return e && atoi(e) != 0; }();
-    const bool fuse = INL && fuse_env && a.best_key && P_ == 1 && max_n <= 256 * CHK * kWrec &&
-                      (int64_t)((H + 31) / 32) >= resident;
-    auto plan = [&](int64_t Hc, int64_t &cell_pts, int64_t &cells, int64_t &tb, int64_t &units, int64_t &bound) {
-        const int64_t tiles = (int64_t)P_ * ((Hc + 31) / 32);
-        static const int64_t cell0 = std::max<int64_t>(256, env_i64("RSAC_MF_CELL_PTS", 2048) / 256 * 256);
-        cell_pts = cell0;
-        while (cell_pts > 256 && tiles * ((max_n + cell_pts - 1) / cell_pts) < resident) cell_pts /= 2;
-        int64_t cell_tiles = std::min<int64_t>(tiles, g_sc_cell_tiles > 0 ? g_sc_cell_tiles : resident);
-        if (fuse) cell_tiles = 0;
-        // INL: a wave lists at most kWrec windows per unit, so problems longer than that many
-        // windows run every tile by cells (of up to that length; shorter while the units would
-        // not give each resident block four)
-        constexpr int64_t win_pts = 256 * CHK * kWrec;
-        if (INL && max_n > win_pts) {
-            int64_t cp = win_pts;
-            while (cp > cell_pts && tiles * ((max_n + cp - 1) / cp) < 4 * resident) cp /= 2;
-            cell_pts = cp;
-            cell_tiles = tiles;
-        }
-        cells = (max_n + cell_pts - 1) / cell_pts;
-        tb = tiles - cell_tiles;
-        units = tb + cell_tiles * cells;
-        bound = tb * ((max_n + 63) / 64 + 3) + cell_tiles * cells * ((cell_pts + 63) / 64 + 3);
-    };
-    int64_t cell_pts, cells, tb, units, bound;
-    plan(H, cell_pts, cells, tb, units, bound);
-    int64_t Hc = H;
-    // a block's records go to segment blockIdx % kQSub of a.mf_list: bound each by its share
-    const int64_t seg = a.mf_cap / kQSub;
-    if (FB && (bound + kQSub - 1) / kQSub + 2 * ((max_n + 63) / 64 + 3) > seg) {
-        const int64_t per_tile = (int64_t)P_ * std::max<int64_t>((max_n + 63) / 64 + 3, cells * ((256 + 63) / 64 + 3) +
-                                                                                           (max_n + 63) / 64);
-        const int64_t tiles_c = seg / std::max<int64_t>(1, per_tile);
-        if (tiles_c < 1) return hipErrorOutOfMemory;  // one 32-hypothesis tile per problem exceeds the list
-        Hc = 32 * tiles_c;
+    const int64_t tiles = (int64_t)P_ * ((H + 31) / 32);
+    int64_t cell_pts = 2048;
+    while (cell_pts > 256 && tiles * ((max_n + cell_pts - 1) / cell_pts) < resident) cell_pts /= 2;
+    int64_t cell_tiles = std::min<int64_t>(tiles, resident);
+    constexpr int64_t win_pts = 256 * kWrec;
+    if (max_n > win_pts) {
+        int64_t cp = win_pts;
+        while (cp > cell_pts && tiles * ((max_n + cp - 1) / cp) < 4 * resident) cp /= 2;
+        cell_pts = cp;
+        cell_tiles = tiles;
     }
-    PnpArgs ka = a;
-    if (!fuse) ka.best_key = nullptr;  // reduced below from the complete counts
-    for (int64_t h = 0; h < H; h += Hc) {
-        const int32_t Hh = (int32_t)std::min<int64_t>(Hc, H - h);
-        if (Hc < H) {
-            plan(Hh, cell_pts, cells, tb, units, bound);
-            hipError_t e = hipMemsetAsync(a.queue + 32, 0, (kQWords - 32) * sizeof(int), s);
-            if (e != hipSuccess) return e;
-        }
-        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, a.queue, counts, (int)tb,
-                           (int)cells, (int)cell_pts);
-        if (FB) {
-            static const bool dbg = getenv("RSAC_DBG_MF") != nullptr;  // diagnostics: flagged records per launch
-            if (dbg) {
-                int q[kQWords];
-                (void)hipMemcpyAsync(q, a.queue, sizeof q, hipMemcpyDeviceToHost, s);
-                (void)hipStreamSynchronize(s);
-                q[2] = 0;
-                for (int k = 0; k < kQSub; ++k) q[2] += q[32 + 32 * kQSub + 32 * k];
-                fprintf(stderr, "rsac mf: units %lld records %d of bound %lld (H %d, cells %lld x %lld)\n",
-                        (long long)units, q[2], (long long)bound, Hh, (long long)cells, (long long)cell_pts);
-            }
-            // one wave per record, records latency-bound (a chain of dependent loads): a wide grid
-            // (blocks past the record count exit at once)
-            if (!INL)
-                hipLaunchKernelGGL(k_pnp_mf_recount, dim3(2048), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, counts,
-                                   kQSub, 0, 0);
-        }
-    }
-    if (a.best_key && !fuse) {
-        unsigned g = cdiv(H, 1024);
-        if (g > 128) g = 128;
-        hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
-                           a.rng_base + hyp_begin, a.best_key);
-    }
-    return hipGetLastError();
-}
-
-// k_pnp_score_mw: units of 32 hypotheses x a cell, big cells (cbig points) for all but the last
-// `tail` tiles, small cells (csmall) for those, so the queue ends on short units.  Cells halve
-// (down to 64 points) while the units would not give every resident wave work (an adaptive run's
-// first rounds).  A unit appends at most one flagged record per iteration, so a launch whose
-// bound exceeds a.mf_cap is split into hypothesis chunks (counters reset before each).
-// RSAC_MW_BIG / RSAC_MW_SMALL / RSAC_MW_TAIL: tuning knobs (points, points, tiles).
-template <int CHK, int PD, int XP = 0>
-static hipError_t launch_mw(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
-                            hipStream_t s) {
-    auto kern = k_pnp_score_mw<CHK, PD, XP>;
-    static int resident = 0;  // resident blocks of 4 waves
-    if (resident == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
-        resident = std::max(1, cus) * std::max(1, per_cu);
-    }
-    static const int64_t big0 = std::max<int64_t>(64, env_i64("RSAC_MW_BIG", 2048) / 64 * 64);
-    static const int64_t small0 = std::max<int64_t>(64, env_i64("RSAC_MW_SMALL", 512) / 64 * 64);
-    static const int64_t tail0 = env_i64("RSAC_MW_TAIL", -1);
-    if (a.counts_out != counts) {
-        if (P_ == 1)
-            (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
-        else
-            (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P_, s);
-    }
-    const int64_t max_n = std::max<int64_t>(1, a.max_n);
-    const int64_t waves = 4 * (int64_t)resident;
-    struct Plan {
-        int64_t ta, cb, cbig, cs, csmall, units, bound;
-    };
-    auto plan = [&](int64_t Hc) {
-        Plan p;
-        const int64_t tiles = (int64_t)P_ * ((Hc + 31) / 32);
-        p.cbig = std::min<int64_t>(big0, (max_n + 63) / 64 * 64);
-        while (p.cbig > 64 && tiles * ((max_n + p.cbig - 1) / p.cbig) < waves) p.cbig /= 2;
-        p.csmall = std::min(p.cbig, small0);
-        p.cb = (max_n + p.cbig - 1) / p.cbig;
-        p.cs = (max_n + p.csmall - 1) / p.csmall;
-        const int64_t tail = std::min<int64_t>(tiles, tail0 >= 0 ? tail0 : waves / 8);
-        p.ta = tiles - tail;
-        p.units = p.ta * p.cb + tail * p.cs;
-        p.bound = p.ta * p.cb * ((p.cbig + 63) / 64) + tail * p.cs * ((p.csmall + 63) / 64);
-        return p;
-    };
-    Plan pl = plan(H);
-    int64_t Hc = H;
-    // a block's records go to segment blockIdx % kQSub: bound each segment by its units' share
-    const int64_t seg = a.mf_cap / kQSub;
-    auto seg_bound = [&](const Plan &p) { return (p.bound + kQSub - 1) / kQSub + 2 * ((std::max(p.cbig, p.csmall) + 63) / 64); };
-    if (seg_bound(pl) > seg) {
-        const int64_t per_tile = (int64_t)P_ * std::max(pl.cb * ((pl.cbig + 63) / 64), pl.cs * ((pl.csmall + 63) / 64));
-        const int64_t tiles_c = seg / std::max<int64_t>(1, per_tile);
-        if (tiles_c < 1) return hipErrorOutOfMemory;  // one 32-hypothesis tile per problem exceeds the list
-        Hc = 32 * tiles_c;
-    }
+    const int64_t cells = (max_n + cell_pts - 1) / cell_pts;
+    const int64_t tb = tiles - cell_tiles;
+    const int64_t units = tb + cell_tiles * cells;
+    if (units + kQSub * (int64_t)resident > INT32_MAX || tiles * 32 > INT32_MAX) return hipErrorInvalidValue;
     PnpArgs ka = a;
     ka.best_key = nullptr;  // reduced below from the complete counts
-    for (int64_t h = 0; h < H; h += Hc) {
-        const int32_t Hh = (int32_t)std::min<int64_t>(Hc, H - h);
-        if (Hc < H) {
-            pl = plan(Hh);
-            hipError_t e = hipMemsetAsync(a.queue + 32, 0, (kQWords - 32) * sizeof(int), s);
-            if (e != hipSuccess) return e;
-        }
-        if (pl.units > INT32_MAX) return hipErrorInvalidValue;
-        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((pl.units + 3) / 4, resident));
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, a.queue, counts, (int)pl.ta,
-                           (int)pl.cb, (int)pl.cbig, (int)pl.cs, (int)pl.csmall);
-        static const bool dbg = getenv("RSAC_DBG_MF") != nullptr;  // diagnostics: flagged records per launch
-        if (dbg) {
-            int q[kQWords];
-            (void)hipMemcpyAsync(q, a.queue, sizeof q, hipMemcpyDeviceToHost, s);
-            (void)hipStreamSynchronize(s);
-            q[2] = 0;
-            for (int k = 0; k < kQSub; ++k) q[2] += q[32 + 32 * kQSub + 32 * k];
-            fprintf(stderr, "rsac mw: units %lld records %d of bound %lld (H %d, %lld x %lld big, %lld x %lld small)\n",
-                    (long long)pl.units, q[2], (long long)pl.bound, Hh, (long long)pl.cb, (long long)pl.cbig,
-                    (long long)pl.cs, (long long)pl.csmall);
-        }
-        hipLaunchKernelGGL(k_pnp_mf_recount, dim3(2048), dim3(256), 0, s, ka, hyp_begin + h, Hh, P_, counts, kQSub, 0,
-                           0);
-    }
-    if (a.best_key) {
-        unsigned g = cdiv(H, 1024);
-        if (g > 128) g = 128;
-        hipLaunchKernelGGL(k_best_key, dim3(g), dim3(256), 0, s, counts + hyp_begin, a.status + hyp_begin, H,
-                           a.rng_base + hyp_begin, a.best_key);
-    }
+    hipLaunchKernelGGL(k_pnp_score_mf, dim3(queue_grid(units, resident)), dim3(256), 0, s, ka, hyp_begin, H, P_,
+                       a.queue, counts, (int)tb, (int)cells, (int)cell_pts);
+    if (a.best_key) launch_best_key_of(a, hyp_begin, H, counts, s);
     return hipGetLastError();
-}
-
-// RSAC_SMALL_PP / RSAC_SMALL_TILES: tuning knobs of the small-round scoring instance
-static int small_round_pp() {
-    static const int v = [] { const char *e = getenv("RSAC_SMALL_PP"); return e ? atoi(e) : 2; }();
-    return v;
-}
-static int64_t small_round_tiles() {
-    static const int64_t v = [] { const char *e = getenv("RSAC_SMALL_TILES"); return e ? atoll(e) : 16; }();
-    return v;
 }
 
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
@@ -3883,138 +2159,11 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     if (a.max_n > 0 && a.max_n <= kLanePts) {
         hipLaunchKernelGGL(k_pnp_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
     } else if (a.fmodels && !a.exact_only) {
-        if (a.fform == 2 && small_round(P, H)) {  // form-1 records (round_args): the small-round instance
+        if (small_round(P, H)) {  // form-1 records (round_args): the small-round instance
             launch_sc<2, 5>(a, P, hyp_begin, H, counts, s);
             return hipGetLastError();
         }
-        switch (g_score_variant) {
-            case 1: launch_f32<4, 32>(a, P, hyp_begin, H, counts, s); break;
-            case 2: launch_f32<8, 64>(a, P, hyp_begin, H, counts, s); break;
-            case 3: launch_f32<16, 32>(a, P, hyp_begin, H, counts, s); break;
-            case 4: launch_f32<6, 32>(a, P, hyp_begin, H, counts, s); break;
-            case 5: launch_f32<8, 16>(a, P, hyp_begin, H, counts, s); break;
-            case 6: launch_f32<4, 64>(a, P, hyp_begin, H, counts, s); break;
-            case 7: launch_f32<4, 32, 1>(a, P, hyp_begin, H, counts, s); break;
-            case 8: launch_f32<8, 32, 1>(a, P, hyp_begin, H, counts, s); break;
-            case 9: launch_f32<4, 16, 1>(a, P, hyp_begin, H, counts, s); break;
-            case 10: launch_f32<6, 32, 1>(a, P, hyp_begin, H, counts, s); break;
-            case 11: launch_f32<4, 16, 2>(a, P, hyp_begin, H, counts, s); break;
-            case 12: launch_f32<2, 16, 2>(a, P, hyp_begin, H, counts, s); break;
-            case 13: launch_f32<4, 32, 2>(a, P, hyp_begin, H, counts, s); break;
-            case 14: launch_f32<8, 16, 2>(a, P, hyp_begin, H, counts, s); break;
-            case 15: launch_f32<2, 32, 2>(a, P, hyp_begin, H, counts, s); break;
-            case 16: launch_f32<4, 32, 3>(a, P, hyp_begin, H, counts, s); break;
-            case 17: launch_f32<4, 16, 3>(a, P, hyp_begin, H, counts, s); break;
-            case 18: launch_f32<8, 32, 3>(a, P, hyp_begin, H, counts, s); break;
-            case 19: launch_f32<2, 32, 3>(a, P, hyp_begin, H, counts, s); break;
-            case 20: launch_f32<6, 32, 3>(a, P, hyp_begin, H, counts, s); break;
-            case 21: launch_f32<4, 32, 3, 5>(a, P, hyp_begin, H, counts, s); break;
-            case 22: launch_f32<4, 32, 3, 6>(a, P, hyp_begin, H, counts, s); break;
-            case 23: launch_f32<8, 32, 3, 5>(a, P, hyp_begin, H, counts, s); break;
-            case 24: launch_f32<2, 32, 3, 6>(a, P, hyp_begin, H, counts, s); break;
-            case 25:
-                // a round of only a few hypothesis tiles (an adaptive run's first 256): 2 points per
-                // lane, so the point split gives 4x the units and the GPU fills
-                if ((int64_t)P * ((H + 31) / 32) <= small_round_tiles())
-                    switch (small_round_pp()) {
-                        case 102: launch_f32<2, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
-                        case 105: launch_f32<2, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-                        case 104: launch_f32<4, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
-                        case 4: launch_f32<4, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-                        case 8: launch_f32<8, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-                        case 1: launch_f32<1, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-                        case 16: launch_f32<2, 16, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-                        default: launch_f32<2, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-                    }
-                else
-                    launch_f32<8, 32, 3, 5, true, true>(a, P, hyp_begin, H, counts, s);
-                break;
-            case 26: launch_f32<8, 32, 3, 5, false, true>(a, P, hyp_begin, H, counts, s); break;
-            case 27: launch_f32<8, 32, 3, 5, true, false>(a, P, hyp_begin, H, counts, s); break;
-            case 28: launch_f32<4, 32, 3, 6, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 48:
-                // default: the lean hypothesis loop (k_pnp_score_ab LEAN); small rounds (an adaptive
-                // run's first 256 hypotheses) with 2 points per lane so the point split fills the GPU
-                if ((int64_t)P * ((H + 31) / 32) <= small_round_tiles())
-                    launch_f32<2, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s);
-                else
-                    launch_f32<8, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s);
-                break;
-            case 49:
-                // the scaled form (k_pnp_score_sc): records written by write_fmodel_sc (fform 1)
-                if ((int64_t)P * ((H + 31) / 32) <= small_round_tiles())
-                    launch_sc<2, 5>(a, P, hyp_begin, H, counts, s);
-                else
-                    launch_sc<8, 4>(a, P, hyp_begin, H, counts, s);
-                break;
-            case 60: return launch_mf<true, 2>(a, P, hyp_begin, H, counts, s);
-            case 61: return launch_mf<false, 1>(a, P, hyp_begin, H, counts, s);  // timing only: no recount
-            case 62: return launch_mf<true, 1>(a, P, hyp_begin, H, counts, s);
-            case 63: return launch_mf<true, 4>(a, P, hyp_begin, H, counts, s);
-            case 64: return launch_mf<true, 2, 3>(a, P, hyp_begin, H, counts, s);
-            case 65: return launch_mf<true, 4, 3>(a, P, hyp_begin, H, counts, s);
-            case 66: return launch_mf<true, 1, 3>(a, P, hyp_begin, H, counts, s);
-            case 67: return launch_mf<true, 2, 3, 1>(a, P, hyp_begin, H, counts, s);
-            case 68: return launch_mf<false, 1, 3, 1>(a, P, hyp_begin, H, counts, s);  // timing only
-            case 69: return launch_mf<true, 2, 2, 1>(a, P, hyp_begin, H, counts, s);
-            case 70: return launch_mf<true, 2, 3, 0, true>(a, P, hyp_begin, H, counts, s);
-            case 71: return launch_mf<true, 4, 3, 0, true>(a, P, hyp_begin, H, counts, s);
-            case 72: return launch_mf<false, 1, 3, 0, true>(a, P, hyp_begin, H, counts, s);  // timing only
-            case 73: return launch_mf<true, 2, 3, 1, true>(a, P, hyp_begin, H, counts, s);
-            case 74: return launch_mw<2, 1>(a, P, hyp_begin, H, counts, s);
-            case 75: return launch_mw<2, 0>(a, P, hyp_begin, H, counts, s);
-            case 76: return launch_mw<1, 1>(a, P, hyp_begin, H, counts, s);
-            case 77: return launch_mw<2, 1, 1>(a, P, hyp_begin, H, counts, s);  // timing only
-            case 78: return launch_mw<2, 1, 2>(a, P, hyp_begin, H, counts, s);  // timing only
-            case 79: return launch_mw<2, 1, 3>(a, P, hyp_begin, H, counts, s);  // timing only
-            case 80: return launch_mf<true, 2, 2, 1, true, true>(a, P, hyp_begin, H, counts, s);
-            case 81: return launch_mf<true, 2, 3, 1, true, true>(a, P, hyp_begin, H, counts, s);
-            case 82: return launch_mf<true, 2, 2, 1, false, true>(a, P, hyp_begin, H, counts, s);
-            case 83: return launch_mf<true, 2, 3, 0, false, true>(a, P, hyp_begin, H, counts, s);
-            case 85: return launch_mf<true, 2, 3, 1, true, false, false, true>(a, P, hyp_begin, H, counts, s);
-            case 90: return launch_mf<true, 2, 3, 1, true, false, false, false, false, 1>(a, P, hyp_begin, H, counts, s);
-            case 93: return launch_mf<true, 1, 3, 1, true, false, false, false, true, 1>(a, P, hyp_begin, H, counts, s);
-            case 94: return launch_mf<true, 2, 3, 1, true, false, false, false, true, 1>(a, P, hyp_begin, H, counts, s);
-            case 91: return launch_mf<true, 2, 3, 1, true, false, false, false, false, 2>(a, P, hyp_begin, H, counts, s);
-            case 92: return launch_mf<true, 2, 3, 1, true, false, false, false, false, 3>(a, P, hyp_begin, H, counts, s);
-            case 88:  // 73 with the flagged windows recounted inside the unit (no recount launch)
-                return launch_mf<true, 2, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
-            case 89:  // the same, band checked every iteration (default)
-                return launch_mf<true, 1, 3, 1, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
-            case 95: return launch_mf<true, 1, 4, 1, false, false, false, false, true>(a, P, hyp_begin, H, counts, s);
-            case 96: return launch_mf<true, 1, 4, 0, false, false, false, false, true>(a, P, hyp_begin, H, counts, s);
-            case 97: return launch_mf<true, 1, 3, 1, false, false, false, false, true>(a, P, hyp_begin, H, counts, s);
-            case 98: return launch_mf<true, 1, 3, 0, true, false, false, false, true>(a, P, hyp_begin, H, counts, s);
-            case 99:  // 98 with the count / band minimum of a group issued behind the next group's MFMAs
-                return launch_mf<true, 1, 3, 0, true, false, false, false, true, 4>(a, P, hyp_begin, H, counts, s);
-            case 86: return launch_mf<true, 2, 3, 1, false, false, false, true>(a, P, hyp_begin, H, counts, s);
-            case 84:
-            case 87: {  // 73 / 85 with s_memtime phase totals (diagnostics)
-                hipError_t e = g_score_variant == 84
-                                   ? launch_mf<true, 2, 3, 1, true, false, true>(a, P, hyp_begin, H, counts, s)
-                                   : launch_mf<true, 2, 3, 1, true, false, true, true>(a, P, hyp_begin, H, counts, s);
-                unsigned long long t[8];
-                (void)hipMemcpyFromSymbolAsync(t, HIP_SYMBOL(g_mf_timing), sizeof t, 0, hipMemcpyDeviceToHost, s);
-                (void)hipStreamSynchronize(s);
-                const double w = t[5] ? (double)t[5] : 1.0;
-                fprintf(stderr, "rsac mf timing per wave (memtime ticks): kernel %.0f pro %.0f loop %.0f epi %.0f between %.0f units %.2f\n",
-                        t[0] / w, t[1] / w, t[2] / w, t[3] / w, t[4] / w, t[6] / w);
-                return e;
-            }
-            case 50: launch_sc<8, 5>(a, P, hyp_begin, H, counts, s); break;
-            case 51: launch_sc<4, 4>(a, P, hyp_begin, H, counts, s); break;
-            case 52: launch_sc<6, 4>(a, P, hyp_begin, H, counts, s); break;
-            case 53: launch_sc<8, 4, true>(a, P, hyp_begin, H, counts, s); break;
-            case 40: launch_f32<8, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 41: launch_f32<4, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 42: launch_f32<8, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 43: launch_f32<6, 32, 4, 5, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 44: launch_f32<8, 32, 4, 3, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 45: launch_f32<12, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 46: launch_f32<8, 16, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
-            case 47: launch_f32<6, 32, 4, 4, true, true>(a, P, hyp_begin, H, counts, s); break;
-            default: launch_f32<kScoreP, kScoreHB>(a, P, hyp_begin, H, counts, s); break;
-        }
+        return launch_mf(a, P, hyp_begin, H, counts, s);
     } else
         hipLaunchKernelGGL((k_pnp_score<kScoreP, kScoreHB>), dim3(cdiv(H, kScoreHB), P), dim3(256), 0, s, a,
                            hyp_begin, H, counts);
@@ -5307,14 +3456,7 @@ hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32
     else if (a.fmodels && a.fm_queue) {
         // k_fm_score_q: whole-tile units, then the last `resident` tiles by cells (launch_sc)
         constexpr int FP = 8;
-        static int resident = 0;
-        if (resident == 0) {
-            int dev = 0, cus = 0, per_cu = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fm_score_q<FP>, 256, 0);
-            resident = std::max(1, cus) * std::max(1, per_cu);
-        }
+        static const int resident = resident_blocks(k_fm_score_q<FP>);
         const int64_t cells = std::max<int64_t>(1, ((int64_t)a.max_n + 256 * FP - 1) / (256 * FP));
         const int64_t tiles = (int64_t)P * ((H + 31) / 32);
         const int64_t cell_tiles = std::min<int64_t>(tiles, resident);
@@ -5327,8 +3469,7 @@ hipError_t launch_fm_score(const HomArgs &a, int32_t P, int64_t hyp_begin, int32
                 e = hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * a.hyp_stride, 0, sizeof(int32_t) * H, P, s);
         }
         if (e != hipSuccess) return e;
-        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
-        hipLaunchKernelGGL(k_fm_score_q<FP>, dim3(grid), dim3(256), 0, s, a, hyp_begin, H, P, counts, (int)tb,
+        hipLaunchKernelGGL(k_fm_score_q<FP>, dim3(queue_grid(units, resident)), dim3(256), 0, s, a, hyp_begin, H, P, counts, (int)tb,
                            (int)cells);
     } else
         hipLaunchKernelGGL((k_fm_score<4, 32>), dim3(cdiv(H, 32), P), dim3(256), 0, s, a, hyp_begin, H, counts);
@@ -5407,6 +3548,71 @@ hipError_t launch_pnp_winner(const double *p3, const double *p2, int32_t n, cons
         if (g > 1024) g = 1024;
         hipLaunchKernelGGL(k_pnp_winner_mask, dim3(g), dim3(256), 0, s, p3, p2, n, cam, rec, mask);
     }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// compute_reprojection_error (testpro-K.py:32-36) on f64 inputs: cv2.projectPoints + the
+// residual's L2 norm per point (pnp_reproj_err).  p3 / p2: f64 AoS (device).
+// ---------------------------------------------------------------------------
+// one pose: the projections (proj, n x 2, optional) and errors (err, n, optional)
+__global__ void k_pnp_reproj(const double *__restrict__ p3, const double *__restrict__ p2, int32_t n, PoseCam pc,
+                             double *__restrict__ proj, double *__restrict__ err) {
+    const Cam k{pc.cam[0], pc.cam[1], pc.cam[2], pc.cam[3]};
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        double pu, pv;
+        const double e = pnp_reproj_err(pc.R, pc.t, k, p3[3 * i], p3[3 * i + 1], p3[3 * i + 2], p2[2 * i],
+                                        p2[2 * i + 1], pu, pv);
+        if (proj) {
+            proj[2 * i] = pu;
+            proj[2 * i + 1] = pv;
+        }
+        if (err) err[i] = e;
+    }
+}
+
+// the mean inlier error of every problem p (testpro-K.py:80-82: np.mean over the inliers): one
+// wave per problem over the shared points, poses[p] (R 9, t 3) and cams[p] (fx fy cx cy), masks
+// p x n.  Order (the oracle's orc_reproj_mean): lane l sums its points l, l + 64, ... ascending,
+// then the xor butterfly (o = 32 .. 1) of the 64 lane sums; out[p] = {sum, count}
+__global__ __launch_bounds__(64) void k_pnp_reproj_mean(const double *__restrict__ p3, const double *__restrict__ p2,
+                                                        int32_t n, const double *__restrict__ poses,
+                                                        const double *__restrict__ cams,
+                                                        const uint8_t *__restrict__ masks, double *__restrict__ out) {
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const double *m = poses + 12 * p;
+    const Cam k{cams[4 * p], cams[4 * p + 1], cams[4 * p + 2], cams[4 * p + 3]};
+    const uint8_t *mk = masks + (int64_t)p * n;
+    double s = 0.0;
+    int c = 0;
+    for (int i = lane; i < n; i += 64)
+        if (mk[i]) {
+            double pu, pv;
+            s = s + pnp_reproj_err(m, m + 9, k, p3[3 * i], p3[3 * i + 1], p3[3 * i + 2], p2[2 * i], p2[2 * i + 1],
+                                   pu, pv);
+            ++c;
+        }
+    for (int o = 32; o > 0; o >>= 1) {
+        s = s + __shfl_xor(s, o);
+        c += __shfl_xor(c, o);
+    }
+    if (lane == 0) {
+        out[2 * p] = s;
+        out[2 * p + 1] = (double)c;
+    }
+}
+
+hipError_t launch_pnp_reproj(const double *p3, const double *p2, int32_t n, const PoseCam &pc, double *proj,
+                             double *err, hipStream_t s) {
+    unsigned g = cdiv(n > 0 ? n : 1, 256);
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_pnp_reproj, dim3(g), dim3(256), 0, s, p3, p2, n, pc, proj, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_reproj_mean(const double *p3, const double *p2, int32_t n, int32_t P, const double *poses,
+                                  const double *cams, const uint8_t *masks, double *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_pnp_reproj_mean, dim3(P), dim3(64), 0, s, p3, p2, n, poses, cams, masks, out);
     return hipGetLastError();
 }
 

@@ -114,6 +114,23 @@ RSAC_HD float pnp_err(const double *R, const double *t, const Cam &k, double X, 
     return e1 + e2;
 }
 
+// compute_reprojection_error (testpro-K.py:32-36): cv2.projectPoints of f64 inputs in f64 (the
+// operations of pnp_err, zero distortion, no rounding to f32), then np.linalg.norm of the pixel
+// residual: sqrt(dx^2 + dy^2).  pu, pv: the projection (projectPoints' output).
+RSAC_HD double pnp_reproj_err(const double *R, const double *t, const Cam &k, double X, double Y, double Z, double u,
+                              double v, double &pu, double &pv) {
+    double x = R[0] * X + R[1] * Y; x = x + R[2] * Z; x = x + t[0];
+    double y = R[3] * X + R[4] * Y; y = y + R[5] * Z; y = y + t[1];
+    double z = R[6] * X + R[7] * Y; z = z + R[8] * Z; z = z + t[2];
+    double iz = (z != 0.0) ? 1.0 / z : 1.0;
+    x = x * iz; y = y * iz;
+    pu = x * k.fx + k.cx;
+    pv = y * k.fy + k.cy;
+    const double dx = u - pu, dy = v - pv;
+    const double s2 = dx * dx + dy * dy;
+    return dsqrt(s2);
+}
+
 // ---------------------------------------------------------------------------
 // P3P, Lambda Twist (Persson & Nordberg, ECCV 2018).
 // ---------------------------------------------------------------------------

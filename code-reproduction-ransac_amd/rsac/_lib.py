@@ -63,7 +63,6 @@ SIGNATURES = [
     ("rsac_abi_version", C.c_int, []),
     ("rsac_device_count", C.c_int, []),
     ("rsac_set_round_size", C.c_int, [_vp, _i64]),
-    ("rsac_set_score_variant", C.c_int, [C.c_int]),
     ("rsac_refit_blocks", C.c_int, [_vp, _i32, C.POINTER(_i32), C.POINTER(_i32)]),
     ("rsac_debug_set", C.c_int, [_vp, _i32, _i64]),
     ("rsac_pnp_ransac", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
@@ -101,6 +100,10 @@ SIGNATURES = [
     ("rsac_scan_raise", C.c_int, [_vp, _i32, _i32, _i32, _d]),
     ("rsac_pnp_local_opt", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _d, _u32, _vp, _vp, _vp, _vp]),
     ("rsac_scan", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d]),
+    ("rsac_pnp_refine_lm", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
+    ("rsac_pnp_reprojection_errors", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
+    ("rsac_pnp_orientation_sweep", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _i32, _d, _d, _u64, _u32, _i32, _vp,
+                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 ]
 
 _lib = None

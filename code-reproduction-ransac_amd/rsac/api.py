@@ -512,6 +512,151 @@ def refine_pose(points2D, points3D, K, R, t, mask=None, max_iter: int = 20):
     return Rr.reshape(3, 3), tr
 
 
+def refine_pose_device(points2D, points3D, K, R, t, mask=None, device=None):
+    """cv2.solvePnPRefineLM (main_v1.py:508, testpro-K.py:122) on the GPU: LM from (R, t) over the
+    (masked) correspondences -> (R, t).  Host arrays; the same bits as refine_pose (host)."""
+    P3 = np.ascontiguousarray(np.asarray(points3D, np.float64).reshape(-1, 3))
+    P2 = np.ascontiguousarray(np.asarray(points2D, np.float64).reshape(-1, 2))
+    if P3.shape[0] != P2.shape[0]:
+        raise ValueError("points3D and points2D differ in length")
+    Rr = np.ascontiguousarray(np.asarray(R, np.float64).reshape(9)).copy()
+    tr = np.ascontiguousarray(np.asarray(t, np.float64).reshape(3)).copy()
+    m = None if mask is None else np.ascontiguousarray(np.asarray(mask, np.uint8).reshape(-1))
+    ctx = L.context(0 if device is None else int(device))
+    with ctx.lock:
+        L.check(L.lib().rsac_pnp_refine_lm(ctx.handle, P3.ctypes.data, P2.ctypes.data, P3.shape[0], _K9(K).ctypes.data,
+                                           None if m is None else m.ctypes.data, Rr.ctypes.data, tr.ctypes.data, None))
+    return Rr.reshape(3, 3), tr
+
+
+def reprojection_errors(points3D, points2D, K, R, t, *, device=None, return_projection: bool = False):
+    """compute_reprojection_error (testpro-K.py:32-36) on the GPU: ||pixel - projectPoints(X)||_2
+    per point, f64 throughout (zero distortion).  R (3,3) or a Rodrigues vector (3,), t (3,).
+    GPU tensor inputs keep the outputs on the device.  -> errors (N,) [, projections (N, 2)]."""
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    if p3.n != p2.n:
+        raise ValueError("points3D and points2D differ in length")
+    if p3.device != p2.device:
+        raise ValueError("points3D and points2D must both be host arrays or both GPU tensors")
+    r = np.asarray(R, np.float64)
+    R9 = np.ascontiguousarray(rodrigues(r).reshape(9) if r.size == 3 else r.reshape(9))
+    t3 = np.ascontiguousarray(np.asarray(t, np.float64).reshape(3))
+    n = p3.n
+    ctx = L.context(_device_of(p3, device))
+    if p3.device:
+        import torch
+        err = torch.empty(max(n, 1), dtype=torch.float64, device=p3.keep.device)
+        proj = torch.empty((max(n, 1), 2), dtype=torch.float64, device=p3.keep.device) if return_projection else None
+        eptr, pptr = err.data_ptr(), (proj.data_ptr() if proj is not None else None)
+        flags = L.F_DEVICE_IN
+    else:
+        err = np.zeros(max(n, 1))
+        proj = np.zeros((max(n, 1), 2)) if return_projection else None
+        eptr, pptr = err.ctypes.data, (proj.ctypes.data if proj is not None else None)
+        flags = 0
+    with ctx.lock:
+        L.check(L.lib().rsac_pnp_reprojection_errors(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), n,
+                                                     _K9(K).ctypes.data, R9.ctypes.data, t3.ctypes.data, flags,
+                                                     C.c_void_p(pptr) if pptr else None, C.c_void_p(eptr),
+                                                     _stream_of(p3)))
+    return (err[:n], proj[:n]) if return_projection else err[:n]
+
+
+def compute_reprojection_error(pos3d, pixels, K, dist_coeffs, rvec, tvec):
+    """The reference's helper (testpro-K.py:32-36) with its signature: projectPoints through the
+    Rodrigues vector rvec, then the per-point L2 norm -- on the GPU (reprojection_errors)."""
+    if dist_coeffs is not None and np.any(np.asarray(dist_coeffs, np.float64) != 0):
+        raise NotImplementedError("zero distortion only (as every reference call site uses)")
+    rv = np.asarray(rvec, np.float64).reshape(-1)
+    R = rodrigues(rv) if rv.size == 3 else rv.reshape(3, 3)
+    e = reprojection_errors(pos3d, pixels, K, R, tvec)
+    return e
+
+
+@dataclass
+class OrientationResult:
+    """Outputs of estimate_camera_orientation (testpro-K.py:39-162), one row per intrinsic."""
+    rvec: np.ndarray | None          # (3, 1) solvePnPRefineLM's rotation vector (None: every K failed)
+    tvec: np.ndarray | None          # (3, 1)
+    best: int                        # index of the chosen K (-1: none)
+    K: np.ndarray                    # (P, 3, 3) the candidates, loop order (focal outer, sensor inner)
+    mean_error: np.ndarray           # (P,) mean inlier reprojection error (NaN: failed the gate)
+    ok: np.ndarray                   # (P,) passed "success and >= 6 inliers" (testpro-K.py:77)
+    n_inliers: np.ndarray            # (P,)
+    rvec_initial: np.ndarray         # (P, 3) solvePnPRansac's rotation vectors
+    tvec_initial: np.ndarray         # (P, 3)
+    masks: np.ndarray                # (P, N) RANSAC-phase inlier masks
+    focal_sensor: list               # (focal length, (sensor w, sensor h)) of every K
+    ranking: list                    # (distance to the known origin, mean error, K index, camera origin), sorted
+
+    @property
+    def best_K(self):
+        return self.K[self.best] if self.best >= 0 else None
+
+
+def intrinsics_grid(focal_lengths, sensor_sizes, image_size):
+    """The candidate intrinsics of testpro-K.py:58-70, in its loop order."""
+    Ks, fs = [], []
+    for focal_length in focal_lengths:
+        for (sensor_width, sensor_height) in sensor_sizes:
+            fx = focal_length / (sensor_width / image_size[0])
+            fy = focal_length / (sensor_height / image_size[1])
+            Ks.append(np.array([[fx, 0, image_size[0] / 2], [0, fy, image_size[1] / 2], [0, 0, 1]], np.float64))
+            fs.append((focal_length, (sensor_width, sensor_height)))
+    return np.stack(Ks), fs
+
+
+def estimate_camera_orientation(pos3d, pixels, focal_lengths, sensor_sizes, image_size, known_camera_origin=None, *,
+                                n_iters: int = 5000, reproj_thresh: float = 30.0, confidence: float = 0.99,
+                                seed: int = 0x5EED, sampler: str = "philox", refine="lm", min_inliers: int = 6,
+                                device: int = 0, return_info: bool = False):
+    """estimate_camera_orientation of testpro-K.py:39-125 as one GPU call sequence
+    (rsac_pnp_orientation_sweep): solvePnPRansac under every candidate K (one batched launch), the
+    mean inlier reprojection error of each on the device, the first K with the smallest, then
+    solvePnPRefineLM of its pose on its inliers.  Returns (rvec, tvec) like the reference
+    ((None, None) when every K failed), or the OrientationResult with return_info=True."""
+    P3 = np.ascontiguousarray(np.asarray(pos3d, np.float64).reshape(-1, 3))
+    P2 = np.ascontiguousarray(np.asarray(pixels, np.float64).reshape(-1, 2))
+    if P3.shape[0] != P2.shape[0]:
+        raise ValueError("pos3d and pixels differ in length")
+    Ks, fs = intrinsics_grid(focal_lengths, sensor_sizes, image_size)
+    P, n = Ks.shape[0], P3.shape[0]
+    K9 = np.ascontiguousarray(Ks.reshape(P, 9))
+    best = C.c_int32(-1)
+    mean = np.zeros(P)
+    models = np.zeros((P, 12))
+    status = np.zeros(P, np.int32)
+    ninl = np.zeros(P, np.int32)
+    masks = np.zeros((P, max(n, 1)), np.uint8)
+    R, t = np.zeros(9), np.zeros(3)
+    ctx = L.context(device)
+    with ctx.lock:
+        code = L.check(L.lib().rsac_pnp_orientation_sweep(
+            ctx.handle, P3.ctypes.data, P2.ctypes.data, n, K9.ctypes.data, P, int(n_iters), float(reproj_thresh),
+            float(confidence), int(seed) & (2**64 - 1), _flags(True, refine, sampler), int(min_inliers),
+            C.byref(best), mean.ctypes.data, models.ctypes.data, status.ctypes.data, ninl.ctypes.data,
+            masks.ctypes.data, R.ctypes.data, t.ctypes.data, None))
+    ok = status == L.OK
+    b = int(best.value)
+    rvec = rodrigues(R.reshape(3, 3)).reshape(3, 1) if code == L.OK else None
+    tvec = t.reshape(3, 1).copy() if code == L.OK else None
+    if not return_info:
+        return rvec, tvec
+    rv0 = np.stack([rodrigues(models[k, :9].reshape(3, 3)).reshape(3) for k in range(P)])
+    ranking = []
+    if known_camera_origin is not None:
+        o = np.asarray(known_camera_origin, np.float64).reshape(3)
+        for k in np.flatnonzero(ok):
+            Rk = rodrigues(rv0[k])
+            origin = -Rk.T @ models[k, 9:12]
+            ranking.append((float(np.linalg.norm(origin - o)), float(mean[k]), int(k), origin))
+        ranking.sort(key=lambda x: x[0])  # testpro-K.py:103 (stable, as Python's sort)
+    return OrientationResult(rvec=rvec, tvec=tvec, best=b, K=Ks, mean_error=mean, ok=ok, n_inliers=ninl,
+                             rvec_initial=rv0, tvec_initial=models[:, 9:12].copy(), masks=masks[:, :n].astype(bool),
+                             focal_sensor=fs, ranking=ranking)
+
+
 def epnp_pose(points2D, points3D, K, mask=None):
     """EPnP on all (or the masked) points, cv2.solvePnP(..., flags=SOLVEPNP_EPNP) -> (R, t) or
     (None, None) for < 4 points / a planar cloud.  Host arrays; the same numbers as the device pass

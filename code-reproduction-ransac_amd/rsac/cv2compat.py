@@ -92,27 +92,29 @@ def findHomography(srcPoints, dstPoints, method=0, ransacReprojThreshold=3.0, ma
 
 def projectPoints(objectPoints, rvec, tvec, cameraMatrix, distCoeffs, imagePoints=None, jacobian=None,
                   aspectRatio=0):
-    """(N,3) -> ((N,1,2) pixels, None), zero distortion, float64 as cv2 returns for f64 input."""
+    """(N,3) -> ((N,1,2) pixels, None): zero distortion, float64 as cv2 returns for f64 input; the
+    projection runs on the GPU (rsac_pnp_reprojection_errors, testpro-K.py:33)."""
     _check_dist(distCoeffs)
     X = np.asarray(objectPoints, np.float64).reshape(-1, 3)
     r = np.asarray(rvec, np.float64).reshape(-1)
     R = api.rodrigues(r) if r.size == 3 else r.reshape(3, 3)
     t = np.asarray(tvec, np.float64).reshape(3)
-    K = np.asarray(cameraMatrix, np.float64).reshape(3, 3)
-    pc = X @ R.T + t
-    z = pc[:, 2]
-    iz = np.where(z != 0, 1.0 / np.where(z != 0, z, 1.0), 1.0)
-    u = pc[:, 0] * iz * K[0, 0] + K[0, 2]
-    v = pc[:, 1] * iz * K[1, 1] + K[1, 2]
-    return np.stack([u, v], axis=1).reshape(-1, 1, 2), None
+    # the pixel argument only feeds the error, which projectPoints does not return
+    _, proj = api.reprojection_errors(X, np.zeros((X.shape[0], 2)), cameraMatrix, R, t, return_projection=True)
+    return proj.reshape(-1, 1, 2), None
 
 
 def solvePnPRefineLM(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec, tvec, criteria=None):
-    """LM refinement of (rvec, tvec) on the given correspondences -> (rvec, tvec)."""
+    """LM refinement of (rvec, tvec) on the given correspondences -> (rvec, tvec), on the GPU
+    (rsac_pnp_refine_lm: the bits of the host refit rsac_pnp_refine)."""
     _check_dist(distCoeffs)
     P3 = np.asarray(objectPoints, np.float64).reshape(-1, 3)
     P2 = np.asarray(imagePoints, np.float64).reshape(-1, 2)
+    if P3.shape[0] != P2.shape[0]:
+        raise error("objectPoints and imagePoints differ in length")
+    if P3.shape[0] < 3:
+        raise error("solvePnPRefineLM needs at least 3 points")
     R0 = api.rodrigues(np.asarray(rvec, np.float64).reshape(3))
     t0 = np.asarray(tvec, np.float64).reshape(3)
-    R, t = api.refine_pose(P2, P3, cameraMatrix, R0, t0)
+    R, t = api.refine_pose_device(P2, P3, cameraMatrix, R0, t0)
     return api.rodrigues(R).reshape(3, 1), t.reshape(3, 1)

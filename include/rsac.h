@@ -94,24 +94,6 @@ RSAC_EXPORT const char *rsac_last_error(void);
 RSAC_EXPORT int rsac_abi_version(void);
 RSAC_EXPORT int rsac_device_count(void);
 RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* adaptive round length (default 4096) */
-/* tuning knob: PnP scoring-kernel variant, process-wide (-1 = the built-in default, 98;
- * 0..6 VALU f32 tilings, 7..10 packed-f32 tilings, 11..15 f32 MFMA tilings, 16..28 the
- * branch-free alpha-beta band tilings, 40..48 the alpha-beta band with the lean hypothesis
- * loop (48 = 42 with the small-round instance), 49..53 the scaled form (k_pnp_score_sc; 49
- * with the small-round instance), 60..73 the MFMA form (k_pnp_score_mf: xs ys z' by
- * v_mfma_f32_32x32x16_f16 on f16 hi/lo operands; the band checked every 2 iterations; 61 and 68
- * without the exact recount, timing only; 62, 63 checked every 1, 4 iterations; 64..66 = 60, 63,
- * 62 at 3 waves per SIMD; 67 (68, 69) = 64 (61, 64 at 2 waves) with the point operands loaded one
- * iteration ahead; 70..73 = 64, 65, 68 (timing only), 67 with the A operands and slopes in
- * registers); 74..79 the wave-autonomous MFMA kernel (k_pnp_score_mw; 77..79 timing
- * experiments); 80..83 software-pipelined MFMA groups; 84, 87 s_memtime phase totals
- * (diagnostics); 85, 86 dynamic iteration pairs; 88, 89 = 73 with the flagged windows recounted
- * inside the unit (89: checked every iteration; long problems by cells of <= 16384 points);
- * 90..92 s_setprio forms; 93, 94 = 89, 88 + 90; 95..97 = 89 at 4 waves / A operands from LDS;
- * 98 = 89 without the point-operand prefetch, the default; 99 = 98 with the count of a group
- * issued behind the next group's MFMAs).  Counts, masks and models never depend on the
- * variant (61, 68, 72, 78, 79 excepted). */
-RSAC_EXPORT int rsac_set_score_variant(int variant);
 
 /* The pose refit (solvePnPRefineLM, main_v1.py:508-509) of a problem above 4096 points runs
  * on several cooperating blocks that must be resident at once.  rsac_refit_blocks reports, for
@@ -285,6 +267,37 @@ RSAC_EXPORT int rsac_pnp_refine(const double *pts3d, const double *pts2d, int32_
                                 const uint8_t *mask, double R[9], double t[3], int32_t max_iter);
 RSAC_EXPORT int rsac_homography_fit(const double *src, const double *dst, int32_t n, const uint8_t *mask,
                                     double H_out[9]);
+
+/* cv2.solvePnPRefineLM (main_v1.py:508-509, testpro-K.py:122-125) on the device: LM on (R, t)
+ * in place from the given start over the masked points (mask NULL = all); host f64 AoS inputs,
+ * rounded to f32 like the RANSAC path.  The same bits as rsac_pnp_refine (host). */
+RSAC_EXPORT int rsac_pnp_refine_lm(rsac_ctx *ctx, const double *pts3d, const double *pts2d, int32_t n,
+                                   const double K[9], const uint8_t *mask, double R[9], double t[3], void *stream);
+
+/* compute_reprojection_error (testpro-K.py:32-36) = cv2.projectPoints (testpro-K.py:33, zero
+ * distortion) + the per-point L2 norm of the pixel residual, in f64 on the f64 inputs:
+ * proj_out n x 2 (optional), err_out n (optional).  Host arrays, or (RSAC_F_DEVICE_IN) device
+ * arrays for inputs and outputs alike, then only enqueued on `stream`. */
+RSAC_EXPORT int rsac_pnp_reprojection_errors(rsac_ctx *ctx, const double *pts3d, const double *pts2d, int32_t n,
+                                             const double K[9], const double R[9], const double t[3],
+                                             uint32_t flags, double *proj_out, double *err_out, void *stream);
+
+/* estimate_camera_orientation (testpro-K.py:39-125) in one call: solvePnPRansac of the points
+ * under each of the n_k intrinsics Ks (n_k x 9, the loop of :58-75, one batched launch
+ * sequence; flags as rsac_pnp_ransac_batched: the final solve is RSAC_F_REFINE / RSAC_F_EPNP),
+ * the gate "success and >= min_inliers inliers" (:77, 6 in the reference), the mean inlier
+ * reprojection error of every K on the device (:80-82, through the pose's rvec as projectPoints
+ * sees it), the first K with the strictly smallest mean (:90-97), then solvePnPRefineLM of that
+ * K's pose on its inliers (:122-125).  Host f64 arrays.  Outputs: *best_out (-1: every K failed,
+ * RSAC_NO_MODEL), and optionally per K mean_err_out (NaN where gated), models_out (R 9, t 3 of
+ * solvePnPRansac), status_out (RSAC_OK = passed the gate), n_inliers_out, masks_out (n_k x n);
+ * R_out / t_out the refined pose of the winner. */
+RSAC_EXPORT int rsac_pnp_orientation_sweep(rsac_ctx *ctx, const double *pts3d, const double *pts2d, int32_t n,
+                                           const double *Ks, int32_t n_k, int32_t n_iters, double reproj_thresh,
+                                           double confidence, uint64_t seed, uint32_t flags, int32_t min_inliers,
+                                           int32_t *best_out, double *mean_err_out, double *models_out,
+                                           int32_t *status_out, int32_t *n_inliers_out, uint8_t *masks_out,
+                                           double R_out[9], double t_out[3], void *stream);
 
 /* Rodrigues (cv2.Rodrigues, main_v1.py:895): vector <-> matrix. */
 RSAC_EXPORT void rsac_rodrigues_v2m(const double r[3], double R[9]);

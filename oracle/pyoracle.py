@@ -59,6 +59,10 @@ def lib():
     L.orc_pnp_err.restype = C.c_float
     L.orc_thr2.argtypes = [C.c_double]
     L.orc_thr2.restype = C.c_float
+    L.orc_reproj_errors.argtypes = [_f64p, _f64p, _f64p, _f64p, _f64p, C.c_int, C.c_void_p, C.c_void_p]
+    L.orc_reproj_errors.restype = None
+    L.orc_reproj_mean_sum.argtypes = [_f64p, _f64p, _f64p, _f64p, _f64p, _u8p, C.c_int, C.POINTER(C.c_int)]
+    L.orc_reproj_mean_sum.restype = C.c_double
     L.orc_pnp_count.argtypes = [_f64p, _f64p, _f64p, _f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, C.c_float,
                                 C.c_void_p]
     L.orc_pnp_count.restype = C.c_int32
@@ -265,6 +269,64 @@ def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=50
                                    C.byref(iters), C.byref(nlo))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value), lo_improvements=int(nlo.value))
+
+
+def reproj_errors(points3d, points2d, K, R, t, projections=False):
+    """compute_reprojection_error (testpro-K.py:32-36): f64 projectPoints + per-point L2 norm."""
+    p3 = np.ascontiguousarray(np.asarray(points3d, np.float64).reshape(-1, 3))
+    p2 = np.ascontiguousarray(np.asarray(points2d, np.float64).reshape(-1, 2))
+    n = p3.shape[0]
+    err = np.zeros(n)
+    proj = np.zeros((n, 2)) if projections else None
+    lib().orc_reproj_errors(np.ascontiguousarray(R, np.float64).reshape(9), np.ascontiguousarray(t, np.float64),
+                            cam_from_K(K), p3, p2, n, _ptr(proj), _ptr(err))
+    return (err, proj) if projections else err
+
+
+def reproj_mean(points3d, points2d, K, R, t, mask):
+    """Mean inlier error in the GPU's summation order -> (mean, count)."""
+    p3 = np.ascontiguousarray(np.asarray(points3d, np.float64).reshape(-1, 3))
+    p2 = np.ascontiguousarray(np.asarray(points2d, np.float64).reshape(-1, 2))
+    c = C.c_int(0)
+    s = lib().orc_reproj_mean_sum(np.ascontiguousarray(R, np.float64).reshape(9), np.ascontiguousarray(t, np.float64),
+                                  cam_from_K(K), p3, p2, np.ascontiguousarray(mask, np.uint8), p3.shape[0],
+                                  C.byref(c))
+    return s / c.value if c.value else float("nan"), int(c.value)
+
+
+def estimate_camera_orientation(pos3d, pixels, Ks, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED,
+                                sampler="philox", min_inliers=6):
+    """testpro-K.py:39-125 restated on the oracle's pieces: per K the RANSAC (pnp_ransac) + the LM
+    final solve on its inliers (solvePnPRansac's SOLVEPNP_ITERATIVE final solvePnP), the gate,
+    the mean inlier error through the pose's Rodrigues vector, the first strict minimum, then
+    the LM refit (solvePnPRefineLM) of the winner on its inlier subset."""
+    P3 = np.asarray(pos3d, np.float64).reshape(-1, 3)
+    P2 = np.asarray(pixels, np.float64).reshape(-1, 2)
+    soa = soa_pnp(P3, P2)
+    rows = []
+    best, best_err = -1, float("inf")
+    for k, K in enumerate(Ks):
+        r = pnp_ransac(P3, P2, K, thr, confidence, max_iters, seed, sampler=sampler)
+        if r["best"] < 0:
+            rows.append(None)
+            continue
+        R, t, _ = pnp_refine(soa, r["mask"].astype(np.uint8), cam_from_K(K), r["R"], r["t"])
+        row = dict(R=R, t=t, mask=r["mask"], n_inliers=r["n_inliers"])
+        rows.append(row)
+        if r["n_inliers"] < min_inliers:
+            row["mean"] = float("nan")
+            continue
+        Rp = rodrigues_v2m(rodrigues_m2v(R))
+        row["mean"], _ = reproj_mean(P3, P2, K, Rp, t, r["mask"])
+        if row["mean"] < best_err:
+            best_err, best = row["mean"], k
+    if best < 0:
+        return dict(best=-1, rows=rows, R=None, t=None)
+    w = rows[best]
+    sub3, sub2 = P3[w["mask"]], P2[w["mask"]]
+    Rp = rodrigues_v2m(rodrigues_m2v(w["R"]))
+    Rr, tr, _ = pnp_refine(soa_pnp(sub3, sub2), np.ones(len(sub3), np.uint8), cam_from_K(Ks[best]), Rp, w["t"])
+    return dict(best=best, rows=rows, R=Rr, t=tr)
 
 
 def pnp_local_opt(soa, cam, thr, R, t, count):

@@ -197,6 +197,51 @@ ORC_API float orc_pnp_err(const double R[9], const double t[3], const double cam
 
 ORC_API float orc_thr2(double thr) { return (float)(thr * thr); }
 
+/* compute_reprojection_error (testpro-K.py:32-36) itself: cv2.projectPoints of the f64 inputs
+ * (no CV_32F conversion there) in f64, then np.linalg.norm(pixels - projected, axis=1) =
+ * sqrt(dx*dx + dy*dy) per point.  proj (n x 2) and err (n) optional. */
+ORC_API void orc_reproj_errors(const double R[9], const double t[3], const double cam[4], const double *p3,
+                               const double *p2, int n, double *proj, double *err) {
+    for (int i = 0; i < n; ++i) {
+        const double X = p3[3 * i], Y = p3[3 * i + 1], Z = p3[3 * i + 2];
+        double x = R[0] * X + R[1] * Y; x = x + R[2] * Z; x = x + t[0];
+        double y = R[3] * X + R[4] * Y; y = y + R[5] * Z; y = y + t[1];
+        double z = R[6] * X + R[7] * Y; z = z + R[8] * Z; z = z + t[2];
+        double iz = (z != 0.0) ? 1.0 / z : 1.0;
+        x = x * iz; y = y * iz;
+        const double pu = x * cam[0] + cam[2], pv = y * cam[1] + cam[3];
+        const double dx = p2[2 * i] - pu, dy = p2[2 * i + 1] - pv;
+        if (proj) { proj[2 * i] = pu; proj[2 * i + 1] = pv; }
+        if (err) err[i] = sqrt(dx * dx + dy * dy);
+    }
+}
+
+/* np.mean of the inliers' errors (testpro-K.py:80-82), in the summation order of the GPU's
+ * wave reduction: lane l (0..63) sums the masked errors of points l, l + 64, ... ascending, then
+ * the xor butterfly over the 64 lane sums (o = 32 .. 1).  -> the sum; *count = inliers. */
+ORC_API double orc_reproj_mean_sum(const double R[9], const double t[3], const double cam[4], const double *p3,
+                                   const double *p2, const uint8_t *mask, int n, int *count) {
+    double v[64];
+    int c = 0;
+    for (int l = 0; l < 64; ++l) {
+        v[l] = 0.0;
+        for (int i = l; i < n; i += 64)
+            if (mask[i]) {
+                double e;
+                orc_reproj_errors(R, t, cam, p3 + 3 * i, p2 + 2 * i, 1, NULL, &e);
+                v[l] = v[l] + e;
+                ++c;
+            }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        double w[64];
+        for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
+        memcpy(v, w, sizeof v);
+    }
+    *count = c;
+    return v[0];
+}
+
 ORC_API int32_t orc_pnp_count(const double R[9], const double t[3], const double cam[4],
                               const float *X, const float *Y, const float *Z, const float *U, const float *V,
                               int n, float thr2, uint8_t *mask) {
