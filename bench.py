@@ -12,9 +12,11 @@ Weak scaling: rank r owns hypotheses [r*H, (r+1)*H) of the same Philox stream; t
 exchange is rsac.parallel's all-reduce(MAX) of one int64 key; a rank that lost re-derives
 the winner's model from its index (no broadcast).
 
-Also reported: ms-to-best-model (adaptive termination on, LM refit on, wall
-time of the full rsac.pnp_ransac call), the scoring kernel's roofline, and
-the CPU restatement timed on this host (oracle/, 1 thread).
+Also reported: ms-to-best-model (adaptive termination on, LM refit on, wall time of the full
+rsac.pnp_ransac call), the scoring kernel's roofline (VALU issue: the binding roof, DESIGN.md
+§3), the CPU restatement timed on this host (oracle/, 1 thread and OpenMP), and the other
+BASELINE configs: at N = 1 in `extras` (C3, C4, C5, location search, DEM march); at N > 1 in
+`multi_gpu` (C3 problem shards + all-gather, C5 sharded LO-RANSAC, sharded adaptive ms-to-best).
 
 Launch: python bench.py [--gpus 1 --steps 10 --warmup 3]; for N > 1 the driver
 runs it under torch.distributed.run with one rank per GPU.
@@ -45,7 +47,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
 WARMUP_MIN_S = 0.25  # minimum wall time of the untimed warmup steps (clock ramp)
 VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, f32 vector peak
 VALU_ISSUE_PEAK = 1024 * 0.5 * 2.4e9  # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each, 2.4 GHz
-FLOP_PER_PAIR = 11  # k_pnp_score_mf: the VALU test per pair (q1, q2, D, t: 5 FMAs + 1 multiply)
+FLOP_PER_PAIR = 11  # k_pnp_score_mf: f32 flops of the VALU test per pair (q1, q2, D, t: 5 FMAs = 10 + 1 multiply)
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, dense f16 matrix peak
 MFMA_FLOP_PER_PAIR = 32 * 32 * 16 * 2 / 256  # one v_mfma_f32_32x32x16_f16 per 8 hypotheses x 32 points
 
@@ -58,7 +60,9 @@ def parse():
     ap.add_argument("--points", type=int, default=10_000)
     ap.add_argument("--hyps", type=int, default=100_000, help="hypotheses per GPU per step")
     ap.add_argument("--thr", type=float, default=30.0)
-    ap.add_argument("--cpu-hyps", type=int, default=150_000, help="CPU baseline sample (hypotheses, 1 thread)")
+    ap.add_argument("--cpu-hyps", type=int, default=100_000, help="CPU baseline sample (hypotheses, 1 thread)")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0),
+                    help="threads of the CPU baseline's multi-core leg (default: OMP_NUM_THREADS, else all cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ms-to-best", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C3/C4/C5, location-search and DEM-march lines")
@@ -147,11 +151,14 @@ def main():
         elapsed = float(et.item())
 
     cnt = int(key_t.item()) >> 32
-    # kernel times of the same call, from the HIP events of a synchronous run (outside the timed loop)
-    for _ in range(3):
+    # kernel times of the same call, from the HIP events of synchronous runs (outside the timed
+    # loop): score_ms spans the scoring kernel alone (k_pnp_score_mf), solve_ms k_pnp_solve
+    for _ in range(10):
         _, _, info = rsac.evaluate_range(ev.p2, ev.p3, K, base, H, args.thr, return_info=True, device=local)
         score_ms.append(info.score_ms)
         solve_ms.append(info.solve_ms)
+    # N > 1: the other BASELINE configs across the ranks (collectives: every rank takes part)
+    multi = multi_gpu_legs(local, args, pr) if (dist is not None and not args.no_extras) else None
 
     out = None
     if rank == 0:
@@ -159,7 +166,7 @@ def main():
         value = hyps_total / elapsed
         score_avg = statistics.mean(score_ms)
         solve_avg = statistics.mean(solve_ms)
-        achieved = args.points * BYTES_PER_POINT * H / (score_avg * 1e-3) / 1e9
+        algo_gbs = args.points * BYTES_PER_POINT * H / (score_avg * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_score_kernel.json")
         if os.path.exists(pmc):
@@ -169,28 +176,41 @@ def main():
                     traffic = d.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        # the issue-side roofline of the same launch: VALU wave-instructions per second (PMC count
-        # of a profiled run of this command, profiles/pmc_score_valu.json) against the wave64
-        # issue peak, 1024 SIMDs x 1 instruction / 2 cycles at the 2.4 GHz peak clock; and the
-        # algorithmic f32 flops (31 per pair: the 16.5 instructions, FMAs counted twice) against
-        # the 157.3 TFLOP/s vector peak
-        roof_valu = None
-        pv = os.path.join(ROOT, "profiles", "pmc_score_valu.json")
+        # The binding roof of k_pnp_score_mf is VALU issue: the kernel re-reads its
+        # 400 kB of point operands from L2, so HBM is far from busy.  achieved = VALU
+        # wave-instructions per launch (SQ_INSTS_VALU, PMC pass of this same command,
+        # profiles/pmc_score_valu.json) / the kernel's average duration measured here (HIP events
+        # around the scoring kernel alone); peak = 1024 SIMDs x 1 wave64 instruction / 2 cycles at
+        # 2.4 GHz.  HBM traffic (FETCH_SIZE x 2 + WRITE_SIZE, profiles/pmc_score_kernel.json) and
+        # its rate are reported beside it, and SURVEY §8d's algorithmic bytes (20 B per pair) as
+        # a rate, which is not an HBM rate (it exceeds the HBM peak many times).
         pairs = args.points * H
-        tflops = pairs * FLOP_PER_PAIR / (score_avg * 1e-3) / 1e12
-        roof_valu = {"bound": "valu", "flop_per_pair": FLOP_PER_PAIR, "achieved_tflops": tflops,
-                     "peak_tflops": VALU_PEAK_TFLOPS, "frac_flops": tflops / VALU_PEAK_TFLOPS}
+        valu_instr = None
+        pv = os.path.join(ROOT, "profiles", "pmc_score_valu.json")
         if os.path.exists(pv):
             try:
                 d = json.load(open(pv))
                 if d.get("points") == args.points and d.get("hyps") == H:
-                    ips = d["valu_instr_per_launch"] / (score_avg * 1e-3)
-                    roof_valu.update({"achieved": ips / 1e9, "peak": VALU_ISSUE_PEAK / 1e9, "unit": "G wave-instr/s",
-                                      "frac": ips / VALU_ISSUE_PEAK,
-                                      "valu_instr_per_launch": d["valu_instr_per_launch"],
-                                      "effective_clock_ghz_profiled": d.get("effective_clock_ghz")})
+                    valu_instr = d["valu_instr_per_launch"]
             except Exception:
-                pass
+                valu_instr = None
+        t_s = score_avg * 1e-3
+        roofline = {"bound": "valu_issue", "kernel": "k_pnp_score_mf",
+                    "span": "HIP events around the scoring kernel alone (k_pnp_score_mf; the k_best_key "
+                            "reduction follows the second event), mean of 10 synchronous launches",
+                    "kernel_ms": score_avg, "traffic": traffic,
+                    "valu_instr_per_launch": valu_instr, "peak": VALU_ISSUE_PEAK / 1e9,
+                    "unit": "G VALU wave-instructions/s"}
+        if valu_instr:
+            roofline.update({"achieved": valu_instr / t_s / 1e9, "frac": valu_instr / t_s / VALU_ISSUE_PEAK})
+        else:
+            roofline.update({"achieved": None, "frac": None, "note": "no PMC count for this workload"})
+        if traffic:
+            roofline.update({"hbm_gbs": traffic / t_s / 1e9, "hbm_frac": traffic / t_s / 1e9 / HBM_PEAK_GBS})
+        roofline.update({"algorithmic_bytes_per_launch": args.points * BYTES_PER_POINT * H,
+                         "algorithmic_gbs": algo_gbs,
+                         "f32_vector_tflops": pairs * FLOP_PER_PAIR / t_s / 1e12,
+                         "f32_vector_frac": pairs * FLOP_PER_PAIR / t_s / 1e12 / VALU_PEAK_TFLOPS})
         ms_to_best = None
         if not args.no_ms_to_best:
             walls = []
@@ -241,18 +261,15 @@ def main():
             "pcie_inclusive_hyp_s": pcie_rate,
             "best_inliers": int(cnt),
             "kernels_ms": {"pnp_solve": solve_avg, "pnp_score": score_avg},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "scoring stage (HIP events): k_pnp_score_mf (flagged windows recounted inside, variant 98) + k_best_key",
-                         "algorithmic_bytes_per_launch": args.points * BYTES_PER_POINT * H},
-            "roofline_valu": roof_valu,
+            "roofline": roofline,
             "roofline_mfma": {"bound": "mfma", "flop_per_pair": MFMA_FLOP_PER_PAIR,
-                              "achieved": pairs * MFMA_FLOP_PER_PAIR / (score_avg * 1e-3) / 1e12,
+                              "achieved": pairs * MFMA_FLOP_PER_PAIR / t_s / 1e12,
                               "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                              "frac": pairs * MFMA_FLOP_PER_PAIR / (score_avg * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS,
+                              "frac": pairs * MFMA_FLOP_PER_PAIR / t_s / 1e12 / MFMA_PEAK_TFLOPS,
                               "note": "f16 matrix flops of the projection (hi/lo operands), dense peak"},
             "cpu_baseline": cpu,
             "extras": extras,
+            "multi_gpu": multi,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -261,17 +278,57 @@ def main():
     return out
 
 
+def c3_problems():
+    """BASELINE.json configs[2]: 1024 problems x 2000 points (synth seeds 1..1024), concatenated."""
+    probs = [synth.pnp_problem(2000, 0.5, seed=s) for s in range(1, 1025)]
+    off = np.zeros(1025, np.int64)
+    off[1:] = np.cumsum([len(p["points3d"]) for p in probs])
+    return (np.concatenate([p["points2d"] for p in probs]), np.concatenate([p["points3d"] for p in probs]), off,
+            np.stack([p["K"] for p in probs]))
+
+
+def multi_gpu_legs(local, args, pr2):
+    """N > 1 (every rank): the other BASELINE configs across the GPUs, each timed between barriers,
+    max over ranks, median of 3 -- C3 (configs[2]: problem chunks per rank, one all-gather of the
+    per-problem rows), C5 (configs[4]: sharded adaptive LO-RANSAC, per-round all-gather of the
+    {status, count} rows), and ms-to-best-model of C2 through the sharded adaptive loop."""
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    dev = torch.device("cuda", local)
+    sync = torch.cuda.synchronize
+    out = {}
+    p2, p3, off, Ks = c3_problems()
+    g2, g3 = torch.from_numpy(p2).to(dev), torch.from_numpy(p3).to(dev)
+    run = par.pnp_batched_rows(g2, g3, off, Ks, 1024, args.thr, adaptive=False, refine=False)
+    rows, w = par.c3_problem_shards(run, 1024, sync=sync, repeats=3)
+    rows = rows.cpu().numpy()
+    out["c3_problem_shards"] = {"problems": 1024, "points": 2000, "hyps_per_problem": 1024, "ms": w * 1e3,
+                                "hyp_s": 1024 * 1024 / w, "problems_ok": int(rows[:, 0].sum()),
+                                "inliers_total": int(rows[:, 1].sum()),
+                                "note": f"{-(-1024 // world)} problems per rank, pnp_ransac_batched_flat on each "
+                                        "rank's chunk (inputs in HBM), one all-gather of (ok, inliers, R, t) rows"}
+    p5 = synth.pnp_problem(100_000, 0.5, seed=3)
+    ev5 = par.PnPShard(p5["points2d"], p5["points3d"], p5["K"], args.thr, device=local)
+    r5, w5 = par.adaptive_shards(ev5, 5000, 0.99, round_size=4096, lo=True, sync=sync)
+    out["c5_sharded_lo"] = {"points": 100_000, "ms_to_best": w5 * 1e3, "best": r5.best, "iters": r5.iters,
+                            "n_inliers": r5.n_inliers, "lo_improvements": r5.lo_improvements,
+                            "note": "sharded_ransac(lo=True): rounds of 4096 split over the ranks, all-gather of "
+                                    "the rows (RCCL), device-listed scan, LO on every rank"}
+    ev2 = par.PnPShard(pr2["points2d"], pr2["points3d"], pr2["K"], args.thr, device=local)
+    r2, w2 = par.adaptive_shards(ev2, 5000, 0.99, round_size=4096, lo=False, sync=sync)
+    out["ms_to_best_sharded"] = {"ms": w2 * 1e3, "best": r2.best, "iters": r2.iters, "n_inliers": r2.n_inliers,
+                                 "note": "C2 problem, sharded_ransac (adaptive, no refit), max over ranks"}
+    return out
+
+
 def extra_workloads(local, args):
     """Secondary lines (not `value`): C3 of BASELINE.json (1024 problems x 2000 points, 1024
     hypotheses each, one batched call) and the 458-location search of main_v1.py:274/862."""
     out = {}
-    probs = [synth.pnp_problem(2000, 0.5, seed=s) for s in range(1, 1025)]
-    off = np.zeros(1025, np.int64)
-    off[1:] = np.cumsum([len(p["points3d"]) for p in probs])
+    h2, h3, off, Ks = c3_problems()
     dev = torch.device("cuda", local)
-    p2 = torch.from_numpy(np.concatenate([p["points2d"] for p in probs])).to(dev)
-    p3 = torch.from_numpy(np.concatenate([p["points3d"] for p in probs])).to(dev)
-    Ks = np.stack([p["K"] for p in probs])
+    p2 = torch.from_numpy(h2).to(dev)
+    p3 = torch.from_numpy(h3).to(dev)
 
     def c3(p2_, p3_):
         walls = []
@@ -415,12 +472,16 @@ def cpu_baseline_dem(args, n_rays=3):
 
 
 def cpu_baseline(pr, args):
-    """The CPU restatement (oracle/, C, 1 thread) on a bounded sample of the same workload."""
+    """The CPU restatement (oracle/, C, gcc -O2) on bounded samples of the same workloads, on this
+    host: C2 on 1 thread (`value`) and on `threads` OpenMP threads, C2 ms-to-best (OpenCV's
+    sequential loop, stopping at the iteration bound), C3 (problems over the threads), C4 and C5."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import pyoracle as O
     except Exception as e:  # oracle not built
         return {"value": None, "error": str(e)}
+    from concurrent.futures import ThreadPoolExecutor
+    threads = args.cpu_threads or os.cpu_count() or 1
     soa = O.soa_pnp(pr["points3d"], pr["points2d"])
     cam = O.cam_from_K(pr["K"])
     n = args.cpu_hyps
@@ -428,6 +489,38 @@ def cpu_baseline(pr, args):
     t = time.perf_counter()
     O.pnp_hypotheses(soa, cam, args.thr, 0x5EED, n)
     dt = time.perf_counter() - t
+    n_mt = n * max(1, min(threads, 16))
+    t = time.perf_counter()
+    O.pnp_hypotheses_mt(soa, cam, args.thr, 0x5EED, n_mt, threads=threads)
+    dt_mt = time.perf_counter() - t
+    walls = []
+    for _ in range(5):
+        t = time.perf_counter()
+        O.pnp_ransac_seq(pr["points3d"], pr["points2d"], pr["K"], args.thr, 0.99, 5000)
+        walls.append(time.perf_counter() - t)
+    c2_best_ms = statistics.median(walls) * 1e3
+    # C3: 128 of the 1024 problems (seeds 1..128), 1024 hypotheses each, problems over the threads
+    probs = [synth.pnp_problem(2000, 0.5, seed=s) for s in range(1, 129)]
+
+    def c3_one(p):
+        s3 = O.soa_pnp(p["points3d"], p["points2d"])
+        return O.pnp_hypotheses(s3, O.cam_from_K(p["K"]), args.thr, 0x5EED, 1024)
+
+    t = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(c3_one, probs))
+    dt_c3 = time.perf_counter() - t
+    # C4: 1500 fundamental-matrix hypotheses over the 50k matches, 1 thread
+    p4 = synth.fundamental_problem(50_000, 0.8, seed=2)
+    s4 = O.soa_hom(p4["pts1"], p4["pts2"])
+    t = time.perf_counter()
+    O.fm_hypotheses(s4, 1.5, 0x5EED, 1500)
+    dt_c4 = time.perf_counter() - t
+    # C5: LO-RANSAC to the best model on the 100k-point problem, 1 thread
+    p5 = synth.pnp_problem(100_000, 0.5, seed=3)
+    t = time.perf_counter()
+    r5 = O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000)
+    dt_c5 = time.perf_counter() - t
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -439,7 +532,19 @@ def cpu_baseline(pr, args):
     return {"value": n / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
             "sample": f"{n} hypotheses of the same C2 problem (10k points), oracle/rsac_oracle.c -O2, 1 thread, "
                       f"{dt:.1f} s",
-            "cpu_model": model, "os_cpu_count": os.cpu_count()}
+            "cpu_model": model, "os_cpu_count": os.cpu_count(), "threads": threads,
+            "c2_mt": {"value": n_mt / dt_mt, "unit": "hypotheses/s", "cores": threads,
+                      "sample": f"{n_mt} hypotheses, OpenMP over {threads} threads, {dt_mt:.1f} s"},
+            "c2_ms_to_best": {"ms": c2_best_ms, "cores": 1,
+                              "sample": "OpenCV's sequential loop (orc_pnp_ransac_seq), stops at the iteration "
+                                        "bound, no refit, median of 5"},
+            "c3": {"hyp_s": 128 * 1024 / dt_c3, "cores": threads,
+                   "sample": f"128 of the 1024 problems x 1024 hypotheses, problems over {threads} threads, "
+                             f"{dt_c3:.1f} s"},
+            "c4": {"hyp_s": 1500 / dt_c4, "cores": 1, "sample": f"1500 hypotheses, 50k matches, {dt_c4:.1f} s"},
+            "c5": {"ms_to_best": dt_c5 * 1e3, "iters": r5["iters"], "lo_improvements": r5["lo_improvements"],
+                   "cores": 1, "sample": "orc_pnp_ransac_lo on the 100k-point problem (all 5000 hypotheses scored, "
+                                         "then the scan with LO)"}}
 
 
 if __name__ == "__main__":

@@ -1600,10 +1600,10 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
 static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const void *b_pts, int32_t n, const double *K,
                            int64_t hyp_begin, int32_t H, double thr, uint64_t seed, uint32_t flags,
                            const int32_t *subsets, int32_t *counts_out, int8_t *status_out, double *models_out,
-                           void *stream) {
+                           void *stream, int32_t *rows_out = nullptr) {
     int r = check_device(c);
     if (r) return r;
-    if (H <= 0 || !counts_out || !status_out) return fail(RSAC_EINVAL, "bad arguments");
+    if (H <= 0 || (!rows_out && (!counts_out || !status_out))) return fail(RSAC_EINVAL, "bad arguments");
     if (model == Model::PnP && !K) return fail(RSAC_EINVAL, "K required");
     if (model == Model::Fm && subsets) return fail(RSAC_EINVAL, "the fundamental-matrix sampler is Philox only");
     hipStream_t s = pick_stream(c, stream);
@@ -1657,6 +1657,18 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
             HIPCHK(launch_hom_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
         }
     }
+    if (flags & RSAC_F_DEVICE_OUT) {  // device outputs: enqueued, no wait
+        if (rows_out) {
+            HIPCHK(launch_pack_rows(c->status.as<int8_t>(), c->counts.as<int32_t>(), H, rows_out, s));
+        } else {
+            HIPCHK(hipMemcpyAsync(counts_out, c->counts.p, sizeof(int32_t) * H, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(status_out, c->status.p, H, hipMemcpyDeviceToDevice, s));
+        }
+        if (models_out)
+            HIPCHK(hipMemcpyAsync(models_out, c->models.p, sizeof(double) * kModelStride * H,
+                                  hipMemcpyDeviceToDevice, s));
+        return RSAC_OK;
+    }
     HIPCHK(hipMemcpyAsync(counts_out, c->counts.p, sizeof(int32_t) * H, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(status_out, c->status.p, H, hipMemcpyDeviceToHost, s));
     if (models_out)
@@ -1671,6 +1683,69 @@ int rsac_pnp_hypotheses(rsac_ctx *c, const void *pts3d, const void *pts2d, int32
                         void *stream) {
     return hypotheses_core(c, Model::PnP, pts3d, pts2d, n, K, hyp_begin, n_hyps, thr, seed, flags, subsets,
                            counts_out, status_out, models_out, stream);
+}
+
+int rsac_pnp_hypothesis_rows(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                             int64_t hyp_begin, int32_t n_hyps, double thr, uint64_t seed, uint32_t flags,
+                             int32_t *rows_out, void *stream) {
+    if (!rows_out) return fail(RSAC_EINVAL, "rows_out required");
+    return hypotheses_core(c, Model::PnP, pts3d, pts2d, n, K, hyp_begin, n_hyps, thr, seed, flags | RSAC_F_DEVICE_OUT,
+                           nullptr, nullptr, nullptr, nullptr, stream, rows_out);
+}
+
+int rsac_scan_device(rsac_ctx *c, rsac_scan_state *st, const int32_t *rows, int64_t count, int32_t n,
+                     int32_t model_points, double confidence, int32_t stop_on_improve, int32_t *improved,
+                     void *stream) {
+    int r = check_device(c);
+    if (r) return r;
+    if (!st || count < 0 || count > INT32_MAX || n <= 0 || (count > 0 && !rows)) return fail(RSAC_EINVAL, "bad arguments");
+    if (improved) *improved = 0;
+    if (st->done || count == 0) return RSAC_OK;
+    hipStream_t s = pick_stream(c, stream);
+    const int32_t floor0 = std::max(st->max_good, model_points - 1);
+    HIPCHK(c->h_scanrec.ensure(sizeof(ScanRecords)));
+    ScanRecords *rec = c->h_scanrec.as<ScanRecords>();
+    HIPCHK(launch_scan_rows(rows, (int32_t)count, floor0, rec, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (rec->nrec < 0) {  // more improvements than records: scan the copied rows exactly
+        std::vector<int32_t> h(2 * (size_t)count), cn((size_t)count);
+        std::vector<int8_t> sv((size_t)count);
+        HIPCHK(hipMemcpyAsync(h.data(), rows, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int64_t i = 0; i < count; ++i) {
+            sv[i] = (int8_t)h[2 * i];
+            cn[i] = h[2 * i + 1];
+        }
+        int32_t imp = 0;
+        r = stop_on_improve ? rsac_scan_until_best(st, cn.data(), sv.data(), count, n, model_points, confidence, &imp)
+                            : rsac_scan(st, cn.data(), sv.data(), count, n, model_points, confidence);
+        if (improved) *improved = imp;
+        return r;
+    }
+    // scan_step over the rows, replayed on the records: nothing changes between records
+    const int64_t begin = st->iter, end = begin + count, neg = begin + rec->first_neg;
+    for (int k = 0; k < rec->nrec; ++k) {
+        const int64_t pos = begin + rec->idx[k];
+        if (pos >= std::min<int64_t>(neg, st->niters)) break;
+        st->best = pos;
+        st->max_good = rec->cnt[k];
+        st->niters = update_num_iters(confidence, (double)(n - rec->cnt[k]) / n, model_points, (int)st->niters);
+        if (stop_on_improve) {
+            st->iter = pos + 1;
+            if (st->iter >= st->niters) st->done = 1;
+            if (improved) *improved = 1;
+            return RSAC_OK;
+        }
+    }
+    const int64_t stop = std::min<int64_t>(neg, st->niters);
+    if (stop < end) {
+        st->iter = std::max(stop, begin);
+        st->done = 1;
+    } else {
+        st->iter = end;
+        st->done = end >= st->niters;
+    }
+    return RSAC_OK;
 }
 
 int rsac_homography_hypotheses(rsac_ctx *c, const void *src, const void *dst, int32_t n, int64_t hyp_begin,

@@ -118,6 +118,11 @@ struct ScanDecide {
 hipError_t launch_scan_records(const int32_t *counts, const int8_t *status, int64_t stride, int32_t P, int32_t H,
                                int model_points, ScanRecords *out, hipStream_t s, ScanDecide dec = ScanDecide());
 
+// the multi-GPU adaptive scan (rsac_scan_device): records of a gathered round of {status, count}
+// rows above floor0 -> *out (pinned host memory); rows of one problem's (status, counts)
+hipError_t launch_scan_rows(const int32_t *rows, int32_t count, int32_t floor0, ScanRecords *out, hipStream_t s);
+hipError_t launch_pack_rows(const int8_t *status, const int32_t *counts, int32_t H, int32_t *rows, hipStream_t s);
+
 // best packed key of counts[0, H) (+ its model record -> model_out[16]);
 // key = 0 when no hypothesis has a model with >= 1 inlier
 hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t H, int64_t hyp_begin,

@@ -1943,6 +1943,67 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
     }
 }
 
+// The record pass of rsac_scan_device (the multi-GPU adaptive loop's scan of a gathered round):
+// one wave over rows [0, count) of {status, count} int32 pairs: the strict prefix maxima above
+// floor0 (every improvement a sequential scan could make there, in order; the host applies the
+// iteration bound), at most kScanRecs, and the first status < 0.  out: pinned host memory.
+__global__ __launch_bounds__(64) void k_scan_rows(const int32_t *__restrict__ rows, int32_t count, int32_t floor0,
+                                                  ScanRecords *__restrict__ out) {
+    __shared__ int32_t ridx[kScanRecs], rcnt[kScanRecs];
+    const int lane = threadIdx.x;
+    int floor_c = floor0, nrec = 0, first_neg = count;
+    for (int b = 0; b < count; b += 64) {
+        const int i = b + lane;
+        const int sv = i < count ? rows[2 * i] : 0;
+        const uint64_t neg = __ballot(sv < 0);
+        const int lim = neg ? b + __builtin_ctzll(neg) : count;
+        const int v = (i < lim && sv > 0) ? rows[2 * i + 1] : -1;
+        uint64_t cand = __ballot(v > floor_c);
+        while (cand) {
+            const int l = __builtin_ctzll(cand);
+            const int cv = __shfl(v, l);
+            if (nrec < kScanRecs && lane == 0) {
+                ridx[nrec] = b + l;
+                rcnt[nrec] = cv;
+            }
+            ++nrec;
+            floor_c = cv;
+            cand = __ballot(v > floor_c && lane > l);
+        }
+        if (neg) {
+            first_neg = lim;
+            break;
+        }
+    }
+    if (lane == 0) {
+        out->nrec = nrec <= kScanRecs ? nrec : -1;
+        out->first_neg = first_neg;
+        for (int r = 0; r < nrec && r < kScanRecs; ++r) {
+            out->idx[r] = ridx[r];
+            out->cnt[r] = rcnt[r];
+        }
+    }
+}
+
+hipError_t launch_scan_rows(const int32_t *rows, int32_t count, int32_t floor0, ScanRecords *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_rows, dim3(1), dim3(64), 0, s, rows, count, floor0, out);
+    return hipGetLastError();
+}
+
+// {status, count} rows of hypotheses [0, H) of problem 0 (the multi-GPU round's exchange format)
+__global__ void k_pack_rows(const int8_t *__restrict__ status, const int32_t *__restrict__ counts, int32_t H,
+                            int32_t *__restrict__ rows) {
+    for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x)
+        reinterpret_cast<int2 *>(rows)[h] = make_int2((int)status[h], counts[h]);
+}
+
+hipError_t launch_pack_rows(const int8_t *status, const int32_t *counts, int32_t H, int32_t *rows, hipStream_t s) {
+    unsigned g = (unsigned)((std::max(H, 1) + 255) / 256);
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_pack_rows, dim3(g), dim3(256), 0, s, status, counts, H, rows);
+    return hipGetLastError();
+}
+
 hipError_t launch_scan_records(const int32_t *counts, const int8_t *status, int64_t stride, int32_t P, int32_t H,
                                int model_points, ScanRecords *out, hipStream_t s, ScanDecide dec) {
     hipLaunchKernelGGL(k_scan_records, dim3((P + 3) / 4), dim3(256), 0, s, counts, status, stride, P, H, model_points,

@@ -102,6 +102,8 @@ SIGNATURES = [
     ("rsac_scan", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d]),
     ("rsac_pnp_refine_lm", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("rsac_pnp_reprojection_errors", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
+    ("rsac_pnp_hypothesis_rows", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i64, _i32, _d, _u64, _u32, _vp, _vp]),
+    ("rsac_scan_device", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d, _i32, _vp, _vp]),
     ("rsac_pnp_orientation_sweep", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _i32, _d, _d, _u64, _u32, _i32, _vp,
                                              _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 ]

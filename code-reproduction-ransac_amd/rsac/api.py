@@ -417,6 +417,27 @@ def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_th
     return out
 
 
+def hypothesis_rows(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_thresh: float, rows, *,
+                    seed: int = 0x5EED):
+    """{status, count} int32 rows of Philox hypotheses [hyp_begin, hyp_begin + n_hyps) written into
+    the device tensor ``rows`` (at least (n_hyps, 2) int32, contiguous) on the inputs' stream, without
+    waiting -- the multi-GPU round's exchange format (rsac_pnp_hypothesis_rows)."""
+    import torch
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    if not (p3.device and rows.is_cuda and rows.dtype == torch.int32 and rows.is_contiguous()
+            and rows.shape[0] >= n_hyps and rows.shape[-1] == 2):
+        raise ValueError("hypothesis_rows needs GPU tensor inputs and an (n, 2) int32 contiguous device tensor")
+    ctx = L.context(_device_of(p3, None))
+    with ctx.lock:
+        L.check(L.lib().rsac_pnp_hypothesis_rows(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), p3.n,
+                                                 _K9(K).ctypes.data, int(hyp_begin), int(n_hyps),
+                                                 float(reproj_thresh), int(seed) & (2**64 - 1),
+                                                 L.F_DEVICE_IN | L.F_DEVICE_OUT, C.c_void_p(rows.data_ptr()),
+                                                 _stream_of(p3)))
+    return rows
+
+
 def winner(points2D, points3D, K, key, reproj_thresh: float = 30.0, *, seed: int = 0x5EED, with_mask: bool = True):
     """Re-derive the hypothesis named by a device packed key (e.g. after an all-reduce) on this
     GPU: (model12 tensor, mask tensor) without a host round trip (rsac_pnp_winner)."""
@@ -799,6 +820,32 @@ class Scan:
         L.check(L.lib().rsac_scan_until_best(C.byref(self.st), c.ctypes.data, st.ctypes.data, c.size, self.n, self.s,
                                              self.conf, C.byref(imp)))
         self.improved = bool(imp.value)
+        return self.iters - before
+
+    def step_rows(self, rows, count: int, stop_on_improve: bool = False) -> int:
+        """Consume the first ``count`` {status, count} rows of an (m, 2) int32 array or tensor (a
+        gathered multi-GPU round).  GPU tensors are scanned on the device (rsac_scan_device: only
+        the improvements come to the host).  Returns the rows consumed (``improved`` is set when
+        stop_on_improve stopped at a new best)."""
+        before = self.iters
+        if _is_torch(rows) and rows.is_cuda:
+            import torch
+            r = rows[:count]
+            if not r.is_contiguous() or r.dtype != torch.int32:
+                r = r.to(torch.int32).contiguous()
+            imp = C.c_int32(0)
+            ctx = L.context(r.device.index)
+            with ctx.lock:
+                L.check(L.lib().rsac_scan_device(ctx.handle, C.byref(self.st), C.c_void_p(r.data_ptr()), int(count),
+                                                 self.n, self.s, self.conf, 1 if stop_on_improve else 0, C.byref(imp),
+                                                 C.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)))
+            self.improved = bool(imp.value)
+            return self.iters - before
+        a = np.asarray(rows.cpu() if _is_torch(rows) else rows)[:count]
+        if stop_on_improve:
+            return self.step_until_best(a[:, 1], a[:, 0].astype(np.int8))
+        self.step(a[:, 1], a[:, 0].astype(np.int8))
+        self.improved = False
         return self.iters - before
 
     def raise_count(self, count: int):

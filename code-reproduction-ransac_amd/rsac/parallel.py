@@ -4,25 +4,28 @@ SURVEY.md §8e.  Two ways the hot path shards, both without moving point data:
 
 * one problem's hypothesis space (C2, C5): rank r owns a contiguous range of hypothesis
   indices.  Hypothesis i is the Philox draw (seed, i), so the set scored does not depend
-  on the GPU count.  The only exchange is an all-reduce(MAX) of the packed key
-  ``count << 32 | (0xFFFFFFFF - i)``: highest count, lowest index on ties -- the same
-  winner as OpenCV's sequential "first strictly greater" loop (ptsetreg.cpp run()).  The
-  winning model is re-derived from its index on every rank (one P3P solve), so no model
-  broadcast is needed.
+  on the GPU count.
+  - Fixed budget (``sharded_best``): the only exchange is an all-reduce(MAX) of the packed key
+    ``count << 32 | (0xFFFFFFFF - i)``: highest count, lowest index on ties -- the same winner as
+    OpenCV's sequential "first strictly greater" loop (ptsetreg.cpp run()).  The winning model is
+    re-derived from its index on every rank (one P3P solve), so no model broadcast is needed.
+  - Adaptive (``sharded_ransac``, OpenCV's iteration semantics): each round's {status, count}
+    rows are written on the device by every rank for its chunk, all-gathered into one device
+    buffer (RCCL), and every rank runs the same sequential scan over it (rsac_scan_device: the
+    improvements are listed on the device, the host applies the iteration bound), so best index,
+    inlier count and iteration count equal the single-GPU rsac.pnp_ransac result.  With LO the
+    scan stops at each new best, every rank re-derives the model from its index on its GPU and
+    runs the same deterministic local optimisation.
 * independent problems (C3, the K sweep of testpro-K.py:58-75, the location loop of
-  main_v1.py:274): problems are split contiguously across ranks and a single all-gather
-  of the fixed-size per-problem results ends the call.
-
-The adaptive loop (``sharded_ransac``) keeps OpenCV's iteration-count semantics exactly:
-each round's per-hypothesis counts are gathered from every rank and every rank runs the
-same sequential scan (rsac_scan), so best index, inlier count and iteration count equal
-the single-GPU rsac.pnp_ransac result for the same seed.
+  main_v1.py:274): problems are split in contiguous chunks across ranks and a single all-gather
+  of the fixed-size per-problem rows ends the call.
 
 The evaluator is injectable: ``PnPShard`` runs the HIP kernels of this package; the CPU
 tests drive the same code with the gloo backend and a restatement-backed evaluator.
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -39,6 +42,14 @@ def shard(n: int, rank: int, world: int) -> tuple[int, int]:
     base, rem = divmod(int(n), int(world))
     begin = rank * base + min(rank, rem)
     return begin, base + (1 if rank < rem else 0)
+
+
+def chunk(n: int, rank: int, world: int) -> tuple[int, int, int]:
+    """Contiguous split of range(n) in chunks of equal width w = ceil(n / world) (the last ones
+    shorter or empty), the layout of an all-gather of equal-size tensors: (begin, count, w)."""
+    w = -(-int(n) // int(world)) if n > 0 else 0
+    b = min(rank * w, int(n))
+    return b, max(0, min(w, int(n) - b)), w
 
 
 def pack_key(count: int, index: int) -> int:
@@ -69,7 +80,7 @@ def _rank_world(group):
 
 
 def _comm_device(group):
-    if dist.get_backend(group) == "nccl":
+    if dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
 
@@ -84,23 +95,17 @@ def all_reduce_max_key(key: int, group=None) -> int:
     return int(t.item())
 
 
-def _all_gather_rows(arr: np.ndarray, group) -> list[np.ndarray]:
-    """All-gather of a ragged first axis (pads to the longest, one collective for sizes + one for data)."""
+def all_gather_chunks(t: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather of equal-size tensors (one per rank, first axis = the rank's chunk) into one
+    tensor in rank order, on the tensor's device (RCCL for device tensors, no host copy)."""
     _, world = _rank_world(group)
     if world == 1:
-        return [arr]
-    dev = _comm_device(group)
-    n = torch.tensor([arr.shape[0]], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
-    m = max(sizes)
-    pad = np.zeros((m,) + arr.shape[1:], arr.dtype)
-    pad[:arr.shape[0]] = arr
-    t = torch.from_numpy(pad).to(dev)
-    outs = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(outs, t, group=group)
-    return [o.cpu().numpy()[:s] for o, s in zip(outs, sizes)]
+        return t
+    dev = _comm_device(group)  # a gloo rehearsal on GPU tensors goes through the host
+    src = t.to(dev).contiguous()
+    out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=dev)
+    dist.all_gather_into_tensor(out, src, group=group)
+    return out if out.device == t.device else out.to(t.device)
 
 
 class PnPShard:
@@ -123,15 +128,24 @@ class PnPShard:
         st, cn, _ = api.hypotheses("pnp", self.p3, self.p2, self.K, begin, count, self.thr, seed=self.seed)
         return st, cn
 
+    def round_rows(self, begin: int, count: int, width: int) -> torch.Tensor:
+        """{status, count} int32 rows of hypotheses [begin, begin + count), padded to ``width``
+        rows, on this GPU (written by the kernels, nothing waits)."""
+        rows = torch.zeros((max(width, 1), 2), dtype=torch.int32, device=self.p3.device)
+        if count > 0:
+            api.hypothesis_rows(self.p2, self.p3, self.K, begin, count, self.thr, rows, seed=self.seed)
+        return rows[:width]
+
     def model(self, index: int) -> np.ndarray:
-        """(R 9 row-major, t 3) of hypothesis ``index``, re-derived from its Philox counter."""
-        _, _, m = api.hypotheses("pnp", self.p3, self.p2, self.K, index, 1, self.thr, seed=self.seed)
-        return m[0, :12].copy()
+        """(R 9 row-major, t 3) of hypothesis ``index``, re-derived on this GPU from its Philox counter."""
+        key = torch.tensor([pack_key(1, index)], dtype=torch.int64, device=self.p3.device)
+        m, _ = api.winner(self.p2, self.p3, self.K, key, self.thr, seed=self.seed, with_mask=False)
+        return m.cpu().numpy()
 
     def local_opt(self, model12, count: int):
-        """LO-RANSAC step on this rank's copy of the points (identical on every rank)."""
-        m, c, _ = api.local_opt(self.p2, self.p3, self.K, model12, self.thr)
-        return m, c
+        """LO-RANSAC step on this rank's copy of the points (identical on every rank)
+        -> (model12, inlier count, refits that raised it)."""
+        return api.local_opt(self.p2, self.p3, self.K, model12, self.thr)
 
     def mask(self, model12) -> np.ndarray:
         m, _ = api.pose_mask(self.p2, self.p3, self.K, model12, self.thr)
@@ -144,6 +158,7 @@ class ShardedResult:
     n_inliers: int
     iters: int  # hypotheses consumed by the (adaptive) scan
     model: np.ndarray | None  # (R 9, t 3)
+    lo_improvements: int = 0
 
 
 def sharded_best(ev, n_total: int, group=None) -> ShardedResult:
@@ -158,73 +173,143 @@ def sharded_best(ev, n_total: int, group=None) -> ShardedResult:
     return ShardedResult(idx, cnt, n_total, ev.model(idx))
 
 
+def _round_rows(ev, begin: int, count: int, width: int, device) -> torch.Tensor:
+    if hasattr(ev, "round_rows"):
+        return ev.round_rows(begin, count, width)
+    rows = torch.zeros((width, 2), dtype=torch.int32, device=device)
+    if count > 0:
+        st, cn = ev.hypotheses(begin, count)
+        rows[:count, 0] = torch.as_tensor(np.asarray(st, np.int32))
+        rows[:count, 1] = torch.as_tensor(np.asarray(cn, np.int32))
+    return rows
+
+
 def sharded_ransac(ev, max_iters: int, confidence: float = 0.99, round_size: int = 4096, group=None,
                    model_points: int = 4, lo: bool = False) -> ShardedResult:
     """Adaptive RANSAC (OpenCV iteration semantics) with each round's hypotheses split over ranks.
 
-    lo=True: LO-RANSAC (BASELINE.json configs[4]); the scan stops at every new best, every rank
-    runs the same (deterministic) local optimisation on its copy of the points, and the scan
-    continues with the raised count -- the single-GPU rsac.pnp_ransac(lo=True) result.
+    Per round: every rank writes the {status, count} rows of its chunk (on its GPU for
+    PnPShard), one all-gather assembles the round in hypothesis order on every rank, and every
+    rank scans it identically (device-listed improvements for GPU rows).  lo=True: LO-RANSAC
+    (BASELINE.json configs[4]); the scan stops at every new best, every rank runs the same
+    (deterministic) local optimisation on its copy of the points, and the scan continues with
+    the raised count -- the single-GPU rsac.pnp_ransac(lo=True) result.
     """
     rank, world = _rank_world(group)
+    dev = _comm_device(group)
     scan = api.Scan(max_iters, ev.n, confidence, model_points)
     hb = 0
     best_model = None
+    n_lo = 0
     while not scan.done and hb < max_iters:
         hr = min(int(round_size), max_iters - hb, scan.niters - hb)
-        b, c = shard(hr, rank, world)
-        st, cn = ev.hypotheses(hb + b, c) if c > 0 else (np.zeros(0, np.int8), np.zeros(0, np.int32))
-        rows = np.zeros((c, 2), np.int32)
-        rows[:, 0] = st
-        rows[:, 1] = cn
-        full = np.concatenate(_all_gather_rows(rows, group))  # rank order = hypothesis order
+        b, c, w = chunk(hr, rank, world)
+        full = all_gather_chunks(_round_rows(ev, hb + b, c, w, dev), group)  # rank order = hypothesis order
         if not lo:
-            scan.step(full[:, 1], full[:, 0].astype(np.int8))
+            scan.step_rows(full, hr)
         else:
             pos = 0
             while not scan.done and pos < hr:
-                pos += scan.step_until_best(full[pos:, 1], full[pos:, 0].astype(np.int8))
+                pos += scan.step_rows(full[pos:], hr - pos, stop_on_improve=True)
                 if scan.improved:
-                    m, cnt = ev.local_opt(ev.model(scan.best), scan.max_good)
-                    best_model = m if cnt > scan.max_good else ev.model(scan.best)
+                    m0 = ev.model(scan.best)
+                    m, cnt, steps = ev.local_opt(m0, scan.max_good)
+                    n_lo += steps
+                    best_model = m if cnt > scan.max_good else m0
                     scan.raise_count(cnt)
         hb += hr
     if scan.best < 0:
         return ShardedResult(-1, 0, scan.iters, None)
     model = best_model if lo else ev.model(scan.best)
-    return ShardedResult(scan.best, scan.max_good, scan.iters, model)
+    return ShardedResult(scan.best, scan.max_good, scan.iters, model, n_lo)
 
 
 def sharded_batched(run_local, n_problems: int, group=None):
-    """Independent problems split contiguously over ranks.
+    """Independent problems split in contiguous chunks over ranks.
 
     ``run_local(begin, count)`` solves problems [begin, begin + count) on this rank and returns a
-    (count, W) float64 array of fixed-size results (e.g. status, n_inliers, R 9, t 3); the call
-    returns the (n_problems, W) array of all ranks, identical on every rank.
+    (count, W) float64 array (numpy or a torch tensor, e.g. status, n_inliers, R 9, t 3); the
+    call returns the (n_problems, W) rows of all ranks, identical on every rank (a torch tensor
+    on the communication device, all-gathered without a host round trip for device rows).
     """
     rank, world = _rank_world(group)
-    b, c = shard(n_problems, rank, world)
-    local = np.asarray(run_local(b, c), np.float64)
+    b, c, w = chunk(n_problems, rank, world)
+    local = run_local(b, c)
+    local = torch.as_tensor(local, dtype=torch.float64)
     if local.ndim != 2 or local.shape[0] != c:
         raise ValueError("run_local must return one row per problem")
-    return np.concatenate(_all_gather_rows(local, group))
+    dev = _comm_device(group)
+    padded = torch.zeros((max(w, 1), local.shape[1]), dtype=torch.float64, device=dev)
+    padded[:c] = local.to(dev)
+    return all_gather_chunks(padded[:w], group)[:n_problems]
 
 
-def pnp_batched_rows(points2D_list, points3D_list, K_list, n_iters: int = 5000, reproj_thresh: float = 30.0, **kw):
-    """run_local for sharded_batched over rsac.pnp_ransac_batched: rows (ok, n_inliers, R 9, t 3)."""
+def pnp_batched_rows(points2D, points3D, offsets, Ks, n_iters: int = 5000, reproj_thresh: float = 30.0, **kw):
+    """run_local for sharded_batched over rsac.pnp_ransac_batched_flat: the problems'
+    concatenated points (device tensors stay on the device) and offsets; rows
+    (ok, n_inliers, R 9, t 3)."""
+    off = np.asarray(offsets, np.int64)
 
     def run(begin, count):
         rows = np.zeros((count, 14))
         if count == 0:
             return rows
-        sl = slice(begin, begin + count)
-        res = api.pnp_ransac_batched(points2D_list[sl], points3D_list[sl], K_list[sl], n_iters, reproj_thresh, **kw)
-        for i, (R, t, _, ninl) in enumerate(res):
-            if R is not None:
-                rows[i, 0] = 1
-                rows[i, 1] = ninl
-                rows[i, 2:11] = R.reshape(9)
-                rows[i, 11:14] = t
+        o0, o1 = int(off[begin]), int(off[begin + count])
+        R, t, ok, ninl, _ = api.pnp_ransac_batched_flat(points2D[o0:o1], points3D[o0:o1],
+                                                        off[begin:begin + count + 1] - o0,
+                                                        np.asarray(Ks)[begin:begin + count], n_iters, reproj_thresh,
+                                                        **kw)
+        rows[:, 0] = ok
+        rows[:, 1] = ninl
+        rows[:, 2:11] = R.reshape(count, 9)
+        rows[:, 11:14] = t
         return rows
 
     return run
+
+
+# ---------------------------------------------------------------------------------------------
+# the multi-GPU legs of bench.py (BASELINE.json configs[2], configs[4], ms-to-best at N GPUs);
+# the CPU rehearsal test drives the same functions with gloo and restatement-backed evaluators
+# ---------------------------------------------------------------------------------------------
+def _barrier_time(fn, group=None, sync=None):
+    """fn() between barriers (+ device synchronisation); -> (result, max over ranks of the wall time)."""
+    _, world = _rank_world(group)
+    if world > 1:
+        dist.barrier(group=group)
+    if sync:
+        sync()
+    t = time.perf_counter()
+    out = fn()
+    if sync:
+        sync()
+    dt = time.perf_counter() - t
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=_comm_device(group))
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+        dt = float(tt.item())
+    return out, dt
+
+
+def c3_problem_shards(run_local, n_problems: int, group=None, sync=None, repeats: int = 3):
+    """C3 across the ranks: problem chunks solved locally, one all-gather of the rows.
+    -> (rows (n_problems, W) on the comm device, median wall seconds over `repeats`, max over ranks)."""
+    walls = []
+    rows = None
+    for _ in range(max(1, repeats)):
+        rows, dt = _barrier_time(lambda: sharded_batched(run_local, n_problems, group), group, sync)
+        walls.append(dt)
+    return rows, float(np.median(walls))
+
+
+def adaptive_shards(ev, max_iters: int, confidence: float = 0.99, round_size: int = 4096, lo: bool = False,
+                    group=None, sync=None, repeats: int = 3):
+    """C5 (lo=True) / ms-to-best (lo=False) across the ranks with sharded_ransac.
+    -> (ShardedResult, median wall seconds, max over ranks)."""
+    walls = []
+    res = None
+    for _ in range(max(1, repeats)):
+        res, dt = _barrier_time(lambda: sharded_ransac(ev, max_iters, confidence, round_size, group, lo=lo), group,
+                                sync)
+        walls.append(dt)
+    return res, float(np.median(walls))

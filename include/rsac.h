@@ -99,8 +99,9 @@ RSAC_EXPORT int rsac_set_round_size(rsac_ctx *ctx, int64_t hyps_per_round); /* a
  * on several cooperating blocks that must be resident at once.  rsac_refit_blocks reports, for
  * an n-point problem, the ranges of its summation order (lm_blocks) and the blocks that share
  * them on this device (the co-resident limit; fewer blocks walk more ranges each, same order,
- * same bits).  A refit whose blocks were not all resident returns RSAC_EHIP and keeps the
- * RANSAC pose. */
+ * same bits).  The blocks wait on each other's sums (about 1 s at most): when other work keeps
+ * some of them from being resident that long, the call is redone with one block per refit (no
+ * co-residency needed, the same bits), so the caller always gets the refined pose. */
 RSAC_EXPORT int rsac_refit_blocks(rsac_ctx *ctx, int32_t n, int32_t *ranges, int32_t *blocks);
 /* Test hooks, not for production use.  RSAC_DBG_REFIT_MAX_BLOCKS: cap the refit's
  * cooperating blocks (0 = the device limit).  RSAC_DBG_REFIT_DROP_BLOCK (nonzero): launch one
@@ -329,6 +330,20 @@ RSAC_EXPORT int rsac_scan_until_best(rsac_scan_state *st, const int32_t *counts,
                                      int32_t n, int32_t model_points, double confidence, int32_t *improved);
 /* apply a locally optimised inlier count: raises max_good and lowers the iteration bound */
 RSAC_EXPORT int rsac_scan_raise(rsac_scan_state *st, int32_t count, int32_t n, int32_t model_points, double confidence);
+
+/* The multi-GPU adaptive loop's exchange format and scan (rsac/parallel.py):
+ * rsac_pnp_hypothesis_rows evaluates Philox hypotheses [hyp_begin, hyp_begin + n_hyps) of one
+ * problem and writes {status, count} int32 pairs into rows_out (DEVICE, n_hyps x 2), enqueued on
+ * `stream` without waiting; ranks all-gather their rows into one device buffer (RCCL).
+ * rsac_scan_device consumes such rows (device, count x 2) as rsac_scan / rsac_scan_until_best
+ * would (stop_on_improve: return after a new best, *improved = 1): the improvements are listed on
+ * the device and only they reach the host, where the iteration bound is applied. */
+RSAC_EXPORT int rsac_pnp_hypothesis_rows(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n,
+                                         const double K[9], int64_t hyp_begin, int32_t n_hyps, double reproj_thresh,
+                                         uint64_t seed, uint32_t flags, int32_t *rows_out, void *stream);
+RSAC_EXPORT int rsac_scan_device(rsac_ctx *ctx, rsac_scan_state *st, const int32_t *rows, int64_t count, int32_t n,
+                                 int32_t model_points, double confidence, int32_t stop_on_improve,
+                                 int32_t *improved, void *stream);
 
 /* One LO-RANSAC local optimisation (RSAC_F_LO's step) of a pose on the device: up to 4
  * rounds of LM refit on the current RANSAC inliers + recount, kept while the count rises.

@@ -102,6 +102,13 @@ def lib():
                                  C.c_int, C.c_uint64, C.c_int, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
                                  C.POINTER(C.c_int64)]
     L.orc_pnp_ransac.restype = C.c_int64
+    L.orc_pnp_ransac_seq.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
+                                     C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
+                                     C.POINTER(C.c_int64)]
+    L.orc_pnp_ransac_seq.restype = C.c_int64
+    L.orc_pnp_hypotheses_mt.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_float, C.c_uint64,
+                                        C.c_int64, C.c_int64, _i32p, _i8p, C.c_int]
+    L.orc_pnp_hypotheses_mt.restype = None
     L.orc_pnp_ransac_lo.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
                                     C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
                                     C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
@@ -252,6 +259,28 @@ def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000,
                                 mask, C.byref(good), C.byref(iters))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value))
+
+
+def pnp_ransac_seq(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED):
+    """OpenCV's loop one hypothesis at a time, stopping at the iteration bound (orc_pnp_ransac_seq)."""
+    soa = soa_pnp(points3d, points2d)
+    n = len(soa[0])
+    R, t = np.zeros(9), np.zeros(3)
+    mask = np.zeros(n, np.uint8)
+    good = C.c_int32(0)
+    iters = C.c_int64(0)
+    best = lib().orc_pnp_ransac_seq(*soa, n, cam_from_K(K), thr, confidence, max_iters, seed, R, t, mask,
+                                    C.byref(good), C.byref(iters))
+    return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
+                iters=int(iters.value))
+
+
+def pnp_hypotheses_mt(soa, cam, thr, seed, H, hyp0=0, threads=1):
+    """pnp_hypotheses on `threads` OpenMP threads (orc_pnp_hypotheses_mt)."""
+    counts = np.zeros(H, np.int32)
+    status = np.zeros(H, np.int8)
+    lib().orc_pnp_hypotheses_mt(*soa, len(soa[0]), cam, thr2(thr), seed, hyp0, H, counts, status, int(threads))
+    return counts, status
 
 
 def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED):

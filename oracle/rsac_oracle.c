@@ -1486,6 +1486,54 @@ ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, c
     return best;
 }
 
+/* The same loop as OpenCV runs it, one hypothesis at a time: it stops as soon as the iteration
+ * bound (RANSACUpdateNumIters after each new best) is reached, so it scores only `iters`
+ * hypotheses -- the CPU ms-to-best-model baseline (bench.py cpu_baseline).  Philox sampler.
+ * Same results as orc_pnp_ransac (tests/test_oracle_golden.py). */
+ORC_API int64_t orc_pnp_ransac_seq(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                   int n, const double cam[4], double thr, double confidence, int max_iters,
+                                   uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
+                                   int64_t *iters_used) {
+    const float thr2 = orc_thr2(thr);
+    int64_t niters = max_iters > 1 ? max_iters : 1, best = -1, h = 0;
+    int32_t good = 0;
+    double bm[16] = {0};
+    for (; h < niters; ++h) {
+        int32_t c;
+        int8_t st;
+        double m[16];
+        orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, h, 1, NULL, NULL, &c, &st, m);
+        if (st < 0) break;
+        if (st == 0) continue;
+        if (c > (good > 3 ? good : 3)) {
+            best = h;
+            good = c;
+            memcpy(bm, m, sizeof bm);
+            niters = orc_update_num_iters(confidence, (double)(n - c) / n, 4, (int)niters);
+        }
+    }
+    if (iters_used) *iters_used = h;
+    if (best >= 0) {
+        memcpy(R, bm, 9 * sizeof(double));
+        memcpy(t, bm + 9, 3 * sizeof(double));
+        orc_pnp_count(R, t, cam, X, Y, Z, U, V, n, thr2, mask);
+    } else if (mask) {
+        memset(mask, 0, n);
+    }
+    if (n_inliers) *n_inliers = good;
+    return best;
+}
+
+/* orc_pnp_hypotheses over `threads` host threads (OpenMP, hypotheses dealt in chunks of 64):
+ * the CPU baseline's multi-core leg; every hypothesis' result is the single-thread one. */
+ORC_API void orc_pnp_hypotheses_mt(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                   int n, const double cam[4], float thr2, uint64_t seed, int64_t hyp0, int64_t H,
+                                   int32_t *counts, int8_t *status, int threads) {
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 64)
+    for (int64_t h = 0; h < H; ++h)
+        orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, hyp0 + h, 1, NULL, NULL, counts + h, status + h, NULL);
+}
+
 /* LO-RANSAC (BASELINE.json configs[4], C5; Chum et al. 2003, simple LO):
  * the OpenCV loop above, except that whenever hypothesis i becomes the best
  * (count > max(best, 3)) a local optimisation runs before hypothesis i+1:

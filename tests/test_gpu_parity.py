@@ -788,3 +788,60 @@ def test_winner_of_empty_key_is_zero():
     p3 = torch.from_numpy(pr["points3d"]).cuda()
     wm, wmask = rsac.winner(p2, p3, pr["K"], torch.zeros(1, dtype=torch.int64, device="cuda"), 30.0)
     assert not wm.cpu().numpy().any() and not wmask.cpu().numpy().any()
+
+
+# ---------------------------------------------------------------------------------------------
+# the multi-GPU round's device path: {status, count} rows written by the kernels and the
+# device-listed scan (rsac_pnp_hypothesis_rows, rsac_scan_device)
+# ---------------------------------------------------------------------------------------------
+def test_hypothesis_rows_equal_hypotheses():
+    import torch
+    pr = synth.pnp_problem(5000, 0.5, seed=64)
+    p2 = torch.from_numpy(pr["points2d"]).cuda()
+    p3 = torch.from_numpy(pr["points3d"]).cuda()
+    rows = torch.full((3000, 2), -7, dtype=torch.int32, device="cuda")
+    rsac.api.hypothesis_rows(p2, p3, pr["K"], 123, 2500, 30.0, rows)
+    st, cn, _ = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 123, 2500, 30.0)
+    r = rows.cpu().numpy()
+    np.testing.assert_array_equal(r[:2500, 0], st)
+    np.testing.assert_array_equal(r[:2500, 1], cn)
+    assert (r[2500:] == -7).all()
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_scan_device_equals_host_scan(seed):
+    """rsac_scan_device (records listed on the device, bound applied on the host) consumes rows as
+    the host scan does: random counts / statuses (zeros, a sampler failure), rounds of random
+    length, stop_on_improve with raised counts in between (LO), and runs of more improvements
+    than the record list holds (the exact host fallback)."""
+    import torch
+    rng = np.random.default_rng(seed)
+    H = 6000
+    counts = rng.integers(0, 3000, H).astype(np.int32)
+    if seed == 3:
+        counts[:200] = np.arange(200) * 10  # 199 improvements in a row
+    status = rng.choice(np.array([0, 1], np.int8), H, p=[0.1, 0.9])
+    if seed == 1:
+        status[4500] = -1
+    rows = torch.from_numpy(np.stack([status.astype(np.int32), counts], axis=1)).cuda()
+    for lo in (False, True):
+        a = rsac.Scan(H, 5000, 0.999, 4)
+        b = rsac.Scan(H, 5000, 0.999, 4)
+        pos = 0
+        while not a.done and pos < H:
+            step = int(rng.integers(1, 900))
+            step = min(step, H - pos)
+            if lo:
+                ca = a.step_rows(rows[pos:], step, stop_on_improve=True)
+                cb = b.step_rows(rows[pos:].cpu().numpy(), step, stop_on_improve=True)
+                assert (ca, a.improved) == (cb, b.improved)
+                if a.improved:
+                    raised = a.max_good + int(rng.integers(0, 3))
+                    a.raise_count(raised)
+                    b.raise_count(raised)
+                pos += ca
+            else:
+                a.step_rows(rows[pos:], step)
+                b.step_rows(rows[pos:].cpu().numpy(), step)
+                pos += step
+            assert (a.best, a.max_good, a.iters, a.niters, a.done) == (b.best, b.max_good, b.iters, b.niters, b.done)

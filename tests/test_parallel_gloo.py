@@ -42,8 +42,8 @@ class OracleShard:
         return m[0, :12].copy()
 
     def local_opt(self, model12, count):
-        R, t, c, _ = O.pnp_local_opt(self.soa, self.cam, self.thr, model12[:9], model12[9:12], count)
-        return np.concatenate([R.reshape(9), t]), c
+        R, t, c, steps = O.pnp_local_opt(self.soa, self.cam, self.thr, model12[:9], model12[9:12], count)
+        return np.concatenate([R.reshape(9), t]), c, steps
 
 
 def _free_port():
