@@ -47,25 +47,6 @@ static int fail(int code, const char *fmt, ...) {
 
 namespace {
 
-// Run f(p) for p in [0, P) on up to 16 host threads (the per-problem refits of a
-// batch are independent; each writes only its own outputs).
-template <class F>
-void parallel_for(int P, F f) {
-    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    const int nt = std::min({hw, 16, (P + 7) / 8});
-    if (nt <= 1) {
-        for (int p = 0; p < P; ++p) f(p);
-        return;
-    }
-    std::atomic<int> next{0};
-    std::vector<std::thread> pool;
-    for (int k = 0; k < nt; ++k)
-        pool.emplace_back([&] {
-            for (int p; (p = next.fetch_add(1)) < P;) f(p);
-        });
-    for (auto &t : pool) t.join();
-}
-
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -1722,29 +1703,21 @@ int rsac_scan_device(rsac_ctx *c, rsac_scan_state *st, const int32_t *rows, int6
         if (improved) *improved = imp;
         return r;
     }
-    // scan_step over the rows, replayed on the records: nothing changes between records
-    const int64_t begin = st->iter, end = begin + count, neg = begin + rec->first_neg;
-    for (int k = 0; k < rec->nrec; ++k) {
-        const int64_t pos = begin + rec->idx[k];
-        if (pos >= std::min<int64_t>(neg, st->niters)) break;
-        st->best = pos;
-        st->max_good = rec->cnt[k];
-        st->niters = update_num_iters(confidence, (double)(n - rec->cnt[k]) / n, model_points, (int)st->niters);
-        if (stop_on_improve) {
-            st->iter = pos + 1;
-            if (st->iter >= st->niters) st->done = 1;
-            if (improved) *improved = 1;
-            return RSAC_OK;
-        }
-    }
-    const int64_t stop = std::min<int64_t>(neg, st->niters);
-    if (stop < end) {
-        st->iter = std::max(stop, begin);
-        st->done = 1;
-    } else {
-        st->iter = end;
-        st->done = end >= st->niters;
-    }
+    // scan_step over the rows, replayed on the records (rsac_host.hip scan_records)
+    ScanState sc;
+    sc.niters = st->niters;
+    sc.best = st->best;
+    sc.max_good = st->max_good;
+    sc.iter = st->iter;
+    sc.done = st->done != 0;
+    scan_records(sc, rec->idx, rec->cnt, rec->nrec, rec->first_neg, count, n, model_points, confidence,
+                 stop_on_improve != 0);
+    st->niters = sc.niters;
+    st->best = sc.best;
+    st->max_good = sc.max_good;
+    st->iter = sc.iter;
+    st->done = sc.done ? 1 : 0;
+    if (improved) *improved = sc.improved ? 1 : 0;
     return RSAC_OK;
 }
 

@@ -13,9 +13,32 @@
 
 #include <stdint.h>
 
+#include <algorithm>
+#include <atomic>
+#include <thread>
 #include <vector>
 
 namespace rsac {
+
+// Run f(p) for p in [0, P) on up to 16 host threads (the per-problem MWC subset draws and refits
+// of a batch are independent; each writes only its own outputs).  Sanitizer-checked by
+// tests/sanitize (ThreadSanitizer).
+template <class F>
+void parallel_for(int P, F f) {
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nt = std::min({hw, 16, (P + 7) / 8});
+    if (nt <= 1) {
+        for (int p = 0; p < P; ++p) f(p);
+        return;
+    }
+    std::atomic<int> next{0};
+    std::vector<std::thread> pool;
+    for (int k = 0; k < nt; ++k)
+        pool.emplace_back([&] {
+            for (int p; (p = next.fetch_add(1)) < P;) f(p);
+        });
+    for (auto &t : pool) t.join();
+}
 
 struct Mwc {
     uint64_t state = ~(uint64_t)0;
@@ -50,10 +73,11 @@ struct ScanState {
 void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_t count, int n, int model_points,
                double confidence, bool stop_on_improve = false);
 
-// the first round [0, H) of a fresh scan from its improvement records (rsac_internal.h
-// ScanRecords): identical to scan_step over the full rows
+// the round [s.iter, s.iter + H) from its improvement records (rsac_internal.h ScanRecords:
+// the strict prefix maxima above the scan's floor, idx / first_neg relative to the round's
+// start): identical to scan_step over the full rows
 void scan_records(ScanState &s, const int32_t *idx, const int32_t *cnt, int nrec, int32_t first_neg, int64_t H, int n,
-                  int model_points, double confidence);
+                  int model_points, double confidence, bool stop_on_improve = false);
 
 void rodrigues_v2m(const double r[3], double R[9]);
 void rodrigues_m2v(const double R[9], double r[3]);

@@ -88,24 +88,37 @@ void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_
 }
 
 void scan_records(ScanState &s, const int32_t *idx, const int32_t *cnt, int nrec, int32_t first_neg, int64_t H, int n,
-                  int model_points, double confidence) {
-    // the first round [0, H) of a fresh scan (s reset).  scan_step stops at the first index
-    // >= niters (niters only shrinks) or with status < 0; between records nothing changes
+                  int model_points, double confidence, bool stop_on_improve) {
+    // scan_step over the round [s.iter, s.iter + H) replayed on its records: idx / first_neg are
+    // relative to the round's start and the records are the strict prefix maxima above the
+    // scan's floor, so between records nothing changes.  scan_step stops at the first index i
+    // >= niters (niters only shrinks; after an improvement at p the next index checked is p + 1,
+    // so the scan ends at max(p + 1, niters)) or at a status < 0 (first_neg).
+    const int64_t begin = s.iter, end = begin + H, neg = begin + first_neg;
+    int64_t cur = begin;  // the next index the sequential scan would check
+    s.improved = false;
     for (int r = 0; r < nrec; ++r) {
-        const int64_t stop = std::min<int64_t>(first_neg, s.niters);
-        if (idx[r] >= stop) break;
-        s.best = idx[r];
+        const int64_t pos = begin + idx[r];
+        if (pos >= std::min<int64_t>(neg, s.niters)) break;
+        if (cnt[r] <= std::max(s.max_good, model_points - 1)) continue;  // below a raised floor (LO)
+        s.best = pos;
         s.max_good = cnt[r];
         s.niters = update_num_iters(confidence, (double)(n - cnt[r]) / n, model_points, (int)s.niters);
+        cur = pos + 1;
+        if (stop_on_improve) {
+            s.improved = true;
+            s.iter = cur;
+            if (cur >= s.niters) s.done = true;
+            return;
+        }
     }
-    // as scan_step over [0, H): it stops at min(first_neg, niters) inside the round, else at H
-    const int64_t stop = std::min<int64_t>(first_neg, s.niters);
-    if (stop < H) {
+    const int64_t stop = std::min<int64_t>(std::max<int64_t>(cur, s.niters), neg);
+    if (stop < end) {
         s.iter = stop;
         s.done = true;
     } else {
-        s.iter = H;
-        s.done = H >= s.niters;
+        s.iter = end;
+        s.done = end >= s.niters;
     }
 }
 

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
-TAG=${TAG:-r01}
+TAG=${TAG:-r03}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o run --output-format csv -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/bench_under_rocprof.log 2>&1
 rc=$?; echo "rocprof kernel-trace rc=$rc"; tail -2 gpurun_out/prof/bench_under_rocprof.log
@@ -23,5 +23,11 @@ if [ -n "$PMC" ]; then
       -d gpurun_out/prof/pmc_valu -o run --output-format csv -- \
       python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/pmc_valu.log 2>&1
   rc=$?; echo "rocprof pmc VALU rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  # where the waves wait: parked (s_waitcnt / barrier) vs issue stalls, and the LDS side
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS \
+      SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_VALU_MFMA_BUSY_CYCLES \
+      -d gpurun_out/prof/pmc_wait -o run --output-format csv -- \
+      python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/pmc_wait.log 2>&1
+  rc=$?; echo "rocprof pmc wait rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 find gpurun_out/prof -name "*.csv" | head -20

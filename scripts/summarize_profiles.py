@@ -37,6 +37,36 @@ def counter(path, name):
     return list(per.values()) or None
 
 
+def per_kernel(path, name):
+    """{kernel name: median per-launch value of counter `name`} over every kernel of the run"""
+    if not os.path.exists(path):
+        return {}
+    per = {}
+    for row in csv.DictReader(open(path)):
+        if row["Counter_Name"] == name:
+            k = (row["Kernel_Name"].split("(")[0][:60], row["Dispatch_Id"])
+            per[k] = per.get(k, 0.0) + float(row["Counter_Value"])
+    by = {}
+    for (k, _), v in per.items():
+        by.setdefault(k, []).append(v)
+    return {k: statistics.median(v) for k, v in by.items()}
+
+
+def wait_summary(path, points, hyps):
+    names = ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_INSTS_LDS",
+             "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_SMEM", "SQ_VALU_MFMA_BUSY_CYCLES"]
+    vals = {n: counter(path, n) for n in names}
+    if not vals["SQ_WAVE_CYCLES"]:
+        return None
+    m = {n: statistics.median(v) for n, v in vals.items() if v}
+    w = m["SQ_WAVE_CYCLES"]
+    return {"kernel": SCORE, "points": points, "hyps": hyps, "counters_median": m,
+            "wait_any_frac": m.get("SQ_WAIT_ANY", 0) / w, "wait_inst_any_frac": m.get("SQ_WAIT_INST_ANY", 0) / w,
+            "wait_inst_lds_frac": m.get("SQ_WAIT_INST_LDS", 0) / w,
+            "note": "fractions of SQ_WAVE_CYCLES (quad-cycles): WAIT_ANY = parked on s_waitcnt / barrier, "
+                    "WAIT_INST_ANY = issue stalls (dependencies, pipe busy), WAIT_INST_LDS a part of the latter"}
+
+
 def valu_summary(path, points, hyps):
     names = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY",
              "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"]
@@ -97,7 +127,20 @@ def main():
     valu = valu_summary(os.path.join(PROF, "pmc_valu", "run_counter_collection.csv"), args.points, args.hyps)
     if valu:
         json.dump(valu, open(os.path.join(OUT, "pmc_score_valu.json"), "w"), indent=1)
+    wait = wait_summary(os.path.join(PROF, "pmc_wait", "run_counter_collection.csv"), args.points, args.hyps)
+    if wait:
+        json.dump(wait, open(os.path.join(OUT, "pmc_score_wait.json"), "w"), indent=1)
+    fk_all = per_kernel(os.path.join(PROF, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    wk_all = per_kernel(os.path.join(PROF, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    if fk_all or wk_all:
+        lines += ["", "| kernel | FETCH_SIZE KiB/launch (x2 = bytes read) | WRITE_SIZE KiB/launch |", "|---|---|---|"]
+        for k in sorted(set(fk_all) | set(wk_all)):
+            lines.append(f"| `{k}` | {fk_all.get(k, float('nan')):.0f} | {wk_all.get(k, float('nan')):.0f} |")
     lines += ["", f"scoring kernel average: {score_avg:.1f} us" if score_avg else "scoring kernel not found"]
+    if wait:
+        lines += [f"scoring kernel wave cycles: {100 * wait['wait_any_frac']:.1f} % parked (SQ_WAIT_ANY), "
+                  f"{100 * wait['wait_inst_any_frac']:.1f} % issue-stalled (SQ_WAIT_INST_ANY, of which LDS "
+                  f"{100 * wait['wait_inst_lds_frac']:.1f} %)"]
     if valu:
         lines += [f"scoring kernel VALU instructions/launch (PMC): {valu['valu_instr_per_launch']:.4g}; "
                   f"effective clock {valu.get('effective_clock_ghz', float('nan')):.3f} GHz; "

@@ -202,3 +202,22 @@ def test_fundamental_degenerate_sample_rejected():
     pts = np.c_[np.arange(8.0), 2 * np.arange(8.0)]  # collinear in both images
     ok, _ = O.fm_minimal(O.soa_hom(pts, pts * 3 + 1), np.arange(8))
     assert not ok
+
+
+@pytest.mark.parametrize("n,outl,seed", [(300, 0.5, 1), (3000, 0.7, 2), (12, 0.2, 3)])
+def test_sequential_and_parallel_cpu_loops_equal_the_restatement(n, outl, seed):
+    """The CPU baseline's loops (bench.py cpu_baseline): OpenCV's one-at-a-time loop that stops at
+    the iteration bound (orc_pnp_ransac_seq) and the OpenMP hypothesis loop equal the restatement."""
+    from rsac import synth
+    pr = synth.pnp_problem(n, outl, seed=seed)
+    a = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
+    b = O.pnp_ransac_seq(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
+    assert (a["best"], a["n_inliers"], a["iters"]) == (b["best"], b["n_inliers"], b["iters"])
+    np.testing.assert_array_equal(a["R"], b["R"])
+    np.testing.assert_array_equal(a["mask"], b["mask"])
+    soa = O.soa_pnp(pr["points3d"], pr["points2d"])
+    cam = O.cam_from_K(pr["K"])
+    c1, s1 = O.pnp_hypotheses(soa, cam, 30.0, 0x5EED, 2000, hyp0=5)
+    c2, s2 = O.pnp_hypotheses_mt(soa, cam, 30.0, 0x5EED, 2000, hyp0=5, threads=4)
+    np.testing.assert_array_equal(c1, c2)
+    np.testing.assert_array_equal(s1, s2)
