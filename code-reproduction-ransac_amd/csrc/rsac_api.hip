@@ -286,9 +286,9 @@ int ensure_hyp_buffers(rsac_ctx *c, int P, int64_t stride, bool subsets) {
     HIPCHK(c->h_best.ensure(sizeof(int64_t) * P));
     HIPCHK(c->h_bestmodels.ensure(sizeof(double) * kModelStride * P));
     if (subsets) {
-        HIPCHK(c->subsets.ensure(recs * 4 * sizeof(int32_t)));
+        HIPCHK(c->subsets.ensure(recs * 5 * sizeof(int32_t)));  // up to 5 indices per sample
         HIPCHK(c->substatus.ensure(recs));
-        HIPCHK(c->h_subsets.ensure(recs * 4 * sizeof(int32_t)));
+        HIPCHK(c->h_subsets.ensure(recs * 5 * sizeof(int32_t)));
         HIPCHK(c->h_substatus.ensure(recs));
     }
     return RSAC_OK;
@@ -322,6 +322,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     HIPCHK(c->fconst.ensure(sizeof(float) * kFconstStride * P));
     a.queue = c->queue.as<int>();
     a.exact_only = (flags & RSAC_F_EXACT_ONLY) ? 1 : 0;
+    a.sample_k = (flags & RSAC_F_MINIMAL_EPNP5) ? 5 : 4;
     float *C = c->centred.as<float>();
     int32_t max_n = 0;
     for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
@@ -471,7 +472,7 @@ int local_opt(rsac_ctx *c, const PnpArgs &a, int32_t n, ScanState &sc, double co
     improvements += hst->improvements;
     if (hst->improvements > 0 && hst->cur > sc.max_good) {
         sc.max_good = hst->cur;
-        sc.niters = update_num_iters(confidence, (double)(n - hst->cur) / n, 4, (int)sc.niters);
+        sc.niters = update_num_iters(confidence, (double)(n - hst->cur) / n, a.sample_k, (int)sc.niters);
         if (sc.iter >= sc.niters) sc.done = true;
     }
     return RSAC_OK;
@@ -499,7 +500,9 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
 
     PnpArgs *pa = model == Model::PnP ? (PnpArgs *)args : nullptr;
     HomArgs *ha = model != Model::PnP ? (HomArgs *)args : nullptr;
-    const int model_points = model == Model::Fm ? 8 : 4;
+    // RANSACUpdateNumIters' model_points = the sample size (5 for the EPnP-5 minimal solver)
+    const int model_points = model == Model::Fm ? 8 : pa ? pa->sample_k : 4;
+    const int sk = model_points;  // indices per drawn subset
 #define SETARG(field, val) \
     do {                   \
         if (pa) pa->field = (val); else ha->field = (val); \
@@ -541,19 +544,18 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
             parallel_for(P, [&](int p) {
                 int8_t *os = hss + (size_t)p * stride + hb;
                 const int np = (int)(st.off[p + 1] - st.off[p]);
-                if (np < 4 || out.scan[p].done) {  // nothing to draw: the solve skips status < 0
+                if (np < sk || out.scan[p].done) {  // nothing to draw: the solve skips status < 0
                     memset(os, -1, Hr);
                     return;
                 }
                 const float *hom[4];
                 if (model == Model::Hom)
                     for (int k = 0; k < 4; ++k) hom[k] = st.h[k] + st.off[p];
-                mwc_subsets(rngs[p], np, Hr, model == Model::Hom ? hom : nullptr, hs + ((size_t)p * stride + hb) * 4,
-                            os);
+                mwc_subsets(rngs[p], np, Hr, model == Model::Hom ? hom : nullptr, hs + ((size_t)p * stride + hb) * sk,
+                            os, sk);
             });
-            HIPCHK(copy_rows(c->subsets.as<int32_t>() + hb * 4, sizeof(int32_t) * 4 * stride, hs + hb * 4,
-                                    sizeof(int32_t) * 4 * stride, sizeof(int32_t) * 4 * Hr, P, hipMemcpyHostToDevice,
-                                    s));
+            HIPCHK(copy_rows(c->subsets.as<int32_t>() + hb * sk, sizeof(int32_t) * sk * stride, hs + hb * sk,
+                             sizeof(int32_t) * sk * stride, sizeof(int32_t) * sk * Hr, P, hipMemcpyHostToDevice, s));
             HIPCHK(copy_rows(c->substatus.as<int8_t>() + hb, stride, hss + hb, stride, Hr, P,
                                     hipMemcpyHostToDevice, s));
         }
@@ -846,7 +848,7 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     if (r) return r;
     if (lo.spec_pending) {
         bool ok = false;
-        r = spec_resolve(c, st, lo, 4, conf, ok);
+        r = spec_resolve(c, st, lo, a.sample_k, conf, ok);
         if (r) return r;
         if (!ok) {
             // the host's replay rules: later rounds if the scan goes on, then the finish again
@@ -1596,14 +1598,15 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
     r = ensure_hyp_buffers(c, 1, H, subsets != nullptr);
     if (r) return r;
     if (subsets) {
+        const int sk = model == Model::PnP && (flags & RSAC_F_MINIMAL_EPNP5) ? 5 : 4;  // indices per subset
         int8_t *hss = c->h_substatus.as<int8_t>();
-        memcpy(c->h_subsets.p, subsets, sizeof(int32_t) * 4 * (size_t)H);
+        memcpy(c->h_subsets.p, subsets, sizeof(int32_t) * sk * (size_t)H);
         for (int32_t h = 0; h < H; ++h) {
             bool ok = true;
-            for (int j = 0; j < 4; ++j) ok = ok && subsets[4 * h + j] >= 0 && subsets[4 * h + j] < n;
+            for (int j = 0; j < sk; ++j) ok = ok && subsets[sk * h + j] >= 0 && subsets[sk * h + j] < n;
             hss[h] = ok ? 1 : -1;
         }
-        HIPCHK(hipMemcpyAsync(c->subsets.p, c->h_subsets.p, sizeof(int32_t) * 4 * (size_t)H, hipMemcpyHostToDevice,
+        HIPCHK(hipMemcpyAsync(c->subsets.p, c->h_subsets.p, sizeof(int32_t) * sk * (size_t)H, hipMemcpyHostToDevice,
                               s));
         HIPCHK(hipMemcpyAsync(c->substatus.p, hss, H, hipMemcpyHostToDevice, s));
     }

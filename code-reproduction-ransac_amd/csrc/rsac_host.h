@@ -49,9 +49,9 @@ struct Mwc {
     int uniform(int a, int b) { return a == b ? a : (int)(next() % (uint32_t)(b - a) + (uint32_t)a); }
 };
 
-// OpenCV getSubset sequence for H consecutive iterations; hom != nullptr
-// applies HomographyEstimatorCallback::checkSubset (sx, sy, dx, dy SoA).
-void mwc_subsets(Mwc &rng, int n, int64_t H, const float *const *hom, int32_t *out, int8_t *status);
+// OpenCV getSubset sequence for H consecutive iterations of k-point samples (out: H x k);
+// hom != nullptr applies HomographyEstimatorCallback::checkSubset (sx, sy, dx, dy SoA; k = 4).
+void mwc_subsets(Mwc &rng, int n, int64_t H, const float *const *hom, int32_t *out, int8_t *status, int k = 4);
 
 int update_num_iters(double p, double ep, int model_points, int max_iters);
 

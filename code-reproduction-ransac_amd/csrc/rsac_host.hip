@@ -13,12 +13,12 @@
 
 namespace rsac {
 
-void mwc_subsets(Mwc &rng, int n, int64_t H, const float *const *hom, int32_t *out, int8_t *status) {
+void mwc_subsets(Mwc &rng, int n, int64_t H, const float *const *hom, int32_t *out, int8_t *status, int k) {
     for (int64_t h = 0; h < H; ++h) {
-        int32_t *idx = out + 4 * h;
+        int32_t *idx = out + k * h;
         bool found = false;
         for (int att = 0; att < kMaxSubsetAttempts; ++att) {
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < k; ++i) {
                 int r;
                 for (;;) {
                     r = rng.uniform(0, n);

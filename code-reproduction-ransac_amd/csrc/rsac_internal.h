@@ -54,6 +54,9 @@ struct PnpArgs {
     // UV = (u - cx, v - cy) / sqrt(T)
     uint4 *PF = nullptr;
     float2 *UV = nullptr;
+    // sample size and minimal solver: 4 = P3P (SOLVEPNP_P3P), 5 = EPnP on 5 points (the
+    // default SOLVEPNP_ITERATIVE kernel, RSAC_F_MINIMAL_EPNP5); subsets then hold sample_k indices
+    int32_t sample_k = 4;
 };
 
 constexpr int kFrameStride = 8;

@@ -736,6 +736,60 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
                      a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
 }
 
+// The default minimal solver of solvePnPRansac (SOLVEPNP_ITERATIVE: 5-point samples, EPnP on the
+// sample; OpenCV solvepnp.cpp PnPRansacCallback::runKernel), one lane per hypothesis: the same
+// record layout as k_pnp_solve.  rsac_math.h pnp_epnp_minimal<5> (the sums in pnp_epnp_host's
+// order for the 5 points) -- bit-identical to the host EPnP and the oracle's orc_pnp_minimal_epnp5.
+__global__ __launch_bounds__(256) void k_pnp_solve_epnp5(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    const int prob = blockIdx.y;
+    const int hl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (hl == 0 && prob == 0) {
+        if (a.queue) reset_pnp_queue(a.queue);
+    }
+    if (hl >= H) return;
+    const int64_t h = hyp_begin + hl;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
+    double *m = a.models + rec * kModelStride;
+    int32_t idx[5];
+    int8_t st = 1;
+    if (a.subsets) {
+        st = a.sub_status[rec];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) idx[j] = a.subsets[rec * 5 + j];
+    } else {
+        Philox rng;
+        rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
+        st = (n >= 5 && rng.subset<5>(n, idx) == 0) ? 1 : -1;
+    }
+    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
+    if (st > 0) {
+        float X[5], Y[5], Z[5], U[5], V[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int64_t i = p0 + idx[j];
+            X[j] = a.X[i]; Y[j] = a.Y[i]; Z[j] = a.Z[i]; U[j] = a.U[i]; V[j] = a.V[i];
+        }
+        const double *c = a.cams + 4 * prob;
+        st = pnp_epnp_minimal<5>(X, Y, Z, U, V, Cam{c[0], c[1], c[2], c[3]}, R, t) ? 1 : 0;
+        if (st == 0)
+            for (int q = 0; q < 9; ++q) R[q] = 0.0;
+        if (st == 0)
+            for (int q = 0; q < 3; ++q) t[q] = 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) m[q] = R[q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
+    m[kValidSlot] = st > 0 ? 1.0 : 0.0;
+    a.status[rec] = st;
+    if (a.counts_out) a.counts_out[rec] = 0;
+    if (a.fmodels)
+        write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
+}
+
 // Small rounds (an adaptive run's first 256 hypotheses: one block, every lane's latency is the
 // launch's): four lanes per hypothesis.  All four draw the sample and run lt_common; lane c
 // then takes candidate c = (sign, root) of the Lambda Twist solution list (lt_sign, lt_tau:
@@ -2115,8 +2169,10 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
 
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
+    if (a.sample_k == 5)
+        hipLaunchKernelGGL(k_pnp_solve_epnp5, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
-    if ((int64_t)P * H <= kSolve4MaxHyps)
+    else if ((int64_t)P * H <= kSolve4MaxHyps)
         hipLaunchKernelGGL(k_pnp_solve4, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     else
         hipLaunchKernelGGL(k_pnp_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);

@@ -1207,7 +1207,7 @@ RSAC_HD void epnp_mtm(EpnpShared *sh, const double *pairs, const Cam &k) {
         }
 }
 
-inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, EpnpStage2 &s2) {
+__host__ __device__ inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, EpnpStage2 &s2) {
     EpnpShared shm;
     EpnpShared *sh = &shm;
     const EpnpFrame &f = s1.f;
@@ -1428,6 +1428,66 @@ inline bool pnp_epnp(Red &red, const Cam &k, double *R_out, double *t_out) {
     EpnpStage2 s2;
     epnp_stage2(s1, k, s2);
     return epnp_stage3(red, k, s1, s2, R_out, t_out);
+}
+
+// The minimal EPnP of solvePnPRansac's default kernel (SOLVEPNP_ITERATIVE: model_points = 5,
+// ransac_kernel_method = SOLVEPNP_EPNP, OpenCV solvepnp.cpp PnPRansacCallback::runKernel): EPnP on
+// the N sampled points, one lane per hypothesis.  The sums take lm_reduce_host's order for an
+// N-point problem with every point masked in (point i -> slot i, the 64-lane xor butterfly whose
+// other slots and waves add exact zeros), and the frame is centred on the sample's first point,
+// so pnp_epnp_host on the same N points (in sample order) returns the same bits.
+template <int N>
+struct MinimalEpnpReducer {
+    static_assert(N >= 4 && N <= 8, "the butterfly below covers slots 0..7");
+    double X[N], Y[N], Z[N], u[N], v[N];  // centred on point 0
+    template <int NV, class F>
+    RSAC_HD void sum(F f, double *out) {
+        double w[8][NV];
+        for (int l = 0; l < 8; ++l)
+            for (int q = 0; q < NV; ++q) w[l][q] = 0.0;
+        for (int i = 0; i < N; ++i) f(X[i], Y[i], Z[i], u[i], v[i], w[i]);
+        for (int l = 0; l < 8; ++l)  // the butterfly's offsets 32, 16, 8: partners hold zeros
+            for (int q = 0; q < NV; ++q) w[l][q] = ((w[l][q] + 0.0) + 0.0) + 0.0;
+        for (int o = 4; o > 0; o >>= 1) {
+            double x[8][NV];
+            for (int l = 0; l < 8; ++l)
+                for (int q = 0; q < NV; ++q) x[l][q] = w[l][q] + w[l ^ o][q];
+            for (int l = 0; l < 8; ++l)
+                for (int q = 0; q < NV; ++q) w[l][q] = x[l][q];
+        }
+        for (int q = 0; q < NV; ++q) {  // waves 1..7 of the block add their zero sums
+            double b = w[0][q];
+            for (int wv = 1; wv < kLmThreads / 64; ++wv) b = b + 0.0;
+            out[q] = b;
+        }
+    }
+    RSAC_HD bool first(double *p) {
+        p[0] = X[0]; p[1] = Y[0]; p[2] = Z[0];
+        return true;
+    }
+};
+
+// (R, t) in the world frame; false for a degenerate sample (planar, or no valid beta)
+template <int N>
+__host__ __device__ inline bool pnp_epnp_minimal(const float *X, const float *Y, const float *Z, const float *U,
+                                                 const float *V, const Cam &k, double *R, double *t) {
+    MinimalEpnpReducer<N> red;
+    const double c[3] = {(double)X[0], (double)Y[0], (double)Z[0]};
+    for (int i = 0; i < N; ++i) {
+        red.X[i] = (double)X[i] - c[0];
+        red.Y[i] = (double)Y[i] - c[1];
+        red.Z[i] = (double)Z[i] - c[2];
+        red.u[i] = (double)U[i];
+        red.v[i] = (double)V[i];
+    }
+    EpnpStage1 s1;
+    epnp_stage1(red, k, s1);
+    if (s1.ok == 0.0) return false;
+    EpnpStage2 s2;
+    epnp_stage2(s1, k, s2);
+    if (!epnp_stage3(red, k, s1, s2, R, t)) return false;
+    lm_from_centred(R, c, t);
+    return true;
 }
 
 }  // namespace rsac

@@ -32,6 +32,7 @@ F_EXACT_ONLY = 1 << 6
 F_LO = 1 << 7
 F_ASYNC = 1 << 8
 F_EPNP = 1 << 9
+F_MINIMAL_EPNP5 = 1 << 10
 
 DBG_REFIT_MAX_BLOCKS = 1
 DBG_REFIT_DROP_BLOCK = 2

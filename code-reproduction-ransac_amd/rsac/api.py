@@ -69,8 +69,14 @@ def _device_of(inp: _In, device):
     return 0
 
 
-def _flags(adaptive, refine, sampler, exact_only=False):
+def _flags(adaptive, refine, sampler, exact_only=False, minimal="p3p"):
     f = 0
+    # minimal: "p3p" (4-point samples, SOLVEPNP_P3P: the reference's kernel) or "epnp5" (5-point
+    # samples solved by EPnP: solvePnPRansac's default SOLVEPNP_ITERATIVE kernel, model_points 5)
+    if minimal == "epnp5":
+        f |= L.F_MINIMAL_EPNP5
+    elif minimal != "p3p":
+        raise ValueError(f"minimal must be 'p3p' or 'epnp5', got {minimal!r}")
     if adaptive:
         f |= L.F_ADAPTIVE
     # refine: True / "lm" -> LM from the minimal model; "epnp" -> EPnP on the inliers (solvePnPRansac
@@ -137,7 +143,7 @@ def _K9(K) -> np.ndarray:
 def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
                confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox", adaptive: bool = True,
                refine: bool = True, device=None, return_info: bool = False, exact_only: bool = False,
-               lo: bool = False):
+               lo: bool = False, minimal: str = "p3p"):
     """RANSAC PnP on the GPU: (points2D, points3D, K, n_iters, reproj_thresh) -> (R, t, inlier_mask).
 
     Defaults follow the reference call (iterationsCount=5000, reprojectionError=30,
@@ -145,6 +151,8 @@ def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float 
     x_cam = R X + t; ``inlier_mask`` is the RANSAC-phase mask (OpenCV's
     convention).  On failure R and t are None and the mask is all False.
     lo=True runs LO-RANSAC (local optimisation at every new best; BASELINE.json C5).
+    minimal="epnp5" samples 5 points and solves them with EPnP (OpenCV's default
+    SOLVEPNP_ITERATIVE kernel; RANSACUpdateNumIters with model_points 5).
     """
     p3 = _In(points3D, 3)
     p2 = _In(points2D, 2)
@@ -154,7 +162,7 @@ def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float 
         raise ValueError("points3D and points2D must both be host arrays or both GPU tensors")
     n = p3.n
     ctx = L.context(_device_of(p3, device))
-    flags = _flags(adaptive, refine, sampler, exact_only) | (L.F_LO if lo else 0)
+    flags = _flags(adaptive, refine, sampler, exact_only, minimal) | (L.F_LO if lo else 0)
     if p3.device:
         flags |= L.F_DEVICE_IN
     K9 = _K9(K)
@@ -242,7 +250,7 @@ def _concat(parts, cols):
 
 def pnp_ransac_batched(points2D_list, points3D_list, K_list, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
                        confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox", adaptive: bool = True,
-                       refine: bool = True, device: int = 0):
+                       refine: bool = True, device: int = 0, minimal: str = "p3p"):
     """P independent PnP problems in one call (K sweep of testpro-K.py:58-75, C3 of BASELINE.json).
 
     Returns a list of (R, t, mask, n_inliers) per problem (R, t None on failure).
@@ -258,7 +266,7 @@ def pnp_ransac_batched(points2D_list, points3D_list, K_list, n_iters: int = 5000
     if P and np.diff(off).min() < 4:
         raise ValueError("every problem needs >= 4 correspondences")
     ctx = L.context(device)
-    flags = _flags(adaptive, refine, sampler)
+    flags = _flags(adaptive, refine, sampler, minimal=minimal)
     R = np.zeros((P, 9))
     t = np.zeros((P, 3))
     status = np.zeros(P, np.int32)
@@ -279,7 +287,7 @@ def pnp_ransac_batched(points2D_list, points3D_list, K_list, n_iters: int = 5000
 
 def pnp_ransac_batched_flat(points2D, points3D, offsets, Ks, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
                             confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox",
-                            adaptive: bool = True, refine: bool = True, device=None):
+                            adaptive: bool = True, refine: bool = True, device=None, minimal: str = "p3p"):
     """Batched PnP over problems already concatenated: points2D (N,2), points3D (N,3) f64 (numpy,
     or torch cuda tensors that stay on the device), offsets (P+1) int64, Ks (P,3,3).
 
@@ -296,7 +304,7 @@ def pnp_ransac_batched_flat(points2D, points3D, offsets, Ks, n_iters: int = 5000
         raise ValueError("every problem needs >= 4 correspondences")
     Kf = np.ascontiguousarray(np.asarray(Ks, np.float64).reshape(P, 9))
     ctx = L.context(_device_of(p3, device))
-    flags = _flags(adaptive, refine, sampler) | (L.F_DEVICE_IN if p3.device else 0)
+    flags = _flags(adaptive, refine, sampler, minimal=minimal) | (L.F_DEVICE_IN if p3.device else 0)
     mask, mptr, mflag = _mask_buffer(p3, p3.n)
     flags |= mflag
     R = np.zeros((P, 9))
@@ -460,13 +468,14 @@ def winner(points2D, points3D, K, key, reproj_thresh: float = 30.0, *, seed: int
 
 
 def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024, reproj_thresh: float = 30.0, *,
-               seed: int = 0x5EED, subsets=None, device=None, exact_only: bool = False):
+               seed: int = 0x5EED, subsets=None, device=None, exact_only: bool = False, minimal: str = "p3p"):
     """Raw per-hypothesis (status, counts, models) of the GPU hot path for one problem.
 
     model "pnp": a = points3D (N,3), b = points2D (N,2), K required.
     model "homography": a = src (N,2), b = dst (N,2).
     model "fundamental": a = pts1 (N,2), b = pts2 (N,2).
-    subsets: optional (n_hyps, 4) int32 index table replacing the Philox draw.
+    subsets: optional (n_hyps, 4) int32 index table replacing the Philox draw ((n_hyps, 5) for
+    minimal="epnp5", PnP's 5-point EPnP kernel).
     """
     pnp = model == "pnp"
     if model not in ("pnp", "homography", "fundamental"):
@@ -475,10 +484,18 @@ def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024,
     B = _In(b, 2)
     ctx = L.context(_device_of(A, device))
     flags = (L.F_DEVICE_IN if A.device else 0) | (L.F_EXACT_ONLY if exact_only else 0)
+    k = 4
+    if minimal == "epnp5":
+        if not pnp:
+            raise ValueError("minimal='epnp5' is a PnP kernel")
+        flags |= L.F_MINIMAL_EPNP5
+        k = 5
+    elif minimal != "p3p":
+        raise ValueError(f"minimal must be 'p3p' or 'epnp5', got {minimal!r}")
     counts = np.zeros(n_hyps, np.int32)
     status = np.zeros(n_hyps, np.int8)
     models = np.zeros((n_hyps, 16))
-    sub = None if subsets is None else np.ascontiguousarray(np.asarray(subsets, np.int32).reshape(n_hyps, 4))
+    sub = None if subsets is None else np.ascontiguousarray(np.asarray(subsets, np.int32).reshape(n_hyps, k))
     with ctx.lock:
         if pnp:
             K9 = _K9(K)

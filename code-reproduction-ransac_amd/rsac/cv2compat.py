@@ -49,11 +49,14 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
                    inliers=None, flags=SOLVEPNP_ITERATIVE):
     """-> (retval, rvec (3,1), tvec (3,1), inliers (M,1) int32 or None).
 
-    Minimal kernel: P3P on 4 points (the north star's kernel; OpenCV's default
-    would be EPnP on 5).  Final pose on the RANSAC inliers as OpenCV's: for
-    SOLVEPNP_P3P / AP3P / EPNP, EPnP (OpenCV re-solves P3P's inliers with
-    EPnP); otherwise LM started from the best minimal model (what
-    SOLVEPNP_ITERATIVE's final solvePnP with the RANSAC guess does).
+    OpenCV's structure (solvepnp.cpp solvePnPRansac): the MWC subset sequence of
+    RANSACPointSetRegistrator; the minimal kernel by flags -- SOLVEPNP_P3P / AP3P (and any
+    4-point input): P3P on 4-point samples (the reference's call, main_v1.py:497);
+    otherwise (the default SOLVEPNP_ITERATIVE, EPNP, ...): EPnP on 5-point samples, with
+    model_points = 5 in RANSACUpdateNumIters.  Final pose on the RANSAC inliers: EPnP for
+    P3P / AP3P / EPNP (OpenCV re-solves P3P's inliers with EPnP); otherwise LM started from
+    the best minimal model (SOLVEPNP_ITERATIVE's final solvePnP).  The inlier list is the
+    RANSAC-phase mask, as OpenCV returns it.
     """
     _check_dist(distCoeffs)
     P3 = np.asarray(objectPoints, np.float64).reshape(-1, 3)
@@ -62,9 +65,11 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
         raise error("objectPoints and imagePoints differ in length")
     if P3.shape[0] < 4:
         raise error("solvePnPRansac needs at least 4 points")
+    p3p = flags in (SOLVEPNP_P3P, SOLVEPNP_AP3P) or P3.shape[0] == 4
     refine = "epnp" if flags in (SOLVEPNP_P3P, SOLVEPNP_AP3P, SOLVEPNP_EPNP) else "lm"
     R, t, mask = api.pnp_ransac(P2, P3, cameraMatrix, int(iterationsCount), float(reprojectionError),
-                                confidence=float(confidence), adaptive=True, refine=refine)
+                                confidence=float(confidence), sampler="opencv", adaptive=True, refine=refine,
+                                minimal="p3p" if p3p else "epnp5")
     if R is None:
         return False, (np.zeros((3, 1)) if rvec is None else rvec), (np.zeros((3, 1)) if tvec is None else tvec), None
     idx = np.flatnonzero(mask).astype(np.int32).reshape(-1, 1)

@@ -69,6 +69,9 @@ extern "C" {
 #define RSAC_F_ASYNC (1u << 8)          /* rsac_pnp_evaluate_range: device outputs, no host wait (see there) */
 #define RSAC_F_EPNP (1u << 9)           /* PnP: EPnP on the inliers as the final solve (solvePnPRansac with
                                            SOLVEPNP_P3P); with RSAC_F_REFINE, LM from the EPnP pose */
+#define RSAC_F_MINIMAL_EPNP5 (1u << 10) /* PnP: 5-point samples solved by EPnP -- solvePnPRansac's default
+                                           SOLVEPNP_ITERATIVE kernel (model_points = 5, also in
+                                           RANSACUpdateNumIters); explicit subsets are then n x 5 */
 #define RSAC_F_LO (1u << 7)             /* LO-RANSAC (PnP, one problem): local optimisation at every new best,
                                            BASELINE.json configs[4]; see DESIGN.md "LO-RANSAC" */
 
@@ -233,7 +236,7 @@ RSAC_EXPORT int rsac_pnp_evaluate_range(rsac_ctx *ctx, const void *pts3d, const 
 /* Raw hot-path outputs for hypotheses [hyp_begin, hyp_begin + n_hyps) of
  * one problem: per-hypothesis status (1 model, 0 solver failed, -1 no
  * subset), inlier count and model (16 f64: R 9, t 3 | H 9; then valid).
- * subsets (host int32 n_hyps x 4, optional) replaces the Philox draw, e.g.
+ * subsets (host int32 n_hyps x 4, or x 5 with RSAC_F_MINIMAL_EPNP5; optional) replaces the Philox draw, e.g.
  * with OpenCV's MWC sequence.  This is what the parity tests compare with
  * the CPU restatement hypothesis by hypothesis. */
 RSAC_EXPORT int rsac_pnp_hypotheses(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n, const double K[9],

@@ -85,6 +85,12 @@ def lib():
                                      C.c_uint32, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, _i32p, _i8p,
                                      C.c_void_p]
     L.orc_pnp_hypotheses.restype = None
+    L.orc_pnp_hypotheses_k.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_float, C.c_uint64,
+                                       C.c_uint32, C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, _i32p, _i8p,
+                                       C.c_void_p]
+    L.orc_pnp_hypotheses_k.restype = None
+    L.orc_pnp_minimal_epnp5.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, _i32p, _f64p, _f64p, _f64p]
+    L.orc_pnp_minimal_epnp5.restype = C.c_int
     L.orc_hom_hypotheses.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_float, C.c_uint64, C.c_uint32,
                                      C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, _i32p, _i8p, C.c_void_p]
     L.orc_hom_hypotheses.restype = None
@@ -102,6 +108,10 @@ def lib():
                                  C.c_int, C.c_uint64, C.c_int, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
                                  C.POINTER(C.c_int64)]
     L.orc_pnp_ransac.restype = C.c_int64
+    L.orc_pnp_ransac_k.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
+                                   C.c_int, C.c_uint64, C.c_int, C.c_int, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
+                                   C.POINTER(C.c_int64)]
+    L.orc_pnp_ransac_k.restype = C.c_int64
     L.orc_pnp_ransac_seq.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
                                      C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
                                      C.POINTER(C.c_int64)]
@@ -234,19 +244,24 @@ def pnp_count(R, t, soa, cam, thr, mask=False):
     return (c, m.astype(bool)) if mask else c
 
 
-def pnp_hypotheses(soa, cam, thr, seed, H, hyp0=0, problem=0, subsets=None, sub_status=None, models=False):
+def pnp_hypotheses(soa, cam, thr, seed, H, hyp0=0, problem=0, subsets=None, sub_status=None, models=False,
+                   minimal="p3p"):
+    """minimal: "p3p" (4-point samples, SOLVEPNP_P3P) or "epnp5" (5-point samples, EPnP: the
+    default SOLVEPNP_ITERATIVE kernel of solvePnPRansac); subsets H x 4 or H x 5."""
     n = len(soa[0])
+    k = 5 if minimal == "epnp5" else 4
     counts = np.zeros(H, np.int32)
     status = np.zeros(H, np.int8)
     mdl = np.zeros((H, 16)) if models else None
     subs = None if subsets is None else np.ascontiguousarray(subsets, np.int32)
     sst = None if sub_status is None else np.ascontiguousarray(sub_status, np.int8)
-    lib().orc_pnp_hypotheses(*soa, n, cam, thr2(thr), seed, problem, hyp0, H, _ptr(subs), _ptr(sst), counts, status,
-                             _ptr(mdl))
+    lib().orc_pnp_hypotheses_k(*soa, n, cam, thr2(thr), seed, problem, hyp0, H, k, _ptr(subs), _ptr(sst), counts,
+                               status, _ptr(mdl))
     return (counts, status, mdl) if models else (counts, status)
 
 
-def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED, sampler="philox"):
+def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED, sampler="philox",
+               minimal="p3p"):
     soa = soa_pnp(points3d, points2d)
     n = len(soa[0])
     cam = cam_from_K(K)
@@ -255,10 +270,17 @@ def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000,
     mask = np.zeros(n, np.uint8)
     good = C.c_int32(0)
     iters = C.c_int64(0)
-    best = lib().orc_pnp_ransac(*soa, n, cam, thr, confidence, max_iters, seed, 1 if sampler == "opencv" else 0, R, t,
-                                mask, C.byref(good), C.byref(iters))
+    best = lib().orc_pnp_ransac_k(*soa, n, cam, thr, confidence, max_iters, seed, 1 if sampler == "opencv" else 0,
+                                  5 if minimal == "epnp5" else 4, R, t, mask, C.byref(good), C.byref(iters))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value))
+
+
+def pnp_minimal_epnp5(soa, cam, idx):
+    """EPnP on the 5 sampled points (orc_pnp_minimal_epnp5) -> (R, t) or None."""
+    R, t = np.zeros(9), np.zeros(3)
+    ok = lib().orc_pnp_minimal_epnp5(*soa, np.ascontiguousarray(idx, np.int32), cam, R, t)
+    return (R.reshape(3, 3), t) if ok else None
 
 
 def pnp_ransac_seq(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED):

@@ -730,23 +730,42 @@ static int philox_hom_subset(orc_stream *st, int n, const float *sx, const float
 /* subsets == NULL -> Philox sampler (seed, problem, hyp0 + h).              */
 /* models: H x 16 doubles (R 9, t 3, pad); may be NULL.                      */
 /* ------------------------------------------------------------------------ */
-ORC_API void orc_pnp_hypotheses(const float *X, const float *Y, const float *Z, const float *U, const float *V, int n,
-                                const double cam[4], float thr2, uint64_t seed, uint32_t problem, int64_t hyp0,
-                                int64_t H, const int32_t *subsets, const int8_t *sub_status, int32_t *counts,
-                                int8_t *status, double *models) {
+ORC_API int orc_pnp_epnp(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                         const uint8_t *mask, int n, const double cam[4], double R_out[9], double t_out[3]);
+
+/* The minimal solver of solvePnPRansac's default SOLVEPNP_ITERATIVE mode (OpenCV solvepnp.cpp:
+ * model_points = 5, ransac_kernel_method = SOLVEPNP_EPNP; PnPRansacCallback::runKernel): EPnP on
+ * the 5 sampled points, in sample order, every point in (the frame centred on the first). */
+ORC_API int orc_pnp_minimal_epnp5(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                  const int32_t idx[5], const double cam[4], double R[9], double t[3]) {
+    float x[5], y[5], z[5], u[5], v[5];
+    uint8_t m[5] = {1, 1, 1, 1, 1};
+    for (int j = 0; j < 5; ++j) {
+        x[j] = X[idx[j]]; y[j] = Y[idx[j]]; z[j] = Z[idx[j]]; u[j] = U[idx[j]]; v[j] = V[idx[j]];
+    }
+    return orc_pnp_epnp(x, y, z, u, v, m, 5, cam, R, t);
+}
+
+/* k = 4: P3P on 4-point samples (SOLVEPNP_P3P); k = 5: EPnP on 5-point samples (the default).
+ * subsets: H x k indices (the OpenCV sampler), else Philox subsets of size k. */
+ORC_API void orc_pnp_hypotheses_k(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                  int n, const double cam[4], float thr2, uint64_t seed, uint32_t problem,
+                                  int64_t hyp0, int64_t H, int k, const int32_t *subsets, const int8_t *sub_status,
+                                  int32_t *counts, int8_t *status, double *models) {
     for (int64_t h = 0; h < H; ++h) {
-        int32_t idx[4];
+        int32_t idx[5];
         double R[9] = {0}, t[3] = {0};
         int8_t st;
         if (subsets) {
             st = sub_status ? sub_status[h] : 1;
-            memcpy(idx, subsets + 4 * h, sizeof(idx));
+            memcpy(idx, subsets + k * h, sizeof(int32_t) * k);
         } else {
-            st = orc_philox_subset(seed, problem, (uint64_t)(hyp0 + h), n, 4, idx) < 0 ? -1 : 1;
+            st = orc_philox_subset(seed, problem, (uint64_t)(hyp0 + h), n, k, idx) < 0 ? -1 : 1;
         }
         int32_t c = 0;
         if (st > 0) {
-            st = (int8_t)orc_pnp_minimal(X, Y, Z, U, V, idx, cam, R, t);
+            st = (int8_t)(k == 5 ? orc_pnp_minimal_epnp5(X, Y, Z, U, V, idx, cam, R, t)
+                                 : orc_pnp_minimal(X, Y, Z, U, V, idx, cam, R, t));
             if (st) c = orc_pnp_count(R, t, cam, X, Y, Z, U, V, n, thr2, NULL);
         }
         counts[h] = c;
@@ -758,6 +777,14 @@ ORC_API void orc_pnp_hypotheses(const float *X, const float *Y, const float *Z, 
             memcpy(m + 9, t, 3 * sizeof(double));
         }
     }
+}
+
+ORC_API void orc_pnp_hypotheses(const float *X, const float *Y, const float *Z, const float *U, const float *V, int n,
+                                const double cam[4], float thr2, uint64_t seed, uint32_t problem, int64_t hyp0,
+                                int64_t H, const int32_t *subsets, const int8_t *sub_status, int32_t *counts,
+                                int8_t *status, double *models) {
+    orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, problem, hyp0, H, 4, subsets, sub_status, counts, status,
+                         models);
 }
 
 ORC_API void orc_hom_hypotheses(const float *sx, const float *sy, const float *dx, const float *dy, int n,
@@ -1454,10 +1481,11 @@ ORC_API int orc_hom_refine(const float *sx, const float *sy, const float *dx, co
 /* sampler: 0 = Philox (seed, problem 0), 1 = OpenCV MWC (seed ignored).     */
 /* Returns best hypothesis index (<0: no model); mask = RANSAC-phase mask.   */
 /* ------------------------------------------------------------------------ */
-ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, const float *U, const float *V, int n,
-                               const double cam[4], double thr, double confidence, int max_iters, uint64_t seed,
-                               int sampler, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
-                               int64_t *iters_used) {
+/* k: the sample size / minimal solver (4 P3P, 5 EPnP), also RANSACUpdateNumIters' model_points */
+ORC_API int64_t orc_pnp_ransac_k(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                 int n, const double cam[4], double thr, double confidence, int max_iters,
+                                 uint64_t seed, int sampler, int k, double R[9], double t[3], uint8_t *mask,
+                                 int32_t *n_inliers, int64_t *iters_used) {
     int64_t H = max_iters > 1 ? max_iters : 1;
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * H);
     int8_t *status = (int8_t *)malloc(H);
@@ -1465,15 +1493,15 @@ ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, c
     int32_t *subs = NULL;
     int8_t *sst = NULL;
     if (sampler == 1) {
-        subs = (int32_t *)malloc(sizeof(int32_t) * 4 * H);
+        subs = (int32_t *)malloc(sizeof(int32_t) * k * H);
         sst = (int8_t *)malloc(H);
         uint64_t st = ~(uint64_t)0;
-        orc_mwc_subsets(&st, n, 4, H, NULL, NULL, NULL, NULL, subs, sst);
+        orc_mwc_subsets(&st, n, k, H, NULL, NULL, NULL, NULL, subs, sst);
     }
     float thr2 = orc_thr2(thr);
-    orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, 0, H, subs, sst, counts, status, models);
+    orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, 0, 0, H, k, subs, sst, counts, status, models);
     int32_t good = 0;
-    int64_t best = orc_scan(counts, status, H, n, 4, confidence, max_iters, &good, iters_used);
+    int64_t best = orc_scan(counts, status, H, n, k, confidence, max_iters, &good, iters_used);
     if (best >= 0) {
         memcpy(R, models + 16 * best, 9 * sizeof(double));
         memcpy(t, models + 16 * best + 9, 3 * sizeof(double));
@@ -1484,6 +1512,14 @@ ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, c
     if (n_inliers) *n_inliers = good;
     free(counts); free(status); free(models); free(subs); free(sst);
     return best;
+}
+
+ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, const float *U, const float *V, int n,
+                               const double cam[4], double thr, double confidence, int max_iters, uint64_t seed,
+                               int sampler, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
+                               int64_t *iters_used) {
+    return orc_pnp_ransac_k(X, Y, Z, U, V, n, cam, thr, confidence, max_iters, seed, sampler, 4, R, t, mask, n_inliers,
+                            iters_used);
 }
 
 /* The same loop as OpenCV runs it, one hypothesis at a time: it stops as soon as the iteration

@@ -105,5 +105,5 @@ def test_gpu_batched_epnp_and_cv2_flags():
     p = probs[1]
     ok, rvec, tvec, inl = rcv.solvePnPRansac(p["points3d"], p["points2d"], p["K"], np.zeros((4, 1)),
                                              iterationsCount=2000, reprojectionError=30.0, flags=rcv.SOLVEPNP_P3P)
-    R, t, m = rsac.pnp_ransac(p["points2d"], p["points3d"], p["K"], 2000, 30.0, refine="epnp")
+    R, t, m = rsac.pnp_ransac(p["points2d"], p["points3d"], p["K"], 2000, 30.0, refine="epnp", sampler="opencv")
     assert ok and _bits_equal(rcv.Rodrigues(rvec)[0], rsac.rodrigues(rsac.rodrigues(R))) and _bits_equal(tvec.ravel(), t)

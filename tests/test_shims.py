@@ -139,7 +139,9 @@ def test_solve_pnp_ransac_shim_shapes_and_gate():
                                              iterationsCount=5000, reprojectionError=30.0, confidence=0.99)
     assert ok and rvec.shape == (3, 1) and tvec.shape == (3, 1) and inl.dtype == np.int32 and inl.shape[1] == 1
     assert len(inl) >= 6
-    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000, 0x5EED)
+    # the default flags (SOLVEPNP_ITERATIVE): OpenCV's MWC sequence of 5-point EPnP samples
+    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000, 0x5EED, sampler="opencv",
+                       minimal="epnp5")
     np.testing.assert_array_equal(inl[:, 0], np.flatnonzero(ref["mask"]))
     P3 = np.tile(np.array([[739000.0, 2888500.0, 700.0]]), (50, 1))
     ok, _, _, inl = rcv.solvePnPRansac(P3, np.tile([[100.0, 200.0]], (50, 1)), pr["K"], np.zeros((4, 1)))
