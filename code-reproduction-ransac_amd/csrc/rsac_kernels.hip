@@ -1153,10 +1153,20 @@ struct MfPair {
     float D, t;
 };
 // the test quantities of slot g of an MFMA output (lambda units; the expressions of sc_pair)
+#ifndef RSAC_MF_V
+#define RSAC_MF_V 0
+#endif
+typedef float mf_f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ MfPair mf_pair(const mf_f16v &x, int g, float2 uv, float ag) {
     const float z = x[4 * g + 2];
+#if RSAC_MF_V & 4
+    // (q1, q2) in one packed FMA (v_pk_fma_f32): the same two roundings
+    const mf_f2v q = __builtin_elementwise_fma(mf_f2v{uv.x, uv.y}, mf_f2v{z, z}, mf_f2v{x[4 * g], x[4 * g + 1]});
+    const float q1 = q.x, q2 = q.y;
+#else
     const float q1 = __builtin_fmaf(uv.x, z, x[4 * g]);
     const float q2 = __builtin_fmaf(uv.y, z, x[4 * g + 1]);
+#endif
     const float D = __builtin_fmaf(-z, z, __builtin_fmaf(q1, q1, q2 * q2));
     const float tt = __builtin_fmaf(-ag, __builtin_fabsf(z), __builtin_fabsf(D));
     return MfPair{D, tt};
@@ -1372,6 +1382,31 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
     }
     auto body = [&](int i, const mf_h8 &Ba, const mf_h8 &Bb, const float2 &ua, const float2 &ub)
         __attribute__((always_inline)) {
+#if RSAC_MF_V & 2
+        // the band compared per group as soon as its t's exist (b' of the group read before its
+        // MFMAs): no minima held across the iteration
+        uint32_t fl = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float4 av = avr[t];
+            const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
+            const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Ba, mf_f16v{}, 0, 0, 0);
+            const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Bb, mf_f16v{}, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
+                const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
+                const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
+                vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
+                fl |= __ballot(!(__builtin_fminf(ra.t, rb.t) > bg)) ? (1u << (4 * t + g)) : 0u;
+            }
+        }
+        if (__builtin_expect(fl != 0, 0)) {
+            if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)i, fl);
+            ++nw;
+        }
+    };
+#else
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const float4 av = avr[t];
@@ -1418,13 +1453,30 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
             ++nw;
         }
     };
+#endif
     const int full = n >= b0 + 64 ? (n - b0 - 64) / 256 + 1 : 0;  // iterations with 64 points in range
+#if RSAC_MF_V & 1
+    // the next iteration's point operands loaded while this one computes
+    if (full > 0) {
+        mf_h8 Ba, Bb;
+        float2 ua, ub;
+        mf_load_full(PF, UV, b0, col, half, Ba, Bb, ua, ub);
+        for (int i = 0; i < full; ++i) {
+            mf_h8 Na = Ba, Nb = Bb;
+            float2 va = ua, vb = ub;
+            if (i + 1 < full) mf_load_full(PF, UV, b0 + 256 * (i + 1), col, half, Na, Nb, va, vb);
+            body(i, Ba, Bb, ua, ub);
+            Ba = Na; Bb = Nb; ua = va; ub = vb;
+        }
+    }
+#else
     for (int i = 0; i < full; ++i) {
         mf_h8 Ba, Bb;
         float2 ua, ub;
         mf_load_full(PF, UV, b0 + 256 * i, col, half, Ba, Bb, ua, ub);
         body(i, Ba, Bb, ua, ub);
     }
+#endif
     if (full < iters) {
         mf_h8 Ba, Bb;
         float2 ua, ub;

@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librsac.so")
+# RSAC_LIB_PATH: another build of the same library (kernel A/B scripts, scripts/mf_ab.py)
+LIB_PATH = os.environ.get("RSAC_LIB_PATH") or os.path.join(_HERE, "librsac.so")
 
 # status codes / flags (include/rsac.h)
 OK = 0

@@ -1,0 +1,85 @@
+"""Interleaved A/B of librsac builds on the C2 step (scoring kernel time + async step time).
+
+    python scripts/mf_ab.py build/ab/a.so build/ab/b.so ... [--rounds 3]
+
+Each (round, build) runs in its own process (RSAC_LIB_PATH selects the build), in the order
+a b c a b c ..., so clock drift spreads over all builds.  Prints one JSON line per run and a
+summary (median over rounds of each run's median).
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def worker(calls, steps):
+    sys.path[:0] = [os.path.join(ROOT, "code-reproduction-ransac_amd")]
+    import torch
+    import rsac
+    from rsac import parallel as par
+    from rsac import synth
+    pr = synth.pnp_problem(10_000, 0.5, seed=0)
+    K = pr["K"]
+    ev = par.PnPShard(pr["points2d"], pr["points3d"], K, 30.0, device=0)
+    H = 100_000
+
+    def step():
+        return rsac.evaluate_range(ev.p2, ev.p3, K, 0, H, 30.0, with_mask=True, device_result=True)
+
+    t = time.perf_counter()
+    while time.perf_counter() - t < 1.0:
+        step()
+        torch.cuda.synchronize()
+    sc, so = [], []
+    for _ in range(calls):
+        _, _, info = rsac.evaluate_range(ev.p2, ev.p3, K, 0, H, 30.0, return_info=True, device=0)
+        sc.append(info.score_ms)
+        so.append(info.solve_ms)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        k = step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    print(json.dumps({"lib": os.environ.get("RSAC_LIB_PATH"), "score_ms": statistics.median(sc),
+                      "score_min": min(sc), "solve_ms": statistics.median(so), "step_ms": ms,
+                      "key": int(k[0].item())}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="*")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--calls", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--worker", action="store_true")
+    a = ap.parse_args()
+    if a.worker:
+        worker(a.calls, a.steps)
+        return
+    res = {lib: [] for lib in a.libs}
+    for r in range(a.rounds):
+        for lib in a.libs:
+            env = dict(os.environ, RSAC_LIB_PATH=os.path.abspath(lib))
+            out = subprocess.run([sys.executable, "-u", __file__, "--worker", "--calls", str(a.calls), "--steps",
+                                  str(a.steps)], env=env, capture_output=True, text=True, timeout=300)
+            if out.returncode != 0:
+                print(out.stdout, out.stderr, flush=True)
+                sys.exit(out.returncode)
+            line = out.stdout.strip().splitlines()[-1]
+            print(line, flush=True)
+            res[lib].append(json.loads(line))
+    keys = {json.dumps(v[0]["key"]) for v in res.values()}
+    print("summary (median over rounds): lib score_ms step_ms solve_ms; keys agree:", len(keys) == 1)
+    for lib, v in res.items():
+        print(f"  {os.path.basename(lib):24s} {statistics.median(x['score_ms'] for x in v):.4f} "
+              f"{statistics.median(x['step_ms'] for x in v):.4f} {statistics.median(x['solve_ms'] for x in v):.4f}")
+
+
+if __name__ == "__main__":
+    main()

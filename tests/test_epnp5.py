@@ -151,7 +151,8 @@ def test_gpu_cv2_default_flags_use_epnp5():
     Rl, tl, _ = O.pnp_refine(soa, ref["mask"].astype(np.uint8), cam, ref["R"].reshape(9), ref["t"])
     assert _bits_equal(tvec.ravel(), tl)
     assert _bits_equal(rcv.Rodrigues(rvec)[0], rsac.rodrigues(rsac.rodrigues(Rl)))
-    # 4 points: OpenCV switches to P3P (model_points 4)
-    ok4, _, _, inl4 = rcv.solvePnPRansac(pr["points3d"][:4], pr["points2d"][:4], pr["K"], None,
+    # 4 points (4 inliers): OpenCV switches to P3P (model_points 4), which needs all 4 to agree
+    i4 = np.flatnonzero(pr["inlier"])[:4]
+    ok4, _, _, inl4 = rcv.solvePnPRansac(pr["points3d"][i4], pr["points2d"][i4], pr["K"], None,
                                          iterationsCount=50, reprojectionError=30.0)
-    assert ok4 and inl4 is not None
+    assert ok4 and len(inl4) == 4
