@@ -1153,20 +1153,10 @@ struct MfPair {
     float D, t;
 };
 // the test quantities of slot g of an MFMA output (lambda units; the expressions of sc_pair)
-#ifndef RSAC_MF_V
-#define RSAC_MF_V 0
-#endif
-typedef float mf_f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ MfPair mf_pair(const mf_f16v &x, int g, float2 uv, float ag) {
     const float z = x[4 * g + 2];
-#if RSAC_MF_V & 4
-    // (q1, q2) in one packed FMA (v_pk_fma_f32): the same two roundings
-    const mf_f2v q = __builtin_elementwise_fma(mf_f2v{uv.x, uv.y}, mf_f2v{z, z}, mf_f2v{x[4 * g], x[4 * g + 1]});
-    const float q1 = q.x, q2 = q.y;
-#else
     const float q1 = __builtin_fmaf(uv.x, z, x[4 * g]);
     const float q2 = __builtin_fmaf(uv.y, z, x[4 * g + 1]);
-#endif
     const float D = __builtin_fmaf(-z, z, __builtin_fmaf(q1, q1, q2 * q2));
     const float tt = __builtin_fmaf(-ag, __builtin_fabsf(z), __builtin_fabsf(D));
     return MfPair{D, tt};
@@ -1330,11 +1320,12 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 // One unit of k_pnp_score_mf: hypotheses [h0, h0 + nh) of problem prob (records at rec0) over
 // the points [start, n) of the problem (p0 its first point, n_all_pts its length).  Per
 // iteration a wave takes 2 x 32 points: 4 MFMA groups x 2 tiles, the counts (255 x, v_sad_u8)
-// and the band minimum per slot; after every iteration the 16 slot minima are compared with b'
-// and a flagged iteration goes to the wave's LDS list (at most kWrec: the launcher bounds a
-// unit's points by 256 kWrec).  After its point loop the wave recounts its listed iterations
+// and each slot's band check (the smaller t of its two pairs against b'); a flagged iteration
+// goes to the wave's LDS list (at most kWrec: the launcher bounds a unit's points by 256 kWrec).  After its point loop the wave recounts its listed iterations
 // exactly (mf_recount) into the unit's LDS corrections, which the epilogue adds to the counts.
-constexpr int kWrec = 64;  // flagged iterations a wave lists per unit (k_pnp_score_mf)
+constexpr int kMfW = 4;          // waves per block of k_pnp_score_mf (2: 13 % slower, scripts/mf_ab.py)
+constexpr int kWrec = 64;        // flagged iterations a wave lists per unit
+constexpr int kMfT = 64 * kMfW;  // threads per block = points one pass of the block covers
 
 __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
                                         int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64],
@@ -1353,42 +1344,35 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
         ab[0][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 12] : 0.f;
         ab[1][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 13] : -__builtin_inff();
     }
-    {  // the unit's A operands (the same for the 4 waves): thread (t, lane) stages group t's
-        const int tl = threadIdx.x & 63;
-        alds[threadIdx.x >> 6][tl] = mf_operand(recs, threadIdx.x >> 6, tl & 31, tl >> 5, nh);
+    // the unit's A operands (the same for every wave): entry (t, lane) holds group t's
+    for (int e = threadIdx.x; e < 256; e += kMfT) {
+        const int tl = e & 63;
+        alds[e >> 6][tl] = mf_operand(recs, e >> 6, tl & 31, tl >> 5, nh);
     }
     __syncthreads();
     const uint4 *__restrict__ PF = a.PF + 2 * p0;
     const float2 *__restrict__ UV = a.UV + p0;
     uint32_t vc[4][4];
-    float tm[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            vc[t][g] = 0u;
-            tm[t][g] = __builtin_inff();
-        }
+        for (int g = 0; g < 4; ++g) vc[t][g] = 0u;
     int nw = 0;  // flagged iterations in the wave's list (uniform)
     const int b0 = start + wave * 64;
-    const int iters = n > b0 ? (n - b0 + 255) / 256 : 0;
-    // the A operands and slopes a' in registers for the whole unit
+    const int iters = n > b0 ? (n - b0 + kMfT - 1) / kMfT : 0;
+    // the A operands in registers for the whole unit; the slopes a' and bands b' are read from
+    // LDS per group, ahead of the group's MFMAs (in registers they would cost 32 VGPRs)
     mf_h8 Ar[4];
-    float4 avr[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        Ar[t] = alds[t][lane];
-        avr[t] = *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
-    }
+    for (int t = 0; t < 4; ++t) Ar[t] = alds[t][lane];
     auto body = [&](int i, const mf_h8 &Ba, const mf_h8 &Bb, const float2 &ua, const float2 &ub)
         __attribute__((always_inline)) {
-#if RSAC_MF_V & 2
-        // the band compared per group as soon as its t's exist (b' of the group read before its
-        // MFMAs): no minima held across the iteration
+        // each slot's band compared as soon as its two t's exist: min(t_a, t_b) <= b' flags the
+        // slot; no minima are held across the iteration
         uint32_t fl = 0;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            const float4 av = avr[t];
+            const float4 av = *reinterpret_cast<const float4 *>(&ab[0][half][t][0]);
             const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
             const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Ba, mf_f16v{}, 0, 0, 0);
             const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Bb, mf_f16v{}, 0, 0, 0);
@@ -1406,81 +1390,17 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
             ++nw;
         }
     };
-#else
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const float4 av = avr[t];
-            const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Ba, mf_f16v{}, 0, 0, 0);
-            const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Bb, mf_f16v{}, 0, 0, 0);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
-                const MfPair ra = mf_pair(xa, g, ua, ag), rb = mf_pair(xb, g, ub, ag);
-                vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
-                tm[t][g] = mf_min3(tm[t][g], ra.t, rb.t);
-            }
-        }
-        // one OR of the 16 slots' ballots (a compare and a scalar OR per slot); the slot bits
-        // only when some slot is flagged (rare)
-        uint64_t any = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
-                any |= __ballot(!(tm[t][g] > bg));
-            }
-        }
-        uint32_t fl = 0;
-        if (__builtin_expect(any != 0, 0)) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float bg = g == 0 ? bv.x : g == 1 ? bv.y : g == 2 ? bv.z : bv.w;
-                    fl |= __ballot(!(tm[t][g] > bg)) ? (1u << (4 * t + g)) : 0u;
-                }
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) tm[t][g] = __builtin_inff();
-        if (__builtin_expect(fl != 0, 0)) {
-            if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)i, fl);
-            ++nw;
-        }
-    };
-#endif
-    const int full = n >= b0 + 64 ? (n - b0 - 64) / 256 + 1 : 0;  // iterations with 64 points in range
-#if RSAC_MF_V & 1
-    // the next iteration's point operands loaded while this one computes
-    if (full > 0) {
-        mf_h8 Ba, Bb;
-        float2 ua, ub;
-        mf_load_full(PF, UV, b0, col, half, Ba, Bb, ua, ub);
-        for (int i = 0; i < full; ++i) {
-            mf_h8 Na = Ba, Nb = Bb;
-            float2 va = ua, vb = ub;
-            if (i + 1 < full) mf_load_full(PF, UV, b0 + 256 * (i + 1), col, half, Na, Nb, va, vb);
-            body(i, Ba, Bb, ua, ub);
-            Ba = Na; Bb = Nb; ua = va; ub = vb;
-        }
-    }
-#else
+    const int full = n >= b0 + 64 ? (n - b0 - 64) / kMfT + 1 : 0;  // iterations with 64 points in range
     for (int i = 0; i < full; ++i) {
         mf_h8 Ba, Bb;
         float2 ua, ub;
-        mf_load_full(PF, UV, b0 + 256 * i, col, half, Ba, Bb, ua, ub);
+        mf_load_full(PF, UV, b0 + kMfT * i, col, half, Ba, Bb, ua, ub);
         body(i, Ba, Bb, ua, ub);
     }
-#endif
     if (full < iters) {
         mf_h8 Ba, Bb;
         float2 ua, ub;
-        mf_load_part(PF, UV, b0 + 256 * full, n, col, half, Ba, Bb, ua, ub);
+        mf_load_part(PF, UV, b0 + kMfT * full, n, col, half, Ba, Bb, ua, ub);
         body(full, Ba, Bb, ua, ub);
     }
     // the wave's flagged iterations recounted here: the wave's exact-test latency overlaps the
@@ -1490,7 +1410,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
 #pragma unroll 1
     for (int k = 0; k < nw; ++k) {
         const uint2 w = wrec[wave][k];
-        mf_recount(a, rec0, p0, n, w.y, nh, b0 + 256 * (int)w.x, col, half, lcorr);
+        mf_recount(a, rec0, p0, n, w.y, nh, b0 + kMfT * (int)w.x, col, half, lcorr);
     }
     // counts: lane (c, half) of wave w holds slot (t, g)'s count over its points; hypothesis j =
     // 8t + 2g + half sums 4 waves x 32 lanes (8 threads of 16 values each, then a shuffle tree)
@@ -1499,16 +1419,16 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
 #pragma unroll
         for (int g = 0; g < 4; ++g) cl[wave][4 * t + g][lane] = vc[t][g];
     __syncthreads();
-    const int j = threadIdx.x >> 3, p = threadIdx.x & 7;
-    const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + 4 * p;
+    constexpr int TPH = kMfT / 32, LPT = 32 / TPH;  // threads per hypothesis, lanes per thread
+    const int j = threadIdx.x / TPH, p = threadIdx.x % TPH;
+    const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + LPT * p;
     uint32_t sum = 0;
 #pragma unroll
-    for (int w = 0; w < 4; ++w)
+    for (int w = 0; w < kMfW; ++w)
 #pragma unroll
-        for (int l = 0; l < 4; ++l) sum += cl[w][slot][l0 + l];
-    sum += __shfl_xor(sum, 1);
-    sum += __shfl_xor(sum, 2);
-    sum += __shfl_xor(sum, 4);
+        for (int l = 0; l < LPT; ++l) sum += cl[w][slot][l0 + l];
+#pragma unroll
+    for (int o = 1; o < TPH; o <<= 1) sum += __shfl_xor(sum, o);
     if (p == 0 && j < nh) {
         // + the unit's corrections (in LDS, complete at the barrier above).  A unit over all of
         // its problem's points is the only writer of its counts: a store (an atomic is
@@ -1525,8 +1445,9 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
 // Units from the split queue: block b takes units b % kQSub + kQSub i from counter b % kQSub.
 // Unit numbering as k_pnp_score_sc (the first tb tiles whole, then one unit per cell of cell_pts
 // points).  Problems whose centred coordinates leave the f16 operand range (fconst[11] = 0) carry
-// form-1 records and run the sc_unit body.  3 waves per SIMD (168 VGPRs).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_pnp_score_mf(
+// form-1 records and run the sc_unit body.  3 waves per SIMD (168 VGPRs; forcing 4 spills and
+// costs 23 %, scripts/mf_ab.py).
+__global__ __launch_bounds__(kMfT) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_pnp_score_mf(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int tb, int cells, int cell_pts) {
     constexpr int HB = 32;
@@ -1534,9 +1455,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
     // while the other waves may still be reading this one's (a skipped cell runs no barrier
     // between the read at the loop's top and that write)
     __shared__ int unit_s[2];
-    __shared__ uint32_t cl[4][16][64];
+    __shared__ uint32_t cl[kMfW][16][64];
     __shared__ __attribute__((aligned(16))) float ab[2][2][4][4];
-    __shared__ uint2 wrec[4][kWrec];
+    __shared__ uint2 wrec[kMfW][kWrec];
     __shared__ int lcorr[32];  // the unit's exact-recount corrections
     __shared__ mf_h8 alds[4][64];
     __shared__ int red[4][HB];                                                 // sc_unit
@@ -1547,11 +1468,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
     const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
     const int qk = blockIdx.x % kQSub;  // this block's units: qk + kQSub i, i from counter qk
     int *const uq = unit_queue(queue, qk);
-    if (threadIdx.x == 0) unit_s[0] = qk + kQSub * atomicAdd(uq, 1);
-    __syncthreads();
     int last_prob = -1, n_all = 0;
     int64_t p0 = 0;
     bool in_range = false;
+    if (threadIdx.x == 0) unit_s[0] = qk + kQSub * atomicAdd(uq, 1);
+    __syncthreads();
     for (int par = 0;; par ^= 1) {
         const int unit = __builtin_amdgcn_readfirstlane(unit_s[par]);
         if (unit >= n_units) break;  // uniform: every wave of every block reaches it
@@ -1596,6 +1517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
         __syncthreads();  // the unit's LDS and the slot are rewritten by the next unit
     }
 }
+
 
 // ---------------------------------------------------------------------------
 // PnP scoring.  Block = 4 waves; a block owns HB consecutive hypotheses of
@@ -2231,13 +2153,13 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     return hipGetLastError();
 }
 
-// blocks of `kern` (256 threads) the whole GPU keeps resident
+// blocks of `kern` (`threads` threads) the whole GPU keeps resident
 template <class Kern>
-static int resident_blocks(Kern kern) {
+static int resident_blocks(Kern kern, int threads = 256) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0);
     return std::max(1, cus) * std::max(1, per_cu);
 }
 
@@ -2297,14 +2219,14 @@ static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H
 // Returns hipErrorInvalidValue only for launches past the int32 unit space.
 static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    static const int resident = resident_blocks(k_pnp_score_mf);
+    static const int resident = resident_blocks(k_pnp_score_mf, kMfT);
     if (a.counts_out != counts) zero_counts(counts, hyp_begin, H, P_, a.hyp_stride, s);
     const int64_t max_n = std::max<int64_t>(1, a.max_n);
     const int64_t tiles = (int64_t)P_ * ((H + 31) / 32);
     int64_t cell_pts = 2048;
     while (cell_pts > 256 && tiles * ((max_n + cell_pts - 1) / cell_pts) < resident) cell_pts /= 2;
     int64_t cell_tiles = std::min<int64_t>(tiles, resident);
-    constexpr int64_t win_pts = 256 * kWrec;
+    constexpr int64_t win_pts = (int64_t)kMfT * kWrec;
     if (max_n > win_pts) {
         int64_t cp = win_pts;
         while (cp > cell_pts && tiles * ((max_n + cp - 1) / cp) < 4 * resident) cp /= 2;
@@ -2317,7 +2239,7 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
     if (units + kQSub * (int64_t)resident > INT32_MAX || tiles * 32 > INT32_MAX) return hipErrorInvalidValue;
     PnpArgs ka = a;
     ka.best_key = nullptr;  // reduced below from the complete counts
-    hipLaunchKernelGGL(k_pnp_score_mf, dim3(queue_grid(units, resident)), dim3(256), 0, s, ka, hyp_begin, H, P_,
+    hipLaunchKernelGGL(k_pnp_score_mf, dim3(queue_grid(units, resident)), dim3(kMfT), 0, s, ka, hyp_begin, H, P_,
                        a.queue, counts, (int)tb, (int)cells, (int)cell_pts);
     if (a.best_key) launch_best_key_of(a, hyp_begin, H, counts, s);
     return hipGetLastError();

@@ -41,6 +41,16 @@ def worker(calls, steps):
         sc.append(info.score_ms)
         so.append(info.solve_ms)
     torch.cuda.synchronize()
+    prof = None
+    L = rsac._lib.lib()
+    if hasattr(L, "rsac_debug_mf_prof"):  # phase-timing build (RSAC_MF_V & 32): one call's phase sums
+        import ctypes as C
+        buf = (C.c_ulonglong * 8)()
+        L.rsac_debug_mf_prof(buf, 1)
+        rsac.evaluate_range(ev.p2, ev.p3, K, 0, H, 30.0, return_info=True, device=0)
+        L.rsac_debug_mf_prof(buf, 1)
+        tot = sum(buf[:5])
+        prof = {n: round(buf[i] / tot, 4) for i, n in enumerate(["stage", "loop", "recount", "epilogue", "queue"])}
     t0 = time.perf_counter()
     for _ in range(steps):
         k = step()
@@ -48,7 +58,7 @@ def worker(calls, steps):
     ms = (time.perf_counter() - t0) * 1e3 / steps
     print(json.dumps({"lib": os.environ.get("RSAC_LIB_PATH"), "score_ms": statistics.median(sc),
                       "score_min": min(sc), "solve_ms": statistics.median(so), "step_ms": ms,
-                      "key": int(k[0].item())}), flush=True)
+                      "key": int(k[0].item()), "prof": prof}), flush=True)
 
 
 def main():
