@@ -125,6 +125,7 @@ struct rsac_ctx {
     PinBuf h_lo;                                               // LO chain state, written by the device
     PinBuf h_lmfail;                                           // multi-block refit failure word (device-written)
     int dbg_refit_max_blocks = 0;                              // RSAC_DBG_REFIT_MAX_BLOCKS (0: device limit)
+    int64_t spec_finishes = 0, spec_redos = 0;                 // RSAC_DBG_SPEC_FINISHES / _REDOS
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf reproj;                                             // reprojection errors / the K sweep's inputs
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
@@ -669,21 +670,51 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
 // after the stream synchronised: the host's replay of a speculative first round (one problem).
 // ok: it ended the scan with the winner the device picked (the finish enqueued on the device's
 // pick is the result); otherwise the caller starts over without speculation.
-int spec_resolve(rsac_ctx *c, const Staged &st, LoopOut &out, int model_points, double confidence, bool &ok) {
-    const ScanRecords &rec = *c->h_scanrec.as<ScanRecords>();
+int spec_resolve(rsac_ctx *c, const Staged &st, LoopOut &out, int model_points, double confidence, bool &ok,
+                 bool fixed, int64_t stride, hipStream_t s) {
+    const int P = fixed ? st.P : 1;
+    const ScanRecords *recs = c->h_scanrec.as<ScanRecords>();
     out.spec_pending = false;
     ok = false;
-    if (rec.nrec < 0) {  // more improvements than records: the caller runs the loop afresh
+    if (!fixed && recs[0].nrec < 0) {  // more improvements than records: the caller runs the loop afresh
         out.scan[0].reset((int)out.scan[0].niters);
         out.spec_H = 0;
         return RSAC_OK;
     }
-    const int np = (int)(st.off[1] - st.off[0]);
-    scan_records(out.scan[0], rec.idx, rec.cnt, rec.nrec, rec.first_neg, out.spec_H, np, model_points, confidence);
+    std::vector<int> full;  // problems with more improvements than records: their full rows
+    for (int p = 0; p < P; ++p) {
+        const ScanRecords &rec = recs[p];
+        if (rec.nrec < 0) {
+            full.push_back(p);
+            continue;
+        }
+        const int np = (int)(st.off[p + 1] - st.off[p]);
+        scan_records(out.scan[p], rec.idx, rec.cnt, rec.nrec, rec.first_neg, out.spec_H, np, model_points,
+                     confidence);
+    }
+    if (!full.empty()) {
+        const int64_t Hr = out.spec_H;
+        HIPCHK(c->h_counts.ensure(sizeof(int32_t) * P * Hr));
+        HIPCHK(c->h_status.ensure((size_t)P * Hr));
+        HIPCHK(copy_rows(c->h_counts.p, sizeof(int32_t) * Hr, c->counts.as<int32_t>(), sizeof(int32_t) * stride,
+                         sizeof(int32_t) * Hr, P, hipMemcpyDeviceToHost, s));
+        HIPCHK(copy_rows(c->h_status.p, Hr, c->status.as<int8_t>(), stride, Hr, P, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int p : full) {
+            const int np = (int)(st.off[p + 1] - st.off[p]);
+            scan_step(out.scan[p], c->h_counts.as<int32_t>() + (size_t)p * Hr,
+                      c->h_status.as<int8_t>() + (size_t)p * Hr, Hr, np, model_points, confidence);
+        }
+    }
     if (out.timing) add_times(c, out.gpu_ms, out.solve_ms, out.score_ms);
     out.rounds = 1;
     out.scored = out.spec_H;
-    ok = out.scan[0].done && rec.dev_done && out.scan[0].best == (int64_t)rec.dev_best;
+    ok = true;
+    for (int p = 0; p < P; ++p) {
+        const ScanRecords &rec = recs[p];
+        // (fixed budget: the round was the whole budget, whether or not the scan flagged it done)
+        ok = ok && (fixed || out.scan[p].done) && rec.dev_done && out.scan[p].best == (int64_t)rec.dev_best;
+    }
     return RSAC_OK;
 }
 
@@ -830,14 +861,21 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     // and refit are enqueued behind it, so the call synchronises once; the host verifies the
     // device's pick afterwards and redoes the call without speculation on a mismatch (a libm
     // ulp in RANSACUpdateNumIters) or when the first round did not end the scan
-    const bool spec = P == 1 && (flags & RSAC_F_ADAPTIVE) && !(flags & (RSAC_F_LO | RSAC_F_SAMPLER_OPENCV)) &&
-                      st.total > 0;
+    // fixed budget (adaptive off, any number of problems): the one round covers every problem's
+    // budget and the device replays every problem's scan, so the finish is enqueued behind the
+    // scan the same way, with no host round trip in between
+    const bool adaptive = (flags & RSAC_F_ADAPTIVE) != 0;
+    const bool spec_fixed = !adaptive && !(flags & RSAC_F_LO) && st.total > 0;
+    const bool spec = spec_fixed || (P == 1 && adaptive && !(flags & (RSAC_F_LO | RSAC_F_SAMPLER_OPENCV)) &&
+                                     st.total > 0);
     ScanDecide dec;
     if (spec) {
         dec.best_out = c->best.as<int64_t>();
         dec.n = (int32_t)st.total;
         dec.max_iters = std::max(n_iters, 1);
         dec.confidence = conf;
+        dec.fixed = spec_fixed ? 1 : 0;
+        dec.offsets = spec_fixed ? c->d_off : nullptr;
     }
     LoopOut lo;
     lo.timing = stats != nullptr;
@@ -848,11 +886,13 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     if (r) return r;
     if (lo.spec_pending) {
         bool ok = false;
-        r = spec_resolve(c, st, lo, a.sample_k, conf, ok);
+        r = spec_resolve(c, st, lo, a.sample_k, conf, ok, spec_fixed, stride, s);
         if (r) return r;
+        c->spec_finishes++;
         if (!ok) {
+            c->spec_redos++;
             // the host's replay rules: later rounds if the scan goes on, then the finish again
-            if (!lo.scan[0].done) {
+            if (!spec_fixed && !lo.scan[0].done) {
                 r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, nullptr, true);
                 if (r) return r;
             }
@@ -1026,6 +1066,20 @@ int rsac_debug_set(rsac_ctx *c, int32_t key, int64_t value) {
         return RSAC_OK;
     case RSAC_DBG_REFIT_DROP_BLOCK:
         c->lm.drop_block = value != 0;
+        return RSAC_OK;
+    default:
+        return fail(RSAC_EINVAL, "unknown debug key %d", key);
+    }
+}
+
+int rsac_debug_get(rsac_ctx *c, int32_t key, int64_t *value) {
+    if (!c || !value) return fail(RSAC_EINVAL, "null argument");
+    switch (key) {
+    case RSAC_DBG_SPEC_FINISHES:
+        *value = c->spec_finishes;
+        return RSAC_OK;
+    case RSAC_DBG_SPEC_REDOS:
+        *value = c->spec_redos;
         return RSAC_OK;
     default:
         return fail(RSAC_EINVAL, "unknown debug key %d", key);

@@ -109,14 +109,20 @@ struct ScanRecords {
     int32_t idx[kScanRecs], cnt[kScanRecs];
     int32_t dev_best, dev_done;  // the device's replay (ScanDecide), for the host to verify
 };
-// optional device replay of problem 0's first round (scan_records with the device's libm):
-// best record index (stride 0 problem: the hypothesis) -> *best_out, so the final mask and refit
-// can be enqueued before the host has seen the records; the host's own replay decides
+// optional device replay of the first round (scan_records with the device's libm), so the final
+// mask and refit can be enqueued before the host has seen the records; the host's own replay
+// decides, and redoes the finish if it picked another winner (a last-ulp difference in
+// RANSACUpdateNumIters):
+//   fixed = 0 (adaptive, one problem): problem 0's replay; its best hypothesis -> best_out[0];
+//   fixed = 1 (the round is every problem's whole budget): every problem's replay (its point
+//   count from offsets); record index prob * stride + best -> best_out[prob] (-1: no model)
 struct ScanDecide {
     int64_t *best_out = nullptr;
-    int32_t n = 0;
+    int32_t n = 0;                      // points (fixed = 0)
+    const int64_t *offsets = nullptr;   // device problem offsets (fixed = 1)
     int64_t max_iters = 0;
     double confidence = 0;
+    int32_t fixed = 0;
 };
 hipError_t launch_scan_records(const int32_t *counts, const int8_t *status, int64_t stride, int32_t P, int32_t H,
                                int model_points, ScanRecords *out, hipStream_t s, ScanDecide dec = ScanDecide());

@@ -1931,7 +1931,7 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
             o.cnt[r] = rcnt[r];
         }
     }
-    if (dec.best_out && prob == 0) {  // wave-uniform
+    if (dec.best_out && (dec.fixed || prob == 0)) {  // wave-uniform
         // scan_records (rsac_host.hip) on the records lane 0 just wrote.  update_num_iters'
         // logarithms (the latency) for every record at once, lane r for record r; the
         // sequential part on them is uniform across the wave.
@@ -1944,8 +1944,9 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
         num = log(num);
         double ldenom = 0.;
         int zero = 0;  // update_num_iters returns 0 (denominator below DBL_MIN)
+        const int32_t np = dec.offsets ? (int32_t)(dec.offsets[prob + 1] - dec.offsets[prob]) : dec.n;
         if (lane < nr) {
-            double ep = (double)(dec.n - rcnt[lane]) / dec.n;
+            double ep = (double)(np - rcnt[lane]) / np;
             ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
             const double denom = 1. - pow(1. - ep, model_points);
             if (denom < 2.2250738585072014e-308) zero = 1;
@@ -1962,9 +1963,12 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
             niters = z ? 0 : ((ld >= 0 || -num >= mi * (-ld)) ? mi : (int)lrint(num / ld));
         }
         const int64_t stop = first_neg < niters ? first_neg : niters;
-        const bool done = nrec <= kScanRecs && (stop < H || H >= niters);
+        // fixed budget: the round is the whole budget, so the replay always ends in it
+        const bool done = nrec <= kScanRecs && (dec.fixed || stop < H || H >= niters);
         if (lane == 0) {
-            *dec.best_out = done ? best : -1;  // not done: the speculative finish has no model (cheap no-op)
+            // not done: the speculative finish has no model (cheap no-op); the record index of
+            // problem prob's winner (problem 0: the hypothesis itself)
+            dec.best_out[prob] = done && best >= 0 ? (int64_t)prob * stride + best : -1;
             o.dev_best = (int32_t)best;
             o.dev_done = done;
         }

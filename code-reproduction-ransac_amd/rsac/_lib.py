@@ -67,6 +67,7 @@ SIGNATURES = [
     ("rsac_set_round_size", C.c_int, [_vp, _i64]),
     ("rsac_refit_blocks", C.c_int, [_vp, _i32, C.POINTER(_i32), C.POINTER(_i32)]),
     ("rsac_debug_set", C.c_int, [_vp, _i32, _i64]),
+    ("rsac_debug_get", C.c_int, [_vp, _i32, _vp]),
     ("rsac_pnp_ransac", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
                                   C.POINTER(Stats), _vp]),
     ("rsac_pnp_ransac_batched", C.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,

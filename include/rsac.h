@@ -112,6 +112,12 @@ RSAC_EXPORT int rsac_refit_blocks(rsac_ctx *ctx, int32_t n, int32_t *ranges, int
 #define RSAC_DBG_REFIT_MAX_BLOCKS 1
 #define RSAC_DBG_REFIT_DROP_BLOCK 2
 RSAC_EXPORT int rsac_debug_set(rsac_ctx *ctx, int32_t key, int64_t value);
+/* RSAC_DBG_SPEC_FINISHES / RSAC_DBG_SPEC_REDOS (read only): rsac_pnp_ransac(_batched) calls whose
+ * finish was enqueued behind the device's own pick of the winners, and those of them the host's
+ * replay rejected (the finish then ran again on the host's winners). */
+#define RSAC_DBG_SPEC_FINISHES 3
+#define RSAC_DBG_SPEC_REDOS 4
+RSAC_EXPORT int rsac_debug_get(rsac_ctx *ctx, int32_t key, int64_t *value);
 
 /* cv2.solvePnPRansac (main_v1.py:497).  K: 3x3 row-major f64.  Minimal
  * solver: P3P (Lambda Twist) on 4 points.  n_iters = iterationsCount cap,

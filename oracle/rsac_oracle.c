@@ -688,6 +688,10 @@ ORC_API int32_t orc_hom_count(const double H[9], const float *sx, const float *s
  * -1 not found (the RANSAC loop then stops). */
 ORC_API void orc_mwc_subsets(uint64_t *state, int n, int s, int64_t H, const float *sx, const float *sy,
                              const float *dx, const float *dy, int32_t *out, int8_t *status) {
+    if (n < s) { /* run() returns no model when count < modelPoints: nothing is drawn */
+        for (int64_t h = 0; h < H; ++h) status[h] = -1;
+        return;
+    }
     for (int64_t h = 0; h < H; ++h) {
         int32_t *idx = out + s * h;
         int found = 0;

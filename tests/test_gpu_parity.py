@@ -845,3 +845,53 @@ def test_scan_device_equals_host_scan(seed):
                 b.step_rows(rows[pos:].cpu().numpy(), step)
                 pos += step
             assert (a.best, a.max_good, a.iters, a.niters, a.done) == (b.best, b.max_good, b.iters, b.niters, b.done)
+
+
+def _spec_counters():
+    import ctypes as C
+    ctx = rsac.context(0)
+    f, r = C.c_int64(0), C.c_int64(0)
+    rsac.lib().rsac_debug_get(ctx.handle, 3, C.byref(f))  # RSAC_DBG_SPEC_FINISHES
+    rsac.lib().rsac_debug_get(ctx.handle, 4, C.byref(r))  # RSAC_DBG_SPEC_REDOS
+    return f.value, r.value
+
+
+@pytest.mark.parametrize("sampler,minimal", [("philox", "p3p"), ("opencv", "p3p"), ("opencv", "epnp5")])
+def test_fixed_budget_device_pick_batched(sampler, minimal):
+    """adaptive off: k_scan_records picks every problem's winner on the device and the masks are
+    enqueued behind it (no host round trip).  A ragged batch with a problem that has no model
+    (all points equal) and one of 4 points: every result equals the oracle's sequential loop, the
+    speculative finish is taken once per call and never redone."""
+    probs = [synth.pnp_problem(n, 0.4, seed=170 + i) for i, n in enumerate([900, 50, 2600, 4, 300])]
+    dead = dict(probs[1])
+    dead["points3d"] = np.tile(probs[1]["points3d"][:1], (50, 1))
+    probs[1] = dead
+    f0, r0 = _spec_counters()
+    out = rsac.pnp_ransac_batched([p["points2d"] for p in probs], [p["points3d"] for p in probs],
+                                  [p["K"] for p in probs], 700, 30.0, adaptive=False, refine=False, sampler=sampler,
+                                  minimal=minimal)
+    f1, r1 = _spec_counters()
+    assert (f1 - f0, r1 - r0) == (1, 0)
+    for p, (R, t, m, ni) in zip(probs, out):
+        ref = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 0.99, 700, 0x5EED, sampler=sampler,
+                           minimal=minimal)
+        assert (R is None) == (ref["best"] < 0)
+        assert ni == ref["n_inliers"]
+        np.testing.assert_array_equal(m, ref["mask"])
+        if R is not None:
+            assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+    # the same batch with the LM refit enqueued behind the device's pick: the refined poses are
+    # the oracle's refit of its own winners
+    out2 = rsac.pnp_ransac_batched([p["points2d"] for p in probs], [p["points3d"] for p in probs],
+                                   [p["K"] for p in probs], 700, 30.0, adaptive=False, refine=True, sampler=sampler,
+                                   minimal=minimal)
+    assert _spec_counters()[1] == r0
+    for p, (R, t, m, ni) in zip(probs, out2):
+        ref = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 0.99, 700, 0x5EED, sampler=sampler,
+                           minimal=minimal)
+        if ref["best"] < 0:
+            assert R is None
+            continue
+        soa, cam = O.soa_pnp(p["points3d"], p["points2d"]), O.cam_from_K(p["K"])
+        Rl, tl, _ = O.pnp_refine(soa, ref["mask"].astype(np.uint8), cam, ref["R"].reshape(9), ref["t"])
+        assert _bits_equal(R, Rl) and _bits_equal(t, tl)
