@@ -10,6 +10,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o run 
     python3 bench.py --steps 10 --warmup 3 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/bench_under_rocprof.log 2>&1
 rc=$?; echo "rocprof kernel-trace rc=$rc"; tail -2 gpurun_out/prof/bench_under_rocprof.log
 [ $rc -eq 0 ] || exit $rc
+# C3 (BASELINE configs[2]) alone: where a 1024-problem batched call spends its time
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/c3 -o run --output-format csv -- \
+    python3 scripts/c3_prof.py > gpurun_out/prof/c3_under_rocprof.log 2>&1
+rc=$?; echo "rocprof C3 kernel-trace rc=$rc"; tail -1 gpurun_out/prof/c3_under_rocprof.log
+[ $rc -eq 0 ] || exit $rc
 if [ -n "$PMC" ]; then
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/pmc_fetch -o run --output-format csv -- \
       python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/pmc_fetch.log 2>&1

@@ -5,6 +5,7 @@
 Writes
   profiles/TAG_kernel_stats.csv      -- the --kernel-trace --stats summary of the bench command
   profiles/TAG_summary.md            -- per-kernel table + the scoring kernel's average duration
+  profiles/TAG_c3_kernel_stats.csv   -- the same for scripts/c3_prof.py (BASELINE configs[2])
   profiles/pmc_score_kernel.json     -- HBM bytes per scoring launch (FETCH_SIZE x 2 per
                                         MI355X_MICROARCH.md "HBM", + WRITE_SIZE), read by bench.py
   profiles/pmc_score_valu.json       -- VALU instructions per scoring launch and the issue-side
@@ -149,6 +150,14 @@ def main():
         lines += [f"scoring kernel HBM bytes/launch (PMC): {pmc['hbm_bytes_per_launch'] / 1e6:.2f} MB "
                   f"(FETCH_SIZE {pmc['fetch_size_kib']:.0f} KiB x2 + WRITE_SIZE {pmc['write_size_kib']:.0f} KiB); "
                   f"algorithmic {algo / 1e9:.1f} GB"]
+    c3 = os.path.join(PROF, "c3", "run_kernel_stats.csv")
+    if os.path.exists(c3):  # scripts/c3_prof.py under --kernel-trace --stats (BASELINE configs[2])
+        shutil.copyfile(c3, os.path.join(OUT, f"{args.tag}_c3_kernel_stats.csv"))
+        lines += ["", "C3 (1024 problems x 2000 points x 1024 hypotheses, `scripts/c3_prof.py`, 12 calls):", "",
+                  "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
+        for r in csv.DictReader(open(c3)):
+            lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
+                         f"{float(r['Percentage']):.2f} |")
     open(os.path.join(OUT, f"{args.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
