@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--cpu-hyps", type=int, default=100_000, help="CPU baseline sample (hypotheses, 1 thread)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0),
                     help="threads of the CPU baseline's multi-core leg (default: OMP_NUM_THREADS, else all cores)")
+    ap.add_argument("--streams", type=int, default=2, help="contexts / HIP streams the steps alternate over "
+                                                               "(1: one after another on one stream)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ms-to-best", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C3/C4/C5, location-search and DEM-march lines")
@@ -99,31 +101,41 @@ def main():
     ev = par.PnPShard(pr["points2d"], pr["points3d"], K, args.thr, device=local)
     nccl = dist is not None and args.backend == "nccl"
 
-    def step():
+    # steps are independent batches: they alternate between `--streams` rsac contexts (each its own
+    # device scratch) on as many HIP streams, so step i + 1's solve starts on the CUs step i's
+    # scoring tail frees (scripts/stream_pipe_ab.py: 0.262 vs 0.285 ms/step); --streams 1 is the
+    # serial form, also measured below (ms_per_step_serial)
+    nstreams = max(1, args.streams)
+    ctxs = [rsac.context(local)] + [rsac.Context(local) for _ in range(nstreams - 1)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
+
+    def step(i=0, serial=False):
         # one pass over the batch, asynchronous end to end: solve + score + fused best key + the
         # winner's mask stay on the device; for N > 1 the key is all-reduced (RCCL, MAX) and every
         # rank re-derives the global winner's model and mask from it (rsac_pnp_winner), so no
         # step waits for the host
-        key_t, model_t, mask = rsac.evaluate_range(ev.p2, ev.p3, K, base, H, args.thr, with_mask=True,
-                                                   device_result=True)
-        if dist is None:
+        j = 0 if serial else i % nstreams
+        with torch.cuda.stream(streams[j]):
+            key_t, model_t, mask = rsac.evaluate_range(ev.p2, ev.p3, K, base, H, args.thr, with_mask=True,
+                                                       device_result=True, context=ctxs[j])
+            if dist is None:
+                return key_t
+            if nccl:
+                dist.all_reduce(key_t, op=dist.ReduceOp.MAX)
+            else:  # gloo rehearsal: host round trip
+                kc = key_t.cpu()
+                dist.all_reduce(kc, op=dist.ReduceOp.MAX)
+                key_t.copy_(kc)
+            rsac.winner(ev.p2, ev.p3, K, key_t, args.thr, context=ctxs[j])
             return key_t
-        if nccl:
-            dist.all_reduce(key_t, op=dist.ReduceOp.MAX)
-        else:  # gloo rehearsal: host round trip
-            kc = key_t.cpu()
-            dist.all_reduce(kc, op=dist.ReduceOp.MAX)
-            key_t.copy_(kc)
-        rsac.winner(ev.p2, ev.p3, K, key_t, args.thr)
-        return key_t
 
     # W untimed warmup steps, continued until at least WARMUP_MIN_S of them have run: the GPU's
     # clock ramps up under sustained load, and 10 steps after 3 warmup steps ran 13 % slower than
     # at steady state (0.367 vs 0.325 ms/step on one box); the timed region is still exactly K steps
     # (the extra count is agreed over the ranks, so every rank runs the same number of steps)
     t_w = time.perf_counter()
-    for _ in range(max(1, args.warmup)):
-        step()
+    for i in range(max(1, args.warmup)):
+        step(i)
     torch.cuda.synchronize()
     spent = time.perf_counter() - t_w
     extra = max(0, math.ceil((WARMUP_MIN_S - spent) / (spent / max(1, args.warmup))))
@@ -132,25 +144,32 @@ def main():
         dist.all_reduce(ex, op=dist.ReduceOp.MAX)
         extra = int(ex.item())
     for i in range(extra):
-        step()
+        step(i)
         if i % 16 == 15:
             torch.cuda.synchronize()  # keep the host within a few steps of the GPU
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        key_t = step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        et = torch.tensor([elapsed], dtype=torch.float64, device=par._comm_device(None))
-        dist.all_reduce(et, op=dist.ReduceOp.MAX)
-        elapsed = float(et.item())
 
+    def timed(serial):
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            key_t = step(i, serial)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if dist is not None:
+            et = torch.tensor([elapsed], dtype=torch.float64, device=par._comm_device(None))
+            dist.all_reduce(et, op=dist.ReduceOp.MAX)
+            elapsed = float(et.item())
+        return elapsed, key_t
+
+    elapsed, key_t = timed(False)
+    elapsed_serial, key_serial = timed(True) if nstreams > 1 else (elapsed, key_t)
     cnt = int(key_t.item()) >> 32
+    if int(key_serial.item()) != int(key_t.item()):
+        raise RuntimeError("pipelined and serial steps picked different winners")
     # kernel times of the same call, from the HIP events of synchronous runs (outside the timed
     # loop): score_ms spans the scoring kernel alone (k_pnp_score_mf), solve_ms k_pnp_solve
     for _ in range(10):
@@ -248,13 +267,16 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step_serial": elapsed_serial / args.steps * 1e3,
+            "streams": nstreams,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32+f64",
             "data": "synthetic (rsac.synth.pnp_problem seed 0: UTM-scale points, main_v1.py K, N(0,1px) noise)",
             "config": {"workload": "C2: 10k 2D-3D correspondences, 50% outliers, P3P, thr 30 px, "
-                                   f"{H} hypotheses per GPU per step, global best via RCCL all-reduce(MAX)",
+                                   f"{H} hypotheses per GPU per step, global best via RCCL all-reduce(MAX); "
+                                   f"steps alternate over {nstreams} contexts / HIP streams",
                        "points": args.points, "hypotheses_per_gpu": H, "outlier_ratio": 0.5,
                        "parallelism": f"dp{world} (hypothesis shards)"},
             "ms_to_best_model": ms_to_best,

@@ -126,6 +126,7 @@ struct rsac_ctx {
     PinBuf h_lmfail;                                           // multi-block refit failure word (device-written)
     int dbg_refit_max_blocks = 0;                              // RSAC_DBG_REFIT_MAX_BLOCKS (0: device limit)
     int64_t spec_finishes = 0, spec_redos = 0;                 // RSAC_DBG_SPEC_FINISHES / _REDOS
+    int32_t dbg_cell_pts = 0;                                  // RSAC_DBG_MF_CELL_PTS
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf reproj;                                             // reprojection errors / the K sweep's inputs
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
@@ -324,6 +325,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     a.queue = c->queue.as<int>();
     a.exact_only = (flags & RSAC_F_EXACT_ONLY) ? 1 : 0;
     a.sample_k = (flags & RSAC_F_MINIMAL_EPNP5) ? 5 : 4;
+    a.dbg_cell_pts = c->dbg_cell_pts;
     float *C = c->centred.as<float>();
     int32_t max_n = 0;
     for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
@@ -1066,6 +1068,10 @@ int rsac_debug_set(rsac_ctx *c, int32_t key, int64_t value) {
         return RSAC_OK;
     case RSAC_DBG_REFIT_DROP_BLOCK:
         c->lm.drop_block = value != 0;
+        return RSAC_OK;
+    case RSAC_DBG_MF_CELL_PTS:
+        if (value < 0 || value > (1 << 30)) return fail(RSAC_EINVAL, "bad cell size");
+        c->dbg_cell_pts = (int32_t)value;
         return RSAC_OK;
     default:
         return fail(RSAC_EINVAL, "unknown debug key %d", key);

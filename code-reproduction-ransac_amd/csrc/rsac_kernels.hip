@@ -2237,6 +2237,10 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
         cell_pts = cp;
         cell_tiles = tiles;
     }
+    if (a.dbg_cell_pts > 0) {  // test hook: every tile by cells of dbg_cell_pts points (a multiple of 256)
+        cell_pts = std::min<int64_t>(std::max<int64_t>(256, a.dbg_cell_pts / 256 * 256), win_pts);
+        cell_tiles = tiles;
+    }
     const int64_t cells = (max_n + cell_pts - 1) / cell_pts;
     const int64_t tb = tiles - cell_tiles;
     const int64_t units = tb + cell_tiles * cells;

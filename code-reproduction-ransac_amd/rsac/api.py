@@ -370,7 +370,7 @@ def score_poses(points2D, points3D, K, poses, reproj_thresh: float = 30.0, devic
 
 def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_thresh: float = 30.0, *,
                    seed: int = 0x5EED, device=None, return_info: bool = False, exact_only: bool = False,
-                   with_mask: bool = False, device_result: bool = False):
+                   with_mask: bool = False, device_result: bool = False, context=None):
     """Evaluate Philox hypotheses [hyp_begin, hyp_begin + n_hyps) of one problem.
 
     Returns (key, model12[, mask][, info]) where key = (count << 32) | (0xFFFFFFFF - best_index)
@@ -379,12 +379,14 @@ def evaluate_range(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_th
 
     device_result=True (GPU tensor inputs): nothing waits for the GPU; key is a 1-element int64
     tensor (raw packed key, 0 = no model) and model12 a float64 tensor, both on the device.
+    context: an rsac Context of its own (default: the device's shared one) -- calls on different
+    contexts and torch streams may run concurrently (each context has its own device scratch).
     """
     p3 = _In(points3D, 3)
     p2 = _In(points2D, 2)
     if device_result and not p3.device:
         raise ValueError("device_result needs GPU tensor inputs")
-    ctx = L.context(_device_of(p3, device))
+    ctx = context if context is not None else L.context(_device_of(p3, device))
     flags = (L.F_DEVICE_IN if p3.device else 0) | (L.F_EXACT_ONLY if exact_only else 0)
     K9 = _K9(K)
     st = L.Stats()
@@ -446,15 +448,17 @@ def hypothesis_rows(points2D, points3D, K, hyp_begin: int, n_hyps: int, reproj_t
     return rows
 
 
-def winner(points2D, points3D, K, key, reproj_thresh: float = 30.0, *, seed: int = 0x5EED, with_mask: bool = True):
+def winner(points2D, points3D, K, key, reproj_thresh: float = 30.0, *, seed: int = 0x5EED, with_mask: bool = True,
+           context=None):
     """Re-derive the hypothesis named by a device packed key (e.g. after an all-reduce) on this
-    GPU: (model12 tensor, mask tensor) without a host round trip (rsac_pnp_winner)."""
+    GPU: (model12 tensor, mask tensor) without a host round trip (rsac_pnp_winner).  context: as
+    evaluate_range."""
     import torch
     p3 = _In(points3D, 3)
     p2 = _In(points2D, 2)
     if not p3.device:
         raise ValueError("winner() needs GPU tensor inputs")
-    ctx = L.context(_device_of(p3, None))
+    ctx = context if context is not None else L.context(_device_of(p3, None))
     dev = p3.keep.device
     model_t = torch.zeros(12, dtype=torch.float64, device=dev)
     mask_t = torch.empty(max(p3.n, 1), dtype=torch.uint8, device=dev) if with_mask else None

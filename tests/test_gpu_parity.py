@@ -895,3 +895,32 @@ def test_fixed_budget_device_pick_batched(sampler, minimal):
         soa, cam = O.soa_pnp(p["points3d"], p["points2d"]), O.cam_from_K(p["K"])
         Rl, tl, _ = O.pnp_refine(soa, ref["mask"].astype(np.uint8), cam, ref["R"].reshape(9), ref["t"])
         assert _bits_equal(R, Rl) and _bits_equal(t, tl)
+
+
+def test_two_contexts_on_two_streams_equal_serial():
+    """bench.py's pipelined steps: evaluate_range calls alternating between two contexts on two
+    torch streams (running concurrently) give every step the serial call's key, model and mask."""
+    import torch
+    from rsac import parallel as par
+    pr, soa, cam = _pnp_case(10000, 0.5, 0)
+    ev = par.PnPShard(pr["points2d"], pr["points3d"], pr["K"], 30.0, device=0)
+    H = 40_000
+    k0, m0, mk0 = rsac.evaluate_range(ev.p2, ev.p3, pr["K"], 0, H, 30.0, with_mask=True, device_result=True)
+    torch.cuda.synchronize()
+    ctxs = [rsac.context(0), rsac.Context(0)]
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    outs = []
+    for i in range(8):
+        j = i & 1
+        with torch.cuda.stream(streams[j]):
+            base = (i // 2) * 1000  # different ranges in flight at once
+            outs.append((base,) + rsac.evaluate_range(ev.p2, ev.p3, pr["K"], base, H, 30.0, with_mask=True,
+                                                      device_result=True, context=ctxs[j]))
+    torch.cuda.synchronize()
+    for base, k, m, mk in outs:
+        kr, mr, mkr = rsac.evaluate_range(ev.p2, ev.p3, pr["K"], base, H, 30.0, with_mask=True, device_result=True)
+        torch.cuda.synchronize()
+        assert int(k.item()) == int(kr.item())
+        assert _bits_equal(m.cpu().numpy(), mr.cpu().numpy())
+        np.testing.assert_array_equal(mk.cpu().numpy(), mkr.cpu().numpy())
+    assert int(outs[0][1].item()) == int(k0.item())
