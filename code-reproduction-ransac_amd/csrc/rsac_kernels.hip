@@ -688,6 +688,8 @@ __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
 // ---------------------------------------------------------------------------
 // PnP: sample + minimal solve, one lane per hypothesis
 // ---------------------------------------------------------------------------
+// 154 VGPRs, 3 waves/SIMD: capping it at 128 (4 waves) or 96 (5) spills and is slower on C2 (latency-
+// bound, 1.5 waves/SIMD) and on C3 (1M hypotheses) alike (scripts/mf_ab.py + scripts/c3_prof.py)
 __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
     const int hl = blockIdx.x * blockDim.x + threadIdx.x;
