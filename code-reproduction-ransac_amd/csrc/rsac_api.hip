@@ -209,11 +209,20 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
     HIPCHK(c->h_pts.ensure(sizeof(float) * nc * std::max<int64_t>(N, 1)));
     float *H = c->h_pts.as<float>();
     const double *A = (const double *)a, *B = (const double *)b;
-    for (int64_t i = 0; i < N; ++i) {
-        for (int k = 0; k < ncomp_a; ++k) H[k * N + i] = (float)A[ncomp_a * i + k];
-        H[ncomp_a * N + i] = (float)B[2 * i];
-        H[(ncomp_a + 1) * N + i] = (float)B[2 * i + 1];
-    }
+    auto convert = [&](int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            for (int k = 0; k < ncomp_a; ++k) H[k * N + i] = (float)A[ncomp_a * i + k];
+            H[ncomp_a * N + i] = (float)B[2 * i];
+            H[(ncomp_a + 1) * N + i] = (float)B[2 * i + 1];
+        }
+    };
+    // large batches (C3 handed over as host arrays: 2M points) convert in chunks on the host pool
+    constexpr int64_t kChunk = 16384;
+    if (N > 4 * kChunk)
+        parallel_for((int)((N + kChunk - 1) / kChunk),
+                     [&](int ch) { convert(ch * kChunk, std::min<int64_t>(N, (int64_t)(ch + 1) * kChunk)); });
+    else
+        convert(0, N);
     HIPCHK(hipMemcpyAsync(D, H, sizeof(float) * nc * N, hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(c->ev_pts, s));
     for (int k = 0; k < nc; ++k) st.h[k] = H + k * N;
