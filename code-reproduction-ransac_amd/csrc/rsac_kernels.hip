@@ -1467,7 +1467,12 @@ __global__ __launch_bounds__(kMfT) __attribute__((amdgpu_waves_per_eu(3, 8))) vo
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tiles_per_prob = (H + HB - 1) / HB;
-    const int n_units = tb + (tiles_per_prob * n_prob - tb) * cells;
+    // whole-tile units by XCD: blocks are dealt round-robin over the 8 XCDs, so counter k (blocks
+    // b = k mod 8) runs on XCD k; its units k + 8 i take the contiguous tiles k cpx + i, and a
+    // problem's tiles (and points) stay in one XCD's L2 (C3: 1.109 -> 1.077 ms per call, C2 +-0,
+    // scripts/mf_ab.py --c3).  Units past tb are empty.  Placement changes speed only.
+    const int cpx = (tb + kQSub - 1) / kQSub, tbx = cpx * kQSub;
+    const int n_units = tbx + (tiles_per_prob * n_prob - tb) * cells;
     const int qk = blockIdx.x % kQSub;  // this block's units: qk + kQSub i, i from counter qk
     int *const uq = unit_queue(queue, qk);
     int last_prob = -1, n_all = 0;
@@ -1484,14 +1489,22 @@ __global__ __launch_bounds__(kMfT) __attribute__((amdgpu_waves_per_eu(3, 8))) vo
         int nx = 0;
         if (threadIdx.x == 0) nx = atomicAdd(uq, 1);
         int tile, c0, c1;
-        if (unit < tb) {
-            tile = unit;
+        if (unit < tbx) {
+            tile = (unit % kQSub) * cpx + unit / kQSub;
             c0 = 0;
             c1 = cells;
         } else {
-            tile = tb + (unit - tb) / cells;
-            c0 = (unit - tb) % cells;
+            tile = tb + (unit - tbx) / cells;
+            c0 = (unit - tbx) % cells;
             c1 = c0 + 1;
+        }
+        if (unit < tbx && tile >= tb) {  // an empty unit (uniform): the slot protocol as a skipped cell
+            if (threadIdx.x == 0) {
+                asm volatile("" : "+v"(nx));
+                unit_s[par ^ 1] = qk + kQSub * nx;
+            }
+            __syncthreads();
+            continue;
         }
         const int prob = tile / tiles_per_prob;
         const int64_t h0 = hyp_begin + (int64_t)(tile % tiles_per_prob) * HB;

@@ -17,7 +17,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def worker(calls, steps):
+def worker(calls, steps, c3_calls=0):
     sys.path[:0] = [os.path.join(ROOT, "code-reproduction-ransac_amd")]
     import torch
     import rsac
@@ -56,9 +56,25 @@ def worker(calls, steps):
         k = step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / steps
+    c3 = None
+    if c3_calls:  # C3 (configs[2]) wall time per call, inputs in HBM
+        sys.path.insert(0, ROOT)
+        from bench import c3_problems
+        h2, h3, off, Ks = c3_problems()
+        g2, g3 = torch.from_numpy(h2).cuda(), torch.from_numpy(h3).cuda()
+        walls = []
+        for i in range(c3_calls + 3):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            out = rsac.pnp_ransac_batched_flat(g2, g3, off, Ks, 1024, 30.0, adaptive=False, refine=False)
+            torch.cuda.synchronize()
+            if i >= 3:
+                walls.append((time.perf_counter() - t) * 1e3)
+        c3 = {"ms": statistics.median(walls), "ninl_sum": int(out[3].sum())}
     print(json.dumps({"lib": os.environ.get("RSAC_LIB_PATH"), "score_ms": statistics.median(sc),
                       "score_min": min(sc), "solve_ms": statistics.median(so), "step_ms": ms,
-                      "key": int(k[0].item()), "prof": prof}), flush=True)
+                      "key": [int(k[0].item()), c3 and c3["ninl_sum"]], "c3_ms": c3 and c3["ms"],
+                      "prof": prof}), flush=True)
 
 
 def main():
@@ -68,16 +84,17 @@ def main():
     ap.add_argument("--calls", type=int, default=40)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--worker", action="store_true")
+    ap.add_argument("--c3", type=int, default=0, help="also time this many C3 calls per run")
     a = ap.parse_args()
     if a.worker:
-        worker(a.calls, a.steps)
+        worker(a.calls, a.steps, a.c3)
         return
     res = {lib: [] for lib in a.libs}
     for r in range(a.rounds):
         for lib in a.libs:
             env = dict(os.environ, RSAC_LIB_PATH=os.path.abspath(lib))
             out = subprocess.run([sys.executable, "-u", __file__, "--worker", "--calls", str(a.calls), "--steps",
-                                  str(a.steps)], env=env, capture_output=True, text=True, timeout=300)
+                                  str(a.steps), "--c3", str(a.c3)], env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(out.stdout, out.stderr, flush=True)
                 sys.exit(out.returncode)
@@ -85,10 +102,11 @@ def main():
             print(line, flush=True)
             res[lib].append(json.loads(line))
     keys = {json.dumps(v[0]["key"]) for v in res.values()}
-    print("summary (median over rounds): lib score_ms step_ms solve_ms; keys agree:", len(keys) == 1)
+    print("summary (median over rounds): lib score_ms step_ms solve_ms [c3_ms]; keys agree:", len(keys) == 1)
     for lib, v in res.items():
+        c3 = f" {statistics.median(x['c3_ms'] for x in v):.4f}" if a.c3 else ""
         print(f"  {os.path.basename(lib):24s} {statistics.median(x['score_ms'] for x in v):.4f} "
-              f"{statistics.median(x['step_ms'] for x in v):.4f} {statistics.median(x['solve_ms'] for x in v):.4f}")
+              f"{statistics.median(x['step_ms'] for x in v):.4f} {statistics.median(x['solve_ms'] for x in v):.4f}{c3}")
 
 
 if __name__ == "__main__":
