@@ -34,5 +34,11 @@ if [ -n "$PMC" ]; then
       -d gpurun_out/prof/pmc_wait -o run --output-format csv -- \
       python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/pmc_wait.log 2>&1
   rc=$?; echo "rocprof pmc wait rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  # VALU issue per quad-cycle: one or two VALU issued, MFMA co-execution
+  timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_VALU_MFMA_COEXEC_CYCLES \
+      SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA SQ_INSTS GRBM_GUI_ACTIVE \
+      -d gpurun_out/prof/pmc_issue -o run --output-format csv -- \
+      python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ms-to-best --no-extras > gpurun_out/prof/pmc_issue.log 2>&1
+  rc=$?; echo "rocprof pmc issue rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 find gpurun_out/prof -name "*.csv" | head -20

@@ -92,6 +92,34 @@ def valu_summary(path, points, hyps):
     return out
 
 
+def issue_summary(path):
+    """VALU issue per SIMD quad-cycle (one / two VALU), from SQ_ACTIVE_INST_VALU(2)"""
+    names = ["SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_VALU2", "SQ_VALU_MFMA_COEXEC_CYCLES", "SQ_ACTIVE_INST_ANY",
+             "SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_SCA", "SQ_INSTS", "GRBM_GUI_ACTIVE"]
+    vals = {n: counter(path, n) for n in names}
+    if not vals["SQ_INSTS_VALU"] or not vals["GRBM_GUI_ACTIVE"]:
+        return None
+    m = {n: statistics.median(v) for n, v in vals.items() if v}
+    simds, quad = 1024, m["GRBM_GUI_ACTIVE"] / 8 / 4
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3 for r in csv.DictReader(open(path))
+           if SCORE in r["Kernel_Name"] and r.get("Start_Timestamp")]
+    us = statistics.median(dur)
+    return {"kernel": SCORE, "launches": len(vals["SQ_INSTS_VALU"]), "kernel_us_median_profiled": us,
+            "counters_median": m,
+            "derived": {"clock_ghz_profiled": m["GRBM_GUI_ACTIVE"] / 8 / us / 1e3,
+                        "valu_instr_per_simd": m["SQ_INSTS_VALU"] / simds, "simd_quad_cycles": quad,
+                        "quad_cycles_with_valu_issue_frac":
+                            (m["SQ_ACTIVE_INST_VALU"] - m.get("SQ_ACTIVE_INST_VALU2", 0)) / simds / quad,
+                        "quad_cycles_with_two_valu_frac": m.get("SQ_ACTIVE_INST_VALU2", 0) / simds / quad,
+                        "valu_issue_frac_of_2_per_quad": m["SQ_INSTS_VALU"] / simds / (2 * quad),
+                        "wave_active_frac": m["SQ_ACTIVE_INST_ANY"] / m["SQ_WAVE_CYCLES"],
+                        "mfma_coexec_cycles_per_simd": m.get("SQ_VALU_MFMA_COEXEC_CYCLES", 0) / simds},
+            "note": "SQ_ACTIVE_INST_* and SQ_WAVE_CYCLES in quad-cycles summed over waves; SQ_ACTIVE_INST_VALU2 = "
+                    "quad-cycles in which two VALU instructions issued on a SIMD; GRBM_GUI_ACTIVE summed over 8 "
+                    "XCDs. Its own rocprofv3 --pmc pass over bench.py --steps 3 --warmup 1 --no-cpu "
+                    "--no-ms-to-best --no-extras."}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
@@ -131,6 +159,9 @@ def main():
     wait = wait_summary(os.path.join(PROF, "pmc_wait", "run_counter_collection.csv"), args.points, args.hyps)
     if wait:
         json.dump(wait, open(os.path.join(OUT, "pmc_score_wait.json"), "w"), indent=1)
+    issue = issue_summary(os.path.join(PROF, "pmc_issue", "run_counter_collection.csv"))
+    if issue:
+        json.dump(issue, open(os.path.join(OUT, "pmc_score_issue.json"), "w"), indent=1)
     fk_all = per_kernel(os.path.join(PROF, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     wk_all = per_kernel(os.path.join(PROF, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     if fk_all or wk_all:
