@@ -120,6 +120,21 @@ def issue_summary(path):
                     "--no-ms-to-best --no-extras."}
 
 
+def solo_split(path):
+    """durations (us) of the scoring kernel's launches that overlap no other kernel, and of those that
+    do (bench.py's pipelined steps run two streams; its roofline times synchronous launches)"""
+    if not os.path.exists(path):
+        return [], []
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(path)))
+    solo, over = [], []
+    for s, e, n in iv:
+        if SCORE not in n:
+            continue
+        ov = any(o[0] < e and o[1] > s for o in iv if o != (s, e, n))
+        (over if ov else solo).append((e - s) / 1e3)
+    return solo, over
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
@@ -169,6 +184,12 @@ def main():
         for k in sorted(set(fk_all) | set(wk_all)):
             lines.append(f"| `{k}` | {fk_all.get(k, float('nan')):.0f} | {wk_all.get(k, float('nan')):.0f} |")
     lines += ["", f"scoring kernel average: {score_avg:.1f} us" if score_avg else "scoring kernel not found"]
+    solo, over = solo_split(os.path.join(PROF, "kt", "run_kernel_trace.csv"))
+    if solo:
+        lines.append(f"scoring kernel launches with no other kernel running: {len(solo)}, median "
+                     f"{statistics.median(solo):.1f} us (the span of bench.py's roofline: synchronous launches); "
+                     f"launches overlapping the other stream's kernels (pipelined steps): {len(over)}, median "
+                     f"{statistics.median(over):.1f} us" if over else "")
     if wait:
         lines += [f"scoring kernel wave cycles: {100 * wait['wait_any_frac']:.1f} % parked (SQ_WAIT_ANY), "
                   f"{100 * wait['wait_inst_any_frac']:.1f} % issue-stalled (SQ_WAIT_INST_ANY, of which LDS "
