@@ -415,6 +415,10 @@ LmScratch *lm_scratch(rsac_ctx *c, hipStream_t s) {
         c->lm.gran = (unsigned long long *)c->lmscr.p;
         c->lm.fail = c->h_lmfail.as<int32_t>();
         c->lm.launch = 0;
+        int coop = 0;
+        const char *ev = getenv("RSAC_REFIT_COOP");
+        if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device) == hipSuccess)
+            c->lm.coop = coop && ev && ev[0] == '1';  // opt-in: +25 us on C2 ms-to-best (scripts/refit_coop_ab.py)
     }
     if (c->lm.max_blocks == 0) {
         c->lm.max_blocks = pnp_refine_coresident(c->device);

@@ -207,6 +207,9 @@ struct LmScratch {
     int max_blocks = 0;        // blocks of one problem that can run at once (pnp_refine_coresident)
     int drop_block = 0;        // test hook RSAC_DBG_REFIT_DROP_BLOCK
     int32_t *fail = nullptr;   // pinned host word: a refit's range sums never arrived
+    int coop = 0;              // RSAC_REFIT_COOP=1: multi-block refits through hipLaunchCooperativeKernel
+                               // (co-residency guaranteed or the launch refused, then one block);
+                               // off by default: +25 us on C2 ms-to-best, +0.3 ms on C5
 };
 // co-resident k_pnp_refine blocks on `device` (occupancy x CUs, capped at kLmMaxBlocks; >= 1)
 int pnp_refine_coresident(int device);

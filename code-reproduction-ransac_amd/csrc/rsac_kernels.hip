@@ -3026,8 +3026,32 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
                 if (e != hipSuccess) return e;
                 scratch->launch = 1;
             }
-            hipLaunchKernelGGL(k_pnp_refine, dim3(launched, 1), dim3(kLmThreads), 0, s, a, mask, models, iters, p,
-                               scratch->gran, scratch->launch << 10, host_models, src, stop, G, scratch->fail);
+            if (!scratch->coop || launched < 2) {
+                hipLaunchKernelGGL(k_pnp_refine, dim3(launched, 1), dim3(kLmThreads), 0, s, a, mask, models, iters,
+                                   p, scratch->gran, scratch->launch << 10, host_models, src, stop, G, scratch->fail);
+                continue;
+            }
+            // the runtime either makes the G blocks co-resident or refuses the launch; refused
+            // (other work holds the CUs), one block walks every range: the same bits, no exchange
+            PnpArgs ka = a;
+            const uint8_t *kmask = mask;
+            double *kmodels = models, *khm = host_models;
+            int32_t *kiters = iters, *kfail = scratch->fail;
+            int kp = p, kstride = G;
+            unsigned long long *kgran = scratch->gran;
+            unsigned ktag = scratch->launch << 10;
+            const double *ksrc = src;
+            const int32_t *kstop = stop;
+            void *args[] = {&ka, &kmask, &kmodels, &kiters, &kp, &kgran, &ktag, &khm, &ksrc, &kstop, &kstride, &kfail};
+            const hipError_t e = hipLaunchCooperativeKernel((const void *)k_pnp_refine, dim3(launched, 1),
+                                                            dim3(kLmThreads), args, 0, s);
+            if (e == hipErrorCooperativeLaunchTooLarge) {
+                (void)hipGetLastError();
+                hipLaunchKernelGGL(k_pnp_refine, dim3(1, 1), dim3(kLmThreads), 0, s, a, mask, models, iters, p,
+                                   scratch->gran, scratch->launch << 10, host_models, src, stop, 1, scratch->fail);
+            } else if (e != hipSuccess) {
+                return e;
+            }
         }
     }
     return hipGetLastError();

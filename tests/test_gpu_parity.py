@@ -694,6 +694,35 @@ def test_refit_missing_block_recovers_with_one_block():
     assert _bits_equal(R, Ro) and _bits_equal(t, to)
 
 
+_COOP_CHILD = """
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import rsac
+from rsac import synth
+for n in (20000, 65537):
+    pr = synth.pnp_problem(n, 0.5, seed=77)
+    R, t, m = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=True)
+    print(np.asarray(R, np.float64).tobytes().hex(), np.asarray(t, np.float64).tobytes().hex())
+"""
+
+
+def test_refit_cooperative_launch_bit_exact():
+    # RSAC_REFIT_COOP=1 (read when a context first refits, hence a child process): the multi-block
+    # refit goes through hipLaunchCooperativeKernel; the pose is the oracle's, bit for bit
+    import subprocess
+    import sys
+    pkg = os.path.dirname(os.path.dirname(rsac.__file__))
+    out = subprocess.run([sys.executable, "-c", _COOP_CHILD, pkg], env=dict(os.environ, RSAC_REFIT_COOP="1"),
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = out.stdout.split("\n")
+    for n, line in zip((20000, 65537), lines):
+        _, _, Ro, to = _refit_case(n, 0.5)
+        rh, th = line.split()
+        assert rh == np.asarray(Ro, np.float64).tobytes().hex() and th == np.asarray(to, np.float64).tobytes().hex()
+
+
 # ---------------------------------------------------------------------------------------------
 # LO-RANSAC (BASELINE.json configs[4])
 # ---------------------------------------------------------------------------------------------
