@@ -164,8 +164,9 @@ struct Staged {
 };
 
 // ncomp3 = 3 for PnP (pts3d N x 3, pts2d N x 2 -> X Y Z U V), 2 for 2D-2D (src, dst -> SX SY DX DY)
-// defer: one device-input PnP problem of <= 65536 points is converted by pnp_args' frame
-// launch (the caller must call pnp_args next)
+// defer: one device-input PnP problem of <= 65536 points, or a batch of problems of at most
+// kSetupBatchMaxN points each, is converted by pnp_args' frame launch (the caller must call
+// pnp_args next)
 int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const int64_t *offsets, int32_t P, int32_t n,
                  uint32_t flags, hipStream_t s, Staged &st, bool defer = false) {
     st.P = P;
@@ -193,7 +194,9 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
     float *D = c->pts.as<float>();
     for (int k = 0; k < nc; ++k) st.d[k] = D + k * N;
     if (flags & RSAC_F_DEVICE_IN) {
-        if (ncomp_a == 3 && defer && P == 1 && N > 0 && N <= 65536) {
+        int64_t max_n = 0;
+        for (int p = 0; p < P; ++p) max_n = std::max<int64_t>(max_n, st.off[p + 1] - st.off[p]);
+        if (ncomp_a == 3 && defer && N > 0 && (P == 1 ? N <= 65536 : max_n <= kSetupBatchMaxN)) {
             st.prep = PnpPrepare{(const double *)a, (const double *)b, D, D + N, D + 2 * N, D + 3 * N, D + 4 * N};
             return RSAC_OK;
         }

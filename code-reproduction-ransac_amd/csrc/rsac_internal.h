@@ -158,6 +158,8 @@ struct PnpPrepare {
     int *ticket = nullptr;
 };
 constexpr int kSetupMaxBlocks = 256;
+// batches whose problems all have at most this many points set up in one launch (k_pnp_setup_b)
+constexpr int kSetupBatchMaxN = 8192;
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *bounds_ws, float *XC, float *YC,
                             float *ZC, double *frame, float *fconst, hipStream_t s,
                             const PnpPrepare *prep = nullptr);

@@ -129,15 +129,20 @@ __global__ __launch_bounds__(256) void k_pnp_bounds(PnpArgs a, int32_t P, int *_
     }
 }
 
-// B >= |XC|inf of problem prob (the frame's f[3]; recomputed identically wherever needed)
-__device__ __forceinline__ double frame_bound(const int *__restrict__ ws, int32_t P, int prob, int n) {
+// B >= |XC|inf of a problem from its ordered-int bounds wlo[0..2], whi[0..2] (the frame's f[3];
+// recomputed identically wherever needed)
+__device__ __forceinline__ double frame_bound2(const int *__restrict__ wlo, const int *__restrict__ whi, int n) {
     double B = 0;
     if (n > 0)
         for (int k = 0; k < 3; ++k) {
-            const double lo = ord2f(ws[5 * prob + k]), hi = ord2f(ws[5 * P + 5 * prob + k]);
+            const double lo = ord2f(wlo[k]), hi = ord2f(whi[k]);
             B = fmax(B, (hi - lo) * 0.5);
         }
     return B * (1.0 + 4.0 * kU32) + 1e-30;
+}
+// the same for problem prob of the bounds workspace ws ([0, 5P) mins, [5P, 10P) maxes)
+__device__ __forceinline__ double frame_bound(const int *__restrict__ ws, int32_t P, int prob, int n) {
+    return frame_bound2(ws + 5 * prob, ws + 5 * P + 5 * prob, n);
 }
 
 // k_pnp_bounds for one problem in one 1024-thread block: min / max written directly (the
@@ -184,9 +189,10 @@ __global__ __launch_bounds__(1024) void k_pnp_bounds1(PnpArgs a, int *__restrict
 // fconst = {fx fy cx cy T 2.002 sqrt(T) 1e-6 T thr 2/fx 2/fy cu cv cc0} (see the scoring kernel).
 // cgiven: the frame's centre (else the bounding box's midpoint); B then bounds |X - c| from the
 // bounds around that centre
-__device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *__restrict__ ws,
-                              double *__restrict__ frame, float *__restrict__ fconst,
-                              const double *cgiven = nullptr) {
+// wlo / whi: the problem's five ordered-int minima / maxima (X Y Z U V)
+__device__ void pnp_frame_core(const PnpArgs &a, int prob, const int *__restrict__ wlo, const int *__restrict__ whi,
+                               double *__restrict__ frame, float *__restrict__ fconst,
+                               const double *cgiven = nullptr) {
     const int n = (int)(a.offsets[prob + 1] - a.offsets[prob]);
     const double *cm = a.cams + 4 * prob;
     const double fx = fabs(cm[0]), fy = fabs(cm[1]), cx = cm[2], cy = cm[3];
@@ -194,17 +200,17 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
     const double thr = sqrt(T);
     double c[3] = {0, 0, 0}, du = 0, dv = 0;
     if (n > 0) {
-        for (int k = 0; k < 3; ++k) c[k] = ((double)ord2f(ws[5 * prob + k]) + (double)ord2f(ws[5 * P + 5 * prob + k])) * 0.5;
-        du = fmax(fabs(ord2f(ws[5 * prob + 3]) - cx), fabs(ord2f(ws[5 * P + 5 * prob + 3]) - cx));
-        dv = fmax(fabs(ord2f(ws[5 * prob + 4]) - cy), fabs(ord2f(ws[5 * P + 5 * prob + 4]) - cy));
+        for (int k = 0; k < 3; ++k) c[k] = ((double)ord2f(wlo[k]) + (double)ord2f(whi[k])) * 0.5;
+        du = fmax(fabs(ord2f(wlo[3]) - cx), fabs(ord2f(whi[3]) - cx));
+        dv = fmax(fabs(ord2f(wlo[4]) - cy), fabs(ord2f(whi[4]) - cy));
     }
-    double B = frame_bound(ws, P, prob, n);
+    double B = frame_bound2(wlo, whi, n);
     if (cgiven) {
         double Bg = 0;
         for (int k = 0; k < 3; ++k) {
             c[k] = cgiven[k];
             if (n > 0)
-                Bg = fmax(Bg, fmax((double)ord2f(ws[5 * P + 5 * prob + k]) - c[k], c[k] - (double)ord2f(ws[5 * prob + k])));
+                Bg = fmax(Bg, fmax((double)ord2f(whi[k]) - c[k], c[k] - (double)ord2f(wlo[k])));
         }
         B = Bg * (1.0 + 4.0 * kU32) + 1e-30;
     }
@@ -231,6 +237,11 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
     q[11] = (B <= 32768.0 && B >= 0.015625) ? 1.f : 0.f;
     q[12] = 0.f;
     for (int k = 13; k < kFconstStride; ++k) q[k] = 0.f;
+}
+__device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *__restrict__ ws,
+                              double *__restrict__ frame, float *__restrict__ fconst,
+                              const double *cgiven = nullptr) {
+    pnp_frame_core(a, prob, ws + 5 * prob, ws + 5 * P + 5 * prob, frame, fconst, cgiven);
 }
 
 // MFMA point operands (PnpArgs::PF / UV, k_pnp_score_mf) of one point from its centred
@@ -297,6 +308,87 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const 
         YC[q] = yc;
         ZC[q] = zc;
         if (a.PF) mx_point(a, q, xc, yc, zc, a.U[q], a.V[q], mk);
+    }
+}
+
+// A batch of short problems (each <= kSetupBatchMaxN points), one 256-thread block per problem:
+// k_pnp_prepare (CONVERT: the f64 AoS inputs rounded to the f32 SoA) + k_pnp_init + k_pnp_bounds
+// + k_pnp_center in one launch instead of four, the same values (the f32 conversion, the
+// ordered-int bounds as the sentinels + atomics leave them, the bounding-box frame, the centred
+// and MFMA coordinates).  CONVERT = false: the points are already a.X .. a.V.
+template <bool CONVERT>
+__global__ __launch_bounds__(256) void k_pnp_setup_b(const double *__restrict__ p3, const double *__restrict__ p2,
+                                                     PnpArgs a, int32_t P, float *__restrict__ X,
+                                                     float *__restrict__ Y, float *__restrict__ Z,
+                                                     float *__restrict__ U, float *__restrict__ V,
+                                                     int *__restrict__ ws, double *__restrict__ frame,
+                                                     float *__restrict__ fconst, float *__restrict__ XC,
+                                                     float *__restrict__ YC, float *__restrict__ ZC) {
+    __shared__ float sl[4][5], sh[4][5];
+    __shared__ int wsl[10];
+    const int prob = blockIdx.x;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const float *sX = CONVERT ? X : a.X, *sY = CONVERT ? Y : a.Y, *sZ = CONVERT ? Z : a.Z;
+    const float *sU = CONVERT ? U : a.U, *sV = CONVERT ? V : a.V;
+    float lo[5], hi[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
+#pragma unroll 4
+    for (int j = threadIdx.x; j < n; j += 256) {
+        const int64_t i = p0 + j;
+        float v[5];
+        if constexpr (CONVERT) {
+            v[0] = (float)p3[3 * i]; v[1] = (float)p3[3 * i + 1]; v[2] = (float)p3[3 * i + 2];
+            v[3] = (float)p2[2 * i]; v[4] = (float)p2[2 * i + 1];
+            X[i] = v[0]; Y[i] = v[1]; Z[i] = v[2]; U[i] = v[3]; V[i] = v[4];
+        } else {
+            v[0] = a.X[i]; v[1] = a.Y[i]; v[2] = a.Z[i]; v[3] = a.U[i]; v[4] = a.V[i];
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { lo[k] = fminf(lo[k], v[k]); hi[k] = fmaxf(hi[k], v[k]); }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
+        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { sl[wave][k] = lo[k]; sh[wave][k] = hi[k]; }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        const int k = threadIdx.x;
+        const float l = fminf(fminf(sl[0][k], sl[1][k]), fminf(sl[2][k], sl[3][k]));
+        const float h = fmaxf(fmaxf(sh[0][k], sh[1][k]), fmaxf(sh[2][k], sh[3][k]));
+        // as k_pnp_init's sentinels (0x7F7F7F7F / 0x80808080) after atomicMin / Max of f2ord
+        const int wl = n > 0 ? min(0x7F7F7F7F, f2ord(l)) : 0x7F7F7F7F;
+        const int wh = n > 0 ? max((int)0x80808080, f2ord(h)) : (int)0x80808080;
+        ws[5 * prob + k] = wl;
+        ws[5 * P + 5 * prob + k] = wh;
+        wsl[k] = wl;
+        wsl[5 + k] = wh;
+    }
+    if (prob == 0 && threadIdx.x == 0) {
+        if (a.best_key) *a.best_key = 0ull;
+        reset_pnp_queue(a.queue);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) pnp_frame_core(a, prob, wsl, wsl + 5, frame, fconst);
+    double cc[3] = {0, 0, 0};
+    if (n > 0)
+        for (int k = 0; k < 3; ++k) cc[k] = ((double)ord2f(wsl[k]) + (double)ord2f(wsl[5 + k])) * 0.5;
+    const MxPixel mk = mx_pixel(a, prob);
+    for (int j = threadIdx.x; j < n; j += 256) {  // this thread's own stores above: visible
+        const int64_t q = p0 + j;
+        const float xc = (float)((double)sX[q] - cc[0]), yc = (float)((double)sY[q] - cc[1]),
+                    zc = (float)((double)sZ[q] - cc[2]);
+        XC[q] = xc;
+        YC[q] = yc;
+        ZC[q] = zc;
+        if (a.PF) mx_point(a, q, xc, yc, zc, sU[q], sV[q], mk);
     }
 }
 
@@ -992,10 +1084,11 @@ __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p
 // rec0) over the points [start, n) of the problem (p0 its first point).  The unit's HB records are
 // staged in mlds; the counts are added atomically into zeroed counts.  Shared with
 // k_pnp_score_mf, which runs its problems outside the f16 operand range through it.
-template <int P, int HB>
+// NW: waves of the block (4; 2 in k_pnp_score_mf<2>)
+template <int P, int HB, int NW = 4>
 __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
                                         int lane, int wave, int (*red)[HB], float *mlds, int32_t *__restrict__ counts) {
-    constexpr int kStride = 4 * 64 * P;  // points one pass of the block covers: one cell
+    constexpr int kStride = NW * 64 * P;  // points one pass of the block covers
     const float *__restrict__ fc = a.fconst + (int64_t)prob * kFconstStride;
     const float cx = fc[2], cy = fc[3], inv_s = fc[9];
     const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
@@ -1063,7 +1156,9 @@ __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, 
     if (lane < HB) red[wave][lane] = cnt;
     __syncthreads();
     if (wave == 0 && lane < nh) {
-        const int sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+        int sum = red[0][lane];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) sum += red[w][lane];
         if (sum) atomicAdd(&counts[(int64_t)prob * a.hyp_stride + h0 + lane], sum);
     }
 }
@@ -1311,11 +1406,12 @@ typedef const __attribute__((address_space(4))) PnpArgs *KernargPnp;
 __device__ __forceinline__ KernargPnp kernarg_pnp() {
     return (KernargPnp)__builtin_amdgcn_kernarg_segment_ptr();
 }
+template <int W>
 __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, int64_t h0, int nh, int64_t p0,
                                                      int start, int n, int lane, int wave, int (*red)[32], float *mlds,
                                                      int32_t *__restrict__ counts) {
     const PnpArgs a = *(const PnpArgs *)ka;  // generic view (the host pass has no address spaces)
-    sc_unit<8, 32>(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
+    sc_unit<8, 32, W>(a, prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
 }
 
 
@@ -1325,15 +1421,18 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 // and each slot's band check (the smaller t of its two pairs against b'); a flagged iteration
 // goes to the wave's LDS list (at most kWrec: the launcher bounds a unit's points by 256 kWrec).  After its point loop the wave recounts its listed iterations
 // exactly (mf_recount) into the unit's LDS corrections, which the epilogue adds to the counts.
-constexpr int kMfW = 4;          // waves per block of k_pnp_score_mf (2: 13 % slower, scripts/mf_ab.py)
+// waves per block of k_pnp_score_mf<W>: 4 for long problems; 2 for batches of short ones, whose
+// units then run twice the iterations per wave over the same unit overhead (launch_mf; C3
+// 1.081 -> 1.028 ms, while C2 at 2 waves is 66 % slower: scripts/mf_ab.py)
+constexpr int kMfW = 4;
 constexpr int kWrec = 64;        // flagged iterations a wave lists per unit
-constexpr int kMfT = 64 * kMfW;  // threads per block = points one pass of the block covers
 
+template <int W>
 __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
                                         int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64],
                                         float (*ab)[2][4][4], mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *lcorr,
                                         int32_t *__restrict__ counts) {
-    constexpr int HB = 32;
+    constexpr int HB = 32, T = 64 * W;  // T: threads = points one pass of the block covers
     const int col = lane & 31, half = lane >> 5;
     const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
     const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
@@ -1347,7 +1446,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
         ab[1][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 13] : -__builtin_inff();
     }
     // the unit's A operands (the same for every wave): entry (t, lane) holds group t's
-    for (int e = threadIdx.x; e < 256; e += kMfT) {
+    for (int e = threadIdx.x; e < 256; e += T) {
         const int tl = e & 63;
         alds[e >> 6][tl] = mf_operand(recs, e >> 6, tl & 31, tl >> 5, nh);
     }
@@ -1361,7 +1460,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
         for (int g = 0; g < 4; ++g) vc[t][g] = 0u;
     int nw = 0;  // flagged iterations in the wave's list (uniform)
     const int b0 = start + wave * 64;
-    const int iters = n > b0 ? (n - b0 + kMfT - 1) / kMfT : 0;
+    const int iters = n > b0 ? (n - b0 + T - 1) / T : 0;
     // the A operands in registers for the whole unit; the slopes a' and bands b' are read from
     // LDS per group, ahead of the group's MFMAs (in registers they would cost 32 VGPRs)
     mf_h8 Ar[4];
@@ -1392,17 +1491,17 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
             ++nw;
         }
     };
-    const int full = n >= b0 + 64 ? (n - b0 - 64) / kMfT + 1 : 0;  // iterations with 64 points in range
+    const int full = n >= b0 + 64 ? (n - b0 - 64) / T + 1 : 0;  // iterations with 64 points in range
     for (int i = 0; i < full; ++i) {
         mf_h8 Ba, Bb;
         float2 ua, ub;
-        mf_load_full(PF, UV, b0 + kMfT * i, col, half, Ba, Bb, ua, ub);
+        mf_load_full(PF, UV, b0 + T * i, col, half, Ba, Bb, ua, ub);
         body(i, Ba, Bb, ua, ub);
     }
     if (full < iters) {
         mf_h8 Ba, Bb;
         float2 ua, ub;
-        mf_load_part(PF, UV, b0 + kMfT * full, n, col, half, Ba, Bb, ua, ub);
+        mf_load_part(PF, UV, b0 + T * full, n, col, half, Ba, Bb, ua, ub);
         body(full, Ba, Bb, ua, ub);
     }
     // the wave's flagged iterations recounted here: the wave's exact-test latency overlaps the
@@ -1412,7 +1511,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
 #pragma unroll 1
     for (int k = 0; k < nw; ++k) {
         const uint2 w = wrec[wave][k];
-        mf_recount(a, rec0, p0, n, w.y, nh, b0 + kMfT * (int)w.x, col, half, lcorr);
+        mf_recount(a, rec0, p0, n, w.y, nh, b0 + T * (int)w.x, col, half, lcorr);
     }
     // counts: lane (c, half) of wave w holds slot (t, g)'s count over its points; hypothesis j =
     // 8t + 2g + half sums 4 waves x 32 lanes (8 threads of 16 values each, then a shuffle tree)
@@ -1421,12 +1520,12 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
 #pragma unroll
         for (int g = 0; g < 4; ++g) cl[wave][4 * t + g][lane] = vc[t][g];
     __syncthreads();
-    constexpr int TPH = kMfT / 32, LPT = 32 / TPH;  // threads per hypothesis, lanes per thread
+    constexpr int TPH = T / 32, LPT = 32 / TPH;  // threads per hypothesis, lanes per thread
     const int j = threadIdx.x / TPH, p = threadIdx.x % TPH;
     const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + LPT * p;
     uint32_t sum = 0;
 #pragma unroll
-    for (int w = 0; w < kMfW; ++w)
+    for (int w = 0; w < W; ++w)
 #pragma unroll
         for (int l = 0; l < LPT; ++l) sum += cl[w][slot][l0 + l];
 #pragma unroll
@@ -1449,7 +1548,8 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
 // points).  Problems whose centred coordinates leave the f16 operand range (fconst[11] = 0) carry
 // form-1 records and run the sc_unit body.  3 waves per SIMD (168 VGPRs; forcing 4 spills and
 // costs 23 %, scripts/mf_ab.py).
-__global__ __launch_bounds__(kMfT) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_pnp_score_mf(
+template <int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_pnp_score_mf(
     PnpArgs a, int64_t hyp_begin, int32_t H, int32_t n_prob, int *__restrict__ queue, int32_t *__restrict__ counts,
     int tb, int cells, int cell_pts) {
     constexpr int HB = 32;
@@ -1457,9 +1557,9 @@ __global__ __launch_bounds__(kMfT) __attribute__((amdgpu_waves_per_eu(3, 8))) vo
     // while the other waves may still be reading this one's (a skipped cell runs no barrier
     // between the read at the loop's top and that write)
     __shared__ int unit_s[2];
-    __shared__ uint32_t cl[kMfW][16][64];
+    __shared__ uint32_t cl[W][16][64];
     __shared__ __attribute__((aligned(16))) float ab[2][2][4][4];
-    __shared__ uint2 wrec[kMfW][kWrec];
+    __shared__ uint2 wrec[W][kWrec];
     __shared__ int lcorr[32];  // the unit's exact-recount corrections
     __shared__ mf_h8 alds[4][64];
     __shared__ int red[4][HB];                                                 // sc_unit
@@ -1519,9 +1619,9 @@ __global__ __launch_bounds__(kMfT) __attribute__((amdgpu_waves_per_eu(3, 8))) vo
         const int n = min(n_all, c1 * cell_pts);
         if (start < n_all) {  // else a cell past a short problem of a batch (uniform)
             if (in_range)
-                mf_unit(a, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds, wrec, lcorr, counts);
+                mf_unit<W>(a, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds, wrec, lcorr, counts);
             else
-                mf_sc_unit(kernarg_pnp(), prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
+                mf_sc_unit<W>(kernarg_pnp(), prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
         }
         // the next unit (the other slot); the empty asm keeps the arithmetic on nx (and so the
         // wait for it) here
@@ -2099,10 +2199,25 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 
 // rounds of at most this many hypotheses (problems x hypotheses) are solved 4 lanes per
 // hypothesis (k_pnp_solve4); larger ones one lane per hypothesis (k_pnp_solve)
-constexpr int64_t kSolve4MaxHyps = 4096;
+#ifndef RSAC_SOLVE4_MAX
+#define RSAC_SOLVE4_MAX 4096
+#endif
+constexpr int64_t kSolve4MaxHyps = RSAC_SOLVE4_MAX;
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
                             double *frame, float *fconst, hipStream_t s, const PnpPrepare *prep) {
+    if (P > 1 && max_n <= kSetupBatchMaxN) {
+        // a batch of short problems: conversion (when deferred), bounds, frame and centring in
+        // one launch, one block per problem
+        if (prep && prep->p3)
+            hipLaunchKernelGGL(k_pnp_setup_b<true>, dim3(P), dim3(256), 0, s, prep->p3, prep->p2, a, P, prep->X,
+                               prep->Y, prep->Z, prep->U, prep->V, ws, frame, fconst, XC, YC, ZC);
+        else
+            hipLaunchKernelGGL(k_pnp_setup_b<false>, dim3(P), dim3(256), 0, s, (const double *)nullptr,
+                               (const double *)nullptr, a, P, (float *)nullptr, (float *)nullptr, (float *)nullptr,
+                               (float *)nullptr, (float *)nullptr, ws, frame, fconst, XC, YC, ZC);
+        return hipGetLastError();
+    }
     if (prep && prep->p3) {  // the deferred f64 -> f32 conversion of one problem, fused
         if (P != 1 || max_n > 65536) return hipErrorInvalidValue;
         if (prep->part && prep->ticket) {
@@ -2236,9 +2351,14 @@ static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H
 // flagged iterations per unit, so problems longer than 256 kWrec points run every tile by cells
 // (of up to that length; shorter while the units would not give each resident block four).
 // Returns hipErrorInvalidValue only for launches past the int32 unit space.
-static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
-                            hipStream_t s) {
-    static const int resident = resident_blocks(k_pnp_score_mf, kMfT);
+// Batches of short problems (more than one problem, every one of at most kMfShortN points) run the
+// 2-wave instance.
+constexpr int64_t kMfShortN = 4096;
+template <int W>
+static hipError_t launch_mf_w(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
+                              hipStream_t s) {
+    constexpr int kMfT = 64 * W;
+    static const int resident = resident_blocks(k_pnp_score_mf<W>, kMfT);
     if (a.counts_out != counts) zero_counts(counts, hyp_begin, H, P_, a.hyp_stride, s);
     const int64_t max_n = std::max<int64_t>(1, a.max_n);
     const int64_t tiles = (int64_t)P_ * ((H + 31) / 32);
@@ -2262,10 +2382,15 @@ static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
     if (units + kQSub * (int64_t)resident > INT32_MAX || tiles * 32 > INT32_MAX) return hipErrorInvalidValue;
     PnpArgs ka = a;
     ka.best_key = nullptr;  // reduced below from the complete counts
-    hipLaunchKernelGGL(k_pnp_score_mf, dim3(queue_grid(units, resident)), dim3(kMfT), 0, s, ka, hyp_begin, H, P_,
-                       a.queue, counts, (int)tb, (int)cells, (int)cell_pts);
+    hipLaunchKernelGGL(k_pnp_score_mf<W>, dim3(queue_grid(units, resident)), dim3(kMfT), 0, s, ka, hyp_begin, H,
+                       P_, a.queue, counts, (int)tb, (int)cells, (int)cell_pts);
     if (a.best_key) launch_best_key_of(a, hyp_begin, H, counts, s);
     return hipGetLastError();
+}
+static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
+                            hipStream_t s) {
+    if (P_ > 1 && a.max_n <= kMfShortN) return launch_mf_w<2>(a, P_, hyp_begin, H, counts, s);
+    return launch_mf_w<kMfW>(a, P_, hyp_begin, H, counts, s);
 }
 
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
