@@ -126,6 +126,7 @@ struct rsac_ctx {
     PinBuf h_lmfail;                                           // multi-block refit failure word (device-written)
     int dbg_refit_max_blocks = 0;                              // RSAC_DBG_REFIT_MAX_BLOCKS (0: device limit)
     int64_t spec_finishes = 0, spec_redos = 0;                 // RSAC_DBG_SPEC_FINISHES / _REDOS
+    int32_t scanrec_copy = 0;  // problems whose device scan records still go to h_scanrec (issue_scanrec_copy)
     int32_t dbg_cell_pts = 0;                                  // RSAC_DBG_MF_CELL_PTS
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf reproj;                                             // reprojection errors / the K sweep's inputs
@@ -219,14 +220,31 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
             H[(ncomp_a + 1) * N + i] = (float)B[2 * i + 1];
         }
     };
-    // large batches (C3 handed over as host arrays: 2M points) convert in chunks on the host pool
-    constexpr int64_t kChunk = 16384;
-    if (N > 4 * kChunk)
-        parallel_for((int)((N + kChunk - 1) / kChunk),
-                     [&](int ch) { convert(ch * kChunk, std::min<int64_t>(N, (int64_t)(ch + 1) * kChunk)); });
-    else
-        convert(0, N);
-    HIPCHK(hipMemcpyAsync(D, H, sizeof(float) * nc * N, hipMemcpyHostToDevice, s));
+    // large batches (C3 handed over as host arrays: 2M points) convert in chunks on the host pool;
+    // past kPipeMin points in kSlices slices, each copied (one 2D copy of its nc component ranges)
+    // while the pool converts the next
+    constexpr int64_t kChunk = 16384, kPipeMin = 16 * kChunk;
+    constexpr int kSlices = 4;
+    if (N > kPipeMin) {
+        const int64_t chunks = (N + kChunk - 1) / kChunk;
+        for (int sl = 0; sl < kSlices; ++sl) {
+            const int64_t c0 = chunks * sl / kSlices, c1 = chunks * (sl + 1) / kSlices;
+            parallel_for((int)(c1 - c0), [&](int ch) {
+                convert((c0 + ch) * kChunk, std::min<int64_t>(N, (c0 + ch + 1) * kChunk));
+            });
+            const int64_t i0 = c0 * kChunk, i1 = std::min<int64_t>(N, c1 * kChunk);
+            if (i1 > i0)
+                HIPCHK(hipMemcpy2DAsync(D + i0, sizeof(float) * N, H + i0, sizeof(float) * N,
+                                        sizeof(float) * (i1 - i0), nc, hipMemcpyHostToDevice, s));
+        }
+    } else {
+        if (N > 4 * kChunk)
+            parallel_for((int)((N + kChunk - 1) / kChunk),
+                         [&](int ch) { convert(ch * kChunk, std::min<int64_t>(N, (int64_t)(ch + 1) * kChunk)); });
+        else
+            convert(0, N);
+        HIPCHK(hipMemcpyAsync(D, H, sizeof(float) * nc * N, hipMemcpyHostToDevice, s));
+    }
     HIPCHK(hipEventRecord(c->ev_pts, s));
     for (int k = 0; k < nc; ++k) st.h[k] = H + k * N;
     st.host_ready = true;
@@ -611,8 +629,13 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
                 HIPCHK(launch_scan_records(c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, P, (int32_t)Hr,
                                            model_points, c->scanrec.as<ScanRecords>(), s,
                                            spec ? *spec : ScanDecide()));
-                HIPCHK(hipMemcpyAsync(c->h_scanrec.p, c->scanrec.p, sizeof(ScanRecords) * P, hipMemcpyDeviceToHost,
-                                      s));
+                // a speculative finish: copied behind the finish's mask kernel (issue_scanrec_copy),
+                // which would otherwise wait for the copy
+                if (spec)
+                    c->scanrec_copy = P;
+                else
+                    HIPCHK(hipMemcpyAsync(c->h_scanrec.p, c->scanrec.p, sizeof(ScanRecords) * P,
+                                          hipMemcpyDeviceToHost, s));
             }
             if (spec) {  // no synchronisation: the caller enqueues the finish, then spec_resolve
                 out.spec_pending = true;
@@ -685,12 +708,24 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
     return RSAC_OK;
 }
 
+// the deferred copy of a speculative round's device scan records to the host (run_loop)
+hipError_t issue_scanrec_copy(rsac_ctx *c, hipStream_t s) {
+    if (!c->scanrec_copy) return hipSuccess;
+    const size_t bytes = sizeof(ScanRecords) * c->scanrec_copy;
+    c->scanrec_copy = 0;
+    return hipMemcpyAsync(c->h_scanrec.p, c->scanrec.p, bytes, hipMemcpyDeviceToHost, s);
+}
+
 // after the stream synchronised: the host's replay of a speculative first round (one problem).
 // ok: it ended the scan with the winner the device picked (the finish enqueued on the device's
 // pick is the result); otherwise the caller starts over without speculation.
 int spec_resolve(rsac_ctx *c, const Staged &st, LoopOut &out, int model_points, double confidence, bool &ok,
                  bool fixed, int64_t stride, hipStream_t s) {
     const int P = fixed ? st.P : 1;
+    if (c->scanrec_copy) {  // not yet issued by a finish: copy and wait here
+        HIPCHK(issue_scanrec_copy(c, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
     const ScanRecords *recs = c->h_scanrec.as<ScanRecords>();
     out.spec_pending = false;
     ok = false;
@@ -773,6 +808,7 @@ int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const L
         else
             HIPCHK(launch_hom_mask(*(HomArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
     }
+    HIPCHK(issue_scanrec_copy(c, s));
     // the winners' records for the host (a refit copies the refined ones instead)
     if (!defer_sync && !(model == Model::PnP && N > 0))
         HIPCHK(hipMemcpyAsync(c->h_bestmodels.p, c->bestmodels.p, sizeof(double) * kModelStride * P,

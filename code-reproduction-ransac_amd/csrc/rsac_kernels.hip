@@ -1424,6 +1424,13 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 // waves per block of k_pnp_score_mf<W>: 4 for long problems; 2 for batches of short ones, whose
 // units then run twice the iterations per wave over the same unit overhead (launch_mf; C3
 // 1.081 -> 1.028 ms, while C2 at 2 waves is 66 % slower: scripts/mf_ab.py)
+// wave priority (s_setprio) of the scorer: 1 = raised (2) from the end of a wave's point loop
+// through its recounts, the count epilogue and the next unit's staging, back to 0 for the point
+// loop, so the waves a block's barriers wait for get the SIMD first (C2 scoring -1 %,
+// scripts/mf_ab.py r03d; 2 / 3 / 4: static priority by block group / wave probes)
+#ifndef RSAC_MF_PRIO
+#define RSAC_MF_PRIO 1
+#endif
 constexpr int kMfW = 4;
 constexpr int kWrec = 64;        // flagged iterations a wave lists per unit
 
@@ -1492,6 +1499,11 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
         }
     };
     const int full = n >= b0 + 64 ? (n - b0 - 64) / T + 1 : 0;  // iterations with 64 points in range
+#if RSAC_MF_PRIO == 1
+    __builtin_amdgcn_s_setprio(0);
+#elif RSAC_MF_PRIO == 4
+    if ((blockIdx.x / kQSub) & 1) __builtin_amdgcn_s_setprio(1); else __builtin_amdgcn_s_setprio(0);
+#endif
     for (int i = 0; i < full; ++i) {
         mf_h8 Ba, Bb;
         float2 ua, ub;
@@ -1506,6 +1518,11 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
     }
     // the wave's flagged iterations recounted here: the wave's exact-test latency overlaps the
     // other blocks' waves on its SIMD
+#if RSAC_MF_PRIO == 1
+    __builtin_amdgcn_s_setprio(2);
+#elif RSAC_MF_PRIO == 4
+    if ((blockIdx.x / kQSub) & 1) __builtin_amdgcn_s_setprio(3); else __builtin_amdgcn_s_setprio(2);
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
@@ -1574,6 +1591,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     const int cpx = (tb + kQSub - 1) / kQSub, tbx = cpx * kQSub;
     const int n_units = tbx + (tiles_per_prob * n_prob - tb) * cells;
     const int qk = blockIdx.x % kQSub;  // this block's units: qk + kQSub i, i from counter qk
+#if RSAC_MF_PRIO == 2
+    if ((blockIdx.x / kQSub) & 1) __builtin_amdgcn_s_setprio(1);
+#elif RSAC_MF_PRIO == 3
+    if (wave >= 2) __builtin_amdgcn_s_setprio(1);
+#endif
     int *const uq = unit_queue(queue, qk);
     int last_prob = -1, n_all = 0;
     int64_t p0 = 0;
@@ -2354,6 +2376,9 @@ static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H
 // Batches of short problems (more than one problem, every one of at most kMfShortN points) run the
 // 2-wave instance.
 constexpr int64_t kMfShortN = 4096;
+#ifndef RSAC_MF_SHORT_W
+#define RSAC_MF_SHORT_W 2
+#endif
 template <int W>
 static hipError_t launch_mf_w(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
                               hipStream_t s) {
@@ -2389,7 +2414,7 @@ static hipError_t launch_mf_w(const PnpArgs &a, int32_t P_, int64_t hyp_begin, i
 }
 static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    if (P_ > 1 && a.max_n <= kMfShortN) return launch_mf_w<2>(a, P_, hyp_begin, H, counts, s);
+    if (P_ > 1 && a.max_n <= kMfShortN) return launch_mf_w<RSAC_MF_SHORT_W>(a, P_, hyp_begin, H, counts, s);
     return launch_mf_w<kMfW>(a, P_, hyp_begin, H, counts, s);
 }
 

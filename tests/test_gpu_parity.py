@@ -227,6 +227,30 @@ def test_device_inputs_match_host_inputs():
     assert _bits_equal(Rd, R) and _bits_equal(td, t)
 
 
+def test_batched_host_inputs_pipelined_staging_match_device_inputs():
+    # host f64 batches past 262 144 points are converted and copied in slices (2D copies of the
+    # SoA components, rsac_api.hip stage_points): the same winners, counts and masks as the same
+    # batch handed over as device tensors
+    import torch
+    probs = [synth.pnp_problem(2000, 0.5, seed=500 + s) for s in range(160)]
+    off = np.zeros(161, np.int64)
+    off[1:] = np.cumsum([len(p["points3d"]) for p in probs])
+    h2 = np.concatenate([p["points2d"] for p in probs])
+    h3 = np.concatenate([p["points3d"] for p in probs])
+    Ks = np.stack([p["K"] for p in probs])
+    Rh, th, okh, nh, mh = rsac.pnp_ransac_batched_flat(h2, h3, off, Ks, 256, 30.0, adaptive=False, refine=False)
+    Rd, td, okd, nd, md = rsac.pnp_ransac_batched_flat(torch.from_numpy(h2).cuda(), torch.from_numpy(h3).cuda(),
+                                                       off, Ks, 256, 30.0, adaptive=False, refine=False)
+    np.testing.assert_array_equal(okh, okd)
+    np.testing.assert_array_equal(nh, nd)
+    np.testing.assert_array_equal(np.asarray(mh), md.cpu().numpy())
+    assert _bits_equal(Rh, Rd) and _bits_equal(th, td)
+    for i in (0, 79, 159):  # and the oracle on a few problems of each slice
+        ref = O.pnp_ransac(probs[i]["points3d"], probs[i]["points2d"], probs[i]["K"], 30.0, 0.99, 256, 0x5EED)
+        assert nh[i] == ref["n_inliers"]
+        assert _bits_equal(Rh[i], ref["R"]) and _bits_equal(th[i], ref["t"])
+
+
 def test_score_poses_vs_oracle_counts():
     pr, soa, cam = _pnp_case(7000, 0.5, 41)
     rng = np.random.default_rng(0)
