@@ -233,9 +233,16 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
                 convert((c0 + ch) * kChunk, std::min<int64_t>(N, (c0 + ch + 1) * kChunk));
             });
             const int64_t i0 = c0 * kChunk, i1 = std::min<int64_t>(N, c1 * kChunk);
-            if (i1 > i0)
+            if (i1 > i0) {
+#if RSAC_STAGE_1D
+                for (int k = 0; k < nc; ++k)
+                    HIPCHK(hipMemcpyAsync(D + k * N + i0, H + k * N + i0, sizeof(float) * (i1 - i0),
+                                          hipMemcpyHostToDevice, s));
+#else
                 HIPCHK(hipMemcpy2DAsync(D + i0, sizeof(float) * N, H + i0, sizeof(float) * N,
                                         sizeof(float) * (i1 - i0), nc, hipMemcpyHostToDevice, s));
+#endif
+            }
         }
     } else {
         if (N > 4 * kChunk)
