@@ -220,38 +220,16 @@ int stage_points(rsac_ctx *c, const void *a, const void *b, int ncomp_a, const i
             H[(ncomp_a + 1) * N + i] = (float)B[2 * i + 1];
         }
     };
-    // large batches (C3 handed over as host arrays: 2M points) convert in chunks on the host pool;
-    // past kPipeMin points in kSlices slices, each copied (one 2D copy of its nc component ranges)
-    // while the pool converts the next
-    constexpr int64_t kChunk = 16384, kPipeMin = 16 * kChunk;
-    constexpr int kSlices = 4;
-    if (N > kPipeMin) {
-        const int64_t chunks = (N + kChunk - 1) / kChunk;
-        for (int sl = 0; sl < kSlices; ++sl) {
-            const int64_t c0 = chunks * sl / kSlices, c1 = chunks * (sl + 1) / kSlices;
-            parallel_for((int)(c1 - c0), [&](int ch) {
-                convert((c0 + ch) * kChunk, std::min<int64_t>(N, (c0 + ch + 1) * kChunk));
-            });
-            const int64_t i0 = c0 * kChunk, i1 = std::min<int64_t>(N, c1 * kChunk);
-            if (i1 > i0) {
-#if RSAC_STAGE_1D
-                for (int k = 0; k < nc; ++k)
-                    HIPCHK(hipMemcpyAsync(D + k * N + i0, H + k * N + i0, sizeof(float) * (i1 - i0),
-                                          hipMemcpyHostToDevice, s));
-#else
-                HIPCHK(hipMemcpy2DAsync(D + i0, sizeof(float) * N, H + i0, sizeof(float) * N,
-                                        sizeof(float) * (i1 - i0), nc, hipMemcpyHostToDevice, s));
-#endif
-            }
-        }
-    } else {
-        if (N > 4 * kChunk)
-            parallel_for((int)((N + kChunk - 1) / kChunk),
-                         [&](int ch) { convert(ch * kChunk, std::min<int64_t>(N, (int64_t)(ch + 1) * kChunk)); });
-        else
-            convert(0, N);
-        HIPCHK(hipMemcpyAsync(D, H, sizeof(float) * nc * N, hipMemcpyHostToDevice, s));
-    }
+    // large batches (C3 handed over as host arrays: 2M points) convert in chunks on the host pool
+    // (converting and copying in slices, the copies overlapping the conversion, measured no
+    // faster within the host's run-to-run spread: DESIGN.md §6)
+    constexpr int64_t kChunk = 16384;
+    if (N > 4 * kChunk)
+        parallel_for((int)((N + kChunk - 1) / kChunk),
+                     [&](int ch) { convert(ch * kChunk, std::min<int64_t>(N, (int64_t)(ch + 1) * kChunk)); });
+    else
+        convert(0, N);
+    HIPCHK(hipMemcpyAsync(D, H, sizeof(float) * nc * N, hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(c->ev_pts, s));
     for (int k = 0; k < nc; ++k) st.h[k] = H + k * N;
     st.host_ready = true;

@@ -227,10 +227,10 @@ def test_device_inputs_match_host_inputs():
     assert _bits_equal(Rd, R) and _bits_equal(td, t)
 
 
-def test_batched_host_inputs_pipelined_staging_match_device_inputs():
-    # host f64 batches past 262 144 points are converted and copied in slices (2D copies of the
-    # SoA components, rsac_api.hip stage_points): the same winners, counts and masks as the same
-    # batch handed over as device tensors
+def test_batched_large_host_inputs_match_device_inputs():
+    # a host f64 batch of 320 000 points (converted on the host pool in chunks, one copy,
+    # rsac_api.hip stage_points): the same winners, counts and masks as the same batch handed
+    # over as device tensors (converted on the device by k_pnp_setup_b)
     import torch
     probs = [synth.pnp_problem(2000, 0.5, seed=500 + s) for s in range(160)]
     off = np.zeros(161, np.int64)
@@ -245,7 +245,7 @@ def test_batched_host_inputs_pipelined_staging_match_device_inputs():
     np.testing.assert_array_equal(nh, nd)
     np.testing.assert_array_equal(np.asarray(mh), md.cpu().numpy())
     assert _bits_equal(Rh, Rd) and _bits_equal(th, td)
-    for i in (0, 79, 159):  # and the oracle on a few problems of each slice
+    for i in (0, 79, 159):  # and the oracle on a few problems
         ref = O.pnp_ransac(probs[i]["points3d"], probs[i]["points2d"], probs[i]["K"], 30.0, 0.99, 256, 0x5EED)
         assert nh[i] == ref["n_inliers"]
         assert _bits_equal(Rh[i], ref["R"]) and _bits_equal(th[i], ref["t"])
