@@ -204,6 +204,27 @@ def test_pnp_batched_long_problem_cells_equals_oracle():
         assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
 
 
+def test_pnp_batched_many_long_problems_by_cells():
+    # a large batch of problems longer than one inline-recount unit (16 384 points):
+    # 48 x 20 000 points, so every tile runs by cells on the 4-wave scorer; no segment bound, no
+    # launch split, every problem's winner equals a one-problem call's, a few the oracle's
+    probs = [synth.pnp_problem(20000, 0.6, seed=700 + i) for i in range(48)]
+    out = rsac.pnp_ransac_batched([p["points2d"] for p in probs], [p["points3d"] for p in probs],
+                                  [p["K"] for p in probs], 512, 30.0, refine=False, adaptive=False)
+    for i in (0, 23, 47):
+        p = probs[i]
+        R, t, m, ni = out[i]
+        ref = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 0.99, 512, 0x5EED)
+        assert ni == ref["n_inliers"]
+        np.testing.assert_array_equal(m, ref["mask"])
+        assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+    for i in range(0, 48, 6):
+        R1, t1, m1 = rsac.pnp_ransac(probs[i]["points2d"], probs[i]["points3d"], probs[i]["K"], 512, 30.0,
+                                     refine=False, adaptive=False)
+        np.testing.assert_array_equal(m1, out[i][2])
+        assert _bits_equal(R1, out[i][0]) and _bits_equal(t1, out[i][1])
+
+
 def test_k_sweep_batched():
     """testpro-K.py:58-75 as one batched call over the 27 intrinsics."""
     Ks = synth.testpro_k_candidates()
