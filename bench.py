@@ -430,7 +430,7 @@ def extra_workloads(local, args):
                 walls.append((time.perf_counter() - t) * 1e3)
         fin[str(mode).lower()] = statistics.median(walls)
     out["final_solve_ms_to_best"] = dict(fin, note="pnp_ransac wall time, adaptive, C2 problem; refine=False/lm/"
-                                                    "epnp (solvePnPRansac SOLVEPNP_P3P)/epnp+lm")
+                                                    "epnp (solvePnPRansac's final solve after SOLVEPNP_P3P)/epnp+lm")
     return out
 
 

@@ -1466,6 +1466,8 @@ int rsac_pnp_orientation_sweep(rsac_ctx *c, const double *pts3d, const double *p
     if (r) return r;
     if (n < 4) return fail(RSAC_ETOOFEW, "solvePnPRansac needs >= 4 correspondences (got %d)", n);
     if (n_k < 1 || !pts3d || !pts2d || !Ks || !best_out) return fail(RSAC_EINVAL, "bad arguments");
+    // solvePnPRefineLM on the winner needs >= 3 inliers: a lower gate would fail only after the sweep
+    if (min_inliers < 3) return fail(RSAC_EINVAL, "min_inliers must be >= 3 (got %d)", min_inliers);
     if (flags & (RSAC_F_DEVICE_IN | RSAC_F_DEVICE_SOA | RSAC_F_DEVICE_OUT | RSAC_F_LO | RSAC_F_ASYNC))
         return fail(RSAC_EINVAL, "the K sweep takes host arrays (no device, LO or async flags)");
     hipStream_t s = pick_stream(c, stream);

@@ -2326,11 +2326,11 @@ static unsigned queue_grid(int64_t units, int resident) {
     return (unsigned)std::max<int64_t>(1, g);
 }
 
-static void zero_counts(int32_t *counts, int64_t hyp_begin, int32_t H, int32_t P, int64_t stride, hipStream_t s) {
-    if (P == 1)
-        (void)hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
-    else
-        (void)hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * stride, 0, sizeof(int32_t) * H, P, s);
+// the cell units add their counts atomically onto these zeros: a failed memset must fail the launch
+static hipError_t zero_counts(int32_t *counts, int64_t hyp_begin, int32_t H, int32_t P, int64_t stride,
+                              hipStream_t s) {
+    if (P == 1) return hipMemsetAsync(counts + hyp_begin, 0, sizeof(int32_t) * H, s);
+    return hipMemset2DAsync(counts + hyp_begin, sizeof(int32_t) * stride, 0, sizeof(int32_t) * H, P, s);
 }
 
 static void launch_best_key_of(const PnpArgs &a, int64_t hyp_begin, int32_t H, const int32_t *counts, hipStream_t s) {
@@ -2350,7 +2350,8 @@ hipError_t launch_pnp_best_key(const PnpArgs &a, int64_t hyp_begin, int32_t H, c
 // blocks' finishing times.  Counts are zeroed (by the solve kernel, else here) and added
 // atomically; the best key is reduced afterwards.
 template <int P, int W>
-static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts, hipStream_t s) {
+static hipError_t launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
+                            hipStream_t s) {
     auto kern = k_pnp_score_sc<P, 32, W>;
     static const int resident = resident_blocks(kern);
     const int64_t cells = std::max<int64_t>(1, ((int64_t)a.max_n + 256 * P - 1) / (256 * P));
@@ -2358,13 +2359,17 @@ static void launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H
     const int64_t cell_tiles = std::min<int64_t>(tiles, resident);
     const int64_t tb = tiles - cell_tiles;
     const int64_t units = tb + cell_tiles * cells;
-    if (a.counts_out != counts) zero_counts(counts, hyp_begin, H, P_, a.hyp_stride, s);
+    if (a.counts_out != counts) {
+        const hipError_t e = zero_counts(counts, hyp_begin, H, P_, a.hyp_stride, s);
+        if (e != hipSuccess) return e;
+    }
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, resident));
     PnpArgs ka = a;
     ka.best_key = nullptr;  // reduced below from the complete counts
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ka, hyp_begin, H, P_, a.queue, counts, (int)tb,
                        (int)cells);
     if (a.best_key) launch_best_key_of(a, hyp_begin, H, counts, s);
+    return hipGetLastError();
 }
 
 // k_pnp_score_mf: whole-tile units, then one unit per cell for the last `resident` tiles (as
@@ -2384,7 +2389,10 @@ static hipError_t launch_mf_w(const PnpArgs &a, int32_t P_, int64_t hyp_begin, i
                               hipStream_t s) {
     constexpr int kMfT = 64 * W;
     static const int resident = resident_blocks(k_pnp_score_mf<W>, kMfT);
-    if (a.counts_out != counts) zero_counts(counts, hyp_begin, H, P_, a.hyp_stride, s);
+    if (a.counts_out != counts) {
+        const hipError_t e = zero_counts(counts, hyp_begin, H, P_, a.hyp_stride, s);
+        if (e != hipSuccess) return e;
+    }
     const int64_t max_n = std::max<int64_t>(1, a.max_n);
     const int64_t tiles = (int64_t)P_ * ((H + 31) / 32);
     int64_t cell_pts = 2048;
@@ -2424,8 +2432,7 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
         hipLaunchKernelGGL(k_pnp_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
     } else if (a.fmodels && !a.exact_only) {
         if (small_round(P, H)) {  // form-1 records (round_args): the small-round instance
-            launch_sc<2, 5>(a, P, hyp_begin, H, counts, s);
-            return hipGetLastError();
+            return launch_sc<2, 5>(a, P, hyp_begin, H, counts, s);
         }
         return launch_mf(a, P, hyp_begin, H, counts, s);
     } else

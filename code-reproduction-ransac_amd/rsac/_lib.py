@@ -38,7 +38,7 @@ F_MINIMAL_EPNP5 = 1 << 10
 DBG_REFIT_MAX_BLOCKS = 1
 DBG_REFIT_DROP_BLOCK = 2
 
-ABI_VERSION = 1
+ABI_VERSION = 2  # include/rsac.h RSAC_ABI_VERSION
 
 
 class Stats(C.Structure):

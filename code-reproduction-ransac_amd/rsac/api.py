@@ -71,8 +71,9 @@ def _device_of(inp: _In, device):
 
 def _flags(adaptive, refine, sampler, exact_only=False, minimal="p3p"):
     f = 0
-    # minimal: "p3p" (4-point samples, SOLVEPNP_P3P: the reference's kernel) or "epnp5" (5-point
-    # samples solved by EPnP: solvePnPRansac's default SOLVEPNP_ITERATIVE kernel, model_points 5)
+    # minimal: "p3p" (4-point samples, SOLVEPNP_P3P: this project's benchmark kernel, north_star's)
+    # or "epnp5" (5-point samples solved by EPnP: solvePnPRansac's default SOLVEPNP_ITERATIVE
+    # kernel, model_points 5 -- what the reference's calls run, main_v1.py:497, testpro-K.py:72)
     if minimal == "epnp5":
         f |= L.F_MINIMAL_EPNP5
     elif minimal != "p3p":
@@ -651,13 +652,20 @@ def intrinsics_grid(focal_lengths, sensor_sizes, image_size):
 
 def estimate_camera_orientation(pos3d, pixels, focal_lengths, sensor_sizes, image_size, known_camera_origin=None, *,
                                 n_iters: int = 5000, reproj_thresh: float = 30.0, confidence: float = 0.99,
-                                seed: int = 0x5EED, sampler: str = "philox", refine="lm", min_inliers: int = 6,
-                                device: int = 0, return_info: bool = False):
+                                seed: int = 0x5EED, sampler: str = "opencv", minimal: str = "epnp5", refine="lm",
+                                min_inliers: int = 6, device: int = 0, return_info: bool = False):
     """estimate_camera_orientation of testpro-K.py:39-125 as one GPU call sequence
     (rsac_pnp_orientation_sweep): solvePnPRansac under every candidate K (one batched launch), the
     mean inlier reprojection error of each on the device, the first K with the smallest, then
     solvePnPRefineLM of its pose on its inliers.  Returns (rvec, tvec) like the reference
-    ((None, None) when every K failed), or the OrientationResult with return_info=True."""
+    ((None, None) when every K failed), or the OrientationResult with return_info=True.
+
+    The defaults are what testpro-K.py:72-75 executes: cv2.solvePnPRansac with no `flags`, i.e.
+    SOLVEPNP_ITERATIVE -- EPnP on 5-point samples drawn from OpenCV's MWC stream
+    (minimal="epnp5", sampler="opencv"), then the LM final solve on the inliers (refine="lm").
+    minimal="p3p" / sampler="philox" run this project's benchmark kernel instead."""
+    if int(min_inliers) < 3:
+        raise ValueError("min_inliers must be >= 3 (solvePnPRefineLM needs 3 inliers)")
     P3 = np.ascontiguousarray(np.asarray(pos3d, np.float64).reshape(-1, 3))
     P2 = np.ascontiguousarray(np.asarray(pixels, np.float64).reshape(-1, 2))
     if P3.shape[0] != P2.shape[0]:
@@ -676,7 +684,7 @@ def estimate_camera_orientation(pos3d, pixels, focal_lengths, sensor_sizes, imag
     with ctx.lock:
         code = L.check(L.lib().rsac_pnp_orientation_sweep(
             ctx.handle, P3.ctypes.data, P2.ctypes.data, n, K9.ctypes.data, P, int(n_iters), float(reproj_thresh),
-            float(confidence), int(seed) & (2**64 - 1), _flags(True, refine, sampler), int(min_inliers),
+            float(confidence), int(seed) & (2**64 - 1), _flags(True, refine, sampler, minimal=minimal), int(min_inliers),
             C.byref(best), mean.ctypes.data, models.ctypes.data, status.ctypes.data, ninl.ctypes.data,
             masks.ctypes.data, R.ctypes.data, t.ctypes.data, None))
     ok = status == L.OK

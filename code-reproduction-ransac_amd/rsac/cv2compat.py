@@ -51,7 +51,7 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
 
     OpenCV's structure (solvepnp.cpp solvePnPRansac): the MWC subset sequence of
     RANSACPointSetRegistrator; the minimal kernel by flags -- SOLVEPNP_P3P / AP3P (and any
-    4-point input): P3P on 4-point samples (the reference's call, main_v1.py:497);
+    4-point input): P3P on 4-point samples (the benchmark kernel; no reference call passes it);
     otherwise (the default SOLVEPNP_ITERATIVE, EPNP, ...): EPnP on 5-point samples, with
     model_points = 5 in RANSACUpdateNumIters.  Final pose on the RANSAC inliers: EPnP for
     P3P / AP3P / EPNP (OpenCV re-solves P3P's inliers with EPnP); otherwise LM started from

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RSAC_ABI_VERSION 1
+#define RSAC_ABI_VERSION 2  /* 2: rsac_set_score_variant removed; rsac_pnp_hypotheses subset width follows RSAC_F_MINIMAL_EPNP5 */
 
 #if defined(__GNUC__)
 #define RSAC_EXPORT __attribute__((visibility("default")))
@@ -67,10 +67,13 @@ extern "C" {
 #define RSAC_F_DEVICE_OUT (1u << 5)     /* inlier mask output is a device pointer */
 #define RSAC_F_EXACT_ONLY (1u << 6)     /* disable the float32 pre-filter in scoring (A/B and tests) */
 #define RSAC_F_ASYNC (1u << 8)          /* rsac_pnp_evaluate_range: device outputs, no host wait (see there) */
-#define RSAC_F_EPNP (1u << 9)           /* PnP: EPnP on the inliers as the final solve (solvePnPRansac with
-                                           SOLVEPNP_P3P); with RSAC_F_REFINE, LM from the EPnP pose */
+#define RSAC_F_EPNP (1u << 9)           /* PnP: EPnP on the inliers as the final solve (what solvePnPRansac
+                                           runs after a SOLVEPNP_P3P minimal kernel); with RSAC_F_REFINE,
+                                           LM from the EPnP pose */
 #define RSAC_F_MINIMAL_EPNP5 (1u << 10) /* PnP: 5-point samples solved by EPnP -- solvePnPRansac's default
-                                           SOLVEPNP_ITERATIVE kernel (model_points = 5, also in
+                                           SOLVEPNP_ITERATIVE kernel, the one every reference call runs
+                                           (main_v1.py:497, testpro-K.py:72 pass no flags;
+                                           model_points = 5, also in
                                            RANSACUpdateNumIters); explicit subsets are then n x 5 */
 #define RSAC_F_LO (1u << 7)             /* LO-RANSAC (PnP, one problem): local optimisation at every new best,
                                            BASELINE.json configs[4]; see DESIGN.md "LO-RANSAC" */
@@ -262,7 +265,7 @@ RSAC_EXPORT int rsac_pnp_mask(rsac_ctx *ctx, const void *pts3d, const void *pts2
 
 /* cv2.solvePnP(..., flags=SOLVEPNP_EPNP) on the masked points (mask NULL = all), the
  * final solve cv2.solvePnPRansac runs on its inliers when the minimal solver is P3P
- * (main_v1.py:497).  Host arrays; the same computation as the device
+ * (flags=SOLVEPNP_P3P).  Host arrays; the same computation as the device
  * pass of RSAC_F_EPNP, bit for bit.  Returns RSAC_NO_MODEL for < 4 points or a degenerate
  * (planar) cloud. */
 RSAC_EXPORT int rsac_pnp_epnp(const double *pts3d, const double *pts2d, int32_t n, const double K[9],

@@ -346,18 +346,26 @@ def reproj_mean(points3d, points2d, K, R, t, mask):
 
 
 def estimate_camera_orientation(pos3d, pixels, Ks, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED,
-                                sampler="philox", min_inliers=6):
+                                sampler="opencv", min_inliers=6, minimal="epnp5"):
     """testpro-K.py:39-125 restated on the oracle's pieces: per K the RANSAC (pnp_ransac) + the LM
     final solve on its inliers (solvePnPRansac's SOLVEPNP_ITERATIVE final solvePnP), the gate,
     the mean inlier error through the pose's Rodrigues vector, the first strict minimum, then
-    the LM refit (solvePnPRefineLM) of the winner on its inlier subset."""
+    the LM refit (solvePnPRefineLM) of the winner on its inlier subset.  The defaults are the
+    reference's own mode (testpro-K.py:72-75 passes no flags: SOLVEPNP_ITERATIVE = EPnP on 5-point
+    MWC samples, model_points 5); minimal="p3p" / sampler="philox" is the benchmark kernel."""
     P3 = np.asarray(pos3d, np.float64).reshape(-1, 3)
     P2 = np.asarray(pixels, np.float64).reshape(-1, 2)
     soa = soa_pnp(P3, P2)
     rows = []
     best, best_err = -1, float("inf")
+    # the per-K RANSACs are independent (ctypes drops the GIL): run them on a thread pool, then
+    # select in the reference's loop order
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(len(Ks), os.cpu_count() or 1, 16)) as ex:
+        runs = list(ex.map(lambda K: pnp_ransac(P3, P2, K, thr, confidence, max_iters, seed, sampler=sampler,
+                                                minimal=minimal), Ks))
     for k, K in enumerate(Ks):
-        r = pnp_ransac(P3, P2, K, thr, confidence, max_iters, seed, sampler=sampler)
+        r = runs[k]
         if r["best"] < 0:
             rows.append(None)
             continue

@@ -1,5 +1,5 @@
 """EPnP on the inliers: the non-minimal final solve cv2.solvePnPRansac runs
-when its minimal solver is P3P (main_v1.py:497 with flags=SOLVEPNP_P3P).
+when its minimal solver is P3P (cv2.solvePnPRansac with flags=SOLVEPNP_P3P).
 
 OpenCV is not installed, so the algorithm is pinned to its restatement (oracle/rsac_oracle.c
 orc_pnp_epnp, the steps of OpenCV's epnp.cpp with this project's numerics) -- "parity unpinned"

@@ -1,8 +1,9 @@
 """The OpenCV-default minimal solver: cv2.solvePnPRansac with flags=SOLVEPNP_ITERATIVE samples
 5 points (model_points = 5) and solves each sample with EPnP (OpenCV solvepnp.cpp,
 PnPRansacCallback::runKernel with ransac_kernel_method = SOLVEPNP_EPNP); RANSACUpdateNumIters
-runs with model_points 5.  The reference's own call passes SOLVEPNP_P3P (main_v1.py:497), so this
-mode serves users of the default flags (rsac.cv2compat.solvePnPRansac).
+runs with model_points 5.  This is the kernel every reference call site runs (main_v1.py:497-502,
+testpro-K.py:72-75 pass no `flags`), and the default of rsac.estimate_camera_orientation and of
+rsac.cv2compat.solvePnPRansac.
 
 Oracle: orc_pnp_minimal_epnp5 (oracle/rsac_oracle.c) = orc_pnp_epnp on the 5 sampled points in
 sample order, the same restatement the final-solve EPnP tests pin (tests/test_epnp.py; "parity

@@ -151,17 +151,21 @@ def test_solve_pnp_ransac_shim_shapes_and_gate():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sampler", ["philox", "opencv"])
-def test_estimate_camera_orientation_matches_restatement(sampler):
+@pytest.mark.parametrize("sampler,minimal", [("opencv", "epnp5"), ("philox", "p3p"), ("opencv", "p3p")])
+def test_estimate_camera_orientation_matches_restatement(sampler, minimal):
     """testpro-K.py:39-125 on its own data (12 points, 27 intrinsics): the chosen K, every K's gate,
     mean inlier error (bitwise: the oracle restates the device's summation order) and pose, and the
-    refined (rvec, tvec) equal the oracle's composition of the same steps."""
+    refined (rvec, tvec) equal the oracle's composition of the same steps.  The first case is the
+    reference's own mode (testpro-K.py:72-75 passes no flags: EPnP on 5-point MWC samples + the LM
+    final solve), which is also the function's default; the others run the P3P benchmark kernel."""
+    kw = {} if (sampler, minimal) == ("opencv", "epnp5") else dict(sampler=sampler, minimal=minimal)
     res = rsac.estimate_camera_orientation(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, synth.TESTPRO_K_FOCALS,
                                            synth.TESTPRO_K_SENSORS, synth.TESTPRO_K_IMAGE, synth.TESTPRO_K_ORIGIN,
-                                           sampler=sampler, return_info=True)
+                                           return_info=True, **kw)
     Ks = synth.testpro_k_candidates()
     np.testing.assert_array_equal(res.K, np.stack(Ks))
-    ref = O.estimate_camera_orientation(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, Ks, sampler=sampler)
+    ref = O.estimate_camera_orientation(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, Ks, sampler=sampler,
+                                        minimal=minimal)
     assert res.best == ref["best"]
     for k, row in enumerate(ref["rows"]):
         if row is None:
@@ -185,14 +189,14 @@ def test_estimate_camera_orientation_matches_restatement(sampler):
     # reported, not asserted: test_pro.py:801-802 hard-codes fx=2529, fy=1365 (f=150 mm, 127x178
     # film), the reference sweep's pick under OpenCV's EPnP kernel
     f, (sw, sh) = res.focal_sensor[res.best]
-    print(f"K sweep ({sampler}): chose f={f} mm, {sw}x{sh} mm (fx={res.K[res.best][0, 0]:.1f}); "
+    print(f"K sweep ({sampler}, {minimal}): chose f={f} mm, {sw}x{sh} mm (fx={res.K[res.best][0, 0]:.1f}); "
           f"test_pro.py:801 hint f=150 mm 127x178 -> {'same' if (f, sw, sh) == (150, 127, 178) else 'different'}")
     # the ranking by distance to the known origin (testpro-K.py:103) is sorted
     d = [r[0] for r in res.ranking]
     assert d == sorted(d) and len(d) == int(res.ok.sum())
     # the plain call returns the reference's (rvec, tvec)
     rv, tv = rsac.estimate_camera_orientation(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, synth.TESTPRO_K_FOCALS,
-                                              synth.TESTPRO_K_SENSORS, synth.TESTPRO_K_IMAGE, sampler=sampler)
+                                              synth.TESTPRO_K_SENSORS, synth.TESTPRO_K_IMAGE, **kw)
     assert _bits_equal(rv, res.rvec) and _bits_equal(tv, res.tvec)
 
 
@@ -204,3 +208,11 @@ def test_estimate_camera_orientation_all_fail():
     P2 = np.tile(np.array([[100.0, 200.0]]), (8, 1))
     rv, tv = rsac.estimate_camera_orientation(P3, P2, [90, 100], [(102, 127)], (2142, 1620))
     assert rv is None and tv is None
+
+
+def test_estimate_camera_orientation_rejects_gate_below_three():
+    """ADVICE r03: a gate below 3 would let a winner through that solvePnPRefineLM cannot refine;
+    it is rejected before any device work (the C-ABI rejects it too: rsac_pnp_orientation_sweep)."""
+    with pytest.raises(ValueError, match="min_inliers"):
+        rsac.estimate_camera_orientation(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, [150], [(127, 178)],
+                                         synth.TESTPRO_K_IMAGE, min_inliers=2)
