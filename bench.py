@@ -334,12 +334,15 @@ def multi_gpu_legs(local, args, pr2):
     r5, w5 = par.adaptive_shards(ev5, 5000, 0.99, round_size=4096, lo=True, sync=sync)
     out["c5_sharded_lo"] = {"points": 100_000, "ms_to_best": w5 * 1e3, "best": r5.best, "iters": r5.iters,
                             "n_inliers": r5.n_inliers, "lo_improvements": r5.lo_improvements,
-                            "note": "sharded_ransac(lo=True): rounds of 4096 split over the ranks, all-gather of "
+                            "note": "sharded_ransac(lo=True): round 1 (256 hypotheses, LO) redundantly on every "
+                                    "rank with no collective; later rounds split over the ranks, all-gather of "
                                     "the rows (RCCL), device-listed scan, LO on every rank"}
     ev2 = par.PnPShard(pr2["points2d"], pr2["points3d"], pr2["K"], args.thr, device=local)
     r2, w2 = par.adaptive_shards(ev2, 5000, 0.99, round_size=4096, lo=False, sync=sync)
     out["ms_to_best_sharded"] = {"ms": w2 * 1e3, "best": r2.best, "iters": r2.iters, "n_inliers": r2.n_inliers,
-                                 "note": "C2 problem, sharded_ransac (adaptive, no refit), max over ranks"}
+                                 "note": "C2 problem, sharded_ransac (adaptive, no refit; round 1 redundantly on "
+                                         "every rank with the device's speculative finish, no collective when it "
+                                         "ends the scan), max over ranks"}
     return out
 
 

@@ -508,7 +508,8 @@ void add_times(rsac_ctx *c, double &gpu, double &solve, double &score) {
 }
 
 int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max_iters, double confidence,
-             uint32_t flags, hipStream_t s, LoopOut &out, const ScanDecide *spec = nullptr, bool resume = false) {
+             uint32_t flags, hipStream_t s, LoopOut &out, const ScanDecide *spec = nullptr, bool resume = false,
+             int max_rounds = 0) {
     const int P = st.P;
     const int64_t H = std::max(max_iters, 1);
     const bool adaptive = (flags & RSAC_F_ADAPTIVE) != 0;
@@ -558,6 +559,7 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
         for (auto &sc : out.scan) sc.reset((int)H);
     }
     for (int64_t hb = hb0, Hr = 0; hb < H; hb += Hr) {
+        if (max_rounds > 0 && out.rounds >= max_rounds) break;  // the caller goes on (first-round mode)
         Hr = std::min<int64_t>(cur, H - hb);
         cur = std::min<int64_t>(cur * 2, round);
         if (opencv) {
@@ -881,10 +883,12 @@ int pnp_finish(rsac_ctx *c, const Staged &st, const PnpArgs &a, const LoopOut &l
 int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *offsets, int32_t P, int32_t n,
              const double *K, int32_t n_iters, double thr, double conf, uint64_t seed, uint32_t flags, double *R_out,
              double *t_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out, rsac_stats *stats,
-             hipStream_t s) {
+             hipStream_t s, rsac_scan_state *first_round = nullptr) {
     int r = check_device(c);
     if (r) return r;
     if (P <= 0 || !K) return fail(RSAC_EINVAL, "bad problem count or K");
+    if (first_round && (P != 1 || !(flags & RSAC_F_ADAPTIVE) || (flags & RSAC_F_SAMPLER_OPENCV)))
+        return fail(RSAC_EINVAL, "first-round mode: one problem, adaptive, Philox sampler");
     Staged st;
     r = stage_points(c, pts3d, pts2d, 3, offsets, P, n, flags, s, st, true);
     if (r) return r;
@@ -918,8 +922,34 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     }
     LoopOut lo;
     lo.timing = stats != nullptr;
-    r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, spec ? &dec : nullptr);
+    // first-round mode (rsac_pnp_ransac_first_round): the loop stops after its first round when
+    // that round did not end the scan; the caller continues from the exported scan state
+    auto more = [&]() -> int {
+        const ScanState &sc = lo.scan[0];
+        *first_round = rsac_scan_state{sc.niters, sc.best, sc.iter, sc.max_good, sc.done ? 1 : 0};
+        if (sc.best >= 0 && (R_out || t_out)) {  // the best record so far (LO: the optimised model)
+            double m[kModelStride];
+            HIPCHK(hipMemcpyAsync(m, c->models.as<double>() + (size_t)kModelStride * sc.best,
+                                  sizeof(double) * kModelStride, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (R_out) memcpy(R_out, m, 9 * sizeof(double));
+            if (t_out) memcpy(t_out, m + 9, 3 * sizeof(double));
+        }
+        if (ninl_out) ninl_out[0] = sc.max_good;
+        if (stats) {
+            stats->best_hyp = sc.best;
+            stats->iters = sc.iter;
+            stats->hyps_scored = lo.scored;
+            stats->n_inliers = sc.max_good;
+            stats->rounds = lo.rounds;
+            stats->lo_improvements = lo.lo_improvements;
+        }
+        return RSAC_MORE;
+    };
+    r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, spec ? &dec : nullptr, false,
+                 first_round ? 1 : 0);
     if (r) return r;
+    if (first_round && !spec && !lo.scan[0].done) return more();
     const bool refit = (flags & (RSAC_F_REFINE | RSAC_F_EPNP)) != 0;
     r = pnp_finish(c, st, a, lo, stride, K, mask_out, flags, s, refit, lo.spec_pending);
     if (r) return r;
@@ -931,6 +961,13 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         if (!ok) {
             c->spec_redos++;
             // the host's replay rules: later rounds if the scan goes on, then the finish again
+            if (first_round && !lo.scan[0].done) {
+                if (lo.spec_H == 0) {  // the replay started over: the first round without speculation
+                    r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, nullptr, false, 1);
+                    if (r) return r;
+                }
+                if (!lo.scan[0].done) return more();
+            }
             if (!spec_fixed && !lo.scan[0].done) {
                 r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, nullptr, true);
                 if (r) return r;
@@ -950,6 +987,10 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     }
     int any = 0;
     for (int p = 0; p < P; ++p) any |= lo.scan[p].best >= 0;
+    if (first_round) {  // the call ran to the end: the caller has rsac_pnp_ransac's result
+        const ScanState &sc = lo.scan[0];
+        *first_round = rsac_scan_state{sc.niters, sc.best, sc.iter, sc.max_good, 1};
+    }
     if (stats) {
         stats->best_hyp = lo.scan[0].best;
         stats->iters = lo.scan[0].iter;
@@ -1155,6 +1196,19 @@ int rsac_pnp_ransac(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n
     return with_one_refit_block(c, [&] {
         return pnp_core(c, pts3d, pts2d, nullptr, 1, n, K, n_iters, thr, conf, seed, flags, R_out, t_out, &status,
                         &ninl, mask_out, stats, pick_stream(c, stream));
+    });
+}
+
+int rsac_pnp_ransac_first_round(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t n, const double K[9],
+                                int32_t n_iters, double thr, double conf, uint64_t seed, uint32_t flags,
+                                double R_out[9], double t_out[3], uint8_t *mask_out, rsac_scan_state *st_out,
+                                rsac_stats *stats, void *stream) {
+    if (n < 4) return fail(RSAC_ETOOFEW, "solvePnPRansac needs >= 4 correspondences (got %d)", n);
+    if (!st_out) return fail(RSAC_EINVAL, "st_out required");
+    int32_t status = 0, ninl = 0;
+    return with_one_refit_block(c, [&] {
+        return pnp_core(c, pts3d, pts2d, nullptr, 1, n, K, n_iters, thr, conf, seed, flags, R_out, t_out, &status,
+                        &ninl, mask_out, stats, pick_stream(c, stream), st_out);
     });
 }
 

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("RSAC_LIB_PATH") or os.path.join(_HERE, "librsac.so")
 # status codes / flags (include/rsac.h)
 OK = 0
 NO_MODEL = 1
+MORE = 2  # rsac_pnp_ransac_first_round: the first round did not end the scan
 EINVAL = -1
 ETOOFEW = -2
 EHIP = -3
@@ -105,6 +106,8 @@ SIGNATURES = [
     ("rsac_scan", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d]),
     ("rsac_pnp_refine_lm", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("rsac_pnp_reprojection_errors", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
+    ("rsac_pnp_ransac_first_round", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
+                                              C.POINTER(ScanState), C.POINTER(Stats), _vp]),
     ("rsac_pnp_hypothesis_rows", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i64, _i32, _d, _u64, _u32, _vp, _vp]),
     ("rsac_scan_device", C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _d, _i32, _vp, _vp]),
     ("rsac_pnp_orientation_sweep", C.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _i32, _d, _d, _u64, _u32, _i32, _vp,

@@ -183,6 +183,42 @@ def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float 
     return out + (_info(code, st),) if return_info else out
 
 
+def pnp_ransac_first_round(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
+                           confidence: float = 0.99, seed: int = 0x5EED, refine: bool = True, lo: bool = False,
+                           device=None):
+    """The multi-GPU adaptive loop's first round (rsac_pnp_ransac_first_round):
+    pnp_ransac (Philox, adaptive) capped at its first 256-hypothesis round, run redundantly on
+    every rank with no collective.  Returns (done, R, t, mask, scan, info) where scan is the Scan
+    after the round and info the RansacInfo: done=True -> (R, t, mask) is pnp_ransac's result (R
+    None: no model); done=False -> the scan goes on from scan.iters and (R, t) is the best model
+    so far (mask None)."""
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    if p3.n != p2.n:
+        raise ValueError(f"points3D ({p3.n}) and points2D ({p2.n}) differ in length")
+    if p3.device != p2.device:
+        raise ValueError("points3D and points2D must both be host arrays or both GPU tensors")
+    n = p3.n
+    ctx = L.context(_device_of(p3, device))
+    flags = _flags(True, refine, "philox") | (L.F_LO if lo else 0) | (L.F_DEVICE_IN if p3.device else 0)
+    R, t = np.zeros(9), np.zeros(3)
+    mask, mptr, mflag = _mask_buffer(p3, n)
+    flags |= mflag
+    scan = Scan(n_iters, n, confidence, 4)
+    st = L.Stats()
+    with ctx.lock:
+        code = L.check(L.lib().rsac_pnp_ransac_first_round(
+            ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr), n, _K9(K).ctypes.data, int(n_iters),
+            float(reproj_thresh), float(confidence), int(seed) & (2**64 - 1), flags, R.ctypes.data, t.ctypes.data,
+            C.c_void_p(mptr), C.byref(scan.st), C.byref(st), _stream_of(p3)))
+    info = _info(code, st)
+    if code == L.MORE:
+        has = scan.best >= 0
+        return False, (R.reshape(3, 3) if has else None), (t if has else None), None, scan, info
+    m = _finish_mask(mask, n)
+    return True, (R.reshape(3, 3) if code == L.OK else None), (t if code == L.OK else None), m, scan, info
+
+
 def homography_ransac(src, dst, reproj_thresh: float = 3.0, *, max_iters: int = 2000, confidence: float = 0.995,
                       seed: int = 0x5EED, sampler: str = "opencv", adaptive: bool = True, refine: bool = True,
                       device=None, return_info: bool = False):

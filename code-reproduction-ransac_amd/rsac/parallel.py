@@ -35,6 +35,9 @@ import torch.distributed as dist
 from . import api
 
 KEY_IDX_MASK = 0xFFFFFFFF
+FIRST_ROUND = 256  # the single-GPU adaptive loop's first round (rsac_api.hip run_loop)
+MIN_SHARE = 256  # hypotheses per rank and sharded round, at least (one first round's worth)
+COLLECTIVES = 0  # data-path collectives issued by this module (the tests count them)
 
 
 def shard(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -87,9 +90,11 @@ def _comm_device(group):
 
 def all_reduce_max_key(key: int, group=None) -> int:
     """Global best packed key (all-reduce MAX of one int64; keys are < 2**63)."""
+    global COLLECTIVES
     _, world = _rank_world(group)
     if world == 1:
         return int(key)
+    COLLECTIVES += 1
     t = torch.tensor([int(key)], dtype=torch.int64, device=_comm_device(group))
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return int(t.item())
@@ -98,9 +103,11 @@ def all_reduce_max_key(key: int, group=None) -> int:
 def all_gather_chunks(t: torch.Tensor, group=None) -> torch.Tensor:
     """All-gather of equal-size tensors (one per rank, first axis = the rank's chunk) into one
     tensor in rank order, on the tensor's device (RCCL for device tensors, no host copy)."""
+    global COLLECTIVES
     _, world = _rank_world(group)
     if world == 1:
         return t
+    COLLECTIVES += 1
     dev = _comm_device(group)  # a gloo rehearsal on GPU tensors goes through the host
     src = t.to(dev).contiguous()
     out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=dev)
@@ -135,6 +142,16 @@ class PnPShard:
         if count > 0:
             api.hypothesis_rows(self.p2, self.p3, self.K, begin, count, self.thr, rows, seed=self.seed)
         return rows[:width]
+
+    def first_round(self, max_iters: int, confidence: float, lo: bool):
+        """The single-GPU adaptive loop's first round on this rank alone (rsac_pnp_ransac_first_round:
+        the device's speculative finish, one synchronisation) -> (done, model12 or None, Scan,
+        LO refits that raised the count)."""
+        done, R, t, _, scan, info = api.pnp_ransac_first_round(self.p2, self.p3, self.K, max_iters, self.thr,
+                                                               confidence=confidence, seed=self.seed, refine=False,
+                                                               lo=lo)
+        model = None if R is None else np.concatenate([np.asarray(R).reshape(9), np.asarray(t).reshape(3)])
+        return done, model, scan, info.lo_improvements
 
     def model(self, index: int) -> np.ndarray:
         """(R 9 row-major, t 3) of hypothesis ``index``, re-derived on this GPU from its Philox counter."""
@@ -184,39 +201,61 @@ def _round_rows(ev, begin: int, count: int, width: int, device) -> torch.Tensor:
     return rows
 
 
+def _scan_round(ev, scan, rows, hr: int, lo: bool, best_model, n_lo: int):
+    """Scan one round's {status, count} rows (hypothesis order) -> (best_model, n_lo)."""
+    if not lo:
+        scan.step_rows(rows, hr)
+        return best_model, n_lo
+    pos = 0
+    while not scan.done and pos < hr:
+        pos += scan.step_rows(rows[pos:], hr - pos, stop_on_improve=True)
+        if scan.improved:
+            m0 = ev.model(scan.best)
+            m, cnt, steps = ev.local_opt(m0, scan.max_good)
+            n_lo += steps
+            best_model = m if cnt > scan.max_good else m0
+            scan.raise_count(cnt)
+    return best_model, n_lo
+
+
 def sharded_ransac(ev, max_iters: int, confidence: float = 0.99, round_size: int = 4096, group=None,
                    model_points: int = 4, lo: bool = False) -> ShardedResult:
     """Adaptive RANSAC (OpenCV iteration semantics) with each round's hypotheses split over ranks.
 
-    Per round: every rank writes the {status, count} rows of its chunk (on its GPU for
-    PnPShard), one all-gather assembles the round in hypothesis order on every rank, and every
-    rank scans it identically (device-listed improvements for GPU rows).  lo=True: LO-RANSAC
-    (BASELINE.json configs[4]); the scan stops at every new best, every rank runs the same
-    (deterministic) local optimisation on its copy of the points, and the scan continues with
-    the raised count -- the single-GPU rsac.pnp_ransac(lo=True) result.
+    Round 1 is the single-GPU loop's first round (FIRST_ROUND hypotheses), run redundantly on
+    every rank with no collective (PnPShard: rsac_pnp_ransac_first_round, the device's speculative
+    finish); most scans end there (C2, C5), so a multi-GPU call costs what a one-GPU call does.
+    Later rounds double from max(2 FIRST_ROUND, MIN_SHARE x ranks) up to max(round_size,
+    MIN_SHARE x ranks) and are split over the ranks: every rank writes the {status, count} rows
+    of its chunk (on its GPU for PnPShard), one all-gather assembles the round in hypothesis order
+    on every rank, and every rank scans it identically (device-listed improvements for GPU rows).
+    lo=True: LO-RANSAC (BASELINE.json configs[4]); the scan stops at every new best, every rank
+    runs the same (deterministic) local optimisation on its copy of the points, and the scan
+    continues with the raised count -- the single-GPU rsac.pnp_ransac(lo=True) result.
     """
     rank, world = _rank_world(group)
     dev = _comm_device(group)
-    scan = api.Scan(max_iters, ev.n, confidence, model_points)
-    hb = 0
     best_model = None
     n_lo = 0
+    if hasattr(ev, "first_round"):
+        done, best_model, scan, n_lo = ev.first_round(max_iters, confidence, lo)
+        if done:
+            if scan.best < 0:
+                return ShardedResult(-1, 0, scan.iters, None)
+            return ShardedResult(scan.best, scan.max_good, scan.iters, best_model, n_lo)
+    else:
+        scan = api.Scan(max_iters, ev.n, confidence, model_points)
+        hr = min(FIRST_ROUND, max_iters, scan.niters)
+        best_model, n_lo = _scan_round(ev, scan, _round_rows(ev, 0, hr, hr, dev), hr, lo, best_model, n_lo)
+    hb = scan.iters
+    cur = max(2 * FIRST_ROUND, MIN_SHARE * world)
+    cap = max(int(round_size), MIN_SHARE * world)
     while not scan.done and hb < max_iters:
-        hr = min(int(round_size), max_iters - hb, scan.niters - hb)
+        hr = min(cur, max_iters - hb, scan.niters - hb)
+        cur = min(2 * cur, cap)
         b, c, w = chunk(hr, rank, world)
         full = all_gather_chunks(_round_rows(ev, hb + b, c, w, dev), group)  # rank order = hypothesis order
-        if not lo:
-            scan.step_rows(full, hr)
-        else:
-            pos = 0
-            while not scan.done and pos < hr:
-                pos += scan.step_rows(full[pos:], hr - pos, stop_on_improve=True)
-                if scan.improved:
-                    m0 = ev.model(scan.best)
-                    m, cnt, steps = ev.local_opt(m0, scan.max_good)
-                    n_lo += steps
-                    best_model = m if cnt > scan.max_good else m0
-                    scan.raise_count(cnt)
+        best_model, n_lo = _scan_round(ev, scan, full, hr, lo, best_model, n_lo)
         hb += hr
     if scan.best < 0:
         return ShardedResult(-1, 0, scan.iters, None)

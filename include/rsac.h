@@ -52,6 +52,7 @@ extern "C" {
 /* status codes */
 #define RSAC_OK 0
 #define RSAC_NO_MODEL 1
+#define RSAC_MORE 2 /* rsac_pnp_ransac_first_round: the first round did not end the scan */
 #define RSAC_EINVAL (-1)
 #define RSAC_ETOOFEW (-2) /* fewer than 4 correspondences (cv2 raises) */
 #define RSAC_EHIP (-3)
@@ -351,6 +352,22 @@ RSAC_EXPORT int rsac_scan_raise(rsac_scan_state *st, int32_t count, int32_t n, i
  * rsac_scan_device consumes such rows (device, count x 2) as rsac_scan / rsac_scan_until_best
  * would (stop_on_improve: return after a new best, *improved = 1): the improvements are listed on
  * the device and only they reach the host, where the iteration bound is applied. */
+/* The sharded adaptive loop's first round (rsac/parallel.py sharded_ransac):
+ * rsac_pnp_ransac of one problem (RSAC_F_ADAPTIVE, Philox sampler; RSAC_F_LO allowed) capped at
+ * its first round, the 256 hypotheses rsac_pnp_ransac starts with.  Every rank runs it
+ * redundantly, with no collective: most scans end inside that round (C2, C5).
+ *   - The round ended the scan: the call IS rsac_pnp_ransac (R, t, mask, refit as there; the
+ *     device's speculative finish, one synchronisation) and returns RSAC_OK / RSAC_NO_MODEL,
+ *     with *st_out the final scan state (done = 1).
+ *   - Otherwise it returns RSAC_MORE: *st_out is the scan state after the round (iter = its
+ *     length, done = 0), R_out / t_out the best model so far (LO: the locally optimised one),
+ *     mask_out undefined; the caller continues the scan from st_out->iter (sharded rounds).
+ * stats (optional) as rsac_pnp_ransac. */
+RSAC_EXPORT int rsac_pnp_ransac_first_round(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n,
+                                            const double K[9], int32_t n_iters, double reproj_thresh,
+                                            double confidence, uint64_t seed, uint32_t flags, double R_out[9],
+                                            double t_out[3], uint8_t *mask_out, rsac_scan_state *st_out,
+                                            rsac_stats *stats, void *stream);
 RSAC_EXPORT int rsac_pnp_hypothesis_rows(rsac_ctx *ctx, const void *pts3d, const void *pts2d, int32_t n,
                                          const double K[9], int64_t hyp_begin, int32_t n_hyps, double reproj_thresh,
                                          uint64_t seed, uint32_t flags, int32_t *rows_out, void *stream);

@@ -998,3 +998,39 @@ def test_two_contexts_on_two_streams_equal_serial():
         assert _bits_equal(m.cpu().numpy(), mr.cpu().numpy())
         np.testing.assert_array_equal(mk.cpu().numpy(), mkr.cpu().numpy())
     assert int(outs[0][1].item()) == int(k0.item())
+
+
+@pytest.mark.parametrize("n,outl,seed,lo", [(3000, 0.5, 41, False), (4000, 0.8, 42, False), (4000, 0.8, 43, True),
+                                            (3000, 0.4, 44, True)])
+def test_first_round_mode_equals_pnp_ransac(n, outl, seed, lo):
+    """rsac_pnp_ransac_first_round (the sharded loop's redundant round 1): when
+    the 256-hypothesis round ends the scan it is pnp_ransac bit for bit; otherwise its scan state
+    is the sequential scan of hypotheses [0, 256) and the best model so far, and the sharded loop
+    continued from it (one rank) ends where pnp_ransac does."""
+    from rsac import parallel as par
+    pr = synth.pnp_problem(n, outl, seed=seed)
+    done, R, t, mask, scan, finfo = rsac.pnp_ransac_first_round(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0,
+                                                         refine=False, lo=lo)
+    Rf, tf, mf, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0, refine=False, lo=lo,
+                                       return_info=True)
+    if done:
+        assert (scan.best, scan.max_good, scan.iters) == (info.best_hyp, info.n_inliers, info.iters)
+        assert finfo.lo_improvements == info.lo_improvements
+        assert _bits_equal(R, Rf) and _bits_equal(t, tf)
+        np.testing.assert_array_equal(mask, mf)
+    else:
+        assert scan.iters == par.FIRST_ROUND and info.iters > par.FIRST_ROUND
+        assert mask is None
+        if not lo:  # the scan of the round's rows, replayed on the host
+            st, cn, _ = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, par.FIRST_ROUND, 30.0)
+            ref = rsac.Scan(5000, n, 0.99, 4).step(cn, st)
+            assert (scan.best, scan.max_good, scan.niters) == (ref.best, ref.max_good, ref.niters)
+            m = np.concatenate([R.reshape(9), t])
+            ev = par.PnPShard(pr["points2d"], pr["points3d"], pr["K"], 30.0, device=0)
+            assert _bits_equal(m, ev.model(scan.best))
+    # the sharded loop (one rank) goes on from the exported state to pnp_ransac's result
+    ev = par.PnPShard(pr["points2d"], pr["points3d"], pr["K"], 30.0, device=0)
+    res = par.sharded_ransac(ev, 5000, 0.99, round_size=1024, lo=lo)
+    assert (res.best, res.n_inliers, res.iters) == (info.best_hyp, info.n_inliers, info.iters)
+    assert res.lo_improvements == info.lo_improvements
+    assert _bits_equal(res.model[:9].reshape(3, 3), Rf) and _bits_equal(res.model[9:], tf)

@@ -59,8 +59,15 @@ def _worker(rank, world, port, out_dir):
         pr = synth.pnp_problem(600, 0.6, seed=21)
         ev = OracleShard(pr)
         best = par.sharded_best(ev, 3001)
+        c0 = par.COLLECTIVES
         ada = par.sharded_ransac(ev, 5000, 0.99, round_size=100)
+        c1 = par.COLLECTIVES
+        ada2 = par.sharded_ransac(OracleShard(synth.pnp_problem(800, 0.75, seed=22)), 5000, 0.99, round_size=700)
+        c2 = par.COLLECTIVES
         lo = par.sharded_ransac(OracleShard(synth.pnp_problem(1500, 0.8, seed=8)), 5000, 0.99, round_size=97, lo=True)
+        c3 = par.COLLECTIVES
+        lo1 = par.sharded_ransac(OracleShard(synth.pnp_problem(700, 0.5, seed=23)), 5000, 0.99, round_size=97, lo=True)
+        c4 = par.COLLECTIVES
         # problem sharding: 5 problems over the ranks, rows computed locally from the restatement
         probs = [synth.pnp_problem(300, 0.4, seed=s) for s in range(5)]
 
@@ -75,7 +82,10 @@ def _worker(rank, world, port, out_dir):
         rows = par.sharded_batched(run_local, len(probs))
         res = {"best": [best.best, best.n_inliers, best.model.tolist()],
                "ada": [ada.best, ada.n_inliers, ada.iters, ada.model.tolist()],
+               "ada2": [ada2.best, ada2.n_inliers, ada2.iters, ada2.model.tolist()],
                "lo": [lo.best, lo.n_inliers, lo.iters, lo.model.tolist()],
+               "lo1": [lo1.best, lo1.n_inliers, lo1.iters, lo1.model.tolist()],
+               "collectives": [c1 - c0, c2 - c1, c3 - c2, c4 - c3],
                "rows": rows.tolist()}
         json.dump(res, open(os.path.join(out_dir, f"rank{rank}.json"), "w"))
     finally:
@@ -107,22 +117,39 @@ def test_sharded_best_equals_single_process(gloo_results):
     np.testing.assert_array_equal(model, ev.model(idx))
 
 
-def test_sharded_adaptive_equals_sequential_loop(gloo_results):
-    pr = synth.pnp_problem(600, 0.6, seed=21)
+@pytest.mark.parametrize("key,n,outl,seed", [("ada", 600, 0.6, 21), ("ada2", 800, 0.75, 22)])
+def test_sharded_adaptive_equals_sequential_loop(gloo_results, key, n, outl, seed):
+    pr = synth.pnp_problem(n, outl, seed=seed)
     ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
-    b, n, iters, model = gloo_results[0]["ada"]
-    assert (b, n, iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    b, cnt, iters, model = gloo_results[0][key]
+    assert (b, cnt, iters) == (ref["best"], ref["n_inliers"], ref["iters"])
     np.testing.assert_array_equal(np.array(model[:9]).reshape(3, 3), ref["R"])
     np.testing.assert_array_equal(model[9:], ref["t"])
 
 
-def test_sharded_lo_ransac_equals_sequential_loop(gloo_results):
-    pr = synth.pnp_problem(1500, 0.8, seed=8)
+@pytest.mark.parametrize("key,n,outl,seed", [("lo", 1500, 0.8, 8), ("lo1", 700, 0.5, 23)])
+def test_sharded_lo_ransac_equals_sequential_loop(gloo_results, key, n, outl, seed):
+    pr = synth.pnp_problem(n, outl, seed=seed)
     ref = O.pnp_ransac_lo(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000)
-    b, n, iters, model = gloo_results[0]["lo"]
-    assert (b, n, iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    b, cnt, iters, model = gloo_results[0][key]
+    assert (b, cnt, iters) == (ref["best"], ref["n_inliers"], ref["iters"])
     np.testing.assert_array_equal(np.array(model[:9]).reshape(3, 3), ref["R"])
     np.testing.assert_array_equal(model[9:], ref["t"])
+
+
+def test_sharded_first_round_runs_without_collectives(gloo_results):
+    """Round 1 (FIRST_ROUND hypotheses) runs redundantly on every rank: a scan that ends inside it
+    issues no collective at all; one that goes on all-gathers once per later round."""
+    iters = {k: gloo_results[0][k][2] for k in ("ada", "ada2", "lo", "lo1")}
+    coll = dict(zip(("ada", "ada2", "lo", "lo1"), gloo_results[0]["collectives"]))
+    for k, it in iters.items():
+        if it <= par.FIRST_ROUND:
+            assert coll[k] == 0, (k, it, coll[k])
+        else:
+            assert coll[k] >= 1, (k, it, coll[k])
+    # both kinds of scan are exercised
+    assert min(iters.values()) <= par.FIRST_ROUND < max(iters.values())
+    assert iters["ada"] <= par.FIRST_ROUND and iters["ada2"] > par.FIRST_ROUND
 
 
 def test_problem_shards_gather_in_order(gloo_results):
