@@ -141,6 +141,7 @@ struct rsac_ctx {
     DevBuf scanrec;                                            // first-round improvement records (P > 1)
     PinBuf h_scanrec;
     PinBuf h_pts, h_small, h_counts, h_status, h_subsets, h_substatus, h_best, h_bestmodels, h_mask, h_epnp;
+    PinBuf h_rowinfo;  // rsac_pnp_ransac_batched_rows: {record, n_inliers} per problem
 };
 
 // ---------------------------------------------------------------------------
@@ -883,7 +884,7 @@ int pnp_finish(rsac_ctx *c, const Staged &st, const PnpArgs &a, const LoopOut &l
 int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *offsets, int32_t P, int32_t n,
              const double *K, int32_t n_iters, double thr, double conf, uint64_t seed, uint32_t flags, double *R_out,
              double *t_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out, rsac_stats *stats,
-             hipStream_t s, rsac_scan_state *first_round = nullptr) {
+             hipStream_t s, rsac_scan_state *first_round = nullptr, double *rows_dev = nullptr) {
     int r = check_device(c);
     if (r) return r;
     if (P <= 0 || !K) return fail(RSAC_EINVAL, "bad problem count or K");
@@ -987,6 +988,16 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     }
     int any = 0;
     for (int p = 0; p < P; ++p) any |= lo.scan[p].best >= 0;
+    if (rows_dev) {  // the result rows on the device (rsac_pnp_ransac_batched_rows)
+        HIPCHK(c->h_rowinfo.ensure(sizeof(int64_t) * 2 * P));
+        int64_t *info = c->h_rowinfo.as<int64_t>();
+        for (int p = 0; p < P; ++p) {
+            info[2 * p] = lo.scan[p].best;
+            info[2 * p + 1] = lo.scan[p].max_good;
+        }
+        HIPCHK(launch_pnp_rows(info, c->bestmodels.as<double>(), P, rows_dev, s));
+        HIPCHK(hipStreamSynchronize(s));  // h_rowinfo is reused by the next call
+    }
     if (first_round) {  // the call ran to the end: the caller has rsac_pnp_ransac's result
         const ScanState &sc = lo.scan[0];
         *first_round = rsac_scan_state{sc.niters, sc.best, sc.iter, sc.max_good, 1};
@@ -1123,7 +1134,7 @@ void rsac_destroy(rsac_ctx *c) {
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_lmfail, &c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,
-                     &c->h_epnp};
+                     &c->h_epnp, &c->h_rowinfo};
     for (PinBuf *b : pin) b->release();
     c->lo_state_base = nullptr;
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1209,6 +1220,16 @@ int rsac_pnp_ransac_first_round(rsac_ctx *c, const void *pts3d, const void *pts2
     return with_one_refit_block(c, [&] {
         return pnp_core(c, pts3d, pts2d, nullptr, 1, n, K, n_iters, thr, conf, seed, flags, R_out, t_out, &status,
                         &ninl, mask_out, stats, pick_stream(c, stream), st_out);
+    });
+}
+
+int rsac_pnp_ransac_batched_rows(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *offsets, int32_t P,
+                                 const double *K, int32_t n_iters, double thr, double conf, uint64_t seed,
+                                 uint32_t flags, double *rows_out, uint8_t *mask_out, void *stream) {
+    if (!offsets || !rows_out) return fail(RSAC_EINVAL, "offsets and rows_out required");
+    return with_one_refit_block(c, [&] {
+        return pnp_core(c, pts3d, pts2d, offsets, P, 0, K, n_iters, thr, conf, seed, flags, nullptr, nullptr,
+                        nullptr, nullptr, mask_out, nullptr, pick_stream(c, stream), nullptr, rows_out);
     });
 }
 

@@ -145,6 +145,10 @@ hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t 
 hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s,
                                 int64_t rec0 = -1);
 
+// the problems' result rows (ok, n_inliers, R 9, t 3; f64, P x 14) on the device: info = P x
+// {record index (< 0: no model), n_inliers} int64 (host-pinned), models = the winners' records
+hipError_t launch_pnp_rows(const int64_t *info, const double *models, int32_t P, double *rows, hipStream_t s);
+
 // frame of every problem (centre, bounds, f32 constants) + centred coords;
 // also resets a.best_key (if set) and a.queue.  bounds_ws: P x 10 ints.
 // prep: a deferred device f64 -> f32 conversion of one problem (<= 65536 points) to fuse into

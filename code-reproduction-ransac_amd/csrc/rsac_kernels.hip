@@ -2479,6 +2479,27 @@ hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_
     return hipGetLastError();
 }
 
+// (ok, n_inliers, R 9, t 3) per problem from the winners' records (device) and the host's final
+// scan (pinned, read over the bus): the C3 problem-shard rows, handed to the all-gather on the
+// device (rsac_pnp_ransac_batched_rows)
+__global__ void k_pnp_rows(const int64_t *__restrict__ info, const double *__restrict__ models, int32_t P,
+                           double *__restrict__ rows) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P * 14) return;
+    const int p = i / 14, q = i % 14;
+    const bool ok = info[2 * p] >= 0;
+    double v = 0.0;
+    if (q == 0) v = ok ? 1.0 : 0.0;
+    else if (q == 1) v = ok ? (double)info[2 * p + 1] : 0.0;
+    else if (ok) v = models[(int64_t)p * kModelStride + (q - 2)];
+    rows[i] = v;
+}
+
+hipError_t launch_pnp_rows(const int64_t *info, const double *models, int32_t P, double *rows, hipStream_t s) {
+    hipLaunchKernelGGL(k_pnp_rows, dim3(cdiv((int64_t)P * 14, 256)), dim3(256), 0, s, info, models, P, rows);
+    return hipGetLastError();
+}
+
 hipError_t launch_pnp_mask_key(const PnpArgs &a, int32_t n, const unsigned long long *key, uint8_t *mask,
                                hipStream_t s) {
     unsigned g = cdiv(n > 0 ? n : 1, 256);

@@ -73,6 +73,8 @@ SIGNATURES = [
                                   C.POINTER(Stats), _vp]),
     ("rsac_pnp_ransac_batched", C.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,
                                           _vp, _vp, _vp]),
+    ("rsac_pnp_ransac_batched_rows", C.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _i32, _d, _d, _u64, _u32, _vp, _vp,
+                                               _vp]),
     ("rsac_homography_ransac", C.c_int, [_vp, _vp, _vp, _i32, _i32, _d, _d, _u64, _u32, _vp, _vp,
                                          C.POINTER(Stats), _vp]),
     ("rsac_homography_ransac_batched", C.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _d, _d, _u64, _u32, _vp, _vp, _vp,

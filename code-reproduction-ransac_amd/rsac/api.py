@@ -357,6 +357,38 @@ def pnp_ransac_batched_flat(points2D, points3D, offsets, Ks, n_iters: int = 5000
     return R.reshape(P, 3, 3), t, status == L.OK, ninl, _finish_mask(mask, p3.n)
 
 
+def pnp_ransac_batched_rows(points2D, points3D, offsets, Ks, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
+                            confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox",
+                            adaptive: bool = True, refine: bool = True, device=None, minimal: str = "p3p"):
+    """pnp_ransac_batched_flat with the results as one (P, 14) float64 tensor of rows (ok, n_inliers,
+    R 9, t 3) on the device, written there by the library (rsac_pnp_ransac_batched_rows): the
+    multi-GPU problem shards all-gather them with no host arrays in between.  Inputs as
+    pnp_ransac_batched_flat (device tensors stay on the device) -> (rows, mask)."""
+    import torch
+    p3 = _In(points3D, 3)
+    p2 = _In(points2D, 2)
+    off = np.ascontiguousarray(np.asarray(offsets, np.int64).reshape(-1))
+    P = off.size - 1
+    if P < 1 or off[0] != 0 or off[-1] != p3.n or p2.n != p3.n:
+        raise ValueError("offsets must run from 0 to the number of points")
+    if np.diff(off).min() < 4:
+        raise ValueError("every problem needs >= 4 correspondences")
+    Kf = np.ascontiguousarray(np.asarray(Ks, np.float64).reshape(P, 9))
+    dev = _device_of(p3, device)
+    ctx = L.context(dev)
+    flags = _flags(adaptive, refine, sampler, minimal=minimal) | (L.F_DEVICE_IN if p3.device else 0)
+    mask, mptr, mflag = _mask_buffer(p3, p3.n)
+    flags |= mflag
+    rows = torch.empty((P, 14), dtype=torch.float64, device=torch.device("cuda", dev))
+    stream = _stream_of(p3) if p3.device else C.c_void_p(torch.cuda.current_stream(rows.device).cuda_stream)
+    with ctx.lock:
+        L.check(L.lib().rsac_pnp_ransac_batched_rows(ctx.handle, C.c_void_p(p3.ptr), C.c_void_p(p2.ptr),
+                                                     off.ctypes.data, P, Kf.ctypes.data, int(n_iters),
+                                                     float(reproj_thresh), float(confidence), int(seed) & (2**64 - 1),
+                                                     flags, C.c_void_p(rows.data_ptr()), C.c_void_p(mptr), stream))
+    return rows, _finish_mask(mask, p3.n)
+
+
 def homography_ransac_batched(src_list, dst_list, reproj_thresh: float = 3.0, *, max_iters: int = 2000,
                               confidence: float = 0.995, seed: int = 0x5EED, sampler: str = "opencv",
                               adaptive: bool = True, refine: bool = True, device: int = 0):

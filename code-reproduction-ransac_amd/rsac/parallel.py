@@ -284,24 +284,17 @@ def sharded_batched(run_local, n_problems: int, group=None):
 
 
 def pnp_batched_rows(points2D, points3D, offsets, Ks, n_iters: int = 5000, reproj_thresh: float = 30.0, **kw):
-    """run_local for sharded_batched over rsac.pnp_ransac_batched_flat: the problems'
-    concatenated points (device tensors stay on the device) and offsets; rows
-    (ok, n_inliers, R 9, t 3)."""
+    """run_local for sharded_batched over rsac.pnp_ransac_batched_rows: the problems'
+    concatenated points (device tensors stay on the device) and offsets; rows (ok, n_inliers,
+    R 9, t 3) written on this rank's GPU by the library, so the all-gather takes them from HBM."""
     off = np.asarray(offsets, np.int64)
 
     def run(begin, count):
-        rows = np.zeros((count, 14))
         if count == 0:
-            return rows
+            return torch.zeros((0, 14), dtype=torch.float64)
         o0, o1 = int(off[begin]), int(off[begin + count])
-        R, t, ok, ninl, _ = api.pnp_ransac_batched_flat(points2D[o0:o1], points3D[o0:o1],
-                                                        off[begin:begin + count + 1] - o0,
-                                                        np.asarray(Ks)[begin:begin + count], n_iters, reproj_thresh,
-                                                        **kw)
-        rows[:, 0] = ok
-        rows[:, 1] = ninl
-        rows[:, 2:11] = R.reshape(count, 9)
-        rows[:, 11:14] = t
+        rows, _ = api.pnp_ransac_batched_rows(points2D[o0:o1], points3D[o0:o1], off[begin:begin + count + 1] - o0,
+                                              np.asarray(Ks)[begin:begin + count], n_iters, reproj_thresh, **kw)
         return rows
 
     return run

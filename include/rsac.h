@@ -142,6 +142,17 @@ RSAC_EXPORT int rsac_pnp_ransac_batched(rsac_ctx *ctx, const void *pts3d, const 
                             double confidence, uint64_t seed, uint32_t flags, double *R_out, double *t_out,
                             int32_t *status_out, int32_t *n_inliers_out, uint8_t *inlier_mask_out, void *stream);
 
+/* rsac_pnp_ransac_batched with the per-problem results written as f64 rows (ok 0/1, n_inliers,
+ * R 9 row-major, t 3) into rows_out, a DEVICE buffer of n_problems x 14 doubles, by a kernel
+ * reading the winners' records where they already are: the rows of a rank's problem chunk go to
+ * the multi-GPU all-gather without passing through host arrays (rsac/parallel.py
+ * pnp_batched_rows).  Returns with the stream synchronised. */
+RSAC_EXPORT int rsac_pnp_ransac_batched_rows(rsac_ctx *ctx, const void *pts3d, const void *pts2d,
+                                             const int64_t *offsets, int32_t n_problems, const double *K,
+                                             int32_t n_iters, double reproj_thresh, double confidence, uint64_t seed,
+                                             uint32_t flags, double *rows_out, uint8_t *inlier_mask_out,
+                                             void *stream);
+
 /* cv2.findHomography(src, dst, cv2.RANSAC, thr) (main_v1.py:312):
  * src, dst N x 2.  Defaults of OpenCV: max_iters 2000, confidence 0.995. */
 RSAC_EXPORT int rsac_homography_ransac(rsac_ctx *ctx, const void *src, const void *dst, int32_t n, int32_t max_iters,

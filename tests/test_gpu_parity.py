@@ -1034,3 +1034,31 @@ def test_first_round_mode_equals_pnp_ransac(n, outl, seed, lo):
     assert (res.best, res.n_inliers, res.iters) == (info.best_hyp, info.n_inliers, info.iters)
     assert res.lo_improvements == info.lo_improvements
     assert _bits_equal(res.model[:9].reshape(3, 3), Rf) and _bits_equal(res.model[9:], tf)
+
+
+@pytest.mark.parametrize("refine,adaptive", [(False, False), (True, True)])
+def test_batched_rows_on_device_equal_flat_outputs(refine, adaptive):
+    """rsac_pnp_ransac_batched_rows (the C3 problem-shard rows, written on the device) carries
+    exactly pnp_ransac_batched_flat's (ok, n_inliers, R, t), and parallel.pnp_batched_rows hands
+    the device tensor to the all-gather (one rank here)."""
+    import torch
+    from rsac import parallel as par
+    probs = [synth.pnp_problem(n, o, seed=s) for s, (n, o) in enumerate([(500, 0.4), (64, 0.9), (2000, 0.5),
+                                                                          (6, 0.0), (1200, 0.7)])]
+    off = np.zeros(len(probs) + 1, np.int64)
+    off[1:] = np.cumsum([len(p["points3d"]) for p in probs])
+    p2 = torch.from_numpy(np.concatenate([p["points2d"] for p in probs])).cuda()
+    p3 = torch.from_numpy(np.concatenate([p["points3d"] for p in probs])).cuda()
+    Ks = np.stack([p["K"] for p in probs])
+    R, t, ok, ninl, mask = rsac.pnp_ransac_batched_flat(p2, p3, off, Ks, 700, 30.0, adaptive=adaptive, refine=refine)
+    rows, mask2 = rsac.pnp_ransac_batched_rows(p2, p3, off, Ks, 700, 30.0, adaptive=adaptive, refine=refine)
+    assert rows.is_cuda and rows.shape == (len(probs), 14)
+    h = rows.cpu().numpy()
+    np.testing.assert_array_equal(h[:, 0], ok.astype(np.float64))
+    np.testing.assert_array_equal(h[:, 1], np.where(ok, ninl, 0))
+    assert _bits_equal(h[ok, 2:11], R.reshape(-1, 9)[ok]) and _bits_equal(h[ok, 11:14], t[ok])
+    assert not h[~ok, 2:].any()
+    np.testing.assert_array_equal(mask2.cpu().numpy(), mask.cpu().numpy())
+    g = par.sharded_batched(par.pnp_batched_rows(p2, p3, off, Ks, 700, 30.0, adaptive=adaptive, refine=refine),
+                            len(probs))
+    assert _bits_equal(g.cpu().numpy(), h)
