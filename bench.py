@@ -434,6 +434,23 @@ def extra_workloads(local, args):
         fin[str(mode).lower()] = statistics.median(walls)
     out["final_solve_ms_to_best"] = dict(fin, note="pnp_ransac wall time, adaptive, C2 problem; refine=False/lm/"
                                                     "epnp (solvePnPRansac's final solve after SOLVEPNP_P3P)/epnp+lm")
+    # C1 (BASELINE.json configs[0], the reference plumbing): the reference call's own mode on its 12
+    # testpro-K points under main_v1's K -- solvePnPRansac defaults (EPnP-5, MWC subsets, LM final
+    # solve), 1000 iterations cap, thr 30; host arrays in and out, as the reference passes them
+    K1 = synth.main_v1_K()
+    walls = []
+    for i in range(8):
+        t = time.perf_counter()
+        R1, t1, m1, info1 = rsac.pnp_ransac(synth.TESTPRO_K_PIXELS, synth.TESTPRO_K_POS3D, K1, 1000, 30.0,
+                                            sampler="opencv", minimal="epnp5", refine=True, return_info=True,
+                                            device=local)
+        if i >= 1:
+            walls.append(time.perf_counter() - t)
+    out["c1_reference_mode"] = {"points": 12, "ms": statistics.median(walls) * 1e3, "iters": info1.iters,
+                                "n_inliers": info1.n_inliers, "inliers": [int(k) for k in np.flatnonzero(m1)],
+                                "note": "rsac.pnp_ransac with host arrays, sampler=opencv, minimal=epnp5, LM final "
+                                        "solve (cv2.solvePnPRansac defaults), median of 7; CPU legs in "
+                                        "cpu_baseline.c1"}
     return out
 
 
@@ -496,56 +513,87 @@ def cpu_baseline_dem(args, n_rays=3):
             "sample": f"{n_rays} rays of the dem_ray_march scene, literal Python loop, {dt:.1f} s"}
 
 
+def _cpu_quota():
+    """The CPU share of this process: (affinity CPUs, cgroup quota in CPUs or None)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
+def _median_rate(fn, units, samples=5):
+    """median over `samples` runs of units / seconds of fn() -> (rate, median seconds)"""
+    walls = []
+    for _ in range(samples):
+        t = time.perf_counter()
+        fn()
+        walls.append(time.perf_counter() - t)
+    w = statistics.median(walls)
+    return units / w, w
+
+
 def cpu_baseline(pr, args):
-    """The CPU restatement (oracle/, C, gcc -O2) on bounded samples of the same workloads, on this
-    host: C2 on 1 thread (`value`) and on `threads` OpenMP threads, C2 ms-to-best (OpenCV's
-    sequential loop, stopping at the iteration bound), C3 (problems over the threads), C4 and C5."""
+    """The CPU restatement (oracle/, C, gcc -O3) on bounded samples of the same workloads, on this
+    host, each leg the median of 5 (C1: 7) samples: C2 on 1 thread (`value`), on the
+    OMP_NUM_THREADS share and on every CPU of the affinity mask, C2 ms-to-best (OpenCV's
+    sequential loop, stopping at the iteration bound), C1 (BASELINE.json configs[0]: the reference
+    plumbing, C restatement and the NumPy path), C3 (problems over the threads), C4 and C5 (LO,
+    sequential)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
+        import np_ransac as NR
         import pyoracle as O
     except Exception as e:  # oracle not built
         return {"value": None, "error": str(e)}
     from concurrent.futures import ThreadPoolExecutor
-    threads = args.cpu_threads or os.cpu_count() or 1
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    threads = args.cpu_threads or env_threads or os.cpu_count() or 1
+    aff, quota = _cpu_quota()
     soa = O.soa_pnp(pr["points3d"], pr["points2d"])
     cam = O.cam_from_K(pr["K"])
-    n = args.cpu_hyps
+    n = max(1000, args.cpu_hyps // 5)
     O.pnp_hypotheses(soa, cam, args.thr, 0x5EED, 50)  # warm
-    t = time.perf_counter()
-    O.pnp_hypotheses(soa, cam, args.thr, 0x5EED, n)
-    dt = time.perf_counter() - t
-    n_mt = n * max(1, min(threads, 16))
-    t = time.perf_counter()
-    O.pnp_hypotheses_mt(soa, cam, args.thr, 0x5EED, n_mt, threads=threads)
-    dt_mt = time.perf_counter() - t
-    walls = []
-    for _ in range(5):
-        t = time.perf_counter()
-        O.pnp_ransac_seq(pr["points3d"], pr["points2d"], pr["K"], args.thr, 0.99, 5000)
-        walls.append(time.perf_counter() - t)
-    c2_best_ms = statistics.median(walls) * 1e3
-    # C3: 128 of the 1024 problems (seeds 1..128), 1024 hypotheses each, problems over the threads
-    probs = [synth.pnp_problem(2000, 0.5, seed=s) for s in range(1, 129)]
+    rate1, w1 = _median_rate(lambda: O.pnp_hypotheses(soa, cam, args.thr, 0x5EED, n), n)
+    n_mt = 2000 * threads
+    rate_mt, w_mt = _median_rate(lambda: O.pnp_hypotheses_mt(soa, cam, args.thr, 0x5EED, n_mt, threads=threads), n_mt)
+    n_all = 500 * aff
+    rate_all, w_all = _median_rate(lambda: O.pnp_hypotheses_mt(soa, cam, args.thr, 0x5EED, n_all, threads=aff), n_all)
+    _, w_best = _median_rate(lambda: O.pnp_ransac_seq(pr["points3d"], pr["points2d"], pr["K"], args.thr, 0.99, 5000), 1)
+    # C1 (BASELINE.json configs[0]): the 12 testpro-K points (testpro-K.py:198-225) under main_v1's K
+    # (main_v1.py:870-883), 1000 iterations, thr 30, the reference call's own mode (no flags:
+    # EPnP on 5-point MWC samples, testpro-K.py:72 / main_v1.py:497)
+    P3, P2, K1 = synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, synth.main_v1_K()
+    c1 = O.pnp_ransac_seq(P3, P2, K1, 30.0, 0.99, 1000, sampler="opencv", minimal="epnp5")
+    _, w_c1 = _median_rate(lambda: O.pnp_ransac_seq(P3, P2, K1, 30.0, 0.99, 1000, sampler="opencv",
+                                                    minimal="epnp5"), 1, samples=7)
+    c1n = NR.pnp_ransac(P3, P2, K1, 30.0, 0.99, 1000, "epnp5")
+    _, w_c1n = _median_rate(lambda: NR.pnp_ransac(P3, P2, K1, 30.0, 0.99, 1000, "epnp5"), 1, samples=7)
+    # C3: 32 of the 1024 problems (seeds 1..32), 1024 hypotheses each, problems over the threads
+    probs = [synth.pnp_problem(2000, 0.5, seed=s) for s in range(1, 33)]
+    soas = [(O.soa_pnp(p["points3d"], p["points2d"]), O.cam_from_K(p["K"])) for p in probs]
 
-    def c3_one(p):
-        s3 = O.soa_pnp(p["points3d"], p["points2d"])
-        return O.pnp_hypotheses(s3, O.cam_from_K(p["K"]), args.thr, 0x5EED, 1024)
+    def c3_run():
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            list(ex.map(lambda sc: O.pnp_hypotheses(sc[0], sc[1], args.thr, 0x5EED, 1024), soas))
 
-    t = time.perf_counter()
-    with ThreadPoolExecutor(max_workers=threads) as ex:
-        list(ex.map(c3_one, probs))
-    dt_c3 = time.perf_counter() - t
-    # C4: 1500 fundamental-matrix hypotheses over the 50k matches, 1 thread
+    rate_c3, w_c3 = _median_rate(c3_run, 32 * 1024)
+    # C4: 300 fundamental-matrix hypotheses over the 50k matches, 1 thread
     p4 = synth.fundamental_problem(50_000, 0.8, seed=2)
     s4 = O.soa_hom(p4["pts1"], p4["pts2"])
-    t = time.perf_counter()
-    O.fm_hypotheses(s4, 1.5, 0x5EED, 1500)
-    dt_c4 = time.perf_counter() - t
-    # C5: LO-RANSAC to the best model on the 100k-point problem, 1 thread
+    rate_c4, w_c4 = _median_rate(lambda: O.fm_hypotheses(s4, 1.5, 0x5EED, 300), 300)
+    # C5: LO-RANSAC to the best model on the 100k-point problem, 1 thread, OpenCV's loop shape
     p5 = synth.pnp_problem(100_000, 0.5, seed=3)
-    t = time.perf_counter()
-    r5 = O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000)
-    dt_c5 = time.perf_counter() - t
+    r5 = O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000, lazy=True)
+    _, w_c5 = _median_rate(lambda: O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000,
+                                                   lazy=True), 1)
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -554,22 +602,37 @@ def cpu_baseline(pr, args):
                 break
     except OSError:
         pass
-    return {"value": n / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
-            "sample": f"{n} hypotheses of the same C2 problem (10k points), oracle/rsac_oracle.c -O2, 1 thread, "
-                      f"{dt:.1f} s",
-            "cpu_model": model, "os_cpu_count": os.cpu_count(), "threads": threads,
-            "c2_mt": {"value": n_mt / dt_mt, "unit": "hypotheses/s", "cores": threads,
-                      "sample": f"{n_mt} hypotheses, OpenMP over {threads} threads, {dt_mt:.1f} s"},
-            "c2_ms_to_best": {"ms": c2_best_ms, "cores": 1,
+    share = f"cgroup quota {quota:g} CPUs" if quota else "no cgroup quota"
+    return {"value": rate1, "unit": "hypotheses/s", "cores": 1, "kind": "port",
+            "sample": f"{n} hypotheses of the same C2 problem (10k points), oracle/rsac_oracle.c -O3, 1 thread, "
+                      f"median of 5 ({w1:.2f} s each)",
+            "cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+            "omp_num_threads_env": env_threads, "threads": threads,
+            "c2_mt": {"value": rate_mt, "unit": "hypotheses/s", "cores": threads,
+                      "sample": f"{n_mt} hypotheses, OpenMP over {threads} threads (OMP_NUM_THREADS share), "
+                                f"median of 5 ({w_mt:.2f} s each)"},
+            "c2_all_cpus": {"value": rate_all, "unit": "hypotheses/s", "cores": aff,
+                            "sample": f"{n_all} hypotheses, OpenMP over all {aff} CPUs of the affinity mask "
+                                      f"({share}), median of 5 ({w_all:.2f} s each)"},
+            "c2_ms_to_best": {"ms": w_best * 1e3, "cores": 1,
                               "sample": "OpenCV's sequential loop (orc_pnp_ransac_seq), stops at the iteration "
                                         "bound, no refit, median of 5"},
-            "c3": {"hyp_s": 128 * 1024 / dt_c3, "cores": threads,
-                   "sample": f"128 of the 1024 problems x 1024 hypotheses, problems over {threads} threads, "
-                             f"{dt_c3:.1f} s"},
-            "c4": {"hyp_s": 1500 / dt_c4, "cores": 1, "sample": f"1500 hypotheses, 50k matches, {dt_c4:.1f} s"},
-            "c5": {"ms_to_best": dt_c5 * 1e3, "iters": r5["iters"], "lo_improvements": r5["lo_improvements"],
-                   "cores": 1, "sample": "orc_pnp_ransac_lo on the 100k-point problem (all 5000 hypotheses scored, "
-                                         "then the scan with LO)"}}
+            "c1": {"ms_c": w_c1 * 1e3, "ms_numpy": w_c1n * 1e3, "cores": 1, "iters": c1["iters"],
+                   "best": c1["best"], "n_inliers": c1["n_inliers"],
+                   "inliers": [int(i) for i in np.flatnonzero(c1["mask"])],
+                   "numpy_equal": bool(c1n["best"] == c1["best"] and np.array_equal(c1n["mask"], c1["mask"])),
+                   "sample": "BASELINE configs[0]: 12 testpro-K points, main_v1 K, 1000 iterations cap, thr 30, "
+                             "EPnP-5 on OpenCV's MWC subsets, sequential loop to the bound; C restatement "
+                             "(orc_pnp_ransac_seq_k) and the NumPy path (oracle/np_ransac.py), ms per solve, "
+                             "median of 7"},
+            "c3": {"hyp_s": rate_c3, "cores": threads,
+                   "sample": f"32 of the 1024 problems x 1024 hypotheses, problems over {threads} threads, "
+                             f"median of 5 ({w_c3:.2f} s each)"},
+            "c4": {"hyp_s": rate_c4, "cores": 1, "sample": f"300 hypotheses, 50k matches, median of 5 ({w_c4:.2f} s each)"},
+            "c5": {"ms_to_best": w_c5 * 1e3, "iters": r5["iters"], "lo_improvements": r5["lo_improvements"],
+                   "cores": 1, "sample": "orc_pnp_ransac_lo_seq on the 100k-point problem (each hypothesis "
+                                         "evaluated when the scan reaches it, LO at every new best, stops at the "
+                                         "bound), median of 5"}}
 
 
 if __name__ == "__main__":

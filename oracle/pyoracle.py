@@ -116,6 +116,10 @@ def lib():
                                      C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
                                      C.POINTER(C.c_int64)]
     L.orc_pnp_ransac_seq.restype = C.c_int64
+    L.orc_pnp_ransac_seq_k.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
+                                       C.c_int, C.c_uint64, C.c_int, C.c_int, _f64p, _f64p, _u8p,
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
+    L.orc_pnp_ransac_seq_k.restype = C.c_int64
     L.orc_pnp_hypotheses_mt.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_float, C.c_uint64,
                                         C.c_int64, C.c_int64, _i32p, _i8p, C.c_int]
     L.orc_pnp_hypotheses_mt.restype = None
@@ -123,6 +127,10 @@ def lib():
                                     C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
                                     C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
     L.orc_pnp_ransac_lo.restype = C.c_int64
+    L.orc_pnp_ransac_lo_seq.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
+                                    C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
+                                    C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
+    L.orc_pnp_ransac_lo_seq.restype = C.c_int64
     L.orc_pnp_local_opt.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_float, _f64p, _f64p,
                                     C.c_int32, C.POINTER(C.c_int32)]
     L.orc_pnp_local_opt.restype = C.c_int32
@@ -283,16 +291,20 @@ def pnp_minimal_epnp5(soa, cam, idx):
     return (R.reshape(3, 3), t) if ok else None
 
 
-def pnp_ransac_seq(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED):
-    """OpenCV's loop one hypothesis at a time, stopping at the iteration bound (orc_pnp_ransac_seq)."""
+def pnp_ransac_seq(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED,
+                   sampler="philox", minimal="p3p"):
+    """OpenCV's loop one hypothesis at a time, stopping at the iteration bound (orc_pnp_ransac_seq_k;
+    sampler "opencv" draws each iteration's MWC subset as OpenCV does, minimal "epnp5" = the default
+    SOLVEPNP_ITERATIVE kernel)."""
     soa = soa_pnp(points3d, points2d)
     n = len(soa[0])
     R, t = np.zeros(9), np.zeros(3)
     mask = np.zeros(n, np.uint8)
     good = C.c_int32(0)
     iters = C.c_int64(0)
-    best = lib().orc_pnp_ransac_seq(*soa, n, cam_from_K(K), thr, confidence, max_iters, seed, R, t, mask,
-                                    C.byref(good), C.byref(iters))
+    best = lib().orc_pnp_ransac_seq_k(*soa, n, cam_from_K(K), thr, confidence, max_iters, seed,
+                                      1 if sampler == "opencv" else 0, 5 if minimal == "epnp5" else 4, R, t, mask,
+                                      C.byref(good), C.byref(iters))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value))
 
@@ -305,8 +317,10 @@ def pnp_hypotheses_mt(soa, cam, thr, seed, H, hyp0=0, threads=1):
     return counts, status
 
 
-def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED):
-    """LO-RANSAC restatement (orc_pnp_ransac_lo): local optimisation at every new best."""
+def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED, lazy=False):
+    """LO-RANSAC restatement (orc_pnp_ransac_lo): local optimisation at every new best.  lazy=True
+    evaluates each hypothesis when the scan reaches it and stops at the bound (orc_pnp_ransac_lo_seq:
+    OpenCV's loop shape, the C5 CPU leg); the results are the same."""
     soa = soa_pnp(points3d, points2d)
     n = len(soa[0])
     cam = cam_from_K(K)
@@ -316,8 +330,8 @@ def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=50
     good = C.c_int32(0)
     iters = C.c_int64(0)
     nlo = C.c_int32(0)
-    best = lib().orc_pnp_ransac_lo(*soa, n, cam, thr, confidence, max_iters, seed, R, t, mask, C.byref(good),
-                                   C.byref(iters), C.byref(nlo))
+    fn = lib().orc_pnp_ransac_lo_seq if lazy else lib().orc_pnp_ransac_lo
+    best = fn(*soa, n, cam, thr, confidence, max_iters, seed, R, t, mask, C.byref(good), C.byref(iters), C.byref(nlo))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value), lo_improvements=int(nlo.value))
 

@@ -1530,26 +1530,35 @@ ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, c
  * bound (RANSACUpdateNumIters after each new best) is reached, so it scores only `iters`
  * hypotheses -- the CPU ms-to-best-model baseline (bench.py cpu_baseline).  Philox sampler.
  * Same results as orc_pnp_ransac (tests/test_oracle_golden.py). */
-ORC_API int64_t orc_pnp_ransac_seq(const float *X, const float *Y, const float *Z, const float *U, const float *V,
-                                   int n, const double cam[4], double thr, double confidence, int max_iters,
-                                   uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
-                                   int64_t *iters_used) {
+/* k: sample size / minimal solver (4 P3P, 5 EPnP-5, also model_points); sampler 0 Philox, 1 the
+ * MWC getSubset sequence drawn one subset per iteration, as OpenCV draws it (the C1 CPU leg:
+ * main_v1.py:497 / testpro-K.py:72 run EPnP-5 on MWC samples) */
+ORC_API int64_t orc_pnp_ransac_seq_k(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                     int n, const double cam[4], double thr, double confidence, int max_iters,
+                                     uint64_t seed, int sampler, int k, double R[9], double t[3], uint8_t *mask,
+                                     int32_t *n_inliers, int64_t *iters_used) {
     const float thr2 = orc_thr2(thr);
     int64_t niters = max_iters > 1 ? max_iters : 1, best = -1, h = 0;
     int32_t good = 0;
     double bm[16] = {0};
+    uint64_t mwc = ~(uint64_t)0;
     for (; h < niters; ++h) {
-        int32_t c;
-        int8_t st;
+        int32_t c, sub[5];
+        int8_t st, sst = 1;
         double m[16];
-        orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, h, 1, NULL, NULL, &c, &st, m);
+        if (sampler == 1) {
+            orc_mwc_subsets(&mwc, n, k, 1, NULL, NULL, NULL, NULL, sub, &sst);
+            orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, 0, h, 1, k, sub, &sst, &c, &st, m);
+        } else {
+            orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, 0, h, 1, k, NULL, NULL, &c, &st, m);
+        }
         if (st < 0) break;
         if (st == 0) continue;
-        if (c > (good > 3 ? good : 3)) {
+        if (c > (good > k - 1 ? good : k - 1)) {
             best = h;
             good = c;
             memcpy(bm, m, sizeof bm);
-            niters = orc_update_num_iters(confidence, (double)(n - c) / n, 4, (int)niters);
+            niters = orc_update_num_iters(confidence, (double)(n - c) / n, k, (int)niters);
         }
     }
     if (iters_used) *iters_used = h;
@@ -1562,6 +1571,14 @@ ORC_API int64_t orc_pnp_ransac_seq(const float *X, const float *Y, const float *
     }
     if (n_inliers) *n_inliers = good;
     return best;
+}
+
+ORC_API int64_t orc_pnp_ransac_seq(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                   int n, const double cam[4], double thr, double confidence, int max_iters,
+                                   uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
+                                   int64_t *iters_used) {
+    return orc_pnp_ransac_seq_k(X, Y, Z, U, V, n, cam, thr, confidence, max_iters, seed, 0, 4, R, t, mask, n_inliers,
+                                iters_used);
 }
 
 /* orc_pnp_hypotheses over `threads` host threads (OpenMP, hypotheses dealt in chunks of 64):
@@ -1612,30 +1629,36 @@ ORC_API int32_t orc_pnp_local_opt(const float *X, const float *Y, const float *Z
     return c;
 }
 
-ORC_API int64_t orc_pnp_ransac_lo(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+/* lazy = 1: each hypothesis is drawn, solved and counted when the scan reaches it, so the loop
+ * stops at the iteration bound as OpenCV's does (the C5 CPU leg); lazy = 0: all max_iters are
+ * evaluated first (the form the GPU's rounds are checked against).  Same results either way. */
+static int64_t pnp_ransac_lo_impl(const float *X, const float *Y, const float *Z, const float *U, const float *V,
                                   int n, const double cam[4], double thr, double confidence, int max_iters,
                                   uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
-                                  int64_t *iters_used, int32_t *lo_improvements) {
+                                  int64_t *iters_used, int32_t *lo_improvements, int lazy) {
     int64_t H = max_iters > 1 ? max_iters : 1;
-    int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * H);
-    int8_t *status = (int8_t *)malloc(H);
-    double *models = (double *)malloc(sizeof(double) * 16 * H);
+    const int64_t Hm = lazy ? 1 : H;
+    int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * Hm);
+    int8_t *status = (int8_t *)malloc(Hm);
+    double *models = (double *)malloc(sizeof(double) * 16 * Hm);
     float thr2 = orc_thr2(thr);
-    orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, 0, H, NULL, NULL, counts, status, models);
+    if (!lazy) orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, 0, H, NULL, NULL, counts, status, models);
     int64_t niters = H, best = -1, i;
     int32_t max_good = 0, nlo = 0;
     double BR[9] = {0}, Bt[3] = {0};
     for (i = 0; i < H && i < niters; ++i) {
-        if (status[i] < 0) break;
-        if (status[i] == 0) continue;
-        int32_t c = counts[i];
+        const int64_t j = lazy ? 0 : i;
+        if (lazy) orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, i, 1, NULL, NULL, counts, status, models);
+        if (status[j] < 0) break;
+        if (status[j] == 0) continue;
+        int32_t c = counts[j];
         int32_t floor_c = max_good > 3 ? max_good : 3;
         if (c <= floor_c) continue;
         best = i; max_good = c;
         niters = orc_update_num_iters(confidence, (double)(n - c) / n, 4, (int)niters);
         double MR[9], Mt[3];
-        memcpy(MR, models + 16 * i, sizeof MR);
-        memcpy(Mt, models + 16 * i + 9, sizeof Mt);
+        memcpy(MR, models + 16 * j, sizeof MR);
+        memcpy(Mt, models + 16 * j + 9, sizeof Mt);
         int32_t steps = 0;
         c = orc_pnp_local_opt(X, Y, Z, U, V, n, cam, thr2, MR, Mt, c, &steps);
         nlo += steps;
@@ -1658,6 +1681,22 @@ ORC_API int64_t orc_pnp_ransac_lo(const float *X, const float *Y, const float *Z
     if (lo_improvements) *lo_improvements = nlo;
     free(counts); free(status); free(models);
     return best;
+}
+
+ORC_API int64_t orc_pnp_ransac_lo(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                  int n, const double cam[4], double thr, double confidence, int max_iters,
+                                  uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
+                                  int64_t *iters_used, int32_t *lo_improvements) {
+    return pnp_ransac_lo_impl(X, Y, Z, U, V, n, cam, thr, confidence, max_iters, seed, R, t, mask, n_inliers,
+                              iters_used, lo_improvements, 0);
+}
+
+ORC_API int64_t orc_pnp_ransac_lo_seq(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                      int n, const double cam[4], double thr, double confidence, int max_iters,
+                                      uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
+                                      int64_t *iters_used, int32_t *lo_improvements) {
+    return pnp_ransac_lo_impl(X, Y, Z, U, V, n, cam, thr, confidence, max_iters, seed, R, t, mask, n_inliers,
+                              iters_used, lo_improvements, 1);
 }
 
 ORC_API int64_t orc_hom_ransac(const float *sx, const float *sy, const float *dx, const float *dy, int n, double thr,
@@ -1710,6 +1749,34 @@ typedef void (*ep_fn)(const void *prm, double X, double Y, double Z, double u, d
 
 static void ep_reduce(epctx *c, int nv, ep_fn f, const void *prm, double *out) {
     double *part = c->part;
+    if (c->n <= 64) {
+        /* every point in its own slot of wave 0, the other slots +0: the same tree restricted to the
+         * first m = 2^k >= n lanes.  Levels o >= m add a lane whose coset holds only empty slots
+         * (+0.0, which also turns a -0.0 sum into +0.0, as the full tree does), and so does the sum
+         * over the 7 empty waves.  Bit-identical to the loop below, without its 512 x nv slots
+         * (the EPnP-5 minimal solver reduces 5 points per hypothesis). */
+        int m = 1;
+        while (m < c->n) m <<= 1;
+        for (int q = 0; q < m * nv; ++q) part[q] = 0.0;
+        for (int i = 0; i < c->n; ++i)
+            if (c->mask[i])
+                f(prm, (double)c->X[i] - c->c[0], (double)c->Y[i] - c->c[1], (double)c->Z[i] - c->c[2],
+                  (double)c->U[i], (double)c->V[i], part + i * nv);
+        double v[64], w[64];
+        for (int q = 0; q < nv; ++q) {
+            for (int l = 0; l < m; ++l) v[l] = part[l * nv + q];
+            for (int o = 32; o > 0; o >>= 1) {
+                if (o >= m) {
+                    for (int l = 0; l < m; ++l) v[l] = v[l] + 0.0;
+                    continue;
+                }
+                for (int l = 0; l < m; ++l) w[l] = v[l] + v[l ^ o];
+                for (int l = 0; l < m; ++l) v[l] = w[l];
+            }
+            out[q] = LM_THREADS / 64 > 1 ? v[0] + 0.0 : v[0];
+        }
+        return;
+    }
     for (int q = 0; q < LM_THREADS * nv; ++q) part[q] = 0.0;
     for (int tid = 0; tid < LM_THREADS; ++tid)
         for (int i = tid; i < c->n; i += LM_THREADS)
@@ -1930,7 +1997,7 @@ ORC_API int orc_pnp_epnp(const float *X, const float *Y, const float *Z, const f
                          const uint8_t *mask, int n, const double cam[4], double R_out[9], double t_out[3]) {
     if (n <= 0) return 0;
     epctx c = {X, Y, Z, U, V, mask, n, {cam[0], cam[1], cam[2], cam[3]}, {X[0], Y[0], Z[0]}, NULL};
-    c.part = (double *)malloc(sizeof(double) * LM_THREADS * EP_MAXV);
+    c.part = (double *)malloc(sizeof(double) * (n <= 64 ? 64 : LM_THREADS) * EP_MAXV);
     int ok = 0;
     double s4[4], cw[4][3], cov[6];
     ep_reduce(&c, 4, ep_f_mean, NULL, s4);

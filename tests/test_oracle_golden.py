@@ -221,3 +221,27 @@ def test_sequential_and_parallel_cpu_loops_equal_the_restatement(n, outl, seed):
     c2, s2 = O.pnp_hypotheses_mt(soa, cam, 30.0, 0x5EED, 2000, hyp0=5, threads=4)
     np.testing.assert_array_equal(c1, c2)
     np.testing.assert_array_equal(s1, s2)
+
+
+@pytest.mark.parametrize("minimal", ["epnp5", "p3p"])
+@pytest.mark.parametrize("case", ["c1", "synthetic"])
+def test_numpy_path_equals_sequential_c_loop(minimal, case):
+    """The "CPU NumPy path" of BASELINE.json configs[0] (oracle/np_ransac.py: OpenCV's sequential
+    loop with NumPy computeError) equals the C restatement's sequential loop (orc_pnp_ransac_seq_k:
+    MWC subsets drawn per iteration) and its all-hypotheses form (orc_pnp_ransac_k) on best,
+    inlier count, iterations, mask and pose.  C1: the 12 testpro-K points under main_v1's K
+    (main_v1.py:870-883), 1000 iterations, thr 30."""
+    import np_ransac as NR
+    if case == "c1":
+        P3, P2, K = synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, synth.main_v1_K()
+    else:
+        pr = synth.pnp_problem(1500, 0.6, seed=17)
+        P3, P2, K = pr["points3d"], pr["points2d"], pr["K"]
+    r = NR.pnp_ransac(P3, P2, K, 30.0, 0.99, 1000, minimal)
+    seq = O.pnp_ransac_seq(P3, P2, K, 30.0, 0.99, 1000, sampler="opencv", minimal=minimal)
+    full = O.pnp_ransac(P3, P2, K, 30.0, 0.99, 1000, sampler="opencv", minimal=minimal)
+    for ref in (seq, full):
+        assert (r["best"], r["n_inliers"], r["iters"]) == (ref["best"], ref["n_inliers"], ref["iters"])
+        np.testing.assert_array_equal(r["mask"], ref["mask"])
+        np.testing.assert_array_equal(r["R"], ref["R"])
+        np.testing.assert_array_equal(r["t"], ref["t"])
