@@ -284,6 +284,8 @@ def main():
             "best_inliers": int(cnt),
             "kernels_ms": {"pnp_solve": solve_avg, "pnp_score": score_avg},
             "roofline": roofline,
+            "roofline_solve": sec_roofline("c2", "k_pnp_solve", solve_avg,
+                                           "HIP events around the solve launch, mean of 10 synchronous launches"),
             "roofline_mfma": {"bound": "mfma", "flop_per_pair": MFMA_FLOP_PER_PAIR,
                               "achieved": pairs * MFMA_FLOP_PER_PAIR / t_s / 1e12,
                               "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -346,6 +348,33 @@ def multi_gpu_legs(local, args, pr2):
     return out
 
 
+def sec_roofline(cfg, kernel, kernel_ms, span):
+    """Roofline object of a secondary config's dominant kernel: VALU wave-instructions and HBM bytes
+    per launch from profiles/pmc_secondary.json (scripts/gpu_secondary_profile.sh +
+    scripts/summarize_secondary.py: its own --pmc passes of the same workload), divided by the
+    launch's duration measured here (kernel_ms; `span` says how).  kernel_ms None: the kernel
+    trace's mean duration from the same JSON."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_secondary.json")))
+        e = d["configs"][cfg]["kernels"][kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    src = "profile"
+    if not kernel_ms:
+        kernel_ms, src = e["mean_us"] / 1e3, "kernel trace mean (profiles/pmc_secondary.json)"
+    t_s = kernel_ms * 1e-3
+    r = {"bound": "valu_issue", "kernel": kernel, "kernel_ms": kernel_ms, "span": span if src == "profile" else src,
+         "peak": VALU_ISSUE_PEAK / 1e9, "unit": "G VALU wave-instructions/s", "profile": d.get("tag")}
+    v = e.get("valu_instr_per_launch")
+    if v:
+        r.update({"valu_instr_per_launch": v, "achieved": v / t_s / 1e9, "frac": v / t_s / VALU_ISSUE_PEAK})
+    h = e.get("hbm")
+    if h:
+        r.update({"traffic": h["traffic_bytes"], "hbm_gbs": h["traffic_bytes"] / t_s / 1e9,
+                  "hbm_frac": h["traffic_bytes"] / t_s / 1e9 / HBM_PEAK_GBS, "write_bytes": e["write_kib"] * 1024})
+    return r
+
+
 def extra_workloads(local, args):
     """Secondary lines (not `value`): C3 of BASELINE.json (1024 problems x 2000 points, 1024
     hypotheses each, one batched call) and the 458-location search of main_v1.py:274/862."""
@@ -368,8 +397,20 @@ def extra_workloads(local, args):
 
     w = c3(p2, p3)
     wh = c3(p2.cpu().numpy(), p3.cpu().numpy())
+    # the scoring kernel's span of one call (HIP events around its launch, rsac_set_timing)
+    ctx = rsac.context(local)
+    ctx.set_timing(True)
+    rsac.pnp_ransac_batched_flat(p2, p3, off, Ks, 1024, args.thr, adaptive=False, refine=False)
+    torch.cuda.synchronize()
+    st3 = ctx.last_stats()
+    ctx.set_timing(False)
     out["c3_batched"] = {"problems": 1024, "points": 2000, "hyps_per_problem": 1024, "ms": w * 1e3,
                          "hyp_s": 1024 * 1024 / w, "host_inputs_ms": wh * 1e3, "host_inputs_hyp_s": 1024 * 1024 / wh,
+                         "score_ms": st3["score_ms"], "solve_ms": st3["solve_ms"],
+                         "roofline": sec_roofline("c3", "k_pnp_score_mf<2>", st3["score_ms"],
+                                                  "HIP events around the scoring launch of one call"),
+                         "roofline_solve": sec_roofline("c3", "k_pnp_solve", st3["solve_ms"],
+                                                        "HIP events around the solve launch of one call"),
                          "note": "inputs resident in HBM (and, second figure, handed over as host f64 arrays); "
                                  "per-problem winners + RANSAC masks, adaptive off, no refit"}
     # C5 (BASELINE.json configs[4]): LO-RANSAC, 100k correspondences, adaptive, inputs in HBM
@@ -387,7 +428,9 @@ def extra_workloads(local, args):
             walls.append(time.perf_counter() - t)
     out["c5_lo_ransac"] = {"points": 100_000, "outlier_ratio": 0.5, "ms_to_best": statistics.median(walls) * 1e3,
                            "iters": info.iters, "n_inliers": info.n_inliers, "lo_improvements": info.lo_improvements,
-                           "note": "1 GPU; the multi-GPU form is rsac.parallel.sharded_ransac(lo=True)"}
+                           "roofline_lo_chain": sec_roofline("c5", "k_pnp_refine", None, ""),
+                           "note": "1 GPU; the multi-GPU form is rsac.parallel.sharded_ransac(lo=True); the LO "
+                                   "chain's refits (k_pnp_refine) are latency-bound, see roofline_lo_chain"}
     # C4 (BASELINE.json configs[3]): fundamental matrix, 50k matches, 80 % outliers, 100k hypotheses
     p4 = synth.fundamental_problem(50_000, 0.8, seed=2)
     f1 = torch.from_numpy(p4["pts1"]).to(dev)
@@ -405,6 +448,10 @@ def extra_workloads(local, args):
     out["c4_fundamental"] = {"matches": 50_000, "outlier_ratio": 0.8, "hyps": 100_000, "ms": w4 * 1e3,
                              "hyp_s": 100_000 / w4, "n_inliers": info4.n_inliers, "score_ms": info4.score_ms,
                              "solve_ms": info4.solve_ms,
+                             "roofline": sec_roofline("c4", "k_fm_score_q<8>", info4.score_ms,
+                                                      "HIP events around the scoring launch (rsac_stats score_ms)"),
+                             "roofline_solve": sec_roofline("c4", "k_fm_solve", info4.solve_ms,
+                                                            "HIP events around the solve launch (rsac_stats solve_ms)"),
                              "note": "8-point + Sampson (f64), inputs in HBM, fixed budget (adaptive off)"}
     lp = synth.location_problem(seed=0)
     walls = []

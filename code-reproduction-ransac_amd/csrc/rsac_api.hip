@@ -112,6 +112,10 @@ struct rsac_ctx {
     // buffer (calls may return before their copies ran, RSAC_F_ASYNC)
     hipEvent_t ev_pts = nullptr, ev_small = nullptr;
     int64_t round_size = 4096;
+    // rsac_set_timing: every PnP call records HIP events around its solve and score launches and
+    // leaves its statistics in last_stats (rsac_last_stats)
+    bool timing = false;
+    rsac_stats last_stats{};
     // device scratch
     DevBuf pts, tables, models, status, counts, subsets, substatus, best, bestmodels, mask;
     int64_t *d_off = nullptr;  // views into `tables`: offsets (P+1), cams (P x 4), thr2 (P)
@@ -922,7 +926,7 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         dec.offsets = spec_fixed ? c->d_off : nullptr;
     }
     LoopOut lo;
-    lo.timing = stats != nullptr;
+    lo.timing = stats != nullptr || c->timing;
     // first-round mode (rsac_pnp_ransac_first_round): the loop stops after its first round when
     // that round did not end the scan; the caller continues from the exported scan state
     auto more = [&]() -> int {
@@ -1001,6 +1005,19 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     if (first_round) {  // the call ran to the end: the caller has rsac_pnp_ransac's result
         const ScanState &sc = lo.scan[0];
         *first_round = rsac_scan_state{sc.niters, sc.best, sc.iter, sc.max_good, 1};
+    }
+    if (c->timing) {
+        rsac_stats &ls = c->last_stats;
+        ls = rsac_stats{};
+        ls.best_hyp = lo.scan[0].best;
+        ls.iters = lo.scan[0].iter;
+        ls.hyps_scored = lo.scored;
+        ls.n_inliers = lo.scan[0].max_good;
+        ls.rounds = lo.rounds;
+        ls.gpu_ms = lo.gpu_ms;
+        ls.solve_ms = lo.solve_ms;
+        ls.score_ms = lo.score_ms;
+        ls.lo_improvements = lo.lo_improvements;
     }
     if (stats) {
         stats->best_hyp = lo.scan[0].best;
@@ -1190,6 +1207,18 @@ int rsac_refit_blocks(rsac_ctx *c, int32_t n, int32_t *ranges, int32_t *blocks) 
     const int nb = lm_blocks(n);
     if (ranges) *ranges = nb;
     if (blocks) *blocks = nb > 1 ? std::min(nb, lm->max_blocks) : 1;
+    return RSAC_OK;
+}
+
+int rsac_set_timing(rsac_ctx *c, int32_t on) {
+    if (!c) return fail(RSAC_EINVAL, "null context");
+    c->timing = on != 0;
+    return RSAC_OK;
+}
+
+int rsac_last_stats(rsac_ctx *c, rsac_stats *out) {
+    if (!c || !out) return fail(RSAC_EINVAL, "bad arguments");
+    *out = c->last_stats;
     return RSAC_OK;
 }
 

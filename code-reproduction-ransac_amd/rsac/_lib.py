@@ -65,6 +65,8 @@ SIGNATURES = [
     ("rsac_last_error", C.c_char_p, []),
     ("rsac_abi_version", C.c_int, []),
     ("rsac_device_count", C.c_int, []),
+    ("rsac_set_timing", C.c_int, [_vp, _i32]),
+    ("rsac_last_stats", C.c_int, [_vp, C.POINTER(Stats)]),
     ("rsac_set_round_size", C.c_int, [_vp, _i64]),
     ("rsac_refit_blocks", C.c_int, [_vp, _i32, C.POINTER(_i32), C.POINTER(_i32)]),
     ("rsac_debug_set", C.c_int, [_vp, _i32, _i64]),
@@ -189,6 +191,16 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def set_timing(self, on: bool = True):
+        """HIP events around every PnP call's solve and scoring launches (rsac_set_timing)"""
+        check(lib().rsac_set_timing(self._h, 1 if on else 0))
+
+    def last_stats(self) -> dict:
+        """rsac_stats of the last PnP call on this context (with set_timing on)"""
+        st = Stats()
+        check(lib().rsac_last_stats(self._h, C.byref(st)))
+        return st.as_dict()
 
     def set_round_size(self, n: int):
         check(lib().rsac_set_round_size(self._h, int(n)))

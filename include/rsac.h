@@ -95,6 +95,13 @@ typedef struct rsac_stats {
     int32_t reserved;
 } rsac_stats;
 
+/* Timing of any PnP call on the context (batched ones included, which take no stats argument):
+ * with rsac_set_timing(ctx, 1) every call records HIP events around its solve and scoring
+ * launches on the call's stream, and rsac_last_stats returns the last call's rsac_stats
+ * (gpu_ms / solve_ms / score_ms summed over its rounds).  Off by default (no events). */
+RSAC_EXPORT int rsac_set_timing(rsac_ctx *ctx, int32_t on);
+RSAC_EXPORT int rsac_last_stats(rsac_ctx *ctx, rsac_stats *out);
+
 RSAC_EXPORT int rsac_create(int device, rsac_ctx **out);
 RSAC_EXPORT void rsac_destroy(rsac_ctx *ctx);
 RSAC_EXPORT const char *rsac_last_error(void);
