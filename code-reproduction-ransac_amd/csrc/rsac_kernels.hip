@@ -1431,7 +1431,10 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 #ifndef RSAC_MF_PRIO
 #define RSAC_MF_PRIO 1
 #endif
-constexpr int kMfW = 4;
+#ifndef RSAC_MF_LONG_W
+#define RSAC_MF_LONG_W 4
+#endif
+constexpr int kMfW = RSAC_MF_LONG_W;  // A/B knob (scripts/build_ab.sh): waves per block for one long problem
 constexpr int kWrec = 64;        // flagged iterations a wave lists per unit
 
 template <int W>
@@ -1597,6 +1600,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     if (wave >= 2) __builtin_amdgcn_s_setprio(1);
 #endif
     int *const uq = unit_queue(queue, qk);
+#ifdef RSAC_MF_CLOCK
+    // diagnostic build (scripts/clock_probe.sh): the in-kernel shader clock of this block's
+    // lifetime, s_memtime (shader cycles) against s_memrealtime (100 MHz)
+    const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     int last_prob = -1, n_all = 0;
     int64_t p0 = 0;
     bool in_range = false;
@@ -1653,6 +1661,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         }
         __syncthreads();  // the unit's LDS and the slot are rewritten by the next unit
     }
+#ifdef RSAC_MF_CLOCK
+    if (threadIdx.x == 0 && (blockIdx.x % 97) == 0)
+        printf("mfclock block %u cycles %llu realticks %llu\n", blockIdx.x, __builtin_amdgcn_s_memtime() - clk0,
+               __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
 }
 
 
@@ -2020,6 +2033,53 @@ __global__ __launch_bounds__(256) void k_best_key(const int32_t *__restrict__ co
     }
 }
 
+// the device replay of a problem's scan on its records (scan_records of rsac_host.hip): one wave,
+// wave-uniform; ridx / rcnt in LDS, written before the call
+__device__ __forceinline__ void scan_decide(const int32_t *ridx, const int32_t *rcnt, int nrec, int first_neg, int H,
+                                            int model_points, int prob, int64_t stride, const ScanDecide &dec,
+                                            ScanRecords &o, int lane) {
+    // scan_records (rsac_host.hip) on the records lane 0 just wrote.  update_num_iters'
+    // logarithms (the latency) for every record at once, lane r for record r; the
+    // sequential part on them is uniform across the wave.
+    __builtin_amdgcn_wave_barrier();
+    const int nr = nrec <= kScanRecs ? nrec : 0;
+    double p = dec.confidence;
+    p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
+    double num = 1. - p;
+    if (num < 2.2250738585072014e-308) num = 2.2250738585072014e-308;
+    num = log(num);
+    double ldenom = 0.;
+    int zero = 0;  // update_num_iters returns 0 (denominator below DBL_MIN)
+    const int32_t np = dec.offsets ? (int32_t)(dec.offsets[prob + 1] - dec.offsets[prob]) : dec.n;
+    if (lane < nr) {
+        double ep = (double)(np - rcnt[lane]) / np;
+        ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
+        const double denom = 1. - pow(1. - ep, model_points);
+        if (denom < 2.2250738585072014e-308) zero = 1;
+        else ldenom = log(denom);
+    }
+    int64_t niters = dec.max_iters > 1 ? dec.max_iters : 1, best = -1;
+    for (int r = 0; r < nr; ++r) {
+        const double ld = __shfl(ldenom, r);
+        const int z = __shfl(zero, r);
+        const int64_t stop = first_neg < niters ? first_neg : niters;
+        if (ridx[r] >= stop) break;
+        best = ridx[r];
+        const int mi = (int)niters;
+        niters = z ? 0 : ((ld >= 0 || -num >= mi * (-ld)) ? mi : (int)lrint(num / ld));
+    }
+    const int64_t stop = first_neg < niters ? first_neg : niters;
+    // fixed budget: the round is the whole budget, so the replay always ends in it
+    const bool done = nrec <= kScanRecs && (dec.fixed || stop < H || H >= niters);
+    if (lane == 0) {
+        // not done: the speculative finish has no model (cheap no-op); the record index of
+        // problem prob's winner (problem 0: the hypothesis itself)
+        dec.best_out[prob] = done && best >= 0 ? (int64_t)prob * stride + best : -1;
+        o.dev_best = (int32_t)best;
+        o.dev_done = done;
+    }
+}
+
 // one wave per problem: 64 hypotheses per step, the running maximum carried across steps
 __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict__ counts,
                                                       const int8_t *__restrict__ status, int64_t stride, int32_t P,
@@ -2069,47 +2129,146 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
         }
     }
     if (dec.best_out && (dec.fixed || prob == 0)) {  // wave-uniform
-        // scan_records (rsac_host.hip) on the records lane 0 just wrote.  update_num_iters'
-        // logarithms (the latency) for every record at once, lane r for record r; the
-        // sequential part on them is uniform across the wave.
         __builtin_amdgcn_wave_barrier();
-        const int nr = nrec <= kScanRecs ? nrec : 0;
-        double p = dec.confidence;
-        p = p > 0. ? p : 0.; p = p < 1. ? p : 1.;
-        double num = 1. - p;
-        if (num < 2.2250738585072014e-308) num = 2.2250738585072014e-308;
-        num = log(num);
-        double ldenom = 0.;
-        int zero = 0;  // update_num_iters returns 0 (denominator below DBL_MIN)
-        const int32_t np = dec.offsets ? (int32_t)(dec.offsets[prob + 1] - dec.offsets[prob]) : dec.n;
-        if (lane < nr) {
-            double ep = (double)(np - rcnt[lane]) / np;
-            ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
-            const double denom = 1. - pow(1. - ep, model_points);
-            if (denom < 2.2250738585072014e-308) zero = 1;
-            else ldenom = log(denom);
+        scan_decide(ridx, rcnt, nrec, first_neg, H, model_points, prob, stride, dec, o, lane);
+    }
+}
+
+// k_scan_records for long rounds (H >= kScanBlockH: a fixed budget of 100k hypotheses, C4): one
+// 1024-thread block per problem instead of one wave stepping 64 hypotheses at a time (C4: 778 us
+// for one 100k round).  Thread t owns the contiguous range [t L, t L + L): pass 1 finds its first
+// status < 0 and the maximum count before it; a block min gives first_neg and an exclusive
+// block prefix maximum (from the floor model_points - 1) the floor each range starts from; pass 2
+// lists each range's strict prefix maxima above its floor, placed by an exclusive block prefix
+// sum of the per-range counts.  The records, their order and nrec (-1 past kScanRecs) are those
+// of the one-wave scan; then wave 0 replays them (scan_decide).
+constexpr int kScanBlockH = 8192;
+__global__ __launch_bounds__(1024) void k_scan_records_blk(const int32_t *__restrict__ counts,
+                                                           const int8_t *__restrict__ status, int64_t stride,
+                                                           int32_t H, int model_points, ScanRecords *__restrict__ out,
+                                                           ScanDecide dec) {
+    __shared__ int32_t ridx[kScanRecs], rcnt[kScanRecs];
+    __shared__ int32_t wv[16], wv2[16];
+    __shared__ int32_t s_first_neg;
+    const int prob = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int32_t *c = counts + (int64_t)prob * stride;
+    const int8_t *st = status + (int64_t)prob * stride;
+    const int L = (H + 1023) / 1024, i0 = min(H, t * L), i1 = min(H, i0 + L);
+    // pass 1: the range's first status < 0 and its maximum count before it
+    int lneg = H, lmax = -1;
+    for (int b = i0; b < i1 && lneg == H; b += 8) {
+        int8_t sv[8];
+        int32_t cv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = b + k;
+            sv[k] = i < i1 ? st[i] : (int8_t)0;
+            cv[k] = i < i1 ? c[i] : -1;
         }
-        int64_t niters = dec.max_iters > 1 ? dec.max_iters : 1, best = -1;
-        for (int r = 0; r < nr; ++r) {
-            const double ld = __shfl(ldenom, r);
-            const int z = __shfl(zero, r);
-            const int64_t stop = first_neg < niters ? first_neg : niters;
-            if (ridx[r] >= stop) break;
-            best = ridx[r];
-            const int mi = (int)niters;
-            niters = z ? 0 : ((ld >= 0 || -num >= mi * (-ld)) ? mi : (int)lrint(num / ld));
-        }
-        const int64_t stop = first_neg < niters ? first_neg : niters;
-        // fixed budget: the round is the whole budget, so the replay always ends in it
-        const bool done = nrec <= kScanRecs && (dec.fixed || stop < H || H >= niters);
-        if (lane == 0) {
-            // not done: the speculative finish has no model (cheap no-op); the record index of
-            // problem prob's winner (problem 0: the hypothesis itself)
-            dec.best_out[prob] = done && best >= 0 ? (int64_t)prob * stride + best : -1;
-            o.dev_best = (int32_t)best;
-            o.dev_done = done;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (lneg != H) break;
+            if (sv[k] < 0) lneg = b + k;
+            else if (sv[k] > 0) lmax = max(lmax, cv[k]);
         }
     }
+    // block min of lneg
+    int m = lneg;
+    for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
+    if (lane == 0) wv[wave] = m;
+    if (t == 0) s_first_neg = H;
+    __syncthreads();
+    if (t == 0) {
+        int f = H;
+        for (int w = 0; w < 16; ++w) f = min(f, wv[w]);
+        s_first_neg = f;
+    }
+    __syncthreads();
+    const int first_neg = s_first_neg;
+    if (i0 > first_neg) lmax = -1;  // ranges past the first status < 0 take no part
+    // exclusive prefix maximum of the ranges' maxima, from the floor
+    int inc = lmax;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(inc, o);
+        if (lane >= o) inc = max(inc, u);
+    }
+    __syncthreads();
+    if (lane == 63) wv[wave] = inc;
+    __syncthreads();
+    int wpre = model_points - 1;
+    for (int w = 0; w < wave; ++w) wpre = max(wpre, wv[w]);
+    int ex = __shfl_up(inc, 1);
+    int floor_c = max(wpre, lane > 0 ? ex : -1);
+    // pass 2: the range's records (strict prefix maxima above its floor), counted, then placed
+    const int lim = min(i1, first_neg);
+    // the range's valid counts, 8 loads in flight at a time (-1: status <= 0 or past lim)
+    auto chunk8 = [&](int b, int32_t (&v)[8]) __attribute__((always_inline)) {
+        int8_t sv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            sv[k] = b + k < lim ? st[b + k] : (int8_t)0;
+            v[k] = b + k < lim ? c[b + k] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = sv[k] > 0 ? v[k] : -1;
+    };
+    int nr = 0;
+    {
+        int f = floor_c;
+        for (int b = i0; b < lim; b += 8) {
+            int32_t v[8];
+            chunk8(b, v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (v[k] > f) {
+                    f = v[k];
+                    ++nr;
+                }
+        }
+    }
+    int pre = nr;  // inclusive prefix sum of the record counts
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(pre, o);
+        if (lane >= o) pre += u;
+    }
+    if (lane == 63) wv2[wave] = pre;
+    __syncthreads();
+    int base = pre - nr;
+    int total = 0;
+    for (int w = 0; w < 16; ++w) {
+        if (w < wave) base += wv2[w];
+        total += wv2[w];
+    }
+    if (nr && base < kScanRecs) {
+        int f = floor_c, r = base;
+        for (int b = i0; b < lim && r < kScanRecs; b += 8) {
+            int32_t v[8];
+            chunk8(b, v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (v[k] > f) {
+                    f = v[k];
+                    if (r < kScanRecs) {
+                        ridx[r] = b + k;
+                        rcnt[r] = f;
+                    }
+                    ++r;
+                }
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    ScanRecords &o = out[prob];
+    if (lane == 0) {
+        o.nrec = total <= kScanRecs ? total : -1;
+        o.first_neg = first_neg;
+        for (int r = 0; r < total && r < kScanRecs; ++r) {
+            o.idx[r] = ridx[r];
+            o.cnt[r] = rcnt[r];
+        }
+    }
+    if (dec.best_out && (dec.fixed || prob == 0)) scan_decide(ridx, rcnt, total, first_neg, H, model_points, prob,
+                                                                stride, dec, o, lane);
 }
 
 // The record pass of rsac_scan_device (the multi-GPU adaptive loop's scan of a gathered round):
@@ -2175,8 +2334,12 @@ hipError_t launch_pack_rows(const int8_t *status, const int32_t *counts, int32_t
 
 hipError_t launch_scan_records(const int32_t *counts, const int8_t *status, int64_t stride, int32_t P, int32_t H,
                                int model_points, ScanRecords *out, hipStream_t s, ScanDecide dec) {
-    hipLaunchKernelGGL(k_scan_records, dim3((P + 3) / 4), dim3(256), 0, s, counts, status, stride, P, H, model_points,
-                       out, dec);
+    if (H >= kScanBlockH)
+        hipLaunchKernelGGL(k_scan_records_blk, dim3(P), dim3(1024), 0, s, counts, status, stride, H, model_points,
+                           out, dec);
+    else
+        hipLaunchKernelGGL(k_scan_records, dim3((P + 3) / 4), dim3(256), 0, s, counts, status, stride, P, H,
+                           model_points, out, dec);
     return hipGetLastError();
 }
 
@@ -2405,6 +2568,12 @@ static hipError_t launch_mf_w(const PnpArgs &a, int32_t P_, int64_t hyp_begin, i
         cell_pts = cp;
         cell_tiles = tiles;
     }
+#ifdef RSAC_MF_FORCE_CELL  // A/B knob: every tile by cells of this many points
+    if (a.dbg_cell_pts <= 0) {
+        cell_pts = std::min<int64_t>(RSAC_MF_FORCE_CELL, win_pts);
+        cell_tiles = tiles;
+    }
+#endif
     if (a.dbg_cell_pts > 0) {  // test hook: every tile by cells of dbg_cell_pts points (a multiple of 256)
         cell_pts = std::min<int64_t>(std::max<int64_t>(256, a.dbg_cell_pts / 256 * 256), win_pts);
         cell_tiles = tiles;
@@ -3518,35 +3687,152 @@ __global__ void k_fm_bounds_init(int32_t P, int *__restrict__ ws) {
         ws[i] = (i % 8) < 4 ? 0x7FFFFFFF : (int)0x80000000;
 }
 
-__global__ __launch_bounds__(256) void k_fm_solve(HomArgs a, int64_t hyp_begin, int32_t H) {
+// fm_minimal8 on 8 lanes (one row of the 8 x 9 DLT system per lane, in registers): the same
+// operations in the same order, so the same bits (tests: every hypothesis against the oracle).
+// The one-lane form keeps A, its row / column swaps and the permutation in scratch (704 B per
+// lane; 620 MB of WRITE_SIZE per 100k hypotheses, C4); here a row swap is a lane exchange, a
+// column swap selects over the row's 9 registers, and the pivot search is a group reduction.
+// g: the group's first lane; q = lane - g: this lane's point and row.  Group-uniform result.
+__device__ __forceinline__ bool fm_minimal8_g8(float x1, float y1, float x2, float y2, int g, int q, double *F) {
+    // Hartley normalisation of both images (fm_norm8): the sums in point order on every lane
+    double c[2][2], sc[2];
+#pragma unroll
+    for (int im = 0; im < 2; ++im) {
+        const float xs = im ? x2 : x1, ys = im ? y2 : y1;
+        double cx = 0.0, cy = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            cx = cx + (double)__shfl(xs, g + k);
+            cy = cy + (double)__shfl(ys, g + k);
+        }
+        cx = cx * 0.125;
+        cy = cy * 0.125;
+        const double dx = (double)xs - cx, dy = (double)ys - cy;
+        const double tq = dsqrt(dx * dx + dy * dy);
+        double d = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d = d + __shfl(tq, g + k);
+        d = d * 0.125;
+        if (!(d > 1e-300)) return false;
+        c[im][0] = cx;
+        c[im][1] = cy;
+        sc[im] = 1.4142135623730951 / d;
+    }
+    const double u1 = ((double)x1 - c[0][0]) * sc[0], v1 = ((double)y1 - c[0][1]) * sc[0];
+    const double u2 = ((double)x2 - c[1][0]) * sc[1], v2 = ((double)y2 - c[1][1]) * sc[1];
+    double A[9] = {u2 * u1, u2 * v1, u2, v2 * u1, v2 * v1, v2, u1, v1, 1.0};
+    double amax = 0.0;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) amax = dabs(A[j]) > amax ? dabs(A[j]) : amax;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+        const double w = __shfl_xor(amax, o);
+        amax = w > amax ? w : amax;
+    }
+    int perm[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8};
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        // pivot: the first maximum of |A[i][j]|, i >= r, j >= r, in row-major order
+        double best = q >= r ? -1.0 : -2.0;
+        int pc = r;
+#pragma unroll
+        for (int j = r; j < 9; ++j)
+            if (q >= r && dabs(A[j]) > best) { best = dabs(A[j]); pc = j; }
+        int pr = q;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const double ob = __shfl_xor(best, o);
+            const int opr = __shfl_xor(pr, o), opc = __shfl_xor(pc, o);
+            if (ob > best || (ob == best && opr < pr)) { best = ob; pr = opr; pc = opc; }
+        }
+        if (!(best > 1e-12 * amax)) return false;
+        if (pr != r) {  // group-uniform: rows r and pr trade lanes
+            const int src = g + (q == r ? pr : q == pr ? r : q);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) A[j] = __shfl(A[j], src);
+        }
+        if (pc != r) {
+            double apc = A[r];
+#pragma unroll
+            for (int j = r + 1; j < 9; ++j) apc = j == pc ? A[j] : apc;
+            const double ar = A[r];
+#pragma unroll
+            for (int j = r + 1; j < 9; ++j) A[j] = j == pc ? ar : A[j];
+            A[r] = apc;
+            int ppc = perm[r];
+#pragma unroll
+            for (int j = r + 1; j < 9; ++j) ppc = j == pc ? perm[j] : ppc;
+            const int pr0 = perm[r];
+#pragma unroll
+            for (int j = r + 1; j < 9; ++j) perm[j] = j == pc ? pr0 : perm[j];
+            perm[r] = ppc;
+        }
+        double prow[9];
+#pragma unroll
+        for (int j = r; j < 9; ++j) prow[j] = __shfl(A[j], g + r);
+        const double ip = 1.0 / prow[r];
+        if (q != r) {
+            const double f = A[r] * ip;
+            if (f != 0.0) {
+#pragma unroll
+                for (int j = r; j < 9; ++j) A[j] = A[j] - f * prow[j];
+            }
+        }
+    }
+    // f[perm[r]] = -A[r][8] / A[r][r]; f[perm[8]] = 1
+    double arr = A[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) arr = q == j ? A[j] : arr;
+    const double val = -A[8] / arr;
+    double f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = perm[8] == k ? 1.0 : 0.0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const double fr = __shfl(val, g + r);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) f[k] = perm[r] == k ? fr : f[k];
+    }
+    return fm_finish(f, c[0][0], c[0][1], sc[0], c[1][0], c[1][1], sc[1], F);
+}
+
+// 8 lanes per hypothesis (fm_minimal8_g8): 32 hypotheses per 256-thread block
+__global__ __launch_bounds__(256) void k_fm_solve_g8(HomArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
-    const int hl = blockIdx.x * blockDim.x + threadIdx.x;
-    if (hl >= H) return;
-    const int64_t h = hyp_begin + hl;
+    const int lane = threadIdx.x & 63, q = lane & 7, g = lane & ~7;
+    const int hl = blockIdx.x * 32 + (threadIdx.x >> 3);
+    const bool live = hl < H;  // group-uniform; dead groups still reach every shuffle
+    const int64_t h = hyp_begin + (live ? hl : 0);
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
-    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
-    double *m = a.models + rec * kModelStride;
     int8_t st = -1;
     double F[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    bool go = false;
+    float x1 = 0.f, y1 = 0.f, x2 = 0.f, y2 = 0.f;
     if (n >= 8) {
         Philox rng;
         rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
         int32_t idx[8];
         if (rng.subset<8>(n, idx) == 0) {
-            float x1[8], y1[8], x2[8], y2[8];
+            int my = idx[0];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int64_t i = p0 + idx[j];
-                x1[j] = a.SX[i]; y1[j] = a.SY[i]; x2[j] = a.DX[i]; y2[j] = a.DY[i];
-            }
-            st = fm_minimal8(x1, y1, x2, y2, F) ? 1 : 0;
-            if (st == 0)
-                for (int q = 0; q < 9; ++q) F[q] = 0.0;
+            for (int j = 1; j < 8; ++j) my = q == j ? idx[j] : my;
+            const int64_t i = p0 + my;
+            x1 = a.SX[i]; y1 = a.SY[i]; x2 = a.DX[i]; y2 = a.DY[i];
+            go = true;
         }
     }
+    if (go) {  // group-uniform (the subset is the group's)
+        st = fm_minimal8_g8(x1, y1, x2, y2, g, q, F) ? 1 : 0;
+        if (st == 0)
 #pragma unroll
-    for (int q = 0; q < 9; ++q) m[q] = F[q];
+            for (int k = 0; k < 9; ++k) F[k] = 0.0;
+    }
+    if (!live || q != 0) return;
+    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
+    double *m = a.models + rec * kModelStride;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) m[k] = F[k];
     m[kValidSlot] = st > 0 ? 1.0 : 0.0;
     a.status[rec] = st;
     if (a.fmodels) fm_write_record(F, st > 0, a.fbounds, prob, (double)a.thr2[prob], a.fmodels + rec * kFModelStride);
@@ -3762,7 +4048,7 @@ __global__ void k_fm_mask(HomArgs a, const int64_t *__restrict__ best, int64_t b
 }
 
 hipError_t launch_fm_solve(const HomArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
-    hipLaunchKernelGGL(k_fm_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H);
+    hipLaunchKernelGGL(k_fm_solve_g8, dim3(cdiv(H, 32), P), dim3(256), 0, s, a, hyp_begin, H);
     return hipGetLastError();
 }
 

@@ -607,6 +607,9 @@ RSAC_HD void sym3_min_evec(double (&A)[9], double (&v)[3]) {
     v[2] = V[6 + mi];
 }
 
+RSAC_HD bool fm_finish(const double (&f)[9], double c1x, double c1y, double s1, double c2x, double c2y, double s2,
+                       double *F);
+
 // x1,y1 -> x2,y2 (x2^T F x1 = 0); F row-major 3x3.  false for degenerate samples.
 RSAC_HD bool fm_minimal8(const float (&x1)[8], const float (&y1)[8], const float (&x2)[8], const float (&y2)[8],
                          double *F) {
@@ -647,6 +650,13 @@ RSAC_HD bool fm_minimal8(const float (&x1)[8], const float (&y1)[8], const float
     double f[9];
     f[perm[8]] = 1.0;
     for (int r = 0; r < 8; ++r) f[perm[r]] = -A[r][8] / A[r][r];
+    return fm_finish(f, c1x, c1y, s1, c2x, c2y, s2, F);
+}
+
+// the rest of the 8-point solver from the null vector f of the normalised system: rank 2,
+// denormalisation, unit Frobenius norm (shared by fm_minimal8 and the GPU's 8-lane solver)
+RSAC_HD bool fm_finish(const double (&f)[9], double c1x, double c1y, double s1, double c2x, double c2y, double s2,
+                       double *F) {
     // rank 2: Fn (I - v v^T), v the smallest right-singular vector of Fn
     double M[9];
     for (int i = 0; i < 3; ++i)

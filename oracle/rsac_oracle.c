@@ -26,10 +26,13 @@
  *   - homography RANSAC (MWC sampler, OpenCV getSubset/checkSubset, f32 error,
  *     RANSAC-phase mask) is pinned against the 24 complete findHomography
  *     blocks recorded in the reference's debug.log (tests/golden/);
- *   - PnP: OpenCV's default EPnP kernel is not restated; the north-star P3P
- *     kernel (Lambda Twist, Persson & Nordberg, ECCV 2018) is.  PnP parity vs
- *     OpenCV is therefore *unpinned* except for the loose known-answer camera
- *     origin of testpro-K.py:234; GPU parity is against this restatement.
+ *   - PnP: both minimal kernels are restated -- OpenCV's default
+ *     SOLVEPNP_ITERATIVE kernel, EPnP on 5-point MWC samples (orc_pnp_minimal_epnp5,
+ *     the mode every reference call site runs), and the north-star P3P kernel
+ *     (Lambda Twist, Persson & Nordberg, ECCV 2018) -- in this project's own
+ *     numerics (OpenCV is absent).  PnP parity vs OpenCV is therefore *unpinned*
+ *     except for the loose known-answer camera origin of testpro-K.py:234; GPU
+ *     parity is against this restatement.
  *
  * Numerics contract shared with the HIP path (bit-exact on counts/masks):
  *   compile with -ffp-contract=off, no -ffast-math; only + - * / sqrt in any

@@ -1062,3 +1062,40 @@ def test_batched_rows_on_device_equal_flat_outputs(refine, adaptive):
     g = par.sharded_batched(par.pnp_batched_rows(p2, p3, off, Ks, 700, 30.0, adaptive=adaptive, refine=refine),
                             len(probs))
     assert _bits_equal(g.cpu().numpy(), h)
+
+
+@pytest.mark.parametrize("sampler", ["philox", "opencv"])
+def test_fixed_budget_long_round_block_scan(sampler):
+    """Rounds of >= 8192 hypotheses replay their scan in one 1024-thread block per problem
+    (k_scan_records_blk, C4's 100k round): a ragged batch (a dead problem, a 4-point one, a 97 %
+    outlier one with many improvements) over 9000 hypotheses equals the oracle's sequential loop,
+    the device's pick is never redone."""
+    probs = [synth.pnp_problem(n, o, seed=190 + i) for i, (n, o) in
+             enumerate([(1200, 0.6), (40, 0.4), (3000, 0.97), (4, 0.0), (700, 0.85)])]
+    dead = dict(probs[1])
+    dead["points3d"] = np.tile(probs[1]["points3d"][:1], (40, 1))
+    probs[1] = dead
+    f0, r0 = _spec_counters()
+    out = rsac.pnp_ransac_batched([p["points2d"] for p in probs], [p["points3d"] for p in probs],
+                                  [p["K"] for p in probs], 9000, 30.0, adaptive=False, refine=False, sampler=sampler)
+    f1, r1 = _spec_counters()
+    assert (f1 - f0, r1 - r0) == (1, 0)
+    for p, (R, t, m, ni) in zip(probs, out):
+        ref = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 0.99, 9000, 0x5EED, sampler=sampler)
+        assert (R is None) == (ref["best"] < 0)
+        assert ni == ref["n_inliers"]
+        np.testing.assert_array_equal(m, ref["mask"])
+        if R is not None:
+            assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+
+
+def test_fundamental_fixed_budget_long_round():
+    """C4's shape at test size: adaptive off, 12000 hypotheses in one round (block scan), bit-exact
+    against the restatement's scan."""
+    pr = synth.fundamental_problem(20000, 0.8, seed=4)
+    F, m, info = rsac.fundamental_ransac(pr["pts1"], pr["pts2"], 1.5, max_iters=12000, adaptive=False,
+                                         return_info=True)
+    ref = O.fm_ransac(pr["pts1"], pr["pts2"], 1.5, 0.99, 12000)
+    assert (info.best_hyp, info.n_inliers) == (ref["best"], ref["n_inliers"])
+    assert _bits_equal(F, ref["F"])
+    np.testing.assert_array_equal(m, ref["mask"])
