@@ -1431,6 +1431,16 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 #ifndef RSAC_MF_PRIO
 #define RSAC_MF_PRIO 1
 #endif
+// 1: the group body as hand-scheduled inline asm (rsac_mf_asm.inc, scripts/gen_mf_asm.py): its
+// counts equal the compiler's body (the whole -m gpu suite green on it), and it is no faster
+// (C2 scoring 0.2329 against 0.2316 ms, C3 0.998 against 0.984 ms), so the
+// compiler's schedule stays the default
+#ifndef RSAC_MF_ASM
+#define RSAC_MF_ASM 0
+#endif
+#if RSAC_MF_ASM
+#include "rsac_mf_asm.inc"
+#endif
 #ifndef RSAC_MF_LONG_W
 #define RSAC_MF_LONG_W 4
 #endif
@@ -1487,6 +1497,16 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
             const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
             const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Ba, mf_f16v{}, 0, 0, 0);
             const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Bb, mf_f16v{}, 0, 0, 0);
+#if RSAC_MF_ASM
+            // the group's VALU stage by stage, its flags through one SGPR test (rsac_mf_asm.inc)
+            const float a4[4] = {av.x, av.y, av.z, av.w}, b4[4] = {bv.x, bv.y, bv.z, bv.w};
+            switch (t) {
+                case 0: mf_group_asm<0>(xa, xb, ua, ub, a4, b4, 0x0C0C0B09u, vc[0], fl); break;
+                case 1: mf_group_asm<1>(xa, xb, ua, ub, a4, b4, 0x0C0C0B09u, vc[1], fl); break;
+                case 2: mf_group_asm<2>(xa, xb, ua, ub, a4, b4, 0x0C0C0B09u, vc[2], fl); break;
+                default: mf_group_asm<3>(xa, xb, ua, ub, a4, b4, 0x0C0C0B09u, vc[3], fl); break;
+            }
+#else
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
@@ -1495,6 +1515,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
                 vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
                 fl |= __ballot(!(__builtin_fminf(ra.t, rb.t) > bg)) ? (1u << (4 * t + g)) : 0u;
             }
+#endif
         }
         if (__builtin_expect(fl != 0, 0)) {
             if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)i, fl);
