@@ -34,7 +34,7 @@ struct PnpArgs {
     // frame / constants, per-hypothesis float32 records.  fmodels == nullptr
     // (or exact_only) selects the all-f64 scoring kernel.
     const float *XC, *YC, *ZC;
-    const double *frame;  // P x kFrameStride: c0 c1 c2 B rho cmax wmax
+    const double *frame;  // P x kFrameStride: c0 c1 c2 B rho cmax wmax 0 | write_fmodel_mx's terms (8..15)
     const float *fconst;  // P x kFconstStride
     float *fmodels;       // P x hyp_stride x kFModelStride
     // set when the solve kernel precedes the scoring launch: the solve zeroes these counts, so a
@@ -62,7 +62,7 @@ struct PnpArgs {
     int32_t dbg_cell_pts = 0;
 };
 
-constexpr int kFrameStride = 8;
+constexpr int kFrameStride = 16;
 constexpr int kFconstStride = 16;
 constexpr int kFModelStride = 16;
 

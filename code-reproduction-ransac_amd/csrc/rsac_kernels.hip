@@ -184,6 +184,26 @@ __global__ __launch_bounds__(1024) void k_pnp_bounds1(PnpArgs a, int *__restrict
     }
 }
 
+// The per-problem terms of write_fmodel_mx's band (frame[8..15]), computed once per problem
+// instead of once per hypothesis (with fconst's f32 T, Trel and Cmax: q6, q7): s = sqrt(T) (1 when
+// T is out of range), c1 = 2 Cmax / s, Trel' / T, sqrt(1.00001 T), umax, and for the evaluation
+// error of the three rows an upward reciprocal of |sc_r| = (fx, fy, s): RN(RN(1/|sc|)(1 + 2^-50))
+// >= (1/|sc|)(1 + 2^-52), so RN(err x it) >= err / |sc| (the division it replaces)
+__device__ __forceinline__ void pnp_frame_mx_consts(double *f, double fx, double fy, double T, double q6, double q7) {
+    const bool t_ok = T > 1e-12 && T < 1e30;
+    const double s = t_ok ? sqrt(T) : 1.0;
+    const double Cp = 2.0 * q7, Trelp = q6 + 1e-6 * T;
+    f[8] = s;
+    f[9] = Cp / s;
+    f[10] = Trelp / T;
+    f[11] = sqrt(T * 1.00001);
+    f[12] = q7 / (2.5 * kU32);
+    const double up = 1.0 + 0x1p-50;
+    f[13] = (1.0 / fx) * up;
+    f[14] = (1.0 / fy) * up;
+    f[15] = (1.0 / s) * up;
+}
+
 // Per problem: frame = {c0 c1 c2 (bbox centre), B >= |XC|inf, rho >= |XC - (Xf - c)|,
 // max|Xf|, wmax (bound on |x/z| of any projection within thr of a pixel), 0};
 // fconst = {fx fy cx cy T 2.002 sqrt(T) 1e-6 T thr 2/fx 2/fy cu cv cc0} (see the scoring kernel).
@@ -222,6 +242,8 @@ __device__ void pnp_frame_core(const PnpArgs &a, int prob, const int *__restrict
     f[6] = fmax(2.0 * (du + thr) / fx, 2.0 * (dv + thr) / fy) + 2e-3;  // wmax (>= every per-point wa, wb)
     f[7] = 0;
     float *q = fconst + (int64_t)prob * kFconstStride;
+    pnp_frame_mx_consts(f, fx, fy, T, (double)(float)(4e-6 * T + 1e-30),
+                        (double)(float)(2.5 * kU32 * (du + dv + fabs(cx) + fabs(cy) + 2.0 * thr + 3.0) + 1e-6));
     q[0] = (float)cm[0]; q[1] = (float)cm[1]; q[2] = (float)cx; q[3] = (float)cy;
     q[4] = (float)T;
     q[5] = (float)(2.002 * thr);
@@ -651,27 +673,29 @@ __device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t
     fm[15] = fits ? (float)((b + a * Zp) * (1.0 + 1e-6)) : __builtin_inff();  // constant band b + a Zmax
 }
 
-// The band constants of the scaled form (write_fmodel_sc) from the camera-frame evaluation error
-// bounds eps (rows x y z) and the row magnitudes mag: {a, b, zg, b + a Zp}; fits = false when a
-// quantity of the test could leave the f32 range (then b = +inf: every pair recounted exactly)
+// The band constants of the scaled form (write_fmodel_sc's formulas) from the camera-frame
+// evaluation error bounds eps (rows x y z) and the row magnitudes mag: {a, b, zg, b + a Zp}; fits =
+// false when a quantity of the test could leave the f32 range (then b = +inf: every pair recounted
+// exactly)
 struct ScBand {
     double a, b, zg, bcb, Zp, qmax;
 };
-__device__ __forceinline__ ScBand sc_band(const double (&eps)[3], const double (&mag)[3], double fx, double fy,
-                                          double wmax, double T, double s, const float *fconst) {
+// for write_fmodel_mx, with the frame's per-problem terms (pnp_frame_mx_consts: s, 2 Cmax / s,
+// Trel' / T, sqrt(1.00001 T), umax, computed once per problem)
+__device__ __forceinline__ ScBand sc_band_h(const double (&eps)[3], const double (&mag)[3], double fx, double fy,
+                                            double wmax, double T, const double *frame, const float *fconst) {
     ScBand r;
+    const double s = frame[8], c1 = frame[9], Trel_T = frame[10], sqT = frame[11], umax = frame[12];
     const double D0 = 1.01 * (fx * eps[0] + fy * eps[1] + eps[2] * (fx + fy) * wmax);
     r.zg = 100.0 * (fmax(eps[0], eps[1]) + wmax * eps[2]) + 2.02 * eps[2] + 1e-30;
-    const double Cp = 2.0 * (double)fconst[7], Trelp = (double)fconst[6] + 1e-6 * T;
-    const double c1 = Cp / s;
+    const double Cp = 2.0 * (double)fconst[7];
     r.Zp = s * (mag[2] + eps[2]) * (1.0 + 1e-6);
-    r.a = 1.01 * (D0 * (2.002 + 2.0 * c1) + (c1 * (2.002 + c1) + Trelp / T) * r.Zp);
+    r.a = 1.01 * (D0 * (2.002 + 2.0 * c1) + (c1 * (2.002 + c1) + Trel_T) * r.Zp);
     r.b = 1.01 * D0 * D0;
     const double zr = r.zg + eps[2];
-    const double Kq = D0 + Cp * zr + sqrt(T * 1.00001) * zr;
+    const double Kq = D0 + Cp * zr + sqT * zr;
     r.b = fmax(r.b, (1.0 + 1e-6) * Kq * Kq);
     r.b = fmax(r.b, T * r.zg * r.zg * (1.0 + 1e-5));
-    const double umax = (double)fconst[7] / (2.5 * kU32);
     r.qmax = fx * mag[0] + fy * mag[1] + umax * (mag[2] + eps[2]) + D0;
     r.bcb = (r.b + r.a * r.Zp) * (1.0 + 1e-6);
     return r;
@@ -711,7 +735,7 @@ __device__ __forceinline__ void write_fmodel_mx(const double *R, const double *t
     const double fx = fabs(cam[0]), fy = fabs(cam[1]);
     const double T = fconst[4];
     const bool t_ok = T > 1e-12 && T < 1e30;
-    const double s = t_ok ? sqrt(T) : 1.0;
+    const double s = frame[8];  // sqrt(T), 1 when T is out of range (pnp_frame_mx_consts)
     const double sc[3] = {-cam[0], -cam[1], s};
     double A[3][4], r1[3], mag[3], tp[3];
     double M = 0.0;
@@ -754,9 +778,10 @@ __device__ __forceinline__ void write_fmodel_mx(const double *R, const double *t
         // A side + B side (2^-21 relative on XC YC ZC, 2^-13 absolute) + the accumulation (16u: 16
         // exact products summed in round-to-nearest f32, any order)
         const double err = 1.001 * (dA + 0x1p-21 * AB + 0x1p-13 * SA + 0x1p-20 * (AB + dA + 0x1p-13 * SA + 1.0));
-        eps[r] = err / (lam * fabs(sc[r])) + r1[r] * rho + 4e-15 * (r1[r] * cmax + fabs(t[r]));
+        // err / (lam |sc_r|), rounded up: the frame's upward reciprocal of |sc_r| and the exact 2^-kx
+        eps[r] = ldexp(err * frame[13 + r], -kx) + r1[r] * rho + 4e-15 * (r1[r] * cmax + fabs(t[r]));
     }
-    ScBand bd = sc_band(eps, mag, fx, fy, wmax, T, s, fconst);
+    ScBand bd = sc_band_h(eps, mag, fx, fy, wmax, T, frame, fconst);
     const double ap = bd.a * lam, bp = bd.b * lam * lam, cbp = bd.bcb * lam * lam;
     const bool fits = t_ok && M > 0.0 && bd.qmax * lam < 1e17 && bd.Zp * lam < 1e17 && ap * bd.Zp * lam < 1e30 &&
                       bp < 1e30 && cbp < 1e30 && bp > 1e-30;
@@ -825,7 +850,11 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     m[kValidSlot] = st > 0 ? 1.0 : 0.0;
     a.status[rec] = st;
     if (a.counts_out) a.counts_out[rec] = 0;  // the scoring launch that follows may accumulate
+#ifdef RSAC_PROBE_NOFM
+    if (a.fmodels && a.hyp_stride < 0)  // timing probe only: the records of the previous call stay
+#else
     if (a.fmodels)
+#endif
         write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
                      a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
 }

@@ -377,6 +377,11 @@ RSAC_HD int p3p_lambdatwist(const double *y, const double *x, Emit &&emit) {
 }
 
 RSAC_HD void bearing(const Cam &k, float uf, float vf, double *out) {
+#if defined(RSAC_PROBE_BEARING) && defined(__HIP_DEVICE_COMPILE__)
+    // timing probe only (scripts/build_ab.sh): the bearing without divisions or sqrt (wrong bits)
+    { double xq = ((double)uf - k.cx) * 1e-3, yq = ((double)vf - k.cy) * 1e-3;
+      out[0] = xq; out[1] = yq; out[2] = 1.0 - 0.5 * (xq * xq + yq * yq); return; }
+#endif
     double xn = ((double)uf - k.cx) / k.fx;
     double yn = ((double)vf - k.cy) / k.fy;
     double nrm = dsqrt(xn * xn + yn * yn + 1.0);
