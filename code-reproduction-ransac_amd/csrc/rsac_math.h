@@ -208,11 +208,9 @@ RSAC_HD void lt_refine(double &L0, double &L1, double &L2, double a12, double a1
 // (R, t); returns the count.
 // One candidate (lambda1..3) of the Lambda Twist solver: Gauss-Newton refine, then
 // the pose from the scaled bearings; emitted if finite.  Returns 1 if emitted.
-template <class Emit>
-RSAC_HD int p3p_pose(double l1, double l2, double l3, double a12, double a13, double a23, double b12, double b13,
-                     double b23, const double *y1, const double *y2, const double *y3, const double *x1,
-                     const double *Xi, Emit &emit) {
-    lt_refine(l1, l2, l3, a12, a13, a23, b12, b13, b23);
+// The pose of refined lambdas (l1..l3): false when not finite
+RSAC_HD bool p3p_pose_of(double l1, double l2, double l3, const double *y1, const double *y2, const double *y3,
+                         const double *x1, const double *Xi, double (&R)[9], double (&t)[3]) {
     double ry1[3], ry2[3], ry3[3], yd1[3], yd2[3], yc[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) { ry1[k] = y1[k] * l1; ry2[k] = y2[k] * l2; ry3[k] = y3[k] * l3; }
@@ -222,7 +220,6 @@ RSAC_HD int p3p_pose(double l1, double l2, double l3, double a12, double a13, do
     yc[1] = yd1[2] * yd2[0] - yd1[0] * yd2[2];
     yc[2] = yd1[0] * yd2[1] - yd1[1] * yd2[0];
     const double Y[9] = {yd1[0], yd2[0], yc[0], yd1[1], yd2[1], yc[1], yd1[2], yd2[2], yc[2]};
-    double R[9], t[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -237,7 +234,15 @@ RSAC_HD int p3p_pose(double l1, double l2, double l3, double a12, double a13, do
     }
 #pragma unroll
     for (int k = 0; k < 9; ++k) fin = fin && dfinite(R[k]);
-    if (!fin) return 0;
+    return fin;
+}
+template <class Emit>
+RSAC_HD int p3p_pose(double l1, double l2, double l3, double a12, double a13, double a23, double b12, double b13,
+                     double b23, const double *y1, const double *y2, const double *y3, const double *x1,
+                     const double *Xi, Emit &emit) {
+    lt_refine(l1, l2, l3, a12, a13, a23, b12, b13, b23);
+    double R[9], t[3];
+    if (!p3p_pose_of(l1, l2, l3, y1, y2, y3, x1, Xi, R, t)) return 0;
     emit(R, t);
     return 1;
 }
@@ -377,11 +382,6 @@ RSAC_HD int p3p_lambdatwist(const double *y, const double *x, Emit &&emit) {
 }
 
 RSAC_HD void bearing(const Cam &k, float uf, float vf, double *out) {
-#if defined(RSAC_PROBE_BEARING) && defined(__HIP_DEVICE_COMPILE__)
-    // timing probe only (scripts/build_ab.sh): the bearing without divisions or sqrt (wrong bits)
-    { double xq = ((double)uf - k.cx) * 1e-3, yq = ((double)vf - k.cy) * 1e-3;
-      out[0] = xq; out[1] = yq; out[2] = 1.0 - 0.5 * (xq * xq + yq * yq); return; }
-#endif
     double xn = ((double)uf - k.cx) / k.fx;
     double yn = ((double)vf - k.cy) / k.fy;
     double nrm = dsqrt(xn * xn + yn * yn + 1.0);
@@ -402,13 +402,13 @@ RSAC_HD double pnp_fourth_error(const double *Rk, const double *tk, const float 
 }
 
 // 4-point minimal PnP: P3P on the first three, disambiguated by the fourth.
-// pts: per sample point (X, Y, Z, u, v) already gathered.
-RSAC_HD bool pnp_minimal(const float (&X)[4], const float (&Y)[4], const float (&Z)[4], const float (&U)[4],
-                         const float (&V)[4], const Cam &k, double *R, double *t) {
-    double yb[9], xw[9];
+// pts: per sample point (X, Y, Z, u, v) already gathered; yb: the first three points' bearings
+// (bearing(), here or from a table of them built with the same function)
+RSAC_HD bool pnp_minimal_yb(const float (&X)[4], const float (&Y)[4], const float (&Z)[4], const float (&U)[4],
+                            const float (&V)[4], const Cam &k, const double (&yb)[9], double *R, double *t) {
+    double xw[9];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        bearing(k, U[j], V[j], yb + 3 * j);
         xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
     }
     bool have = false;
@@ -428,6 +428,61 @@ RSAC_HD bool pnp_minimal(const float (&X)[4], const float (&Y)[4], const float (
     });
     if (ns == 0 || !have) return false;
     return true;
+}
+// pnp_minimal_yb for one GPU lane: the best candidate is held as its refined lambdas (3 doubles
+// instead of R and t's 12, fewer registers live across the candidate loop) and its pose is
+// rebuilt from them at the end with p3p_pose_of's operations: the same candidates in the same
+// order (p3p_lambdatwist), the same first-smallest rule, the same bits
+RSAC_HD bool pnp_minimal_lam(const float (&X)[4], const float (&Y)[4], const float (&Z)[4], const float (&U)[4],
+                             const float (&V)[4], const Cam &k, const double (&yb)[9], double (&R)[9], double (&t)[3]) {
+    double xw[9];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
+    }
+    LtCommon L;
+    if (!lt_common(yb, xw, L)) return false;
+    bool have = false;
+    double best_e = 0.0, bl[3] = {0.0, 0.0, 0.0};
+    // both signs' (w0, w1, tau) first: v, v1, v2 are then dead across the candidate loop
+    double w0s[2], w1s[2], taus[2][2];
+    bool oks[2];
+#pragma unroll
+    for (int sgn = 0; sgn < 2; ++sgn) oks[sgn] = lt_sign(L, sgn, w0s[sgn], w1s[sgn], taus[sgn]);
+    for (int sgn = 0; sgn < 2; ++sgn) {
+        if (!oks[sgn]) continue;
+        const double w0 = w0s[sgn], w1 = w1s[sgn];
+        for (int q = 0; q < 2; ++q) {
+            // lt_tau, then p3p_pose
+            const double tq = taus[sgn][q];
+            if (!(tq > 0.0)) continue;
+            const double d = L.a23 / (tq * (L.b23 + tq) + 1.0);
+            if (!(d > 0.0)) continue;
+            double l2 = dsqrt(d);
+            double l3 = tq * l2;
+            double l1 = w0 * l2 + w1 * l3;
+            if (!(l1 >= 0.0)) continue;
+            lt_refine(l1, l2, l3, L.a12, L.a13, L.a23, L.b12, L.b13, L.b23);
+            double Rk[9], tk[3];
+            if (!p3p_pose_of(l1, l2, l3, yb, yb + 3, yb + 6, xw, L.Xi, Rk, tk)) continue;
+            const double e = pnp_fourth_error(Rk, tk, X, Y, Z, U, V, k);
+            if (!(e == e)) continue;
+            if (!have || e < best_e) {
+                have = true;
+                best_e = e;
+                bl[0] = l1; bl[1] = l2; bl[2] = l3;
+            }
+        }
+    }
+    if (!have) return false;
+    return p3p_pose_of(bl[0], bl[1], bl[2], yb, yb + 3, yb + 6, xw, L.Xi, R, t);
+}
+RSAC_HD bool pnp_minimal(const float (&X)[4], const float (&Y)[4], const float (&Z)[4], const float (&U)[4],
+                         const float (&V)[4], const Cam &k, double *R, double *t) {
+    double yb[9];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) bearing(k, U[j], V[j], yb + 3 * j);
+    return pnp_minimal_yb(X, Y, Z, U, V, k, yb, R, t);
 }
 
 // ---------------------------------------------------------------------------

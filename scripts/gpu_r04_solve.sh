@@ -7,3 +7,6 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
     > gpurun_out/r04_solve_tests.log 2>&1
 rc=$?; tail -4 gpurun_out/r04_solve_tests.log; [ $rc -eq 0 ] || exit $rc
 bash scripts/gpu_solve_probe.sh "$@"
+rc=$?; [ $rc -eq 0 ] || exit $rc
+# the reference's default minimal solver (EPnP-5) against P3P, fixed budget, C2 problem
+timeout -k 10 300 python3 scripts/epnp5_prof.py 20000 3
