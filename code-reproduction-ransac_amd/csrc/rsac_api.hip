@@ -352,10 +352,9 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     // resets best_key and the queue, then builds the frame (also in exact mode: cheap)
     // one problem: k_pnp_setup_fc's scratch (its ticket starts at 0; the kernel resets it)
     if (!a.exact_only) {  // the MFMA scorer's point operands, written with the centring
-        HIPCHK(c->mxpts.ensure(64 * std::max<int64_t>(N, 1)));
+        HIPCHK(c->mxpts.ensure(40 * std::max<int64_t>(N, 1)));
         a.PF = c->mxpts.as<uint4>();
         a.UV = reinterpret_cast<float2 *>(c->mxpts.as<char>() + 32 * std::max<int64_t>(N, 1));
-        a.BR = reinterpret_cast<double *>(c->mxpts.as<char>() + 40 * std::max<int64_t>(N, 1));
     }
     PnpPrepare prep = st.prep;
     if (P == 1) {

@@ -54,10 +54,6 @@ struct PnpArgs {
     // UV = (u - cx, v - cy) / sqrt(T)
     uint4 *PF = nullptr;
     float2 *UV = nullptr;
-    // per point the unit bearing of its pixel (rsac_math.h bearing(), 3 doubles), written with the
-    // MFMA operands: the P3P solve reads its sample's bearings instead of computing them (each point
-    // is drawn about 4H/N times per call)
-    double *BR = nullptr;
     // sample size and minimal solver: 4 = P3P (SOLVEPNP_P3P), 5 = EPnP on 5 points (the
     // default SOLVEPNP_ITERATIVE kernel, RSAC_F_MINIMAL_EPNP5); subsets then hold sample_k indices
     int32_t sample_k = 4;

@@ -274,13 +274,11 @@ __device__ void pnp_frame_one(const PnpArgs &a, int32_t P, int prob, const int *
 // (the origin, pixel at 3e38).
 struct MxPixel {
     float cx, cy, inv_s;
-    Cam k;  // the bearings' camera (PnpArgs::BR)
 };
 __device__ __forceinline__ MxPixel mx_pixel(const PnpArgs &a, int prob) {
     const double T = a.thr2[prob];
     const float inv_s = (T > 1e-12 && T < 1e30) ? (float)(1.0 / sqrt(T)) : 1.f;  // = fconst[9]
-    const double *c = a.cams + 4 * prob;
-    return MxPixel{(float)c[2], (float)c[3], inv_s, Cam{c[0], c[1], c[2], c[3]}};
+    return MxPixel{(float)a.cams[4 * prob + 2], (float)a.cams[4 * prob + 3], inv_s};
 }
 __device__ __forceinline__ uint32_t mx_pack2(_Float16 lo16, _Float16 hi16) {
     return (uint32_t)__builtin_bit_cast(uint16_t, lo16) | ((uint32_t)__builtin_bit_cast(uint16_t, hi16) << 16);
@@ -305,7 +303,6 @@ __device__ __forceinline__ void mx_point(const PnpArgs &a, int64_t q, float xc, 
     a.PF[2 * q] = f;
     a.PF[2 * q + 1] = g;
     a.UV[q] = uv;
-    if (a.BR) bearing(k.k, uu, vv, a.BR + 3 * q);  // as the solve would (pnp_minimal)
 }
 
 // centred coordinates; block 0 of each problem also writes the problem's frame and
@@ -852,16 +849,11 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
         }
         const double *c = a.cams + 4 * prob;
         Cam k{c[0], c[1], c[2], c[3]};
+        // (a per-point table of bearings written by the setup measured no faster: the solve then
+        // waits on three gathers per sample instead of computing them, r04)
         double yb[9];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            if (a.BR) {  // the setup's table: the same bits as bearing() here
-                const double *b = a.BR + 3 * (p0 + idx[j]);
-                yb[3 * j] = b[0]; yb[3 * j + 1] = b[1]; yb[3 * j + 2] = b[2];
-            } else {
-                bearing(k, U[j], V[j], yb + 3 * j);
-            }
-        }
+        for (int j = 0; j < 3; ++j) bearing(k, U[j], V[j], yb + 3 * j);
 #ifdef RSAC_SOLVE_RT
         st = pnp_minimal_yb(X, Y, Z, U, V, k, yb, R, t) ? 1 : 0;
 #else
@@ -984,12 +976,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
         double yb[9], xw[9];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            if (a.BR) {
-                const double *b = a.BR + 3 * (p0 + idx[j]);
-                yb[3 * j] = b[0]; yb[3 * j + 1] = b[1]; yb[3 * j + 2] = b[2];
-            } else {
-                bearing(k, U[j], V[j], yb + 3 * j);
-            }
+            bearing(k, U[j], V[j], yb + 3 * j);
             xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
         }
         LtCommon L;
