@@ -123,6 +123,7 @@ struct rsac_ctx {
     float *d_thr2 = nullptr;
     DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
     DevBuf mxpts;                                              // MFMA point operands (PF, UV: 40 B / point)
+    DevBuf epnp5;                                              // EPnP-5 minimal solve: 112 doubles / hypothesis
     DevBuf loc;                                                // location search: inputs, pos2, H, err
     DevBuf lo;                                                 // LO-RANSAC: 2 model records, chain state, 2 masks
     const void *lo_state_base = nullptr;                       // the lo allocation whose LoState is zeroed
@@ -345,6 +346,14 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     a.queue = c->queue.as<int>();
     a.exact_only = (flags & RSAC_F_EXACT_ONLY) ? 1 : 0;
     a.sample_k = (flags & RSAC_F_MINIMAL_EPNP5) ? 5 : 4;
+    const char *split = getenv("RSAC_EPNP5_SPLIT");  // "0": the one-kernel form (A/B)
+    if (a.sample_k == 5 && !(split && split[0] == '0')) {
+        // the three-launch EPnP-5 solve's records, one per hypothesis record of c->models (sized
+        // by ensure_hyp_buffers before this call)
+        const size_t recs = c->models.cap / (sizeof(double) * kModelStride);
+        HIPCHK(c->epnp5.ensure(std::max<size_t>(recs, 1) * 112 * sizeof(double)));
+        a.epnp = c->epnp5.as<double>();
+    }
     a.dbg_cell_pts = c->dbg_cell_pts;
     float *C = c->centred.as<float>();
     int32_t max_n = 0;
@@ -1147,7 +1156,7 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->lmscr, &c->setup_scr, &c->scanrec, &c->mxpts, &c->reproj};
+                     &c->epnp, &c->epnp5, &c->lmscr, &c->setup_scr, &c->scanrec, &c->mxpts, &c->reproj};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_lmfail, &c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,

@@ -57,6 +57,9 @@ struct PnpArgs {
     // sample size and minimal solver: 4 = P3P (SOLVEPNP_P3P), 5 = EPnP on 5 points (the
     // default SOLVEPNP_ITERATIVE kernel, RSAC_F_MINIMAL_EPNP5); subsets then hold sample_k indices
     int32_t sample_k = 4;
+    // EPnP-5 minimal solve in three launches (k_epnp5_*): per hypothesis record kEpnpRec doubles
+    // of stage-1 results and eigenvectors; nullptr = the one-kernel form (k_pnp_solve_epnp5)
+    double *epnp = nullptr;
     // test hook (RSAC_DBG_MF_CELL_PTS): > 0 splits every tile of the MFMA scorer into cells of
     // this many points (the unit-size sweep of scripts/mf_units.py); 0 = the launcher's policy
     int32_t dbg_cell_pts = 0;

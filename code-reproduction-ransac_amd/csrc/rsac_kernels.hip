@@ -930,6 +930,235 @@ __global__ __launch_bounds__(256) void k_pnp_solve_epnp5(PnpArgs a, int64_t hyp_
                      a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
 }
 
+// The EPnP-5 minimal solve in three launches (RSAC_EPNP5_SPLIT, the default): the 12 x 12 Jacobi
+// eigen-decomposition of M^T M, ~88 % of the solve's arithmetic, runs on 16 lanes per hypothesis
+// (one row of A and of V per lane, the rotation parameters and the exchanged rows through
+// ds_bpermute) instead of in one lane's scratch memory; the stages before and after it stay one
+// lane per hypothesis.  Every element sees the operations of jacobi_eig<12> in the same order, so
+// the records are bit-identical to k_pnp_solve_epnp5's (and the oracle's orc_pnp_minimal_epnp5).
+// Per hypothesis a.epnp holds EpnpStage1 (doubles 0..63) and the 4 eigenvectors ut (64..111).
+constexpr int kEpnpRec = 112;
+static_assert(sizeof(EpnpStage1) <= 64 * sizeof(double), "EpnpStage1 exceeds its slot");
+
+// the sample of hypothesis rec (OpenCV subsets or Philox), status 1 drawn / -1 not
+__device__ __forceinline__ int8_t epnp5_sample(const PnpArgs &a, int64_t rec, int64_t h, int n, int32_t (&idx)[5]) {
+    if (a.subsets) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) idx[j] = a.subsets[rec * 5 + j];
+        return a.sub_status[rec];
+    }
+    Philox rng;
+    rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
+    return (n >= 5 && rng.subset<5>(n, idx) == 0) ? 1 : -1;
+}
+// pnp_epnp_minimal<5>'s reducer: the sample centred on its first point
+__device__ __forceinline__ void epnp5_reducer(const PnpArgs &a, int64_t p0, const int32_t (&idx)[5],
+                                              MinimalEpnpReducer<5> &red, double (&c)[3]) {
+    float X[5], Y[5], Z[5], U[5], V[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const int64_t i = p0 + idx[j];
+        X[j] = a.X[i]; Y[j] = a.Y[i]; Z[j] = a.Z[i]; U[j] = a.U[i]; V[j] = a.V[i];
+    }
+    c[0] = (double)X[0]; c[1] = (double)Y[0]; c[2] = (double)Z[0];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        red.X[i] = (double)X[i] - c[0];
+        red.Y[i] = (double)Y[i] - c[1];
+        red.Z[i] = (double)Z[i] - c[2];
+        red.u[i] = (double)U[i];
+        red.v[i] = (double)V[i];
+    }
+}
+
+// 1 of 3: sample, stage 1 (centroid, principal axes, the control-point pair sums)
+__global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    const int prob = blockIdx.y;
+    const int hl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (hl == 0 && prob == 0) {
+        if (a.queue) reset_pnp_queue(a.queue);
+    }
+    if (hl >= H) return;
+    const int64_t h = hyp_begin + hl;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
+    int32_t idx[5];
+    const int8_t st = epnp5_sample(a, rec, h, n, idx);
+    EpnpStage1 s1;
+    s1.ok = 0.0;
+    s1.n = 0.0;
+    if (st > 0) {
+        MinimalEpnpReducer<5> red;
+        double c[3];
+        epnp5_reducer(a, p0, idx, red, c);
+        const double *cm = a.cams + 4 * prob;
+        epnp_stage1(red, Cam{cm[0], cm[1], cm[2], cm[3]}, s1);
+    }
+    a.status[rec] = st;
+    *reinterpret_cast<EpnpStage1 *>(a.epnp + rec * kEpnpRec) = s1;
+}
+
+__device__ __forceinline__ double bperm_f64(double x, int src_lane) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)(u >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+typedef double epnp_row __attribute__((ext_vector_type(16)));
+
+// 2 of 3: M^T M's eigenvectors, 16 lanes per hypothesis (4 per wave).  Lane j < 12 builds row j
+// of A (epnp_mtm's entries) and holds row j of V; a rotation (p, q) reads A[p][p], A[p][q],
+// A[q][q] from lanes p and q, updates columns p and q of every row in place (the row's own
+// elements, indexed by the wave-uniform p, q), then lanes p and q swap their updated rows and
+// form the new rows p and q: jacobi_eig<12>'s column, row and V loops element for element.  The
+// sweep test sums A's upper triangle in jacobi_eig's order.  Groups whose sweeps end early idle
+// until the wave's last group is done.
+__global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    const int prob = blockIdx.y;
+    const int lane = threadIdx.x & 63, j = lane & 15, g0 = lane & ~15;
+    const int hl = (int)((blockIdx.x * 256u + threadIdx.x) >> 4);
+    const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
+    double *E = a.epnp + rec * kEpnpRec;
+    const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
+    bool run = hl < H && a.status[rec] > 0 && s1->ok != 0.0;
+    epnp_row A, V;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        A[c] = 0.0;
+        V[c] = c == j ? 1.0 : 0.0;
+    }
+    if (run && j < 12) {  // row j = 3i + p of epnp_mtm's matrix
+        const double *cm = a.cams + 4 * prob;
+        const double fx = cm[0], fy = cm[1];
+        const int i = j / 3, p = j - 3 * i;
+        constexpr int first[4] = {0, 4, 7, 9};  // pair (x <= y) -> sum block x's first + (y - x)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int lo = min(i, jj), hi = max(i, jj);
+            const double *ps = s1->pairs + 4 * (first[lo] + hi - lo);
+            const double s0 = ps[0], su = ps[1], sv = ps[2], sw = ps[3];
+            const double blk[9] = {fx * fx * s0, 0.0, fx * su, 0.0, fy * fy * s0, fy * sv, fx * su, fy * sv, sw};
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) A[3 * jj + rr] = p == 0 ? blk[rr] : p == 1 ? blk[3 + rr] : blk[6 + rr];
+        }
+    }
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        if (run) {
+            double off = 0.0, diag = 0.0;
+#pragma unroll
+            for (int p = 0; p < 12; ++p) {
+#pragma unroll
+                for (int q = p; q < 12; ++q) {
+                    const double x = bperm_f64(A[q], g0 + p);
+                    if (q == p)
+                        diag = diag + x * x;
+                    else
+                        off = off + x * x;
+                }
+            }
+            if (!(off > 1e-32 * diag)) run = false;
+        }
+        if (__ballot(run) == 0) break;
+        if (!run) continue;
+#pragma unroll 1
+        for (int p = 0; p < 11; ++p) {
+#pragma unroll 1
+            for (int q = p + 1; q < 12; ++q) {
+                const double apq = bperm_f64(A[q], g0 + p);
+                if (apq == 0.0) continue;
+                const double app = bperm_f64(A[p], g0 + p), aqq = bperm_f64(A[q], g0 + q);
+                const double theta = (aqq - app) / (2.0 * apq);
+                const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
+                const double cs = 1.0 / dsqrt(tt * tt + 1.0), sn = tt * cs;
+                {
+                    const double akp = A[p], akq = A[q];
+                    A[p] = cs * akp - sn * akq;
+                    A[q] = sn * akp + cs * akq;
+                }
+                const int partner = g0 + (j == p ? q : p);
+#pragma unroll
+                for (int k = 0; k < 12; ++k) {
+                    const double o = bperm_f64(A[k], partner);
+                    const double np = cs * A[k] - sn * o, nq = sn * o + cs * A[k];
+                    A[k] = j == p ? np : j == q ? nq : A[k];
+                }
+                {
+                    const double vkp = V[p], vkq = V[q];
+                    V[p] = cs * vkp - sn * vkq;
+                    V[q] = sn * vkp + cs * vkq;
+                }
+            }
+        }
+    }
+    if (!(hl < H && a.status[rec] > 0 && s1->ok != 0.0)) return;
+    double d[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) d[k] = bperm_f64(A[k], g0 + k);
+    int o[12];
+    eig_order_desc<12>(d, o);
+    if (j >= 12) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int col = o[11 - i];
+        double v = 0.0;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) v = c == col ? V[c] : v;
+        E[64 + 12 * i + j] = v;  // ut[i][j] = V[j][o[11 - i]]
+    }
+}
+
+// 3 of 3: stage 2's rest (L, rho, the beta estimates), stage 3 (the poses, the lowest mean error),
+// the records (as k_pnp_solve_epnp5)
+__global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    const int prob = blockIdx.y;
+    const int hl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (hl >= H) return;
+    const int64_t h = hyp_begin + hl;
+    const int64_t p0 = a.offsets[prob];
+    const int n = (int)(a.offsets[prob + 1] - p0);
+    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
+    double *m = a.models + rec * kModelStride;
+    const double *E = a.epnp + rec * kEpnpRec;
+    int8_t st = a.status[rec];
+    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
+    if (st > 0) {
+        const EpnpStage1 s1 = *reinterpret_cast<const EpnpStage1 *>(E);
+        bool ok = s1.ok != 0.0;
+        if (ok) {
+            EpnpStage2 s2;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 12; ++c) s2.ut[i][c] = E[64 + 12 * i + c];
+            epnp_stage2_post(s1, s2);
+            int32_t idx[5];
+            (void)epnp5_sample(a, rec, h, n, idx);
+            MinimalEpnpReducer<5> red;
+            double c[3];
+            epnp5_reducer(a, p0, idx, red, c);
+            const double *cm = a.cams + 4 * prob;
+            ok = epnp_stage3(red, Cam{cm[0], cm[1], cm[2], cm[3]}, s1, s2, R, t);
+            if (ok) lm_from_centred(R, c, t);
+        }
+        st = ok ? 1 : 0;
+        if (!ok)
+            for (int q = 0; q < 9; ++q) R[q] = 0.0;
+        if (!ok)
+            for (int q = 0; q < 3; ++q) t[q] = 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) m[q] = R[q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
+    m[kValidSlot] = st > 0 ? 1.0 : 0.0;
+    a.status[rec] = st;
+    if (a.counts_out) a.counts_out[rec] = 0;
+    if (a.fmodels)
+        write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
+}
+
 // Small rounds (an adaptive run's first 256 hypotheses: one block, every lane's latency is the
 // launch's): four lanes per hypothesis.  All four draw the sample and run lt_common; lane c
 // then takes candidate c = (sign, root) of the Lambda Twist solution list (lt_sign, lt_tau:
@@ -2529,7 +2758,11 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
 
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
-    if (a.sample_k == 5)
+    if (a.sample_k == 5 && a.epnp) {  // the three-launch form (k_epnp5_a / _jacobi / _c)
+        hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+        hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv(16 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+        hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+    } else if (a.sample_k == 5)
         hipLaunchKernelGGL(k_pnp_solve_epnp5, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     else if ((int64_t)P * H <= kSolve4MaxHyps)

@@ -1277,36 +1277,33 @@ RSAC_HD void epnp_mtm(EpnpShared *sh, const double *pairs, const Cam &k) {
         }
 }
 
-__host__ __device__ inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, EpnpStage2 &s2) {
-    EpnpShared shm;
-    EpnpShared *sh = &shm;
+// Stage 2 after the eigen-decomposition: s2.ut (the eigenvectors of M^T M's 4 smallest
+// eigenvalues) given, the L 6x10 / rho system and the three beta estimates with Gauss-Newton.
+// (epnp_stage2 below; the GPU's minimal EPnP runs the 12 x 12 Jacobi on 16 lanes in between,
+// k_epnp5_jacobi)
+__host__ __device__ inline void epnp_stage2_post(const EpnpStage1 &s1, EpnpStage2 &s2) {
+    double L[60], rho[6];
     const EpnpFrame &f = s1.f;
-    epnp_mtm(sh, s1.pairs, k);
-    jacobi_eig<12>(sh->A, sh->V, sh->d);
     int q = 0;
-    int o[12];
-    eig_order_desc<12>(sh->d, o);
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 12; ++j) s2.ut[i][j] = sh->V[12 * j + o[11 - i]];
     const double *vv[4] = {s2.ut[0], s2.ut[1], s2.ut[2], s2.ut[3]};
-    epnp_l6x10(vv, sh->L);
+    epnp_l6x10(vv, L);
     q = 0;
     for (int a = 0; a < 4; ++a)
         for (int b = a + 1; b < 4; ++b, ++q) {
             const double dx = f.cw[a][0] - f.cw[b][0], dy = f.cw[a][1] - f.cw[b][1], dz = f.cw[a][2] - f.cw[b][2];
-            sh->rho[q] = dx * dx + dy * dy + dz * dz;
+            rho[q] = dx * dx + dy * dy + dz * dz;
         }
     for (int approx = 1; approx <= 3; ++approx) {
         double *be = s2.be[approx - 1];
         for (int j = 0; j < 4; ++j) be[j] = 0.0;
         double b[6];
-        for (int i = 0; i < 6; ++i) b[i] = sh->rho[i];
+        for (int i = 0; i < 6; ++i) b[i] = rho[i];
         bool ok = true;
         if (approx == 1) {  // columns 0 1 3 6: beta1^2, b1 b2, b1 b3, b1 b4
             const int cols[4] = {0, 1, 3, 6};
             double A[24], x[4];
             for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 4; ++j) A[4 * i + j] = sh->L[10 * i + cols[j]];
+                for (int j = 0; j < 4; ++j) A[4 * i + j] = L[10 * i + cols[j]];
             householder_ls<6, 4>(A, b, x);
             const double sg = x[0] < 0.0 ? -1.0 : 1.0;
             be[0] = dsqrt(sg * x[0]);
@@ -1316,7 +1313,7 @@ __host__ __device__ inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, 
         } else if (approx == 2) {  // columns 0 1 2: beta1^2, b1 b2, b2^2
             double A[18], x[3];
             for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 3; ++j) A[3 * i + j] = sh->L[10 * i + j];
+                for (int j = 0; j < 3; ++j) A[3 * i + j] = L[10 * i + j];
             householder_ls<6, 3>(A, b, x);
             if (x[0] < 0.0) {
                 be[0] = dsqrt(-x[0]);
@@ -1329,7 +1326,7 @@ __host__ __device__ inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, 
         } else {  // columns 0..4: beta1^2, b1 b2, b2^2, b1 b3, b2 b3
             double A[30], x[5];
             for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 5; ++j) A[5 * i + j] = sh->L[10 * i + j];
+                for (int j = 0; j < 5; ++j) A[5 * i + j] = L[10 * i + j];
             householder_ls<6, 5>(A, b, x);
             if (x[0] < 0.0) {
                 be[0] = dsqrt(-x[0]);
@@ -1342,10 +1339,22 @@ __host__ __device__ inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, 
             ok = be[0] != 0.0;
             if (ok) be[2] = x[3] / be[0];
         }
-        if (ok) epnp_gauss_newton(sh->L, sh->rho, be);
+        if (ok) epnp_gauss_newton(L, rho, be);
         s2.valid[approx - 1] = ok;
     }
-    }
+}
+
+__host__ __device__ inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, EpnpStage2 &s2) {
+    EpnpShared shm;
+    EpnpShared *sh = &shm;
+    epnp_mtm(sh, s1.pairs, k);
+    jacobi_eig<12>(sh->A, sh->V, sh->d);
+    int o[12];
+    eig_order_desc<12>(sh->d, o);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 12; ++j) s2.ut[i][j] = sh->V[12 * j + o[11 - i]];
+    epnp_stage2_post(s1, s2);
+}
 
 // Red provides:
 //   template <int NV, class F> void sum(F f, double *out): out[q] = sum over the inliers of

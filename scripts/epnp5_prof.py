@@ -37,3 +37,17 @@ for minimal in ("p3p", "epnp5"):
     print(f"{minimal}: {H} hyps, ms per call {statistics.median(walls):.3f} (solve {statistics.median(sol):.3f}, "
           f"score {statistics.median(sco):.3f}), {H / statistics.median(walls) * 1e3:.3e} hyp/s, "
           f"inliers {int(m.sum())}", flush=True)
+# the reference's own call (main_v1.py:497-502: default flags, iterationsCount 5000, thr 30, conf 0.99),
+# adaptive with the LM final solve, in both minimal modes: ms to the best model
+for minimal, sampler in (("p3p", "philox"), ("epnp5", "opencv"), ("epnp5", "philox")):
+    walls = []
+    for i in range(reps + 2):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        R, t_, m, info = rsac.pnp_ransac(p2, p3, pr["K"], 5000, 30.0, adaptive=True, refine=True, minimal=minimal,
+                                         sampler=sampler, return_info=True)
+        torch.cuda.synchronize()
+        if i >= 2:
+            walls.append((time.perf_counter() - t) * 1e3)
+    print(f"ms-to-best {minimal}/{sampler}: {statistics.median(walls):.3f} ms, iterations {info.iters}, "
+          f"inliers {int(m.sum())}, solve {info.solve_ms:.3f} ms, score {info.score_ms:.3f} ms", flush=True)
