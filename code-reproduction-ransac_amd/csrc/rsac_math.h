@@ -1028,34 +1028,44 @@ constexpr int kEpnpPairSums = 40;  // 10 control-point pairs x 4 sums
 
 // Cyclic Jacobi of a symmetric N x N matrix (row-major, destroyed): d[k]
 // eigenvalues, V[i * N + k] the k-th eigenvector.  Fixed rotation order.
+// (N <= 4: the rotation loops unrolled, every index static, so a GPU lane keeps A and V in
+// registers; the order of operations is the same either way)
 template <int N>
 RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
+    constexpr int U = N <= 4 ? N : 1;
     for (int i = 0; i < N * N; ++i) V[i] = 0.0;
     for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
     for (int sweep = 0; sweep < 60; ++sweep) {
         double off = 0.0, diag = 0.0;
+#pragma unroll U
         for (int p = 0; p < N; ++p) {
             diag = diag + A[p * N + p] * A[p * N + p];
+#pragma unroll U
             for (int q = p + 1; q < N; ++q) off = off + A[p * N + q] * A[p * N + q];
         }
         if (!(off > 1e-32 * diag)) break;
+#pragma unroll U
         for (int p = 0; p < N - 1; ++p)
+#pragma unroll U
             for (int q = p + 1; q < N; ++q) {
                 const double apq = A[p * N + q];
                 if (apq == 0.0) continue;
                 const double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
                 const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
                 const double c = 1.0 / dsqrt(tt * tt + 1.0), sn = tt * c;
+#pragma unroll U
                 for (int k = 0; k < N; ++k) {
                     const double akp = A[k * N + p], akq = A[k * N + q];
                     A[k * N + p] = c * akp - sn * akq;
                     A[k * N + q] = sn * akp + c * akq;
                 }
+#pragma unroll U
                 for (int k = 0; k < N; ++k) {
                     const double apk = A[p * N + k], aqk = A[q * N + k];
                     A[p * N + k] = c * apk - sn * aqk;
                     A[q * N + k] = sn * apk + c * aqk;
                 }
+#pragma unroll U
                 for (int k = 0; k < N; ++k) {
                     const double vkp = V[k * N + p], vkq = V[k * N + q];
                     V[k * N + p] = c * vkp - sn * vkq;
@@ -1085,31 +1095,42 @@ RSAC_HD void eig_order_desc(const double *d, int *order) {
 // A and b are destroyed.  A vanishing pivot gives x_k = 0.
 template <int M, int N>
 RSAC_HD void householder_ls(double *A, double *b, double *x) {
+#pragma unroll
     for (int k = 0; k < N; ++k) {
         double nrm = 0.0;
+#pragma unroll
         for (int i = k; i < M; ++i) nrm = nrm + A[i * N + k] * A[i * N + k];
         nrm = dsqrt(nrm);
         if (nrm == 0.0) continue;
         const double alpha = A[k * N + k] > 0.0 ? -nrm : nrm;
         double v[M];
+#pragma unroll
         for (int i = k; i < M; ++i) v[i] = A[i * N + k];
         v[k] = v[k] - alpha;
         double vv = 0.0;
+#pragma unroll
         for (int i = k; i < M; ++i) vv = vv + v[i] * v[i];
         if (vv == 0.0) continue;
+#pragma unroll
         for (int j = k; j < N; ++j) {
             double sdot = 0.0;
+#pragma unroll
             for (int i = k; i < M; ++i) sdot = sdot + v[i] * A[i * N + j];
             const double f = 2.0 * sdot / vv;
+#pragma unroll
             for (int i = k; i < M; ++i) A[i * N + j] = A[i * N + j] - f * v[i];
         }
         double sdot = 0.0;
+#pragma unroll
         for (int i = k; i < M; ++i) sdot = sdot + v[i] * b[i];
         const double f = 2.0 * sdot / vv;
+#pragma unroll
         for (int i = k; i < M; ++i) b[i] = b[i] - f * v[i];
     }
+#pragma unroll
     for (int k = N - 1; k >= 0; --k) {
         double sacc = b[k];
+#pragma unroll
         for (int j = k + 1; j < N; ++j) sacc = sacc - A[k * N + j] * x[j];
         const double rkk = A[k * N + k];
         x[k] = dabs(rkk) > 1e-300 ? sacc / rkk : 0.0;
@@ -1189,6 +1210,7 @@ RSAC_HD void epnp_l6x10(const double *const v[4], double *L) {
 RSAC_HD void epnp_gauss_newton(const double *L, const double *rho, double *be) {
     for (int it = 0; it < 5; ++it) {
         double A[24], b[6], x[4];
+#pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double *r = L + 10 * i;
             A[4 * i + 0] = 2.0 * r[0] * be[0] + r[1] * be[1] + r[3] * be[2] + r[6] * be[3];
@@ -1293,6 +1315,7 @@ __host__ __device__ inline void epnp_stage2_post(const EpnpStage1 &s1, EpnpStage
             const double dx = f.cw[a][0] - f.cw[b][0], dy = f.cw[a][1] - f.cw[b][1], dz = f.cw[a][2] - f.cw[b][2];
             rho[q] = dx * dx + dy * dy + dz * dz;
         }
+#pragma unroll
     for (int approx = 1; approx <= 3; ++approx) {
         double *be = s2.be[approx - 1];
         for (int j = 0; j < 4; ++j) be[j] = 0.0;
@@ -1443,6 +1466,7 @@ RSAC_HD bool epnp_stage3(Red &red, const Cam &k, const EpnpStage1 &s1, const Epn
     epnp_alphas(af, p1[0], p1[1], p1[2], a1);
     double best_err = 0.0, bestR[9], bestt[3];
     bool have = false;
+#pragma unroll
     for (int approx = 0; approx < 3; ++approx) {
         if (s2.valid[approx] == 0.0) continue;
         const double *be = s2.be[approx];
@@ -1521,22 +1545,25 @@ struct MinimalEpnpReducer {
     double X[N], Y[N], Z[N], u[N], v[N];  // centred on point 0
     template <int NV, class F>
     RSAC_HD void sum(F f, double *out) {
-        double w[8][NV];
-        for (int l = 0; l < 8; ++l)
+        // only the N occupied slots are held: the butterfly's other slots stay +0.0
+        double w[N][NV];
+#pragma unroll
+        for (int l = 0; l < N; ++l)
+#pragma unroll
             for (int q = 0; q < NV; ++q) w[l][q] = 0.0;
+#pragma unroll
         for (int i = 0; i < N; ++i) f(X[i], Y[i], Z[i], u[i], v[i], w[i]);
-        for (int l = 0; l < 8; ++l)  // the butterfly's offsets 32, 16, 8: partners hold zeros
+#pragma unroll
+        for (int l = 0; l < N; ++l)  // the butterfly's offsets 32, 16, 8: partners hold zeros
+#pragma unroll
             for (int q = 0; q < NV; ++q) w[l][q] = ((w[l][q] + 0.0) + 0.0) + 0.0;
-        for (int o = 4; o > 0; o >>= 1) {
-            double x[8][NV];
-            for (int l = 0; l < 8; ++l)
-                for (int q = 0; q < NV; ++q) x[l][q] = w[l][q] + w[l ^ o][q];
-            for (int l = 0; l < 8; ++l)
-                for (int q = 0; q < NV; ++q) w[l][q] = x[l][q];
-        }
-        for (int q = 0; q < NV; ++q) {  // waves 1..7 of the block add their zero sums
-            double b = w[0][q];
-            for (int wv = 1; wv < kLmThreads / 64; ++wv) b = b + 0.0;
+        // the xor butterfly over slots 0..7 (offsets 4, 2, 1) as slot 0 receives it:
+        // ((s0 + s4) + (s2 + s6)) + ((s1 + s5) + (s3 + s7))
+        auto sl = [&](int l, int q) { return l < N ? w[l][q] : 0.0; };
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            double b = ((sl(0, q) + sl(4, q)) + (sl(2, q) + sl(6, q))) + ((sl(1, q) + sl(5, q)) + (sl(3, q) + sl(7, q)));
+            for (int wv = 1; wv < kLmThreads / 64; ++wv) b = b + 0.0;  // waves 1..7 add their zero sums
             out[q] = b;
         }
     }
