@@ -1065,9 +1065,10 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_beg
         for (int p = 0; p < 11; ++p) {
 #pragma unroll 1
             for (int q = p + 1; q < 12; ++q) {
-                const double apq = bperm_f64(A[q], g0 + p);
+                // the three reads in one round trip (app and aqq are unused when apq is 0)
+                const double apq = bperm_f64(A[q], g0 + p), app = bperm_f64(A[p], g0 + p),
+                             aqq = bperm_f64(A[q], g0 + q);
                 if (apq == 0.0) continue;
-                const double app = bperm_f64(A[p], g0 + p), aqq = bperm_f64(A[q], g0 + q);
                 const double theta = (aqq - app) / (2.0 * apq);
                 const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
                 const double cs = 1.0 / dsqrt(tt * tt + 1.0), sn = tt * cs;
