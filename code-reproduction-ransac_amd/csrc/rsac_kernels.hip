@@ -1007,21 +1007,41 @@ __device__ __forceinline__ double bperm_f64(double x, int src_lane) {
 }
 typedef double epnp_row __attribute__((ext_vector_type(16)));
 
-// 2 of 3: M^T M's eigenvectors, 16 lanes per hypothesis (4 per wave).  Lane j < 12 builds row j
-// of A (epnp_mtm's entries) and holds row j of V; a rotation (p, q) reads A[p][p], A[p][q],
-// A[q][q] from lanes p and q, updates columns p and q of every row in place (the row's own
-// elements, indexed by the wave-uniform p, q), then lanes p and q swap their updated rows and
-// form the new rows p and q: jacobi_eig<12>'s column, row and V loops element for element.  The
-// sweep test sums A's upper triangle in jacobi_eig's order.  Groups whose sweeps end early idle
-// until the wave's last group is done.
+__device__ __forceinline__ double readlane_f64(double x, int lane) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// lane src of this lane's group: G = 16 through ds_bpermute (4 groups per wave), G = 64 (one
+// group per wave) through v_readlane, a few cycles instead of an LDS round trip (the rotation
+// parameters and the sweep test; the rows are exchanged through ds_bpermute in both forms)
+template <int G>
+__device__ __forceinline__ double grp_read(double x, int g0, int src) {
+    if constexpr (G == 64)
+        return readlane_f64(x, src);
+    else
+        return bperm_f64(x, g0 + src);
+}
+
+// 2 of 3: M^T M's eigenvectors, G lanes per hypothesis (G = 16: 4 per wave, the throughput form;
+// G = 64: one per wave, the latency form for short rounds).  Lane j < 12 builds row j of A
+// (epnp_mtm's entries) and holds row j of V; a rotation (p, q) reads A[p][p], A[p][q], A[q][q]
+// from lanes p and q, updates columns p and q of every row in place (the row's own elements,
+// indexed by the wave-uniform p, q), then lanes p and q take each other's updated row and form the
+// new rows p and q: jacobi_eig<12>'s column, row and V loops element for element.  The sweep test
+// sums A's upper triangle in jacobi_eig's order.  Groups whose sweeps end early idle until the
+// wave's last group is done.
+template <int G>
 __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
-    const int lane = threadIdx.x & 63, j = lane & 15, g0 = lane & ~15;
-    const int hl = (int)((blockIdx.x * 256u + threadIdx.x) >> 4);
+    const int lane = threadIdx.x & 63, j = lane & (G - 1), g0 = lane & ~(G - 1);
+    const int hl = (int)((blockIdx.x * 256u + threadIdx.x) / G);
     const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
     double *E = a.epnp + rec * kEpnpRec;
     const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
-    bool run = hl < H && a.status[rec] > 0 && s1->ok != 0.0;
+    const bool live = hl < H && a.status[rec] > 0 && s1->ok != 0.0;
+    bool run = live;
     epnp_row A, V;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -1050,7 +1070,7 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_beg
             for (int p = 0; p < 12; ++p) {
 #pragma unroll
                 for (int q = p; q < 12; ++q) {
-                    const double x = bperm_f64(A[q], g0 + p);
+                    const double x = grp_read<G>(A[q], g0, p);
                     if (q == p)
                         diag = diag + x * x;
                     else
@@ -1066,8 +1086,8 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_beg
 #pragma unroll 1
             for (int q = p + 1; q < 12; ++q) {
                 // the three reads in one round trip (app and aqq are unused when apq is 0)
-                const double apq = bperm_f64(A[q], g0 + p), app = bperm_f64(A[p], g0 + p),
-                             aqq = bperm_f64(A[q], g0 + q);
+                const double apq = grp_read<G>(A[q], g0, p), app = grp_read<G>(A[p], g0, p),
+                             aqq = grp_read<G>(A[q], g0, q);
                 if (apq == 0.0) continue;
                 const double theta = (aqq - app) / (2.0 * apq);
                 const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
@@ -1077,12 +1097,17 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_beg
                     A[p] = cs * akp - sn * akq;
                     A[q] = sn * akp + cs * akq;
                 }
+                // the rows: lane p forms cs a - sn o, lane q sn o + cs a, o the partner's element:
+                // both as cs a + x o with x = -sn / +sn (negation exact, the sum commutes: the same
+                // bits), the partner's row through ds_bpermute (one per-lane source, no selects)
                 const int partner = g0 + (j == p ? q : p);
+                const double x = j == p ? -sn : sn;
+                const bool mine = j == p || j == q;
 #pragma unroll
                 for (int k = 0; k < 12; ++k) {
                     const double o = bperm_f64(A[k], partner);
-                    const double np = cs * A[k] - sn * o, nq = sn * o + cs * A[k];
-                    A[k] = j == p ? np : j == q ? nq : A[k];
+                    const double nv = cs * A[k] + x * o;
+                    A[k] = mine ? nv : A[k];
                 }
                 {
                     const double vkp = V[p], vkq = V[q];
@@ -1092,10 +1117,10 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_beg
             }
         }
     }
-    if (!(hl < H && a.status[rec] > 0 && s1->ok != 0.0)) return;
+    if (!live) return;
     double d[12];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) d[k] = bperm_f64(A[k], g0 + k);
+    for (int k = 0; k < 12; ++k) d[k] = grp_read<G>(A[k], g0, k);
     int o[12];
     eig_order_desc<12>(d, o);
     if (j >= 12) return;
@@ -1109,45 +1134,80 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_beg
     }
 }
 
-// 3 of 3: stage 2's rest (L, rho, the beta estimates), stage 3 (the poses, the lowest mean error),
-// the records (as k_pnp_solve_epnp5)
+// 3 of 3: stage 2's rest (L, rho, the beta estimates) and stage 3 (a pose and mean error per
+// estimate, the lowest wins), 4 lanes per hypothesis: lane c < 3 takes estimate c + 1
+// (epnp_beta, epnp_pose_err: the loop bodies of epnp_stage2_post and epnp_stage3), the group
+// then applies epnp_stage3's rule (valid, lowest error, first on ties) to the three and lane 0
+// writes the records (as k_pnp_solve_epnp5)
 __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
-    const int hl = blockIdx.x * blockDim.x + threadIdx.x;
-    if (hl >= H) return;
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int hl = gt >> 2, c = gt & 3;
+    const bool live = hl < H;
     const int64_t h = hyp_begin + hl;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
-    double *m = a.models + rec * kModelStride;
     const double *E = a.epnp + rec * kEpnpRec;
-    int8_t st = a.status[rec];
-    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
+    int8_t st = live ? a.status[rec] : -1;
+    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0}, err = 0.0, cen[3] = {0, 0, 0};
+    bool mine = false;  // this lane's estimate gave a pose
+    bool s1ok = false;
     if (st > 0) {
         const EpnpStage1 s1 = *reinterpret_cast<const EpnpStage1 *>(E);
-        bool ok = s1.ok != 0.0;
-        if (ok) {
+        s1ok = s1.ok != 0.0;
+        if (s1ok && c < 3) {
             EpnpStage2 s2;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int c = 0; c < 12; ++c) s2.ut[i][c] = E[64 + 12 * i + c];
-            epnp_stage2_post(s1, s2);
-            int32_t idx[5];
-            (void)epnp5_sample(a, rec, h, n, idx);
-            MinimalEpnpReducer<5> red;
-            double c[3];
-            epnp5_reducer(a, p0, idx, red, c);
-            const double *cm = a.cams + 4 * prob;
-            ok = epnp_stage3(red, Cam{cm[0], cm[1], cm[2], cm[3]}, s1, s2, R, t);
-            if (ok) lm_from_centred(R, c, t);
+                for (int q = 0; q < 12; ++q) s2.ut[i][q] = E[64 + 12 * i + q];
+            double L[60], rho[6], be[4];
+            epnp_l_rho(s1, s2, L, rho);
+            if (epnp_beta(c + 1, L, rho, be)) {
+                int32_t idx[5];
+                (void)epnp5_sample(a, rec, h, n, idx);
+                MinimalEpnpReducer<5> red;
+                epnp5_reducer(a, p0, idx, red, cen);
+                double p1[3], a1[4];
+                red.first(p1);
+                epnp_alphas(epnp_alpha_frame(s1.f), p1[0], p1[1], p1[2], a1);
+                const double *cm = a.cams + 4 * prob;
+                mine = epnp_pose_err(red, Cam{cm[0], cm[1], cm[2], cm[3]}, s1, s2, be, a1, R, t, err);
+            }
         }
+    }
+    // epnp_stage3's pick over the group's three lanes, in estimate order
+    const int base = threadIdx.x & ~3;
+    int win = -1;
+    double best = 0.0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        const bool ok_e = __shfl(mine ? 1 : 0, base + e) != 0;
+        const double err_e = __shfl(err, base + e);
+        if (ok_e && (win < 0 || err_e < best)) {
+            win = e;
+            best = err_e;
+        }
+    }
+    const int src = base + (win < 0 ? 0 : win);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) R[q] = __shfl(R[q], src);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) t[q] = __shfl(t[q], src);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) cen[q] = __shfl(cen[q], src);
+    if (!live || c != 0) return;
+    if (st > 0) {
+        const bool ok = s1ok && win >= 0;
+        if (ok) lm_from_centred(R, cen, t);
         st = ok ? 1 : 0;
         if (!ok)
             for (int q = 0; q < 9; ++q) R[q] = 0.0;
         if (!ok)
             for (int q = 0; q < 3; ++q) t[q] = 0.0;
     }
+    double *m = a.models + rec * kModelStride;
 #pragma unroll
     for (int q = 0; q < 9; ++q) m[q] = R[q];
 #pragma unroll
@@ -2757,12 +2817,22 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
     return hipGetLastError();
 }
 
+#ifndef RSAC_EPNP_WAVE_MAX
+#define RSAC_EPNP_WAVE_MAX 4096
+#endif
+constexpr int64_t kEpnpWaveMaxHyps = RSAC_EPNP_WAVE_MAX;  // one wave per hypothesis up to this many (A/B knob)
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
     if (a.sample_k == 5 && a.epnp) {  // the three-launch form (k_epnp5_a / _jacobi / _c)
         hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-        hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv(16 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-        hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+        // short rounds (an adaptive run's first 256 hypotheses): one wave per hypothesis, readlane
+        // exchanges (the round's latency is one hypothesis' Jacobi); longer ones 16 lanes each
+        if ((int64_t)P * H <= kEpnpWaveMaxHyps)
+            hipLaunchKernelGGL(k_epnp5_jacobi<64>, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+        else
+            hipLaunchKernelGGL(k_epnp5_jacobi<16>, dim3(cdiv(16 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin,
+                               H);
+        hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     } else if (a.sample_k == 5)
         hipLaunchKernelGGL(k_pnp_solve_epnp5, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes

@@ -1299,72 +1299,79 @@ RSAC_HD void epnp_mtm(EpnpShared *sh, const double *pairs, const Cam &k) {
         }
 }
 
-// Stage 2 after the eigen-decomposition: s2.ut (the eigenvectors of M^T M's 4 smallest
-// eigenvalues) given, the L 6x10 / rho system and the three beta estimates with Gauss-Newton.
-// (epnp_stage2 below; the GPU's minimal EPnP runs the 12 x 12 Jacobi on 16 lanes in between,
-// k_epnp5_jacobi)
-__host__ __device__ inline void epnp_stage2_post(const EpnpStage1 &s1, EpnpStage2 &s2) {
-    double L[60], rho[6];
+// One beta estimate of stage 2 (approximation 1, 2 or 3) from L and rho, polished by Gauss-Newton:
+// false if it is not usable (OpenCV epnp.cpp find_betas_approx_1..3 + gauss_newton)
+RSAC_HD bool epnp_beta(int approx, const double *L, const double *rho, double *be) {
+    for (int j = 0; j < 4; ++j) be[j] = 0.0;
+    double b[6];
+    for (int i = 0; i < 6; ++i) b[i] = rho[i];
+    bool ok = true;
+    if (approx == 1) {  // columns 0 1 3 6: beta1^2, b1 b2, b1 b3, b1 b4
+        const int cols[4] = {0, 1, 3, 6};
+        double A[24], x[4];
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 4; ++j) A[4 * i + j] = L[10 * i + cols[j]];
+        householder_ls<6, 4>(A, b, x);
+        const double sg = x[0] < 0.0 ? -1.0 : 1.0;
+        be[0] = dsqrt(sg * x[0]);
+        ok = be[0] != 0.0;
+        if (ok)
+            for (int j = 1; j < 4; ++j) be[j] = sg * x[j] / be[0];
+    } else if (approx == 2) {  // columns 0 1 2: beta1^2, b1 b2, b2^2
+        double A[18], x[3];
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 3; ++j) A[3 * i + j] = L[10 * i + j];
+        householder_ls<6, 3>(A, b, x);
+        if (x[0] < 0.0) {
+            be[0] = dsqrt(-x[0]);
+            be[1] = x[2] < 0.0 ? dsqrt(-x[2]) : 0.0;
+        } else {
+            be[0] = dsqrt(x[0]);
+            be[1] = x[2] > 0.0 ? dsqrt(x[2]) : 0.0;
+        }
+        if (x[1] < 0.0) be[0] = -be[0];
+    } else {  // columns 0..4: beta1^2, b1 b2, b2^2, b1 b3, b2 b3
+        double A[30], x[5];
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 5; ++j) A[5 * i + j] = L[10 * i + j];
+        householder_ls<6, 5>(A, b, x);
+        if (x[0] < 0.0) {
+            be[0] = dsqrt(-x[0]);
+            be[1] = x[2] < 0.0 ? dsqrt(-x[2]) : 0.0;
+        } else {
+            be[0] = dsqrt(x[0]);
+            be[1] = x[2] > 0.0 ? dsqrt(x[2]) : 0.0;
+        }
+        if (x[1] < 0.0) be[0] = -be[0];
+        ok = be[0] != 0.0;
+        if (ok) be[2] = x[3] / be[0];
+    }
+    if (ok) epnp_gauss_newton(L, rho, be);
+    return ok;
+}
+
+// L (6 x 10) from the eigenvectors and rho (the squared control-point distances)
+RSAC_HD void epnp_l_rho(const EpnpStage1 &s1, const EpnpStage2 &s2, double *L, double *rho) {
     const EpnpFrame &f = s1.f;
-    int q = 0;
     const double *vv[4] = {s2.ut[0], s2.ut[1], s2.ut[2], s2.ut[3]};
     epnp_l6x10(vv, L);
-    q = 0;
+    int q = 0;
     for (int a = 0; a < 4; ++a)
         for (int b = a + 1; b < 4; ++b, ++q) {
             const double dx = f.cw[a][0] - f.cw[b][0], dy = f.cw[a][1] - f.cw[b][1], dz = f.cw[a][2] - f.cw[b][2];
             rho[q] = dx * dx + dy * dy + dz * dz;
         }
+}
+
+// Stage 2 after the eigen-decomposition: s2.ut (the eigenvectors of M^T M's 4 smallest
+// eigenvalues) given, the L 6x10 / rho system and the three beta estimates with Gauss-Newton.
+// (epnp_stage2 below; the GPU's minimal EPnP runs the 12 x 12 Jacobi on 16 or 64 lanes in between,
+// k_epnp5_jacobi, and the three estimates on three lanes, k_epnp5_c)
+__host__ __device__ inline void epnp_stage2_post(const EpnpStage1 &s1, EpnpStage2 &s2) {
+    double L[60], rho[6];
+    epnp_l_rho(s1, s2, L, rho);
 #pragma unroll
-    for (int approx = 1; approx <= 3; ++approx) {
-        double *be = s2.be[approx - 1];
-        for (int j = 0; j < 4; ++j) be[j] = 0.0;
-        double b[6];
-        for (int i = 0; i < 6; ++i) b[i] = rho[i];
-        bool ok = true;
-        if (approx == 1) {  // columns 0 1 3 6: beta1^2, b1 b2, b1 b3, b1 b4
-            const int cols[4] = {0, 1, 3, 6};
-            double A[24], x[4];
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 4; ++j) A[4 * i + j] = L[10 * i + cols[j]];
-            householder_ls<6, 4>(A, b, x);
-            const double sg = x[0] < 0.0 ? -1.0 : 1.0;
-            be[0] = dsqrt(sg * x[0]);
-            ok = be[0] != 0.0;
-            if (ok)
-                for (int j = 1; j < 4; ++j) be[j] = sg * x[j] / be[0];
-        } else if (approx == 2) {  // columns 0 1 2: beta1^2, b1 b2, b2^2
-            double A[18], x[3];
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 3; ++j) A[3 * i + j] = L[10 * i + j];
-            householder_ls<6, 3>(A, b, x);
-            if (x[0] < 0.0) {
-                be[0] = dsqrt(-x[0]);
-                be[1] = x[2] < 0.0 ? dsqrt(-x[2]) : 0.0;
-            } else {
-                be[0] = dsqrt(x[0]);
-                be[1] = x[2] > 0.0 ? dsqrt(x[2]) : 0.0;
-            }
-            if (x[1] < 0.0) be[0] = -be[0];
-        } else {  // columns 0..4: beta1^2, b1 b2, b2^2, b1 b3, b2 b3
-            double A[30], x[5];
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 5; ++j) A[5 * i + j] = L[10 * i + j];
-            householder_ls<6, 5>(A, b, x);
-            if (x[0] < 0.0) {
-                be[0] = dsqrt(-x[0]);
-                be[1] = x[2] < 0.0 ? dsqrt(-x[2]) : 0.0;
-            } else {
-                be[0] = dsqrt(x[0]);
-                be[1] = x[2] > 0.0 ? dsqrt(x[2]) : 0.0;
-            }
-            if (x[1] < 0.0) be[0] = -be[0];
-            ok = be[0] != 0.0;
-            if (ok) be[2] = x[3] / be[0];
-        }
-        if (ok) epnp_gauss_newton(L, rho, be);
-        s2.valid[approx - 1] = ok;
-    }
+    for (int approx = 1; approx <= 3; ++approx) s2.valid[approx - 1] = epnp_beta(approx, L, rho, s2.be[approx - 1]);
 }
 
 __host__ __device__ inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, EpnpStage2 &s2) {
@@ -1452,15 +1459,63 @@ RSAC_HD void epnp_stage1(Red &red, const Cam &k, EpnpStage1 &s1) {
     s1.ok = 1.0;
 }
 
-// Stage 3 (O(n) sums): for each valid beta estimate, the camera-frame control points (sign from
-// the first inlier's depth), the pose by SVD of the centred cross-covariance, the mean
-// reprojection error; the lowest wins.  (R, t) in the centred frame; false if none.
+// Stage 3 for one beta estimate: the camera-frame control points (sign from the first inlier's
+// depth a1), the pose by SVD of the centred cross-covariance, the mean reprojection error.
+// false when the cross-covariance is degenerate.
 template <class Red>
-RSAC_HD bool epnp_stage3(Red &red, const Cam &k, const EpnpStage1 &s1, const EpnpStage2 &s2, double *R_out,
-                         double *t_out) {
+RSAC_HD bool epnp_pose_err(Red &red, const Cam &k, const EpnpStage1 &s1, const EpnpStage2 &s2, const double *be,
+                           const double (&a1)[4], double (&Rk)[9], double (&tk)[3], double &err) {
     const double n = s1.n;
     const EpnpAlpha af = epnp_alpha_frame(s1.f);
     const double c0x = s1.f.cw[0][0], c0y = s1.f.cw[0][1], c0z = s1.f.cw[0][2];
+    double cc[4][3];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 3; ++j)
+            cc[i][j] = be[0] * s2.ut[0][3 * i + j] + be[1] * s2.ut[1][3 * i + j] + be[2] * s2.ut[2][3 * i + j] +
+                       be[3] * s2.ut[3][3 * i + j];
+    const double z1 = a1[0] * cc[0][2] + a1[1] * cc[1][2] + a1[2] * cc[2][2] + a1[3] * cc[3][2];
+    if (z1 < 0.0)
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 3; ++j) cc[i][j] = -cc[i][j];
+    double pc0[3];
+    red.template sum<3>([=](double X, double Y, double Z, double, double, double *acc) {
+        double a[4];
+        epnp_alphas(af, X, Y, Z, a);
+        for (int j = 0; j < 3; ++j) acc[j] += a[0] * cc[0][j] + a[1] * cc[1][j] + a[2] * cc[2][j] + a[3] * cc[3][j];
+    }, pc0);
+    for (int j = 0; j < 3; ++j) pc0[j] = pc0[j] / n;
+    double H[9];
+    red.template sum<9>([=](double X, double Y, double Z, double, double, double *acc) {
+        double a[4], pc[3];
+        epnp_alphas(af, X, Y, Z, a);
+        for (int j = 0; j < 3; ++j)
+            pc[j] = a[0] * cc[0][j] + a[1] * cc[1][j] + a[2] * cc[2][j] + a[3] * cc[3][j] - pc0[j];
+        const double pw[3] = {X - c0x, Y - c0y, Z - c0z};
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) acc[3 * i + j] += pc[i] * pw[j];
+    }, H);
+    if (!epnp_rotation(H, Rk)) return false;
+    for (int i = 0; i < 3; ++i) tk[i] = pc0[i] - (Rk[3 * i] * c0x + Rk[3 * i + 1] * c0y + Rk[3 * i + 2] * c0z);
+    double es;
+    const double R0 = Rk[0], R1 = Rk[1], R2 = Rk[2], R3 = Rk[3], R4 = Rk[4], R5 = Rk[5], R6 = Rk[6], R7 = Rk[7],
+                 R8 = Rk[8], t0 = tk[0], t1 = tk[1], t2 = tk[2];
+    red.template sum<1>([=](double X, double Y, double Z, double u, double v, double *acc) {
+        const double x = R0 * X + R1 * Y + R2 * Z + t0;
+        const double y = R3 * X + R4 * Y + R5 * Z + t1;
+        const double iz = 1.0 / (R6 * X + R7 * Y + R8 * Z + t2);
+        const double du = u - (k.cx + k.fx * x * iz), dv = v - (k.cy + k.fy * y * iz);
+        acc[0] += dsqrt(du * du + dv * dv);
+    }, &es);
+    err = es / n;
+    return true;
+}
+
+// Stage 3 (O(n) sums): for each valid beta estimate its pose and mean reprojection error
+// (epnp_pose_err); the lowest wins, the first on ties.  (R, t) in the centred frame; false if none.
+template <class Red>
+RSAC_HD bool epnp_stage3(Red &red, const Cam &k, const EpnpStage1 &s1, const EpnpStage2 &s2, double *R_out,
+                         double *t_out) {
+    const EpnpAlpha af = epnp_alpha_frame(s1.f);
     double p1[3], a1[4];
     if (!red.first(p1)) return false;
     epnp_alphas(af, p1[0], p1[1], p1[2], a1);
@@ -1469,45 +1524,8 @@ RSAC_HD bool epnp_stage3(Red &red, const Cam &k, const EpnpStage1 &s1, const Epn
 #pragma unroll
     for (int approx = 0; approx < 3; ++approx) {
         if (s2.valid[approx] == 0.0) continue;
-        const double *be = s2.be[approx];
-        double cc[4][3];
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 3; ++j)
-                cc[i][j] = be[0] * s2.ut[0][3 * i + j] + be[1] * s2.ut[1][3 * i + j] + be[2] * s2.ut[2][3 * i + j] +
-                           be[3] * s2.ut[3][3 * i + j];
-        const double z1 = a1[0] * cc[0][2] + a1[1] * cc[1][2] + a1[2] * cc[2][2] + a1[3] * cc[3][2];
-        if (z1 < 0.0)
-            for (int i = 0; i < 4; ++i)
-                for (int j = 0; j < 3; ++j) cc[i][j] = -cc[i][j];
-        double pc0[3];
-        red.template sum<3>([=](double X, double Y, double Z, double, double, double *acc) {
-            double a[4];
-            epnp_alphas(af, X, Y, Z, a);
-            for (int j = 0; j < 3; ++j) acc[j] += a[0] * cc[0][j] + a[1] * cc[1][j] + a[2] * cc[2][j] + a[3] * cc[3][j];
-        }, pc0);
-        for (int j = 0; j < 3; ++j) pc0[j] = pc0[j] / n;
-        double H[9];
-        red.template sum<9>([=](double X, double Y, double Z, double, double, double *acc) {
-            double a[4], pc[3];
-            epnp_alphas(af, X, Y, Z, a);
-            for (int j = 0; j < 3; ++j)
-                pc[j] = a[0] * cc[0][j] + a[1] * cc[1][j] + a[2] * cc[2][j] + a[3] * cc[3][j] - pc0[j];
-            const double pw[3] = {X - c0x, Y - c0y, Z - c0z};
-            for (int i = 0; i < 3; ++i)
-                for (int j = 0; j < 3; ++j) acc[3 * i + j] += pc[i] * pw[j];
-        }, H);
-        double Rk[9], tk[3];
-        if (!epnp_rotation(H, Rk)) continue;
-        for (int i = 0; i < 3; ++i) tk[i] = pc0[i] - (Rk[3 * i] * c0x + Rk[3 * i + 1] * c0y + Rk[3 * i + 2] * c0z);
-        double es;
-        red.template sum<1>([=](double X, double Y, double Z, double u, double v, double *acc) {
-            const double x = Rk[0] * X + Rk[1] * Y + Rk[2] * Z + tk[0];
-            const double y = Rk[3] * X + Rk[4] * Y + Rk[5] * Z + tk[1];
-            const double iz = 1.0 / (Rk[6] * X + Rk[7] * Y + Rk[8] * Z + tk[2]);
-            const double du = u - (k.cx + k.fx * x * iz), dv = v - (k.cy + k.fy * y * iz);
-            acc[0] += dsqrt(du * du + dv * dv);
-        }, &es);
-        const double err = es / n;
+        double Rk[9], tk[3], err;
+        if (!epnp_pose_err(red, k, s1, s2, s2.be[approx], a1, Rk, tk, err)) continue;
         if (!have || err < best_err) {
             have = true;
             best_err = err;
