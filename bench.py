@@ -481,6 +481,35 @@ def extra_workloads(local, args):
         fin[str(mode).lower()] = statistics.median(walls)
     out["final_solve_ms_to_best"] = dict(fin, note="pnp_ransac wall time, adaptive, C2 problem; refine=False/lm/"
                                                     "epnp (solvePnPRansac's final solve after SOLVEPNP_P3P)/epnp+lm")
+    # the reference call's own mode on the C2 problem (main_v1.py:497-502: no flags = EPnP on 5-point
+    # MWC samples, iterationsCount 5000, thr 30, conf 0.99, then the LM final solve): ms to the best
+    # model, and the EPnP-5 minimal solver's throughput at a fixed 20k-hypothesis budget
+    walls = []
+    for i in range(12):
+        t = time.perf_counter()
+        _, _, mr, infr = rsac.pnp_ransac(g2, g3, p2c["K"], 5000, args.thr, sampler="opencv", minimal="epnp5",
+                                         refine=True, return_info=True, device=local)
+        torch.cuda.synchronize()
+        if i >= 2:
+            walls.append((time.perf_counter() - t) * 1e3)
+    walls_f, sol_f = [], []
+    for i in range(5):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        _, _, _, inff = rsac.pnp_ransac(g2, g3, p2c["K"], 20_000, args.thr, minimal="epnp5", adaptive=False,
+                                        refine=False, return_info=True, device=local)
+        torch.cuda.synchronize()
+        if i >= 1:
+            walls_f.append(time.perf_counter() - t)
+            sol_f.append(inff.solve_ms)
+    out["c2_reference_mode"] = {"points": args.points, "ms_to_best": statistics.median(walls), "iters": infr.iters,
+                                "n_inliers": infr.n_inliers, "epnp5_fixed_hyps": 20_000,
+                                "epnp5_fixed_hyp_s": 20_000 / statistics.median(walls_f),
+                                "epnp5_solve_ms": statistics.median(sol_f),
+                                "note": "cv2.solvePnPRansac defaults (EPnP-5 minimal solver on MWC subsets, LM final "
+                                        "solve) on the C2 problem, inputs in HBM, median of 10; the EPnP-5 solve "
+                                        "runs as k_epnp5_a / k_epnp5_jacobi / k_epnp5_c; CPU leg in "
+                                        "cpu_baseline.c2_reference_mode"}
     # C1 (BASELINE.json configs[0], the reference plumbing): the reference call's own mode on its 12
     # testpro-K points under main_v1's K -- solvePnPRansac defaults (EPnP-5, MWC subsets, LM final
     # solve), 1000 iterations cap, thr 30; host arrays in and out, as the reference passes them
@@ -614,6 +643,9 @@ def cpu_baseline(pr, args):
     n_all = 500 * aff
     rate_all, w_all = _median_rate(lambda: O.pnp_hypotheses_mt(soa, cam, args.thr, 0x5EED, n_all, threads=aff), n_all)
     _, w_best = _median_rate(lambda: O.pnp_ransac_seq(pr["points3d"], pr["points2d"], pr["K"], args.thr, 0.99, 5000), 1)
+    # the reference call's own mode on the same problem (EPnP-5 on MWC subsets, main_v1.py:497-502)
+    _, w_ref = _median_rate(lambda: O.pnp_ransac_seq(pr["points3d"], pr["points2d"], pr["K"], args.thr, 0.99, 5000,
+                                                     sampler="opencv", minimal="epnp5"), 1)
     # C1 (BASELINE.json configs[0]): the 12 testpro-K points (testpro-K.py:198-225) under main_v1's K
     # (main_v1.py:870-883), 1000 iterations, thr 30, the reference call's own mode (no flags:
     # EPnP on 5-point MWC samples, testpro-K.py:72 / main_v1.py:497)
@@ -664,6 +696,10 @@ def cpu_baseline(pr, args):
             "c2_ms_to_best": {"ms": w_best * 1e3, "cores": 1,
                               "sample": "OpenCV's sequential loop (orc_pnp_ransac_seq), stops at the iteration "
                                         "bound, no refit, median of 5"},
+            "c2_reference_mode": {"ms_to_best": w_ref * 1e3, "cores": 1,
+                                  "sample": "orc_pnp_ransac_seq with EPnP-5 on MWC subsets (the reference call's "
+                                            "defaults) on the C2 problem, stops at the iteration bound, no refit, "
+                                            "median of 5"},
             "c1": {"ms_c": w_c1 * 1e3, "ms_numpy": w_c1n * 1e3, "cores": 1, "iters": c1["iters"],
                    "best": c1["best"], "n_inliers": c1["n_inliers"],
                    "inliers": [int(i) for i in np.flatnonzero(c1["mask"])],
