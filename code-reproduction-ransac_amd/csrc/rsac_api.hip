@@ -13,6 +13,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <string>
 #include <thread>
@@ -898,6 +899,17 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
              const double *K, int32_t n_iters, double thr, double conf, uint64_t seed, uint32_t flags, double *R_out,
              double *t_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out, rsac_stats *stats,
              hipStream_t s, rsac_scan_state *first_round = nullptr, double *rows_dev = nullptr) {
+    // RSAC_DBG_PHASES=1: the host-side phases of every call on stderr (microseconds; a diagnostic)
+    static const bool dbg_phases = [] {
+        const char *e = getenv("RSAC_DBG_PHASES");
+        return e && e[0] == '1';
+    }();
+    using dbg_clock = std::chrono::steady_clock;
+    dbg_clock::time_point tp[6];
+    auto mark = [&](int i) {
+        if (dbg_phases) tp[i] = dbg_clock::now();
+    };
+    mark(0);
     int r = check_device(c);
     if (r) return r;
     if (P <= 0 || !K) return fail(RSAC_EINVAL, "bad problem count or K");
@@ -936,6 +948,7 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     }
     LoopOut lo;
     lo.timing = stats != nullptr || c->timing;
+    mark(1);
     // first-round mode (rsac_pnp_ransac_first_round): the loop stops after its first round when
     // that round did not end the scan; the caller continues from the exported scan state
     auto more = [&]() -> int {
@@ -964,9 +977,11 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
                  first_round ? 1 : 0);
     if (r) return r;
     if (first_round && !spec && !lo.scan[0].done) return more();
+    mark(2);
     const bool refit = (flags & (RSAC_F_REFINE | RSAC_F_EPNP)) != 0;
     r = pnp_finish(c, st, a, lo, stride, K, mask_out, flags, s, refit, lo.spec_pending);
     if (r) return r;
+    mark(3);
     if (lo.spec_pending) {
         bool ok = false;
         r = spec_resolve(c, st, lo, a.sample_k, conf, ok, spec_fixed, stride, s);
@@ -991,6 +1006,7 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         }
     }
 
+    mark(4);
     const double *bm = c->h_bestmodels.as<double>();
     for (int p = 0; p < P; ++p) {
         const bool ok = lo.scan[p].best >= 0;
@@ -1038,6 +1054,12 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         stats->solve_ms = lo.solve_ms;
         stats->score_ms = lo.score_ms;
         stats->lo_improvements = lo.lo_improvements;
+    }
+    mark(5);
+    if (dbg_phases) {
+        auto us = [&](int i, int j) { return std::chrono::duration<double, std::micro>(tp[j] - tp[i]).count(); };
+        fprintf(stderr, "rsac phases (us): setup %.1f loop %.1f finish %.1f resolve %.1f out %.1f total %.1f\n",
+                us(0, 1), us(1, 2), us(2, 3), us(3, 4), us(4, 5), us(0, 5));
     }
     return any ? RSAC_OK : RSAC_NO_MODEL;
 }
