@@ -54,6 +54,8 @@ struct Mwc {
 void mwc_subsets(Mwc &rng, int n, int64_t H, const float *const *hom, int32_t *out, int8_t *status, int k = 4);
 
 int update_num_iters(double p, double ep, int model_points, int max_iters);
+// update_num_iters(p, (n - c) / n, ...) through a per-thread table of its pow and logs (the scan replays)
+int update_num_iters_count(double p, int n, int c, int model_points, int max_iters);
 
 struct ScanState {
     int64_t niters = 1;

@@ -60,6 +60,37 @@ int update_num_iters(double p, double ep, int model_points, int max_iters) {
     return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)lrint(num / denom);
 }
 
+// update_num_iters(p, (n - c) / n, model_points, max_iters) with its pow and logs (~47 ns) kept in
+// a per-thread direct-mapped table keyed by (p, n, c, model_points): the same num and denom, so
+// the same result; the scan replays of a batched call (C3: ~1500 updates over 1024 problems of
+// equal size) see few distinct counts
+int update_num_iters_count(double p, int n, int c, int model_points, int max_iters) {
+    struct Entry {
+        double p = -1.0, num = 0.0, denom = 0.0;
+        int n = -1, c = -1, mp = -1;
+        bool zero = false;  // denom < DBL_MIN: the result is 0
+    };
+    static thread_local Entry table[1024];
+    if (model_points <= 0) return -1;
+    Entry &e = table[((unsigned)c * 2654435761u ^ (unsigned)n * 40503u ^ (unsigned)model_points) & 1023u];
+    if (!(e.p == p && e.n == n && e.c == c && e.mp == model_points)) {
+        double pc = p > 0. ? p : 0.; pc = pc < 1. ? pc : 1.;
+        double ep = (double)(n - c) / n;
+        ep = ep > 0. ? ep : 0.; ep = ep < 1. ? ep : 1.;
+        double num = 1. - pc;
+        if (num < DBL_MIN) num = DBL_MIN;
+        double denom = 1. - pow(1. - ep, model_points);
+        e.p = p; e.n = n; e.c = c; e.mp = model_points;
+        e.zero = denom < DBL_MIN;
+        if (!e.zero) {
+            e.num = log(num);
+            e.denom = log(denom);
+        }
+    }
+    if (e.zero) return 0;
+    return (e.denom >= 0 || -e.num >= max_iters * (-e.denom)) ? max_iters : (int)lrint(e.num / e.denom);
+}
+
 void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_t count, int n, int model_points,
                double confidence, bool stop_on_improve) {
     if (s.done) return;
@@ -103,7 +134,7 @@ void scan_records(ScanState &s, const int32_t *idx, const int32_t *cnt, int nrec
         if (cnt[r] <= std::max(s.max_good, model_points - 1)) continue;  // below a raised floor (LO)
         s.best = pos;
         s.max_good = cnt[r];
-        s.niters = update_num_iters(confidence, (double)(n - cnt[r]) / n, model_points, (int)s.niters);
+        s.niters = update_num_iters_count(confidence, n, cnt[r], model_points, (int)s.niters);
         cur = pos + 1;
         if (stop_on_improve) {
             s.improved = true;
