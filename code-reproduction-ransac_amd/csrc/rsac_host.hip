@@ -106,7 +106,7 @@ void scan_step(ScanState &s, const int32_t *counts, const int8_t *status, int64_
         if (c > floor_c) {
             s.best = i;
             s.max_good = c;
-            s.niters = update_num_iters(confidence, (double)(n - c) / n, model_points, (int)s.niters);
+            s.niters = update_num_iters_count(confidence, n, c, model_points, (int)s.niters);
             if (stop_on_improve) {
                 s.improved = true;
                 ++i;
