@@ -2575,117 +2575,101 @@ __global__ __launch_bounds__(1024) void k_scan_records_blk(const int32_t *__rest
                                                            const int8_t *__restrict__ status, int64_t stride,
                                                            int32_t H, int model_points, ScanRecords *__restrict__ out,
                                                            ScanDecide dec) {
+    // wave w takes the contiguous segment [w S, (w + 1) S) and walks it 64 hypotheses a step,
+    // lane l reading hypothesis step + l (coalesced): pass 1 its first status < 0 and the largest
+    // valid count before it; pass 2, from the floor the earlier segments leave, the strict prefix
+    // maxima (a step with no count above the floor costs one compare and one ballot)
     __shared__ int32_t ridx[kScanRecs], rcnt[kScanRecs];
-    __shared__ int32_t wv[16], wv2[16];
-    __shared__ int32_t s_first_neg;
+    __shared__ int32_t widx[16][kScanRecs], wcnt[16][kScanRecs];
+    __shared__ int32_t wmx[16], wng[16], wnr[16];
     const int prob = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int32_t *c = counts + (int64_t)prob * stride;
     const int8_t *st = status + (int64_t)prob * stride;
-    const int L = (H + 1023) / 1024, i0 = min(H, t * L), i1 = min(H, i0 + L);
-    // pass 1: the range's first status < 0 and its maximum count before it
+    const int S = ((H + 15) / 16 + 63) & ~63;
+    const int s0 = min(H, wave * S), s1 = min(H, s0 + S);
+    // pass 1 (8 steps' loads in flight at a time)
+    constexpr int U = 8;
     int lneg = H, lmax = -1;
-    for (int b = i0; b < i1 && lneg == H; b += 8) {
-        int8_t sv[8];
-        int32_t cv[8];
+    for (int b0 = s0; b0 < s1 && lneg == H; b0 += 64 * U) {
+        int8_t sv[U];
+        int32_t cv[U];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int i = b + k;
-            sv[k] = i < i1 ? st[i] : (int8_t)0;
-            cv[k] = i < i1 ? c[i] : -1;
+        for (int u = 0; u < U; ++u) {
+            const int i = b0 + 64 * u + lane;
+            sv[u] = i < s1 ? st[i] : (int8_t)0;
+            cv[u] = i < s1 ? c[i] : -1;
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int u = 0; u < U; ++u) {
             if (lneg != H) break;
-            if (sv[k] < 0) lneg = b + k;
-            else if (sv[k] > 0) lmax = max(lmax, cv[k]);
+            const unsigned long long neg = __ballot(sv[u] < 0);
+            const int f = neg ? (int)__builtin_ctzll(neg) : 64;
+            if (sv[u] > 0 && lane < f) lmax = max(lmax, cv[u]);
+            if (neg) lneg = b0 + 64 * u + f;
         }
     }
-    // block min of lneg
-    int m = lneg;
-    for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
-    if (lane == 0) wv[wave] = m;
-    if (t == 0) s_first_neg = H;
-    __syncthreads();
-    if (t == 0) {
-        int f = H;
-        for (int w = 0; w < 16; ++w) f = min(f, wv[w]);
-        s_first_neg = f;
+    for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, __shfl_xor(lmax, o));
+    if (lane == 0) {
+        wmx[wave] = lmax;
+        wng[wave] = lneg;
     }
     __syncthreads();
-    const int first_neg = s_first_neg;
-    if (i0 > first_neg) lmax = -1;  // ranges past the first status < 0 take no part
-    // exclusive prefix maximum of the ranges' maxima, from the floor
-    int inc = lmax;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(inc, o);
-        if (lane >= o) inc = max(inc, u);
-    }
-    __syncthreads();
-    if (lane == 63) wv[wave] = inc;
-    __syncthreads();
-    int wpre = model_points - 1;
-    for (int w = 0; w < wave; ++w) wpre = max(wpre, wv[w]);
-    int ex = __shfl_up(inc, 1);
-    int floor_c = max(wpre, lane > 0 ? ex : -1);
-    // pass 2: the range's records (strict prefix maxima above its floor), counted, then placed
-    const int lim = min(i1, first_neg);
-    // the range's valid counts, 8 loads in flight at a time (-1: status <= 0 or past lim)
-    auto chunk8 = [&](int b, int32_t (&v)[8]) __attribute__((always_inline)) {
-        int8_t sv[8];
+    int first_neg = H, floor_c = model_points - 1;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            sv[k] = b + k < lim ? st[b + k] : (int8_t)0;
-            v[k] = b + k < lim ? c[b + k] : -1;
+    for (int w = 0; w < 16; ++w) first_neg = min(first_neg, wng[w]);
+    for (int w = 0; w < wave; ++w)
+        if (w * S < first_neg) floor_c = max(floor_c, wmx[w]);  // segments from the first status < 0 on take no part
+    // pass 2
+    const int lim = min(s1, first_neg);
+    int nr = 0, f = floor_c;
+    for (int b0 = s0; b0 < lim; b0 += 64 * U) {
+        int32_t vv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b0 + 64 * u + lane;
+            const int8_t sv = i < lim ? st[i] : (int8_t)0;
+            const int32_t cv = i < lim ? c[i] : -1;
+            vv[u] = sv > 0 ? cv : -1;
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = sv[k] > 0 ? v[k] : -1;
-    };
-    int nr = 0;
-    {
-        int f = floor_c;
-        for (int b = i0; b < lim; b += 8) {
-            int32_t v[8];
-            chunk8(b, v);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (v[k] > f) {
-                    f = v[k];
-                    ++nr;
+        for (int u = 0; u < U; ++u) {
+            const int i = b0 + 64 * u + lane;
+            const int32_t v = vv[u];
+            if (__ballot(v > f) == 0) continue;
+            int pm = v;  // inclusive prefix maximum over the step's lanes
+            for (int o = 1; o < 64; o <<= 1) {
+                const int up = __shfl_up(pm, o);
+                if (lane >= o) pm = max(pm, up);
+            }
+            int ex = __shfl_up(pm, 1);
+            if (lane == 0) ex = -1;
+            unsigned long long rec = __ballot(v > f && v > ex);
+            while (rec) {
+                const int r = (int)__builtin_ctzll(rec);
+                rec &= rec - 1;
+                if (nr < kScanRecs && lane == r) {
+                    widx[wave][nr] = i;
+                    wcnt[wave][nr] = v;
                 }
+                ++nr;
+            }
+            f = max(f, __shfl(pm, 63));
         }
     }
-    int pre = nr;  // inclusive prefix sum of the record counts
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(pre, o);
-        if (lane >= o) pre += u;
-    }
-    if (lane == 63) wv2[wave] = pre;
-    __syncthreads();
-    int base = pre - nr;
-    int total = 0;
-    for (int w = 0; w < 16; ++w) {
-        if (w < wave) base += wv2[w];
-        total += wv2[w];
-    }
-    if (nr && base < kScanRecs) {
-        int f = floor_c, r = base;
-        for (int b = i0; b < lim && r < kScanRecs; b += 8) {
-            int32_t v[8];
-            chunk8(b, v);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (v[k] > f) {
-                    f = v[k];
-                    if (r < kScanRecs) {
-                        ridx[r] = b + k;
-                        rcnt[r] = f;
-                    }
-                    ++r;
-                }
-        }
-    }
+    if (lane == 0) wnr[wave] = nr;
     __syncthreads();
     if (wave != 0) return;
+    int total = 0;
+    for (int w = 0; w < 16; ++w) {  // the segments' records in order
+        const int nw = wnr[w];
+        if (lane < nw && lane < kScanRecs && total + lane < kScanRecs) {
+            ridx[total + lane] = widx[w][lane];
+            rcnt[total + lane] = wcnt[w][lane];
+        }
+        total += nw;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     ScanRecords &o = out[prob];
     if (lane == 0) {
         o.nrec = total <= kScanRecs ? total : -1;
