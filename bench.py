@@ -450,7 +450,7 @@ def extra_workloads(local, args):
                              "solve_ms": info4.solve_ms,
                              "roofline": sec_roofline("c4", "k_fm_score_q<8>", info4.score_ms,
                                                       "HIP events around the scoring launch (rsac_stats score_ms)"),
-                             "roofline_solve": sec_roofline("c4", "k_fm_solve", info4.solve_ms,
+                             "roofline_solve": sec_roofline("c4", "k_fm_solve_g8", info4.solve_ms,
                                                             "HIP events around the solve launch (rsac_stats solve_ms)"),
                              "note": "8-point + Sampson (f64), inputs in HBM, fixed budget (adaptive off)"}
     lp = synth.location_problem(seed=0)
