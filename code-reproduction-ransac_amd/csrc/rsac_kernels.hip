@@ -2524,28 +2524,43 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
     int floor_c = model_points - 1;  // the scan's floor: max(s - 1, best count so far)
     int nrec = 0, first_neg = H;
     ScanRecords &o = out[prob];
-    for (int b = 0; b < H; b += 64) {
-        const int i = b + lane;
-        const int8_t sv = i < H ? st[i] : (int8_t)0;
-        const uint64_t neg = __ballot(sv < 0);
-        const int lim = neg ? b + __builtin_ctzll(neg) : H;  // hypotheses before the first status < 0
-        int v = (i < lim && sv > 0) ? c[i] : -1;
-        // candidates: above the floor; take them in order, each raising the floor
-        uint64_t cand = __ballot(v > floor_c);
-        while (cand) {
-            const int l = __builtin_ctzll(cand);
-            const int cv = __shfl(v, l);
-            if (nrec < kScanRecs && lane == 0) {
-                ridx[nrec] = b + l;
-                rcnt[nrec] = cv;
-            }
-            ++nrec;
-            floor_c = cv;
-            cand = __ballot(v > floor_c && lane > l);
+    // 8 steps' loads in flight at a time (one step's round trip each was the kernel's time)
+    constexpr int U = 8;
+    bool stop = false;
+    for (int b0 = 0; b0 < H && !stop; b0 += 64 * U) {
+        int8_t svs[U];
+        int32_t cvs[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b0 + 64 * u + lane;
+            svs[u] = i < H ? st[i] : (int8_t)0;
+            cvs[u] = i < H ? c[i] : -1;
         }
-        if (neg) {
-            first_neg = lim;
-            break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (stop) break;
+            const int b = b0 + 64 * u, i = b + lane;
+            const int8_t sv = svs[u];
+            const uint64_t neg = __ballot(sv < 0);
+            const int lim = neg ? b + __builtin_ctzll(neg) : H;  // hypotheses before the first status < 0
+            int v = (i < lim && sv > 0) ? cvs[u] : -1;
+            // candidates: above the floor; take them in order, each raising the floor
+            uint64_t cand = __ballot(v > floor_c);
+            while (cand) {
+                const int l = __builtin_ctzll(cand);
+                const int cv = __shfl(v, l);
+                if (nrec < kScanRecs && lane == 0) {
+                    ridx[nrec] = b + l;
+                    rcnt[nrec] = cv;
+                }
+                ++nrec;
+                floor_c = cv;
+                cand = __ballot(v > floor_c && lane > l);
+            }
+            if (neg) {
+                first_neg = lim;
+                stop = true;
+            }
         }
     }
     if (lane == 0) {
