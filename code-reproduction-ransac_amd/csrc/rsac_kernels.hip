@@ -999,59 +999,118 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
     *reinterpret_cast<EpnpStage1 *>(a.epnp + rec * kEpnpRec) = s1;
 }
 
-__device__ __forceinline__ double bperm_f64(double x, int src_lane) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, x);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)u);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)(u >> 32));
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+// 2 of 3: M^T M's eigenvectors by the round-robin Jacobi of jacobi_eig_rr<12>, 16 lanes per
+// hypothesis (4 per wave).  Lane j < 12 builds row j of A (epnp_mtm's entries) and holds rows j
+// of A and V in registers; the group's A is mirrored row by row in LDS (the step-start matrix
+// after every step), where each lane reads its pair's A[p][p], A[q][q], A[p][q] and, after the
+// column phase, its partner's row.  A step (static r, every pair's indices compile-time constants):
+//   params:  both lanes of pair (p, q) form its cs, sn from the step-start matrix (the same
+//            operations, so the same bits); lane p posts them (cs = 0: pair skipped, apq = 0);
+//   columns: every lane rotates its elements (p_i, q_i) of A and of V for the 6 pairs;
+//   rows:    lanes p and q exchange their column-rotated rows through LDS and form
+//            cs a + x o (x = -sn on lane p, +sn on lane q: jacobi_eig_rr's cs a - sn o and
+//            sn o + cs a, the same bits).
+// A sweep is 11 steps instead of 66 dependent rotations; the sweep test reads the upper triangle
+// from LDS in jacobi_eig_rr's order.  Groups whose sweeps end early idle until the wave's last
+// group is done.
+constexpr int kEpG = 16;  // lanes per hypothesis
+struct EpnpJacLds {
+    double A[256 / kEpG][12 * 12];
+    double cs[256 / kEpG][12];  // pair i: cs at 2i (0: skipped), sn at 2i + 1
+};
+RSAC_HD constexpr int jrr_p(int r, int i) {
+    return jrr_pos(12, r, i) < jrr_pos(12, r, 11 - i) ? jrr_pos(12, r, i) : jrr_pos(12, r, 11 - i);
 }
-typedef double epnp_row __attribute__((ext_vector_type(16)));
+RSAC_HD constexpr int jrr_q(int r, int i) {
+    return jrr_pos(12, r, i) < jrr_pos(12, r, 11 - i) ? jrr_pos(12, r, 11 - i) : jrr_pos(12, r, i);
+}
+__device__ __forceinline__ void ep_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <int R>
+__device__ __forceinline__ void epnp_rr_step(int j, double (&A)[12], double (&V)[12], double *LA, double *LC) {
+    // this lane's position, its partner, its pair
+    const int m = j == 0 ? 0 : (j - 1 - R + 11) % 11 + 1;
+    const int mo = 11 - m;
+    const int o = mo == 0 ? 0 : 1 + (mo - 1 + R) % 11;
+    const int pi = m < mo ? m : mo;
+    const int p = j < o ? j : o, q = j < o ? o : j;
+    const double app = LA[13 * p], aqq = LA[13 * q], apq = LA[12 * p + q];
+    const bool act = apq != 0.0;
+    double cs = 0.0, sn = 0.0;
+    if (act) {
+        const double theta = (aqq - app) / (2.0 * apq);
+        const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
+        cs = 1.0 / dsqrt(tt * tt + 1.0);
+        sn = tt * cs;
+    }
+    if (j == p) {
+        LC[2 * pi] = cs;
+        LC[2 * pi + 1] = sn;
+    }
+    ep_wave_sync();
+    // columns of A and V (every pair; static indices)
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int P = jrr_p(R, i), Q = jrr_q(R, i);
+        const double c = LC[2 * i], s = LC[2 * i + 1];
+        if (c != 0.0) {
+            const double akp = A[P], akq = A[Q];
+            A[P] = c * akp - s * akq;
+            A[Q] = s * akp + c * akq;
+            const double vkp = V[P], vkq = V[Q];
+            V[P] = c * vkp - s * vkq;
+            V[Q] = s * vkp + c * vkq;
+        }
+    }
+    // rows: the partner's column-rotated row through LDS
+#pragma unroll
+    for (int k = 0; k < 12; ++k) LA[12 * j + k] = A[k];
+    ep_wave_sync();
+    double O[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) O[k] = LA[12 * o + k];
+    ep_wave_sync();
+    const double x = j == p ? -sn : sn;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const double nv = cs * A[k] + x * O[k];
+        A[k] = act ? nv : A[k];
+    }
+    // the step-start matrix of the next step
+#pragma unroll
+    for (int k = 0; k < 12; ++k) LA[12 * j + k] = A[k];
+    ep_wave_sync();
+}
+template <int R>
+__device__ __forceinline__ void epnp_rr_sweep(int j, double (&A)[12], double (&V)[12], double *LA, double *LC) {
+    if constexpr (R < 11) {
+        epnp_rr_step<R>(j, A, V, LA, LC);
+        epnp_rr_sweep<R + 1>(j, A, V, LA, LC);
+    }
+}
 
-__device__ __forceinline__ double readlane_f64(double x, int lane) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, x);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-#ifndef RSAC_EPNP_PIPE
-#define RSAC_EPNP_PIPE 1  // A/B knob: 0 = one rotation after another (k_epnp5_jacobi<64>)
-#endif
-// lane src of this lane's group: G = 16 through ds_bpermute (4 groups per wave), G = 64 (one
-// group per wave) through v_readlane, a few cycles instead of an LDS round trip (the rotation
-// parameters and the sweep test; the rows are exchanged through ds_bpermute in both forms)
-template <int G>
-__device__ __forceinline__ double grp_read(double x, int g0, int src) {
-    if constexpr (G == 64)
-        return readlane_f64(x, src);
-    else
-        return bperm_f64(x, g0 + src);
-}
-
-// 2 of 3: M^T M's eigenvectors, G lanes per hypothesis (G = 16: 4 per wave, the throughput form;
-// G = 64: one per wave, the latency form for short rounds).  Lane j < 12 builds row j of A
-// (epnp_mtm's entries) and holds row j of V; a rotation (p, q) reads A[p][p], A[p][q], A[q][q]
-// from lanes p and q, updates columns p and q of every row in place (the row's own elements,
-// indexed by the wave-uniform p, q), then lanes p and q take each other's updated row and form the
-// new rows p and q: jacobi_eig<12>'s column, row and V loops element for element.  The sweep test
-// sums A's upper triangle in jacobi_eig's order.  Groups whose sweeps end early idle until the
-// wave's last group is done.
-template <int G>
 __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    __shared__ EpnpJacLds L;
     const int prob = blockIdx.y;
-    const int lane = threadIdx.x & 63, j = lane & (G - 1), g0 = lane & ~(G - 1);
-    const int hl = (int)((blockIdx.x * 256u + threadIdx.x) / G);
+    const int j = threadIdx.x & (kEpG - 1), hb = threadIdx.x / kEpG;
+    const int hl = (int)((blockIdx.x * 256u + threadIdx.x) / kEpG);
     const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
     double *E = a.epnp + rec * kEpnpRec;
     const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
     const bool live = hl < H && a.status[rec] > 0 && s1->ok != 0.0;
+    const bool row = j < 12;
     bool run = live;
-    epnp_row A, V;
+    double *LA = L.A[hb], *LC = L.cs[hb];
+    double A[12], V[12];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
+    for (int c = 0; c < 12; ++c) {
         A[c] = 0.0;
         V[c] = c == j ? 1.0 : 0.0;
     }
-    if (run && j < 12) {  // row j = 3i + p of epnp_mtm's matrix
+    if (run && row) {  // row j = 3i + p of epnp_mtm's matrix
         const double *cm = a.cams + 4 * prob;
         const double fx = cm[0], fy = cm[1];
         const int i = j / 3, p = j - 3 * i;
@@ -1065,136 +1124,30 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_beg
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr) A[3 * jj + rr] = p == 0 ? blk[rr] : p == 1 ? blk[3 + rr] : blk[6 + rr];
         }
+#pragma unroll
+        for (int k = 0; k < 12; ++k) LA[12 * j + k] = A[k];
     }
+    ep_wave_sync();
     for (int sweep = 0; sweep < 60; ++sweep) {
         if (run) {
             double off = 0.0, diag = 0.0;
 #pragma unroll
             for (int p = 0; p < 12; ++p) {
+                diag = diag + LA[13 * p] * LA[13 * p];
 #pragma unroll
-                for (int q = p; q < 12; ++q) {
-                    const double x = grp_read<G>(A[q], g0, p);
-                    if (q == p)
-                        diag = diag + x * x;
-                    else
-                        off = off + x * x;
-                }
+                for (int q = p + 1; q < 12; ++q) off = off + LA[12 * p + q] * LA[12 * p + q];
             }
             if (!(off > 1e-32 * diag)) run = false;
         }
         if (__ballot(run) == 0) break;
-        if (!run) continue;
-        if constexpr (G == 64 && RSAC_EPNP_PIPE) {
-        // Software-pipelined rotations (the one-wave form, 3 % faster; the 16-lane form measured
-        // slower with it, 1.09 -> 1.27 ms for 20k hypotheses): rotation (p, q + 1)'s parameters
-        // follow from rotation (p, q)'s cs, sn and values read before (p, q) changes A:
-        //   A[p][p]' = cs (cs app - sn apq) - sn (cs aqp - sn aqq),
-        //   A[p][q+1]' = cs A[p][q+1] - sn A[q][q+1],  A[q+1][q+1]' = A[q+1][q+1],
-        //   A[q+1][p]' = cs A[q+1][p] - sn A[q+1][q]
-        // (the operations the column and row updates apply to those elements, so the same bits),
-        // and (p, q)'s row exchange completes during (p, q + 1)'s parameter chain.  Branch-free: a
-        // skipped rotation (apq = 0) computes and discards.  The chain of three divisions and two
-        // square roots per rotation is the floor either way.
-#pragma unroll 1
-        for (int p = 0; p < 11; ++p) {
-            double app = grp_read<G>(A[p], g0, p), apq = grp_read<G>(A[p + 1], g0, p),
-                   aqq = grp_read<G>(A[p + 1], g0, p + 1), aqp = grp_read<G>(A[p], g0, p + 1);
-            double po[12], pcs = 0.0, px = 0.0;  // the previous rotation's exchange in flight
-            bool pmine = false;
-#pragma unroll
-            for (int k = 0; k < 12; ++k) po[k] = 0.0;
-#pragma unroll 1
-            for (int q = p + 1; q < 12; ++q) {
-                const bool act = apq != 0.0;
-                const double theta = (aqq - app) / (2.0 * apq);
-                const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
-                const double cs = 1.0 / dsqrt(tt * tt + 1.0), sn = tt * cs;
-                // the previous rotation's rows p and q
-#pragma unroll
-                for (int k = 0; k < 12; ++k) {
-                    const double nv = pcs * A[k] + px * po[k];
-                    A[k] = pmine ? nv : A[k];
-                }
-                // what the next rotation's parameters need, read before this rotation changes A
-                const int q1 = q < 11 ? q + 1 : 11;
-                const double n_pq1 = grp_read<G>(A[q1], g0, p), n_qq1 = grp_read<G>(A[q1], g0, q),
-                             n_q1q1 = grp_read<G>(A[q1], g0, q1), n_q1p = grp_read<G>(A[p], g0, q1),
-                             n_q1q = grp_read<G>(A[q], g0, q1);
-                // columns p and q of every row, and of V
-                {
-                    const double akp = A[p], akq = A[q];
-                    A[p] = act ? cs * akp - sn * akq : akp;
-                    A[q] = act ? sn * akp + cs * akq : akq;
-                    const double vkp = V[p], vkq = V[q];
-                    V[p] = act ? cs * vkp - sn * vkq : vkp;
-                    V[q] = act ? sn * vkp + cs * vkq : vkq;
-                }
-                // rows p and q: cs a + x o (x = -sn on lane p, +sn on lane q), o the partner's
-                // element after the column update; formed at the next rotation's start
-                const int partner = g0 + (j == p ? q : p);
-#pragma unroll
-                for (int k = 0; k < 12; ++k) po[k] = bperm_f64(A[k], partner);
-                pcs = cs;
-                px = j == p ? -sn : sn;
-                pmine = act && (j == p || j == q);
-                // the next rotation's parameters
-                const double cpp = cs * app - sn * apq, cqp = cs * aqp - sn * aqq;
-                app = act ? cs * cpp - sn * cqp : app;
-                apq = act ? cs * n_pq1 - sn * n_qq1 : n_pq1;
-                aqp = act ? cs * n_q1p - sn * n_q1q : n_q1p;
-                aqq = n_q1q1;
-            }
-#pragma unroll
-            for (int k = 0; k < 12; ++k) {  // the row's last rotation's rows
-                const double nv = pcs * A[k] + px * po[k];
-                A[k] = pmine ? nv : A[k];
-            }
-        }
-        } else {
-#pragma unroll 1
-        for (int p = 0; p < 11; ++p) {
-#pragma unroll 1
-            for (int q = p + 1; q < 12; ++q) {
-                // the three reads in one round trip (app and aqq are unused when apq is 0)
-                const double apq = grp_read<G>(A[q], g0, p), app = grp_read<G>(A[p], g0, p),
-                             aqq = grp_read<G>(A[q], g0, q);
-                if (apq == 0.0) continue;
-                const double theta = (aqq - app) / (2.0 * apq);
-                const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
-                const double cs = 1.0 / dsqrt(tt * tt + 1.0), sn = tt * cs;
-                {
-                    const double akp = A[p], akq = A[q];
-                    A[p] = cs * akp - sn * akq;
-                    A[q] = sn * akp + cs * akq;
-                }
-                // the rows: lane p forms cs a - sn o, lane q sn o + cs a, o the partner's element:
-                // both as cs a + x o with x = -sn / +sn (negation exact, the sum commutes: the same
-                // bits), the partner's row through ds_bpermute (one per-lane source, no selects)
-                const int partner = g0 + (j == p ? q : p);
-                const double x = j == p ? -sn : sn;
-                const bool mine = j == p || j == q;
-#pragma unroll
-                for (int k = 0; k < 12; ++k) {
-                    const double o = bperm_f64(A[k], partner);
-                    const double nv = cs * A[k] + x * o;
-                    A[k] = mine ? nv : A[k];
-                }
-                {
-                    const double vkp = V[p], vkq = V[q];
-                    V[p] = cs * vkp - sn * vkq;
-                    V[q] = sn * vkp + cs * vkq;
-                }
-            }
-        }
-        }
+        if (run && row) epnp_rr_sweep<0>(j, A, V, LA, LC);
     }
-    if (!live) return;
+    if (!live || !row) return;
     double d[12];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) d[k] = grp_read<G>(A[k], g0, k);
+    for (int k = 0; k < 12; ++k) d[k] = LA[13 * k];
     int o[12];
     eig_order_desc<12>(d, o);
-    if (j >= 12) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int col = o[11 - i];
@@ -2887,21 +2840,11 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
     return hipGetLastError();
 }
 
-#ifndef RSAC_EPNP_WAVE_MAX
-#define RSAC_EPNP_WAVE_MAX 4096
-#endif
-constexpr int64_t kEpnpWaveMaxHyps = RSAC_EPNP_WAVE_MAX;  // one wave per hypothesis up to this many (A/B knob)
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
     if (a.sample_k == 5 && a.epnp) {  // the three-launch form (k_epnp5_a / _jacobi / _c)
         hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-        // short rounds (an adaptive run's first 256 hypotheses): one wave per hypothesis, readlane
-        // exchanges (the round's latency is one hypothesis' Jacobi); longer ones 16 lanes each
-        if ((int64_t)P * H <= kEpnpWaveMaxHyps)
-            hipLaunchKernelGGL(k_epnp5_jacobi<64>, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-        else
-            hipLaunchKernelGGL(k_epnp5_jacobi<16>, dim3(cdiv(16 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin,
-                               H);
+        hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv((int64_t)kEpG * H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
         hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     } else if (a.sample_k == 5)
         hipLaunchKernelGGL(k_pnp_solve_epnp5, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);

@@ -1076,6 +1076,74 @@ RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
     for (int k = 0; k < N; ++k) d[k] = A[k * N + k];
 }
 
+// Round-robin ("parallel order") Jacobi of a symmetric N x N matrix, N even (EPnP's 12 x 12 M^T M):
+// a sweep is N - 1 steps, each rotating N / 2 disjoint pairs whose parameters all come from the
+// matrix at the step's start; then the columns of every pair (every row), the rows of every pair,
+// and V's columns.  Pairs are disjoint, so each element sees one fixed sequence of operations
+// whatever the order within a phase: the GPU runs a step's pairs on different lanes
+// (k_epnp5_jacobi) with the bits of this loop.  Schedule (circle method): in step r, position 0
+// holds index 0 and position m > 0 holds 1 + (m - 1 + r) % (N - 1); pair i is positions i and
+// N - 1 - i, p the smaller index.  Sweep test and rotation formula as jacobi_eig.
+RSAC_HD constexpr int jrr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
+template <int N>
+RSAC_HD void jacobi_eig_rr(double *A, double *V, double *d) {
+    static_assert(N % 2 == 0, "round-robin Jacobi needs an even order");
+    constexpr int H = N / 2;
+    for (int i = 0; i < N * N; ++i) V[i] = 0.0;
+    for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0, diag = 0.0;
+        for (int p = 0; p < N; ++p) {
+            diag = diag + A[p * N + p] * A[p * N + p];
+            for (int q = p + 1; q < N; ++q) off = off + A[p * N + q] * A[p * N + q];
+        }
+        if (!(off > 1e-32 * diag)) break;
+        for (int r = 0; r < N - 1; ++r) {
+            int P[H], Q[H];
+            bool act[H];
+            double cs[H], sn[H];
+            for (int i = 0; i < H; ++i) {
+                const int a = jrr_pos(N, r, i), b = jrr_pos(N, r, N - 1 - i);
+                const int p = a < b ? a : b, q = a < b ? b : a;
+                P[i] = p;
+                Q[i] = q;
+                const double apq = A[p * N + q];
+                act[i] = apq != 0.0;
+                cs[i] = 1.0;
+                sn[i] = 0.0;
+                if (!act[i]) continue;
+                const double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
+                const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
+                cs[i] = 1.0 / dsqrt(tt * tt + 1.0);
+                sn[i] = tt * cs[i];
+            }
+            for (int k = 0; k < N; ++k)
+                for (int i = 0; i < H; ++i) {
+                    if (!act[i]) continue;
+                    const double akp = A[k * N + P[i]], akq = A[k * N + Q[i]];
+                    A[k * N + P[i]] = cs[i] * akp - sn[i] * akq;
+                    A[k * N + Q[i]] = sn[i] * akp + cs[i] * akq;
+                }
+            for (int i = 0; i < H; ++i) {
+                if (!act[i]) continue;
+                for (int k = 0; k < N; ++k) {
+                    const double apk = A[P[i] * N + k], aqk = A[Q[i] * N + k];
+                    A[P[i] * N + k] = cs[i] * apk - sn[i] * aqk;
+                    A[Q[i] * N + k] = sn[i] * apk + cs[i] * aqk;
+                }
+            }
+            for (int k = 0; k < N; ++k)
+                for (int i = 0; i < H; ++i) {
+                    if (!act[i]) continue;
+                    const double vkp = V[k * N + P[i]], vkq = V[k * N + Q[i]];
+                    V[k * N + P[i]] = cs[i] * vkp - sn[i] * vkq;
+                    V[k * N + Q[i]] = sn[i] * vkp + cs[i] * vkq;
+                }
+        }
+    }
+    for (int k = 0; k < N; ++k) d[k] = A[k * N + k];
+}
+
 // order[] = eigenvalue indices by decreasing value (ties: lower index first)
 template <int N>
 RSAC_HD void eig_order_desc(const double *d, int *order) {
@@ -1378,7 +1446,7 @@ __host__ __device__ inline void epnp_stage2(const EpnpStage1 &s1, const Cam &k, 
     EpnpShared shm;
     EpnpShared *sh = &shm;
     epnp_mtm(sh, s1.pairs, k);
-    jacobi_eig<12>(sh->A, sh->V, sh->d);
+    jacobi_eig_rr<12>(sh->A, sh->V, sh->d);
     int o[12];
     eig_order_desc<12>(sh->d, o);
     for (int i = 0; i < 4; ++i)

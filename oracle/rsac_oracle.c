@@ -1740,7 +1740,8 @@ ORC_API int64_t orc_hom_ransac(const float *sx, const float *sy, const float *dx
  * barycentric alphas, M^T M, its 4 smallest eigenvectors, L 6x10 and rho, beta
  * approximations 1-3 each + 5 Gauss-Newton steps, the pose by SVD of the
  * cross-covariance, the lowest mean reprojection error wins.  Numerics of this
- * project (no OpenCV here to pin them): cyclic Jacobi eigen-decompositions,
+ * project (no OpenCV here to pin them): Jacobi eigen-decompositions (M^T M's
+ * 12 x 12 in round-robin order, ep_jacobi_rr; the 3 x 3 ones cyclic),
  * Householder least squares, M^T M assembled from per-control-point-pair sums,
  * the frame centred on the problem's first point, sums in the GPU order
  * (LM_THREADS strided partials, 64-lane butterfly, wave sums in order).
@@ -1837,6 +1838,68 @@ static void ep_jacobi(int N, double *A, double *V, double *d) {
                     V[k * N + q] = sn * vkp + cs * vkq;
                 }
             }
+    }
+    for (int k = 0; k < N; ++k) d[k] = A[k * N + k];
+}
+
+/* round-robin ("parallel order") Jacobi, symmetric N x N, N even (EPnP's 12 x 12 M^T M): a sweep
+   is N - 1 steps; step r pairs position i with position N - 1 - i, where position 0 holds index 0
+   and position m > 0 holds 1 + (m - 1 + r) % (N - 1) (circle method).  All pairs' rotations are
+   formed from the matrix at the step's start, then applied to the columns (every row), the rows
+   and V's columns.  The pairs are disjoint, so each element's sequence of operations is fixed
+   (the device runs a step's pairs on different lanes).  Sweep test and rotation formula as
+   ep_jacobi. */
+static int ep_rr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
+static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
+    int P[8], Q[8], act[8];
+    double cs[8], sn[8];
+    const int H = N / 2;
+    for (int i = 0; i < N * N; ++i) V[i] = 0.0;
+    for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0, diag = 0.0;
+        for (int p = 0; p < N; ++p) {
+            diag = diag + A[p * N + p] * A[p * N + p];
+            for (int q = p + 1; q < N; ++q) off = off + A[p * N + q] * A[p * N + q];
+        }
+        if (!(off > 1e-32 * diag)) break;
+        for (int r = 0; r < N - 1; ++r) {
+            for (int i = 0; i < H; ++i) {
+                int a = ep_rr_pos(N, r, i), b = ep_rr_pos(N, r, N - 1 - i);
+                int p = a < b ? a : b, q = a < b ? b : a;
+                double apq = A[p * N + q];
+                P[i] = p; Q[i] = q;
+                act[i] = apq != 0.0;
+                cs[i] = 1.0; sn[i] = 0.0;
+                if (!act[i]) continue;
+                double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
+                double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                cs[i] = 1.0 / sqrt(tt * tt + 1.0);
+                sn[i] = tt * cs[i];
+            }
+            for (int k = 0; k < N; ++k)
+                for (int i = 0; i < H; ++i) {
+                    if (!act[i]) continue;
+                    double akp = A[k * N + P[i]], akq = A[k * N + Q[i]];
+                    A[k * N + P[i]] = cs[i] * akp - sn[i] * akq;
+                    A[k * N + Q[i]] = sn[i] * akp + cs[i] * akq;
+                }
+            for (int i = 0; i < H; ++i) {
+                if (!act[i]) continue;
+                for (int k = 0; k < N; ++k) {
+                    double apk = A[P[i] * N + k], aqk = A[Q[i] * N + k];
+                    A[P[i] * N + k] = cs[i] * apk - sn[i] * aqk;
+                    A[Q[i] * N + k] = sn[i] * apk + cs[i] * aqk;
+                }
+            }
+            for (int k = 0; k < N; ++k)
+                for (int i = 0; i < H; ++i) {
+                    if (!act[i]) continue;
+                    double vkp = V[k * N + P[i]], vkq = V[k * N + Q[i]];
+                    V[k * N + P[i]] = cs[i] * vkp - sn[i] * vkq;
+                    V[k * N + Q[i]] = sn[i] * vkp + cs[i] * vkq;
+                }
+        }
     }
     for (int k = 0; k < N; ++k) d[k] = A[k * N + k];
 }
@@ -2064,7 +2127,7 @@ ORC_API int orc_pnp_epnp(const float *X, const float *Y, const float *Z, const f
                         A[12 * (3 * j + r) + 3 * i + p] = blk[3 * p + r];
                     }
             }
-        ep_jacobi(12, A, Vv, d);
+        ep_jacobi_rr(12, A, Vv, d);
         ep_order(12, d, o);
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 12; ++j) ut[i][j] = Vv[12 * j + o[11 - i]];
