@@ -1005,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
 // after every step), where each lane reads its pair's A[p][p], A[q][q], A[p][q] and, after the
 // column phase, its partner's row.  A step (static r, every pair's indices compile-time constants):
 //   params:  both lanes of pair (p, q) form its cs, sn from the step-start matrix (the same
-//            operations, so the same bits); lane p posts them (cs = 0: pair skipped, apq = 0);
+//            operations, so the same bits); lane p posts them (a skipped pair: cs 1, sn 0);
 //   columns: every lane rotates its elements (p_i, q_i) of A and of V for the 6 pairs;
 //   rows:    lanes p and q exchange their column-rotated rows through LDS and form
 //            cs a + x o (x = -sn on lane p, +sn on lane q: jacobi_eig_rr's cs a - sn o and
@@ -1016,7 +1016,8 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
 constexpr int kEpG = 16;  // lanes per hypothesis
 struct EpnpJacLds {
     double A[256 / kEpG][12 * 12];
-    double cs[256 / kEpG][12];  // pair i: cs at 2i (0: skipped), sn at 2i + 1
+    double cs[256 / kEpG][12];  // pair i: cs at 2i, sn at 2i + 1
+    int ord[256 / kEpG][12];    // eig_order_desc's order of the eigenvalues
 };
 RSAC_HD constexpr int jrr_p(int r, int i) {
     return jrr_pos(12, r, i) < jrr_pos(12, r, 11 - i) ? jrr_pos(12, r, i) : jrr_pos(12, r, 11 - i);
@@ -1030,7 +1031,11 @@ __device__ __forceinline__ void ep_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 template <int R>
-__device__ __forceinline__ void epnp_rr_step(int j, double (&A)[12], double (&V)[12], double *LA, double *LC) {
+__device__ __forceinline__ void epnp_rr_step(int sweep, int j, double (&A)[12], double (&V)[12], double *LA,
+                                             double *LC) {
+    // the lane's step constants (partner, pair, addresses) formed here, not hoisted out of the
+    // sweep loop, where 11 steps' worth of them held in registers spill
+    asm volatile("" : "+v"(j));
     // this lane's position, its partner, its pair
     const int m = j == 0 ? 0 : (j - 1 - R + 11) % 11 + 1;
     const int mo = 11 - m;
@@ -1038,33 +1043,35 @@ __device__ __forceinline__ void epnp_rr_step(int j, double (&A)[12], double (&V)
     const int pi = m < mo ? m : mo;
     const int p = j < o ? j : o, q = j < o ? o : j;
     const double app = LA[13 * p], aqq = LA[13 * q], apq = LA[12 * p + q];
-    const bool act = apq != 0.0;
-    double cs = 0.0, sn = 0.0;
-    if (act) {
-        const double theta = (aqq - app) / (2.0 * apq);
-        const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
-        cs = 1.0 / dsqrt(tt * tt + 1.0);
-        sn = tt * cs;
-    }
+    double cs = 1.0, sn = 0.0;  // a skipped pair: the identity rotation (jacobi_eig_rr)
+    (void)jrr_rotation(sweep, app, aqq, apq, cs, sn);
     if (j == p) {
         LC[2 * pi] = cs;
         LC[2 * pi + 1] = sn;
     }
     ep_wave_sync();
-    // columns of A and V (every pair; static indices)
+    // columns of A and V (every pair; static indices): the 6 rotations in one LDS round trip
+    double c6[6], s6[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        c6[i] = LC[2 * i];
+        s6[i] = LC[2 * i + 1];
+    }
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         const int P = jrr_p(R, i), Q = jrr_q(R, i);
-        const double c = LC[2 * i], s = LC[2 * i + 1];
-        if (c != 0.0) {
-            const double akp = A[P], akq = A[Q];
-            A[P] = c * akp - s * akq;
-            A[Q] = s * akp + c * akq;
-            const double vkp = V[P], vkq = V[Q];
-            V[P] = c * vkp - s * vkq;
-            V[Q] = s * vkp + c * vkq;
-        }
+        const double c = c6[i], s = s6[i];
+        const double akp = A[P], akq = A[Q];
+        A[P] = c * akp - s * akq;
+        A[Q] = s * akp + c * akq;
+        const double vkp = V[P], vkq = V[Q];
+        V[P] = c * vkp - s * vkq;
+        V[Q] = s * vkp + c * vkq;
     }
+    // V's rotations complete inside the step: left free, the scheduler sinks them to the sweep's
+    // end and holds every step's cs, sn live (24 VGPRs a step, spilled)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) asm volatile("" : "+v"(V[k]));
     // rows: the partner's column-rotated row through LDS
 #pragma unroll
     for (int k = 0; k < 12; ++k) LA[12 * j + k] = A[k];
@@ -1075,24 +1082,26 @@ __device__ __forceinline__ void epnp_rr_step(int j, double (&A)[12], double (&V)
     ep_wave_sync();
     const double x = j == p ? -sn : sn;
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const double nv = cs * A[k] + x * O[k];
-        A[k] = act ? nv : A[k];
-    }
+    for (int k = 0; k < 12; ++k) A[k] = cs * A[k] + x * O[k];
     // the step-start matrix of the next step
 #pragma unroll
     for (int k = 0; k < 12; ++k) LA[12 * j + k] = A[k];
     ep_wave_sync();
 }
 template <int R>
-__device__ __forceinline__ void epnp_rr_sweep(int j, double (&A)[12], double (&V)[12], double *LA, double *LC) {
+__device__ __forceinline__ void epnp_rr_sweep(int sweep, int j, double (&A)[12], double (&V)[12], double *LA,
+                                              double *LC) {
     if constexpr (R < 11) {
-        epnp_rr_step<R>(j, A, V, LA, LC);
-        epnp_rr_sweep<R + 1>(j, A, V, LA, LC);
+        epnp_rr_step<R>(sweep, j, A, V, LA, LC);
+        epnp_rr_sweep<R + 1>(sweep, j, A, V, LA, LC);
     }
 }
 
-__global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_begin, int32_t H) {
+#ifndef RSAC_EPNP_WAVES
+#define RSAC_EPNP_WAVES 2  // A/B knob: waves per SIMD asked of k_epnp5_jacobi (4: 128 VGPRs, 16 spilled)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_WAVES, 8))) void k_epnp5_jacobi(
+    PnpArgs a, int64_t hyp_begin, int32_t H) {
     __shared__ EpnpJacLds L;
     const int prob = blockIdx.y;
     const int j = threadIdx.x & (kEpG - 1), hb = threadIdx.x / kEpG;
@@ -1130,31 +1139,195 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi(PnpArgs a, int64_t hyp_beg
     ep_wave_sync();
     for (int sweep = 0; sweep < 60; ++sweep) {
         if (run) {
+            // one row of loads at a time (all 78 at once would hold 156 VGPRs)
             double off = 0.0, diag = 0.0;
-#pragma unroll
+#pragma unroll 1
             for (int p = 0; p < 12; ++p) {
-                diag = diag + LA[13 * p] * LA[13 * p];
+                double rw[12];
 #pragma unroll
-                for (int q = p + 1; q < 12; ++q) off = off + LA[12 * p + q] * LA[12 * p + q];
+                for (int q = 0; q < 12; ++q) rw[q] = LA[12 * p + q];
+                double dp = 0.0;
+#pragma unroll
+                for (int q = 0; q < 12; ++q) dp = q == p ? rw[q] : dp;
+                diag = diag + dp * dp;
+#pragma unroll
+                for (int q = 1; q < 12; ++q)
+                    if (q > p) off = off + rw[q] * rw[q];
             }
             if (!(off > 1e-32 * diag)) run = false;
         }
         if (__ballot(run) == 0) break;
-        if (run && row) epnp_rr_sweep<0>(j, A, V, LA, LC);
+        if (run && row) epnp_rr_sweep<0>(sweep, j, A, V, LA, LC);
     }
     if (!live || !row) return;
-    double d[12];
+    // eig_order_desc<12> on the diagonal, by lane 0 of the group with its arrays in LDS (in
+    // registers its dynamic indices become select chains), then V's row through LDS
+    int *O = L.ord[hb];
+    if (j == 0) {
+        for (int i = 0; i < 12; ++i) O[i] = i;
+        for (int i = 1; i < 12; ++i) {
+            const int k = O[i];
+            const double dk = LA[13 * k];
+            int jx = i - 1;
+            while (jx >= 0 && LA[13 * O[jx]] < dk) {
+                O[jx + 1] = O[jx];
+                --jx;
+            }
+            O[jx + 1] = k;
+        }
+    }
+    ep_wave_sync();
 #pragma unroll
-    for (int k = 0; k < 12; ++k) d[k] = LA[13 * k];
-    int o[12];
-    eig_order_desc<12>(d, o);
+    for (int c = 0; c < 12; ++c) LA[12 * j + c] = V[c];  // lane 0's sort has read the diagonal
+    ep_wave_sync();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int col = o[11 - i];
-        double v = 0.0;
+    for (int i = 0; i < 4; ++i) E[64 + 12 * i + j] = LA[12 * j + O[11 - i]];  // ut[i][j] = V[j][o[11 - i]]
+}
+
+// The latency form of k_epnp5_jacobi for short rounds (an adaptive run's first 256 hypotheses):
+// one wave per hypothesis, so a step's instructions per wave halve.  Lane L < 48: kind = L / 24
+// (0: a row of A, 1: the same row of V), row j = (L % 24) / 2, half h = L % 2; in each step half h
+// owns the 6 columns of pairs 3h .. 3h + 2 (read from the LDS copy at the step's start, rotated,
+// written back), so the column phase is 3 pairs per lane and the row phase 6 elements; both
+// matrices live in LDS between steps.  The same operations on every element as jacobi_eig_rr.
+struct EpnpJacLdsW {
+    double A[4][12 * 12];
+    double V[4][12 * 12];
+    double cs[4][12];
+    int ord[4][12];
+};
+template <int R>
+__device__ __forceinline__ void epnp_rrw_step(int sweep, int j, int h, bool isA, double *LA, double *LM, double *LC) {
+    asm volatile("" : "+v"(j), "+v"(h));
+    const int m = j == 0 ? 0 : (j - 1 - R + 11) % 11 + 1;
+    const int mo = 11 - m;
+    const int o = mo == 0 ? 0 : 1 + (mo - 1 + R) % 11;
+    const int pi = m < mo ? m : mo;
+    const int p = j < o ? j : o, q = j < o ? o : j;
+    // this lane's 6 columns: pairs 3h .. 3h + 2
+    int col[6];
 #pragma unroll
-        for (int c = 0; c < 12; ++c) v = c == col ? V[c] : v;
-        E[64 + 12 * i + j] = v;  // ut[i][j] = V[j][o[11 - i]]
+    for (int e = 0; e < 3; ++e) {
+        col[2 * e] = h ? jrr_p(R, 3 + e) : jrr_p(R, e);
+        col[2 * e + 1] = h ? jrr_q(R, 3 + e) : jrr_q(R, e);
+    }
+    double x[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) x[e] = LM[12 * j + col[e]];
+    const double app = LA[13 * p], aqq = LA[13 * q], apq = LA[12 * p + q];
+    double cs = 1.0, sn = 0.0;  // a skipped pair: the identity rotation (jacobi_eig_rr)
+    (void)jrr_rotation(sweep, app, aqq, apq, cs, sn);
+    if (isA && h == 0 && j == p) {
+        LC[2 * pi] = cs;
+        LC[2 * pi + 1] = sn;
+    }
+    ep_wave_sync();
+    double c3[3], s3[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        c3[e] = LC[2 * (3 * h + e)];
+        s3[e] = LC[2 * (3 * h + e) + 1];
+    }
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        const double a0 = x[2 * e], a1 = x[2 * e + 1];
+        x[2 * e] = c3[e] * a0 - s3[e] * a1;
+        x[2 * e + 1] = s3[e] * a0 + c3[e] * a1;
+    }
+#pragma unroll
+    for (int e = 0; e < 6; ++e) LM[12 * j + col[e]] = x[e];
+    ep_wave_sync();
+    if (isA) {  // rows: the partner's column-rotated elements of the same columns
+        double y[6];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) y[e] = LA[12 * o + col[e]];
+        ep_wave_sync();
+        const double xs = j == p ? -sn : sn;
+#pragma unroll
+        for (int e = 0; e < 6; ++e) x[e] = cs * x[e] + xs * y[e];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) LA[12 * j + col[e]] = x[e];
+    }
+    ep_wave_sync();
+}
+template <int R>
+__device__ __forceinline__ void epnp_rrw_sweep(int sweep, int j, int h, bool isA, double *LA, double *LM, double *LC) {
+    if constexpr (R < 11) {
+        epnp_rrw_step<R>(sweep, j, h, isA, LA, LM, LC);
+        epnp_rrw_sweep<R + 1>(sweep, j, h, isA, LA, LM, LC);
+    }
+}
+__global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    __shared__ EpnpJacLdsW L;
+    const int prob = blockIdx.y;
+    const int lane = threadIdx.x & 63, hb = threadIdx.x >> 6;
+    const int hl = (int)((blockIdx.x * 256u + threadIdx.x) >> 6);
+    const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
+    double *E = a.epnp + rec * kEpnpRec;
+    const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
+    const bool live = hl < H && a.status[rec] > 0 && s1->ok != 0.0;  // wave-uniform
+    if (!live) return;
+    const bool act = lane < 48, isA = lane < 24;
+    const int j = (lane % 24) >> 1, h = lane & 1;
+    double *LA = L.A[hb], *LV = L.V[hb], *LC = L.cs[hb];
+    double *LM = isA ? LA : LV;
+    if (lane < 12) {  // row `lane` of epnp_mtm's matrix, and of V = I
+        const int jr = lane;
+        const double *cm = a.cams + 4 * prob;
+        const double fx = cm[0], fy = cm[1];
+        const int i = jr / 3, pp = jr - 3 * i;
+        constexpr int first[4] = {0, 4, 7, 9};  // pair (x <= y) -> sum block x's first + (y - x)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int lo = min(i, jj), hi = max(i, jj);
+            const double *ps = s1->pairs + 4 * (first[lo] + hi - lo);
+            const double s0 = ps[0], su = ps[1], sv = ps[2], sw = ps[3];
+            const double blk[9] = {fx * fx * s0, 0.0, fx * su, 0.0, fy * fy * s0, fy * sv, fx * su, fy * sv, sw};
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr)
+                LA[12 * jr + 3 * jj + rr] = pp == 0 ? blk[rr] : pp == 1 ? blk[3 + rr] : blk[6 + rr];
+        }
+#pragma unroll
+        for (int c = 0; c < 12; ++c) LV[12 * jr + c] = c == jr ? 1.0 : 0.0;
+    }
+    ep_wave_sync();
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0, diag = 0.0;  // every lane, in jacobi_eig_rr's order (wave-uniform verdict)
+#pragma unroll 1
+        for (int pr = 0; pr < 12; ++pr) {
+            double rw[12];
+#pragma unroll
+            for (int qq = 0; qq < 12; ++qq) rw[qq] = LA[12 * pr + qq];
+            double dp = 0.0;
+#pragma unroll
+            for (int qq = 0; qq < 12; ++qq) dp = qq == pr ? rw[qq] : dp;
+            diag = diag + dp * dp;
+#pragma unroll
+            for (int qq = 1; qq < 12; ++qq)
+                if (qq > pr) off = off + rw[qq] * rw[qq];
+        }
+        if (!(off > 1e-32 * diag)) break;
+        if (act) epnp_rrw_sweep<0>(sweep, j, h, isA, LA, LM, LC);
+        ep_wave_sync();
+    }
+    int *O = L.ord[hb];
+    if (lane == 0) {  // eig_order_desc<12> on the diagonal
+        for (int i = 0; i < 12; ++i) O[i] = i;
+        for (int i = 1; i < 12; ++i) {
+            const int k = O[i];
+            const double dk = LA[13 * k];
+            int jx = i - 1;
+            while (jx >= 0 && LA[13 * O[jx]] < dk) {
+                O[jx + 1] = O[jx];
+                --jx;
+            }
+            O[jx + 1] = k;
+        }
+    }
+    ep_wave_sync();
+    if (lane < 12) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) E[64 + 12 * i + lane] = LV[12 * lane + O[11 - i]];  // ut[i][j] = V[j][o[11 - i]]
     }
 }
 
@@ -2840,11 +3013,21 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
     return hipGetLastError();
 }
 
+#ifndef RSAC_EPNP_WAVE_MAX
+#define RSAC_EPNP_WAVE_MAX 4096
+#endif
+constexpr int64_t kEpnpWaveMaxHyps = RSAC_EPNP_WAVE_MAX;  // one wave per hypothesis up to this many (A/B knob)
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
     if (a.sample_k == 5 && a.epnp) {  // the three-launch form (k_epnp5_a / _jacobi / _c)
         hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-        hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv((int64_t)kEpG * H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+        // short rounds (an adaptive run's first 256 hypotheses): one wave per hypothesis (the round's
+        // latency is one hypothesis' Jacobi); longer ones 16 lanes each
+        if ((int64_t)P * H <= kEpnpWaveMaxHyps)
+            hipLaunchKernelGGL(k_epnp5_jacobi_w, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+        else
+            hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv((int64_t)kEpG * H, 256), P), dim3(256), 0, s, ka, hyp_begin,
+                               H);
         hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     } else if (a.sample_k == 5)
         hipLaunchKernelGGL(k_pnp_solve_epnp5, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);

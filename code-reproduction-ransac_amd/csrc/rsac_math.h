@@ -1083,8 +1083,25 @@ RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
 // whatever the order within a phase: the GPU runs a step's pairs on different lanes
 // (k_epnp5_jacobi) with the bits of this loop.  Schedule (circle method): in step r, position 0
 // holds index 0 and position m > 0 holds 1 + (m - 1 + r) % (N - 1); pair i is positions i and
-// N - 1 - i, p the smaller index.  Sweep test and rotation formula as jacobi_eig.
+// N - 1 - i, p the smaller index.  Sweep test as jacobi_eig; the rotation by jrr_rotation.
 RSAC_HD constexpr int jrr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
+// the rotation of pair (p, q): false (skipped) for apq = 0 or, from the fifth sweep on, apq
+// negligible next to both diagonal entries (Numerical Recipes' rule); t = sgn(theta) / (|theta| +
+// sqrt(theta^2 + 1)) with theta = d / w, d = aqq - app, w = 2 apq, formed as sgn |w| / (|d| +
+// sqrt(d^2 + w^2)) (one division fewer; MᵀM's entries are far from the square's overflow)
+RSAC_HD inline bool jrr_rotation(int sweep, double app, double aqq, double apq, double &cs, double &sn) {
+    if (!(apq != 0.0)) return false;
+    if (sweep >= 4) {
+        const double g = 100.0 * dabs(apq);
+        if (dabs(app) + g == dabs(app) && dabs(aqq) + g == dabs(aqq)) return false;
+    }
+    const double d = aqq - app, w = 2.0 * apq;
+    const double sg = (d == 0.0 || ((d < 0.0) == (w < 0.0))) ? 1.0 : -1.0;
+    const double tt = sg * dabs(w) / (dabs(d) + dsqrt(d * d + w * w));
+    cs = 1.0 / dsqrt(tt * tt + 1.0);
+    sn = tt * cs;
+    return true;
+}
 template <int N>
 RSAC_HD void jacobi_eig_rr(double *A, double *V, double *d) {
     static_assert(N % 2 == 0, "round-robin Jacobi needs an even order");
@@ -1100,32 +1117,24 @@ RSAC_HD void jacobi_eig_rr(double *A, double *V, double *d) {
         if (!(off > 1e-32 * diag)) break;
         for (int r = 0; r < N - 1; ++r) {
             int P[H], Q[H];
-            bool act[H];
             double cs[H], sn[H];
             for (int i = 0; i < H; ++i) {
                 const int a = jrr_pos(N, r, i), b = jrr_pos(N, r, N - 1 - i);
                 const int p = a < b ? a : b, q = a < b ? b : a;
                 P[i] = p;
                 Q[i] = q;
-                const double apq = A[p * N + q];
-                act[i] = apq != 0.0;
                 cs[i] = 1.0;
                 sn[i] = 0.0;
-                if (!act[i]) continue;
-                const double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
-                const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
-                cs[i] = 1.0 / dsqrt(tt * tt + 1.0);
-                sn[i] = tt * cs[i];
+                (void)jrr_rotation(sweep, A[p * N + p], A[q * N + q], A[p * N + q], cs[i], sn[i]);
             }
+            // a skipped pair applies cs = 1, sn = 0 like any other (the device runs branch-free)
             for (int k = 0; k < N; ++k)
                 for (int i = 0; i < H; ++i) {
-                    if (!act[i]) continue;
                     const double akp = A[k * N + P[i]], akq = A[k * N + Q[i]];
                     A[k * N + P[i]] = cs[i] * akp - sn[i] * akq;
                     A[k * N + Q[i]] = sn[i] * akp + cs[i] * akq;
                 }
             for (int i = 0; i < H; ++i) {
-                if (!act[i]) continue;
                 for (int k = 0; k < N; ++k) {
                     const double apk = A[P[i] * N + k], aqk = A[Q[i] * N + k];
                     A[P[i] * N + k] = cs[i] * apk - sn[i] * aqk;
@@ -1134,7 +1143,6 @@ RSAC_HD void jacobi_eig_rr(double *A, double *V, double *d) {
             }
             for (int k = 0; k < N; ++k)
                 for (int i = 0; i < H; ++i) {
-                    if (!act[i]) continue;
                     const double vkp = V[k * N + P[i]], vkq = V[k * N + Q[i]];
                     V[k * N + P[i]] = cs[i] * vkp - sn[i] * vkq;
                     V[k * N + Q[i]] = sn[i] * vkp + cs[i] * vkq;

@@ -1847,8 +1847,10 @@ static void ep_jacobi(int N, double *A, double *V, double *d) {
    and position m > 0 holds 1 + (m - 1 + r) % (N - 1) (circle method).  All pairs' rotations are
    formed from the matrix at the step's start, then applied to the columns (every row), the rows
    and V's columns.  The pairs are disjoint, so each element's sequence of operations is fixed
-   (the device runs a step's pairs on different lanes).  Sweep test and rotation formula as
-   ep_jacobi. */
+   (the device runs a step's pairs on different lanes).  Sweep test as ep_jacobi; the rotation's
+   t from d = aqq - app and w = 2 apq (one division fewer than through theta), and from the fifth
+   sweep on a pair whose apq is negligible next to both diagonal entries is skipped (the rule of
+   Numerical Recipes' jacobi). */
 static int ep_rr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
 static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
     int P[8], Q[8], act[8];
@@ -1867,25 +1869,31 @@ static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
             for (int i = 0; i < H; ++i) {
                 int a = ep_rr_pos(N, r, i), b = ep_rr_pos(N, r, N - 1 - i);
                 int p = a < b ? a : b, q = a < b ? b : a;
-                double apq = A[p * N + q];
+                double apq = A[p * N + q], app = A[p * N + p], aqq = A[q * N + q];
                 P[i] = p; Q[i] = q;
                 act[i] = apq != 0.0;
                 cs[i] = 1.0; sn[i] = 0.0;
+                if (act[i] && sweep >= 4) { /* negligible next to both diagonal entries: skipped */
+                    double g = 100.0 * fabs(apq);
+                    if (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq)) act[i] = 0;
+                }
                 if (!act[i]) continue;
-                double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
-                double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                /* t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)), theta = d / w, without forming theta */
+                double d = aqq - app, w = 2.0 * apq;
+                double sg = (d == 0.0 || ((d < 0.0) == (w < 0.0))) ? 1.0 : -1.0;
+                double tt = sg * fabs(w) / (fabs(d) + sqrt(d * d + w * w));
                 cs[i] = 1.0 / sqrt(tt * tt + 1.0);
                 sn[i] = tt * cs[i];
             }
+            /* a skipped pair applies cs = 1, sn = 0 like any other (no special case, so the device
+               runs every step branch-free with the same bits) */
             for (int k = 0; k < N; ++k)
                 for (int i = 0; i < H; ++i) {
-                    if (!act[i]) continue;
                     double akp = A[k * N + P[i]], akq = A[k * N + Q[i]];
                     A[k * N + P[i]] = cs[i] * akp - sn[i] * akq;
                     A[k * N + Q[i]] = sn[i] * akp + cs[i] * akq;
                 }
             for (int i = 0; i < H; ++i) {
-                if (!act[i]) continue;
                 for (int k = 0; k < N; ++k) {
                     double apk = A[P[i] * N + k], aqk = A[Q[i] * N + k];
                     A[P[i] * N + k] = cs[i] * apk - sn[i] * aqk;
@@ -1894,7 +1902,6 @@ static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
             }
             for (int k = 0; k < N; ++k)
                 for (int i = 0; i < H; ++i) {
-                    if (!act[i]) continue;
                     double vkp = V[k * N + P[i]], vkq = V[k * N + Q[i]];
                     V[k * N + P[i]] = cs[i] * vkp - sn[i] * vkq;
                     V[k * N + Q[i]] = sn[i] * vkp + cs[i] * vkq;
