@@ -1198,7 +1198,7 @@ struct EpnpJacLdsW {
 };
 template <int R>
 __device__ __forceinline__ void epnp_rrw_step(int sweep, int j, int h, bool isA, double *LA, double *LM, double *LC) {
-    asm volatile("" : "+v"(j), "+v"(h));
+    // (the lane's step constants may be hoisted out of the sweep loop: this form has the registers)
     const int m = j == 0 ? 0 : (j - 1 - R + 11) % 11 + 1;
     const int mo = 11 - m;
     const int o = mo == 0 ? 0 : 1 + (mo - 1 + R) % 11;
@@ -3014,9 +3014,9 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
 }
 
 #ifndef RSAC_EPNP_WAVE_MAX
-#define RSAC_EPNP_WAVE_MAX 4096
+#define RSAC_EPNP_WAVE_MAX 2048
 #endif
-constexpr int64_t kEpnpWaveMaxHyps = RSAC_EPNP_WAVE_MAX;  // one wave per hypothesis up to this many (A/B knob)
+constexpr int64_t kEpnpWaveMaxHyps = RSAC_EPNP_WAVE_MAX;  // one wave per hypothesis up to this many (2 waves/SIMD at 250 VGPRs: one round of waves; A/B knob)
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
     if (a.sample_k == 5 && a.epnp) {  // the three-launch form (k_epnp5_a / _jacobi / _c)
