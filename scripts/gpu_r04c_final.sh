@@ -1,7 +1,7 @@
 #!/bin/bash
-# r04c final pass: GPU suite + smoke + bench line, then the rocprofv3 kernel trace and PMC passes of
-# the bench command (summarised on the host: scripts/summarize_profiles.py r04c) and the EPnP-5 trace
+# r04 final pass (r04c, r04d): GPU suite + smoke + bench line, then the rocprofv3 kernel trace and PMC passes of
+# the bench command (summarised on the host: scripts/summarize_profiles.py r04d) and the EPnP-5 trace
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 bash scripts/gpu_check.sh || exit $?
-TAG=r04c PMC=1 bash scripts/gpu_profile.sh || exit $?
+TAG=r04d PMC=1 bash scripts/gpu_profile.sh || exit $?
 bash scripts/gpu_epnp_trace.sh
