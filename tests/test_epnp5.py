@@ -82,11 +82,13 @@ def test_oracle_ransac_epnp5_finds_the_inliers():
 # --------------------------------------------------------------------------------------------- GPU
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,outl,seed,H", [(300, 0.3, 31, 1024), (2000, 0.5, 32, 1024), (300, 0.4, 33, 6000)])
+@pytest.mark.parametrize("n,outl,seed,H", [(300, 0.3, 31, 1024), (2000, 0.5, 32, 1024), (300, 0.4, 33, 6000),
+                                           (400, 0.5, 34, 2048), (400, 0.5, 34, 2049)])
 def test_gpu_epnp5_hypotheses_bit_exact(n, outl, seed, H):
     """Every hypothesis (Philox 5-subsets, then explicit MWC 5-subsets): status, count, model.
-    H <= 4096 runs the Jacobi of the three-launch solve one wave per hypothesis (readlane), larger
-    rounds 16 lanes per hypothesis (ds_bpermute): both forms against the oracle."""
+    Rounds of H <= 2048 run the round-robin Jacobi of the three-launch solve one wave per
+    hypothesis (k_epnp5_jacobi_w), larger rounds 16 lanes per hypothesis (k_epnp5_jacobi): both
+    forms, and the boundary between them, against the oracle's ep_jacobi_rr."""
     pr = synth.pnp_problem(n, outl, seed=seed)
     soa, cam = O.soa_pnp(pr["points3d"], pr["points2d"]), O.cam_from_K(pr["K"])
     st, cn, md = rsac.hypotheses("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, H, 30.0, seed=77,
