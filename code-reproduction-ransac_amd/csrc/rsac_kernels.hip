@@ -1014,8 +1014,12 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
 // from LDS in jacobi_eig_rr's order.  Groups whose sweeps end early idle until the wave's last
 // group is done.
 constexpr int kEpG = 16;  // lanes per hypothesis
+// LDS row stride of the mirrored matrices (doubles): 13, not 12, so the 12 rows of one column (and
+// the 4 groups of a wave, the A and V rows of the latency form) fall in distinct banks: 2-way at
+// most where 12 gave 6- to 8-way (SQ_LDS_BANK_CONFLICT, profiles/r04_epnp_pmc.json)
+constexpr int kEpR = 13;
 struct EpnpJacLds {
-    double A[256 / kEpG][12 * 12];
+    double A[256 / kEpG][12 * kEpR];
     double cs[256 / kEpG][12];  // pair i: cs at 2i, sn at 2i + 1
     int ord[256 / kEpG][12];    // eig_order_desc's order of the eigenvalues
 };
@@ -1042,7 +1046,7 @@ __device__ __forceinline__ void epnp_rr_step(int sweep, int j, double (&A)[12], 
     const int o = mo == 0 ? 0 : 1 + (mo - 1 + R) % 11;
     const int pi = m < mo ? m : mo;
     const int p = j < o ? j : o, q = j < o ? o : j;
-    const double app = LA[13 * p], aqq = LA[13 * q], apq = LA[12 * p + q];
+    const double app = LA[(kEpR + 1) * p], aqq = LA[(kEpR + 1) * q], apq = LA[kEpR * p + q];
     double cs = 1.0, sn = 0.0;  // a skipped pair: the identity rotation (jacobi_eig_rr)
     (void)jrr_rotation(sweep, app, aqq, apq, cs, sn);
     if (j == p) {
@@ -1074,18 +1078,18 @@ __device__ __forceinline__ void epnp_rr_step(int sweep, int j, double (&A)[12], 
     for (int k = 0; k < 12; ++k) asm volatile("" : "+v"(V[k]));
     // rows: the partner's column-rotated row through LDS
 #pragma unroll
-    for (int k = 0; k < 12; ++k) LA[12 * j + k] = A[k];
+    for (int k = 0; k < 12; ++k) LA[kEpR * j + k] = A[k];
     ep_wave_sync();
     double O[12];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) O[k] = LA[12 * o + k];
+    for (int k = 0; k < 12; ++k) O[k] = LA[kEpR * o + k];
     ep_wave_sync();
     const double x = j == p ? -sn : sn;
 #pragma unroll
     for (int k = 0; k < 12; ++k) A[k] = cs * A[k] + x * O[k];
     // the step-start matrix of the next step
 #pragma unroll
-    for (int k = 0; k < 12; ++k) LA[12 * j + k] = A[k];
+    for (int k = 0; k < 12; ++k) LA[kEpR * j + k] = A[k];
     ep_wave_sync();
 }
 template <int R>
@@ -1134,7 +1138,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
             for (int rr = 0; rr < 3; ++rr) A[3 * jj + rr] = p == 0 ? blk[rr] : p == 1 ? blk[3 + rr] : blk[6 + rr];
         }
 #pragma unroll
-        for (int k = 0; k < 12; ++k) LA[12 * j + k] = A[k];
+        for (int k = 0; k < 12; ++k) LA[kEpR * j + k] = A[k];
     }
     ep_wave_sync();
     for (int sweep = 0; sweep < 60; ++sweep) {
@@ -1145,7 +1149,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
             for (int p = 0; p < 12; ++p) {
                 double rw[12];
 #pragma unroll
-                for (int q = 0; q < 12; ++q) rw[q] = LA[12 * p + q];
+                for (int q = 0; q < 12; ++q) rw[q] = LA[kEpR * p + q];
                 double dp = 0.0;
 #pragma unroll
                 for (int q = 0; q < 12; ++q) dp = q == p ? rw[q] : dp;
@@ -1167,9 +1171,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
         for (int i = 0; i < 12; ++i) O[i] = i;
         for (int i = 1; i < 12; ++i) {
             const int k = O[i];
-            const double dk = LA[13 * k];
+            const double dk = LA[(kEpR + 1) * k];
             int jx = i - 1;
-            while (jx >= 0 && LA[13 * O[jx]] < dk) {
+            while (jx >= 0 && LA[(kEpR + 1) * O[jx]] < dk) {
                 O[jx + 1] = O[jx];
                 --jx;
             }
@@ -1178,10 +1182,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
     }
     ep_wave_sync();
 #pragma unroll
-    for (int c = 0; c < 12; ++c) LA[12 * j + c] = V[c];  // lane 0's sort has read the diagonal
+    for (int c = 0; c < 12; ++c) LA[kEpR * j + c] = V[c];  // lane 0's sort has read the diagonal
     ep_wave_sync();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) E[64 + 12 * i + j] = LA[12 * j + O[11 - i]];  // ut[i][j] = V[j][o[11 - i]]
+    for (int i = 0; i < 4; ++i) E[64 + 12 * i + j] = LA[kEpR * j + O[11 - i]];  // ut[i][j] = V[j][o[11 - i]]
 }
 
 // The latency form of k_epnp5_jacobi for short rounds (an adaptive run's first 256 hypotheses):
@@ -1191,8 +1195,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
 // written back), so the column phase is 3 pairs per lane and the row phase 6 elements; both
 // matrices live in LDS between steps.  The same operations on every element as jacobi_eig_rr.
 struct EpnpJacLdsW {
-    double A[4][12 * 12];
-    double V[4][12 * 12];
+    double A[4][12 * kEpR];
+    double V[4][12 * kEpR];
     double cs[4][12];
     int ord[4][12];
 };
@@ -1213,8 +1217,8 @@ __device__ __forceinline__ void epnp_rrw_step(int sweep, int j, int h, bool isA,
     }
     double x[6];
 #pragma unroll
-    for (int e = 0; e < 6; ++e) x[e] = LM[12 * j + col[e]];
-    const double app = LA[13 * p], aqq = LA[13 * q], apq = LA[12 * p + q];
+    for (int e = 0; e < 6; ++e) x[e] = LM[kEpR * j + col[e]];
+    const double app = LA[(kEpR + 1) * p], aqq = LA[(kEpR + 1) * q], apq = LA[kEpR * p + q];
     double cs = 1.0, sn = 0.0;  // a skipped pair: the identity rotation (jacobi_eig_rr)
     (void)jrr_rotation(sweep, app, aqq, apq, cs, sn);
     if (isA && h == 0 && j == p) {
@@ -1235,18 +1239,18 @@ __device__ __forceinline__ void epnp_rrw_step(int sweep, int j, int h, bool isA,
         x[2 * e + 1] = s3[e] * a0 + c3[e] * a1;
     }
 #pragma unroll
-    for (int e = 0; e < 6; ++e) LM[12 * j + col[e]] = x[e];
+    for (int e = 0; e < 6; ++e) LM[kEpR * j + col[e]] = x[e];
     ep_wave_sync();
     if (isA) {  // rows: the partner's column-rotated elements of the same columns
         double y[6];
 #pragma unroll
-        for (int e = 0; e < 6; ++e) y[e] = LA[12 * o + col[e]];
+        for (int e = 0; e < 6; ++e) y[e] = LA[kEpR * o + col[e]];
         ep_wave_sync();
         const double xs = j == p ? -sn : sn;
 #pragma unroll
         for (int e = 0; e < 6; ++e) x[e] = cs * x[e] + xs * y[e];
 #pragma unroll
-        for (int e = 0; e < 6; ++e) LA[12 * j + col[e]] = x[e];
+        for (int e = 0; e < 6; ++e) LA[kEpR * j + col[e]] = x[e];
     }
     ep_wave_sync();
 }
@@ -1285,10 +1289,10 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_b
             const double blk[9] = {fx * fx * s0, 0.0, fx * su, 0.0, fy * fy * s0, fy * sv, fx * su, fy * sv, sw};
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr)
-                LA[12 * jr + 3 * jj + rr] = pp == 0 ? blk[rr] : pp == 1 ? blk[3 + rr] : blk[6 + rr];
+                LA[kEpR * jr + 3 * jj + rr] = pp == 0 ? blk[rr] : pp == 1 ? blk[3 + rr] : blk[6 + rr];
         }
 #pragma unroll
-        for (int c = 0; c < 12; ++c) LV[12 * jr + c] = c == jr ? 1.0 : 0.0;
+        for (int c = 0; c < 12; ++c) LV[kEpR * jr + c] = c == jr ? 1.0 : 0.0;
     }
     ep_wave_sync();
     for (int sweep = 0; sweep < 60; ++sweep) {
@@ -1297,7 +1301,7 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_b
         for (int pr = 0; pr < 12; ++pr) {
             double rw[12];
 #pragma unroll
-            for (int qq = 0; qq < 12; ++qq) rw[qq] = LA[12 * pr + qq];
+            for (int qq = 0; qq < 12; ++qq) rw[qq] = LA[kEpR * pr + qq];
             double dp = 0.0;
 #pragma unroll
             for (int qq = 0; qq < 12; ++qq) dp = qq == pr ? rw[qq] : dp;
@@ -1315,9 +1319,9 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_b
         for (int i = 0; i < 12; ++i) O[i] = i;
         for (int i = 1; i < 12; ++i) {
             const int k = O[i];
-            const double dk = LA[13 * k];
+            const double dk = LA[(kEpR + 1) * k];
             int jx = i - 1;
-            while (jx >= 0 && LA[13 * O[jx]] < dk) {
+            while (jx >= 0 && LA[(kEpR + 1) * O[jx]] < dk) {
                 O[jx + 1] = O[jx];
                 --jx;
             }
@@ -1327,7 +1331,7 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_b
     ep_wave_sync();
     if (lane < 12) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) E[64 + 12 * i + lane] = LV[12 * lane + O[11 - i]];  // ut[i][j] = V[j][o[11 - i]]
+        for (int i = 0; i < 4; ++i) E[64 + 12 * i + lane] = LV[kEpR * lane + O[11 - i]];  // ut[i][j] = V[j][o[11 - i]]
     }
 }
 
