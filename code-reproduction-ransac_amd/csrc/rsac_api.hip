@@ -124,7 +124,9 @@ struct rsac_ctx {
     float *d_thr2 = nullptr;
     DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
     DevBuf mxpts;                                              // MFMA point operands (PF, UV: 40 B / point)
-    DevBuf epnp5;                                              // EPnP-5 minimal solve: 112 doubles / hypothesis
+    DevBuf epnp5;                                              // EPnP-5 minimal solve: kEpnpRec doubles / hypothesis of a launch
+    DevBuf direct;                                             // count == model_points problems (direct_solve)
+    PinBuf h_direct;
     DevBuf loc;                                                // location search: inputs, pos2, H, err
     DevBuf lo;                                                 // LO-RANSAC: 2 model records, chain state, 2 masks
     const void *lo_state_base = nullptr;                       // the lo allocation whose LoState is zeroed
@@ -346,15 +348,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     HIPCHK(c->fconst.ensure(sizeof(float) * kFconstStride * P));
     a.queue = c->queue.as<int>();
     a.exact_only = (flags & RSAC_F_EXACT_ONLY) ? 1 : 0;
-    a.sample_k = (flags & RSAC_F_MINIMAL_EPNP5) ? 5 : 4;
-    const char *split = getenv("RSAC_EPNP5_SPLIT");  // "0": the one-kernel form (A/B)
-    if (a.sample_k == 5 && !(split && split[0] == '0')) {
-        // the three-launch EPnP-5 solve's records, one per hypothesis record of c->models (sized
-        // by ensure_hyp_buffers before this call)
-        const size_t recs = c->models.cap / (sizeof(double) * kModelStride);
-        HIPCHK(c->epnp5.ensure(std::max<size_t>(recs, 1) * 112 * sizeof(double)));
-        a.epnp = c->epnp5.as<double>();
-    }
+    a.sample_k = (flags & RSAC_F_MINIMAL_EPNP5) ? 5 : 4;  // EPnP-5: ensure_epnp5 before each solve
     a.dbg_cell_pts = c->dbg_cell_pts;
     float *C = c->centred.as<float>();
     int32_t max_n = 0;
@@ -385,6 +379,20 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
         a.fmodels = c->fmodels.as<float>();
         a.fform = 2;  // MFMA records (form 1 for small rounds and out-of-f16-range problems)
     }
+    return RSAC_OK;
+}
+
+// the EPnP-5 solve's scratch for launches of up to P x H hypotheses (kEpnpRec doubles each, at
+// launch-local positions: one round's worth, not one per hypothesis record), within the resident
+// budget; a no-op for P3P
+int ensure_epnp5(rsac_ctx *c, PnpArgs &a, int32_t P, int64_t H) {
+    if (a.sample_k != 5) return RSAC_OK;
+    const size_t bytes = (size_t)std::max(P, 1) * (size_t)std::max<int64_t>(H, 1) * kEpnpRec * sizeof(double);
+    if (bytes > kMaxModelBytes)
+        return fail(RSAC_ENOMEM, "EPnP-5 scratch for %lld hypotheses exceeds the resident budget",
+                    (long long)P * (long long)H);
+    HIPCHK(c->epnp5.ensure(bytes));
+    a.epnp = c->epnp5.as<double>();
     return RSAC_OK;
 }
 
@@ -538,6 +546,10 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
 
     PnpArgs *pa = model == Model::PnP ? (PnpArgs *)args : nullptr;
     HomArgs *ha = model != Model::PnP ? (HomArgs *)args : nullptr;
+    if (pa) {  // a round is at most `round` hypotheses of each problem
+        r = ensure_epnp5(c, *pa, P, round);
+        if (r) return r;
+    }
     // RANSACUpdateNumIters' model_points = the sample size (5 for the EPnP-5 minimal solver)
     const int model_points = model == Model::Fm ? 8 : pa ? pa->sample_k : 4;
     const int sk = model_points;  // indices per drawn subset
@@ -895,6 +907,115 @@ int pnp_finish(rsac_ctx *c, const Staged &st, const PnpArgs &a, const LoopOut &l
     return RSAC_OK;
 }
 
+// OpenCV's `count == model_points` branches ([OpenCV, unvendored] solvepnp.cpp solvePnPRansac,
+// fundam.cpp findHomography; reached from main_v1.py:497-502, testpro-K.py:72-75, main_v1.py:312):
+// no RANSAC.  The minimal kernel runs once on all the points in input order (no subset check), the
+// result is its model with every index an inlier, and there is no final solve (no LM / EPnP refit,
+// no homography LM).  PnP: 4 points -> P3P whatever the flags (model_points is 4 for
+// SOLVEPNP_P3P / AP3P and for npoints == 4), 5 points under the default flags -> EPnP
+// (model_points 5; RSAC_F_MINIMAL_EPNP5).  Homography: 4 points -> runKernel, method 0's path.
+// A failed solve -> no model and no inliers.  kind[p] = the direct sample size of problem p, 0 for
+// a RANSAC problem.
+std::vector<int8_t> direct_kinds(const Staged &st, Model model, int sample_k, int &count) {
+    std::vector<int8_t> kind(st.P, 0);
+    count = 0;
+    for (int p = 0; p < st.P; ++p) {
+        const int64_t np = st.off[p + 1] - st.off[p];
+        int8_t k = 0;
+        if (model == Model::PnP)
+            k = np == 4 ? 4 : (np == 5 && sample_k == 5) ? 5 : 0;
+        else if (model == Model::Hom)
+            k = np == 4 ? 4 : 0;
+        kind[p] = k;
+        count += k != 0;
+    }
+    return kind;
+}
+
+// the direct problems' minimal solves (one record per problem and kind, sample = 0 .. k-1 with
+// status 1, every other problem status -1 so the kernels skip it), then k_direct_finish: their
+// records -> c->bestmodels / the pinned c->h_bestmodels and their mask rows (dmask, device) set
+// to 1 (model) or 0.  The caller synchronises, then reads the outcome with direct_apply.
+int direct_solve(rsac_ctx *c, Model model, const Staged &st, const void *args, const std::vector<int8_t> &kind,
+                 uint8_t *dmask, hipStream_t s) {
+    const int P = st.P;
+    // device layout: rec4, rec5 (P x kModelStride f64 each) | sub4 (P x 4), sub5 (P x 5) i32 |
+    // sst4, sst5, st4, st5, kind (P i8 each)
+    const size_t recb = sizeof(double) * kModelStride * P, subb = sizeof(int32_t) * 9 * P;
+    const size_t bytes = 2 * recb + subb + 5 * (size_t)P;
+    HIPCHK(c->direct.ensure(bytes));
+    HIPCHK(c->h_direct.ensure(subb + 5 * (size_t)P));
+    char *d = c->direct.as<char>();
+    double *rec4 = (double *)d, *rec5 = rec4 + (size_t)kModelStride * P;
+    int32_t *dsub4 = (int32_t *)(d + 2 * recb), *dsub5 = dsub4 + 4 * (size_t)P;
+    int8_t *dsst4 = (int8_t *)(d + 2 * recb + subb), *dsst5 = dsst4 + P, *dst4 = dsst5 + P, *dst5 = dst4 + P,
+           *dkind = dst5 + P;
+    char *h = c->h_direct.as<char>();
+    int32_t *hsub4 = (int32_t *)h, *hsub5 = hsub4 + 4 * (size_t)P;
+    int8_t *hsst4 = (int8_t *)(h + subb), *hsst5 = hsst4 + P, *hkind = hsst5 + 3 * (size_t)P;
+    bool any5 = false;
+    for (int p = 0; p < P; ++p) {
+        for (int j = 0; j < 4; ++j) hsub4[4 * p + j] = j;
+        for (int j = 0; j < 5; ++j) hsub5[5 * p + j] = j;
+        hsst4[p] = kind[p] == 4 ? 1 : -1;
+        hsst5[p] = kind[p] == 5 ? 1 : -1;
+        hkind[p] = kind[p];
+        any5 = any5 || kind[p] == 5;
+    }
+    HIPCHK(hipMemcpyAsync(dsub4, h, subb + 2 * (size_t)P, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dkind, hkind, P, hipMemcpyHostToDevice, s));
+    if (model == Model::PnP) {
+        for (int k = 4; k <= 5; ++k) {
+            if (k == 5 && !any5) break;
+            PnpArgs ad = *(const PnpArgs *)args;
+            ad.models = k == 4 ? rec4 : rec5;
+            ad.status = k == 4 ? dst4 : dst5;
+            ad.hyp_stride = 1;
+            ad.subsets = k == 4 ? dsub4 : dsub5;
+            ad.sub_status = k == 4 ? dsst4 : dsst5;
+            ad.sample_k = k;
+            ad.counts_out = nullptr;
+            ad.fmodels = nullptr;
+            ad.queue = nullptr;
+            ad.best_key = nullptr;
+            int r = ensure_epnp5(c, ad, P, 1);
+            if (r) return r;
+            HIPCHK(launch_pnp_solve(ad, P, 0, 1, s));
+        }
+    } else {
+        HomArgs ad = *(const HomArgs *)args;
+        ad.models = rec4;
+        ad.status = dst4;
+        ad.hyp_stride = 1;
+        ad.subsets = dsub4;
+        ad.sub_status = dsst4;
+        HIPCHK(launch_hom_solve(ad, P, 0, 1, s));
+    }
+    HIPCHK(c->bestmodels.ensure(sizeof(double) * kModelStride * P));
+    HIPCHK(c->h_bestmodels.ensure(sizeof(double) * kModelStride * P));
+    HIPCHK(launch_direct_finish(rec4, rec5, dkind, c->d_off, P, c->bestmodels.as<double>(),
+                                c->h_bestmodels.as<double>(), dmask, s));
+    return RSAC_OK;
+}
+
+// after the synchronisation that follows direct_solve: the direct problems' scan states (best 0 or
+// -1, every point or none an inlier, no iterations) and their rows of a host mask
+void direct_apply(rsac_ctx *c, const Staged &st, const std::vector<int8_t> &kind, std::vector<ScanState> &scan,
+                  uint8_t *host_mask) {
+    const double *bm = c->h_bestmodels.as<double>();
+    for (int p = 0; p < st.P; ++p) {
+        if (!kind[p]) continue;
+        const int np = (int)(st.off[p + 1] - st.off[p]);
+        const bool ok = bm[(size_t)kModelStride * p + kValidSlot] != 0.0;
+        ScanState &sc = scan[p];
+        sc.best = ok ? 0 : -1;
+        sc.max_good = ok ? np : 0;
+        sc.iter = 0;
+        sc.done = true;
+        if (host_mask) memset(host_mask + st.off[p], ok ? 1 : 0, np);
+    }
+}
+
 int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *offsets, int32_t P, int32_t n,
              const double *K, int32_t n_iters, double thr, double conf, uint64_t seed, uint32_t flags, double *R_out,
              double *t_out, int32_t *status_out, int32_t *ninl_out, uint8_t *mask_out, rsac_stats *stats,
@@ -913,8 +1034,10 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     int r = check_device(c);
     if (r) return r;
     if (P <= 0 || !K) return fail(RSAC_EINVAL, "bad problem count or K");
-    if (first_round && (P != 1 || !(flags & RSAC_F_ADAPTIVE) || (flags & RSAC_F_SAMPLER_OPENCV)))
-        return fail(RSAC_EINVAL, "first-round mode: one problem, adaptive, Philox sampler");
+    // (first-round mode continues in the caller with model_points 4: P3P only)
+    if (first_round &&
+        (P != 1 || !(flags & RSAC_F_ADAPTIVE) || (flags & (RSAC_F_SAMPLER_OPENCV | RSAC_F_MINIMAL_EPNP5))))
+        return fail(RSAC_EINVAL, "first-round mode: one problem, adaptive, Philox sampler, P3P");
     Staged st;
     r = stage_points(c, pts3d, pts2d, 3, offsets, P, n, flags, s, st, true);
     if (r) return r;
@@ -926,6 +1049,9 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     PnpArgs a;
     r = pnp_args(c, st, flags, seed, stride, 0, s, a);
     if (r) return r;
+    int n_direct = 0;  // problems of OpenCV's count == model_points branch (direct_kinds)
+    const std::vector<int8_t> dkind = direct_kinds(st, Model::PnP, a.sample_k, n_direct);
+    const bool all_direct = n_direct == P;
     // one adaptive problem: the device replays the first round's scan itself and the final mask
     // and refit are enqueued behind it, so the call synchronises once; the host verifies the
     // device's pick afterwards and redoes the call without speculation on a mismatch (a libm
@@ -951,6 +1077,18 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     mark(1);
     // first-round mode (rsac_pnp_ransac_first_round): the loop stops after its first round when
     // that round did not end the scan; the caller continues from the exported scan state
+    auto fill_stats = [&](rsac_stats &o) {
+        o = rsac_stats{};
+        o.best_hyp = lo.scan[0].best;
+        o.iters = lo.scan[0].iter;
+        o.hyps_scored = lo.scored;
+        o.n_inliers = lo.scan[0].max_good;
+        o.rounds = lo.rounds;
+        o.gpu_ms = lo.gpu_ms;
+        o.solve_ms = lo.solve_ms;
+        o.score_ms = lo.score_ms;
+        o.lo_improvements = lo.lo_improvements;
+    };
     auto more = [&]() -> int {
         const ScanState &sc = lo.scan[0];
         *first_round = rsac_scan_state{sc.niters, sc.best, sc.iter, sc.max_good, sc.done ? 1 : 0};
@@ -963,16 +1101,14 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
             if (t_out) memcpy(t_out, m + 9, 3 * sizeof(double));
         }
         if (ninl_out) ninl_out[0] = sc.max_good;
-        if (stats) {
-            stats->best_hyp = sc.best;
-            stats->iters = sc.iter;
-            stats->hyps_scored = lo.scored;
-            stats->n_inliers = sc.max_good;
-            stats->rounds = lo.rounds;
-            stats->lo_improvements = lo.lo_improvements;
-        }
+        if (stats) fill_stats(*stats);  // the first round's figures (timing fields included)
+        if (c->timing) fill_stats(c->last_stats);
         return RSAC_MORE;
     };
+    if (all_direct) {  // no RANSAC at all: direct_solve below is the whole call
+        lo.scan.assign(P, ScanState());
+        for (auto &sc : lo.scan) sc.reset(std::max(n_iters, 1));
+    } else {
     r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, spec ? &dec : nullptr, false,
                  first_round ? 1 : 0);
     if (r) return r;
@@ -1005,6 +1141,15 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
             if (r) return r;
         }
     }
+    }  // !all_direct
+    if (n_direct) {  // OpenCV's count == model_points problems: their minimal model, every point an inlier
+        const bool dev_mask = (flags & RSAC_F_DEVICE_OUT) && mask_out;
+        if (!dev_mask) HIPCHK(c->mask.ensure(std::max<int64_t>(st.total, 1)));
+        r = direct_solve(c, Model::PnP, st, &a, dkind, dev_mask ? mask_out : c->mask.as<uint8_t>(), s);
+        if (r) return r;
+        HIPCHK(hipStreamSynchronize(s));
+        direct_apply(c, st, dkind, lo.scan, dev_mask ? nullptr : mask_out);
+    }
 
     mark(4);
     const double *bm = c->h_bestmodels.as<double>();
@@ -1031,30 +1176,8 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
         const ScanState &sc = lo.scan[0];
         *first_round = rsac_scan_state{sc.niters, sc.best, sc.iter, sc.max_good, 1};
     }
-    if (c->timing) {
-        rsac_stats &ls = c->last_stats;
-        ls = rsac_stats{};
-        ls.best_hyp = lo.scan[0].best;
-        ls.iters = lo.scan[0].iter;
-        ls.hyps_scored = lo.scored;
-        ls.n_inliers = lo.scan[0].max_good;
-        ls.rounds = lo.rounds;
-        ls.gpu_ms = lo.gpu_ms;
-        ls.solve_ms = lo.solve_ms;
-        ls.score_ms = lo.score_ms;
-        ls.lo_improvements = lo.lo_improvements;
-    }
-    if (stats) {
-        stats->best_hyp = lo.scan[0].best;
-        stats->iters = lo.scan[0].iter;
-        stats->hyps_scored = lo.scored;
-        stats->n_inliers = lo.scan[0].max_good;
-        stats->rounds = lo.rounds;
-        stats->gpu_ms = lo.gpu_ms;
-        stats->solve_ms = lo.solve_ms;
-        stats->score_ms = lo.score_ms;
-        stats->lo_improvements = lo.lo_improvements;
-    }
+    if (c->timing) fill_stats(c->last_stats);
+    if (stats) fill_stats(*stats);
     mark(5);
     if (dbg_phases) {
         auto us = [&](int i, int j) { return std::chrono::duration<double, std::micro>(tp[j] - tp[i]).count(); };
@@ -1088,11 +1211,29 @@ int hom_core(rsac_ctx *c, const void *src, const void *dst, const int64_t *offse
     a.seed = seed;
     a.rng_base = 0;
     LoopOut lo;
-    r = run_loop(c, Model::Hom, st, &a, max_iters, conf, flags, s, lo);
-    if (r) return r;
+    int n_direct = 0;  // 4-point problems: findHomography's method-0 path (direct_kinds)
+    const std::vector<int8_t> dkind = direct_kinds(st, Model::Hom, 4, n_direct);
     const int64_t stride = std::max(max_iters, 1);
-    r = finish_masks(c, Model::Hom, st, &a, lo, stride, mask_out, flags, s);
-    if (r) return r;
+    if (n_direct == P) {
+        r = ensure_hyp_buffers(c, P, 1, false);
+        if (r) return r;
+        lo.scan.assign(P, ScanState());
+        for (auto &sc : lo.scan) sc.reset((int)stride);
+    } else {
+        r = run_loop(c, Model::Hom, st, &a, max_iters, conf, flags, s, lo);
+        if (r) return r;
+        r = finish_masks(c, Model::Hom, st, &a, lo, stride, mask_out, flags, s);
+        if (r) return r;
+    }
+    if (n_direct) {  // runKernel on the 4 points, mask all ones, no LM; rows of c->mask too (the
+                     // location search scores every problem from it)
+        const bool dev_mask = (flags & RSAC_F_DEVICE_OUT) && mask_out;
+        if (!dev_mask) HIPCHK(c->mask.ensure(std::max<int64_t>(st.total, 1)));
+        r = direct_solve(c, Model::Hom, st, &a, dkind, dev_mask ? mask_out : c->mask.as<uint8_t>(), s);
+        if (r) return r;
+        HIPCHK(hipStreamSynchronize(s));
+        direct_apply(c, st, dkind, lo.scan, dev_mask ? nullptr : mask_out);
+    }
     const double *bm = c->h_bestmodels.as<double>();
     std::vector<uint8_t> tmpmask;
     const uint8_t *hm = nullptr;
@@ -1178,11 +1319,11 @@ void rsac_destroy(rsac_ctx *c) {
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
                      &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
-                     &c->epnp, &c->epnp5, &c->lmscr, &c->setup_scr, &c->scanrec, &c->mxpts, &c->reproj};
+                     &c->epnp, &c->epnp5, &c->direct, &c->lmscr, &c->setup_scr, &c->scanrec, &c->mxpts, &c->reproj};
     for (DevBuf *b : dev) b->release();
     PinBuf *pin[] = {&c->h_lmfail, &c->h_pts, &c->h_small, &c->h_counts, &c->h_status, &c->h_subsets,
                      &c->h_substatus, &c->h_best, &c->h_bestmodels, &c->h_mask, &c->h_scanrec, &c->h_lo,
-                     &c->h_epnp, &c->h_rowinfo};
+                     &c->h_epnp, &c->h_rowinfo, &c->h_direct};
     for (PinBuf *b : pin) b->release();
     c->lo_state_base = nullptr;
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1748,6 +1889,8 @@ int rsac_pnp_evaluate_range(rsac_ctx *c, const void *pts3d, const void *pts2d, i
     r = pnp_args(c, st, flags, seed, n_hyps, hyp_begin, s, a, dkey);
     if (r) return r;
     const int32_t H = (int32_t)n_hyps;
+    r = ensure_epnp5(c, a, 1, H);
+    if (r) return r;
     const bool async = (flags & RSAC_F_ASYNC) != 0;
     // timing events only for a synchronous call that reports stats: each event record in the
     // stream costs a gap of several microseconds between the kernels around it
@@ -1850,6 +1993,8 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
         if (r) return r;
         a.subsets = subsets ? c->subsets.as<int32_t>() : nullptr;
         a.sub_status = subsets ? c->substatus.as<int8_t>() : nullptr;
+        r = ensure_epnp5(c, a, 1, H);
+        if (r) return r;
         HIPCHK(launch_pnp_solve(a, 1, 0, H, s));
         HIPCHK(launch_pnp_score(a, 1, 0, H, c->counts.as<int32_t>(), s));
     } else {

@@ -57,13 +57,17 @@ struct PnpArgs {
     // sample size and minimal solver: 4 = P3P (SOLVEPNP_P3P), 5 = EPnP on 5 points (the
     // default SOLVEPNP_ITERATIVE kernel, RSAC_F_MINIMAL_EPNP5); subsets then hold sample_k indices
     int32_t sample_k = 4;
-    // EPnP-5 minimal solve in three launches (k_epnp5_*): per hypothesis record kEpnpRec doubles
-    // of stage-1 results and eigenvectors; nullptr = the one-kernel form (k_pnp_solve_epnp5)
+    // EPnP-5 minimal solve in three launches (k_epnp5_*): kEpnpRec doubles of stage-1 results and
+    // eigenvectors per hypothesis of one launch (P x H, launch-local positions); required when
+    // sample_k == 5
     double *epnp = nullptr;
     // test hook (RSAC_DBG_MF_CELL_PTS): > 0 splits every tile of the MFMA scorer into cells of
     // this many points (the unit-size sweep of scripts/mf_units.py); 0 = the launcher's policy
     int32_t dbg_cell_pts = 0;
 };
+
+// EPnP-5 solve scratch per hypothesis of one launch (doubles): EpnpStage1 (0..63) + 4 eigenvectors
+constexpr int kEpnpRec = 112;
 
 constexpr int kFrameStride = 16;
 constexpr int kFconstStride = 16;
@@ -147,6 +151,12 @@ hipError_t launch_best_key(const int32_t *counts, const int8_t *status, int32_t 
 // rec (device, P entries) or, with rec == nullptr, rec0 for the one problem
 hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_t P, double *out, hipStream_t s,
                                 int64_t rec0 = -1);
+
+// OpenCV's count == model_points branch: per problem with kind[p] = 4 / 5 the record p of rec4 /
+// rec5 (the minimal model of its points in input order) -> out[p] (+ host_out[p], pinned), and its
+// mask rows all 1 (model) or all 0 (none); kind[p] = 0: untouched.  kind, offsets on the device.
+hipError_t launch_direct_finish(const double *rec4, const double *rec5, const int8_t *kind, const int64_t *offsets,
+                                int32_t P, double *out, double *host_out, uint8_t *mask, hipStream_t s);
 
 // the problems' result rows (ok, n_inliers, R 9, t 3; f64, P x 14) on the device: info = P x
 // {record index (< 0: no model), n_inliers} int64 (host-pinned), models = the winners' records

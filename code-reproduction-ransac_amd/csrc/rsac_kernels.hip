@@ -877,67 +877,20 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 }
 
 // The default minimal solver of solvePnPRansac (SOLVEPNP_ITERATIVE: 5-point samples, EPnP on the
-// sample; OpenCV solvepnp.cpp PnPRansacCallback::runKernel), one lane per hypothesis: the same
-// record layout as k_pnp_solve.  rsac_math.h pnp_epnp_minimal<5> (the sums in pnp_epnp_host's
-// order for the 5 points) -- bit-identical to the host EPnP and the oracle's orc_pnp_minimal_epnp5.
-__global__ __launch_bounds__(256) void k_pnp_solve_epnp5(PnpArgs a, int64_t hyp_begin, int32_t H) {
-    const int prob = blockIdx.y;
-    const int hl = blockIdx.x * blockDim.x + threadIdx.x;
-    if (hl == 0 && prob == 0) {
-        if (a.queue) reset_pnp_queue(a.queue);
-    }
-    if (hl >= H) return;
-    const int64_t h = hyp_begin + hl;
-    const int64_t p0 = a.offsets[prob];
-    const int n = (int)(a.offsets[prob + 1] - p0);
-    const int64_t rec = (int64_t)prob * a.hyp_stride + h;
-    double *m = a.models + rec * kModelStride;
-    int32_t idx[5];
-    int8_t st = 1;
-    if (a.subsets) {
-        st = a.sub_status[rec];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) idx[j] = a.subsets[rec * 5 + j];
-    } else {
-        Philox rng;
-        rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
-        st = (n >= 5 && rng.subset<5>(n, idx) == 0) ? 1 : -1;
-    }
-    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
-    if (st > 0) {
-        float X[5], Y[5], Z[5], U[5], V[5];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int64_t i = p0 + idx[j];
-            X[j] = a.X[i]; Y[j] = a.Y[i]; Z[j] = a.Z[i]; U[j] = a.U[i]; V[j] = a.V[i];
-        }
-        const double *c = a.cams + 4 * prob;
-        st = pnp_epnp_minimal<5>(X, Y, Z, U, V, Cam{c[0], c[1], c[2], c[3]}, R, t) ? 1 : 0;
-        if (st == 0)
-            for (int q = 0; q < 9; ++q) R[q] = 0.0;
-        if (st == 0)
-            for (int q = 0; q < 3; ++q) t[q] = 0.0;
-    }
-#pragma unroll
-    for (int q = 0; q < 9; ++q) m[q] = R[q];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
-    m[kValidSlot] = st > 0 ? 1.0 : 0.0;
-    a.status[rec] = st;
-    if (a.counts_out) a.counts_out[rec] = 0;
-    if (a.fmodels)
-        write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
-                     a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
-}
-
-// The EPnP-5 minimal solve in three launches (RSAC_EPNP5_SPLIT, the default): the 12 x 12 Jacobi
-// eigen-decomposition of M^T M, ~88 % of the solve's arithmetic, runs on 16 lanes per hypothesis
-// (one row of A and of V per lane, the rotation parameters and the exchanged rows through
-// ds_bpermute) instead of in one lane's scratch memory; the stages before and after it stay one
-// lane per hypothesis.  Every element sees the operations of jacobi_eig<12> in the same order, so
-// the records are bit-identical to k_pnp_solve_epnp5's (and the oracle's orc_pnp_minimal_epnp5).
-// Per hypothesis a.epnp holds EpnpStage1 (doubles 0..63) and the 4 eigenvectors ut (64..111).
-constexpr int kEpnpRec = 112;
+// sample; OpenCV solvepnp.cpp PnPRansacCallback::runKernel) in three launches: k_epnp5_a (sample,
+// stage 1: centroid, principal axes, control-point pair sums; one lane per hypothesis), the 12 x 12
+// eigen-decomposition of M^T M (~88 % of the arithmetic) by the round-robin Jacobi of
+// jacobi_eig_rr<12> on 16 lanes per hypothesis (k_epnp5_jacobi; rows of A and V per lane, the
+// step-start matrix mirrored in LDS for the pair parameters and the row exchange) or one wave per
+// hypothesis for short rounds (k_epnp5_jacobi_w), then k_epnp5_c (L, rho, the three beta estimates
+// and their poses, 4 lanes per hypothesis).  Every element sees jacobi_eig_rr's operations in its
+// order (the rotation formula and skip rule of jrr_rotation), so the records are bit-identical to
+// rsac_math.h pnp_epnp_minimal<5> and the oracle's orc_pnp_minimal_epnp5 (ep_jacobi_rr).  (The
+// round-robin order replaced round 3's cyclic jacobi_eig<12>: EPnP's numerics changed with it, in
+// the oracle and the host EPnP alike.)
+// Per hypothesis a.epnp holds EpnpStage1 (doubles 0..63) and the 4 eigenvectors ut (64..111), at
+// the launch-local position prob * H + hl (the three launches share hyp_begin and H), so the
+// scratch is sized by one launch's P x H (ensure_epnp5), not by the hypothesis records.
 static_assert(sizeof(EpnpStage1) <= 64 * sizeof(double), "EpnpStage1 exceeds its slot");
 
 // the sample of hypothesis rec (OpenCV subsets or Philox), status 1 drawn / -1 not
@@ -996,7 +949,7 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
         epnp_stage1(red, Cam{cm[0], cm[1], cm[2], cm[3]}, s1);
     }
     a.status[rec] = st;
-    *reinterpret_cast<EpnpStage1 *>(a.epnp + rec * kEpnpRec) = s1;
+    *reinterpret_cast<EpnpStage1 *>(a.epnp + ((int64_t)prob * H + hl) * kEpnpRec) = s1;
 }
 
 // 2 of 3: M^T M's eigenvectors by the round-robin Jacobi of jacobi_eig_rr<12>, 16 lanes per
@@ -1111,7 +1064,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
     const int j = threadIdx.x & (kEpG - 1), hb = threadIdx.x / kEpG;
     const int hl = (int)((blockIdx.x * 256u + threadIdx.x) / kEpG);
     const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
-    double *E = a.epnp + rec * kEpnpRec;
+    double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;  // launch-local scratch
     const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
     const bool live = hl < H && a.status[rec] > 0 && s1->ok != 0.0;
     const bool row = j < 12;
@@ -1267,7 +1220,7 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_b
     const int lane = threadIdx.x & 63, hb = threadIdx.x >> 6;
     const int hl = (int)((blockIdx.x * 256u + threadIdx.x) >> 6);
     const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
-    double *E = a.epnp + rec * kEpnpRec;
+    double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;  // launch-local scratch
     const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
     const bool live = hl < H && a.status[rec] > 0 && s1->ok != 0.0;  // wave-uniform
     if (!live) return;
@@ -1339,7 +1292,7 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_b
 // estimate, the lowest wins), 4 lanes per hypothesis: lane c < 3 takes estimate c + 1
 // (epnp_beta, epnp_pose_err: the loop bodies of epnp_stage2_post and epnp_stage3), the group
 // then applies epnp_stage3's rule (valid, lowest error, first on ties) to the three and lane 0
-// writes the records (as k_pnp_solve_epnp5)
+// writes the records (as k_pnp_solve does for P3P)
 __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1349,7 +1302,7 @@ __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, i
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
-    const double *E = a.epnp + rec * kEpnpRec;
+    const double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;  // launch-local scratch
     int8_t st = live ? a.status[rec] : -1;
     double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0}, err = 0.0, cen[3] = {0, 0, 0};
     bool mine = false;  // this lane's estimate gave a pose
@@ -2562,6 +2515,27 @@ __global__ void k_gather_models(const double *__restrict__ models, const int64_t
     out[i] = r >= 0 ? models[r * kModelStride + q] : 0.0;
 }
 
+// OpenCV's count == model_points branch (solvePnPRansac / findHomography): problem p's result is the
+// one minimal model of its points in input order -- record p of rec4 (4-point kind) or rec5 (5-point
+// kind) -- copied to out[p] (and the pinned host_out[p]), and every one of its points is an inlier
+// when that model exists, none when it does not.  One block per problem; kind[p] == 0: untouched.
+__global__ void k_direct_finish(const double *__restrict__ rec4, const double *__restrict__ rec5,
+                                const int8_t *__restrict__ kind, const int64_t *__restrict__ offsets,
+                                double *__restrict__ out, double *__restrict__ host_out, uint8_t *__restrict__ mask) {
+    const int p = blockIdx.x;
+    const int k = kind[p];
+    if (k == 0) return;
+    const double *m = (k == 5 ? rec5 : rec4) + (int64_t)p * kModelStride;
+    const bool ok = m[kValidSlot] != 0.0;
+    const int t = threadIdx.x;
+    if (t < kModelStride) {
+        out[(int64_t)p * kModelStride + t] = m[t];
+        if (host_out) host_out[(int64_t)p * kModelStride + t] = m[t];
+    }
+    const int64_t o = offsets[p];
+    if (mask && t < (int)(offsets[p + 1] - o)) mask[o + t] = ok ? 1 : 0;
+}
+
 // packed key of the best hypothesis of a range (count desc, index asc):
 // (count << 32) | (0xFFFFFFFF - (hyp_begin + h)); *key must be 0 on entry.
 __global__ __launch_bounds__(256) void k_best_key(const int32_t *__restrict__ counts,
@@ -3023,7 +2997,8 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
 constexpr int64_t kEpnpWaveMaxHyps = RSAC_EPNP_WAVE_MAX;  // one wave per hypothesis up to this many (2 waves/SIMD at 250 VGPRs: one round of waves; A/B knob)
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
-    if (a.sample_k == 5 && a.epnp) {  // the three-launch form (k_epnp5_a / _jacobi / _c)
+    if (a.sample_k == 5) {  // EPnP-5: the three-launch form (k_epnp5_a / _jacobi / _c)
+        if (!a.epnp) return hipErrorInvalidValue;  // its scratch (ensure_epnp5) is required
         hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
         // short rounds (an adaptive run's first 256 hypotheses): one wave per hypothesis (the round's
         // latency is one hypothesis' Jacobi); longer ones 16 lanes each
@@ -3033,8 +3008,7 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
             hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv((int64_t)kEpG * H, 256), P), dim3(256), 0, s, ka, hyp_begin,
                                H);
         hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-    } else if (a.sample_k == 5)
-        hipLaunchKernelGGL(k_pnp_solve_epnp5, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+    }
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     else if ((int64_t)P * H <= kSolve4MaxHyps)
         hipLaunchKernelGGL(k_pnp_solve4, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
@@ -3209,6 +3183,12 @@ hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
     if (g > 1024) g = 1024;
     hipLaunchKernelGGL(k_hom_mask, dim3(g, P), dim3(256), 0, s, a, best, best0, mask);
+    return hipGetLastError();
+}
+
+hipError_t launch_direct_finish(const double *rec4, const double *rec5, const int8_t *kind, const int64_t *offsets,
+                                int32_t P, double *out, double *host_out, uint8_t *mask, hipStream_t s) {
+    hipLaunchKernelGGL(k_direct_finish, dim3(P), dim3(64), 0, s, rec4, rec5, kind, offsets, out, host_out, mask);
     return hipGetLastError();
 }
 

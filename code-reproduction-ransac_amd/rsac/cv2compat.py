@@ -65,6 +65,9 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
         raise error("objectPoints and imagePoints differ in length")
     if P3.shape[0] < 4:
         raise error("solvePnPRansac needs at least 4 points")
+    # model_points: 4 for P3P / AP3P and for 4 points, 5 otherwise; when it equals the point count
+    # (4 points, or 5 under the other flags) the engine takes OpenCV's direct branch: one solvePnP
+    # on all points, every index an inlier, no final solve
     p3p = flags in (SOLVEPNP_P3P, SOLVEPNP_AP3P) or P3.shape[0] == 4
     refine = "epnp" if flags in (SOLVEPNP_P3P, SOLVEPNP_AP3P, SOLVEPNP_EPNP) else "lm"
     R, t, mask = api.pnp_ransac(P2, P3, cameraMatrix, int(iterationsCount), float(reprojectionError),
@@ -87,9 +90,12 @@ def findHomography(srcPoints, dstPoints, method=0, ransacReprojThreshold=3.0, ma
         raise error("findHomography needs at least 4 point correspondences")
     if method not in (0, RANSAC):
         raise NotImplementedError("only method=0 and cv2.RANSAC are provided")
-    if method == 0 or s.shape[0] == 4:
-        # all points, no RANSAC: one least-squares fit (as OpenCV does for method 0 / 4 points)
-        return api.homography_fit(s, d), np.ones((s.shape[0], 1), np.uint8)
+    if method == 0 and s.shape[0] > 4:
+        # all points, no RANSAC: runKernel's least-squares DLT, then the LM polish (npoints > 4)
+        H = api.homography_fit(s, d)
+        return H, (np.ones if H is not None else np.zeros)((s.shape[0], 1), np.uint8)
+    # RANSAC; 4 points (either method) take findHomography's `method == 0 || npoints == 4` branch
+    # inside the engine: runKernel on the 4 points, mask all ones, no LM
     H, m = api.homography_ransac(s, d, float(ransacReprojThreshold), max_iters=int(maxIters),
                                  confidence=float(confidence))
     return H, np.asarray(m, np.uint8).reshape(-1, 1)

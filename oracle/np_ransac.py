@@ -56,8 +56,15 @@ def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=1000,
     X, Y, Z = (soa[0].astype(np.float64), soa[1].astype(np.float64), soa[2].astype(np.float64))
     U, V = soa[3], soa[4]
     thr2 = np.float32(O.thr2(thr))
-    subsets, sst = O.mwc_subsets(n, max(max_iters, 1), s=k)
     solve = O.pnp_minimal_epnp5 if k == 5 else (lambda s, c, idx: O.pnp_minimal(s, idx, c))
+    if n == 4 or (n == 5 and k == 5):
+        # solvePnPRansac's model_points == npoints branch: one solvePnP on all points (P3P for 4),
+        # every index an inlier, no RANSAC (pyoracle.pnp_ransac / rsac_oracle.c pnp_direct)
+        m = (O.pnp_minimal if n == 4 else (lambda s, idx, c: O.pnp_minimal_epnp5(s, c, idx)))(soa, np.arange(n), cam)
+        if m is None:
+            return dict(best=-1, n_inliers=0, iters=0, R=None, t=None, mask=np.zeros(n, bool))
+        return dict(best=0, n_inliers=n, iters=0, R=m[0], t=m[1], mask=np.ones(n, bool))
+    subsets, sst = O.mwc_subsets(n, max(max_iters, 1), s=k)
     niters = max(max_iters, 1)
     best, max_good, best_model = -1, 0, None
     i = 0

@@ -270,6 +270,9 @@ def pnp_hypotheses(soa, cam, thr, seed, H, hyp0=0, problem=0, subsets=None, sub_
 
 def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED, sampler="philox",
                minimal="p3p"):
+    """orc_pnp_ransac_k: OpenCV's loop; 4 points (5 under minimal="epnp5") take solvePnPRansac's
+    count == model_points branch instead (one minimal solve on all points, every index an inlier,
+    best 0, iters 0)."""
     soa = soa_pnp(points3d, points2d)
     n = len(soa[0])
     cam = cam_from_K(K)
@@ -378,12 +381,17 @@ def estimate_camera_orientation(pos3d, pixels, Ks, thr=30.0, confidence=0.99, ma
     with ThreadPoolExecutor(max_workers=min(len(Ks), os.cpu_count() or 1, 16)) as ex:
         runs = list(ex.map(lambda K: pnp_ransac(P3, P2, K, thr, confidence, max_iters, seed, sampler=sampler,
                                                 minimal=minimal), Ks))
+    # solvePnPRansac's count == model_points branch (4 points; 5 under EPnP-5) has no final solve
+    direct = P3.shape[0] == 4 or (P3.shape[0] == 5 and minimal == "epnp5")
     for k, K in enumerate(Ks):
         r = runs[k]
         if r["best"] < 0:
             rows.append(None)
             continue
-        R, t, _ = pnp_refine(soa, r["mask"].astype(np.uint8), cam_from_K(K), r["R"], r["t"])
+        if direct:
+            R, t = r["R"], r["t"]
+        else:
+            R, t, _ = pnp_refine(soa, r["mask"].astype(np.uint8), cam_from_K(K), r["R"], r["t"])
         row = dict(R=R, t=t, mask=r["mask"], n_inliers=r["n_inliers"])
         rows.append(row)
         if r["n_inliers"] < min_inliers:

@@ -33,6 +33,11 @@
  *     numerics (OpenCV is absent).  PnP parity vs OpenCV is therefore *unpinned*
  *     except for the loose known-answer camera origin of testpro-K.py:234; GPU
  *     parity is against this restatement.
+ *   - OpenCV's count == model_points branches ([OpenCV, unvendored] solvepnp.cpp
+ *     solvePnPRansac: 4 points, or 5 under the default flags -> one solvePnP on
+ *     all points, every index an inlier, no final solve; fundam.cpp
+ *     findHomography: 4 points -> runKernel, mask all ones, no LM) are restated
+ *     in pnp_direct and orc_hom_ransac.
  *
  * Numerics contract shared with the HIP path (bit-exact on counts/masks):
  *   compile with -ffp-contract=off, no -ffast-math; only + - * / sqrt in any
@@ -1488,11 +1493,34 @@ ORC_API int orc_hom_refine(const float *sx, const float *sy, const float *dx, co
 /* sampler: 0 = Philox (seed, problem 0), 1 = OpenCV MWC (seed ignored).     */
 /* Returns best hypothesis index (<0: no model); mask = RANSAC-phase mask.   */
 /* ------------------------------------------------------------------------ */
+/* OpenCV's `model_points == npoints` branch of solvePnPRansac ([OpenCV 4.x, unvendored]
+ * modules/calib3d/src/solvepnp.cpp; call sites main_v1.py:497-502, testpro-K.py:72-75): no
+ * RANSAC.  model_points is 4 for SOLVEPNP_P3P / AP3P and for npoints == 4 (kernel P3P), 5
+ * otherwise (kernel EPnP), so 4 points always, and 5 points under the default flags (k == 5),
+ * call solvePnP once with that kernel on all the points in input order; every index is an
+ * inlier and there is no final solve.  A failed solve: no model, no inliers.
+ * Returns 1 when the branch applies (outputs written), 0 when RANSAC runs. */
+static int pnp_direct(const float *X, const float *Y, const float *Z, const float *U, const float *V, int n,
+                      const double cam[4], int k, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
+                      int64_t *iters_used, int64_t *best) {
+    if (!(n == 4 || (n == 5 && k == 5))) return 0;
+    static const int32_t idx[5] = {0, 1, 2, 3, 4};
+    const int ok = n == 4 ? orc_pnp_minimal(X, Y, Z, U, V, idx, cam, R, t)
+                          : orc_pnp_minimal_epnp5(X, Y, Z, U, V, idx, cam, R, t);
+    if (mask) memset(mask, ok ? 1 : 0, n);
+    if (n_inliers) *n_inliers = ok ? n : 0;
+    if (iters_used) *iters_used = 0;
+    *best = ok ? 0 : -1;
+    return 1;
+}
+
 /* k: the sample size / minimal solver (4 P3P, 5 EPnP), also RANSACUpdateNumIters' model_points */
 ORC_API int64_t orc_pnp_ransac_k(const float *X, const float *Y, const float *Z, const float *U, const float *V,
                                  int n, const double cam[4], double thr, double confidence, int max_iters,
                                  uint64_t seed, int sampler, int k, double R[9], double t[3], uint8_t *mask,
                                  int32_t *n_inliers, int64_t *iters_used) {
+    int64_t direct_best;
+    if (pnp_direct(X, Y, Z, U, V, n, cam, k, R, t, mask, n_inliers, iters_used, &direct_best)) return direct_best;
     int64_t H = max_iters > 1 ? max_iters : 1;
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * H);
     int8_t *status = (int8_t *)malloc(H);
@@ -1540,6 +1568,8 @@ ORC_API int64_t orc_pnp_ransac_seq_k(const float *X, const float *Y, const float
                                      int n, const double cam[4], double thr, double confidence, int max_iters,
                                      uint64_t seed, int sampler, int k, double R[9], double t[3], uint8_t *mask,
                                      int32_t *n_inliers, int64_t *iters_used) {
+    int64_t direct_best;
+    if (pnp_direct(X, Y, Z, U, V, n, cam, k, R, t, mask, n_inliers, iters_used, &direct_best)) return direct_best;
     const float thr2 = orc_thr2(thr);
     int64_t niters = max_iters > 1 ? max_iters : 1, best = -1, h = 0;
     int32_t good = 0;
@@ -1639,6 +1669,9 @@ static int64_t pnp_ransac_lo_impl(const float *X, const float *Y, const float *Z
                                   int n, const double cam[4], double thr, double confidence, int max_iters,
                                   uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
                                   int64_t *iters_used, int32_t *lo_improvements, int lazy) {
+    int64_t direct_best;
+    if (lo_improvements) *lo_improvements = 0;
+    if (pnp_direct(X, Y, Z, U, V, n, cam, 4, R, t, mask, n_inliers, iters_used, &direct_best)) return direct_best;
     int64_t H = max_iters > 1 ? max_iters : 1;
     const int64_t Hm = lazy ? 1 : H;
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * Hm);
@@ -1705,6 +1738,18 @@ ORC_API int64_t orc_pnp_ransac_lo_seq(const float *X, const float *Y, const floa
 ORC_API int64_t orc_hom_ransac(const float *sx, const float *sy, const float *dx, const float *dy, int n, double thr,
                                double confidence, int max_iters, uint64_t seed, int sampler, double Hout[9],
                                uint8_t *mask, int32_t *n_inliers, int64_t *iters_used) {
+    if (n == 4) {
+        /* findHomography's `method == 0 || npoints == 4` branch ([OpenCV 4.x, unvendored]
+         * modules/calib3d/src/fundam.cpp; main_v1.py:312): runKernel on the 4 points in input
+         * order (no checkSubset), mask all ones, and no LM (that runs only for npoints > 4).
+         * runKernel for 4 points is this build's minimal kernel (orc_hom_minimal). */
+        static const int32_t idx[4] = {0, 1, 2, 3};
+        const int ok = orc_hom_minimal(sx, sy, dx, dy, idx, Hout);
+        if (mask) memset(mask, ok ? 1 : 0, 4);
+        if (n_inliers) *n_inliers = ok ? 4 : 0;
+        if (iters_used) *iters_used = 0;
+        return ok ? 0 : -1;
+    }
     int64_t H = max_iters > 1 ? max_iters : 1;
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * H);
     int8_t *status = (int8_t *)malloc(H);

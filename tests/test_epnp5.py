@@ -8,8 +8,8 @@ rsac.cv2compat.solvePnPRansac.
 Oracle: orc_pnp_minimal_epnp5 (oracle/rsac_oracle.c) = orc_pnp_epnp on the 5 sampled points in
 sample order, the same restatement the final-solve EPnP tests pin (tests/test_epnp.py; "parity
 unpinned" against OpenCV itself, which is not installed).  Bar: bit-identical models, counts,
-winner, mask and iteration count between the GPU solve (k_epnp5_a / k_epnp5_jacobi / k_epnp5_c, or
-the one-kernel k_pnp_solve_epnp5 under RSAC_EPNP5_SPLIT=0) and the oracle.
+winner, mask and iteration count between the GPU solve (k_epnp5_a / k_epnp5_jacobi(_w) / k_epnp5_c)
+and the oracle.
 """
 import numpy as np
 import pytest
@@ -163,16 +163,3 @@ def test_gpu_cv2_default_flags_use_epnp5():
     assert ok4 and len(inl4) == 4
 
 
-@pytest.mark.gpu
-def test_gpu_epnp5_one_kernel_form_equals_split(monkeypatch):
-    """RSAC_EPNP5_SPLIT=0 (the one-kernel k_pnp_solve_epnp5, the Jacobi in one lane's scratch) and
-    the default three-launch solve give the same statuses, counts and model bits."""
-    pr = synth.pnp_problem(800, 0.4, seed=34)
-    args = ("pnp", pr["points3d"], pr["points2d"], pr["K"], 0, 512, 30.0)
-    st, cn, md = rsac.hypotheses(*args, seed=78, minimal="epnp5")
-    monkeypatch.setenv("RSAC_EPNP5_SPLIT", "0")
-    st1, cn1, md1 = rsac.hypotheses(*args, seed=78, minimal="epnp5")
-    np.testing.assert_array_equal(st, st1)
-    np.testing.assert_array_equal(cn, cn1)
-    assert (st > 0).sum() > 400
-    assert _bits_equal(md[:, :12], md1[:, :12])

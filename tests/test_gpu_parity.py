@@ -966,6 +966,9 @@ def test_fixed_budget_device_pick_batched(sampler, minimal):
         if ref["best"] < 0:
             assert R is None
             continue
+        if len(p["points3d"]) == 4:  # solvePnPRansac's count == model_points branch: no final solve
+            assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"]) and m.all()
+            continue
         soa, cam = O.soa_pnp(p["points3d"], p["points2d"]), O.cam_from_K(p["K"])
         Rl, tl, _ = O.pnp_refine(soa, ref["mask"].astype(np.uint8), cam, ref["R"].reshape(9), ref["t"])
         assert _bits_equal(R, Rl) and _bits_equal(t, tl)
