@@ -349,6 +349,7 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     a.queue = c->queue.as<int>();
     a.exact_only = (flags & RSAC_F_EXACT_ONLY) ? 1 : 0;
     a.sample_k = (flags & RSAC_F_MINIMAL_EPNP5) ? 5 : 4;  // EPnP-5: ensure_epnp5 before each solve
+    a.rvec_rt = (flags & RSAC_F_RVEC_ROUNDTRIP) ? 1 : 0;
     a.dbg_cell_pts = c->dbg_cell_pts;
     float *C = c->centred.as<float>();
     int32_t max_n = 0;

@@ -153,40 +153,10 @@ void scan_records(ScanState &s, const int32_t *idx, const int32_t *cnt, int nrec
     }
 }
 
-void rodrigues_v2m(const double r[3], double R[9]) {
-    double th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
-    if (th < DBL_EPSILON) {
-        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
-        return;
-    }
-    double c = cos(th), s = sin(th), c1 = 1. - c, it = 1. / th;
-    double x = r[0] * it, y = r[1] * it, z = r[2] * it;
-    R[0] = c + c1 * x * x;     R[1] = c1 * x * y - s * z; R[2] = c1 * x * z + s * y;
-    R[3] = c1 * x * y + s * z; R[4] = c + c1 * y * y;     R[5] = c1 * y * z - s * x;
-    R[6] = c1 * x * z - s * y; R[7] = c1 * y * z + s * x; R[8] = c + c1 * z * z;
-}
-
-void rodrigues_m2v(const double R[9], double r[3]) {
-    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
-    double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
-    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
-    c = c > 1. ? 1. : c < -1. ? -1. : c;
-    double th = acos(c);
-    if (s < 1e-5) {
-        if (c > 0) { r[0] = r[1] = r[2] = 0; return; }
-        double t;
-        t = (R[0] + 1) * 0.5; rx = sqrt(t > 0 ? t : 0);
-        t = (R[4] + 1) * 0.5; ry = sqrt(t > 0 ? t : 0) * (R[1] < 0 ? -1. : 1.);
-        t = (R[8] + 1) * 0.5; rz = sqrt(t > 0 ? t : 0) * (R[2] < 0 ? -1. : 1.);
-        if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
-        double nn = sqrt(rx * rx + ry * ry + rz * rz);
-        th = th / nn;
-        r[0] = rx * th; r[1] = ry * th; r[2] = rz * th;
-        return;
-    }
-    double vth = 1 / (2 * s) * th;
-    r[0] = rx * vth; r[1] = ry * vth; r[2] = rz * vth;
-}
+// cv::Rodrigues on the host: the deterministic forms of rsac_math.h (the device's and the
+// oracle's bits)
+void rodrigues_v2m(const double r[3], double R[9]) { rodrigues_v2m_det(r, R); }
+void rodrigues_m2v(const double R[9], double r[3]) { rodrigues_m2v_det(R, r); }
 
 namespace {
 

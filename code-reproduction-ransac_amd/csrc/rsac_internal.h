@@ -61,6 +61,9 @@ struct PnpArgs {
     // eigenvectors per hypothesis of one launch (P x H, launch-local positions); required when
     // sample_k == 5
     double *epnp = nullptr;
+    // RSAC_F_RVEC_ROUNDTRIP: the solve kernels replace each minimal model's R by
+    // Rodrigues(Rodrigues(R)) (rsac_math.h rodrigues_roundtrip) before writing its records
+    int32_t rvec_rt = 0;
     // test hook (RSAC_DBG_MF_CELL_PTS): > 0 splits every tile of the MFMA scorer into cells of
     // this many points (the unit-size sweep of scripts/mf_units.py); 0 = the launcher's policy
     int32_t dbg_cell_pts = 0;

@@ -859,6 +859,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 #else
         st = pnp_minimal_lam(X, Y, Z, U, V, k, yb, R, t) ? 1 : 0;
 #endif
+        if (st > 0 && a.rvec_rt) rodrigues_roundtrip(R);
     }
 #pragma unroll
     for (int q = 0; q < 9; ++q) m[q] = R[q];
@@ -1355,6 +1356,7 @@ __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, i
     if (st > 0) {
         const bool ok = s1ok && win >= 0;
         if (ok) lm_from_centred(R, cen, t);
+        if (ok && a.rvec_rt) rodrigues_roundtrip(R);
         st = ok ? 1 : 0;
         if (!ok)
             for (int q = 0; q < 9; ++q) R[q] = 0.0;
@@ -1456,6 +1458,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
     if (ok ? cand != win : cand != 0) return;  // one writer per hypothesis
     const int8_t sv = st > 0 ? (ok ? 1 : 0) : st;
     double *m = a.models + rec * kModelStride;
+    if (sv > 0 && a.rvec_rt) rodrigues_roundtrip(R);
     if (!ok)
         for (int q = 0; q < 9; ++q) R[q] = 0.0;
     if (!ok)

@@ -35,6 +35,168 @@ RSAC_HD double dabs(double v) { return __builtin_fabs(v); }
 RSAC_HD double dsqrt(double v) { return __builtin_sqrt(v); }
 
 // ---------------------------------------------------------------------------
+// Rodrigues (cv::Rodrigues, [OpenCV 4.x, unvendored] calibration.cpp cvRodrigues2; main_v1.py:895,
+// testpro-K.py:84) from + - * / sqrt only, so host, device and the oracle (rsac_oracle.c
+// orc_rodrigues_*) give the same bits: acos, sin and cos are polynomials with exactly rounded
+// series coefficients (about 1 ulp from the true values, not libm's bits), OpenCV's SVD
+// orthogonalisation R = U Vt is the polar factor by Newton's iteration.
+// ---------------------------------------------------------------------------
+constexpr double kPio2Hi = 0x1.921fb54442d18p+0, kPio2Lo = 0x1.1a62633145c07p-54;
+constexpr double kPio2A = 0x1.921fb544p+0, kPio2B = 0x1.0b4611a626331p-34;  // pi/2: 33 bits + the rest
+constexpr double k2OverPi = 0x1.45f306dc9c883p-1;
+
+// asin(x) = x + x z Q(z), z = x^2 <= 1/4: Q(z) = sum_k (2k)! / (4^k (k!)^2 (2k + 1)) z^(k-1), k = 1..26
+RSAC_HD double rodr_asin_q(double z) {
+    const double c[26] = {0x1.5555555555555p-3, 0x1.3333333333333p-4, 0x1.6db6db6db6db7p-5, 0x1.f1c71c71c71c7p-6,
+                          0x1.6e8ba2e8ba2e9p-6, 0x1.1c4ec4ec4ec4fp-6, 0x1.c99999999999ap-7, 0x1.7a87878787878p-7,
+                          0x1.3fde50d79435ep-7, 0x1.12ef3cf3cf3cfp-7, 0x1.df3bd37a6f4dfp-8, 0x1.a6863d70a3d71p-8,
+                          0x1.782dda12f684cp-8, 0x1.51ba308d3dcb1p-8, 0x1.31683bdef7bdfp-8, 0x1.15ee9d45d1746p-8,
+                          0x1.fcaf8fb6db6dbp-9, 0x1.d3d2a8e0dd67dp-9, 0x1.b026f57b13b14p-9, 0x1.90cb77f60c7cep-9,
+                          0x1.750de64d7d05fp-9, 0x1.5c5f56efaaaabp-9, 0x1.464c0950f7d47p-9, 0x1.3275586c5f2f0p-9,
+                          0x1.208d3570ae5a6p-9, 0x1.1052bc5fa960ap-9};
+    double p = c[25];
+#pragma unroll
+    for (int i = 24; i >= 0; --i) p = p * z + c[i];
+    return p;
+}
+
+// acos(x), x in [-1, 1] (callers clamp), with fdlibm's argument reduction
+RSAC_HD double rodr_acos(double x) {
+    if (x >= 1.0) return 0.0;
+    if (x <= -1.0) return 2.0 * kPio2Hi;
+    const double ax = dabs(x);
+    if (ax <= 0.5) {
+        const double z = x * x;
+        const double r = x * z * rodr_asin_q(z);  // asin(x) - x
+        return kPio2Hi - (x - (kPio2Lo - r));
+    }
+    const double z = (1.0 - ax) * 0.5;  // acos(|x|) = 2 asin(sqrt(z))
+    const double s = dsqrt(z);
+    const double w = s * z * rodr_asin_q(z);
+    if (x > 0.0) return 2.0 * (s + w);
+    return 2.0 * (kPio2Hi - (s + (w - kPio2Lo)));  // pi - 2 asin(s)
+}
+
+// sin and cos of th >= 0: the nearest multiple n of pi/2 taken off in two parts (exact products for
+// n < 2^20), then the Taylor polynomials on [-pi/4, pi/4] (to y^21 / y^22)
+RSAC_HD void rodr_sincos(double th, double &sn, double &cs) {
+    const double fn = (double)(int64_t)(th * k2OverPi + 0.5);
+    const int n = (int)((int64_t)fn & 3);
+    const double y = (th - fn * kPio2A) - fn * kPio2B;
+    const double z = y * y;
+    const double sc[10] = {-0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19,
+                           -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49,
+                           -0x1.2f49b46814157p-57, 0x1.71b8ef6dcf572p-66};
+    const double cc[10] = {0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22,
+                           0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45, -0x1.6827863b97d97p-53,
+                           0x1.e542ba4020225p-62, -0x1.0ce396db7f853p-70};
+    double ps = sc[9], pc = cc[9];
+#pragma unroll
+    for (int i = 8; i >= 0; --i) {
+        ps = ps * z + sc[i];
+        pc = pc * z + cc[i];
+    }
+    const double s = y + y * z * ps;
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + z * z * pc);
+    sn = n == 0 ? s : n == 1 ? c : n == 2 ? -s : -c;
+    cs = n == 0 ? c : n == 1 ? -s : n == 2 ? -c : s;
+}
+
+// OpenCV's R = U Vt (SVD::compute, the orthogonal polar factor) by Newton's iteration
+// X <- (X + X^-T) / 2, X^-T = cof(X) / det X, until no element moves by more than 1e-15 (at most
+// 30 steps: one for a rotation from a minimal solver); a singular X is left as it is
+RSAC_HD void rodr_polar(double X[9]) {
+    for (int it = 0; it < 30; ++it) {
+        double cf[9];
+        cf[0] = X[4] * X[8] - X[5] * X[7];
+        cf[1] = X[5] * X[6] - X[3] * X[8];
+        cf[2] = X[3] * X[7] - X[4] * X[6];
+        cf[3] = X[2] * X[7] - X[1] * X[8];
+        cf[4] = X[0] * X[8] - X[2] * X[6];
+        cf[5] = X[1] * X[6] - X[0] * X[7];
+        cf[6] = X[1] * X[5] - X[2] * X[4];
+        cf[7] = X[2] * X[3] - X[0] * X[5];
+        cf[8] = X[0] * X[4] - X[1] * X[3];
+        const double det = X[0] * cf[0] + X[1] * cf[1] + X[2] * cf[2];
+        if (!(dabs(det) > 1e-30) || !dfinite(det)) return;
+        const double id = 1.0 / det;
+        double mv = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const double nx = 0.5 * (X[k] + cf[k] * id);
+            const double d = dabs(nx - X[k]);
+            mv = d > mv ? d : mv;
+            X[k] = nx;
+        }
+        if (!(mv > 1e-15)) return;
+    }
+}
+
+// cv::Rodrigues vector -> matrix
+RSAC_HD void rodrigues_v2m_det(const double r[3], double R[9]) {
+    const double th = dsqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    if (th < 0x1p-52) {  // DBL_EPSILON
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    double s, c;
+    rodr_sincos(th, s, c);
+    const double c1 = 1. - c, it = 1. / th;
+    const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+    R[0] = c + c1 * x * x;     R[1] = c1 * x * y - s * z; R[2] = c1 * x * z + s * y;
+    R[3] = c1 * x * y + s * z; R[4] = c + c1 * y * y;     R[5] = c1 * y * z - s * x;
+    R[6] = c1 * x * z - s * y; R[7] = c1 * y * z + s * x; R[8] = c + c1 * z * z;
+}
+
+// cv::Rodrigues matrix -> vector: checkRange(R, -100, 100) (else zeros), R = U Vt, the angle from
+// the antisymmetric part, the theta ~ pi branch from the symmetric part
+RSAC_HD void rodrigues_m2v_det(const double Rin[9], double r[3]) {
+    double R[9];
+    bool in_range = true;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        R[k] = Rin[k];
+        in_range = in_range && dabs(R[k]) <= 100.0;
+    }
+    if (!in_range) {
+        r[0] = r[1] = r[2] = 0.0;
+        return;
+    }
+    rodr_polar(R);
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    const double s = dsqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double th = rodr_acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            r[0] = r[1] = r[2] = 0.0;
+            return;
+        }
+        double t;
+        t = (R[0] + 1) * 0.5; rx = dsqrt(t > 0 ? t : 0);
+        t = (R[4] + 1) * 0.5; ry = dsqrt(t > 0 ? t : 0) * (R[1] < 0 ? -1. : 1.);
+        t = (R[8] + 1) * 0.5; rz = dsqrt(t > 0 ? t : 0) * (R[2] < 0 ? -1. : 1.);
+        if (dabs(rx) < dabs(ry) && dabs(rx) < dabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+        th = th / dsqrt(rx * rx + ry * ry + rz * rz);
+        r[0] = rx * th; r[1] = ry * th; r[2] = rz * th;
+        return;
+    }
+    const double vth = 1 / (2 * s) * th;
+    r[0] = rx * vth; r[1] = ry * vth; r[2] = rz * vth;
+}
+
+// PnPRansacCallback keeps each minimal model as (rvec, tvec) and computeError projects through
+// Rodrigues(rvec): R' = Rodrigues(Rodrigues(R)) is the rotation OpenCV scores (RSAC_F_RVEC_ROUNDTRIP)
+RSAC_HD void rodrigues_roundtrip(double R[9]) {
+    double rv[3];
+    rodrigues_m2v_det(R, rv);
+    rodrigues_v2m_det(rv, R);
+}
+
+// ---------------------------------------------------------------------------
 // Philox-4x32-10: counter (hyp_lo, hyp_hi, problem, block), key = seed.
 // ---------------------------------------------------------------------------
 struct Philox {

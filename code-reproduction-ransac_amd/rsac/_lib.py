@@ -35,6 +35,7 @@ F_LO = 1 << 7
 F_ASYNC = 1 << 8
 F_EPNP = 1 << 9
 F_MINIMAL_EPNP5 = 1 << 10
+F_RVEC_ROUNDTRIP = 1 << 11
 
 DBG_REFIT_MAX_BLOCKS = 1
 DBG_REFIT_DROP_BLOCK = 2

@@ -69,8 +69,13 @@ def _device_of(inp: _In, device):
     return 0
 
 
-def _flags(adaptive, refine, sampler, exact_only=False, minimal="p3p"):
+def _flags(adaptive, refine, sampler, exact_only=False, minimal="p3p", rvec=None):
     f = 0
+    # rvec (PnP): each minimal model's rotation through Rodrigues(Rodrigues(R)) before it is scored,
+    # as OpenCV's PnPRansacCallback keeps the model as (rvec, tvec) (main_v1.py:497, testpro-K.py:72);
+    # default: on with OpenCV's sampler (the reference's own mode), off for Philox
+    if (sampler == "opencv") if rvec is None else rvec:
+        f |= L.F_RVEC_ROUNDTRIP
     # minimal: "p3p" (4-point samples, SOLVEPNP_P3P: this project's benchmark kernel, north_star's)
     # or "epnp5" (5-point samples solved by EPnP: solvePnPRansac's default SOLVEPNP_ITERATIVE
     # kernel, model_points 5 -- what the reference's calls run, main_v1.py:497, testpro-K.py:72)
@@ -144,7 +149,7 @@ def _K9(K) -> np.ndarray:
 def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
                confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox", adaptive: bool = True,
                refine: bool = True, device=None, return_info: bool = False, exact_only: bool = False,
-               lo: bool = False, minimal: str = "p3p"):
+               lo: bool = False, minimal: str = "p3p", rvec=None):
     """RANSAC PnP on the GPU: (points2D, points3D, K, n_iters, reproj_thresh) -> (R, t, inlier_mask).
 
     Defaults follow the reference call (iterationsCount=5000, reprojectionError=30,
@@ -154,6 +159,10 @@ def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float 
     lo=True runs LO-RANSAC (local optimisation at every new best; BASELINE.json C5).
     minimal="epnp5" samples 5 points and solves them with EPnP (OpenCV's default
     SOLVEPNP_ITERATIVE kernel; RANSACUpdateNumIters with model_points 5).
+    rvec (default: sampler == "opencv"): score each minimal model as Rodrigues(Rodrigues(R)), the
+    rotation OpenCV's computeError projects with.  4 points (5 under minimal="epnp5") take
+    solvePnPRansac's count == model_points branch: one minimal solve on all points, every index
+    an inlier, no final solve.
     """
     p3 = _In(points3D, 3)
     p2 = _In(points2D, 2)
@@ -163,7 +172,7 @@ def pnp_ransac(points2D, points3D, K, n_iters: int = 5000, reproj_thresh: float 
         raise ValueError("points3D and points2D must both be host arrays or both GPU tensors")
     n = p3.n
     ctx = L.context(_device_of(p3, device))
-    flags = _flags(adaptive, refine, sampler, exact_only, minimal) | (L.F_LO if lo else 0)
+    flags = _flags(adaptive, refine, sampler, exact_only, minimal, rvec) | (L.F_LO if lo else 0)
     if p3.device:
         flags |= L.F_DEVICE_IN
     K9 = _K9(K)
@@ -287,7 +296,7 @@ def _concat(parts, cols):
 
 def pnp_ransac_batched(points2D_list, points3D_list, K_list, n_iters: int = 5000, reproj_thresh: float = 30.0, *,
                        confidence: float = 0.99, seed: int = 0x5EED, sampler: str = "philox", adaptive: bool = True,
-                       refine: bool = True, device: int = 0, minimal: str = "p3p"):
+                       refine: bool = True, device: int = 0, minimal: str = "p3p", rvec=None):
     """P independent PnP problems in one call (K sweep of testpro-K.py:58-75, C3 of BASELINE.json).
 
     Returns a list of (R, t, mask, n_inliers) per problem (R, t None on failure).
@@ -303,7 +312,7 @@ def pnp_ransac_batched(points2D_list, points3D_list, K_list, n_iters: int = 5000
     if P and np.diff(off).min() < 4:
         raise ValueError("every problem needs >= 4 correspondences")
     ctx = L.context(device)
-    flags = _flags(adaptive, refine, sampler, minimal=minimal)
+    flags = _flags(adaptive, refine, sampler, minimal=minimal, rvec=rvec)
     R = np.zeros((P, 9))
     t = np.zeros((P, 3))
     status = np.zeros(P, np.int32)
@@ -541,14 +550,15 @@ def winner(points2D, points3D, K, key, reproj_thresh: float = 30.0, *, seed: int
 
 
 def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024, reproj_thresh: float = 30.0, *,
-               seed: int = 0x5EED, subsets=None, device=None, exact_only: bool = False, minimal: str = "p3p"):
+               seed: int = 0x5EED, subsets=None, device=None, exact_only: bool = False, minimal: str = "p3p",
+               rvec: bool = False):
     """Raw per-hypothesis (status, counts, models) of the GPU hot path for one problem.
 
     model "pnp": a = points3D (N,3), b = points2D (N,2), K required.
     model "homography": a = src (N,2), b = dst (N,2).
     model "fundamental": a = pts1 (N,2), b = pts2 (N,2).
     subsets: optional (n_hyps, 4) int32 index table replacing the Philox draw ((n_hyps, 5) for
-    minimal="epnp5", PnP's 5-point EPnP kernel).
+    minimal="epnp5", PnP's 5-point EPnP kernel).  rvec: PnP models through Rodrigues(Rodrigues(R)).
     """
     pnp = model == "pnp"
     if model not in ("pnp", "homography", "fundamental"):
@@ -557,6 +567,7 @@ def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024,
     B = _In(b, 2)
     ctx = L.context(_device_of(A, device))
     flags = (L.F_DEVICE_IN if A.device else 0) | (L.F_EXACT_ONLY if exact_only else 0)
+    flags |= L.F_RVEC_ROUNDTRIP if (rvec and pnp) else 0
     k = 4
     if minimal == "epnp5":
         if not pnp:
@@ -721,7 +732,7 @@ def intrinsics_grid(focal_lengths, sensor_sizes, image_size):
 def estimate_camera_orientation(pos3d, pixels, focal_lengths, sensor_sizes, image_size, known_camera_origin=None, *,
                                 n_iters: int = 5000, reproj_thresh: float = 30.0, confidence: float = 0.99,
                                 seed: int = 0x5EED, sampler: str = "opencv", minimal: str = "epnp5", refine="lm",
-                                min_inliers: int = 6, device: int = 0, return_info: bool = False):
+                                min_inliers: int = 6, device: int = 0, return_info: bool = False, rvec=None):
     """estimate_camera_orientation of testpro-K.py:39-125 as one GPU call sequence
     (rsac_pnp_orientation_sweep): solvePnPRansac under every candidate K (one batched launch), the
     mean inlier reprojection error of each on the device, the first K with the smallest, then
@@ -752,7 +763,7 @@ def estimate_camera_orientation(pos3d, pixels, focal_lengths, sensor_sizes, imag
     with ctx.lock:
         code = L.check(L.lib().rsac_pnp_orientation_sweep(
             ctx.handle, P3.ctypes.data, P2.ctypes.data, n, K9.ctypes.data, P, int(n_iters), float(reproj_thresh),
-            float(confidence), int(seed) & (2**64 - 1), _flags(True, refine, sampler, minimal=minimal), int(min_inliers),
+            float(confidence), int(seed) & (2**64 - 1), _flags(True, refine, sampler, minimal=minimal, rvec=rvec), int(min_inliers),
             C.byref(best), mean.ctypes.data, models.ctypes.data, status.ctypes.data, ninl.ctypes.data,
             masks.ctypes.data, R.ctypes.data, t.ctypes.data, None))
     ok = status == L.OK

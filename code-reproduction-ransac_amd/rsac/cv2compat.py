@@ -56,7 +56,8 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
     model_points = 5 in RANSACUpdateNumIters.  Final pose on the RANSAC inliers: EPnP for
     P3P / AP3P / EPNP (OpenCV re-solves P3P's inliers with EPnP); otherwise LM started from
     the best minimal model (SOLVEPNP_ITERATIVE's final solvePnP).  The inlier list is the
-    RANSAC-phase mask, as OpenCV returns it.
+    RANSAC-phase mask, as OpenCV returns it.  Each minimal model is scored through
+    Rodrigues(Rodrigues(R)), as PnPRansacCallback keeps it as an rvec (RSAC_F_RVEC_ROUNDTRIP).
     """
     _check_dist(distCoeffs)
     P3 = np.asarray(objectPoints, np.float64).reshape(-1, 3)
@@ -72,7 +73,7 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
     refine = "epnp" if flags in (SOLVEPNP_P3P, SOLVEPNP_AP3P, SOLVEPNP_EPNP) else "lm"
     R, t, mask = api.pnp_ransac(P2, P3, cameraMatrix, int(iterationsCount), float(reprojectionError),
                                 confidence=float(confidence), sampler="opencv", adaptive=True, refine=refine,
-                                minimal="p3p" if p3p else "epnp5")
+                                minimal="p3p" if p3p else "epnp5", rvec=True)
     if R is None:
         return False, (np.zeros((3, 1)) if rvec is None else rvec), (np.zeros((3, 1)) if tvec is None else tvec), None
     idx = np.flatnonzero(mask).astype(np.int32).reshape(-1, 1)

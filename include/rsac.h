@@ -78,6 +78,12 @@ extern "C" {
                                            RANSACUpdateNumIters); explicit subsets are then n x 5 */
 #define RSAC_F_LO (1u << 7)             /* LO-RANSAC (PnP, one problem): local optimisation at every new best,
                                            BASELINE.json configs[4]; see DESIGN.md "LO-RANSAC" */
+#define RSAC_F_RVEC_ROUNDTRIP (1u << 11) /* PnP: every minimal model's rotation goes through
+                                           R' = Rodrigues(Rodrigues(R)) before it is scored, as
+                                           OpenCV's PnPRansacCallback keeps (rvec, tvec) and
+                                           computeError projects through Rodrigues(rvec)
+                                           (main_v1.py:497, testpro-K.py:72); the deterministic
+                                           Rodrigues of rsac_rodrigues_* */
 
 typedef struct rsac_ctx rsac_ctx;
 
@@ -332,7 +338,10 @@ RSAC_EXPORT int rsac_pnp_orientation_sweep(rsac_ctx *ctx, const double *pts3d, c
                                            int32_t *status_out, int32_t *n_inliers_out, uint8_t *masks_out,
                                            double R_out[9], double t_out[3], void *stream);
 
-/* Rodrigues (cv2.Rodrigues, main_v1.py:895): vector <-> matrix. */
+/* Rodrigues (cv2.Rodrigues, main_v1.py:895): vector <-> matrix.  cvRodrigues2's steps (range
+ * check, SVD orthogonalisation as the polar factor, the theta ~ pi branch) from + - * / sqrt
+ * only: acos / sin / cos are series polynomials (~1 ulp), so the bits are the device's and the
+ * oracle's, not libm's. */
 RSAC_EXPORT void rsac_rodrigues_v2m(const double r[3], double R[9]);
 RSAC_EXPORT void rsac_rodrigues_m2v(const double R[9], double r[3]);
 

@@ -47,8 +47,9 @@ def compute_error(R, t, cam, X, Y, Z, U, V):
         return dx * dx + dy * dy
 
 
-def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=1000, minimal="epnp5"):
-    """OpenCV's sequential loop with NumPy scoring -> dict(best, n_inliers, iters, R, t, mask)."""
+def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=1000, minimal="epnp5", rvec=True):
+    """OpenCV's sequential loop with NumPy scoring -> dict(best, n_inliers, iters, R, t, mask).
+    rvec: each minimal model scored as Rodrigues(Rodrigues(R)) (PnPRansacCallback's rvec model)."""
     soa = O.soa_pnp(points3d, points2d)
     cam = O.cam_from_K(K)
     n = len(soa[0])
@@ -56,11 +57,18 @@ def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=1000,
     X, Y, Z = (soa[0].astype(np.float64), soa[1].astype(np.float64), soa[2].astype(np.float64))
     U, V = soa[3], soa[4]
     thr2 = np.float32(O.thr2(thr))
-    solve = O.pnp_minimal_epnp5 if k == 5 else (lambda s, c, idx: O.pnp_minimal(s, idx, c))
+    solve0 = O.pnp_minimal_epnp5 if k == 5 else (lambda s, c, idx: O.pnp_minimal(s, idx, c))
+
+    def solve(s, c, idx):
+        m = solve0(s, c, idx)
+        return m if (m is None or not rvec) else (O.rvec_roundtrip(m[0]), m[1])
+
     if n == 4 or (n == 5 and k == 5):
         # solvePnPRansac's model_points == npoints branch: one solvePnP on all points (P3P for 4),
         # every index an inlier, no RANSAC (pyoracle.pnp_ransac / rsac_oracle.c pnp_direct)
         m = (O.pnp_minimal if n == 4 else (lambda s, idx, c: O.pnp_minimal_epnp5(s, c, idx)))(soa, np.arange(n), cam)
+        if m is not None and rvec:
+            m = (O.rvec_roundtrip(m[0]), m[1])
         if m is None:
             return dict(best=-1, n_inliers=0, iters=0, R=None, t=None, mask=np.zeros(n, bool))
         return dict(best=0, n_inliers=n, iters=0, R=m[0], t=m[1], mask=np.ones(n, bool))

@@ -87,7 +87,7 @@ def lib():
     L.orc_pnp_hypotheses.restype = None
     L.orc_pnp_hypotheses_k.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_float, C.c_uint64,
                                        C.c_uint32, C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, _i32p, _i8p,
-                                       C.c_void_p]
+                                       C.c_void_p, C.c_int]
     L.orc_pnp_hypotheses_k.restype = None
     L.orc_pnp_minimal_epnp5.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, _i32p, _f64p, _f64p, _f64p]
     L.orc_pnp_minimal_epnp5.restype = C.c_int
@@ -110,7 +110,7 @@ def lib():
     L.orc_pnp_ransac.restype = C.c_int64
     L.orc_pnp_ransac_k.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
                                    C.c_int, C.c_uint64, C.c_int, C.c_int, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
-                                   C.POINTER(C.c_int64)]
+                                   C.POINTER(C.c_int64), C.c_int]
     L.orc_pnp_ransac_k.restype = C.c_int64
     L.orc_pnp_ransac_seq.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
                                      C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
@@ -118,7 +118,13 @@ def lib():
     L.orc_pnp_ransac_seq.restype = C.c_int64
     L.orc_pnp_ransac_seq_k.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
                                        C.c_int, C.c_uint64, C.c_int, C.c_int, _f64p, _f64p, _u8p,
-                                       C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_int]
+    L.orc_rvec_roundtrip.argtypes = [_f64p]
+    L.orc_rvec_roundtrip.restype = None
+    L.orc_rd_acos.argtypes = [C.c_double]
+    L.orc_rd_acos.restype = C.c_double
+    L.orc_rd_sincos.argtypes = [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.orc_rd_sincos.restype = None
     L.orc_pnp_ransac_seq_k.restype = C.c_int64
     L.orc_pnp_hypotheses_mt.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_float, C.c_uint64,
                                         C.c_int64, C.c_int64, _i32p, _i8p, C.c_int]
@@ -253,9 +259,10 @@ def pnp_count(R, t, soa, cam, thr, mask=False):
 
 
 def pnp_hypotheses(soa, cam, thr, seed, H, hyp0=0, problem=0, subsets=None, sub_status=None, models=False,
-                   minimal="p3p"):
+                   minimal="p3p", rvec=False):
     """minimal: "p3p" (4-point samples, SOLVEPNP_P3P) or "epnp5" (5-point samples, EPnP: the
-    default SOLVEPNP_ITERATIVE kernel of solvePnPRansac); subsets H x 4 or H x 5."""
+    default SOLVEPNP_ITERATIVE kernel of solvePnPRansac); subsets H x 4 or H x 5.  rvec: every
+    model's R -> Rodrigues(Rodrigues(R)) before it is counted (RSAC_F_RVEC_ROUNDTRIP)."""
     n = len(soa[0])
     k = 5 if minimal == "epnp5" else 4
     counts = np.zeros(H, np.int32)
@@ -264,15 +271,17 @@ def pnp_hypotheses(soa, cam, thr, seed, H, hyp0=0, problem=0, subsets=None, sub_
     subs = None if subsets is None else np.ascontiguousarray(subsets, np.int32)
     sst = None if sub_status is None else np.ascontiguousarray(sub_status, np.int8)
     lib().orc_pnp_hypotheses_k(*soa, n, cam, thr2(thr), seed, problem, hyp0, H, k, _ptr(subs), _ptr(sst), counts,
-                               status, _ptr(mdl))
+                               status, _ptr(mdl), int(bool(rvec)))
     return (counts, status, mdl) if models else (counts, status)
 
 
 def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED, sampler="philox",
-               minimal="p3p"):
+               minimal="p3p", rvec=None):
     """orc_pnp_ransac_k: OpenCV's loop; 4 points (5 under minimal="epnp5") take solvePnPRansac's
     count == model_points branch instead (one minimal solve on all points, every index an inlier,
-    best 0, iters 0)."""
+    best 0, iters 0).  rvec (default: sampler == "opencv", as rsac.pnp_ransac): the minimal
+    models' Rodrigues round trip."""
+    rvec = sampler == "opencv" if rvec is None else rvec
     soa = soa_pnp(points3d, points2d)
     n = len(soa[0])
     cam = cam_from_K(K)
@@ -282,9 +291,27 @@ def pnp_ransac(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000,
     good = C.c_int32(0)
     iters = C.c_int64(0)
     best = lib().orc_pnp_ransac_k(*soa, n, cam, thr, confidence, max_iters, seed, 1 if sampler == "opencv" else 0,
-                                  5 if minimal == "epnp5" else 4, R, t, mask, C.byref(good), C.byref(iters))
+                                  5 if minimal == "epnp5" else 4, R, t, mask, C.byref(good), C.byref(iters),
+                                  int(bool(rvec)))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value))
+
+
+def rvec_roundtrip(R):
+    """Rodrigues(Rodrigues(R)) in the deterministic restatement (orc_rvec_roundtrip)."""
+    R = np.ascontiguousarray(R, np.float64).reshape(9).copy()
+    lib().orc_rvec_roundtrip(R)
+    return R.reshape(3, 3)
+
+
+def rd_acos(x):
+    return lib().orc_rd_acos(float(x))
+
+
+def rd_sincos(th):
+    s, c = C.c_double(0), C.c_double(0)
+    lib().orc_rd_sincos(float(th), C.byref(s), C.byref(c))
+    return s.value, c.value
 
 
 def pnp_minimal_epnp5(soa, cam, idx):
@@ -295,10 +322,11 @@ def pnp_minimal_epnp5(soa, cam, idx):
 
 
 def pnp_ransac_seq(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED,
-                   sampler="philox", minimal="p3p"):
+                   sampler="philox", minimal="p3p", rvec=None):
     """OpenCV's loop one hypothesis at a time, stopping at the iteration bound (orc_pnp_ransac_seq_k;
     sampler "opencv" draws each iteration's MWC subset as OpenCV does, minimal "epnp5" = the default
-    SOLVEPNP_ITERATIVE kernel)."""
+    SOLVEPNP_ITERATIVE kernel); rvec as pnp_ransac."""
+    rvec = sampler == "opencv" if rvec is None else rvec
     soa = soa_pnp(points3d, points2d)
     n = len(soa[0])
     R, t = np.zeros(9), np.zeros(3)
@@ -307,7 +335,7 @@ def pnp_ransac_seq(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5
     iters = C.c_int64(0)
     best = lib().orc_pnp_ransac_seq_k(*soa, n, cam_from_K(K), thr, confidence, max_iters, seed,
                                       1 if sampler == "opencv" else 0, 5 if minimal == "epnp5" else 4, R, t, mask,
-                                      C.byref(good), C.byref(iters))
+                                      C.byref(good), C.byref(iters), int(bool(rvec)))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value))
 
@@ -363,13 +391,15 @@ def reproj_mean(points3d, points2d, K, R, t, mask):
 
 
 def estimate_camera_orientation(pos3d, pixels, Ks, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED,
-                                sampler="opencv", min_inliers=6, minimal="epnp5"):
+                                sampler="opencv", min_inliers=6, minimal="epnp5", rvec=None):
     """testpro-K.py:39-125 restated on the oracle's pieces: per K the RANSAC (pnp_ransac) + the LM
     final solve on its inliers (solvePnPRansac's SOLVEPNP_ITERATIVE final solvePnP), the gate,
     the mean inlier error through the pose's Rodrigues vector, the first strict minimum, then
     the LM refit (solvePnPRefineLM) of the winner on its inlier subset.  The defaults are the
     reference's own mode (testpro-K.py:72-75 passes no flags: SOLVEPNP_ITERATIVE = EPnP on 5-point
-    MWC samples, model_points 5); minimal="p3p" / sampler="philox" is the benchmark kernel."""
+    MWC samples, model_points 5); minimal="p3p" / sampler="philox" is the benchmark kernel.  rvec
+    (default: sampler == "opencv"): the minimal models' Rodrigues round trip."""
+    rvec = sampler == "opencv" if rvec is None else bool(rvec)
     P3 = np.asarray(pos3d, np.float64).reshape(-1, 3)
     P2 = np.asarray(pixels, np.float64).reshape(-1, 2)
     soa = soa_pnp(P3, P2)
@@ -380,7 +410,7 @@ def estimate_camera_orientation(pos3d, pixels, Ks, thr=30.0, confidence=0.99, ma
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(max_workers=min(len(Ks), os.cpu_count() or 1, 16)) as ex:
         runs = list(ex.map(lambda K: pnp_ransac(P3, P2, K, thr, confidence, max_iters, seed, sampler=sampler,
-                                                minimal=minimal), Ks))
+                                                minimal=minimal, rvec=rvec), Ks))
     # solvePnPRansac's count == model_points branch (4 points; 5 under EPnP-5) has no final solve
     direct = P3.shape[0] == 4 or (P3.shape[0] == 5 and minimal == "epnp5")
     for k, K in enumerate(Ks):

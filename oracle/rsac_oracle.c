@@ -758,12 +758,16 @@ ORC_API int orc_pnp_minimal_epnp5(const float *X, const float *Y, const float *Z
     return orc_pnp_epnp(x, y, z, u, v, m, 5, cam, R, t);
 }
 
+ORC_API void orc_rvec_roundtrip(double R[9]);
+
 /* k = 4: P3P on 4-point samples (SOLVEPNP_P3P); k = 5: EPnP on 5-point samples (the default).
- * subsets: H x k indices (the OpenCV sampler), else Philox subsets of size k. */
+ * subsets: H x k indices (the OpenCV sampler), else Philox subsets of size k.
+ * rvec_rt: each model's R -> Rodrigues(Rodrigues(R)) before it is counted (OpenCV keeps the
+ * model as rvec; RSAC_F_RVEC_ROUNDTRIP). */
 ORC_API void orc_pnp_hypotheses_k(const float *X, const float *Y, const float *Z, const float *U, const float *V,
                                   int n, const double cam[4], float thr2, uint64_t seed, uint32_t problem,
                                   int64_t hyp0, int64_t H, int k, const int32_t *subsets, const int8_t *sub_status,
-                                  int32_t *counts, int8_t *status, double *models) {
+                                  int32_t *counts, int8_t *status, double *models, int rvec_rt) {
     for (int64_t h = 0; h < H; ++h) {
         int32_t idx[5];
         double R[9] = {0}, t[3] = {0};
@@ -778,6 +782,7 @@ ORC_API void orc_pnp_hypotheses_k(const float *X, const float *Y, const float *Z
         if (st > 0) {
             st = (int8_t)(k == 5 ? orc_pnp_minimal_epnp5(X, Y, Z, U, V, idx, cam, R, t)
                                  : orc_pnp_minimal(X, Y, Z, U, V, idx, cam, R, t));
+            if (st && rvec_rt) orc_rvec_roundtrip(R);
             if (st) c = orc_pnp_count(R, t, cam, X, Y, Z, U, V, n, thr2, NULL);
         }
         counts[h] = c;
@@ -796,7 +801,7 @@ ORC_API void orc_pnp_hypotheses(const float *X, const float *Y, const float *Z, 
                                 int64_t H, const int32_t *subsets, const int8_t *sub_status, int32_t *counts,
                                 int8_t *status, double *models) {
     orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, problem, hyp0, H, 4, subsets, sub_status, counts, status,
-                         models);
+                         models, 0);
 }
 
 ORC_API void orc_hom_hypotheses(const float *sx, const float *sy, const float *dx, const float *dy, int n,
@@ -831,29 +836,129 @@ ORC_API void orc_hom_hypotheses(const float *sx, const float *sy, const float *d
 }
 
 /* ------------------------------------------------------------------------ */
-/* Rodrigues (cv::Rodrigues, main_v1.py:895)                                  */
+/* Rodrigues (cv::Rodrigues, main_v1.py:895; [OpenCV 4.x, unvendored]        */
+/* calibration.cpp cvRodrigues2).  The steps of cvRodrigues2 -- checkRange   */
+/* (-100, 100), the SVD orthogonalisation R = U Vt, the angle from the       */
+/* antisymmetric part, the theta ~ pi branch -- in + - * / sqrt only, so the */
+/* GPU (rsac_math.h rodrigues_*_det) gives the same bits: acos via fdlibm's  */
+/* reduction and the asin series (26 exactly rounded coefficients, |x|<=1/2),*/
+/* sin / cos via a 2-part pi/2 reduction and Taylor polynomials to y^22,     */
+/* U Vt as the polar factor by Newton's iteration X <- (X + X^-T)/2.          */
 /* ------------------------------------------------------------------------ */
+static const double RD_PIO2_HI = 0x1.921fb54442d18p+0, RD_PIO2_LO = 0x1.1a62633145c07p-54;
+static const double RD_PIO2_A = 0x1.921fb544p+0, RD_PIO2_B = 0x1.0b4611a626331p-34;
+static const double RD_2_OVER_PI = 0x1.45f306dc9c883p-1;
+/* (2k)! / (4^k (k!)^2 (2k+1)), k = 1..26: asin(x) = x + x z Q(z), z = x^2 */
+static const double RD_ASIN[26] = {
+    0x1.5555555555555p-3, 0x1.3333333333333p-4, 0x1.6db6db6db6db7p-5, 0x1.f1c71c71c71c7p-6, 0x1.6e8ba2e8ba2e9p-6,
+    0x1.1c4ec4ec4ec4fp-6, 0x1.c99999999999ap-7, 0x1.7a87878787878p-7, 0x1.3fde50d79435ep-7, 0x1.12ef3cf3cf3cfp-7,
+    0x1.df3bd37a6f4dfp-8, 0x1.a6863d70a3d71p-8, 0x1.782dda12f684cp-8, 0x1.51ba308d3dcb1p-8, 0x1.31683bdef7bdfp-8,
+    0x1.15ee9d45d1746p-8, 0x1.fcaf8fb6db6dbp-9, 0x1.d3d2a8e0dd67dp-9, 0x1.b026f57b13b14p-9, 0x1.90cb77f60c7cep-9,
+    0x1.750de64d7d05fp-9, 0x1.5c5f56efaaaabp-9, 0x1.464c0950f7d47p-9, 0x1.3275586c5f2f0p-9, 0x1.208d3570ae5a6p-9,
+    0x1.1052bc5fa960ap-9};
+/* (-1)^k / (2k+1)!, k = 1..10 and (-1)^k / (2k)!, k = 2..11 */
+static const double RD_SIN[10] = {-0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13,
+                                  0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33,
+                                  -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49, -0x1.2f49b46814157p-57,
+                                  0x1.71b8ef6dcf572p-66};
+static const double RD_COS[10] = {0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16,
+                                  -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37,
+                                  0x1.ae7f3e733b81fp-45, -0x1.6827863b97d97p-53, 0x1.e542ba4020225p-62,
+                                  -0x1.0ce396db7f853p-70};
+
+static double rd_horner(const double *c, int n, double z) {
+    double p = c[n - 1];
+    for (int i = n - 2; i >= 0; --i) p = p * z + c[i];
+    return p;
+}
+
+ORC_API double orc_rd_acos(double x) {
+    if (x >= 1.0) return 0.0;
+    if (x <= -1.0) return 2.0 * RD_PIO2_HI;
+    double ax = fabs(x);
+    if (ax <= 0.5) {
+        double z = x * x;
+        double r = x * z * rd_horner(RD_ASIN, 26, z);
+        return RD_PIO2_HI - (x - (RD_PIO2_LO - r));
+    }
+    double z = (1.0 - ax) * 0.5;
+    double s = sqrt(z);
+    double w = s * z * rd_horner(RD_ASIN, 26, z);
+    if (x > 0.0) return 2.0 * (s + w);
+    return 2.0 * (RD_PIO2_HI - (s + (w - RD_PIO2_LO)));
+}
+
+ORC_API void orc_rd_sincos(double th, double *sn, double *cs) {
+    double fn = (double)(int64_t)(th * RD_2_OVER_PI + 0.5);
+    int n = (int)((int64_t)fn & 3);
+    double y = (th - fn * RD_PIO2_A) - fn * RD_PIO2_B;
+    double z = y * y;
+    double ps = RD_SIN[9], pc = RD_COS[9];
+    for (int i = 8; i >= 0; --i) {
+        ps = ps * z + RD_SIN[i];
+        pc = pc * z + RD_COS[i];
+    }
+    double s = y + y * z * ps;
+    double hz = 0.5 * z, w = 1.0 - hz;
+    double c = w + (((1.0 - w) - hz) + z * z * pc);
+    *sn = n == 0 ? s : n == 1 ? c : n == 2 ? -s : -c;
+    *cs = n == 0 ? c : n == 1 ? -s : n == 2 ? -c : s;
+}
+
+/* polar factor of X (OpenCV: U Vt of SVD::compute): Newton steps until no element moves by more
+ * than 1e-15, at most 30; singular X unchanged */
+static void rd_polar(double X[9]) {
+    for (int it = 0; it < 30; ++it) {
+        double cf[9];
+        cf[0] = X[4] * X[8] - X[5] * X[7];
+        cf[1] = X[5] * X[6] - X[3] * X[8];
+        cf[2] = X[3] * X[7] - X[4] * X[6];
+        cf[3] = X[2] * X[7] - X[1] * X[8];
+        cf[4] = X[0] * X[8] - X[2] * X[6];
+        cf[5] = X[1] * X[6] - X[0] * X[7];
+        cf[6] = X[1] * X[5] - X[2] * X[4];
+        cf[7] = X[2] * X[3] - X[0] * X[5];
+        cf[8] = X[0] * X[4] - X[1] * X[3];
+        double det = X[0] * cf[0] + X[1] * cf[1] + X[2] * cf[2];
+        if (!(fabs(det) > 1e-30) || !isfinite(det)) return;
+        double id = 1.0 / det, mv = 0.0;
+        for (int k = 0; k < 9; ++k) {
+            double nx = 0.5 * (X[k] + cf[k] * id);
+            double d = fabs(nx - X[k]);
+            mv = d > mv ? d : mv;
+            X[k] = nx;
+        }
+        if (!(mv > 1e-15)) return;
+    }
+}
+
 ORC_API void orc_rodrigues_v2m(const double r[3], double R[9]) {
     double th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
     if (th < DBL_EPSILON) {
         for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
         return;
     }
-    double c = cos(th), s = sin(th), c1 = 1. - c, it = 1. / th;
+    double s, c;
+    orc_rd_sincos(th, &s, &c);
+    double c1 = 1. - c, it = 1. / th;
     double x = r[0] * it, y = r[1] * it, z = r[2] * it;
     R[0] = c + c1 * x * x;     R[1] = c1 * x * y - s * z; R[2] = c1 * x * z + s * y;
     R[3] = c1 * x * y + s * z; R[4] = c + c1 * y * y;     R[5] = c1 * y * z - s * x;
     R[6] = c1 * x * z - s * y; R[7] = c1 * y * z + s * x; R[8] = c + c1 * z * z;
 }
 
-ORC_API void orc_rodrigues_m2v(const double R[9], double r[3]) {
-    /* rotation angle/axis from the antisymmetric part, with the theta ~ pi
-     * branch taken from the symmetric part (as cv::Rodrigues does) */
+ORC_API void orc_rodrigues_m2v(const double Rin[9], double r[3]) {
+    double R[9];
+    for (int k = 0; k < 9; ++k) {
+        if (!(fabs(Rin[k]) <= 100.0)) { r[0] = r[1] = r[2] = 0; return; }  /* checkRange */
+        R[k] = Rin[k];
+    }
+    rd_polar(R);
     double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
     double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;
     c = c > 1. ? 1. : c < -1. ? -1. : c;
-    double th = acos(c);
+    double th = orc_rd_acos(c);
     if (s < 1e-5) {
         if (c > 0) { r[0] = r[1] = r[2] = 0; return; }
         double t;
@@ -861,13 +966,21 @@ ORC_API void orc_rodrigues_m2v(const double R[9], double r[3]) {
         t = (R[4] + 1) * 0.5; ry = sqrt(t > 0 ? t : 0) * (R[1] < 0 ? -1. : 1.);
         t = (R[8] + 1) * 0.5; rz = sqrt(t > 0 ? t : 0) * (R[2] < 0 ? -1. : 1.);
         if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
-        double n = sqrt(rx * rx + ry * ry + rz * rz);
-        th = th / n;
+        th = th / sqrt(rx * rx + ry * ry + rz * rz);
         r[0] = rx * th; r[1] = ry * th; r[2] = rz * th;
         return;
     }
     double vth = 1 / (2 * s) * th;
     r[0] = rx * vth; r[1] = ry * vth; r[2] = rz * vth;
+}
+
+/* PnPRansacCallback stores a minimal model as (rvec, tvec) and computeError projects through
+ * Rodrigues(rvec) (solvepnp.cpp; main_v1.py:497, testpro-K.py:72): the rotation it scores is
+ * Rodrigues(Rodrigues(R)) (RSAC_F_RVEC_ROUNDTRIP) */
+ORC_API void orc_rvec_roundtrip(double R[9]) {
+    double rv[3];
+    orc_rodrigues_m2v(R, rv);
+    orc_rodrigues_v2m(rv, R);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1501,12 +1614,13 @@ ORC_API int orc_hom_refine(const float *sx, const float *sy, const float *dx, co
  * inlier and there is no final solve.  A failed solve: no model, no inliers.
  * Returns 1 when the branch applies (outputs written), 0 when RANSAC runs. */
 static int pnp_direct(const float *X, const float *Y, const float *Z, const float *U, const float *V, int n,
-                      const double cam[4], int k, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
-                      int64_t *iters_used, int64_t *best) {
+                      const double cam[4], int k, int rvec_rt, double R[9], double t[3], uint8_t *mask,
+                      int32_t *n_inliers, int64_t *iters_used, int64_t *best) {
     if (!(n == 4 || (n == 5 && k == 5))) return 0;
     static const int32_t idx[5] = {0, 1, 2, 3, 4};
     const int ok = n == 4 ? orc_pnp_minimal(X, Y, Z, U, V, idx, cam, R, t)
                           : orc_pnp_minimal_epnp5(X, Y, Z, U, V, idx, cam, R, t);
+    if (ok && rvec_rt) orc_rvec_roundtrip(R);  /* the pose as Rodrigues(rvec) */
     if (mask) memset(mask, ok ? 1 : 0, n);
     if (n_inliers) *n_inliers = ok ? n : 0;
     if (iters_used) *iters_used = 0;
@@ -1518,9 +1632,10 @@ static int pnp_direct(const float *X, const float *Y, const float *Z, const floa
 ORC_API int64_t orc_pnp_ransac_k(const float *X, const float *Y, const float *Z, const float *U, const float *V,
                                  int n, const double cam[4], double thr, double confidence, int max_iters,
                                  uint64_t seed, int sampler, int k, double R[9], double t[3], uint8_t *mask,
-                                 int32_t *n_inliers, int64_t *iters_used) {
+                                 int32_t *n_inliers, int64_t *iters_used, int rvec_rt) {
     int64_t direct_best;
-    if (pnp_direct(X, Y, Z, U, V, n, cam, k, R, t, mask, n_inliers, iters_used, &direct_best)) return direct_best;
+    if (pnp_direct(X, Y, Z, U, V, n, cam, k, rvec_rt, R, t, mask, n_inliers, iters_used, &direct_best))
+        return direct_best;
     int64_t H = max_iters > 1 ? max_iters : 1;
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * H);
     int8_t *status = (int8_t *)malloc(H);
@@ -1534,7 +1649,7 @@ ORC_API int64_t orc_pnp_ransac_k(const float *X, const float *Y, const float *Z,
         orc_mwc_subsets(&st, n, k, H, NULL, NULL, NULL, NULL, subs, sst);
     }
     float thr2 = orc_thr2(thr);
-    orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, 0, 0, H, k, subs, sst, counts, status, models);
+    orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, 0, 0, H, k, subs, sst, counts, status, models, rvec_rt);
     int32_t good = 0;
     int64_t best = orc_scan(counts, status, H, n, k, confidence, max_iters, &good, iters_used);
     if (best >= 0) {
@@ -1554,7 +1669,7 @@ ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, c
                                int sampler, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
                                int64_t *iters_used) {
     return orc_pnp_ransac_k(X, Y, Z, U, V, n, cam, thr, confidence, max_iters, seed, sampler, 4, R, t, mask, n_inliers,
-                            iters_used);
+                            iters_used, 0);
 }
 
 /* The same loop as OpenCV runs it, one hypothesis at a time: it stops as soon as the iteration
@@ -1567,9 +1682,10 @@ ORC_API int64_t orc_pnp_ransac(const float *X, const float *Y, const float *Z, c
 ORC_API int64_t orc_pnp_ransac_seq_k(const float *X, const float *Y, const float *Z, const float *U, const float *V,
                                      int n, const double cam[4], double thr, double confidence, int max_iters,
                                      uint64_t seed, int sampler, int k, double R[9], double t[3], uint8_t *mask,
-                                     int32_t *n_inliers, int64_t *iters_used) {
+                                     int32_t *n_inliers, int64_t *iters_used, int rvec_rt) {
     int64_t direct_best;
-    if (pnp_direct(X, Y, Z, U, V, n, cam, k, R, t, mask, n_inliers, iters_used, &direct_best)) return direct_best;
+    if (pnp_direct(X, Y, Z, U, V, n, cam, k, rvec_rt, R, t, mask, n_inliers, iters_used, &direct_best))
+        return direct_best;
     const float thr2 = orc_thr2(thr);
     int64_t niters = max_iters > 1 ? max_iters : 1, best = -1, h = 0;
     int32_t good = 0;
@@ -1581,9 +1697,9 @@ ORC_API int64_t orc_pnp_ransac_seq_k(const float *X, const float *Y, const float
         double m[16];
         if (sampler == 1) {
             orc_mwc_subsets(&mwc, n, k, 1, NULL, NULL, NULL, NULL, sub, &sst);
-            orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, 0, h, 1, k, sub, &sst, &c, &st, m);
+            orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, 0, h, 1, k, sub, &sst, &c, &st, m, rvec_rt);
         } else {
-            orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, 0, h, 1, k, NULL, NULL, &c, &st, m);
+            orc_pnp_hypotheses_k(X, Y, Z, U, V, n, cam, thr2, seed, 0, h, 1, k, NULL, NULL, &c, &st, m, rvec_rt);
         }
         if (st < 0) break;
         if (st == 0) continue;
@@ -1611,7 +1727,7 @@ ORC_API int64_t orc_pnp_ransac_seq(const float *X, const float *Y, const float *
                                    uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
                                    int64_t *iters_used) {
     return orc_pnp_ransac_seq_k(X, Y, Z, U, V, n, cam, thr, confidence, max_iters, seed, 0, 4, R, t, mask, n_inliers,
-                                iters_used);
+                                iters_used, 0);
 }
 
 /* orc_pnp_hypotheses over `threads` host threads (OpenMP, hypotheses dealt in chunks of 64):
@@ -1671,7 +1787,7 @@ static int64_t pnp_ransac_lo_impl(const float *X, const float *Y, const float *Z
                                   int64_t *iters_used, int32_t *lo_improvements, int lazy) {
     int64_t direct_best;
     if (lo_improvements) *lo_improvements = 0;
-    if (pnp_direct(X, Y, Z, U, V, n, cam, 4, R, t, mask, n_inliers, iters_used, &direct_best)) return direct_best;
+    if (pnp_direct(X, Y, Z, U, V, n, cam, 4, 0, R, t, mask, n_inliers, iters_used, &direct_best)) return direct_best;
     int64_t H = max_iters > 1 ? max_iters : 1;
     const int64_t Hm = lazy ? 1 : H;
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * Hm);

@@ -39,11 +39,13 @@ def test_oracle_four_points_is_one_p3p_solve(sampler, minimal):
     soa, cam = O.soa_pnp(pr["points3d"], pr["points2d"]), O.cam_from_K(pr["K"])
     ref = O.pnp_minimal(soa, np.arange(4), cam)
     assert ref is not None
+    # OpenCV's sampler turns the Rodrigues round trip on: the pose is Rodrigues(rvec)
+    Rexp = O.rvec_roundtrip(ref[0]) if sampler == "opencv" else ref[0]
     for fn in (O.pnp_ransac, O.pnp_ransac_seq):
         r = fn(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 500, 0x5EED, sampler=sampler, minimal=minimal)
         assert (r["best"], r["n_inliers"], r["iters"]) == (0, 4, 0)
         assert r["mask"].all()
-        assert _bits_equal(r["R"], ref[0]) and _bits_equal(r["t"], ref[1])
+        assert _bits_equal(r["R"], Rexp) and _bits_equal(r["t"], ref[1])
 
 
 def test_oracle_five_points_default_flags_is_one_epnp_solve():
@@ -53,10 +55,14 @@ def test_oracle_five_points_default_flags_is_one_epnp_solve():
     assert ref is not None
     r = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 500, sampler="opencv", minimal="epnp5")
     assert (r["best"], r["n_inliers"], r["iters"]) == (0, 5, 0) and r["mask"].all()
-    assert _bits_equal(r["R"], ref[0]) and _bits_equal(r["t"], ref[1])
+    Rexp = O.rvec_roundtrip(ref[0])  # OpenCV's sampler: the pose as Rodrigues(rvec)
+    assert _bits_equal(r["R"], Rexp) and _bits_equal(r["t"], ref[1])
     npr = np_ransac.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 500, minimal="epnp5")
     assert (npr["best"], npr["n_inliers"], npr["iters"]) == (0, 5, 0)
-    assert _bits_equal(npr["R"], ref[0]) and _bits_equal(npr["t"], ref[1])
+    assert _bits_equal(npr["R"], Rexp) and _bits_equal(npr["t"], ref[1])
+    raw = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 500, sampler="opencv", minimal="epnp5",
+                       rvec=False)
+    assert _bits_equal(raw["R"], ref[0])
 
 
 def test_oracle_five_points_p3p_flags_run_ransac():
@@ -100,7 +106,7 @@ def test_oracle_sweep_direct_has_no_final_solve():
         if ref is None:
             assert row is None
         else:
-            assert _bits_equal(row["R"], ref[0]) and _bits_equal(row["t"], ref[1])
+            assert _bits_equal(row["R"], O.rvec_roundtrip(ref[0])) and _bits_equal(row["t"], ref[1])
 
 
 # ---------------------------------------------------------------------------------------------
@@ -204,12 +210,13 @@ def test_gpu_cv2_shim_direct():
     soa, cam = O.soa_pnp(pr["points3d"], pr["points2d"]), O.cam_from_K(pr["K"])
     ref = O.pnp_minimal_epnp5(soa, cam, np.arange(5))
     assert ok and inl.shape == (5, 1) and np.array_equal(inl.ravel(), np.arange(5))
-    assert _bits_equal(rvec, rsac.rodrigues(ref[0])) and _bits_equal(tvec.ravel(), ref[1])
+    # the shim's models go through the Rodrigues round trip (OpenCV keeps them as rvecs)
+    assert _bits_equal(rvec, rsac.rodrigues(O.rvec_roundtrip(ref[0]))) and _bits_equal(tvec.ravel(), ref[1])
     ok4, rvec4, tvec4, inl4 = cv2.solvePnPRansac(pr["points3d"][:4], pr["points2d"][:4], pr["K"], None,
                                                  flags=cv2.SOLVEPNP_EPNP)
     ref4 = O.pnp_minimal(soa, np.arange(4), cam)
     assert ok4 and np.array_equal(inl4.ravel(), np.arange(4))
-    assert _bits_equal(rvec4, rsac.rodrigues(ref4[0])) and _bits_equal(tvec4.ravel(), ref4[1])
+    assert _bits_equal(rvec4, rsac.rodrigues(O.rvec_roundtrip(ref4[0]))) and _bits_equal(tvec4.ravel(), ref4[1])
     bad = np.repeat(pr["points3d"][:1], 4, axis=0)
     okb, _, _, inlb = cv2.solvePnPRansac(bad, pr["points2d"][:4], pr["K"], None)
     assert not okb and inlb is None
