@@ -805,17 +805,9 @@ __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
 // ---------------------------------------------------------------------------
 // PnP: sample + minimal solve, one lane per hypothesis
 // ---------------------------------------------------------------------------
-// 154 VGPRs, 3 waves/SIMD: capping it at 128 (4 waves) or 96 (5) spills and is slower on C2 (latency-
-// bound, 1.5 waves/SIMD) and on C3 (1M hypotheses) alike (scripts/mf_ab.py + scripts/c3_prof.py)
-#ifndef RSAC_SOLVE_WAVES
-#define RSAC_SOLVE_WAVES 0  // A/B knob: > 0 asks for that many waves per SIMD (spills past 128 VGPRs)
-#endif
-#if RSAC_SOLVE_WAVES > 0
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_SOLVE_WAVES, 8))) void k_pnp_solve(
-    PnpArgs a, int64_t hyp_begin, int32_t H) {
-#else
+// 124 VGPRs, 4 waves/SIMD (r04: the best candidate held as its refined lambdas); asking for 5 waves
+// spills (scripts/ubench/probes_r04.patch keeps the knob)
 __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin, int32_t H) {
-#endif
     const int prob = blockIdx.y;
     const int hl = blockIdx.x * blockDim.x + threadIdx.x;
     // every round's scoring launch follows a solve on the same stream: reset its work queue here
@@ -854,11 +846,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
         double yb[9];
 #pragma unroll
         for (int j = 0; j < 3; ++j) bearing(k, U[j], V[j], yb + 3 * j);
-#ifdef RSAC_SOLVE_RT
-        st = pnp_minimal_yb(X, Y, Z, U, V, k, yb, R, t) ? 1 : 0;
-#else
         st = pnp_minimal_lam(X, Y, Z, U, V, k, yb, R, t) ? 1 : 0;
-#endif
         if (st > 0 && a.rvec_rt) rodrigues_roundtrip(R);
     }
 #pragma unroll
@@ -868,11 +856,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     m[kValidSlot] = st > 0 ? 1.0 : 0.0;
     a.status[rec] = st;
     if (a.counts_out) a.counts_out[rec] = 0;  // the scoring launch that follows may accumulate
-#ifdef RSAC_PROBE_NOFM
-    if (a.fmodels && a.hyp_stride < 0)  // timing probe only: the records of the previous call stay
-#else
     if (a.fmodels)
-#endif
         write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
                      a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
 }
@@ -1917,23 +1901,11 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 // waves per block of k_pnp_score_mf<W>: 4 for long problems; 2 for batches of short ones, whose
 // units then run twice the iterations per wave over the same unit overhead (launch_mf; C3
 // 1.081 -> 1.028 ms, while C2 at 2 waves is 66 % slower: scripts/mf_ab.py)
-// wave priority (s_setprio) of the scorer: 1 = raised (2) from the end of a wave's point loop
-// through its recounts, the count epilogue and the next unit's staging, back to 0 for the point
-// loop, so the waves a block's barriers wait for get the SIMD first (C2 scoring -1 %,
-// scripts/mf_ab.py r03d; 2 / 3 / 4: static priority by block group / wave probes)
-#ifndef RSAC_MF_PRIO
-#define RSAC_MF_PRIO 1
-#endif
-// 1: the group body as hand-scheduled inline asm (rsac_mf_asm.inc, scripts/gen_mf_asm.py): its
-// counts equal the compiler's body (the whole -m gpu suite green on it), and it is no faster
-// (C2 scoring 0.2329 against 0.2316 ms, C3 0.998 against 0.984 ms), so the
-// compiler's schedule stays the default
-#ifndef RSAC_MF_ASM
-#define RSAC_MF_ASM 0
-#endif
-#if RSAC_MF_ASM
-#include "rsac_mf_asm.inc"
-#endif
+// wave priority (s_setprio) of the scorer: raised (2) from the end of a wave's point loop through
+// its recounts, the count epilogue and the next unit's staging, back to 0 for the point loop, so
+// the waves a block's barriers wait for get the SIMD first (C2 scoring -1 %, scripts/mf_ab.py r03d).
+// (The static-priority and hand-scheduled asm probes of rounds 3-4 are kept as
+// scripts/ubench/probes_r04.patch; DESIGN.md §3 has their numbers.)
 #ifndef RSAC_MF_LONG_W
 #define RSAC_MF_LONG_W 4
 #endif
@@ -1990,16 +1962,6 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
             const float4 bv = *reinterpret_cast<const float4 *>(&ab[1][half][t][0]);
             const mf_f16v xa = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Ba, mf_f16v{}, 0, 0, 0);
             const mf_f16v xb = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ar[t], Bb, mf_f16v{}, 0, 0, 0);
-#if RSAC_MF_ASM
-            // the group's VALU stage by stage, its flags through one SGPR test (rsac_mf_asm.inc)
-            const float a4[4] = {av.x, av.y, av.z, av.w}, b4[4] = {bv.x, bv.y, bv.z, bv.w};
-            switch (t) {
-                case 0: mf_group_asm<0>(xa, xb, ua, ub, a4, b4, 0x0C0C0B09u, vc[0], fl); break;
-                case 1: mf_group_asm<1>(xa, xb, ua, ub, a4, b4, 0x0C0C0B09u, vc[1], fl); break;
-                case 2: mf_group_asm<2>(xa, xb, ua, ub, a4, b4, 0x0C0C0B09u, vc[2], fl); break;
-                default: mf_group_asm<3>(xa, xb, ua, ub, a4, b4, 0x0C0C0B09u, vc[3], fl); break;
-            }
-#else
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float ag = g == 0 ? av.x : g == 1 ? av.y : g == 2 ? av.z : av.w;
@@ -2008,7 +1970,6 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
                 vc[t][g] = mf_cnt255(vc[t][g], ra.D, rb.D);  // 255 x the count
                 fl |= __ballot(!(__builtin_fminf(ra.t, rb.t) > bg)) ? (1u << (4 * t + g)) : 0u;
             }
-#endif
         }
         if (__builtin_expect(fl != 0, 0)) {
             if (lane == 0) wrec[wave][nw] = make_uint2((uint32_t)i, fl);
@@ -2016,11 +1977,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
         }
     };
     const int full = n >= b0 + 64 ? (n - b0 - 64) / T + 1 : 0;  // iterations with 64 points in range
-#if RSAC_MF_PRIO == 1
     __builtin_amdgcn_s_setprio(0);
-#elif RSAC_MF_PRIO == 4
-    if ((blockIdx.x / kQSub) & 1) __builtin_amdgcn_s_setprio(1); else __builtin_amdgcn_s_setprio(0);
-#endif
     for (int i = 0; i < full; ++i) {
         mf_h8 Ba, Bb;
         float2 ua, ub;
@@ -2035,11 +1992,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
     }
     // the wave's flagged iterations recounted here: the wave's exact-test latency overlaps the
     // other blocks' waves on its SIMD
-#if RSAC_MF_PRIO == 1
     __builtin_amdgcn_s_setprio(2);
-#elif RSAC_MF_PRIO == 4
-    if ((blockIdx.x / kQSub) & 1) __builtin_amdgcn_s_setprio(3); else __builtin_amdgcn_s_setprio(2);
-#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
@@ -2108,17 +2061,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     const int cpx = (tb + kQSub - 1) / kQSub, tbx = cpx * kQSub;
     const int n_units = tbx + (tiles_per_prob * n_prob - tb) * cells;
     const int qk = blockIdx.x % kQSub;  // this block's units: qk + kQSub i, i from counter qk
-#if RSAC_MF_PRIO == 2
-    if ((blockIdx.x / kQSub) & 1) __builtin_amdgcn_s_setprio(1);
-#elif RSAC_MF_PRIO == 3
-    if (wave >= 2) __builtin_amdgcn_s_setprio(1);
-#endif
     int *const uq = unit_queue(queue, qk);
-#ifdef RSAC_MF_CLOCK
-    // diagnostic build (scripts/clock_probe.sh): the in-kernel shader clock of this block's
-    // lifetime, s_memtime (shader cycles) against s_memrealtime (100 MHz)
-    const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
     int last_prob = -1, n_all = 0;
     int64_t p0 = 0;
     bool in_range = false;
@@ -2175,11 +2118,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         }
         __syncthreads();  // the unit's LDS and the slot are rewritten by the next unit
     }
-#ifdef RSAC_MF_CLOCK
-    if (threadIdx.x == 0 && (blockIdx.x % 97) == 0)
-        printf("mfclock block %u cycles %llu realticks %llu\n", blockIdx.x, __builtin_amdgcn_s_memtime() - clk0,
-               __builtin_amdgcn_s_memrealtime() - rt0);
-#endif
 }
 
 
@@ -3116,12 +3054,6 @@ static hipError_t launch_mf_w(const PnpArgs &a, int32_t P_, int64_t hyp_begin, i
         cell_pts = cp;
         cell_tiles = tiles;
     }
-#ifdef RSAC_MF_FORCE_CELL  // A/B knob: every tile by cells of this many points
-    if (a.dbg_cell_pts <= 0) {
-        cell_pts = std::min<int64_t>(RSAC_MF_FORCE_CELL, win_pts);
-        cell_tiles = tiles;
-    }
-#endif
     if (a.dbg_cell_pts > 0) {  // test hook: every tile by cells of dbg_cell_pts points (a multiple of 256)
         cell_pts = std::min<int64_t>(std::max<int64_t>(256, a.dbg_cell_pts / 256 * 256), win_pts);
         cell_tiles = tiles;
