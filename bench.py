@@ -321,6 +321,9 @@ def multi_gpu_legs(local, args, pr2):
     dev = torch.device("cuda", local)
     sync = torch.cuda.synchronize
     out = {}
+    # what the line runs on: backend, world size as the backend sees it, an 8-byte all-reduce's latency,
+    # every rank's share of C3's problems and of C2's hypotheses
+    out["comm"] = par.comm_report(1024, args.hyps * world, sync=sync)
     p2, p3, off, Ks = c3_problems()
     g2, g3 = torch.from_numpy(p2).to(dev), torch.from_numpy(p3).to(dev)
     run = par.pnp_batched_rows(g2, g3, off, Ks, 1024, args.thr, adaptive=False, refine=False)
@@ -509,10 +512,22 @@ def extra_workloads(local, args):
         if i >= 1:
             walls_f.append(time.perf_counter() - t)
             sol_f.append(inff.solve_ms)
+    # the cost of OpenCV's Rodrigues round trip (RSAC_F_RVEC_ROUNDTRIP, on in the reference mode):
+    # the same 20k EPnP-5 solve with and without it, HIP events around the solve launches
+    rt_ms = {}
+    for rv in (False, True):
+        ms = []
+        for i in range(5):
+            _, _, _, inf_rt = rsac.pnp_ransac(g2, g3, p2c["K"], 20_000, args.thr, minimal="epnp5", adaptive=False,
+                                              refine=False, rvec=rv, return_info=True, device=local)
+            if i >= 1:
+                ms.append(inf_rt.solve_ms)
+        rt_ms[rv] = statistics.median(ms)
     out["c2_reference_mode"] = {"points": args.points, "ms_to_best": statistics.median(walls), "iters": infr.iters,
                                 "n_inliers": infr.n_inliers, "epnp5_fixed_hyps": 20_000,
                                 "epnp5_fixed_hyp_s": 20_000 / statistics.median(walls_f),
                                 "epnp5_solve_ms": statistics.median(sol_f),
+                                "epnp5_solve_ms_rvec_roundtrip": rt_ms[True], "epnp5_solve_ms_no_roundtrip": rt_ms[False],
                                 "note": "cv2.solvePnPRansac defaults (EPnP-5 minimal solver on MWC subsets, LM final "
                                         "solve) on the C2 problem, inputs in HBM, median of 10; the EPnP-5 solve "
                                         "runs as k_epnp5_a / k_epnp5_jacobi / k_epnp5_c; CPU leg in "
@@ -612,8 +627,11 @@ def _cpu_quota():
     return aff, quota
 
 
-def _median_rate(fn, units, samples=5):
-    """median over `samples` runs of units / seconds of fn() -> (rate, median seconds)"""
+def _median_rate(fn, units, samples=5, warmup=0):
+    """median over `samples` runs of units / seconds of fn(), after `warmup` untimed runs ->
+    (rate, median seconds)"""
+    for _ in range(warmup):
+        fn()
     walls = []
     for _ in range(samples):
         t = time.perf_counter()
@@ -625,11 +643,14 @@ def _median_rate(fn, units, samples=5):
 
 def cpu_baseline(pr, args):
     """The CPU restatement (oracle/, C, gcc -O3) on bounded samples of the same workloads, on this
-    host, each leg the median of 5 (C1: 7) samples: C2 on 1 thread (`value`), on the
-    OMP_NUM_THREADS share and on every CPU of the affinity mask, C2 ms-to-best (OpenCV's
-    sequential loop, stopping at the iteration bound), C1 (BASELINE.json configs[0]: the reference
-    plumbing, C restatement and the NumPy path), C3 (problems over the threads), C4 and C5 (LO,
-    sequential)."""
+    host: C2 on 1 thread (`value`), on the OMP_NUM_THREADS share and on every CPU of the affinity
+    mask, C2 ms-to-best (OpenCV's sequential loop, stopping at the iteration bound; P3P and the
+    reference's own EPnP-5 mode), C1 (BASELINE.json configs[0]: the reference plumbing, C
+    restatement and the NumPy path, under main_v1's K and under testpro-K's f = 150 mm K), C3
+    (problems over the threads), C4 (1 thread and the threads) and C5 (LO: OpenCV's sequential loop
+    on 1 thread, and its rounds' hypotheses over the threads).  Throughput legs: median of 5
+    samples; the short latency legs (C1, both ms-to-best legs): median of 21 after 3 warm-ups
+    (BASELINE.md)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import np_ransac as NR
@@ -649,19 +670,29 @@ def cpu_baseline(pr, args):
     rate_mt, w_mt = _median_rate(lambda: O.pnp_hypotheses_mt(soa, cam, args.thr, 0x5EED, n_mt, threads=threads), n_mt)
     n_all = 500 * aff
     rate_all, w_all = _median_rate(lambda: O.pnp_hypotheses_mt(soa, cam, args.thr, 0x5EED, n_all, threads=aff), n_all)
-    _, w_best = _median_rate(lambda: O.pnp_ransac_seq(pr["points3d"], pr["points2d"], pr["K"], args.thr, 0.99, 5000), 1)
-    # the reference call's own mode on the same problem (EPnP-5 on MWC subsets, main_v1.py:497-502)
+    _, w_best = _median_rate(lambda: O.pnp_ransac_seq(pr["points3d"], pr["points2d"], pr["K"], args.thr, 0.99, 5000), 1,
+                             samples=21, warmup=3)
+    # the reference call's own mode on the same problem (EPnP-5 on MWC subsets, each model through
+    # the Rodrigues round trip, main_v1.py:497-502)
     _, w_ref = _median_rate(lambda: O.pnp_ransac_seq(pr["points3d"], pr["points2d"], pr["K"], args.thr, 0.99, 5000,
-                                                     sampler="opencv", minimal="epnp5"), 1)
+                                                     sampler="opencv", minimal="epnp5"), 1, samples=21, warmup=3)
     # C1 (BASELINE.json configs[0]): the 12 testpro-K points (testpro-K.py:198-225) under main_v1's K
     # (main_v1.py:870-883), 1000 iterations, thr 30, the reference call's own mode (no flags:
     # EPnP on 5-point MWC samples, testpro-K.py:72 / main_v1.py:497)
     P3, P2, K1 = synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, synth.main_v1_K()
     c1 = O.pnp_ransac_seq(P3, P2, K1, 30.0, 0.99, 1000, sampler="opencv", minimal="epnp5")
     _, w_c1 = _median_rate(lambda: O.pnp_ransac_seq(P3, P2, K1, 30.0, 0.99, 1000, sampler="opencv",
-                                                    minimal="epnp5"), 1, samples=7)
+                                                    minimal="epnp5"), 1, samples=21, warmup=3)
     c1n = NR.pnp_ransac(P3, P2, K1, 30.0, 0.99, 1000, "epnp5")
-    _, w_c1n = _median_rate(lambda: NR.pnp_ransac(P3, P2, K1, 30.0, 0.99, 1000, "epnp5"), 1, samples=7)
+    _, w_c1n = _median_rate(lambda: NR.pnp_ransac(P3, P2, K1, 30.0, 0.99, 1000, "epnp5"), 1, samples=21, warmup=3)
+    # ... and under a K of testpro-K.py's sweep, as configs[0] words it: f = 150 mm on the 127 x 178 mm
+    # cell (testpro-K.py:58-70), fx 2529.9, fy 1365.2 -- the K test_pro.py:801-802 hard-codes
+    Kt = synth.testpro_k_candidates()[10]
+    c1k = O.pnp_ransac_seq(P3, P2, Kt, 30.0, 0.99, 1000, sampler="opencv", minimal="epnp5")
+    _, w_c1k = _median_rate(lambda: O.pnp_ransac_seq(P3, P2, Kt, 30.0, 0.99, 1000, sampler="opencv",
+                                                     minimal="epnp5"), 1, samples=21, warmup=3)
+    c1kn = NR.pnp_ransac(P3, P2, Kt, 30.0, 0.99, 1000, "epnp5")
+    _, w_c1kn = _median_rate(lambda: NR.pnp_ransac(P3, P2, Kt, 30.0, 0.99, 1000, "epnp5"), 1, samples=21, warmup=3)
     # C3: 32 of the 1024 problems (seeds 1..32), 1024 hypotheses each, problems over the threads
     probs = [synth.pnp_problem(2000, 0.5, seed=s) for s in range(1, 33)]
     soas = [(O.soa_pnp(p["points3d"], p["points2d"]), O.cam_from_K(p["K"])) for p in probs]
@@ -675,11 +706,16 @@ def cpu_baseline(pr, args):
     p4 = synth.fundamental_problem(50_000, 0.8, seed=2)
     s4 = O.soa_hom(p4["pts1"], p4["pts2"])
     rate_c4, w_c4 = _median_rate(lambda: O.fm_hypotheses(s4, 1.5, 0x5EED, 300), 300)
+    n4 = 60 * threads
+    rate_c4mt, w_c4mt = _median_rate(lambda: O.fm_hypotheses_mt(s4, 1.5, 0x5EED, n4, threads=threads), n4)
     # C5: LO-RANSAC to the best model on the 100k-point problem, 1 thread, OpenCV's loop shape
     p5 = synth.pnp_problem(100_000, 0.5, seed=3)
     r5 = O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000, lazy=True)
     _, w_c5 = _median_rate(lambda: O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000,
                                                    lazy=True), 1)
+    r5m = O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000, threads=threads)
+    _, w_c5mt = _median_rate(lambda: O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000,
+                                                     threads=threads), 1)
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -702,11 +738,12 @@ def cpu_baseline(pr, args):
                                       f"({share}), median of 5 ({w_all:.2f} s each)"},
             "c2_ms_to_best": {"ms": w_best * 1e3, "cores": 1,
                               "sample": "OpenCV's sequential loop (orc_pnp_ransac_seq), stops at the iteration "
-                                        "bound, no refit, median of 5"},
+                                        "bound, no refit, median of 21 after 3 warm-ups"},
             "c2_reference_mode": {"ms_to_best": w_ref * 1e3, "cores": 1,
                                   "sample": "orc_pnp_ransac_seq with EPnP-5 on MWC subsets (the reference call's "
-                                            "defaults) on the C2 problem, stops at the iteration bound, no refit, "
-                                            "median of 5"},
+                                            "defaults, each model through the Rodrigues round trip) on the C2 "
+                                            "problem, stops at the iteration bound, no refit, median of 21 after 3 "
+                                            "warm-ups"},
             "c1": {"ms_c": w_c1 * 1e3, "ms_numpy": w_c1n * 1e3, "cores": 1, "iters": c1["iters"],
                    "best": c1["best"], "n_inliers": c1["n_inliers"],
                    "inliers": [int(i) for i in np.flatnonzero(c1["mask"])],
@@ -714,15 +751,33 @@ def cpu_baseline(pr, args):
                    "sample": "BASELINE configs[0]: 12 testpro-K points, main_v1 K, 1000 iterations cap, thr 30, "
                              "EPnP-5 on OpenCV's MWC subsets, sequential loop to the bound; C restatement "
                              "(orc_pnp_ransac_seq_k) and the NumPy path (oracle/np_ransac.py), ms per solve, "
-                             "median of 7"},
+                             "median of 21 after 3 warm-ups"},
+            "c1_testpro_k": {"ms_c": w_c1k * 1e3, "ms_numpy": w_c1kn * 1e3, "cores": 1, "iters": c1k["iters"],
+                             "best": c1k["best"], "n_inliers": c1k["n_inliers"],
+                             "inliers": [int(i) for i in np.flatnonzero(c1k["mask"])],
+                             "K": [float(Kt[0, 0]), float(Kt[1, 1]), float(Kt[0, 2]), float(Kt[1, 2])],
+                             "numpy_equal": bool(c1kn["best"] == c1k["best"] and np.array_equal(c1kn["mask"],
+                                                                                                c1k["mask"])),
+                             "sample": "configs[0] with K from testpro-K.py (f 150 mm, 127 x 178 mm cell: the K "
+                                       "test_pro.py:801-802 prints), otherwise as c1, median of 21 after 3 "
+                                       "warm-ups"},
             "c3": {"hyp_s": rate_c3, "cores": threads,
                    "sample": f"32 of the 1024 problems x 1024 hypotheses, problems over {threads} threads, "
                              f"median of 5 ({w_c3:.2f} s each)"},
             "c4": {"hyp_s": rate_c4, "cores": 1, "sample": f"300 hypotheses, 50k matches, median of 5 ({w_c4:.2f} s each)"},
+            "c4_mt": {"hyp_s": rate_c4mt, "cores": threads,
+                      "sample": f"{n4} hypotheses, 50k matches, OpenMP over {threads} threads "
+                                f"(orc_fm_hypotheses_mt), median of 5 ({w_c4mt:.2f} s each)"},
             "c5": {"ms_to_best": w_c5 * 1e3, "iters": r5["iters"], "lo_improvements": r5["lo_improvements"],
                    "cores": 1, "sample": "orc_pnp_ransac_lo_seq on the 100k-point problem (each hypothesis "
                                          "evaluated when the scan reaches it, LO at every new best, stops at the "
-                                         "bound), median of 5"}}
+                                         "bound), median of 5"},
+            "c5_mt": {"ms_to_best": w_c5mt * 1e3, "iters": r5m["iters"], "lo_improvements": r5m["lo_improvements"],
+                      "cores": threads,
+                      "sample": f"orc_pnp_ransac_lo_mt: rounds of hypotheses (256 doubling to 4096) evaluated over "
+                                f"{threads} OpenMP threads, each round scanned with its LO steps in order on one "
+                                f"thread (OpenCV's loop is sequential: every new best moves the bound), median of "
+                                f"5"}}
 
 
 if __name__ == "__main__":

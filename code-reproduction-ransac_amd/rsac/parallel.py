@@ -345,3 +345,39 @@ def adaptive_shards(ev, max_iters: int, confidence: float = 0.99, round_size: in
                                 sync)
         walls.append(dt)
     return res, float(np.median(walls))
+
+
+def comm_report(n_problems: int = 0, n_hyps: int = 0, group=None, sync=None, samples: int = 50) -> dict:
+    """What an N > 1 bench line needs to describe itself: the process-group backend
+    (nccl = RCCL), the world size the backend reports, the median latency of an 8-byte (one int64)
+    all-reduce(MAX) -- the exchange of the hypothesis-shard and adaptive paths -- over `samples`
+    timed calls after 5 untimed ones (each synchronised, max over ranks), and every rank's share:
+    its C3-style problem chunk (chunk(), the all-gather layout) and its hypothesis shard
+    (shard())."""
+    rank, world = _rank_world(group)
+    backend = dist.get_backend(group) if (dist.is_available() and dist.is_initialized()) else "none"
+    dev = _comm_device(group)
+    t = torch.zeros(1, dtype=torch.int64, device=dev)
+    lat = []
+    for i in range(5 + max(1, samples)):
+        if world > 1:
+            dist.barrier(group=group)
+        if sync:
+            sync()
+        t0 = time.perf_counter()
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        if sync:
+            sync()
+        dt = time.perf_counter() - t0
+        if i >= 5:
+            lat.append(dt)
+    us = float(np.median(lat)) * 1e6
+    if world > 1:
+        tt = torch.tensor([us], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+        us = float(tt.item())
+    return {"backend": backend, "world_size": world, "rank": rank, "allreduce_8b_us": us,
+            "allreduce_samples": max(1, samples),
+            "problem_shares": [list(chunk(n_problems, r, world)[:2]) for r in range(world)],
+            "hypothesis_shares": [list(shard(n_hyps, r, world)) for r in range(world)]}

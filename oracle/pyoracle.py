@@ -150,6 +150,13 @@ def lib():
     L.orc_fm_hypotheses.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_float, C.c_uint64, C.c_int64,
                                     C.c_int64, _i32p, _i8p, C.c_void_p]
     L.orc_fm_hypotheses.restype = None
+    L.orc_fm_hypotheses_mt.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_float, C.c_uint64, C.c_int64,
+                                       C.c_int64, _i32p, _i8p, C.c_int]
+    L.orc_fm_hypotheses_mt.restype = None
+    L.orc_pnp_ransac_lo_mt.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_int, _f64p, C.c_double, C.c_double,
+                                       C.c_int, C.c_uint64, _f64p, _f64p, _u8p, C.POINTER(C.c_int32),
+                                       C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.c_int]
+    L.orc_pnp_ransac_lo_mt.restype = C.c_int64
     L.orc_fm_ransac.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_double, C.c_double, C.c_int, C.c_uint64,
                                 _f64p, _u8p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     L.orc_fm_ransac.restype = C.c_int64
@@ -348,10 +355,12 @@ def pnp_hypotheses_mt(soa, cam, thr, seed, H, hyp0=0, threads=1):
     return counts, status
 
 
-def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED, lazy=False):
+def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED, lazy=False,
+                  threads=0):
     """LO-RANSAC restatement (orc_pnp_ransac_lo): local optimisation at every new best.  lazy=True
     evaluates each hypothesis when the scan reaches it and stops at the bound (orc_pnp_ransac_lo_seq:
-    OpenCV's loop shape, the C5 CPU leg); the results are the same."""
+    OpenCV's loop shape, the C5 CPU leg); threads > 0 evaluates rounds of hypotheses over that many
+    OpenMP threads and scans them in order (orc_pnp_ransac_lo_mt); the results are the same."""
     soa = soa_pnp(points3d, points2d)
     n = len(soa[0])
     cam = cam_from_K(K)
@@ -361,8 +370,13 @@ def pnp_ransac_lo(points3d, points2d, K, thr=30.0, confidence=0.99, max_iters=50
     good = C.c_int32(0)
     iters = C.c_int64(0)
     nlo = C.c_int32(0)
-    fn = lib().orc_pnp_ransac_lo_seq if lazy else lib().orc_pnp_ransac_lo
-    best = fn(*soa, n, cam, thr, confidence, max_iters, seed, R, t, mask, C.byref(good), C.byref(iters), C.byref(nlo))
+    if threads > 0:
+        best = lib().orc_pnp_ransac_lo_mt(*soa, n, cam, thr, confidence, max_iters, seed, R, t, mask, C.byref(good),
+                                          C.byref(iters), C.byref(nlo), int(threads))
+    else:
+        fn = lib().orc_pnp_ransac_lo_seq if lazy else lib().orc_pnp_ransac_lo
+        best = fn(*soa, n, cam, thr, confidence, max_iters, seed, R, t, mask, C.byref(good), C.byref(iters),
+                  C.byref(nlo))
     return dict(best=int(best), R=R.reshape(3, 3), t=t, mask=mask.astype(bool), n_inliers=int(good.value),
                 iters=int(iters.value), lo_improvements=int(nlo.value))
 
@@ -614,6 +628,14 @@ def fm_hypotheses(soa, thr, seed, H, hyp0=0, models=False):
     mdl = np.zeros((H, 16)) if models else None
     lib().orc_fm_hypotheses(*soa, n, thr2(thr), seed, hyp0, H, counts, status, _ptr(mdl))
     return (counts, status, mdl) if models else (counts, status)
+
+
+def fm_hypotheses_mt(soa, thr, seed, H, hyp0=0, threads=1):
+    """fm_hypotheses over `threads` OpenMP threads (orc_fm_hypotheses_mt)."""
+    counts = np.zeros(H, np.int32)
+    status = np.zeros(H, np.int8)
+    lib().orc_fm_hypotheses_mt(*soa, len(soa[0]), thr2(thr), seed, hyp0, H, counts, status, int(threads))
+    return counts, status
 
 
 def fm_ransac(pts1, pts2, thr=1.5, confidence=0.99, max_iters=100000, seed=0x5EED):

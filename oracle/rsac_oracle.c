@@ -1147,6 +1147,16 @@ ORC_API void orc_fm_hypotheses(const float *x1, const float *y1, const float *x2
     }
 }
 
+/* orc_fm_hypotheses over `threads` host threads (OpenMP, hypotheses in chunks of 16): the C4 CPU
+ * baseline's multi-core leg; every hypothesis' result is the single-thread one. */
+ORC_API void orc_fm_hypotheses_mt(const float *x1, const float *y1, const float *x2, const float *y2, int n,
+                                  float thr2, uint64_t seed, int64_t hyp0, int64_t H, int32_t *counts, int8_t *status,
+                                  int threads) {
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 16)
+    for (int64_t h = 0; h < H; ++h)
+        orc_fm_hypotheses(x1, y1, x2, y2, n, thr2, seed, hyp0 + h, 1, counts + h, status + h, NULL);
+}
+
 ORC_API int64_t orc_fm_ransac(const float *x1, const float *y1, const float *x2, const float *y2, int n, double thr,
                               double confidence, int max_iters, uint64_t seed, double Fout[9], uint8_t *mask,
                               int32_t *n_inliers, int64_t *iters_used) {
@@ -1820,6 +1830,70 @@ static int64_t pnp_ransac_lo_impl(const float *X, const float *Y, const float *Z
         }
         memcpy(BR, MR, sizeof BR);
         memcpy(Bt, Mt, sizeof Bt);
+    }
+    if (best >= 0) {
+        memcpy(R, BR, sizeof BR);
+        memcpy(t, Bt, sizeof Bt);
+        orc_pnp_count(R, t, cam, X, Y, Z, U, V, n, thr2, mask);
+    } else if (mask) {
+        memset(mask, 0, n);
+    }
+    if (n_inliers) *n_inliers = max_good;
+    if (iters_used) *iters_used = i;
+    if (lo_improvements) *lo_improvements = nlo;
+    free(counts); free(status); free(models);
+    return best;
+}
+
+/* The C5 CPU baseline over `threads` host threads: OpenCV's LO loop is sequential (each new best
+ * changes the iteration bound the next hypothesis is judged against), so the hypotheses are
+ * evaluated in rounds (256, doubling to 4096, as the GPU's adaptive rounds) with OpenMP, and each
+ * round is scanned -- and every new best locally optimised -- in index order on one thread, up to
+ * the bound.  Results equal orc_pnp_ransac_lo's. */
+ORC_API int64_t orc_pnp_ransac_lo_mt(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                                     int n, const double cam[4], double thr, double confidence, int max_iters,
+                                     uint64_t seed, double R[9], double t[3], uint8_t *mask, int32_t *n_inliers,
+                                     int64_t *iters_used, int32_t *lo_improvements, int threads) {
+    int64_t direct_best;
+    if (lo_improvements) *lo_improvements = 0;
+    if (pnp_direct(X, Y, Z, U, V, n, cam, 4, 0, R, t, mask, n_inliers, iters_used, &direct_best)) return direct_best;
+    const int64_t H = max_iters > 1 ? max_iters : 1;
+    int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * 4096);
+    int8_t *status = (int8_t *)malloc(4096);
+    double *models = (double *)malloc(sizeof(double) * 16 * 4096);
+    const float thr2 = orc_thr2(thr);
+    int64_t niters = H, best = -1, i = 0, cur = 256;
+    int32_t max_good = 0, nlo = 0;
+    double BR[9] = {0}, Bt[3] = {0};
+    int stop = 0;
+    for (int64_t hb = 0; hb < H && hb < niters && !stop; hb += cur, cur = cur < 4096 ? 2 * cur : 4096) {
+        const int64_t hr = (hb + cur < H ? cur : H - hb);
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 4)
+        for (int64_t h = 0; h < hr; ++h)
+            orc_pnp_hypotheses(X, Y, Z, U, V, n, cam, thr2, seed, 0, hb + h, 1, NULL, NULL, counts + h, status + h,
+                               models + 16 * h);
+        for (i = hb; i < hb + hr && i < niters; ++i) {
+            const int64_t j = i - hb;
+            if (status[j] < 0) { stop = 1; break; }
+            if (status[j] == 0) continue;
+            int32_t c = counts[j];
+            int32_t floor_c = max_good > 3 ? max_good : 3;
+            if (c <= floor_c) continue;
+            best = i; max_good = c;
+            niters = orc_update_num_iters(confidence, (double)(n - c) / n, 4, (int)niters);
+            double MR[9], Mt[3];
+            memcpy(MR, models + 16 * j, sizeof MR);
+            memcpy(Mt, models + 16 * j + 9, sizeof Mt);
+            int32_t steps = 0;
+            c = orc_pnp_local_opt(X, Y, Z, U, V, n, cam, thr2, MR, Mt, c, &steps);
+            nlo += steps;
+            if (c > max_good) {
+                max_good = c;
+                niters = orc_update_num_iters(confidence, (double)(n - c) / n, 4, (int)niters);
+            }
+            memcpy(BR, MR, sizeof BR);
+            memcpy(Bt, Mt, sizeof Bt);
+        }
     }
     if (best >= 0) {
         memcpy(R, BR, sizeof BR);

@@ -70,7 +70,10 @@ def main():
         lo, _ = par.adaptive_shards(c5, 5000, 0.99, round_size=512, lo=True, repeats=1)
         ada, _ = par.adaptive_shards(OracleShard(synth.pnp_problem(3000, 0.7, seed=12)), 5000, 0.99, round_size=256,
                                      lo=False, repeats=1)
-        res = {"c3": rows.cpu().numpy().tolist(),
+        comm = par.comm_report(C3_PROBLEMS, 1000, samples=10)
+        comm.pop("rank")
+        comm.pop("allreduce_8b_us")  # timing: differs between ranks only before the max
+        res = {"comm": comm, "c3": rows.cpu().numpy().tolist(),
                "c5": [lo.best, lo.n_inliers, lo.iters, lo.lo_improvements, lo.model.tolist()],
                "ada": [ada.best, ada.n_inliers, ada.iters, ada.model.tolist()]}
         json.dump(res, open(os.path.join(out, f"rank{rank}.json"), "w"))

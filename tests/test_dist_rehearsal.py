@@ -41,6 +41,22 @@ def test_ranks_agree(ranks):
     assert ranks[0] == ranks[1]
 
 
+def test_comm_report_describes_the_line(ranks):
+    """bench.py's multi_gpu.comm: backend, world size as the backend reports
+    it, the timed 8-byte all-reduce, each rank's problem and hypothesis share."""
+    c = ranks[0]["comm"]
+    assert c["backend"] == "gloo" and c["world_size"] == 2 and c["allreduce_samples"] == 10
+    assert c["problem_shares"] == [[0, 8], [8, 8]]
+    assert c["hypothesis_shares"] == [[0, 500], [500, 500]]
+
+
+def test_comm_report_single_process():
+    from rsac import parallel as par
+    c = par.comm_report(10, 7, samples=3)
+    assert (c["backend"], c["world_size"], c["rank"]) == ("none", 1, 0)
+    assert c["problem_shares"] == [[0, 10]] and c["hypothesis_shares"] == [[0, 7]] and c["allreduce_8b_us"] >= 0
+
+
 def test_c3_rows_equal_single_process(ranks):
     rows = np.array(ranks[0]["c3"])
     assert rows.shape == (W.C3_PROBLEMS, 14)

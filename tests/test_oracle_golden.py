@@ -245,3 +245,19 @@ def test_numpy_path_equals_sequential_c_loop(minimal, case):
         np.testing.assert_array_equal(r["mask"], ref["mask"])
         np.testing.assert_array_equal(r["R"], ref["R"])
         np.testing.assert_array_equal(r["t"], ref["t"])
+
+
+def test_cpu_baseline_parallel_legs_equal_sequential():
+    """bench.py's multi-thread C4 and C5 CPU legs compute what the single-thread ones do."""
+    p4 = synth.fundamental_problem(4000, 0.8, seed=2)
+    s4 = O.soa_hom(p4["pts1"], p4["pts2"])
+    a, b = O.fm_hypotheses(s4, 1.5, 0x5EED, 150), O.fm_hypotheses_mt(s4, 1.5, 0x5EED, 150, threads=4)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    p5 = synth.pnp_problem(8000, 0.5, seed=3)
+    r = O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], 30.0, 0.99, 5000)
+    m = O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], 30.0, 0.99, 5000, threads=4)
+    assert (r["best"], r["n_inliers"], r["iters"], r["lo_improvements"]) == \
+        (m["best"], m["n_inliers"], m["iters"], m["lo_improvements"])
+    np.testing.assert_array_equal(r["R"], m["R"])
+    np.testing.assert_array_equal(r["mask"], m["mask"])
