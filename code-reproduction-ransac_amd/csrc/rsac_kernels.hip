@@ -867,7 +867,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 // eigen-decomposition of M^T M (~88 % of the arithmetic) by the round-robin Jacobi of
 // jacobi_eig_rr<12> on 16 lanes per hypothesis (k_epnp5_jacobi; rows of A and V per lane, the
 // step-start matrix mirrored in LDS for the pair parameters and the row exchange) or one wave per
-// hypothesis for short rounds (k_epnp5_jacobi_w), then k_epnp5_c (L, rho, the three beta estimates
+// hypothesis in 2 x 2 blocks for short rounds (k_epnp5_jacobi_b), then k_epnp5_c (L, rho, the three beta estimates
 // and their poses, 4 lanes per hypothesis).  Every element sees jacobi_eig_rr's operations in its
 // order (the rotation formula and skip rule of jrr_rotation), so the records are bit-identical to
 // rsac_math.h pnp_epnp_minimal<5> and the oracle's orc_pnp_minimal_epnp5 (ep_jacobi_rr).  (The
@@ -1092,9 +1092,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
 #pragma unroll
                 for (int q = 0; q < 12; ++q) dp = q == p ? rw[q] : dp;
                 diag = diag + dp * dp;
+                double rp = 0.0;
 #pragma unroll
                 for (int q = 1; q < 12; ++q)
-                    if (q > p) off = off + rw[q] * rw[q];
+                    if (q > p) rp = rp + rw[q] * rw[q];
+                off = off + rp;
             }
             if (!(off > 1e-32 * diag)) run = false;
         }
@@ -1127,80 +1129,75 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
 }
 
 // The latency form of k_epnp5_jacobi for short rounds (an adaptive run's first 256 hypotheses):
-// one wave per hypothesis, so a step's instructions per wave halve.  Lane L < 48: kind = L / 24
-// (0: a row of A, 1: the same row of V), row j = (L % 24) / 2, half h = L % 2; in each step half h
-// owns the 6 columns of pairs 3h .. 3h + 2 (read from the LDS copy at the step's start, rotated,
-// written back), so the column phase is 3 pairs per lane and the row phase 6 elements; both
-// matrices live in LDS between steps.  The same operations on every element as jacobi_eig_rr.
-struct EpnpJacLdsW {
+// one wave per hypothesis in 2 x 2 blocks.  In step r the 12 indices form the 6 pairs of
+// jacobi_eig_rr; lane (a, b) < 36 holds A's block at rows pair a x columns pair b and V's block at
+// rows 2a, 2a + 1 x columns pair b.  A step: the diagonal lanes (a, a) form their pair's cs, sn from
+// their own block (app, apq, aqq) and post them; every lane rotates its A block's columns by pair b
+// then its rows by pair a, and its V block's columns by pair b (the operations jacobi_eig_rr applies
+// to those elements, in its order: the same bits); the blocks go to the LDS mirrors of A and V, from
+// which every lane takes the next step's blocks.  Per step one chain of the rotation parameters,
+// 2 wave synchronisations and one round trip of 8 doubles per lane, where the half-row form (r04)
+// spent 4 synchronisations, 3 round trips and 196 instructions.  The sweep test: lanes 0..11 each
+// form their row's partial sums from the mirror (jacobi_eig_rr's order), every lane adds the 12 in
+// row order.
+struct EpnpJacLdsB {
     double A[4][12 * kEpR];
     double V[4][12 * kEpR];
-    double cs[4][12];
+    double cs[4][14];    // pair i: cs at 2i, sn at 2i + 1; 12, 13: the off-diagonal lanes' spare slot
+    double part[4][24];  // row p: A_pp^2 at 2p, sum_{q > p} A_pq^2 at 2p + 1
     int ord[4][12];
 };
+// position m of step R's circle (jrr_pos(12, R, m)) for a position known only at run time
 template <int R>
-__device__ __forceinline__ void epnp_rrw_step(int sweep, int j, int h, bool isA, double *LA, double *LM, double *LC) {
-    // (the lane's step constants may be hoisted out of the sweep loop: this form has the registers)
-    const int m = j == 0 ? 0 : (j - 1 - R + 11) % 11 + 1;
-    const int mo = 11 - m;
-    const int o = mo == 0 ? 0 : 1 + (mo - 1 + R) % 11;
-    const int pi = m < mo ? m : mo;
-    const int p = j < o ? j : o, q = j < o ? o : j;
-    // this lane's 6 columns: pairs 3h .. 3h + 2
-    int col[6];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        col[2 * e] = h ? jrr_p(R, 3 + e) : jrr_p(R, e);
-        col[2 * e + 1] = h ? jrr_q(R, 3 + e) : jrr_q(R, e);
-    }
-    double x[6];
-#pragma unroll
-    for (int e = 0; e < 6; ++e) x[e] = LM[kEpR * j + col[e]];
-    const double app = LA[(kEpR + 1) * p], aqq = LA[(kEpR + 1) * q], apq = LA[kEpR * p + q];
-    double cs = 1.0, sn = 0.0;  // a skipped pair: the identity rotation (jacobi_eig_rr)
-    (void)jrr_rotation(sweep, app, aqq, apq, cs, sn);
-    if (isA && h == 0 && j == p) {
-        LC[2 * pi] = cs;
-        LC[2 * pi + 1] = sn;
-    }
+__device__ __forceinline__ int jrr_pos_r(int m) {
+    int v = m - 1 + R;  // 0 .. 20 for m >= 1
+    v = v >= 11 ? v - 11 : v;
+    return m == 0 ? 0 : 1 + v;
+}
+// Step R of the block form, branch-free: lanes 36..63 repeat lanes 0..27's blocks (the same values
+// to the same addresses), every lane forms its row pair's rotation and only the diagonal lanes'
+// land in LC (the others in a spare slot), so the wave runs one instruction stream.
+template <int R>
+__device__ __forceinline__ void epnp_blk_step(int sweep, int ba, int bb, int vr0, double *LA, double *LV,
+                                              double *LC) {
+    int pa = jrr_pos_r<R>(ba), qa = jrr_pos_r<R>(11 - ba), pb = jrr_pos_r<R>(bb), qb = jrr_pos_r<R>(11 - bb);
+    if (pa > qa) { const int x = pa; pa = qa; qa = x; }
+    if (pb > qb) { const int x = pb; pb = qb; qb = x; }
+    double *A0 = LA + kEpR * pa, *A1 = LA + kEpR * qa;
+    double *V0 = LV + vr0, *V1 = LV + vr0 + kEpR;
+    const double x00 = A0[pb], x01 = A0[qb], x10 = A1[pb], x11 = A1[qb];
+    const double v00 = V0[pb], v01 = V0[qb], v10 = V1[pb], v11 = V1[qb];
+    double cs, sn;  // meaningful on the diagonal lanes (ba == bb: app, apq, aqq of pair ba)
+    jrr_rotation_sel(sweep, x00, x11, x01, cs, sn);
+    const int slot = ba == bb ? 2 * ba : 12;
+    LC[slot] = cs;
+    LC[slot + 1] = sn;
     ep_wave_sync();
-    double c3[3], s3[3];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        c3[e] = LC[2 * (3 * h + e)];
-        s3[e] = LC[2 * (3 * h + e) + 1];
-    }
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        const double a0 = x[2 * e], a1 = x[2 * e + 1];
-        x[2 * e] = c3[e] * a0 - s3[e] * a1;
-        x[2 * e + 1] = s3[e] * a0 + c3[e] * a1;
-    }
-#pragma unroll
-    for (int e = 0; e < 6; ++e) LM[kEpR * j + col[e]] = x[e];
-    ep_wave_sync();
-    if (isA) {  // rows: the partner's column-rotated elements of the same columns
-        double y[6];
-#pragma unroll
-        for (int e = 0; e < 6; ++e) y[e] = LA[kEpR * o + col[e]];
-        ep_wave_sync();
-        const double xs = j == p ? -sn : sn;
-#pragma unroll
-        for (int e = 0; e < 6; ++e) x[e] = cs * x[e] + xs * y[e];
-#pragma unroll
-        for (int e = 0; e < 6; ++e) LA[kEpR * j + col[e]] = x[e];
-    }
-    ep_wave_sync();
+    const double ca = LC[2 * ba], sa = LC[2 * ba + 1], cb = LC[2 * bb], sb = LC[2 * bb + 1];
+    // columns (pair b) of rows pa, qa; then rows (pair a) of the column-rotated block
+    const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
+    const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
+    A0[pb] = ca * y00 - sa * y10;
+    A1[pb] = sa * y00 + ca * y10;
+    A0[qb] = ca * y01 - sa * y11;
+    A1[qb] = sa * y01 + ca * y11;
+    // V's columns (pair b)
+    V0[pb] = cb * v00 - sb * v01;
+    V0[qb] = sb * v00 + cb * v01;
+    V1[pb] = cb * v10 - sb * v11;
+    V1[qb] = sb * v10 + cb * v11;
+    ep_wave_sync();  // the mirrors hold the step's result; LC may be rewritten
 }
 template <int R>
-__device__ __forceinline__ void epnp_rrw_sweep(int sweep, int j, int h, bool isA, double *LA, double *LM, double *LC) {
+__device__ __forceinline__ void epnp_blk_sweep(int sweep, int ba, int bb, int vr0, double *LA, double *LV,
+                                               double *LC) {
     if constexpr (R < 11) {
-        epnp_rrw_step<R>(sweep, j, h, isA, LA, LM, LC);
-        epnp_rrw_sweep<R + 1>(sweep, j, h, isA, LA, LM, LC);
+        epnp_blk_step<R>(sweep, ba, bb, vr0, LA, LV, LC);
+        epnp_blk_sweep<R + 1>(sweep, ba, bb, vr0, LA, LV, LC);
     }
 }
-__global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_begin, int32_t H) {
-    __shared__ EpnpJacLdsW L;
+__global__ __launch_bounds__(256) void k_epnp5_jacobi_b(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    __shared__ EpnpJacLdsB L;
     const int prob = blockIdx.y;
     const int lane = threadIdx.x & 63, hb = threadIdx.x >> 6;
     const int hl = (int)((blockIdx.x * 256u + threadIdx.x) >> 6);
@@ -1209,10 +1206,7 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_b
     const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
     const bool live = hl < H && a.status[rec] > 0 && s1->ok != 0.0;  // wave-uniform
     if (!live) return;
-    const bool act = lane < 48, isA = lane < 24;
-    const int j = (lane % 24) >> 1, h = lane & 1;
-    double *LA = L.A[hb], *LV = L.V[hb], *LC = L.cs[hb];
-    double *LM = isA ? LA : LV;
+    double *LA = L.A[hb], *LV = L.V[hb], *LP = L.part[hb];
     if (lane < 12) {  // row `lane` of epnp_mtm's matrix, and of V = I
         const int jr = lane;
         const double *cm = a.cams + 4 * prob;
@@ -1232,25 +1226,35 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_b
 #pragma unroll
         for (int c = 0; c < 12; ++c) LV[kEpR * jr + c] = c == jr ? 1.0 : 0.0;
     }
+    const int bl = lane < 36 ? lane : lane - 36;  // lanes 36..63 repeat blocks 0..27
+    const int ba = bl / 6, bb = bl - 6 * (bl / 6), vr0 = kEpR * 2 * ba;
+    const int tr = lane < 12 ? lane : lane - 12 * (lane / 12);  // the sweep test's row (repeated)
     ep_wave_sync();
     for (int sweep = 0; sweep < 60; ++sweep) {
-        double off = 0.0, diag = 0.0;  // every lane, in jacobi_eig_rr's order (wave-uniform verdict)
-#pragma unroll 1
-        for (int pr = 0; pr < 12; ++pr) {
+        {  // row tr's terms of the sweep test, from the mirror
             double rw[12];
 #pragma unroll
-            for (int qq = 0; qq < 12; ++qq) rw[qq] = LA[kEpR * pr + qq];
+            for (int q = 0; q < 12; ++q) rw[q] = LA[kEpR * tr + q];
             double dp = 0.0;
 #pragma unroll
-            for (int qq = 0; qq < 12; ++qq) dp = qq == pr ? rw[qq] : dp;
-            diag = diag + dp * dp;
+            for (int q = 0; q < 12; ++q) dp = q == tr ? rw[q] : dp;
+            double rp = 0.0;
 #pragma unroll
-            for (int qq = 1; qq < 12; ++qq)
-                if (qq > pr) off = off + rw[qq] * rw[qq];
+            for (int q = 1; q < 12; ++q)
+                if (q > tr) rp = rp + rw[q] * rw[q];
+            LP[2 * tr] = dp * dp;
+            LP[2 * tr + 1] = rp;
+        }
+        ep_wave_sync();
+        double off = 0.0, diag = 0.0;  // every lane, rows in order: a wave-uniform verdict
+#pragma unroll
+        for (int p = 0; p < 12; ++p) {
+            diag = diag + LP[2 * p];
+            off = off + LP[2 * p + 1];
         }
         if (!(off > 1e-32 * diag)) break;
-        if (act) epnp_rrw_sweep<0>(sweep, j, h, isA, LA, LM, LC);
-        ep_wave_sync();
+        epnp_blk_sweep<0>(sweep, ba, bb, vr0, LA, LV, L.cs[hb]);
+        ep_wave_sync();  // (the test's partials are rewritten next sweep)
     }
     int *O = L.ord[hb];
     if (lane == 0) {  // eig_order_desc<12> on the diagonal
@@ -1267,9 +1271,9 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_w(PnpArgs a, int64_t hyp_b
         }
     }
     ep_wave_sync();
-    if (lane < 12) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) E[64 + 12 * i + lane] = LV[kEpR * lane + O[11 - i]];  // ut[i][j] = V[j][o[11 - i]]
+    if (lane < 48) {  // ut[i][j] = V[j][o[11 - i]]
+        const int i = lane / 12, j = lane - 12 * (lane / 12);
+        E[64 + lane] = LV[kEpR * j + O[11 - i]];
     }
 }
 
@@ -2944,7 +2948,7 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
         // short rounds (an adaptive run's first 256 hypotheses): one wave per hypothesis (the round's
         // latency is one hypothesis' Jacobi); longer ones 16 lanes each
         if ((int64_t)P * H <= kEpnpWaveMaxHyps)
-            hipLaunchKernelGGL(k_epnp5_jacobi_w, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+            hipLaunchKernelGGL(k_epnp5_jacobi_b, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
         else
             hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv((int64_t)kEpG * H, 256), P), dim3(256), 0, s, ka, hyp_begin,
                                H);

@@ -1248,9 +1248,11 @@ RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
 // N - 1 - i, p the smaller index.  Sweep test as jacobi_eig; the rotation by jrr_rotation.
 RSAC_HD constexpr int jrr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
 // the rotation of pair (p, q): false (skipped) for apq = 0 or, from the fifth sweep on, apq
-// negligible next to both diagonal entries (Numerical Recipes' rule); t = sgn(theta) / (|theta| +
-// sqrt(theta^2 + 1)) with theta = d / w, d = aqq - app, w = 2 apq, formed as sgn |w| / (|d| +
-// sqrt(d^2 + w^2)) (one division fewer; MᵀM's entries are far from the square's overflow)
+// negligible next to both diagonal entries (Numerical Recipes' rule).  With d = aqq - app, w = 2 apq,
+// h = |d| + sqrt(d^2 + w^2): t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)) = sg |w| / h (theta =
+// d / w), so cs = 1 / sqrt(t^2 + 1) = h / sqrt(h^2 + w^2) and sn = t cs = sg |w| / sqrt(h^2 + w^2):
+// two square roots and one division in the chain (r05; one division fewer than forming t first).
+// MᵀM's entries are far from the squares' overflow.
 RSAC_HD inline bool jrr_rotation(int sweep, double app, double aqq, double apq, double &cs, double &sn) {
     if (!(apq != 0.0)) return false;
     if (sweep >= 4) {
@@ -1259,11 +1261,28 @@ RSAC_HD inline bool jrr_rotation(int sweep, double app, double aqq, double apq, 
     }
     const double d = aqq - app, w = 2.0 * apq;
     const double sg = (d == 0.0 || ((d < 0.0) == (w < 0.0))) ? 1.0 : -1.0;
-    const double tt = sg * dabs(w) / (dabs(d) + dsqrt(d * d + w * w));
-    cs = 1.0 / dsqrt(tt * tt + 1.0);
-    sn = tt * cs;
+    const double aw = dabs(w), h = dabs(d) + dsqrt(d * d + w * w);
+    const double iq = 1.0 / dsqrt(h * h + aw * aw);
+    cs = h * iq;
+    sn = sg * aw * iq;
     return true;
 }
+// jrr_rotation without branches (the GPU's block form): every lane forms the parameters, a skipped
+// pair then selects cs 1, sn 0; the same bits as jrr_rotation
+RSAC_HD void jrr_rotation_sel(int sweep, double app, double aqq, double apq, double &cs, double &sn) {
+    const double d = aqq - app, w = 2.0 * apq;
+    const double sg = (d == 0.0 || ((d < 0.0) == (w < 0.0))) ? 1.0 : -1.0;
+    const double aw = dabs(w), h = dabs(d) + dsqrt(d * d + w * w);
+    const double iq = 1.0 / dsqrt(h * h + aw * aw);
+    const double g = 100.0 * dabs(apq);
+    const bool skip = !(apq != 0.0) || (sweep >= 4 && dabs(app) + g == dabs(app) && dabs(aqq) + g == dabs(aqq));
+    const double c = h * iq, sv = sg * aw * iq;
+    cs = skip ? 1.0 : c;
+    sn = skip ? 0.0 : sv;
+}
+// the sweep test's sums: diag = sum_p A_pp^2 in p order; off = sum over the rows p, in order, of
+// the row's partial sum_{q > p} A_pq^2 in q order (r05: a row's partial is one lane's, so the
+// 16-lane kernel forms it from its registers)
 template <int N>
 RSAC_HD void jacobi_eig_rr(double *A, double *V, double *d) {
     static_assert(N % 2 == 0, "round-robin Jacobi needs an even order");
@@ -1274,7 +1293,9 @@ RSAC_HD void jacobi_eig_rr(double *A, double *V, double *d) {
         double off = 0.0, diag = 0.0;
         for (int p = 0; p < N; ++p) {
             diag = diag + A[p * N + p] * A[p * N + p];
-            for (int q = p + 1; q < N; ++q) off = off + A[p * N + q] * A[p * N + q];
+            double rp = 0.0;
+            for (int q = p + 1; q < N; ++q) rp = rp + A[p * N + q] * A[p * N + q];
+            off = off + rp;
         }
         if (!(off > 1e-32 * diag)) break;
         for (int r = 0; r < N - 1; ++r) {
@@ -1446,6 +1467,9 @@ RSAC_HD void epnp_l6x10(const double *const v[4], double *L) {
 
 // 5 Gauss-Newton steps on the betas (OpenCV gauss_newton)
 RSAC_HD void epnp_gauss_newton(const double *L, const double *rho, double *be) {
+    // (not unrolled: a latency-bound GPU lane then runs one iteration's code five times from a warm
+    // instruction cache instead of five cold copies)
+#pragma unroll 1
     for (int it = 0; it < 5; ++it) {
         double A[24], b[6], x[4];
 #pragma unroll

@@ -2094,10 +2094,13 @@ static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
     for (int i = 0; i < N * N; ++i) V[i] = 0.0;
     for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
     for (int sweep = 0; sweep < 60; ++sweep) {
+        /* diag in p order; off = the rows' partial sums (q > p, q order) added in row order */
         double off = 0.0, diag = 0.0;
         for (int p = 0; p < N; ++p) {
             diag = diag + A[p * N + p] * A[p * N + p];
-            for (int q = p + 1; q < N; ++q) off = off + A[p * N + q] * A[p * N + q];
+            double rp = 0.0;
+            for (int q = p + 1; q < N; ++q) rp = rp + A[p * N + q] * A[p * N + q];
+            off = off + rp;
         }
         if (!(off > 1e-32 * diag)) break;
         for (int r = 0; r < N - 1; ++r) {
@@ -2113,12 +2116,15 @@ static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
                     if (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq)) act[i] = 0;
                 }
                 if (!act[i]) continue;
-                /* t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)), theta = d / w, without forming theta */
+                /* t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)) = sg |w| / h, theta = d / w,
+                   h = |d| + sqrt(d^2 + w^2); cs = 1 / sqrt(t^2 + 1) = h / sqrt(h^2 + w^2),
+                   sn = t cs = sg |w| / sqrt(h^2 + w^2) (one division) */
                 double d = aqq - app, w = 2.0 * apq;
                 double sg = (d == 0.0 || ((d < 0.0) == (w < 0.0))) ? 1.0 : -1.0;
-                double tt = sg * fabs(w) / (fabs(d) + sqrt(d * d + w * w));
-                cs[i] = 1.0 / sqrt(tt * tt + 1.0);
-                sn[i] = tt * cs[i];
+                double aw = fabs(w), h = fabs(d) + sqrt(d * d + w * w);
+                double iq = 1.0 / sqrt(h * h + aw * aw);
+                cs[i] = h * iq;
+                sn[i] = sg * aw * iq;
             }
             /* a skipped pair applies cs = 1, sn = 0 like any other (no special case, so the device
                runs every step branch-free with the same bits) */
