@@ -93,6 +93,9 @@ struct PinBuf {
 };
 
 constexpr size_t kMaxModelBytes = size_t(32) << 30;  // hypothesis records kept resident per call
+// OpenCV-sampler rounds up to this many bytes of subsets + statuses are read by the solve kernels
+// from pinned host memory instead of being copied (run_loop)
+constexpr int64_t kSubsetZeroCopyBytes = 64 << 10;
 
 // hipMemcpy2DAsync, as one linear copy when the rows are contiguous (one problem): the 2-D path
 // costs tens of microseconds more per call on this runtime (measured in the adaptive loop)
@@ -426,6 +429,9 @@ struct LoopOut {
     bool spec_pending = false;
     int64_t spec_H = 0;
     bool timing = true;  // HIP events around solve / score (the caller wants rsac_stats)
+    // OpenCV's sampler: one MWC state per problem, carried across rounds and across the resume of a
+    // speculative first round
+    std::vector<Mwc> rngs;
 };
 
 // LO-RANSAC local optimisation of the new best of problem 0 (DESIGN.md "LO-RANSAC";
@@ -568,9 +574,9 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
     // states persist across rounds, each round's slice is drawn on the host (problems in
     // parallel) and uploaded before its solve
     const bool opencv = (flags & RSAC_F_SAMPLER_OPENCV) != 0;
-    std::vector<Mwc> rngs;
+    std::vector<Mwc> &rngs = out.rngs;
     if (opencv) {
-        rngs.assign(P, Mwc());
+        if (!resume) rngs.assign(P, Mwc());
         SETARG(subsets, c->subsets.as<int32_t>());
         SETARG(sub_status, c->substatus.as<int8_t>());
     }
@@ -579,7 +585,7 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
     // adaptive: the first round is short (most runs stop within it), later ones double
     int64_t cur = adaptive ? std::min<int64_t>(round, 256) : round;
     int64_t hb0 = 0;
-    if (resume) {  // after a verified speculative first round (philox: no sampler state to carry)
+    if (resume) {  // after a verified speculative first round (OpenCV's sampler: out.rngs carries on)
         hb0 = out.spec_H;
         cur = std::min<int64_t>(cur * 2, round);
     } else {
@@ -606,10 +612,27 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
                 mwc_subsets(rngs[p], np, Hr, model == Model::Hom ? hom : nullptr, hs + ((size_t)p * stride + hb) * sk,
                             os, sk);
             });
-            HIPCHK(copy_rows(c->subsets.as<int32_t>() + hb * sk, sizeof(int32_t) * sk * stride, hs + hb * sk,
-                             sizeof(int32_t) * sk * stride, sizeof(int32_t) * sk * Hr, P, hipMemcpyHostToDevice, s));
-            HIPCHK(copy_rows(c->substatus.as<int8_t>() + hb, stride, hss + hb, stride, Hr, P,
-                                    hipMemcpyHostToDevice, s));
+            // a small round's subsets are read by the solve straight from the pinned host rows (no
+            // copy launches in the latency path: an adaptive run's first round); larger rounds go
+            // to the device in two copies.  Either way the host rewrites the rows only after the
+            // round's synchronisation.
+            const bool zero_copy = (int64_t)P * Hr * (4 * sk + 1) <= kSubsetZeroCopyBytes;
+            const int32_t *sub = zero_copy ? hs : c->subsets.as<int32_t>();
+            const int8_t *sst = zero_copy ? hss : c->substatus.as<int8_t>();
+            if (!zero_copy) {
+                HIPCHK(copy_rows(c->subsets.as<int32_t>() + hb * sk, sizeof(int32_t) * sk * stride, hs + hb * sk,
+                                 sizeof(int32_t) * sk * stride, sizeof(int32_t) * sk * Hr, P, hipMemcpyHostToDevice,
+                                 s));
+                HIPCHK(copy_rows(c->substatus.as<int8_t>() + hb, stride, hss + hb, stride, Hr, P,
+                                 hipMemcpyHostToDevice, s));
+            }
+            if (pa) {
+                pa->subsets = sub;
+                pa->sub_status = sst;
+            } else {
+                ha->subsets = sub;
+                ha->sub_status = sst;
+            }
         }
         if (out.timing) HIPCHK(hipEventRecord(c->ev0, s));
         if (pa) {
@@ -1062,8 +1085,8 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     // scan the same way, with no host round trip in between
     const bool adaptive = (flags & RSAC_F_ADAPTIVE) != 0;
     const bool spec_fixed = !adaptive && !(flags & RSAC_F_LO) && st.total > 0;
-    const bool spec = spec_fixed || (P == 1 && adaptive && !(flags & (RSAC_F_LO | RSAC_F_SAMPLER_OPENCV)) &&
-                                     st.total > 0);
+    // (OpenCV's sampler too: its MWC state after the first round is kept in lo.rngs for the resume)
+    const bool spec = spec_fixed || (P == 1 && adaptive && !(flags & RSAC_F_LO) && st.total > 0);
     ScanDecide dec;
     if (spec) {
         dec.best_out = c->best.as<int64_t>();

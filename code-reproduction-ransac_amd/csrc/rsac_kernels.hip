@@ -1913,29 +1913,45 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 #ifndef RSAC_MF_LONG_W
 #define RSAC_MF_LONG_W 4
 #endif
+#ifndef RSAC_MF_TID_OPAQUE
+#define RSAC_MF_TID_OPAQUE 1
+#endif
 constexpr int kMfW = RSAC_MF_LONG_W;  // A/B knob (scripts/build_ab.sh): waves per block for one long problem
 constexpr int kWrec = 64;        // flagged iterations a wave lists per unit
 
+// the thread index as a value the compiler cannot hoist: the unit's lane-dependent offsets are then
+// formed inside each unit (a few integer instructions) instead of being held across the unit loop,
+// where at the 168-VGPR budget of 3 waves/SIMD they were spilled (548 B of scratch per lane, r04)
+__device__ __forceinline__ int mf_tid() {
+    int t = (int)threadIdx.x;
+#if RSAC_MF_TID_OPAQUE  // A/B knob (scripts/build_ab.sh): 0 lets the compiler hoist again
+    asm volatile("" : "+v"(t));
+#endif
+    return t;
+}
+
 template <int W>
 __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, int nh, int64_t p0, int start, int n,
-                                        int n_all_pts, int lane, int wave, uint32_t (*cl)[16][64],
-                                        float (*ab)[2][4][4], mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *lcorr,
+                                        int n_all_pts, uint32_t (*cl)[16][64], float (*ab)[2][4][4],
+                                        mf_h8 (*alds)[64], uint2 (*wrec)[kWrec], int *lcorr,
                                         int32_t *__restrict__ counts) {
     constexpr int HB = 32, T = 64 * W;  // T: threads = points one pass of the block covers
+    const int tid = mf_tid();
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int col = lane & 31, half = lane >> 5;
     const int64_t rec0 = (int64_t)prob * a.hyp_stride + h0;
     const float *__restrict__ recs = a.fmodels + rec0 * kFModelStride;
-    if (threadIdx.x < HB) {
-        lcorr[threadIdx.x] = 0;  // the unit's corrections (before the barrier)
+    if (tid < HB) {
+        lcorr[tid] = 0;  // the unit's corrections (before the barrier)
         // a' and b' of slot (t, g, half) = hypothesis 8t + 2g + half; past the round: b' = -inf
         // (records without a model carry a' = 0, b' = -inf themselves)
-        const int j = threadIdx.x;
+        const int j = tid;
         const bool v = j < nh;
         ab[0][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 12] : 0.f;
         ab[1][j & 1][j >> 3][(j >> 1) & 3] = v ? gview(recs)[j * kFModelStride + 13] : -__builtin_inff();
     }
     // the unit's A operands (the same for every wave): entry (t, lane) holds group t's
-    for (int e = threadIdx.x; e < 256; e += T) {
+    for (int e = tid; e < 256; e += T) {
         const int tl = e & 63;
         alds[e >> 6][tl] = mf_operand(recs, e >> 6, tl & 31, tl >> 5, nh);
     }
@@ -2012,7 +2028,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
         for (int g = 0; g < 4; ++g) cl[wave][4 * t + g][lane] = vc[t][g];
     __syncthreads();
     constexpr int TPH = T / 32, LPT = 32 / TPH;  // threads per hypothesis, lanes per thread
-    const int j = threadIdx.x / TPH, p = threadIdx.x % TPH;
+    const int j = tid / TPH, p = tid % TPH;
     const int slot = 4 * (j >> 3) + ((j >> 1) & 3), l0 = (j & 1) * 32 + LPT * p;
     uint32_t sum = 0;
 #pragma unroll
@@ -2110,7 +2126,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         const int n = min(n_all, c1 * cell_pts);
         if (start < n_all) {  // else a cell past a short problem of a batch (uniform)
             if (in_range)
-                mf_unit<W>(a, prob, h0, nh, p0, start, n, n_all, lane, wave, cl, ab, alds, wrec, lcorr, counts);
+                mf_unit<W>(a, prob, h0, nh, p0, start, n, n_all, cl, ab, alds, wrec, lcorr, counts);
             else
                 mf_sc_unit<W>(kernarg_pnp(), prob, h0, nh, p0, start, n, lane, wave, red, mlds, counts);
         }

@@ -1102,3 +1102,19 @@ def test_fundamental_fixed_budget_long_round():
     assert (info.best_hyp, info.n_inliers) == (ref["best"], ref["n_inliers"])
     assert _bits_equal(F, ref["F"])
     np.testing.assert_array_equal(m, ref["mask"])
+
+
+@pytest.mark.parametrize("minimal,outl", [("p3p", 0.8), ("epnp5", 0.7), ("epnp5", 0.85)])
+def test_speculative_first_round_opencv_sampler(minimal, outl):
+    """OpenCV's sampler also takes the speculative first round (r05): when the round ends the scan
+    the device's finish stands; when it does not, the loop resumes with the MWC state the first
+    round left (LoopOut::rngs).  Both equal the restatement's sequential loop."""
+    pr = synth.pnp_problem(3000, outl, seed=int(outl * 100) + 7)
+    f0, _ = _spec_counters()
+    R, t, m, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 5000, 30.0, sampler="opencv",
+                                    minimal=minimal, refine=False, return_info=True)
+    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 5000, sampler="opencv", minimal=minimal)
+    assert _spec_counters()[0] == f0 + 1
+    assert (info.best_hyp, info.n_inliers, info.iters) == (ref["best"], ref["n_inliers"], ref["iters"])
+    np.testing.assert_array_equal(m, ref["mask"])
+    assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
