@@ -889,23 +889,27 @@ __device__ __forceinline__ int8_t epnp5_sample(const PnpArgs &a, int64_t rec, in
     rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
     return (n >= 5 && rng.subset<5>(n, idx) == 0) ? 1 : -1;
 }
-// pnp_epnp_minimal<5>'s reducer: the sample centred on its first point
-__device__ __forceinline__ void epnp5_reducer(const PnpArgs &a, int64_t p0, const int32_t (&idx)[5],
-                                              MinimalEpnpReducer<5> &red, double (&c)[3]) {
+// the sample's points (a gather; stage 3 issues it before its beta arithmetic, which hides it)
+struct Epnp5Pts {
     float X[5], Y[5], Z[5], U[5], V[5];
+};
+__device__ __forceinline__ void epnp5_gather(const PnpArgs &a, int64_t p0, const int32_t (&idx)[5], Epnp5Pts &q) {
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
         const int64_t i = p0 + idx[j];
-        X[j] = a.X[i]; Y[j] = a.Y[i]; Z[j] = a.Z[i]; U[j] = a.U[i]; V[j] = a.V[i];
+        q.X[j] = a.X[i]; q.Y[j] = a.Y[i]; q.Z[j] = a.Z[i]; q.U[j] = a.U[i]; q.V[j] = a.V[i];
     }
-    c[0] = (double)X[0]; c[1] = (double)Y[0]; c[2] = (double)Z[0];
+}
+// pnp_epnp_minimal<5>'s reducer: the sample centred on its first point
+__device__ __forceinline__ void epnp5_reducer(const Epnp5Pts &q, MinimalEpnpReducer<5> &red, double (&c)[3]) {
+    c[0] = (double)q.X[0]; c[1] = (double)q.Y[0]; c[2] = (double)q.Z[0];
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-        red.X[i] = (double)X[i] - c[0];
-        red.Y[i] = (double)Y[i] - c[1];
-        red.Z[i] = (double)Z[i] - c[2];
-        red.u[i] = (double)U[i];
-        red.v[i] = (double)V[i];
+        red.X[i] = (double)q.X[i] - c[0];
+        red.Y[i] = (double)q.Y[i] - c[1];
+        red.Z[i] = (double)q.Z[i] - c[2];
+        red.u[i] = (double)q.U[i];
+        red.v[i] = (double)q.V[i];
     }
 }
 
@@ -927,9 +931,11 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
     s1.ok = 0.0;
     s1.n = 0.0;
     if (st > 0) {
+        Epnp5Pts q;
+        epnp5_gather(a, p0, idx, q);
         MinimalEpnpReducer<5> red;
         double c[3];
-        epnp5_reducer(a, p0, idx, red, c);
+        epnp5_reducer(q, red, c);
         const double *cm = a.cams + 4 * prob;
         epnp_stage1(red, Cam{cm[0], cm[1], cm[2], cm[3]}, s1);
     }
@@ -1297,6 +1303,10 @@ __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, i
     bool mine = false;  // this lane's estimate gave a pose
     bool s1ok = false;
     if (st > 0) {
+        int32_t idx[5];
+        (void)epnp5_sample(a, rec, h, n, idx);
+        Epnp5Pts q;
+        epnp5_gather(a, p0, idx, q);
         const EpnpStage1 s1 = *reinterpret_cast<const EpnpStage1 *>(E);
         s1ok = s1.ok != 0.0;
         if (s1ok && c < 3) {
@@ -1308,10 +1318,8 @@ __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, i
             double L[60], rho[6], be[4];
             epnp_l_rho(s1, s2, L, rho);
             if (epnp_beta(c + 1, L, rho, be)) {
-                int32_t idx[5];
-                (void)epnp5_sample(a, rec, h, n, idx);
                 MinimalEpnpReducer<5> red;
-                epnp5_reducer(a, p0, idx, red, cen);
+                epnp5_reducer(q, red, cen);
                 double p1[3], a1[4];
                 red.first(p1);
                 epnp_alphas(epnp_alpha_frame(s1.f), p1[0], p1[1], p1[2], a1);
@@ -2960,15 +2968,19 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     PnpArgs ka = round_args(a, P, H);
     if (a.sample_k == 5) {  // EPnP-5: the three-launch form (k_epnp5_a / _jacobi / _c)
         if (!a.epnp) return hipErrorInvalidValue;  // its scratch (ensure_epnp5) is required
-        hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-        // short rounds (an adaptive run's first 256 hypotheses): one wave per hypothesis (the round's
-        // latency is one hypothesis' Jacobi); longer ones 16 lanes each
-        if ((int64_t)P * H <= kEpnpWaveMaxHyps)
+        // short rounds (an adaptive run's first 256 hypotheses): their latency is one hypothesis', so
+        // one wave per block in stages 1 and 3 (4 and 16 CUs for 256 hypotheses, 64 and 16 per wave;
+        // sparser waves were slower, r05 A/B) and one wave per hypothesis in 2 x 2 blocks for the Jacobi; longer
+        // rounds 16 lanes per Jacobi
+        const bool short_round = (int64_t)P * H <= kEpnpWaveMaxHyps;
+        const int tb = short_round ? 64 : 256;  // threads per block of stages 1 and 3
+        hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
+        if (short_round)
             hipLaunchKernelGGL(k_epnp5_jacobi_b, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
         else
             hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv((int64_t)kEpG * H, 256), P), dim3(256), 0, s, ka, hyp_begin,
                                H);
-        hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+        hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(4 * (int64_t)H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
     }
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     else if ((int64_t)P * H <= kSolve4MaxHyps)

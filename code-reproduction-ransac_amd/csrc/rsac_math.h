@@ -1188,8 +1188,30 @@ inline void lm_reduce_blocks_host(int n, const uint8_t *mask, int nv, double *pa
 // ---------------------------------------------------------------------------
 constexpr int kEpnpPairSums = 40;  // 10 control-point pairs x 4 sums
 
+// the rotation of pair (p, q): false (skipped) for apq = 0 or, from the fifth sweep on, apq
+// negligible next to both diagonal entries (Numerical Recipes' rule).  With d = aqq - app, w = 2 apq,
+// h = |d| + sqrt(d^2 + w^2): t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)) = sg |w| / h (theta =
+// d / w), so cs = 1 / sqrt(t^2 + 1) = h / sqrt(h^2 + w^2) and sn = t cs = sg |w| / sqrt(h^2 + w^2):
+// two square roots and one division in the chain (r05; one division fewer than forming t first).
+// MᵀM's entries are far from the squares' overflow.
+RSAC_HD inline bool jrr_rotation(int sweep, double app, double aqq, double apq, double &cs, double &sn) {
+    if (!(apq != 0.0)) return false;
+    if (sweep >= 4) {
+        const double g = 100.0 * dabs(apq);
+        if (dabs(app) + g == dabs(app) && dabs(aqq) + g == dabs(aqq)) return false;
+    }
+    const double d = aqq - app, w = 2.0 * apq;
+    const double sg = (d == 0.0 || ((d < 0.0) == (w < 0.0))) ? 1.0 : -1.0;
+    const double aw = dabs(w), h = dabs(d) + dsqrt(d * d + w * w);
+    const double iq = 1.0 / dsqrt(h * h + aw * aw);
+    cs = h * iq;
+    sn = sg * aw * iq;
+    return true;
+}
 // Cyclic Jacobi of a symmetric N x N matrix (row-major, destroyed): d[k]
-// eigenvalues, V[i * N + k] the k-th eigenvector.  Fixed rotation order.
+// eigenvalues, V[i * N + k] the k-th eigenvector.  Fixed rotation order; the rotation and its
+// skip rule are jrr_rotation's (r05: two square roots and one division in the chain, not three
+// divisions).
 // (N <= 4: the rotation loops unrolled, every index static, so a GPU lane keeps A and V in
 // registers; the order of operations is the same either way)
 template <int N>
@@ -1210,11 +1232,8 @@ RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
         for (int p = 0; p < N - 1; ++p)
 #pragma unroll U
             for (int q = p + 1; q < N; ++q) {
-                const double apq = A[p * N + q];
-                if (apq == 0.0) continue;
-                const double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
-                const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (dabs(theta) + dsqrt(theta * theta + 1.0));
-                const double c = 1.0 / dsqrt(tt * tt + 1.0), sn = tt * c;
+                double c, sn;
+                if (!jrr_rotation(sweep, A[p * N + p], A[q * N + q], A[p * N + q], c, sn)) continue;
 #pragma unroll U
                 for (int k = 0; k < N; ++k) {
                     const double akp = A[k * N + p], akq = A[k * N + q];
@@ -1247,26 +1266,6 @@ RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
 // holds index 0 and position m > 0 holds 1 + (m - 1 + r) % (N - 1); pair i is positions i and
 // N - 1 - i, p the smaller index.  Sweep test as jacobi_eig; the rotation by jrr_rotation.
 RSAC_HD constexpr int jrr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
-// the rotation of pair (p, q): false (skipped) for apq = 0 or, from the fifth sweep on, apq
-// negligible next to both diagonal entries (Numerical Recipes' rule).  With d = aqq - app, w = 2 apq,
-// h = |d| + sqrt(d^2 + w^2): t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)) = sg |w| / h (theta =
-// d / w), so cs = 1 / sqrt(t^2 + 1) = h / sqrt(h^2 + w^2) and sn = t cs = sg |w| / sqrt(h^2 + w^2):
-// two square roots and one division in the chain (r05; one division fewer than forming t first).
-// MᵀM's entries are far from the squares' overflow.
-RSAC_HD inline bool jrr_rotation(int sweep, double app, double aqq, double apq, double &cs, double &sn) {
-    if (!(apq != 0.0)) return false;
-    if (sweep >= 4) {
-        const double g = 100.0 * dabs(apq);
-        if (dabs(app) + g == dabs(app) && dabs(aqq) + g == dabs(aqq)) return false;
-    }
-    const double d = aqq - app, w = 2.0 * apq;
-    const double sg = (d == 0.0 || ((d < 0.0) == (w < 0.0))) ? 1.0 : -1.0;
-    const double aw = dabs(w), h = dabs(d) + dsqrt(d * d + w * w);
-    const double iq = 1.0 / dsqrt(h * h + aw * aw);
-    cs = h * iq;
-    sn = sg * aw * iq;
-    return true;
-}
 // jrr_rotation without branches (the GPU's block form): every lane forms the parameters, a skipped
 // pair then selects cs 1, sn 0; the same bits as jrr_rotation
 RSAC_HD void jrr_rotation_sel(int sweep, double app, double aqq, double apq, double &cs, double &sn) {
@@ -1490,8 +1489,9 @@ RSAC_HD void epnp_gauss_newton(const double *L, const double *rho, double *be) {
 }
 
 // R = U V^T of the 3 x 3 cross-covariance H = sum (pc - pc0)(pw - pw0)^T, with
-// OpenCV's determinant fix (negate the last row); false if H has rank < 2
-RSAC_HD bool epnp_rotation(const double *H, double *R) {
+// OpenCV's determinant fix (negate the last row); false if H has rank < 2.  By the eigen-
+// decomposition of H^T H: epnp_rotation's route for a nearly singular H.
+RSAC_HD bool epnp_rotation_svd(const double *H, double *R) {
     double B[9], V[9], d[3];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) B[3 * i + j] = H[i] * H[j] + H[3 + i] * H[3 + j] + H[6 + i] * H[6 + j];
@@ -1516,6 +1516,72 @@ RSAC_HD bool epnp_rotation(const double *H, double *R) {
     }
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) R[3 * i + j] = u[0][i] * v[0][j] + u[1][i] * v[1][j] + u[2][i] * v[2][j];
+    const double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                       R[2] * (R[3] * R[7] - R[4] * R[6]);
+    if (det < 0.0)
+        for (int j = 0; j < 3; ++j) R[6 + j] = -R[6 + j];
+    return true;
+}
+
+// The orthogonal polar factor U V^T of a well-conditioned 3 x 3 X (in place) by Newton's iteration
+// X <- (g X + X^-T / g) / 2, X^-T = cof(X) / det X, with Frobenius scaling g = (|X^-T|_F / |X|_F)^(1/2)
+// while a step moves an element by more than 1e-2 and g = 1 after, until no element moves by more
+// than 1e-15 (at most 30 steps).  (Unscaled, it is rodr_polar's step.)
+RSAC_HD void polar_newton3(double X[9]) {
+    bool scale = true;
+    for (int it = 0; it < 30; ++it) {
+        double Y[9];
+        Y[0] = X[4] * X[8] - X[5] * X[7];
+        Y[1] = X[5] * X[6] - X[3] * X[8];
+        Y[2] = X[3] * X[7] - X[4] * X[6];
+        Y[3] = X[2] * X[7] - X[1] * X[8];
+        Y[4] = X[0] * X[8] - X[2] * X[6];
+        Y[5] = X[1] * X[6] - X[0] * X[7];
+        Y[6] = X[1] * X[5] - X[2] * X[4];
+        Y[7] = X[2] * X[3] - X[0] * X[5];
+        Y[8] = X[0] * X[4] - X[1] * X[3];
+        const double det = X[0] * Y[0] + X[1] * Y[1] + X[2] * Y[2];
+        if (!(dabs(det) > 1e-300) || !dfinite(det)) return;
+        const double id = 1.0 / det;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Y[k] = Y[k] * id;
+        double g = 1.0, ig = 1.0;
+        if (scale) {
+            double sx = 0.0, sy = 0.0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                sx = sx + X[k] * X[k];
+                sy = sy + Y[k] * Y[k];
+            }
+            g = dsqrt(dsqrt(sy / sx));
+            ig = 1.0 / g;
+        }
+        double mv = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const double nx = 0.5 * (g * X[k] + ig * Y[k]);
+            const double d = dabs(nx - X[k]);
+            mv = d > mv ? d : mv;
+            X[k] = nx;
+        }
+        if (!(mv > 1e-15)) return;
+        scale = mv > 1e-2;
+    }
+}
+
+// epnp_rotation_svd's R: for |det H| > 1e-10 |H|_F^3 (then the smallest singular value exceeds
+// 1e-10 of the largest: full rank) the polar factor of H by polar_newton3 (r05: some 8 short steps
+// in place of two 3 x 3 Jacobi eigen-decompositions), else epnp_rotation_svd itself
+RSAC_HD bool epnp_rotation(const double *H, double *R) {
+    double n2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) n2 = n2 + H[k] * H[k];
+    const double dh = H[0] * (H[4] * H[8] - H[5] * H[7]) - H[1] * (H[3] * H[8] - H[5] * H[6]) +
+                      H[2] * (H[3] * H[7] - H[4] * H[6]);
+    if (!(dabs(dh) > 1e-10 * n2 * dsqrt(n2))) return epnp_rotation_svd(H, R);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = H[k];
+    polar_newton3(R);
     const double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
                        R[2] * (R[3] * R[7] - R[4] * R[6]);
     if (det < 0.0)
@@ -1568,22 +1634,27 @@ RSAC_HD bool epnp_beta(int approx, const double *L, const double *rho, double *b
     double b[6];
     for (int i = 0; i < 6; ++i) b[i] = rho[i];
     bool ok = true;
-    if (approx == 1) {  // columns 0 1 3 6: beta1^2, b1 b2, b1 b3, b1 b4
-        const int cols[4] = {0, 1, 3, 6};
-        double A[24], x[4];
-        for (int i = 0; i < 6; ++i)
-            for (int j = 0; j < 4; ++j) A[4 * i + j] = L[10 * i + cols[j]];
-        householder_ls<6, 4>(A, b, x);
+    // the estimate's columns of L (1: 0 1 3 6, beta1^2, b1 b2, b1 b3, b1 b4; 2: 0 1 2, beta1^2, b1 b2,
+    // b2^2; 3: 0..4, beta1^2, b1 b2, b2^2, b1 b3, b2 b3), zero-padded to 5: householder_ls skips a zero
+    // column's reflection, leaves it zero and gives it x = 0, so x[0, N) carry the 6 x N solve's bits
+    // and the three estimates run one instruction stream (a GPU lane each, k_epnp5_c)
+    double A[30], x[5];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int col = approx == 1 ? (j == 2 ? 3 : j == 3 ? 6 : j) : j;
+            const bool used = approx == 1 ? j < 4 : approx == 2 ? j < 3 : true;
+            A[5 * i + j] = used ? L[10 * i + col] : 0.0;
+        }
+    householder_ls<6, 5>(A, b, x);
+    if (approx == 1) {
         const double sg = x[0] < 0.0 ? -1.0 : 1.0;
         be[0] = dsqrt(sg * x[0]);
         ok = be[0] != 0.0;
         if (ok)
             for (int j = 1; j < 4; ++j) be[j] = sg * x[j] / be[0];
-    } else if (approx == 2) {  // columns 0 1 2: beta1^2, b1 b2, b2^2
-        double A[18], x[3];
-        for (int i = 0; i < 6; ++i)
-            for (int j = 0; j < 3; ++j) A[3 * i + j] = L[10 * i + j];
-        householder_ls<6, 3>(A, b, x);
+    } else {  // 2 and 3
         if (x[0] < 0.0) {
             be[0] = dsqrt(-x[0]);
             be[1] = x[2] < 0.0 ? dsqrt(-x[2]) : 0.0;
@@ -1592,21 +1663,10 @@ RSAC_HD bool epnp_beta(int approx, const double *L, const double *rho, double *b
             be[1] = x[2] > 0.0 ? dsqrt(x[2]) : 0.0;
         }
         if (x[1] < 0.0) be[0] = -be[0];
-    } else {  // columns 0..4: beta1^2, b1 b2, b2^2, b1 b3, b2 b3
-        double A[30], x[5];
-        for (int i = 0; i < 6; ++i)
-            for (int j = 0; j < 5; ++j) A[5 * i + j] = L[10 * i + j];
-        householder_ls<6, 5>(A, b, x);
-        if (x[0] < 0.0) {
-            be[0] = dsqrt(-x[0]);
-            be[1] = x[2] < 0.0 ? dsqrt(-x[2]) : 0.0;
-        } else {
-            be[0] = dsqrt(x[0]);
-            be[1] = x[2] > 0.0 ? dsqrt(x[2]) : 0.0;
+        if (approx == 3) {
+            ok = be[0] != 0.0;
+            if (ok) be[2] = x[3] / be[0];
         }
-        if (x[1] < 0.0) be[0] = -be[0];
-        ok = be[0] != 0.0;
-        if (ok) be[2] = x[3] / be[0];
     }
     if (ok) epnp_gauss_newton(L, rho, be);
     return ok;

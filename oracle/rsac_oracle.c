@@ -2039,7 +2039,28 @@ static void ep_reduce(epctx *c, int nv, ep_fn f, const void *prm, double *out) {
     }
 }
 
-/* cyclic Jacobi, symmetric N x N (destroyed): d eigenvalues, V[i*N+k] k-th eigenvector */
+/* the rotation of pair (p, q) (rsac_math.h jrr_rotation): 0 (skipped) for apq = 0 or, from the fifth
+   sweep on, apq negligible next to both diagonal entries (the rule of Numerical Recipes' jacobi).
+   t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)) = sg |w| / h, theta = d / w, d = aqq - app,
+   w = 2 apq, h = |d| + sqrt(d^2 + w^2); cs = 1 / sqrt(t^2 + 1) = h / sqrt(h^2 + w^2),
+   sn = t cs = sg |w| / sqrt(h^2 + w^2) (one division) */
+static int ep_rot(int sweep, double app, double aqq, double apq, double *cs, double *sn) {
+    if (!(apq != 0.0)) return 0;
+    if (sweep >= 4) {
+        double g = 100.0 * fabs(apq);
+        if (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq)) return 0;
+    }
+    double d = aqq - app, w = 2.0 * apq;
+    double sg = (d == 0.0 || ((d < 0.0) == (w < 0.0))) ? 1.0 : -1.0;
+    double aw = fabs(w), h = fabs(d) + sqrt(d * d + w * w);
+    double iq = 1.0 / sqrt(h * h + aw * aw);
+    *cs = h * iq;
+    *sn = sg * aw * iq;
+    return 1;
+}
+
+/* cyclic Jacobi, symmetric N x N (destroyed): d eigenvalues, V[i*N+k] k-th eigenvector; the
+   rotation and skip rule of ep_rot (r05) */
 static void ep_jacobi(int N, double *A, double *V, double *d) {
     for (int i = 0; i < N * N; ++i) V[i] = 0.0;
     for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
@@ -2052,11 +2073,8 @@ static void ep_jacobi(int N, double *A, double *V, double *d) {
         if (!(off > 1e-32 * diag)) break;
         for (int p = 0; p < N - 1; ++p)
             for (int q = p + 1; q < N; ++q) {
-                double apq = A[p * N + q];
-                if (apq == 0.0) continue;
-                double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
-                double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                double cs = 1.0 / sqrt(tt * tt + 1.0), sn = tt * cs;
+                double cs, sn;
+                if (!ep_rot(sweep, A[p * N + p], A[q * N + q], A[p * N + q], &cs, &sn)) continue;
                 for (int k = 0; k < N; ++k) {
                     double akp = A[k * N + p], akq = A[k * N + q];
                     A[k * N + p] = cs * akp - sn * akq;
@@ -2088,7 +2106,7 @@ static void ep_jacobi(int N, double *A, double *V, double *d) {
    Numerical Recipes' jacobi). */
 static int ep_rr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
 static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
-    int P[8], Q[8], act[8];
+    int P[8], Q[8];
     double cs[8], sn[8];
     const int H = N / 2;
     for (int i = 0; i < N * N; ++i) V[i] = 0.0;
@@ -2109,22 +2127,8 @@ static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
                 int p = a < b ? a : b, q = a < b ? b : a;
                 double apq = A[p * N + q], app = A[p * N + p], aqq = A[q * N + q];
                 P[i] = p; Q[i] = q;
-                act[i] = apq != 0.0;
                 cs[i] = 1.0; sn[i] = 0.0;
-                if (act[i] && sweep >= 4) { /* negligible next to both diagonal entries: skipped */
-                    double g = 100.0 * fabs(apq);
-                    if (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq)) act[i] = 0;
-                }
-                if (!act[i]) continue;
-                /* t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)) = sg |w| / h, theta = d / w,
-                   h = |d| + sqrt(d^2 + w^2); cs = 1 / sqrt(t^2 + 1) = h / sqrt(h^2 + w^2),
-                   sn = t cs = sg |w| / sqrt(h^2 + w^2) (one division) */
-                double d = aqq - app, w = 2.0 * apq;
-                double sg = (d == 0.0 || ((d < 0.0) == (w < 0.0))) ? 1.0 : -1.0;
-                double aw = fabs(w), h = fabs(d) + sqrt(d * d + w * w);
-                double iq = 1.0 / sqrt(h * h + aw * aw);
-                cs[i] = h * iq;
-                sn[i] = sg * aw * iq;
+                (void)ep_rot(sweep, app, aqq, apq, &cs[i], &sn[i]);
             }
             /* a skipped pair applies cs = 1, sn = 0 like any other (no special case, so the device
                runs every step branch-free with the same bits) */
@@ -2255,8 +2259,9 @@ static void ep_f_err(const void *prm, double X, double Y, double Z, double u, do
 }
 
 /* R = U V^T of the cross-covariance H (SVD via the eigen-decomposition of H^T H), last row
- * negated when det < 0 (OpenCV's estimate_R_and_t); 0 when H has rank < 2 */
-static int ep_rotation(const double *H, double *R) {
+ * negated when det < 0 (OpenCV's estimate_R_and_t); 0 when H has rank < 2.  ep_rotation's route
+ * for a nearly singular H (rsac_math.h epnp_rotation_svd). */
+static int ep_rotation_svd(const double *H, double *R) {
     double B[9], V[9], d[3], v[3][3], u[3][3];
     int o[3];
     for (int i = 0; i < 3; ++i)
@@ -2280,6 +2285,64 @@ static int ep_rotation(const double *H, double *R) {
     }
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) R[3 * i + j] = u[0][i] * v[0][j] + u[1][i] * v[1][j] + u[2][i] * v[2][j];
+    double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) + R[2] * (R[3] * R[7] - R[4] * R[6]);
+    if (det < 0.0)
+        for (int j = 0; j < 3; ++j) R[6 + j] = -R[6 + j];
+    return 1;
+}
+
+/* the orthogonal polar factor of a well-conditioned 3 x 3 X, in place (rsac_math.h polar_newton3):
+   Newton's X <- (g X + X^-T / g) / 2, X^-T = cof(X) / det X, g = (|X^-T|_F / |X|_F)^(1/2) while a step
+   moves an element by more than 1e-2, g = 1 after, until no element moves by more than 1e-15 (at
+   most 30 steps) */
+static void ep_polar(double *X) {
+    int scale = 1;
+    for (int it = 0; it < 30; ++it) {
+        double Y[9];
+        Y[0] = X[4] * X[8] - X[5] * X[7];
+        Y[1] = X[5] * X[6] - X[3] * X[8];
+        Y[2] = X[3] * X[7] - X[4] * X[6];
+        Y[3] = X[2] * X[7] - X[1] * X[8];
+        Y[4] = X[0] * X[8] - X[2] * X[6];
+        Y[5] = X[1] * X[6] - X[0] * X[7];
+        Y[6] = X[1] * X[5] - X[2] * X[4];
+        Y[7] = X[2] * X[3] - X[0] * X[5];
+        Y[8] = X[0] * X[4] - X[1] * X[3];
+        double det = X[0] * Y[0] + X[1] * Y[1] + X[2] * Y[2];
+        if (!(fabs(det) > 1e-300) || !isfinite(det)) return;
+        double id = 1.0 / det;
+        for (int k = 0; k < 9; ++k) Y[k] = Y[k] * id;
+        double g = 1.0, ig = 1.0;
+        if (scale) {
+            double sx = 0.0, sy = 0.0;
+            for (int k = 0; k < 9; ++k) {
+                sx = sx + X[k] * X[k];
+                sy = sy + Y[k] * Y[k];
+            }
+            g = sqrt(sqrt(sy / sx));
+            ig = 1.0 / g;
+        }
+        double mv = 0.0;
+        for (int k = 0; k < 9; ++k) {
+            double nx = 0.5 * (g * X[k] + ig * Y[k]);
+            double dd = fabs(nx - X[k]);
+            mv = dd > mv ? dd : mv;
+            X[k] = nx;
+        }
+        if (!(mv > 1e-15)) return;
+        scale = mv > 1e-2;
+    }
+}
+
+/* ep_rotation_svd's R: the polar factor of H (ep_polar) when |det H| > 1e-10 |H|_F^3 (full rank),
+ * else ep_rotation_svd itself (rsac_math.h epnp_rotation) */
+static int ep_rotation(const double *H, double *R) {
+    double n2 = 0.0;
+    for (int k = 0; k < 9; ++k) n2 = n2 + H[k] * H[k];
+    double dh = H[0] * (H[4] * H[8] - H[5] * H[7]) - H[1] * (H[3] * H[8] - H[5] * H[6]) + H[2] * (H[3] * H[7] - H[4] * H[6]);
+    if (!(fabs(dh) > 1e-10 * n2 * sqrt(n2))) return ep_rotation_svd(H, R);
+    for (int k = 0; k < 9; ++k) R[k] = H[k];
+    ep_polar(R);
     double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) + R[2] * (R[3] * R[7] - R[4] * R[6]);
     if (det < 0.0)
         for (int j = 0; j < 3; ++j) R[6 + j] = -R[6 + j];

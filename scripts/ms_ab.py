@@ -1,0 +1,86 @@
+"""Interleaved A/B of librsac builds on ms-to-best (the reference-mode pnp_ransac call on the C2
+problem: adaptive, LM refit) and, with --hyps, the fixed-budget EPnP-5 solve rate.
+
+    python scripts/ms_ab.py build/ab/librsac_a.so build/ab/librsac_b.so ... [--rounds 3]
+
+Each (round, build) runs in its own process (RSAC_LIB_PATH selects the build), in the order
+a b c a b c ..., so clock drift spreads over all builds.  Prints one JSON line per run and the
+median over rounds of each run's median.
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MODES = (("epnp5", "opencv"), ("p3p", "philox"))
+
+
+def worker(calls, hyps):
+    sys.path[:0] = [os.path.join(ROOT, "code-reproduction-ransac_amd")]
+    import torch
+    import rsac
+    from rsac import synth
+    pr = synth.pnp_problem(10_000, 0.5, seed=0)
+    dev = torch.device("cuda", 0)
+    p2, p3 = torch.from_numpy(pr["points2d"]).to(dev), torch.from_numpy(pr["points3d"]).to(dev)
+    out = {"lib": os.path.basename(os.environ.get("RSAC_LIB_PATH", ""))}
+    for minimal, sampler in MODES:
+        walls = []
+        for i in range(calls + 5):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            R, t_, m, info = rsac.pnp_ransac(p2, p3, pr["K"], 5000, 30.0, adaptive=True, refine=True,
+                                             minimal=minimal, sampler=sampler, return_info=True)
+            torch.cuda.synchronize()
+            if i >= 5:
+                walls.append((time.perf_counter() - t) * 1e3)
+        out[f"{minimal}_{sampler}"] = statistics.median(walls)
+        out[f"{minimal}_{sampler}_key"] = [info.iters, int(m.sum())]
+    if hyps:
+        walls = []
+        for i in range(8):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            rsac.pnp_ransac(p2, p3, pr["K"], hyps, 30.0, adaptive=False, refine=False, minimal="epnp5")
+            torch.cuda.synchronize()
+            if i >= 3:
+                walls.append((time.perf_counter() - t) * 1e3)
+        out["epnp5_fixed_hyp_s"] = hyps / statistics.median(walls) * 1e3
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="*")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--calls", type=int, default=30)
+    ap.add_argument("--hyps", type=int, default=0)
+    ap.add_argument("--worker", action="store_true")
+    a = ap.parse_args()
+    if a.worker:
+        worker(a.calls, a.hyps)
+        return
+    res = {lib: [] for lib in a.libs}
+    for _ in range(a.rounds):
+        for lib in a.libs:
+            env = dict(os.environ, RSAC_LIB_PATH=os.path.abspath(lib))
+            r = subprocess.run([sys.executable, "-u", __file__, "--worker", "--calls", str(a.calls), "--hyps",
+                                str(a.hyps)], env=env, capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                print(r.stdout, r.stderr, flush=True)
+                sys.exit(r.returncode)
+            line = r.stdout.strip().splitlines()[-1]
+            print(line, flush=True)
+            res[lib].append(json.loads(line))
+    keys = [k for k in res[a.libs[0]][0] if k != "lib" and not k.endswith("_key")]
+    print("summary (median over rounds):", " ".join(keys))
+    for lib, v in res.items():
+        print(f"  {os.path.basename(lib):28s} " + " ".join(f"{statistics.median(x[k] for x in v):.4g}" for k in keys))
+
+
+if __name__ == "__main__":
+    main()
