@@ -3488,22 +3488,72 @@ struct GpuLmReducer {
         return a + __hiloint2double(dhi, dlo);
     }
 
-    // the range sum of every term of a[0, nv): the wave trees, then the 8 wave sums left to
-    // right; the result is valid in thread q < nv (returns 0 elsewhere)
-    __device__ double range_sum(double *a, int nv) {
+    // x + y of lanes l and l ^ O in the halves a reduce-scatter keeps (O = 32, 16): lanes with bit O
+    // clear keep x's pair, the others y's; v_permlane{32,16}_swap moves each half to the lane that
+    // adds it, and the sum is the xor butterfly's (own + partner on the lower lane; the upper lane's
+    // y[l - O] + y[l] is the lower lane's own + partner)
+    template <int O>
+    __device__ static double add_swap(double x, double y) {
+        const int xl = __double2loint(x), xh = __double2hiint(x), yl = __double2loint(y), yh = __double2hiint(y);
+        int nxl, nxh, nyl, nyh;
+        if constexpr (O == 32) {
+            const auto l = __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+            const auto h = __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+            nxl = l[0]; nyl = l[1]; nxh = h[0]; nyh = h[1];
+        } else {
+            const auto l = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+            const auto h = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+            nxl = l[0]; nyl = l[1]; nxh = h[0]; nyh = h[1];
+        }
+        return __hiloint2double(nxh, nxl) + __hiloint2double(nyh, nyl);
+    }
+
+    // the range sum of every term of a[0, NV): the wave trees, then the 8 wave sums left to
+    // right; the result is valid in thread q < NV (returns 0 elsewhere)
+    template <int NV>
+    __device__ double range_sum(double *a) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        // levels outside, terms inside: the nv reductions are independent and overlap
-        for (int q = 0; q < nv; ++q) a[q] = add_down<32>(a[q]);
-        for (int q = 0; q < nv; ++q) a[q] = add_down<16>(a[q]);
-        for (int q = 0; q < nv; ++q) a[q] = add_down<8>(a[q]);
-        for (int q = 0; q < nv; ++q) a[q] = add_down<4>(a[q]);
-        for (int q = 0; q < nv; ++q) a[q] = add_down<2>(a[q]);
-        for (int q = 0; q < nv; ++q) a[q] = add_down<1>(a[q]);
+        if constexpr (NV == 28) {
+            // the fused cost + normal equations: the same butterfly as a reduce-scatter.  Level 32
+            // pairs term q with q + 14, level 16 pairs q with q + 7 (add_swap), so a lane adds 14
+            // then 7 terms instead of 28 twice; levels 8 .. 1 as below on the 7 left.  Every lane
+            // pair holds one value (a + b == b + a), so each term gets the butterfly's bits; term
+            // 7 r + j ends in c[j] of lane 16 r.  (r05: 21 adds and 42 swaps where the plain trees
+            // spent 56 adds and 112 cross-lane moves on the first two levels)
+            double b[14], c[7];
+#pragma unroll
+            for (int q = 0; q < 14; ++q) b[q] = add_swap<32>(a[q], a[q + 14]);
+#pragma unroll
+            for (int q = 0; q < 7; ++q) c[q] = add_swap<16>(b[q], b[q + 7]);
+#pragma unroll
+            for (int q = 0; q < 7; ++q) c[q] = add_down<8>(c[q]);
+#pragma unroll
+            for (int q = 0; q < 7; ++q) c[q] = add_down<4>(c[q]);
+#pragma unroll
+            for (int q = 0; q < 7; ++q) c[q] = add_down<2>(c[q]);
+#pragma unroll
+            for (int q = 0; q < 7; ++q) c[q] = add_down<1>(c[q]);
 #ifdef RSAC_TRACE
-        mark(21);
+            mark(21);
 #endif
-        if (lane == 0)
-            for (int q = 0; q < nv; ++q) wsum[wave][q] = a[q];
+            if ((lane & 15) == 0)
+#pragma unroll
+                for (int j = 0; j < 7; ++j) wsum[wave][7 * (lane >> 4) + j] = c[j];
+        } else {
+            // levels outside, terms inside: the NV reductions are independent and overlap
+            for (int q = 0; q < NV; ++q) a[q] = add_down<32>(a[q]);
+            for (int q = 0; q < NV; ++q) a[q] = add_down<16>(a[q]);
+            for (int q = 0; q < NV; ++q) a[q] = add_down<8>(a[q]);
+            for (int q = 0; q < NV; ++q) a[q] = add_down<4>(a[q]);
+            for (int q = 0; q < NV; ++q) a[q] = add_down<2>(a[q]);
+            for (int q = 0; q < NV; ++q) a[q] = add_down<1>(a[q]);
+#ifdef RSAC_TRACE
+            mark(21);
+#endif
+            if (lane == 0)
+                for (int q = 0; q < NV; ++q) wsum[wave][q] = a[q];
+        }
+        const int nv = NV;
         __syncthreads();
         double bsum = 0.0;
         if (threadIdx.x < nv) {
@@ -3528,7 +3578,7 @@ struct GpuLmReducer {
 #ifdef RSAC_TRACE
             mark(20);
 #endif
-            const double bsum = range_sum(a, NV);
+            const double bsum = range_sum<NV>(a);
             const int r = first + kk * G;
             if (threadIdx.x < NV) {
                 const int q = threadIdx.x;
