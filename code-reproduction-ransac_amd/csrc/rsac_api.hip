@@ -427,6 +427,7 @@ struct LoopOut {
     // speculative first round (run_loop with a ScanDecide): the records are on their way to
     // the host and the device has picked the winner; spec_resolve replays and verifies
     bool spec_pending = false;
+    ScanFuse fuse;  // a pending speculative PnP scan: the finish's mask launch runs it (k_scan_mask)
     int64_t spec_H = 0;
     bool timing = true;  // HIP events around solve / score (the caller wants rsac_stats)
     // OpenCV's sampler: one MWC state per problem, carried across rounds and across the resume of a
@@ -655,10 +656,22 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
         std::vector<int> full;  // problems scanned from their full count / status rows
         if (!lo && hb == 0) {
             HIPCHK(c->h_scanrec.ensure(sizeof(ScanRecords) * P));
-            // one problem: the kernel writes its record straight into pinned host memory (no copy
-            // launch); many problems: device records and one copy (thousands of scattered 4-byte
-            // writes over PCIe cost more than the copy)
-            if (P == 1) {
+            // a speculative PnP round: the finish's mask launch replays the scan itself
+            // (k_scan_mask), one launch fewer in front of the refit
+            const bool fuse = spec && model == Model::PnP && scan_mask_fusable((int32_t)Hr);
+            if (fuse) {
+                ScanRecords *recs = c->h_scanrec.as<ScanRecords>();
+                if (P > 1) {
+                    HIPCHK(c->scanrec.ensure(sizeof(ScanRecords) * P));
+                    recs = c->scanrec.as<ScanRecords>();
+                    c->scanrec_copy = P;  // copied behind the finish's mask launch
+                }
+                out.fuse = ScanFuse{true, c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, (int32_t)Hr,
+                                    model_points, recs, *spec};
+            } else if (P == 1) {
+                // one problem: the kernel writes its record straight into pinned host memory (no
+                // copy launch); many problems: device records and one copy (thousands of scattered
+                // 4-byte writes over PCIe cost more than the copy)
                 HIPCHK(launch_scan_records(c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, P, (int32_t)Hr,
                                            model_points, c->h_scanrec.as<ScanRecords>(), s,
                                            spec ? *spec : ScanDecide()));
@@ -838,9 +851,14 @@ int finish_masks(rsac_ctx *c, Model model, const Staged &st, void *args, const L
         dmask = c->mask.as<uint8_t>();
     }
     if (N > 0) {
-        if (model == Model::PnP)  // without a refit the winners also go straight to the pinned host records
+        // without a refit the winners also go straight to the pinned host records
+        double *hmodels = defer_sync ? nullptr : c->h_bestmodels.as<double>();
+        if (model == Model::PnP && dev_best && lo.fuse.pending)  // the speculative round's scan, then the masks
+            HIPCHK(launch_scan_mask(lo.fuse, *(PnpArgs *)args, P, max_n, dmask, c->bestmodels.as<double>(), hmodels,
+                                    s));
+        else if (model == Model::PnP)
             HIPCHK(launch_pnp_mask(*(PnpArgs *)args, P, max_n, dbest, dmask, s, hb[0], c->bestmodels.as<double>(),
-                                   defer_sync ? nullptr : c->h_bestmodels.as<double>()));
+                                   hmodels));
         else if (model == Model::Fm)
             HIPCHK(launch_fm_mask(*(HomArgs *)args, P, max_n, dbest, dmask, s, hb[0]));
         else

@@ -137,6 +137,17 @@ struct ScanDecide {
     double confidence = 0;
     int32_t fixed = 0;
 };
+// a speculative PnP round's scan, left to the finish's mask launch (k_scan_mask)
+struct ScanFuse {
+    bool pending = false;
+    const int32_t *counts = nullptr;
+    const int8_t *status = nullptr;
+    int64_t stride = 0;
+    int32_t H = 0;
+    int model_points = 0;
+    ScanRecords *out = nullptr;
+    ScanDecide dec;
+};
 hipError_t launch_scan_records(const int32_t *counts, const int8_t *status, int64_t stride, int32_t P, int32_t H,
                                int model_points, ScanRecords *out, hipStream_t s, ScanDecide dec = ScanDecide());
 
@@ -196,6 +207,9 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 // the packed best key of counts [hyp_begin, hyp_begin + H) of one problem into *a.best_key (no-op
 // without it); launch_pnp_score does this itself when a.best_key is set
 hipError_t launch_pnp_best_key(const PnpArgs &a, int64_t hyp_begin, int32_t H, const int32_t *counts, hipStream_t s);
+bool scan_mask_fusable(int32_t H);
+hipError_t launch_scan_mask(const ScanFuse &f, const PnpArgs &a, int32_t P, int32_t max_n, uint8_t *mask,
+                            double *model_out, double *host_model_out, hipStream_t s);
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
                            hipStream_t s, int64_t best0 = -1, double *model_out = nullptr,
                            double *host_model_out = nullptr);

@@ -1284,15 +1284,17 @@ __global__ __launch_bounds__(256) void k_epnp5_jacobi_b(PnpArgs a, int64_t hyp_b
 }
 
 // 3 of 3: stage 2's rest (L, rho, the beta estimates) and stage 3 (a pose and mean error per
-// estimate, the lowest wins), 4 lanes per hypothesis: lane c < 3 takes estimate c + 1
-// (epnp_beta, epnp_pose_err: the loop bodies of epnp_stage2_post and epnp_stage3), the group
-// then applies epnp_stage3's rule (valid, lowest error, first on ties) to the three and lane 0
-// writes the records (as k_pnp_solve does for P3P)
-__global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, int32_t H) {
+// estimate, the lowest wins), 3 lanes per hypothesis, hpw <= 21 hypotheses per wave (long rounds
+// 21, lane 63 idle: at 430 VGPRs one wave per SIMD, so a 20k-hypothesis round fits the GPU in one
+// pass, r05; short rounds 16, launch_pnp_solve): lane c takes estimate c + 1 (epnp_beta,
+// epnp_pose_err: the loop bodies of epnp_stage2_post and epnp_stage3), the group then applies
+// epnp_stage3's rule (valid, lowest error, first on ties) to the three and lane 0 writes the
+// records (as k_pnp_solve does for P3P)
+__global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, int32_t H, int hpw) {
     const int prob = blockIdx.y;
-    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-    const int hl = gt >> 2, c = gt & 3;
-    const bool live = hl < H;
+    const int lane = threadIdx.x & 63, g = lane / 3, c = lane - 3 * g;
+    const int hl = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * hpw + g;
+    const bool live = g < hpw && hl < H;
     const int64_t h = hyp_begin + hl;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
@@ -1309,7 +1311,7 @@ __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, i
         epnp5_gather(a, p0, idx, q);
         const EpnpStage1 s1 = *reinterpret_cast<const EpnpStage1 *>(E);
         s1ok = s1.ok != 0.0;
-        if (s1ok && c < 3) {
+        if (s1ok) {
             EpnpStage2 s2;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -1329,7 +1331,7 @@ __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, i
         }
     }
     // epnp_stage3's pick over the group's three lanes, in estimate order
-    const int base = threadIdx.x & ~3;
+    const int base = 3 * g;
     int win = -1;
     double best = 0.0;
 #pragma unroll
@@ -2210,12 +2212,10 @@ __global__ __launch_bounds__(256) void k_pnp_score(PnpArgs a, int64_t hyp_begin,
 // mask of one model per problem (best[prob] indexes the models buffer; <0 = none)
 // model_out (optional): block 0 of every problem also copies the winner's record there
 // (k_gather_models' output, one launch fewer)
-__global__ void k_pnp_mask(PnpArgs a, const int64_t *__restrict__ best, int64_t best0, uint8_t *__restrict__ mask,
-                           double *__restrict__ model_out, double *__restrict__ host_model_out) {
-    const int prob = blockIdx.y;
+__device__ __forceinline__ void pnp_mask_body(const PnpArgs &a, int prob, int64_t b, uint8_t *__restrict__ mask,
+                                              double *__restrict__ model_out, double *__restrict__ host_model_out) {
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
-    const int64_t b = best ? best[prob] : best0;  // best0: the one problem's record, no upload
     if (model_out && blockIdx.x == 0 && threadIdx.x < kModelStride) {
         const double v = b >= 0 ? a.models[b * kModelStride + threadIdx.x] : 0.0;
         model_out[(int64_t)prob * kModelStride + threadIdx.x] = v;
@@ -2233,6 +2233,12 @@ __global__ void k_pnp_mask(PnpArgs a, const int64_t *__restrict__ best, int64_t 
         }
         mask[p0 + i] = f;
     }
+}
+__global__ void k_pnp_mask(PnpArgs a, const int64_t *__restrict__ best, int64_t best0, uint8_t *__restrict__ mask,
+                           double *__restrict__ model_out, double *__restrict__ host_model_out) {
+    const int prob = blockIdx.y;
+    // best0: the one problem's record, no upload
+    pnp_mask_body(a, prob, best ? best[prob] : best0, mask, model_out, host_model_out);
 }
 
 // mask of the hypothesis named by a packed key (problem 0, records from hypothesis 0)
@@ -2536,9 +2542,9 @@ __global__ __launch_bounds__(256) void k_best_key(const int32_t *__restrict__ co
 
 // the device replay of a problem's scan on its records (scan_records of rsac_host.hip): one wave,
 // wave-uniform; ridx / rcnt in LDS, written before the call
-__device__ __forceinline__ void scan_decide(const int32_t *ridx, const int32_t *rcnt, int nrec, int first_neg, int H,
-                                            int model_points, int prob, int64_t stride, const ScanDecide &dec,
-                                            ScanRecords &o, int lane) {
+__device__ __forceinline__ int64_t scan_decide(const int32_t *ridx, const int32_t *rcnt, int nrec, int first_neg, int H,
+                                               int model_points, int prob, int64_t stride, const ScanDecide &dec,
+                                               ScanRecords &o, int lane, bool write = true) {
     // scan_records (rsac_host.hip) on the records lane 0 just wrote.  update_num_iters'
     // logarithms (the latency) for every record at once, lane r for record r; the
     // sequential part on them is uniform across the wave.
@@ -2572,31 +2578,25 @@ __device__ __forceinline__ void scan_decide(const int32_t *ridx, const int32_t *
     const int64_t stop = first_neg < niters ? first_neg : niters;
     // fixed budget: the round is the whole budget, so the replay always ends in it
     const bool done = nrec <= kScanRecs && (dec.fixed || stop < H || H >= niters);
-    if (lane == 0) {
-        // not done: the speculative finish has no model (cheap no-op); the record index of
-        // problem prob's winner (problem 0: the hypothesis itself)
-        dec.best_out[prob] = done && best >= 0 ? (int64_t)prob * stride + best : -1;
+    // not done: the speculative finish has no model (cheap no-op); the record index of problem
+    // prob's winner (problem 0: the hypothesis itself)
+    const int64_t pick = done && best >= 0 ? (int64_t)prob * stride + best : -1;
+    if (lane == 0 && write) {
+        dec.best_out[prob] = pick;
         o.dev_best = (int32_t)best;
         o.dev_done = done;
     }
+    return pick;
 }
 
-// one wave per problem: 64 hypotheses per step, the running maximum carried across steps
-__global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict__ counts,
-                                                      const int8_t *__restrict__ status, int64_t stride, int32_t P,
-                                                      int32_t H, int model_points, ScanRecords *__restrict__ out,
-                                                      ScanDecide dec) {
-    // records kept in LDS and written out once: out may be pinned host memory (no copy back)
-    __shared__ int32_t sidx[4][kScanRecs], scnt[4][kScanRecs];
-    const int prob = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (prob >= P) return;  // wave-uniform
-    const int lane = threadIdx.x & 63;
-    int32_t *ridx = sidx[threadIdx.x >> 6], *rcnt = scnt[threadIdx.x >> 6];
-    const int32_t *c = counts + (int64_t)prob * stride;
-    const int8_t *st = status + (int64_t)prob * stride;
+// One wave's replay of a problem's scan over its round (c, st: the problem's count and status
+// rows): the prefix-maximum records (ridx, rcnt in LDS, lane 0 writes; at most kScanRecs kept,
+// nrec counts them all) and the first status < 0 (H if none); nrec and first_neg wave-uniform.
+__device__ __forceinline__ void scan_wave(const int32_t *__restrict__ c, const int8_t *__restrict__ st, int H,
+                                          int model_points, int lane, int32_t *ridx, int32_t *rcnt, int &nrec_out,
+                                          int &first_neg_out) {
     int floor_c = model_points - 1;  // the scan's floor: max(s - 1, best count so far)
     int nrec = 0, first_neg = H;
-    ScanRecords &o = out[prob];
     // 8 steps' loads in flight at a time (one step's round trip each was the kernel's time)
     constexpr int U = 8;
     bool stop = false;
@@ -2636,6 +2636,25 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
             }
         }
     }
+    nrec_out = nrec;
+    first_neg_out = first_neg;
+}
+
+// one wave per problem: 64 hypotheses per step, the running maximum carried across steps
+__global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict__ counts,
+                                                      const int8_t *__restrict__ status, int64_t stride, int32_t P,
+                                                      int32_t H, int model_points, ScanRecords *__restrict__ out,
+                                                      ScanDecide dec) {
+    // records kept in LDS and written out once: out may be pinned host memory (no copy back)
+    __shared__ int32_t sidx[4][kScanRecs], scnt[4][kScanRecs];
+    const int prob = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (prob >= P) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    int32_t *ridx = sidx[threadIdx.x >> 6], *rcnt = scnt[threadIdx.x >> 6];
+    int nrec, first_neg;
+    scan_wave(counts + (int64_t)prob * stride, status + (int64_t)prob * stride, H, model_points, lane, ridx, rcnt,
+              nrec, first_neg);
+    ScanRecords &o = out[prob];
     if (lane == 0) {
         o.nrec = nrec <= kScanRecs ? nrec : -1;
         o.first_neg = first_neg;
@@ -2646,8 +2665,43 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
     }
     if (dec.best_out && (dec.fixed || prob == 0)) {  // wave-uniform
         __builtin_amdgcn_wave_barrier();
-        scan_decide(ridx, rcnt, nrec, first_neg, H, model_points, prob, stride, dec, o, lane);
+        (void)scan_decide(ridx, rcnt, nrec, first_neg, H, model_points, prob, stride, dec, o, lane);
     }
+}
+// The speculative finish's scan and masks in one launch (PnP, rounds below kScanBlockH): block
+// (x, prob)'s first wave replays problem prob's scan (scan_wave + scan_decide, the operations of
+// k_scan_records; block 0 writes the records and the pick), then the block masks its points for
+// the pick as k_pnp_mask does, and block 0 gathers the winner's record.  Every block replays the
+// scan itself (a few records), so no block waits for another (r05: one launch and its dispatch
+// gap fewer on the ms-to-best path).
+__global__ __launch_bounds__(256) void k_scan_mask(const int32_t *__restrict__ counts, const int8_t *__restrict__ status,
+                                                   int64_t stride, int32_t H, int model_points, ScanRecords *out,
+                                                   ScanDecide dec, PnpArgs a, uint8_t *__restrict__ mask,
+                                                   double *__restrict__ model_out, double *__restrict__ host_model_out) {
+    __shared__ int32_t ridx[kScanRecs], rcnt[kScanRecs];
+    __shared__ int64_t sbest;
+    const int prob = blockIdx.y;
+    if (threadIdx.x < 64) {  // wave 0
+        const int lane = threadIdx.x;
+        int nrec, first_neg;
+        scan_wave(counts + (int64_t)prob * stride, status + (int64_t)prob * stride, H, model_points, lane, ridx, rcnt,
+                  nrec, first_neg);
+        ScanRecords &o = out[prob];
+        const bool lead = blockIdx.x == 0;
+        if (lead && lane == 0) {
+            o.nrec = nrec <= kScanRecs ? nrec : -1;
+            o.first_neg = first_neg;
+            for (int r = 0; r < nrec && r < kScanRecs; ++r) {
+                o.idx[r] = ridx[r];
+                o.cnt[r] = rcnt[r];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int64_t b = scan_decide(ridx, rcnt, nrec, first_neg, H, model_points, prob, stride, dec, o, lane, lead);
+        if (lane == 0) sbest = b;
+    }
+    __syncthreads();
+    pnp_mask_body(a, prob, sbest, mask, model_out, host_model_out);
 }
 
 // k_scan_records for long rounds (H >= kScanBlockH: a fixed budget of 100k hypotheses, C4): one
@@ -2980,7 +3034,8 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
         else
             hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv((int64_t)kEpG * H, 256), P), dim3(256), 0, s, ka, hyp_begin,
                                H);
-        hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(4 * (int64_t)H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
+        const int hpw = short_round ? 16 : 21;  // hypotheses per wave of stage 3 (3 lanes each)
+        hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(cdiv(H, hpw), tb / 64), P), dim3(tb), 0, s, ka, hyp_begin, H, hpw);
     }
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     else if ((int64_t)P * H <= kSolve4MaxHyps)
@@ -3122,6 +3177,15 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     return hipGetLastError();
 }
 
+bool scan_mask_fusable(int32_t H) { return H < kScanBlockH; }
+hipError_t launch_scan_mask(const ScanFuse &f, const PnpArgs &a, int32_t P, int32_t max_n, uint8_t *mask,
+                            double *model_out, double *host_model_out, hipStream_t s) {
+    unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_scan_mask, dim3(g, P), dim3(256), 0, s, f.counts, f.status, f.stride, f.H, f.model_points,
+                       f.out, f.dec, a, mask, model_out, host_model_out);
+    return hipGetLastError();
+}
 hipError_t launch_pnp_mask(const PnpArgs &a, int32_t P, int32_t max_n, const int64_t *best, uint8_t *mask,
                            hipStream_t s, int64_t best0, double *model_out, double *host_model_out) {
     unsigned g = cdiv(max_n > 0 ? max_n : 1, 256);
