@@ -943,9 +943,10 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
     *reinterpret_cast<EpnpStage1 *>(a.epnp + ((int64_t)prob * H + hl) * kEpnpRec) = s1;
 }
 
-// 2 of 3: M^T M's eigenvectors by the round-robin Jacobi of jacobi_eig_rr<12>, 16 lanes per
-// hypothesis (4 per wave).  Lane j < 12 builds row j of A (epnp_mtm's entries) and holds rows j
-// of A and V in registers; the group's A is mirrored row by row in LDS (the step-start matrix
+// 2 of 3: M^T M's eigenvectors by the round-robin Jacobi of jacobi_eig_rr<12>, 12 lanes per
+// hypothesis (5 per wave, lanes 60..63 idle; r05, 4 of 16 lanes were idle).  Lane j builds row j of
+// A (epnp_mtm's entries) and holds rows j of A and V in registers; the group's A is mirrored row by
+// row in LDS (the step-start matrix
 // after every step), where each lane reads its pair's A[p][p], A[q][q], A[p][q] and, after the
 // column phase, its partner's row.  A step (static r, every pair's indices compile-time constants):
 //   params:  both lanes of pair (p, q) form its cs, sn from the step-start matrix (the same
@@ -954,18 +955,22 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
 //   rows:    lanes p and q exchange their column-rotated rows through LDS and form
 //            cs a + x o (x = -sn on lane p, +sn on lane q: jacobi_eig_rr's cs a - sn o and
 //            sn o + cs a, the same bits).
-// A sweep is 11 steps instead of 66 dependent rotations; the sweep test reads the upper triangle
-// from LDS in jacobi_eig_rr's order.  Groups whose sweeps end early idle until the wave's last
-// group is done.
-constexpr int kEpG = 16;  // lanes per hypothesis
+// A sweep is 11 steps instead of 66 dependent rotations; for the sweep test lane j forms its row's
+// terms from its registers (A_jj^2 and the partial sum_{q > j} A_jq^2 in q order, jacobi_eig_rr's)
+// and every lane adds the group's 12 in row order (r05: each lane had read the whole upper
+// triangle from LDS).  Groups whose sweeps end early idle until the wave's last group is done.
+constexpr int kEpG = 12;                // lanes per hypothesis
+constexpr int kEpGW = 5;                // hypotheses per wave
+constexpr int kEpGB = 256 / 64 * kEpGW;  // hypotheses per 256-thread block
 // LDS row stride of the mirrored matrices (doubles): 13, not 12, so the 12 rows of one column (and
 // the 4 groups of a wave, the A and V rows of the latency form) fall in distinct banks: 2-way at
 // most where 12 gave 6- to 8-way (SQ_LDS_BANK_CONFLICT, profiles/r04_epnp_pmc.json)
 constexpr int kEpR = 13;
 struct EpnpJacLds {
-    double A[256 / kEpG][12 * kEpR];
-    double cs[256 / kEpG][12];  // pair i: cs at 2i, sn at 2i + 1
-    int ord[256 / kEpG][12];    // eig_order_desc's order of the eigenvalues
+    double A[kEpGB][12 * kEpR];
+    double cs[kEpGB][12];    // pair i: cs at 2i, sn at 2i + 1
+    double part[kEpGB][24];  // the sweep test's row terms: A_pp^2 at 2p, sum_{q > p} A_pq^2 at 2p + 1
+    int ord[kEpGB][12];      // eig_order_desc's order of the eigenvalues
 };
 RSAC_HD constexpr int jrr_p(int r, int i) {
     return jrr_pos(12, r, i) < jrr_pos(12, r, 11 - i) ? jrr_pos(12, r, i) : jrr_pos(12, r, 11 - i);
@@ -1052,15 +1057,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
     PnpArgs a, int64_t hyp_begin, int32_t H) {
     __shared__ EpnpJacLds L;
     const int prob = blockIdx.y;
-    const int j = threadIdx.x & (kEpG - 1), hb = threadIdx.x / kEpG;
-    const int hl = (int)((blockIdx.x * 256u + threadIdx.x) / kEpG);
+    const int lane = threadIdx.x & 63, gw = lane / kEpG, j = lane - kEpG * gw;
+    const bool row = gw < kEpGW;  // lanes 60..63: no group
+    const int hb = (int)(threadIdx.x >> 6) * kEpGW + (row ? gw : 0);
+    const int hl = (int)blockIdx.x * kEpGB + hb;
     const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
     double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;  // launch-local scratch
     const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
-    const bool live = hl < H && a.status[rec] > 0 && s1->ok != 0.0;
-    const bool row = j < 12;
+    const bool live = row && hl < H && a.status[rec] > 0 && s1->ok != 0.0;
     bool run = live;
-    double *LA = L.A[hb], *LC = L.cs[hb];
+    double *LA = L.A[hb], *LC = L.cs[hb], *LP = L.part[hb];
     double A[12], V[12];
 #pragma unroll
     for (int c = 0; c < 12; ++c) {
@@ -1086,23 +1092,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
     }
     ep_wave_sync();
     for (int sweep = 0; sweep < 60; ++sweep) {
+        if (run) {  // row j's terms from the registers (they hold the mirror's row j)
+            double dp = 0.0, rp = 0.0;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) {
+                dp = q == j ? A[q] : dp;
+                rp = q > j ? rp + A[q] * A[q] : rp;
+            }
+            LP[2 * j] = dp * dp;
+            LP[2 * j + 1] = rp;
+        }
+        ep_wave_sync();
         if (run) {
-            // one row of loads at a time (all 78 at once would hold 156 VGPRs)
             double off = 0.0, diag = 0.0;
-#pragma unroll 1
+#pragma unroll
             for (int p = 0; p < 12; ++p) {
-                double rw[12];
-#pragma unroll
-                for (int q = 0; q < 12; ++q) rw[q] = LA[kEpR * p + q];
-                double dp = 0.0;
-#pragma unroll
-                for (int q = 0; q < 12; ++q) dp = q == p ? rw[q] : dp;
-                diag = diag + dp * dp;
-                double rp = 0.0;
-#pragma unroll
-                for (int q = 1; q < 12; ++q)
-                    if (q > p) rp = rp + rw[q] * rw[q];
-                off = off + rp;
+                diag = diag + LP[2 * p];
+                off = off + LP[2 * p + 1];
             }
             if (!(off > 1e-32 * diag)) run = false;
         }
@@ -3032,8 +3038,7 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
         if (short_round)
             hipLaunchKernelGGL(k_epnp5_jacobi_b, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
         else
-            hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv((int64_t)kEpG * H, 256), P), dim3(256), 0, s, ka, hyp_begin,
-                               H);
+            hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv(H, kEpGB), P), dim3(256), 0, s, ka, hyp_begin, H);
         const int hpw = short_round ? 16 : 21;  // hypotheses per wave of stage 3 (3 lanes each)
         hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(cdiv(H, hpw), tb / 64), P), dim3(tb), 0, s, ka, hyp_begin, H, hpw);
     }
