@@ -656,18 +656,14 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
         std::vector<int> full;  // problems scanned from their full count / status rows
         if (!lo && hb == 0) {
             HIPCHK(c->h_scanrec.ensure(sizeof(ScanRecords) * P));
-            // a speculative PnP round: the finish's mask launch replays the scan itself
-            // (k_scan_mask), one launch fewer in front of the refit
-            const bool fuse = spec && model == Model::PnP && scan_mask_fusable((int32_t)Hr);
+            // a speculative one-problem PnP round: the finish's mask launch replays the scan itself
+            // (k_scan_mask), one launch fewer in front of the refit.  (Batches keep the two launches:
+            // every mask block of every problem replaying its problem's scan made C3's scan + masks
+            // 39 us against 21, r05.)
+            const bool fuse = spec && P == 1 && model == Model::PnP && scan_mask_fusable((int32_t)Hr);
             if (fuse) {
-                ScanRecords *recs = c->h_scanrec.as<ScanRecords>();
-                if (P > 1) {
-                    HIPCHK(c->scanrec.ensure(sizeof(ScanRecords) * P));
-                    recs = c->scanrec.as<ScanRecords>();
-                    c->scanrec_copy = P;  // copied behind the finish's mask launch
-                }
                 out.fuse = ScanFuse{true, c->counts.as<int32_t>(), c->status.as<int8_t>(), stride, (int32_t)Hr,
-                                    model_points, recs, *spec};
+                                    model_points, c->h_scanrec.as<ScanRecords>(), *spec};
             } else if (P == 1) {
                 // one problem: the kernel writes its record straight into pinned host memory (no
                 // copy launch); many problems: device records and one copy (thousands of scattered

@@ -2674,7 +2674,8 @@ __global__ __launch_bounds__(256) void k_scan_records(const int32_t *__restrict_
         (void)scan_decide(ridx, rcnt, nrec, first_neg, H, model_points, prob, stride, dec, o, lane);
     }
 }
-// The speculative finish's scan and masks in one launch (PnP, rounds below kScanBlockH): block
+// The speculative finish's scan and masks in one launch (one PnP problem, rounds below
+// kScanBlockH; the kernel takes any number of problems, the host launches it for one): block
 // (x, prob)'s first wave replays problem prob's scan (scan_wave + scan_decide, the operations of
 // k_scan_records; block 0 writes the records and the pick), then the block masks its points for
 // the pick as k_pnp_mask does, and block 0 gathers the winner's record.  Every block replays the
