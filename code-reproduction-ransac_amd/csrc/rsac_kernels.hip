@@ -1929,6 +1929,16 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 #ifndef RSAC_MF_LONG_W
 #define RSAC_MF_LONG_W 4
 #endif
+#ifndef RSAC_MF_SHORT_W
+#define RSAC_MF_SHORT_W 2
+#endif
+// the batch instance (W = RSAC_MF_SHORT_W: many short problems, C3) loads iteration i + 1's point
+// operands before iteration i computes: its problems' points miss L2 more often (C3 92 % hits
+// against C2's 98 %, profiles/r05/pmc_scorer_c2_c3.json) and the prefetch took C3 0.956 -> 0.931 ms,
+// while the long-problem instance ran 4 % slower with it (scripts/mf_ab.py, r05)
+#ifndef RSAC_MF_PREFETCH_W
+#define RSAC_MF_PREFETCH_W RSAC_MF_SHORT_W
+#endif
 #ifndef RSAC_MF_TID_OPAQUE
 #define RSAC_MF_TID_OPAQUE 1
 #endif
@@ -2014,11 +2024,26 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
     };
     const int full = n >= b0 + 64 ? (n - b0 - 64) / T + 1 : 0;  // iterations with 64 points in range
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (W == RSAC_MF_PREFETCH_W) {
+    if (full > 0) {  // the next iteration's operands in flight while this one computes
+        mf_h8 Ba, Bb;
+        float2 ua, ub;
+        mf_load_full(PF, UV, b0, col, half, Ba, Bb, ua, ub);
+        for (int i = 0; i < full; ++i) {
+            mf_h8 Na = Ba, Nb = Bb;
+            float2 na = ua, nb = ub;
+            if (i + 1 < full) mf_load_full(PF, UV, b0 + T * (i + 1), col, half, Na, Nb, na, nb);
+            body(i, Ba, Bb, ua, ub);
+            Ba = Na; Bb = Nb; ua = na; ub = nb;
+        }
+    }
+    } else {
     for (int i = 0; i < full; ++i) {
         mf_h8 Ba, Bb;
         float2 ua, ub;
         mf_load_full(PF, UV, b0 + T * i, col, half, Ba, Bb, ua, ub);
         body(i, Ba, Bb, ua, ub);
+    }
     }
     if (full < iters) {
         mf_h8 Ba, Bb;
@@ -3123,9 +3148,6 @@ static hipError_t launch_sc(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int
 // Batches of short problems (more than one problem, every one of at most kMfShortN points) run the
 // 2-wave instance.
 constexpr int64_t kMfShortN = 4096;
-#ifndef RSAC_MF_SHORT_W
-#define RSAC_MF_SHORT_W 2
-#endif
 template <int W>
 static hipError_t launch_mf_w(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
                               hipStream_t s) {
