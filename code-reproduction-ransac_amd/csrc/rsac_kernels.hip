@@ -1140,6 +1140,214 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_W
     for (int i = 0; i < 4; ++i) E[64 + 12 * i + j] = LA[kEpR * j + O[11 - i]];  // ut[i][j] = V[j][o[11 - i]]
 }
 
+// position m of step R's circle (jrr_pos(12, R, m)) for a position known only at run time
+template <int R>
+__device__ __forceinline__ int jrr_pos_r(int m) {
+    int v = m - 1 + R;  // 0 .. 20 for m >= 1
+    v = v >= 11 ? v - 11 : v;
+    return m == 0 ? 0 : 1 + v;
+}
+// The throughput form by rotation pairs (r05): 6 lanes per hypothesis, 10 per wave (lanes 60..63
+// idle).  Lane i owns pair i of every step, i.e. the rows at positions i and 11 - i of the circle
+// (jrr_pos: at step r the indices pos(r, i), pos(r, 11 - i)), and rows 2i, 2i + 1 of V.  A step:
+//   params:  the pair's app, aqq, apq from the LDS mirror of the step-start matrix (row-indexed);
+//   post:    cs, sn to the group's 12 slots; every lane reads all 12;
+//   columns: the 6 pairs' column rotations on the lane's two A rows and two V rows (static indices);
+//   rows:    the row rotation of its own pair (both rows in the lane: no exchange);
+//   mirror:  the two rows back to the mirror at their indices, then the next step's two rows read.
+// Each element sees jacobi_eig_rr's operations in its order (the same bits as k_epnp5_jacobi and the
+// oracle's ep_jacobi_rr).  Per hypothesis and step 6 lanes move 2 rows each through LDS where the
+// 12-lane form moves 12 rows twice; the VALU work is the same.
+constexpr int kJ6W = 10;              // hypotheses per wave
+constexpr int kJ6B = 256 / 64 * kJ6W;  // per 256-thread block
+struct EpnpJ6Lds {
+    double M[kJ6B][12 * kEpR];  // the step-start matrix (row-indexed); at the end V's rows
+    double cs[kJ6B][24];        // pair i: cs at 2i, sn at 2i + 1; the sweep test's row terms at the sweep's start
+    int ord[kJ6B][12];
+};
+template <int R>
+__device__ __forceinline__ void epnp_j6_step(int sweep, int i, double (&a0)[12], double (&a1)[12], double (&v0)[12],
+                                             double (&v1)[12], double *LM, double *LC) {
+    const int i0 = jrr_pos_r<R>(i), i1 = jrr_pos_r<R>(11 - i);
+    const bool f = i0 < i1;  // slot 0 holds row p
+    const int p = f ? i0 : i1, q = f ? i1 : i0;
+    double cs = 1.0, sn = 0.0;  // a skipped pair: the identity rotation (jacobi_eig_rr)
+    (void)jrr_rotation(sweep, LM[(kEpR + 1) * p], LM[(kEpR + 1) * q], LM[kEpR * p + q], cs, sn);
+    LC[2 * i] = cs;
+    LC[2 * i + 1] = sn;
+    ep_wave_sync();
+    double c6[6], s6[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        c6[k] = LC[2 * k];
+        s6[k] = LC[2 * k + 1];
+    }
+    // columns (every pair; static indices) of the two A rows and the two V rows
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int P = jrr_p(R, k), Q = jrr_q(R, k);
+        const double c = c6[k], s = s6[k];
+        double x, y;
+        x = a0[P]; y = a0[Q]; a0[P] = c * x - s * y; a0[Q] = s * x + c * y;
+        x = a1[P]; y = a1[Q]; a1[P] = c * x - s * y; a1[Q] = s * x + c * y;
+        x = v0[P]; y = v0[Q]; v0[P] = c * x - s * y; v0[Q] = s * x + c * y;
+        x = v1[P]; y = v1[Q]; v1[P] = c * x - s * y; v1[Q] = s * x + c * y;
+    }
+    // rows of the lane's own pair: row p <- cs p - sn q, row q <- sn p + cs q (as the 12-lane form:
+    // cs a + x o with x = -sn on row p, +sn on row q: the same bits)
+    const double x0 = f ? -sn : sn, x1 = f ? sn : -sn;
+    double n0[12], n1[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        n0[k] = cs * a0[k] + x0 * a1[k];
+        n1[k] = cs * a1[k] + x1 * a0[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        LM[kEpR * i0 + k] = n0[k];
+        LM[kEpR * i1 + k] = n1[k];
+    }
+    ep_wave_sync();
+    // the next step's rows (step R + 1; after step 10 the next sweep's step 0)
+    constexpr int Rn = R + 1 < 11 ? R + 1 : 0;
+    const int j0 = jrr_pos_r<Rn>(i), j1 = jrr_pos_r<Rn>(11 - i);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        a0[k] = LM[kEpR * j0 + k];
+        a1[k] = LM[kEpR * j1 + k];
+    }
+    // V's rotations complete inside the step (left free, the scheduler sinks them and holds every
+    // step's cs, sn live)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        asm volatile("" : "+v"(v0[k]));
+        asm volatile("" : "+v"(v1[k]));
+    }
+}
+template <int R>
+__device__ __forceinline__ void epnp_j6_sweep(int sweep, int i, double (&a0)[12], double (&a1)[12], double (&v0)[12],
+                                              double (&v1)[12], double *LM, double *LC) {
+    if constexpr (R < 11) {
+        epnp_j6_step<R>(sweep, i, a0, a1, v0, v1, LM, LC);
+        epnp_j6_sweep<R + 1>(sweep, i, a0, a1, v0, v1, LM, LC);
+    }
+}
+// a row's sweep-test terms (jacobi_eig_rr's): A_rr^2 and sum_{q > r} A_rq^2 in q order
+__device__ __forceinline__ void j6_row_terms(const double (&a)[12], int r, double &dd, double &rp) {
+    double d = 0.0;
+    rp = 0.0;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        d = k == r ? a[k] : d;
+        rp = k > r ? rp + a[k] * a[k] : rp;
+    }
+    dd = d * d;
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_epnp5_jacobi6(
+    PnpArgs a, int64_t hyp_begin, int32_t H) {
+    __shared__ EpnpJ6Lds L;
+    const int prob = blockIdx.y;
+    const int lane = threadIdx.x & 63, gw = lane / 6, i = lane - 6 * gw;
+    const bool slot = gw < kJ6W;  // lanes 60..63: no group
+    const int hb = (int)(threadIdx.x >> 6) * kJ6W + (slot ? gw : 0);
+    const int hl = (int)blockIdx.x * kJ6B + hb;
+    const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
+    double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;  // launch-local scratch
+    const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
+    const bool live = slot && hl < H && a.status[rec] > 0 && s1->ok != 0.0;
+    bool run = live;
+    double *LM = L.M[hb], *LC = L.cs[hb];
+    double a0[12], a1[12], v0[12], v1[12];
+    // rows 2i, 2i + 1 of V = I; rows pos(0, i), pos(0, 11 - i) of epnp_mtm's matrix
+    const int r0 = jrr_pos_r<0>(i), r1 = jrr_pos_r<0>(11 - i);
+#pragma unroll
+    for (int c = 0; c < 12; ++c) {
+        v0[c] = c == 2 * i ? 1.0 : 0.0;
+        v1[c] = c == 2 * i + 1 ? 1.0 : 0.0;
+        a0[c] = 0.0;
+        a1[c] = 0.0;
+    }
+    if (run) {
+        const double *cm = a.cams + 4 * prob;
+        const double fx = cm[0], fy = cm[1];
+        constexpr int first[4] = {0, 4, 7, 9};  // pair (x <= y) -> sum block x's first + (y - x)
+        auto build = [&](int jr, double (&row)[12]) {  // row jr = 3 ib + pp
+            const int ib = jr / 3, pp = jr - 3 * ib;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const int lo = min(ib, jj), hi = max(ib, jj);
+                const double *ps = s1->pairs + 4 * (first[lo] + hi - lo);
+                const double s0 = ps[0], su = ps[1], sv = ps[2], sw = ps[3];
+                const double blk[9] = {fx * fx * s0, 0.0, fx * su, 0.0, fy * fy * s0, fy * sv, fx * su, fy * sv, sw};
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) row[3 * jj + rr] = pp == 0 ? blk[rr] : pp == 1 ? blk[3 + rr] : blk[6 + rr];
+            }
+        };
+        build(r0, a0);
+        build(r1, a1);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            LM[kEpR * r0 + k] = a0[k];
+            LM[kEpR * r1 + k] = a1[k];
+        }
+    }
+    ep_wave_sync();
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        // the sweep test: the lane's two rows' terms (a0, a1 hold rows pos(0, i), pos(0, 11 - i)),
+        // every lane of the group adds the 12 rows' in row order
+        if (run) {
+            double d0, p0, d1, p1;
+            j6_row_terms(a0, r0, d0, p0);
+            j6_row_terms(a1, r1, d1, p1);
+            LC[2 * r0] = d0;
+            LC[2 * r0 + 1] = p0;
+            LC[2 * r1] = d1;
+            LC[2 * r1 + 1] = p1;
+        }
+        ep_wave_sync();
+        if (run) {
+            double off = 0.0, diag = 0.0;
+#pragma unroll
+            for (int r = 0; r < 12; ++r) {
+                diag = diag + LC[2 * r];
+                off = off + LC[2 * r + 1];
+            }
+            if (!(off > 1e-32 * diag)) run = false;
+        }
+        if (__ballot(run) == 0) break;
+        ep_wave_sync();  // every lane has read the test's terms before the first step posts
+        if (run) epnp_j6_sweep<0>(sweep, i, a0, a1, v0, v1, LM, LC);
+    }
+    if (!live) return;
+    // eig_order_desc<12> on the diagonal (the mirror holds the final matrix), then V's rows
+    int *O = L.ord[hb];
+    if (i == 0) {
+        for (int k = 0; k < 12; ++k) O[k] = k;
+        for (int k = 1; k < 12; ++k) {
+            const int kk = O[k];
+            const double dk = LM[(kEpR + 1) * kk];
+            int jx = k - 1;
+            while (jx >= 0 && LM[(kEpR + 1) * O[jx]] < dk) {
+                O[jx + 1] = O[jx];
+                --jx;
+            }
+            O[jx + 1] = kk;
+        }
+    }
+    ep_wave_sync();
+#pragma unroll
+    for (int c = 0; c < 12; ++c) {  // lane 0's sort has read the diagonal
+        LM[kEpR * (2 * i) + c] = v0[c];
+        LM[kEpR * (2 * i + 1) + c] = v1[c];
+    }
+    ep_wave_sync();
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {  // ut[ii][j] = V[j][o[11 - ii]], element 8 i + t of 48
+        const int e = 8 * i + t, ii = e / 12, j = e - 12 * ii;
+        E[64 + e] = LM[kEpR * j + O[11 - ii]];
+    }
+}
+
 // The latency form of k_epnp5_jacobi for short rounds (an adaptive run's first 256 hypotheses):
 // one wave per hypothesis in 2 x 2 blocks.  In step r the 12 indices form the 6 pairs of
 // jacobi_eig_rr; lane (a, b) < 36 holds A's block at rows pair a x columns pair b and V's block at
@@ -1159,13 +1367,6 @@ struct EpnpJacLdsB {
     double part[4][24];  // row p: A_pp^2 at 2p, sum_{q > p} A_pq^2 at 2p + 1
     int ord[4][12];
 };
-// position m of step R's circle (jrr_pos(12, R, m)) for a position known only at run time
-template <int R>
-__device__ __forceinline__ int jrr_pos_r(int m) {
-    int v = m - 1 + R;  // 0 .. 20 for m >= 1
-    v = v >= 11 ? v - 11 : v;
-    return m == 0 ? 0 : 1 + v;
-}
 // Step R of the block form, branch-free: lanes 36..63 repeat lanes 0..27's blocks (the same values
 // to the same addresses), every lane forms its row pair's rotation and only the diagonal lanes'
 // land in LC (the others in a spare slot), so the wave runs one instruction stream.
@@ -3046,6 +3247,9 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
     return hipGetLastError();
 }
 
+#ifndef RSAC_EPNP_J6
+#define RSAC_EPNP_J6 1  // A/B knob: long rounds' Jacobi by rotation pairs (k_epnp5_jacobi6) or by rows
+#endif
 #ifndef RSAC_EPNP_WAVE_MAX
 #define RSAC_EPNP_WAVE_MAX 2048
 #endif
@@ -3063,6 +3267,8 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
         hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
         if (short_round)
             hipLaunchKernelGGL(k_epnp5_jacobi_b, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+        else if (RSAC_EPNP_J6)
+            hipLaunchKernelGGL(k_epnp5_jacobi6, dim3(cdiv(H, kJ6B), P), dim3(256), 0, s, ka, hyp_begin, H);
         else
             hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv(H, kEpGB), P), dim3(256), 0, s, ka, hyp_begin, H);
         const int hpw = short_round ? 16 : 21;  // hypotheses per wave of stage 3 (3 lanes each)
