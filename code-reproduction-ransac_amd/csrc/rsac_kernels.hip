@@ -1196,16 +1196,10 @@ __device__ __forceinline__ void epnp_j6_step(int sweep, int i, double (&a0)[12],
     // rows of the lane's own pair: row p <- cs p - sn q, row q <- sn p + cs q (as the 12-lane form:
     // cs a + x o with x = -sn on row p, +sn on row q: the same bits)
     const double x0 = f ? -sn : sn, x1 = f ? sn : -sn;
-    double n0[12], n1[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
-        n0[k] = cs * a0[k] + x0 * a1[k];
-        n1[k] = cs * a1[k] + x1 * a0[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        LM[kEpR * i0 + k] = n0[k];
-        LM[kEpR * i1 + k] = n1[k];
+        LM[kEpR * i0 + k] = cs * a0[k] + x0 * a1[k];
+        LM[kEpR * i1 + k] = cs * a1[k] + x1 * a0[k];
     }
     ep_wave_sync();
     // the next step's rows (step R + 1; after step 10 the next sweep's step 0)
