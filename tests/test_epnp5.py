@@ -141,6 +141,24 @@ def test_gpu_epnp5_batched_matches_per_problem_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sampler", ["opencv", "philox"])
+def test_gpu_epnp5_batched_long_rounds(sampler):
+    """A batch whose later rounds exceed 2048 hypotheses in all (confidence 1: every round runs to
+    the budget; 3 problems x 1024 in round 3), so the long-round Jacobi (k_epnp5_jacobi6, a grid row
+    per problem) runs beside the latency form: every problem against the oracle's own loop."""
+    probs = [synth.pnp_problem(nn, 0.5, seed=170 + i) for i, nn in enumerate([300, 900, 2000])]
+    out = rsac.pnp_ransac_batched([p["points2d"] for p in probs], [p["points3d"] for p in probs],
+                                  [p["K"] for p in probs], 2000, 30.0, confidence=1.0, sampler=sampler,
+                                  refine=False, minimal="epnp5")
+    for p, (R, t, m, ni) in zip(probs, out):
+        ref = O.pnp_ransac(p["points3d"], p["points2d"], p["K"], 30.0, 1.0, 2000, 0x5EED, sampler=sampler,
+                           minimal="epnp5")
+        assert ni == ref["n_inliers"]
+        np.testing.assert_array_equal(m, ref["mask"])
+        assert _bits_equal(R, ref["R"]) and _bits_equal(t, ref["t"])
+
+
+@pytest.mark.gpu
 def test_gpu_cv2_default_flags_use_epnp5():
     """cv2compat.solvePnPRansac(flags=SOLVEPNP_ITERATIVE): MWC 5-point samples, EPnP kernel, the
     RANSAC-phase inliers of the oracle's run, LM from the winner on them."""
