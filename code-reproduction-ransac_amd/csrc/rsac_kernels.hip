@@ -1150,29 +1150,48 @@ __device__ __forceinline__ int jrr_pos_r(int m) {
 // The throughput form by rotation pairs (r05): 6 lanes per hypothesis, 10 per wave (lanes 60..63
 // idle).  Lane i owns pair i of every step, i.e. the rows at positions i and 11 - i of the circle
 // (jrr_pos: at step r the indices pos(r, i), pos(r, 11 - i)), and rows 2i, 2i + 1 of V.  A step:
-//   params:  the pair's app, aqq, apq from the LDS mirror of the step-start matrix (row-indexed);
+//   params:  the pair's app, aqq, apq, read where the lane's two rows were stored;
 //   post:    cs, sn to the group's 12 slots; every lane reads all 12;
 //   columns: the 6 pairs' column rotations on the lane's two A rows and two V rows (static indices);
 //   rows:    the row rotation of its own pair (both rows in the lane: no exchange);
-//   mirror:  the two rows back to the mirror at their indices, then the next step's two rows read.
+//   pass:    the two rows to the wave's lane-linear exchange buffer X[t][k][lane] (one wave-wide
+//            write per element, no bank conflicts), then the next step's two rows from the lanes
+//            that hold them: the circle moves position m + 1 to m, so lane i takes slot 0 from lane
+//            i + 1's slot 0 and slot 1 from lane i - 1's slot 1 (lane 0 keeps index 0 and takes
+//            lane 1's slot 0; lane 5 takes its own slot 1 and lane 4's slot 1), whatever the step.
 // Each element sees jacobi_eig_rr's operations in its order (the same bits as k_epnp5_jacobi and the
 // oracle's ep_jacobi_rr).  Per hypothesis and step 6 lanes move 2 rows each through LDS where the
-// 12-lane form moves 12 rows twice; the VALU work is the same.
+// 12-lane form moves 12 rows twice; the VALU work is the same.  (A row-indexed mirror, r05's first
+// form, spent a third of its LDS time in bank conflicts: profiles/r05/probes.md.)
 constexpr int kJ6W = 10;              // hypotheses per wave
 constexpr int kJ6B = 256 / 64 * kJ6W;  // per 256-thread block
+constexpr int kJ6X = 12 * 64 + 1;      // doubles per slot array of a wave's X (+1: slot 1 one bank over)
 struct EpnpJ6Lds {
-    double M[kJ6B][12 * kEpR];  // the step-start matrix (row-indexed); at the end V's rows
-    double cs[kJ6B][24];        // pair i: cs at 2i, sn at 2i + 1; the sweep test's row terms at the sweep's start
+    double X[4][2 * kJ6X];  // per wave: X[t][k][lane] at t * kJ6X + 64 k + lane
+    double cs[kJ6B][24];    // pair i: cs at 2i, sn at 2i + 1; the sweep test's row terms at the sweep's start
     int ord[kJ6B][12];
 };
+// where slot t's row of lane i (of group base g6 = 6 gw) goes at the next step: (source lane, slot)
+__device__ __forceinline__ void j6_sources(int i, int g6, int &l0, int &t0, int &l1, int &t1) {
+    l0 = i == 0 ? g6 : i == 5 ? g6 + 5 : g6 + i + 1;
+    t0 = i == 5 ? 1 : 0;
+    l1 = i == 0 ? g6 + 1 : g6 + i - 1;
+    t1 = i == 0 ? 0 : 1;
+}
+// (s_l0, s_t0), (s_l1, s_t1): where the lane's two rows are stored at the step's start (the circle's
+// pattern, or the lane's own slots before the first exchange); (l0, t0), (l1, t1): the pattern
 template <int R>
-__device__ __forceinline__ void epnp_j6_step(int sweep, int i, double (&a0)[12], double (&a1)[12], double (&v0)[12],
-                                             double (&v1)[12], double *LM, double *LC) {
+__device__ __forceinline__ void epnp_j6_step(int sweep, int i, int lane, int s_l0, int s_t0, int s_l1, int s_t1,
+                                             int l0, int t0, int l1, int t1, double (&a0)[12], double (&a1)[12],
+                                             double (&v0)[12], double (&v1)[12], double *X, double *LC) {
     const int i0 = jrr_pos_r<R>(i), i1 = jrr_pos_r<R>(11 - i);
     const bool f = i0 < i1;  // slot 0 holds row p
     const int p = f ? i0 : i1, q = f ? i1 : i0;
+    // the step-start values app, aqq, apq where the lane's rows are stored
+    const int lp = f ? s_l0 : s_l1, tp = f ? s_t0 : s_t1, lq = f ? s_l1 : s_l0, tq = f ? s_t1 : s_t0;
     double cs = 1.0, sn = 0.0;  // a skipped pair: the identity rotation (jacobi_eig_rr)
-    (void)jrr_rotation(sweep, LM[(kEpR + 1) * p], LM[(kEpR + 1) * q], LM[kEpR * p + q], cs, sn);
+    (void)jrr_rotation(sweep, X[tp * kJ6X + 64 * p + lp], X[tq * kJ6X + 64 * q + lq], X[tp * kJ6X + 64 * q + lp],
+                       cs, sn);
     LC[2 * i] = cs;
     LC[2 * i + 1] = sn;
     ep_wave_sync();
@@ -1194,21 +1213,18 @@ __device__ __forceinline__ void epnp_j6_step(int sweep, int i, double (&a0)[12],
         x = v1[P]; y = v1[Q]; v1[P] = c * x - s * y; v1[Q] = s * x + c * y;
     }
     // rows of the lane's own pair: row p <- cs p - sn q, row q <- sn p + cs q (as the 12-lane form:
-    // cs a + x o with x = -sn on row p, +sn on row q: the same bits)
+    // cs a + x o with x = -sn on row p, +sn on row q: the same bits), straight to the exchange buffer
     const double x0 = f ? -sn : sn, x1 = f ? sn : -sn;
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
-        LM[kEpR * i0 + k] = cs * a0[k] + x0 * a1[k];
-        LM[kEpR * i1 + k] = cs * a1[k] + x1 * a0[k];
+        X[64 * k + lane] = cs * a0[k] + x0 * a1[k];
+        X[kJ6X + 64 * k + lane] = cs * a1[k] + x1 * a0[k];
     }
     ep_wave_sync();
-    // the next step's rows (step R + 1; after step 10 the next sweep's step 0)
-    constexpr int Rn = R + 1 < 11 ? R + 1 : 0;
-    const int j0 = jrr_pos_r<Rn>(i), j1 = jrr_pos_r<Rn>(11 - i);
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
-        a0[k] = LM[kEpR * j0 + k];
-        a1[k] = LM[kEpR * j1 + k];
+        a0[k] = X[t0 * kJ6X + 64 * k + l0];
+        a1[k] = X[t1 * kJ6X + 64 * k + l1];
     }
     // V's rotations complete inside the step (left free, the scheduler sinks them and holds every
     // step's cs, sn live)
@@ -1219,11 +1235,12 @@ __device__ __forceinline__ void epnp_j6_step(int sweep, int i, double (&a0)[12],
     }
 }
 template <int R>
-__device__ __forceinline__ void epnp_j6_sweep(int sweep, int i, double (&a0)[12], double (&a1)[12], double (&v0)[12],
-                                              double (&v1)[12], double *LM, double *LC) {
+__device__ __forceinline__ void epnp_j6_sweep(int sweep, int i, int lane, int l0, int t0, int l1, int t1,
+                                              double (&a0)[12], double (&a1)[12], double (&v0)[12],
+                                              double (&v1)[12], double *X, double *LC) {
     if constexpr (R < 11) {
-        epnp_j6_step<R>(sweep, i, a0, a1, v0, v1, LM, LC);
-        epnp_j6_sweep<R + 1>(sweep, i, a0, a1, v0, v1, LM, LC);
+        epnp_j6_step<R>(sweep, i, lane, l0, t0, l1, t1, l0, t0, l1, t1, a0, a1, v0, v1, X, LC);
+        epnp_j6_sweep<R + 1>(sweep, i, lane, l0, t0, l1, t1, a0, a1, v0, v1, X, LC);
     }
 }
 // a row's sweep-test terms (jacobi_eig_rr's): A_rr^2 and sum_{q > r} A_rq^2 in q order
@@ -1250,7 +1267,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
     const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
     const bool live = slot && hl < H && a.status[rec] > 0 && s1->ok != 0.0;
     bool run = live;
-    double *LM = L.M[hb], *LC = L.cs[hb];
+    double *X = L.X[threadIdx.x >> 6], *LC = L.cs[hb];
+    int l0, t0, l1, t1;  // where the next step's rows come from (the circle's fixed pattern)
+    j6_sources(i, 6 * gw, l0, t0, l1, t1);
     double a0[12], a1[12], v0[12], v1[12];
     // rows 2i, 2i + 1 of V = I; rows pos(0, i), pos(0, 11 - i) of epnp_mtm's matrix
     const int r0 = jrr_pos_r<0>(i), r1 = jrr_pos_r<0>(11 - i);
@@ -1279,11 +1298,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
         };
         build(r0, a0);
         build(r1, a1);
+    }
+    // the first step's parameters are read where the rows are: the lane's own slots at first (the
+    // step's pattern takes over after the first exchange)
+    int s_l0 = lane, s_t0 = 0, s_l1 = lane, s_t1 = 1;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            LM[kEpR * r0 + k] = a0[k];
-            LM[kEpR * r1 + k] = a1[k];
-        }
+    for (int k = 0; k < 12; ++k) {
+        X[64 * k + lane] = a0[k];
+        X[kJ6X + 64 * k + lane] = a1[k];
     }
     ep_wave_sync();
     for (int sweep = 0; sweep < 60; ++sweep) {
@@ -1310,18 +1332,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
         }
         if (__ballot(run) == 0) break;
         ep_wave_sync();  // every lane has read the test's terms before the first step posts
-        if (run) epnp_j6_sweep<0>(sweep, i, a0, a1, v0, v1, LM, LC);
+        if (run) {
+            // step 0 reads its parameters at (s_l, s_t); the sweep's later steps at the pattern
+            epnp_j6_step<0>(sweep, i, lane, s_l0, s_t0, s_l1, s_t1, l0, t0, l1, t1, a0, a1, v0, v1, X, LC);
+            epnp_j6_sweep<1>(sweep, i, lane, l0, t0, l1, t1, a0, a1, v0, v1, X, LC);
+        }
+        s_l0 = l0; s_t0 = t0; s_l1 = l1; s_t1 = t1;
     }
     if (!live) return;
-    // eig_order_desc<12> on the diagonal (the mirror holds the final matrix), then V's rows
+    // eig_order_desc<12> on the diagonal (each lane posts its two rows' diagonal entries), then V's rows
+    {
+        double d0, p0, d1, p1;
+        j6_row_terms(a0, r0, d0, p0);
+        j6_row_terms(a1, r1, d1, p1);
+        (void)p0;
+        (void)p1;
+        double dg0 = 0.0, dg1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            dg0 = k == r0 ? a0[k] : dg0;
+            dg1 = k == r1 ? a1[k] : dg1;
+        }
+        LC[r0] = dg0;
+        LC[r1] = dg1;
+    }
+    ep_wave_sync();
     int *O = L.ord[hb];
     if (i == 0) {
         for (int k = 0; k < 12; ++k) O[k] = k;
         for (int k = 1; k < 12; ++k) {
             const int kk = O[k];
-            const double dk = LM[(kEpR + 1) * kk];
+            const double dk = LC[kk];
             int jx = k - 1;
-            while (jx >= 0 && LM[(kEpR + 1) * O[jx]] < dk) {
+            while (jx >= 0 && LC[O[jx]] < dk) {
                 O[jx + 1] = O[jx];
                 --jx;
             }
@@ -1329,16 +1372,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
         }
     }
     ep_wave_sync();
+    // V's rows through the wave's exchange buffer: row r of the group at X + 12 * 12 * gw + 12 r
+    double *VX = X + 144 * gw;
 #pragma unroll
-    for (int c = 0; c < 12; ++c) {  // lane 0's sort has read the diagonal
-        LM[kEpR * (2 * i) + c] = v0[c];
-        LM[kEpR * (2 * i + 1) + c] = v1[c];
+    for (int c = 0; c < 12; ++c) {
+        VX[12 * (2 * i) + c] = v0[c];
+        VX[12 * (2 * i + 1) + c] = v1[c];
     }
     ep_wave_sync();
 #pragma unroll
     for (int t = 0; t < 8; ++t) {  // ut[ii][j] = V[j][o[11 - ii]], element 8 i + t of 48
         const int e = 8 * i + t, ii = e / 12, j = e - 12 * ii;
-        E[64 + e] = LM[kEpR * j + O[11 - ii]];
+        E[64 + e] = VX[12 * j + O[11 - ii]];
     }
 }
 
