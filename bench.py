@@ -506,15 +506,18 @@ def extra_workloads(local, args):
     _, _, mr, infr = rsac.pnp_ransac(g2, g3, p2c["K"], 5000, args.thr, sampler="opencv", minimal="epnp5",
                                      refine=True, return_info=True, device=local)
     walls_f, sol_f = [], []
-    for i in range(5):
+    for i in range(13):  # the plain call timed (3 warm-up calls), the solve's HIP-event time from a stats call
         torch.cuda.synchronize()
         t = time.perf_counter()
+        rsac.pnp_ransac(g2, g3, p2c["K"], 20_000, args.thr, minimal="epnp5", adaptive=False, refine=False,
+                        device=local)
+        torch.cuda.synchronize()
+        if i >= 3:
+            walls_f.append(time.perf_counter() - t)
+    for i in range(3):
         _, _, _, inff = rsac.pnp_ransac(g2, g3, p2c["K"], 20_000, args.thr, minimal="epnp5", adaptive=False,
                                         refine=False, return_info=True, device=local)
-        torch.cuda.synchronize()
-        if i >= 1:
-            walls_f.append(time.perf_counter() - t)
-            sol_f.append(inff.solve_ms)
+        sol_f.append(inff.solve_ms)
     # the cost of OpenCV's Rodrigues round trip (RSAC_F_RVEC_ROUNDTRIP, on in the reference mode):
     # the same 20k EPnP-5 solve with and without it, HIP events around the solve launches
     rt_ms = {}
