@@ -865,10 +865,9 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 // sample; OpenCV solvepnp.cpp PnPRansacCallback::runKernel) in three launches: k_epnp5_a (sample,
 // stage 1: centroid, principal axes, control-point pair sums; one lane per hypothesis), the 12 x 12
 // eigen-decomposition of M^T M (~88 % of the arithmetic) by the round-robin Jacobi of
-// jacobi_eig_rr<12> on 16 lanes per hypothesis (k_epnp5_jacobi; rows of A and V per lane, the
-// step-start matrix mirrored in LDS for the pair parameters and the row exchange) or one wave per
-// hypothesis in 2 x 2 blocks for short rounds (k_epnp5_jacobi_b), then k_epnp5_c (L, rho, the three beta estimates
-// and their poses, 4 lanes per hypothesis).  Every element sees jacobi_eig_rr's operations in its
+// jacobi_eig_rr<12> on 6 lanes per hypothesis (k_epnp5_jacobi6; each lane owns one rotation pair's
+// two rows) or one wave per hypothesis in 2 x 2 blocks for short rounds (k_epnp5_jacobi_b), then
+// k_epnp5_c (L, rho, the three beta estimates and their poses, 3 lanes per hypothesis).  Every element sees jacobi_eig_rr's operations in its
 // order (the rotation formula and skip rule of jrr_rotation), so the records are bit-identical to
 // rsac_math.h pnp_epnp_minimal<5> and the oracle's orc_pnp_minimal_epnp5 (ep_jacobi_rr).  (The
 // round-robin order replaced round 3's cyclic jacobi_eig<12>: EPnP's numerics changed with it, in
@@ -943,35 +942,14 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
     *reinterpret_cast<EpnpStage1 *>(a.epnp + ((int64_t)prob * H + hl) * kEpnpRec) = s1;
 }
 
-// 2 of 3: M^T M's eigenvectors by the round-robin Jacobi of jacobi_eig_rr<12>, 12 lanes per
-// hypothesis (5 per wave, lanes 60..63 idle; r05, 4 of 16 lanes were idle).  Lane j builds row j of
-// A (epnp_mtm's entries) and holds rows j of A and V in registers; the group's A is mirrored row by
-// row in LDS (the step-start matrix
-// after every step), where each lane reads its pair's A[p][p], A[q][q], A[p][q] and, after the
-// column phase, its partner's row.  A step (static r, every pair's indices compile-time constants):
-//   params:  both lanes of pair (p, q) form its cs, sn from the step-start matrix (the same
-//            operations, so the same bits); lane p posts them (a skipped pair: cs 1, sn 0);
-//   columns: every lane rotates its elements (p_i, q_i) of A and of V for the 6 pairs;
-//   rows:    lanes p and q exchange their column-rotated rows through LDS and form
-//            cs a + x o (x = -sn on lane p, +sn on lane q: jacobi_eig_rr's cs a - sn o and
-//            sn o + cs a, the same bits).
-// A sweep is 11 steps instead of 66 dependent rotations; for the sweep test lane j forms its row's
-// terms from its registers (A_jj^2 and the partial sum_{q > j} A_jq^2 in q order, jacobi_eig_rr's)
-// and every lane adds the group's 12 in row order (r05: each lane had read the whole upper
-// triangle from LDS).  Groups whose sweeps end early idle until the wave's last group is done.
-constexpr int kEpG = 12;                // lanes per hypothesis
-constexpr int kEpGW = 5;                // hypotheses per wave
-constexpr int kEpGB = 256 / 64 * kEpGW;  // hypotheses per 256-thread block
-// LDS row stride of the mirrored matrices (doubles): 13, not 12, so the 12 rows of one column (and
-// the 4 groups of a wave, the A and V rows of the latency form) fall in distinct banks: 2-way at
-// most where 12 gave 6- to 8-way (SQ_LDS_BANK_CONFLICT, profiles/r04_epnp_pmc.json)
+// 2 of 3: M^T M's eigenvectors by the round-robin Jacobi of jacobi_eig_rr<12>: k_epnp5_jacobi6 for
+// long rounds (6 lanes per hypothesis, below) and k_epnp5_jacobi_b for short ones (one wave per
+// hypothesis in 2 x 2 blocks).  (r05's 12-lane row form, lane j holding rows j of A and V and the
+// step-start matrix mirrored in LDS, was replaced by the pair-owned form: profiles/r05/probes.md.)
+// LDS row stride of the mirrored matrices (doubles): 13, not 12, so the 12 rows of one column (the
+// A and V rows of the latency form) fall in distinct banks: 2-way at most where 12 gave 6- to 8-way
+// (SQ_LDS_BANK_CONFLICT, profiles/r04_epnp_pmc.json)
 constexpr int kEpR = 13;
-struct EpnpJacLds {
-    double A[kEpGB][12 * kEpR];
-    double cs[kEpGB][12];    // pair i: cs at 2i, sn at 2i + 1
-    double part[kEpGB][24];  // the sweep test's row terms: A_pp^2 at 2p, sum_{q > p} A_pq^2 at 2p + 1
-    int ord[kEpGB][12];      // eig_order_desc's order of the eigenvalues
-};
 RSAC_HD constexpr int jrr_p(int r, int i) {
     return jrr_pos(12, r, i) < jrr_pos(12, r, 11 - i) ? jrr_pos(12, r, i) : jrr_pos(12, r, 11 - i);
 }
@@ -982,162 +960,6 @@ __device__ __forceinline__ void ep_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-template <int R>
-__device__ __forceinline__ void epnp_rr_step(int sweep, int j, double (&A)[12], double (&V)[12], double *LA,
-                                             double *LC) {
-    // the lane's step constants (partner, pair, addresses) formed here, not hoisted out of the
-    // sweep loop, where 11 steps' worth of them held in registers spill
-    asm volatile("" : "+v"(j));
-    // this lane's position, its partner, its pair
-    const int m = j == 0 ? 0 : (j - 1 - R + 11) % 11 + 1;
-    const int mo = 11 - m;
-    const int o = mo == 0 ? 0 : 1 + (mo - 1 + R) % 11;
-    const int pi = m < mo ? m : mo;
-    const int p = j < o ? j : o, q = j < o ? o : j;
-    const double app = LA[(kEpR + 1) * p], aqq = LA[(kEpR + 1) * q], apq = LA[kEpR * p + q];
-    double cs = 1.0, sn = 0.0;  // a skipped pair: the identity rotation (jacobi_eig_rr)
-    (void)jrr_rotation(sweep, app, aqq, apq, cs, sn);
-    if (j == p) {
-        LC[2 * pi] = cs;
-        LC[2 * pi + 1] = sn;
-    }
-    ep_wave_sync();
-    // columns of A and V (every pair; static indices): the 6 rotations in one LDS round trip
-    double c6[6], s6[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        c6[i] = LC[2 * i];
-        s6[i] = LC[2 * i + 1];
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const int P = jrr_p(R, i), Q = jrr_q(R, i);
-        const double c = c6[i], s = s6[i];
-        const double akp = A[P], akq = A[Q];
-        A[P] = c * akp - s * akq;
-        A[Q] = s * akp + c * akq;
-        const double vkp = V[P], vkq = V[Q];
-        V[P] = c * vkp - s * vkq;
-        V[Q] = s * vkp + c * vkq;
-    }
-    // V's rotations complete inside the step: left free, the scheduler sinks them to the sweep's
-    // end and holds every step's cs, sn live (24 VGPRs a step, spilled)
-#pragma unroll
-    for (int k = 0; k < 12; ++k) asm volatile("" : "+v"(V[k]));
-    // rows: the partner's column-rotated row through LDS
-#pragma unroll
-    for (int k = 0; k < 12; ++k) LA[kEpR * j + k] = A[k];
-    ep_wave_sync();
-    double O[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) O[k] = LA[kEpR * o + k];
-    ep_wave_sync();
-    const double x = j == p ? -sn : sn;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) A[k] = cs * A[k] + x * O[k];
-    // the step-start matrix of the next step
-#pragma unroll
-    for (int k = 0; k < 12; ++k) LA[kEpR * j + k] = A[k];
-    ep_wave_sync();
-}
-template <int R>
-__device__ __forceinline__ void epnp_rr_sweep(int sweep, int j, double (&A)[12], double (&V)[12], double *LA,
-                                              double *LC) {
-    if constexpr (R < 11) {
-        epnp_rr_step<R>(sweep, j, A, V, LA, LC);
-        epnp_rr_sweep<R + 1>(sweep, j, A, V, LA, LC);
-    }
-}
-
-#ifndef RSAC_EPNP_WAVES
-#define RSAC_EPNP_WAVES 2  // A/B knob: waves per SIMD asked of k_epnp5_jacobi (4: 128 VGPRs, 16 spilled)
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSAC_EPNP_WAVES, 8))) void k_epnp5_jacobi(
-    PnpArgs a, int64_t hyp_begin, int32_t H) {
-    __shared__ EpnpJacLds L;
-    const int prob = blockIdx.y;
-    const int lane = threadIdx.x & 63, gw = lane / kEpG, j = lane - kEpG * gw;
-    const bool row = gw < kEpGW;  // lanes 60..63: no group
-    const int hb = (int)(threadIdx.x >> 6) * kEpGW + (row ? gw : 0);
-    const int hl = (int)blockIdx.x * kEpGB + hb;
-    const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
-    double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;  // launch-local scratch
-    const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
-    const bool live = row && hl < H && a.status[rec] > 0 && s1->ok != 0.0;
-    bool run = live;
-    double *LA = L.A[hb], *LC = L.cs[hb], *LP = L.part[hb];
-    double A[12], V[12];
-#pragma unroll
-    for (int c = 0; c < 12; ++c) {
-        A[c] = 0.0;
-        V[c] = c == j ? 1.0 : 0.0;
-    }
-    if (run && row) {  // row j = 3i + p of epnp_mtm's matrix
-        const double *cm = a.cams + 4 * prob;
-        const double fx = cm[0], fy = cm[1];
-        const int i = j / 3, p = j - 3 * i;
-        constexpr int first[4] = {0, 4, 7, 9};  // pair (x <= y) -> sum block x's first + (y - x)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int lo = min(i, jj), hi = max(i, jj);
-            const double *ps = s1->pairs + 4 * (first[lo] + hi - lo);
-            const double s0 = ps[0], su = ps[1], sv = ps[2], sw = ps[3];
-            const double blk[9] = {fx * fx * s0, 0.0, fx * su, 0.0, fy * fy * s0, fy * sv, fx * su, fy * sv, sw};
-#pragma unroll
-            for (int rr = 0; rr < 3; ++rr) A[3 * jj + rr] = p == 0 ? blk[rr] : p == 1 ? blk[3 + rr] : blk[6 + rr];
-        }
-#pragma unroll
-        for (int k = 0; k < 12; ++k) LA[kEpR * j + k] = A[k];
-    }
-    ep_wave_sync();
-    for (int sweep = 0; sweep < 60; ++sweep) {
-        if (run) {  // row j's terms from the registers (they hold the mirror's row j)
-            double dp = 0.0, rp = 0.0;
-#pragma unroll
-            for (int q = 0; q < 12; ++q) {
-                dp = q == j ? A[q] : dp;
-                rp = q > j ? rp + A[q] * A[q] : rp;
-            }
-            LP[2 * j] = dp * dp;
-            LP[2 * j + 1] = rp;
-        }
-        ep_wave_sync();
-        if (run) {
-            double off = 0.0, diag = 0.0;
-#pragma unroll
-            for (int p = 0; p < 12; ++p) {
-                diag = diag + LP[2 * p];
-                off = off + LP[2 * p + 1];
-            }
-            if (!(off > 1e-32 * diag)) run = false;
-        }
-        if (__ballot(run) == 0) break;
-        if (run && row) epnp_rr_sweep<0>(sweep, j, A, V, LA, LC);
-    }
-    if (!live || !row) return;
-    // eig_order_desc<12> on the diagonal, by lane 0 of the group with its arrays in LDS (in
-    // registers its dynamic indices become select chains), then V's row through LDS
-    int *O = L.ord[hb];
-    if (j == 0) {
-        for (int i = 0; i < 12; ++i) O[i] = i;
-        for (int i = 1; i < 12; ++i) {
-            const int k = O[i];
-            const double dk = LA[(kEpR + 1) * k];
-            int jx = i - 1;
-            while (jx >= 0 && LA[(kEpR + 1) * O[jx]] < dk) {
-                O[jx + 1] = O[jx];
-                --jx;
-            }
-            O[jx + 1] = k;
-        }
-    }
-    ep_wave_sync();
-#pragma unroll
-    for (int c = 0; c < 12; ++c) LA[kEpR * j + c] = V[c];  // lane 0's sort has read the diagonal
-    ep_wave_sync();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) E[64 + 12 * i + j] = LA[kEpR * j + O[11 - i]];  // ut[i][j] = V[j][o[11 - i]]
 }
 
 // position m of step R's circle (jrr_pos(12, R, m)) for a position known only at run time
@@ -1159,8 +981,8 @@ __device__ __forceinline__ int jrr_pos_r(int m) {
 //            that hold them: the circle moves position m + 1 to m, so lane i takes slot 0 from lane
 //            i + 1's slot 0 and slot 1 from lane i - 1's slot 1 (lane 0 keeps index 0 and takes
 //            lane 1's slot 0; lane 5 takes its own slot 1 and lane 4's slot 1), whatever the step.
-// Each element sees jacobi_eig_rr's operations in its order (the same bits as k_epnp5_jacobi and the
-// oracle's ep_jacobi_rr).  Per hypothesis and step 6 lanes move 2 rows each through LDS where the
+// Each element sees jacobi_eig_rr's operations in its order (the same bits as k_epnp5_jacobi_b and
+// the oracle's ep_jacobi_rr).  Per hypothesis and step 6 lanes move 2 rows each through LDS where the
 // 12-lane form moves 12 rows twice; the VALU work is the same.  (A row-indexed mirror, r05's first
 // form, spent a third of its LDS time in bank conflicts: profiles/r05/probes.md.)
 constexpr int kJ6W = 10;              // hypotheses per wave
@@ -1387,7 +1209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
     }
 }
 
-// The latency form of k_epnp5_jacobi for short rounds (an adaptive run's first 256 hypotheses):
+// The latency form of the Jacobi for short rounds (an adaptive run's first 256 hypotheses):
 // one wave per hypothesis in 2 x 2 blocks.  In step r the 12 indices form the 6 pairs of
 // jacobi_eig_rr; lane (a, b) < 36 holds A's block at rows pair a x columns pair b and V's block at
 // rows 2a, 2a + 1 x columns pair b.  A step: the diagonal lanes (a, a) form their pair's cs, sn from
@@ -1882,8 +1704,8 @@ __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, 
             }
             const uint64_t und = __ballot(!(tmin > m[13]));
             // v_writelane_b32 (no clang builtin); the lane select goes through M0 (two SGPR
-            // operands would exceed the constant bus); cc and h are SALU results: no hazard
-            asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
+            // operands would exceed the constant bus), which the compiler loads itself ("{m0}")
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(ccl) : "s"(cc), "{m0}"(h));
             wund |= und ? (1u << h) : 0u;
         }
         cnt += ccl;
@@ -3286,30 +3108,25 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
     return hipGetLastError();
 }
 
-#ifndef RSAC_EPNP_J6
-#define RSAC_EPNP_J6 1  // A/B knob: long rounds' Jacobi by rotation pairs (k_epnp5_jacobi6) or by rows
-#endif
 #ifndef RSAC_EPNP_WAVE_MAX
 #define RSAC_EPNP_WAVE_MAX 2048
 #endif
 constexpr int64_t kEpnpWaveMaxHyps = RSAC_EPNP_WAVE_MAX;  // one wave per hypothesis up to this many (2 waves/SIMD at 250 VGPRs: one round of waves; A/B knob)
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
-    if (a.sample_k == 5) {  // EPnP-5: the three-launch form (k_epnp5_a / _jacobi / _c)
+    if (a.sample_k == 5) {  // EPnP-5: the three-launch form (k_epnp5_a / _jacobi6 or _jacobi_b / _c)
         if (!a.epnp) return hipErrorInvalidValue;  // its scratch (ensure_epnp5) is required
         // short rounds (an adaptive run's first 256 hypotheses): their latency is one hypothesis', so
         // one wave per block in stages 1 and 3 (4 and 16 CUs for 256 hypotheses, 64 and 16 per wave;
-        // sparser waves were slower, r05 A/B) and one wave per hypothesis in 2 x 2 blocks for the Jacobi; longer
-        // rounds 16 lanes per Jacobi
+        // sparser waves were slower, r05 A/B) and one wave per hypothesis in 2 x 2 blocks for the
+        // Jacobi; longer rounds 6 lanes per hypothesis's Jacobi
         const bool short_round = (int64_t)P * H <= kEpnpWaveMaxHyps;
         const int tb = short_round ? 64 : 256;  // threads per block of stages 1 and 3
         hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
         if (short_round)
             hipLaunchKernelGGL(k_epnp5_jacobi_b, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-        else if (RSAC_EPNP_J6)
-            hipLaunchKernelGGL(k_epnp5_jacobi6, dim3(cdiv(H, kJ6B), P), dim3(256), 0, s, ka, hyp_begin, H);
         else
-            hipLaunchKernelGGL(k_epnp5_jacobi, dim3(cdiv(H, kEpGB), P), dim3(256), 0, s, ka, hyp_begin, H);
+            hipLaunchKernelGGL(k_epnp5_jacobi6, dim3(cdiv(H, kJ6B), P), dim3(256), 0, s, ka, hyp_begin, H);
         const int hpw = short_round ? 16 : 21;  // hypotheses per wave of stage 3 (3 lanes each)
         hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(cdiv(H, hpw), tb / 64), P), dim3(tb), 0, s, ka, hyp_begin, H, hpw);
     }
@@ -4905,7 +4722,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                     und |= ~(mi | mo);
                 }
                 // v_writelane_b32 (no clang builtin); lane select through M0; SALU operands
-                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(ccl) : "s"(cc), "s"(h) : "m0");
+                asm("v_writelane_b32 %0, %1, %2" : "+v"(ccl) : "s"(cc), "{m0}"(h));
                 wund |= und ? (1u << h) : 0u;
             }
             cnt += ccl;

@@ -1194,7 +1194,7 @@ constexpr int kEpnpPairSums = 40;  // 10 control-point pairs x 4 sums
 // d / w), so cs = 1 / sqrt(t^2 + 1) = h / sqrt(h^2 + w^2) and sn = t cs = sg |w| / sqrt(h^2 + w^2):
 // two square roots and one division in the chain (r05; one division fewer than forming t first).
 // MᵀM's entries are far from the squares' overflow.
-RSAC_HD inline bool jrr_rotation(int sweep, double app, double aqq, double apq, double &cs, double &sn) {
+RSAC_HD bool jrr_rotation(int sweep, double app, double aqq, double apq, double &cs, double &sn) {
     if (!(apq != 0.0)) return false;
     if (sweep >= 4) {
         const double g = 100.0 * dabs(apq);
@@ -1262,7 +1262,7 @@ RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
 // matrix at the step's start; then the columns of every pair (every row), the rows of every pair,
 // and V's columns.  Pairs are disjoint, so each element sees one fixed sequence of operations
 // whatever the order within a phase: the GPU runs a step's pairs on different lanes
-// (k_epnp5_jacobi) with the bits of this loop.  Schedule (circle method): in step r, position 0
+// (k_epnp5_jacobi6, k_epnp5_jacobi_b) with the bits of this loop.  Schedule (circle method): in step r, position 0
 // holds index 0 and position m > 0 holds 1 + (m - 1 + r) % (N - 1); pair i is positions i and
 // N - 1 - i, p the smaller index.  Sweep test as jacobi_eig; the rotation by jrr_rotation.
 RSAC_HD constexpr int jrr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
@@ -1687,8 +1687,8 @@ RSAC_HD void epnp_l_rho(const EpnpStage1 &s1, const EpnpStage2 &s2, double *L, d
 
 // Stage 2 after the eigen-decomposition: s2.ut (the eigenvectors of M^T M's 4 smallest
 // eigenvalues) given, the L 6x10 / rho system and the three beta estimates with Gauss-Newton.
-// (epnp_stage2 below; the GPU's minimal EPnP runs the 12 x 12 Jacobi on 16 or 64 lanes in between,
-// k_epnp5_jacobi, and the three estimates on three lanes, k_epnp5_c)
+// (epnp_stage2 below; the GPU's minimal EPnP runs the 12 x 12 Jacobi on 6 or 64 lanes in between,
+// k_epnp5_jacobi6 / _b, and the three estimates on three lanes, k_epnp5_c)
 __host__ __device__ inline void epnp_stage2_post(const EpnpStage1 &s1, EpnpStage2 &s2) {
     double L[60], rho[6];
     epnp_l_rho(s1, s2, L, rho);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # EPnP-5 path PMC passes (its own runs, no other tracing domain): VALU issue side and LDS of the
-# three-launch solve (k_epnp5_a / k_epnp5_jacobi(_w) / k_epnp5_c) under scripts/epnp5_prof.py
+# three-launch solve (k_epnp5_a / k_epnp5_jacobi6 or _jacobi_b / k_epnp5_c) under scripts/epnp5_prof.py
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 P=gpurun_out/epmc

@@ -8,7 +8,7 @@ rsac.cv2compat.solvePnPRansac.
 Oracle: orc_pnp_minimal_epnp5 (oracle/rsac_oracle.c) = orc_pnp_epnp on the 5 sampled points in
 sample order, the same restatement the final-solve EPnP tests pin (tests/test_epnp.py; "parity
 unpinned" against OpenCV itself, which is not installed).  Bar: bit-identical models, counts,
-winner, mask and iteration count between the GPU solve (k_epnp5_a / k_epnp5_jacobi(_w) / k_epnp5_c)
+winner, mask and iteration count between the GPU solve (k_epnp5_a / k_epnp5_jacobi6 or _b / k_epnp5_c)
 and the oracle.
 """
 import numpy as np
@@ -87,7 +87,7 @@ def test_oracle_ransac_epnp5_finds_the_inliers():
 def test_gpu_epnp5_hypotheses_bit_exact(n, outl, seed, H):
     """Every hypothesis (Philox 5-subsets, then explicit MWC 5-subsets): status, count, model.
     Rounds of H <= 2048 run the round-robin Jacobi of the three-launch solve one wave per
-    hypothesis (k_epnp5_jacobi_w), larger rounds 16 lanes per hypothesis (k_epnp5_jacobi): both
+    hypothesis (k_epnp5_jacobi_b), larger rounds 6 lanes per hypothesis (k_epnp5_jacobi6): both
     forms, and the boundary between them, against the oracle's ep_jacobi_rr."""
     pr = synth.pnp_problem(n, outl, seed=seed)
     soa, cam = O.soa_pnp(pr["points3d"], pr["points2d"]), O.cam_from_K(pr["K"])
