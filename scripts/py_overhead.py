@@ -8,6 +8,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "code-reproduction-ransac_amd"))
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import rsac  # noqa: E402
@@ -40,3 +41,25 @@ for _ in range(N):
     torch.cuda.synchronize()
 pr_.disable()
 pstats.Stats(pr_).sort_stats("tottime").print_stats(14)
+
+# the wrapper's torch calls one by one (us per call)
+def per_call(f, n=20000):
+    for _ in range(200):
+        f()
+    t = time.perf_counter()
+    for _ in range(n):
+        f()
+    return (time.perf_counter() - t) / n * 1e6
+
+
+dev = p3.device
+print("torch.empty u8        %.2f us" % per_call(lambda: torch.empty(10000, dtype=torch.uint8, device=dev)))
+print("torch.empty bool      %.2f us" % per_call(lambda: torch.empty(10000, dtype=torch.bool, device=dev)))
+m8 = torch.empty(10000, dtype=torch.uint8, device=dev)
+print("view(bool)            %.2f us" % per_call(lambda: m8.view(dtype=torch.bool)))
+print("current_stream        %.2f us" % per_call(lambda: torch.cuda.current_stream(dev).cuda_stream))
+print("raw current stream    %.2f us" % per_call(lambda: torch._C._cuda_getCurrentRawStream(0)))
+print("data_ptr              %.2f us" % per_call(lambda: p3.data_ptr()))
+print("_In                   %.2f us" % per_call(lambda: rsac.api._In(p3, 3)))
+print("_K9                   %.2f us" % per_call(lambda: rsac.api._K9(pr["K"])))
+print("np.zeros(9)           %.2f us" % per_call(lambda: np.zeros(9)))
