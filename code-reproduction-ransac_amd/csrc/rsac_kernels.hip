@@ -987,7 +987,12 @@ __device__ __forceinline__ int jrr_pos_r(int m) {
 // form, spent a third of its LDS time in bank conflicts: profiles/r05/probes.md.)
 constexpr int kJ6W = 10;              // hypotheses per wave
 constexpr int kJ6B = 256 / 64 * kJ6W;  // per 256-thread block
-constexpr int kJ6X = 12 * 64 + 1;      // doubles per slot array of a wave's X (+1: slot 1 one bank over)
+// doubles per slot array of a wave's X.  +2: slot 1 sits two doubles over, where the reads that
+// take it land on the positions no slot-0 read of the same 16-lane bank group uses (lane 5 reads
+// its own slot 1 at 6g + 7, the next group's hole at 6g + 6 + 1; the second read's sources become
+// 6g + 1 .. 6g + 6, consecutive).  +1 made both reads 2-way conflicted (SQ_LDS_BANK_CONFLICT 24 M
+// cycles per 20k launch, r05).
+constexpr int kJ6X = 12 * 64 + 2;
 struct EpnpJ6Lds {
     double X[4][2 * kJ6X];  // per wave: X[t][k][lane] at t * kJ6X + 64 k + lane
     double cs[kJ6B][24];    // pair i: cs at 2i, sn at 2i + 1; the sweep test's row terms at the sweep's start
