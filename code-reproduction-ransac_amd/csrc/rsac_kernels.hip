@@ -995,7 +995,10 @@ constexpr int kJ6B = 256 / 64 * kJ6W;  // per 256-thread block
 constexpr int kJ6X = 12 * 64 + 2;
 struct EpnpJ6Lds {
     double X[4][2 * kJ6X];  // per wave: X[t][k][lane] at t * kJ6X + 64 k + lane
-    double cs[kJ6B][24];    // pair i: cs at 2i, sn at 2i + 1; the sweep test's row terms at the sweep's start
+    // pair i: cs at 2i, sn at 2i + 1; the sweep test's row terms at the sweep's start.  Rows of
+    // 25 doubles (odd): the wave's hypotheses read slot j at distinct banks (24 put every other
+    // hypothesis on the same bank)
+    double cs[kJ6B][25];
     int ord[kJ6B][12];
 };
 // where slot t's row of lane i (of group base g6 = 6 gw) goes at the next step: (source lane, slot)
