@@ -1031,7 +1031,7 @@ int direct_solve(rsac_ctx *c, Model model, const Staged &st, const void *args, c
     }
     HIPCHK(c->bestmodels.ensure(sizeof(double) * kModelStride * P));
     HIPCHK(c->h_bestmodels.ensure(sizeof(double) * kModelStride * P));
-    HIPCHK(launch_direct_finish(rec4, rec5, dkind, c->d_off, P, c->bestmodels.as<double>(),
+    HIPCHK(launch_direct_finish(rec4, rec5, dst4, dst5, dkind, c->d_off, P, c->bestmodels.as<double>(),
                                 c->h_bestmodels.as<double>(), dmask, s));
     return RSAC_OK;
 }
@@ -1889,6 +1889,7 @@ int rsac_score_poses(rsac_ctx *c, const void *pts3d, const void *pts2d, int32_t 
         rec[(size_t)h * kModelStride + kValidSlot] = 1.0;
     }
     HIPCHK(hipMemcpyAsync(c->models.p, rec.data(), rec.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(c->status.p, 1, (size_t)n_poses, s));  // every pose valid (the scorers read status)
     PnpArgs a;
     r = pnp_args(c, st, flags, 0, n_poses, 0, s, a);
     if (r) return r;
@@ -2075,6 +2076,9 @@ static int hypotheses_core(rsac_ctx *c, Model model, const void *a_pts, const vo
     if (models_out)
         HIPCHK(hipMemcpyAsync(models_out, c->models.p, sizeof(double) * kModelStride * H, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    // PnP hypothesis records leave the validity slot to the status byte: filled in for the caller
+    if (models_out && model == Model::PnP)
+        for (int64_t h = 0; h < H; ++h) models_out[h * kModelStride + kValidSlot] = status_out[h] > 0 ? 1.0 : 0.0;
     return RSAC_OK;
 }
 

@@ -169,8 +169,9 @@ hipError_t launch_gather_models(const double *models, const int64_t *rec, int32_
 // OpenCV's count == model_points branch: per problem with kind[p] = 4 / 5 the record p of rec4 /
 // rec5 (the minimal model of its points in input order) -> out[p] (+ host_out[p], pinned), and its
 // mask rows all 1 (model) or all 0 (none); kind[p] = 0: untouched.  kind, offsets on the device.
-hipError_t launch_direct_finish(const double *rec4, const double *rec5, const int8_t *kind, const int64_t *offsets,
-                                int32_t P, double *out, double *host_out, uint8_t *mask, hipStream_t s);
+hipError_t launch_direct_finish(const double *rec4, const double *rec5, const int8_t *st4, const int8_t *st5,
+                                const int8_t *kind, const int64_t *offsets, int32_t P, double *out, double *host_out,
+                                uint8_t *mask, hipStream_t s);
 
 // the problems' result rows (ok, n_inliers, R 9, t 3; f64, P x 14) on the device: info = P x
 // {record index (< 0: no model), n_inliers} int64 (host-pinned), models = the winners' records
@@ -258,7 +259,7 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
 struct LoState {
     int32_t cur, stopped, best_buf, improvements, count, ticket, last_total, pad;
 };
-hipError_t launch_pnp_lo_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, LoState *st, int step,
+hipError_t launch_pnp_lo_count(const PnpArgs &a, int32_t n, double *model, uint8_t *mask, LoState *st, int step,
                                int32_t init_cur, double *best_out, LoState *host_st, hipStream_t s);
 
 // mask + inlier count (atomically into *count, zeroed by the caller) of one model record, problem 0

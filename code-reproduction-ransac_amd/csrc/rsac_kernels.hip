@@ -798,7 +798,7 @@ __global__ void k_pnp_fmodels(PnpArgs a, int32_t H) {
     if (h >= H) return;
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
     const double *m = a.models + rec * kModelStride;
-    write_fmodel(m, m + 9, m[kValidSlot] != 0.0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
+    write_fmodel(m, m + 9, a.status[rec] > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
                  a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
 }
 
@@ -853,8 +853,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
     for (int q = 0; q < 9; ++q) m[q] = R[q];
 #pragma unroll
     for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
-    m[kValidSlot] = st > 0 ? 1.0 : 0.0;
-    a.status[rec] = st;
+    a.status[rec] = st;  // the record's validity (kValidSlot is left unwritten)
     if (a.counts_out) a.counts_out[rec] = 0;  // the scoring launch that follows may accumulate
     if (a.fmodels)
         write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
@@ -1442,8 +1441,7 @@ __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, i
     for (int q = 0; q < 9; ++q) m[q] = R[q];
 #pragma unroll
     for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
-    m[kValidSlot] = st > 0 ? 1.0 : 0.0;
-    a.status[rec] = st;
+    a.status[rec] = st;  // the record's validity (kValidSlot is left unwritten)
     if (a.counts_out) a.counts_out[rec] = 0;
     if (a.fmodels)
         write_fmodel(R, t, st > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
@@ -1541,8 +1539,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
     for (int q = 0; q < 9; ++q) m[q] = R[q];
 #pragma unroll
     for (int q = 0; q < 3; ++q) m[9 + q] = t[q];
-    m[kValidSlot] = sv > 0 ? 1.0 : 0.0;
-    a.status[rec] = sv;
+    a.status[rec] = sv;  // the record's validity (kValidSlot is left unwritten)
     if (a.counts_out) a.counts_out[rec] = 0;
     if (a.fmodels)
         write_fmodel(R, t, sv > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
@@ -1628,6 +1625,7 @@ __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p
         wund &= wund - 1;
         const float *m = mlds + h * kFModelStride;
         const double *md = a.models + (rec0 + h) * kModelStride;
+        const bool mv = a.status[rec0 + h] > 0;
         int cc = 0;
 #pragma unroll
         for (int j = 0; j < P; ++j) {
@@ -1637,7 +1635,7 @@ __device__ __forceinline__ int sc_fallback(const PnpArgs &a, int prob, int64_t p
             bool ex = false;
             if (und && i < n) {
                 const int64_t q = p0 + i;
-                ex = md[kValidSlot] != 0.0 &&
+                ex = mv &&
                      pnp_err(md, md + 9, k, (double)a.X[q], (double)a.Y[q], (double)a.Z[q], a.U[q], a.V[q]) <= thr2;
             }
             cc += __popcll(__ballot(und && ex)) - __popcll(__ballot(und && r.D < 0.f));
@@ -1949,7 +1947,7 @@ __device__ __forceinline__ void mf_recount(const PnpArgs &a, int64_t rec0, int64
             const bool wa = !(ra.t > bg) && ia < n, wb = !(rb.t > bg) && ib < n;
             if (wa || wb) {
                 const double *md = a.models + (rec0 + j) * kModelStride;
-                const bool mv = md[kValidSlot] != 0.0;
+                const bool mv = a.status[rec0 + j] > 0;
                 int c = 0;
                 if (wa)
                     c += (mv && pnp_err(md, md + 9, k, (double)Xa, (double)Ya, (double)Za, Uxa, Vxa) <= thr2 ? 1 : 0) -
@@ -2275,6 +2273,7 @@ __global__ __launch_bounds__(256) void k_pnp_score(PnpArgs a, int64_t hyp_begin,
     const Cam k{c[0], c[1], c[2], c[3]};
     const float thr2 = a.thr2[prob];
     const double *__restrict__ mb = a.models + ((int64_t)prob * a.hyp_stride + h0) * kModelStride;
+    const int8_t *__restrict__ sb = a.status + (int64_t)prob * a.hyp_stride + h0;
     const float *__restrict__ X = a.X + p0, *__restrict__ Y = a.Y + p0, *__restrict__ Z = a.Z + p0;
     const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
 
@@ -2293,7 +2292,7 @@ __global__ __launch_bounds__(256) void k_pnp_score(PnpArgs a, int64_t hyp_begin,
         }
         for (int h = 0; h < nh; ++h) {
             const double *__restrict__ m = mb + h * kModelStride;
-            if (m[kValidSlot] == 0.0) continue;
+            if (sb[h] <= 0) continue;
             const double R[9] = {m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7], m[8]};
             const double t[3] = {m[9], m[10], m[11]};
             int cc = 0;
@@ -2318,7 +2317,10 @@ __device__ __forceinline__ void pnp_mask_body(const PnpArgs &a, int prob, int64_
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
     if (model_out && blockIdx.x == 0 && threadIdx.x < kModelStride) {
-        const double v = b >= 0 ? a.models[b * kModelStride + threadIdx.x] : 0.0;
+        // (a hypothesis record's validity is its status byte; the per-problem copy carries it in
+        // kValidSlot)
+        const int q = threadIdx.x;
+        const double v = b < 0 ? 0.0 : q == kValidSlot ? (a.status[b] > 0 ? 1.0 : 0.0) : a.models[b * kModelStride + q];
         model_out[(int64_t)prob * kModelStride + threadIdx.x] = v;
         if (host_model_out) host_model_out[(int64_t)prob * kModelStride + threadIdx.x] = v;  // pinned host copy
     }
@@ -2375,7 +2377,7 @@ __global__ void k_pnp_key_finish(PnpArgs a, int32_t n, const unsigned long long 
     }
     if (blockIdx.x == 0 && threadIdx.x < kModelStride) {
         const int q = threadIdx.x;
-        const double v = m ? m[q] : 0.0;
+        const double v = m ? (q == kValidSlot ? 1.0 : m[q]) : 0.0;  // a nonzero key: status > 0 (k_best_key)
         rec16[q] = v;
         if (model12 && q < 12) model12[q] = v;
         if (key_out && q == 0) *key_out = (int64_t)k;
@@ -2538,7 +2540,7 @@ __global__ __launch_bounds__(256) void k_pnp_score_lane(PnpArgs a, int64_t hyp_b
     if (hl < H) {
         const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
         const double *__restrict__ m = a.models + rec * kModelStride;
-        if (m[kValidSlot] != 0.0) {
+        if (a.status[rec] > 0) {
             const double *cm = a.cams + 4 * prob;
             const Cam k{cm[0], cm[1], cm[2], cm[3]};
             const float thr2 = a.thr2[prob];
@@ -2596,17 +2598,19 @@ __global__ void k_gather_models(const double *__restrict__ models, const int64_t
 // kind) -- copied to out[p] (and the pinned host_out[p]), and every one of its points is an inlier
 // when that model exists, none when it does not.  One block per problem; kind[p] == 0: untouched.
 __global__ void k_direct_finish(const double *__restrict__ rec4, const double *__restrict__ rec5,
+                                const int8_t *__restrict__ st4, const int8_t *__restrict__ st5,
                                 const int8_t *__restrict__ kind, const int64_t *__restrict__ offsets,
                                 double *__restrict__ out, double *__restrict__ host_out, uint8_t *__restrict__ mask) {
     const int p = blockIdx.x;
     const int k = kind[p];
     if (k == 0) return;
     const double *m = (k == 5 ? rec5 : rec4) + (int64_t)p * kModelStride;
-    const bool ok = m[kValidSlot] != 0.0;
+    const bool ok = (k == 5 ? st5 : st4)[p] > 0;  // the solve's status byte (PnP records leave kValidSlot)
     const int t = threadIdx.x;
     if (t < kModelStride) {
-        out[(int64_t)p * kModelStride + t] = m[t];
-        if (host_out) host_out[(int64_t)p * kModelStride + t] = m[t];
+        const double v = t == kValidSlot ? (ok ? 1.0 : 0.0) : m[t];
+        out[(int64_t)p * kModelStride + t] = v;
+        if (host_out) host_out[(int64_t)p * kModelStride + t] = v;
     }
     const int64_t o = offsets[p];
     if (mask && t < (int)(offsets[p + 1] - o)) mask[o + t] = ok ? 1 : 0;
@@ -3008,7 +3012,7 @@ __global__ void k_key_model(const double *__restrict__ models, const unsigned lo
     if (k == 0) { out[q] = 0.0; return; }
     const uint64_t low = 0xFFFFFFFFull - (k & 0xFFFFFFFFull);
     const int64_t h = (int64_t)((low - ((uint64_t)hyp_begin & 0xFFFFFFFFull)) & 0xFFFFFFFFull);
-    out[q] = models[h * kModelStride + q];
+    out[q] = q == kValidSlot ? 1.0 : models[h * kModelStride + q];  // a nonzero key: status > 0 (k_best_key)
 }
 
 // ---------------------------------------------------------------------------
@@ -3315,9 +3319,11 @@ hipError_t launch_hom_mask(const HomArgs &a, int32_t P, int32_t max_n, const int
     return hipGetLastError();
 }
 
-hipError_t launch_direct_finish(const double *rec4, const double *rec5, const int8_t *kind, const int64_t *offsets,
-                                int32_t P, double *out, double *host_out, uint8_t *mask, hipStream_t s) {
-    hipLaunchKernelGGL(k_direct_finish, dim3(P), dim3(64), 0, s, rec4, rec5, kind, offsets, out, host_out, mask);
+hipError_t launch_direct_finish(const double *rec4, const double *rec5, const int8_t *st4, const int8_t *st5,
+                                const int8_t *kind, const int64_t *offsets, int32_t P, double *out, double *host_out,
+                                uint8_t *mask, hipStream_t s) {
+    hipLaunchKernelGGL(k_direct_finish, dim3(P), dim3(64), 0, s, rec4, rec5, st4, st5, kind, offsets, out, host_out,
+                       mask);
     return hipGetLastError();
 }
 
@@ -4162,7 +4168,7 @@ __global__ __launch_bounds__(256) void k_pnp_model_count(PnpArgs a, const double
 // chain; a higher count makes m the best (st->best_buf = step's output buffer, improvements++)
 // and, when best_out is set, copies m there; otherwise the chain stops.  count / ticket go back
 // to 0, and the state is mirrored into pinned host memory (host_st).
-__global__ __launch_bounds__(256) void k_pnp_lo_count(PnpArgs a, const double *__restrict__ m,
+__global__ __launch_bounds__(256) void k_pnp_lo_count(PnpArgs a, double *__restrict__ m,
                                                       uint8_t *__restrict__ mask, LoState *st, int step,
                                                       int32_t init_cur, double *best_out, LoState *host_st) {
     __shared__ int wsum[4];
@@ -4171,7 +4177,11 @@ __global__ __launch_bounds__(256) void k_pnp_lo_count(PnpArgs a, const double *_
     const int n = (int)(a.offsets[1] - p0);
     const Cam k{a.cams[0], a.cams[1], a.cams[2], a.cams[3]};
     const float thr2 = a.thr2[0];
-    const bool valid = m[kValidSlot] != 0.0;
+    // the chain's start (step < 0) is the scan's best hypothesis record, valid by construction
+    // (a count above the floor needs status > 0) but without kValidSlot (hypothesis records leave
+    // it to the status byte): stamped here for the refits and recounts that copy and read it
+    const bool valid = step < 0 || m[kValidSlot] != 0.0;
+    if (step < 0 && blockIdx.x == 0 && threadIdx.x == 0) m[kValidSlot] = 1.0;
     int local = 0;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int64_t q = p0 + i;
@@ -4223,7 +4233,7 @@ __global__ __launch_bounds__(256) void k_pnp_lo_count(PnpArgs a, const double *_
     if (host_st) *host_st = v;
 }
 
-hipError_t launch_pnp_lo_count(const PnpArgs &a, int32_t n, const double *model, uint8_t *mask, LoState *st, int step,
+hipError_t launch_pnp_lo_count(const PnpArgs &a, int32_t n, double *model, uint8_t *mask, LoState *st, int step,
                                int32_t init_cur, double *best_out, LoState *host_st, hipStream_t s) {
     unsigned g = cdiv(n > 0 ? n : 1, 256);
     if (g > 2048) g = 2048;

@@ -28,6 +28,11 @@ namespace rsac {
 constexpr int kMaxDrawsPerSubset = 256;
 constexpr int kMaxSubsetAttempts = 10000;  // getSubset(..., rng, 10000) of RANSACPointSetRegistrator::run
 constexpr int kModelStride = 16;           // doubles per hypothesis record (R 9, t 3, valid, pad 3) / (H 9, valid@12)
+// slot 12: validity of single-model records (the winners' bestmodels, uploaded poses, the LO
+// chain's records, homography / fundamental hypotheses).  PnP hypothesis records (the minimal
+// solves' output) leave it unwritten: their validity is the status byte (status > 0), and the
+// solve writes 96 of each record's 128 bytes (k_pnp_solve WRITE_SIZE 19.2 -> 16.1 MB per 100k
+// hypotheses, r05; scripts/ubench/jacobi_probe.py novalid)
 constexpr int kValidSlot = 12;
 
 RSAC_HD bool dfinite(double v) { return __builtin_isfinite(v); }

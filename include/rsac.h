@@ -270,7 +270,9 @@ RSAC_EXPORT int rsac_pnp_evaluate_range(rsac_ctx *ctx, const void *pts3d, const 
 
 /* Raw hot-path outputs for hypotheses [hyp_begin, hyp_begin + n_hyps) of
  * one problem: per-hypothesis status (1 model, 0 solver failed, -1 no
- * subset), inlier count and model (16 f64: R 9, t 3 | H 9; then valid).
+ * subset), inlier count and model (16 f64: R 9, t 3 | H 9; then valid.  PnP
+ * records leave valid to the status byte on the device: host outputs get it
+ * filled in, RSAC_F_DEVICE_OUT outputs carry an unspecified slot 12).
  * subsets (host int32 n_hyps x 4, or x 5 with RSAC_F_MINIMAL_EPNP5; optional) replaces the Philox draw, e.g.
  * with OpenCV's MWC sequence.  This is what the parity tests compare with
  * the CPU restatement hypothesis by hypothesis. */

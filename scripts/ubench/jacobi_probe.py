@@ -7,6 +7,8 @@
   pack12 -- k_pnp_solve writes 12-double records (R, t; validity left to the status byte) instead
             of 13 doubles at a 16-double stride: its write traffic and time (only that kernel's
             figures mean anything in this build; the records' readers still assume 16)
+  novalid -- k_pnp_solve keeps the 16-double stride and leaves the validity slot unwritten: does the
+            write traffic follow the written bytes (96 of each 128-byte record) or the lines touched
 
     python3 scripts/ubench/jacobi_probe.py      -> build/ab/librsac_{jfixed,jcheap,pack12}.so
     then time the kernels under rocprofv3 (scripts/gpu_r05_jprobe.sh)
@@ -49,6 +51,11 @@ PACK12 = [("    double *m = a.models + rec * kModelStride;\n    int32_t idx[4];"
            "    for (int q = 0; q < 3; ++q) m[9 + q] = t[q];\n    a.status[rec] = st;\n"
            "    if (a.counts_out) a.counts_out[rec] = 0;  // the scoring launch")]
 
+NOVALID = [("    for (int q = 0; q < 3; ++q) m[9 + q] = t[q];\n    m[kValidSlot] = st > 0 ? 1.0 : 0.0;\n    a.status[rec] = st;\n"
+            "    if (a.counts_out) a.counts_out[rec] = 0;  // the scoring launch",
+            "    for (int q = 0; q < 3; ++q) m[9 + q] = t[q];\n    a.status[rec] = st;\n"
+            "    if (a.counts_out) a.counts_out[rec] = 0;  // the scoring launch")]
+
 os.makedirs(os.path.join(ROOT, "build", "ab"), exist_ok=True)
 for name in sys.argv[1:] or ["jfixed", "jcheap", "pack12"]:
-    build(name, {"jfixed": FIXED, "jcheap": CHEAP, "pack12": PACK12}[name])
+    build(name, {"jfixed": FIXED, "jcheap": CHEAP, "pack12": PACK12, "novalid": NOVALID}[name])
