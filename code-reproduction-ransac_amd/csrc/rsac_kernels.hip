@@ -1036,18 +1036,19 @@ __device__ __forceinline__ void epnp_j6_step(int sweep, int i, int lane, int s_l
         const int P = jrr_p(R, k), Q = jrr_q(R, k);
         const double c = c6[k], s = s6[k];
         double x, y;
-        x = a0[P]; y = a0[Q]; a0[P] = c * x - s * y; a0[Q] = s * x + c * y;
-        x = a1[P]; y = a1[Q]; a1[P] = c * x - s * y; a1[Q] = s * x + c * y;
-        x = v0[P]; y = v0[Q]; v0[P] = c * x - s * y; v0[Q] = s * x + c * y;
-        x = v1[P]; y = v1[Q]; v1[P] = c * x - s * y; v1[Q] = s * x + c * y;
+        x = a0[P]; y = a0[Q]; a0[P] = jrr_lo(c, s, x, y); a0[Q] = jrr_hi(c, s, x, y);
+        x = a1[P]; y = a1[Q]; a1[P] = jrr_lo(c, s, x, y); a1[Q] = jrr_hi(c, s, x, y);
+        x = v0[P]; y = v0[Q]; v0[P] = jrr_lo(c, s, x, y); v0[Q] = jrr_hi(c, s, x, y);
+        x = v1[P]; y = v1[Q]; v1[P] = jrr_lo(c, s, x, y); v1[Q] = jrr_hi(c, s, x, y);
     }
-    // rows of the lane's own pair: row p <- cs p - sn q, row q <- sn p + cs q (as the 12-lane form:
-    // cs a + x o with x = -sn on row p, +sn on row q: the same bits), straight to the exchange buffer
+    // rows of the lane's own pair: row p <- jrr_lo, row q <- jrr_hi, i.e. fma(cs, own, x other) with
+    // x = -sn on row p, +sn on row q (x other = -(sn other) exactly: the same bits), straight to
+    // the exchange buffer
     const double x0 = f ? -sn : sn, x1 = f ? sn : -sn;
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
-        X[64 * k + lane] = cs * a0[k] + x0 * a1[k];
-        X[kJ6X + 64 * k + lane] = cs * a1[k] + x1 * a0[k];
+        X[64 * k + lane] = dfma(cs, a0[k], x0 * a1[k]);
+        X[kJ6X + 64 * k + lane] = dfma(cs, a1[k], x1 * a0[k]);
     }
     ep_wave_sync();
 #pragma unroll
@@ -1256,17 +1257,17 @@ __device__ __forceinline__ void epnp_blk_step(int sweep, int ba, int bb, int vr0
     ep_wave_sync();
     const double ca = LC[2 * ba], sa = LC[2 * ba + 1], cb = LC[2 * bb], sb = LC[2 * bb + 1];
     // columns (pair b) of rows pa, qa; then rows (pair a) of the column-rotated block
-    const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
-    const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
-    A0[pb] = ca * y00 - sa * y10;
-    A1[pb] = sa * y00 + ca * y10;
-    A0[qb] = ca * y01 - sa * y11;
-    A1[qb] = sa * y01 + ca * y11;
+    const double y00 = jrr_lo(cb, sb, x00, x01), y01 = jrr_hi(cb, sb, x00, x01);
+    const double y10 = jrr_lo(cb, sb, x10, x11), y11 = jrr_hi(cb, sb, x10, x11);
+    A0[pb] = jrr_lo(ca, sa, y00, y10);
+    A1[pb] = jrr_hi(ca, sa, y00, y10);
+    A0[qb] = jrr_lo(ca, sa, y01, y11);
+    A1[qb] = jrr_hi(ca, sa, y01, y11);
     // V's columns (pair b)
-    V0[pb] = cb * v00 - sb * v01;
-    V0[qb] = sb * v00 + cb * v01;
-    V1[pb] = cb * v10 - sb * v11;
-    V1[qb] = sb * v10 + cb * v11;
+    V0[pb] = jrr_lo(cb, sb, v00, v01);
+    V0[qb] = jrr_hi(cb, sb, v00, v01);
+    V1[pb] = jrr_lo(cb, sb, v10, v11);
+    V1[qb] = jrr_hi(cb, sb, v10, v11);
     ep_wave_sync();  // the mirrors hold the step's result; LC may be rewritten
 }
 template <int R>

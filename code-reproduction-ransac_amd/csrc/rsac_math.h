@@ -1284,6 +1284,12 @@ RSAC_HD void jrr_rotation_sel(int sweep, double app, double aqq, double apq, dou
     cs = skip ? 1.0 : c;
     sn = skip ? 0.0 : sv;
 }
+// One rotated pair of elements (x_p, x_q) -> (c x_p - s x_q, s x_p + c x_q), each as c times its
+// own element fused with the rounded product of s and the other (r05: one multiply and one fma
+// per element instead of two multiplies and an add; the oracle's ep_jacobi_rr, the host and both
+// device forms use exactly these two expressions)
+RSAC_HD double jrr_lo(double c, double s, double xp, double xq) { return dfma(c, xp, -(s * xq)); }
+RSAC_HD double jrr_hi(double c, double s, double xp, double xq) { return dfma(c, xq, s * xp); }
 // the sweep test's sums: diag = sum_p A_pp^2 in p order; off = sum over the rows p, in order, of
 // the row's partial sum_{q > p} A_pq^2 in q order (r05: a row's partial is one lane's, so the
 // 16-lane kernel forms it from its registers)
@@ -1318,21 +1324,21 @@ RSAC_HD void jacobi_eig_rr(double *A, double *V, double *d) {
             for (int k = 0; k < N; ++k)
                 for (int i = 0; i < H; ++i) {
                     const double akp = A[k * N + P[i]], akq = A[k * N + Q[i]];
-                    A[k * N + P[i]] = cs[i] * akp - sn[i] * akq;
-                    A[k * N + Q[i]] = sn[i] * akp + cs[i] * akq;
+                    A[k * N + P[i]] = jrr_lo(cs[i], sn[i], akp, akq);
+                    A[k * N + Q[i]] = jrr_hi(cs[i], sn[i], akp, akq);
                 }
             for (int i = 0; i < H; ++i) {
                 for (int k = 0; k < N; ++k) {
                     const double apk = A[P[i] * N + k], aqk = A[Q[i] * N + k];
-                    A[P[i] * N + k] = cs[i] * apk - sn[i] * aqk;
-                    A[Q[i] * N + k] = sn[i] * apk + cs[i] * aqk;
+                    A[P[i] * N + k] = jrr_lo(cs[i], sn[i], apk, aqk);
+                    A[Q[i] * N + k] = jrr_hi(cs[i], sn[i], apk, aqk);
                 }
             }
             for (int k = 0; k < N; ++k)
                 for (int i = 0; i < H; ++i) {
                     const double vkp = V[k * N + P[i]], vkq = V[k * N + Q[i]];
-                    V[k * N + P[i]] = cs[i] * vkp - sn[i] * vkq;
-                    V[k * N + Q[i]] = sn[i] * vkp + cs[i] * vkq;
+                    V[k * N + P[i]] = jrr_lo(cs[i], sn[i], vkp, vkq);
+                    V[k * N + Q[i]] = jrr_hi(cs[i], sn[i], vkp, vkq);
                 }
         }
     }

@@ -2103,8 +2103,13 @@ static void ep_jacobi(int N, double *A, double *V, double *d) {
    (the device runs a step's pairs on different lanes).  Sweep test as ep_jacobi; the rotation's
    t from d = aqq - app and w = 2 apq (one division fewer than through theta), and from the fifth
    sweep on a pair whose apq is negligible next to both diagonal entries is skipped (the rule of
-   Numerical Recipes' jacobi). */
+   Numerical Recipes' jacobi).  Each rotated element is ep_rr_lo / ep_rr_hi: one rounding fewer
+   than c a - s b (r05). */
 static int ep_rr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
+/* one rotated pair (x_p, x_q) -> (c x_p - s x_q, s x_p + c x_q), c times the element's own value
+   fused with the rounded product of s and the other (rsac_math.h jrr_lo / jrr_hi, r05) */
+static double ep_rr_lo(double c, double s, double xp, double xq) { return fma(c, xp, -(s * xq)); }
+static double ep_rr_hi(double c, double s, double xp, double xq) { return fma(c, xq, s * xp); }
 static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
     int P[8], Q[8];
     double cs[8], sn[8];
@@ -2135,21 +2140,21 @@ static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
             for (int k = 0; k < N; ++k)
                 for (int i = 0; i < H; ++i) {
                     double akp = A[k * N + P[i]], akq = A[k * N + Q[i]];
-                    A[k * N + P[i]] = cs[i] * akp - sn[i] * akq;
-                    A[k * N + Q[i]] = sn[i] * akp + cs[i] * akq;
+                    A[k * N + P[i]] = ep_rr_lo(cs[i], sn[i], akp, akq);
+                    A[k * N + Q[i]] = ep_rr_hi(cs[i], sn[i], akp, akq);
                 }
             for (int i = 0; i < H; ++i) {
                 for (int k = 0; k < N; ++k) {
                     double apk = A[P[i] * N + k], aqk = A[Q[i] * N + k];
-                    A[P[i] * N + k] = cs[i] * apk - sn[i] * aqk;
-                    A[Q[i] * N + k] = sn[i] * apk + cs[i] * aqk;
+                    A[P[i] * N + k] = ep_rr_lo(cs[i], sn[i], apk, aqk);
+                    A[Q[i] * N + k] = ep_rr_hi(cs[i], sn[i], apk, aqk);
                 }
             }
             for (int k = 0; k < N; ++k)
                 for (int i = 0; i < H; ++i) {
                     double vkp = V[k * N + P[i]], vkq = V[k * N + Q[i]];
-                    V[k * N + P[i]] = cs[i] * vkp - sn[i] * vkq;
-                    V[k * N + Q[i]] = sn[i] * vkp + cs[i] * vkq;
+                    V[k * N + P[i]] = ep_rr_lo(cs[i], sn[i], vkp, vkq);
+                    V[k * N + Q[i]] = ep_rr_hi(cs[i], sn[i], vkp, vkq);
                 }
         }
     }
