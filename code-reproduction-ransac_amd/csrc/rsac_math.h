@@ -1219,6 +1219,12 @@ RSAC_HD bool jrr_rotation(int sweep, double app, double aqq, double apq, double 
 // divisions).
 // (N <= 4: the rotation loops unrolled, every index static, so a GPU lane keeps A and V in
 // registers; the order of operations is the same either way)
+// One rotated pair of elements (x_p, x_q) -> (c x_p - s x_q, s x_p + c x_q), each as c times its
+// own element fused with the rounded product of s and the other (r05: one multiply and one fma
+// per element instead of two multiplies and an add; the oracle's ep_jacobi / ep_jacobi_rr, the
+// host and the device forms use exactly these two expressions)
+RSAC_HD double jrr_lo(double c, double s, double xp, double xq) { return dfma(c, xp, -(s * xq)); }
+RSAC_HD double jrr_hi(double c, double s, double xp, double xq) { return dfma(c, xq, s * xp); }
 template <int N>
 RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
     constexpr int U = N <= 4 ? N : 1;
@@ -1242,20 +1248,20 @@ RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
 #pragma unroll U
                 for (int k = 0; k < N; ++k) {
                     const double akp = A[k * N + p], akq = A[k * N + q];
-                    A[k * N + p] = c * akp - sn * akq;
-                    A[k * N + q] = sn * akp + c * akq;
+                    A[k * N + p] = jrr_lo(c, sn, akp, akq);
+                    A[k * N + q] = jrr_hi(c, sn, akp, akq);
                 }
 #pragma unroll U
                 for (int k = 0; k < N; ++k) {
                     const double apk = A[p * N + k], aqk = A[q * N + k];
-                    A[p * N + k] = c * apk - sn * aqk;
-                    A[q * N + k] = sn * apk + c * aqk;
+                    A[p * N + k] = jrr_lo(c, sn, apk, aqk);
+                    A[q * N + k] = jrr_hi(c, sn, apk, aqk);
                 }
 #pragma unroll U
                 for (int k = 0; k < N; ++k) {
                     const double vkp = V[k * N + p], vkq = V[k * N + q];
-                    V[k * N + p] = c * vkp - sn * vkq;
-                    V[k * N + q] = sn * vkp + c * vkq;
+                    V[k * N + p] = jrr_lo(c, sn, vkp, vkq);
+                    V[k * N + q] = jrr_hi(c, sn, vkp, vkq);
                 }
             }
     }
@@ -1284,12 +1290,6 @@ RSAC_HD void jrr_rotation_sel(int sweep, double app, double aqq, double apq, dou
     cs = skip ? 1.0 : c;
     sn = skip ? 0.0 : sv;
 }
-// One rotated pair of elements (x_p, x_q) -> (c x_p - s x_q, s x_p + c x_q), each as c times its
-// own element fused with the rounded product of s and the other (r05: one multiply and one fma
-// per element instead of two multiplies and an add; the oracle's ep_jacobi_rr, the host and both
-// device forms use exactly these two expressions)
-RSAC_HD double jrr_lo(double c, double s, double xp, double xq) { return dfma(c, xp, -(s * xq)); }
-RSAC_HD double jrr_hi(double c, double s, double xp, double xq) { return dfma(c, xq, s * xp); }
 // the sweep test's sums: diag = sum_p A_pp^2 in p order; off = sum over the rows p, in order, of
 // the row's partial sum_{q > p} A_pq^2 in q order (r05: a row's partial is one lane's, so the
 // 16-lane kernel forms it from its registers)

@@ -2059,8 +2059,12 @@ static int ep_rot(int sweep, double app, double aqq, double apq, double *cs, dou
     return 1;
 }
 
+/* one rotated pair (x_p, x_q) -> (c x_p - s x_q, s x_p + c x_q), c times the element's own value
+   fused with the rounded product of s and the other (rsac_math.h jrr_lo / jrr_hi, r05) */
+static double ep_rr_lo(double c, double s, double xp, double xq) { return fma(c, xp, -(s * xq)); }
+static double ep_rr_hi(double c, double s, double xp, double xq) { return fma(c, xq, s * xp); }
 /* cyclic Jacobi, symmetric N x N (destroyed): d eigenvalues, V[i*N+k] k-th eigenvector; the
-   rotation and skip rule of ep_rot (r05) */
+   rotation and skip rule of ep_rot, the fused element updates ep_rr_lo / ep_rr_hi (r05) */
 static void ep_jacobi(int N, double *A, double *V, double *d) {
     for (int i = 0; i < N * N; ++i) V[i] = 0.0;
     for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
@@ -2077,18 +2081,18 @@ static void ep_jacobi(int N, double *A, double *V, double *d) {
                 if (!ep_rot(sweep, A[p * N + p], A[q * N + q], A[p * N + q], &cs, &sn)) continue;
                 for (int k = 0; k < N; ++k) {
                     double akp = A[k * N + p], akq = A[k * N + q];
-                    A[k * N + p] = cs * akp - sn * akq;
-                    A[k * N + q] = sn * akp + cs * akq;
+                    A[k * N + p] = ep_rr_lo(cs, sn, akp, akq);
+                    A[k * N + q] = ep_rr_hi(cs, sn, akp, akq);
                 }
                 for (int k = 0; k < N; ++k) {
                     double apk = A[p * N + k], aqk = A[q * N + k];
-                    A[p * N + k] = cs * apk - sn * aqk;
-                    A[q * N + k] = sn * apk + cs * aqk;
+                    A[p * N + k] = ep_rr_lo(cs, sn, apk, aqk);
+                    A[q * N + k] = ep_rr_hi(cs, sn, apk, aqk);
                 }
                 for (int k = 0; k < N; ++k) {
                     double vkp = V[k * N + p], vkq = V[k * N + q];
-                    V[k * N + p] = cs * vkp - sn * vkq;
-                    V[k * N + q] = sn * vkp + cs * vkq;
+                    V[k * N + p] = ep_rr_lo(cs, sn, vkp, vkq);
+                    V[k * N + q] = ep_rr_hi(cs, sn, vkp, vkq);
                 }
             }
     }
@@ -2106,10 +2110,6 @@ static void ep_jacobi(int N, double *A, double *V, double *d) {
    Numerical Recipes' jacobi).  Each rotated element is ep_rr_lo / ep_rr_hi: one rounding fewer
    than c a - s b (r05). */
 static int ep_rr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
-/* one rotated pair (x_p, x_q) -> (c x_p - s x_q, s x_p + c x_q), c times the element's own value
-   fused with the rounded product of s and the other (rsac_math.h jrr_lo / jrr_hi, r05) */
-static double ep_rr_lo(double c, double s, double xp, double xq) { return fma(c, xp, -(s * xq)); }
-static double ep_rr_hi(double c, double s, double xp, double xq) { return fma(c, xq, s * xp); }
 static void ep_jacobi_rr(int N, double *A, double *V, double *d) {
     int P[8], Q[8];
     double cs[8], sn[8];
