@@ -1361,14 +1361,15 @@ RSAC_HD void eig_order_desc(const double *d, int *order) {
 }
 
 // Least squares min |A x - b|, A M x N row-major (M >= N), by Householder QR;
-// A and b are destroyed.  A vanishing pivot gives x_k = 0.
+// A and b are destroyed.  A vanishing pivot gives x_k = 0.  Sums of products and the reflector
+// updates accumulate by fma (r05; the oracle's ep_lsq alike)
 template <int M, int N>
 RSAC_HD void householder_ls(double *A, double *b, double *x) {
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         double nrm = 0.0;
 #pragma unroll
-        for (int i = k; i < M; ++i) nrm = nrm + A[i * N + k] * A[i * N + k];
+        for (int i = k; i < M; ++i) nrm = dfma(A[i * N + k], A[i * N + k], nrm);
         nrm = dsqrt(nrm);
         if (nrm == 0.0) continue;
         const double alpha = A[k * N + k] > 0.0 ? -nrm : nrm;
@@ -1378,29 +1379,29 @@ RSAC_HD void householder_ls(double *A, double *b, double *x) {
         v[k] = v[k] - alpha;
         double vv = 0.0;
 #pragma unroll
-        for (int i = k; i < M; ++i) vv = vv + v[i] * v[i];
+        for (int i = k; i < M; ++i) vv = dfma(v[i], v[i], vv);
         if (vv == 0.0) continue;
 #pragma unroll
         for (int j = k; j < N; ++j) {
             double sdot = 0.0;
 #pragma unroll
-            for (int i = k; i < M; ++i) sdot = sdot + v[i] * A[i * N + j];
+            for (int i = k; i < M; ++i) sdot = dfma(v[i], A[i * N + j], sdot);
             const double f = 2.0 * sdot / vv;
 #pragma unroll
-            for (int i = k; i < M; ++i) A[i * N + j] = A[i * N + j] - f * v[i];
+            for (int i = k; i < M; ++i) A[i * N + j] = dfma(-f, v[i], A[i * N + j]);
         }
         double sdot = 0.0;
 #pragma unroll
-        for (int i = k; i < M; ++i) sdot = sdot + v[i] * b[i];
+        for (int i = k; i < M; ++i) sdot = dfma(v[i], b[i], sdot);
         const double f = 2.0 * sdot / vv;
 #pragma unroll
-        for (int i = k; i < M; ++i) b[i] = b[i] - f * v[i];
+        for (int i = k; i < M; ++i) b[i] = dfma(-f, v[i], b[i]);
     }
 #pragma unroll
     for (int k = N - 1; k >= 0; --k) {
         double sacc = b[k];
 #pragma unroll
-        for (int j = k + 1; j < N; ++j) sacc = sacc - A[k * N + j] * x[j];
+        for (int j = k + 1; j < N; ++j) sacc = dfma(-A[k * N + j], x[j], sacc);
         const double rkk = A[k * N + k];
         x[k] = dabs(rkk) > 1e-300 ? sacc / rkk : 0.0;
     }
@@ -1485,14 +1486,23 @@ RSAC_HD void epnp_gauss_newton(const double *L, const double *rho, double *be) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double *r = L + 10 * i;
-            A[4 * i + 0] = 2.0 * r[0] * be[0] + r[1] * be[1] + r[3] * be[2] + r[6] * be[3];
-            A[4 * i + 1] = r[1] * be[0] + 2.0 * r[2] * be[1] + r[4] * be[2] + r[7] * be[3];
-            A[4 * i + 2] = r[3] * be[0] + r[4] * be[1] + 2.0 * r[5] * be[2] + r[8] * be[3];
-            A[4 * i + 3] = r[6] * be[0] + r[7] * be[1] + r[8] * be[2] + 2.0 * r[9] * be[3];
-            b[i] = rho[i] - (r[0] * be[0] * be[0] + r[1] * be[0] * be[1] + r[2] * be[1] * be[1] +
-                             r[3] * be[0] * be[2] + r[4] * be[1] * be[2] + r[5] * be[2] * be[2] +
-                             r[6] * be[0] * be[3] + r[7] * be[1] * be[3] + r[8] * be[2] * be[3] +
-                             r[9] * be[3] * be[3]);
+            // the Jacobian row and the residual as fma chains in OpenCV's term order (r05; the
+            // oracle's ep_gauss_newton alike)
+            A[4 * i + 0] = dfma(r[6], be[3], dfma(r[3], be[2], dfma(r[1], be[1], 2.0 * r[0] * be[0])));
+            A[4 * i + 1] = dfma(r[7], be[3], dfma(r[4], be[2], dfma(2.0 * r[2], be[1], r[1] * be[0])));
+            A[4 * i + 2] = dfma(r[8], be[3], dfma(2.0 * r[5], be[2], dfma(r[4], be[1], r[3] * be[0])));
+            A[4 * i + 3] = dfma(2.0 * r[9], be[3], dfma(r[8], be[2], dfma(r[7], be[1], r[6] * be[0])));
+            double q = r[0] * be[0] * be[0];
+            q = dfma(r[1] * be[0], be[1], q);
+            q = dfma(r[2] * be[1], be[1], q);
+            q = dfma(r[3] * be[0], be[2], q);
+            q = dfma(r[4] * be[1], be[2], q);
+            q = dfma(r[5] * be[2], be[2], q);
+            q = dfma(r[6] * be[0], be[3], q);
+            q = dfma(r[7] * be[1], be[3], q);
+            q = dfma(r[8] * be[2], be[3], q);
+            q = dfma(r[9] * be[3], be[3], q);
+            b[i] = rho[i] - q;
         }
         householder_ls<6, 4>(A, b, x);
         for (int j = 0; j < 4; ++j) be[j] = be[j] + x[j];

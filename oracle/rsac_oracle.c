@@ -2171,33 +2171,34 @@ static void ep_order(int N, const double *d, int *o) {
     }
 }
 
-/* min |A x - b|, A 6 x N (N <= 5), Householder QR; a vanishing pivot gives x_k = 0 */
+/* min |A x - b|, A 6 x N (N <= 5), Householder QR; a vanishing pivot gives x_k = 0.  Sums of
+   products and the reflector updates accumulate by fma (rsac_math.h householder_ls, r05) */
 static void ep_lsq(int N, double *A, double *b, double *x) {
     const int M = 6;
     for (int k = 0; k < N; ++k) {
         double nrm = 0.0, v[6], vv = 0.0, sdot, f;
-        for (int i = k; i < M; ++i) nrm = nrm + A[i * N + k] * A[i * N + k];
+        for (int i = k; i < M; ++i) nrm = fma(A[i * N + k], A[i * N + k], nrm);
         nrm = sqrt(nrm);
         if (nrm == 0.0) continue;
         double alpha = A[k * N + k] > 0.0 ? -nrm : nrm;
         for (int i = k; i < M; ++i) v[i] = A[i * N + k];
         v[k] = v[k] - alpha;
-        for (int i = k; i < M; ++i) vv = vv + v[i] * v[i];
+        for (int i = k; i < M; ++i) vv = fma(v[i], v[i], vv);
         if (vv == 0.0) continue;
         for (int j = k; j < N; ++j) {
             sdot = 0.0;
-            for (int i = k; i < M; ++i) sdot = sdot + v[i] * A[i * N + j];
+            for (int i = k; i < M; ++i) sdot = fma(v[i], A[i * N + j], sdot);
             f = 2.0 * sdot / vv;
-            for (int i = k; i < M; ++i) A[i * N + j] = A[i * N + j] - f * v[i];
+            for (int i = k; i < M; ++i) A[i * N + j] = fma(-f, v[i], A[i * N + j]);
         }
         sdot = 0.0;
-        for (int i = k; i < M; ++i) sdot = sdot + v[i] * b[i];
+        for (int i = k; i < M; ++i) sdot = fma(v[i], b[i], sdot);
         f = 2.0 * sdot / vv;
-        for (int i = k; i < M; ++i) b[i] = b[i] - f * v[i];
+        for (int i = k; i < M; ++i) b[i] = fma(-f, v[i], b[i]);
     }
     for (int k = N - 1; k >= 0; --k) {
         double s = b[k];
-        for (int j = k + 1; j < N; ++j) s = s - A[k * N + j] * x[j];
+        for (int j = k + 1; j < N; ++j) s = fma(-A[k * N + j], x[j], s);
         double rkk = A[k * N + k];
         x[k] = fabs(rkk) > 1e-300 ? s / rkk : 0.0;
     }
@@ -2360,14 +2361,22 @@ static void ep_gauss_newton(const double *L, const double *rho, double *be) {
         double A[24], b[6], x[4];
         for (int i = 0; i < 6; ++i) {
             const double *r = L + 10 * i;
-            A[4 * i + 0] = 2.0 * r[0] * be[0] + r[1] * be[1] + r[3] * be[2] + r[6] * be[3];
-            A[4 * i + 1] = r[1] * be[0] + 2.0 * r[2] * be[1] + r[4] * be[2] + r[7] * be[3];
-            A[4 * i + 2] = r[3] * be[0] + r[4] * be[1] + 2.0 * r[5] * be[2] + r[8] * be[3];
-            A[4 * i + 3] = r[6] * be[0] + r[7] * be[1] + r[8] * be[2] + 2.0 * r[9] * be[3];
-            b[i] = rho[i] - (r[0] * be[0] * be[0] + r[1] * be[0] * be[1] + r[2] * be[1] * be[1] +
-                             r[3] * be[0] * be[2] + r[4] * be[1] * be[2] + r[5] * be[2] * be[2] +
-                             r[6] * be[0] * be[3] + r[7] * be[1] * be[3] + r[8] * be[2] * be[3] +
-                             r[9] * be[3] * be[3]);
+            /* fma chains in OpenCV's term order (rsac_math.h epnp_gauss_newton, r05) */
+            A[4 * i + 0] = fma(r[6], be[3], fma(r[3], be[2], fma(r[1], be[1], 2.0 * r[0] * be[0])));
+            A[4 * i + 1] = fma(r[7], be[3], fma(r[4], be[2], fma(2.0 * r[2], be[1], r[1] * be[0])));
+            A[4 * i + 2] = fma(r[8], be[3], fma(2.0 * r[5], be[2], fma(r[4], be[1], r[3] * be[0])));
+            A[4 * i + 3] = fma(2.0 * r[9], be[3], fma(r[8], be[2], fma(r[7], be[1], r[6] * be[0])));
+            double q = r[0] * be[0] * be[0];
+            q = fma(r[1] * be[0], be[1], q);
+            q = fma(r[2] * be[1], be[1], q);
+            q = fma(r[3] * be[0], be[2], q);
+            q = fma(r[4] * be[1], be[2], q);
+            q = fma(r[5] * be[2], be[2], q);
+            q = fma(r[6] * be[0], be[3], q);
+            q = fma(r[7] * be[1], be[3], q);
+            q = fma(r[8] * be[2], be[3], q);
+            q = fma(r[9] * be[3], be[3], q);
+            b[i] = rho[i] - q;
         }
         ep_lsq(4, A, b, x);
         for (int j = 0; j < 4; ++j) be[j] = be[j] + x[j];
