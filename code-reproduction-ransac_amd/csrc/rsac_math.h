@@ -1426,7 +1426,8 @@ RSAC_HD EpnpAlpha epnp_alpha_frame(const EpnpFrame &f) {
 
 RSAC_HD void epnp_alphas(const EpnpAlpha &f, double X, double Y, double Z, double *a) {
     const double dx = X - f.c[0], dy = Y - f.c[1], dz = Z - f.c[2];
-    for (int j = 0; j < 3; ++j) a[1 + j] = f.ci[3 * j] * dx + f.ci[3 * j + 1] * dy + f.ci[3 * j + 2] * dz;
+    // (dot products as fma chains from r05, the oracle's ep_alphas alike; also cc, pc and H below)
+    for (int j = 0; j < 3; ++j) a[1 + j] = dfma(f.ci[3 * j + 2], dz, dfma(f.ci[3 * j + 1], dy, f.ci[3 * j] * dx));
     a[0] = 1.0 - a[1] - a[2] - a[3];
 }
 
@@ -1814,9 +1815,9 @@ RSAC_HD bool epnp_pose_err(Red &red, const Cam &k, const EpnpStage1 &s1, const E
     double cc[4][3];
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 3; ++j)
-            cc[i][j] = be[0] * s2.ut[0][3 * i + j] + be[1] * s2.ut[1][3 * i + j] + be[2] * s2.ut[2][3 * i + j] +
-                       be[3] * s2.ut[3][3 * i + j];
-    const double z1 = a1[0] * cc[0][2] + a1[1] * cc[1][2] + a1[2] * cc[2][2] + a1[3] * cc[3][2];
+            cc[i][j] = dfma(be[3], s2.ut[3][3 * i + j],
+                            dfma(be[2], s2.ut[2][3 * i + j], dfma(be[1], s2.ut[1][3 * i + j], be[0] * s2.ut[0][3 * i + j])));
+    const double z1 = dfma(a1[3], cc[3][2], dfma(a1[2], cc[2][2], dfma(a1[1], cc[1][2], a1[0] * cc[0][2])));
     if (z1 < 0.0)
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 3; ++j) cc[i][j] = -cc[i][j];
@@ -1824,7 +1825,7 @@ RSAC_HD bool epnp_pose_err(Red &red, const Cam &k, const EpnpStage1 &s1, const E
     red.template sum<3>([=](double X, double Y, double Z, double, double, double *acc) {
         double a[4];
         epnp_alphas(af, X, Y, Z, a);
-        for (int j = 0; j < 3; ++j) acc[j] += a[0] * cc[0][j] + a[1] * cc[1][j] + a[2] * cc[2][j] + a[3] * cc[3][j];
+        for (int j = 0; j < 3; ++j) acc[j] += dfma(a[3], cc[3][j], dfma(a[2], cc[2][j], dfma(a[1], cc[1][j], a[0] * cc[0][j])));
     }, pc0);
     for (int j = 0; j < 3; ++j) pc0[j] = pc0[j] / n;
     double H[9];
@@ -1832,13 +1833,13 @@ RSAC_HD bool epnp_pose_err(Red &red, const Cam &k, const EpnpStage1 &s1, const E
         double a[4], pc[3];
         epnp_alphas(af, X, Y, Z, a);
         for (int j = 0; j < 3; ++j)
-            pc[j] = a[0] * cc[0][j] + a[1] * cc[1][j] + a[2] * cc[2][j] + a[3] * cc[3][j] - pc0[j];
+            pc[j] = dfma(a[3], cc[3][j], dfma(a[2], cc[2][j], dfma(a[1], cc[1][j], a[0] * cc[0][j]))) - pc0[j];
         const double pw[3] = {X - c0x, Y - c0y, Z - c0z};
         for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) acc[3 * i + j] += pc[i] * pw[j];
+            for (int j = 0; j < 3; ++j) acc[3 * i + j] = dfma(pc[i], pw[j], acc[3 * i + j]);
     }, H);
     if (!epnp_rotation(H, Rk)) return false;
-    for (int i = 0; i < 3; ++i) tk[i] = pc0[i] - (Rk[3 * i] * c0x + Rk[3 * i + 1] * c0y + Rk[3 * i + 2] * c0z);
+    for (int i = 0; i < 3; ++i) tk[i] = pc0[i] - dfma(Rk[3 * i + 2], c0z, dfma(Rk[3 * i + 1], c0y, Rk[3 * i] * c0x));
     double es;
     const double R0 = Rk[0], R1 = Rk[1], R2 = Rk[2], R3 = Rk[3], R4 = Rk[4], R5 = Rk[5], R6 = Rk[6], R7 = Rk[7],
                  R8 = Rk[8], t0 = tk[0], t1 = tk[1], t2 = tk[2];

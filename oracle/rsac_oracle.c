@@ -2208,7 +2208,7 @@ typedef struct { double c[3], ci[9]; } ep_alpha;
 
 static void ep_alphas(const ep_alpha *f, double X, double Y, double Z, double *a) {
     double dx = X - f->c[0], dy = Y - f->c[1], dz = Z - f->c[2];
-    for (int j = 0; j < 3; ++j) a[1 + j] = f->ci[3 * j] * dx + f->ci[3 * j + 1] * dy + f->ci[3 * j + 2] * dz;
+    for (int j = 0; j < 3; ++j) a[1 + j] = fma(f->ci[3 * j + 2], dz, fma(f->ci[3 * j + 1], dy, f->ci[3 * j] * dx));
     a[0] = 1.0 - a[1] - a[2] - a[3];
 }
 
@@ -2241,17 +2241,17 @@ static void ep_f_pc0(const void *prm, double X, double Y, double Z, double u, do
     const ep_pose_prm *p = (const ep_pose_prm *)prm;
     double a[4];
     ep_alphas(&p->af, X, Y, Z, a);
-    for (int j = 0; j < 3; ++j) acc[j] += a[0] * p->cc[0][j] + a[1] * p->cc[1][j] + a[2] * p->cc[2][j] + a[3] * p->cc[3][j];
+    for (int j = 0; j < 3; ++j) acc[j] += fma(a[3], p->cc[3][j], fma(a[2], p->cc[2][j], fma(a[1], p->cc[1][j], a[0] * p->cc[0][j])));
 }
 static void ep_f_cross(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
     const ep_pose_prm *p = (const ep_pose_prm *)prm;
     double a[4], pc[3];
     ep_alphas(&p->af, X, Y, Z, a);
     for (int j = 0; j < 3; ++j)
-        pc[j] = a[0] * p->cc[0][j] + a[1] * p->cc[1][j] + a[2] * p->cc[2][j] + a[3] * p->cc[3][j] - p->pc0[j];
+        pc[j] = fma(a[3], p->cc[3][j], fma(a[2], p->cc[2][j], fma(a[1], p->cc[1][j], a[0] * p->cc[0][j]))) - p->pc0[j];
     double pw[3] = {X - p->c0[0], Y - p->c0[1], Z - p->c0[2]};
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) acc[3 * i + j] += pc[i] * pw[j];
+        for (int j = 0; j < 3; ++j) acc[3 * i + j] = fma(pc[i], pw[j], acc[3 * i + j]);
 }
 typedef struct { double R[9], t[3], cam[4]; } ep_err_prm;
 static void ep_f_err(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
@@ -2539,8 +2539,8 @@ ORC_API int orc_pnp_epnp(const float *X, const float *Y, const float *Z, const f
         for (int j = 0; j < 3; ++j) pp.c0[j] = cw[0][j];
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 3; ++j)
-                pp.cc[i][j] = be[0] * ut[0][3 * i + j] + be[1] * ut[1][3 * i + j] + be[2] * ut[2][3 * i + j] + be[3] * ut[3][3 * i + j];
-        double z1 = a1[0] * pp.cc[0][2] + a1[1] * pp.cc[1][2] + a1[2] * pp.cc[2][2] + a1[3] * pp.cc[3][2];
+                pp.cc[i][j] = fma(be[3], ut[3][3 * i + j], fma(be[2], ut[2][3 * i + j], fma(be[1], ut[1][3 * i + j], be[0] * ut[0][3 * i + j])));
+        double z1 = fma(a1[3], pp.cc[3][2], fma(a1[2], pp.cc[2][2], fma(a1[1], pp.cc[1][2], a1[0] * pp.cc[0][2])));
         if (z1 < 0.0)
             for (int i = 0; i < 4; ++i)
                 for (int j = 0; j < 3; ++j) pp.cc[i][j] = -pp.cc[i][j];
@@ -2550,7 +2550,7 @@ ORC_API int orc_pnp_epnp(const float *X, const float *Y, const float *Z, const f
         ep_reduce(&c, 9, ep_f_cross, &pp, H);
         ep_err_prm ep;
         if (!ep_rotation(H, ep.R)) continue;
-        for (int i = 0; i < 3; ++i) ep.t[i] = pp.pc0[i] - (ep.R[3 * i] * cw[0][0] + ep.R[3 * i + 1] * cw[0][1] + ep.R[3 * i + 2] * cw[0][2]);
+        for (int i = 0; i < 3; ++i) ep.t[i] = pp.pc0[i] - fma(ep.R[3 * i + 2], cw[0][2], fma(ep.R[3 * i + 1], cw[0][1], ep.R[3 * i] * cw[0][0]));
         memcpy(ep.cam, cam, sizeof(ep.cam));
         double es;
         ep_reduce(&c, 1, ep_f_err, &ep, &es);
