@@ -1439,14 +1439,14 @@ RSAC_HD void epnp_pair_acc(const EpnpAlpha &af, const Cam &k, double X, double Y
     constexpr int pi[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3}, pj[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
     double a[4];
     epnp_alphas(af, X, Y, Z, a);
-    const double du = k.cx - u, dv = k.cy - v, w = du * du + dv * dv;
+    const double du = k.cx - u, dv = k.cy - v, w = dfma(dv, dv, du * du);
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
         const double aa = a[pi[5 * H + r]] * a[pj[5 * H + r]];
         acc[4 * r] += aa;
-        acc[4 * r + 1] += aa * du;
-        acc[4 * r + 2] += aa * dv;
-        acc[4 * r + 3] += aa * w;
+        acc[4 * r + 1] = dfma(aa, du, acc[4 * r + 1]);
+        acc[4 * r + 2] = dfma(aa, dv, acc[4 * r + 2]);
+        acc[4 * r + 3] = dfma(aa, w, acc[4 * r + 3]);
     }
 }
 
@@ -1463,7 +1463,7 @@ RSAC_HD void epnp_l6x10(const double *const v[4], double *L) {
             b = a + 1;
         }
         double *r = L + 10 * i;
-        auto dot = [&](int p, int q) { return dv[p][0] * dv[q][0] + dv[p][1] * dv[q][1] + dv[p][2] * dv[q][2]; };
+        auto dot = [&](int p, int q) { return dfma(dv[p][2], dv[q][2], dfma(dv[p][1], dv[q][1], dv[p][0] * dv[q][0])); };
         r[0] = dot(0, 0);
         r[1] = 2.0 * dot(0, 1);
         r[2] = dot(1, 1);
@@ -1703,7 +1703,7 @@ RSAC_HD void epnp_l_rho(const EpnpStage1 &s1, const EpnpStage2 &s2, double *L, d
     for (int a = 0; a < 4; ++a)
         for (int b = a + 1; b < 4; ++b, ++q) {
             const double dx = f.cw[a][0] - f.cw[b][0], dy = f.cw[a][1] - f.cw[b][1], dz = f.cw[a][2] - f.cw[b][2];
-            rho[q] = dx * dx + dy * dy + dz * dz;
+            rho[q] = dfma(dz, dz, dfma(dy, dy, dx * dx));
         }
 }
 
@@ -1755,7 +1755,8 @@ RSAC_HD void epnp_stage1(Red &red, const Cam &k, EpnpStage1 &s1) {
     double cov[6];
     red.template sum<6>([=](double X, double Y, double Z, double, double, double *acc) {
         const double x = X - c0x, y = Y - c0y, z = Z - c0z;
-        acc[0] += x * x; acc[1] += x * y; acc[2] += x * z; acc[3] += y * y; acc[4] += y * z; acc[5] += z * z;
+        acc[0] = dfma(x, x, acc[0]); acc[1] = dfma(x, y, acc[1]); acc[2] = dfma(x, z, acc[2]);
+        acc[3] = dfma(y, y, acc[3]); acc[4] = dfma(y, z, acc[4]); acc[5] = dfma(z, z, acc[5]);
     }, cov);
     {
         double A[9] = {cov[0], cov[1], cov[2], cov[1], cov[3], cov[4], cov[2], cov[4], cov[5]}, V[9], d[3];

@@ -2218,22 +2218,23 @@ static void ep_f_mean(const void *prm, double X, double Y, double Z, double u, d
 static void ep_f_cov(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
     const double *c0 = (const double *)prm;
     double x = X - c0[0], y = Y - c0[1], z = Z - c0[2];
-    acc[0] += x * x; acc[1] += x * y; acc[2] += x * z; acc[3] += y * y; acc[4] += y * z; acc[5] += z * z;
+    acc[0] = fma(x, x, acc[0]); acc[1] = fma(x, y, acc[1]); acc[2] = fma(x, z, acc[2]);
+    acc[3] = fma(y, y, acc[3]); acc[4] = fma(y, z, acc[4]); acc[5] = fma(z, z, acc[5]);
 }
 typedef struct { ep_alpha af; double cam[4]; } ep_pair_prm;
 static void ep_f_pairs(const void *prm, double X, double Y, double Z, double u, double v, double *acc) {
     const ep_pair_prm *p = (const ep_pair_prm *)prm;
     double a[4];
     ep_alphas(&p->af, X, Y, Z, a);
-    double du = p->cam[2] - u, dv = p->cam[3] - v, w = du * du + dv * dv;
+    double du = p->cam[2] - u, dv = p->cam[3] - v, w = fma(dv, dv, du * du);
     int q = 0;
     for (int i = 0; i < 4; ++i)
         for (int j = i; j < 4; ++j, q += 4) {
             double aa = a[i] * a[j];
             acc[q] += aa;
-            acc[q + 1] += aa * du;
-            acc[q + 2] += aa * dv;
-            acc[q + 3] += aa * w;
+            acc[q + 1] = fma(aa, du, acc[q + 1]);
+            acc[q + 2] = fma(aa, dv, acc[q + 2]);
+            acc[q + 3] = fma(aa, w, acc[q + 3]);
         }
 }
 typedef struct { ep_alpha af; double cc[4][3]; double pc0[3]; double c0[3]; } ep_pose_prm;
@@ -2464,7 +2465,7 @@ ORC_API int orc_pnp_epnp(const float *X, const float *Y, const float *Z, const f
                 for (int qq = 0; qq < 3; ++qq) dv[p][qq] = ut[p][3 * a + qq] - ut[p][3 * b + qq];
             ++b;
             if (b > 3) { ++a; b = a + 1; }
-#define EPDOT(p, qd) (dv[p][0] * dv[qd][0] + dv[p][1] * dv[qd][1] + dv[p][2] * dv[qd][2])
+#define EPDOT(p, qd) fma(dv[p][2], dv[qd][2], fma(dv[p][1], dv[qd][1], dv[p][0] * dv[qd][0]))
             double *r = L + 10 * i;
             r[0] = EPDOT(0, 0);
             r[1] = 2.0 * EPDOT(0, 1);
@@ -2482,7 +2483,7 @@ ORC_API int orc_pnp_epnp(const float *X, const float *Y, const float *Z, const f
         for (int i = 0; i < 4; ++i)
             for (int j = i + 1; j < 4; ++j, ++q) {
                 double dx = cw[i][0] - cw[j][0], dy = cw[i][1] - cw[j][1], dz = cw[i][2] - cw[j][2];
-                rho[q] = dx * dx + dy * dy + dz * dz;
+                rho[q] = fma(dz, dz, fma(dy, dy, dx * dx));
             }
         for (int ap = 1; ap <= 3; ++ap) {
             double *be = be3[ap - 1], bb[6];
