@@ -958,12 +958,13 @@ constexpr int kLmTerms = 27;  // J^T J lower triangle (21, row-major packed), J^
 constexpr int kLmMaxIter = 20;
 constexpr int kRedMax = 40;   // widest reduction (EPnP's pair sums)
 
-// adds point (X, Y, Z) -> (u, v)'s terms of J^T J and J^T r to acc
+// adds point (X, Y, Z) -> (u, v)'s terms of J^T J and J^T r to acc.  The rotation's dot products
+// and the accumulations are fma chains (r05; the oracle's lm_point alike)
 RSAC_HD void pnp_lm_point(const double *R, const double *t, const Cam &k, double Xd, double Yd, double Zd, double u,
                           double v, double *acc) {
-    const double px = R[0] * Xd + R[1] * Yd + R[2] * Zd;
-    const double py = R[3] * Xd + R[4] * Yd + R[5] * Zd;
-    const double pz = R[6] * Xd + R[7] * Yd + R[8] * Zd;
+    const double px = dfma(R[2], Zd, dfma(R[1], Yd, R[0] * Xd));
+    const double py = dfma(R[5], Zd, dfma(R[4], Yd, R[3] * Xd));
+    const double pz = dfma(R[8], Zd, dfma(R[7], Yd, R[6] * Xd));
     const double cx = px + t[0], cy = py + t[1], cz = pz + t[2];
     const double iz = 1.0 / cz;
     const double ru = k.fx * cx * iz + k.cx - u;
@@ -977,19 +978,19 @@ RSAC_HD void pnp_lm_point(const double *R, const double *t, const Cam &k, double
     Jv[3] = 0; Jv[4] = dvy; Jv[5] = dvz;
     int q = 0;
     for (int a = 0; a < 6; ++a)
-        for (int b = 0; b <= a; ++b, ++q) acc[q] += Ju[a] * Ju[b] + Jv[a] * Jv[b];
-    for (int a = 0; a < 6; ++a) acc[21 + a] += Ju[a] * ru + Jv[a] * rv;
+        for (int b = 0; b <= a; ++b, ++q) acc[q] = dfma(Jv[a], Jv[b], dfma(Ju[a], Ju[b], acc[q]));
+    for (int a = 0; a < 6; ++a) acc[21 + a] = dfma(Jv[a], rv, dfma(Ju[a], ru, acc[21 + a]));
 }
 
 RSAC_HD double pnp_lm_cost_point(const double *R, const double *t, const Cam &k, double Xd, double Yd, double Zd,
                                  double u, double v) {
-    const double x = R[0] * Xd + R[1] * Yd + R[2] * Zd + t[0];
-    const double y = R[3] * Xd + R[4] * Yd + R[5] * Zd + t[1];
-    const double z = R[6] * Xd + R[7] * Yd + R[8] * Zd + t[2];
+    const double x = dfma(R[2], Zd, dfma(R[1], Yd, R[0] * Xd)) + t[0];
+    const double y = dfma(R[5], Zd, dfma(R[4], Yd, R[3] * Xd)) + t[1];
+    const double z = dfma(R[8], Zd, dfma(R[7], Yd, R[6] * Xd)) + t[2];
     const double iz = 1.0 / z;
     const double ru = k.fx * x * iz + k.cx - u;
     const double rv = k.fy * y * iz + k.cy - v;
-    return ru * ru + rv * rv;
+    return dfma(rv, rv, ru * ru);
 }
 
 // (A + lam diag(A)) x = b by Cholesky, A 6 x 6 SPD, on the packed normal equations of
@@ -1004,8 +1005,8 @@ RSAC_HD bool chol6_solve_packed(const double *acc, double lam, double *x) {
 #pragma unroll
         for (int j = 0; j <= i; ++j) {
             double s = acc[i * (i + 1) / 2 + j];
-            if (i == j) s = s + lam * acc[i * (i + 1) / 2 + i];
-            for (int q = 0; q < j; ++q) s = s - L[i * 6 + q] * L[j * 6 + q];
+            if (i == j) s = dfma(lam, acc[i * (i + 1) / 2 + i], s);
+            for (int q = 0; q < j; ++q) s = dfma(-L[i * 6 + q], L[j * 6 + q], s);  // (r05: fused, the oracle's chol6 alike)
             if (i == j) {
                 if (!(s > 0)) return false;
                 L[i * 6 + i] = dsqrt(s);
@@ -1017,13 +1018,13 @@ RSAC_HD bool chol6_solve_packed(const double *acc, double lam, double *x) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         double s = -acc[21 + i];
-        for (int q = 0; q < i; ++q) s = s - L[i * 6 + q] * y[q];
+        for (int q = 0; q < i; ++q) s = dfma(-L[i * 6 + q], y[q], s);
         y[i] = s * inv[i];
     }
 #pragma unroll
     for (int i = 5; i >= 0; --i) {
         double s = y[i];
-        for (int q = i + 1; q < 6; ++q) s = s - L[q * 6 + i] * x[q];
+        for (int q = i + 1; q < 6; ++q) s = dfma(-L[q * 6 + i], x[q], s);
         x[i] = s * inv[i];
     }
     return true;

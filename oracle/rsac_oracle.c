@@ -1217,9 +1217,10 @@ typedef struct { const float *X, *Y, *Z, *U, *V; const uint8_t *mask; int n; dou
 static void lm_point(const lmctx *c, const double *R, const double *t, int i, double *acc) {
     double Xd = (double)c->X[i] - c->c[0], Yd = (double)c->Y[i] - c->c[1], Zd = (double)c->Z[i] - c->c[2];
     double u = c->U[i], v = c->V[i];
-    double px = R[0] * Xd + R[1] * Yd + R[2] * Zd;
-    double py = R[3] * Xd + R[4] * Yd + R[5] * Zd;
-    double pz = R[6] * Xd + R[7] * Yd + R[8] * Zd;
+    /* dot products and accumulations as fma chains (rsac_math.h pnp_lm_point, r05) */
+    double px = fma(R[2], Zd, fma(R[1], Yd, R[0] * Xd));
+    double py = fma(R[5], Zd, fma(R[4], Yd, R[3] * Xd));
+    double pz = fma(R[8], Zd, fma(R[7], Yd, R[6] * Xd));
     double cx = px + t[0], cy = py + t[1], cz = pz + t[2];
     double iz = 1.0 / cz;
     double ru = c->cam[0] * cx * iz + c->cam[2] - u;
@@ -1233,20 +1234,20 @@ static void lm_point(const lmctx *c, const double *R, const double *t, int i, do
     Jv[3] = 0; Jv[4] = dvy; Jv[5] = dvz;
     int q = 0;
     for (int a = 0; a < 6; ++a)
-        for (int b = 0; b <= a; ++b, ++q) acc[q] += Ju[a] * Ju[b] + Jv[a] * Jv[b];
-    for (int a = 0; a < 6; ++a) acc[21 + a] += Ju[a] * ru + Jv[a] * rv;
+        for (int b = 0; b <= a; ++b, ++q) acc[q] = fma(Jv[a], Jv[b], fma(Ju[a], Ju[b], acc[q]));
+    for (int a = 0; a < 6; ++a) acc[21 + a] = fma(Jv[a], rv, fma(Ju[a], ru, acc[21 + a]));
 }
 
 static double lm_cost_point(const lmctx *c, const double *R, const double *t, int i) {
     double Xd = (double)c->X[i] - c->c[0], Yd = (double)c->Y[i] - c->c[1], Zd = (double)c->Z[i] - c->c[2];
     double u = c->U[i], v = c->V[i];
-    double x = R[0] * Xd + R[1] * Yd + R[2] * Zd + t[0];
-    double y = R[3] * Xd + R[4] * Yd + R[5] * Zd + t[1];
-    double z = R[6] * Xd + R[7] * Yd + R[8] * Zd + t[2];
+    double x = fma(R[2], Zd, fma(R[1], Yd, R[0] * Xd)) + t[0];
+    double y = fma(R[5], Zd, fma(R[4], Yd, R[3] * Xd)) + t[1];
+    double z = fma(R[8], Zd, fma(R[7], Yd, R[6] * Xd)) + t[2];
     double iz = 1.0 / z;
     double ru = c->cam[0] * x * iz + c->cam[2] - u;
     double rv = c->cam[1] * y * iz + c->cam[3] - v;
-    return ru * ru + rv * rv;
+    return fma(rv, rv, ru * ru);
 }
 
 /* nv = LM_TERMS: normal equations; nv = 1: cost */
@@ -1286,8 +1287,8 @@ static int chol6(const double *A, double lam, const double *b, double *x) {
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j <= i; ++j) {
             double s = A[i * 6 + j];
-            if (i == j) s = s + lam * A[i * 6 + i];
-            for (int k = 0; k < j; ++k) s = s - L[i * 6 + k] * L[j * 6 + k];
+            if (i == j) s = fma(lam, A[i * 6 + i], s);
+            for (int k = 0; k < j; ++k) s = fma(-L[i * 6 + k], L[j * 6 + k], s);  /* fused (r05) */
             if (i == j) {
                 if (!(s > 0)) return 0;
                 L[i * 6 + i] = sqrt(s);
@@ -1298,12 +1299,12 @@ static int chol6(const double *A, double lam, const double *b, double *x) {
         }
     for (int i = 0; i < 6; ++i) {
         double s = b[i];
-        for (int k = 0; k < i; ++k) s = s - L[i * 6 + k] * y[k];
+        for (int k = 0; k < i; ++k) s = fma(-L[i * 6 + k], y[k], s);
         y[i] = s * inv[i];
     }
     for (int i = 5; i >= 0; --i) {
         double s = y[i];
-        for (int k = i + 1; k < 6; ++k) s = s - L[k * 6 + i] * x[k];
+        for (int k = i + 1; k < 6; ++k) s = fma(-L[k * 6 + i], x[k], s);
         x[i] = s * inv[i];
     }
     return 1;
