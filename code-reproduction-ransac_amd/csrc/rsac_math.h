@@ -36,6 +36,8 @@ constexpr int kModelStride = 16;           // doubles per hypothesis record (R 9
 constexpr int kValidSlot = 12;
 
 RSAC_HD bool dfinite(double v) { return __builtin_isfinite(v); }
+// a * b + c with one rounding (the oracle's fma(); correctly rounded on every backend)
+RSAC_HD double dfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 RSAC_HD double dabs(double v) { return __builtin_fabs(v); }
 RSAC_HD double dsqrt(double v) { return __builtin_sqrt(v); }
 
@@ -330,9 +332,10 @@ RSAC_HD double cubic_root(double b, double c, double d) {
      * 50; lanes whose |f| stalls at the rounding level above 1e-13 -- about 4 % of C2's samples --
      * then stop at 12 instead of 50, so a GPU wave no longer runs 50 divisions for one of them) */
     for (int it = 0; it < 12; ++it) {
-        double fx = ((r0 + b) * r0 + c) * r0 + d;
+        // Horner by fma (r05; the oracle's cubic_root alike)
+        double fx = dfma(dfma(r0 + b, r0, c), r0, d);
         if (it >= 7 && !(dabs(fx) > 1e-13)) break;
-        double fpx = (3.0 * r0 + 2.0 * b) * r0 + c;
+        double fpx = dfma(3.0 * r0 + 2.0 * b, r0, c);
         r0 = r0 - fx / fpx;
     }
     return r0;
@@ -340,9 +343,10 @@ RSAC_HD double cubic_root(double b, double c, double d) {
 
 RSAC_HD double lt_resid(double l1, double l2, double l3, double a12, double a13, double a23, double b12, double b13,
                         double b23, double &r0, double &r1, double &r2) {
-    r0 = l1 * l1 + l2 * l2 + b12 * l1 * l2 - a12;
-    r1 = l1 * l1 + l3 * l3 + b13 * l1 * l3 - a13;
-    r2 = l2 * l2 + l3 * l3 + b23 * l2 * l3 - a23;
+    // (fma chains from r05, the oracle's lt_resid alike)
+    r0 = dfma(b12 * l1, l2, dfma(l2, l2, l1 * l1)) - a12;
+    r1 = dfma(b13 * l1, l3, dfma(l3, l3, l1 * l1)) - a13;
+    r2 = dfma(b23 * l2, l3, dfma(l3, l3, l2 * l2)) - a23;
     return dabs(r0) + dabs(r1) + dabs(r2);
 }
 
@@ -363,7 +367,7 @@ RSAC_HD void lt_refine(double &L0, double &L1, double &L2, double a12, double a1
         double d0 = -j5 * j7 * r0 + -j1 * j8 * r1 + j1 * j5 * r2;
         double d1 = -j3 * j8 * r0 + j0 * j8 * r1 + -j0 * j5 * r2;
         double d2 = j3 * j7 * r0 + -j0 * j7 * r1 + -j1 * j3 * r2;
-        double n0 = l1 - det * d0, n1 = l2 - det * d1, n2 = l3 - det * d2;
+        double n0 = dfma(-det, d0, l1), n1 = dfma(-det, d1, l2), n2 = dfma(-det, d2, l3);
         double q0, q1, q2;
         double s1 = lt_resid(n0, n1, n2, a12, a13, a23, b12, b13, b23, q0, q1, q2);
         if (s1 > s0) break;
@@ -391,11 +395,11 @@ RSAC_HD bool p3p_pose_of(double l1, double l2, double l3, const double *y1, cons
     for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int cc = 0; cc < 3; ++cc)
-            R[3 * r + cc] = Y[3 * r] * Xi[cc] + Y[3 * r + 1] * Xi[3 + cc] + Y[3 * r + 2] * Xi[6 + cc];
+            R[3 * r + cc] = dfma(Y[3 * r + 2], Xi[6 + cc], dfma(Y[3 * r + 1], Xi[3 + cc], Y[3 * r] * Xi[cc]));  // (r05: fma)
     bool fin = true;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-        const double rx = R[3 * r] * x1[0] + R[3 * r + 1] * x1[1] + R[3 * r + 2] * x1[2];
+        const double rx = dfma(R[3 * r + 2], x1[2], dfma(R[3 * r + 1], x1[1], R[3 * r] * x1[0]));
         t[r] = ry1[r] - rx;
         fin = fin && dfinite(t[r]);
     }
@@ -773,7 +777,6 @@ RSAC_HD float hom_err(const float *h, float x, float y, float u, float v) {
 //   evaluated division-free as r^2 <= T (a^2 + b^2 + a'^2 + b'^2) in f64 with
 //   explicit fma (bit-identical on every backend).
 // ---------------------------------------------------------------------------
-RSAC_HD double dfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
 RSAC_HD bool fm_norm8(const float (&x)[8], const float (&y)[8], double &cx, double &cy, double &s) {
     cx = 0.0;

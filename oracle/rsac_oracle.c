@@ -299,9 +299,10 @@ static double cubic_root(double b, double c, double d) {
      * 50; lanes whose |f| stalls at the rounding level above 1e-13 -- about 4 % of C2's samples --
      * then stop at 12 instead of 50, so a GPU wave no longer runs 50 divisions for one of them) */
     for (int it = 0; it < 12; ++it) {
-        double fx = ((r0 + b) * r0 + c) * r0 + d;
+        /* Horner by fma (rsac_math.h cubic_root, r05) */
+        double fx = fma(fma(r0 + b, r0, c), r0, d);
         if (it >= 7 && !(fabs(fx) > 1e-13)) break;
-        double fpx = (3.0 * r0 + 2.0 * b) * r0 + c;
+        double fpx = fma(3.0 * r0 + 2.0 * b, r0, c);
         r0 = r0 - fx / fpx;
     }
     return r0;
@@ -342,9 +343,10 @@ static void eig_known0(const double A[9], double v1[3], double v2[3], double *e1
 static double lt_resid(const double L[3], double a12, double a13, double a23, double b12, double b13, double b23,
                        double r[3]) {
     double l1 = L[0], l2 = L[1], l3 = L[2];
-    r[0] = l1 * l1 + l2 * l2 + b12 * l1 * l2 - a12;
-    r[1] = l1 * l1 + l3 * l3 + b13 * l1 * l3 - a13;
-    r[2] = l2 * l2 + l3 * l3 + b23 * l2 * l3 - a23;
+    /* fma chains (rsac_math.h lt_resid, r05) */
+    r[0] = fma(b12 * l1, l2, fma(l2, l2, l1 * l1)) - a12;
+    r[1] = fma(b13 * l1, l3, fma(l3, l3, l1 * l1)) - a13;
+    r[2] = fma(b23 * l2, l3, fma(l3, l3, l2 * l2)) - a23;
     return fabs(r[0]) + fabs(r[1]) + fabs(r[2]);
 }
 
@@ -365,7 +367,7 @@ static void lt_refine(double L[3], double a12, double a13, double a23, double b1
         double d1 = -j3 * j8 * r[0] + j0 * j8 * r[1] + -j0 * j5 * r[2];
         double d2 = j3 * j7 * r[0] + -j0 * j7 * r[1] + -j1 * j3 * r[2];
         double Ln[3];
-        Ln[0] = l1 - det * d0; Ln[1] = l2 - det * d1; Ln[2] = l3 - det * d2;
+        Ln[0] = fma(-det, d0, l1); Ln[1] = fma(-det, d1, l2); Ln[2] = fma(-det, d2, l3);
         double rn[3];
         double s1 = lt_resid(Ln, a12, a13, a23, b12, b13, b23, rn);
         if (s1 > s0) break;
@@ -477,10 +479,10 @@ ORC_API int orc_p3p(const double y[9], const double x[9], double Rs[36], double 
         double *R = Rs + 9 * nout, *t = ts + 3 * nout;
         for (int r = 0; r < 3; ++r)
             for (int cc = 0; cc < 3; ++cc)
-                R[3 * r + cc] = Ym[3 * r] * Xi[cc] + Ym[3 * r + 1] * Xi[3 + cc] + Ym[3 * r + 2] * Xi[6 + cc];
+                R[3 * r + cc] = fma(Ym[3 * r + 2], Xi[6 + cc], fma(Ym[3 * r + 1], Xi[3 + cc], Ym[3 * r] * Xi[cc]));
         int fin = 1;
         for (int r = 0; r < 3; ++r) {
-            double rx = R[3 * r] * x1[0] + R[3 * r + 1] * x1[1] + R[3 * r + 2] * x1[2];
+            double rx = fma(R[3 * r + 2], x1[2], fma(R[3 * r + 1], x1[1], R[3 * r] * x1[0]));
             t[r] = ry1[r] - rx;
             fin &= isfinite(t[r]) != 0;
         }
