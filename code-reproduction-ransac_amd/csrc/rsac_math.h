@@ -357,16 +357,16 @@ RSAC_HD void lt_refine(double &L0, double &L1, double &L2, double a12, double a1
         double s0 = lt_resid(L0, L1, L2, a12, a13, a23, b12, b13, b23, r0, r1, r2);
         if (s0 < 1e-10) break;
         double l1 = L0, l2 = L1, l3 = L2;
-        double j0 = 2.0 * l1 + b12 * l2;
-        double j1 = 2.0 * l2 + b12 * l1;
-        double j3 = 2.0 * l1 + b13 * l3;
-        double j5 = 2.0 * l3 + b13 * l1;
-        double j7 = 2.0 * l2 + b23 * l3;
-        double j8 = 2.0 * l3 + b23 * l2;
+        double j0 = dfma(b12, l2, 2.0 * l1);
+        double j1 = dfma(b12, l1, 2.0 * l2);
+        double j3 = dfma(b13, l3, 2.0 * l1);
+        double j5 = dfma(b13, l1, 2.0 * l3);
+        double j7 = dfma(b23, l3, 2.0 * l2);
+        double j8 = dfma(b23, l2, 2.0 * l3);
         double det = 1.0 / (-j0 * j5 * j7 - j1 * j3 * j8);
-        double d0 = -j5 * j7 * r0 + -j1 * j8 * r1 + j1 * j5 * r2;
-        double d1 = -j3 * j8 * r0 + j0 * j8 * r1 + -j0 * j5 * r2;
-        double d2 = j3 * j7 * r0 + -j0 * j7 * r1 + -j1 * j3 * r2;
+        double d0 = dfma(j1 * j5, r2, dfma(-j1 * j8, r1, -j5 * j7 * r0));
+        double d1 = dfma(-j0 * j5, r2, dfma(j0 * j8, r1, -j3 * j8 * r0));
+        double d2 = dfma(-j1 * j3, r2, dfma(-j0 * j7, r1, j3 * j7 * r0));
         double n0 = dfma(-det, d0, l1), n1 = dfma(-det, d1, l2), n2 = dfma(-det, d2, l3);
         double q0, q1, q2;
         double s1 = lt_resid(n0, n1, n2, a12, a13, a23, b12, b13, b23, q0, q1, q2);
@@ -430,18 +430,18 @@ struct LtCommon {
 RSAC_HD bool lt_common(const double *y, const double *x, LtCommon &L) {
     const double *y1 = y, *y2 = y + 3, *y3 = y + 6;
     const double *x1 = x, *x2 = x + 3, *x3 = x + 6;
-    double b12 = -2.0 * (y1[0] * y2[0] + y1[1] * y2[1] + y1[2] * y2[2]);
-    double b13 = -2.0 * (y1[0] * y3[0] + y1[1] * y3[1] + y1[2] * y3[2]);
-    double b23 = -2.0 * (y2[0] * y3[0] + y2[1] * y3[1] + y2[2] * y3[2]);
+    double b12 = -2.0 * dfma(y1[2], y2[2], dfma(y1[1], y2[1], y1[0] * y2[0]));
+    double b13 = -2.0 * dfma(y1[2], y3[2], dfma(y1[1], y3[1], y1[0] * y3[0]));
+    double b23 = -2.0 * dfma(y2[2], y3[2], dfma(y2[1], y3[1], y2[0] * y3[0]));
     double d12[3], d13[3], d23[3], d12xd13[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) { d12[k] = x1[k] - x2[k]; d13[k] = x1[k] - x3[k]; d23[k] = x2[k] - x3[k]; }
     d12xd13[0] = d12[1] * d13[2] - d12[2] * d13[1];
     d12xd13[1] = d12[2] * d13[0] - d12[0] * d13[2];
     d12xd13[2] = d12[0] * d13[1] - d12[1] * d13[0];
-    double a12 = d12[0] * d12[0] + d12[1] * d12[1] + d12[2] * d12[2];
-    double a13 = d13[0] * d13[0] + d13[1] * d13[1] + d13[2] * d13[2];
-    double a23 = d23[0] * d23[0] + d23[1] * d23[1] + d23[2] * d23[2];
+    double a12 = dfma(d12[2], d12[2], dfma(d12[1], d12[1], d12[0] * d12[0]));
+    double a13 = dfma(d13[2], d13[2], dfma(d13[1], d13[1], d13[0] * d13[0]));
+    double a23 = dfma(d23[2], d23[2], dfma(d23[1], d23[1], d23[0] * d23[0]));
 
     double c31 = -0.5 * b13, c23 = -0.5 * b23, c12 = -0.5 * b12;
     double blob = c12 * c23 * c31 - 1.0;
@@ -563,9 +563,9 @@ RSAC_HD void bearing(const Cam &k, float uf, float vf, double *out) {
 RSAC_HD double pnp_fourth_error(const double *Rk, const double *tk, const float (&X)[4], const float (&Y)[4],
                                 const float (&Z)[4], const float (&U)[4], const float (&V)[4], const Cam &k) {
     const double X4 = X[3], Y4 = Y[3], Z4 = Z[3];
-    double x = Rk[0] * X4 + Rk[1] * Y4; x = x + Rk[2] * Z4; x = x + tk[0];
-    double y = Rk[3] * X4 + Rk[4] * Y4; y = y + Rk[5] * Z4; y = y + tk[1];
-    double z = Rk[6] * X4 + Rk[7] * Y4; z = z + Rk[8] * Z4; z = z + tk[2];
+    const double x = dfma(Rk[2], Z4, dfma(Rk[1], Y4, Rk[0] * X4)) + tk[0];
+    const double y = dfma(Rk[5], Z4, dfma(Rk[4], Y4, Rk[3] * X4)) + tk[1];
+    const double z = dfma(Rk[8], Z4, dfma(Rk[7], Y4, Rk[6] * X4)) + tk[2];
     const double iz = (z != 0.0) ? 1.0 / z : 1.0;
     const double du = (x * iz) * k.fx + k.cx - (double)U[3];
     const double dv = (y * iz) * k.fy + k.cy - (double)V[3];

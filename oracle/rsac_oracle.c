@@ -356,16 +356,16 @@ static void lt_refine(double L[3], double a12, double a13, double a23, double b1
         double s0 = lt_resid(L, a12, a13, a23, b12, b13, b23, r);
         if (s0 < 1e-10) break;
         double l1 = L[0], l2 = L[1], l3 = L[2];
-        double j0 = 2.0 * l1 + b12 * l2;  /* dr1/dl1 */
-        double j1 = 2.0 * l2 + b12 * l1;  /* dr1/dl2 */
-        double j3 = 2.0 * l1 + b13 * l3;  /* dr2/dl1 */
-        double j5 = 2.0 * l3 + b13 * l1;  /* dr2/dl3 */
-        double j7 = 2.0 * l2 + b23 * l3;  /* dr3/dl2 */
-        double j8 = 2.0 * l3 + b23 * l2;  /* dr3/dl3 */
+        double j0 = fma(b12, l2, 2.0 * l1);  /* dr1/dl1 */
+        double j1 = fma(b12, l1, 2.0 * l2);  /* dr1/dl2 */
+        double j3 = fma(b13, l3, 2.0 * l1);  /* dr2/dl1 */
+        double j5 = fma(b13, l1, 2.0 * l3);  /* dr2/dl3 */
+        double j7 = fma(b23, l3, 2.0 * l2);  /* dr3/dl2 */
+        double j8 = fma(b23, l2, 2.0 * l3);  /* dr3/dl3 */
         double det = 1.0 / (-j0 * j5 * j7 - j1 * j3 * j8);
-        double d0 = -j5 * j7 * r[0] + -j1 * j8 * r[1] + j1 * j5 * r[2];
-        double d1 = -j3 * j8 * r[0] + j0 * j8 * r[1] + -j0 * j5 * r[2];
-        double d2 = j3 * j7 * r[0] + -j0 * j7 * r[1] + -j1 * j3 * r[2];
+        double d0 = fma(j1 * j5, r[2], fma(-j1 * j8, r[1], -j5 * j7 * r[0]));
+        double d1 = fma(-j0 * j5, r[2], fma(j0 * j8, r[1], -j3 * j8 * r[0]));
+        double d2 = fma(-j1 * j3, r[2], fma(-j0 * j7, r[1], j3 * j7 * r[0]));
         double Ln[3];
         Ln[0] = fma(-det, d0, l1); Ln[1] = fma(-det, d1, l2); Ln[2] = fma(-det, d2, l3);
         double rn[3];
@@ -400,15 +400,15 @@ static int inv3(const double M[9], double I[9]) {
 ORC_API int orc_p3p(const double y[9], const double x[9], double Rs[36], double ts[12]) {
     const double *y1 = y, *y2 = y + 3, *y3 = y + 6;
     const double *x1 = x, *x2 = x + 3, *x3 = x + 6;
-    double b12 = -2.0 * (y1[0] * y2[0] + y1[1] * y2[1] + y1[2] * y2[2]);
-    double b13 = -2.0 * (y1[0] * y3[0] + y1[1] * y3[1] + y1[2] * y3[2]);
-    double b23 = -2.0 * (y2[0] * y3[0] + y2[1] * y3[1] + y2[2] * y3[2]);
+    double b12 = -2.0 * fma(y1[2], y2[2], fma(y1[1], y2[1], y1[0] * y2[0]));
+    double b13 = -2.0 * fma(y1[2], y3[2], fma(y1[1], y3[1], y1[0] * y3[0]));
+    double b23 = -2.0 * fma(y2[2], y3[2], fma(y2[1], y3[1], y2[0] * y3[0]));
     double d12[3], d13[3], d23[3], d12xd13[3];
     for (int k = 0; k < 3; ++k) { d12[k] = x1[k] - x2[k]; d13[k] = x1[k] - x3[k]; d23[k] = x2[k] - x3[k]; }
     cross3(d12, d13, d12xd13);
-    double a12 = d12[0] * d12[0] + d12[1] * d12[1] + d12[2] * d12[2];
-    double a13 = d13[0] * d13[0] + d13[1] * d13[1] + d13[2] * d13[2];
-    double a23 = d23[0] * d23[0] + d23[1] * d23[1] + d23[2] * d23[2];
+    double a12 = fma(d12[2], d12[2], fma(d12[1], d12[1], d12[0] * d12[0]));
+    double a13 = fma(d13[2], d13[2], fma(d13[1], d13[1], d13[0] * d13[0]));
+    double a23 = fma(d23[2], d23[2], fma(d23[1], d23[1], d23[0] * d23[0]));
 
     double c31 = -0.5 * b13, c23 = -0.5 * b23, c12 = -0.5 * b12;
     double blob = c12 * c23 * c31 - 1.0;
@@ -521,9 +521,9 @@ ORC_API int orc_pnp_minimal(const float *X, const float *Y, const float *Z, cons
     double best_e = 0.0;
     for (int s = 0; s < ns; ++s) {
         const double *Rk = Rs + 9 * s, *tk = ts + 3 * s;
-        double x = Rk[0] * X4 + Rk[1] * Y4; x = x + Rk[2] * Z4; x = x + tk[0];
-        double y = Rk[3] * X4 + Rk[4] * Y4; y = y + Rk[5] * Z4; y = y + tk[1];
-        double z = Rk[6] * X4 + Rk[7] * Y4; z = z + Rk[8] * Z4; z = z + tk[2];
+        double x = fma(Rk[2], Z4, fma(Rk[1], Y4, Rk[0] * X4)) + tk[0];
+        double y = fma(Rk[5], Z4, fma(Rk[4], Y4, Rk[3] * X4)) + tk[1];
+        double z = fma(Rk[8], Z4, fma(Rk[7], Y4, Rk[6] * X4)) + tk[2];
         double iz = (z != 0.0) ? 1.0 / z : 1.0;
         double du = (x * iz) * cam[0] + cam[2] - (double)U[i4];
         double dv = (y * iz) * cam[1] + cam[3] - (double)V[i4];

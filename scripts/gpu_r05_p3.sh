@@ -6,9 +6,9 @@ O=gpurun_out/p3
 rm -rf $O && mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/suite.log 2>&1
 rc=$?; echo "suite rc=$rc"; tail -3 $O/suite.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python scripts/ms_ab.py build/ab/librsac_pre3.so build/ab/librsac_p3fma.so --rounds 4 > $O/ab.log 2>&1 || exit $?
+timeout -k 10 400 python scripts/ms_ab.py build/ab/librsac_p3a.so build/ab/librsac_p3b.so --rounds 4 > $O/ab.log 2>&1 || exit $?
 tail -3 $O/ab.log
-for v in pre3 p3fma; do
+for v in p3a p3b; do
   d=$O/kt_$v
   RSAC_LIB_PATH=$PWD/build/ab/librsac_$v.so timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
       python3 scripts/workload_prof.py c2 10 > $d.log 2>&1 || { tail -3 $d.log; exit 1; }
