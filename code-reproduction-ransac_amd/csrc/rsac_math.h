@@ -446,10 +446,11 @@ RSAC_HD bool lt_common(const double *y, const double *x, LtCommon &L) {
     double c31 = -0.5 * b13, c23 = -0.5 * b23, c12 = -0.5 * b12;
     double blob = c12 * c23 * c31 - 1.0;
     double s31 = 1.0 - c31 * c31, s23 = 1.0 - c23 * c23, s12 = 1.0 - c12 * c12;
-    double p3 = a13 * (a23 * s31 - a13 * s23);
-    double p2 = 2.0 * blob * a23 * a13 + a13 * (2.0 * a12 + a13) * s23 + a23 * (a23 - a12) * s31;
-    double p1 = a23 * (a13 - a23) * s12 - a12 * a12 * s23 - 2.0 * a12 * (blob * a23 + a13 * s23);
-    double p0 = a12 * (a12 * s23 - a23 * s12);
+    // (fma chains from r05, the oracle's orc_p3p / eig_known0 alike)
+    double p3 = a13 * dfma(a23, s31, -(a13 * s23));
+    double p2 = dfma(a23 * (a23 - a12), s31, dfma(a13 * (2.0 * a12 + a13), s23, 2.0 * blob * a23 * a13));
+    double p1 = dfma(-(2.0 * a12), dfma(a13, s23, blob * a23), dfma(-(a12 * a12), s23, a23 * (a13 - a23) * s12));
+    double p0 = a12 * dfma(a12, s23, -(a23 * s12));
     if (p3 == 0.0 || !dfinite(p3)) return false;
     double ip3 = 1.0 / p3;
     p2 = p2 * ip3; p1 = p1 * ip3; p0 = p0 * ip3;
@@ -467,26 +468,26 @@ RSAC_HD bool lt_common(const double *y, const double *x, LtCommon &L) {
     {
         double a01sq = A01 * A01;
         double b = -A00 - A11 - A22;
-        double c = -a01sq - A02 * A02 - A12 * A12 + A00 * (A11 + A22) + A11 * A22;
+        double c = dfma(A11, A22, dfma(A00, A11 + A22, dfma(-A12, A12, dfma(-A02, A02, -a01sq))));
         root2real(b, c, e1, e2);
         if (dabs(e1) < dabs(e2)) { double tmp = e1; e1 = e2; e2 = tmp; }
         double m0011 = -A00 * A11;
-        double pr0 = A01 * A12 - A02 * A11;
-        double pr1 = A01 * A02 - A00 * A12;
+        double pr0 = dfma(A01, A12, -(A02 * A11));
+        double pr1 = dfma(A01, A02, -(A00 * A12));
         {
             double e = e1;
-            double tmp = 1.0 / (e * (A00 + A11) + m0011 - e * e + a01sq);
-            double q1 = -(e * A02 + pr0) * tmp;
-            double q2 = -(e * A12 + pr1) * tmp;
-            double rn = 1.0 / dsqrt(q1 * q1 + q2 * q2 + 1.0);
+            double tmp = 1.0 / (dfma(-e, e, dfma(e, A00 + A11, m0011)) + a01sq);
+            double q1 = -dfma(e, A02, pr0) * tmp;
+            double q2 = -dfma(e, A12, pr1) * tmp;
+            double rn = 1.0 / dsqrt(dfma(q2, q2, q1 * q1) + 1.0);
             L.v1[0] = q1 * rn; L.v1[1] = q2 * rn; L.v1[2] = rn;
         }
         {
             double e = e2;
-            double tmp = 1.0 / (e * (A00 + A11) + m0011 - e * e + a01sq);
-            double q1 = -(e * A02 + pr0) * tmp;
-            double q2 = -(e * A12 + pr1) * tmp;
-            double rn = 1.0 / dsqrt(q1 * q1 + q2 * q2 + 1.0);
+            double tmp = 1.0 / (dfma(-e, e, dfma(e, A00 + A11, m0011)) + a01sq);
+            double q1 = -dfma(e, A02, pr0) * tmp;
+            double q2 = -dfma(e, A12, pr1) * tmp;
+            double rn = 1.0 / dsqrt(dfma(q2, q2, q1 * q1) + 1.0);
             L.v2[0] = q1 * rn; L.v2[1] = q2 * rn; L.v2[2] = rn;
         }
     }
@@ -513,12 +514,12 @@ RSAC_HD bool lt_common(const double *y, const double *x, LtCommon &L) {
 RSAC_HD bool lt_sign(const LtCommon &L, int sgn, double &w0, double &w1, double *tau) {
     const double a12 = L.a12, a13 = L.a13, b12 = L.b12, b13 = L.b13;
     double s = sgn == 0 ? L.v : -L.v;
-    double w2 = 1.0 / (s * L.v2[0] - L.v1[0]);
-    w0 = (L.v1[1] - s * L.v2[1]) * w2;
-    w1 = (L.v1[2] - s * L.v2[2]) * w2;
-    double a = 1.0 / ((a13 - a12) * w1 * w1 - a12 * b13 * w1 - a12);
-    double b = (a13 * b12 * w1 - a12 * b13 * w0 - 2.0 * w0 * w1 * (a12 - a13)) * a;
-    double c = ((a13 - a12) * w0 * w0 + a13 * b12 * w0 + a13) * a;
+    double w2 = 1.0 / dfma(s, L.v2[0], -L.v1[0]);
+    w0 = dfma(-s, L.v2[1], L.v1[1]) * w2;
+    w1 = dfma(-s, L.v2[2], L.v1[2]) * w2;
+    double a = 1.0 / (dfma(-(a12 * b13), w1, (a13 - a12) * w1 * w1) - a12);
+    double b = dfma(-(2.0 * w0 * w1), a12 - a13, dfma(-(a12 * b13), w0, a13 * b12 * w1)) * a;
+    double c = (dfma(a13 * b12, w0, (a13 - a12) * w0 * w0) + a13) * a;
     if (!(b * b - 4.0 * c >= 0.0)) return false;
     root2real(b, c, tau[0], tau[1]);
     return true;

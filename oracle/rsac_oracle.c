@@ -314,27 +314,27 @@ static void eig_known0(const double A[9], double v1[3], double v2[3], double *e1
     double a00 = A[0], a01 = A[1], a02 = A[2], a11 = A[4], a12 = A[5], a22 = A[8];
     double a01sq = a01 * a01;
     double b = -a00 - a11 - a22;
-    double c = -a01sq - a02 * a02 - a12 * a12 + a00 * (a11 + a22) + a11 * a22;
+    double c = fma(a11, a22, fma(a00, a11 + a22, fma(-a12, a12, fma(-a02, a02, -a01sq))));
     double e1, e2; int ok;
     root2real(b, c, &e1, &e2, &ok);
     if (fabs(e1) < fabs(e2)) { double tmp = e1; e1 = e2; e2 = tmp; }
     double m0011 = -a00 * a11;
-    double pr0 = a01 * a12 - a02 * a11;
-    double pr1 = a01 * a02 - a00 * a12;
+    double pr0 = fma(a01, a12, -(a02 * a11));
+    double pr1 = fma(a01, a02, -(a00 * a12));
     {
         double e = e1;
-        double tmp = 1.0 / (e * (a00 + a11) + m0011 - e * e + a01sq);
-        double q1 = -(e * a02 + pr0) * tmp;
-        double q2 = -(e * a12 + pr1) * tmp;
-        double rn = 1.0 / sqrt(q1 * q1 + q2 * q2 + 1.0);
+        double tmp = 1.0 / (fma(-e, e, fma(e, a00 + a11, m0011)) + a01sq);
+        double q1 = -fma(e, a02, pr0) * tmp;
+        double q2 = -fma(e, a12, pr1) * tmp;
+        double rn = 1.0 / sqrt(fma(q2, q2, q1 * q1) + 1.0);
         v1[0] = q1 * rn; v1[1] = q2 * rn; v1[2] = rn;
     }
     {
         double e = e2;
-        double tmp = 1.0 / (e * (a00 + a11) + m0011 - e * e + a01sq);
-        double q1 = -(e * a02 + pr0) * tmp;
-        double q2 = -(e * a12 + pr1) * tmp;
-        double rn = 1.0 / sqrt(q1 * q1 + q2 * q2 + 1.0);
+        double tmp = 1.0 / (fma(-e, e, fma(e, a00 + a11, m0011)) + a01sq);
+        double q1 = -fma(e, a02, pr0) * tmp;
+        double q2 = -fma(e, a12, pr1) * tmp;
+        double rn = 1.0 / sqrt(fma(q2, q2, q1 * q1) + 1.0);
         v2[0] = q1 * rn; v2[1] = q2 * rn; v2[2] = rn;
     }
     *e1o = e1; *e2o = e2;
@@ -414,10 +414,11 @@ ORC_API int orc_p3p(const double y[9], const double x[9], double Rs[36], double 
     double blob = c12 * c23 * c31 - 1.0;
     double s31 = 1.0 - c31 * c31, s23 = 1.0 - c23 * c23, s12 = 1.0 - c12 * c12;
 
-    double p3 = a13 * (a23 * s31 - a13 * s23);
-    double p2 = 2.0 * blob * a23 * a13 + a13 * (2.0 * a12 + a13) * s23 + a23 * (a23 - a12) * s31;
-    double p1 = a23 * (a13 - a23) * s12 - a12 * a12 * s23 - 2.0 * a12 * (blob * a23 + a13 * s23);
-    double p0 = a12 * (a12 * s23 - a23 * s12);
+    /* fma chains (rsac_math.h lt_common, r05) */
+    double p3 = a13 * fma(a23, s31, -(a13 * s23));
+    double p2 = fma(a23 * (a23 - a12), s31, fma(a13 * (2.0 * a12 + a13), s23, 2.0 * blob * a23 * a13));
+    double p1 = fma(-(2.0 * a12), fma(a13, s23, blob * a23), fma(-(a12 * a12), s23, a23 * (a13 - a23) * s12));
+    double p0 = a12 * fma(a12, s23, -(a23 * s12));
     if (p3 == 0.0 || !isfinite(p3)) return 0;
     double ip3 = 1.0 / p3;
     p2 = p2 * ip3; p1 = p1 * ip3; p0 = p0 * ip3;
@@ -441,12 +442,12 @@ ORC_API int orc_p3p(const double y[9], const double x[9], double Rs[36], double 
     int valid = 0;
     for (int sgn = 0; sgn < 2; ++sgn) {
         double s = sgn == 0 ? v : -v;
-        double w2 = 1.0 / (s * v2[0] - v1[0]);
-        double w0 = (v1[1] - s * v2[1]) * w2;
-        double w1 = (v1[2] - s * v2[2]) * w2;
-        double a = 1.0 / ((a13 - a12) * w1 * w1 - a12 * b13 * w1 - a12);
-        double b = (a13 * b12 * w1 - a12 * b13 * w0 - 2.0 * w0 * w1 * (a12 - a13)) * a;
-        double c = ((a13 - a12) * w0 * w0 + a13 * b12 * w0 + a13) * a;
+        double w2 = 1.0 / fma(s, v2[0], -v1[0]);
+        double w0 = fma(-s, v2[1], v1[1]) * w2;
+        double w1 = fma(-s, v2[2], v1[2]) * w2;
+        double a = 1.0 / (fma(-(a12 * b13), w1, (a13 - a12) * w1 * w1) - a12);
+        double b = fma(-(2.0 * w0 * w1), a12 - a13, fma(-(a12 * b13), w0, a13 * b12 * w1)) * a;
+        double c = (fma(a13 * b12, w0, (a13 - a12) * w0 * w0) + a13) * a;
         if (b * b - 4.0 * c >= 0.0) {
             double tau[2]; int ok;
             root2real(b, c, &tau[0], &tau[1], &ok);
