@@ -42,6 +42,8 @@ def test_pnp_hypotheses_bit_exact_philox(n, outl, seed, H):
     np.testing.assert_array_equal(st, os_)
     np.testing.assert_array_equal(cnt, oc)
     assert _bits_equal(mdl[:, :12], om[:, :12])
+    # the solves leave the validity slot to the status byte; the host probe output fills it in
+    np.testing.assert_array_equal(mdl[:, 12], (st > 0).astype(np.float64))
 
 
 def test_pnp_hypotheses_bit_exact_opencv_subsets():
