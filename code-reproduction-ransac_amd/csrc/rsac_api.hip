@@ -2285,6 +2285,20 @@ int rsac_pnp_epnp(const double *pts3d, const double *pts2d, int32_t n, const dou
     return pnp_epnp_host(b, b + n, b + 2 * n, b + 3 * n, b + 4 * n, m.data(), n, cam, R, t) ? RSAC_OK : RSAC_NO_MODEL;
 }
 
+int rsac_pnp_epnp_minimal(const double *pts3d, const double *pts2d, const double K[9], double R[9], double t[3]) {
+    if (!pts3d || !pts2d || !K || !R || !t) return fail(RSAC_EINVAL, "bad arguments");
+    float X[5], Y[5], Z[5], U[5], V[5];
+    for (int i = 0; i < 5; ++i) {
+        X[i] = (float)pts3d[3 * i];
+        Y[i] = (float)pts3d[3 * i + 1];
+        Z[i] = (float)pts3d[3 * i + 2];
+        U[i] = (float)pts2d[2 * i];
+        V[i] = (float)pts2d[2 * i + 1];
+    }
+    cvq::epnp5_pose(X, Y, Z, U, V, Cam{K[0], K[4], K[2], K[5]}, R, t);
+    return RSAC_OK;
+}
+
 int rsac_homography_fit(const double *src, const double *dst, int32_t n, const uint8_t *mask, double H_out[9]) {
     if (n < 4 || !src || !dst || !H_out) return fail(RSAC_ETOOFEW, "need >= 4 correspondences");
     std::vector<float> soa((size_t)4 * n);

@@ -57,8 +57,8 @@ struct PnpArgs {
     // sample size and minimal solver: 4 = P3P (SOLVEPNP_P3P), 5 = EPnP on 5 points (the
     // default SOLVEPNP_ITERATIVE kernel, RSAC_F_MINIMAL_EPNP5); subsets then hold sample_k indices
     int32_t sample_k = 4;
-    // EPnP-5 minimal solve in three launches (k_epnp5_*): kEpnpRec doubles of stage-1 results and
-    // eigenvectors per hypothesis of one launch (P x H, launch-local positions); required when
+    // EPnP-5 minimal solve in three launches (k_cvepnp5_*): kEpnpRec doubles of M^T M, its sorted
+    // rows and the frame per hypothesis of one launch (P x H, launch-local positions); required when
     // sample_k == 5
     double *epnp = nullptr;
     // RSAC_F_RVEC_ROUNDTRIP: the solve kernels replace each minimal model's R by
@@ -69,8 +69,8 @@ struct PnpArgs {
     int32_t dbg_cell_pts = 0;
 };
 
-// EPnP-5 solve scratch per hypothesis of one launch (doubles): EpnpStage1 (0..63) + 4 eigenvectors
-constexpr int kEpnpRec = 112;
+// EPnP-5 solve scratch per hypothesis of one launch (doubles): rsac_kernels.hip k_cvepnp5_* layout
+constexpr int kEpnpRec = 192;
 
 constexpr int kFrameStride = 16;
 constexpr int kFconstStride = 16;

@@ -860,21 +860,30 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
                      a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
 }
 
-// The default minimal solver of solvePnPRansac (SOLVEPNP_ITERATIVE: 5-point samples, EPnP on the
-// sample; OpenCV solvepnp.cpp PnPRansacCallback::runKernel) in three launches: k_epnp5_a (sample,
-// stage 1: centroid, principal axes, control-point pair sums; one lane per hypothesis), the 12 x 12
-// eigen-decomposition of M^T M (~88 % of the arithmetic) by the round-robin Jacobi of
-// jacobi_eig_rr<12> on 6 lanes per hypothesis (k_epnp5_jacobi6; each lane owns one rotation pair's
-// two rows) or one wave per hypothesis in 2 x 2 blocks for short rounds (k_epnp5_jacobi_b), then
-// k_epnp5_c (L, rho, the three beta estimates and their poses, 3 lanes per hypothesis).  Every element sees jacobi_eig_rr's operations in its
-// order (the rotation formula and skip rule of jrr_rotation), so the records are bit-identical to
-// rsac_math.h pnp_epnp_minimal<5> and the oracle's orc_pnp_minimal_epnp5 (ep_jacobi_rr).  (The
-// round-robin order replaced round 3's cyclic jacobi_eig<12>: EPnP's numerics changed with it, in
-// the oracle and the host EPnP alike.)
-// Per hypothesis a.epnp holds EpnpStage1 (doubles 0..63) and the 4 eigenvectors ut (64..111), at
-// the launch-local position prob * H + hl (the three launches share hyp_begin and H), so the
-// scratch is sized by one launch's P x H (ensure_epnp5), not by the hypothesis records.
-static_assert(sizeof(EpnpStage1) <= 64 * sizeof(double), "EpnpStage1 exceeds its slot");
+// The default minimal solver of solvePnPRansac (SOLVEPNP_ITERATIVE: 5-point samples, each solved
+// by solvePnP(SOLVEPNP_EPNP); [OpenCV 4.x, unvendored] solvepnp.cpp PnPRansacCallback::runKernel)
+// in OpenCV's own operation sequence (rsac_cvepnp.h, the oracle's oracle/cv_epnp.c), three
+// launches:
+//   k_cvepnp5_a    one lane per hypothesis: the sample, undistortPoints' f32 normalised points,
+//                  the control points (cvSVD of PW0^T PW0), the barycentric alphas (cvInvert),
+//                  fill_M + cvMulTransposed: M^T M's upper triangle, alphas and control points
+//                  into the launch-local scratch;
+//   k_cvepnp5_svd  four lanes (a quad) per hypothesis: cvSVD(M^T M)'s JacobiSVDImpl_ -- cyclic
+//                  pair order, every sum over k = 0..11 left to right: lane q holds elements
+//                  3q .. 3q + 2 of all 12 rows, a sum runs 3 additions on lane 0, moves to lane 1
+//                  by DPP, and so on (the sequential order, ~ the latency of one lane), the
+//                  rotation (hypot form) computed by all four; then the row norms, the selection
+//                  sort and the normalisation of the four smallest rows (a zero row's random
+//                  fill in memory, cvq_fill_rows);
+//   k_cvepnp5_c    three lanes per hypothesis, one beta estimate each (find_betas_approx_1..3 +
+//                  gauss_newton + compute_R_and_t), epnp::compute_pose's pick, the Rodrigues
+//                  round trip of the (rvec, tvec) model, the records.
+// Per hypothesis a.epnp holds kEpnpRec doubles at the launch-local position prob * H + hl:
+// [0, 78) M^T M's upper triangle (stage 1) / [0, 144) the 12 rows and [144, 156) their norms
+// (the rare fill path) / [0, 48) the sorted rows 8 .. 11, normalised (stage 2); [156, 176) the
+// alphas and [176, 188) the control points (stage 1).
+constexpr int kCvRows = 0, kCvW = 144, kCvAlpha = 156, kCvCws = 176;
+static_assert(kCvCws + 12 <= kEpnpRec, "cv EPnP scratch");
 
 // the sample of hypothesis rec (OpenCV subsets or Philox), status 1 drawn / -1 not
 __device__ __forceinline__ int8_t epnp5_sample(const PnpArgs &a, int64_t rec, int64_t h, int n, int32_t (&idx)[5]) {
@@ -887,7 +896,7 @@ __device__ __forceinline__ int8_t epnp5_sample(const PnpArgs &a, int64_t rec, in
     rng.init(a.seed, 0u, (uint64_t)(a.rng_base + h));
     return (n >= 5 && rng.subset<5>(n, idx) == 0) ? 1 : -1;
 }
-// the sample's points (a gather; stage 3 issues it before its beta arithmetic, which hides it)
+// the sample's points (solvePnPRansac's CV_32F copies)
 struct Epnp5Pts {
     float X[5], Y[5], Z[5], U[5], V[5];
 };
@@ -898,21 +907,9 @@ __device__ __forceinline__ void epnp5_gather(const PnpArgs &a, int64_t p0, const
         q.X[j] = a.X[i]; q.Y[j] = a.Y[i]; q.Z[j] = a.Z[i]; q.U[j] = a.U[i]; q.V[j] = a.V[i];
     }
 }
-// pnp_epnp_minimal<5>'s reducer: the sample centred on its first point
-__device__ __forceinline__ void epnp5_reducer(const Epnp5Pts &q, MinimalEpnpReducer<5> &red, double (&c)[3]) {
-    c[0] = (double)q.X[0]; c[1] = (double)q.Y[0]; c[2] = (double)q.Z[0];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        red.X[i] = (double)q.X[i] - c[0];
-        red.Y[i] = (double)q.Y[i] - c[1];
-        red.Z[i] = (double)q.Z[i] - c[2];
-        red.u[i] = (double)q.U[i];
-        red.v[i] = (double)q.V[i];
-    }
-}
 
-// 1 of 3: sample, stage 1 (centroid, principal axes, the control-point pair sums)
-__global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, int32_t H) {
+// 1 of 3: sample, epnp's set-up through M^T M
+__global__ __launch_bounds__(256) void k_cvepnp5_a(PnpArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
     const int hl = blockIdx.x * blockDim.x + threadIdx.x;
     if (hl == 0 && prob == 0) {
@@ -925,448 +922,217 @@ __global__ __launch_bounds__(256) void k_epnp5_a(PnpArgs a, int64_t hyp_begin, i
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
     int32_t idx[5];
     const int8_t st = epnp5_sample(a, rec, h, n, idx);
-    EpnpStage1 s1;
-    s1.ok = 0.0;
-    s1.n = 0.0;
     if (st > 0) {
         Epnp5Pts q;
         epnp5_gather(a, p0, idx, q);
-        MinimalEpnpReducer<5> red;
-        double c[3];
-        epnp5_reducer(q, red, c);
         const double *cm = a.cams + 4 * prob;
-        epnp_stage1(red, Cam{cm[0], cm[1], cm[2], cm[3]}, s1);
+        cvq::Epnp5 e;
+        cvq::epnp5_init(q.X, q.Y, q.Z, q.U, q.V, Cam{cm[0], cm[1], cm[2], cm[3]}, e);
+        cvq::epnp5_frame(e);
+        double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;
+        cvq::epnp5_mtm(e, E);
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) E[kCvAlpha + 4 * i + j] = e.alphas[i][j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) E[kCvCws + 3 * i + j] = e.cws[i][j];
     }
     a.status[rec] = st;
-    *reinterpret_cast<EpnpStage1 *>(a.epnp + ((int64_t)prob * H + hl) * kEpnpRec) = s1;
 }
 
-// 2 of 3: M^T M's eigenvectors by the round-robin Jacobi of jacobi_eig_rr<12>: k_epnp5_jacobi6 for
-// long rounds (6 lanes per hypothesis, below) and k_epnp5_jacobi_b for short ones (one wave per
-// hypothesis in 2 x 2 blocks).  (r05's 12-lane row form, lane j holding rows j of A and V and the
-// step-start matrix mirrored in LDS, was replaced by the pair-owned form: profiles/r05/probes.md.)
-// LDS row stride of the mirrored matrices (doubles): 13, not 12, so the 12 rows of one column (the
-// A and V rows of the latency form) fall in distinct banks: 2-way at most where 12 gave 6- to 8-way
-// (SQ_LDS_BANK_CONFLICT, profiles/r04_epnp_pmc.json)
-constexpr int kEpR = 13;
-RSAC_HD constexpr int jrr_p(int r, int i) {
-    return jrr_pos(12, r, i) < jrr_pos(12, r, 11 - i) ? jrr_pos(12, r, i) : jrr_pos(12, r, 11 - i);
+// 2 of 3: the 12 x 12 JacobiSVD on a quad per hypothesis
+// DPP within a quad: lane q takes lane q - 1's value (lane 0 its own) / every lane takes lane 3's
+__device__ __forceinline__ double quad_dpp(double v, int ctrl) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    int rlo, rhi;
+    if (ctrl == 0x90) {
+        rlo = __builtin_amdgcn_mov_dpp(lo, 0x90, 0xF, 0xF, false);
+        rhi = __builtin_amdgcn_mov_dpp(hi, 0x90, 0xF, 0xF, false);
+    } else {
+        rlo = __builtin_amdgcn_mov_dpp(lo, 0xFF, 0xF, 0xF, false);
+        rhi = __builtin_amdgcn_mov_dpp(hi, 0xFF, 0xF, 0xF, false);
+    }
+    return __hiloint2double(rhi, rlo);
 }
-RSAC_HD constexpr int jrr_q(int r, int i) {
-    return jrr_pos(12, r, i) < jrr_pos(12, r, 11 - i) ? jrr_pos(12, r, 11 - i) : jrr_pos(12, r, i);
-}
-__device__ __forceinline__ void ep_wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// sum over k = 0..11 of x[k] left to right, from +0, where lane q of the quad holds x[3q .. 3q + 2];
+// every lane returns the sum
+__device__ __forceinline__ double quad_sum(double x0, double x1, double x2) {
+    double s = 0.0;
+    s = s + x0; s = s + x1; s = s + x2;
+#pragma unroll
+    for (int hop = 0; hop < 3; ++hop) {
+        s = quad_dpp(s, 0x90);
+        s = s + x0; s = s + x1; s = s + x2;
+    }
+    return quad_dpp(s, 0xFF);
 }
 
-// position m of step R's circle (jrr_pos(12, R, m)) for a position known only at run time
-template <int R>
-__device__ __forceinline__ int jrr_pos_r(int m) {
-    int v = m - 1 + R;  // 0 .. 20 for m >= 1
-    v = v >= 11 ? v - 11 : v;
-    return m == 0 ? 0 : 1 + v;
+// JacobiSVDImpl_'s tail in memory (one lane, the rare case of a row norm <= DBL_MIN): the selection
+// sort of the 12 rows by their norms and the normalisation of every row, a zero one replaced by
+// RNG(0x12345678)'s random direction projected off the earlier rows (rsac_cvepnp.h jacobi_svd);
+// rows 8 .. 11 end at [0, 48)
+__device__ __attribute__((noinline)) void cvq_fill_rows(double *E) {
+    double *A = E + kCvRows, *W = E + kCvW;
+    for (int i = 0; i < 11; ++i) {
+        int j = i;
+        for (int k = i + 1; k < 12; ++k)
+            if (W[j] < W[k]) j = k;
+        if (i != j) {
+            double t = W[i]; W[i] = W[j]; W[j] = t;
+            for (int k = 0; k < 12; ++k) { t = A[12 * i + k]; A[12 * i + k] = A[12 * j + k]; A[12 * j + k] = t; }
+        }
+    }
+    uint64_t rng = 0x12345678;
+    for (int i = 0; i < 12; ++i) {
+        double sd = W[i];
+        for (int ii = 0; ii < 100 && sd <= cvq::kDblMin; ii++) {
+            const double val0 = 1. / 12;
+            for (int k = 0; k < 12; ++k) A[12 * i + k] = (cvq::rng_next(rng) & 256) != 0 ? val0 : -val0;
+            for (int it = 0; it < 2; ++it)
+                for (int j = 0; j < i; ++j) {
+                    sd = 0;
+                    for (int k = 0; k < 12; ++k) sd += A[12 * i + k] * A[12 * j + k];
+                    double asum = 0;
+                    for (int k = 0; k < 12; ++k) {
+                        const double t = A[12 * i + k] - sd * A[12 * j + k];
+                        A[12 * i + k] = t;
+                        asum += dabs(t);
+                    }
+                    asum = asum > cvq::kSvdEps * 100 ? 1 / asum : 0;
+                    for (int k = 0; k < 12; ++k) A[12 * i + k] *= asum;
+                }
+            sd = 0;
+            for (int k = 0; k < 12; ++k) sd += A[12 * i + k] * A[12 * i + k];
+            sd = dsqrt(sd);
+        }
+        const double s = sd > cvq::kDblMin ? 1 / sd : 0.;
+        for (int k = 0; k < 12; ++k) A[12 * i + k] *= s;
+    }
+    for (int k = 0; k < 48; ++k) E[k] = A[96 + k];
 }
-// The throughput form by rotation pairs (r05): 6 lanes per hypothesis, 10 per wave (lanes 60..63
-// idle).  Lane i owns pair i of every step, i.e. the rows at positions i and 11 - i of the circle
-// (jrr_pos: at step r the indices pos(r, i), pos(r, 11 - i)), and rows 2i, 2i + 1 of V.  A step:
-//   params:  the pair's app, aqq, apq, read where the lane's two rows were stored;
-//   post:    cs, sn to the group's 12 slots; every lane reads all 12;
-//   columns: the 6 pairs' column rotations on the lane's two A rows and two V rows (static indices);
-//   rows:    the row rotation of its own pair (both rows in the lane: no exchange);
-//   pass:    the two rows to the wave's lane-linear exchange buffer X[t][k][lane] (one wave-wide
-//            write per element, no bank conflicts), then the next step's two rows from the lanes
-//            that hold them: the circle moves position m + 1 to m, so lane i takes slot 0 from lane
-//            i + 1's slot 0 and slot 1 from lane i - 1's slot 1 (lane 0 keeps index 0 and takes
-//            lane 1's slot 0; lane 5 takes its own slot 1 and lane 4's slot 1), whatever the step.
-// Each element sees jacobi_eig_rr's operations in its order (the same bits as k_epnp5_jacobi_b and
-// the oracle's ep_jacobi_rr).  Per hypothesis and step 6 lanes move 2 rows each through LDS where the
-// 12-lane form moves 12 rows twice; the VALU work is the same.  (A row-indexed mirror, r05's first
-// form, spent a third of its LDS time in bank conflicts: profiles/r05/probes.md.)
-constexpr int kJ6W = 10;              // hypotheses per wave
-constexpr int kJ6B = 256 / 64 * kJ6W;  // per 256-thread block
-// doubles per slot array of a wave's X.  +2: slot 1 sits two doubles over, where the reads that
-// take it land on the positions no slot-0 read of the same 16-lane bank group uses (lane 5 reads
-// its own slot 1 at 6g + 7, the next group's hole at 6g + 6 + 1; the second read's sources become
-// 6g + 1 .. 6g + 6, consecutive).  +1 made both reads 2-way conflicted (SQ_LDS_BANK_CONFLICT 24 M
-// cycles per 20k launch, r05).
-constexpr int kJ6X = 12 * 64 + 2;
-struct EpnpJ6Lds {
-    double X[4][2 * kJ6X];  // per wave: X[t][k][lane] at t * kJ6X + 64 k + lane
-    // pair i: cs at 2i, sn at 2i + 1; the sweep test's row terms at the sweep's start.  Rows of
-    // 25 doubles (odd): the wave's hypotheses read slot j at distinct banks (24 put every other
-    // hypothesis on the same bank)
-    double cs[kJ6B][25];
-    int ord[kJ6B][12];
-};
-// where slot t's row of lane i (of group base g6 = 6 gw) goes at the next step: (source lane, slot)
-__device__ __forceinline__ void j6_sources(int i, int g6, int &l0, int &t0, int &l1, int &t1) {
-    l0 = i == 0 ? g6 : i == 5 ? g6 + 5 : g6 + i + 1;
-    t0 = i == 5 ? 1 : 0;
-    l1 = i == 0 ? g6 + 1 : g6 + i - 1;
-    t1 = i == 0 ? 0 : 1;
+
+// rotation (i = row B[0], j = row B[J]) of one cyclic sweep; the rows live in a register file rotated
+// by one row after each i (B[0] = row i, B[1 .. 11 - i] = rows i + 1 .. 11)
+template <int J>
+__device__ __forceinline__ void cvsvd_pair(double (&B)[12][3], double (&W)[12], bool &changed) {
+    double p = quad_sum(B[0][0] * B[J][0], B[0][1] * B[J][1], B[0][2] * B[J][2]);
+    const double a = W[0], b = W[J];
+    if (dabs(p) <= cvq::kSvdEps * dsqrt(a * b)) return;  // quad-uniform: p, a, b are the quad's
+    p *= 2;
+    double c, s;
+    cvq::svd_rotation(p, a, b, c, s);
+    double t0[3], t1[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        t0[e] = c * B[0][e] + s * B[J][e];
+        t1[e] = -s * B[0][e] + c * B[J][e];
+        B[0][e] = t0[e];
+        B[J][e] = t1[e];
+    }
+    W[0] = quad_sum(t0[0] * t0[0], t0[1] * t0[1], t0[2] * t0[2]);
+    W[J] = quad_sum(t1[0] * t1[0], t1[1] * t1[1], t1[2] * t1[2]);
+    changed = true;
 }
-// (s_l0, s_t0), (s_l1, s_t1): where the lane's two rows are stored at the step's start (the circle's
-// pattern, or the lane's own slots before the first exchange); (l0, t0), (l1, t1): the pattern
-template <int R>
-__device__ __forceinline__ void epnp_j6_step(int sweep, int i, int lane, int s_l0, int s_t0, int s_l1, int s_t1,
-                                             int l0, int t0, int l1, int t1, double (&a0)[12], double (&a1)[12],
-                                             double (&v0)[12], double (&v1)[12], double *X, double *LC) {
-    const int i0 = jrr_pos_r<R>(i), i1 = jrr_pos_r<R>(11 - i);
-    const bool f = i0 < i1;  // slot 0 holds row p
-    const int p = f ? i0 : i1, q = f ? i1 : i0;
-    // the step-start values app, aqq, apq where the lane's rows are stored
-    const int lp = f ? s_l0 : s_l1, tp = f ? s_t0 : s_t1, lq = f ? s_l1 : s_l0, tq = f ? s_t1 : s_t0;
-    double cs = 1.0, sn = 0.0;  // a skipped pair: the identity rotation (jacobi_eig_rr)
-    (void)jrr_rotation(sweep, X[tp * kJ6X + 64 * p + lp], X[tq * kJ6X + 64 * q + lq], X[tp * kJ6X + 64 * q + lp],
-                       cs, sn);
-    LC[2 * i] = cs;
-    LC[2 * i + 1] = sn;
-    ep_wave_sync();
-    double c6[6], s6[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        c6[k] = LC[2 * k];
-        s6[k] = LC[2 * k + 1];
-    }
-    // columns (every pair; static indices) of the two A rows and the two V rows
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        const int P = jrr_p(R, k), Q = jrr_q(R, k);
-        const double c = c6[k], s = s6[k];
-        double x, y;
-        x = a0[P]; y = a0[Q]; a0[P] = jrr_lo(c, s, x, y); a0[Q] = jrr_hi(c, s, x, y);
-        x = a1[P]; y = a1[Q]; a1[P] = jrr_lo(c, s, x, y); a1[Q] = jrr_hi(c, s, x, y);
-        x = v0[P]; y = v0[Q]; v0[P] = jrr_lo(c, s, x, y); v0[Q] = jrr_hi(c, s, x, y);
-        x = v1[P]; y = v1[Q]; v1[P] = jrr_lo(c, s, x, y); v1[Q] = jrr_hi(c, s, x, y);
-    }
-    // rows of the lane's own pair: row p <- jrr_lo, row q <- jrr_hi, i.e. fma(cs, own, x other) with
-    // x = -sn on row p, +sn on row q (x other = -(sn other) exactly: the same bits), straight to
-    // the exchange buffer
-    const double x0 = f ? -sn : sn, x1 = f ? sn : -sn;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        X[64 * k + lane] = dfma(cs, a0[k], x0 * a1[k]);
-        X[kJ6X + 64 * k + lane] = dfma(cs, a1[k], x1 * a0[k]);
-    }
-    ep_wave_sync();
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        a0[k] = X[t0 * kJ6X + 64 * k + l0];
-        a1[k] = X[t1 * kJ6X + 64 * k + l1];
-    }
-    // V's rotations complete inside the step (left free, the scheduler sinks them and holds every
-    // step's cs, sn live)
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        asm volatile("" : "+v"(v0[k]));
-        asm volatile("" : "+v"(v1[k]));
+template <int J>
+__device__ __forceinline__ void cvsvd_row(double (&B)[12][3], double (&W)[12], bool &changed, int last) {
+    if constexpr (J <= 11) {
+        if (J <= last) cvsvd_pair<J>(B, W, changed);
+        cvsvd_row<J + 1>(B, W, changed, last);
     }
 }
-template <int R>
-__device__ __forceinline__ void epnp_j6_sweep(int sweep, int i, int lane, int l0, int t0, int l1, int t1,
-                                              double (&a0)[12], double (&a1)[12], double (&v0)[12],
-                                              double (&v1)[12], double *X, double *LC) {
-    if constexpr (R < 11) {
-        epnp_j6_step<R>(sweep, i, lane, l0, t0, l1, t1, l0, t0, l1, t1, a0, a1, v0, v1, X, LC);
-        epnp_j6_sweep<R + 1>(sweep, i, lane, l0, t0, l1, t1, a0, a1, v0, v1, X, LC);
-    }
-}
-// a row's sweep-test terms (jacobi_eig_rr's): A_rr^2 and sum_{q > r} A_rq^2 in q order
-__device__ __forceinline__ void j6_row_terms(const double (&a)[12], int r, double &dd, double &rp) {
-    double d = 0.0;
-    rp = 0.0;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        d = k == r ? a[k] : d;
-        rp = k > r ? rp + a[k] * a[k] : rp;
-    }
-    dd = d * d;
-}
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_epnp5_jacobi6(
-    PnpArgs a, int64_t hyp_begin, int32_t H) {
-    __shared__ EpnpJ6Lds L;
+
+__global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begin, int32_t H) {
     const int prob = blockIdx.y;
-    const int lane = threadIdx.x & 63, gw = lane / 6, i = lane - 6 * gw;
-    const bool slot = gw < kJ6W;  // lanes 60..63: no group
-    const int hb = (int)(threadIdx.x >> 6) * kJ6W + (slot ? gw : 0);
-    const int hl = (int)blockIdx.x * kJ6B + hb;
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int hl = gt >> 2, q = gt & 3;
+    const bool live = hl < H;  // a quad shares its hypothesis: every branch below is quad-uniform
     const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
-    double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;  // launch-local scratch
-    const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
-    const bool live = slot && hl < H && a.status[rec] > 0 && s1->ok != 0.0;
-    bool run = live;
-    double *X = L.X[threadIdx.x >> 6], *LC = L.cs[hb];
-    int l0, t0, l1, t1;  // where the next step's rows come from (the circle's fixed pattern)
-    j6_sources(i, 6 * gw, l0, t0, l1, t1);
-    double a0[12], a1[12], v0[12], v1[12];
-    // rows 2i, 2i + 1 of V = I; rows pos(0, i), pos(0, 11 - i) of epnp_mtm's matrix
-    const int r0 = jrr_pos_r<0>(i), r1 = jrr_pos_r<0>(11 - i);
+    if (!(live && a.status[rec] > 0)) return;
+    double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;
+    // At = (M^T M)^T = M^T M: element (r, 3q + e) from the upper triangle
+    double B[12][3], W[12];
 #pragma unroll
-    for (int c = 0; c < 12; ++c) {
-        v0[c] = c == 2 * i ? 1.0 : 0.0;
-        v1[c] = c == 2 * i + 1 ? 1.0 : 0.0;
-        a0[c] = 0.0;
-        a1[c] = 0.0;
-    }
-    if (run) {
-        const double *cm = a.cams + 4 * prob;
-        const double fx = cm[0], fy = cm[1];
-        constexpr int first[4] = {0, 4, 7, 9};  // pair (x <= y) -> sum block x's first + (y - x)
-        auto build = [&](int jr, double (&row)[12]) {  // row jr = 3 ib + pp
-            const int ib = jr / 3, pp = jr - 3 * ib;
+    for (int r = 0; r < 12; ++r)
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const int lo = min(ib, jj), hi = max(ib, jj);
-                const double *ps = s1->pairs + 4 * (first[lo] + hi - lo);
-                const double s0 = ps[0], su = ps[1], sv = ps[2], sw = ps[3];
-                const double blk[9] = {fx * fx * s0, 0.0, fx * su, 0.0, fy * fy * s0, fy * sv, fx * su, fy * sv, sw};
+        for (int e = 0; e < 3; ++e) {
+            const int c = 3 * q + e, lo = r < c ? r : c, hi = r < c ? c : r;
+            B[r][e] = E[lo * 12 - lo * (lo - 1) / 2 + (hi - lo)];
+        }
 #pragma unroll
-                for (int rr = 0; rr < 3; ++rr) row[3 * jj + rr] = pp == 0 ? blk[rr] : pp == 1 ? blk[3 + rr] : blk[6 + rr];
+    for (int r = 0; r < 12; ++r) W[r] = quad_sum(B[r][0] * B[r][0], B[r][1] * B[r][1], B[r][2] * B[r][2]);
+    for (int iter = 0; iter < 30; ++iter) {
+        bool changed = false;
+        for (int i = 0; i < 12; ++i) {
+            cvsvd_row<1>(B, W, changed, 11 - i);
+            // rotate the register file by one row: row i parks at the end
+            double b0[3] = {B[0][0], B[0][1], B[0][2]}, w0 = W[0];
+#pragma unroll
+            for (int r = 0; r < 11; ++r) {
+#pragma unroll
+                for (int e = 0; e < 3; ++e) B[r][e] = B[r + 1][e];
+                W[r] = W[r + 1];
             }
-        };
-        build(r0, a0);
-        build(r1, a1);
-    }
-    // the first step's parameters are read where the rows are: the lane's own slots at first (the
-    // step's pattern takes over after the first exchange)
-    int s_l0 = lane, s_t0 = 0, s_l1 = lane, s_t1 = 1;
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        X[64 * k + lane] = a0[k];
-        X[kJ6X + 64 * k + lane] = a1[k];
-    }
-    ep_wave_sync();
-    for (int sweep = 0; sweep < 60; ++sweep) {
-        // the sweep test: the lane's two rows' terms (a0, a1 hold rows pos(0, i), pos(0, 11 - i)),
-        // every lane of the group adds the 12 rows' in row order
-        if (run) {
-            double d0, p0, d1, p1;
-            j6_row_terms(a0, r0, d0, p0);
-            j6_row_terms(a1, r1, d1, p1);
-            LC[2 * r0] = d0;
-            LC[2 * r0 + 1] = p0;
-            LC[2 * r1] = d1;
-            LC[2 * r1 + 1] = p1;
+            for (int e = 0; e < 3; ++e) B[11][e] = b0[e];
+            W[11] = w0;
         }
-        ep_wave_sync();
-        if (run) {
-            double off = 0.0, diag = 0.0;
+        if (!changed) break;
+    }
+    // the row norms, the selection sort (descending, first maximum), the normalisation
 #pragma unroll
-            for (int r = 0; r < 12; ++r) {
-                diag = diag + LC[2 * r];
-                off = off + LC[2 * r + 1];
+    for (int r = 0; r < 12; ++r) W[r] = dsqrt(quad_sum(B[r][0] * B[r][0], B[r][1] * B[r][1], B[r][2] * B[r][2]));
+    int perm[12];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) perm[r] = r;
+#pragma unroll
+    for (int i = 0; i < 11; ++i) {
+        int j = i;
+#pragma unroll
+        for (int k = i + 1; k < 12; ++k)
+            if (W[j] < W[k]) j = k;
+#pragma unroll
+        for (int k = i + 1; k < 12; ++k)
+            if (k == j) {
+                const double tw = W[i]; W[i] = W[k]; W[k] = tw;
+                const int tp = perm[i]; perm[i] = perm[k]; perm[k] = tp;
             }
-            if (!(off > 1e-32 * diag)) run = false;
-        }
-        if (__ballot(run) == 0) break;
-        ep_wave_sync();  // every lane has read the test's terms before the first step posts
-        if (run) {
-            // step 0 reads its parameters at (s_l, s_t); the sweep's later steps at the pattern
-            epnp_j6_step<0>(sweep, i, lane, s_l0, s_t0, s_l1, s_t1, l0, t0, l1, t1, a0, a1, v0, v1, X, LC);
-            epnp_j6_sweep<1>(sweep, i, lane, l0, t0, l1, t1, a0, a1, v0, v1, X, LC);
-        }
-        s_l0 = l0; s_t0 = t0; s_l1 = l1; s_t1 = t1;
     }
-    if (!live) return;
-    // eig_order_desc<12> on the diagonal (each lane posts its two rows' diagonal entries), then V's rows
-    {
-        double d0, p0, d1, p1;
-        j6_row_terms(a0, r0, d0, p0);
-        j6_row_terms(a1, r1, d1, p1);
-        (void)p0;
-        (void)p1;
-        double dg0 = 0.0, dg1 = 0.0;
+    if (W[11] > cvq::kDblMin) {
+        // rows 8 .. 11 (every row's norm > DBL_MIN: no random fill anywhere), times 1 / norm
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            dg0 = k == r0 ? a0[k] : dg0;
-            dg1 = k == r1 ? a1[k] : dg1;
-        }
-        LC[r0] = dg0;
-        LC[r1] = dg1;
-    }
-    ep_wave_sync();
-    int *O = L.ord[hb];
-    if (i == 0) {
-        for (int k = 0; k < 12; ++k) O[k] = k;
-        for (int k = 1; k < 12; ++k) {
-            const int kk = O[k];
-            const double dk = LC[kk];
-            int jx = k - 1;
-            while (jx >= 0 && LC[O[jx]] < dk) {
-                O[jx + 1] = O[jx];
-                --jx;
-            }
-            O[jx + 1] = kk;
-        }
-    }
-    ep_wave_sync();
-    // V's rows through the wave's exchange buffer: row r of the group at X + 12 * 12 * gw + 12 r
-    double *VX = X + 144 * gw;
+        for (int p = 8; p < 12; ++p) {
+            const double inv = 1 / W[p];
+            double v[3] = {0, 0, 0};
 #pragma unroll
-    for (int c = 0; c < 12; ++c) {
-        VX[12 * (2 * i) + c] = v0[c];
-        VX[12 * (2 * i + 1) + c] = v1[c];
-    }
-    ep_wave_sync();
+            for (int r = 0; r < 12; ++r)
+                if (perm[p] == r) {
+                    v[0] = B[r][0]; v[1] = B[r][1]; v[2] = B[r][2];
+                }
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {  // ut[ii][j] = V[j][o[11 - ii]], element 8 i + t of 48
-        const int e = 8 * i + t, ii = e / 12, j = e - 12 * ii;
-        E[64 + e] = VX[12 * j + O[11 - ii]];
+            for (int e = 0; e < 3; ++e) E[(p - 8) * 12 + 3 * q + e] = v[e] * inv;
+        }
+        return;
     }
+    // a row of zero norm: the rows and their (unsorted) norms to memory, lane 0 finishes in memory
+#pragma unroll
+    for (int r = 0; r < 12; ++r)
+#pragma unroll
+        for (int e = 0; e < 3; ++e) E[kCvRows + 12 * r + 3 * q + e] = B[r][e];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) {
+        const double wr = dsqrt(quad_sum(B[r][0] * B[r][0], B[r][1] * B[r][1], B[r][2] * B[r][2]));  // every lane: DPP
+        if (q == 0) E[kCvW + r] = wr;
+    }
+    __threadfence();
+    if (q == 0) cvq_fill_rows(E);
 }
 
-// The latency form of the Jacobi for short rounds (an adaptive run's first 256 hypotheses):
-// one wave per hypothesis in 2 x 2 blocks.  In step r the 12 indices form the 6 pairs of
-// jacobi_eig_rr; lane (a, b) < 36 holds A's block at rows pair a x columns pair b and V's block at
-// rows 2a, 2a + 1 x columns pair b.  A step: the diagonal lanes (a, a) form their pair's cs, sn from
-// their own block (app, apq, aqq) and post them; every lane rotates its A block's columns by pair b
-// then its rows by pair a, and its V block's columns by pair b (the operations jacobi_eig_rr applies
-// to those elements, in its order: the same bits); the blocks go to the LDS mirrors of A and V, from
-// which every lane takes the next step's blocks.  Per step one chain of the rotation parameters,
-// 2 wave synchronisations and one round trip of 8 doubles per lane, where the half-row form (r04)
-// spent 4 synchronisations, 3 round trips and 196 instructions.  The sweep test: lanes 0..11 each
-// form their row's partial sums from the mirror (jacobi_eig_rr's order), every lane adds the 12 in
-// row order.
-struct EpnpJacLdsB {
-    double A[4][12 * kEpR];
-    double V[4][12 * kEpR];
-    double cs[4][14];    // pair i: cs at 2i, sn at 2i + 1; 12, 13: the off-diagonal lanes' spare slot
-    double part[4][24];  // row p: A_pp^2 at 2p, sum_{q > p} A_pq^2 at 2p + 1
-    int ord[4][12];
-};
-// Step R of the block form, branch-free: lanes 36..63 repeat lanes 0..27's blocks (the same values
-// to the same addresses), every lane forms its row pair's rotation and only the diagonal lanes'
-// land in LC (the others in a spare slot), so the wave runs one instruction stream.
-template <int R>
-__device__ __forceinline__ void epnp_blk_step(int sweep, int ba, int bb, int vr0, double *LA, double *LV,
-                                              double *LC) {
-    int pa = jrr_pos_r<R>(ba), qa = jrr_pos_r<R>(11 - ba), pb = jrr_pos_r<R>(bb), qb = jrr_pos_r<R>(11 - bb);
-    if (pa > qa) { const int x = pa; pa = qa; qa = x; }
-    if (pb > qb) { const int x = pb; pb = qb; qb = x; }
-    double *A0 = LA + kEpR * pa, *A1 = LA + kEpR * qa;
-    double *V0 = LV + vr0, *V1 = LV + vr0 + kEpR;
-    const double x00 = A0[pb], x01 = A0[qb], x10 = A1[pb], x11 = A1[qb];
-    const double v00 = V0[pb], v01 = V0[qb], v10 = V1[pb], v11 = V1[qb];
-    double cs, sn;  // meaningful on the diagonal lanes (ba == bb: app, apq, aqq of pair ba)
-    jrr_rotation_sel(sweep, x00, x11, x01, cs, sn);
-    const int slot = ba == bb ? 2 * ba : 12;
-    LC[slot] = cs;
-    LC[slot + 1] = sn;
-    ep_wave_sync();
-    const double ca = LC[2 * ba], sa = LC[2 * ba + 1], cb = LC[2 * bb], sb = LC[2 * bb + 1];
-    // columns (pair b) of rows pa, qa; then rows (pair a) of the column-rotated block
-    const double y00 = jrr_lo(cb, sb, x00, x01), y01 = jrr_hi(cb, sb, x00, x01);
-    const double y10 = jrr_lo(cb, sb, x10, x11), y11 = jrr_hi(cb, sb, x10, x11);
-    A0[pb] = jrr_lo(ca, sa, y00, y10);
-    A1[pb] = jrr_hi(ca, sa, y00, y10);
-    A0[qb] = jrr_lo(ca, sa, y01, y11);
-    A1[qb] = jrr_hi(ca, sa, y01, y11);
-    // V's columns (pair b)
-    V0[pb] = jrr_lo(cb, sb, v00, v01);
-    V0[qb] = jrr_hi(cb, sb, v00, v01);
-    V1[pb] = jrr_lo(cb, sb, v10, v11);
-    V1[qb] = jrr_hi(cb, sb, v10, v11);
-    ep_wave_sync();  // the mirrors hold the step's result; LC may be rewritten
-}
-template <int R>
-__device__ __forceinline__ void epnp_blk_sweep(int sweep, int ba, int bb, int vr0, double *LA, double *LV,
-                                               double *LC) {
-    if constexpr (R < 11) {
-        epnp_blk_step<R>(sweep, ba, bb, vr0, LA, LV, LC);
-        epnp_blk_sweep<R + 1>(sweep, ba, bb, vr0, LA, LV, LC);
-    }
-}
-__global__ __launch_bounds__(256) void k_epnp5_jacobi_b(PnpArgs a, int64_t hyp_begin, int32_t H) {
-    __shared__ EpnpJacLdsB L;
-    const int prob = blockIdx.y;
-    const int lane = threadIdx.x & 63, hb = threadIdx.x >> 6;
-    const int hl = (int)((blockIdx.x * 256u + threadIdx.x) >> 6);
-    const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
-    double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;  // launch-local scratch
-    const EpnpStage1 *s1 = reinterpret_cast<const EpnpStage1 *>(E);
-    const bool live = hl < H && a.status[rec] > 0 && s1->ok != 0.0;  // wave-uniform
-    if (!live) return;
-    double *LA = L.A[hb], *LV = L.V[hb], *LP = L.part[hb];
-    if (lane < 12) {  // row `lane` of epnp_mtm's matrix, and of V = I
-        const int jr = lane;
-        const double *cm = a.cams + 4 * prob;
-        const double fx = cm[0], fy = cm[1];
-        const int i = jr / 3, pp = jr - 3 * i;
-        constexpr int first[4] = {0, 4, 7, 9};  // pair (x <= y) -> sum block x's first + (y - x)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int lo = min(i, jj), hi = max(i, jj);
-            const double *ps = s1->pairs + 4 * (first[lo] + hi - lo);
-            const double s0 = ps[0], su = ps[1], sv = ps[2], sw = ps[3];
-            const double blk[9] = {fx * fx * s0, 0.0, fx * su, 0.0, fy * fy * s0, fy * sv, fx * su, fy * sv, sw};
-#pragma unroll
-            for (int rr = 0; rr < 3; ++rr)
-                LA[kEpR * jr + 3 * jj + rr] = pp == 0 ? blk[rr] : pp == 1 ? blk[3 + rr] : blk[6 + rr];
-        }
-#pragma unroll
-        for (int c = 0; c < 12; ++c) LV[kEpR * jr + c] = c == jr ? 1.0 : 0.0;
-    }
-    const int bl = lane < 36 ? lane : lane - 36;  // lanes 36..63 repeat blocks 0..27
-    const int ba = bl / 6, bb = bl - 6 * (bl / 6), vr0 = kEpR * 2 * ba;
-    const int tr = lane < 12 ? lane : lane - 12 * (lane / 12);  // the sweep test's row (repeated)
-    ep_wave_sync();
-    for (int sweep = 0; sweep < 60; ++sweep) {
-        {  // row tr's terms of the sweep test, from the mirror
-            double rw[12];
-#pragma unroll
-            for (int q = 0; q < 12; ++q) rw[q] = LA[kEpR * tr + q];
-            double dp = 0.0;
-#pragma unroll
-            for (int q = 0; q < 12; ++q) dp = q == tr ? rw[q] : dp;
-            double rp = 0.0;
-#pragma unroll
-            for (int q = 1; q < 12; ++q)
-                if (q > tr) rp = rp + rw[q] * rw[q];
-            LP[2 * tr] = dp * dp;
-            LP[2 * tr + 1] = rp;
-        }
-        ep_wave_sync();
-        double off = 0.0, diag = 0.0;  // every lane, rows in order: a wave-uniform verdict
-#pragma unroll
-        for (int p = 0; p < 12; ++p) {
-            diag = diag + LP[2 * p];
-            off = off + LP[2 * p + 1];
-        }
-        if (!(off > 1e-32 * diag)) break;
-        epnp_blk_sweep<0>(sweep, ba, bb, vr0, LA, LV, L.cs[hb]);
-        ep_wave_sync();  // (the test's partials are rewritten next sweep)
-    }
-    int *O = L.ord[hb];
-    if (lane == 0) {  // eig_order_desc<12> on the diagonal
-        for (int i = 0; i < 12; ++i) O[i] = i;
-        for (int i = 1; i < 12; ++i) {
-            const int k = O[i];
-            const double dk = LA[(kEpR + 1) * k];
-            int jx = i - 1;
-            while (jx >= 0 && LA[(kEpR + 1) * O[jx]] < dk) {
-                O[jx + 1] = O[jx];
-                --jx;
-            }
-            O[jx + 1] = k;
-        }
-    }
-    ep_wave_sync();
-    if (lane < 48) {  // ut[i][j] = V[j][o[11 - i]]
-        const int i = lane / 12, j = lane - 12 * (lane / 12);
-        E[64 + lane] = LV[kEpR * j + O[11 - i]];
-    }
-}
-
-// 3 of 3: stage 2's rest (L, rho, the beta estimates) and stage 3 (a pose and mean error per
-// estimate, the lowest wins), 3 lanes per hypothesis, hpw <= 21 hypotheses per wave (long rounds
-// 21, lane 63 idle: at 430 VGPRs one wave per SIMD, so a 20k-hypothesis round fits the GPU in one
-// pass, r05; short rounds 16, launch_pnp_solve): lane c takes estimate c + 1 (epnp_beta,
-// epnp_pose_err: the loop bodies of epnp_stage2_post and epnp_stage3), the group then applies
-// epnp_stage3's rule (valid, lowest error, first on ties) to the three and lane 0 writes the
-// records (as k_pnp_solve does for P3P)
-__global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, int32_t H, int hpw) {
+// 3 of 3: lane c of a group of three takes estimate c + 1, then epnp::compute_pose's pick,
+// Rodrigues(Rodrigues(R)) (the (rvec, tvec) model computeError projects), the records
+__global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin, int32_t H, int hpw) {
     const int prob = blockIdx.y;
     const int lane = threadIdx.x & 63, g = lane / 3, c = lane - 3 * g;
     const int hl = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * hpw + g;
@@ -1375,67 +1141,58 @@ __global__ __launch_bounds__(256) void k_epnp5_c(PnpArgs a, int64_t hyp_begin, i
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
     const int64_t rec = (int64_t)prob * a.hyp_stride + h;
-    const double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;  // launch-local scratch
+    const double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;
     int8_t st = live ? a.status[rec] : -1;
-    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0}, err = 0.0, cen[3] = {0, 0, 0};
-    bool mine = false;  // this lane's estimate gave a pose
-    bool s1ok = false;
+    double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0}, err = 0.0;
     if (st > 0) {
+        double L[6][10], rho[6], be[4];
+        {
+            double v[4][12];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int k = 0; k < 12; ++k) v[i][k] = E[(3 - i) * 12 + k];
+            cvq::epnp_l6x10(v, L);
+            cvq::Epnp5 cw;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) cw.cws[i][j] = E[kCvCws + 3 * i + j];
+            cvq::epnp_rho(cw, rho);
+        }
+        cvq::betas_approx(c + 1, L, rho, be);
+        cvq::gauss_newton(L, rho, be);
         int32_t idx[5];
         (void)epnp5_sample(a, rec, h, n, idx);
         Epnp5Pts q;
         epnp5_gather(a, p0, idx, q);
-        const EpnpStage1 s1 = *reinterpret_cast<const EpnpStage1 *>(E);
-        s1ok = s1.ok != 0.0;
-        if (s1ok) {
-            EpnpStage2 s2;
+        const double *cm = a.cams + 4 * prob;
+        cvq::Epnp5 e;
+        cvq::epnp5_init(q.X, q.Y, q.Z, q.U, q.V, Cam{cm[0], cm[1], cm[2], cm[3]}, e);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 5; ++i)
 #pragma unroll
-                for (int q = 0; q < 12; ++q) s2.ut[i][q] = E[64 + 12 * i + q];
-            double L[60], rho[6], be[4];
-            epnp_l_rho(s1, s2, L, rho);
-            if (epnp_beta(c + 1, L, rho, be)) {
-                MinimalEpnpReducer<5> red;
-                epnp5_reducer(q, red, cen);
-                double p1[3], a1[4];
-                red.first(p1);
-                epnp_alphas(epnp_alpha_frame(s1.f), p1[0], p1[1], p1[2], a1);
-                const double *cm = a.cams + 4 * prob;
-                mine = epnp_pose_err(red, Cam{cm[0], cm[1], cm[2], cm[3]}, s1, s2, be, a1, R, t, err);
-            }
-        }
+            for (int j = 0; j < 4; ++j) e.alphas[i][j] = E[kCvAlpha + 4 * i + j];
+        double v[4][12];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int k = 0; k < 12; ++k) v[i][k] = E[(3 - i) * 12 + k];
+        err = cvq::epnp5_r_and_t(e, v, be, R, t);
     }
-    // epnp_stage3's pick over the group's three lanes, in estimate order
+    // epnp::compute_pose's pick over the group's three lanes (estimates 1, 2, 3)
     const int base = 3 * g;
-    int win = -1;
-    double best = 0.0;
+    const double err3[3] = {__shfl(err, base), __shfl(err, base + 1), __shfl(err, base + 2)};
+    const int src = base + cvq::epnp_pick(err3);
 #pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        const bool ok_e = __shfl(mine ? 1 : 0, base + e) != 0;
-        const double err_e = __shfl(err, base + e);
-        if (ok_e && (win < 0 || err_e < best)) {
-            win = e;
-            best = err_e;
-        }
-    }
-    const int src = base + (win < 0 ? 0 : win);
+    for (int k = 0; k < 9; ++k) R[k] = __shfl(R[k], src);
 #pragma unroll
-    for (int q = 0; q < 9; ++q) R[q] = __shfl(R[q], src);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) t[q] = __shfl(t[q], src);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) cen[q] = __shfl(cen[q], src);
+    for (int k = 0; k < 3; ++k) t[k] = __shfl(t[k], src);
     if (!live || c != 0) return;
+    // OpenCV's EPnP always reports a pose (a degenerate sample's NaN scores no inlier)
     if (st > 0) {
-        const bool ok = s1ok && win >= 0;
-        if (ok) lm_from_centred(R, cen, t);
-        if (ok && a.rvec_rt) rodrigues_roundtrip(R);
-        st = ok ? 1 : 0;
-        if (!ok)
-            for (int q = 0; q < 9; ++q) R[q] = 0.0;
-        if (!ok)
-            for (int q = 0; q < 3; ++q) t[q] = 0.0;
+        st = 1;
+        if (a.rvec_rt) rodrigues_roundtrip(R);
     }
     double *m = a.models + rec * kModelStride;
 #pragma unroll
@@ -3121,27 +2878,18 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
     return hipGetLastError();
 }
 
-#ifndef RSAC_EPNP_WAVE_MAX
-#define RSAC_EPNP_WAVE_MAX 2048
-#endif
-constexpr int64_t kEpnpWaveMaxHyps = RSAC_EPNP_WAVE_MAX;  // one wave per hypothesis up to this many (2 waves/SIMD at 250 VGPRs: one round of waves; A/B knob)
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
-    if (a.sample_k == 5) {  // EPnP-5: the three-launch form (k_epnp5_a / _jacobi6 or _jacobi_b / _c)
+    if (a.sample_k == 5) {  // EPnP-5 in OpenCV's sequence: k_cvepnp5_a / _svd / _c
         if (!a.epnp) return hipErrorInvalidValue;  // its scratch (ensure_epnp5) is required
-        // short rounds (an adaptive run's first 256 hypotheses): their latency is one hypothesis', so
-        // one wave per block in stages 1 and 3 (4 and 16 CUs for 256 hypotheses, 64 and 16 per wave;
-        // sparser waves were slower, r05 A/B) and one wave per hypothesis in 2 x 2 blocks for the
-        // Jacobi; longer rounds 6 lanes per hypothesis's Jacobi
-        const bool short_round = (int64_t)P * H <= kEpnpWaveMaxHyps;
-        const int tb = short_round ? 64 : 256;  // threads per block of stages 1 and 3
-        hipLaunchKernelGGL(k_epnp5_a, dim3(cdiv(H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
-        if (short_round)
-            hipLaunchKernelGGL(k_epnp5_jacobi_b, dim3(cdiv(64 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
-        else
-            hipLaunchKernelGGL(k_epnp5_jacobi6, dim3(cdiv(H, kJ6B), P), dim3(256), 0, s, ka, hyp_begin, H);
-        const int hpw = short_round ? 16 : 21;  // hypotheses per wave of stage 3 (3 lanes each)
-        hipLaunchKernelGGL(k_epnp5_c, dim3(cdiv(cdiv(H, hpw), tb / 64), P), dim3(tb), 0, s, ka, hyp_begin, H, hpw);
+        // short rounds (an adaptive run's first 256 hypotheses): their latency is one hypothesis',
+        // so one wave per block in stages 1 and 3
+        const bool short_round = (int64_t)P * H <= 2048;
+        const int tb = short_round ? 64 : 256;
+        hipLaunchKernelGGL(k_cvepnp5_a, dim3(cdiv(H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
+        hipLaunchKernelGGL(k_cvepnp5_svd, dim3(cdiv(4 * (int64_t)H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
+        const int hpw = 21;  // hypotheses per wave of stage 3 (3 lanes each)
+        hipLaunchKernelGGL(k_cvepnp5_c, dim3(cdiv(cdiv(H, hpw), tb / 64), P), dim3(tb), 0, s, ka, hyp_begin, H, hpw);
     }
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     else if ((int64_t)P * H <= kSolve4MaxHyps)

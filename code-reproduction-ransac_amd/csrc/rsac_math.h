@@ -43,10 +43,9 @@ RSAC_HD double dsqrt(double v) { return __builtin_sqrt(v); }
 
 // ---------------------------------------------------------------------------
 // Rodrigues (cv::Rodrigues, [OpenCV 4.x, unvendored] calibration.cpp cvRodrigues2; main_v1.py:895,
-// testpro-K.py:84) from + - * / sqrt only, so host, device and the oracle (rsac_oracle.c
-// orc_rodrigues_*) give the same bits: acos, sin and cos are polynomials with exactly rounded
-// series coefficients (about 1 ulp from the true values, not libm's bits), OpenCV's SVD
-// orthogonalisation R = U Vt is the polar factor by Newton's iteration.
+// testpro-K.py:84): acos, sin and cos as polynomials with exactly rounded series coefficients
+// (about 1 ulp from the true values, not libm's bits), so host, device and the oracle
+// (rsac_oracle.c orc_rd_*) give the same bits; the rest of cvRodrigues2 is rsac_cvepnp.h.
 // ---------------------------------------------------------------------------
 constexpr double kPio2Hi = 0x1.921fb54442d18p+0, kPio2Lo = 0x1.1a62633145c07p-54;
 constexpr double kPio2A = 0x1.921fb544p+0, kPio2B = 0x1.0b4611a626331p-34;  // pi/2: 33 bits + the rest
@@ -108,99 +107,6 @@ RSAC_HD void rodr_sincos(double th, double &sn, double &cs) {
     const double c = w + (((1.0 - w) - hz) + z * z * pc);
     sn = n == 0 ? s : n == 1 ? c : n == 2 ? -s : -c;
     cs = n == 0 ? c : n == 1 ? -s : n == 2 ? -c : s;
-}
-
-// OpenCV's R = U Vt (SVD::compute, the orthogonal polar factor) by Newton's iteration
-// X <- (X + X^-T) / 2, X^-T = cof(X) / det X, until no element moves by more than 1e-15 (at most
-// 30 steps: one for a rotation from a minimal solver); a singular X is left as it is
-RSAC_HD void rodr_polar(double X[9]) {
-    for (int it = 0; it < 30; ++it) {
-        double cf[9];
-        cf[0] = X[4] * X[8] - X[5] * X[7];
-        cf[1] = X[5] * X[6] - X[3] * X[8];
-        cf[2] = X[3] * X[7] - X[4] * X[6];
-        cf[3] = X[2] * X[7] - X[1] * X[8];
-        cf[4] = X[0] * X[8] - X[2] * X[6];
-        cf[5] = X[1] * X[6] - X[0] * X[7];
-        cf[6] = X[1] * X[5] - X[2] * X[4];
-        cf[7] = X[2] * X[3] - X[0] * X[5];
-        cf[8] = X[0] * X[4] - X[1] * X[3];
-        const double det = X[0] * cf[0] + X[1] * cf[1] + X[2] * cf[2];
-        if (!(dabs(det) > 1e-30) || !dfinite(det)) return;
-        const double id = 1.0 / det;
-        double mv = 0.0;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const double nx = 0.5 * (X[k] + cf[k] * id);
-            const double d = dabs(nx - X[k]);
-            mv = d > mv ? d : mv;
-            X[k] = nx;
-        }
-        if (!(mv > 1e-15)) return;
-    }
-}
-
-// cv::Rodrigues vector -> matrix
-RSAC_HD void rodrigues_v2m_det(const double r[3], double R[9]) {
-    const double th = dsqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
-    if (th < 0x1p-52) {  // DBL_EPSILON
-#pragma unroll
-        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
-        return;
-    }
-    double s, c;
-    rodr_sincos(th, s, c);
-    const double c1 = 1. - c, it = 1. / th;
-    const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
-    R[0] = c + c1 * x * x;     R[1] = c1 * x * y - s * z; R[2] = c1 * x * z + s * y;
-    R[3] = c1 * x * y + s * z; R[4] = c + c1 * y * y;     R[5] = c1 * y * z - s * x;
-    R[6] = c1 * x * z - s * y; R[7] = c1 * y * z + s * x; R[8] = c + c1 * z * z;
-}
-
-// cv::Rodrigues matrix -> vector: checkRange(R, -100, 100) (else zeros), R = U Vt, the angle from
-// the antisymmetric part, the theta ~ pi branch from the symmetric part
-RSAC_HD void rodrigues_m2v_det(const double Rin[9], double r[3]) {
-    double R[9];
-    bool in_range = true;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        R[k] = Rin[k];
-        in_range = in_range && dabs(R[k]) <= 100.0;
-    }
-    if (!in_range) {
-        r[0] = r[1] = r[2] = 0.0;
-        return;
-    }
-    rodr_polar(R);
-    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
-    const double s = dsqrt((rx * rx + ry * ry + rz * rz) * 0.25);
-    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
-    c = c > 1. ? 1. : c < -1. ? -1. : c;
-    double th = rodr_acos(c);
-    if (s < 1e-5) {
-        if (c > 0) {
-            r[0] = r[1] = r[2] = 0.0;
-            return;
-        }
-        double t;
-        t = (R[0] + 1) * 0.5; rx = dsqrt(t > 0 ? t : 0);
-        t = (R[4] + 1) * 0.5; ry = dsqrt(t > 0 ? t : 0) * (R[1] < 0 ? -1. : 1.);
-        t = (R[8] + 1) * 0.5; rz = dsqrt(t > 0 ? t : 0) * (R[2] < 0 ? -1. : 1.);
-        if (dabs(rx) < dabs(ry) && dabs(rx) < dabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
-        th = th / dsqrt(rx * rx + ry * ry + rz * rz);
-        r[0] = rx * th; r[1] = ry * th; r[2] = rz * th;
-        return;
-    }
-    const double vth = 1 / (2 * s) * th;
-    r[0] = rx * vth; r[1] = ry * vth; r[2] = rz * vth;
-}
-
-// PnPRansacCallback keeps each minimal model as (rvec, tvec) and computeError projects through
-// Rodrigues(rvec): R' = Rodrigues(Rodrigues(R)) is the rotation OpenCV scores (RSAC_F_RVEC_ROUNDTRIP)
-RSAC_HD void rodrigues_roundtrip(double R[9]) {
-    double rv[3];
-    rodrigues_m2v_det(R, rv);
-    rodrigues_v2m_det(rv, R);
 }
 
 // ---------------------------------------------------------------------------
@@ -267,6 +173,18 @@ struct Philox {
 struct Cam {
     double fx, fy, cx, cy;
 };
+
+}  // namespace rsac
+#include "rsac_cvepnp.h"
+namespace rsac {
+
+// cv::Rodrigues both ways in OpenCV's operation sequence (rsac_cvepnp.h: cvRodrigues2 through
+// JacobiSVD, c I + c1 r r^T + s [r]x element by element)
+RSAC_HD void rodrigues_v2m_det(const double r[3], double R[9]) { cvq::rodrigues_v2m(r, R); }
+RSAC_HD void rodrigues_m2v_det(const double Rin[9], double r[3]) { cvq::rodrigues_m2v(Rin, r); }
+// PnPRansacCallback keeps each minimal model as (rvec, tvec) and computeError projects through
+// Rodrigues(rvec): R' = Rodrigues(Rodrigues(R)) is the rotation OpenCV scores (RSAC_F_RVEC_ROUNDTRIP)
+RSAC_HD void rodrigues_roundtrip(double R[9]) { cvq::rvec_roundtrip(R); }
 
 RSAC_HD float pnp_err(const double *R, const double *t, const Cam &k, double X, double Y, double Z, float uf,
                       float vf) {
@@ -1278,7 +1196,7 @@ RSAC_HD void jacobi_eig(double *A, double *V, double *d) {
 // matrix at the step's start; then the columns of every pair (every row), the rows of every pair,
 // and V's columns.  Pairs are disjoint, so each element sees one fixed sequence of operations
 // whatever the order within a phase: the GPU runs a step's pairs on different lanes
-// (k_epnp5_jacobi6, k_epnp5_jacobi_b) with the bits of this loop.  Schedule (circle method): in step r, position 0
+// with the bits of this loop.  Schedule (circle method): in step r, position 0
 // holds index 0 and position m > 0 holds 1 + (m - 1 + r) % (N - 1); pair i is positions i and
 // N - 1 - i, p the smaller index.  Sweep test as jacobi_eig; the rotation by jrr_rotation.
 RSAC_HD constexpr int jrr_pos(int N, int r, int m) { return m == 0 ? 0 : 1 + (m - 1 + r) % (N - 1); }
@@ -1553,7 +1471,7 @@ RSAC_HD bool epnp_rotation_svd(const double *H, double *R) {
 // The orthogonal polar factor U V^T of a well-conditioned 3 x 3 X (in place) by Newton's iteration
 // X <- (g X + X^-T / g) / 2, X^-T = cof(X) / det X, with Frobenius scaling g = (|X^-T|_F / |X|_F)^(1/2)
 // while a step moves an element by more than 1e-2 and g = 1 after, until no element moves by more
-// than 1e-15 (at most 30 steps).  (Unscaled, it is rodr_polar's step.)
+// than 1e-15 (at most 30 steps).  (Unscaled, it is the classical polar Newton step.)
 RSAC_HD void polar_newton3(double X[9]) {
     bool scale = true;
     for (int it = 0; it < 30; ++it) {
@@ -1664,7 +1582,7 @@ RSAC_HD bool epnp_beta(int approx, const double *L, const double *rho, double *b
     // the estimate's columns of L (1: 0 1 3 6, beta1^2, b1 b2, b1 b3, b1 b4; 2: 0 1 2, beta1^2, b1 b2,
     // b2^2; 3: 0..4, beta1^2, b1 b2, b2^2, b1 b3, b2 b3), zero-padded to 5: householder_ls skips a zero
     // column's reflection, leaves it zero and gives it x = 0, so x[0, N) carry the 6 x N solve's bits
-    // and the three estimates run one instruction stream (a GPU lane each, k_epnp5_c)
+    // and the three estimates run one instruction stream
     double A[30], x[5];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -1715,7 +1633,7 @@ RSAC_HD void epnp_l_rho(const EpnpStage1 &s1, const EpnpStage2 &s2, double *L, d
 // Stage 2 after the eigen-decomposition: s2.ut (the eigenvectors of M^T M's 4 smallest
 // eigenvalues) given, the L 6x10 / rho system and the three beta estimates with Gauss-Newton.
 // (epnp_stage2 below; the GPU's minimal EPnP runs the 12 x 12 Jacobi on 6 or 64 lanes in between,
-// k_epnp5_jacobi6 / _b, and the three estimates on three lanes, k_epnp5_c)
+// and the three estimates)
 __host__ __device__ inline void epnp_stage2_post(const EpnpStage1 &s1, EpnpStage2 &s2) {
     double L[60], rho[6];
     epnp_l_rho(s1, s2, L, rho);
@@ -1899,69 +1817,6 @@ inline bool pnp_epnp(Red &red, const Cam &k, double *R_out, double *t_out) {
     EpnpStage2 s2;
     epnp_stage2(s1, k, s2);
     return epnp_stage3(red, k, s1, s2, R_out, t_out);
-}
-
-// The minimal EPnP of solvePnPRansac's default kernel (SOLVEPNP_ITERATIVE: model_points = 5,
-// ransac_kernel_method = SOLVEPNP_EPNP, OpenCV solvepnp.cpp PnPRansacCallback::runKernel): EPnP on
-// the N sampled points, one lane per hypothesis.  The sums take lm_reduce_host's order for an
-// N-point problem with every point masked in (point i -> slot i, the 64-lane xor butterfly whose
-// other slots and waves add exact zeros), and the frame is centred on the sample's first point,
-// so pnp_epnp_host on the same N points (in sample order) returns the same bits.
-template <int N>
-struct MinimalEpnpReducer {
-    static_assert(N >= 4 && N <= 8, "the butterfly below covers slots 0..7");
-    double X[N], Y[N], Z[N], u[N], v[N];  // centred on point 0
-    template <int NV, class F>
-    RSAC_HD void sum(F f, double *out) {
-        // only the N occupied slots are held: the butterfly's other slots stay +0.0
-        double w[N][NV];
-#pragma unroll
-        for (int l = 0; l < N; ++l)
-#pragma unroll
-            for (int q = 0; q < NV; ++q) w[l][q] = 0.0;
-#pragma unroll
-        for (int i = 0; i < N; ++i) f(X[i], Y[i], Z[i], u[i], v[i], w[i]);
-#pragma unroll
-        for (int l = 0; l < N; ++l)  // the butterfly's offsets 32, 16, 8: partners hold zeros
-#pragma unroll
-            for (int q = 0; q < NV; ++q) w[l][q] = ((w[l][q] + 0.0) + 0.0) + 0.0;
-        // the xor butterfly over slots 0..7 (offsets 4, 2, 1) as slot 0 receives it:
-        // ((s0 + s4) + (s2 + s6)) + ((s1 + s5) + (s3 + s7))
-        auto sl = [&](int l, int q) { return l < N ? w[l][q] : 0.0; };
-#pragma unroll
-        for (int q = 0; q < NV; ++q) {
-            double b = ((sl(0, q) + sl(4, q)) + (sl(2, q) + sl(6, q))) + ((sl(1, q) + sl(5, q)) + (sl(3, q) + sl(7, q)));
-            for (int wv = 1; wv < kLmThreads / 64; ++wv) b = b + 0.0;  // waves 1..7 add their zero sums
-            out[q] = b;
-        }
-    }
-    RSAC_HD bool first(double *p) {
-        p[0] = X[0]; p[1] = Y[0]; p[2] = Z[0];
-        return true;
-    }
-};
-
-// (R, t) in the world frame; false for a degenerate sample (planar, or no valid beta)
-template <int N>
-__host__ __device__ inline bool pnp_epnp_minimal(const float *X, const float *Y, const float *Z, const float *U,
-                                                 const float *V, const Cam &k, double *R, double *t) {
-    MinimalEpnpReducer<N> red;
-    const double c[3] = {(double)X[0], (double)Y[0], (double)Z[0]};
-    for (int i = 0; i < N; ++i) {
-        red.X[i] = (double)X[i] - c[0];
-        red.Y[i] = (double)Y[i] - c[1];
-        red.Z[i] = (double)Z[i] - c[2];
-        red.u[i] = (double)U[i];
-        red.v[i] = (double)V[i];
-    }
-    EpnpStage1 s1;
-    epnp_stage1(red, k, s1);
-    if (s1.ok == 0.0) return false;
-    EpnpStage2 s2;
-    epnp_stage2(s1, k, s2);
-    if (!epnp_stage3(red, k, s1, s2, R, t)) return false;
-    lm_from_centred(R, c, t);
-    return true;
 }
 
 }  // namespace rsac

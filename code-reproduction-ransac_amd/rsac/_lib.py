@@ -91,6 +91,7 @@ SIGNATURES = [
                                              _vp]),
     ("rsac_pnp_mask", C.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _d, _u32, _vp, C.POINTER(_i32), _vp]),
     ("rsac_pnp_epnp", C.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    ("rsac_pnp_epnp_minimal", C.c_int, [_vp, _vp, _vp, _vp, _vp]),
     ("rsac_pnp_refine", C.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32]),
     ("rsac_homography_fit", C.c_int, [_vp, _vp, _i32, _vp, _vp]),
     ("rsac_rodrigues_v2m", None, [_vp, _vp]),

@@ -806,6 +806,18 @@ def epnp_pose(points2D, points3D, K, mask=None):
     return (R.reshape(3, 3), t) if code == L.OK else (None, None)
 
 
+def epnp_minimal(points2D, points3D, K):
+    """solvePnPRansac's default minimal solver on one 5-point sample, on the host: solvePnP(...,
+    SOLVEPNP_EPNP) in OpenCV's operation sequence (rsac_cvepnp.h, the source the k_cvepnp5_*
+    kernels run) -> (R, t).  Inputs are rounded to f32 like solvePnPRansac's CV_32F copies."""
+    P3 = np.ascontiguousarray(np.asarray(points3D, np.float64).reshape(5, 3))
+    P2 = np.ascontiguousarray(np.asarray(points2D, np.float64).reshape(5, 2))
+    R, t = np.zeros(9), np.zeros(3)
+    L.check(L.lib().rsac_pnp_epnp_minimal(P3.ctypes.data, P2.ctypes.data, _K9(K).ctypes.data, R.ctypes.data,
+                                          t.ctypes.data))
+    return R.reshape(3, 3), t
+
+
 def homography_fit(src, dst, mask=None):
     """Least-squares normalised DLT + LM on all (or masked) points -> H (findHomography method 0)."""
     s = np.ascontiguousarray(np.asarray(src, np.float64).reshape(-1, 2))

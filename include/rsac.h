@@ -298,6 +298,16 @@ RSAC_EXPORT int rsac_pnp_mask(rsac_ctx *ctx, const void *pts3d, const void *pts2
 RSAC_EXPORT int rsac_pnp_epnp(const double *pts3d, const double *pts2d, int32_t n, const double K[9],
                               const uint8_t *mask, double R_out[9], double t_out[3]);
 
+/* The minimal solver of cv2.solvePnPRansac's default flags on one 5-point sample, on the host
+ * (no GPU needed): solvePnP(..., SOLVEPNP_EPNP) in OpenCV's operation sequence (undistortPoints
+ * to f32 normalised points, epnp.cpp with lapack.cpp's JacobiSVD; rsac_cvepnp.h, the source the
+ * k_cvepnp5_* kernels run, the 12 x 12 JacobiSVD there on four lanes).  pts3d 5 x 3 and pts2d
+ * 5 x 2 f64 AoS, rounded to f32 like solvePnPRansac's CV_32F copies (main_v1.py:497,
+ * testpro-K.py:72).  Always RSAC_OK (OpenCV's EPnP reports a pose for any sample; a degenerate
+ * one gives NaN). */
+RSAC_EXPORT int rsac_pnp_epnp_minimal(const double *pts3d, const double *pts2d, const double K[9], double R_out[9],
+                                      double t_out[3]);
+
 /* Host-side non-minimal fits (no GPU needed), f64 AoS host inputs rounded
  * to f32 like the RANSAC path.  mask may be NULL (= all points).
  * rsac_pnp_refine: LM on (R, t) in place, cv2.solvePnPRefineLM
@@ -340,10 +350,10 @@ RSAC_EXPORT int rsac_pnp_orientation_sweep(rsac_ctx *ctx, const double *pts3d, c
                                            int32_t *status_out, int32_t *n_inliers_out, uint8_t *masks_out,
                                            double R_out[9], double t_out[3], void *stream);
 
-/* Rodrigues (cv2.Rodrigues, main_v1.py:895): vector <-> matrix.  cvRodrigues2's steps (range
- * check, SVD orthogonalisation as the polar factor, the theta ~ pi branch) from + - * / sqrt
- * only: acos / sin / cos are series polynomials (~1 ulp), so the bits are the device's and the
- * oracle's, not libm's. */
+/* Rodrigues (cv2.Rodrigues, main_v1.py:895): vector <-> matrix in cvRodrigues2's operation
+ * sequence (range check, R = U V^T through lapack.cpp's JacobiSVD, the theta ~ pi branch;
+ * c I + c1 r r^T + s [r]x element by element); acos / sin / cos are series polynomials (~1 ulp),
+ * so the bits are the device's and the oracle's, not libm's. */
 RSAC_EXPORT void rsac_rodrigues_v2m(const double r[3], double R[9]);
 RSAC_EXPORT void rsac_rodrigues_m2v(const double R[9], double r[3]);
 

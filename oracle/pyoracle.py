@@ -18,7 +18,36 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "liboracle.so")
-_lib = None
+_LIB_UNFUSED = os.path.join(_HERE, "liboracle_unfused.so")
+_libs = {}
+# The PnP restatement in use (oracle/rsac_oracle.c orc_set_sequence):
+#   "cv"         OpenCV's operation sequence for the EPnP-5 minimal solver and the Rodrigues round
+#                trip (oracle/cv_epnp.c) -- the default, the one the GPU reproduces;
+#   "rr"         the round-4/5 restatement (round-robin Jacobi EPnP with fused steps, polar Rodrigues);
+#   "rr_unfused" the same built with every explicit fma as a rounded product + a rounded sum.
+# The last two exist for the decision-change study (tests/test_cv_epnp.py, scripts/epnp_variants.py).
+SEQUENCES = ("cv", "rr", "rr_unfused")
+_sequence = "cv"
+
+
+class sequence:
+    """Context manager: ``with pyoracle.sequence("rr"): ...`` runs the PnP oracle in another
+    restatement (not thread-safe: the study runs one variant at a time)."""
+
+    def __init__(self, name):
+        if name not in SEQUENCES:
+            raise ValueError(f"unknown sequence {name!r}")
+        self.name = name
+
+    def __enter__(self):
+        global _sequence
+        self.prev, _sequence = _sequence, self.name
+        return self
+
+    def __exit__(self, *exc):
+        global _sequence
+        _sequence = self.prev
+        return False
 
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
 _f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
@@ -35,13 +64,33 @@ def build() -> str:
 
 
 def lib():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
-            os.path.join(_HERE, "rsac_oracle.c")):
-        build()
-    L = C.CDLL(_LIB_PATH)
+    key = _LIB_UNFUSED if _sequence == "rr_unfused" else _LIB_PATH
+    L = _libs.get(key)
+    if L is None:
+        srcs = [os.path.join(_HERE, f) for f in ("rsac_oracle.c", "cv_epnp.c")]
+        if not os.path.exists(key) or os.path.getmtime(key) < max(os.path.getmtime(f) for f in srcs):
+            build()
+        L = _libs[key] = _load(key)
+    L.orc_set_sequence(0 if _sequence == "cv" else 1)
+    return L
+
+
+def _load(path):
+    L = C.CDLL(path)
+    L.orc_set_sequence.argtypes = [C.c_int]
+    L.orc_set_sequence.restype = None
+    L.orc_cv_epnp.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_void_p, C.c_int, _f64p, _f64p, _f64p]
+    L.orc_cv_epnp.restype = C.c_int
+    L.cvq_hypot.argtypes = [C.c_double, C.c_double]
+    L.cvq_hypot.restype = C.c_double
+    L.cvq_jacobi_svd.argtypes = [_f64p, C.c_int, _f64p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.cvq_jacobi_svd.restype = None
+    L.cvq_svd3.argtypes = [_f64p, _f64p, _f64p, _f64p]
+    L.cvq_svd3.restype = None
+    L.cvq_invert3.argtypes = [_f64p, _f64p]
+    L.cvq_invert3.restype = None
+    L.cvq_solve6.argtypes = [_f64p, C.c_int, _f64p, _f64p]
+    L.cvq_solve6.restype = None
     L.orc_mwc_next.argtypes = [C.POINTER(C.c_uint64)]
     L.orc_mwc_next.restype = C.c_uint32
     L.orc_mwc_uniform.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.c_int]
@@ -160,7 +209,6 @@ def lib():
     L.orc_fm_ransac.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_double, C.c_double, C.c_int, C.c_uint64,
                                 _f64p, _u8p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     L.orc_fm_ransac.restype = C.c_int64
-    _lib = L
     return L
 
 

@@ -52,6 +52,27 @@
 
 #define ORC_API __attribute__((visibility("default")))
 
+#ifdef ORC_UNFUSED
+/* liboracle_unfused.so (test infrastructure for the decision-change study): every explicit fused
+ * step of the restated solvers evaluated as a rounded product and a rounded sum */
+#define fma(a, b, c) ((a) * (b) + (c))
+#endif
+
+/* The EPnP-5 minimal solver and the Rodrigues round trip of the PnP models:
+ *   ORC_SEQ_CV (default) OpenCV's operation sequence (cv_epnp.c orc_cv_epnp, orc_cv_rvec_roundtrip);
+ *   ORC_SEQ_RR           this project's round-4/5 EPnP (round-robin Jacobi, Householder betas,
+ *                        polar-factor rotation; orc_pnp_epnp) and Rodrigues (polar Newton), kept
+ *                        for the comparison of tests/test_cv_epnp.py and scripts/epnp_variants.py */
+enum { ORC_SEQ_CV = 0, ORC_SEQ_RR = 1 };
+static int g_seq = ORC_SEQ_CV;
+ORC_API void orc_set_sequence(int v) { g_seq = v; }
+ORC_API int orc_get_sequence(void) { return g_seq; }
+ORC_API int orc_cv_epnp(const float *X, const float *Y, const float *Z, const float *U, const float *V,
+                        const int32_t *idx, int n, const double cam[4], double R[9], double t[3]);
+ORC_API void orc_cv_rvec_roundtrip(double R[9]);
+ORC_API void orc_cv_rodrigues_m2v(const double Rin[9], double r[3]);
+ORC_API void orc_cv_rodrigues_v2m(const double rin[3], double R[9]);
+
 /* ------------------------------------------------------------------------ */
 /* RNG 1: OpenCV cv::RNG, multiply-with-carry, seeded (uint64)-1 in         */
 /* RANSACPointSetRegistrator::run (ptsetreg.cpp) -- behind every cv2.* call  */
@@ -753,6 +774,7 @@ ORC_API int orc_pnp_epnp(const float *X, const float *Y, const float *Z, const f
  * the 5 sampled points, in sample order, every point in (the frame centred on the first). */
 ORC_API int orc_pnp_minimal_epnp5(const float *X, const float *Y, const float *Z, const float *U, const float *V,
                                   const int32_t idx[5], const double cam[4], double R[9], double t[3]) {
+    if (g_seq == ORC_SEQ_CV) return orc_cv_epnp(X, Y, Z, U, V, idx, 5, cam, R, t);
     float x[5], y[5], z[5], u[5], v[5];
     uint8_t m[5] = {1, 1, 1, 1, 1};
     for (int j = 0; j < 5; ++j) {
@@ -936,6 +958,10 @@ static void rd_polar(double X[9]) {
 }
 
 ORC_API void orc_rodrigues_v2m(const double r[3], double R[9]) {
+    if (g_seq == ORC_SEQ_CV) {
+        orc_cv_rodrigues_v2m(r, R);
+        return;
+    }
     double th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
     if (th < DBL_EPSILON) {
         for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
@@ -951,6 +977,10 @@ ORC_API void orc_rodrigues_v2m(const double r[3], double R[9]) {
 }
 
 ORC_API void orc_rodrigues_m2v(const double Rin[9], double r[3]) {
+    if (g_seq == ORC_SEQ_CV) {
+        orc_cv_rodrigues_m2v(Rin, r);
+        return;
+    }
     double R[9];
     for (int k = 0; k < 9; ++k) {
         if (!(fabs(Rin[k]) <= 100.0)) { r[0] = r[1] = r[2] = 0; return; }  /* checkRange */
@@ -981,6 +1011,10 @@ ORC_API void orc_rodrigues_m2v(const double Rin[9], double r[3]) {
  * Rodrigues(rvec) (solvepnp.cpp; main_v1.py:497, testpro-K.py:72): the rotation it scores is
  * Rodrigues(Rodrigues(R)) (RSAC_F_RVEC_ROUNDTRIP) */
 ORC_API void orc_rvec_roundtrip(double R[9]) {
+    if (g_seq == ORC_SEQ_CV) {
+        orc_cv_rvec_roundtrip(R);
+        return;
+    }
     double rv[3];
     orc_rodrigues_m2v(R, rv);
     orc_rodrigues_v2m(rv, R);

@@ -35,6 +35,11 @@ double orc_reproj_mean_sum(const double *, const double *, const double *, const
                            const uint8_t *, int, int *);
 float orc_thr2(double);
 void orc_rodrigues_v2m(const double *, double *);
+int orc_cv_epnp(const float *, const float *, const float *, const float *, const float *, const int32_t *, int,
+                const double *, double *, double *);
+int64_t orc_pnp_ransac_k(const float *, const float *, const float *, const float *, const float *, int, const double *,
+                         double, double, int, uint64_t, int, int, double *, double *, uint8_t *, int32_t *, int64_t *,
+                         int);
 
 static int g_fail = 0;
 #define CHECK(c)                                                                          \
@@ -109,6 +114,13 @@ static void pnp_checks(int n, double outl, int degenerate) {
             double sum = orc_reproj_mean_sum(R, t, s.cam, s.p3, s.p2, m, n, &c);
             CHECK(c == good && isfinite(sum));
         }
+    }
+    /* OpenCV's default minimal solver (cv_epnp.c): EPnP-5 RANSAC on MWC subsets, and one
+       degenerate (coincident) sample through JacobiSVD's zero-singular-value fill */
+    orc_pnp_ransac_k(s.X, s.Y, s.Z, s.U, s.V, n, s.cam, 8.0, 0.99, 500, 7, 1, 5, R, t, m, &good, &it, 1);
+    {
+        const int32_t dup[5] = {0, 0, 0, 0, 0};
+        orc_cv_epnp(s.X, s.Y, s.Z, s.U, s.V, dup, 5, s.cam, R2, t2);
     }
     orc_pnp_ransac_lo(s.X, s.Y, s.Z, s.U, s.V, n, s.cam, 8.0, 0.99, 2000, 7, R, t, m, &good, &it, &nlo);
     int32_t *c1 = malloc(sizeof(int32_t) * 600), *c2 = malloc(sizeof(int32_t) * 600);
