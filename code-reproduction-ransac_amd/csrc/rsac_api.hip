@@ -139,6 +139,7 @@ struct rsac_ctx {
     int64_t spec_finishes = 0, spec_redos = 0;                 // RSAC_DBG_SPEC_FINISHES / _REDOS
     int32_t scanrec_copy = 0;  // problems whose device scan records still go to h_scanrec (issue_scanrec_copy)
     int32_t dbg_cell_pts = 0;                                  // RSAC_DBG_MF_CELL_PTS
+    bool dbg_spec_overflow = false;                            // RSAC_DBG_SPEC_OVERFLOW
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf reproj;                                             // reprojection errors / the K sweep's inputs
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
@@ -776,7 +777,7 @@ int spec_resolve(rsac_ctx *c, const Staged &st, LoopOut &out, int model_points, 
     const ScanRecords *recs = c->h_scanrec.as<ScanRecords>();
     out.spec_pending = false;
     ok = false;
-    if (!fixed && recs[0].nrec < 0) {  // more improvements than records: the caller runs the loop afresh
+    if (!fixed && (recs[0].nrec < 0 || c->dbg_spec_overflow)) {  // more improvements than records: the caller runs the loop afresh
         out.scan[0].reset((int)out.scan[0].niters);
         out.spec_H = 0;
         return RSAC_OK;
@@ -1172,7 +1173,9 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
                 if (!lo.scan[0].done) return more();
             }
             if (!spec_fixed && !lo.scan[0].done) {
-                r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, nullptr, true);
+                // resume after the verified first round; a replay that started over (spec_H = 0)
+                // runs afresh, so OpenCV's MWC states restart with the scan
+                r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, nullptr, lo.spec_H > 0);
                 if (r) return r;
             }
             r = pnp_finish(c, st, a, lo, stride, K, mask_out, flags, s, refit, false);
@@ -1388,6 +1391,9 @@ int rsac_debug_set(rsac_ctx *c, int32_t key, int64_t value) {
     case RSAC_DBG_MF_CELL_PTS:
         if (value < 0 || value > (1 << 30)) return fail(RSAC_EINVAL, "bad cell size");
         c->dbg_cell_pts = (int32_t)value;
+        return RSAC_OK;
+    case RSAC_DBG_SPEC_OVERFLOW:
+        c->dbg_spec_overflow = value != 0;
         return RSAC_OK;
     default:
         return fail(RSAC_EINVAL, "unknown debug key %d", key);

@@ -214,7 +214,8 @@ class Context:
         return r.value, b.value
 
     def debug_set(self, key: int, value: int):
-        """test hooks of include/rsac.h (DBG_REFIT_MAX_BLOCKS, DBG_REFIT_DROP_BLOCK)"""
+        """test hooks of include/rsac.h (DBG_REFIT_MAX_BLOCKS, DBG_REFIT_DROP_BLOCK, DBG_MF_CELL_PTS,
+        DBG_SPEC_OVERFLOW)"""
         check(lib().rsac_debug_set(self._h, int(key), int(value)))
 
     def close(self):

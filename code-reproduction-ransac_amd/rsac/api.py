@@ -558,15 +558,19 @@ def winner(points2D, points3D, K, key, reproj_thresh: float = 30.0, *, seed: int
 
 def hypotheses(model: str, a, b, K=None, hyp_begin: int = 0, n_hyps: int = 1024, reproj_thresh: float = 30.0, *,
                seed: int = 0x5EED, subsets=None, device=None, exact_only: bool = False, minimal: str = "p3p",
-               rvec: bool = False):
+               rvec=None):
     """Raw per-hypothesis (status, counts, models) of the GPU hot path for one problem.
 
     model "pnp": a = points3D (N,3), b = points2D (N,2), K required.
     model "homography": a = src (N,2), b = dst (N,2).
     model "fundamental": a = pts1 (N,2), b = pts2 (N,2).
     subsets: optional (n_hyps, 4) int32 index table replacing the Philox draw ((n_hyps, 5) for
-    minimal="epnp5", PnP's 5-point EPnP kernel).  rvec: PnP models through Rodrigues(Rodrigues(R)).
+    minimal="epnp5", PnP's 5-point EPnP kernel).  rvec: PnP models through Rodrigues(Rodrigues(R));
+    the default (None) is on exactly when subsets are given, as pnp_ransac(sampler="opencv") scores
+    OpenCV's MWC subsets, so the probe returns the rotations that run scores.
     """
+    if rvec is None:
+        rvec = subsets is not None
     pnp = model == "pnp"
     if model not in ("pnp", "homography", "fundamental"):
         raise ValueError(f"unknown model {model!r}")

@@ -58,8 +58,16 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
     the best minimal model (SOLVEPNP_ITERATIVE's final solvePnP).  The inlier list is the
     RANSAC-phase mask, as OpenCV returns it.  Each minimal model is scored through
     Rodrigues(Rodrigues(R)), as PnPRansacCallback keeps it as an rvec (RSAC_F_RVEC_ROUNDTRIP).
+
+    useExtrinsicGuess (testpro-K.py:73 passes False): as in solvePnPRansac, the guess never reaches
+    the minimal solves (solvePnPGeneric drops it for the EPnP / P3P kernels) nor the
+    count == model_points branch; with SOLVEPNP_ITERATIVE the final solve on the inliers starts
+    from (rvec, tvec) instead of the RANSAC model, and both must then be given (OpenCV asserts).
     """
     _check_dist(distCoeffs)
+    guess = bool(useExtrinsicGuess)
+    if guess and (rvec is None or tvec is None):
+        raise error("useExtrinsicGuess=True needs rvec and tvec")
     P3 = np.asarray(objectPoints, np.float64).reshape(-1, 3)
     P2 = np.asarray(imagePoints, np.float64).reshape(-1, 2)
     if P3.shape[0] != P2.shape[0]:
@@ -71,11 +79,18 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
     # on all points, every index an inlier, no final solve
     p3p = flags in (SOLVEPNP_P3P, SOLVEPNP_AP3P) or P3.shape[0] == 4
     refine = "epnp" if flags in (SOLVEPNP_P3P, SOLVEPNP_AP3P, SOLVEPNP_EPNP) else "lm"
+    direct = P3.shape[0] == (4 if p3p else 5)  # solvePnPRansac's model_points == npoints branch
+    from_guess = guess and refine == "lm" and not direct
     R, t, mask = api.pnp_ransac(P2, P3, cameraMatrix, int(iterationsCount), float(reprojectionError),
-                                confidence=float(confidence), sampler="opencv", adaptive=True, refine=refine,
-                                minimal="p3p" if p3p else "epnp5", rvec=True)
+                                confidence=float(confidence), sampler="opencv", adaptive=True,
+                                refine=False if from_guess else refine, minimal="p3p" if p3p else "epnp5",
+                                rvec=True)
     if R is None:
         return False, (np.zeros((3, 1)) if rvec is None else rvec), (np.zeros((3, 1)) if tvec is None else tvec), None
+    if from_guess:  # the final SOLVEPNP_ITERATIVE solve on the inliers, from the caller's pose
+        R0 = api.rodrigues(np.asarray(rvec, np.float64).reshape(3))
+        R, t = api.refine_pose_device(P2, P3, cameraMatrix, R0, np.asarray(tvec, np.float64).reshape(3),
+                                      mask=np.asarray(mask))
     idx = np.flatnonzero(mask).astype(np.int32).reshape(-1, 1)
     return True, api.rodrigues(R).reshape(3, 1), t.reshape(3, 1), idx
 

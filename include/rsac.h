@@ -129,6 +129,9 @@ RSAC_EXPORT int rsac_refit_blocks(rsac_ctx *ctx, int32_t n, int32_t *ranges, int
 #define RSAC_DBG_REFIT_MAX_BLOCKS 1
 #define RSAC_DBG_REFIT_DROP_BLOCK 2
 #define RSAC_DBG_MF_CELL_PTS 5 /* > 0: the MFMA scorer runs every tile by cells of this many points */
+/* RSAC_DBG_SPEC_OVERFLOW (nonzero): the host's replay of a speculative first round treats it as
+ * having more improvements than the device records (the restart-from-hypothesis-0 branch) */
+#define RSAC_DBG_SPEC_OVERFLOW 6
 RSAC_EXPORT int rsac_debug_set(rsac_ctx *ctx, int32_t key, int64_t value);
 /* RSAC_DBG_SPEC_FINISHES / RSAC_DBG_SPEC_REDOS (read only): rsac_pnp_ransac(_batched) calls whose
  * finish was enqueued behind the device's own pick of the winners, and those of them the host's

@@ -94,6 +94,11 @@ static uint32_t cvq_rng_next(uint64_t *st) {
 /* lapack.cpp JacobiSVDImpl_<double>(At, astep, W, Vt, vstep, m, n, n1, DBL_MIN, 10 DBL_EPSILON):
  * At is n x m (row stride astep), its rows the columns being orthogonalised; Vt n x n (stride
  * vstep) or NULL; the first n1 rows of At are normalised on exit. */
+/* test hook: how many rows JacobiSVD has filled with a random direction (zero singular values),
+ * per matrix size n (tests/test_cv_epnp.py checks that the degenerate fixtures reach the branch) */
+static long g_fill[16];
+ORC_API long orc_cvq_fill_events(int n) { return n >= 0 && n < 16 ? g_fill[n] : 0; }
+
 ORC_API void cvq_jacobi_svd(double *At, int astep, double *Wout, double *Vt, int vstep, int m, int n, int n1) {
     const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
     double W[16];
@@ -177,6 +182,7 @@ ORC_API void cvq_jacobi_svd(double *At, int astep, double *Wout, double *Vt, int
     uint64_t rng = 0x12345678;
     for (int i = 0; i < n1; ++i) {
         double sd = i < n ? W[i] : 0;
+        if (sd <= minval && n < 16) __atomic_fetch_add(&g_fill[n], 1, __ATOMIC_RELAXED);
         for (int ii = 0; ii < 100 && sd <= minval; ii++) {
             /* a zero singular value: a random vector, projected off the earlier rows, normalised */
             const double val0 = 1. / m;

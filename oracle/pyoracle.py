@@ -81,6 +81,8 @@ def _load(path):
     L.orc_set_sequence.restype = None
     L.orc_cv_epnp.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, C.c_void_p, C.c_int, _f64p, _f64p, _f64p]
     L.orc_cv_epnp.restype = C.c_int
+    L.orc_cvq_fill_events.argtypes = [C.c_int]
+    L.orc_cvq_fill_events.restype = C.c_long
     L.cvq_hypot.argtypes = [C.c_double, C.c_double]
     L.cvq_hypot.restype = C.c_double
     L.cvq_jacobi_svd.argtypes = [_f64p, C.c_int, _f64p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
@@ -314,10 +316,13 @@ def pnp_count(R, t, soa, cam, thr, mask=False):
 
 
 def pnp_hypotheses(soa, cam, thr, seed, H, hyp0=0, problem=0, subsets=None, sub_status=None, models=False,
-                   minimal="p3p", rvec=False):
+                   minimal="p3p", rvec=None):
     """minimal: "p3p" (4-point samples, SOLVEPNP_P3P) or "epnp5" (5-point samples, EPnP: the
     default SOLVEPNP_ITERATIVE kernel of solvePnPRansac); subsets H x 4 or H x 5.  rvec: every
-    model's R -> Rodrigues(Rodrigues(R)) before it is counted (RSAC_F_RVEC_ROUNDTRIP)."""
+    model's R -> Rodrigues(Rodrigues(R)) before it is counted (RSAC_F_RVEC_ROUNDTRIP); default on
+    exactly when subsets are given (as rsac.hypotheses)."""
+    if rvec is None:
+        rvec = subsets is not None
     n = len(soa[0])
     k = 5 if minimal == "epnp5" else 4
     counts = np.zeros(H, np.int32)

@@ -100,11 +100,14 @@ def test_host_twin_equals_oracle_on_degenerate_samples():
         np.array([[0, 0, 0], [0, 0, 0], [5, 1, 2], [1, 7, 3], [2, 2, 9]], float),      # duplicate point
     ]
     px = np.array([[100, 200], [300, 210], [120, 400], [310, 420], [500, 430]], float)
+    f0 = [O.lib().orc_cvq_fill_events(n) for n in (3, 12)]
     for P in cases:
         P3 = P * 30.0 + base
         R, t = rsac.epnp_minimal(px, P3, K)
         Ro, to = O.pnp_minimal_epnp5(O.soa_pnp(P3, px), O.cam_from_K(K), [0, 1, 2, 3, 4])
         assert _bits_equal(R, Ro) and _bits_equal(t, to)
+    # the planar and collinear samples reach the fill branch of the 3 x 3 and of the 12 x 12 SVD
+    assert O.lib().orc_cvq_fill_events(3) > f0[0] and O.lib().orc_cvq_fill_events(12) > f0[1]
 
 
 def test_rodrigues_is_cvrodrigues2():

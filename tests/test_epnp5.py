@@ -108,6 +108,30 @@ def test_gpu_epnp5_hypotheses_bit_exact(n, outl, seed, H):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("H", [500, 4096])
+def test_gpu_epnp5_degenerate_samples_bit_exact(H):
+    """Half the points on the plane z = 700 m: a sample of five of them leaves M^T M with exact
+    zero rows, so cvSVD's JacobiSVD fills those directions from RNG(0x12345678)
+    (k_cvepnp5_svd's in-memory branch, cvq_fill_rows; the oracle counts the fills): status, count
+    and model of every hypothesis against the oracle, both launch shapes."""
+    pr = synth.pnp_problem(300, 0.3, seed=5)
+    P3 = pr["points3d"].copy()
+    P3[::2, 2] = 700.0
+    soa, cam = O.soa_pnp(P3, pr["points2d"]), O.cam_from_K(pr["K"])
+    subs, sst = _mwc5(300, H)
+    f0 = O.lib().orc_cvq_fill_events(12)
+    oc, os_, om = O.pnp_hypotheses(soa, cam, 30.0, 0, H, subsets=subs, sub_status=sst, models=True,
+                                   minimal="epnp5", rvec=True)
+    assert O.lib().orc_cvq_fill_events(12) > f0
+    st, cn, md = rsac.hypotheses("pnp", P3, pr["points2d"], pr["K"], 0, H, 30.0, subsets=subs, minimal="epnp5",
+                                 rvec=True)
+    np.testing.assert_array_equal(st, os_)
+    np.testing.assert_array_equal(cn, oc)
+    ok = st > 0
+    assert _bits_equal(md[ok, :12], om[ok, :12])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("sampler", ["opencv", "philox"])
 @pytest.mark.parametrize("n,outl,seed", [(600, 0.4, 41), (3000, 0.6, 42)])
 def test_gpu_epnp5_ransac_matches_oracle(sampler, n, outl, seed):

@@ -932,6 +932,32 @@ def _spec_counters():
     return f.value, r.value
 
 
+@pytest.mark.parametrize("sampler,minimal", [("opencv", "p3p"), ("opencv", "epnp5"), ("philox", "p3p")])
+def test_speculative_first_round_overflow_restarts_the_sampler(sampler, minimal):
+    """when the host's replay of a speculative first round finds more
+    improvements than the device records, the scan restarts at hypothesis 0 -- and so must
+    OpenCV's MWC sampler (a resumed state would redraw hypotheses 0.. from positions 256.. of its
+    sequence).  RSAC_DBG_SPEC_OVERFLOW forces that branch on a run that needs later rounds; the
+    result must still be the oracle's sequential loop."""
+    pr = synth.pnp_problem(1500, 0.8, seed=91)
+    ctx = rsac.context(0)
+    ref = O.pnp_ransac(pr["points3d"], pr["points2d"], pr["K"], 30.0, 0.99, 3000, 0x5EED, sampler=sampler,
+                       minimal=minimal)
+    assert ref["iters"] > 256  # the run goes past the speculative first round
+    f0, r0 = _spec_counters()
+    ctx.debug_set(6, 1)  # RSAC_DBG_SPEC_OVERFLOW
+    try:
+        R, t, m, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 3000, 30.0, sampler=sampler,
+                                        minimal=minimal, refine=False, return_info=True)
+    finally:
+        ctx.debug_set(6, 0)
+    f1, r1 = _spec_counters()
+    assert f1 - f0 == 1 and r1 - r0 == 1  # the speculative finish ran and was redone
+    assert info.best_hyp == ref["best"] and info.n_inliers == ref["n_inliers"] and info.iters == ref["iters"]
+    np.testing.assert_array_equal(m, ref["mask"])
+    assert np.array_equal(R, ref["R"]) and np.array_equal(t, ref["t"])
+
+
 @pytest.mark.parametrize("sampler,minimal", [("philox", "p3p"), ("opencv", "p3p"), ("opencv", "epnp5")])
 def test_fixed_budget_device_pick_batched(sampler, minimal):
     """adaptive off: k_scan_records picks every problem's winner on the device and the masks are

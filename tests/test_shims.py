@@ -216,3 +216,35 @@ def test_estimate_camera_orientation_rejects_gate_below_three():
     with pytest.raises(ValueError, match="min_inliers"):
         rsac.estimate_camera_orientation(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, [150], [(127, 178)],
                                          synth.TESTPRO_K_IMAGE, min_inliers=2)
+
+
+def test_solve_pnp_ransac_shim_guess_needs_rvec_tvec():
+    """cv2.solvePnPRansac asserts rvec / tvec are given when useExtrinsicGuess is set (testpro-K.py:73
+    passes the flag, False); the shim raises before any device work."""
+    with pytest.raises(rcv.error):
+        rcv.solvePnPRansac(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, synth.testpro_k_candidates()[10],
+                           np.zeros((4, 1)), useExtrinsicGuess=True, iterationsCount=100, reprojectionError=30.0)
+
+
+@pytest.mark.gpu
+def test_solve_pnp_ransac_shim_extrinsic_guess():
+    """useExtrinsicGuess=True with SOLVEPNP_ITERATIVE: the RANSAC phase is unchanged (same inliers),
+    and the final solve on those inliers starts from the caller's (rvec, tvec) -- the LM from that
+    start on the RANSAC-phase mask (the oracle's refit), not from the minimal model."""
+    pr = synth.pnp_problem(1500, 0.4, seed=61)
+    K = pr["K"]
+    ok0, rv0, tv0, in0 = rcv.solvePnPRansac(pr["points3d"], pr["points2d"], K, np.zeros((4, 1)), iterationsCount=800,
+                                            reprojectionError=30.0)
+    rv_g = rv0 + np.array([[2e-3], [-1e-3], [1e-3]])
+    tv_g = tv0 + np.array([[5.0], [-3.0], [2.0]])
+    ok, rv, tv, inl = rcv.solvePnPRansac(pr["points3d"], pr["points2d"], K, np.zeros((4, 1)), rvec=rv_g.copy(),
+                                         tvec=tv_g.copy(), useExtrinsicGuess=True, iterationsCount=800,
+                                         reprojectionError=30.0)
+    assert ok0 and ok
+    np.testing.assert_array_equal(inl, in0)
+    mask = np.zeros(len(pr["points3d"]), np.uint8)
+    mask[inl.ravel()] = 1
+    soa, cam = O.soa_pnp(pr["points3d"], pr["points2d"]), O.cam_from_K(K)
+    Rl, tl, _ = O.pnp_refine(soa, mask, cam, O.rodrigues_v2m(rv_g.ravel()).reshape(9), tv_g.ravel())
+    assert _bits_equal(tv.ravel(), tl)
+    assert _bits_equal(rcv.Rodrigues(rv)[0], rsac.rodrigues(rsac.rodrigues(Rl)))
