@@ -536,7 +536,8 @@ def extra_workloads(local, args):
                                 "epnp5_solve_ms_rvec_roundtrip": rt_ms[True], "epnp5_solve_ms_no_roundtrip": rt_ms[False],
                                 "note": "cv2.solvePnPRansac defaults (EPnP-5 minimal solver on MWC subsets, LM final "
                                         "solve) on the C2 problem, inputs in HBM, median of 10; the EPnP-5 solve "
-                                        "runs as k_epnp5_a / k_epnp5_jacobi6 (long rounds; k_epnp5_jacobi_b for adaptive first rounds) / k_epnp5_c; CPU leg in "
+                                        "runs OpenCV's operation sequence as k_cvepnp5_a / k_cvepnp5_svd (the 12 x 12 "
+                                        "JacobiSVD, a quad per hypothesis) / k_cvepnp5_c; CPU leg in "
                                         "cpu_baseline.c2_reference_mode"}
     # C1 (BASELINE.json configs[0], the reference plumbing): the reference call's own mode on its 12
     # testpro-K points under main_v1's K -- solvePnPRansac defaults (EPnP-5, MWC subsets, LM final

@@ -667,6 +667,13 @@ __device__ __forceinline__ void write_fmodel_sc(const double *R, const double *t
     const double umax = (double)fconst[7] / (2.5 * kU32);  // >= |u - cx| + |v - cy| (pnp_frame_one)
     const double qmax = fx * mag[0] + fy * mag[1] + umax * (mag[2] + eps[2]) + D0;
     const bool fits = t_ok && qmax < 1e17 && Zp < 1e17 && a * Zp < 1e30 && b < 1e30;
+    if (!fits) {
+        // every pair undecided (b = +inf) and recounted exactly; the rows are zeroed so D = 0 and
+        // t = 0 stay finite for every pair, pads included (rows past the f32 range would make D a
+        // NaN whose sign bit the fast count reads: r06, an EPnP pose with |t| ~ 1e37)
+#pragma unroll
+        for (int q = 0; q < 12; ++q) fm[q] = 0.f;
+    }
     fm[12] = fits ? (float)a : 0.f;
     fm[13] = fits ? (float)b : __builtin_inff();
     fm[14] = (float)zg;
@@ -783,8 +790,14 @@ __device__ __forceinline__ void write_fmodel_mx(const double *R, const double *t
     }
     ScBand bd = sc_band_h(eps, mag, fx, fy, wmax, T, frame, fconst);
     const double ap = bd.a * lam, bp = bd.b * lam * lam, cbp = bd.bcb * lam * lam;
-    const bool fits = t_ok && M > 0.0 && bd.qmax * lam < 1e17 && bd.Zp * lam < 1e17 && ap * bd.Zp * lam < 1e30 &&
-                      bp < 1e30 && cbp < 1e30 && bp > 1e-30;
+    // M lam <= 2^15: the scale was not clamped (|t| past ~1e36 would put f16 infinities in the
+    // operands, and the fast count would read a NaN's sign bit: r06, a degenerate EPnP pose)
+    const bool fits = t_ok && M > 0.0 && M * lam <= 0x1p15 && bd.qmax * lam < 1e17 && bd.Zp * lam < 1e17 &&
+                      ap * bd.Zp * lam < 1e30 && bp < 1e30 && cbp < 1e30 && bp > 1e-30;
+    if (!fits) {  // every pair undecided and recounted exactly; zero operands keep D = t = 0 finite
+#pragma unroll
+        for (int q = 0; q < 24; ++q) hm[q] = (_Float16)0.0f;
+    }
     fm[12] = fits ? (float)ap : 0.f;
     fm[13] = fits ? (float)bp : __builtin_inff();
     fm[14] = (float)bd.zg;

@@ -504,6 +504,30 @@ def test_f32_prefilter_nonfinite_and_huge_coordinates(score_path):
     np.testing.assert_array_equal(fast, np.resize(ref, len(batch)))
 
 
+def test_f32_prefilter_poses_past_the_f32_range(score_path):
+    """Poses whose translation leaves the range the f32 / f16 record can hold (degenerate EPnP-5
+    samples produce |t| ~ 1e37 .. 1e93, r06): the record falls back to "every pair undecided" with
+    finite zero operands, so the fast count never reads a NaN (the pads of a 300-point problem once
+    counted as inliers: 320 > n); counts equal the oracle's exact ones, for ragged problem sizes."""
+    for n in (300, 2000):
+        pr = synth.pnp_problem(n, 0.3, seed=46)
+        R, t = pr["R"], pr["t"]
+        rng = np.random.default_rng(4)
+        poses = [np.concatenate([R.reshape(9), t])]
+        for s in (1e20, 1e30, 1e36, 1e37, 3e38, 1e40, 1e93, 1e300):
+            d = rng.normal(size=3)
+            poses.append(np.concatenate([R.reshape(9), t + d / np.linalg.norm(d) * s]))
+            poses.append(np.concatenate([R.reshape(9), -t * s / np.linalg.norm(t)]))
+        poses = np.array(poses)
+        cam = O.cam_from_K(pr["K"])
+        batch, _ = _pose_batch(poses, score_path)
+        fast = rsac.score_poses(pr["points2d"], pr["points3d"], pr["K"], batch, 30.0)
+        ref = [O.pnp_count(p[:9].reshape(3, 3), p[9:], O.soa_pnp(pr["points3d"], pr["points2d"]), cam, 30.0)
+               for p in poses]
+        np.testing.assert_array_equal(fast, np.resize(ref, len(batch)))
+        assert ref[0] > 0.6 * n and max(ref[1:]) <= n
+
+
 def test_f32_prefilter_points_behind_and_on_camera_plane(score_path):
     pr = synth.pnp_problem(3000, 0.3, seed=44)
     R, t = pr["R"], pr["t"]
