@@ -80,6 +80,40 @@ RSAC_HD void svd_rotation(double p, double a, double b, double &c, double &s) {
     }
 }
 
+// Branch-free forms of hypot_glibc and svd_rotation (the GPU's anti-diagonal JacobiSVD runs up to
+// six rotations side by side, and a branch per rotation would serialise them): every case's
+// operations are computed and the one the branchy form takes is selected, so the bits are equal.
+RSAC_HD double hypot_glibc_sel(double x, double y) {
+    const double fx = dabs(x), fy = dabs(y);
+    const double ax = fx < fy ? fy : fx, ay = fx < fy ? fx : fy;
+    const bool huge = ax > 0x1p+511, tiny = !huge && ay < 0x1p-511;
+    // glibc: kernel(ax SCALE, ay SCALE) / SCALE for huge operands, kernel(ax / SCALE, ay / SCALE) SCALE
+    // for tiny ones (SCALE = 2^-600): exact power-of-two scalings either way
+    const double up = huge ? 0x1p-600 : tiny ? 0x1p+600 : 1.0, down = huge ? 0x1p+600 : tiny ? 0x1p-600 : 1.0;
+    const double sx = ax * up, sy = ay * up;
+    const double h0 = dsqrt(sx * sx + sy * sy);
+    const double d1 = h0 - sy, d2 = h0 - sx;
+    const double t1a = sx * (2.0 * d1 - sx), t2a = (d1 - 2.0 * (sx - sy)) * d1;
+    const double t1b = 2.0 * d2 * (sx - 2.0 * sy), t2b = (4.0 * d2 - sy) * sy + d2 * d2;
+    const bool first = h0 <= 2.0 * sy;
+    const double t1 = first ? t1a : t1b, t2 = first ? t2a : t2b;
+    const double h = (h0 - (t1 + t2) / (2.0 * h0)) * down;
+    const bool small = huge ? ay <= ax * 0x1p-54 : tiny ? ax >= ay / 0x1p-54 : ay <= ax * 0x1p-54;
+    double r = small ? ax + ay : h;
+    if (!dfinite(x) || !dfinite(y)) r = (__builtin_isinf(x) || __builtin_isinf(y)) ? __builtin_huge_val() : x + y;
+    return r;
+}
+RSAC_HD void svd_rotation_sel(double p, double a, double b, double &c, double &s) {
+    const double beta = a - b, gamma = hypot_glibc_sel(p, beta);
+    const bool neg = beta < 0;
+    // beta < 0: s = sqrt(((gamma - beta) 0.5) / gamma), c = p / (gamma s 2); else
+    // c = sqrt((gamma + beta) / (gamma 2)), s = p / (gamma c 2)
+    const double num = neg ? (gamma - beta) * 0.5 : gamma + beta, den = neg ? gamma : gamma * 2;
+    const double r = dsqrt(num / den), o = p / (gamma * r * 2);
+    c = neg ? o : r;
+    s = neg ? r : o;
+}
+
 RSAC_HD uint32_t rng_next(uint64_t &st) {
     st = (uint64_t)(uint32_t)st * 4164903690u + (st >> 32);
     return (uint32_t)st;
@@ -90,8 +124,11 @@ RSAC_HD uint32_t rng_next(uint64_t &st) {
 // of the decomposed matrix) are orthogonalised in cyclic pair order, W = their norms, sorted
 // descending with the rows of At and Vt, the rows of At normalised (a zero one replaced by a
 // random direction orthogonal to the earlier rows).
+// n1 (<= N): the rows normalised on exit (OpenCV's n1 = n; a zero-padded caller passes its real
+// column count).  Device code takes the branch-free rotation (svd_rotation_sel, selects for a
+// skipped pair): the same bits, and the lanes of a wave do not diverge on every pair.
 template <int M, int N>
-RSAC_HD void jacobi_svd(double (&At)[N][M], double (&Wout)[N], double (&Vt)[N][N]) {
+RSAC_HD void jacobi_svd(double (&At)[N][M], double (&Wout)[N], double (&Vt)[N][N], int n1 = N) {
     double W[N];
     constexpr int max_iter = M > 30 ? M : 30;
 #pragma unroll
@@ -114,29 +151,36 @@ RSAC_HD void jacobi_svd(double (&At)[N][M], double (&Wout)[N], double (&Vt)[N][N
                 double p = 0;
 #pragma unroll
                 for (int k = 0; k < M; ++k) p += At[i][k] * At[j][k];
-                if (dabs(p) <= kSvdEps * dsqrt(a * b)) continue;
+                const bool skip = dabs(p) <= kSvdEps * dsqrt(a * b);
+#ifndef __HIP_DEVICE_COMPILE__
+                if (skip) continue;
+#endif
                 p *= 2;
                 double c, s;
+#ifdef __HIP_DEVICE_COMPILE__
+                svd_rotation_sel(p, a, b, c, s);
+#else
                 svd_rotation(p, a, b, c, s);
+#endif
                 double na = 0, nb = 0;
 #pragma unroll
                 for (int k = 0; k < M; ++k) {
                     const double t0 = c * At[i][k] + s * At[j][k];
                     const double t1 = -s * At[i][k] + c * At[j][k];
-                    At[i][k] = t0;
-                    At[j][k] = t1;
+                    At[i][k] = skip ? At[i][k] : t0;
+                    At[j][k] = skip ? At[j][k] : t1;
                     na += t0 * t0;
                     nb += t1 * t1;
                 }
-                W[i] = na;
-                W[j] = nb;
-                changed = true;
+                W[i] = skip ? a : na;
+                W[j] = skip ? b : nb;
+                changed = changed || !skip;
 #pragma unroll
                 for (int k = 0; k < N; ++k) {
                     const double t0 = c * Vt[i][k] + s * Vt[j][k];
                     const double t1 = -s * Vt[i][k] + c * Vt[j][k];
-                    Vt[i][k] = t0;
-                    Vt[j][k] = t1;
+                    Vt[i][k] = skip ? Vt[i][k] : t0;
+                    Vt[j][k] = skip ? Vt[j][k] : t1;
                 }
             }
         if (!changed) break;
@@ -172,6 +216,7 @@ RSAC_HD void jacobi_svd(double (&At)[N][M], double (&Wout)[N], double (&Vt)[N][N
     uint64_t rng = 0x12345678;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
+        if (i >= n1) break;
         double sd = W[i];
         for (int ii = 0; ii < 100 && sd <= kDblMin; ii++) {
             const double val0 = 1. / M;
@@ -281,6 +326,37 @@ RSAC_HD void solve6(const double (&A)[6][K], const double (&b)[6], double (&x)[K
     }
 }
 
+// solve6<K> on a 6 x 5 matrix whose columns K .. 4 are zero (x[K..4] = 0 on return): the padded
+// columns' pairs are all skipped (p = +0 <= eps sqrt(a 0) = 0), they sort last with norm 0, only
+// the first K rows are normalised (n1 = K), and they add +0 to the threshold and nothing to x, so
+// x[0..K-1] are solve6<K>'s bits.  One instruction stream for the three beta estimates.
+RSAC_HD void solve6_padded(const double (&A)[6][5], int K, const double (&b)[6], double (&x)[5]) {
+    double a[5][6], w[5], v[5][5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) a[i][j] = A[j][i];
+    jacobi_svd<6, 5>(a, w, v, K);
+    double threshold = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) threshold += w[i];
+    threshold *= kDblEps * 2;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) x[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        double wi = w[i];
+        if (dabs(wi) <= threshold) continue;
+        wi = 1 / wi;
+        double s = 0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) s += a[i][j] * b[j];
+        s *= wi;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) x[j] = x[j] + s * v[i][j];
+    }
+}
+
 RSAC_HD double dot3(const double *a, const double *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
 // epnp::qr_solve of the 6 x 4 Gauss-Newton system (Householder): a vanishing column returns
@@ -357,6 +433,40 @@ RSAC_HD void gauss_newton(const double (&L)[6][10], const double (&rho)[6], doub
         qr_solve(A, b, x);
 #pragma unroll
         for (int i = 0; i < 4; i++) be[i] += x[i];
+    }
+}
+
+// find_betas_approx_1..3 on one instruction stream (the GPU's three lanes per hypothesis): the
+// column subset of L zero-padded to 6 x 5 (solve6_padded), then OpenCV's sign rules by selects
+RSAC_HD void betas_approx_padded(int approx, const double (&L)[6][10], const double (&rho)[6], double (&be)[4]) {
+    double l[6][5], x[5];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        l[i][0] = L[i][0];
+        l[i][1] = L[i][1];
+        l[i][2] = approx == 1 ? L[i][3] : L[i][2];
+        l[i][3] = approx == 1 ? L[i][6] : approx == 3 ? L[i][3] : 0.0;
+        l[i][4] = approx == 3 ? L[i][4] : 0.0;
+    }
+    solve6_padded(l, approx == 1 ? 4 : approx == 2 ? 3 : 5, rho, x);
+    if (approx == 1) {
+        const bool neg = x[0] < 0;
+        be[0] = dsqrt(neg ? -x[0] : x[0]);
+        be[1] = (neg ? -x[1] : x[1]) / be[0];
+        be[2] = (neg ? -x[2] : x[2]) / be[0];
+        be[3] = (neg ? -x[3] : x[3]) / be[0];
+    } else {
+        // approx 2 (b3 = x[0..2]) and 3 (b5 = x[0..4]) share the first two betas' rule
+        if (x[0] < 0) {
+            be[0] = dsqrt(-x[0]);
+            be[1] = (x[2] < 0) ? dsqrt(-x[2]) : 0.0;
+        } else {
+            be[0] = dsqrt(x[0]);
+            be[1] = (x[2] > 0) ? dsqrt(x[2]) : 0.0;
+        }
+        if (x[1] < 0) be[0] = -be[0];
+        be[2] = approx == 3 ? x[3] / be[0] : 0.0;
+        be[3] = 0.0;
     }
 }
 

@@ -882,12 +882,13 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 //                  fill_M + cvMulTransposed: M^T M's upper triangle, alphas and control points
 //                  into the launch-local scratch;
 //   k_cvepnp5_svd  four lanes (a quad) per hypothesis: cvSVD(M^T M)'s JacobiSVDImpl_ -- cyclic
-//                  pair order, every sum over k = 0..11 left to right: lane q holds elements
-//                  3q .. 3q + 2 of all 12 rows, a sum runs 3 additions on lane 0, moves to lane 1
-//                  by DPP, and so on (the sequential order, ~ the latency of one lane), the
-//                  rotation (hypot form) computed by all four; then the row norms, the selection
-//                  sort and the normalisation of the four smallest rows (a zero row's random
-//                  fill in memory, cvq_fill_rows);
+//                  pair order run by anti-diagonals (cvsvd_sweep: each row sees the sequential
+//                  loop's operations), every sum over k = 0..11 left to right: lane q holds
+//                  elements 3q .. 3q + 2 of all 12 rows, a sum runs 3 additions on lane 0, moves
+//                  to lane 1 by DPP, and so on (the sequential order, ~ the latency of one lane),
+//                  the rotation (hypot form) computed by all four; then the row norms, the
+//                  selection sort and the normalisation of the four smallest rows (a zero row's
+//                  random fill in memory, cvq_fill_rows);
 //   k_cvepnp5_c    three lanes per hypothesis, one beta estimate each (find_betas_approx_1..3 +
 //                  gauss_newton + compute_R_and_t), epnp::compute_pose's pick, the Rodrigues
 //                  round trip of the (rvec, tvec) model, the records.
@@ -1027,33 +1028,49 @@ __device__ __attribute__((noinline)) void cvq_fill_rows(double *E) {
     for (int k = 0; k < 48; ++k) E[k] = A[96 + k];
 }
 
-// rotation (i = row B[0], j = row B[J]) of one cyclic sweep; the rows live in a register file rotated
-// by one row after each i (B[0] = row i, B[1 .. 11 - i] = rows i + 1 .. 11)
-template <int J>
+// One sweep of JacobiSVDImpl_'s cyclic order (i < j, i outer) on the quad.  Rotation (i, j) reads
+// rows i and j as the last earlier rotation touching each left them, so the pairs of one
+// anti-diagonal i + j = t (disjoint rows) are independent, and running t = 1 .. 21 in turn, each
+// t's pairs side by side, gives every row the sequential loop's operations in its order: 21
+// dependent steps per sweep instead of 66.  The rotations are branch-free (svd_rotation_sel; a
+// skipped pair keeps its rows and norms by selects), so a step's six rotations interleave.
+template <int I, int J>
 __device__ __forceinline__ void cvsvd_pair(double (&B)[12][3], double (&W)[12], bool &changed) {
-    double p = quad_sum(B[0][0] * B[J][0], B[0][1] * B[J][1], B[0][2] * B[J][2]);
-    const double a = W[0], b = W[J];
-    if (dabs(p) <= cvq::kSvdEps * dsqrt(a * b)) return;  // quad-uniform: p, a, b are the quad's
-    p *= 2;
+    const double p = quad_sum(B[I][0] * B[J][0], B[I][1] * B[J][1], B[I][2] * B[J][2]);
+    const double a = W[I], b = W[J];
+    const bool skip = dabs(p) <= cvq::kSvdEps * dsqrt(a * b);  // quad-uniform: p, a, b are the quad's
     double c, s;
-    cvq::svd_rotation(p, a, b, c, s);
+    cvq::svd_rotation_sel(p * 2, a, b, c, s);
     double t0[3], t1[3];
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
-        t0[e] = c * B[0][e] + s * B[J][e];
-        t1[e] = -s * B[0][e] + c * B[J][e];
-        B[0][e] = t0[e];
-        B[J][e] = t1[e];
+        t0[e] = c * B[I][e] + s * B[J][e];
+        t1[e] = -s * B[I][e] + c * B[J][e];
     }
-    W[0] = quad_sum(t0[0] * t0[0], t0[1] * t0[1], t0[2] * t0[2]);
-    W[J] = quad_sum(t1[0] * t1[0], t1[1] * t1[1], t1[2] * t1[2]);
-    changed = true;
+    const double na = quad_sum(t0[0] * t0[0], t0[1] * t0[1], t0[2] * t0[2]);
+    const double nb = quad_sum(t1[0] * t1[0], t1[1] * t1[1], t1[2] * t1[2]);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        B[I][e] = skip ? B[I][e] : t0[e];
+        B[J][e] = skip ? B[J][e] : t1[e];
+    }
+    W[I] = skip ? a : na;
+    W[J] = skip ? b : nb;
+    changed = changed || !skip;
 }
-template <int J>
-__device__ __forceinline__ void cvsvd_row(double (&B)[12][3], double (&W)[12], bool &changed, int last) {
-    if constexpr (J <= 11) {
-        if (J <= last) cvsvd_pair<J>(B, W, changed);
-        cvsvd_row<J + 1>(B, W, changed, last);
+// the pairs (I, T - I), I < T - I <= 11, of anti-diagonal T
+template <int T, int I>
+__device__ __forceinline__ void cvsvd_diag(double (&B)[12][3], double (&W)[12], bool &changed) {
+    if constexpr (I < T - I) {
+        if constexpr (T - I <= 11) cvsvd_pair<I, T - I>(B, W, changed);
+        cvsvd_diag<T, I + 1>(B, W, changed);
+    }
+}
+template <int T>
+__device__ __forceinline__ void cvsvd_sweep(double (&B)[12][3], double (&W)[12], bool &changed) {
+    if constexpr (T <= 21) {
+        cvsvd_diag<T, 0>(B, W, changed);
+        cvsvd_sweep<T + 1>(B, W, changed);
     }
 }
 
@@ -1076,23 +1093,14 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
         }
 #pragma unroll
     for (int r = 0; r < 12; ++r) W[r] = quad_sum(B[r][0] * B[r][0], B[r][1] * B[r][1], B[r][2] * B[r][2]);
+    // OpenCV's loop: sweeps until one changes nothing (at most max(m, 30) = 30); a quad that is
+    // done idles (masked) while the wave's other quads sweep on
+    bool active = true;
     for (int iter = 0; iter < 30; ++iter) {
         bool changed = false;
-        for (int i = 0; i < 12; ++i) {
-            cvsvd_row<1>(B, W, changed, 11 - i);
-            // rotate the register file by one row: row i parks at the end
-            double b0[3] = {B[0][0], B[0][1], B[0][2]}, w0 = W[0];
-#pragma unroll
-            for (int r = 0; r < 11; ++r) {
-#pragma unroll
-                for (int e = 0; e < 3; ++e) B[r][e] = B[r + 1][e];
-                W[r] = W[r + 1];
-            }
-#pragma unroll
-            for (int e = 0; e < 3; ++e) B[11][e] = b0[e];
-            W[11] = w0;
-        }
-        if (!changed) break;
+        if (active) cvsvd_sweep<1>(B, W, changed);
+        active = active && changed;
+        if (!__any(active)) break;
     }
     // the row norms, the selection sort (descending, first maximum), the normalisation
 #pragma unroll
@@ -1173,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
                 for (int j = 0; j < 3; ++j) cw.cws[i][j] = E[kCvCws + 3 * i + j];
             cvq::epnp_rho(cw, rho);
         }
-        cvq::betas_approx(c + 1, L, rho, be);
+        cvq::betas_approx_padded(c + 1, L, rho, be);  // one instruction stream for the three lanes
         cvq::gauss_newton(L, rho, be);
         int32_t idx[5];
         (void)epnp5_sample(a, rec, h, n, idx);
@@ -1765,23 +1773,15 @@ __device__ __attribute__((noinline)) void mf_sc_unit(KernargPnp ka, int prob, in
 // the waves a block's barriers wait for get the SIMD first (C2 scoring -1 %, scripts/mf_ab.py r03d).
 // (The static-priority and hand-scheduled asm probes of rounds 3-4 are kept as
 // scripts/ubench/probes_r04.patch; DESIGN.md §3 has their numbers.)
-#ifndef RSAC_MF_LONG_W
-#define RSAC_MF_LONG_W 4
-#endif
-#ifndef RSAC_MF_SHORT_W
-#define RSAC_MF_SHORT_W 2
-#endif
-// the batch instance (W = RSAC_MF_SHORT_W: many short problems, C3) loads iteration i + 1's point
+constexpr int kMfLongW = 4;   // waves per block for one long problem
+constexpr int kMfShortW = 2;  // waves per block for batches of short problems (C3)
+// the batch instance (W = kMfShortW: many short problems, C3) loads iteration i + 1's point
 // operands before iteration i computes: its problems' points miss L2 more often (C3 92 % hits
 // against C2's 98 %, profiles/r05/pmc_scorer_c2_c3.json) and the prefetch took C3 0.956 -> 0.931 ms,
-// while the long-problem instance ran 4 % slower with it (scripts/mf_ab.py, r05)
-#ifndef RSAC_MF_PREFETCH_W
-#define RSAC_MF_PREFETCH_W RSAC_MF_SHORT_W
-#endif
-#ifndef RSAC_MF_TID_OPAQUE
-#define RSAC_MF_TID_OPAQUE 1
-#endif
-constexpr int kMfW = RSAC_MF_LONG_W;  // A/B knob (scripts/build_ab.sh): waves per block for one long problem
+// while the long-problem instance ran 4 % slower with it (scripts/mf_ab.py, r05).  (The A/B
+// builds of these choices and of mf_tid's opacity are scripts/ubench/mf_knobs_r05.patch.)
+constexpr int kMfPrefetchW = kMfShortW;
+constexpr int kMfW = kMfLongW;
 constexpr int kWrec = 64;        // flagged iterations a wave lists per unit
 
 // the thread index as a value the compiler cannot hoist: the unit's lane-dependent offsets are then
@@ -1789,9 +1789,7 @@ constexpr int kWrec = 64;        // flagged iterations a wave lists per unit
 // where at the 168-VGPR budget of 3 waves/SIMD they were spilled (548 B of scratch per lane, r04)
 __device__ __forceinline__ int mf_tid() {
     int t = (int)threadIdx.x;
-#if RSAC_MF_TID_OPAQUE  // A/B knob (scripts/build_ab.sh): 0 lets the compiler hoist again
     asm volatile("" : "+v"(t));
-#endif
     return t;
 }
 
@@ -1863,7 +1861,7 @@ __device__ __forceinline__ void mf_unit(const PnpArgs &a, int prob, int64_t h0, 
     };
     const int full = n >= b0 + 64 ? (n - b0 - 64) / T + 1 : 0;  // iterations with 64 points in range
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (W == RSAC_MF_PREFETCH_W) {
+    if constexpr (W == kMfPrefetchW) {
     if (full > 0) {  // the next iteration's operands in flight while this one computes
         mf_h8 Ba, Bb;
         float2 ua, ub;
@@ -2815,10 +2813,7 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 
 // rounds of at most this many hypotheses (problems x hypotheses) are solved 4 lanes per
 // hypothesis (k_pnp_solve4); larger ones one lane per hypothesis (k_pnp_solve)
-#ifndef RSAC_SOLVE4_MAX
-#define RSAC_SOLVE4_MAX 4096
-#endif
-constexpr int64_t kSolve4MaxHyps = RSAC_SOLVE4_MAX;
+constexpr int64_t kSolve4MaxHyps = 4096;
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
                             double *frame, float *fconst, hipStream_t s, const PnpPrepare *prep) {
@@ -3022,7 +3017,7 @@ static hipError_t launch_mf_w(const PnpArgs &a, int32_t P_, int64_t hyp_begin, i
 }
 static hipError_t launch_mf(const PnpArgs &a, int32_t P_, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s) {
-    if (P_ > 1 && a.max_n <= kMfShortN) return launch_mf_w<RSAC_MF_SHORT_W>(a, P_, hyp_begin, H, counts, s);
+    if (P_ > 1 && a.max_n <= kMfShortN) return launch_mf_w<kMfShortW>(a, P_, hyp_begin, H, counts, s);
     return launch_mf_w<kMfW>(a, P_, hyp_begin, H, counts, s);
 }
 

@@ -26,23 +26,32 @@
  *   - homography RANSAC (MWC sampler, OpenCV getSubset/checkSubset, f32 error,
  *     RANSAC-phase mask) is pinned against the 24 complete findHomography
  *     blocks recorded in the reference's debug.log (tests/golden/);
- *   - PnP: both minimal kernels are restated -- OpenCV's default
- *     SOLVEPNP_ITERATIVE kernel, EPnP on 5-point MWC samples (orc_pnp_minimal_epnp5,
- *     the mode every reference call site runs), and the north-star P3P kernel
- *     (Lambda Twist, Persson & Nordberg, ECCV 2018) -- in this project's own
- *     numerics (OpenCV is absent).  PnP parity vs OpenCV is therefore *unpinned*
- *     except for the loose known-answer camera origin of testpro-K.py:234; GPU
- *     parity is against this restatement.
+ *   - PnP, OpenCV's default minimal solver (EPnP on 5-point MWC samples, the mode every reference
+ *     call site runs) and the Rodrigues round trip of its models are OpenCV's own operation
+ *     sequence (cv_epnp.c: undistortPoints' f32 round trip, epnp.cpp, lapack.cpp's JacobiSVD,
+ *     cvRodrigues2), unfused, and the default here (ORC_SEQ_CV).  The round-4/5 restatement of that
+ *     solver (ORC_SEQ_RR: round-robin Jacobi, fused steps) stays for the decision-change study
+ *     (scripts/epnp_variants.py, profiles/r06/epnp_variants.md), as does its unfused build
+ *     (liboracle_unfused.so).  PnP parity vs OpenCV itself is *unpinned* (OpenCV is absent) except
+ *     for the loose known-answer camera origin of testpro-K.py:234; GPU parity is against this
+ *     restatement.
+ *   - The north-star P3P kernel (Lambda Twist, Persson & Nordberg, ECCV 2018; OpenCV's P3P is a
+ *     different algorithm and no reference call selects it), the LM refit, the non-minimal EPnP of
+ *     the P3P mode's final solve and the fundamental-matrix solver are this project's own
+ *     arithmetic: explicit fma() where the GPU fuses (the same correctly rounded result on every
+ *     backend).
  *   - OpenCV's count == model_points branches ([OpenCV, unvendored] solvepnp.cpp
- *     solvePnPRansac: 4 points, or 5 under the default flags -> one solvePnP on
- *     all points, every index an inlier, no final solve; fundam.cpp
- *     findHomography: 4 points -> runKernel, mask all ones, no LM) are restated
- *     in pnp_direct and orc_hom_ransac.
+ *     solvePnPRansac: 4 points, or 5 under the default flags -> one solvePnP on all points, every
+ *     index an inlier, no final solve; fundam.cpp findHomography: 4 points -> runKernel, mask all
+ *     ones, no LM) are restated in pnp_direct and orc_hom_ransac.
  *
- * Numerics contract shared with the HIP path (bit-exact on counts/masks):
- *   compile with -ffp-contract=off, no -ffast-math; only + - * / sqrt in any
- *   quantity that decides a count; f64 projection of f32-rounded inputs,
- *   rounded to f32, f32 squared error, `err <= (float)(thr*thr)`.
+ * Numerics contract shared with the HIP path (bit-exact on counts/masks/models):
+ *   compile with -ffp-contract=off, no -ffast-math; every quantity that decides a count is
+ *   computed as OpenCV computes it where OpenCV defines it (computeError: f64 projection of
+ *   f32-rounded inputs, rounded to f32, f32 squared error, `err <= (float)(thr*thr)`; the EPnP-5
+ *   models above; the homography DLT and error), with only + - * / sqrt (libm's hypot, acos, sin
+ *   and cos restated deterministically); fused operations appear only in the project's own
+ *   solvers listed above, written explicitly as fma().
  */
 #include <math.h>
 #include <stdint.h>

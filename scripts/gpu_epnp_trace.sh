@@ -15,8 +15,8 @@ f=$(find gpurun_out/ep/kt -name "*kernel_trace.csv" | head -1)
 python3 - "$f" <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
-# the last ms-to-best call's kernels (epnp5/philox): every kernel from the last k_epnp5_a on
-last = max(i for i, r in enumerate(rows) if "k_epnp5_a" in r["Kernel_Name"])
+# the last ms-to-best call's kernels (epnp5/philox): every kernel from the last k_cvepnp5_a on
+last = max(i for i, r in enumerate(rows) if "k_cvepnp5_a" in r["Kernel_Name"])
 t0 = int(rows[last]["Start_Timestamp"])
 for r in rows[last:last + 16]:
     print("  %-40s start %8.1f us  dur %8.1f us" % (r["Kernel_Name"][:40], (int(r["Start_Timestamp"]) - t0) / 1e3,
