@@ -356,18 +356,23 @@ def sec_roofline(cfg, kernel, kernel_ms, span):
     per launch from profiles/pmc_secondary.json (scripts/gpu_secondary_profile.sh +
     scripts/summarize_secondary.py: its own --pmc passes of the same workload), divided by the
     launch's duration measured here (kernel_ms; `span` says how).  kernel_ms None: the kernel
-    trace's mean duration from the same JSON."""
+    trace's mean duration from the same JSON.  kernel None: the config's dominant kernel (the
+    largest share of the trace's kernel time)."""
     try:
         d = json.load(open(os.path.join(ROOT, "profiles", "pmc_secondary.json")))
-        e = d["configs"][cfg]["kernels"][kernel]
-    except (OSError, KeyError, ValueError):
+        ks = d["configs"][cfg]["kernels"]
+        kernel = kernel or next(iter(ks))
+        e = ks[kernel]
+        tag = d["configs"][cfg].get("tag", d.get("tag"))
+    except (OSError, KeyError, ValueError, StopIteration):
         return None
     src = "profile"
     if not kernel_ms:
         kernel_ms, src = e["mean_us"] / 1e3, "kernel trace mean (profiles/pmc_secondary.json)"
     t_s = kernel_ms * 1e-3
     r = {"bound": "valu_issue", "kernel": kernel, "kernel_ms": kernel_ms, "span": span if src == "profile" else src,
-         "peak": VALU_ISSUE_PEAK / 1e9, "unit": "G VALU wave-instructions/s", "profile": d.get("tag")}
+         "peak": VALU_ISSUE_PEAK / 1e9, "unit": "G VALU wave-instructions/s", "profile": tag,
+         "share_of_kernel_time": e.get("share")}
     v = e.get("valu_instr_per_launch")
     if v:
         r.update({"valu_instr_per_launch": v, "achieved": v / t_s / 1e9, "frac": v / t_s / VALU_ISSUE_PEAK})
@@ -472,8 +477,48 @@ def extra_workloads(local, args):
             walls.append(time.perf_counter() - t)
     out["location_search"] = {"locations": len(lp["locations"]), "features": len(lp["pos3d"]),
                               "ms": statistics.median(walls) * 1e3,
+                              "roofline": sec_roofline("loc", None, None, ""),
                               "note": "find_homographies of main_v1.py:254-297 (OpenCV-sampler RANSAC + LM refit + "
-                                      "err1/err2) for every candidate, one call"}
+                                      "err1/err2) for every candidate, one call, host arrays; the roofline is the "
+                                      "dominant kernel of the call's kernel trace (profiles/pmc_secondary.json 'loc'); "
+                                      "CPU legs in cpu_baseline.location_search"}
+    # the K sweep (testpro-K.py:39-162): 27 intrinsics x the 12 points, the reference's own mode
+    # (EPnP-5 on MWC subsets, LM final solve), then solvePnPRefineLM of the winner; host arrays
+    walls = []
+    for i in range(8):
+        t = time.perf_counter()
+        ks = rsac.estimate_camera_orientation(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS, synth.TESTPRO_K_FOCALS,
+                                              synth.TESTPRO_K_SENSORS, synth.TESTPRO_K_IMAGE, device=local,
+                                              return_info=True)
+        if i >= 2:
+            walls.append(time.perf_counter() - t)
+    fs = [(f, s) for f in synth.TESTPRO_K_FOCALS for s in synth.TESTPRO_K_SENSORS]
+    out["k_sweep"] = {"intrinsics": len(fs), "points": 12, "ms": statistics.median(walls) * 1e3,
+                      "pick": {"focal_mm": fs[ks.best][0], "sensor_mm": list(fs[ks.best][1])} if ks.best >= 0 else None,
+                      "accepted": int(np.sum(np.asarray(ks.ok))),
+                      "roofline": sec_roofline("ksweep", None, None, ""),
+                      "note": "rsac.estimate_camera_orientation on testpro-K.py:198-234 (27 Ks: 9 focal lengths x "
+                              "3 film cells), one call sequence: the batched RANSACs, the gate, the mean inlier "
+                              "errors, the pick, the LM refit; median of 6; CPU legs in cpu_baseline.k_sweep"}
+    # C3 at the per-rank loads of N = 8 / 4 / 2 / 1 GPUs (128 .. 1024 problems of 2000 points x 1024
+    # hypotheses): the one-GPU curve the multi-GPU problem shards follow
+    scal = {}
+    for P in (128, 256, 512, 1024):
+        n_pts = int(off[P])
+        a2, a3 = p2[:n_pts], p3[:n_pts]
+        ws = []
+        for i in range(8):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            rsac.pnp_ransac_batched_flat(a2, a3, off[:P + 1], Ks[:P], 1024, args.thr, adaptive=False, refine=False)
+            torch.cuda.synchronize()
+            if i >= 2:
+                ws.append(time.perf_counter() - t)
+        w = statistics.median(ws)
+        scal[str(P)] = {"ms": w * 1e3, "hyp_s": P * 1024 / w}
+    out["c3_per_rank_loads"] = dict(scal, note="C3 problem shards as one GPU sees them at 8 / 4 / 2 / 1 ranks "
+                                             "(128 / 256 / 512 / 1024 problems x 2000 points x 1024 hypotheses, "
+                                             "one batched call, inputs in HBM, median of 6)")
     out["dem_ray_march"] = dem_workload(local)
     # the final solve on the C2 problem's inliers: ms-to-best-model for each refit choice
     p2c = synth.pnp_problem(args.points, 0.5, seed=0)
@@ -538,7 +583,8 @@ def extra_workloads(local, args):
                                         "solve) on the C2 problem, inputs in HBM, median of 10; the EPnP-5 solve "
                                         "runs OpenCV's operation sequence as k_cvepnp5_a / k_cvepnp5_svd (the 12 x 12 "
                                         "JacobiSVD, a quad per hypothesis) / k_cvepnp5_c; CPU leg in "
-                                        "cpu_baseline.c2_reference_mode"}
+                                        "cpu_baseline.c2_reference_mode",
+                                "roofline": sec_roofline("epnp", None, None, "")}
     # C1 (BASELINE.json configs[0], the reference plumbing): the reference call's own mode on its 12
     # testpro-K points under main_v1's K -- solvePnPRansac defaults (EPnP-5, MWC subsets, LM final
     # solve), 1000 iterations cap, thr 30; host arrays in and out, as the reference passes them
@@ -723,6 +769,27 @@ def cpu_baseline(pr, args):
     r5m = O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000, threads=threads)
     _, w_c5mt = _median_rate(lambda: O.pnp_ransac_lo(p5["points3d"], p5["points2d"], p5["K"], args.thr, 0.99, 5000,
                                                      threads=threads), 1)
+    # location search (main_v1.py:254-297): the reference's loop over the 458 candidates, each
+    # find_homography (pos2, the C restatement's findHomography, the literal err1/err2 loop), 1 thread
+    # and the candidates over the threads
+    lp = synth.location_problem(seed=0)
+
+    def loc_one(c):
+        return O.find_homography(lp["pixels"], lp["pos3d"], c, 75.0)
+
+    _, w_loc = _median_rate(lambda: [loc_one(c) for c in lp["locations"]], 1, samples=3)
+
+    def loc_mt():
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            list(ex.map(loc_one, lp["locations"]))
+
+    _, w_loc_mt = _median_rate(loc_mt, 1, samples=3)
+    # the K sweep (testpro-K.py:39-162): 27 RANSACs + refits, 1 thread and the Ks over the threads
+    Ks27 = synth.testpro_k_candidates()
+    ks1 = O.estimate_camera_orientation(P3, P2, Ks27, threads=1)
+    _, w_ks = _median_rate(lambda: O.estimate_camera_orientation(P3, P2, Ks27, threads=1), 1, samples=5)
+    _, w_ks_mt = _median_rate(lambda: O.estimate_camera_orientation(P3, P2, Ks27, threads=min(threads, 27)), 1,
+                              samples=5)
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -768,6 +835,16 @@ def cpu_baseline(pr, args):
                              "sample": "configs[0] with K from testpro-K.py (f 150 mm, 127 x 178 mm cell: the K "
                                        "test_pro.py:801-802 prints), otherwise as c1, median of 21 after 3 "
                                        "warm-ups"},
+            "location_search": {"ms": w_loc * 1e3, "ms_mt": w_loc_mt * 1e3, "cores": 1, "cores_mt": threads,
+                                "sample": "the 458 candidates of rsac.synth.location_problem: pyoracle.find_homography "
+                                          "per candidate (main_v1.py:300-348 + 419 restated: pos2, the C findHomography "
+                                          "with OpenCV's sampler + refit, the literal err1/err2 loop), 1 thread and "
+                                          f"the candidates over {threads} threads, median of 3"},
+            "k_sweep": {"ms": w_ks * 1e3, "ms_mt": w_ks_mt * 1e3, "cores": 1, "cores_mt": min(threads, 27),
+                        "pick": int(ks1["best"]),
+                        "sample": "pyoracle.estimate_camera_orientation on testpro-K.py:198-234 (27 Ks, EPnP-5 on "
+                                  "MWC subsets, the oracle's LM refits), the Ks on 1 thread and over "
+                                  f"{min(threads, 27)} threads, median of 5"},
             "c3": {"hyp_s": rate_c3, "cores": threads,
                    "sample": f"32 of the 1024 problems x 1024 hypotheses, problems over {threads} threads, "
                              f"median of 5 ({w_c3:.2f} s each)"},

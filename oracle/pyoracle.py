@@ -458,7 +458,7 @@ def reproj_mean(points3d, points2d, K, R, t, mask):
 
 
 def estimate_camera_orientation(pos3d, pixels, Ks, thr=30.0, confidence=0.99, max_iters=5000, seed=0x5EED,
-                                sampler="opencv", min_inliers=6, minimal="epnp5", rvec=None):
+                                sampler="opencv", min_inliers=6, minimal="epnp5", rvec=None, threads=None):
     """testpro-K.py:39-125 restated on the oracle's pieces: per K the RANSAC (pnp_ransac) + the LM
     final solve on its inliers (solvePnPRansac's SOLVEPNP_ITERATIVE final solvePnP), the gate,
     the mean inlier error through the pose's Rodrigues vector, the first strict minimum, then
@@ -475,7 +475,7 @@ def estimate_camera_orientation(pos3d, pixels, Ks, thr=30.0, confidence=0.99, ma
     # the per-K RANSACs are independent (ctypes drops the GIL): run them on a thread pool, then
     # select in the reference's loop order
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(max_workers=min(len(Ks), os.cpu_count() or 1, 16)) as ex:
+    with ThreadPoolExecutor(max_workers=threads or min(len(Ks), os.cpu_count() or 1, 16)) as ex:
         runs = list(ex.map(lambda K: pnp_ransac(P3, P2, K, thr, confidence, max_iters, seed, sampler=sampler,
                                                 minimal=minimal, rvec=rvec), Ks))
     # solvePnPRansac's count == model_points branch (4 points; 5 under EPnP-5) has no final solve

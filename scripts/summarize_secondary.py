@@ -22,7 +22,12 @@ HBM_PEAK = 8e12
 CONFIGS = {"c2": "C2 bench step: 100k P3P hypotheses x 10k points (evaluate_range)",
            "c3": "C3: 1024 problems x 2000 points x 1024 hypotheses, one batched call",
            "c4": "C4: fundamental matrix, 50k matches, 100k hypotheses, adaptive off",
-           "c5": "C5: LO-RANSAC, 100k points, adaptive + LO + LM refit"}
+           "c5": "C5: LO-RANSAC, 100k points, adaptive + LO + LM refit",
+           "loc": "location search (main_v1.py:254-297): 458 candidates x 13 features, OpenCV-sampler "
+                  "homography RANSAC + refit + err1/err2, one call",
+           "ksweep": "K sweep (testpro-K.py:39-162): 12 points x 27 intrinsics, reference mode (EPnP-5 on MWC "
+                     "subsets, LM final solve), one call",
+           "epnp": "reference-mode minimal solver: 20k EPnP-5 hypotheses on MWC subsets over the C2 problem"}
 
 
 def short(name):
@@ -85,8 +90,18 @@ def main():
             ks[k] = e
         out["configs"][w] = {"workload": desc, "kernels": ks}
     out["tag"] = tag
-    for name in (f"{tag}_pmc_secondary.json", "pmc_secondary.json"):  # the untagged copy is read by bench.py
-        json.dump(out, open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
+    json.dump(out, open(os.path.join(ROOT, "profiles", f"{tag}_pmc_secondary.json"), "w"), indent=1)
+    # the untagged copy, read by bench.py, keeps the configs this pass did not profile
+    merged = os.path.join(ROOT, "profiles", "pmc_secondary.json")
+    try:
+        prev = json.load(open(merged))
+    except (OSError, ValueError):
+        prev = {"configs": {}}
+    for w, d in out["configs"].items():
+        d["tag"] = tag
+        prev["configs"][w] = d
+    prev.update({k: v for k, v in out.items() if k != "configs"})
+    json.dump(prev, open(merged, "w"), indent=1)
     for w, d in out["configs"].items():
         print(w)
         for k, e in list(d["kernels"].items())[:6]:

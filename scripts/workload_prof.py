@@ -1,12 +1,15 @@
 """One BASELINE workload alone, for rocprofv3 passes (kernel trace and separate --pmc passes) that
 attribute every kernel to its config (scripts/gpu_secondary_profile.sh):
 
-    python3 scripts/workload_prof.py c2|c3|c4|c5 [repeats]
+    python3 scripts/workload_prof.py c2|c3|c4|c5|loc|ksweep|epnp [repeats]
 
 c2: the bench step (rsac.evaluate_range, 100k hypotheses over the 10k-point problem: solve + score
     + key + mask); c3: pnp_ransac_batched_flat over 1024 x 2000 points, 1024 hypotheses each; c4:
     fundamental_ransac, 50k matches, 100k hypotheses, adaptive off; c5: pnp_ransac(lo=True) on the
-    100k-point problem (the LO chain: k_pnp_refine with a source record + k_pnp_lo_count).
+    100k-point problem (the LO chain: k_pnp_refine with a source record + k_pnp_lo_count); loc:
+    location_search over the 458 synthetic candidates (main_v1.py:254-297); ksweep:
+    estimate_camera_orientation on testpro-K's 12 points x 27 intrinsics (testpro-K.py:39-162,
+    reference mode); epnp: 20k EPnP-5 hypotheses on MWC subsets, adaptive off (k_cvepnp5_*).
 Inputs resident in HBM, as in bench.py.
 """
 import os
@@ -40,6 +43,18 @@ elif which == "c5":
     p5 = synth.pnp_problem(100_000, 0.5, seed=3)
     q2, q3 = torch.from_numpy(p5["points2d"]).to(dev), torch.from_numpy(p5["points3d"]).to(dev)
     run = lambda: rsac.pnp_ransac(q2, q3, p5["K"], 5000, 30.0, lo=True, refine=True)
+elif which == "loc":  # find_homographies of main_v1.py:254-297 for the 458 candidates, one call
+    lp = synth.location_problem(seed=0)
+    run = lambda: rsac.location_search(lp["pos3d"], lp["pixels"], lp["locations"], 75.0)
+elif which == "ksweep":  # estimate_camera_orientation of testpro-K.py:39-162, the reference's own mode
+    run = lambda: rsac.estimate_camera_orientation(synth.TESTPRO_K_POS3D, synth.TESTPRO_K_PIXELS,
+                                                   synth.TESTPRO_K_FOCALS, synth.TESTPRO_K_SENSORS,
+                                                   synth.TESTPRO_K_IMAGE)
+elif which == "epnp":  # the reference mode's minimal solver at a fixed 20k budget on the C2 problem
+    pr = synth.pnp_problem(10_000, 0.5, seed=0)
+    p2, p3 = torch.from_numpy(pr["points2d"]).to(dev), torch.from_numpy(pr["points3d"]).to(dev)
+    run = lambda: rsac.pnp_ransac(p2, p3, pr["K"], 20_000, 30.0, sampler="opencv", minimal="epnp5", adaptive=False,
+                                  refine=False)
 else:
     raise SystemExit(f"unknown workload {which}")
 walls = []
