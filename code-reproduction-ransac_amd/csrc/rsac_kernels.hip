@@ -1096,10 +1096,21 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
     // OpenCV's loop: sweeps until one changes nothing (at most max(m, 30) = 30); a quad that is
     // done idles (masked) while the wave's other quads sweep on
     bool active = true;
+#ifdef RSAC_TRACE
+    unsigned long long tr_c = __builtin_amdgcn_s_memtime(), tr_r = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int iter = 0; iter < 30; ++iter) {
         bool changed = false;
         if (active) cvsvd_sweep<1>(B, W, changed);
         active = active && changed;
+#ifdef RSAC_TRACE
+        if (hl == 0 && q == 0) {
+            const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            printf("svd sweep %d: %llu cycles %llu ticks changed %d\n", iter, c1 - tr_c, r1 - tr_r, (int)changed);
+            tr_c = c1;
+            tr_r = r1;
+        }
+#endif
         if (!__any(active)) break;
     }
     // the row norms, the selection sort (descending, first maximum), the normalisation
@@ -3297,6 +3308,32 @@ struct GpuLmReducer {
     double (*accs)[kLmRed] = nullptr;  // LDS [2][kLmRed]: pnp_lm_refine's normal equations
     double *res = nullptr;             // LDS [1]: a cost reduction's result
     __device__ double *acc_buf(int k) { return accs[k]; }
+    // the LM step's solve (Cholesky, Cayley map, step test: ~300 dependent f64 operations) runs
+    // on wave 0 alone, not on the 8 waves two to a SIMD; the block reads the candidate from
+    // LDS.  Two alternating buffers: wave 0 writes buffer k + 1 while the others may still read k.
+    static constexpr bool kSolveStep = true;
+    double (*steps)[16] = nullptr;  // LDS [2][16]: Rn[9], tn[3], ok, small
+    int nstep = 0;
+    __device__ bool solve_step(const double *acc, double lam, const double *R, const double *t, double *Rn,
+                               double *tn, bool &small) {
+        double *sb = steps[nstep++ & 1];
+        if (threadIdx.x < 64) {
+            double r[9], u[3];
+            bool sm = false;
+            const bool ok = lm_solve_step(acc, lam, R, t, r, u, sm);
+            if (threadIdx.x == 0) {
+                for (int j = 0; j < 9; ++j) sb[j] = r[j];
+                for (int j = 0; j < 3; ++j) sb[9 + j] = u[j];
+                sb[12] = ok ? 1.0 : 0.0;
+                sb[13] = sm ? 1.0 : 0.0;
+            }
+        }
+        __syncthreads();
+        for (int j = 0; j < 9; ++j) Rn[j] = sb[j];
+        for (int j = 0; j < 3; ++j) tn[j] = sb[9 + j];
+        small = sb[13] != 0.0;
+        return sb[12] != 0.0;
+    }
 
     __device__ void range_of(int r, int &lo, int &hi) const {
         const int C = lm_chunk(n);
@@ -3587,20 +3624,22 @@ struct GpuLmReducer {
                             acc);
     }
 #ifdef RSAC_TRACE
-    unsigned long long stamp[96];
+    unsigned long long stamp[96], cyc[96];
     int phase_of[96];
     int ns = 0;
     __device__ void mark(int phase) {
         __syncthreads();
         if (ns < 96) {
             stamp[ns] = __builtin_amdgcn_s_memrealtime();
+            cyc[ns] = __builtin_amdgcn_s_memtime();
             phase_of[ns++] = phase;
         }
     }
     __device__ void dump() {
         if (threadIdx.x == 0 && blockIdx.x == 0)
             for (int i = 1; i < ns; ++i)
-                printf("trace %d->%d %llu ticks\n", phase_of[i - 1], phase_of[i], stamp[i] - stamp[i - 1]);
+                printf("trace %d->%d %llu ticks %llu cycles\n", phase_of[i - 1], phase_of[i], stamp[i] - stamp[i - 1],
+                       cyc[i] - cyc[i - 1]);
     }
 #endif
     __device__ double cost(const double *R, const double *t) {
@@ -3633,7 +3672,7 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
                                                            double *host_models, const double *src,
                                                            const int32_t *stop, int stride, int32_t *fail) {
     __shared__ double wsum[kLmThreads / 64][kLmRed];
-    __shared__ double accs[2][kLmRed], res[1];
+    __shared__ double accs[2][kLmRed], res[1], steps[2][16];
     __shared__ int scan[kLmThreads / 64];
     __shared__ int rtab[2][kLmMaxBlocks];
     __shared__ __attribute__((aligned(16))) char lds[kLmLdsBytes];  // 94 KB
@@ -3669,6 +3708,7 @@ __global__ __launch_bounds__(kLmThreads) void k_pnp_refine(PnpArgs a, const uint
     red.wsums = (double *)(lds + 5 * kLmStage * 4);
     red.accs = accs;
     red.res = res;
+    red.steps = steps;
     red.set_ranges(blockIdx.x, nb > 1 ? stride : 1);
     double R[9], t[3];
     for (int j = 0; j < 9; ++j) R[j] = ms[j];

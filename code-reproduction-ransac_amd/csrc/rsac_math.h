@@ -980,6 +980,32 @@ struct LmFused<Red, decltype((void)Red::kFused)> {
     static constexpr bool value = Red::kFused;
 };
 
+// One LM step's solve: d from (A + lam diag(A)) d = -J^T r (false: not positive definite), the
+// candidate Rn = Cay(d) R, tn = t + d[3..5], and CvLevMarq's step criterion on it, |d| <
+// FLT_EPSILON (|tn| + 1) (used only if the candidate is accepted, when tn becomes t).
+RSAC_HD bool lm_solve_step(const double *acc, double lam, const double *R, const double *t, double *Rn, double *tn,
+                           bool &small) {
+    double d[6];
+    if (!chol6_solve_packed(acc, lam, d)) return false;
+    cayley_apply(d, R, Rn);
+    for (int j = 0; j < 3; ++j) tn[j] = t[j] + d[3 + j];
+    double dd = 0, tt = 0;
+    for (int j = 0; j < 6; ++j) dd += d[j] * d[j];
+    for (int j = 0; j < 3; ++j) tt += tn[j] * tn[j];
+    small = dsqrt(dd) < 1.1920928955078125e-07 * (dsqrt(tt) + 1.0);
+    return true;
+}
+// A reducer with kSolveStep = true provides solve_step(...) = lm_solve_step(...) (the GPU
+// reducer: one wave solves, the block reads the result)
+template <class Red, class = void>
+struct LmSolveStep {
+    static constexpr bool value = false;
+};
+template <class Red>
+struct LmSolveStep<Red, decltype((void)Red::kSolveStep)> {
+    static constexpr bool value = Red::kSolveStep;
+};
+
 // Red::acc_buf(k), k = 0, 1: two buffers of kLmTerms doubles for the current and the next
 // normal equations (the GPU reducer's are in LDS, written by its reductions)
 template <class Red>
@@ -1009,15 +1035,15 @@ RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
         RSAC_TRACE_MARK(red, 12);
         bool accepted = false;
         while (!accepted) {
-            double d[6];
-            if (!chol6_solve_packed(acc, lam, d)) {
+            double Rn[9], tn[3];
+            bool small, ok;
+            if constexpr (LmSolveStep<Red>::value) ok = red.solve_step(acc, lam, R, t, Rn, tn, small);
+            else ok = lm_solve_step(acc, lam, R, t, Rn, tn, small);
+            if (!ok) {
                 lam *= 10;
                 if (lam > 1e10) return it;
                 continue;
             }
-            double Rn[9], tn[3];
-            cayley_apply(d, R, Rn);
-            for (int j = 0; j < 3; ++j) tn[j] = t[j] + d[3 + j];
             RSAC_TRACE_MARK(red, 13);
             double cn;
             if constexpr (fused) cn = red.cost_normal(Rn, tn, acc_next);
@@ -1033,10 +1059,7 @@ RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
                 accepted = true;
                 // converged: negligible cost decrease, or a step below FLT_EPSILON relative to
                 // the pose (CvLevMarq's criterion for solvePnP, on |d| / (|t| + 1))
-                double dd = 0, tt = 0;
-                for (int j = 0; j < 6; ++j) dd += d[j] * d[j];
-                for (int j = 0; j < 3; ++j) tt += t[j] * t[j];
-                if (rel < 1e-12 || dsqrt(dd) < 1.1920928955078125e-07 * (dsqrt(tt) + 1.0)) return it + 1;
+                if (rel < 1e-12 || small) return it + 1;
             } else {
                 lam *= 10;
                 if (lam > 1e10) return it;

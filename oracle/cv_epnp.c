@@ -98,6 +98,11 @@ static uint32_t cvq_rng_next(uint64_t *st) {
  * per matrix size n (tests/test_cv_epnp.py checks that the degenerate fixtures reach the branch) */
 static long g_fill[16];
 ORC_API long orc_cvq_fill_events(int n) { return n >= 0 && n < 16 ? g_fill[n] : 0; }
+/* study hook (scripts/jacobi_sweeps.py): per matrix size n, how many decompositions ran k sweeps,
+ * and how many rotations (pairs not skipped) sweep k made in total */
+static long g_sweeps[16][32], g_rots[16][32];
+ORC_API long orc_cvq_sweep_hist(int n, int k) { return n >= 0 && n < 16 && k >= 0 && k < 32 ? g_sweeps[n][k] : 0; }
+ORC_API long orc_cvq_rot_hist(int n, int k) { return n >= 0 && n < 16 && k >= 0 && k < 32 ? g_rots[n][k] : 0; }
 
 ORC_API void cvq_jacobi_svd(double *At, int astep, double *Wout, double *Vt, int vstep, int m, int n, int n1) {
     const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
@@ -115,7 +120,8 @@ ORC_API void cvq_jacobi_svd(double *At, int astep, double *Wout, double *Vt, int
             Vt[i * vstep + i] = 1;
         }
     }
-    for (int iter = 0; iter < max_iter; ++iter) {
+    int iter;
+    for (iter = 0; iter < max_iter; ++iter) {
         int changed = 0;
         for (int i = 0; i < n - 1; ++i)
             for (int j = i + 1; j < n; ++j) {
@@ -145,6 +151,7 @@ ORC_API void cvq_jacobi_svd(double *At, int astep, double *Wout, double *Vt, int
                 W[i] = a;
                 W[j] = b;
                 changed = 1;
+                if (n < 16 && iter < 32) __atomic_fetch_add(&g_rots[n][iter], 1, __ATOMIC_RELAXED);
                 if (Vt) {
                     double *Vi = Vt + i * vstep, *Vj = Vt + j * vstep;
                     for (int k = 0; k < n; ++k) {
@@ -157,6 +164,7 @@ ORC_API void cvq_jacobi_svd(double *At, int astep, double *Wout, double *Vt, int
             }
         if (!changed) break;
     }
+    if (n < 16) __atomic_fetch_add(&g_sweeps[n][iter < max_iter ? iter + 1 : 31], 1, __ATOMIC_RELAXED);
     for (int i = 0; i < n; ++i) {
         double sd = 0;
         for (int k = 0; k < m; ++k) {
