@@ -881,14 +881,12 @@ __global__ __launch_bounds__(256) void k_pnp_solve(PnpArgs a, int64_t hyp_begin,
 //                  the control points (cvSVD of PW0^T PW0), the barycentric alphas (cvInvert),
 //                  fill_M + cvMulTransposed: M^T M's upper triangle, alphas and control points
 //                  into the launch-local scratch;
-//   k_cvepnp5_svd  four lanes (a quad) per hypothesis: cvSVD(M^T M)'s JacobiSVDImpl_ -- cyclic
-//                  pair order run by anti-diagonals (cvsvd_sweep: each row sees the sequential
-//                  loop's operations), every sum over k = 0..11 left to right: lane q holds
-//                  elements 3q .. 3q + 2 of all 12 rows, a sum runs 3 additions on lane 0, moves
-//                  to lane 1 by DPP, and so on (the sequential order, ~ the latency of one lane),
-//                  the rotation (hypot form) computed by all four; then the row norms, the
-//                  selection sort and the normalisation of the four smallest rows (a zero row's
-//                  random fill in memory, cvq_fill_rows);
+//   k_cvepnp5_svd  six lanes per hypothesis, ten per wave: cvSVD(M^T M)'s JacobiSVDImpl_ -- the
+//                  cyclic pair order run by anti-diagonals (each row sees the sequential loop's
+//                  operations), lane m making pair m of each diagonal on rows kept in LDS, every
+//                  sum over k = 0..11 left to right in one lane; then the row norms, the selection
+//                  sort and the normalisation of the four smallest rows (a zero row's random fill
+//                  in memory, cvq_fill_rows);
 //   k_cvepnp5_c    three lanes per hypothesis, one beta estimate each (find_betas_approx_1..3 +
 //                  gauss_newton + compute_R_and_t), epnp::compute_pose's pick, the Rodrigues
 //                  round trip of the (rvec, tvec) model, the records.
@@ -957,33 +955,7 @@ __global__ __launch_bounds__(256) void k_cvepnp5_a(PnpArgs a, int64_t hyp_begin,
     a.status[rec] = st;
 }
 
-// 2 of 3: the 12 x 12 JacobiSVD on a quad per hypothesis
-// DPP within a quad: lane q takes lane q - 1's value (lane 0 its own) / every lane takes lane 3's
-__device__ __forceinline__ double quad_dpp(double v, int ctrl) {
-    const int lo = __double2loint(v), hi = __double2hiint(v);
-    int rlo, rhi;
-    if (ctrl == 0x90) {
-        rlo = __builtin_amdgcn_mov_dpp(lo, 0x90, 0xF, 0xF, false);
-        rhi = __builtin_amdgcn_mov_dpp(hi, 0x90, 0xF, 0xF, false);
-    } else {
-        rlo = __builtin_amdgcn_mov_dpp(lo, 0xFF, 0xF, 0xF, false);
-        rhi = __builtin_amdgcn_mov_dpp(hi, 0xFF, 0xF, 0xF, false);
-    }
-    return __hiloint2double(rhi, rlo);
-}
-// sum over k = 0..11 of x[k] left to right, from +0, where lane q of the quad holds x[3q .. 3q + 2];
-// every lane returns the sum
-__device__ __forceinline__ double quad_sum(double x0, double x1, double x2) {
-    double s = 0.0;
-    s = s + x0; s = s + x1; s = s + x2;
-#pragma unroll
-    for (int hop = 0; hop < 3; ++hop) {
-        s = quad_dpp(s, 0x90);
-        s = s + x0; s = s + x1; s = s + x2;
-    }
-    return quad_dpp(s, 0xFF);
-}
-
+// 2 of 3: the 12 x 12 JacobiSVD, six lanes per hypothesis
 // JacobiSVDImpl_'s tail in memory (one lane, the rare case of a row norm <= DBL_MIN): the selection
 // sort of the 12 rows by their norms and the normalisation of every row, a zero one replaced by
 // RNG(0x12345678)'s random direction projected off the earlier rows (rsac_cvepnp.h jacobi_svd);
@@ -1028,97 +1000,120 @@ __device__ __attribute__((noinline)) void cvq_fill_rows(double *E) {
     for (int k = 0; k < 48; ++k) E[k] = A[96 + k];
 }
 
-// One sweep of JacobiSVDImpl_'s cyclic order (i < j, i outer) on the quad.  Rotation (i, j) reads
+// JacobiSVDImpl_'s cyclic pair order (i < j, i outer) run by anti-diagonals: rotation (i, j) reads
 // rows i and j as the last earlier rotation touching each left them, so the pairs of one
-// anti-diagonal i + j = t (disjoint rows) are independent, and running t = 1 .. 21 in turn, each
-// t's pairs side by side, gives every row the sequential loop's operations in its order: 21
-// dependent steps per sweep instead of 66.  The rotations are branch-free (svd_rotation_sel; a
-// skipped pair keeps its rows and norms by selects), so a step's six rotations interleave.
-template <int I, int J>
-__device__ __forceinline__ void cvsvd_pair(double (&B)[12][3], double (&W)[12], bool &changed) {
-    const double p = quad_sum(B[I][0] * B[J][0], B[I][1] * B[J][1], B[I][2] * B[J][2]);
-    const double a = W[I], b = W[J];
-    const bool skip = dabs(p) <= cvq::kSvdEps * dsqrt(a * b);  // quad-uniform: p, a, b are the quad's
-    double c, s;
-    cvq::svd_rotation_sel(p * 2, a, b, c, s);
-    double t0[3], t1[3];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        t0[e] = c * B[I][e] + s * B[J][e];
-        t1[e] = -s * B[I][e] + c * B[J][e];
-    }
-    const double na = quad_sum(t0[0] * t0[0], t0[1] * t0[1], t0[2] * t0[2]);
-    const double nb = quad_sum(t1[0] * t1[0], t1[1] * t1[1], t1[2] * t1[2]);
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        B[I][e] = skip ? B[I][e] : t0[e];
-        B[J][e] = skip ? B[J][e] : t1[e];
-    }
-    W[I] = skip ? a : na;
-    W[J] = skip ? b : nb;
-    changed = changed || !skip;
+// anti-diagonal i + j = t (disjoint rows) are independent, and running t = 1 .. 21 in turn gives every
+// row the sequential loop's operations in its order.  Lane m of a hypothesis's six owns pair
+// i = max(0, t - 11) + m of diagonal t (at most six pairs): it reads rows i, j and their norms from
+// the hypothesis's LDS copy of the matrix, makes OpenCV's whole rotation on them alone (every sum
+// over k = 0..11 left to right in one lane), and writes them back.  The six lanes are one wave's:
+// its LDS operations execute in order, so a diagonal reads what the last one wrote without a barrier
+// (lds_wave_order keeps the compiler from moving them).  A sweep is 21 dependent steps of one
+// rotation per lane, where the quad layout (r06 first cut) ran all 66 on every lane.  A hypothesis
+// whose sweep changed nothing stays as it is in further sweeps (every pair skips again), so the wave
+// sweeps until none of its hypotheses changed (at most OpenCV's 30).
+constexpr int kSvdHpw = 10;      // hypotheses per wave (60 of 64 lanes)
+constexpr int kSvdStride = 158;  // LDS doubles per hypothesis: rows [12][12], norms [12], 16-B pad
+__device__ __forceinline__ void lds_wave_order() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
 }
-// the pairs (I, T - I), I < T - I <= 11, of anti-diagonal T
-template <int T, int I>
-__device__ __forceinline__ void cvsvd_diag(double (&B)[12][3], double (&W)[12], bool &changed) {
-    if constexpr (I < T - I) {
-        if constexpr (T - I <= 11) cvsvd_pair<I, T - I>(B, W, changed);
-        cvsvd_diag<T, I + 1>(B, W, changed);
+__device__ __forceinline__ void cvsvd_load_row(const double *S, int r, double (&x)[12]) {
+    const double2 *v = (const double2 *)(S + 12 * r);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const double2 w = v[k];
+        x[2 * k] = w.x;
+        x[2 * k + 1] = w.y;
     }
 }
-template <int T>
-__device__ __forceinline__ void cvsvd_sweep(double (&B)[12][3], double (&W)[12], bool &changed) {
-    if constexpr (T <= 21) {
-        cvsvd_diag<T, 0>(B, W, changed);
-        cvsvd_sweep<T + 1>(B, W, changed);
-    }
+__device__ __forceinline__ void cvsvd_store_row(double *S, int r, const double (&x)[12]) {
+    double2 *v = (double2 *)(S + 12 * r);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = make_double2(x[2 * k], x[2 * k + 1]);
 }
 
 __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    extern __shared__ __attribute__((aligned(16))) double svd_lds[];  // [waves][kSvdHpw][kSvdStride]
     const int prob = blockIdx.y;
-    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-    const int hl = gt >> 2, q = gt & 3;
-    const bool live = hl < H;  // a quad shares its hypothesis: every branch below is quad-uniform
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane / 6, m = lane - 6 * g;
+    const int hl = (blockIdx.x * (int)(blockDim.x >> 6) + wave) * kSvdHpw + g;
+    if (g >= kSvdHpw || hl >= H) return;  // six-lane-uniform from here on
     const int64_t rec = (int64_t)prob * a.hyp_stride + hyp_begin + hl;
-    if (!(live && a.status[rec] > 0)) return;
+    if (a.status[rec] <= 0) return;
     double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;
-    // At = (M^T M)^T = M^T M: element (r, 3q + e) from the upper triangle
-    double B[12][3], W[12];
+    double *S = svd_lds + (wave * kSvdHpw + g) * kSvdStride;  // row r at S[12 r], norms at S[144]
+    // At = (M^T M)^T = M^T M from the upper triangle: lane m fills rows 2m, 2m + 1 and their
+    // squared norms (JacobiSVDImpl_'s W)
 #pragma unroll
-    for (int r = 0; r < 12; ++r)
+    for (int rr = 0; rr < 2; ++rr) {
+        const int r = 2 * m + rr;
+        double x[12], sd = 0;
 #pragma unroll
-        for (int e = 0; e < 3; ++e) {
-            const int c = 3 * q + e, lo = r < c ? r : c, hi = r < c ? c : r;
-            B[r][e] = E[lo * 12 - lo * (lo - 1) / 2 + (hi - lo)];
+        for (int c = 0; c < 12; ++c) {
+            const int lo = r < c ? r : c, hi = r < c ? c : r;
+            x[c] = E[lo * 12 - lo * (lo - 1) / 2 + (hi - lo)];
+            sd += x[c] * x[c];
         }
-#pragma unroll
-    for (int r = 0; r < 12; ++r) W[r] = quad_sum(B[r][0] * B[r][0], B[r][1] * B[r][1], B[r][2] * B[r][2]);
-    // OpenCV's loop: sweeps until one changes nothing (at most max(m, 30) = 30); a quad that is
-    // done idles (masked) while the wave's other quads sweep on
-    bool active = true;
-#ifdef RSAC_TRACE
-    unsigned long long tr_c = __builtin_amdgcn_s_memtime(), tr_r = __builtin_amdgcn_s_memrealtime();
-#endif
+        cvsvd_store_row(S, r, x);
+        S[144 + r] = sd;
+    }
+    lds_wave_order();
     for (int iter = 0; iter < 30; ++iter) {
         bool changed = false;
-        if (active) cvsvd_sweep<1>(B, W, changed);
-        active = active && changed;
-#ifdef RSAC_TRACE
-        if (hl == 0 && q == 0) {
-            const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-            printf("svd sweep %d: %llu cycles %llu ticks changed %d\n", iter, c1 - tr_c, r1 - tr_r, (int)changed);
-            tr_c = c1;
-            tr_r = r1;
+        for (int t = 1; t <= 21; ++t) {
+            const int i = (t > 11 ? t - 11 : 0) + m, j = t - i;
+            if (i < j) {
+                double Ai[12], Aj[12];
+                cvsvd_load_row(S, i, Ai);
+                cvsvd_load_row(S, j, Aj);
+                const double wa = S[144 + i], wb = S[144 + j];
+                double p = 0;
+#pragma unroll
+                for (int k = 0; k < 12; ++k) p += Ai[k] * Aj[k];
+                if (!(dabs(p) <= cvq::kSvdEps * dsqrt(wa * wb))) {
+                    double c, s;
+                    cvq::svd_rotation_sel(p * 2, wa, wb, c, s);
+                    double na = 0, nb = 0;
+#pragma unroll
+                    for (int k = 0; k < 12; ++k) {
+                        const double t0 = c * Ai[k] + s * Aj[k];
+                        const double t1 = -s * Ai[k] + c * Aj[k];
+                        Ai[k] = t0;
+                        Aj[k] = t1;
+                        na += t0 * t0;
+                        nb += t1 * t1;
+                    }
+                    cvsvd_store_row(S, i, Ai);
+                    cvsvd_store_row(S, j, Aj);
+                    S[144 + i] = na;
+                    S[144 + j] = nb;
+                    changed = true;
+                }
+            }
+            lds_wave_order();
         }
-#endif
-        if (!__any(active)) break;
+        if (!__any(changed)) break;
     }
     // the row norms, the selection sort (descending, first maximum), the normalisation
 #pragma unroll
-    for (int r = 0; r < 12; ++r) W[r] = dsqrt(quad_sum(B[r][0] * B[r][0], B[r][1] * B[r][1], B[r][2] * B[r][2]));
+    for (int rr = 0; rr < 2; ++rr) {
+        const int r = 2 * m + rr;
+        double x[12], sd = 0;
+        cvsvd_load_row(S, r, x);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) sd += x[k] * x[k];
+        S[144 + r] = dsqrt(sd);
+    }
+    lds_wave_order();
+    double W[12];
     int perm[12];
 #pragma unroll
-    for (int r = 0; r < 12; ++r) perm[r] = r;
+    for (int r = 0; r < 12; ++r) {
+        W[r] = S[144 + r];
+        perm[r] = r;
+    }
 #pragma unroll
     for (int i = 0; i < 11; ++i) {
         int j = i;
@@ -1133,33 +1128,33 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
             }
     }
     if (W[11] > cvq::kDblMin) {
-        // rows 8 .. 11 (every row's norm > DBL_MIN: no random fill anywhere), times 1 / norm
+        // rows 8 .. 11 (every row's norm > DBL_MIN: no random fill anywhere), times 1 / norm: lane
+        // m < 4 writes row 8 + m
+        if (m < 4) {
+            int r = 0;
+            double w = 0;
 #pragma unroll
-        for (int p = 8; p < 12; ++p) {
-            const double inv = 1 / W[p];
-            double v[3] = {0, 0, 0};
-#pragma unroll
-            for (int r = 0; r < 12; ++r)
-                if (perm[p] == r) {
-                    v[0] = B[r][0]; v[1] = B[r][1]; v[2] = B[r][2];
+            for (int q = 0; q < 4; ++q)
+                if (q == m) {
+                    r = perm[8 + q];
+                    w = W[8 + q];
                 }
+            const double inv = 1 / w;
+            double x[12];
+            cvsvd_load_row(S, r, x);
 #pragma unroll
-            for (int e = 0; e < 3; ++e) E[(p - 8) * 12 + 3 * q + e] = v[e] * inv;
+            for (int k = 0; k < 12; ++k) E[m * 12 + k] = x[k] * inv;
         }
         return;
     }
-    // a row of zero norm: the rows and their (unsorted) norms to memory, lane 0 finishes in memory
-#pragma unroll
-    for (int r = 0; r < 12; ++r)
-#pragma unroll
-        for (int e = 0; e < 3; ++e) E[kCvRows + 12 * r + 3 * q + e] = B[r][e];
-#pragma unroll
-    for (int r = 0; r < 12; ++r) {
-        const double wr = dsqrt(quad_sum(B[r][0] * B[r][0], B[r][1] * B[r][1], B[r][2] * B[r][2]));  // every lane: DPP
-        if (q == 0) E[kCvW + r] = wr;
+    // a row of zero norm: lane 0 puts the rows and their (unsorted) norms in memory and finishes there
+    if (m == 0) {
+        for (int r = 0; r < 12; ++r) {
+            for (int k = 0; k < 12; ++k) E[kCvRows + 12 * r + k] = S[12 * r + k];
+            E[kCvW + r] = S[144 + r];
+        }
+        cvq_fill_rows(E);
     }
-    __threadfence();
-    if (q == 0) cvq_fill_rows(E);
 }
 
 // 3 of 3: lane c of a group of three takes estimate c + 1, then epnp::compute_pose's pick,
@@ -2906,7 +2901,8 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
         const bool short_round = (int64_t)P * H <= 2048;
         const int tb = short_round ? 64 : 256;
         hipLaunchKernelGGL(k_cvepnp5_a, dim3(cdiv(H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
-        hipLaunchKernelGGL(k_cvepnp5_svd, dim3(cdiv(4 * (int64_t)H, tb), P), dim3(tb), 0, s, ka, hyp_begin, H);
+        hipLaunchKernelGGL(k_cvepnp5_svd, dim3(cdiv(cdiv(H, kSvdHpw), tb / 64), P), dim3(tb),
+                           (tb / 64) * kSvdHpw * kSvdStride * sizeof(double), s, ka, hyp_begin, H);
         const int hpw = 21;  // hypotheses per wave of stage 3 (3 lanes each)
         hipLaunchKernelGGL(k_cvepnp5_c, dim3(cdiv(cdiv(H, hpw), tb / 64), P), dim3(tb), 0, s, ka, hyp_begin, H, hpw);
     }
