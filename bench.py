@@ -582,7 +582,7 @@ def extra_workloads(local, args):
                                 "note": "cv2.solvePnPRansac defaults (EPnP-5 minimal solver on MWC subsets, LM final "
                                         "solve) on the C2 problem, inputs in HBM, median of 10; the EPnP-5 solve "
                                         "runs OpenCV's operation sequence as k_cvepnp5_a / k_cvepnp5_svd (the 12 x 12 "
-                                        "JacobiSVD, a quad per hypothesis) / k_cvepnp5_c; CPU leg in "
+                                        "JacobiSVD, six lanes per hypothesis) / k_cvepnp5_c; CPU leg in "
                                         "cpu_baseline.c2_reference_mode",
                                 "roofline": sec_roofline("epnp", None, None, "")}
     # C1 (BASELINE.json configs[0], the reference plumbing): the reference call's own mode on its 12

@@ -1060,21 +1060,48 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
         S[144 + r] = sd;
     }
     lds_wave_order();
+#ifdef RSAC_TRACE
+    // per-phase cycle sums of lane 0 (s_memtime after the phase's values exist)
+    unsigned long long tr_c[4] = {0, 0, 0, 0}, tr_prev = 0;
+    int tr_n[2] = {0, 0};
+#define TR_STAMP(k, v)                                                          \
+    do {                                                                        \
+        const double tr_v = (v);                                                \
+        asm volatile("; trace sink %0" ::"v"(tr_v) : "memory");                 \
+        __builtin_amdgcn_s_waitcnt(0);                                          \
+        const unsigned long long now = __builtin_amdgcn_s_memtime();            \
+        tr_c[k] += now - ((k) == 0 ? c0 : tr_prev);                             \
+        tr_prev = now;                                                          \
+    } while (0)
+#endif
     for (int iter = 0; iter < 30; ++iter) {
         bool changed = false;
         for (int t = 1; t <= 21; ++t) {
             const int i = (t > 11 ? t - 11 : 0) + m, j = t - i;
             if (i < j) {
+#ifdef RSAC_TRACE
+                const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
                 double Ai[12], Aj[12];
                 cvsvd_load_row(S, i, Ai);
                 cvsvd_load_row(S, j, Aj);
                 const double wa = S[144 + i], wb = S[144 + j];
+#ifdef RSAC_TRACE
+                TR_STAMP(0, Ai[11] + Aj[11] + wa + wb);
+#endif
                 double p = 0;
 #pragma unroll
                 for (int k = 0; k < 12; ++k) p += Ai[k] * Aj[k];
-                if (!(dabs(p) <= cvq::kSvdEps * dsqrt(wa * wb))) {
+                const bool rot = !(dabs(p) <= cvq::kSvdEps * dsqrt(wa * wb));
+#ifdef RSAC_TRACE
+                TR_STAMP(1, p + wa);
+#endif
+                if (rot) {
                     double c, s;
                     cvq::svd_rotation_sel(p * 2, wa, wb, c, s);
+#ifdef RSAC_TRACE
+                    TR_STAMP(2, c + s);
+#endif
                     double na = 0, nb = 0;
 #pragma unroll
                     for (int k = 0; k < 12; ++k) {
@@ -1090,12 +1117,23 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
                     S[144 + i] = na;
                     S[144 + j] = nb;
                     changed = true;
+#ifdef RSAC_TRACE
+                    TR_STAMP(3, na + nb);
+#endif
                 }
+#ifdef RSAC_TRACE
+                tr_n[rot ? 1 : 0]++;
+#endif
             }
             lds_wave_order();
         }
         if (!__any(changed)) break;
     }
+#ifdef RSAC_TRACE
+    if (hl == 0 && m == 0)
+        printf("svd lane0: rotations %d skips %d | cycles load %llu p+test %llu rot-cs %llu update+store %llu\n", tr_n[1],
+               tr_n[0], tr_c[0], tr_c[1], tr_c[2], tr_c[3]);
+#endif
     // the row norms, the selection sort (descending, first maximum), the normalisation
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
@@ -1206,6 +1244,9 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
 #pragma unroll
             for (int k = 0; k < 12; ++k) v[i][k] = E[(3 - i) * 12 + k];
         err = cvq::epnp5_r_and_t(e, v, be, R, t);
+        // the (rvec, tvec) model's Rodrigues(Rodrigues(R)) on every lane before the pick: the
+        // three run side by side instead of the winner's after it
+        if (a.rvec_rt) rodrigues_roundtrip(R);
     }
     // epnp::compute_pose's pick over the group's three lanes (estimates 1, 2, 3)
     const int base = 3 * g;
@@ -1217,10 +1258,7 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
     for (int k = 0; k < 3; ++k) t[k] = __shfl(t[k], src);
     if (!live || c != 0) return;
     // OpenCV's EPnP always reports a pose (a degenerate sample's NaN scores no inlier)
-    if (st > 0) {
-        st = 1;
-        if (a.rvec_rt) rodrigues_roundtrip(R);
-    }
+    if (st > 0) st = 1;
     double *m = a.models + rec * kModelStride;
 #pragma unroll
     for (int q = 0; q < 9; ++q) m[q] = R[q];
