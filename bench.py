@@ -519,6 +519,25 @@ def extra_workloads(local, args):
     out["c3_per_rank_loads"] = dict(scal, note="C3 problem shards as one GPU sees them at 8 / 4 / 2 / 1 ranks "
                                              "(128 / 256 / 512 / 1024 problems x 2000 points x 1024 hypotheses, "
                                              "one batched call, inputs in HBM, median of 6)")
+    # the alternative split: every rank all 1024 problems, 1024 / N hypotheses each
+    hsh = {}
+    n_all = int(off[1024])
+    for Hs in (128, 256, 512):
+        ws = []
+        for i in range(8):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            rsac.pnp_ransac_batched_flat(p2[:n_all], p3[:n_all], off[:1025], Ks[:1024], Hs, args.thr, adaptive=False,
+                                         refine=False)
+            torch.cuda.synchronize()
+            if i >= 2:
+                ws.append(time.perf_counter() - t)
+        w = statistics.median(ws)
+        hsh[str(Hs)] = {"ms": w * 1e3, "hyp_s": 1024 * Hs / w}
+    out["c3_hyp_shard_loads"] = dict(hsh, note="C3 hypothesis shards as one GPU would see them at 8 / 4 / 2 ranks "
+                                             "(1024 problems x 2000 points x 128 / 256 / 512 hypotheses, one batched "
+                                             "call, inputs in HBM, median of 6; the shards' winners would need one "
+                                             "all-reduce per problem)")
     out["dem_ray_march"] = dem_workload(local)
     # the final solve on the C2 problem's inliers: ms-to-best-model for each refit choice
     p2c = synth.pnp_problem(args.points, 0.5, seed=0)

@@ -1244,9 +1244,6 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
 #pragma unroll
             for (int k = 0; k < 12; ++k) v[i][k] = E[(3 - i) * 12 + k];
         err = cvq::epnp5_r_and_t(e, v, be, R, t);
-        // the (rvec, tvec) model's Rodrigues(Rodrigues(R)) on every lane before the pick: the
-        // three run side by side instead of the winner's after it
-        if (a.rvec_rt) rodrigues_roundtrip(R);
     }
     // epnp::compute_pose's pick over the group's three lanes (estimates 1, 2, 3)
     const int base = 3 * g;
@@ -1257,8 +1254,13 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
 #pragma unroll
     for (int k = 0; k < 3; ++k) t[k] = __shfl(t[k], src);
     if (!live || c != 0) return;
-    // OpenCV's EPnP always reports a pose (a degenerate sample's NaN scores no inlier)
-    if (st > 0) st = 1;
+    // OpenCV's EPnP always reports a pose (a degenerate sample's NaN scores no inlier); the
+    // winner's (rvec, tvec) model is Rodrigues(Rodrigues(R)) (on all three lanes before the pick
+    // the stage took 85 instead of 78 us, r06)
+    if (st > 0) {
+        st = 1;
+        if (a.rvec_rt) rodrigues_roundtrip(R);
+    }
     double *m = a.models + rec * kModelStride;
 #pragma unroll
     for (int q = 0; q < 9; ++q) m[q] = R[q];
