@@ -1280,14 +1280,16 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
 // lanes pick the smallest error, the lowest candidate on ties (= pnp_minimal's first-one rule),
 // and the winner writes the record.  Results equal k_pnp_solve's bit for bit.
 
-__global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin, int32_t H) {
+template <int L>
+__global__ __launch_bounds__(256) void k_pnp_solve_l(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    constexpr int CPL = 4 / L;  // Lambda Twist candidates per lane: lane c takes c CPL .. c CPL + CPL - 1
     const int prob = blockIdx.y;
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-    const int hl = gt >> 2, cand = gt & 3;
+    const int hl = gt / L, lc = gt % L;
     if (gt == 0 && prob == 0) {
         if (a.queue) reset_pnp_queue(a.queue);
     }
-    const bool live = hl < H;  // the 4 lanes of a hypothesis share it: shuffles stay in the group
+    const bool live = hl < H;  // the L lanes of a hypothesis share it: shuffles stay in the group
     const int64_t h = hyp_begin + hl;
     const int64_t p0 = a.offsets[prob];
     const int n = (int)(a.offsets[prob + 1] - p0);
@@ -1307,7 +1309,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
     }
     double R[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[3] = {0, 0, 0};
     double e = 0.0;
-    bool mine = false;  // this lane's candidate was emitted with a usable error
+    int mine = 4;  // the lane's first smallest-error candidate (4: none emitted with a usable error)
     const Cam k{a.cams[4 * prob], a.cams[4 * prob + 1], a.cams[4 * prob + 2], a.cams[4 * prob + 3]};
     if (st > 0) {
         float X[4], Y[4], Z[4], U[4], V[4];
@@ -1322,27 +1324,31 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
             bearing(k, U[j], V[j], yb + 3 * j);
             xw[3 * j] = X[j]; xw[3 * j + 1] = Y[j]; xw[3 * j + 2] = Z[j];
         }
-        LtCommon L;
+        LtCommon Lc;
         double w0, w1, tau[2];
-        if (lt_common(yb, xw, L) && lt_sign(L, cand >> 1, w0, w1, tau)) {
-            auto emit = [&](const double *Rk, const double *tk) {
-                const double ek = pnp_fourth_error(Rk, tk, X, Y, Z, U, V, k);
-                if (!(ek == ek)) return;
-                mine = true;
-                e = ek;
+        if (lt_common(yb, xw, Lc) && lt_sign(Lc, (lc * CPL) >> 1, w0, w1, tau)) {
+            for (int r = 0; r < CPL; ++r) {
+                const int cand = lc * CPL + r;
+                auto emit = [&](const double *Rk, const double *tk) {
+                    const double ek = pnp_fourth_error(Rk, tk, X, Y, Z, U, V, k);
+                    if (!(ek == ek)) return;
+                    if (mine < 4 && !(ek < e)) return;  // the first smallest stays
+                    mine = cand;
+                    e = ek;
 #pragma unroll
-                for (int q = 0; q < 9; ++q) R[q] = Rk[q];
+                    for (int q = 0; q < 9; ++q) R[q] = Rk[q];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) t[q] = tk[q];
-            };
-            (void)lt_tau(L, w0, w1, tau[cand & 1], yb, xw, emit);
+                    for (int q = 0; q < 3; ++q) t[q] = tk[q];
+                };
+                (void)lt_tau(Lc, w0, w1, tau[cand & 1], yb, xw, emit);
+            }
         }
     }
-    // the group's winner: smallest e, then the lowest candidate (all 4 lanes agree)
-    int win = mine ? cand : 4;
-    double we = mine ? e : 0.0;
+    // the group's winner: smallest e, then the lowest candidate (all L lanes agree)
+    int win = mine;
+    double we = mine < 4 ? e : 0.0;
 #pragma unroll
-    for (int o = 1; o < 4; o <<= 1) {
+    for (int o = 1; o < L; o <<= 1) {
         const int ow = __shfl_xor(win, o);
         const double oe = __shfl_xor(we, o);
         if (ow < 4 && (win == 4 || oe < we || (oe == we && ow < win))) {
@@ -1352,7 +1358,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve4(PnpArgs a, int64_t hyp_begin
     }
     if (!live) return;
     const bool ok = win < 4;
-    if (ok ? cand != win : cand != 0) return;  // one writer per hypothesis
+    if (ok ? mine != win : lc != 0) return;  // one writer per hypothesis
     const int8_t sv = st > 0 ? (ok ? 1 : 0) : st;
     double *m = a.models + rec * kModelStride;
     if (sv > 0 && a.rvec_rt) rodrigues_roundtrip(R);
@@ -2858,7 +2864,7 @@ hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, f
 }
 
 // rounds of at most this many hypotheses (problems x hypotheses) are solved 4 lanes per
-// hypothesis (k_pnp_solve4); larger ones one lane per hypothesis (k_pnp_solve)
+// hypothesis (k_pnp_solve_l<4>); larger ones one lane per hypothesis (k_pnp_solve)
 constexpr int64_t kSolve4MaxHyps = 4096;
 
 hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t *ws, float *XC, float *YC, float *ZC,
@@ -2932,6 +2938,12 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
     return hipGetLastError();
 }
 
+// rounds up to this many hypotheses (one lane each: <= 4 waves per SIMD) run the P3P solve on two
+// lanes per hypothesis, two Lambda Twist candidates each (r06, scripts/gpu_r06_solve2.sh: the
+// kernel 33.6 -> 36 us but the C2 step 0.2600 -> 0.2580 ms in three interleaved rounds, as the
+// solve of one step overlaps the other stream's scoring better); larger rounds (C3) stay on one
+constexpr int64_t kSolve2MaxHyps = 262144;
+
 hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
     PnpArgs ka = round_args(a, P, H);
     if (a.sample_k == 5) {  // EPnP-5 in OpenCV's sequence: k_cvepnp5_a / _svd / _c
@@ -2948,7 +2960,9 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     }
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     else if ((int64_t)P * H <= kSolve4MaxHyps)
-        hipLaunchKernelGGL(k_pnp_solve4, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+        hipLaunchKernelGGL(k_pnp_solve_l<4>, dim3(cdiv(4 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
+    else if ((int64_t)P * H <= kSolve2MaxHyps)
+        hipLaunchKernelGGL(k_pnp_solve_l<2>, dim3(cdiv(2 * (int64_t)H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     else
         hipLaunchKernelGGL(k_pnp_solve, dim3(cdiv(H, 256), P), dim3(256), 0, s, ka, hyp_begin, H);
     return hipGetLastError();

@@ -337,7 +337,7 @@ RSAC_HD int p3p_pose(double l1, double l2, double l3, double a12, double a13, do
 }
 
 // The Lambda Twist solver in three pieces, so that the GPU can also run the (up to 4)
-// candidates of one sample on 4 lanes (k_pnp_solve4) with the same operations:
+// candidates of one sample on 4 lanes (k_pnp_solve_l<4>) with the same operations:
 //   lt_common: the cubic, the two eigenvectors, v and the inverse of [d12 d13 d12xd13]
 //   lt_sign:   for s = +v / -v: w0, w1 and the quadratic's roots tau (false: no real root)
 //   lt_tau:    one root: lambdas, Gauss-Newton refine, pose, emit (1 if emitted)
