@@ -1198,6 +1198,9 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
 // 3 of 3: lane c of a group of three takes estimate c + 1, then epnp::compute_pose's pick,
 // Rodrigues(Rodrigues(R)) (the (rvec, tvec) model computeError projects), the records
 __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin, int32_t H, int hpw) {
+#ifdef RSAC_TRACE
+    const unsigned long long tk0 = __builtin_amdgcn_s_memtime();
+#endif
     const int prob = blockIdx.y;
     const int lane = threadIdx.x & 63, g = lane / 3, c = lane - 3 * g;
     const int hl = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * hpw + g;
@@ -1225,8 +1228,24 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
                 for (int j = 0; j < 3; ++j) cw.cws[i][j] = E[kCvCws + 3 * i + j];
             cvq::epnp_rho(cw, rho);
         }
+#ifdef RSAC_TRACE
+        const unsigned long long tc0 = __builtin_amdgcn_s_memtime();
+        asm volatile("; trace sink %0" ::"v"(L[5][9] + rho[5]) : "memory");
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tc1 = __builtin_amdgcn_s_memtime();
+#endif
         cvq::betas_approx_padded(c + 1, L, rho, be);  // one instruction stream for the three lanes
+#ifdef RSAC_TRACE
+        asm volatile("; trace sink %0" ::"v"(be[0] + be[3]) : "memory");
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tc2 = __builtin_amdgcn_s_memtime();
+#endif
         cvq::gauss_newton(L, rho, be);
+#ifdef RSAC_TRACE
+        asm volatile("; trace sink %0" ::"v"(be[0] + be[3]) : "memory");
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tc3 = __builtin_amdgcn_s_memtime();
+#endif
         int32_t idx[5];
         (void)epnp5_sample(a, rec, h, n, idx);
         Epnp5Pts q;
@@ -1244,6 +1263,14 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
 #pragma unroll
             for (int k = 0; k < 12; ++k) v[i][k] = E[(3 - i) * 12 + k];
         err = cvq::epnp5_r_and_t(e, v, be, R, t);
+#ifdef RSAC_TRACE
+        asm volatile("; trace sink %0" ::"v"(err + R[0] + t[2]) : "memory");
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tc4 = __builtin_amdgcn_s_memtime();
+        if (hl == 0 && prob == 0)
+            printf("epnp c lane %d: setup %llu betas %llu gauss-newton %llu r_and_t %llu cycles (from kernel start %llu)\n",
+                   c, tc1 - tc0, tc2 - tc1, tc3 - tc2, tc4 - tc3, tc1 - tk0);
+#endif
     }
     // epnp::compute_pose's pick over the group's three lanes (estimates 1, 2, 3)
     const int base = 3 * g;
@@ -1259,7 +1286,17 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
     // the stage took 85 instead of 78 us, r06)
     if (st > 0) {
         st = 1;
+#ifdef RSAC_TRACE
+        const unsigned long long tr0 = __builtin_amdgcn_s_memtime();
+#endif
         if (a.rvec_rt) rodrigues_roundtrip(R);
+#ifdef RSAC_TRACE
+        asm volatile("; trace sink %0" ::"v"(R[0] + R[8]) : "memory");
+        __builtin_amdgcn_s_waitcnt(0);
+        if (hl == 0 && prob == 0)
+            printf("epnp c roundtrip %llu cycles, total %llu\n", __builtin_amdgcn_s_memtime() - tr0,
+                   __builtin_amdgcn_s_memtime() - tk0);
+#endif
     }
     double *m = a.models + rec * kModelStride;
 #pragma unroll
