@@ -304,7 +304,7 @@ RSAC_EXPORT int rsac_pnp_epnp(const double *pts3d, const double *pts2d, int32_t 
 /* The minimal solver of cv2.solvePnPRansac's default flags on one 5-point sample, on the host
  * (no GPU needed): solvePnP(..., SOLVEPNP_EPNP) in OpenCV's operation sequence (undistortPoints
  * to f32 normalised points, epnp.cpp with lapack.cpp's JacobiSVD; rsac_cvepnp.h, the source the
- * k_cvepnp5_* kernels run, the 12 x 12 JacobiSVD there on four lanes).  pts3d 5 x 3 and pts2d
+ * k_cvepnp5_* kernels run, the 12 x 12 JacobiSVD there on six lanes).  pts3d 5 x 3 and pts2d
  * 5 x 2 f64 AoS, rounded to f32 like solvePnPRansac's CV_32F copies (main_v1.py:497,
  * testpro-K.py:72).  Always RSAC_OK (OpenCV's EPnP reports a pose for any sample; a degenerate
  * one gives NaN). */
