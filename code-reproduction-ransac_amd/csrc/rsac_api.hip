@@ -125,7 +125,7 @@ struct rsac_ctx {
     int64_t *d_off = nullptr;  // views into `tables`: offsets (P+1), cams (P x 4), thr2 (P)
     double *d_cams = nullptr;
     float *d_thr2 = nullptr;
-    DevBuf centred, bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
+    DevBuf bounds_ws, frame, fconst, fmodels, queue;  // float32 pre-filter state (PnP)
     DevBuf mxpts;                                              // MFMA point operands (PF, UV: 40 B / point)
     DevBuf epnp5;                                              // EPnP-5 minimal solve: kEpnpRec doubles / hypothesis of a launch
     DevBuf direct;                                             // count == model_points problems (direct_solve)
@@ -346,7 +346,6 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     const int P = st.P;
     const int64_t N = st.total;
     HIPCHK(c->queue.ensure(4096));  // kQWords ints (rsac_kernels.hip)
-    HIPCHK(c->centred.ensure(sizeof(float) * 3 * std::max<int64_t>(N, 1)));
     HIPCHK(c->bounds_ws.ensure(sizeof(int32_t) * 10 * P));
     HIPCHK(c->frame.ensure(sizeof(double) * kFrameStride * P));
     HIPCHK(c->fconst.ensure(sizeof(float) * kFconstStride * P));
@@ -355,7 +354,6 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
     a.sample_k = (flags & RSAC_F_MINIMAL_EPNP5) ? 5 : 4;  // EPnP-5: ensure_epnp5 before each solve
     a.rvec_rt = (flags & RSAC_F_RVEC_ROUNDTRIP) ? 1 : 0;
     a.dbg_cell_pts = c->dbg_cell_pts;
-    float *C = c->centred.as<float>();
     int32_t max_n = 0;
     for (int p = 0; p < P; ++p) max_n = std::max<int32_t>(max_n, (int32_t)(st.off[p + 1] - st.off[p]));
     // resets best_key and the queue, then builds the frame (also in exact mode: cheap)
@@ -374,11 +372,10 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
         prep.ticket = c->setup_scr.as<int>();
         prep.part = (float *)(c->setup_scr.as<char>() + 64);
     }
-    HIPCHK(launch_pnp_frame(a, P, max_n, c->bounds_ws.as<int32_t>(), C, C + N, C + 2 * N, c->frame.as<double>(),
+    HIPCHK(launch_pnp_frame(a, P, max_n, c->bounds_ws.as<int32_t>(), nullptr, nullptr, nullptr, c->frame.as<double>(),
                             c->fconst.as<float>(), s, &prep));
     if (!a.exact_only) {
         a.counts_out = c->counts.as<int32_t>();
-        a.XC = C; a.YC = C + N; a.ZC = C + 2 * N;
         a.frame = c->frame.as<double>();
         a.fconst = c->fconst.as<float>();
         a.fmodels = c->fmodels.as<float>();
@@ -1358,7 +1355,7 @@ void rsac_destroy(rsac_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *dev[] = {&c->pts,  &c->tables,     &c->models,  &c->status,  &c->counts,    &c->subsets,
-                     &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->centred, &c->bounds_ws,
+                     &c->substatus, &c->best, &c->bestmodels, &c->mask, &c->bounds_ws,
                      &c->frame, &c->fconst,   &c->fmodels, &c->queue, &c->loc, &c->lo, &c->win, &c->geo,
                      &c->epnp, &c->epnp5, &c->direct, &c->lmscr, &c->setup_scr, &c->scanrec, &c->mxpts, &c->reproj};
     for (DevBuf *b : dev) b->release();

@@ -30,10 +30,9 @@ struct PnpArgs {
     int64_t hyp_stride;
     int64_t rng_base;
     uint64_t seed;
-    // float32 pre-filter (DESIGN.md "Scoring"): centred coordinates, per-problem
-    // frame / constants, per-hypothesis float32 records.  fmodels == nullptr
-    // (or exact_only) selects the all-f64 scoring kernel.
-    const float *XC, *YC, *ZC;
+    // float32 pre-filter (DESIGN.md "Scoring"): per-problem frame / constants (the points are
+    // centred on frame[0..2] where they are used), per-hypothesis float32 records.  fmodels ==
+    // nullptr (or exact_only) selects the all-f64 scoring kernel.
     const double *frame;  // P x kFrameStride: c0 c1 c2 B rho cmax wmax 0 | write_fmodel_mx's terms (8..15)
     const float *fconst;  // P x kFconstStride
     float *fmodels;       // P x hyp_stride x kFModelStride

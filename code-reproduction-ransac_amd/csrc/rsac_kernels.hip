@@ -326,9 +326,11 @@ __global__ __launch_bounds__(256) void k_pnp_center(PnpArgs a, int32_t P, const 
         const int64_t q = p0 + i;
         const float xc = (float)((double)a.X[q] - c0), yc = (float)((double)a.Y[q] - c1),
                     zc = (float)((double)a.Z[q] - c2);
-        XC[q] = xc;
-        YC[q] = yc;
-        ZC[q] = zc;
+        if (XC) {  // (no caller keeps them from r06: sc_unit centres X, Y, Z itself)
+            XC[q] = xc;
+            YC[q] = yc;
+            ZC[q] = zc;
+        }
         if (a.PF) mx_point(a, q, xc, yc, zc, a.U[q], a.V[q], mk);
     }
 }
@@ -407,9 +409,11 @@ __global__ __launch_bounds__(256) void k_pnp_setup_b(const double *__restrict__ 
         const int64_t q = p0 + j;
         const float xc = (float)((double)sX[q] - cc[0]), yc = (float)((double)sY[q] - cc[1]),
                     zc = (float)((double)sZ[q] - cc[2]);
-        XC[q] = xc;
-        YC[q] = yc;
-        ZC[q] = zc;
+        if (XC) {  // (no caller keeps them from r06: sc_unit centres X, Y, Z itself)
+            XC[q] = xc;
+            YC[q] = yc;
+            ZC[q] = zc;
+        }
         if (a.PF) mx_point(a, q, xc, yc, zc, sU[q], sV[q], mk);
     }
 }
@@ -473,9 +477,11 @@ __global__ __launch_bounds__(1024) void k_pnp_setup1(const double *__restrict__ 
     for (int i = threadIdx.x; i < n; i += 1024) {  // this thread's own stores above: visible
         const float xc = (float)((double)X[i] - cc[0]), yc = (float)((double)Y[i] - cc[1]),
                     zc = (float)((double)Z[i] - cc[2]);
-        XC[i] = xc;
-        YC[i] = yc;
-        ZC[i] = zc;
+        if (XC) {  // (no caller keeps them from r06: sc_unit centres X, Y, Z itself)
+            XC[i] = xc;
+            YC[i] = yc;
+            ZC[i] = zc;
+        }
         if (a.PF) mx_point(a, i, xc, yc, zc, U[i], V[i], mk);
     }
 }
@@ -519,9 +525,11 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
         }
         const float xc = (float)((double)v[0] - c[0]), yc = (float)((double)v[1] - c[1]),
                     zc = (float)((double)v[2] - c[2]);
-        XC[i] = xc;
-        YC[i] = yc;
-        ZC[i] = zc;
+        if (XC) {  // (no caller keeps them from r06: sc_unit centres X, Y, Z itself)
+            XC[i] = xc;
+            YC[i] = yc;
+            ZC[i] = zc;
+        }
         if (a.PF) mx_point(a, i, xc, yc, zc, v[3], v[4], mk);
 #pragma unroll
         for (int k = 0; k < 5; ++k) { lo[k] = fminf(lo[k], v[k]); hi[k] = fmaxf(hi[k], v[k]); }
@@ -1541,7 +1549,12 @@ __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, 
         }
     }
     __syncthreads();
-    const float *__restrict__ XC = a.XC + p0, *__restrict__ YC = a.YC + p0, *__restrict__ ZC = a.ZC + p0;
+    // the points centred on the problem's frame centre c as the setup kernels centre them,
+    // (float)((double)X - c) (r06: computed here per tile instead of read from a stored copy;
+    // the batch setup writes 12 B per point less, C3 24 MB per call)
+    const double *fr = a.frame + (int64_t)prob * kFrameStride;
+    const double c0 = fr[0], c1 = fr[1], c2 = fr[2];
+    const float *__restrict__ X = a.X + p0, *__restrict__ Y = a.Y + p0, *__restrict__ Z = a.Z + p0;
     const float *__restrict__ U = a.U + p0, *__restrict__ V = a.V + p0;
 
     int cnt = 0;
@@ -1552,7 +1565,8 @@ __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, 
             const int i = base + j * 64 + lane;
             const bool in = i < n;
             const int ii = in ? i : 0;
-            const float x = XC[ii], y = YC[ii], z = ZC[ii], uu = U[ii], vv = V[ii];
+            const float x = (float)((double)X[ii] - c0), y = (float)((double)Y[ii] - c1),
+                        z = (float)((double)Z[ii] - c2), uu = U[ii], vv = V[ii];
             // out of range or a non-finite coordinate: a pixel at 3e38 at the centre's depth
             // makes the pair a decided outlier (or D = xs^2 + ys^2 >= 0 when z' = 0)
             const bool ok = in && __builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z) &&
