@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstddef>
 
 namespace rsac {
 
@@ -256,8 +257,11 @@ hipError_t launch_pnp_refine(const PnpArgs &a, int32_t P, const uint8_t *mask, d
                              const int32_t *stop = nullptr); // nonzero: no-op (an ended LO chain)
 // device state of an LO-RANSAC chain (k_pnp_lo_count)
 struct LoState {
-    int32_t cur, stopped, best_buf, improvements, count, ticket, last_total, pad;
+    int32_t cur, stopped, best_buf, improvements;
+    alignas(8) int32_t count;  // count and ticket: one 64-bit atomic (k_pnp_lo_count)
+    int32_t ticket, last_total, pad;
 };
+static_assert(offsetof(LoState, ticket) == offsetof(LoState, count) + 4, "count, ticket adjacent");
 hipError_t launch_pnp_lo_count(const PnpArgs &a, int32_t n, double *model, uint8_t *mask, LoState *st, int step,
                                int32_t init_cur, double *best_out, LoState *host_st, hipStream_t s);
 

@@ -3421,6 +3421,14 @@ struct GpuLmReducer {
         if (threadIdx.x < 64) {
             double r[9], u[3];
             bool sm = false;
+#ifdef RSAC_PROBE_DOUBLE_SOLVE
+            {  // A/B probe: the solve twice
+                double r2[9], u2[3];
+                bool sm2 = false;
+                const bool ok2 = lm_solve_step(acc, lam * (1.0 + 0x1p-52), R, t, r2, u2, sm2);
+                asm volatile("; probe sink %0 %1" ::"v"(r2[0] + u2[2]), "v"((int)ok2));
+            }
+#endif
             const bool ok = lm_solve_step(acc, lam, R, t, r, u, sm);
             if (threadIdx.x == 0) {
                 for (int j = 0; j < 9; ++j) sb[j] = r[j];
@@ -3638,10 +3646,28 @@ struct GpuLmReducer {
             double a[NV];
             for (int q = 0; q < NV; ++q) a[q] = 0.0;
             for_points(kk, [&](double Xd, double Yd, double Zd, double u, double v) { f(Xd, Yd, Zd, u, v, a); });
+#ifdef RSAC_PROBE_DOUBLE_POINTS
+            {  // A/B probe: the point pass twice (the copy's sums discarded), the same LM path
+                double b[NV];
+                for (int q = 0; q < NV; ++q) b[q] = 0.0;
+                for_points(kk, [&](double Xd, double Yd, double Zd, double u, double v) { f(Xd, Yd, Zd, u, v, b); });
+                for (int q = 0; q < NV; ++q) asm volatile("; probe sink %0" ::"v"(b[q]));
+            }
+#endif
 #ifdef RSAC_TRACE
             mark(20);
 #endif
             const double bsum = range_sum<NV>(a);
+#ifdef RSAC_PROBE_DOUBLE_SUMS
+            {  // A/B probe: the wave and block sums twice
+                __syncthreads();
+                double b[NV];
+                for (int q = 0; q < NV; ++q) b[q] = a[q];
+                const double bs2 = range_sum<NV>(b);
+                asm volatile("; probe sink %0" ::"v"(bs2));
+                __syncthreads();
+            }
+#endif
             const int r = first + kk * G;
             if (threadIdx.x < NV) {
                 const int q = threadIdx.x;
@@ -4093,11 +4119,14 @@ __global__ __launch_bounds__(256) void k_pnp_lo_count(PnpArgs a, double *__restr
     __syncthreads();
     if (threadIdx.x != 0) return;
     const int blk = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    if (blk) atomicAdd(&st->count, blk);
-    __threadfence();
-    if (atomicAdd(&st->ticket, 1) != (int)gridDim.x - 1) return;
+    // count (low word) and ticket (high word) in one 64-bit atomic: the block that takes the last
+    // ticket gets every other block's count in the returned value, so no fence orders two atomics
+    // (r06: a __threadfence and a second atomic per block before)
+    const unsigned long long old =
+        atomicAdd(reinterpret_cast<unsigned long long *>(&st->count), (1ull << 32) | (unsigned)blk);
+    if ((unsigned)(old >> 32) != gridDim.x - 1) return;
     // the last block: every block's count is in
-    const int total = __hip_atomic_load(&st->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int total = (int)(unsigned)old + blk;
     LoState v;
     if (step < 0) {
         v.cur = init_cur;
@@ -4133,7 +4162,9 @@ __global__ __launch_bounds__(256) void k_pnp_lo_count(PnpArgs a, double *__restr
 
 hipError_t launch_pnp_lo_count(const PnpArgs &a, int32_t n, double *model, uint8_t *mask, LoState *st, int step,
                                int32_t init_cur, double *best_out, LoState *host_st, hipStream_t s) {
-    unsigned g = cdiv(n > 0 ? n : 1, 256);
+    // 8 points per thread: one ticket atomic per 2048 points (the atomics of one address
+    // serialise, ~10 ns each; 391 blocks at 100k points before r06)
+    unsigned g = cdiv(n > 0 ? n : 1, 2048);
     if (g > 2048) g = 2048;
     hipLaunchKernelGGL(k_pnp_lo_count, dim3(g), dim3(256), 0, s, a, model, mask, st, step, init_cur, best_out,
                        host_st);

@@ -1,5 +1,6 @@
 """Interleaved A/B of librsac builds on ms-to-best (the reference-mode pnp_ransac call on the C2
-problem: adaptive, LM refit) and, with --hyps, the fixed-budget EPnP-5 solve rate.
+problem: adaptive, LM refit), with --hyps the fixed-budget EPnP-5 solve rate, and with --c5 the
+LO-RANSAC call on BASELINE configs[4] (100k correspondences).
 
     python scripts/ms_ab.py build/ab/librsac_a.so build/ab/librsac_b.so ... [--rounds 3]
 
@@ -19,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODES = (("epnp5", "opencv"), ("p3p", "philox"))
 
 
-def worker(calls, hyps):
+def worker(calls, hyps, c5=False):
     sys.path[:0] = [os.path.join(ROOT, "code-reproduction-ransac_amd")]
     import torch
     import rsac
@@ -52,6 +53,19 @@ def worker(calls, hyps):
             if i >= 3:
                 walls.append((time.perf_counter() - t) * 1e3)
         out["epnp5_fixed_hyp_s"] = hyps / statistics.median(walls) * 1e3
+    if c5:
+        p5 = synth.pnp_problem(100_000, 0.5, seed=3)
+        q2, q3 = torch.from_numpy(p5["points2d"]).to(dev), torch.from_numpy(p5["points3d"]).to(dev)
+        walls = []
+        for i in range(calls + 3):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            R, t_, m = rsac.pnp_ransac(q2, q3, p5["K"], 5000, 30.0, lo=True, refine=True)
+            torch.cuda.synchronize()
+            if i >= 3:
+                walls.append((time.perf_counter() - t) * 1e3)
+        out["c5_lo"] = statistics.median(walls)
+        out["c5_lo_key"] = [int(m.sum())]
     print(json.dumps(out), flush=True)
 
 
@@ -62,16 +76,17 @@ def main():
     ap.add_argument("--calls", type=int, default=30)
     ap.add_argument("--hyps", type=int, default=0)
     ap.add_argument("--worker", action="store_true")
+    ap.add_argument("--c5", action="store_true")
     a = ap.parse_args()
     if a.worker:
-        worker(a.calls, a.hyps)
+        worker(a.calls, a.hyps, a.c5)
         return
     res = {lib: [] for lib in a.libs}
     for _ in range(a.rounds):
         for lib in a.libs:
             env = dict(os.environ, RSAC_LIB_PATH=os.path.abspath(lib))
             r = subprocess.run([sys.executable, "-u", __file__, "--worker", "--calls", str(a.calls), "--hyps",
-                                str(a.hyps)], env=env, capture_output=True, text=True, timeout=300)
+                                str(a.hyps)] + (["--c5"] if a.c5 else []), env=env, capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
                 print(r.stdout, r.stderr, flush=True)
                 sys.exit(r.returncode)
