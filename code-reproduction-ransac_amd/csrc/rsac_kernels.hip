@@ -2976,11 +2976,16 @@ hipError_t launch_pnp_frame(const PnpArgs &a, int32_t P, int32_t max_n, int32_t 
 // fill the GPU); its records are written in form 1 (the solve and the scoring launch apply the
 // same rule)
 constexpr int64_t kSmallRoundTiles = 16;
+// ... on problems of at most this many points: longer ones (C5's 100k) give the MFMA kernel
+// enough cells even for 256 hypotheses (r06: C5's first round 42.5 us on the scaled form)
+constexpr int32_t kSmallRoundMaxN = 32768;
 
-static bool small_round(int32_t P, int32_t H) { return (int64_t)P * ((H + 31) / 32) <= kSmallRoundTiles; }
+static bool small_round(int32_t P, int32_t H, int32_t max_n) {
+    return (int64_t)P * ((H + 31) / 32) <= kSmallRoundTiles && max_n <= kSmallRoundMaxN;
+}
 static PnpArgs round_args(const PnpArgs &a, int32_t P, int32_t H) {
     PnpArgs ka = a;
-    if (ka.fform == 2 && small_round(P, H)) ka.fform = 1;
+    if (ka.fform == 2 && small_round(P, H, a.max_n)) ka.fform = 1;
     return ka;
 }
 
@@ -3138,7 +3143,7 @@ hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
     if (a.max_n > 0 && a.max_n <= kLanePts) {
         hipLaunchKernelGGL(k_pnp_score_lane, dim3(cdiv(H, 256), P), dim3(256), 0, s, a, hyp_begin, H, counts);
     } else if (a.fmodels && !a.exact_only) {
-        if (small_round(P, H)) {  // form-1 records (round_args): the small-round instance
+        if (small_round(P, H, a.max_n)) {  // form-1 records (round_args): the small-round instance
             return launch_sc<2, 5>(a, P, hyp_begin, H, counts, s);
         }
         return launch_mf(a, P, hyp_begin, H, counts, s);
