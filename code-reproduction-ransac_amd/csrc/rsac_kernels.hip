@@ -3426,14 +3426,6 @@ struct GpuLmReducer {
         if (threadIdx.x < 64) {
             double r[9], u[3];
             bool sm = false;
-#ifdef RSAC_PROBE_DOUBLE_SOLVE
-            {  // A/B probe: the solve twice
-                double r2[9], u2[3];
-                bool sm2 = false;
-                const bool ok2 = lm_solve_step(acc, lam * (1.0 + 0x1p-52), R, t, r2, u2, sm2);
-                asm volatile("; probe sink %0 %1" ::"v"(r2[0] + u2[2]), "v"((int)ok2));
-            }
-#endif
             const bool ok = lm_solve_step(acc, lam, R, t, r, u, sm);
             if (threadIdx.x == 0) {
                 for (int j = 0; j < 9; ++j) sb[j] = r[j];
@@ -3651,28 +3643,10 @@ struct GpuLmReducer {
             double a[NV];
             for (int q = 0; q < NV; ++q) a[q] = 0.0;
             for_points(kk, [&](double Xd, double Yd, double Zd, double u, double v) { f(Xd, Yd, Zd, u, v, a); });
-#ifdef RSAC_PROBE_DOUBLE_POINTS
-            {  // A/B probe: the point pass twice (the copy's sums discarded), the same LM path
-                double b[NV];
-                for (int q = 0; q < NV; ++q) b[q] = 0.0;
-                for_points(kk, [&](double Xd, double Yd, double Zd, double u, double v) { f(Xd, Yd, Zd, u, v, b); });
-                for (int q = 0; q < NV; ++q) asm volatile("; probe sink %0" ::"v"(b[q]));
-            }
-#endif
 #ifdef RSAC_TRACE
             mark(20);
 #endif
             const double bsum = range_sum<NV>(a);
-#ifdef RSAC_PROBE_DOUBLE_SUMS
-            {  // A/B probe: the wave and block sums twice
-                __syncthreads();
-                double b[NV];
-                for (int q = 0; q < NV; ++q) b[q] = a[q];
-                const double bs2 = range_sum<NV>(b);
-                asm volatile("; probe sink %0" ::"v"(bs2));
-                __syncthreads();
-            }
-#endif
             const int r = first + kk * G;
             if (threadIdx.x < NV) {
                 const int q = threadIdx.x;

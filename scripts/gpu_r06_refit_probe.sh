@@ -1,6 +1,7 @@
 #!/bin/bash
 # r06: where the LM refit's time goes, by doubling one part at a time (probe builds from
-# scripts/build_ab.sh: base, the point pass twice, the wave/block sums twice, the solve step twice),
+# scripts/build_ab.sh after `git apply scripts/ubench/refit_probes_r06.patch`: base, the point pass twice,
+# the wave/block sums twice, the solve step twice),
 # k_pnp_refine's mean duration from rocprofv3 kernel traces, two interleaved rounds
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
