@@ -1068,80 +1068,61 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
         S[144 + r] = sd;
     }
     lds_wave_order();
-#ifdef RSAC_TRACE
-    // per-phase cycle sums of lane 0 (s_memtime after the phase's values exist)
-    unsigned long long tr_c[4] = {0, 0, 0, 0}, tr_prev = 0;
-    int tr_n[2] = {0, 0};
-#define TR_STAMP(k, v)                                                          \
-    do {                                                                        \
-        const double tr_v = (v);                                                \
-        asm volatile("; trace sink %0" ::"v"(tr_v) : "memory");                 \
-        __builtin_amdgcn_s_waitcnt(0);                                          \
-        const unsigned long long now = __builtin_amdgcn_s_memtime();            \
-        tr_c[k] += now - ((k) == 0 ? c0 : tr_prev);                             \
-        tr_prev = now;                                                          \
-    } while (0)
-#endif
+    // A rotation's two norm sums (the new W of its rows) are formed at the next step, beside that
+    // step's dot product: the two chains are independent, so the wave runs them side by side
+    // (r06: the sums were ≈410 cycles of a ≈2 400-cycle step).  Every lane stores its pending
+    // norms before any lane reads W again (the same wave's LDS order); a lane with nothing pending
+    // stores to the pad slots 156 and 157.  The rows go to LDS at once, as before.  A step is
+    // branch-free up to the skip test (an idle lane reads rows 0 and 1 and discards the result).
+    double Pi[12], Pj[12];
+    int wi = 12, wj = 13;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        Pi[k] = 0;
+        Pj[k] = 0;
+    }
     for (int iter = 0; iter < 30; ++iter) {
         bool changed = false;
         for (int t = 1; t <= 21; ++t) {
             const int i = (t > 11 ? t - 11 : 0) + m, j = t - i;
-            if (i < j) {
-#ifdef RSAC_TRACE
-                const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-#endif
-                double Ai[12], Aj[12];
-                cvsvd_load_row(S, i, Ai);
-                cvsvd_load_row(S, j, Aj);
-                const double wa = S[144 + i], wb = S[144 + j];
-#ifdef RSAC_TRACE
-                TR_STAMP(0, Ai[11] + Aj[11] + wa + wb);
-#endif
-                double p = 0;
+            const bool act = i < j;
+            const int li = act ? i : 0, lj = act ? j : 1;
+            double Ai[12], Aj[12];
+            cvsvd_load_row(S, li, Ai);
+            cvsvd_load_row(S, lj, Aj);
+            double na = 0, nb = 0, p = 0;
 #pragma unroll
-                for (int k = 0; k < 12; ++k) p += Ai[k] * Aj[k];
-                const bool rot = !(dabs(p) <= cvq::kSvdEps * dsqrt(wa * wb));
-#ifdef RSAC_TRACE
-                TR_STAMP(1, p + wa);
-#endif
-                if (rot) {
-                    double c, s;
-                    cvq::svd_rotation_sel(p * 2, wa, wb, c, s);
-#ifdef RSAC_TRACE
-                    TR_STAMP(2, c + s);
-#endif
-                    double na = 0, nb = 0;
+            for (int k = 0; k < 12; ++k) {
+                na += Pi[k] * Pi[k];
+                nb += Pj[k] * Pj[k];
+                p += Ai[k] * Aj[k];
+            }
+            S[144 + wi] = na;
+            S[144 + wj] = nb;
+            wi = 12;
+            wj = 13;
+            const double wa = S[144 + li], wb = S[144 + lj];
+            if (act && !(dabs(p) <= cvq::kSvdEps * dsqrt(wa * wb))) {
+                double c, s;
+                cvq::svd_rotation_sel(p * 2, wa, wb, c, s);
 #pragma unroll
-                    for (int k = 0; k < 12; ++k) {
-                        const double t0 = c * Ai[k] + s * Aj[k];
-                        const double t1 = -s * Ai[k] + c * Aj[k];
-                        Ai[k] = t0;
-                        Aj[k] = t1;
-                        na += t0 * t0;
-                        nb += t1 * t1;
-                    }
-                    cvsvd_store_row(S, i, Ai);
-                    cvsvd_store_row(S, j, Aj);
-                    S[144 + i] = na;
-                    S[144 + j] = nb;
-                    changed = true;
-#ifdef RSAC_TRACE
-                    TR_STAMP(3, na + nb);
-#endif
+                for (int k = 0; k < 12; ++k) {
+                    const double t0 = c * Ai[k] + s * Aj[k];
+                    const double t1 = -s * Ai[k] + c * Aj[k];
+                    Pi[k] = t0;
+                    Pj[k] = t1;
                 }
-#ifdef RSAC_TRACE
-                tr_n[rot ? 1 : 0]++;
-#endif
+                cvsvd_store_row(S, i, Pi);
+                cvsvd_store_row(S, j, Pj);
+                wi = i;
+                wj = j;
+                changed = true;
             }
             lds_wave_order();
         }
         if (!__any(changed)) break;
     }
-#ifdef RSAC_TRACE
-    if (hl == 0 && m == 0)
-        printf("svd lane0: rotations %d skips %d | cycles load %llu p+test %llu rot-cs %llu update+store %llu\n", tr_n[1],
-               tr_n[0], tr_c[0], tr_c[1], tr_c[2], tr_c[3]);
-#endif
+    // (pending norms need no flush: the norms below are recomputed from the rows)
     // the row norms, the selection sort (descending, first maximum), the normalisation
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
