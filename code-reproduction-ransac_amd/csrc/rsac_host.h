@@ -21,23 +21,21 @@
 namespace rsac {
 
 // Run f(p) for p in [0, P) on up to 16 host threads (the per-problem MWC subset draws and refits
-// of a batch are independent; each writes only its own outputs).  Sanitizer-checked by
-// tests/sanitize (ThreadSanitizer).
+// of a batch are independent; each writes only its own outputs).  The workers are a persistent
+// pool (rsac_host.hip: host_pool_run), created on first use, so a call costs a wake-up instead of
+// 16 thread creations and joins (r06); a call made while the pool is busy (another thread's
+// batch) runs on its own thread.  Sanitizer-checked by tests/sanitize (ThreadSanitizer).
+void host_pool_run(int P, int nt, void (*fn)(void *, int), void *arg);
+int host_pool_threads();
+
 template <class F>
 void parallel_for(int P, F f) {
-    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    const int nt = std::min({hw, 16, (P + 7) / 8});
+    const int nt = std::min({host_pool_threads(), 16, (P + 7) / 8});
     if (nt <= 1) {
         for (int p = 0; p < P; ++p) f(p);
         return;
     }
-    std::atomic<int> next{0};
-    std::vector<std::thread> pool;
-    for (int k = 0; k < nt; ++k)
-        pool.emplace_back([&] {
-            for (int p; (p = next.fetch_add(1)) < P;) f(p);
-        });
-    for (auto &t : pool) t.join();
+    host_pool_run(P, nt, [](void *a, int p) { (*static_cast<F *>(a))(p); }, &f);
 }
 
 struct Mwc {

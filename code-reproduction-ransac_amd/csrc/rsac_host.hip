@@ -11,9 +11,111 @@
 
 #include "rsac_math.h"
 
+#include <pthread.h>
+
+#include <condition_variable>
+#include <mutex>
+
 namespace rsac {
 
+namespace {
+// the persistent workers of parallel_for: nw threads wait for a batch (gen changes), take problem
+// indices from next until P, and count themselves out in left; the caller takes indices too
+struct HostPool {
+    std::mutex mu;                 // held by the one batch in flight (try_lock: busy -> serial)
+    std::mutex state;              // guards gen / fn / arg / P / nt / left and the condvars
+    std::condition_variable go, done;
+    uint64_t gen = 0;
+    void (*fn)(void *, int) = nullptr;
+    void *arg = nullptr;
+    int P = 0, nt = 0, left = 0;
+    std::atomic<int> next{0};
+    int nw = 0;
+    explicit HostPool(int workers) : nw(workers) {
+        for (int w = 0; w < nw; ++w) std::thread([this, w] { loop(w); }).detach();
+    }
+    void loop(int w) {
+        uint64_t seen = 0;
+        for (;;) {
+            void (*f)(void *, int);
+            void *a;
+            int n;
+            {
+                std::unique_lock<std::mutex> lk(state);
+                go.wait(lk, [&] { return gen != seen; });
+                seen = gen;
+                if (w + 1 >= nt) continue;  // not one of this batch's nt - 1 workers
+                f = fn;
+                a = arg;
+                n = P;
+            }
+            for (int p; (p = next.fetch_add(1)) < n;) f(a, p);
+            std::lock_guard<std::mutex> lk(state);
+            if (--left == 0) done.notify_one();
+        }
+    }
+};
+std::atomic<HostPool *> g_pool{nullptr};
+std::mutex g_pool_mu;  // creation; held across fork (atfork), so the child finds it unlocked
+int pool_threads() {
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    return std::min(hw, 16);
+}
+void pool_prepare_fork() { g_pool_mu.lock(); }
+void pool_parent_fork() { g_pool_mu.unlock(); }
+void pool_child_fork() {  // the child has none of the workers: a new pool on demand
+    g_pool.store(nullptr, std::memory_order_relaxed);
+    g_pool_mu.unlock();
+}
+HostPool *pool() {
+    HostPool *p = g_pool.load(std::memory_order_acquire);
+    if (p) return p;
+    static std::once_flag atfork_once;
+    std::call_once(atfork_once, [] { pthread_atfork(pool_prepare_fork, pool_parent_fork, pool_child_fork); });
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    p = g_pool.load(std::memory_order_relaxed);
+    if (!p) {
+        p = new HostPool(pool_threads() - 1);  // never destroyed: the workers outlive main
+        g_pool.store(p, std::memory_order_release);
+    }
+    return p;
+}
+}  // namespace
+
+int host_pool_threads() { return pool_threads(); }
+
+void host_pool_run(int P, int nt, void (*fn)(void *, int), void *arg) {
+    HostPool *hp = pool();
+    std::unique_lock<std::mutex> busy(hp->mu, std::try_to_lock);
+    if (!busy.owns_lock()) {  // another batch holds the pool: this one on the calling thread
+        for (int p = 0; p < P; ++p) fn(arg, p);
+        return;
+    }
+    nt = std::min(nt, hp->nw + 1);
+    {
+        std::lock_guard<std::mutex> lk(hp->state);
+        hp->fn = fn;
+        hp->arg = arg;
+        hp->P = P;
+        hp->nt = nt;
+        hp->left = nt - 1;
+        hp->next.store(0);
+        ++hp->gen;
+    }
+    hp->go.notify_all();
+    for (int p; (p = hp->next.fetch_add(1)) < P;) fn(arg, p);
+    std::unique_lock<std::mutex> lk(hp->state);
+    hp->done.wait(lk, [&] { return hp->left == 0; });
+}
+
 void mwc_subsets(Mwc &rng, int n, int64_t H, const float *const *hom, int32_t *out, int8_t *status, int k) {
+    // rng.uniform(0, n) = next() % n, the remainder by Lemire's direct computation (exact for
+    // every 32-bit dividend and divisor; M = ceil(2^64 / n)) instead of a 32-bit division
+    const uint64_t M = n > 0 ? UINT64_C(0xFFFFFFFFFFFFFFFF) / (uint32_t)n + 1 : 0;
+    auto draw = [&]() -> int {
+        const uint64_t lo = M * (uint64_t)rng.next();
+        return (int)(((unsigned __int128)lo * (uint32_t)n) >> 64);
+    };
     for (int64_t h = 0; h < H; ++h) {
         int32_t *idx = out + k * h;
         bool found = false;
@@ -21,7 +123,7 @@ void mwc_subsets(Mwc &rng, int n, int64_t H, const float *const *hom, int32_t *o
             for (int i = 0; i < k; ++i) {
                 int r;
                 for (;;) {
-                    r = rng.uniform(0, n);
+                    r = draw();
                     bool dup = false;
                     for (int j = 0; j < i; ++j) dup |= (idx[j] == r);
                     if (!dup) break;

@@ -6,12 +6,16 @@
 //   2. mwc_subsets of 64 problems through parallel_for (16 threads) == the sequential draws;
 //   3. the LM, EPnP and homography refits of 32 synthetic problems through parallel_for == the
 //      same refits run sequentially (bitwise);
-//   4. Rodrigues round trips.
+//   4. Rodrigues round trips;
+//   5. the persistent parallel_for pool reused batch after batch, from two threads at once (the
+//      second caller's batches run on its own thread while the pool is busy).
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <cmath>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "rsac_host.h"
@@ -194,8 +198,28 @@ static void check_rodrigues(std::mt19937_64 &rng) {
     }
 }
 
+static void check_pool() {
+    std::atomic<long> total{0};
+    auto caller = [&](int salt) {
+        for (int it = 0; it < 300; ++it) {
+            const int P = 17 + (it * 7 + salt) % 150;
+            std::vector<int> v(P, 0);
+            parallel_for(P, [&](int p) { v[p] = p + 1; });
+            long s = 0;
+            for (int x : v) s += x;
+            CHECK(s == (long)P * (P + 1) / 2);
+            total += s;
+        }
+    };
+    std::thread a(caller, 0), b(caller, 1);
+    a.join();
+    b.join();
+    CHECK(total > 0);
+}
+
 int main() {
     std::mt19937_64 rng(20261017);
+    check_pool();
     check_scan(rng);
     check_mwc(rng);
     check_refits(rng);
