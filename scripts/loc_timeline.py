@@ -1,9 +1,12 @@
+"""Kernel / host-API timeline of the last call of a workload from rocprofv3 --kernel-trace --hip-trace CSVs:
+    python3 scripts/loc_timeline.py kernel_trace.csv hip_api_trace.csv [first-kernel marker, default k_loc_pos2]"""
 import csv, sys
 kr = list(csv.DictReader(open(sys.argv[1])))
 ar = list(csv.DictReader(open(sys.argv[2])))
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:50]) for r in kr)
 # last call = kernels after the last k_loc_pos2
-idx = [i for i, k in enumerate(ks) if "k_loc_pos2" in k[2]]
+marker = sys.argv[3] if len(sys.argv) > 3 else "k_loc_pos2"
+idx = [i for i, k in enumerate(ks) if marker in k[2]]
 a = idx[-1]
 b = len(ks)
 g = ks[a:b]
