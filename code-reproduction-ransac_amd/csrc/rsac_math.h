@@ -1046,7 +1046,10 @@ RSAC_HD int pnp_lm_refine(Red &red, double *R, double *t, int max_iter) {
             }
             RSAC_TRACE_MARK(red, 13);
             double cn;
-            if constexpr (fused) cn = red.cost_normal(Rn, tn, acc_next);
+            // a step already below the step criterion needs only the candidate's cost: accepted, the
+            // loop ends; rejected, the next try re-solves the current normal equations (r06: the
+            // last pass of most refits is then the 1-term cost reduction, the same bits)
+            if constexpr (fused) cn = small ? red.cost(Rn, tn) : red.cost_normal(Rn, tn, acc_next);
             else cn = red.cost(Rn, tn);
             RSAC_TRACE_MARK(red, 14);
             if (cn < cost) {
