@@ -109,6 +109,30 @@ static void check_mwc(std::mt19937_64 &rng) {
         mwc_subsets(m, ns[p], Hs, nullptr, &seq[p * Hs * 4], &sst[p * Hs]);
     }
     CHECK(par == seq && pst == sst);
+    // the draws against getSubset written with OpenCV's own remainder (rng.uniform = next() % n):
+    // the sampler's direct-computation remainder must give the same subsets for any n
+    for (int trial = 0; trial < 200; ++trial) {
+        const int n = trial < 100 ? 4 + trial : 4 + (int)(rng() % 2000000);
+        const int k = trial % 2 ? 5 : 4, H = 50;
+        Mwc a, b;
+        a.state = b.state = rng();
+        std::vector<int32_t> got(H * k), want(H * k);
+        std::vector<int8_t> st(H);
+        mwc_subsets(a, n, H, nullptr, got.data(), st.data(), k);
+        for (int h = 0; h < H; ++h)
+            for (int i = 0; i < k; ++i) {
+                int r;
+                for (;;) {
+                    r = b.uniform(0, n);
+                    bool dup = false;
+                    for (int j = 0; j < i; ++j) dup |= want[h * k + j] == r;
+                    if (!dup) break;
+                }
+                want[h * k + i] = r;
+            }
+        CHECK(got == want);
+        CHECK(a.state == b.state);
+    }
 }
 
 struct Problem {
