@@ -83,9 +83,24 @@ RSAC_HD void svd_rotation(double p, double a, double b, double &c, double &s) {
 // Branch-free forms of hypot_glibc and svd_rotation (the GPU's anti-diagonal JacobiSVD runs up to
 // six rotations side by side, and a branch per rotation would serialise them): every case's
 // operations are computed and the one the branchy form takes is selected, so the bits are equal.
-RSAC_HD double hypot_glibc_sel(double x, double y) {
+// FAST: the roots and quotients by the fast cores (dsqrt_fast / ddiv_fast), valid under
+// svd_rotation_sel's range condition below.
+template <bool FAST>
+RSAC_HD double hypot_glibc_sel_t(double x, double y) {
     const double fx = dabs(x), fy = dabs(y);
     const double ax = fx < fy ? fy : fx, ay = fx < fy ? fx : fy;
+    if constexpr (FAST) {
+        // under svd_rotation_sel's range condition x, y are finite and ax lies in [2^-250, 2^202]:
+        // never huge, and a tiny ay (< 2^-511) is below ax 2^-54, glibc's ax + ay case
+        const double h0 = dsqrt_fast(ax * ax + ay * ay);
+        const double d1 = h0 - ay, d2 = h0 - ax;
+        const double t1a = ax * (2.0 * d1 - ax), t2a = (d1 - 2.0 * (ax - ay)) * d1;
+        const double t1b = 2.0 * d2 * (ax - 2.0 * ay), t2b = (4.0 * d2 - ay) * ay + d2 * d2;
+        const bool first = h0 <= 2.0 * ay;
+        const double t1 = first ? t1a : t1b, t2 = first ? t2a : t2b;
+        const double h = h0 - ddiv_fast(t1 + t2, 2.0 * h0);
+        return ay <= ax * 0x1p-54 ? ax + ay : h;
+    }
     const bool huge = ax > 0x1p+511, tiny = !huge && ay < 0x1p-511;
     // glibc: kernel(ax SCALE, ay SCALE) / SCALE for huge operands, kernel(ax / SCALE, ay / SCALE) SCALE
     // for tiny ones (SCALE = 2^-600): exact power-of-two scalings either way
@@ -103,15 +118,46 @@ RSAC_HD double hypot_glibc_sel(double x, double y) {
     if (!dfinite(x) || !dfinite(y)) r = (__builtin_isinf(x) || __builtin_isinf(y)) ? __builtin_huge_val() : x + y;
     return r;
 }
-RSAC_HD void svd_rotation_sel(double p, double a, double b, double &c, double &s) {
-    const double beta = a - b, gamma = hypot_glibc_sel(p, beta);
+RSAC_HD double hypot_glibc_sel(double x, double y) { return hypot_glibc_sel_t<false>(x, y); }
+template <bool FAST>
+RSAC_HD void svd_rotation_sel_t(double p, double a, double b, double &c, double &s) {
+    const double beta = a - b, gamma = hypot_glibc_sel_t<FAST>(p, beta);
     const bool neg = beta < 0;
     // beta < 0: s = sqrt(((gamma - beta) 0.5) / gamma), c = p / (gamma s 2); else
     // c = sqrt((gamma + beta) / (gamma 2)), s = p / (gamma c 2)
     const double num = neg ? (gamma - beta) * 0.5 : gamma + beta, den = neg ? gamma : gamma * 2;
-    const double r = dsqrt(num / den), o = p / (gamma * r * 2);
+    double r, o;
+    if constexpr (FAST) {
+        r = dsqrt_fast(ddiv_fast(num, den));
+        o = ddiv_fast(p, gamma * r * 2);
+    } else {
+        r = dsqrt(num / den);
+        o = p / (gamma * r * 2);
+    }
     c = neg ? o : r;
     s = neg ? r : o;
+}
+// JacobiSVDImpl_'s (c, s) for the pair (p doubled, a = W[i], b = W[j]); `need` = false: a skipped
+// pair, whose (c, s) the caller discards.  On the device (RSAC_FAST_F64) the fast cores run when
+// both norms lie in [2^-200, 2^200]: then |p| <= sqrt(ab) (Cauchy-Schwarz, up to rounding) and a
+// pair that is not skipped has |p| > 10 DBL_EPSILON sqrt(ab) > 2^-250, so gamma, h0 lie in
+// [2^-248, 2^203], the root arguments in [2^-496, 2^404] or [1/2, 1], every operand of a quotient
+// (the kernel's t1 + t2 a multiple of 2^-708 or zero, whose quotient only h0 - q sees) inside the
+// fast division's range, and each result equals the IEEE form's.  A lane outside the range that
+// needs its result runs the IEEE form in a branch (rare: the norms are squared row norms of
+// M^T M or of L's 6 x K columns).
+RSAC_HD void svd_rotation_sel(double p, double a, double b, double &c, double &s, bool need = true) {
+#if RSAC_DEV_FAST_F64
+    const bool in = (a >= 0x1p-200) & (a <= 0x1p+200) & (b >= 0x1p-200) & (b <= 0x1p+200);
+    if (need & !in) {
+        asm volatile("" ::: "memory");  // a branch, not a select
+        svd_rotation_sel_t<false>(p, a, b, c, s);
+    } else {
+        svd_rotation_sel_t<true>(p, a, b, c, s);
+    }
+#else
+    svd_rotation_sel_t<false>(p, a, b, c, s);
+#endif
 }
 
 RSAC_HD uint32_t rng_next(uint64_t &st) {
@@ -158,7 +204,7 @@ RSAC_HD void jacobi_svd(double (&At)[N][M], double (&Wout)[N], double (&Vt)[N][N
                 p *= 2;
                 double c, s;
 #ifdef __HIP_DEVICE_COMPILE__
-                svd_rotation_sel(p, a, b, c, s);
+                svd_rotation_sel(p, a, b, c, s, !skip);  // a skipped pair's (c, s) are discarded
 #else
                 svd_rotation(p, a, b, c, s);
 #endif

@@ -39,7 +39,51 @@ RSAC_HD bool dfinite(double v) { return __builtin_isfinite(v); }
 // a * b + c with one rounding (the oracle's fma(); correctly rounded on every backend)
 RSAC_HD double dfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 RSAC_HD double dabs(double v) { return __builtin_fabs(v); }
+
 RSAC_HD double dsqrt(double v) { return __builtin_sqrt(v); }
+
+// Correctly rounded f64 square root and division with a shorter dependent chain, for operands a
+// caller has proven to lie in range.  The compiler lowers sqrt to v_rsq_f64 + Newton steps, wrapped
+// in a scaling of x < 2^-767 (by 2^256, undone by ldexp) and a class select for 0 / +inf; division
+// to v_rcp_f64 + two Newton steps + Markstein's correction, wrapped in v_div_scale / v_div_fmas /
+// v_div_fixup.  Where the wrapping is the identity -- sqrt: x in [2^-767, DBL_MAX]; division: no
+// v_div_scale case (operand exponents less than 768 apart, |n| > 2^-969, no denormal operand or
+// quotient) and a finite nonzero quotient -- the cores below are those same operations, so the
+// result is the IEEE one; 5 (sqrt) and 2 (division) of the compiler's dependent instructions leave
+// the chain.  A zero numerator gives a zero of possibly the wrong sign.  Host code (and builds
+// without RSAC_FAST_F64) uses the IEEE operators.
+// (on by default; -DRSAC_FAST_F64=0 builds the IEEE operators everywhere, for A/B runs)
+#ifndef RSAC_FAST_F64
+#define RSAC_FAST_F64 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && RSAC_FAST_F64
+#define RSAC_DEV_FAST_F64 1
+__device__ __forceinline__ double dsqrt_fast(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    double d = __builtin_fma(-g, g, x);
+    h = __builtin_fma(h, r, h);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+__device__ __forceinline__ double ddiv_fast(double n, double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = n * r;
+    const double rem = __builtin_fma(-d, q, n);
+    return __builtin_fma(rem, r, q);
+}
+#else
+#define RSAC_DEV_FAST_F64 0
+RSAC_HD double dsqrt_fast(double x) { return __builtin_sqrt(x); }
+RSAC_HD double ddiv_fast(double n, double d) { return n / d; }
+#endif
 
 // ---------------------------------------------------------------------------
 // Rodrigues (cv::Rodrigues, [OpenCV 4.x, unvendored] calibration.cpp cvRodrigues2; main_v1.py:895,
