@@ -1090,9 +1090,12 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
             double Ai[12], Aj[12];
             cvsvd_load_row(S, li, Ai);
             cvsvd_load_row(S, lj, Aj);
-            double na = 0, nb = 0, p = 0;
+            // the sums start at their first product, not at 0 + it (r06): a norm's products are >= +0,
+            // so 0 + x == x; p differs from 0 + ... only in the sign of an all-zero sum, which the skip
+            // test treats alike (|p| = 0), and a NaN norm makes the rotation NaN either way
+            double na = Pi[0] * Pi[0], nb = Pj[0] * Pj[0], p = Ai[0] * Aj[0];
 #pragma unroll
-            for (int k = 0; k < 12; ++k) {
+            for (int k = 1; k < 12; ++k) {
                 na += Pi[k] * Pi[k];
                 nb += Pj[k] * Pj[k];
                 p += Ai[k] * Aj[k];
