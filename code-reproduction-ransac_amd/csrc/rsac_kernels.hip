@@ -1052,35 +1052,29 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
     if (a.status[rec] <= 0) return;
     double *E = a.epnp + ((int64_t)prob * H + hl) * kEpnpRec;
     double *S = svd_lds + (wave * kSvdHpw + g) * kSvdStride;  // row r at S[12 r], norms at S[144]
-    // At = (M^T M)^T = M^T M from the upper triangle: lane m fills rows 2m, 2m + 1 and their
-    // squared norms (JacobiSVDImpl_'s W)
+    // At = (M^T M)^T = M^T M from the upper triangle: lane m fills rows 2m, 2m + 1 (JacobiSVDImpl_'s
+    // initial W, their squared norms, is formed from the rows where it is used, below)
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
         const int r = 2 * m + rr;
-        double x[12], sd = 0;
+        double x[12];
 #pragma unroll
         for (int c = 0; c < 12; ++c) {
             const int lo = r < c ? r : c, hi = r < c ? c : r;
             x[c] = E[lo * 12 - lo * (lo - 1) / 2 + (hi - lo)];
-            sd += x[c] * x[c];
         }
         cvsvd_store_row(S, r, x);
-        S[144 + r] = sd;
     }
     lds_wave_order();
-    // A rotation's two norm sums (the new W of its rows) are formed at the next step, beside that
-    // step's dot product: the two chains are independent, so the wave runs them side by side
-    // (r06: the sums were ≈410 cycles of a ≈2 400-cycle step).  Every lane stores its pending
-    // norms before any lane reads W again (the same wave's LDS order); a lane with nothing pending
-    // stores to the pad slots 156 and 157.  The rows go to LDS at once, as before.  A step is
-    // branch-free up to the skip test (an idle lane reads rows 0 and 1 and discards the result).
-    double Pi[12], Pj[12];
-    int wi = 12, wj = 13;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        Pi[k] = 0;
-        Pj[k] = 0;
-    }
+    // JacobiSVDImpl_'s W[i] is always sum_k At[i][k]^2 of the stored row, in k order: the initial
+    // norms are that sum, and a rotation sets W[i] = sum_k t0_k t0_k of exactly the t0_k it stores
+    // as the row (a skip changes neither).  So a step forms both norms from the rows it loads,
+    // beside their dot product -- three independent 12-term chains -- and no W is kept in LDS
+    // (r06: the norm store and reload, ~150 cycles of a step's critical path, are gone).  The sums
+    // start at their first product, not at 0 + it: a norm's products are >= +0, so 0 + x == x; p
+    // differs from 0 + ... only in the sign of an all-zero sum, which the skip test treats alike
+    // (|p| = 0), and a NaN norm makes the rotation NaN either way.  A step is branch-free up to the
+    // skip test (an idle lane reads rows 0 and 1 and discards the result).
     for (int iter = 0; iter < 30; ++iter) {
         bool changed = false;
         for (int t = 1; t <= 21; ++t) {
@@ -1090,42 +1084,40 @@ __global__ __launch_bounds__(256) void k_cvepnp5_svd(PnpArgs a, int64_t hyp_begi
             double Ai[12], Aj[12];
             cvsvd_load_row(S, li, Ai);
             cvsvd_load_row(S, lj, Aj);
-            // the sums start at their first product, not at 0 + it (r06): a norm's products are >= +0,
-            // so 0 + x == x; p differs from 0 + ... only in the sign of an all-zero sum, which the skip
-            // test treats alike (|p| = 0), and a NaN norm makes the rotation NaN either way
-            double na = Pi[0] * Pi[0], nb = Pj[0] * Pj[0], p = Ai[0] * Aj[0];
+            double wa = Ai[0] * Ai[0], wb = Aj[0] * Aj[0], p = Ai[0] * Aj[0];
 #pragma unroll
             for (int k = 1; k < 12; ++k) {
-                na += Pi[k] * Pi[k];
-                nb += Pj[k] * Pj[k];
+                wa += Ai[k] * Ai[k];
+                wb += Aj[k] * Aj[k];
                 p += Ai[k] * Aj[k];
             }
-            S[144 + wi] = na;
-            S[144 + wj] = nb;
-            wi = 12;
-            wj = 13;
-            const double wa = S[144 + li], wb = S[144 + lj];
-            if (act && !(dabs(p) <= cvq::kSvdEps * dsqrt(wa * wb))) {
-                double c, s;
+            // the skip test's root by the fast core when both norms lie in the rotation's fast range
+            // (their product in [2^-400, 2^400]); p and the core are formed before the branch for
+            // the other lanes, so the scheduler still interleaves them
+            const double ab = wa * wb;
+            const bool in = (wa >= 0x1p-200) & (wa <= 0x1p+200) & (wb >= 0x1p-200) & (wb <= 0x1p+200);
+            double sab = dsqrt_fast(ab);
+            asm volatile("" ::"v"(p), "v"(sab));
+            if (!in) {
+                asm volatile("" ::: "memory");
+                sab = dsqrt(ab);
+            }
+            if (act && !(dabs(p) <= cvq::kSvdEps * sab)) {
+                double c, s, Pi[12], Pj[12];
                 cvq::svd_rotation_sel(p * 2, wa, wb, c, s);
 #pragma unroll
                 for (int k = 0; k < 12; ++k) {
-                    const double t0 = c * Ai[k] + s * Aj[k];
-                    const double t1 = -s * Ai[k] + c * Aj[k];
-                    Pi[k] = t0;
-                    Pj[k] = t1;
+                    Pi[k] = c * Ai[k] + s * Aj[k];
+                    Pj[k] = -s * Ai[k] + c * Aj[k];
                 }
                 cvsvd_store_row(S, i, Pi);
                 cvsvd_store_row(S, j, Pj);
-                wi = i;
-                wj = j;
                 changed = true;
             }
             lds_wave_order();
         }
         if (!__any(changed)) break;
     }
-    // (pending norms need no flush: the norms below are recomputed from the rows)
     // the row norms, the selection sort (descending, first maximum), the normalisation
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
