@@ -197,6 +197,27 @@ RSAC_HD void jacobi_svd(double (&At)[N][M], double (&Wout)[N], double (&Vt)[N][N
                 double p = 0;
 #pragma unroll
                 for (int k = 0; k < M; ++k) p += At[i][k] * At[j][k];
+#if RSAC_DEV_FAST_F64
+                // the skip test and the rotation by the fast cores when both norms lie in
+                // svd_rotation_sel's range (then a b in [2^-400, 2^400]); a pair with p == 0 and a
+                // b not NaN skips exactly (0 <= eps sqrt(ab)), as every pair of a zero-padded column
+                // does; any other lane runs the IEEE test and rotation in a branch
+                bool skip;
+                double c, s;
+                {
+                    const double ab = a * b;
+                    const bool fastc = (a >= 0x1p-200) & (a <= 0x1p+200) & (b >= 0x1p-200) & (b <= 0x1p+200);
+                    const bool trivial = (p == 0.0) & (ab == ab);
+                    if (!fastc & !trivial) {
+                        asm volatile("" ::: "memory");  // a branch, not a select
+                        skip = dabs(p) <= kSvdEps * dsqrt(ab);
+                        svd_rotation_sel_t<false>(p * 2, a, b, c, s);
+                    } else {
+                        skip = fastc ? dabs(p) <= kSvdEps * dsqrt_fast(ab) : true;
+                        svd_rotation_sel_t<true>(p * 2, a, b, c, s);
+                    }
+                }
+#else
                 const bool skip = dabs(p) <= kSvdEps * dsqrt(a * b);
 #ifndef __HIP_DEVICE_COMPILE__
                 if (skip) continue;
@@ -207,6 +228,7 @@ RSAC_HD void jacobi_svd(double (&At)[N][M], double (&Wout)[N], double (&Vt)[N][N
                 svd_rotation_sel(p, a, b, c, s, !skip);  // a skipped pair's (c, s) are discarded
 #else
                 svd_rotation(p, a, b, c, s);
+#endif
 #endif
                 double na = 0, nb = 0;
 #pragma unroll
