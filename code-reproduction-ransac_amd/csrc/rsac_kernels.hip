@@ -3401,8 +3401,11 @@ struct GpuLmReducer {
         double *sb = steps[nstep++ & 1];
         if (threadIdx.x < 64) {
             double r[9], u[3];
-            bool sm = false;
-            const bool ok = lm_solve_step(acc, lam, R, t, r, u, sm);
+            bool sm = false, bad = false;
+            // the fast cores' form; an operand outside their range redoes the step in IEEE form
+            // (the same bits; the values are wave-uniform, so is the branch)
+            bool ok = lm_solve_step_t<RSAC_FAST_F64 != 0>(acc, lam, R, t, r, u, sm, bad);
+            if (bad) ok = lm_solve_step(acc, lam, R, t, r, u, sm);
             if (threadIdx.x == 0) {
                 for (int j = 0; j < 9; ++j) sb[j] = r[j];
                 for (int j = 0; j < 3; ++j) sb[9 + j] = u[j];

@@ -964,7 +964,14 @@ RSAC_HD double pnp_lm_cost_point(const double *R, const double *t, const Cam &k,
 // + j], b = -J^T r; false if not positive definite.  Divisions by the pivots are
 // multiplications by their reciprocals (6 divisions, not 33: the GPU refit runs this on every
 // thread of the block, between two reductions, reading acc from LDS).
-RSAC_HD bool chol6_solve_packed(const double *acc, double lam, double *x) {
+// FAST (device): the pivots' roots and reciprocals, the Cayley map's reciprocal and the step
+// test's roots by the fast cores (rsac_math.h top); `bad` is set when an operand leaves their
+// range, and the caller then redoes the step with the IEEE operators (lm_solve_step), so the
+// result is the same bits either way.
+RSAC_HD bool lm_in300(double v) { return (dabs(v) >= 0x1p-300) & (dabs(v) <= 0x1p+300); }
+RSAC_HD bool lm_root_ok(double v) { return (v >= 0x1p-767) & (v <= 0x1.fffffffffffffp+1023); }
+template <bool FAST>
+RSAC_HD bool chol6_solve_packed_t(const double *acc, double lam, double *x, bool &bad) {
     double L[36], y[6], inv[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -975,8 +982,14 @@ RSAC_HD bool chol6_solve_packed(const double *acc, double lam, double *x) {
             for (int q = 0; q < j; ++q) s = dfma(-L[i * 6 + q], L[j * 6 + q], s);  // (r05: fused, the oracle's chol6 alike)
             if (i == j) {
                 if (!(s > 0)) return false;
-                L[i * 6 + i] = dsqrt(s);
-                inv[i] = 1.0 / L[i * 6 + i];
+                if constexpr (FAST) {
+                    L[i * 6 + i] = dsqrt_fast(s);
+                    inv[i] = ddiv_fast(1.0, L[i * 6 + i]);
+                    bad = bad | !lm_root_ok(s) | !lm_in300(L[i * 6 + i]);
+                } else {
+                    L[i * 6 + i] = dsqrt(s);
+                    inv[i] = 1.0 / L[i * 6 + i];
+                }
             } else {
                 L[i * 6 + j] = s * inv[j];
             }
@@ -995,18 +1008,34 @@ RSAC_HD bool chol6_solve_packed(const double *acc, double lam, double *x) {
     }
     return true;
 }
+RSAC_HD bool chol6_solve_packed(const double *acc, double lam, double *x) {
+    bool bad = false;
+    return chol6_solve_packed_t<false>(acc, lam, x, bad);
+}
 
 // Rn = Cay(d) R, Cay(d) = the rotation of the quaternion (1, d/2) (first order: I + [d]x)
-RSAC_HD void cayley_apply(const double *d, const double *R, double *Rn) {
+template <bool FAST>
+RSAC_HD void cayley_apply_t(const double *d, const double *R, double *Rn, bool &bad) {
     const double w0 = 0.5 * d[0], w1 = 0.5 * d[1], w2 = 0.5 * d[2];
     const double a = w0 * w0, b = w1 * w1, c = w2 * w2;
-    const double is = 1.0 / (1.0 + a + b + c);
+    const double den = 1.0 + a + b + c;
+    double is;
+    if constexpr (FAST) {
+        is = ddiv_fast(1.0, den);
+        bad = bad | !lm_in300(den);
+    } else {
+        is = 1.0 / den;
+    }
     double Q[9];
     Q[0] = (1.0 + a - b - c) * is;       Q[1] = 2.0 * (w0 * w1 - w2) * is; Q[2] = 2.0 * (w0 * w2 + w1) * is;
     Q[3] = 2.0 * (w0 * w1 + w2) * is;    Q[4] = (1.0 - a + b - c) * is;   Q[5] = 2.0 * (w1 * w2 - w0) * is;
     Q[6] = 2.0 * (w0 * w2 - w1) * is;    Q[7] = 2.0 * (w1 * w2 + w0) * is; Q[8] = (1.0 - a - b + c) * is;
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) Rn[3 * i + j] = Q[3 * i] * R[j] + Q[3 * i + 1] * R[3 + j] + Q[3 * i + 2] * R[6 + j];
+}
+RSAC_HD void cayley_apply(const double *d, const double *R, double *Rn) {
+    bool bad = false;
+    cayley_apply_t<false>(d, R, Rn, bad);
 }
 
 // The LM loop.  Red provides normal(R, t, acc[27]) and cost(R, t), reduced in the
@@ -1027,17 +1056,28 @@ struct LmFused<Red, decltype((void)Red::kFused)> {
 // One LM step's solve: d from (A + lam diag(A)) d = -J^T r (false: not positive definite), the
 // candidate Rn = Cay(d) R, tn = t + d[3..5], and CvLevMarq's step criterion on it, |d| <
 // FLT_EPSILON (|tn| + 1) (used only if the candidate is accepted, when tn becomes t).
-RSAC_HD bool lm_solve_step(const double *acc, double lam, const double *R, const double *t, double *Rn, double *tn,
-                           bool &small) {
+template <bool FAST>
+RSAC_HD bool lm_solve_step_t(const double *acc, double lam, const double *R, const double *t, double *Rn, double *tn,
+                             bool &small, bool &bad) {
     double d[6];
-    if (!chol6_solve_packed(acc, lam, d)) return false;
-    cayley_apply(d, R, Rn);
+    if (!chol6_solve_packed_t<FAST>(acc, lam, d, bad)) return false;
+    cayley_apply_t<FAST>(d, R, Rn, bad);
     for (int j = 0; j < 3; ++j) tn[j] = t[j] + d[3 + j];
     double dd = 0, tt = 0;
     for (int j = 0; j < 6; ++j) dd += d[j] * d[j];
     for (int j = 0; j < 3; ++j) tt += tn[j] * tn[j];
-    small = dsqrt(dd) < 1.1920928955078125e-07 * (dsqrt(tt) + 1.0);
+    if constexpr (FAST) {
+        small = dsqrt_fast(dd) < 1.1920928955078125e-07 * (dsqrt_fast(tt) + 1.0);
+        bad = bad | !lm_root_ok(dd) | !lm_root_ok(tt);
+    } else {
+        small = dsqrt(dd) < 1.1920928955078125e-07 * (dsqrt(tt) + 1.0);
+    }
     return true;
+}
+RSAC_HD bool lm_solve_step(const double *acc, double lam, const double *R, const double *t, double *Rn, double *tn,
+                           bool &small) {
+    bool bad = false;
+    return lm_solve_step_t<false>(acc, lam, R, t, Rn, tn, small, bad);
 }
 // A reducer with kSolveStep = true provides solve_step(...) = lm_solve_step(...) (the GPU
 // reducer: one wave solves, the block reads the result)
