@@ -146,6 +146,10 @@ struct rsac_ctx {
     DevBuf epnp;                                               // EPnP stage records (P x (stage 1 + stage 2))
     DevBuf lmscr;                                              // multi-block LM refit: tagged wave sums
     DevBuf setup_scr;                                          // k_pnp_setup_fc: ticket + per-block bounds
+    // a one-problem set-up pnp_args deferred into the first P3P solve (run_loop launches it with
+    // the solve as k_pnp_setup_solve4; flush_setup launches it alone where nothing fuses)
+    PnpSetupFuse pending_setup{};
+    bool pending_on = false;
     LmScratch lm;                                              // ... and its launch counter
     std::vector<char> last_tables;                             // the tables last uploaded (stage_tables)
     void *last_tables_dev = nullptr;
@@ -329,8 +333,13 @@ hipStream_t pick_stream(rsac_ctx *c, void *stream) { return stream ? (hipStream_
 // PnpArgs for a staged problem set, with the float32 pre-filter frame built
 // on the device (unless RSAC_F_EXACT_ONLY).  Call after stage_tables and
 // ensure_hyp_buffers.
+// defer_setup: a one-problem P3P call's set-up (converted device inputs, k_pnp_setup_fc) is left to
+// the first solve launch (c->pending_setup), which runs it beside the solve (k_pnp_setup_solve4);
+// the caller launches nothing that reads the points, the frame or the queue before that solve, or
+// calls flush_setup.
 int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64_t stride, int64_t rng_base,
-             hipStream_t s, PnpArgs &a, unsigned long long *best_key = nullptr) {
+             hipStream_t s, PnpArgs &a, unsigned long long *best_key = nullptr, bool defer_setup = false) {
+    c->pending_on = false;
     a = PnpArgs{};
     a.X = st.d[0]; a.Y = st.d[1]; a.Z = st.d[2]; a.U = st.d[3]; a.V = st.d[4];
     a.offsets = c->d_off;
@@ -372,8 +381,15 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
         prep.ticket = c->setup_scr.as<int>();
         prep.part = (float *)(c->setup_scr.as<char>() + 64);
     }
-    HIPCHK(launch_pnp_frame(a, P, max_n, c->bounds_ws.as<int32_t>(), nullptr, nullptr, nullptr, c->frame.as<double>(),
-                            c->fconst.as<float>(), s, &prep));
+    if (defer_setup && P == 1 && a.sample_k == 4 && !a.exact_only && !(flags & RSAC_F_LO) && prep.p3 && prep.part &&
+        prep.ticket && max_n <= 65536) {
+        c->pending_setup = PnpSetupFuse{prep, max_n, c->bounds_ws.as<int32_t>(), c->frame.as<double>(),
+                                        c->fconst.as<float>()};
+        c->pending_on = true;
+    } else {
+        HIPCHK(launch_pnp_frame(a, P, max_n, c->bounds_ws.as<int32_t>(), nullptr, nullptr, nullptr,
+                                c->frame.as<double>(), c->fconst.as<float>(), s, &prep));
+    }
     if (!a.exact_only) {
         a.counts_out = c->counts.as<int32_t>();
         a.frame = c->frame.as<double>();
@@ -381,6 +397,15 @@ int pnp_args(rsac_ctx *c, const Staged &st, uint32_t flags, uint64_t seed, int64
         a.fmodels = c->fmodels.as<float>();
         a.fform = 2;  // MFMA records (form 1 for small rounds and out-of-f16-range problems)
     }
+    return RSAC_OK;
+}
+
+// the deferred set-up alone (a path that does not start with a fusable P3P solve)
+int flush_setup(rsac_ctx *c, const PnpArgs &a, hipStream_t s) {
+    if (!c->pending_on) return RSAC_OK;
+    c->pending_on = false;
+    const PnpSetupFuse &f = c->pending_setup;
+    HIPCHK(launch_pnp_frame(a, 1, f.max_n, f.ws, nullptr, nullptr, nullptr, f.frame, f.fconst, s, &f.prep));
     return RSAC_OK;
 }
 
@@ -635,9 +660,21 @@ int run_loop(rsac_ctx *c, Model model, const Staged &st, void *args, int32_t max
         }
         if (out.timing) HIPCHK(hipEventRecord(c->ev0, s));
         if (pa) {
-            HIPCHK(launch_pnp_solve(*pa, P, hb, Hr, s));
+            // the deferred set-up beside the round's solve; the scorer then builds the records
+            const bool fused = c->pending_on && P == 1 && pnp_setup_fusable(*pa, (int32_t)Hr);
+            if (fused) {
+                c->pending_on = false;
+                HIPCHK(launch_pnp_solve(*pa, P, hb, Hr, s, &c->pending_setup));
+            } else {
+                r = flush_setup(c, *pa, s);
+                if (r) return r;
+                HIPCHK(launch_pnp_solve(*pa, P, hb, Hr, s));
+            }
             if (out.timing) HIPCHK(hipEventRecord(c->ev1, s));
-            HIPCHK(launch_pnp_score(*pa, P, hb, Hr, c->counts.as<int32_t>(), s));
+            pa->fm_inline = fused ? 1 : 0;
+            const hipError_t se = launch_pnp_score(*pa, P, hb, Hr, c->counts.as<int32_t>(), s);
+            pa->fm_inline = 0;
+            HIPCHK(se);
         } else if (model == Model::Fm) {
             HIPCHK(launch_fm_solve(*ha, P, hb, Hr, s));
             if (out.timing) HIPCHK(hipEventRecord(c->ev1, s));
@@ -1083,11 +1120,16 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     r = ensure_hyp_buffers(c, P, stride, (flags & RSAC_F_SAMPLER_OPENCV) != 0);
     if (r) return r;
     PnpArgs a;
-    r = pnp_args(c, st, flags, seed, stride, 0, s, a);
+    // one P3P problem: the set-up runs inside the first solve launch (k_pnp_setup_solve4)
+    r = pnp_args(c, st, flags, seed, stride, 0, s, a, nullptr, true);
     if (r) return r;
     int n_direct = 0;  // problems of OpenCV's count == model_points branch (direct_kinds)
     const std::vector<int8_t> dkind = direct_kinds(st, Model::PnP, a.sample_k, n_direct);
     const bool all_direct = n_direct == P;
+    if (all_direct || n_direct > 0) {  // the direct branch solves without run_loop
+        r = flush_setup(c, a, s);
+        if (r) return r;
+    }
     // one adaptive problem: the device replays the first round's scan itself and the final mask
     // and refit are enqueued behind it, so the call synchronises once; the host verifies the
     // device's pick afterwards and redoes the call without speculation on a mismatch (a libm
@@ -1147,6 +1189,8 @@ int pnp_core(rsac_ctx *c, const void *pts3d, const void *pts2d, const int64_t *o
     } else {
     r = run_loop(c, Model::PnP, st, &a, n_iters, conf, flags, s, lo, spec ? &dec : nullptr, false,
                  first_round ? 1 : 0);
+    if (r == RSAC_OK) r = flush_setup(c, a, s);  // (a loop that launched no solve)
+    c->pending_on = false;
     if (r) return r;
     if (first_round && !spec && !lo.scan[0].done) return more();
     mark(2);

@@ -64,6 +64,10 @@ struct PnpArgs {
     // RSAC_F_RVEC_ROUNDTRIP: the solve kernels replace each minimal model's R by
     // Rodrigues(Rodrigues(R)) (rsac_math.h rodrigues_roundtrip) before writing its records
     int32_t rvec_rt = 0;
+    // 1: the scaled-form scorer builds this round's form-1 records from the f64 models itself
+    // (write_fmodel_sc at its unit staging): the round's solve ran beside the problem's set-up
+    // (k_pnp_setup_solve4), before the frame existed, and wrote no records
+    int32_t fm_inline = 0;
     // test hook (RSAC_DBG_MF_CELL_PTS): > 0 splits every tile of the MFMA scorer into cells of
     // this many points (the unit-size sweep of scripts/mf_units.py); 0 = the launcher's policy
     int32_t dbg_cell_pts = 0;
@@ -202,7 +206,19 @@ hipError_t launch_pnp_prepare(const double *p3, const double *p2, int64_t n, flo
 hipError_t launch_hom_prepare(const double *src, const double *dst, int64_t n, float *SX, float *SY, float *DX,
                               float *DY, hipStream_t s);
 // solve / score hypotheses [hyp_begin, hyp_begin + H) of every problem
-hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s);
+// a one-problem set-up deferred by pnp_args into the first P3P solve (k_pnp_setup_solve4)
+struct PnpSetupFuse {
+    PnpPrepare prep;
+    int32_t max_n;
+    int32_t *ws;
+    double *frame;
+    float *fconst;
+};
+hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s,
+                            const PnpSetupFuse *fuse = nullptr);
+// whether a one-problem round of H P3P hypotheses can take its set-up into the solve launch: the
+// 4-lane solve, then the scaled-form scorer building the round's records itself (fm_inline)
+bool pnp_setup_fusable(const PnpArgs &a, int32_t H);
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
 // the packed best key of counts [hyp_begin, hyp_begin + H) of one problem into *a.best_key (no-op

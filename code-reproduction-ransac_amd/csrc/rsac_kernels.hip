@@ -492,14 +492,15 @@ __global__ __launch_bounds__(1024) void k_pnp_setup1(const double *__restrict__ 
 // to finish (ticket) reduces the blocks' bounds, writes the frame and resets the ticket.  The
 // pre-filter's bounds hold for any centre, so counts do not depend on the choice.
 // CONVERT = false: the points are already the f32 SoA a.X .. a.V (p3, p2, X .. V unused)
+// (the body takes its block index and block count: k_pnp_setup_solve4 runs it on its first blocks)
 template <bool CONVERT>
-__global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__ p3, const double *__restrict__ p2,
-                                                      PnpArgs a, float *__restrict__ X, float *__restrict__ Y,
-                                                      float *__restrict__ Z, float *__restrict__ U,
-                                                      float *__restrict__ V, int *__restrict__ ws,
-                                                      double *__restrict__ frame, float *__restrict__ fconst,
-                                                      float *__restrict__ XC, float *__restrict__ YC,
-                                                      float *__restrict__ ZC, float *part, int *ticket) {
+__device__ __forceinline__ void setup_fc_body(const double *__restrict__ p3, const double *__restrict__ p2,
+                                              const PnpArgs &a, float *__restrict__ X, float *__restrict__ Y,
+                                              float *__restrict__ Z, float *__restrict__ U, float *__restrict__ V,
+                                              int *__restrict__ ws, double *__restrict__ frame,
+                                              float *__restrict__ fconst, float *__restrict__ XC,
+                                              float *__restrict__ YC, float *__restrict__ ZC, float *part, int *ticket,
+                                              const int bid, const int nblk) {
     __shared__ float sl[4][5], sh[4][5];
     const int64_t p0 = a.offsets[0];
     const int n = (int)(a.offsets[1] - p0);
@@ -513,7 +514,7 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
     const MxPixel mk = mx_pixel(a, 0);
 #pragma unroll
     for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
-    for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+    for (int j = bid * 256 + threadIdx.x; j < n; j += nblk * 256) {
         const int64_t i = p0 + j;
         float v[5];
         if constexpr (CONVERT) {
@@ -550,12 +551,12 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
         const int k = threadIdx.x;
         const float l = fminf(fminf(sl[0][k], sl[1][k]), fminf(sl[2][k], sl[3][k]));
         const float h = fmaxf(fmaxf(sh[0][k], sh[1][k]), fmaxf(sh[2][k], sh[3][k]));
-        __hip_atomic_store(part + 10 * blockIdx.x + k, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(part + 10 * blockIdx.x + 5 + k, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part + 10 * bid + k, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part + 10 * bid + 5 + k, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (sc1 stores)
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1) == nblk - 1;
     __syncthreads();
     if (!last) return;
     // the last block: every block's bounds are in (sc1 stores drained before each ticket add);
@@ -563,7 +564,7 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
     __shared__ int wsl[10];
 #pragma unroll
     for (int k = 0; k < 5; ++k) { lo[k] = __builtin_inff(); hi[k] = -__builtin_inff(); }
-    if (threadIdx.x < gridDim.x)
+    if ((int)threadIdx.x < nblk)
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             lo[k] = __hip_atomic_load(part + 10 * threadIdx.x + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -598,6 +599,17 @@ __global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__
         reset_pnp_queue(a.queue);
         *ticket = 0;  // for the next call (stream order)
     }
+}
+template <bool CONVERT>
+__global__ __launch_bounds__(256) void k_pnp_setup_fc(const double *__restrict__ p3, const double *__restrict__ p2,
+                                                      PnpArgs a, float *__restrict__ X, float *__restrict__ Y,
+                                                      float *__restrict__ Z, float *__restrict__ U,
+                                                      float *__restrict__ V, int *__restrict__ ws,
+                                                      double *__restrict__ frame, float *__restrict__ fconst,
+                                                      float *__restrict__ XC, float *__restrict__ YC,
+                                                      float *__restrict__ ZC, float *part, int *ticket) {
+    setup_fc_body<CONVERT>(p3, p2, a, X, Y, Z, U, V, ws, frame, fconst, XC, YC, ZC, part, ticket, (int)blockIdx.x,
+                           (int)gridDim.x);
 }
 
 // f32 record of one pose for the pre-filter, in the form the scoring launch reads (PnpArgs::fform):
@@ -1301,11 +1313,11 @@ __global__ __launch_bounds__(256) void k_cvepnp5_c(PnpArgs a, int64_t hyp_begin,
 // lanes pick the smallest error, the lowest candidate on ties (= pnp_minimal's first-one rule),
 // and the winner writes the record.  Results equal k_pnp_solve's bit for bit.
 
-template <int L>
-__global__ __launch_bounds__(256) void k_pnp_solve_l(PnpArgs a, int64_t hyp_begin, int32_t H) {
+// gather(p0, idx, X, Y, Z, U, V): the sample's f32 points
+template <int L, class Gather>
+__device__ __forceinline__ void solve_l_body(const PnpArgs &a, int64_t hyp_begin, int32_t H, const int prob,
+                                             const int gt, Gather gather) {
     constexpr int CPL = 4 / L;  // Lambda Twist candidates per lane: lane c takes c CPL .. c CPL + CPL - 1
-    const int prob = blockIdx.y;
-    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
     const int hl = gt / L, lc = gt % L;
     if (gt == 0 && prob == 0) {
         if (a.queue) reset_pnp_queue(a.queue);
@@ -1334,11 +1346,7 @@ __global__ __launch_bounds__(256) void k_pnp_solve_l(PnpArgs a, int64_t hyp_begi
     const Cam k{a.cams[4 * prob], a.cams[4 * prob + 1], a.cams[4 * prob + 2], a.cams[4 * prob + 3]};
     if (st > 0) {
         float X[4], Y[4], Z[4], U[4], V[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int64_t i = p0 + idx[j];
-            X[j] = a.X[i]; Y[j] = a.Y[i]; Z[j] = a.Z[i]; U[j] = a.U[i]; V[j] = a.V[i];
-        }
+        gather(p0, idx, X, Y, Z, U, V);
         double yb[9], xw[9];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -1396,6 +1404,49 @@ __global__ __launch_bounds__(256) void k_pnp_solve_l(PnpArgs a, int64_t hyp_begi
     if (a.fmodels)
         write_fmodel(R, t, sv > 0, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob,
                      a.fconst + (int64_t)prob * kFconstStride, a.fmodels + rec * kFModelStride, a.fform);
+}
+template <int L>
+__global__ __launch_bounds__(256) void k_pnp_solve_l(PnpArgs a, int64_t hyp_begin, int32_t H) {
+    solve_l_body<L>(a, hyp_begin, H, (int)blockIdx.y, (int)(blockIdx.x * blockDim.x + threadIdx.x),
+                    [&](int64_t p0, const int32_t(&idx)[4], float(&X)[4], float(&Y)[4], float(&Z)[4], float(&U)[4],
+                        float(&V)[4]) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int64_t i = p0 + idx[j];
+                            X[j] = a.X[i]; Y[j] = a.Y[i]; Z[j] = a.Z[i]; U[j] = a.U[i]; V[j] = a.V[i];
+                        }
+                    });
+}
+// One problem's first P3P round fused with its set-up (r06): blocks [0, gs) run k_pnp_setup_fc's
+// conversion / bounds / frame / centring pass over the f64 inputs, the others k_pnp_solve_l<4>,
+// whose samples read the same f64 inputs and round them as the conversion does.  The frame does
+// not exist while the solve runs, so the solve writes no f32 records (a.fmodels = nullptr here)
+// and the round's scaled-form scorer builds them from the f64 models (PnpArgs::fm_inline).  One
+// launch and one dependent dispatch fewer, and the set-up overlaps the solve.
+__global__ __launch_bounds__(256) void k_pnp_setup_solve4(const double *__restrict__ p3, const double *__restrict__ p2,
+                                                          PnpArgs a, float *__restrict__ X, float *__restrict__ Y,
+                                                          float *__restrict__ Z, float *__restrict__ U,
+                                                          float *__restrict__ V, int *__restrict__ ws,
+                                                          double *__restrict__ frame, float *__restrict__ fconst,
+                                                          float *part, int *ticket, int gs, int64_t hyp_begin,
+                                                          int32_t H) {
+    if ((int)blockIdx.x < gs) {
+        setup_fc_body<true>(p3, p2, a, X, Y, Z, U, V, ws, frame, fconst, nullptr, nullptr, nullptr, part, ticket,
+                            (int)blockIdx.x, gs);
+        return;
+    }
+    PnpArgs sa = a;
+    sa.fmodels = nullptr;
+    solve_l_body<4>(sa, hyp_begin, H, 0, ((int)blockIdx.x - gs) * 256 + (int)threadIdx.x,
+                    [&](int64_t p0, const int32_t(&idx)[4], float(&Xs)[4], float(&Ys)[4], float(&Zs)[4], float(&Us)[4],
+                        float(&Vs)[4]) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int64_t i = p0 + idx[j];
+                            Xs[j] = (float)p3[3 * i]; Ys[j] = (float)p3[3 * i + 1]; Zs[j] = (float)p3[3 * i + 2];
+                            Us[j] = (float)p2[2 * i]; Vs[j] = (float)p2[2 * i + 1];
+                        }
+                    });
 }
 
 // ---------------------------------------------------------------------------
@@ -1514,10 +1565,23 @@ __device__ __forceinline__ void sc_unit(const PnpArgs &a, int prob, int64_t h0, 
         // decided outlier) and b = -inf (never undecided)
         const int hq = threadIdx.x;
         float *dst = mlds + hq * kFModelStride;
-        const float *src = a.fmodels + (rec0 + hq) * kFModelStride;
-        const bool valid = hq < nh && src[14] >= 0.f;
+        bool valid;
+        if (a.fm_inline) {  // the record the solve would have written (k_pnp_setup_solve4)
+            const int64_t rec = rec0 + hq;
+            const double *md = a.models + rec * kModelStride;
+            valid = hq < nh && a.status[rec] > 0;
+            if (valid) write_fmodel_sc(md, md + 9, true, a.frame + (int64_t)prob * kFrameStride, a.cams + 4 * prob, fc,
+                                       dst);
+            valid = valid && dst[14] >= 0.f;
+            if (!valid)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) dst[q] = valid ? src[q] : 0.f;
+                for (int q = 0; q < 16; ++q) dst[q] = 0.f;
+        } else {
+            const float *src = a.fmodels + (rec0 + hq) * kFModelStride;
+            valid = hq < nh && src[14] >= 0.f;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) dst[q] = valid ? src[q] : 0.f;
+        }
         if (!valid) {
             dst[9] = 1.f;
             dst[13] = -__builtin_inff();
@@ -2976,7 +3040,13 @@ hipError_t launch_pnp_fmodels(const PnpArgs &a, int32_t P, int32_t H, hipStream_
 // solve of one step overlaps the other stream's scoring better); larger rounds (C3) stay on one
 constexpr int64_t kSolve2MaxHyps = 262144;
 
-hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s) {
+bool pnp_setup_fusable(const PnpArgs &a, int32_t H) {
+    return a.sample_k == 4 && a.fmodels && !a.exact_only && H <= kSolve4MaxHyps && a.max_n > kLanePts &&
+           small_round(1, H, a.max_n);
+}
+
+hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, hipStream_t s,
+                            const PnpSetupFuse *fuse) {
     PnpArgs ka = round_args(a, P, H);
     if (a.sample_k == 5) {  // EPnP-5 in OpenCV's sequence: k_cvepnp5_a / _svd / _c
         if (!a.epnp) return hipErrorInvalidValue;  // its scratch (ensure_epnp5) is required
@@ -2989,6 +3059,17 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
                            (tb / 64) * kSvdHpw * kSvdStride * sizeof(double), s, ka, hyp_begin, H);
         const int hpw = 21;  // hypotheses per wave of stage 3 (3 lanes each)
         hipLaunchKernelGGL(k_cvepnp5_c, dim3(cdiv(cdiv(H, hpw), tb / 64), P), dim3(tb), 0, s, ka, hyp_begin, H, hpw);
+    }
+    // one problem's deferred set-up beside the 4-lane solve (the round's scorer builds the records)
+    else if (fuse) {
+        const PnpPrepare &pr = fuse->prep;
+        if (P != 1 || H > kSolve4MaxHyps || !pr.p3 || !pr.part || !pr.ticket || fuse->max_n > 65536)
+            return hipErrorInvalidValue;
+        unsigned gs = cdiv(fuse->max_n > 0 ? fuse->max_n : 1, 256);
+        if (gs > kSetupMaxBlocks) gs = kSetupMaxBlocks;
+        hipLaunchKernelGGL(k_pnp_setup_solve4, dim3(gs + cdiv(4 * (int64_t)H, 256)), dim3(256), 0, s, pr.p3, pr.p2,
+                           ka, pr.X, pr.Y, pr.Z, pr.U, pr.V, fuse->ws, fuse->frame, fuse->fconst, pr.part, pr.ticket,
+                           (int)gs, hyp_begin, H);
     }
     // a few waves of hypotheses in all: their latency is the launch's, so spread each over 4 lanes
     else if ((int64_t)P * H <= kSolve4MaxHyps)
