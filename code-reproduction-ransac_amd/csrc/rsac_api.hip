@@ -140,6 +140,7 @@ struct rsac_ctx {
     int32_t scanrec_copy = 0;  // problems whose device scan records still go to h_scanrec (issue_scanrec_copy)
     int32_t dbg_cell_pts = 0;                                  // RSAC_DBG_MF_CELL_PTS
     bool dbg_spec_overflow = false;                            // RSAC_DBG_SPEC_OVERFLOW
+    int64_t dbg_f64_selftest = -1;                             // RSAC_DBG_F64_SELFTEST's last mismatch count
     DevBuf win;                                                // rsac_pnp_winner: the re-derived record
     DevBuf reproj;                                             // reprojection errors / the K sweep's inputs
     DevBuf geo;                                                // geodesy / DEM: staged host inputs and outputs
@@ -1436,6 +1437,22 @@ int rsac_debug_set(rsac_ctx *c, int32_t key, int64_t value) {
     case RSAC_DBG_SPEC_OVERFLOW:
         c->dbg_spec_overflow = value != 0;
         return RSAC_OK;
+    case RSAC_DBG_F64_SELFTEST: {
+        if (value < 0 || value > (int64_t)1 << 30) return fail(RSAC_EINVAL, "bad self-test size");
+        int r = check_device(c);
+        if (r) return r;
+        int *d = nullptr;
+        HIPCHK(hipMalloc(&d, sizeof(int)));
+        hipError_t e = hipMemsetAsync(d, 0, sizeof(int), c->stream);
+        if (e == hipSuccess) e = launch_f64_selftest(value, d, c->stream);
+        int h = -1;
+        if (e == hipSuccess) e = hipMemcpyAsync(&h, d, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(d);
+        HIPCHK(e);
+        c->dbg_f64_selftest = h;
+        return RSAC_OK;
+    }
     default:
         return fail(RSAC_EINVAL, "unknown debug key %d", key);
     }
@@ -1449,6 +1466,9 @@ int rsac_debug_get(rsac_ctx *c, int32_t key, int64_t *value) {
         return RSAC_OK;
     case RSAC_DBG_SPEC_REDOS:
         *value = c->spec_redos;
+        return RSAC_OK;
+    case RSAC_DBG_F64_SELFTEST:
+        *value = c->dbg_f64_selftest;
         return RSAC_OK;
     default:
         return fail(RSAC_EINVAL, "unknown debug key %d", key);

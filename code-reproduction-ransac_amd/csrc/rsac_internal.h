@@ -219,6 +219,8 @@ hipError_t launch_pnp_solve(const PnpArgs &a, int32_t P, int64_t hyp_begin, int3
 // whether a one-problem round of H P3P hypotheses can take its set-up into the solve launch: the
 // 4-lane solve, then the scaled-form scorer building the round's records itself (fm_inline)
 bool pnp_setup_fusable(const PnpArgs &a, int32_t H);
+// RSAC_DBG_F64_SELFTEST: fast f64 cores vs IEEE on n random operand sets; mismatches added to *bad
+hipError_t launch_f64_selftest(int64_t n, int *bad, hipStream_t s);
 hipError_t launch_pnp_score(const PnpArgs &a, int32_t P, int64_t hyp_begin, int32_t H, int32_t *counts,
                             hipStream_t s);
 // the packed best key of counts [hyp_begin, hyp_begin + H) of one problem into *a.best_key (no-op

@@ -1449,6 +1449,54 @@ __global__ __launch_bounds__(256) void k_pnp_setup_solve4(const double *__restri
                     });
 }
 
+// RSAC_DBG_F64_SELFTEST: the fast f64 cores against the IEEE operators, bit for bit, on random
+// operands inside the ranges their callers prove (rsac_math.h, rsac_cvepnp.h svd_rotation_sel) and
+// on the ranges' ends; every differing result adds one to *bad
+__device__ __forceinline__ double st_rand(Philox &r, int emin, int emax) {
+    const uint64_t m = ((uint64_t)r.next() << 32 | r.next()) & 0xFFFFFFFFFFFFFull;
+    const int e = emin + (int)(r.next() % (uint32_t)(emax - emin + 1));
+    return __builtin_bit_cast(double, (uint64_t)(e + 1023) << 52 | m);
+}
+__global__ __launch_bounds__(256) void k_f64_selftest(int64_t n, int *bad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Philox r;
+    r.init(0x5EEDF64ull, 7u, (uint64_t)i);
+    int nb = 0;
+    auto same = [](double x, double y) { return __builtin_bit_cast(uint64_t, x) == __builtin_bit_cast(uint64_t, y); };
+    // roots: x in [2^-767, DBL_MAX]; the first lanes take the ends
+    double x = st_rand(r, -767, 1023);
+    if (i == 0) x = 0x1p-767;
+    if (i == 1) x = 0x1.fffffffffffffp+1023;
+    nb += !same(dsqrt_fast(x), __builtin_sqrt(x));
+    // quotients: |n|, |d| in [2^-300, 2^300] (either sign)
+    double nn = st_rand(r, -300, 299), dd = st_rand(r, -300, 299);
+    if (i == 2) { nn = 0x1p-300; dd = 0x1.fffffffffffffp+299; }
+    if (i == 3) { nn = 0x1.fffffffffffffp+299; dd = 0x1p-300; }
+    if (r.next() & 1) nn = -nn;
+    if (r.next() & 1) dd = -dd;
+    nb += !same(ddiv_fast(nn, dd), nn / dd);
+    nb += !same(ddiv_fast(1.0, dd), 1.0 / dd);
+    // the Jacobi rotation: a, b in [2^-200, 2^200], p of a pair that is not skipped
+    // (10 DBL_EPSILON sqrt(ab) < |p| <= sqrt(ab)), doubled as the callers pass it
+    const double a = st_rand(r, -200, 199), b = (r.next() & 3) == 0 ? a : st_rand(r, -200, 199);
+    const double sab = __builtin_sqrt(a * b);
+    const double f = (double)(r.next() >> 8) * 0x1p-24;  // [0, 1)
+    double p = sab * (f < 0.5 ? 1e-14 + f * 1e-3 : f);
+    if (!(dabs(p) > cvq::kSvdEps * sab)) p = sab;
+    if (r.next() & 1) p = -p;
+    double c0, s0, c1, s1;
+    cvq::svd_rotation_sel_t<true>(2 * p, a, b, c0, s0);
+    cvq::svd_rotation_sel_t<false>(2 * p, a, b, c1, s1);
+    nb += !same(c0, c1) || !same(s0, s1);
+    if (nb) atomicAdd(bad, nb);
+}
+hipError_t launch_f64_selftest(int64_t n, int *bad, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_f64_selftest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, bad);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // PnP scoring.  The product path is the MFMA kernel k_pnp_score_mf (its small-round and
 // out-of-f16-range forms run the scaled-form body sc_unit); RSAC_F_EXACT_ONLY selects the

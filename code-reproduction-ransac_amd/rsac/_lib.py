@@ -39,6 +39,7 @@ F_RVEC_ROUNDTRIP = 1 << 11
 
 DBG_REFIT_MAX_BLOCKS = 1
 DBG_REFIT_DROP_BLOCK = 2
+DBG_F64_SELFTEST = 7
 
 ABI_VERSION = 2  # include/rsac.h RSAC_ABI_VERSION
 
@@ -215,8 +216,14 @@ class Context:
 
     def debug_set(self, key: int, value: int):
         """test hooks of include/rsac.h (DBG_REFIT_MAX_BLOCKS, DBG_REFIT_DROP_BLOCK, DBG_MF_CELL_PTS,
-        DBG_SPEC_OVERFLOW)"""
+        DBG_SPEC_OVERFLOW, DBG_F64_SELFTEST)"""
         check(lib().rsac_debug_set(self._h, int(key), int(value)))
+
+    def debug_get(self, key: int) -> int:
+        """read-only counters of include/rsac.h (DBG_SPEC_FINISHES, DBG_SPEC_REDOS, DBG_F64_SELFTEST)"""
+        v = C.c_int64(0)
+        check(lib().rsac_debug_get(self._h, int(key), C.byref(v)))
+        return v.value
 
     def close(self):
         if self._h:

@@ -132,6 +132,12 @@ RSAC_EXPORT int rsac_refit_blocks(rsac_ctx *ctx, int32_t n, int32_t *ranges, int
 /* RSAC_DBG_SPEC_OVERFLOW (nonzero): the host's replay of a speculative first round treats it as
  * having more improvements than the device records (the restart-from-hypothesis-0 branch) */
 #define RSAC_DBG_SPEC_OVERFLOW 6
+/* RSAC_DBG_F64_SELFTEST: rsac_debug_set(ctx, RSAC_DBG_F64_SELFTEST, n) runs the fast f64 root /
+ * division cores (rsac_math.h dsqrt_fast / ddiv_fast) and the Jacobi rotation's fast form against
+ * the IEEE operators on the device, over n random operand sets inside their stated ranges plus the
+ * range ends; rsac_debug_get(ctx, RSAC_DBG_F64_SELFTEST, &m) then gives the number of results that
+ * differ in any bit (0 expected). */
+#define RSAC_DBG_F64_SELFTEST 7
 RSAC_EXPORT int rsac_debug_set(rsac_ctx *ctx, int32_t key, int64_t value);
 /* RSAC_DBG_SPEC_FINISHES / RSAC_DBG_SPEC_REDOS (read only): rsac_pnp_ransac(_batched) calls whose
  * finish was enqueued behind the device's own pick of the winners, and those of them the host's

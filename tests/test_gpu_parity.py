@@ -238,16 +238,21 @@ def test_k_sweep_batched():
         np.testing.assert_array_equal(m, ref["mask"])
 
 
-def test_device_inputs_match_host_inputs():
+@pytest.mark.parametrize("refine", [False, True])
+def test_device_inputs_match_host_inputs(refine):
+    # device f64 inputs of one P3P problem take the set-up into the first solve launch
+    # (k_pnp_setup_solve4, the round's records built by the scorer, r06); host inputs do not
     import torch
     pr, soa, cam = _pnp_case(5000, 0.5, 40)
-    R, t, m = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=False)
+    R, t, m, info = rsac.pnp_ransac(pr["points2d"], pr["points3d"], pr["K"], 2000, 30.0, refine=refine,
+                                    return_info=True)
     p2 = torch.from_numpy(pr["points2d"]).cuda()
     p3 = torch.from_numpy(pr["points3d"]).cuda()
-    Rd, td, md = rsac.pnp_ransac(p2, p3, pr["K"], 2000, 30.0, refine=False)
+    Rd, td, md, infod = rsac.pnp_ransac(p2, p3, pr["K"], 2000, 30.0, refine=refine, return_info=True)
     assert md.is_cuda
     np.testing.assert_array_equal(md.cpu().numpy(), m)
     assert _bits_equal(Rd, R) and _bits_equal(td, t)
+    assert (infod.best_hyp, infod.iters, infod.n_inliers) == (info.best_hyp, info.iters, info.n_inliers)
 
 
 def test_batched_large_host_inputs_match_device_inputs():
@@ -945,6 +950,15 @@ def test_scan_device_equals_host_scan(seed):
                 b.step_rows(rows[pos:].cpu().numpy(), step)
                 pos += step
             assert (a.best, a.max_good, a.iters, a.niters, a.done) == (b.best, b.max_good, b.iters, b.niters, b.done)
+
+
+def test_fast_f64_cores_equal_ieee_operators():
+    # rsac_math.h dsqrt_fast / ddiv_fast and the Jacobi rotation's fast form (rsac_cvepnp.h), the
+    # compiler's IEEE sequences without their scaling wrappers, against the IEEE operators on the
+    # device: 4M random operand sets inside the ranges their callers prove, plus the range ends
+    ctx = rsac.context(0)
+    ctx.debug_set(7, 1 << 22)  # RSAC_DBG_F64_SELFTEST
+    assert ctx.debug_get(7) == 0
 
 
 def _spec_counters():
