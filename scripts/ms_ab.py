@@ -21,7 +21,9 @@ MODES = (("epnp5", "opencv"), ("p3p", "philox"))
 
 
 def worker(calls, hyps, c5=False):
-    sys.path[:0] = [os.path.join(ROOT, "code-reproduction-ransac_amd")]
+    # RSAC_PKG_ROOT: another copy of the Python package (wrapper A/B runs); the library stays the tree's
+    # (or RSAC_LIB_PATH's)
+    sys.path[:0] = [os.environ.get("RSAC_PKG_ROOT") or os.path.join(ROOT, "code-reproduction-ransac_amd")]
     import torch
     import rsac
     from rsac import synth
